@@ -1,0 +1,259 @@
+"""Generate golden vectors from the REFERENCE's own modules (this container only).
+
+Test infrastructure.  Runs the reference's PyTorch translate path —
+``encoder/transformer.py``, ``encoder/nano_encoder.py``, ``decoder/
+transformer.py``, ``onmt/modules/*`` and ``translate/translator.py``'s own
+``_translate_random_sampling`` (greedy, :396-503) and ``_fast_translate_batch``
+(--fast beam, :619-825) — on seeded synthetic weights and synthetic signal
+chunks, and writes small ``.npz`` fixtures to ``tests/golden/``.
+
+The reference never travels to the GPU box; only these fixtures (data) do.
+Regenerate with:  ``python oracle/make_golden.py``  (needs /root/reference).
+
+Compat shims: integer ``Tensor.div`` is floor division while
+the --fast beam runs (``translate/translator.py:732`` was written for torch 1.0).
+"""
+from __future__ import annotations
+
+import argparse
+import contextlib
+import hashlib
+import json
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, ROOT)
+
+from nanodecoder_amd import synth  # noqa: E402
+from oracle._refimport import load_reference  # noqa: E402
+
+GOLDEN_DIR = os.path.join(ROOT, "tests", "golden")
+MEM_STRIDE = 16  # memory-bank rows kept in the fixture: t = 0, 16, 32, ...
+
+
+def weights_digest(W):
+    h = hashlib.sha256()
+    for k in sorted(W):
+        h.update(k.encode())
+        h.update(np.ascontiguousarray(W[k]).tobytes())
+    return h.hexdigest()
+
+
+def build_reference_model(ns, cfg: synth.ModelConfig, W):
+    """Instantiate the reference modules (models/model_builder.py:65-214,
+    :326-334) and load W into them."""
+    d = cfg.d_model
+    if cfg.encoder_type == "transformer":
+        enc = ns.TransformerEncoder(cfg.enc_layers, d, cfg.heads, cfg.d_ff, 0.0, 1, None)
+    else:
+        enc = ns.NanoEncoder("LSTM", cfg.enc_layers, cfg.dec_layers, 2 * cfg.rnn_hidden, d, "1",
+                             0.0, 4000, 0.075, 1)
+    emb = ns.Embeddings(d, cfg.vocab, cfg.pad_idx, position_encoding=cfg.position_encoding)
+    dec = ns.TransformerDecoder(cfg.dec_layers, d, cfg.heads, cfg.d_ff, "general", False,
+                                "scaled-dot", 0.0, emb)
+    gen = nn.Sequential(nn.Linear(d, cfg.vocab), nn.LogSoftmax(dim=-1))
+    model = nn.Module()
+    model.encoder, model.decoder = enc, dec
+    sd = {}
+    for k, v in W.items():
+        if k.startswith("generator."):
+            continue
+        sd[k] = torch.from_numpy(np.array(v))
+    missing, unexpected = model.load_state_dict(sd, strict=False)
+    missing = [m for m in missing if not m.endswith(".mask") and not m.endswith("num_batches_tracked")]
+    assert not missing and not unexpected, (missing, unexpected)
+    gen.load_state_dict({"0.weight": torch.from_numpy(W["generator.0.weight"]),
+                         "0.bias": torch.from_numpy(W["generator.0.bias"])})
+    model.generator = gen
+    model.eval()
+    return model
+
+
+class _Field:
+    def __init__(self, itos):
+        self.vocab = types.SimpleNamespace(itos=list(itos), stoi={s: i for i, s in enumerate(itos)})
+        self.init_token, self.eos_token = "<s>", "</s>"
+        self.pad_token, self.unk_token = "<blank>", "<unk>"
+
+
+def make_translator(ns, model, cfg, beam_size, n_best=1, max_length=100, min_length=0, alpha=0.0):
+    opt = types.SimpleNamespace(
+        gpu=-1, n_best=n_best, max_length=max_length, beam_size=beam_size,
+        random_sampling_temp=1.0, random_sampling_topk=1, min_length=min_length,
+        stepwise_penalty=False, dump_beam="", block_ngram_repeat=0, ignore_when_blocking=[],
+        fft=False, sample_rate=4000, window_size=0.075, window_stride=0.015, window="hamming",
+        replace_unk=False, data_type="nano", verbose=False, fast=True)
+    model_opt = types.SimpleNamespace(copy_attn=False)
+    scorer = types.SimpleNamespace(alpha=alpha, beta=0.0)
+    return ns.Translator(model, {"tgt": _Field(cfg.itos)}, opt, model_opt, global_scorer=scorer,
+                         report_score=False, logger=None)
+
+
+def make_batch(chunks):
+    """inputters/inputter.py:86-95 (make_nano) + OrderedIterator sort_within_batch:
+    zero-pad to the longest chunk, batch sorted by length descending (stable)."""
+    order = sorted(range(len(chunks)), key=lambda i: len(chunks[i]), reverse=True)
+    T = max(len(c) for c in chunks)
+    src = torch.zeros(T, len(chunks), 1)
+    for j, i in enumerate(order):
+        src[: len(chunks[i]), j, 0] = torch.from_numpy(chunks[i])
+    lengths = torch.tensor([len(chunks[i]) for i in order], dtype=torch.long)
+    batch = types.SimpleNamespace(src=src, src_lengths=lengths, batch_size=len(chunks),
+                                  indices=torch.tensor(order, dtype=torch.long))
+    return batch, order
+
+
+@contextlib.contextmanager
+def floor_int_div():
+    orig = torch.Tensor.div
+
+    def div(self, other, *a, **k):
+        if not self.is_floating_point() and isinstance(other, int) and not a and not k:
+            return orig(self, other, rounding_mode="floor")
+        return orig(self, other, *a, **k)
+
+    torch.Tensor.div = div
+    try:
+        yield
+    finally:
+        torch.Tensor.div = orig
+
+
+def run_greedy(ns, model, cfg, chunks, max_length=100, min_length=0):
+    tr = make_translator(ns, model, cfg, beam_size=1, max_length=max_length, min_length=min_length)
+    batch, order = make_batch(chunks)
+    rec = []
+    orig = tr._decode_and_generate
+
+    def wrapped(*a, **k):
+        lp, attn = orig(*a, **k)
+        rec.append(lp.detach().clone())
+        return lp, attn
+
+    tr._decode_and_generate = wrapped
+    mem_box = {}
+    enc_fwd = model.encoder.forward
+
+    def enc_wrap(src, lengths=None):
+        out = enc_fwd(src, lengths)
+        mem_box["memory"] = out[1].detach().clone()
+        return out
+
+    model.encoder.forward = enc_wrap
+    with torch.no_grad():
+        res = tr._translate_random_sampling(batch, types.SimpleNamespace(data_type="nano"), max_length,
+                                            min_length=min_length, sampling_temp=1.0, keep_topk=1)
+    model.encoder.forward = enc_fwd
+    B = len(chunks)
+    inv = np.argsort(order)  # batch row j holds chunk order[j]
+    logp = torch.stack(rec, 1).numpy()[inv]                     # [B, S, V]
+    tokens = np.stack([res["predictions"][j][0].numpy() for j in range(B)])[inv].astype(np.int32)
+    scores = np.array([float(res["scores"][j][0]) for j in range(B)], np.float32)[inv]
+    memory = mem_box["memory"].numpy()[:, inv, :]              # [T, B, d]
+    return dict(logp=logp.astype(np.float32), tokens=tokens, scores=scores,
+                memory_sub=np.ascontiguousarray(memory[::MEM_STRIDE]).astype(np.float32),
+                T=np.int32(memory.shape[0]))
+
+
+def run_beam(ns, model, cfg, chunks, beam_size=5, n_best=1, max_length=100, min_length=0, alpha=0.0):
+    tr = make_translator(ns, model, cfg, beam_size=beam_size, n_best=n_best, max_length=max_length,
+                         min_length=min_length, alpha=alpha)
+    batch, order = make_batch(chunks)
+    with torch.no_grad(), floor_int_div():
+        res = tr._fast_translate_batch(batch, types.SimpleNamespace(data_type="nano"), max_length,
+                                       min_length=min_length, n_best=n_best)
+    B = len(chunks)
+    inv = np.argsort(order)
+    tokens = np.full((B, n_best, max_length), -1, np.int32)
+    lens = np.zeros((B, n_best), np.int32)
+    scores = np.zeros((B, n_best), np.float32)
+    for j in range(B):
+        for n in range(n_best):
+            p = res["predictions"][j][n].numpy()
+            tokens[j, n, : len(p)] = p
+            lens[j, n] = len(p)
+            scores[j, n] = float(res["scores"][j][n])
+    return dict(beam_tokens=tokens[inv], beam_lens=lens[inv], beam_scores=scores[inv])
+
+
+SCENARIOS = [
+    # name, model config kwargs, weight seed, eos_bias, chunk spec, runs
+    dict(name="transformer_greedy", cfg=dict(encoder_type="transformer"), seed=11, eos_bias=-3.0,
+         chunks=dict(kind="mixed"), greedy=dict(max_length=100)),
+    dict(name="transformer_pe_short", cfg=dict(encoder_type="transformer", position_encoding=True),
+         seed=12, eos_bias=0.0, chunks=dict(kind="short"), greedy=dict(max_length=40, min_length=5)),
+    dict(name="transformer_beam", cfg=dict(encoder_type="transformer"), seed=13, eos_bias=2.5,
+         chunks=dict(kind="mixed"), beam=dict(beam_size=5, n_best=1, max_length=100),
+         beam2=dict(beam_size=5, n_best=3, max_length=60, min_length=10)),
+    dict(name="nano_greedy", cfg=dict(encoder_type="nano"), seed=14, eos_bias=-2.0,
+         chunks=dict(kind="mixed"), greedy=dict(max_length=60)),
+]
+
+
+def scenario_chunks(kind, seed):
+    if kind == "mixed":
+        # two full chunks, one short tail chunk (zero padded in the batch), one
+        # all-zero chunk (every encoder key masked -> uniform attention rows).
+        full = synth.synth_chunk_batch(2, 512, seed=seed, inject_masks=True)
+        tail = synth.synth_read_chunks(seed + 500, 812)[-1]
+        assert len(tail) == 300
+        zero = np.zeros(512, np.float32)
+        return [full[0], tail, full[1], zero]
+    if kind == "short":
+        # a batch made only of short chunks: T_max < 512 (reference batching quirk)
+        return [synth.synth_read_chunks(seed + 600 + i, 512 + n)[-1] for i, n in enumerate((200, 150, 77))]
+    raise ValueError(kind)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=GOLDEN_DIR)
+    args = ap.parse_args()
+    os.makedirs(args.out, exist_ok=True)
+    torch.manual_seed(0)
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    ns = load_reference()
+    index = {}
+    for sc in SCENARIOS:
+        cfg = synth.ModelConfig(**sc["cfg"])
+        W = synth.make_weights(cfg, seed=sc["seed"], eos_bias=sc["eos_bias"])
+        model = build_reference_model(ns, cfg, W)
+        chunks = scenario_chunks(sc["chunks"]["kind"], sc["seed"])
+        out = {}
+        lens = np.array([len(c) for c in chunks], np.int32)
+        T = int(lens.max())
+        src = np.zeros((len(chunks), T), np.float32)
+        for i, c in enumerate(chunks):
+            src[i, : len(c)] = c
+        out["src"], out["lengths"] = src, lens
+        if "greedy" in sc:
+            g = run_greedy(ns, model, cfg, chunks, **sc["greedy"])
+            out.update(g)
+        if "beam" in sc:
+            b = run_beam(ns, model, cfg, chunks, **sc["beam"])
+            out.update(b)
+        if "beam2" in sc:
+            b = run_beam(ns, model, cfg, chunks, **sc["beam2"])
+            out.update({k + "2": v for k, v in b.items()})
+        meta = dict(name=sc["name"], cfg=sc["cfg"], seed=sc["seed"], eos_bias=sc["eos_bias"],
+                    greedy=sc.get("greedy"), beam=sc.get("beam"), beam2=sc.get("beam2"),
+                    mem_stride=MEM_STRIDE, weights_sha256=weights_digest(W),
+                    torch=torch.__version__, numpy=np.__version__)
+        out["meta"] = np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8)
+        path = os.path.join(args.out, sc["name"] + ".npz")
+        np.savez_compressed(path, **out)
+        index[sc["name"]] = meta
+        print(f"wrote {path} ({os.path.getsize(path)} B)")
+    with open(os.path.join(args.out, "index.json"), "w") as f:
+        json.dump(index, f, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()

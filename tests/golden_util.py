@@ -1,0 +1,31 @@
+"""Helpers to read the committed golden fixtures (tests/golden/*.npz)."""
+import json
+import os
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+NAMES = ["transformer_greedy", "transformer_pe_short", "transformer_beam", "nano_greedy"]
+
+
+def load(name):
+    z = np.load(os.path.join(GOLDEN, name + ".npz"))
+    meta = json.loads(bytes(z["meta"]).decode())
+    return {k: z[k] for k in z.files if k != "meta"}, meta
+
+
+def model_for(meta):
+    from nanodecoder_amd import synth
+    cfg = synth.ModelConfig(**meta["cfg"])
+    W = synth.make_weights(cfg, seed=meta["seed"], eos_bias=meta["eos_bias"])
+    return cfg, W
+
+
+def chunks_of(z):
+    return [z["src"][i, : z["lengths"][i]].copy() for i in range(len(z["lengths"]))]
+
+
+def logp_close(a, b, atol=1e-3, rtol=1e-5):
+    """|a-b| <= atol + rtol*|b| (rtol covers the -1e4-biased specials whose fp32
+    ulp is ~1e-3)."""
+    return np.abs(a - b) <= atol + rtol * np.abs(b)

@@ -1,0 +1,68 @@
+"""The CPU restatement (oracle/ref_cpu.py) against golden vectors recorded from
+the reference's own modules (oracle/make_golden.py).  CPU only."""
+import numpy as np
+import pytest
+
+from nanodecoder_amd import synth
+from oracle import ref_cpu
+from tests import golden_util as gu
+
+try:
+    from oracle.make_golden import weights_digest
+except Exception:  # pragma: no cover
+    weights_digest = None
+
+
+@pytest.mark.parametrize("name", gu.NAMES)
+def test_weights_regenerate_identically(name):
+    z, meta = gu.load(name)
+    cfg, W = gu.model_for(meta)
+    assert weights_digest(W) == meta["weights_sha256"]
+
+
+@pytest.mark.parametrize("name", ["transformer_greedy", "transformer_pe_short", "nano_greedy"])
+def test_greedy_matches_reference(name):
+    z, meta = gu.load(name)
+    cfg, W = gu.model_for(meta)
+    m = ref_cpu.RefModel(cfg, W)
+    chunks = gu.chunks_of(z)
+    src, lens, order = ref_cpu.make_batch(chunks)
+    inv = np.argsort(order)
+    r = ref_cpu.greedy(m, src, lens, **meta["greedy"])
+    assert gu.logp_close(r["logp"][inv], z["logp"], atol=1e-5, rtol=1e-6).all()
+    assert (r["tokens"][inv] == z["tokens"]).all()
+    np.testing.assert_allclose(r["scores"][inv], z["scores"], atol=1e-5)
+    mem = r["memory"][inv].transpose(1, 0, 2)[:: meta["mem_stride"]]
+    np.testing.assert_allclose(mem, z["memory_sub"], atol=1e-5)
+
+
+@pytest.mark.parametrize("which", ["", "2"])
+def test_fast_beam_matches_reference(which):
+    z, meta = gu.load("transformer_beam")
+    cfg, W = gu.model_for(meta)
+    m = ref_cpu.RefModel(cfg, W)
+    chunks = gu.chunks_of(z)
+    src, lens, order = ref_cpu.make_batch(chunks)
+    kw = meta["beam" + which]
+    res = ref_cpu.fast_beam(m, src, lens, **kw)
+    for j, i in enumerate(order):
+        assert len(res[j]) == kw["n_best"]
+        for nb, (s, p) in enumerate(res[j]):
+            L = z["beam_lens" + which][i, nb]
+            assert len(p) == L
+            assert (p == z["beam_tokens" + which][i, nb, :L]).all()
+            assert abs(s - z["beam_scores" + which][i, nb]) < 1e-4
+
+
+def test_translate_batching_and_strings():
+    """Translator.translate semantics: batches of batch_size consecutive chunks
+    padded to their own longest chunk; strings cut at the first EOS."""
+    z, meta = gu.load("transformer_greedy")
+    cfg, W = gu.model_for(meta)
+    m = ref_cpu.RefModel(cfg, W)
+    chunks = gu.chunks_of(z)
+    scores, preds = ref_cpu.translate(m, chunks, batch_size=4, max_length=100)
+    for i in range(len(chunks)):
+        s = ref_cpu.tokens_to_string(z["tokens"][i], cfg.itos, cfg.eos_idx)
+        assert preds[i] == [s]
+        assert abs(scores[i][0] - z["scores"][i]) < 1e-5
