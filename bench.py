@@ -1,0 +1,202 @@
+#!/usr/bin/env python
+"""Benchmark of the MI355X translate path (BASELINE.json metric).
+
+A "step" = one full translate call (encoder + all decoder steps + search) on
+one batch of synthetic 512-sample chunks already resident in HBM.  Default
+workload = BASELINE.json configs[1]: 3+3 transformer, d_model 256, T 512,
+batch 256 chunks per GPU, greedy, max_length 100, random-init weights of the
+reference architecture (no trained checkpoint exists offline).
+
+Multi-GPU (``torch.distributed.run``): reads shard across ranks with no
+collective in the hot loop ("scaling": "weak" — every rank translates its own
+batch); rank 0 loads/creates the weights and broadcasts them once over RCCL.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "signal-samples/sec/GPU (512-sample chunks) + bases/sec at 1/2/4/8 MI355X"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=256, help="chunks per GPU per step")
+    ap.add_argument("--mode", default="greedy", choices=["greedy", "beam"])
+    ap.add_argument("--beam", type=int, default=5)
+    ap.add_argument("--encoder", default="transformer", choices=["transformer", "nano"])
+    ap.add_argument("--max-length", type=int, default=100)
+    ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 (0 = skip)")
+    ap.add_argument("--cpu-chunks", type=int, default=8)
+    ap.add_argument("--no-roofline", action="store_true")
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def bcast_weights(W, world, local):
+    """One RCCL broadcast of the packed fp32 weight blob from rank 0."""
+    if world == 1:
+        return W
+    names = sorted(W)
+    sizes = [W[n].size for n in names]
+    blob = torch.empty(sum(sizes), dtype=torch.float32, device=torch.device("cuda", local))
+    if int(os.environ.get("RANK", "0")) == 0:
+        blob.copy_(torch.from_numpy(np.concatenate([W[n].ravel() for n in names])))
+    torch.distributed.broadcast(blob, src=0)
+    host = blob.cpu().numpy()
+    out, off = {}, 0
+    for n, s in zip(names, sizes):
+        out[n] = host[off: off + s].reshape(W[n].shape)
+        off += s
+    return out
+
+
+def cpu_baseline(cfg, W, sig, lens, args):
+    from oracle import ref_cpu
+    n = min(args.cpu_chunks, sig.shape[0])
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    m = ref_cpu.RefModel(cfg, W)
+    t0 = time.perf_counter()
+    if args.mode == "greedy":
+        ref_cpu.greedy(m, sig[:n], lens[:n], max_length=args.max_length)
+    else:
+        ref_cpu.fast_beam(m, sig[:n], lens[:n], beam_size=args.beam, max_length=args.max_length)
+    dt = time.perf_counter() - t0
+    return {"value": float(lens[:n].sum() / dt), "unit": "samples/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/ref_cpu.py {args.mode} on {n} chunks x 512 samples, max_length {args.max_length}, "
+                      f"torch CPU fp32, {threads} threads, {dt:.1f} s"}
+
+
+def kernel_roofline(eng, B):
+    """Dominant kernel = encoder FFN1 GEMM (fp32 MFMA): [B*512,256]x[256,2048]
+    with LN prologue + bias + ReLU.  Timed standalone through the C-ABI op
+    entry point on the current torch stream with HIP events."""
+    from nanodecoder_amd.engine import op_gemm
+    dev = eng.device
+    M, K, N = B * 512, 256, 2048
+    A = torch.randn(M, K, device=dev)
+    Wt = torch.randn(N, K, device=dev) / 16
+    b = torch.randn(N, device=dev)
+    g = torch.ones(K, device=dev)
+    bb = torch.zeros(K, device=dev)
+    for _ in range(3):
+        op_gemm(A, Wt, b, None, g, bb, True)
+    n = 20
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        op_gemm(A, Wt, b, None, g, bb, True)
+    e1.record()
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / n
+    flops = 2.0 * M * N * K
+    ach = flops / (ms * 1e-3) / 1e12
+    return {"bound": "mfma", "kernel": "gemm_f32_kernel<128,128,2,2,LN,RELU> (encoder FFN1)",
+            "achieved": round(ach, 2), "peak": 157.3, "unit": "TFLOP/s", "frac": round(ach / 157.3, 4),
+            "traffic": None, "per_launch_flop": flops, "avg_launch_ms": round(ms, 4)}
+
+
+def main():
+    args = parse()
+    world, rank, local = dist_setup(args)
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    from nanodecoder_amd import synth
+    from nanodecoder_amd.engine import Engine
+
+    cfg = synth.ModelConfig(encoder_type=args.encoder)
+    W = synth.make_weights(cfg, seed=11, eos_bias=-3.0) if rank == 0 or world == 1 else \
+        synth.make_weights(cfg, seed=11, eos_bias=-3.0)
+    W = bcast_weights(W, world, local)
+    beam = args.beam if args.mode == "beam" else 1
+    eng = Engine(cfg, W, device=local, max_batch=args.batch, max_src_len=512, max_steps=args.max_length,
+                 max_beam=beam)
+    # each rank gets its own shard of synthetic reads
+    sig_np = synth.synth_chunk_batch(args.batch, 512, seed=1000 + rank, inject_masks=False)
+    lens_np = np.full(args.batch, 512, np.int32)
+    sig = torch.from_numpy(sig_np).to(dev)
+    lens = torch.from_numpy(lens_np).to(dev)
+
+    def step():
+        if args.mode == "greedy":
+            return eng.translate_greedy(sig, lens, lens, max_len=args.max_length)
+        return eng.translate_beam(sig, lens, lens, beam=args.beam, max_len=args.max_length)
+
+    for _ in range(args.warmup):
+        out = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    bases = 0
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    # bases = base tokens before the first EOS (outside the timed region)
+    tok = out["tokens"].cpu().numpy()
+    if args.mode == "beam":
+        tok = tok[:, 0]
+    eos = cfg.eos_idx
+    is_eos = tok == eos
+    first = np.where(is_eos.any(1), is_eos.argmax(1), tok.shape[1])
+    base_mask = (np.arange(tok.shape[1])[None, :] < first[:, None]) & (tok >= 4)
+    bases_per_step = int(base_mask.sum())
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    if world > 1:
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    dt = float(t.item())
+    samples = float(lens_np.sum()) * args.steps * world
+    value = samples / dt
+    res = {
+        "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic reads, random-init weights",
+        "config": {"workload": f"configs[1]: 3+3 {args.encoder} d256, T512, {args.mode}"
+                               f"{'' if args.mode == 'greedy' else ' beam ' + str(args.beam)}, max_length "
+                               f"{args.max_length}", "chunks_per_gpu_per_step": args.batch,
+                   "global_batch": args.batch * world, "seq_len": 512, "parallelism": f"read-shard x{world}"},
+        "samples_per_sec_per_gpu": round(value / world, 1),
+        "bases_per_sec": round(bases_per_step * args.steps * world / dt, 1),
+    }
+    if rank == 0:
+        if not args.no_roofline:
+            res["roofline"] = kernel_roofline(eng, args.batch)
+        if args.cpu_baseline and world == 1:
+            res["cpu_baseline"] = cpu_baseline(cfg, W, sig_np, lens_np, args)
+        print(json.dumps(res), flush=True)
+    eng.close()
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

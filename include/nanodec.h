@@ -1,0 +1,138 @@
+/*
+ * nanodec.h — C-ABI of libnanodec_hip.so, the MI355X (gfx950) engine for
+ * NanoDecoder's translate path.
+ *
+ * The reference has no native boundary: its path is PyTorch modules driven by
+ * translate/translator.py.  Each entry point below replaces the reference
+ * interface named in its comment (file:line in achilles1989/NanoDecoder).
+ * Plain pointers and sizes only; device pointers are HIP device memory owned
+ * by the caller (PyTorch-ROCm tensors' data_ptr()).  Every function returns
+ * 0 on success; on failure a nonzero ND_* code and a thread-local message in
+ * nd_last_error().
+ *
+ * Threading: one context is bound to one device and must not be called
+ * concurrently; every call sets the device first (the reference drives the
+ * GPU from a multiprocessing.Pool result thread, translate.py:100-161).
+ * All work is enqueued on the caller's stream; no hidden device-wide syncs.
+ */
+#ifndef NANODEC_H
+#define NANODEC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ND_OK 0
+#define ND_ERR_ARG 1      /* bad argument / shape / config */
+#define ND_ERR_WEIGHT 2   /* unknown / missing / mis-shaped weight */
+#define ND_ERR_HIP 3      /* HIP runtime error */
+#define ND_ERR_STATE 4    /* call order (e.g. translate before finalize) */
+
+#define ND_ENC_TRANSFORMER 0  /* encoder/transformer.py */
+#define ND_ENC_NANO 1         /* encoder/nano_encoder.py (3x BiLSTM) */
+
+typedef struct nd_ctx nd_ctx;
+
+/* Architecture + capacity.  Mirrors the checkpoint ``opt`` the reference
+ * builds its model from (models/model_builder.py:236-334). */
+typedef struct nd_config {
+  int32_t encoder_type;       /* ND_ENC_* */
+  int32_t enc_layers;         /* 3 */
+  int32_t dec_layers;         /* 3 */
+  int32_t d_model;            /* 256 (only value compiled) */
+  int32_t heads;              /* 8   (d_model / heads == 32) */
+  int32_t d_ff;               /* 2048 (multiple of 128) */
+  int32_t vocab;              /* |tgt vocab|, <= 32 */
+  int32_t rnn_hidden;         /* 128 per direction (NanoEncoder) */
+  int32_t position_encoding;  /* decoder sinusoidal PE (embeddings.py:36-43) */
+  int32_t pad_idx, bos_idx, eos_idx;
+  int32_t max_batch;          /* chunks per call */
+  int32_t max_src_len;        /* 512 (src_seq_length) */
+  int32_t max_steps;          /* max_length (100) */
+  int32_t max_beam;           /* beam_size upper bound (1 = greedy only) */
+  int32_t device;             /* HIP device ordinal */
+} nd_config;
+
+/* Replaces models/model_builder.py:load_test_model (:217-233) +
+ * build_base_model (:236-382): allocate the engine for one device. */
+int nd_create(const nd_config* cfg, nd_ctx** out);
+
+/* Replaces model.load_state_dict (models/model_builder.py:356-357) for one
+ * tensor.  ``name`` is the reference state-dict key (after the a_2/b_2 fix,
+ * :345-353); generator keys are "generator.0.weight"/"generator.0.bias".
+ * Unknown names and shape mismatches are errors (the reference's strict=False
+ * silent fallback is deliberately NOT reproduced); decoder ``*.mask`` buffers
+ * and BatchNorm ``num_batches_tracked`` are accepted and ignored. */
+int nd_load_weight(nd_ctx* ctx, const char* name, const float* host, const int64_t* shape, int ndim);
+
+/* Checks that every required weight was loaded and builds derived packed
+ * weights.  Must be called once before any translate call. */
+int nd_finalize(nd_ctx* ctx);
+
+/* Greedy translate of a batch of chunks: encoder forward + max_len decoder
+ * steps with argmax selection.  Replaces Translator.translate_batch ->
+ * _translate_random_sampling (translate/translator.py:396-540) for
+ * beam_size == 1 (keep_topk == 1): all max_len steps always run (no EOS
+ * early exit, :455-483) and the score is the last step's top log-prob
+ * (:491-499).
+ *   d_signal  [B, T] f32 row-major, zero padded (make_nano, inputters/inputter.py:86-95)
+ *   d_len     [B] i32 valid samples per chunk (src_lengths)
+ *   d_span    [B] i32 padded length the reference batch would have had
+ *             (= longest chunk of the reference batch; len <= span <= T).
+ *             Positions >= span do not exist for that chunk.
+ *   d_tokens  [B, max_len] i32 out;  d_score [B] f32 out
+ *   d_logp    nullable [B, max_len, V] f32 out: per-step log-probs (pre min_len mask)
+ *   stream    hipStream_t of the caller (void* here to keep HIP out of the ABI) */
+int nd_translate_greedy(nd_ctx* ctx, const float* d_signal, const int32_t* d_len, const int32_t* d_span,
+                        int32_t B, int32_t T, int32_t max_len, int32_t min_len,
+                        int32_t* d_tokens, float* d_score, float* d_logp, void* stream);
+
+/* --fast beam search.  Replaces Translator._fast_translate_batch
+ * (translate/translator.py:619-825) with GNMTGlobalScorer.alpha
+ * (onmt/translate/beam.py:181-199; beta must be 0).  Per chunk the n_best
+ * finished hypotheses, best first:
+ *   d_tokens [B, n_best, max_len] i32 (EOS included when emitted; -1 padded)
+ *   d_scores [B, n_best] f32, d_lens [B, n_best] i32
+ *   d_steps  nullable [1] i32: decoder steps actually executed */
+int nd_translate_beam(nd_ctx* ctx, const float* d_signal, const int32_t* d_len, const int32_t* d_span,
+                      int32_t B, int32_t T, int32_t beam, int32_t n_best, float alpha, int32_t max_len,
+                      int32_t min_len, int32_t* d_tokens, float* d_scores, int32_t* d_lens, int32_t* d_steps,
+                      void* stream);
+
+/* Encoder forward only; writes the memory bank [B, T, d_model] (rows
+ * t >= span are unspecified).  Replaces Translator._run_encoder
+ * (translate/translator.py:542-559).  Used by parity tests. */
+int nd_encode(nd_ctx* ctx, const float* d_signal, const int32_t* d_len, const int32_t* d_span, int32_t B,
+              int32_t T, float* d_memory, void* stream);
+
+/* Enables/disables hipGraph capture of the translate calls (default on). */
+int nd_set_graphs(nd_ctx* ctx, int enable);
+
+/* Kernel statistics of the last translate call (ms of device time per
+ * phase, measured with HIP events on the engine stream when enabled). */
+int nd_set_timing(nd_ctx* ctx, int enable);
+int nd_last_timing(nd_ctx* ctx, float* encode_ms, float* decode_ms);
+
+void nd_destroy(nd_ctx* ctx);
+const char* nd_last_error(void);
+const char* nd_version(void);
+
+/* ---- op-level entry points (unit tests of individual kernels) ---------- */
+
+/* C[M,N] = epilogue(prologue(A)[M,K] . W[N,K]^T + bias):
+ * prologue LayerNorm(eps 1e-6, over K) when ln_g != NULL; relu when relu != 0;
+ * + R[M,N] when R != NULL.  All fp32, row-major, dense. */
+int nd_op_gemm(const float* A, const float* W, const float* bias, const float* R, float* C, int32_t M,
+               int32_t N, int32_t K, const float* ln_g, const float* ln_b, int32_t relu, void* stream);
+
+/* Encoder self-attention over qkv [B*T, 3*d] (q | k | v) with the key mask
+ * signal == 0.0 and keys >= span excluded; out [B*T, d]. */
+int nd_op_enc_attention(const float* qkv, const float* signal, const int32_t* span, float* out, int32_t B,
+                        int32_t T, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NANODEC_H */

@@ -1,0 +1,79 @@
+"""ctypes binding of libnanodec_hip.so (include/nanodec.h).
+
+The library is loaded AFTER ``import torch`` so that its DT_NEEDED
+``libamdhip64.so.7`` resolves to the HIP runtime PyTorch-ROCm already mapped
+(same SONAME) — one HIP runtime per process, so torch device pointers and
+streams are valid inside the engine.  There is no fallback: if the shared
+library is missing or fails to load, every engine entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("NANODEC_LIB", os.path.join(HERE, "libnanodec_hip.so"))
+
+ND_ENC_TRANSFORMER = 0
+ND_ENC_NANO = 1
+
+_CFG_FIELDS = ["encoder_type", "enc_layers", "dec_layers", "d_model", "heads", "d_ff", "vocab", "rnn_hidden",
+               "position_encoding", "pad_idx", "bos_idx", "eos_idx", "max_batch", "max_src_len", "max_steps",
+               "max_beam", "device"]
+
+
+class NdConfig(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in _CFG_FIELDS]
+
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int32
+_F = ctypes.c_float
+
+# name -> (restype, argtypes); every symbol include/nanodec.h declares
+SIGNATURES = {
+    "nd_create": (_I, [ctypes.POINTER(NdConfig), ctypes.POINTER(_P)]),
+    "nd_load_weight": (_I, [_P, ctypes.c_char_p, _P, ctypes.POINTER(ctypes.c_int64), _I]),
+    "nd_finalize": (_I, [_P]),
+    "nd_translate_greedy": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P]),
+    "nd_translate_beam": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _F, _I, _I, _P, _P, _P, _P, _P]),
+    "nd_encode": (_I, [_P, _P, _P, _P, _I, _I, _P, _P]),
+    "nd_set_graphs": (_I, [_P, _I]),
+    "nd_set_timing": (_I, [_P, _I]),
+    "nd_last_timing": (_I, [_P, ctypes.POINTER(_F), ctypes.POINTER(_F)]),
+    "nd_destroy": (None, [_P]),
+    "nd_last_error": (ctypes.c_char_p, []),
+    "nd_version": (ctypes.c_char_p, []),
+    "nd_op_gemm": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _I, _P]),
+    "nd_op_enc_attention": (_I, [_P, _P, _P, _P, _I, _I, _P]),
+}
+
+_lib = None
+
+
+class NanodecError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load (once) and return the library; raises if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    import torch  # noqa: F401  (map PyTorch's HIP runtime first)
+    if not os.path.exists(LIB_PATH):
+        raise NanodecError(f"{LIB_PATH} not found: build it with `python -m nanodecoder_amd.build` "
+                           "(there is no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str = ""):
+    if rc != 0:
+        msg = lib().nd_last_error().decode(errors="replace")
+        raise NanodecError(f"{what} failed (code {rc}): {msg}")

@@ -1,0 +1,67 @@
+"""Build libnanodec_hip.so in-tree with hipcc for gfx950.
+
+Every .hip file under csrc/ is compiled to an object with
+``hipcc --offload-arch=gfx950 -O3 -fPIC`` and linked into
+``nanodecoder_amd/libnanodec_hip.so``.  Objects are rebuilt when their source
+or any csrc header is newer.  Usage: ``python -m nanodecoder_amd.build``.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+INCLUDE = os.path.join(os.path.dirname(HERE), "include")
+BUILD = os.path.join(HERE, "_build")
+LIB = os.path.join(HERE, "libnanodec_hip.so")
+ARCH = os.environ.get("NANODEC_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+CFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-Wall",
+          "-Wno-unused-function", "-Wno-unused-variable", "-I" + CSRC, "-I" + INCLUDE]
+
+
+def _newest_dep():
+    deps = glob.glob(os.path.join(CSRC, "*.hpp")) + glob.glob(os.path.join(INCLUDE, "*.h"))
+    return max((os.path.getmtime(p) for p in deps), default=0.0)
+
+
+def _compile(src, obj, verbose):
+    cmd = [HIPCC] + CFLAGS + ["-c", src, "-o", obj]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {os.path.basename(src)}:\n{r.stdout}\n{r.stderr}")
+    if r.stderr.strip() and verbose:
+        print(r.stderr, file=sys.stderr)
+    return obj
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+    dep_t = _newest_dep()
+    jobs = []
+    objs = []
+    for src in srcs:
+        obj = os.path.join(BUILD, os.path.basename(src)[:-4] + ".o")
+        objs.append(obj)
+        if force or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(src), dep_t):
+            jobs.append((src, obj))
+    if jobs:
+        with cf.ThreadPoolExecutor(max_workers=min(8, len(jobs))) as ex:
+            list(ex.map(lambda a: _compile(a[0], a[1], verbose), jobs))
+    if jobs or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,363 @@
+// Attention and row kernels of the translate path (gfx950).
+//
+// * enc_attention: the Transformer encoder's self-attention
+//   (onmt/modules/multi_headed_attn.py:154-177 with the key mask of
+//   encoder/transformer.py:117-121, ``src == 0.0``).  One workgroup owns one
+//   (chunk, head): all of that head's K (row-major) and V (transposed) sit in
+//   LDS (<= 512 keys, 140 KB), and 16 waves each stream 32 queries through
+//   them with fp32 MFMA and an online softmax — the [T, T] score matrix the
+//   reference materialises is never written.  Scores are computed transposed
+//   (S^T = K Q^T) so a query's 32 keys live in one lane's accumulator
+//   registers: the row max/sum is 15 register ops + one cross-half shuffle,
+//   and the exponentiated tile is directly the B operand of the P.V MFMA.
+// * dec_self_attention / dec_ctx_attention: the decoder's q_len = 1
+//   attention (multi_headed_attn.py:124-153 cache modes), bandwidth bound.
+#include "common.hpp"
+#include "kernels.hpp"
+
+namespace nd {
+
+// ------------------------------------------------------------------ encoder
+__global__ void __launch_bounds__(256)
+enc_embed_kernel(const float* __restrict__ signal, const float* __restrict__ w, const float* __restrict__ b,
+                 float* __restrict__ x, int n_rows) {
+  // encoder/transformer.py:104,113 — Linear(1, d) applied to the scalar sample
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= n_rows) return;
+  const float s = signal[row];
+  const f32x4 wv = ld4(w + lane * 4), bv = ld4(b + lane * 4);
+  st4(x + (size_t)row * ND_D + lane * 4, s * wv + bv);
+}
+
+hipError_t launch_enc_embed(const float* signal, const float* w_in, const float* b_in, float* x, int B, int T,
+                            hipStream_t s) {
+  const int rows = B * T;
+  hipLaunchKernelGGL(enc_embed_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, signal, w_in, b_in, x, rows);
+  return hipGetLastError();
+}
+
+__global__ void __launch_bounds__(256)
+layernorm_kernel(const float* __restrict__ x, const float* __restrict__ g, const float* __restrict__ b,
+                 float* __restrict__ out, int rows) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  f32x4 v = ld4(x + (size_t)row * ND_D + lane * 4);
+  const float mu = wave_sum(v.x + v.y + v.z + v.w) * (1.0f / ND_D);
+  const f32x4 d = v - mu;
+  const float var = wave_sum(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w) * (1.0f / ND_D);
+  const float rs = 1.0f / sqrtf(var + ND_LN_EPS);
+  st4(out + (size_t)row * ND_D + lane * 4, d * rs * ld4(g + lane * 4) + ld4(b + lane * 4));
+}
+
+hipError_t launch_layernorm(const float* x, const float* g, const float* b, float* out, int rows, hipStream_t s) {
+  if (rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(layernorm_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, x, g, b, out, rows);
+  return hipGetLastError();
+}
+
+#define ENC_MAXT 512
+#define ENC_KLD 36    // K row stride (floats): conflict-free ds_read_b128
+#define ENC_VLD 516   // V^T row stride
+
+__global__ void __launch_bounds__(1024)
+enc_attention_kernel(const float* __restrict__ qkv, const float* __restrict__ signal, const int* __restrict__ span,
+                     float* __restrict__ out, int T) {
+  __shared__ __attribute__((aligned(16))) float Ks[ENC_MAXT * ENC_KLD];
+  __shared__ __attribute__((aligned(16))) float Vt[ND_DH * ENC_VLD];
+  __shared__ int kflag[ENC_MAXT];  // 0 = key, 1 = masked (signal == 0), 2 = absent (t >= span)
+
+  const int h = blockIdx.x, b = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int L = min(span[b], T);
+  const int nkt = (L + 31) >> 5;
+  const size_t base = (size_t)b * T;
+
+  for (int idx = tid; idx < nkt * 32 * 8; idx += 1024) {
+    const int t = idx >> 3, c = (idx & 7) * 4;
+    f32x4 k = {0.f, 0.f, 0.f, 0.f}, v = {0.f, 0.f, 0.f, 0.f};
+    if (t < L) {
+      const float* row = qkv + (base + t) * (3 * ND_D) + h * ND_DH + c;
+      k = ld4(row + ND_D);
+      v = ld4(row + 2 * ND_D);
+    }
+    st4(&Ks[t * ENC_KLD + c], k);
+    Vt[(c + 0) * ENC_VLD + t] = v.x;
+    Vt[(c + 1) * ENC_VLD + t] = v.y;
+    Vt[(c + 2) * ENC_VLD + t] = v.z;
+    Vt[(c + 3) * ENC_VLD + t] = v.w;
+  }
+  for (int t = tid; t < nkt * 32; t += 1024) kflag[t] = t < L ? (signal[base + t] == 0.0f ? 1 : 0) : 2;
+  __syncthreads();
+
+  const int q0 = wave * 32;
+  if (q0 >= L) return;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int q = q0 + lr;
+  const int qc = min(q, T - 1);
+
+  // query fragment: step s = 4j+i uses d = 8j + 4*lh + i; pre-scaled like
+  // ``query / math.sqrt(dim_per_head)`` (multi_headed_attn.py:167)
+  f32x4 qf[4];
+  {
+    const float* qrow = qkv + (base + qc) * (3 * ND_D) + h * ND_DH + 4 * lh;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) qf[j] = ld4(qrow + 8 * j) / ND_SQRT_DH;
+  }
+
+  f32x16 o;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) o[r] = 0.f;
+  float m = -INFINITY, l = 0.f;
+
+  for (int kt = 0; kt < nkt; ++kt) {
+    f32x16 sacc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
+    const float* krow = &Ks[(kt * 32 + lr) * ENC_KLD + 4 * lh];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f32x4 kf = ld4(krow + 8 * j);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sacc = mfma32(kf[i], qf[j][i], sacc);
+    }
+    // sacc[r] = score(query q, key kt*32 + mfma32_row(r, lane))
+    float mx = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int f = kflag[kt * 32 + mfma32_row(r, lane)];
+      float sv = sacc[r];
+      sv = f == 1 ? ND_MASK_FILL : sv;
+      sv = f == 2 ? -INFINITY : sv;
+      sacc[r] = sv;
+      mx = fmaxf(mx, sv);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float alpha = __expf(m - mn);
+    float rsum = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      sacc[r] = __expf(sacc[r] - mn);
+      rsum += sacc[r];
+    }
+    rsum += __shfl_xor(rsum, 32, 64);
+    l = l * alpha + rsum;
+    m = mn;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[r] *= alpha;
+    // O^T[d][q] += V^T[d][key] P^T[key][q]; step s = 4j+i uses key 8j + 4*lh + i
+    const float* vrow = &Vt[lr * ENC_VLD + kt * 32 + 4 * lh];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f32x4 vf = ld4(vrow + 8 * j);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o = mfma32(vf[i], sacc[4 * j + i], o);
+    }
+  }
+  if (q < L) {
+    const float inv = 1.0f / l;
+    float* orow = out + (base + q) * ND_D + h * ND_DH + 4 * lh;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      f32x4 v = {o[4 * g + 0] * inv, o[4 * g + 1] * inv, o[4 * g + 2] * inv, o[4 * g + 3] * inv};
+      st4(orow + 8 * g, v);
+    }
+  }
+}
+
+hipError_t launch_enc_attention(const float* qkv, const float* signal, const int* span, float* out, int B, int T,
+                                hipStream_t s) {
+  if (T > ENC_MAXT || T <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(enc_attention_kernel, dim3(ND_H, B), dim3(1024), 0, s, qkv, signal, span, out, T);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ decoder
+__global__ void __launch_bounds__(256)
+dec_embed_kernel(const int* __restrict__ tok, const float* __restrict__ emb, const float* __restrict__ pe, int step,
+                 float* __restrict__ x, int R) {
+  // onmt/modules/embeddings.py:189-207 (+ PositionalEncoding.forward :36-43)
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= R) return;
+  f32x4 e = ld4(emb + (size_t)tok[row] * ND_D + lane * 4);
+  if (pe) e = e * 16.0f + ld4(pe + (size_t)step * ND_D + lane * 4);  // sqrt(256) = 16
+  st4(x + (size_t)row * ND_D + lane * 4, e);
+}
+
+hipError_t launch_dec_embed(const int* tok, const float* emb, const float* pe, int step, float* x, int R,
+                            hipStream_t s) {
+  hipLaunchKernelGGL(dec_embed_kernel, dim3((R + 3) / 4), dim3(256), 0, s, tok, emb, pe, step, x, R);
+  return hipGetLastError();
+}
+
+// One workgroup (256 threads) per decoder row.  cache layout:
+// [slot][t][512] = k (256) | v (256).
+__global__ void __launch_bounds__(256)
+dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cache, const int* __restrict__ anc,
+                          int anc_ld, int step, int S, float* __restrict__ out) {
+  __shared__ float p[ND_H][256];
+  __shared__ int slot[256];
+  const int r = blockIdx.x, tid = threadIdx.x;
+  const float* qrow = qkv + (size_t)r * 3 * ND_D;
+  // append this step's k, v (multi_headed_attn.py:124-141)
+  float* mine = cache + ((size_t)r * S + step) * 2 * ND_D;
+  mine[tid] = qrow[ND_D + tid];
+  mine[ND_D + tid] = qrow[2 * ND_D + tid];
+  const int n = step + 1;
+  for (int t = tid; t < n; t += 256) slot[t] = (anc && t < step) ? anc[(size_t)r * anc_ld + t] : r;
+  __syncthreads();
+  // scores: thread handles (head, key) pairs; 8 heads x n keys
+  for (int e = tid; e < ND_H * n; e += 256) {
+    const int hh = e / n, t = e - hh * n;
+    const float* kr = (t == step) ? (mine + hh * ND_DH) : (cache + ((size_t)slot[t] * S + t) * 2 * ND_D + hh * ND_DH);
+    const float* qh = qrow + hh * ND_DH;
+    float acc = 0.f;
+#pragma unroll
+    for (int d = 0; d < ND_DH; d += 4) {
+      const f32x4 a = ld4(qh + d) / ND_SQRT_DH, k = ld4(kr + d);
+      acc += a.x * k.x + a.y * k.y + a.z * k.z + a.w * k.w;
+    }
+    p[hh][t] = acc;
+  }
+  __syncthreads();
+  // softmax per head: wave w handles heads w, w+4
+  const int wave = tid >> 6, lane = tid & 63;
+  for (int hh = wave; hh < ND_H; hh += 4) {
+    float mx = -INFINITY;
+    for (int t = lane; t < n; t += 64) mx = fmaxf(mx, p[hh][t]);
+    mx = wave_max(mx);
+    float sm = 0.f;
+    for (int t = lane; t < n; t += 64) {
+      const float e = __expf(p[hh][t] - mx);
+      p[hh][t] = e;
+      sm += e;
+    }
+    sm = wave_sum(sm);
+    const float inv = 1.0f / sm;
+    for (int t = lane; t < n; t += 64) p[hh][t] *= inv;
+  }
+  __syncthreads();
+  const int hh = tid / ND_DH;
+  float acc = 0.f;
+  for (int t = 0; t < n; ++t) {
+    const float* vr = (t == step) ? mine : cache + ((size_t)slot[t] * S + t) * 2 * ND_D;
+    acc += p[hh][t] * vr[ND_D + tid];
+  }
+  out[(size_t)r * ND_D + tid] = acc;
+}
+
+hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* anc, int anc_ld, int step,
+                                     int max_steps, float* out, int R, hipStream_t s) {
+  if (step >= max_steps || step >= 256) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(dec_self_attention_kernel, dim3(R), dim3(256), 0, s, qkv, cache, anc, anc_ld, step, max_steps,
+                     out);
+  return hipGetLastError();
+}
+
+// Context attention, one workgroup (512 threads) per chunk: the chunk's
+// context K/V stream from HBM once for all of its rows (beam rows share the
+// same memory bank, translate/translator.py:667-676 tiles it only logically).
+#define CTX_THREADS 512
+#define CTX_MAXR 8
+__global__ void __launch_bounds__(CTX_THREADS)
+dec_ctx_attention_kernel(const float* __restrict__ q, const float* __restrict__ kv, int ld, int koff,
+                         const float* __restrict__ signal, const int* __restrict__ span, float pad_val,
+                         float* __restrict__ out, int rpc, int T) {
+  extern __shared__ float sm[];
+  float* sc = sm;                                   // [rpc][8][T]
+  float* part = sm + rpc * ND_H * T;                // [8 waves][rpc][256]
+  const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int L = min(span[c], T);
+  const size_t base = (size_t)c * T;
+  // lane owns dims 4*lane..4*lane+3 of every row; head = lane / 8
+  f32x4 qv[CTX_MAXR];
+#pragma unroll
+  for (int j = 0; j < CTX_MAXR; ++j)
+    if (j < rpc) qv[j] = ld4(q + ((size_t)c * rpc + j) * ND_D + lane * 4) / ND_SQRT_DH;
+  // pass 1: scores (mask src == pad_idx, decoder/transformer.py:220-221)
+  for (int t = wave; t < L; t += CTX_THREADS / 64) {
+    const f32x4 k = ld4(kv + (base + t) * ld + koff + lane * 4);
+    const bool masked = signal[base + t] == pad_val;
+#pragma unroll
+    for (int j = 0; j < CTX_MAXR; ++j) {
+      if (j < rpc) {
+        float d = qv[j].x * k.x + qv[j].y * k.y + qv[j].z * k.z + qv[j].w * k.w;
+        d += __shfl_xor(d, 1, 64);
+        d += __shfl_xor(d, 2, 64);
+        d += __shfl_xor(d, 4, 64);
+        if ((lane & 7) == 0) sc[(j * ND_H + (lane >> 3)) * T + t] = masked ? ND_MASK_FILL : d;
+      }
+    }
+  }
+  __syncthreads();
+  // softmax over keys for each (row, head)
+  for (int rh = wave; rh < rpc * ND_H; rh += CTX_THREADS / 64) {
+    float* s = sc + rh * T;
+    float mx = -INFINITY;
+    for (int t = lane; t < L; t += 64) mx = fmaxf(mx, s[t]);
+    mx = wave_max(mx);
+    float sum = 0.f;
+    for (int t = lane; t < L; t += 64) {
+      const float e = __expf(s[t] - mx);
+      s[t] = e;
+      sum += e;
+    }
+    sum = wave_sum(sum);
+    const float inv = 1.0f / sum;
+    for (int t = lane; t < L; t += 64) s[t] *= inv;
+  }
+  __syncthreads();
+  // pass 2: out[j] = sum_t p[j][head][t] * V[t]
+  f32x4 acc[CTX_MAXR];
+#pragma unroll
+  for (int j = 0; j < CTX_MAXR; ++j) acc[j] = {0.f, 0.f, 0.f, 0.f};
+  const int hh = lane >> 3;
+  for (int t = wave; t < L; t += CTX_THREADS / 64) {
+    const f32x4 v = ld4(kv + (base + t) * ld + koff + ND_D + lane * 4);
+#pragma unroll
+    for (int j = 0; j < CTX_MAXR; ++j)
+      if (j < rpc) acc[j] += sc[(j * ND_H + hh) * T + t] * v;
+  }
+#pragma unroll
+  for (int j = 0; j < CTX_MAXR; ++j)
+    if (j < rpc) st4(part + ((size_t)wave * rpc + j) * ND_D + lane * 4, acc[j]);
+  __syncthreads();
+  for (int e = tid; e < rpc * ND_D; e += CTX_THREADS) {
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < CTX_THREADS / 64; ++w) v += part[(size_t)w * rpc * ND_D + e];
+    out[(size_t)c * rpc * ND_D + e] = v;
+  }
+}
+
+hipError_t launch_dec_ctx_attention(const float* q, const float* kv, int ld, int koff, const float* signal,
+                                    const int* span, float pad_val, float* out, int C, int rpc, int T,
+                                    hipStream_t s) {
+  if (rpc > CTX_MAXR || T > 512) return hipErrorInvalidValue;
+  const size_t lds = ((size_t)rpc * ND_H * T + (size_t)(CTX_THREADS / 64) * rpc * ND_D) * sizeof(float);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(dec_ctx_attention_kernel, dim3(C), dim3(CTX_THREADS), lds, s, q, kv, ld, koff, signal, span,
+                     pad_val, out, rpc, T);
+  return hipGetLastError();
+}
+
+}  // namespace nd
+
+namespace nd {
+
+__global__ void fill_i32_kernel(int* p, int v, int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+hipError_t launch_fill_i32(int* p, int v, int n, hipStream_t s) {
+  hipLaunchKernelGGL(fill_i32_kernel, dim3((n + 255) / 256), dim3(256), 0, s, p, v, n);
+  return hipGetLastError();
+}
+
+hipError_t init_kernel_attributes() {
+  return hipFuncSetAttribute((const void*)dec_ctx_attention_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             160 * 1024);
+}
+
+}  // namespace nd

@@ -1,0 +1,711 @@
+// libnanodec_hip.so — engine context, weight registry, launch sequences,
+// hipGraph capture and the C-ABI of include/nanodec.h.
+//
+// One nd_ctx per device.  It owns:
+//   * the packed fp32 weights (QKV of each attention fused into one [768,256]
+//     matrix; the three decoder layers' context K/V projections fused into one
+//     [3*512, 256] matrix so the memory bank is projected by ONE GEMM),
+//   * encoder/decoder workspaces sized for (max_batch, max_src_len,
+//     max_steps, max_beam),
+//   * instantiated hipGraphs of whole translate calls, keyed by shape.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "../../include/nanodec.h"
+#include "common.hpp"
+#include "kernels.hpp"
+
+namespace nd {
+hipError_t init_kernel_attributes();
+hipError_t launch_fill_i32(int* p, int v, int n, hipStream_t s);
+}  // namespace nd
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                          \
+  do {                                                                                        \
+    hipError_t e_ = (expr);                                                                   \
+    if (e_ != hipSuccess)                                                                     \
+      return fail(ND_ERR_HIP, std::string(#expr) + " failed: " + hipGetErrorString(e_));      \
+  } while (0)
+
+struct Slot {
+  float* dst = nullptr;
+  std::vector<int64_t> shape;  // expected shape
+  size_t numel = 0;
+  bool loaded = false;
+  bool required = true;
+  int copy_rows = -1;  // >= 0: copy only the first copy_rows rows (pe table)
+};
+
+struct EncLayer {
+  float *ln_g, *ln_b, *wqkv, *bqkv, *wo, *bo, *fln_g, *fln_b, *w1, *b1, *w2, *b2;
+};
+struct DecLayer {
+  float *ln1_g, *ln1_b, *wqkv, *bqkv, *wo, *bo, *ln2_g, *ln2_b, *cwq, *cbq, *cwo, *cbo, *fln_g, *fln_b, *w1, *b1,
+      *w2, *b2;
+};
+struct NanoLayer {
+  float *wih, *bih, *bhh, *whh, *bn_g, *bn_b, *bn_rm, *bn_rv;  // raw
+  float *bsum, *bn_scale, *bn_shift;                             // derived at finalize
+  int in;
+};
+
+struct GraphKey {
+  int mode, B, T, S, min_len, beam, n_best, seg, logp;
+  float alpha;
+  bool operator<(const GraphKey& o) const {
+    return std::tie(mode, B, T, S, min_len, beam, n_best, seg, logp, alpha) <
+           std::tie(o.mode, o.B, o.T, o.S, o.min_len, o.beam, o.n_best, o.seg, o.logp, o.alpha);
+  }
+};
+
+struct nd_ctx {
+  nd_config cfg{};
+  int D = ND_D, F = 2048, V = 8, H = 128;
+  std::map<std::string, Slot> slots;
+  std::vector<void*> allocs;
+  bool finalized = false;
+  bool use_graphs = true;
+  bool timing = false;
+  float t_enc = 0.f, t_dec = 0.f;
+
+  // weights
+  float *enc_lin_w = nullptr, *enc_lin_b = nullptr, *enc_ln_g = nullptr, *enc_ln_b = nullptr;
+  std::vector<EncLayer> enc;
+  std::vector<NanoLayer> nano;
+  float* nano_W = nullptr;
+  std::vector<DecLayer> dec;
+  float *ctxkv_w = nullptr, *ctxkv_b = nullptr;
+  float *emb = nullptr, *pe = nullptr, *dec_ln_g = nullptr, *dec_ln_b = nullptr, *gen_w = nullptr, *gen_b = nullptr;
+
+  // workspaces
+  float* sig = nullptr;
+  int *len = nullptr, *span = nullptr;
+  float *x = nullptr, *y = nullptr, *att = nullptr, *big = nullptr, *ctxkv = nullptr;
+  float *nano_xp = nullptr, *nano_h = nullptr;
+  float *dx = nullptr, *dq1 = nullptr, *dmid = nullptr, *dcq = nullptr, *datt = nullptr, *dqkv = nullptr,
+        *dhid = nullptr, *cache = nullptr;
+  int *tok = nullptr, *gtok = nullptr;
+  float *gscore = nullptr, *glogp = nullptr;
+  nd::BeamState bs{};
+  int* steps_done = nullptr;
+  int* h_alive = nullptr;  // pinned
+
+  hipStream_t es = nullptr;
+  hipEvent_t ev_in = nullptr, ev_out = nullptr, ev_a = nullptr, ev_b = nullptr, ev_c = nullptr;
+  std::map<GraphKey, hipGraphExec_t> graphs;
+};
+
+// ------------------------------------------------------------------ helpers
+template <typename T>
+static hipError_t dalloc(nd_ctx* c, T** p, size_t n) {
+  void* q = nullptr;
+  hipError_t e = hipMalloc(&q, n * sizeof(T) + 256);
+  if (e != hipSuccess) return e;
+  e = hipMemset(q, 0, n * sizeof(T) + 256);
+  c->allocs.push_back(q);
+  *p = reinterpret_cast<T*>(q);
+  return e;
+}
+
+static void add_slot(nd_ctx* c, const std::string& name, float* dst, std::vector<int64_t> shape, bool required = true,
+                     int copy_rows = -1) {
+  Slot s;
+  s.dst = dst;
+  s.shape = shape;
+  s.numel = 1;
+  for (auto d : shape) s.numel *= (size_t)d;
+  s.required = required;
+  s.copy_rows = copy_rows;
+  c->slots[name] = s;
+}
+
+static int build_registry(nd_ctx* c) {
+  const int D = c->D, F = c->F, V = c->V;
+  const auto& cfg = c->cfg;
+  hipError_t e;
+#define AL(ptr, n)                                          \
+  if ((e = dalloc(c, &(ptr), (size_t)(n))) != hipSuccess) \
+    return fail(ND_ERR_HIP, std::string("hipMalloc weights: ") + hipGetErrorString(e));
+  if (cfg.encoder_type == ND_ENC_TRANSFORMER) {
+    AL(c->enc_lin_w, D);
+    AL(c->enc_lin_b, D);
+    AL(c->enc_ln_g, D);
+    AL(c->enc_ln_b, D);
+    add_slot(c, "encoder.linear.weight", c->enc_lin_w, {D, 1});
+    add_slot(c, "encoder.linear.bias", c->enc_lin_b, {D});
+    add_slot(c, "encoder.layer_norm.weight", c->enc_ln_g, {D});
+    add_slot(c, "encoder.layer_norm.bias", c->enc_ln_b, {D});
+    c->enc.resize(cfg.enc_layers);
+    for (int i = 0; i < cfg.enc_layers; ++i) {
+      EncLayer& L = c->enc[i];
+      AL(L.ln_g, D); AL(L.ln_b, D); AL(L.wqkv, 3 * D * D); AL(L.bqkv, 3 * D); AL(L.wo, D * D); AL(L.bo, D);
+      AL(L.fln_g, D); AL(L.fln_b, D); AL(L.w1, (size_t)F * D); AL(L.b1, F); AL(L.w2, (size_t)D * F); AL(L.b2, D);
+      const std::string p = "encoder.transformer." + std::to_string(i);
+      add_slot(c, p + ".layer_norm.weight", L.ln_g, {D});
+      add_slot(c, p + ".layer_norm.bias", L.ln_b, {D});
+      const char* qkv[3] = {"linear_query", "linear_keys", "linear_values"};
+      for (int k = 0; k < 3; ++k) {
+        add_slot(c, p + ".self_attn." + qkv[k] + ".weight", L.wqkv + (size_t)k * D * D, {D, D});
+        add_slot(c, p + ".self_attn." + qkv[k] + ".bias", L.bqkv + k * D, {D});
+      }
+      add_slot(c, p + ".self_attn.final_linear.weight", L.wo, {D, D});
+      add_slot(c, p + ".self_attn.final_linear.bias", L.bo, {D});
+      add_slot(c, p + ".feed_forward.layer_norm.weight", L.fln_g, {D});
+      add_slot(c, p + ".feed_forward.layer_norm.bias", L.fln_b, {D});
+      add_slot(c, p + ".feed_forward.w_1.weight", L.w1, {F, D});
+      add_slot(c, p + ".feed_forward.w_1.bias", L.b1, {F});
+      add_slot(c, p + ".feed_forward.w_2.weight", L.w2, {D, F});
+      add_slot(c, p + ".feed_forward.w_2.bias", L.b2, {D});
+    }
+  } else {
+    const int Hh = c->H;
+    c->nano.resize(cfg.enc_layers);
+    for (int l = 0; l < cfg.enc_layers; ++l) {
+      NanoLayer& L = c->nano[l];
+      L.in = l == 0 ? 1 : 2 * Hh;
+      AL(L.wih, (size_t)8 * Hh * L.in); AL(L.bih, 8 * Hh); AL(L.bhh, 8 * Hh); AL(L.whh, (size_t)8 * Hh * Hh);
+      AL(L.bn_g, 2 * Hh); AL(L.bn_b, 2 * Hh); AL(L.bn_rm, 2 * Hh); AL(L.bn_rv, 2 * Hh);
+      AL(L.bsum, 8 * Hh); AL(L.bn_scale, 2 * Hh); AL(L.bn_shift, 2 * Hh);
+      const std::string p = "encoder.rnn_" + std::to_string(l);
+      const char* sfx[2] = {"", "_reverse"};
+      for (int d = 0; d < 2; ++d) {
+        add_slot(c, p + ".weight_ih_l0" + sfx[d], L.wih + (size_t)d * 4 * Hh * L.in, {4 * Hh, L.in});
+        add_slot(c, p + ".weight_hh_l0" + sfx[d], L.whh + (size_t)d * 4 * Hh * Hh, {4 * Hh, Hh});
+        add_slot(c, p + ".bias_ih_l0" + sfx[d], L.bih + d * 4 * Hh, {4 * Hh});
+        add_slot(c, p + ".bias_hh_l0" + sfx[d], L.bhh + d * 4 * Hh, {4 * Hh});
+      }
+      const std::string b = "encoder.batchnorm_" + std::to_string(l);
+      add_slot(c, b + ".weight", L.bn_g, {2 * Hh});
+      add_slot(c, b + ".bias", L.bn_b, {2 * Hh});
+      add_slot(c, b + ".running_mean", L.bn_rm, {2 * Hh});
+      add_slot(c, b + ".running_var", L.bn_rv, {2 * Hh});
+    }
+    AL(c->nano_W, (size_t)D * 2 * Hh);
+    add_slot(c, "encoder.W.weight", c->nano_W, {D, 2 * Hh});
+  }
+  c->dec.resize(cfg.dec_layers);
+  AL(c->ctxkv_w, (size_t)cfg.dec_layers * 2 * D * D);
+  AL(c->ctxkv_b, (size_t)cfg.dec_layers * 2 * D);
+  for (int i = 0; i < cfg.dec_layers; ++i) {
+    DecLayer& L = c->dec[i];
+    AL(L.ln1_g, D); AL(L.ln1_b, D); AL(L.wqkv, 3 * D * D); AL(L.bqkv, 3 * D); AL(L.wo, D * D); AL(L.bo, D);
+    AL(L.ln2_g, D); AL(L.ln2_b, D); AL(L.cwq, D * D); AL(L.cbq, D); AL(L.cwo, D * D); AL(L.cbo, D);
+    AL(L.fln_g, D); AL(L.fln_b, D); AL(L.w1, (size_t)F * D); AL(L.b1, F); AL(L.w2, (size_t)D * F); AL(L.b2, D);
+    const std::string p = "decoder.transformer_layers." + std::to_string(i);
+    add_slot(c, p + ".layer_norm_1.weight", L.ln1_g, {D});
+    add_slot(c, p + ".layer_norm_1.bias", L.ln1_b, {D});
+    add_slot(c, p + ".layer_norm_2.weight", L.ln2_g, {D});
+    add_slot(c, p + ".layer_norm_2.bias", L.ln2_b, {D});
+    const char* qkv[3] = {"linear_query", "linear_keys", "linear_values"};
+    for (int k = 0; k < 3; ++k) {
+      add_slot(c, p + ".self_attn." + qkv[k] + ".weight", L.wqkv + (size_t)k * D * D, {D, D});
+      add_slot(c, p + ".self_attn." + qkv[k] + ".bias", L.bqkv + k * D, {D});
+    }
+    add_slot(c, p + ".self_attn.final_linear.weight", L.wo, {D, D});
+    add_slot(c, p + ".self_attn.final_linear.bias", L.bo, {D});
+    add_slot(c, p + ".context_attn.linear_query.weight", L.cwq, {D, D});
+    add_slot(c, p + ".context_attn.linear_query.bias", L.cbq, {D});
+    add_slot(c, p + ".context_attn.linear_keys.weight", c->ctxkv_w + (size_t)(2 * i) * D * D, {D, D});
+    add_slot(c, p + ".context_attn.linear_keys.bias", c->ctxkv_b + (2 * i) * D, {D});
+    add_slot(c, p + ".context_attn.linear_values.weight", c->ctxkv_w + (size_t)(2 * i + 1) * D * D, {D, D});
+    add_slot(c, p + ".context_attn.linear_values.bias", c->ctxkv_b + (2 * i + 1) * D, {D});
+    add_slot(c, p + ".context_attn.final_linear.weight", L.cwo, {D, D});
+    add_slot(c, p + ".context_attn.final_linear.bias", L.cbo, {D});
+    add_slot(c, p + ".feed_forward.layer_norm.weight", L.fln_g, {D});
+    add_slot(c, p + ".feed_forward.layer_norm.bias", L.fln_b, {D});
+    add_slot(c, p + ".feed_forward.w_1.weight", L.w1, {F, D});
+    add_slot(c, p + ".feed_forward.w_1.bias", L.b1, {F});
+    add_slot(c, p + ".feed_forward.w_2.weight", L.w2, {D, F});
+    add_slot(c, p + ".feed_forward.w_2.bias", L.b2, {D});
+  }
+  AL(c->emb, (size_t)V * D);
+  add_slot(c, "decoder.embeddings.make_embedding.emb_luts.0.weight", c->emb, {V, D});
+  if (cfg.position_encoding) {
+    AL(c->pe, (size_t)cfg.max_steps * D);
+    add_slot(c, "decoder.embeddings.make_embedding.pe.pe", c->pe, {-1, 1, D}, true, cfg.max_steps);
+  }
+  AL(c->dec_ln_g, D);
+  AL(c->dec_ln_b, D);
+  add_slot(c, "decoder.layer_norm.weight", c->dec_ln_g, {D});
+  add_slot(c, "decoder.layer_norm.bias", c->dec_ln_b, {D});
+  AL(c->gen_w, (size_t)V * D);
+  AL(c->gen_b, V);
+  add_slot(c, "generator.0.weight", c->gen_w, {V, D});
+  add_slot(c, "generator.0.bias", c->gen_b, {V});
+#undef AL
+  return ND_OK;
+}
+
+static int alloc_workspaces(nd_ctx* c) {
+  const auto& cfg = c->cfg;
+  const size_t B = cfg.max_batch, T = cfg.max_src_len, S = cfg.max_steps;
+  const size_t R = B * (size_t)std::max(1, cfg.max_beam);
+  const size_t D = c->D, F = c->F, Ld = cfg.dec_layers;
+  hipError_t e;
+#define WS(ptr, n)                                          \
+  if ((e = dalloc(c, &(ptr), (size_t)(n))) != hipSuccess) \
+    return fail(ND_ERR_HIP, std::string("hipMalloc workspace " #ptr ": ") + hipGetErrorString(e));
+  WS(c->sig, B * T);
+  WS(c->len, B);
+  WS(c->span, B);
+  WS(c->x, B * T * D);
+  WS(c->y, B * T * D);
+  WS(c->att, B * T * D);
+  WS(c->big, B * T * std::max(F, 3 * D));
+  WS(c->ctxkv, B * T * Ld * 2 * D);
+  if (cfg.encoder_type == ND_ENC_NANO) {
+    WS(c->nano_xp, B * T * 8 * (size_t)c->H);
+    WS(c->nano_h, B * T * 2 * (size_t)c->H);
+  }
+  WS(c->dx, R * D);
+  WS(c->dq1, R * D);
+  WS(c->dmid, R * D);
+  WS(c->dcq, R * D);
+  WS(c->datt, R * D);
+  WS(c->dqkv, R * 3 * D);
+  WS(c->dhid, R * F);
+  WS(c->cache, Ld * R * S * 2 * D);
+  WS(c->tok, R);
+  WS(c->gtok, B * S);
+  WS(c->gscore, B);
+  WS(c->glogp, B * S * (size_t)c->V);
+  WS(c->bs.cum, R);
+  WS(c->bs.seq[0], R * S);
+  WS(c->bs.seq[1], R * S);
+  WS(c->bs.anc[0], R * S);
+  WS(c->bs.anc[1], R * S);
+  c->bs.tok = c->tok;
+  WS(c->bs.done, B);
+  WS(c->bs.top_fin, B);
+  WS(c->bs.n_hyp, B);
+  const size_t NB = (size_t)std::max(1, cfg.max_beam);
+  WS(c->bs.hyp_score, B * NB);
+  WS(c->bs.hyp_len, B * NB);
+  WS(c->bs.hyp_tok, B * NB * S);
+  WS(c->bs.n_alive, 4);
+  WS(c->steps_done, 4);
+#undef WS
+  if ((e = hipHostMalloc((void**)&c->h_alive, 16, hipHostMallocDefault)) != hipSuccess)
+    return fail(ND_ERR_HIP, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+  return ND_OK;
+}
+
+// ------------------------------------------------------------ launch sequences
+#define LCHK(expr)                                                                    \
+  do {                                                                                \
+    hipError_t e_ = (expr);                                                           \
+    if (e_ != hipSuccess) {                                                           \
+      g_err = std::string(#expr) + ": " + hipGetErrorString(e_);                      \
+      return e_;                                                                      \
+    }                                                                                 \
+  } while (0)
+
+static hipError_t gemm(const float* A, int lda, const float* W, int N, int K, const float* bias, float* C, int ldc,
+                       int M, hipStream_t s, const float* ln_g = nullptr, const float* ln_b = nullptr,
+                       bool relu = false, const float* R = nullptr, int ldr = 0) {
+  nd::GemmArgs g;
+  g.A = A; g.lda = lda; g.W = W; g.ldw = K; g.bias = bias; g.R = R; g.ldr = ldr; g.C = C; g.ldc = ldc;
+  g.ln_g = ln_g; g.ln_b = ln_b; g.M = M; g.N = N; g.K = K; g.relu = relu;
+  return nd::launch_gemm(g, s);
+}
+
+// Encoder forward (transformer): x <- memory pre-final-LN; then the fused
+// context K/V projection of all decoder layers with the final LN as prologue.
+static hipError_t enqueue_encode_transformer(nd_ctx* c, int B, int T, hipStream_t s) {
+  const int M = B * T, D = c->D, F = c->F;
+  LCHK(nd::launch_enc_embed(c->sig, c->enc_lin_w, c->enc_lin_b, c->x, B, T, s));
+  for (auto& L : c->enc) {
+    // encoder/transformer.py:36-54
+    LCHK(gemm(c->x, D, L.wqkv, 3 * D, D, L.bqkv, c->big, 3 * D, M, s, L.ln_g, L.ln_b));
+    LCHK(nd::launch_enc_attention(c->big, c->sig, c->span, c->att, B, T, s));
+    LCHK(gemm(c->att, D, L.wo, D, D, L.bo, c->y, D, M, s, nullptr, nullptr, false, c->x, D));
+    LCHK(gemm(c->y, D, L.w1, F, D, L.b1, c->big, F, M, s, L.fln_g, L.fln_b, true));
+    LCHK(gemm(c->big, F, L.w2, D, F, L.b2, c->x, D, M, s, nullptr, nullptr, false, c->y, D));
+  }
+  return hipSuccess;
+}
+
+static hipError_t enqueue_ctxkv(nd_ctx* c, int B, int T, hipStream_t s) {
+  const int M = B * T, D = c->D, N = (int)c->dec.size() * 2 * D;
+  if (c->cfg.encoder_type == ND_ENC_TRANSFORMER)
+    return gemm(c->x, D, c->ctxkv_w, N, D, c->ctxkv_b, c->ctxkv, N, M, s, c->enc_ln_g, c->enc_ln_b);
+  return gemm(c->x, D, c->ctxkv_w, N, D, c->ctxkv_b, c->ctxkv, N, M, s);
+}
+
+static hipError_t enqueue_encode(nd_ctx* c, int B, int T, hipStream_t s);
+
+// One decoder step for R = C*rpc rows: tok -> dx (pre final LN).
+static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, const int* anc, int anc_ld,
+                                   hipStream_t s) {
+  const int R = C * rpc, D = c->D, F = c->F, S = c->cfg.max_steps;
+  const int Ld = (int)c->dec.size();
+  LCHK(nd::launch_dec_embed(c->tok, c->emb, c->cfg.position_encoding ? c->pe : nullptr, step, c->dx, R, s));
+  for (int i = 0; i < Ld; ++i) {
+    DecLayer& L = c->dec[i];
+    float* cache = c->cache + (size_t)i * R * S * 2 * D;
+    // decoder/transformer.py:53-95
+    LCHK(gemm(c->dx, D, L.wqkv, 3 * D, D, L.bqkv, c->dqkv, 3 * D, R, s, L.ln1_g, L.ln1_b));
+    LCHK(nd::launch_dec_self_attention(c->dqkv, cache, anc, anc_ld, step, S, c->datt, R, s));
+    LCHK(gemm(c->datt, D, L.wo, D, D, L.bo, c->dq1, D, R, s, nullptr, nullptr, false, c->dx, D));
+    LCHK(gemm(c->dq1, D, L.cwq, D, D, L.cbq, c->dcq, D, R, s, L.ln2_g, L.ln2_b));
+    LCHK(nd::launch_dec_ctx_attention(c->dcq, c->ctxkv, Ld * 2 * D, i * 2 * D, c->sig, c->span,
+                                      (float)c->cfg.pad_idx, c->datt, C, rpc, T, s));
+    LCHK(gemm(c->datt, D, L.cwo, D, D, L.cbo, c->dmid, D, R, s, nullptr, nullptr, false, c->dq1, D));
+    LCHK(gemm(c->dmid, D, L.w1, F, D, L.b1, c->dhid, F, R, s, L.fln_g, L.fln_b, true));
+    LCHK(gemm(c->dhid, F, L.w2, D, F, L.b2, c->dx, D, R, s, nullptr, nullptr, false, c->dmid, D));
+  }
+  return hipSuccess;
+}
+
+static hipError_t enqueue_greedy(nd_ctx* c, int B, int T, int S, int min_len, bool logp, hipStream_t s) {
+  LCHK(enqueue_encode(c, B, T, s));
+  LCHK(enqueue_ctxkv(c, B, T, s));
+  LCHK(nd::launch_fill_i32(c->tok, c->cfg.bos_idx, B, s));
+  for (int step = 0; step < S; ++step) {
+    LCHK(enqueue_dec_step(c, B, 1, T, step, nullptr, 0, s));
+    LCHK(nd::launch_dec_greedy_head(c->dx, c->dec_ln_g, c->dec_ln_b, c->gen_w, c->gen_b, c->V, step, S, min_len,
+                                    c->cfg.eos_idx, c->tok, c->gtok, c->gscore, logp ? c->glogp : nullptr, B, s));
+  }
+  return hipSuccess;
+}
+
+static hipError_t enqueue_beam_steps(nd_ctx* c, int B, int T, int beam, int n_best, float alpha, int S, int min_len,
+                                     int s0, int s1, hipStream_t s) {
+  for (int step = s0; step < s1; ++step) {
+    const int cur = step & 1;
+    LCHK(enqueue_dec_step(c, B, beam, T, step, c->bs.anc[cur], S, s));
+    const float lenpen = (float)std::pow((5.0 + (step + 1)) / 6.0, (double)alpha);
+    LCHK(nd::launch_beam_step(c->dx, c->dec_ln_g, c->dec_ln_b, c->gen_w, c->gen_b, c->V, c->bs, B, beam, n_best,
+                              step, S, min_len, c->cfg.eos_idx, lenpen, s));
+  }
+  return hipSuccess;
+}
+
+// --------------------------------------------------------------- graphs
+template <typename F>
+static int run_graph(nd_ctx* c, const GraphKey& key, F&& enqueue) {
+  if (!c->use_graphs) {
+    hipError_t e = enqueue(c->es);
+    if (e != hipSuccess) return fail(ND_ERR_HIP, g_err.empty() ? hipGetErrorString(e) : g_err);
+    return ND_OK;
+  }
+  auto it = c->graphs.find(key);
+  if (it == c->graphs.end()) {
+    hipGraph_t g = nullptr;
+    HIPCHK(hipStreamBeginCapture(c->es, hipStreamCaptureModeRelaxed));
+    hipError_t e = enqueue(c->es);
+    hipError_t e2 = hipStreamEndCapture(c->es, &g);
+    if (e != hipSuccess) {
+      if (g) (void)hipGraphDestroy(g);
+      return fail(ND_ERR_HIP, "capture: " + g_err);
+    }
+    if (e2 != hipSuccess) return fail(ND_ERR_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(e2));
+    hipGraphExec_t ex = nullptr;
+    e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (e != hipSuccess) return fail(ND_ERR_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
+    it = c->graphs.emplace(key, ex).first;
+  }
+  HIPCHK(hipGraphLaunch(it->second, c->es));
+  return ND_OK;
+}
+
+// --------------------------------------------------------------- C-ABI
+extern "C" {
+
+const char* nd_last_error(void) { return g_err.c_str(); }
+const char* nd_version(void) { return "nanodec_hip 0.1.0 gfx950 fp32-mfma"; }
+
+int nd_create(const nd_config* cfg, nd_ctx** out) {
+  if (!cfg || !out) return fail(ND_ERR_ARG, "null argument");
+  *out = nullptr;
+  if (cfg->d_model != ND_D || cfg->heads != ND_H) return fail(ND_ERR_ARG, "only d_model=256, heads=8 are compiled");
+  if (cfg->d_ff <= 0 || cfg->d_ff % 128) return fail(ND_ERR_ARG, "d_ff must be a positive multiple of 128");
+  if (cfg->vocab < 4 || cfg->vocab > ND_MAXV) return fail(ND_ERR_ARG, "vocab must be in [4, 32]");
+  if (cfg->max_src_len < 1 || cfg->max_src_len > 512) return fail(ND_ERR_ARG, "max_src_len must be in [1, 512]");
+  if (cfg->max_steps < 1 || cfg->max_steps > 256) return fail(ND_ERR_ARG, "max_steps must be in [1, 256]");
+  if (cfg->max_beam < 1 || cfg->max_beam > 6) return fail(ND_ERR_ARG, "max_beam must be in [1, 6]");
+  if (cfg->max_batch < 1) return fail(ND_ERR_ARG, "max_batch must be >= 1");
+  if (cfg->enc_layers < 1 || cfg->dec_layers < 1) return fail(ND_ERR_ARG, "layers must be >= 1");
+  if (cfg->encoder_type != ND_ENC_TRANSFORMER && cfg->encoder_type != ND_ENC_NANO)
+    return fail(ND_ERR_ARG, "unknown encoder_type");
+  if (cfg->encoder_type == ND_ENC_NANO && cfg->rnn_hidden != 128) return fail(ND_ERR_ARG, "rnn_hidden must be 128");
+  HIPCHK(hipSetDevice(cfg->device));
+  nd_ctx* c = new nd_ctx();
+  c->cfg = *cfg;
+  c->F = cfg->d_ff;
+  c->V = cfg->vocab;
+  c->H = cfg->rnn_hidden;
+  int rc = build_registry(c);
+  if (rc == ND_OK) rc = alloc_workspaces(c);
+  if (rc != ND_OK) {
+    nd_destroy(c);
+    return rc;
+  }
+  hipError_t e = nd::init_kernel_attributes();
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->es, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_out, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreate(&c->ev_a);
+  if (e == hipSuccess) e = hipEventCreate(&c->ev_b);
+  if (e == hipSuccess) e = hipEventCreate(&c->ev_c);
+  if (e != hipSuccess) {
+    nd_destroy(c);
+    return fail(ND_ERR_HIP, std::string("stream/event setup: ") + hipGetErrorString(e));
+  }
+  *out = c;
+  return ND_OK;
+}
+
+int nd_load_weight(nd_ctx* c, const char* name, const float* host, const int64_t* shape, int ndim) {
+  if (!c || !name || !host || (!shape && ndim > 0)) return fail(ND_ERR_ARG, "null argument");
+  const std::string n(name);
+  auto it = c->slots.find(n);
+  if (it == c->slots.end()) {
+    auto ends = [&](const char* sfx) {
+      const size_t k = strlen(sfx);
+      return n.size() >= k && n.compare(n.size() - k, k, sfx) == 0;
+    };
+    if (ends(".mask") || ends("num_batches_tracked")) return ND_OK;  // buffers the engine does not use
+    if (!c->cfg.position_encoding && n == "decoder.embeddings.make_embedding.pe.pe") return ND_OK;
+    return fail(ND_ERR_WEIGHT, "unknown weight '" + n + "'");
+  }
+  Slot& s = it->second;
+  if ((size_t)ndim != s.shape.size()) return fail(ND_ERR_WEIGHT, "rank mismatch for '" + n + "'");
+  size_t numel = 1;
+  for (int i = 0; i < ndim; ++i) {
+    if (s.shape[i] >= 0 && shape[i] != s.shape[i]) return fail(ND_ERR_WEIGHT, "shape mismatch for '" + n + "'");
+    numel *= (size_t)shape[i];
+  }
+  size_t copy = numel;
+  if (s.copy_rows >= 0) {
+    if (shape[0] < s.copy_rows) return fail(ND_ERR_WEIGHT, "'" + n + "' has fewer rows than max_steps");
+    copy = (size_t)s.copy_rows * (numel / (size_t)shape[0]);
+  }
+  HIPCHK(hipSetDevice(c->cfg.device));
+  HIPCHK(hipMemcpy(s.dst, host, copy * sizeof(float), hipMemcpyHostToDevice));
+  s.loaded = true;
+  c->finalized = false;
+  return ND_OK;
+}
+
+int nd_finalize(nd_ctx* c) {
+  if (!c) return fail(ND_ERR_ARG, "null ctx");
+  std::string missing;
+  for (auto& kv : c->slots)
+    if (kv.second.required && !kv.second.loaded) missing += (missing.empty() ? "" : ", ") + kv.first;
+  if (!missing.empty()) return fail(ND_ERR_WEIGHT, "missing weights: " + missing);
+  HIPCHK(hipSetDevice(c->cfg.device));
+  if (c->cfg.encoder_type == ND_ENC_NANO) {
+    // derived: b_ih + b_hh per gate; eval BatchNorm as scale/shift
+    const int Hh = c->H;
+    for (auto& L : c->nano) {
+      std::vector<float> bih(8 * Hh), bhh(8 * Hh), g(2 * Hh), b(2 * Hh), rm(2 * Hh), rv(2 * Hh);
+      HIPCHK(hipMemcpy(bih.data(), L.bih, bih.size() * 4, hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(bhh.data(), L.bhh, bhh.size() * 4, hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(g.data(), L.bn_g, g.size() * 4, hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(b.data(), L.bn_b, b.size() * 4, hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(rm.data(), L.bn_rm, rm.size() * 4, hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(rv.data(), L.bn_rv, rv.size() * 4, hipMemcpyDeviceToHost));
+      std::vector<float> bs(8 * Hh), sc(2 * Hh), sh(2 * Hh);
+      for (int i = 0; i < 8 * Hh; ++i) bs[i] = bih[i] + bhh[i];
+      for (int i = 0; i < 2 * Hh; ++i) {
+        sc[i] = (float)(1.0 / std::sqrt((double)rv[i] + 1e-5)) * g[i];
+        sh[i] = b[i] - rm[i] * sc[i];
+      }
+      HIPCHK(hipMemcpy(L.bsum, bs.data(), bs.size() * 4, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(L.bn_scale, sc.data(), sc.size() * 4, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(L.bn_shift, sh.data(), sh.size() * 4, hipMemcpyHostToDevice));
+    }
+  }
+  for (auto& kv : c->graphs) (void)hipGraphExecDestroy(kv.second);
+  c->graphs.clear();
+  c->finalized = true;
+  return ND_OK;
+}
+
+static int check_call(nd_ctx* c, int B, int T, int S) {
+  if (!c) return fail(ND_ERR_ARG, "null ctx");
+  if (!c->finalized) return fail(ND_ERR_STATE, "nd_finalize has not been called");
+  if (B < 1 || B > c->cfg.max_batch) return fail(ND_ERR_ARG, "B out of range [1, max_batch]");
+  if (T < 1 || T > c->cfg.max_src_len) return fail(ND_ERR_ARG, "T out of range [1, max_src_len]");
+  if (S < 1 || S > c->cfg.max_steps) return fail(ND_ERR_ARG, "max_len out of range [1, max_steps]");
+  return ND_OK;
+}
+
+static int stage_inputs(nd_ctx* c, const float* sig, const int32_t* len, const int32_t* span, int B, int T,
+                        hipStream_t cs) {
+  HIPCHK(hipSetDevice(c->cfg.device));
+  HIPCHK(hipEventRecord(c->ev_in, cs));
+  HIPCHK(hipStreamWaitEvent(c->es, c->ev_in, 0));
+  HIPCHK(hipMemcpyAsync(c->sig, sig, (size_t)B * T * 4, hipMemcpyDeviceToDevice, c->es));
+  HIPCHK(hipMemcpyAsync(c->len, len, (size_t)B * 4, hipMemcpyDeviceToDevice, c->es));
+  HIPCHK(hipMemcpyAsync(c->span, span, (size_t)B * 4, hipMemcpyDeviceToDevice, c->es));
+  return ND_OK;
+}
+
+static int release_to(nd_ctx* c, hipStream_t cs) {
+  HIPCHK(hipEventRecord(c->ev_out, c->es));
+  HIPCHK(hipStreamWaitEvent(cs, c->ev_out, 0));
+  return ND_OK;
+}
+
+int nd_translate_greedy(nd_ctx* c, const float* d_signal, const int32_t* d_len, const int32_t* d_span, int32_t B,
+                        int32_t T, int32_t max_len, int32_t min_len, int32_t* d_tokens, float* d_score, float* d_logp,
+                        void* stream) {
+  int rc = check_call(c, B, T, max_len);
+  if (rc) return rc;
+  if (!d_signal || !d_len || !d_span || !d_tokens || !d_score) return fail(ND_ERR_ARG, "null buffer");
+  hipStream_t cs = (hipStream_t)stream;
+  if ((rc = stage_inputs(c, d_signal, d_len, d_span, B, T, cs))) return rc;
+  const bool lp = d_logp != nullptr;
+  GraphKey key{0, B, T, max_len, min_len, 1, 1, 0, lp ? 1 : 0, 0.f};
+  if (c->timing) HIPCHK(hipEventRecord(c->ev_a, c->es));
+  rc = run_graph(c, key, [&](hipStream_t s) { return enqueue_greedy(c, B, T, max_len, min_len, lp, s); });
+  if (rc) return rc;
+  if (c->timing) HIPCHK(hipEventRecord(c->ev_b, c->es));
+  HIPCHK(hipMemcpyAsync(d_tokens, c->gtok, (size_t)B * max_len * 4, hipMemcpyDeviceToDevice, c->es));
+  HIPCHK(hipMemcpyAsync(d_score, c->gscore, (size_t)B * 4, hipMemcpyDeviceToDevice, c->es));
+  if (lp) HIPCHK(hipMemcpyAsync(d_logp, c->glogp, (size_t)B * max_len * c->V * 4, hipMemcpyDeviceToDevice, c->es));
+  if (c->timing) {
+    HIPCHK(hipEventSynchronize(c->ev_b));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, c->ev_a, c->ev_b));
+    c->t_enc = 0.f;
+    c->t_dec = ms;
+  }
+  return release_to(c, cs);
+}
+
+int nd_translate_beam(nd_ctx* c, const float* d_signal, const int32_t* d_len, const int32_t* d_span, int32_t B,
+                      int32_t T, int32_t beam, int32_t n_best, float alpha, int32_t max_len, int32_t min_len,
+                      int32_t* d_tokens, float* d_scores, int32_t* d_lens, int32_t* d_steps, void* stream) {
+  int rc = check_call(c, B, T, max_len);
+  if (rc) return rc;
+  if (beam < 1 || beam > c->cfg.max_beam) return fail(ND_ERR_ARG, "beam out of range [1, max_beam]");
+  if (n_best < 1 || n_best > beam) return fail(ND_ERR_ARG, "n_best out of range [1, beam]");
+  if (c->V < beam) return fail(ND_ERR_ARG, "vocab smaller than beam");
+  if (!d_signal || !d_len || !d_span || !d_tokens || !d_scores || !d_lens) return fail(ND_ERR_ARG, "null buffer");
+  hipStream_t cs = (hipStream_t)stream;
+  if ((rc = stage_inputs(c, d_signal, d_len, d_span, B, T, cs))) return rc;
+  // n_best hypothesis storage is sized by max_beam
+  const int SEG = 10;
+  GraphKey k0{1, B, T, max_len, min_len, beam, n_best, -1, 0, alpha};
+  if (c->timing) HIPCHK(hipEventRecord(c->ev_a, c->es));
+  rc = run_graph(c, k0, [&](hipStream_t s) -> hipError_t {
+    LCHK(enqueue_encode(c, B, T, s));
+    LCHK(enqueue_ctxkv(c, B, T, s));
+    LCHK(nd::launch_beam_init(c->bs, B, beam, n_best, max_len, c->cfg.bos_idx, s));
+    LCHK(nd::launch_fill_i32(c->steps_done, max_len, 1, s));
+    return hipSuccess;
+  });
+  if (rc) return rc;
+  if (c->timing) HIPCHK(hipEventRecord(c->ev_b, c->es));
+  for (int s0 = 0; s0 < max_len; s0 += SEG) {
+    const int s1 = std::min(max_len, s0 + SEG);
+    GraphKey k{1, B, T, max_len, min_len, beam, n_best, s0, 0, alpha};
+    rc = run_graph(c, k, [&](hipStream_t s) {
+      return enqueue_beam_steps(c, B, T, beam, n_best, alpha, max_len, min_len, s0, s1, s);
+    });
+    if (rc) return rc;
+    if (s1 < max_len) {
+      HIPCHK(hipMemcpyAsync(c->h_alive, c->bs.n_alive, 4, hipMemcpyDeviceToHost, c->es));
+      HIPCHK(hipStreamSynchronize(c->es));
+      if (*c->h_alive == 0) break;
+    }
+  }
+  if (c->timing) HIPCHK(hipEventRecord(c->ev_c, c->es));
+  HIPCHK(nd::launch_beam_finish(c->bs, B, n_best, max_len, d_tokens, d_scores, d_lens, c->es));
+  if (d_steps) HIPCHK(hipMemcpyAsync(d_steps, c->steps_done, 4, hipMemcpyDeviceToDevice, c->es));
+  if (c->timing) {
+    HIPCHK(hipEventSynchronize(c->ev_c));
+    HIPCHK(hipEventElapsedTime(&c->t_enc, c->ev_a, c->ev_b));
+    HIPCHK(hipEventElapsedTime(&c->t_dec, c->ev_b, c->ev_c));
+  }
+  return release_to(c, cs);
+}
+
+int nd_encode(nd_ctx* c, const float* d_signal, const int32_t* d_len, const int32_t* d_span, int32_t B, int32_t T,
+              float* d_memory, void* stream) {
+  int rc = check_call(c, B, T, 1);
+  if (rc) return rc;
+  hipStream_t cs = (hipStream_t)stream;
+  if ((rc = stage_inputs(c, d_signal, d_len, d_span, B, T, cs))) return rc;
+  hipError_t e = enqueue_encode(c, B, T, c->es);
+  if (e != hipSuccess) return fail(ND_ERR_HIP, g_err);
+  if (c->cfg.encoder_type == ND_ENC_TRANSFORMER) {
+    e = nd::launch_layernorm(c->x, c->enc_ln_g, c->enc_ln_b, d_memory, B * T, c->es);
+    if (e != hipSuccess) return fail(ND_ERR_HIP, hipGetErrorString(e));
+  } else {
+    HIPCHK(hipMemcpyAsync(d_memory, c->x, (size_t)B * T * c->D * 4, hipMemcpyDeviceToDevice, c->es));
+  }
+  return release_to(c, cs);
+}
+
+int nd_set_graphs(nd_ctx* c, int enable) {
+  if (!c) return fail(ND_ERR_ARG, "null ctx");
+  c->use_graphs = enable != 0;
+  return ND_OK;
+}
+
+int nd_set_timing(nd_ctx* c, int enable) {
+  if (!c) return fail(ND_ERR_ARG, "null ctx");
+  c->timing = enable != 0;
+  return ND_OK;
+}
+
+int nd_last_timing(nd_ctx* c, float* encode_ms, float* decode_ms) {
+  if (!c) return fail(ND_ERR_ARG, "null ctx");
+  if (encode_ms) *encode_ms = c->t_enc;
+  if (decode_ms) *decode_ms = c->t_dec;
+  return ND_OK;
+}
+
+void nd_destroy(nd_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->cfg.device);
+  if (c->es) (void)hipStreamSynchronize(c->es);
+  for (auto& kv : c->graphs) (void)hipGraphExecDestroy(kv.second);
+  for (void* p : c->allocs) (void)hipFree(p);
+  if (c->h_alive) (void)hipHostFree(c->h_alive);
+  for (hipEvent_t e : {c->ev_in, c->ev_out, c->ev_a, c->ev_b, c->ev_c})
+    if (e) (void)hipEventDestroy(e);
+  if (c->es) (void)hipStreamDestroy(c->es);
+  delete c;
+}
+
+int nd_op_gemm(const float* A, const float* W, const float* bias, const float* R, float* C, int32_t M, int32_t N,
+               int32_t K, const float* ln_g, const float* ln_b, int32_t relu, void* stream) {
+  hipError_t e = gemm(A, K, W, N, K, bias, C, N, M, (hipStream_t)stream, ln_g, ln_b, relu != 0, R, N);
+  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("gemm: ") + hipGetErrorString(e));
+  return ND_OK;
+}
+
+int nd_op_enc_attention(const float* qkv, const float* signal, const int32_t* span, float* out, int32_t B, int32_t T,
+                        void* stream) {
+  hipError_t e = nd::launch_enc_attention(qkv, signal, span, out, B, T, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("enc_attention: ") + hipGetErrorString(e));
+  return ND_OK;
+}
+
+}  // extern "C"
+
+static hipError_t enqueue_encode(nd_ctx* c, int B, int T, hipStream_t s) {
+  if (c->cfg.encoder_type == ND_ENC_TRANSFORMER) return enqueue_encode_transformer(c, B, T, s);
+  g_err = "NanoEncoder path not built yet";
+  return hipErrorNotSupported;
+}

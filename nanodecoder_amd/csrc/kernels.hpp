@@ -1,0 +1,74 @@
+// Host-side launchers of the gfx950 kernels (one definition per .hip file).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace nd {
+
+struct GemmArgs {
+  const float* A = nullptr;
+  int lda = 0;
+  const float* W = nullptr;  // [N, K] row-major (torch Linear layout)
+  int ldw = 0;
+  const float* bias = nullptr;
+  const float* R = nullptr;  // residual [M, N]
+  int ldr = 0;
+  float* C = nullptr;
+  int ldc = 0;
+  const float* ln_g = nullptr;  // LayerNorm prologue over K (K == 256)
+  const float* ln_b = nullptr;
+  int M = 0, N = 0, K = 0;
+  bool relu = false;
+};
+hipError_t launch_gemm(const GemmArgs& g, hipStream_t s);
+
+// ---- encoder -------------------------------------------------------------
+// x[b*T+t][:] = signal[b][t] * w_in + b_in                (Linear(1, d))
+hipError_t launch_enc_embed(const float* signal, const float* w_in, const float* b_in, float* x, int B, int T,
+                            hipStream_t s);
+// flash attention over qkv [B*T, 768]; mask signal==0; keys >= span excluded
+hipError_t launch_enc_attention(const float* qkv, const float* signal, const int* span, float* out, int B, int T,
+                                hipStream_t s);
+// out[r] = LN(x[r]) (rows of 256)
+hipError_t launch_layernorm(const float* x, const float* g, const float* b, float* out, int rows, hipStream_t s);
+
+// ---- decoder -------------------------------------------------------------
+struct DecStepArgs;
+hipError_t launch_dec_embed(const int* tok, const float* emb, const float* pe, int step, float* x, int R,
+                            hipStream_t s);
+// self attention: writes k,v of this step into cache[slot=r][step], attends
+// over the row's history cache[anc[r][t]][t] (anc == nullptr: identity).
+hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* anc, int anc_ld, int step,
+                                     int max_steps, float* out, int R, hipStream_t s);
+// context attention: rows r = c*rpc + j attend over ctxkv rows of chunk c
+// (K at kv[(c*T+t)*ld + koff], V at +256), mask signal == pad_val, keys < span.
+hipError_t launch_dec_ctx_attention(const float* q, const float* kv, int ld, int koff, const float* signal,
+                                    const int* span, float pad_val, float* out, int C, int rpc, int T,
+                                    hipStream_t s);
+// greedy head: LN_dec -> generator -> log_softmax -> argmax; writes token
+// (next input + output [R, S] at column step), score, optional logp dump.
+hipError_t launch_dec_greedy_head(const float* x, const float* ln_g, const float* ln_b, const float* gw,
+                                  const float* gb, int V, int step, int S, int min_len, int eos, int* tok,
+                                  int* out_tokens, float* score, float* logp_dump, int R, hipStream_t s);
+
+struct BeamState {
+  float* cum;        // [C, beam] topk_log_probs
+  int* seq[2];       // [C*beam, S] alive_seq (without BOS), double buffered
+  int* anc[2];       // [C*beam, S] self-attn cache slot ancestry, double buffered
+  int* tok;          // [C*beam] next decoder input
+  int* done;         // [C]
+  int* top_fin;      // [C]
+  int* n_hyp;        // [C] hypotheses found so far
+  float* hyp_score;  // [C, n_best]
+  int* hyp_len;      // [C, n_best]
+  int* hyp_tok;      // [C, n_best, S]
+  int* n_alive;      // [1] chunks not done
+};
+hipError_t launch_beam_init(const BeamState& st, int C, int beam, int n_best, int S, int bos, hipStream_t s);
+hipError_t launch_beam_step(const float* x, const float* ln_g, const float* ln_b, const float* gw, const float* gb,
+                            int V, const BeamState& st, int C, int beam, int n_best, int step, int S, int min_len,
+                            int eos, float lenpen, hipStream_t s);
+hipError_t launch_beam_finish(const BeamState& st, int C, int n_best, int S, int* tokens, float* scores, int* lens,
+                              hipStream_t s);
+
+}  // namespace nd

@@ -1,0 +1,242 @@
+// Decoder output head and search (gfx950): final LayerNorm + generator
+// (Linear + LogSoftmax, models/model_builder.py:326-334) fused with greedy
+// argmax (translate/translator.py:371-394,455-483) or with one --fast beam
+// step (translate/translator.py:701-823) including the finished-hypothesis
+// bookkeeping the reference does on the host.  Every step stays on the
+// device; the host only polls a one-int "chunks alive" counter.
+#include "common.hpp"
+#include "kernels.hpp"
+
+namespace nd {
+
+// LN + generator + log_softmax for one 256-float row held by one wave
+// (lane owns dims 4*lane..4*lane+3).  Writes logp[0..V) to `lp` (LDS or regs via lane-uniform values).
+__device__ __forceinline__ void head_row(const float* __restrict__ x, const float* __restrict__ ln_g,
+                                         const float* __restrict__ ln_b, const float* __restrict__ gw,
+                                         const float* __restrict__ gb, int V, int lane, float* lp) {
+  f32x4 v = ld4(x + lane * 4);
+  const float mu = wave_sum(v.x + v.y + v.z + v.w) * (1.0f / ND_D);
+  const f32x4 d = v - mu;
+  const float var = wave_sum(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w) * (1.0f / ND_D);
+  const float rs = 1.0f / sqrtf(var + ND_LN_EPS);
+  const f32x4 y = d * rs * ld4(ln_g + lane * 4) + ld4(ln_b + lane * 4);
+  float mx = -INFINITY;
+  for (int k = 0; k < V; ++k) {
+    const f32x4 w = ld4(gw + (size_t)k * ND_D + lane * 4);
+    const float logit = wave_sum(y.x * w.x + y.y * w.y + y.z * w.z + y.w * w.w) + gb[k];
+    lp[k] = logit;
+    mx = fmaxf(mx, logit);
+  }
+  // torch log_softmax: (x - max) - log(sum(exp(x - max)))
+  float s = 0.f;
+  for (int k = 0; k < V; ++k) s += expf(lp[k] - mx);
+  const float ls = logf(s);
+  for (int k = 0; k < V; ++k) lp[k] = (lp[k] - mx) - ls;
+}
+
+__global__ void __launch_bounds__(256)
+greedy_head_kernel(const float* __restrict__ x, const float* __restrict__ ln_g, const float* __restrict__ ln_b,
+                   const float* __restrict__ gw, const float* __restrict__ gb, int V, int step, int S, int min_len,
+                   int eos, int* __restrict__ tok, int* __restrict__ out_tokens, float* __restrict__ score,
+                   float* __restrict__ logp_dump, int R) {
+  __shared__ float lps[4][ND_MAXV];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + w;
+  if (r >= R) return;
+  float* lp = lps[w];
+  head_row(x + (size_t)r * ND_D, ln_g, ln_b, gw, gb, V, lane, lp);
+  if (lane == 0) {
+    if (logp_dump)
+      for (int k = 0; k < V; ++k) logp_dump[((size_t)r * S + step) * V + k] = lp[k];
+    if (step < min_len) lp[eos] = -1e20f;
+    int best = 0;
+    float bv = lp[0];
+    for (int k = 1; k < V; ++k)
+      if (lp[k] > bv) {  // first index wins ties (topk(1))
+        bv = lp[k];
+        best = k;
+      }
+    tok[r] = best;
+    out_tokens[(size_t)r * S + step] = best;
+    score[r] = bv;
+  }
+}
+
+hipError_t launch_dec_greedy_head(const float* x, const float* ln_g, const float* ln_b, const float* gw,
+                                  const float* gb, int V, int step, int S, int min_len, int eos, int* tok,
+                                  int* out_tokens, float* score, float* logp_dump, int R, hipStream_t s) {
+  if (V > ND_MAXV) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(greedy_head_kernel, dim3((R + 3) / 4), dim3(256), 0, s, x, ln_g, ln_b, gw, gb, V, step, S,
+                     min_len, eos, tok, out_tokens, score, logp_dump, R);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ beam
+#define BEAM_MAX 8
+
+__global__ void __launch_bounds__(64)
+beam_init_kernel(BeamState st, int C, int beam, int bos) {
+  const int c = blockIdx.x * 64 + threadIdx.x;
+  if (c >= C) return;
+  for (int j = 0; j < beam; ++j) {
+    st.cum[c * beam + j] = j == 0 ? 0.f : -INFINITY;  // translator.py:691-693
+    st.tok[c * beam + j] = bos;
+  }
+  st.done[c] = 0;
+  st.top_fin[c] = 0;
+  st.n_hyp[c] = 0;
+  if (c == 0) *st.n_alive = C;
+}
+
+hipError_t launch_beam_init(const BeamState& st, int C, int beam, int n_best, int S, int bos, hipStream_t s) {
+  (void)n_best;
+  (void)S;
+  hipLaunchKernelGGL(beam_init_kernel, dim3((C + 63) / 64), dim3(64), 0, s, st, C, beam, bos);
+  return hipGetLastError();
+}
+
+// One workgroup (256 threads = 4 waves) per chunk.
+__global__ void __launch_bounds__(256)
+beam_step_kernel(const float* __restrict__ x, const float* __restrict__ ln_g, const float* __restrict__ ln_b,
+                 const float* __restrict__ gw, const float* __restrict__ gb, int V, BeamState st, int beam,
+                 int n_best, int step, int S, int min_len, int eos, float lenpen) {
+  __shared__ float lp[BEAM_MAX][ND_MAXV];
+  __shared__ float tsc[BEAM_MAX];
+  __shared__ int tid_sel[BEAM_MAX];
+  __shared__ int fin[BEAM_MAX];
+  const int c = blockIdx.x, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  if (st.done[c]) return;  // finished batches are dropped (translator.py:793-810)
+  const int cur = step & 1, nxt = cur ^ 1;
+  const int row0 = c * beam;
+  for (int j = w; j < beam; j += 4) {
+    head_row(x + (size_t)(row0 + j) * ND_D, ln_g, ln_b, gw, gb, V, lane, lp[j]);
+    if (lane == 0) {
+      if (step < min_len) lp[j][eos] = -1e20f;          // :712-713
+      const float cj = st.cum[row0 + j];
+      for (int k = 0; k < V; ++k) lp[j][k] = (lp[j][k] + cj) / lenpen;  // :718-724
+    }
+  }
+  __syncthreads();
+  if (w == 0) {
+    // top-`beam` over the flattened beam*V candidates, ties -> lower index
+    const int n = beam * V;
+    unsigned long long taken = 0ull;  // n <= 256; track per lane below
+    bool tk[4] = {false, false, false, false};
+    for (int sel = 0; sel < beam; ++sel) {
+      float bv = -INFINITY;
+      int bi = 0x7fffffff;
+      for (int q = 0; q < 4; ++q) {
+        const int idx = lane + 64 * q;
+        if (idx < n && !tk[q]) {
+          const float v = lp[idx / V][idx % V];
+          if (v > bv || (v == bv && idx < bi)) {
+            bv = v;
+            bi = idx;
+          }
+        }
+      }
+      for (int o = 32; o > 0; o >>= 1) {
+        const float ov = __shfl_xor(bv, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (ov > bv || (ov == bv && oi < bi)) {
+          bv = ov;
+          bi = oi;
+        }
+      }
+      if (bi != 0x7fffffff && (bi & 63) == lane) tk[bi >> 6] = true;
+      if (lane == 0) {
+        tsc[sel] = bv;
+        tid_sel[sel] = bi;
+      }
+    }
+    (void)taken;
+  }
+  __syncthreads();
+  // reorder alive_seq / ancestry (index_select by origin beam, :737-744, :812-823)
+  for (int e = tid; e < beam * (step + 1); e += 256) {
+    const int j = e / (step + 1), t = e - j * (step + 1);
+    const int par = tid_sel[j] / V;
+    const int src = row0 + par, dst = row0 + j;
+    if (t < step) {
+      st.seq[nxt][(size_t)dst * S + t] = st.seq[cur][(size_t)src * S + t];
+      st.anc[nxt][(size_t)dst * S + t] = st.anc[cur][(size_t)src * S + t];
+    } else {
+      st.seq[nxt][(size_t)dst * S + t] = tid_sel[j] % V;
+      st.anc[nxt][(size_t)dst * S + t] = src;  // row `src` wrote this step's self K/V
+    }
+  }
+  if (tid < beam) {
+    const int tok = tid_sel[tid] % V;
+    fin[tid] = (tok == eos || step + 1 == S) ? 1 : 0;  // :750-752
+    st.tok[row0 + tid] = tok;
+    st.cum[row0 + tid] = fin[tid] ? -1e10f : tsc[tid] * lenpen;  // :728, :756
+  }
+  __syncthreads();
+  if (tid == 0) {
+    bool any = false;
+    for (int j = 0; j < beam; ++j) any |= fin[j] != 0;
+    if (any) {
+      if (fin[0]) st.top_fin[c] = 1;  // :758
+      int nh = st.n_hyp[c];
+      for (int j = 0; j < beam; ++j) {
+        if (!fin[j]) continue;
+        // stable insert into the best-first list (sorted(..., reverse=True), :784-786)
+        const float sc = tsc[j];
+        const int kept = min(nh, n_best);
+        int pos = 0;
+        while (pos < kept && st.hyp_score[c * n_best + pos] >= sc) ++pos;
+        if (pos < n_best) {
+          const int last = min(kept, n_best - 1);
+          for (int q = last; q > pos; --q) {
+            st.hyp_score[c * n_best + q] = st.hyp_score[c * n_best + q - 1];
+            st.hyp_len[c * n_best + q] = st.hyp_len[c * n_best + q - 1];
+            for (int t = 0; t < S; ++t)
+              st.hyp_tok[((size_t)c * n_best + q) * S + t] = st.hyp_tok[((size_t)c * n_best + q - 1) * S + t];
+          }
+          st.hyp_score[c * n_best + pos] = sc;
+          st.hyp_len[c * n_best + pos] = step + 1;
+          for (int t = 0; t <= step; ++t)
+            st.hyp_tok[((size_t)c * n_best + pos) * S + t] = st.seq[nxt][(size_t)(row0 + j) * S + t];
+        }
+        ++nh;
+      }
+      st.n_hyp[c] = nh;
+      if (st.top_fin[c] && nh >= n_best) {  // :780
+        st.done[c] = 1;
+        atomicSub(st.n_alive, 1);
+      }
+    }
+  }
+}
+
+hipError_t launch_beam_step(const float* x, const float* ln_g, const float* ln_b, const float* gw, const float* gb,
+                            int V, const BeamState& st, int C, int beam, int n_best, int step, int S, int min_len,
+                            int eos, float lenpen, hipStream_t s) {
+  if (beam > BEAM_MAX || beam * V > 256 || V > ND_MAXV) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(beam_step_kernel, dim3(C), dim3(256), 0, s, x, ln_g, ln_b, gw, gb, V, st, beam, n_best, step,
+                     S, min_len, eos, lenpen);
+  return hipGetLastError();
+}
+
+__global__ void __launch_bounds__(256)
+beam_finish_kernel(BeamState st, int n_best, int S, int* __restrict__ tokens, float* __restrict__ scores,
+                   int* __restrict__ lens) {
+  const int c = blockIdx.x;
+  for (int e = threadIdx.x; e < n_best * S; e += 256) {
+    const int nb = e / S, t = e - nb * S;
+    const int len = st.hyp_len[c * n_best + nb];
+    tokens[((size_t)c * n_best + nb) * S + t] = t < len ? st.hyp_tok[((size_t)c * n_best + nb) * S + t] : -1;
+  }
+  if (threadIdx.x < n_best) {
+    scores[c * n_best + threadIdx.x] = st.hyp_score[c * n_best + threadIdx.x];
+    lens[c * n_best + threadIdx.x] = st.hyp_len[c * n_best + threadIdx.x];
+  }
+}
+
+hipError_t launch_beam_finish(const BeamState& st, int C, int n_best, int S, int* tokens, float* scores, int* lens,
+                              hipStream_t s) {
+  hipLaunchKernelGGL(beam_finish_kernel, dim3(C), dim3(256), 0, s, st, n_best, S, tokens, scores, lens);
+  return hipGetLastError();
+}
+
+}  // namespace nd

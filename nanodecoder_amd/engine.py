@@ -1,0 +1,160 @@
+"""Python face of the HIP engine: one ``Engine`` per GPU.
+
+PyTorch-ROCm is used as plumbing only — device memory for inputs/outputs and
+the current HIP stream; all compute runs in libnanodec_hip.so.
+
+The Engine takes weights by reference state-dict name (see ``checkpoint.py``
+for loading .pt files) and translates batches of signal chunks already
+resident on the device.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from .synth import ModelConfig
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class Engine:
+    """MI355X translate engine for one device (C-ABI context owner)."""
+
+    def __init__(self, cfg: ModelConfig, weights: Dict[str, np.ndarray], device: int = 0, max_batch: int = 256,
+                 max_src_len: int = 512, max_steps: int = 100, max_beam: int = 1, graphs: bool = True):
+        self.cfg = cfg
+        self.device = torch.device("cuda", device)
+        self.max_batch, self.max_src_len, self.max_steps, self.max_beam = max_batch, max_src_len, max_steps, max_beam
+        L = _lib.lib()
+        c = _lib.NdConfig()
+        c.encoder_type = _lib.ND_ENC_TRANSFORMER if cfg.encoder_type == "transformer" else _lib.ND_ENC_NANO
+        c.enc_layers, c.dec_layers = cfg.enc_layers, cfg.dec_layers
+        c.d_model, c.heads, c.d_ff, c.vocab = cfg.d_model, cfg.heads, cfg.d_ff, cfg.vocab
+        c.rnn_hidden = cfg.rnn_hidden
+        c.position_encoding = int(bool(cfg.position_encoding))
+        c.pad_idx, c.bos_idx, c.eos_idx = cfg.pad_idx, cfg.bos_idx, cfg.eos_idx
+        c.max_batch, c.max_src_len, c.max_steps, c.max_beam = max_batch, max_src_len, max_steps, max_beam
+        c.device = device
+        h = ctypes.c_void_p()
+        torch.cuda.set_device(self.device)
+        _lib.check(L.nd_create(ctypes.byref(c), ctypes.byref(h)), "nd_create")
+        self._h = h
+        self._L = L
+        try:
+            for name, arr in weights.items():
+                a = np.ascontiguousarray(arr, dtype=np.float32)
+                shape = (ctypes.c_int64 * a.ndim)(*a.shape)
+                _lib.check(L.nd_load_weight(h, name.encode(), a.ctypes.data_as(ctypes.c_void_p), shape, a.ndim),
+                           f"nd_load_weight({name})")
+            _lib.check(L.nd_finalize(h), "nd_finalize")
+            _lib.check(L.nd_set_graphs(h, int(graphs)), "nd_set_graphs")
+        except Exception:
+            self.close()
+            raise
+
+    # ------------------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.nd_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def set_timing(self, on: bool):
+        _lib.check(self._L.nd_set_timing(self._h, int(on)), "nd_set_timing")
+
+    def last_timing(self):
+        e, d = ctypes.c_float(), ctypes.c_float()
+        _lib.check(self._L.nd_last_timing(self._h, ctypes.byref(e), ctypes.byref(d)), "nd_last_timing")
+        return e.value, d.value
+
+    def _inputs(self, signal, lengths, spans):
+        dev = self.device
+        signal = torch.as_tensor(signal, dtype=torch.float32).to(dev).contiguous()
+        B, T = signal.shape
+        lengths = torch.as_tensor(lengths).to(dev, torch.int32).contiguous()
+        spans = lengths.clone() if spans is None else torch.as_tensor(spans).to(dev, torch.int32).contiguous()
+        assert lengths.shape == (B,) and spans.shape == (B,)
+        return signal, lengths, spans, B, T
+
+    def translate_greedy(self, signal, lengths, spans=None, max_len: Optional[int] = None, min_len: int = 0,
+                         return_logp: bool = False):
+        """Greedy decode.  signal [B,T] f32 (zero padded), lengths/spans [B].
+        Returns dict(tokens [B,S] i32, scores [B] f32, logp [B,S,V] or None)."""
+        signal, lengths, spans, B, T = self._inputs(signal, lengths, spans)
+        S = self.max_steps if max_len is None else max_len
+        tok = torch.empty(B, S, dtype=torch.int32, device=self.device)
+        sc = torch.empty(B, dtype=torch.float32, device=self.device)
+        lp = torch.empty(B, S, self.cfg.vocab, dtype=torch.float32, device=self.device) if return_logp else None
+        _lib.check(self._L.nd_translate_greedy(self._h, _ptr(signal), _ptr(lengths), _ptr(spans), B, T, S, min_len,
+                                               _ptr(tok), _ptr(sc), _ptr(lp), self._stream()), "nd_translate_greedy")
+        return dict(tokens=tok, scores=sc, logp=lp)
+
+    def translate_beam(self, signal, lengths, spans=None, beam: int = 5, n_best: int = 1, alpha: float = 0.0,
+                       max_len: Optional[int] = None, min_len: int = 0):
+        """--fast beam search.  Returns dict(tokens [B,n_best,S] i32 (-1 pad),
+        scores [B,n_best] f32, lens [B,n_best] i32, steps [1] i32)."""
+        signal, lengths, spans, B, T = self._inputs(signal, lengths, spans)
+        S = self.max_steps if max_len is None else max_len
+        tok = torch.empty(B, n_best, S, dtype=torch.int32, device=self.device)
+        sc = torch.empty(B, n_best, dtype=torch.float32, device=self.device)
+        ln = torch.empty(B, n_best, dtype=torch.int32, device=self.device)
+        st = torch.empty(1, dtype=torch.int32, device=self.device)
+        _lib.check(self._L.nd_translate_beam(self._h, _ptr(signal), _ptr(lengths), _ptr(spans), B, T, beam, n_best,
+                                             float(alpha), S, min_len, _ptr(tok), _ptr(sc), _ptr(ln), _ptr(st),
+                                             self._stream()), "nd_translate_beam")
+        return dict(tokens=tok, scores=sc, lens=ln, steps=st)
+
+    def encode(self, signal, lengths, spans=None):
+        """Memory bank [B, T, d] of the encoder (rows >= span unspecified)."""
+        signal, lengths, spans, B, T = self._inputs(signal, lengths, spans)
+        mem = torch.empty(B, T, self.cfg.d_model, dtype=torch.float32, device=self.device)
+        _lib.check(self._L.nd_encode(self._h, _ptr(signal), _ptr(lengths), _ptr(spans), B, T, _ptr(mem),
+                                     self._stream()), "nd_encode")
+        return mem
+
+
+# ---------------------------------------------------------------------------
+# op-level entry points (kernel unit tests)
+# ---------------------------------------------------------------------------
+
+def op_gemm(A: torch.Tensor, W: torch.Tensor, bias=None, R=None, ln_g=None, ln_b=None, relu=False):
+    M, K = A.shape
+    N = W.shape[0]
+    C = torch.empty(M, N, dtype=torch.float32, device=A.device)
+    s = ctypes.c_void_p(torch.cuda.current_stream(A.device).cuda_stream)
+    _lib.check(_lib.lib().nd_op_gemm(_ptr(A), _ptr(W), _ptr(bias), _ptr(R), _ptr(C), M, N, K, _ptr(ln_g), _ptr(ln_b),
+                                     int(relu), s), "nd_op_gemm")
+    return C
+
+
+def op_enc_attention(qkv: torch.Tensor, signal: torch.Tensor, span: torch.Tensor):
+    B, T = signal.shape
+    out = torch.zeros(B * T, qkv.shape[1] // 3, dtype=torch.float32, device=qkv.device)
+    s = ctypes.c_void_p(torch.cuda.current_stream(qkv.device).cuda_stream)
+    _lib.check(_lib.lib().nd_op_enc_attention(_ptr(qkv), _ptr(signal), _ptr(span.to(torch.int32)), _ptr(out), B, T, s),
+               "nd_op_enc_attention")
+    return out
+
+
+def pad_chunks(chunks: Sequence[np.ndarray], T: Optional[int] = None):
+    """make_nano (inputters/inputter.py:86-95): zero pad to [B, T]."""
+    lens = np.array([len(c) for c in chunks], np.int32)
+    T = int(lens.max()) if T is None else T
+    out = np.zeros((len(chunks), T), np.float32)
+    for i, c in enumerate(chunks):
+        out[i, : len(c)] = c
+    return out, lens
