@@ -132,6 +132,20 @@ int nd_op_gemm(const float* A, const float* W, const float* bias, const float* R
 int nd_op_enc_attention(const float* qkv, const float* signal, const int32_t* span, float* out, int32_t B,
                         int32_t T, void* stream);
 
+/* Decoder self-attention for one step (multi_headed_attn.py:124-141):
+ * qkv [R, 3*d]; cache [R, max_steps, 2*d] (this step's k|v is appended at
+ * [r][step]); anc nullable [R, anc_ld] slot ancestry (NULL = identity);
+ * out [R, d]. */
+int nd_op_dec_self_attention(const float* qkv, float* cache, const int32_t* anc, int32_t anc_ld, int32_t step,
+                             int32_t max_steps, float* out, int32_t R, void* stream);
+
+/* Decoder context attention (multi_headed_attn.py:142-177): rows r = c*rpc+j
+ * of q [C*rpc, d] attend over K at kv[(c*T+t)*ld + koff] and V at +d, keys
+ * t < span[c], key mask signal == pad_val; out [C*rpc, d]. */
+int nd_op_dec_ctx_attention(const float* q, const float* kv, int32_t ld, int32_t koff, const float* signal,
+                            const int32_t* span, float pad_val, float* out, int32_t C, int32_t rpc, int32_t T,
+                            void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -190,65 +190,89 @@ hipError_t launch_dec_embed(const int* tok, const float* emb, const float* pe, i
   return hipGetLastError();
 }
 
-// One workgroup (256 threads) per decoder row.  cache layout:
-// [slot][t][512] = k (256) | v (256).
+// Decoder self-attention, one workgroup (256 threads = 4 waves) per row.
+// cache layout: [slot][t][512] = k (256) | v (256).  Lane owns dims
+// 4*lane..4*lane+3 (head = lane/8); waves split the keys, 4 per iteration, so
+// every K/V row is one coalesced 1 KB wave load.
+#define SELF_MAXS 256
 __global__ void __launch_bounds__(256)
 dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cache, const int* __restrict__ anc,
                           int anc_ld, int step, int S, float* __restrict__ out) {
-  __shared__ float p[ND_H][256];
-  __shared__ int slot[256];
-  const int r = blockIdx.x, tid = threadIdx.x;
+  __shared__ float p[ND_H][SELF_MAXS];
+  __shared__ float part[4][ND_D];
+  const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const float* qrow = qkv + (size_t)r * 3 * ND_D;
-  // append this step's k, v (multi_headed_attn.py:124-141)
-  float* mine = cache + ((size_t)r * S + step) * 2 * ND_D;
-  mine[tid] = qrow[ND_D + tid];
-  mine[ND_D + tid] = qrow[2 * ND_D + tid];
+  const f32x4 q = ld4(qrow + lane * 4) / ND_SQRT_DH;
+  const f32x4 kme = ld4(qrow + ND_D + lane * 4), vme = ld4(qrow + 2 * ND_D + lane * 4);
+  // append this step's k, v to the row's own slot (multi_headed_attn.py:124-141)
+  if (wave == 0) {
+    float* mine = cache + ((size_t)r * S + step) * 2 * ND_D;
+    st4(mine + lane * 4, kme);
+    st4(mine + ND_D + lane * 4, vme);
+  }
   const int n = step + 1;
-  for (int t = tid; t < n; t += 256) slot[t] = (anc && t < step) ? anc[(size_t)r * anc_ld + t] : r;
-  __syncthreads();
-  // scores: thread handles (head, key) pairs; 8 heads x n keys
-  for (int e = tid; e < ND_H * n; e += 256) {
-    const int hh = e / n, t = e - hh * n;
-    const float* kr = (t == step) ? (mine + hh * ND_DH) : (cache + ((size_t)slot[t] * S + t) * 2 * ND_D + hh * ND_DH);
-    const float* qh = qrow + hh * ND_DH;
-    float acc = 0.f;
+  const int hh = lane >> 3;
+  auto krow = [&](int t) -> const float* {
+    const int slot = (anc && t < step) ? anc[(size_t)r * anc_ld + t] : r;
+    return cache + ((size_t)slot * S + t) * 2 * ND_D;
+  };
+  // scores: keys t < step come from the cache, key `step` from registers
+  for (int t0 = wave; t0 < n; t0 += 16) {
+    f32x4 k[4];
 #pragma unroll
-    for (int d = 0; d < ND_DH; d += 4) {
-      const f32x4 a = ld4(qh + d) / ND_SQRT_DH, k = ld4(kr + d);
-      acc += a.x * k.x + a.y * k.y + a.z * k.z + a.w * k.w;
+    for (int u = 0; u < 4; ++u) {
+      const int t = t0 + 4 * u;
+      k[u] = (t < step) ? ld4(krow(t) + lane * 4) : kme;
     }
-    p[hh][t] = acc;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int t = t0 + 4 * u;
+      float d = q.x * k[u].x + q.y * k[u].y + q.z * k[u].z + q.w * k[u].w;
+      d += __shfl_xor(d, 1, 64);
+      d += __shfl_xor(d, 2, 64);
+      d += __shfl_xor(d, 4, 64);
+      if ((lane & 7) == 0 && t < n) p[hh][t] = d;
+    }
   }
   __syncthreads();
-  // softmax per head: wave w handles heads w, w+4
-  const int wave = tid >> 6, lane = tid & 63;
-  for (int hh = wave; hh < ND_H; hh += 4) {
+  // softmax per head (no mask while stepping): wave w handles heads w, w+4
+  for (int h2 = wave; h2 < ND_H; h2 += 4) {
     float mx = -INFINITY;
-    for (int t = lane; t < n; t += 64) mx = fmaxf(mx, p[hh][t]);
+    for (int t = lane; t < n; t += 64) mx = fmaxf(mx, p[h2][t]);
     mx = wave_max(mx);
     float sm = 0.f;
     for (int t = lane; t < n; t += 64) {
-      const float e = __expf(p[hh][t] - mx);
-      p[hh][t] = e;
+      const float e = __expf(p[h2][t] - mx);
+      p[h2][t] = e;
       sm += e;
     }
     sm = wave_sum(sm);
     const float inv = 1.0f / sm;
-    for (int t = lane; t < n; t += 64) p[hh][t] *= inv;
+    for (int t = lane; t < n; t += 64) p[h2][t] *= inv;
   }
   __syncthreads();
-  const int hh = tid / ND_DH;
-  float acc = 0.f;
-  for (int t = 0; t < n; ++t) {
-    const float* vr = (t == step) ? mine : cache + ((size_t)slot[t] * S + t) * 2 * ND_D;
-    acc += p[hh][t] * vr[ND_D + tid];
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int t0 = wave; t0 < n; t0 += 16) {
+    f32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int t = t0 + 4 * u;
+      v[u] = (t < step) ? ld4(krow(t) + ND_D + lane * 4) : vme;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int t = t0 + 4 * u;
+      if (t < n) acc += p[hh][t] * v[u];
+    }
   }
-  out[(size_t)r * ND_D + tid] = acc;
+  st4(&part[wave][lane * 4], acc);
+  __syncthreads();
+  out[(size_t)r * ND_D + tid] = part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid];
 }
 
 hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* anc, int anc_ld, int step,
                                      int max_steps, float* out, int R, hipStream_t s) {
-  if (step >= max_steps || step >= 256) return hipErrorInvalidValue;
+  if (step >= max_steps || step >= SELF_MAXS) return hipErrorInvalidValue;
   hipLaunchKernelGGL(dec_self_attention_kernel, dim3(R), dim3(256), 0, s, qkv, cache, anc, anc_ld, step, max_steps,
                      out);
   return hipGetLastError();
@@ -258,11 +282,13 @@ hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* 
 // context K/V stream from HBM once for all of its rows (beam rows share the
 // same memory bank, translate/translator.py:667-676 tiles it only logically).
 #define CTX_THREADS 512
-#define CTX_MAXR 8
+#define CTX_MAXR 6
+template <int RPC>
 __global__ void __launch_bounds__(CTX_THREADS)
 dec_ctx_attention_kernel(const float* __restrict__ q, const float* __restrict__ kv, int ld, int koff,
                          const float* __restrict__ signal, const int* __restrict__ span, float pad_val,
-                         float* __restrict__ out, int rpc, int T) {
+                         float* __restrict__ out, int T) {
+  constexpr int rpc = RPC;
   extern __shared__ float sm[];
   float* sc = sm;                                   // [rpc][8][T]
   float* part = sm + rpc * ND_H * T;                // [8 waves][rpc][256]
@@ -270,22 +296,31 @@ dec_ctx_attention_kernel(const float* __restrict__ q, const float* __restrict__ 
   const int L = min(span[c], T);
   const size_t base = (size_t)c * T;
   // lane owns dims 4*lane..4*lane+3 of every row; head = lane / 8
-  f32x4 qv[CTX_MAXR];
+  f32x4 qv[RPC];
 #pragma unroll
-  for (int j = 0; j < CTX_MAXR; ++j)
-    if (j < rpc) qv[j] = ld4(q + ((size_t)c * rpc + j) * ND_D + lane * 4) / ND_SQRT_DH;
-  // pass 1: scores (mask src == pad_idx, decoder/transformer.py:220-221)
-  for (int t = wave; t < L; t += CTX_THREADS / 64) {
-    const f32x4 k = ld4(kv + (base + t) * ld + koff + lane * 4);
-    const bool masked = signal[base + t] == pad_val;
+  for (int j = 0; j < RPC; ++j) qv[j] = ld4(q + ((size_t)c * rpc + j) * ND_D + lane * 4) / ND_SQRT_DH;
+  // pass 1: scores (mask src == pad_idx, decoder/transformer.py:220-221);
+  // wave w takes keys w, w+8, ... four at a time so 4 KB are in flight per wave
+  constexpr int NW = CTX_THREADS / 64;
+  for (int t0 = wave; t0 < L; t0 += 4 * NW) {
+    f32x4 k[4];
+    bool masked[4];
 #pragma unroll
-    for (int j = 0; j < CTX_MAXR; ++j) {
-      if (j < rpc) {
-        float d = qv[j].x * k.x + qv[j].y * k.y + qv[j].z * k.z + qv[j].w * k.w;
+    for (int u = 0; u < 4; ++u) {
+      const int t = min(t0 + u * NW, L - 1);
+      k[u] = ld4(kv + (base + t) * ld + koff + lane * 4);
+      masked[u] = signal[base + t] == pad_val;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int t = t0 + u * NW;
+#pragma unroll
+      for (int j = 0; j < RPC; ++j) {
+        float d = qv[j].x * k[u].x + qv[j].y * k[u].y + qv[j].z * k[u].z + qv[j].w * k[u].w;
         d += __shfl_xor(d, 1, 64);
         d += __shfl_xor(d, 2, 64);
         d += __shfl_xor(d, 4, 64);
-        if ((lane & 7) == 0) sc[(j * ND_H + (lane >> 3)) * T + t] = masked ? ND_MASK_FILL : d;
+        if ((lane & 7) == 0 && t < L) sc[(j * ND_H + (lane >> 3)) * T + t] = masked[u] ? ND_MASK_FILL : d;
       }
     }
   }
@@ -308,19 +343,25 @@ dec_ctx_attention_kernel(const float* __restrict__ q, const float* __restrict__ 
   }
   __syncthreads();
   // pass 2: out[j] = sum_t p[j][head][t] * V[t]
-  f32x4 acc[CTX_MAXR];
+  f32x4 acc[RPC];
 #pragma unroll
-  for (int j = 0; j < CTX_MAXR; ++j) acc[j] = {0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < RPC; ++j) acc[j] = {0.f, 0.f, 0.f, 0.f};
   const int hh = lane >> 3;
-  for (int t = wave; t < L; t += CTX_THREADS / 64) {
-    const f32x4 v = ld4(kv + (base + t) * ld + koff + ND_D + lane * 4);
+  for (int t0 = wave; t0 < L; t0 += 4 * NW) {
+    f32x4 v[4];
 #pragma unroll
-    for (int j = 0; j < CTX_MAXR; ++j)
-      if (j < rpc) acc[j] += sc[(j * ND_H + hh) * T + t] * v;
+    for (int u = 0; u < 4; ++u) v[u] = ld4(kv + (base + min(t0 + u * NW, L - 1)) * ld + koff + ND_D + lane * 4);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int t = t0 + u * NW;
+      if (t < L) {
+#pragma unroll
+        for (int j = 0; j < RPC; ++j) acc[j] += sc[(j * ND_H + hh) * T + t] * v[u];
+      }
+    }
   }
 #pragma unroll
-  for (int j = 0; j < CTX_MAXR; ++j)
-    if (j < rpc) st4(part + ((size_t)wave * rpc + j) * ND_D + lane * 4, acc[j]);
+  for (int j = 0; j < RPC; ++j) st4(part + ((size_t)wave * rpc + j) * ND_D + lane * 4, acc[j]);
   __syncthreads();
   for (int e = tid; e < rpc * ND_D; e += CTX_THREADS) {
     float v = 0.f;
@@ -333,11 +374,23 @@ dec_ctx_attention_kernel(const float* __restrict__ q, const float* __restrict__ 
 hipError_t launch_dec_ctx_attention(const float* q, const float* kv, int ld, int koff, const float* signal,
                                     const int* span, float pad_val, float* out, int C, int rpc, int T,
                                     hipStream_t s) {
-  if (rpc > CTX_MAXR || T > 512) return hipErrorInvalidValue;
+  if (rpc < 1 || rpc > CTX_MAXR || T > 512) return hipErrorInvalidValue;
   const size_t lds = ((size_t)rpc * ND_H * T + (size_t)(CTX_THREADS / 64) * rpc * ND_D) * sizeof(float);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(dec_ctx_attention_kernel, dim3(C), dim3(CTX_THREADS), lds, s, q, kv, ld, koff, signal, span,
-                     pad_val, out, rpc, T);
+  switch (rpc) {
+#define ND_CTX_CASE(R)                                                                                            \
+  case R:                                                                                                         \
+    hipLaunchKernelGGL(dec_ctx_attention_kernel<R>, dim3(C), dim3(CTX_THREADS), lds, s, q, kv, ld, koff, signal, \
+                       span, pad_val, out, T);                                                                    \
+    break;
+    ND_CTX_CASE(1)
+    ND_CTX_CASE(2)
+    ND_CTX_CASE(3)
+    ND_CTX_CASE(4)
+    ND_CTX_CASE(5)
+    ND_CTX_CASE(6)
+#undef ND_CTX_CASE
+  }
   return hipGetLastError();
 }
 
@@ -356,8 +409,14 @@ hipError_t launch_fill_i32(int* p, int v, int n, hipStream_t s) {
 }
 
 hipError_t init_kernel_attributes() {
-  return hipFuncSetAttribute((const void*)dec_ctx_attention_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             160 * 1024);
+  const void* fns[] = {(const void*)dec_ctx_attention_kernel<1>, (const void*)dec_ctx_attention_kernel<2>,
+                       (const void*)dec_ctx_attention_kernel<3>, (const void*)dec_ctx_attention_kernel<4>,
+                       (const void*)dec_ctx_attention_kernel<5>, (const void*)dec_ctx_attention_kernel<6>};
+  for (const void* f : fns) {
+    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 }  // namespace nd

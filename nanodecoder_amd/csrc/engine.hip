@@ -702,6 +702,27 @@ int nd_op_enc_attention(const float* qkv, const float* signal, const int32_t* sp
   return ND_OK;
 }
 
+int nd_op_dec_self_attention(const float* qkv, float* cache, const int32_t* anc, int32_t anc_ld, int32_t step,
+                             int32_t max_steps, float* out, int32_t R, void* stream) {
+  hipError_t e = nd::launch_dec_self_attention(qkv, cache, anc, anc_ld, step, max_steps, out, R, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("dec_self_attention: ") + hipGetErrorString(e));
+  return ND_OK;
+}
+
+int nd_op_dec_ctx_attention(const float* q, const float* kv, int32_t ld, int32_t koff, const float* signal,
+                            const int32_t* span, float pad_val, float* out, int32_t C, int32_t rpc, int32_t T,
+                            void* stream) {
+  static bool attr = false;
+  if (!attr) {
+    if (nd::init_kernel_attributes() != hipSuccess) return fail(ND_ERR_HIP, "hipFuncSetAttribute failed");
+    attr = true;
+  }
+  hipError_t e = nd::launch_dec_ctx_attention(q, kv, ld, koff, signal, span, pad_val, out, C, rpc, T,
+                                              (hipStream_t)stream);
+  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("dec_ctx_attention: ") + hipGetErrorString(e));
+  return ND_OK;
+}
+
 }  // extern "C"
 
 static hipError_t enqueue_encode(nd_ctx* c, int B, int T, hipStream_t s) {

@@ -150,6 +150,25 @@ def op_enc_attention(qkv: torch.Tensor, signal: torch.Tensor, span: torch.Tensor
     return out
 
 
+def op_dec_self_attention(qkv, cache, step, anc=None, anc_ld=0):
+    R = qkv.shape[0]
+    S = cache.shape[1]
+    out = torch.empty(R, qkv.shape[1] // 3, dtype=torch.float32, device=qkv.device)
+    s = ctypes.c_void_p(torch.cuda.current_stream(qkv.device).cuda_stream)
+    _lib.check(_lib.lib().nd_op_dec_self_attention(_ptr(qkv), _ptr(cache), _ptr(anc), anc_ld, step, S, _ptr(out), R, s),
+               "nd_op_dec_self_attention")
+    return out
+
+
+def op_dec_ctx_attention(q, kv, ld, koff, signal, span, pad_val, rpc):
+    C, T = signal.shape
+    out = torch.empty(q.shape[0], q.shape[1], dtype=torch.float32, device=q.device)
+    s = ctypes.c_void_p(torch.cuda.current_stream(q.device).cuda_stream)
+    _lib.check(_lib.lib().nd_op_dec_ctx_attention(_ptr(q), _ptr(kv), ld, koff, _ptr(signal), _ptr(span), float(pad_val),
+                                                  _ptr(out), C, rpc, T, s), "nd_op_dec_ctx_attention")
+    return out
+
+
 def pad_chunks(chunks: Sequence[np.ndarray], T: Optional[int] = None):
     """make_nano (inputters/inputter.py:86-95): zero pad to [B, T]."""
     lens = np.array([len(c) for c in chunks], np.int32)

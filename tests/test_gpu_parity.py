@@ -30,6 +30,8 @@ def _oracle():
 
 # ----------------------------------------------------------------- kernels
 @pytest.mark.parametrize("M,N,K,ln,relu,res", [(4096, 768, 256, True, False, False),
+                                                (16384, 512, 256, True, True, False),
+                                                (16384, 512, 2048, False, False, True),
                                                 (5000, 256, 2048, False, False, True),
                                                 (256, 2048, 256, True, True, False),
                                                 (37, 256, 256, False, False, True)])

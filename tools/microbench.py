@@ -1,0 +1,76 @@
+"""Time individual kernels through the op-level C-ABI entry points (HIP
+events on the current torch stream).  Usage: python tools/microbench.py"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from nanodecoder_amd import engine as E  # noqa: E402
+
+dev = torch.device("cuda", 0)
+
+
+def timeit(fn, n=50):
+    for _ in range(5):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        fn()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / n * 1e3  # us
+
+
+def gemm_case(M, N, K, ln, relu, res):
+    A = torch.randn(M, K, device=dev)
+    W = torch.randn(N, K, device=dev) / K ** 0.5
+    b = torch.randn(N, device=dev)
+    R = torch.randn(M, N, device=dev) if res else None
+    g = torch.ones(K, device=dev) if ln else None
+    bb = torch.zeros(K, device=dev) if ln else None
+    us = timeit(lambda: E.op_gemm(A, W, b, R, g, bb, relu))
+    tf = 2 * M * N * K / (us * 1e-6) / 1e12
+    print(f"gemm M={M:6d} N={N:5d} K={K:5d} ln={int(ln)} relu={int(relu)} res={int(res)}: {us:9.2f} us  {tf:6.1f} TF/s")
+
+
+for M in (256, 1280, 5120):
+    gemm_case(M, 768, 256, True, False, False)
+    gemm_case(M, 256, 256, False, False, True)
+    gemm_case(M, 256, 256, True, False, False)
+    gemm_case(M, 2048, 256, True, True, False)
+    gemm_case(M, 256, 2048, False, False, True)
+gemm_case(131072, 768, 256, True, False, False)
+gemm_case(131072, 256, 256, False, False, True)
+gemm_case(131072, 2048, 256, True, True, False)
+gemm_case(131072, 256, 2048, False, False, True)
+gemm_case(131072, 1536, 256, True, False, False)
+
+# decoder self-attention at several steps
+for R in (256, 5120):
+    S = 100
+    qkv = torch.randn(R, 768, device=dev)
+    cache = torch.randn(R, S, 512, device=dev)
+    for step in (0, 50, 99):
+        us = timeit(lambda: E.op_dec_self_attention(qkv, cache, step))
+        print(f"self-attn R={R} step={step}: {us:8.2f} us")
+
+# decoder context attention
+for C, rpc in ((256, 1), (1024, 5)):
+    T = 512
+    q = torch.randn(C * rpc, 256, device=dev)
+    kv = torch.randn(C * T, 1536, device=dev)
+    sig = torch.randn(C, T, device=dev)
+    span = torch.full((C,), T, dtype=torch.int32, device=dev)
+    us = timeit(lambda: E.op_dec_ctx_attention(q, kv, 1536, 0, sig, span, 1.0, rpc))
+    gbs = C * T * 512 * 4 / (us * 1e-6) / 1e9
+    print(f"ctx-attn C={C} rpc={rpc}: {us:8.2f} us  {gbs:7.1f} GB/s (K+V bytes)")
+
+# encoder attention
+B, T = 256, 512
+qkv = torch.randn(B * T, 768, device=dev)
+sig = torch.randn(B, T, device=dev)
+span = torch.full((B,), T, dtype=torch.int32, device=dev)
+us = timeit(lambda: E.op_enc_attention(qkv, sig, span), n=10)
+print(f"enc-attn B={B}: {us:9.2f} us  {4*B*8*T*T*32/(us*1e-6)/1e12:6.1f} TF/s")
