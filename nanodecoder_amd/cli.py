@@ -1,0 +1,128 @@
+"""translate.py driver (reference translate.py:59-187) on the MI355X engine.
+
+Same inputs, outputs and resume rule: every ``*.signal`` / ``*.fast5`` in
+``-src_dir`` whose ``result/<read>.fasta`` does not exist yet is normalised
+and windowed in a worker pool (translate.py:131-163), translated, and written
+as result/<read>.fasta, segment/<read>.txt and a line of speed.txt
+(translate.py:81-98).  One bad read prints ``!!!error!!!`` and the run goes
+on (translate.py:97-98).  ``-pack_reads N`` translates N reads per engine pass.
+"""
+from __future__ import annotations
+
+import logging
+import multiprocessing
+import os
+import sys
+import time
+
+from . import frontend
+from .opts import parse_translate_opts
+
+
+def init_logger(log_file=None):
+    """onmt/utils/logging.py:9-24."""
+    fmt = logging.Formatter("[%(asctime)s %(levelname)s] %(message)s")
+    logger = logging.getLogger()
+    logger.setLevel(logging.INFO)
+    h = logging.StreamHandler()
+    h.setFormatter(fmt)
+    logger.handlers = [h]
+    if log_file:
+        fh = logging.FileHandler(log_file)
+        fh.setFormatter(fmt)
+        logger.addHandler(fh)
+    return logger
+
+
+def list_reads(opt):
+    """translate.py:134-163: pending reads (resume = skip existing fasta)."""
+    todo, done = [], 0
+    for name in sorted(os.listdir(opt.src_dir)):
+        if name.endswith("fast5"):
+            prefix, suffix = name.split(".fast5")[0] + ".txt", "fast5"
+        elif name.endswith("signal"):
+            prefix, suffix = name.split(".signal")[0] + ".txt", "signal"
+        else:
+            continue
+        if os.path.exists(os.path.join(opt.save_data, "result", prefix.split(".txt")[0] + ".fasta")):
+            done += 1
+        else:
+            todo.append((os.path.join(opt.src_dir, name), prefix, suffix))
+    return todo, done
+
+
+def _extract(args):
+    path, prefix, suffix, norm, length, stride = args
+    try:
+        return frontend.extract_raw(path, prefix, norm, length, stride, suffix)
+    except Exception as e:  # surfaced per read, like the Pool error path
+        return ["!" + prefix, repr(e)]
+
+
+def write_output(opt, file_src, all_predictions, time_translate):
+    """translate.py:81-98."""
+    try:
+        c_bpread = frontend.assemble_read(all_predictions, opt.src_seq_length, opt.src_seq_stride)
+        name = file_src.split(".txt")[0]
+        with open(os.path.join(opt.save_data, "result", name + ".fasta"), "w") as f:
+            f.writelines(">%s\n%s" % (name, c_bpread))
+        with open(os.path.join(opt.save_data, "segment", file_src), "w+") as f:
+            for n_best_preds in all_predictions:
+                f.write("\n".join(n_best_preds) + "\n")
+        with open(os.path.join(opt.save_data, "speed.txt"), "a+") as f:
+            f.writelines("%s\t%0.2f\t%d\t%0.2f\n" % (name, float(time_translate), len(c_bpread),
+                                                     len(c_bpread) / max(float(time_translate), 1e-9)))
+    except Exception:
+        print("!!!error!!!data src: " + file_src.split(".txt")[0])
+
+
+def main(opt=None):
+    opt = opt or parse_translate_opts()
+    logger = init_logger(opt.log_file)
+    for sub in ("", "result", "segment"):
+        os.makedirs(os.path.join(opt.save_data, sub), exist_ok=True)
+    if opt.attn_debug:
+        raise NotImplementedError("-attn_debug is not supported on the MI355X path")
+    from .translator import build_translator
+    translator = build_translator(opt, report_score=False, logger=logger)
+    todo, done = list_reads(opt)
+    logger.info("%d reads have already translated, remains %d read\n" % (done, len(todo)))
+    jobs = [(p, pre, suf, opt.normalization_raw, opt.src_seq_length, opt.src_seq_stride) for p, pre, suf in todo]
+    ctx = multiprocessing.get_context("spawn")
+    t_start = time.time()
+    n_done = 0
+    with ctx.Pool(max(1, opt.thread)) as pool:
+        pending = []
+        for src in pool.imap(_extract, jobs):
+            if src and src[0].startswith("!"):
+                print("!!!error!!!data src: " + src[0][1:].split(".txt")[0])
+                continue
+            if not src or len(src) == 1:   # translate.py:102-103
+                continue
+            pending.append(src)
+            if len(pending) >= max(1, opt.pack_reads):
+                n_done += _translate_group(opt, translator, pending)
+                pending = []
+        if pending:
+            n_done += _translate_group(opt, translator, pending)
+    logger.info("translated %d reads in %.1f s" % (n_done, time.time() - t_start))
+    return n_done
+
+
+def _translate_group(opt, translator, group):
+    t0 = time.time()
+    try:
+        outs = translator.translate_reads([g[1:] for g in group], batch_size=opt.batch_size)
+    except Exception as e:
+        for g in group:
+            print("!!!error!!!data src: " + g[0].split(".txt")[0] + " (%r)" % (e,))
+        return 0
+    dt = time.time() - t0
+    total = sum(len(g) - 1 for g in group)
+    for g, (_, preds) in zip(group, outs):
+        write_output(opt, g[0], preds, dt * (len(g) - 1) / total)
+    return len(group)
+
+
+if __name__ == "__main__":
+    sys.exit(0 if main() is not None else 1)

@@ -725,8 +725,26 @@ int nd_op_dec_ctx_attention(const float* q, const float* kv, int32_t ld, int32_t
 
 }  // extern "C"
 
+// NanoEncoder (encoder/nano_encoder.py:79-124): 3x BiLSTM; layers 0-1 emit
+// BatchNorm(h) for the next layer, layer 2 emits raw h (zeros at padded
+// steps, as pad_packed_sequence does); memory = h W^T -> c->x.
+static hipError_t enqueue_encode_nano(nd_ctx* c, int B, int T, hipStream_t s) {
+  const int M = B * T, D = c->D, Lz = (int)c->nano.size();
+  float* bufs[2] = {c->y, c->att};
+  for (int l = 0; l < Lz; ++l) {
+    NanoLayer& L = c->nano[l];
+    float* out = bufs[l & 1];
+    const bool last = l == Lz - 1;
+    if (l > 0)
+      LCHK(gemm(bufs[(l - 1) & 1], 2 * c->H, L.wih, 8 * c->H, 2 * c->H, L.bsum, c->nano_xp, 8 * c->H, M, s));
+    if (last) LCHK(hipMemsetAsync(out, 0, (size_t)M * 2 * c->H * sizeof(float), s));
+    LCHK(nd::launch_lstm_layer(c->nano_xp, c->sig, L.wih, L.bsum, L.whh, c->len, B, T, out,
+                               last ? nullptr : L.bn_scale, last ? nullptr : L.bn_shift, l == 0, s));
+  }
+  return gemm(bufs[(Lz - 1) & 1], 2 * c->H, c->nano_W, D, 2 * c->H, nullptr, c->x, D, M, s);
+}
+
 static hipError_t enqueue_encode(nd_ctx* c, int B, int T, hipStream_t s) {
   if (c->cfg.encoder_type == ND_ENC_TRANSFORMER) return enqueue_encode_transformer(c, B, T, s);
-  g_err = "NanoEncoder path not built yet";
-  return hipErrorNotSupported;
+  return enqueue_encode_nano(c, B, T, s);
 }

@@ -29,6 +29,12 @@ hipError_t launch_enc_embed(const float* signal, const float* w_in, const float*
 // flash attention over qkv [B*T, 768]; mask signal==0; keys >= span excluded
 hipError_t launch_enc_attention(const float* qkv, const float* signal, const int* span, float* out, int B, int T,
                                 hipStream_t s);
+// NanoEncoder BiLSTM layer (both directions): xp [B*T, 1024] projections
+// (or, layer0, computed from signal with wih0/bsum [2][512]); whh [2][512][128];
+// out [B*T, 256] (h, or BatchNorm(h) when bn_scale != nullptr).
+hipError_t launch_lstm_layer(const float* xp, const float* signal, const float* wih0, const float* bsum,
+                             const float* whh, const int* len, int B, int T, float* out, const float* bn_scale,
+                             const float* bn_shift, bool layer0, hipStream_t s);
 // out[r] = LN(x[r]) (rows of 256)
 hipError_t launch_layernorm(const float* x, const float* g, const float* b, float* out, int rows, hipStream_t s);
 

@@ -1,0 +1,193 @@
+// NanoEncoder BiLSTM recurrence on gfx950 (encoder/nano_encoder.py:79-124,
+// nn.LSTM through onmt/utils/rnn_factory.py:8-17, packed sequences).
+//
+// One workgroup = 16 sequences x one direction, for ALL time steps: the
+// recurrence never leaves the CU, so a step costs one 16x512x128 MFMA
+// product + one LDS exchange instead of a kernel launch.  W_hh^T (512 x 128
+// fp32 = 256 KB per direction, too big for LDS) is held in REGISTERS across
+// the 16 waves: wave w owns gate columns [32w, 32w+32) as two 16x16 tiles of
+// v_mfma_f32_16x16x4_f32 B operands (64 floats per lane).  h_{t-1} is the A
+// operand, read from LDS.  Gates go through LDS so every thread can apply
+// the PyTorch cell (i, f, g, o order) to 2 (sequence, unit) pairs.
+//
+// Packing semantics (pack_padded_sequence / pad_packed_sequence):
+// sequence b only processes its valid steps; the reverse direction starts
+// at t = len_b - 1.  Outputs at t >= len_b are left as the caller zeroed them.
+//
+// The input projection x_t W_ih^T + b_ih + b_hh is precomputed for all t by a
+// GEMM (layers 1, 2) or computed in-kernel from the scalar sample (layer 0,
+// input_size 1).  When `bn_scale` is set the kernel writes the eval-mode
+// BatchNorm of h (the next layer's input, nano_encoder.py:108); otherwise the
+// raw h (the last layer: memory = W . h, its BatchNorm is unused, :113-115).
+#include "common.hpp"
+#include "kernels.hpp"
+
+namespace nd {
+
+__device__ __forceinline__ f32x4 mfma16x4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+#define LSTM_H 128
+#define LSTM_G 512
+#define LSTM_HS_LD (LSTM_H + 4)
+#define LSTM_GS_LD (LSTM_G + 4)
+
+template <bool LAYER0>
+__global__ void __launch_bounds__(1024)
+lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projections (fwd | bwd), !LAYER0
+                const float* __restrict__ signal,  // [B, T] (LAYER0)
+                const float* __restrict__ wih0,    // [2][512] (LAYER0, input_size 1)
+                const float* __restrict__ bsum,    // [2][512] b_ih + b_hh (LAYER0)
+                const float* __restrict__ whh,     // [2][512][128]
+                const int* __restrict__ len, int B, int T, float* __restrict__ out,  // [B*T, 256]
+                const float* __restrict__ bn_scale, const float* __restrict__ bn_shift) {
+  __shared__ __attribute__((aligned(16))) float hs[2][16 * LSTM_HS_LD];
+  __shared__ float gs[16 * LSTM_GS_LD];
+  __shared__ int s_len[16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int dir = blockIdx.y;
+  const int b0 = blockIdx.x * 16;
+  const int li = lane & 15, lq = lane >> 4;
+
+  // W_hh^T fragments for this wave's two 16-column tiles, k order matching
+  // the A fragment: block kb, step s <-> k = 16*kb + 4*lq + s
+  float wr[2][32];
+  {
+    const float* W = whh + (size_t)dir * LSTM_G * LSTM_H;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int n = wave * 32 + t * 16 + li;
+#pragma unroll
+      for (int kb = 0; kb < 8; ++kb) {
+        const f32x4 v = ld4(W + (size_t)n * LSTM_H + kb * 16 + 4 * lq);
+        wr[t][kb * 4 + 0] = v.x;
+        wr[t][kb * 4 + 1] = v.y;
+        wr[t][kb * 4 + 2] = v.z;
+        wr[t][kb * 4 + 3] = v.w;
+      }
+    }
+  }
+  if (tid < 16) s_len[tid] = (b0 + tid < B) ? len[b0 + tid] : 0;
+  for (int e = tid; e < 16 * LSTM_HS_LD; e += 1024) hs[0][e] = 0.f;
+  __syncthreads();
+  int maxlen = 0;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) maxlen = max(maxlen, s_len[q]);
+
+  // elementwise ownership: pairs p = tid and tid + 1024 -> (seq, unit)
+  int pseq[2], punit[2];
+  float c[2] = {0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int p = tid + u * 1024;
+    pseq[u] = p >> 7;
+    punit[u] = p & 127;
+  }
+  float bnsc[2] = {1.f, 1.f}, bnsh[2] = {0.f, 0.f};
+  if (bn_scale) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      bnsc[u] = bn_scale[dir * LSTM_H + punit[u]];
+      bnsh[u] = bn_shift[dir * LSTM_H + punit[u]];
+    }
+  }
+  float w0[2][4], bb[2][4];
+  if constexpr (LAYER0) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        w0[u][g] = wih0[dir * LSTM_G + g * LSTM_H + punit[u]];
+        bb[u][g] = bsum[dir * LSTM_G + g * LSTM_H + punit[u]];
+      }
+  }
+  auto pos_of = [&](int q, int step) { return dir == 0 ? step : s_len[q] - 1 - step; };
+  auto load_x = [&](int step, float (&x)[2][4]) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int q = pseq[u];
+      const bool act = step < s_len[q];
+      const int pos = act ? pos_of(q, step) : 0;
+      const size_t row = (size_t)(b0 + q) * T + pos;
+      if constexpr (LAYER0) {
+        const float s = act ? signal[row] : 0.f;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) x[u][g] = s * w0[u][g] + bb[u][g];
+      } else {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) x[u][g] = act ? xp[row * 1024 + dir * LSTM_G + g * LSTM_H + punit[u]] : 0.f;
+      }
+    }
+  };
+
+  float xn[2][4];
+  load_x(0, xn);
+  for (int step = 0; step < maxlen; ++step) {
+    const int cur = step & 1;
+    float xc[2][4];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) xc[u][g] = xn[u][g];
+    if (step + 1 < maxlen) load_x(step + 1, xn);  // prefetch next step's projections
+
+    // gates = h_{t-1} W_hh^T on MFMA
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    const float* hrow = &hs[cur][li * LSTM_HS_LD + 4 * lq];
+#pragma unroll
+    for (int kb = 0; kb < 8; ++kb) {
+      const f32x4 a = ld4(hrow + kb * 16);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        acc0 = mfma16x4(a[s], wr[0][kb * 4 + s], acc0);
+        acc1 = mfma16x4(a[s], wr[1][kb * 4 + s], acc1);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int q = lq * 4 + r;
+      gs[q * LSTM_GS_LD + wave * 32 + li] = acc0[r];
+      gs[q * LSTM_GS_LD + wave * 32 + 16 + li] = acc1[r];
+    }
+    __syncthreads();
+    // PyTorch LSTM cell (gates i, f, g, o)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int q = pseq[u], j = punit[u];
+      float h;
+      if (step < s_len[q]) {
+        const float* g = &gs[q * LSTM_GS_LD];
+        const float ig = sigm(g[j] + xc[u][0]);
+        const float fg = sigm(g[LSTM_H + j] + xc[u][1]);
+        const float gg = tanhf(g[2 * LSTM_H + j] + xc[u][2]);
+        const float og = sigm(g[3 * LSTM_H + j] + xc[u][3]);
+        c[u] = fg * c[u] + ig * gg;
+        h = og * tanhf(c[u]);
+        const size_t row = (size_t)(b0 + q) * T + pos_of(q, step);
+        out[row * 2 * LSTM_H + dir * LSTM_H + j] = bn_scale ? h * bnsc[u] + bnsh[u] : h;
+      } else {
+        h = hs[cur][q * LSTM_HS_LD + j];
+      }
+      hs[cur ^ 1][q * LSTM_HS_LD + j] = h;
+    }
+    __syncthreads();
+  }
+}
+
+hipError_t launch_lstm_layer(const float* xp, const float* signal, const float* wih0, const float* bsum,
+                             const float* whh, const int* len, int B, int T, float* out, const float* bn_scale,
+                             const float* bn_shift, bool layer0, hipStream_t s) {
+  dim3 grid((B + 15) / 16, 2), block(1024);
+  if (layer0)
+    hipLaunchKernelGGL(lstm_dir_kernel<true>, grid, block, 0, s, xp, signal, wih0, bsum, whh, len, B, T, out,
+                       bn_scale, bn_shift);
+  else
+    hipLaunchKernelGGL(lstm_dir_kernel<false>, grid, block, 0, s, xp, signal, wih0, bsum, whh, len, B, T, out,
+                       bn_scale, bn_shift);
+  return hipGetLastError();
+}
+
+}  // namespace nd

@@ -1,0 +1,262 @@
+"""Drop-in for translate/translator.py on MI355X.
+
+``build_translator(opt, report_score, logger, out_file)`` and
+``Translator.translate(src, tgt, src_dir, batch_size, attn_debug)`` keep the
+reference's names, arguments, return values and error behaviour
+(translate/translator.py:65-90,181-369), so translate.py's call
+(translate.py:76,113-120) works unchanged.  The model runs in
+libnanodec_hip.so (``Engine``); there is no CPU path — ``-gpu -1`` raises.
+
+Reference semantics reproduced:
+* batches are ``batch_size`` consecutive chunks of ONE read, each zero padded
+  to its own longest chunk (inputters/inputter.py:86-95); that padded length is
+  passed to the engine as the chunk's ``span`` so results are identical to the
+  reference however the engine packs chunks;
+* greedy (beam_size == 1) runs all max_length steps and scores with the last
+  step's top log-prob (:396-503); --fast beam for beam_size > 1 (:619-825);
+* predictions are cut at the first EOS and joined with spaces
+  (translate/translation.py:31-47, translate/translator.py:271-273).
+
+Additions: chunks may be given as float32 arrays instead of strings, and
+``translate_reads`` packs chunks of many reads into full engine batches (same
+per-chunk results, far higher throughput than one read at a time).
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import checkpoint
+from .engine import Engine
+
+
+class GNMTGlobalScorer:
+    """onmt/translate/beam.py:181-199 — only alpha/beta reach --fast beam."""
+
+    def __init__(self, opt):
+        self.alpha = float(getattr(opt, "alpha", 0.0))
+        self.beta = float(getattr(opt, "beta", 0.0))
+
+
+def parse_chunk(c) -> np.ndarray:
+    """NanoDataset.extract_features (inputters/nano_dataset.py:43-83) for
+    corpus_type 'translate': a chunk is a whitespace-separated string of
+    floats, or the path of a file holding one; returns float32."""
+    if isinstance(c, np.ndarray):
+        return np.ascontiguousarray(c, dtype=np.float32)
+    if isinstance(c, torch.Tensor):
+        return c.detach().to(torch.float32).cpu().numpy().reshape(-1)
+    if isinstance(c, (list, tuple)):
+        return np.asarray(c, dtype=np.float64).astype(np.float32)
+    if isinstance(c, str) and os.path.exists(c):
+        with open(c) as f:
+            c = f.read()
+    return np.asarray(str(c).split(), dtype=np.float64).astype(np.float32)
+
+
+def _bucket(n: int, cap: int) -> int:
+    b = 8
+    while b < n:
+        b *= 2
+    return min(max(b, n), cap)
+
+
+def build_translator(opt, report_score=False, logger=None, out_file=None):
+    """translate/translator.py:65-90."""
+    models = getattr(opt, "models", None) or []
+    if len(models) != 1:
+        raise NotImplementedError("exactly one -model is supported (ensembles are not on the MI355X path)")
+    if logger:
+        logger.info("Loading model...")
+    cfg, W = checkpoint.load(models[0])
+    scorer = GNMTGlobalScorer(opt)
+    return Translator(cfg, W, opt, global_scorer=scorer, report_score=report_score, logger=logger)
+
+
+class Translator(object):
+    """translate/translator.py:93-173, engine-backed."""
+
+    def __init__(self, cfg, weights, opt, global_scorer=None, report_score=False, logger=None, engine=None):
+        self.cfg = cfg
+        self.opt = opt
+        self.gpu = getattr(opt, "gpu", -1)
+        if self.gpu < 0 and engine is None:
+            raise RuntimeError("nanodecoder_amd runs on MI355X only: pass -gpu N (there is no CPU path)")
+        self.n_best = int(getattr(opt, "n_best", 1))
+        self.max_length = int(getattr(opt, "max_length", 100))
+        self.min_length = int(getattr(opt, "min_length", 0))
+        self.beam_size = int(getattr(opt, "beam_size", 5))
+        self.random_sampling_temp = float(getattr(opt, "random_sampling_temp", 1.0))
+        self.sample_from_topk = int(getattr(opt, "random_sampling_topk", 1))
+        self.block_ngram_repeat = int(getattr(opt, "block_ngram_repeat", 0))
+        self.dump_beam = getattr(opt, "dump_beam", "")
+        self.replace_unk = bool(getattr(opt, "replace_unk", False))
+        self.verbose = bool(getattr(opt, "verbose", False))
+        self.fast = bool(getattr(opt, "fast", False))
+        self.global_scorer = global_scorer or GNMTGlobalScorer(opt)
+        self.report_score = report_score
+        self.logger = logger
+        self.out_file_attn = None
+        self._check_supported()
+        batch_cap = max(1, int(getattr(opt, "batch_size", 100)))
+        self.max_batch = int(getattr(opt, "engine_max_batch", 0)) or max(batch_cap, 8)
+        if engine is None:
+            dev = torch.cuda.current_device()  # the reference moves tensors to the default "cuda" device
+            engine = Engine(cfg, weights, device=dev, max_batch=self.max_batch,
+                            max_src_len=int(getattr(opt, "src_seq_length", 512)) if
+                            int(getattr(opt, "src_seq_length", 512)) <= 512 else 512,
+                            max_steps=self.max_length, max_beam=max(1, self.beam_size))
+        self.engine = engine
+
+    def _check_supported(self):
+        if self.beam_size == 1:
+            # translator.py:371-394: keep_topk == 1 (or temp == 0) is argmax
+            if not (self.random_sampling_temp == 0.0 or self.sample_from_topk == 1):
+                raise NotImplementedError("random sampling (-random_sampling_topk != 1) is not supported")
+            if self.block_ngram_repeat != 0:
+                raise AssertionError("block_ngram_repeat is not supported (translator.py:430)")
+        else:
+            if not self.fast:
+                raise NotImplementedError("the non --fast Beam path (translator.py:827-926) is not on the MI355X "
+                                          "path; pass --fast")
+            if self.dump_beam:
+                raise AssertionError("dump_beam is not supported with --fast (translator.py:631)")
+            if self.block_ngram_repeat != 0:
+                raise AssertionError("block_ngram_repeat is not supported with --fast (translator.py:633)")
+            if self.global_scorer.beta != 0:
+                raise AssertionError("beta must be 0 with --fast (translator.py:634)")
+            if self.n_best > self.beam_size:
+                raise ValueError("n_best must be <= beam_size")
+        if self.replace_unk:
+            raise NotImplementedError("-replace_unk needs attention dumps, not produced on the MI355X path")
+
+    def setAttnFile(self, out_file_attn):
+        self.out_file_attn = out_file_attn
+
+    # ------------------------------------------------------------------ core
+    def _run(self, chunks: List[np.ndarray], spans: Sequence[int]):
+        """Run the engine on up to max_batch chunks with their reference
+        spans.  Returns per chunk (scores[n_best], token lists[n_best])."""
+        n = len(chunks)
+        lens = np.array([len(c) for c in chunks], np.int32)
+        if (lens < 1).any():
+            raise ValueError("empty signal chunk")
+        spans = np.asarray(spans, np.int32)
+        if spans.max() > self.engine.max_src_len:
+            raise ValueError(f"chunk longer than {self.engine.max_src_len} samples (src_seq_length) is not supported")
+        T = min(self.engine.max_src_len, ((int(spans.max()) + 63) // 64) * 64)
+        B = _bucket(n, self.engine.max_batch)
+        sig = np.zeros((B, T), np.float32)
+        for i, c in enumerate(chunks):
+            sig[i, : len(c)] = c
+        L = np.ones(B, np.int32)
+        S = np.ones(B, np.int32)
+        L[:n], S[:n] = lens, spans
+        out = []
+        if self.beam_size == 1:
+            r = self.engine.translate_greedy(sig, L, S, max_len=self.max_length, min_len=self.min_length)
+            tok = r["tokens"].cpu().numpy()
+            sc = r["scores"].cpu().numpy()
+            for i in range(n):
+                out.append(([float(sc[i])], [tok[i].tolist()]))
+        else:
+            r = self.engine.translate_beam(sig, L, S, beam=self.beam_size, n_best=self.n_best,
+                                           alpha=self.global_scorer.alpha, max_len=self.max_length,
+                                           min_len=self.min_length)
+            tok = r["tokens"].cpu().numpy()
+            sc = r["scores"].cpu().numpy()
+            ln = r["lens"].cpu().numpy()
+            for i in range(n):
+                out.append(([float(sc[i, k]) for k in range(self.n_best)],
+                            [tok[i, k, : ln[i, k]].tolist() for k in range(self.n_best)]))
+        return out
+
+    def _tokens_to_sent(self, toks) -> List[str]:
+        """translate/translation.py:31-47."""
+        words = []
+        for t in toks:
+            w = self.cfg.itos[t]
+            if t == self.cfg.eos_idx:
+                break
+            words.append(w)
+        return words
+
+    def translate(self, src, tgt=None, src_dir=None, batch_size=None, attn_debug=False):
+        """translate/translator.py:181-369.  Returns (all_scores,
+        all_predictions): per chunk, n_best scores and n_best strings."""
+        assert src is not None
+        if batch_size is None:
+            raise ValueError("batch_size must be set")
+        if attn_debug:
+            raise NotImplementedError("-attn_debug attention dumps are not produced on the MI355X path")
+        chunks = [parse_chunk(c) for c in src]
+        res = self.translate_reads([chunks], batch_size=batch_size)[0]
+        return res
+
+    def translate_reads(self, reads: Sequence[Sequence], batch_size: int):
+        """Translate many reads; chunks are packed across reads into engine
+        batches of up to max_batch.  Each chunk keeps the span of the
+        reference batch it would belong to (consecutive ``batch_size`` chunks
+        of its own read), so results equal per-read translate()."""
+        items = []  # (read idx, chunk idx, array, span)
+        for ri, read in enumerate(reads):
+            chunks = [parse_chunk(c) for c in read]
+            for b0 in range(0, len(chunks), batch_size):
+                part = chunks[b0: b0 + batch_size]
+                span = max(len(c) for c in part)
+                for k, c in enumerate(part):
+                    items.append((ri, b0 + k, c, span))
+        results = [[None] * len(r) for r in reads]
+        cap = self.engine.max_batch
+        for s0 in range(0, len(items), cap):
+            grp = items[s0: s0 + cap]
+            outs = self._run([g[2] for g in grp], [g[3] for g in grp])
+            for (ri, ci, _, _), o in zip(grp, outs):
+                results[ri][ci] = o
+        ret = []
+        counter = 0
+        pred_score_total, pred_words_total = 0.0, 0
+        for r in results:
+            all_scores, all_predictions = [], []
+            for scores, toks in r:
+                sents = [self._tokens_to_sent(t) for t in toks]
+                all_scores.append(scores[: self.n_best])
+                all_predictions.append([" ".join(s) for s in sents[: self.n_best]])
+                pred_score_total += scores[0]
+                pred_words_total += len(sents[0])
+                if self.verbose:
+                    counter += 1
+                    msg = "\nSENT {}: {}\n".format(counter, None) + \
+                          "PRED {}: {}\n".format(counter, " ".join(sents[0])) + \
+                          "PRED SCORE: {:.4f}\n".format(scores[0])
+                    if len(sents) > 1:
+                        msg += "\nBEST HYP:\n" + "".join("[{:.4f}] {}\n".format(sc, s)
+                                                         for sc, s in zip(scores, sents))
+                    if self.logger:
+                        self.logger.info(msg)
+                    else:
+                        os.write(1, msg.encode("utf-8"))
+            ret.append((all_scores, all_predictions))
+        if self.report_score and pred_words_total:
+            msg = "PRED AVG SCORE: %.4f, PRED PPL: %.4f" % (pred_score_total / pred_words_total,
+                                                           np.exp(-pred_score_total / pred_words_total))
+            (self.logger.info if self.logger else print)(msg)
+        return ret
+
+    def translate_batch(self, batch, data=None, attn_debug=False, fast=False):
+        """translate/translator.py:505-540 on a batch object with
+        src [T, B, 1], src_lengths [B] (reference batch layout).  Returns the
+        reference's results dict; predictions are token-id tensors (greedy:
+        all max_length tokens; beam: through EOS), scores floats."""
+        src = batch.src[0] if isinstance(batch.src, tuple) else batch.src
+        src = src.detach().to(torch.float32).cpu()
+        T, B = src.shape[0], src.shape[1]
+        lens = batch.src_lengths.detach().cpu().numpy().astype(np.int32)
+        chunks = [src[: lens[i], i, 0].numpy() for i in range(B)]
+        outs = self._run(chunks, [T] * B)
+        return {"predictions": [[torch.tensor(t, dtype=torch.long) for t in toks] for _, toks in outs],
+                "scores": [list(sc) for sc, _ in outs], "attention": [[[]] * len(o[0]) for o in outs],
+                "gold_score": [0] * B, "batch": batch}

@@ -83,7 +83,7 @@ def test_enc_attention_vs_oracle():
 
 
 # ----------------------------------------------------------------- golden
-@pytest.mark.parametrize("name", ["transformer_greedy", "transformer_pe_short"])
+@pytest.mark.parametrize("name", ["transformer_greedy", "transformer_pe_short", "nano_greedy"])
 def test_encoder_memory_vs_golden(name):
     z, meta = gu.load(name)
     cfg, W = gu.model_for(meta)
@@ -98,7 +98,7 @@ def test_encoder_memory_vs_golden(name):
     assert np.abs(sub - z["memory_sub"]).max() < 1e-4
 
 
-@pytest.mark.parametrize("name", ["transformer_greedy", "transformer_pe_short"])
+@pytest.mark.parametrize("name", ["transformer_greedy", "transformer_pe_short", "nano_greedy"])
 @pytest.mark.parametrize("graphs", [True, False])
 def test_greedy_vs_golden(name, graphs):
     z, meta = gu.load(name)
@@ -171,3 +171,28 @@ def test_greedy_vs_oracle_batch32():
     same = (got_tok == o["tokens"]).all(axis=1)
     assert n_tie <= 1
     assert gu.logp_close(got_lp[same], o["logp"][same], atol=LOGP_ATOL).all()
+
+
+def test_nano_greedy_vs_oracle_ragged():
+    """NanoEncoder packing: ragged lengths inside one batch (reverse LSTM
+    starts at len-1), B not a multiple of the 16-sequence LSTM group."""
+    ref = _oracle()
+    cfg = synth.ModelConfig(encoder_type="nano")
+    W = synth.make_weights(cfg, seed=14, eos_bias=-2.0)
+    B = 19
+    sig = synth.synth_chunk_batch(B, 512, seed=9)
+    lens = np.full(B, 512, np.int32)
+    for i, L in ((3, 77), (7, 300), (18, 1)):
+        lens[i] = L
+        sig[i, L:] = 0.0
+    eng = _engine(cfg, W, max_batch=B, max_steps=30)
+    mem = eng.encode(sig, lens, np.full(B, 512, np.int32)).cpu().numpy()
+    m = ref.RefModel(cfg, W)
+    exp_mem = m.encode(torch.from_numpy(sig), lens).numpy()
+    for i in range(B):
+        assert np.abs(mem[i] - exp_mem[i]).max() < 2e-4, i
+    r = eng.translate_greedy(sig, lens, np.full(B, 512, np.int32), max_len=30, return_logp=True)
+    o = ref.greedy(m, sig, lens, max_length=30)
+    n_tie = _compare_tokens(r["tokens"].cpu().numpy(), o["tokens"], o["logp"])
+    assert n_tie == 0
+    assert gu.logp_close(r["logp"].cpu().numpy(), o["logp"], atol=LOGP_ATOL).all()

@@ -1,0 +1,127 @@
+"""Host logic of the Translator drop-in (batching, spans, ordering, EOS cut,
+errors) with a recording stand-in for the HIP engine.  CPU only."""
+import types
+
+import numpy as np
+import pytest
+import torch
+
+from nanodecoder_amd import synth
+from nanodecoder_amd.translator import Translator, parse_chunk
+
+
+class FakeEngine:
+    """Encodes each chunk's (len, span) into its tokens so tests can check
+    what the Translator passed to the engine."""
+
+    def __init__(self, max_batch=8, max_src_len=512):
+        self.max_batch, self.max_src_len = max_batch, max_src_len
+        self.calls = []
+
+    def _tok(self, L, S, n):
+        row = [4 + (L % 4), 4 + (S % 4), 5, 3] + [6] * (n - 4)
+        return row[:n]
+
+    def translate_greedy(self, sig, L, S, max_len, min_len=0):
+        self.calls.append(("greedy", sig.shape, L.copy(), S.copy()))
+        tok = torch.tensor([self._tok(int(a), int(b), max_len) for a, b in zip(L, S)], dtype=torch.int32)
+        return {"tokens": tok, "scores": torch.tensor(L, dtype=torch.float32) * -0.01, "logp": None}
+
+    def translate_beam(self, sig, L, S, beam, n_best, alpha, max_len, min_len=0):
+        self.calls.append(("beam", sig.shape, L.copy(), S.copy()))
+        B = len(L)
+        tok = torch.full((B, n_best, max_len), -1, dtype=torch.int32)
+        lens = torch.zeros(B, n_best, dtype=torch.int32)
+        sc = torch.zeros(B, n_best)
+        for i in range(B):
+            for k in range(n_best):
+                t = self._tok(int(L[i]), int(S[i]) + k, 4)
+                tok[i, k, :4] = torch.tensor(t)
+                lens[i, k] = 4
+                sc[i, k] = -float(k)
+        return {"tokens": tok, "scores": sc, "lens": lens, "steps": torch.tensor([4])}
+
+
+def make_tr(**over):
+    opt = dict(gpu=0, n_best=1, max_length=10, min_length=0, beam_size=1, random_sampling_temp=1.0,
+               random_sampling_topk=1, block_ngram_repeat=0, dump_beam="", replace_unk=False, verbose=False,
+               fast=False, alpha=0.0, beta=0.0, batch_size=3)
+    opt.update(over)
+    eng = FakeEngine()
+    return Translator(synth.ModelConfig(), None, types.SimpleNamespace(**opt), engine=eng), eng
+
+
+def chunks(lens, seed=0):
+    rng = np.random.default_rng(seed)
+    return [rng.normal(size=n).astype(np.float32) for n in lens]
+
+
+def test_parse_chunk_string_matches_float32_cast():
+    x = np.random.default_rng(1).normal(size=20)
+    s = " ".join(str(v) for v in x)      # utils/labelop.py:231 str() round trip
+    np.testing.assert_array_equal(parse_chunk(s), x.astype(np.float32))
+
+
+def test_reference_batching_spans_and_order():
+    tr, eng = make_tr()
+    lens = [512, 512, 512, 512, 300]           # batches of 3: [512x3], [512, 300]
+    sc, preds = tr.translate(chunks(lens), batch_size=3)
+    assert len(preds) == 5 and all(len(p) == 1 for p in preds)
+    # every chunk's span is its own reference batch's longest chunk (512 here)
+    for i, L in enumerate(lens):
+        assert preds[i][0] == " ".join(synth.DEFAULT_ITOS[t] for t in (4 + L % 4, 4 + 512 % 4, 5))
+    # a reference batch made only of short chunks has a short span
+    tr, eng = make_tr()
+    sc, preds = tr.translate(chunks([512, 512, 512, 200, 150]), batch_size=3)
+    assert preds[3][0].split()[1] == synth.DEFAULT_ITOS[4 + 200 % 4]
+    assert preds[4][0].split()[1] == synth.DEFAULT_ITOS[4 + 200 % 4]
+
+
+def test_eos_truncation_and_scores():
+    tr, eng = make_tr()
+    sc, preds = tr.translate(chunks([100]), batch_size=3)
+    assert preds[0][0].count(" ") == 2          # 3 tokens then EOS
+    assert abs(sc[0][0] - (-1.0)) < 1e-6
+
+
+def test_pack_across_reads_equals_per_read():
+    reads = [chunks([512, 512, 77], seed=1), chunks([512, 300], seed=2), chunks([60], seed=3)]
+    tr, eng = make_tr()
+    packed = tr.translate_reads(reads, batch_size=2)
+    for r, exp in zip(reads, packed):
+        tr2, _ = make_tr()
+        assert tr2.translate(r, batch_size=2) == exp
+    # packing fills engine batches across reads
+    assert len(eng.calls) == 1 and eng.calls[0][1][0] >= 6
+
+
+def test_beam_n_best():
+    tr, eng = make_tr(beam_size=5, fast=True, n_best=2)
+    sc, preds = tr.translate(chunks([512, 300]), batch_size=2)
+    assert [len(p) for p in preds] == [2, 2]
+    assert sc[0] == [0.0, -1.0]
+
+
+def test_reference_errors():
+    tr, _ = make_tr()
+    with pytest.raises(ValueError):
+        tr.translate(chunks([10]), batch_size=None)
+    with pytest.raises(NotImplementedError):
+        make_tr(beam_size=5, fast=False)
+    with pytest.raises(NotImplementedError):
+        make_tr(random_sampling_topk=5)
+    with pytest.raises(AssertionError):
+        make_tr(beam_size=5, fast=True, beta=0.5)
+    with pytest.raises(RuntimeError):
+        Translator(synth.ModelConfig(), None, types.SimpleNamespace(gpu=-1))
+
+
+def test_translate_batch_reference_layout():
+    tr, eng = make_tr()
+    src = torch.zeros(512, 2, 1)
+    src[:, 0, 0] = 1.5
+    src[:300, 1, 0] = 2.0
+    b = types.SimpleNamespace(src=src, src_lengths=torch.tensor([512, 300]), batch_size=2)
+    res = tr.translate_batch(b, None, False)
+    assert len(res["predictions"]) == 2 and res["predictions"][0][0].dtype == torch.long
+    assert list(eng.calls[0][3][:2]) == [512, 512]
