@@ -40,8 +40,12 @@ def parse():
     ap.add_argument("--beam", type=int, default=5)
     ap.add_argument("--encoder", default="transformer", choices=["transformer", "nano"])
     ap.add_argument("--max-length", type=int, default=100)
+    ap.add_argument("--min-length", type=int, default=57,
+                    help="-min_length: EOS masked before this step.  The random-init model is EOS-prone, so this "
+                         "sets its decode length to a trained basecaller's ~57 bases per 512 samples (greedy cost "
+                         "is unaffected: all max_length steps always run)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 (0 = skip)")
-    ap.add_argument("--cpu-chunks", type=int, default=8)
+    ap.add_argument("--cpu-chunks", type=int, default=0, help="CPU baseline sample size (0: 128 greedy / 24 beam)")
     ap.add_argument("--no-roofline", action="store_true")
     return ap.parse_args()
 
@@ -56,68 +60,85 @@ def dist_setup(args):
     return world, rank, local
 
 
-def bcast_weights(W, world, local):
-    """One RCCL broadcast of the packed fp32 weight blob from rank 0."""
-    if world == 1:
-        return W
-    names = sorted(W)
-    sizes = [W[n].size for n in names]
-    blob = torch.empty(sum(sizes), dtype=torch.float32, device=torch.device("cuda", local))
-    if int(os.environ.get("RANK", "0")) == 0:
-        blob.copy_(torch.from_numpy(np.concatenate([W[n].ravel() for n in names])))
-    torch.distributed.broadcast(blob, src=0)
-    host = blob.cpu().numpy()
-    out, off = {}, 0
-    for n, s in zip(names, sizes):
-        out[n] = host[off: off + s].reshape(W[n].shape)
-        off += s
-    return out
-
-
 def cpu_baseline(cfg, W, sig, lens, args):
     from oracle import ref_cpu
-    n = min(args.cpu_chunks, sig.shape[0])
+    n = min(args.cpu_chunks or (128 if args.mode == "greedy" else 24), sig.shape[0])
     threads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
     m = ref_cpu.RefModel(cfg, W)
     t0 = time.perf_counter()
     if args.mode == "greedy":
-        ref_cpu.greedy(m, sig[:n], lens[:n], max_length=args.max_length)
+        ref_cpu.greedy(m, sig[:n], lens[:n], max_length=args.max_length, min_length=args.min_length)
     else:
-        ref_cpu.fast_beam(m, sig[:n], lens[:n], beam_size=args.beam, max_length=args.max_length)
+        ref_cpu.fast_beam(m, sig[:n], lens[:n], beam_size=args.beam, max_length=args.max_length,
+                          min_length=args.min_length)
     dt = time.perf_counter() - t0
     return {"value": float(lens[:n].sum() / dt), "unit": "samples/s", "cores": threads, "kind": "port",
             "sample": f"oracle/ref_cpu.py {args.mode} on {n} chunks x 512 samples, max_length {args.max_length}, "
                       f"torch CPU fp32, {threads} threads, {dt:.1f} s"}
 
 
-def kernel_roofline(eng, B):
-    """Dominant kernel = encoder FFN1 GEMM (fp32 MFMA): [B*512,256]x[256,2048]
-    with LN prologue + bias + ReLU.  Timed standalone through the C-ABI op
-    entry point on the current torch stream with HIP events."""
-    from nanodecoder_amd.engine import op_gemm
+def _time(fn, n):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for i in range(n):
+        fn(i)
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / n
+
+
+def _pmc_traffic(name):
+    """HBM bytes per launch for `name` from the committed PMC summary
+    (profiles/pmc_summary.json, written by tools/pmc_summary.py from
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes with the gfx950 x2
+    FETCH_SIZE correction), or None."""
+    p = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    try:
+        with open(p) as f:
+            return json.load(f)["kernels"][name]["hbm_bytes_per_launch"]
+    except Exception:
+        return None
+
+
+def kernel_roofline(eng, B, mode, beam):
+    """Dominant kernel of the translate step: the decoder context attention
+    (HBM-bound: every step streams each chunk's context K and V).  Timed
+    standalone through the C-ABI op entry point on the current torch stream
+    with HIP events, on the engine's shapes, cycling the three layers' K/V
+    column offsets as the decode loop does.  Algorithmic bytes per launch =
+    K+V (2 x 512 keys x 256 f32 per chunk) + q, signal and output rows."""
+    from nanodecoder_amd.engine import op_dec_ctx_attention, op_gemm
     dev = eng.device
-    M, K, N = B * 512, 256, 2048
+    rpc = 1 if mode == "greedy" else beam
+    T, D = 512, 256
+    kv = torch.randn(B * T, 3 * 2 * D, device=dev)
+    q = torch.randn(B * rpc, D, device=dev)
+    sig = torch.randn(B, T, device=dev)
+    span = torch.full((B,), T, dtype=torch.int32, device=dev)
+    fn = lambda i: op_dec_ctx_attention(q, kv, 3 * 2 * D, (i % 3) * 2 * D, sig, span, 1.0, rpc)  # noqa: E731
+    for i in range(6):
+        fn(i)
+    ms = _time(fn, 30)
+    nbytes = B * T * 2 * D * 4 + B * T * 4 + 2 * B * rpc * D * 4
+    ach = nbytes / (ms * 1e-3) / 1e9
+    out = {"bound": "hbm", "kernel": f"dec_ctx_attention_kernel<{rpc}>", "achieved": round(ach, 1), "peak": 8000.0,
+           "unit": "GB/s", "frac": round(ach / 8000.0, 4), "traffic": _pmc_traffic(f"dec_ctx_attention_kernel<{rpc}>"),
+           "algorithmic_bytes_per_launch": nbytes, "avg_launch_ms": round(ms, 5)}
+    # secondary: the dominant MFMA kernel (encoder FFN1 GEMM, LN prologue + bias + ReLU)
+    M, K, N = B * T, 256, 2048
     A = torch.randn(M, K, device=dev)
     Wt = torch.randn(N, K, device=dev) / 16
     b = torch.randn(N, device=dev)
-    g = torch.ones(K, device=dev)
-    bb = torch.zeros(K, device=dev)
+    g1, b1 = torch.ones(K, device=dev), torch.zeros(K, device=dev)
     for _ in range(3):
-        op_gemm(A, Wt, b, None, g, bb, True)
-    n = 20
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(n):
-        op_gemm(A, Wt, b, None, g, bb, True)
-    e1.record()
-    e1.synchronize()
-    ms = e0.elapsed_time(e1) / n
-    flops = 2.0 * M * N * K
-    ach = flops / (ms * 1e-3) / 1e12
-    return {"bound": "mfma", "kernel": "gemm_f32_kernel<128,128,2,2,LN,RELU> (encoder FFN1)",
-            "achieved": round(ach, 2), "peak": 157.3, "unit": "TFLOP/s", "frac": round(ach / 157.3, 4),
-            "traffic": None, "per_launch_flop": flops, "avg_launch_ms": round(ms, 4)}
+        op_gemm(A, Wt, b, None, g1, b1, True)
+    gms = _time(lambda i: op_gemm(A, Wt, b, None, g1, b1, True), 10)
+    tf = 2.0 * M * N * K / (gms * 1e-3) / 1e12
+    out["mfma_kernel"] = {"kernel": "gemm_f32_kernel<128,128,2,2,LN,RELU> (encoder FFN1)", "achieved": round(tf, 2),
+                          "peak": 157.3, "unit": "TFLOP/s", "frac": round(tf / 157.3, 4),
+                          "avg_launch_ms": round(gms, 4)}
+    return out
 
 
 def main():
@@ -129,9 +150,11 @@ def main():
     from nanodecoder_amd.engine import Engine
 
     cfg = synth.ModelConfig(encoder_type=args.encoder)
-    W = synth.make_weights(cfg, seed=11, eos_bias=-3.0) if rank == 0 or world == 1 else \
-        synth.make_weights(cfg, seed=11, eos_bias=-3.0)
-    W = bcast_weights(W, world, local)
+    # rank 0 owns the weights; one RCCL broadcast of the packed blob reaches the others
+    W = synth.make_weights(cfg, seed=11, eos_bias=-3.0) if rank == 0 else None
+    if world > 1:
+        from nanodecoder_amd.shard import broadcast_weights
+        W = broadcast_weights(W, dev)
     beam = args.beam if args.mode == "beam" else 1
     eng = Engine(cfg, W, device=local, max_batch=args.batch, max_src_len=512, max_steps=args.max_length,
                  max_beam=beam)
@@ -143,8 +166,9 @@ def main():
 
     def step():
         if args.mode == "greedy":
-            return eng.translate_greedy(sig, lens, lens, max_len=args.max_length)
-        return eng.translate_beam(sig, lens, lens, beam=args.beam, max_len=args.max_length)
+            return eng.translate_greedy(sig, lens, lens, max_len=args.max_length, min_len=args.min_length)
+        return eng.translate_beam(sig, lens, lens, beam=args.beam, max_len=args.max_length,
+                                  min_len=args.min_length)
 
     for _ in range(args.warmup):
         out = step()
@@ -186,10 +210,13 @@ def main():
                    "global_batch": args.batch * world, "seq_len": 512, "parallelism": f"read-shard x{world}"},
         "samples_per_sec_per_gpu": round(value / world, 1),
         "bases_per_sec": round(bases_per_step * args.steps * world / dt, 1),
+        "min_length": args.min_length,
     }
+    if args.mode == "beam":
+        res["decoder_steps_executed"] = int(out["steps"].cpu().item())
     if rank == 0:
         if not args.no_roofline:
-            res["roofline"] = kernel_roofline(eng, args.batch)
+            res["roofline"] = kernel_roofline(eng, args.batch, args.mode, beam)
         if args.cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(cfg, W, sig_np, lens_np, args)
         print(json.dumps(res), flush=True)

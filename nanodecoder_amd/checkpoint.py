@@ -62,10 +62,9 @@ _ALLOWED = {
     ("torch._utils", "_rebuild_tensor_v2"): torch._utils._rebuild_tensor_v2,
     ("torch._utils", "_rebuild_parameter"): torch._utils._rebuild_parameter,
     ("torch", "Size"): torch.Size,
-    ("builtins", "set"): set,
-    ("builtins", "frozenset"): frozenset,
-    ("builtins", "slice"): slice,
 }
+for _b in (set, frozenset, slice, int, float, complex, bool, str, bytes, bytearray, list, dict, tuple, range):
+    _ALLOWED[("builtins", _b.__name__)] = _b
 for _t in ("FloatStorage", "DoubleStorage", "HalfStorage", "LongStorage", "IntStorage", "ShortStorage",
            "CharStorage", "ByteStorage", "BoolStorage", "BFloat16Storage"):
     if hasattr(torch, _t):
@@ -75,6 +74,12 @@ _STUB_PREFIXES = ("torchtext", "onmt", "torch.optim", "inputters", "models", "ut
 
 class _RestrictedUnpickler(pickle.Unpickler):
     def find_class(self, module, name):
+        # protocol-2 pickles carry Python 2 names (__builtin__.long, ...)
+        import _compat_pickle
+        if (module, name) in _compat_pickle.NAME_MAPPING:
+            module, name = _compat_pickle.NAME_MAPPING[(module, name)]
+        elif module in _compat_pickle.IMPORT_MAPPING:
+            module = _compat_pickle.IMPORT_MAPPING[module]
         if (module, name) in _ALLOWED:
             return _ALLOWED[(module, name)]
         if module.startswith(_STUB_PREFIXES):

@@ -298,6 +298,7 @@ static int alloc_workspaces(nd_ctx* c) {
   WS(c->bs.hyp_tok, B * NB * S);
   WS(c->bs.n_alive, 4);
   WS(c->steps_done, 4);
+  c->bs.steps_done = c->steps_done;
 #undef WS
   if ((e = hipHostMalloc((void**)&c->h_alive, 16, hipHostMallocDefault)) != hipSuccess)
     return fail(ND_ERR_HIP, std::string("hipHostMalloc: ") + hipGetErrorString(e));

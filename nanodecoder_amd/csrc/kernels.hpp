@@ -69,6 +69,7 @@ struct BeamState {
   int* hyp_len;      // [C, n_best]
   int* hyp_tok;      // [C, n_best, S]
   int* n_alive;      // [1] chunks not done
+  int* steps_done;   // [1] decoder steps until the last chunk finished
 };
 hipError_t launch_beam_init(const BeamState& st, int C, int beam, int n_best, int S, int bos, hipStream_t s);
 hipError_t launch_beam_step(const float* x, const float* ln_g, const float* ln_b, const float* gw, const float* gb,

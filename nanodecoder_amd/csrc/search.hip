@@ -203,7 +203,7 @@ beam_step_kernel(const float* __restrict__ x, const float* __restrict__ ln_g, co
       st.n_hyp[c] = nh;
       if (st.top_fin[c] && nh >= n_best) {  // :780
         st.done[c] = 1;
-        atomicSub(st.n_alive, 1);
+        if (atomicSub(st.n_alive, 1) == 1) *st.steps_done = step + 1;
       }
     }
   }

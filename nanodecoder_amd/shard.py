@@ -1,0 +1,175 @@
+"""Multi-GPU read sharding (BASELINE config 5).
+
+Reads are independent, so the path shards with NO collective in the hot
+loop: one process per GPU (torch.distributed.run), reads assigned to ranks by
+a longest-processing-time balance on sample count, rank 0's weights sent once
+as one packed fp32 blob (``broadcast`` — RCCL over xGMI with backend "nccl"),
+and one final ``all_reduce`` of [samples, bases, chunks] (+ MAX of seconds)
+for reporting.  Each rank packs chunks of many reads into full engine
+batches; every chunk keeps the span of its reference batch (consecutive
+``batch_size`` chunks of its own read), so outputs equal the reference's
+per-read translate.
+
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \\
+        -m nanodecoder_amd.shard --reads 1048576
+"""
+from __future__ import annotations
+
+import argparse
+import heapq
+import json
+import os
+import time
+from typing import Callable, Dict, List, Sequence
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import synth
+
+
+def lpt_assign(weights: Sequence[int], world: int) -> List[List[int]]:
+    """Longest-processing-time-first: heaviest item to the least loaded rank
+    (ties: lower item index first, lower rank first).  Deterministic."""
+    order = sorted(range(len(weights)), key=lambda i: (-weights[i], i))
+    heap = [(0, r) for r in range(world)]
+    out = [[] for _ in range(world)]
+    for i in order:
+        load, r = heapq.heappop(heap)
+        out[r].append(i)
+        heapq.heappush(heap, (load + int(weights[i]), r))
+    return [sorted(x) for x in out]
+
+
+def read_lengths(n_reads: int, seed: int = 0, lo: int = 256, hi: int = 1024) -> np.ndarray:
+    """The synthetic 1M-read set's lengths ~ U[lo, hi] samples (§8d config 5)."""
+    return np.random.default_rng(seed).integers(lo, hi + 1, size=n_reads)
+
+
+def synth_read(read_id: int, n: int) -> np.ndarray:
+    """Vectorised synthetic read (same model as synth.synth_raw_read),
+    median/MAD normalised, float64."""
+    rng = np.random.default_rng(1234 + read_id)
+    dw = rng.geometric(1.0 / 9.0, size=n // 2 + 16)
+    lv = rng.normal(90.0, 15.0, size=dw.size)
+    raw = np.round(np.repeat(lv, dw)[:n] + rng.normal(0.0, 2.0, size=n))
+    return synth.normalize_median(raw)
+
+
+def pack_weights(W: Dict[str, np.ndarray]):
+    names = sorted(W)
+    meta = [(n, tuple(W[n].shape)) for n in names]
+    blob = np.concatenate([np.ascontiguousarray(W[n], np.float32).ravel() for n in names]) if names else \
+        np.zeros(0, np.float32)
+    return meta, blob
+
+
+def unpack_weights(meta, blob: np.ndarray) -> Dict[str, np.ndarray]:
+    out, off = {}, 0
+    for n, shp in meta:
+        size = int(np.prod(shp)) if shp else 1
+        out[n] = blob[off: off + size].reshape(shp)
+        off += size
+    return out
+
+
+def broadcast_weights(W, device) -> Dict[str, np.ndarray]:
+    """ONE collective for the weights: rank 0's packed blob to every rank."""
+    rank = dist.get_rank()
+    obj = [pack_weights(W)[0] if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    meta = obj[0]
+    total = sum(int(np.prod(s)) if s else 1 for _, s in meta)
+    t = torch.empty(total, dtype=torch.float32, device=device)
+    if rank == 0:
+        t.copy_(torch.from_numpy(pack_weights(W)[1]))
+    dist.broadcast(t, src=0)
+    return unpack_weights(meta, t.cpu().numpy())
+
+
+class ReadShard:
+    """Translates one rank's reads with a Translator-like object exposing
+    ``translate_reads(list_of_chunk_lists, batch_size)``."""
+
+    def __init__(self, translator, batch_size: int = 100, src_seq_length: int = 512, src_seq_stride: int = 512,
+                 reads_per_pass: int = 256):
+        self.tr = translator
+        self.batch_size = batch_size
+        self.L, self.stride = src_seq_length, src_seq_stride
+        self.reads_per_pass = reads_per_pass
+
+    def run(self, read_ids: Sequence[int], lengths: Sequence[int], keep_predictions: bool = False):
+        samples = bases = chunks = 0
+        preds = {}
+        t0 = time.perf_counter()
+        for g0 in range(0, len(read_ids), self.reads_per_pass):
+            ids = read_ids[g0: g0 + self.reads_per_pass]
+            reads = [synth.window(synth_read(int(i), int(lengths[i])), self.L, self.stride) for i in ids]
+            outs = self.tr.translate_reads(reads, batch_size=self.batch_size)
+            for rid, rd, (_, p) in zip(ids, reads, outs):
+                samples += sum(len(c) for c in rd)
+                chunks += len(rd)
+                bases += sum(len(x[0].replace(" ", "")) for x in p)
+                if keep_predictions:
+                    preds[int(rid)] = p
+        return dict(samples=samples, bases=bases, chunks=chunks, seconds=time.perf_counter() - t0), preds
+
+
+def run_distributed(n_reads: int, translator_factory: Callable, weights_factory: Callable, device,
+                    batch_size: int = 100, seed: int = 0, keep_predictions: bool = False):
+    """Rank-local part of the sharded job; returns (global stats, local preds)."""
+    rank, world = dist.get_rank(), dist.get_world_size()
+    lengths = read_lengths(n_reads, seed)
+    mine = lpt_assign(lengths.tolist(), world)[rank]
+    W = weights_factory() if rank == 0 else None
+    W = broadcast_weights(W, device)
+    tr = translator_factory(W)
+    dist.barrier()
+    stats, preds = ReadShard(tr, batch_size=batch_size).run(mine, lengths, keep_predictions)
+    dist.barrier()
+    red = torch.tensor([stats["samples"], stats["bases"], stats["chunks"]], dtype=torch.float64, device=device)
+    secs = torch.tensor([stats["seconds"]], dtype=torch.float64, device=device)
+    dist.all_reduce(red)
+    dist.all_reduce(secs, op=dist.ReduceOp.MAX)
+    g = dict(samples=int(red[0]), bases=int(red[1]), chunks=int(red[2]), seconds=float(secs[0]), world=world)
+    return g, preds
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reads", type=int, default=4096)
+    ap.add_argument("--batch-size", type=int, default=100, help="reference batch_size (chunks per read batch)")
+    ap.add_argument("--engine-batch", type=int, default=512)
+    ap.add_argument("--max-length", type=int, default=100)
+    ap.add_argument("--min-length", type=int, default=0)
+    ap.add_argument("--seed", type=int, default=0)
+    args = ap.parse_args(argv)
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist.init_process_group("nccl", device_id=dev)
+    from .engine import Engine
+    from .translator import Translator
+    cfg = synth.ModelConfig()
+
+    def weights_factory():
+        return synth.make_weights(cfg, seed=11, eos_bias=-3.0)
+
+    def translator_factory(W):
+        opt = argparse.Namespace(gpu=local, n_best=1, max_length=args.max_length, min_length=args.min_length,
+                                 beam_size=1, batch_size=args.batch_size, engine_max_batch=args.engine_batch)
+        eng = Engine(cfg, W, device=local, max_batch=args.engine_batch, max_steps=args.max_length)
+        return Translator(cfg, W, opt, engine=eng)
+
+    g, _ = run_distributed(args.reads, translator_factory, weights_factory, dev, batch_size=args.batch_size,
+                           seed=args.seed)
+    if dist.get_rank() == 0:
+        g["samples_per_sec"] = g["samples"] / g["seconds"]
+        g["bases_per_sec"] = g["bases"] / g["seconds"]
+        print(json.dumps(g), flush=True)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
