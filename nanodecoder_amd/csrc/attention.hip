@@ -18,21 +18,35 @@
 namespace nd {
 
 // ------------------------------------------------------------------ encoder
+// Full-row statistics {mean, M2} of a 256-wide row held as float4 per lane
+// (the part_n = 1 form of the GEMM row-statistics hand-off).
+__device__ __forceinline__ void row_part(f32x4 v, int lane, float* part) {
+  const float mu = wave_sum(v.x + v.y + v.z + v.w) * (1.0f / ND_D);
+  const f32x4 d = v - mu;
+  const float q = wave_sum(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w);
+  if (lane == 0) {
+    part[0] = mu;
+    part[1] = q;
+  }
+}
+
 __global__ void __launch_bounds__(256)
 enc_embed_kernel(const float* __restrict__ signal, const float* __restrict__ w, const float* __restrict__ b,
-                 float* __restrict__ x, int n_rows) {
+                 float* __restrict__ x, float* __restrict__ part, int n_rows) {
   // encoder/transformer.py:104,113 — Linear(1, d) applied to the scalar sample
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= n_rows) return;
   const float s = signal[row];
   const f32x4 wv = ld4(w + lane * 4), bv = ld4(b + lane * 4);
-  st4(x + (size_t)row * ND_D + lane * 4, s * wv + bv);
+  const f32x4 v = s * wv + bv;
+  st4(x + (size_t)row * ND_D + lane * 4, v);
+  if (part) row_part(v, lane, part + (size_t)row * ND_PART_LD * 2);
 }
 
-hipError_t launch_enc_embed(const float* signal, const float* w_in, const float* b_in, float* x, int B, int T,
-                            hipStream_t s) {
+hipError_t launch_enc_embed(const float* signal, const float* w_in, const float* b_in, float* x, float* part, int B,
+                            int T, hipStream_t s) {
   const int rows = B * T;
-  hipLaunchKernelGGL(enc_embed_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, signal, w_in, b_in, x, rows);
+  hipLaunchKernelGGL(enc_embed_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, signal, w_in, b_in, x, part, rows);
   return hipGetLastError();
 }
 
@@ -175,18 +189,19 @@ hipError_t launch_enc_attention(const float* qkv, const float* signal, const int
 // ------------------------------------------------------------------ decoder
 __global__ void __launch_bounds__(256)
 dec_embed_kernel(const int* __restrict__ tok, const float* __restrict__ emb, const float* __restrict__ pe, int step,
-                 float* __restrict__ x, int R) {
+                 float* __restrict__ x, float* __restrict__ part, int R) {
   // onmt/modules/embeddings.py:189-207 (+ PositionalEncoding.forward :36-43)
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= R) return;
   f32x4 e = ld4(emb + (size_t)tok[row] * ND_D + lane * 4);
   if (pe) e = e * 16.0f + ld4(pe + (size_t)step * ND_D + lane * 4);  // sqrt(256) = 16
   st4(x + (size_t)row * ND_D + lane * 4, e);
+  if (part) row_part(e, lane, part + (size_t)row * ND_PART_LD * 2);
 }
 
-hipError_t launch_dec_embed(const int* tok, const float* emb, const float* pe, int step, float* x, int R,
-                            hipStream_t s) {
-  hipLaunchKernelGGL(dec_embed_kernel, dim3((R + 3) / 4), dim3(256), 0, s, tok, emb, pe, step, x, R);
+hipError_t launch_dec_embed(const int* tok, const float* emb, const float* pe, int step, float* x, float* part,
+                            int R, hipStream_t s) {
+  hipLaunchKernelGGL(dec_embed_kernel, dim3((R + 3) / 4), dim3(256), 0, s, tok, emb, pe, step, x, part, R);
   return hipGetLastError();
 }
 
@@ -195,11 +210,12 @@ hipError_t launch_dec_embed(const int* tok, const float* emb, const float* pe, i
 // 4*lane..4*lane+3 (head = lane/8); waves split the keys, 4 per iteration, so
 // every K/V row is one coalesced 1 KB wave load.
 #define SELF_MAXS 256
-__global__ void __launch_bounds__(256)
+#define SELF_NW 8
+__global__ void __launch_bounds__(SELF_NW * 64)
 dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cache, const int* __restrict__ anc,
                           int anc_ld, int step, int S, float* __restrict__ out) {
   __shared__ float p[ND_H][SELF_MAXS];
-  __shared__ float part[4][ND_D];
+  __shared__ float part[SELF_NW][ND_D];
   const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const float* qrow = qkv + (size_t)r * 3 * ND_D;
   const f32x4 q = ld4(qrow + lane * 4) / ND_SQRT_DH;
@@ -217,16 +233,16 @@ dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cac
     return cache + ((size_t)slot * S + t) * 2 * ND_D;
   };
   // scores: keys t < step come from the cache, key `step` from registers
-  for (int t0 = wave; t0 < n; t0 += 16) {
+  for (int t0 = wave; t0 < n; t0 += 4 * SELF_NW) {
     f32x4 k[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int t = t0 + 4 * u;
+      const int t = t0 + SELF_NW * u;
       k[u] = (t < step) ? ld4(krow(t) + lane * 4) : kme;
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int t = t0 + 4 * u;
+      const int t = t0 + SELF_NW * u;
       float d = q.x * k[u].x + q.y * k[u].y + q.z * k[u].z + q.w * k[u].w;
       d += __shfl_xor(d, 1, 64);
       d += __shfl_xor(d, 2, 64);
@@ -236,7 +252,7 @@ dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cac
   }
   __syncthreads();
   // softmax per head (no mask while stepping): wave w handles heads w, w+4
-  for (int h2 = wave; h2 < ND_H; h2 += 4) {
+  for (int h2 = wave; h2 < ND_H; h2 += SELF_NW) {
     float mx = -INFINITY;
     for (int t = lane; t < n; t += 64) mx = fmaxf(mx, p[h2][t]);
     mx = wave_max(mx);
@@ -252,28 +268,33 @@ dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cac
   }
   __syncthreads();
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (int t0 = wave; t0 < n; t0 += 16) {
+  for (int t0 = wave; t0 < n; t0 += 4 * SELF_NW) {
     f32x4 v[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int t = t0 + 4 * u;
+      const int t = t0 + SELF_NW * u;
       v[u] = (t < step) ? ld4(krow(t) + ND_D + lane * 4) : vme;
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int t = t0 + 4 * u;
+      const int t = t0 + SELF_NW * u;
       if (t < n) acc += p[hh][t] * v[u];
     }
   }
   st4(&part[wave][lane * 4], acc);
   __syncthreads();
-  out[(size_t)r * ND_D + tid] = part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid];
+  if (tid < ND_D) {
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < SELF_NW; ++w) v += part[w][tid];
+    out[(size_t)r * ND_D + tid] = v;
+  }
 }
 
 hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* anc, int anc_ld, int step,
                                      int max_steps, float* out, int R, hipStream_t s) {
   if (step >= max_steps || step >= SELF_MAXS) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(dec_self_attention_kernel, dim3(R), dim3(256), 0, s, qkv, cache, anc, anc_ld, step, max_steps,
+  hipLaunchKernelGGL(dec_self_attention_kernel, dim3(R), dim3(SELF_NW * 64), 0, s, qkv, cache, anc, anc_ld, step, max_steps,
                      out);
   return hipGetLastError();
 }

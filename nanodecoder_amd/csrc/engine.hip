@@ -96,6 +96,8 @@ struct nd_ctx {
   int *len = nullptr, *span = nullptr;
   float *x = nullptr, *y = nullptr, *att = nullptr, *big = nullptr, *ctxkv = nullptr;
   float *nano_xp = nullptr, *nano_h = nullptr;
+  float *x_part = nullptr, *y_part = nullptr, *dx_part = nullptr, *dq1_part = nullptr, *dmid_part = nullptr;
+  int x_pn = 1;
   float *dx = nullptr, *dq1 = nullptr, *dmid = nullptr, *dcq = nullptr, *datt = nullptr, *dqkv = nullptr,
         *dhid = nullptr, *cache = nullptr;
   int *tok = nullptr, *gtok = nullptr;
@@ -267,6 +269,11 @@ static int alloc_workspaces(nd_ctx* c) {
   WS(c->att, B * T * D);
   WS(c->big, B * T * std::max(F, 3 * D));
   WS(c->ctxkv, B * T * Ld * 2 * D);
+  WS(c->x_part, B * T * ND_PART_LD * 2);
+  WS(c->y_part, B * T * ND_PART_LD * 2);
+  WS(c->dx_part, R * ND_PART_LD * 2);
+  WS(c->dq1_part, R * ND_PART_LD * 2);
+  WS(c->dmid_part, R * ND_PART_LD * 2);
   if (cfg.encoder_type == ND_ENC_NANO) {
     WS(c->nano_xp, B * T * 8 * (size_t)c->H);
     WS(c->nano_h, B * T * 2 * (size_t)c->H);
@@ -324,27 +331,50 @@ static hipError_t gemm(const float* A, int lda, const float* W, int N, int K, co
   return nd::launch_gemm(g, s);
 }
 
-// Encoder forward (transformer): x <- memory pre-final-LN; then the fused
-// context K/V projection of all decoder layers with the final LN as prologue.
+// Fluent GEMM launch: G(...).ln(...).res(...).stats(...).run(s, &part_n)
+struct G {
+  nd::GemmArgs a;
+  G(const float* A, int lda, const float* W, int N, int K, const float* bias, float* C, int ldc, int M) {
+    a.A = A; a.lda = lda; a.W = W; a.ldw = K; a.bias = bias; a.C = C; a.ldc = ldc; a.M = M; a.N = N; a.K = K;
+  }
+  G& ln(const float* g, const float* b, const float* part, int pn) {
+    a.ln_g = g; a.ln_b = b; a.part_in = part; a.part_n_in = pn;
+    return *this;
+  }
+  G& relu() { a.relu = true; return *this; }
+  G& res(const float* R, int ldr) { a.R = R; a.ldr = ldr; return *this; }
+  G& stats(float* part) { a.part_out = part; return *this; }
+  hipError_t run(hipStream_t s, int* pn_out = nullptr) {
+    hipError_t e = nd::launch_gemm(a, s);
+    if (pn_out) *pn_out = a.part_n_out;
+    return e;
+  }
+};
+
+// Encoder forward (transformer): x <- memory before the final LayerNorm (its
+// row statistics in x_part); the final LN is the ctx-K/V GEMM's prologue.
 static hipError_t enqueue_encode_transformer(nd_ctx* c, int B, int T, hipStream_t s) {
   const int M = B * T, D = c->D, F = c->F;
-  LCHK(nd::launch_enc_embed(c->sig, c->enc_lin_w, c->enc_lin_b, c->x, B, T, s));
+  LCHK(nd::launch_enc_embed(c->sig, c->enc_lin_w, c->enc_lin_b, c->x, c->x_part, B, T, s));
+  int pnx = 1, pny = 0;
   for (auto& L : c->enc) {
     // encoder/transformer.py:36-54
-    LCHK(gemm(c->x, D, L.wqkv, 3 * D, D, L.bqkv, c->big, 3 * D, M, s, L.ln_g, L.ln_b));
+    LCHK(G(c->x, D, L.wqkv, 3 * D, D, L.bqkv, c->big, 3 * D, M).ln(L.ln_g, L.ln_b, c->x_part, pnx).run(s));
     LCHK(nd::launch_enc_attention(c->big, c->sig, c->span, c->att, B, T, s));
-    LCHK(gemm(c->att, D, L.wo, D, D, L.bo, c->y, D, M, s, nullptr, nullptr, false, c->x, D));
-    LCHK(gemm(c->y, D, L.w1, F, D, L.b1, c->big, F, M, s, L.fln_g, L.fln_b, true));
-    LCHK(gemm(c->big, F, L.w2, D, F, L.b2, c->x, D, M, s, nullptr, nullptr, false, c->y, D));
+    LCHK(G(c->att, D, L.wo, D, D, L.bo, c->y, D, M).res(c->x, D).stats(c->y_part).run(s, &pny));
+    LCHK(G(c->y, D, L.w1, F, D, L.b1, c->big, F, M).ln(L.fln_g, L.fln_b, c->y_part, pny).relu().run(s));
+    LCHK(G(c->big, F, L.w2, D, F, L.b2, c->x, D, M).res(c->y, D).stats(c->x_part).run(s, &pnx));
   }
+  c->x_pn = pnx;
   return hipSuccess;
 }
 
 static hipError_t enqueue_ctxkv(nd_ctx* c, int B, int T, hipStream_t s) {
   const int M = B * T, D = c->D, N = (int)c->dec.size() * 2 * D;
   if (c->cfg.encoder_type == ND_ENC_TRANSFORMER)
-    return gemm(c->x, D, c->ctxkv_w, N, D, c->ctxkv_b, c->ctxkv, N, M, s, c->enc_ln_g, c->enc_ln_b);
-  return gemm(c->x, D, c->ctxkv_w, N, D, c->ctxkv_b, c->ctxkv, N, M, s);
+    return G(c->x, D, c->ctxkv_w, N, D, c->ctxkv_b, c->ctxkv, N, M).ln(c->enc_ln_g, c->enc_ln_b, c->x_part, c->x_pn)
+        .run(s);
+  return G(c->x, D, c->ctxkv_w, N, D, c->ctxkv_b, c->ctxkv, N, M).run(s);
 }
 
 static hipError_t enqueue_encode(nd_ctx* c, int B, int T, hipStream_t s);
@@ -354,20 +384,22 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
                                    hipStream_t s) {
   const int R = C * rpc, D = c->D, F = c->F, S = c->cfg.max_steps;
   const int Ld = (int)c->dec.size();
-  LCHK(nd::launch_dec_embed(c->tok, c->emb, c->cfg.position_encoding ? c->pe : nullptr, step, c->dx, R, s));
+  LCHK(nd::launch_dec_embed(c->tok, c->emb, c->cfg.position_encoding ? c->pe : nullptr, step, c->dx, c->dx_part, R,
+                            s));
+  int pnx = 1, pnq = 0, pnm = 0;
   for (int i = 0; i < Ld; ++i) {
     DecLayer& L = c->dec[i];
     float* cache = c->cache + (size_t)i * R * S * 2 * D;
     // decoder/transformer.py:53-95
-    LCHK(gemm(c->dx, D, L.wqkv, 3 * D, D, L.bqkv, c->dqkv, 3 * D, R, s, L.ln1_g, L.ln1_b));
+    LCHK(G(c->dx, D, L.wqkv, 3 * D, D, L.bqkv, c->dqkv, 3 * D, R).ln(L.ln1_g, L.ln1_b, c->dx_part, pnx).run(s));
     LCHK(nd::launch_dec_self_attention(c->dqkv, cache, anc, anc_ld, step, S, c->datt, R, s));
-    LCHK(gemm(c->datt, D, L.wo, D, D, L.bo, c->dq1, D, R, s, nullptr, nullptr, false, c->dx, D));
-    LCHK(gemm(c->dq1, D, L.cwq, D, D, L.cbq, c->dcq, D, R, s, L.ln2_g, L.ln2_b));
+    LCHK(G(c->datt, D, L.wo, D, D, L.bo, c->dq1, D, R).res(c->dx, D).stats(c->dq1_part).run(s, &pnq));
+    LCHK(G(c->dq1, D, L.cwq, D, D, L.cbq, c->dcq, D, R).ln(L.ln2_g, L.ln2_b, c->dq1_part, pnq).run(s));
     LCHK(nd::launch_dec_ctx_attention(c->dcq, c->ctxkv, Ld * 2 * D, i * 2 * D, c->sig, c->span,
                                       (float)c->cfg.pad_idx, c->datt, C, rpc, T, s));
-    LCHK(gemm(c->datt, D, L.cwo, D, D, L.cbo, c->dmid, D, R, s, nullptr, nullptr, false, c->dq1, D));
-    LCHK(gemm(c->dmid, D, L.w1, F, D, L.b1, c->dhid, F, R, s, L.fln_g, L.fln_b, true));
-    LCHK(gemm(c->dhid, F, L.w2, D, F, L.b2, c->dx, D, R, s, nullptr, nullptr, false, c->dmid, D));
+    LCHK(G(c->datt, D, L.cwo, D, D, L.cbo, c->dmid, D, R).res(c->dq1, D).stats(c->dmid_part).run(s, &pnm));
+    LCHK(G(c->dmid, D, L.w1, F, D, L.b1, c->dhid, F, R).ln(L.fln_g, L.fln_b, c->dmid_part, pnm).relu().run(s));
+    LCHK(G(c->dhid, F, L.w2, D, F, L.b2, c->dx, D, R).res(c->dmid, D).stats(c->dx_part).run(s, &pnx));
   }
   return hipSuccess;
 }

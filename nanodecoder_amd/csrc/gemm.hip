@@ -1,64 +1,98 @@
-// fp32 MFMA GEMM for gfx950 with fused LayerNorm prologue and
-// bias / ReLU / residual epilogue.
+// fp32 MFMA GEMMs for gfx950 with fused LayerNorm prologue and
+// bias / ReLU / residual / row-statistics epilogue.
 //
 // Replaces the reference's nn.Linear addmm calls and the LayerNorm that
 // precedes them (onmt/modules/multi_headed_attn.py:59-67,155-157,179;
-// onmt/modules/position_ffn.py:20-22,38-40; encoder/transformer.py:50;
-// decoder/transformer.py:75,88).  The reference computes in fp32, and gfx950
-// has no xf32 MFMA, so the product runs on v_mfma_f32_32x32x2_f32 (exact f32
-// FMA chains, 64 FLOP/clk/SIMD = the fp32 peak).
+// onmt/modules/position_ffn.py:20-22,38-40; encoder/transformer.py:50,125;
+// decoder/transformer.py:75,88).  The reference computes in fp32 and gfx950
+// has no xf32 MFMA, so products run on v_mfma_f32_32x32x2_f32 /
+// v_mfma_f32_16x16x4_f32 (exact fp32 FMA chains at the fp32 peak).
 //
 //   C[M,N] = epi( pro(A)[M,K] . W[N,K]^T + bias[N] )
-//   pro(A) = LN(A) = (A - mean) * rstd * g + b over K      (when LN)
+//   pro(A) = LN(A) = (A - mean) * rstd * g + b over K          (LN)
 //   epi(v) = relu(v) (RELU); v + R[M,N] (RESID)
 //
-// Tiling: BM x BN x 32, WM x WN waves each owning (BM/WM) x (BN/WN) as
-// 32x32 MFMA blocks.  A and W tiles are staged global -> registers -> LDS
-// (double-buffered, one barrier per K step); row stride 36 floats makes the
-// per-lane ds_read_b128 fragment loads bank-conflict free.  Inside an 8-wide
-// k block, lane half h reads k = 4h..4h+3 with one ds_read_b128 and feeds them
-// to 4 consecutive MFMAs, so MFMA step i sums over k = {i, 4+i} — a fixed
-// permutation of the K order that A and W share.
+// LayerNorm fusion across kernels: every producer of a LayerNorm input (the
+// residual GEMMs and the embed kernels) writes per-row partial statistics
+// {mean_j, M2_j} of its column tile; the consuming GEMM merges them (Chan's
+// parallel-variance formula, exact and stable) instead of re-reading whole
+// rows in every column workgroup.
 #include "common.hpp"
 #include "kernels.hpp"
 
 namespace nd {
 
+// Merge P equal-width partials {mean_j, M2_j} of a 256-wide row.
+__device__ __forceinline__ void merge_stats(const float* __restrict__ p, int P, float& mu, float& rs) {
+  const float w = 256.0f / (float)P;
+  float m = 0.f;
+  for (int j = 0; j < P; ++j) m += p[2 * j];
+  m /= (float)P;
+  float m2 = 0.f;
+  for (int j = 0; j < P; ++j) {
+    const float d = p[2 * j] - m;
+    m2 += p[2 * j + 1] + w * d * d;
+  }
+  mu = m;
+  rs = 1.0f / sqrtf(m2 * (1.0f / 256.0f) + ND_LN_EPS);
+}
+
+// ---------------------------------------------------------------------------
+// LDS-tiled kernel (encoder, large M): BM x BN x 32 tiles, WM x WN waves each
+// owning (BM/WM) x (BN/WN) as 32x32 MFMA blocks.  A and W tiles are staged
+// global -> registers -> LDS (double-buffered, one barrier per K step); row
+// stride 36 floats makes the per-lane ds_read_b128 fragment loads
+// bank-conflict free.  Inside an 8-wide k block, lane half h reads
+// k = 4h..4h+3 with one ds_read_b128 and feeds 4 consecutive MFMAs (MFMA i
+// sums k = {i, 4+i}: a permutation of K that A and W share).  The epilogue
+// stages the C tile through LDS so output / residual traffic is coalesced
+// float4 rows, and row statistics fall out of the same pass.
 template <int BM, int BN, int WM, int WN, bool LN, bool RELU, bool RESID>
-__global__ void __launch_bounds__(WM* WN * 64)
-gemm_f32_kernel(const float* __restrict__ A, int lda, const float* __restrict__ W, int ldw,
-                const float* __restrict__ bias, const float* __restrict__ R, int ldr, float* __restrict__ C,
-                int ldc, const float* __restrict__ ln_g, const float* __restrict__ ln_b, int M, int N, int K) {
+__global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g) {
   constexpr int NT = WM * WN * 64;
-  constexpr int BK = 32, LDK = BK + 4;
+  constexpr int BK = 32, LDK = BK + 4, LDC = BN + 4;
   constexpr int FM = BM / WM / 32, FN = BN / WN / 32;
   constexpr int A4 = BM * BK / 4 / NT;
   constexpr int W4 = BN * BK / 4 / NT;
+  constexpr int SMEM = (2 * (BM + BN) * LDK > BM * LDC) ? 2 * (BM + BN) * LDK : BM * LDC;
   static_assert(A4 >= 1 && W4 >= 1, "tile too small for the thread count");
-  __shared__ __attribute__((aligned(16))) float As[2][BM * LDK];
-  __shared__ __attribute__((aligned(16))) float Ws[2][BN * LDK];
+  __shared__ __attribute__((aligned(16))) float smem[SMEM];
   __shared__ float s_mu[LN ? BM : 1], s_rs[LN ? BM : 1];
+  float* As = smem;                  // [2][BM*LDK]
+  float* Ws = smem + 2 * BM * LDK;   // [2][BN*LDK]
+  float* Cs = smem;                  // [BM][LDC] after the main loop
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+  const int M = g.M, K = g.K;
+  const float* __restrict__ A = g.A;
 
   if constexpr (LN) {
-    // two-pass row statistics, one wave per row, K == 256 (host-checked);
-    // 8 rows' loads are issued together so their L2 latencies overlap
-    constexpr int NW = NT / 64, RPW = BM / NW, G = RPW < 8 ? RPW : 8;
-    for (int r0 = 0; r0 < RPW; r0 += G) {
-      f32x4 v[G];
+    if (g.part_in) {
+      for (int r = tid; r < BM; r += NT) {
+        float mu, rs;
+        merge_stats(g.part_in + (size_t)min(m0 + r, M - 1) * ND_PART_LD * 2, g.part_n_in, mu, rs);
+        s_mu[r] = mu;
+        s_rs[r] = rs;
+      }
+    } else {
+      // two-pass row statistics, one wave per row (K == 256, host-checked);
+      // 8 rows' loads are issued together so their latencies overlap
+      constexpr int NW = NT / 64, RPW = BM / NW, G = RPW < 8 ? RPW : 8;
+      for (int r0 = 0; r0 < RPW; r0 += G) {
+        f32x4 v[G];
 #pragma unroll
-      for (int i = 0; i < G; ++i) v[i] = ld4(A + (size_t)min(m0 + wave + (r0 + i) * NW, M - 1) * lda + lane * 4);
+        for (int i = 0; i < G; ++i) v[i] = ld4(A + (size_t)min(m0 + wave + (r0 + i) * NW, M - 1) * g.lda + lane * 4);
 #pragma unroll
-      for (int i = 0; i < G; ++i) {
-        const int r = wave + (r0 + i) * NW;
-        const float mu = wave_sum(v[i].x + v[i].y + v[i].z + v[i].w) * (1.0f / 256.0f);
-        const f32x4 d = v[i] - mu;
-        const float var = wave_sum(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w) * (1.0f / 256.0f);
-        if (lane == 0) {
-          s_mu[r] = mu;
-          s_rs[r] = 1.0f / sqrtf(var + ND_LN_EPS);
+        for (int i = 0; i < G; ++i) {
+          const int r = wave + (r0 + i) * NW;
+          const float mu = wave_sum(v[i].x + v[i].y + v[i].z + v[i].w) * (1.0f / 256.0f);
+          const f32x4 d = v[i] - mu;
+          const float var = wave_sum(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w) * (1.0f / 256.0f);
+          if (lane == 0) {
+            s_mu[r] = mu;
+            s_rs[r] = 1.0f / sqrtf(var + ND_LN_EPS);
+          }
         }
       }
     }
@@ -73,30 +107,27 @@ gemm_f32_kernel(const float* __restrict__ A, int lda, const float* __restrict__ 
       const int gr = m0 + row;
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
       if (gr < M) {
-        v = ld4(A + (size_t)gr * lda + k0 + c);
-        if constexpr (LN) {
-          const f32x4 g = ld4(ln_g + k0 + c), b = ld4(ln_b + k0 + c);
-          v = (v - s_mu[row]) * s_rs[row] * g + b;
-        }
+        v = ld4(A + (size_t)gr * g.lda + k0 + c);
+        if constexpr (LN) v = (v - s_mu[row]) * s_rs[row] * ld4(g.ln_g + k0 + c) + ld4(g.ln_b + k0 + c);
       }
       ra[i] = v;
     }
 #pragma unroll
     for (int i = 0; i < W4; ++i) {
       const int f = tid + i * NT, row = f >> 3, c = (f & 7) * 4;
-      rw[i] = ld4(W + (size_t)(n0 + row) * ldw + k0 + c);
+      rw[i] = ld4(g.W + (size_t)(n0 + row) * g.ldw + k0 + c);
     }
   };
   auto store_tile = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < A4; ++i) {
       const int f = tid + i * NT, row = f >> 3, c = (f & 7) * 4;
-      st4(&As[buf][row * LDK + c], ra[i]);
+      st4(&As[buf * BM * LDK + row * LDK + c], ra[i]);
     }
 #pragma unroll
     for (int i = 0; i < W4; ++i) {
       const int f = tid + i * NT, row = f >> 3, c = (f & 7) * 4;
-      st4(&Ws[buf][row * LDK + c], rw[i]);
+      st4(&Ws[buf * BN * LDK + row * LDK + c], rw[i]);
     }
   };
 
@@ -122,9 +153,11 @@ gemm_f32_kernel(const float* __restrict__ A, int lda, const float* __restrict__ 
     for (int kb = 0; kb < BK / 8; ++kb) {
       f32x4 af[FM], bf[FN];
 #pragma unroll
-      for (int a = 0; a < FM; ++a) af[a] = ld4(&As[buf][(wm * FM * 32 + a * 32 + lr) * LDK + kb * 8 + lh * 4]);
+      for (int a = 0; a < FM; ++a)
+        af[a] = ld4(&As[buf * BM * LDK + (wm * FM * 32 + a * 32 + lr) * LDK + kb * 8 + lh * 4]);
 #pragma unroll
-      for (int b = 0; b < FN; ++b) bf[b] = ld4(&Ws[buf][(wn * FN * 32 + b * 32 + lr) * LDK + kb * 8 + lh * 4]);
+      for (int b = 0; b < FN; ++b)
+        bf[b] = ld4(&Ws[buf * BN * LDK + (wn * FN * 32 + b * 32 + lr) * LDK + kb * 8 + lh * 4]);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -136,33 +169,57 @@ gemm_f32_kernel(const float* __restrict__ A, int lda, const float* __restrict__ 
     __syncthreads();
   }
 
+  // epilogue 1: bias (+relu) into the LDS C tile
 #pragma unroll
   for (int a = 0; a < FM; ++a)
 #pragma unroll
     for (int b = 0; b < FN; ++b) {
-      const int col = n0 + wn * FN * 32 + b * 32 + lr;
-      const float bv = bias ? bias[col] : 0.f;
+      const int cl = wn * FN * 32 + b * 32 + lr;
+      const float bv = g.bias ? g.bias[n0 + cl] : 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm * FM * 32 + a * 32 + mfma32_row(r, lane);
-        if (row < M) {
-          float v = acc[a][b][r] + bv;
-          if constexpr (RELU) v = fmaxf(v, 0.f);
-          if constexpr (RESID) v += R[(size_t)row * ldr + col];
-          C[(size_t)row * ldc + col] = v;
-        }
+        float v = acc[a][b][r] + bv;
+        if constexpr (RELU) v = fmaxf(v, 0.f);
+        Cs[(wm * FM * 32 + a * 32 + mfma32_row(r, lane)) * LDC + cl] = v;
       }
     }
+  __syncthreads();
+  // epilogue 2: coalesced float4 rows (+ residual), row statistics
+  constexpr int TPR = BN / 4, RPP = NT / TPR;
+  static_assert(TPR <= 64 && (TPR & (TPR - 1)) == 0, "threads per row must be a power of two <= 64");
+  const int c4 = (tid % TPR) * 4;
+  for (int r0 = 0; r0 < BM; r0 += RPP) {
+    const int rl = r0 + tid / TPR, row = m0 + rl;
+    f32x4 v = ld4(&Cs[rl * LDC + c4]);
+    if (row < M) {
+      if constexpr (RESID) v += ld4(g.R + (size_t)row * g.ldr + n0 + c4);
+      st4(g.C + (size_t)row * g.ldc + n0 + c4, v);
+    }
+    if (g.part_out) {
+      float s = v.x + v.y + v.z + v.w;
+#pragma unroll
+      for (int o = 1; o < TPR; o <<= 1) s += __shfl_xor(s, o, 64);
+      const float mu = s * (1.0f / BN);
+      const f32x4 d = v - mu;
+      float q = d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w;
+#pragma unroll
+      for (int o = 1; o < TPR; o <<= 1) q += __shfl_xor(q, o, 64);
+      if ((tid % TPR) == 0 && row < M) {
+        float* p = g.part_out + ((size_t)row * ND_PART_LD + blockIdx.x) * 2;
+        p[0] = mu;
+        p[1] = q;
+      }
+    }
+  }
 }
 
-// Small-M variant (decoder steps: M = rows of the batch, 256 for greedy).
-// One workgroup = one 16x16 output tile on v_mfma_f32_16x16x4_f32; its WAVES
-// waves split K.  Each wave issues ALL of its A/W fragment loads up front
-// (straight from L2 into registers: every fragment is used by exactly one
-// wave, so LDS staging would only add latency), runs two interleaved
-// accumulator chains (40-cycle dependent latency vs 32-cycle issue), and the
-// partial tiles are summed through LDS before the epilogue.  A 256-row
-// decoder GEMM becomes (M/16)*(N/16) >= 256 workgroups, filling every CU.
+// ---------------------------------------------------------------------------
+// Small-M kernel (decoder steps: M = rows of the batch, 256 for greedy).
+// Workgroup = 16 rows x (NT*16) columns on v_mfma_f32_16x16x4_f32; wave (t, s)
+// owns column tile t and K slice s (K = KS*KW).  Each wave issues ALL of its
+// A/W fragment loads up front (L2 -> registers; every fragment is used by one
+// wave), runs two interleaved accumulator chains (40-cycle dependent latency
+// vs 32-cycle issue); K slices are summed through LDS.
 //
 // 16x16x4 fragments: lane l supplies A[l&15][k = l>>4] and B[k = l>>4][l&15];
 // lane l holds D[(l>>4)*4 + r][l&15].  With one float4 per lane covering
@@ -171,53 +228,62 @@ __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-template <int WAVES, int KW, bool LN, bool RELU, bool RESID>
-__global__ void __launch_bounds__(WAVES * 64)
-gemm_f32_small_kernel(const float* __restrict__ A, int lda, const float* __restrict__ W, int ldw,
-                      const float* __restrict__ bias, const float* __restrict__ R, int ldr, float* __restrict__ C,
-                      int ldc, const float* __restrict__ ln_g, const float* __restrict__ ln_b, int M, int N) {
-  // KW = K per wave (K = WAVES * KW); KW % 16 == 0
+template <int NT, int KS, int KW, bool LN, bool RELU, bool RESID>
+__global__ void __launch_bounds__(NT* KS * 64) gemm_f32_small_kernel(const GemmArgs g) {
+  constexpr int WAVES = NT * KS;
   constexpr int NF = KW / 16;  // float4 fragments per lane per operand
-  __shared__ float red[WAVES][256];
+  __shared__ float red[KS > 1 ? WAVES : 1][256];
   __shared__ float s_mu[16], s_rs[16];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int n0 = blockIdx.x * 16, m0 = blockIdx.y * 16;
+  const int wt = wave % NT, ws = wave / NT;
+  const int n0 = blockIdx.x * (NT * 16) + wt * 16, m0 = blockIdx.y * 16;
   const int li = lane & 15, lq = lane >> 4;
+  const int M = g.M;
   const int row = m0 + li;
   const bool row_ok = row < M;
-  const int kb = wave * KW + 4 * lq;
-  const float* arow = A + (size_t)(row_ok ? row : 0) * lda + kb;
-  const float* wrow = W + (size_t)(n0 + li) * ldw + kb;
+  const int kb = ws * KW + 4 * lq;
+  const float* arow = g.A + (size_t)(row_ok ? row : 0) * g.lda + kb;
+  const float* wrow = g.W + (size_t)(n0 + li) * g.ldw + kb;
   f32x4 a[NF], w[NF];
 #pragma unroll
   for (int f = 0; f < NF; ++f) {
     a[f] = ld4(arow + 16 * f);
     w[f] = ld4(wrow + 16 * f);
   }
+  // keep every fragment load in flight before the first MFMA waits
+  __builtin_amdgcn_sched_barrier(0);
   if constexpr (LN) {
-    // 16 rows' statistics: every wave loads its rows at once, then reduces
-    constexpr int RPW = (16 + WAVES - 1) / WAVES;
-    f32x4 v[RPW];
+    if (g.part_in) {
+      if (tid < 16) {
+        float mu, rs;
+        merge_stats(g.part_in + (size_t)min(m0 + tid, M - 1) * ND_PART_LD * 2, g.part_n_in, mu, rs);
+        s_mu[tid] = mu;
+        s_rs[tid] = rs;
+      }
+    } else {
+      constexpr int RPW = (16 + WAVES - 1) / WAVES;
+      f32x4 v[RPW];
 #pragma unroll
-    for (int i = 0; i < RPW; ++i) {
-      const int r = wave + i * WAVES;
-      v[i] = ld4(A + (size_t)min(m0 + min(r, 15), M - 1) * lda + lane * 4);
-    }
+      for (int i = 0; i < RPW; ++i) {
+        const int r = wave + i * WAVES;
+        v[i] = ld4(g.A + (size_t)min(m0 + min(r, 15), M - 1) * g.lda + lane * 4);
+      }
 #pragma unroll
-    for (int i = 0; i < RPW; ++i) {
-      const int r = wave + i * WAVES;
-      const float mu = wave_sum(v[i].x + v[i].y + v[i].z + v[i].w) * (1.0f / 256.0f);
-      const f32x4 d = v[i] - mu;
-      const float var = wave_sum(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w) * (1.0f / 256.0f);
-      if (lane == 0 && r < 16) {
-        s_mu[r] = mu;
-        s_rs[r] = 1.0f / sqrtf(var + ND_LN_EPS);
+      for (int i = 0; i < RPW; ++i) {
+        const int r = wave + i * WAVES;
+        const float mu = wave_sum(v[i].x + v[i].y + v[i].z + v[i].w) * (1.0f / 256.0f);
+        const f32x4 d = v[i] - mu;
+        const float var = wave_sum(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w) * (1.0f / 256.0f);
+        if (lane == 0 && r < 16) {
+          s_mu[r] = mu;
+          s_rs[r] = 1.0f / sqrtf(var + ND_LN_EPS);
+        }
       }
     }
     __syncthreads();
     const float mu = s_mu[li], rs = s_rs[li];
 #pragma unroll
-    for (int f = 0; f < NF; ++f) a[f] = (a[f] - mu) * rs * ld4(ln_g + kb + 16 * f) + ld4(ln_b + kb + 16 * f);
+    for (int f = 0; f < NF; ++f) a[f] = (a[f] - mu) * rs * ld4(g.ln_g + kb + 16 * f) + ld4(g.ln_b + kb + 16 * f);
   }
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -227,85 +293,104 @@ gemm_f32_small_kernel(const float* __restrict__ A, int lda, const float* __restr
     acc0 = mfma16(a[f][2], w[f][2], acc0);
     acc1 = mfma16(a[f][3], w[f][3], acc1);
   }
-  const f32x4 acc = acc0 + acc1;
+  f32x4 acc = acc0 + acc1;
+  if constexpr (KS > 1) {
 #pragma unroll
-  for (int r = 0; r < 4; ++r) red[wave][r * 64 + lane] = acc[r];
-  __syncthreads();
-  if (tid < 256) {
-    float v = 0.f;
+    for (int r = 0; r < 4; ++r) red[wave][r * 64 + lane] = acc[r];
+    __syncthreads();
+    if (ws != 0) return;
 #pragma unroll
-    for (int w2 = 0; w2 < WAVES; ++w2) v += red[w2][tid];
-    const int r = tid >> 6, ln = tid & 63;
-    const int orow = m0 + (ln >> 4) * 4 + r, col = n0 + (ln & 15);
-    if (orow < M) {
-      v += bias ? bias[col] : 0.f;
-      if constexpr (RELU) v = fmaxf(v, 0.f);
-      if constexpr (RESID) v += R[(size_t)orow * ldr + col];
-      C[(size_t)orow * ldc + col] = v;
+    for (int r = 0; r < 4; ++r) {
+      float v = 0.f;
+#pragma unroll
+      for (int s2 = 0; s2 < KS; ++s2) v += red[s2 * NT + wt][r * 64 + lane];
+      acc[r] = v;
+    }
+  }
+  const int col = n0 + li;
+  const float bv = g.bias ? g.bias[col] : 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int orow = m0 + lq * 4 + r;
+    float v = acc[r] + bv;
+    if constexpr (RELU) v = fmaxf(v, 0.f);
+    if constexpr (RESID) v += orow < M ? g.R[(size_t)orow * g.ldr + col] : 0.f;
+    if (orow < M) g.C[(size_t)orow * g.ldc + col] = v;
+    if (g.part_out) {
+      // row statistics over this tile's 16 columns (lanes lq*16 .. lq*16+15)
+      float s = v;
+      s += __shfl_xor(s, 1, 64);
+      s += __shfl_xor(s, 2, 64);
+      s += __shfl_xor(s, 4, 64);
+      s += __shfl_xor(s, 8, 64);
+      const float mu = s * (1.0f / 16.0f);
+      float q = (v - mu) * (v - mu);
+      q += __shfl_xor(q, 1, 64);
+      q += __shfl_xor(q, 2, 64);
+      q += __shfl_xor(q, 4, 64);
+      q += __shfl_xor(q, 8, 64);
+      if (li == 0 && orow < M) {
+        float* p = g.part_out + ((size_t)orow * ND_PART_LD + n0 / 16) * 2;
+        p[0] = mu;
+        p[1] = q;
+      }
     }
   }
 }
 
-template <int WAVES, int KW>
-static hipError_t launch_small(const GemmArgs& g, hipStream_t s) {
-  dim3 grid(g.N / 16, (g.M + 15) / 16), block(WAVES * 64);
-  const bool ln = g.ln_g != nullptr, relu = g.relu, res = g.R != nullptr;
-#define ND_SM_CASE(L, Rl, Rs)                                                                                    \
-  if (ln == L && relu == Rl && res == Rs) {                                                                      \
-    hipLaunchKernelGGL((gemm_f32_small_kernel<WAVES, KW, L, Rl, Rs>), grid, block, 0, s, g.A, g.lda, g.W, g.ldw, \
-                       g.bias, g.R, g.ldr, g.C, g.ldc, g.ln_g, g.ln_b, g.M, g.N);                                \
-    return hipGetLastError();                                                                                    \
-  }
-  ND_SM_CASE(false, false, false)
-  ND_SM_CASE(false, false, true)
-  ND_SM_CASE(false, true, false)
-  ND_SM_CASE(false, true, true)
-  ND_SM_CASE(true, false, false)
-  ND_SM_CASE(true, false, true)
-  ND_SM_CASE(true, true, false)
-  ND_SM_CASE(true, true, true)
-#undef ND_SM_CASE
-  return hipErrorInvalidValue;
-}
+// ---------------------------------------------------------------------------
+#define ND_DISPATCH_FLAGS(KERNEL, ...)                                                          \
+  do {                                                                                          \
+    const bool ln_ = g.ln_g != nullptr, re_ = g.relu, rs_ = g.R != nullptr;                     \
+    if (!ln_ && !re_ && !rs_) hipLaunchKernelGGL((KERNEL<__VA_ARGS__, false, false, false>), grid, block, 0, s, g); \
+    if (!ln_ && !re_ && rs_) hipLaunchKernelGGL((KERNEL<__VA_ARGS__, false, false, true>), grid, block, 0, s, g);   \
+    if (!ln_ && re_ && !rs_) hipLaunchKernelGGL((KERNEL<__VA_ARGS__, false, true, false>), grid, block, 0, s, g);   \
+    if (!ln_ && re_ && rs_) hipLaunchKernelGGL((KERNEL<__VA_ARGS__, false, true, true>), grid, block, 0, s, g);     \
+    if (ln_ && !re_ && !rs_) hipLaunchKernelGGL((KERNEL<__VA_ARGS__, true, false, false>), grid, block, 0, s, g);   \
+    if (ln_ && !re_ && rs_) hipLaunchKernelGGL((KERNEL<__VA_ARGS__, true, false, true>), grid, block, 0, s, g);     \
+    if (ln_ && re_ && !rs_) hipLaunchKernelGGL((KERNEL<__VA_ARGS__, true, true, false>), grid, block, 0, s, g);     \
+    if (ln_ && re_ && rs_) hipLaunchKernelGGL((KERNEL<__VA_ARGS__, true, true, true>), grid, block, 0, s, g);       \
+  } while (0)
 
 template <int BM, int BN, int WM, int WN>
-static hipError_t launch_cfg(const GemmArgs& g, hipStream_t s) {
+static hipError_t launch_cfg(GemmArgs& g, hipStream_t s) {
   dim3 grid(g.N / BN, (g.M + BM - 1) / BM), block(WM * WN * 64);
-  const bool ln = g.ln_g != nullptr, relu = g.relu, res = g.R != nullptr;
-#define ND_GEMM_CASE(L, Rl, Rs)                                                                              \
-  if (ln == L && relu == Rl && res == Rs) {                                                                  \
-    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, L, Rl, Rs>), grid, block, 0, s, g.A, g.lda, g.W, g.ldw, \
-                       g.bias, g.R, g.ldr, g.C, g.ldc, g.ln_g, g.ln_b, g.M, g.N, g.K);                       \
-    return hipGetLastError();                                                                                \
-  }
-  ND_GEMM_CASE(false, false, false)
-  ND_GEMM_CASE(false, false, true)
-  ND_GEMM_CASE(false, true, false)
-  ND_GEMM_CASE(false, true, true)
-  ND_GEMM_CASE(true, false, false)
-  ND_GEMM_CASE(true, false, true)
-  ND_GEMM_CASE(true, true, false)
-  ND_GEMM_CASE(true, true, true)
-#undef ND_GEMM_CASE
-  return hipErrorInvalidValue;
+  g.part_n_out = g.N / BN;
+  ND_DISPATCH_FLAGS(gemm_f32_kernel, BM, BN, WM, WN);
+  return hipGetLastError();
 }
 
-hipError_t launch_gemm(const GemmArgs& g, hipStream_t s) {
+template <int NT, int KS, int KW>
+static hipError_t launch_small(GemmArgs& g, hipStream_t s) {
+  if (g.N % (NT * 16) != 0 || g.K != KS * KW) return hipErrorInvalidValue;
+  dim3 grid(g.N / (NT * 16), (g.M + 15) / 16), block(NT * KS * 64);
+  g.part_n_out = g.N / 16;
+  ND_DISPATCH_FLAGS(gemm_f32_small_kernel, NT, KS, KW);
+  return hipGetLastError();
+}
+
+hipError_t launch_gemm(GemmArgs& g, hipStream_t s) {
   if (g.M <= 0) return hipSuccess;
   if (g.K % 32 != 0 || (g.ln_g && g.K != ND_D)) return hipErrorInvalidValue;
+  if (g.part_in && (g.part_n_in < 1 || g.part_n_in > ND_PART_LD || (ND_D % g.part_n_in) != 0))
+    return hipErrorInvalidValue;
+  if (g.part_out && g.N != ND_D) return hipErrorInvalidValue;  // statistics of whole 256-wide rows
   const long t128 = (long)((g.M + 127) / 128) * (g.N / 128);
   const long t64 = (long)((g.M + 63) / 64) * (g.N / 64);
   if (g.N % 128 == 0 && t128 >= 512) return launch_cfg<128, 128, 2, 2>(g, s);
   if (g.N % 64 == 0 && t64 >= 256) return launch_cfg<64, 64, 2, 2>(g, s);
   if (g.N % 16 != 0) return hipErrorInvalidValue;
-  if (g.K == 256) return launch_small<4, 64>(g, s);
-  if (g.K == 2048) return launch_small<8, 256>(g, s);
-  if (g.K % 64 == 0 && g.K <= 1024) {
-    if (g.K == 64) return launch_small<1, 64>(g, s);
-    if (g.K == 128) return launch_small<2, 64>(g, s);
-    if (g.K == 512) return launch_small<8, 64>(g, s);
-    if (g.K == 1024) return launch_small<8, 128>(g, s);
+  if (g.K == 256) {
+    // LN consumers: share the row statistics across many column tiles
+    if (g.ln_g && g.N % 128 == 0 && (long)(g.N / 128) * ((g.M + 15) / 16) >= 128) return launch_small<8, 1, 256>(g, s);
+    if (g.ln_g && g.N % 64 == 0) return launch_small<4, 2, 128>(g, s);
+    return launch_small<1, 4, 64>(g, s);
   }
+  if (g.K == 2048) return launch_small<1, 8, 256>(g, s);
+  if (g.K == 64) return launch_small<1, 1, 64>(g, s);
+  if (g.K == 128) return launch_small<1, 2, 64>(g, s);
+  if (g.K == 512) return launch_small<1, 8, 64>(g, s);
+  if (g.K == 1024) return launch_small<1, 8, 128>(g, s);
   return launch_cfg<64, 64, 2, 2>(g, s);
 }
 

@@ -19,13 +19,24 @@ struct GemmArgs {
   const float* ln_b = nullptr;
   int M = 0, N = 0, K = 0;
   bool relu = false;
+  // Row statistics hand-off (LayerNorm fusion across kernels):
+  //  part_out: the producer writes, per output row and per column tile j of
+  //            width N/part_n, {mean_j, M2_j} (M2 = sum of squared deviations)
+  //            at part_out[(row*16 + j)*2]; launch_gemm reports part_n.
+  //  part_in:  the LN consumer merges part_n_in such partials per row (Chan's
+  //            formula) instead of re-reading and reducing the row.
+  float* part_out = nullptr;
+  const float* part_in = nullptr;
+  int part_n_in = 0;
+  int part_n_out = 0;  // set by launch_gemm
 };
-hipError_t launch_gemm(const GemmArgs& g, hipStream_t s);
+#define ND_PART_LD 16  // partial-stat slots per row (max column tiles of a 256-wide row)
+hipError_t launch_gemm(GemmArgs& g, hipStream_t s);
 
 // ---- encoder -------------------------------------------------------------
-// x[b*T+t][:] = signal[b][t] * w_in + b_in                (Linear(1, d))
-hipError_t launch_enc_embed(const float* signal, const float* w_in, const float* b_in, float* x, int B, int T,
-                            hipStream_t s);
+// x[b*T+t][:] = signal[b][t] * w_in + b_in (Linear(1, d)); part: full-row stats
+hipError_t launch_enc_embed(const float* signal, const float* w_in, const float* b_in, float* x, float* part, int B,
+                            int T, hipStream_t s);
 // flash attention over qkv [B*T, 768]; mask signal==0; keys >= span excluded
 hipError_t launch_enc_attention(const float* qkv, const float* signal, const int* span, float* out, int B, int T,
                                 hipStream_t s);
@@ -40,8 +51,8 @@ hipError_t launch_layernorm(const float* x, const float* g, const float* b, floa
 
 // ---- decoder -------------------------------------------------------------
 struct DecStepArgs;
-hipError_t launch_dec_embed(const int* tok, const float* emb, const float* pe, int step, float* x, int R,
-                            hipStream_t s);
+hipError_t launch_dec_embed(const int* tok, const float* emb, const float* pe, int step, float* x, float* part,
+                            int R, hipStream_t s);
 // self attention: writes k,v of this step into cache[slot=r][step], attends
 // over the row's history cache[anc[r][t]][t] (anc == nullptr: identity).
 hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* anc, int anc_ld, int step,

@@ -1,0 +1,4 @@
+set -u
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 120 rocprofv3 -L > $GRAFT_REPO_ROOT/gpurun_out/counters.txt 2>&1; echo "rc=$?"

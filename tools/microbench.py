@@ -9,18 +9,31 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from nanodecoder_amd import engine as E  # noqa: E402
 
 dev = torch.device("cuda", 0)
+ONLY = sys.argv[1] if len(sys.argv) > 1 else ""
 
 
 def timeit(fn, n=50):
-    for _ in range(5):
+    """Per-launch time inside a captured graph of n back-to-back launches
+    (the way the engine runs them), in microseconds."""
+    for _ in range(3):
         fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(n):
+                fn()
+    torch.cuda.synchronize()
+    g.replay()
+    torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    for _ in range(n):
-        fn()
+    for _ in range(5):
+        g.replay()
     e1.record()
     e1.synchronize()
-    return e0.elapsed_time(e1) / n * 1e3  # us
+    return e0.elapsed_time(e1) / (5 * n) * 1e3  # us
 
 
 def gemm_case(M, N, K, ln, relu, res):
@@ -35,6 +48,15 @@ def gemm_case(M, N, K, ln, relu, res):
     print(f"gemm M={M:6d} N={N:5d} K={K:5d} ln={int(ln)} relu={int(relu)} res={int(res)}: {us:9.2f} us  {tf:6.1f} TF/s")
 
 
+if ONLY == "dec256":
+    for args in ((256, 768, 256, True, False, False), (256, 256, 256, False, False, True),
+                 (256, 2048, 256, True, True, False), (256, 256, 2048, False, False, True)):
+        gemm_case(*args)
+    qkv = torch.randn(256, 768, device=dev)
+    cache = torch.randn(256, 100, 512, device=dev)
+    us = timeit(lambda: E.op_dec_self_attention(qkv, cache, 60))
+    print(f"self-attn R=256 step=60: {us:8.2f} us")
+    sys.exit(0)
 for M in (256, 1280, 5120):
     gemm_case(M, 768, 256, True, False, False)
     gemm_case(M, 256, 256, False, False, True)
