@@ -122,10 +122,20 @@ const char* nd_version(void);
 /* ---- op-level entry points (unit tests of individual kernels) ---------- */
 
 /* C[M,N] = epilogue(prologue(A)[M,K] . W[N,K]^T + bias):
- * prologue LayerNorm(eps 1e-6, over K) when ln_g != NULL; relu when relu != 0;
- * + R[M,N] when R != NULL.  All fp32, row-major, dense. */
+ * prologue row normalisation (A - mean) / sqrt(var + 1e-6) over K when
+ * norm != 0 (a LayerNorm whose affine was folded into W / bias by
+ * nd_op_fold_layernorm); relu when relu != 0; + R[M,N] when R != NULL.
+ * All fp32, row-major, dense.  Replaces nn.Linear (+ the LayerNorm before it):
+ * onmt/modules/multi_headed_attn.py:155-157, onmt/modules/position_ffn.py:38-40,
+ * decoder/transformer.py:75,88, encoder/transformer.py:50. */
 int nd_op_gemm(const float* A, const float* W, const float* bias, const float* R, float* C, int32_t M,
-               int32_t N, int32_t K, const float* ln_g, const float* ln_b, int32_t relu, void* stream);
+               int32_t N, int32_t K, int32_t norm, int32_t relu, void* stream);
+
+/* Fold a LayerNorm's affine into the Linear that consumes it:
+ * W_out = W diag(ln_g), b_out = bias + W ln_b (bias may be NULL), so that
+ * Linear(LayerNorm(x)) == nd_op_gemm(x, W_out, b_out, norm = 1).  W [N,K]. */
+int nd_op_fold_layernorm(const float* W, const float* bias, const float* ln_g, const float* ln_b, float* W_out,
+                         float* b_out, int32_t N, int32_t K, void* stream);
 
 /* Encoder self-attention over qkv [B*T, 3*d] (q | k | v) with the key mask
  * signal == 0.0 and keys >= span excluded; out [B*T, d]. */

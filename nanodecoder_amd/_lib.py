@@ -44,7 +44,8 @@ SIGNATURES = {
     "nd_destroy": (None, [_P]),
     "nd_last_error": (ctypes.c_char_p, []),
     "nd_version": (ctypes.c_char_p, []),
-    "nd_op_gemm": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _I, _P]),
+    "nd_op_gemm": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
+    "nd_op_fold_layernorm": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _P]),
     "nd_op_enc_attention": (_I, [_P, _P, _P, _P, _I, _I, _P]),
     "nd_op_dec_self_attention": (_I, [_P, _P, _P, _I, _I, _I, _P, _I, _P]),
     "nd_op_dec_ctx_attention": (_I, [_P, _P, _I, _I, _P, _P, _F, _P, _I, _I, _I, _P]),

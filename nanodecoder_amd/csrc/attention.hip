@@ -205,203 +205,228 @@ hipError_t launch_dec_embed(const int* tok, const float* emb, const float* pe, i
   return hipGetLastError();
 }
 
-// Decoder self-attention, one workgroup (256 threads = 4 waves) per row.
-// cache layout: [slot][t][512] = k (256) | v (256).  Lane owns dims
-// 4*lane..4*lane+3 (head = lane/8); waves split the keys, 4 per iteration, so
-// every K/V row is one coalesced 1 KB wave load.
+// ---------------------------------------------------------------------------
+// Single-pass (flash-decoding) building blocks shared by the decoder's self-
+// and context attention.  Lane owns dims 4*lane..4*lane+3 of a 256-wide row
+// (head = lane / 8); a wave keeps a running (max m, sum l, acc) per
+// (row, head) over the keys it owns, and the waves' partial states merge
+// through LDS at the end.  softmax is exp(s - max) / sum as torch computes
+// it; masked keys carry the reference's finite -1e18 fill, keys that do not
+// exist carry -inf (weight 0).
+template <int RPC, int U>
+__device__ __forceinline__ void online_update(const float (&s)[RPC][U], const f32x4 (&v)[U], float (&m)[RPC],
+                                              float (&l)[RPC], f32x4 (&acc)[RPC]) {
+#pragma unroll
+  for (int j = 0; j < RPC; ++j) {
+    float mx = m[j];
+#pragma unroll
+    for (int u = 0; u < U; ++u) mx = fmaxf(mx, s[j][u]);  // finite: the block's first key exists
+    const float sc = __expf(m[j] - mx);
+    acc[j] = acc[j] * sc;
+    l[j] *= sc;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float p = __expf(s[j][u] - mx);
+      l[j] += p;
+      acc[j] += p * v[u];
+    }
+    m[j] = mx;
+  }
+}
+
+// LDS image: accs [NW][RPC][256], ms / ls [NW][RPC][8].  out rows j at out + j*256.
+template <int RPC, int NW>
+__device__ __forceinline__ void merge_waves(float* accs, float* ms, float* ls, const float (&m)[RPC],
+                                            const float (&l)[RPC], const f32x4 (&acc)[RPC], int wave, int lane,
+                                            int tid, float* __restrict__ out) {
+#pragma unroll
+  for (int j = 0; j < RPC; ++j) {
+    st4(accs + ((size_t)wave * RPC + j) * ND_D + lane * 4, acc[j]);
+    if ((lane & 7) == 0) {
+      ms[(wave * RPC + j) * ND_H + (lane >> 3)] = m[j];
+      ls[(wave * RPC + j) * ND_H + (lane >> 3)] = l[j];
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < RPC * ND_D; e += NW * 64) {
+    const int j = e / ND_D, d = e % ND_D, h = d / ND_DH;
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) M = fmaxf(M, ms[(w * RPC + j) * ND_H + h]);
+    float num = 0.f, den = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const float mw = ms[(w * RPC + j) * ND_H + h];
+      const float f = mw == -INFINITY ? 0.f : __expf(mw - M);  // waves that owned no key
+      num += f * accs[((size_t)w * RPC + j) * ND_D + d];
+      den += f * ls[(w * RPC + j) * ND_H + h];
+    }
+    out[e] = den > 0.f ? num / den : 0.f;
+  }
+}
+
+// Decoder self-attention, one workgroup (8 waves) per row, single pass.
+// cache layout: [slot][t][512] = k (256) | v (256), one slot per row; key t
+// of row r lives in slot anc[r][t] (beam ancestry; identity when anc is
+// null), so beam reordering never moves the cache.  This step's k, v come
+// from registers and are appended to the row's own slot
+// (multi_headed_attn.py:124-141).  Wave w owns key blocks w, w+8, ... of 4.
 #define SELF_MAXS 256
 #define SELF_NW 8
+#define SELF_U 4
 __global__ void __launch_bounds__(SELF_NW * 64)
 dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cache, const int* __restrict__ anc,
                           int anc_ld, int step, int S, float* __restrict__ out) {
-  __shared__ float p[ND_H][SELF_MAXS];
-  __shared__ float part[SELF_NW][ND_D];
+  __shared__ float accs[SELF_NW * ND_D];
+  __shared__ float ms[SELF_NW * ND_H], ls[SELF_NW * ND_H];
   const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const float* qrow = qkv + (size_t)r * 3 * ND_D;
-  const f32x4 q = ld4(qrow + lane * 4) / ND_SQRT_DH;
+  const f32x4 qv[1] = {ld4(qrow + lane * 4) / ND_SQRT_DH};
   const f32x4 kme = ld4(qrow + ND_D + lane * 4), vme = ld4(qrow + 2 * ND_D + lane * 4);
-  // append this step's k, v to the row's own slot (multi_headed_attn.py:124-141)
   if (wave == 0) {
     float* mine = cache + ((size_t)r * S + step) * 2 * ND_D;
     st4(mine + lane * 4, kme);
     st4(mine + ND_D + lane * 4, vme);
   }
+  // ancestry of keys < step: lane l holds the slot of key 64*i + l
+  int av[SELF_MAXS / 64];
+#pragma unroll
+  for (int i = 0; i < SELF_MAXS / 64; ++i)
+    av[i] = anc ? anc[(size_t)r * anc_ld + max(min(i * 64 + lane, step - 1), 0)] : r;
   const int n = step + 1;
-  const int hh = lane >> 3;
-  auto krow = [&](int t) -> const float* {
-    const int slot = (anc && t < step) ? anc[(size_t)r * anc_ld + t] : r;
-    return cache + ((size_t)slot * S + t) * 2 * ND_D;
-  };
-  // scores: keys t < step come from the cache, key `step` from registers
-  for (int t0 = wave; t0 < n; t0 += 4 * SELF_NW) {
-    f32x4 k[4];
+  float m[1] = {-INFINITY}, l[1] = {0.f};
+  f32x4 acc[1] = {{0.f, 0.f, 0.f, 0.f}};
+  for (int blk = wave; blk * SELF_U < n; blk += SELF_NW) {
+    f32x4 k[SELF_U], v[SELF_U];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int t = t0 + SELF_NW * u;
-      k[u] = (t < step) ? ld4(krow(t) + lane * 4) : kme;
+    for (int u = 0; u < SELF_U; ++u) {
+      const int t = min(blk * SELF_U + u, step);  // wave-uniform
+      if (t < step) {
+        const int a = t >> 6;
+        const int sv = a == 0 ? av[0] : a == 1 ? av[1] : a == 2 ? av[2] : av[3];
+        const int slot = __builtin_amdgcn_readlane(sv, t & 63);
+        const float* row = cache + ((size_t)slot * S + t) * 2 * ND_D + lane * 4;
+        k[u] = ld4(row);
+        v[u] = ld4(row + ND_D);
+      } else {
+        k[u] = kme;
+        v[u] = vme;
+      }
     }
+    float sc[1][SELF_U];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int t = t0 + SELF_NW * u;
-      float d = q.x * k[u].x + q.y * k[u].y + q.z * k[u].z + q.w * k[u].w;
-      d += __shfl_xor(d, 1, 64);
-      d += __shfl_xor(d, 2, 64);
-      d += __shfl_xor(d, 4, 64);
-      if ((lane & 7) == 0 && t < n) p[hh][t] = d;
+    for (int u = 0; u < SELF_U; ++u) {
+      const float d = sum8(qv[0].x * k[u].x + qv[0].y * k[u].y + qv[0].z * k[u].z + qv[0].w * k[u].w);
+      sc[0][u] = blk * SELF_U + u < n ? d : -INFINITY;
     }
+    online_update<1, SELF_U>(sc, v, m, l, acc);
   }
-  __syncthreads();
-  // softmax per head (no mask while stepping): wave w handles heads w, w+4
-  for (int h2 = wave; h2 < ND_H; h2 += SELF_NW) {
-    float mx = -INFINITY;
-    for (int t = lane; t < n; t += 64) mx = fmaxf(mx, p[h2][t]);
-    mx = wave_max(mx);
-    float sm = 0.f;
-    for (int t = lane; t < n; t += 64) {
-      const float e = __expf(p[h2][t] - mx);
-      p[h2][t] = e;
-      sm += e;
-    }
-    sm = wave_sum(sm);
-    const float inv = 1.0f / sm;
-    for (int t = lane; t < n; t += 64) p[h2][t] *= inv;
-  }
-  __syncthreads();
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (int t0 = wave; t0 < n; t0 += 4 * SELF_NW) {
-    f32x4 v[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int t = t0 + SELF_NW * u;
-      v[u] = (t < step) ? ld4(krow(t) + ND_D + lane * 4) : vme;
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int t = t0 + SELF_NW * u;
-      if (t < n) acc += p[hh][t] * v[u];
-    }
-  }
-  st4(&part[wave][lane * 4], acc);
-  __syncthreads();
-  if (tid < ND_D) {
-    float v = 0.f;
-#pragma unroll
-    for (int w = 0; w < SELF_NW; ++w) v += part[w][tid];
-    out[(size_t)r * ND_D + tid] = v;
-  }
+  merge_waves<1, SELF_NW>(accs, ms, ls, m, l, acc, wave, lane, tid, out + (size_t)r * ND_D);
 }
 
 hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* anc, int anc_ld, int step,
                                      int max_steps, float* out, int R, hipStream_t s) {
   if (step >= max_steps || step >= SELF_MAXS) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(dec_self_attention_kernel, dim3(R), dim3(SELF_NW * 64), 0, s, qkv, cache, anc, anc_ld, step, max_steps,
-                     out);
+  hipLaunchKernelGGL(dec_self_attention_kernel, dim3(R), dim3(SELF_NW * 64), 0, s, qkv, cache, anc, anc_ld, step,
+                     max_steps, out);
   return hipGetLastError();
 }
 
-// Context attention, one workgroup (512 threads) per chunk: the chunk's
-// context K/V stream from HBM once for all of its rows (beam rows share the
-// same memory bank, translate/translator.py:667-676 tiles it only logically).
-#define CTX_THREADS 512
+// Context attention, one workgroup (16 waves) per chunk, single pass over
+// the chunk's context K/V (flash-decoding): the chunk's K/V stream from HBM
+// exactly once for all of its rows (beam rows share the same memory bank,
+// translate/translator.py:667-676 tiles it only logically).  Each wave owns
+// blocks of U consecutive keys (K and V of a key are one contiguous 2 KB run
+// of the ctx K/V row), keeps a running (max, sum, acc) per (row, head) and
+// prefetches its next block while computing the current one, so
+// 16 waves x 2 blocks x U x 2 KB are in flight per CU.  The 16 partial states
+// merge through LDS at the end.  softmax(QK^T/sqrt(d), mask src == pad_idx
+// -> -1e18) V as decoder/transformer.py:220-221 + modules/multi_headed_attn.py.
+#define CTX_NW 16
 #define CTX_MAXR 6
 template <int RPC>
-__global__ void __launch_bounds__(CTX_THREADS)
+struct CtxTile {
+  static constexpr int U = RPC <= 2 ? 4 : 2;  // keys per block (register budget: 128 VGPRs at 16 waves/CU)
+};
+
+template <int RPC>
+__global__ void __launch_bounds__(CTX_NW * 64)
 dec_ctx_attention_kernel(const float* __restrict__ q, const float* __restrict__ kv, int ld, int koff,
                          const float* __restrict__ signal, const int* __restrict__ span, float pad_val,
                          float* __restrict__ out, int T) {
-  constexpr int rpc = RPC;
+  constexpr int U = CtxTile<RPC>::U;
   extern __shared__ float sm[];
-  float* sc = sm;                                   // [rpc][8][T]
-  float* part = sm + rpc * ND_H * T;                // [8 waves][rpc][256]
+  float* accs = sm;                              // [NW][RPC][256]
+  float* ms = sm + CTX_NW * RPC * ND_D;          // [NW][RPC][8]
+  float* ls = ms + CTX_NW * RPC * ND_H;          // [NW][RPC][8]
   const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int L = min(span[c], T);
   const size_t base = (size_t)c * T;
+  const float* kvc = kv + base * ld + koff + lane * 4;
+  const float* sgc = signal + base;
   // lane owns dims 4*lane..4*lane+3 of every row; head = lane / 8
-  f32x4 qv[RPC];
+  f32x4 qv[RPC], acc[RPC];
+  float m[RPC], l[RPC];
 #pragma unroll
-  for (int j = 0; j < RPC; ++j) qv[j] = ld4(q + ((size_t)c * rpc + j) * ND_D + lane * 4) / ND_SQRT_DH;
-  // pass 1: scores (mask src == pad_idx, decoder/transformer.py:220-221);
-  // wave w takes keys w, w+8, ... four at a time so 4 KB are in flight per wave
-  constexpr int NW = CTX_THREADS / 64;
-  for (int t0 = wave; t0 < L; t0 += 4 * NW) {
-    f32x4 k[4];
-    bool masked[4];
+  for (int j = 0; j < RPC; ++j) {
+    qv[j] = ld4(q + ((size_t)c * RPC + j) * ND_D + lane * 4) / ND_SQRT_DH;
+    acc[j] = {0.f, 0.f, 0.f, 0.f};
+    m[j] = -INFINITY;
+    l[j] = 0.f;
+  }
+  f32x4 kc[U], vc[U];
+  float sg[U];
+  auto load = [&](int blk, f32x4* kk, f32x4* vv, float* ss) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int t = min(t0 + u * NW, L - 1);
-      k[u] = ld4(kv + (base + t) * ld + koff + lane * 4);
-      masked[u] = signal[base + t] == pad_val;
+    for (int u = 0; u < U; ++u) {
+      const int t = min(blk * U + u, L - 1);
+      kk[u] = ld4(kvc + (size_t)t * ld);
+      vv[u] = ld4(kvc + (size_t)t * ld + ND_D);
+      ss[u] = sgc[t];
     }
+  };
+  int blk = wave;
+  if (blk * U < L) load(blk, kc, vc, sg);
+  for (; blk * U < L; blk += CTX_NW) {
+    f32x4 kn[U], vn[U];
+    float sn[U];
+    const bool more = (blk + CTX_NW) * U < L;
+    if (more) load(blk + CTX_NW, kn, vn, sn);
+    float sc[RPC][U];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int t = t0 + u * NW;
+    for (int u = 0; u < U; ++u) {
+      const bool valid = blk * U + u < L;
+      const bool masked = sg[u] == pad_val;
 #pragma unroll
       for (int j = 0; j < RPC; ++j) {
-        float d = qv[j].x * k[u].x + qv[j].y * k[u].y + qv[j].z * k[u].z + qv[j].w * k[u].w;
-        d += __shfl_xor(d, 1, 64);
-        d += __shfl_xor(d, 2, 64);
-        d += __shfl_xor(d, 4, 64);
-        if ((lane & 7) == 0 && t < L) sc[(j * ND_H + (lane >> 3)) * T + t] = masked[u] ? ND_MASK_FILL : d;
+        const float d = sum8(qv[j].x * kc[u].x + qv[j].y * kc[u].y + qv[j].z * kc[u].z + qv[j].w * kc[u].w);
+        sc[j][u] = valid ? (masked ? ND_MASK_FILL : d) : -INFINITY;
+      }
+    }
+    online_update<RPC, U>(sc, vc, m, l, acc);
+    if (more) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        kc[u] = kn[u];
+        vc[u] = vn[u];
+        sg[u] = sn[u];
       }
     }
   }
-  __syncthreads();
-  // softmax over keys for each (row, head)
-  for (int rh = wave; rh < rpc * ND_H; rh += CTX_THREADS / 64) {
-    float* s = sc + rh * T;
-    float mx = -INFINITY;
-    for (int t = lane; t < L; t += 64) mx = fmaxf(mx, s[t]);
-    mx = wave_max(mx);
-    float sum = 0.f;
-    for (int t = lane; t < L; t += 64) {
-      const float e = __expf(s[t] - mx);
-      s[t] = e;
-      sum += e;
-    }
-    sum = wave_sum(sum);
-    const float inv = 1.0f / sum;
-    for (int t = lane; t < L; t += 64) s[t] *= inv;
-  }
-  __syncthreads();
-  // pass 2: out[j] = sum_t p[j][head][t] * V[t]
-  f32x4 acc[RPC];
-#pragma unroll
-  for (int j = 0; j < RPC; ++j) acc[j] = {0.f, 0.f, 0.f, 0.f};
-  const int hh = lane >> 3;
-  for (int t0 = wave; t0 < L; t0 += 4 * NW) {
-    f32x4 v[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = ld4(kv + (base + min(t0 + u * NW, L - 1)) * ld + koff + ND_D + lane * 4);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int t = t0 + u * NW;
-      if (t < L) {
-#pragma unroll
-        for (int j = 0; j < RPC; ++j) acc[j] += sc[(j * ND_H + hh) * T + t] * v[u];
-      }
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < RPC; ++j) st4(part + ((size_t)wave * rpc + j) * ND_D + lane * 4, acc[j]);
-  __syncthreads();
-  for (int e = tid; e < rpc * ND_D; e += CTX_THREADS) {
-    float v = 0.f;
-#pragma unroll
-    for (int w = 0; w < CTX_THREADS / 64; ++w) v += part[(size_t)w * rpc * ND_D + e];
-    out[(size_t)c * rpc * ND_D + e] = v;
-  }
+  merge_waves<RPC, CTX_NW>(accs, ms, ls, m, l, acc, wave, lane, tid, out + (size_t)c * RPC * ND_D);
 }
+
+static size_t ctx_lds_bytes(int rpc) { return (size_t)CTX_NW * rpc * (ND_D + 2 * ND_H) * sizeof(float); }
 
 hipError_t launch_dec_ctx_attention(const float* q, const float* kv, int ld, int koff, const float* signal,
                                     const int* span, float pad_val, float* out, int C, int rpc, int T,
                                     hipStream_t s) {
   if (rpc < 1 || rpc > CTX_MAXR || T > 512) return hipErrorInvalidValue;
-  const size_t lds = ((size_t)rpc * ND_H * T + (size_t)(CTX_THREADS / 64) * rpc * ND_D) * sizeof(float);
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  const size_t lds = ctx_lds_bytes(rpc);
   switch (rpc) {
 #define ND_CTX_CASE(R)                                                                                            \
   case R:                                                                                                         \
-    hipLaunchKernelGGL(dec_ctx_attention_kernel<R>, dim3(C), dim3(CTX_THREADS), lds, s, q, kv, ld, koff, signal, \
+    hipLaunchKernelGGL(dec_ctx_attention_kernel<R>, dim3(C), dim3(CTX_NW * 64), lds, s, q, kv, ld, koff, signal,  \
                        span, pad_val, out, T);                                                                    \
     break;
     ND_CTX_CASE(1)

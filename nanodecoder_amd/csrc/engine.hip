@@ -50,12 +50,16 @@ struct Slot {
   int copy_rows = -1;  // >= 0: copy only the first copy_rows rows (pe table)
 };
 
+// n* = LayerNorm-folded copies (gamma into the weight columns, beta into the
+// bias; derived at finalize): the GEMM prologue only normalises rows.
 struct EncLayer {
   float *ln_g, *ln_b, *wqkv, *bqkv, *wo, *bo, *fln_g, *fln_b, *w1, *b1, *w2, *b2;
+  float *nwqkv, *nbqkv, *nw1, *nb1;
 };
 struct DecLayer {
   float *ln1_g, *ln1_b, *wqkv, *bqkv, *wo, *bo, *ln2_g, *ln2_b, *cwq, *cbq, *cwo, *cbo, *fln_g, *fln_b, *w1, *b1,
       *w2, *b2;
+  float *nwqkv, *nbqkv, *ncwq, *ncbq, *nw1, *nb1;
 };
 struct NanoLayer {
   float *wih, *bih, *bhh, *whh, *bn_g, *bn_b, *bn_rm, *bn_rv;  // raw
@@ -88,7 +92,7 @@ struct nd_ctx {
   std::vector<NanoLayer> nano;
   float* nano_W = nullptr;
   std::vector<DecLayer> dec;
-  float *ctxkv_w = nullptr, *ctxkv_b = nullptr;
+  float *ctxkv_w = nullptr, *ctxkv_b = nullptr, *nctxkv_w = nullptr, *nctxkv_b = nullptr;
   float *emb = nullptr, *pe = nullptr, *dec_ln_g = nullptr, *dec_ln_b = nullptr, *gen_w = nullptr, *gen_b = nullptr;
 
   // workspaces
@@ -156,6 +160,7 @@ static int build_registry(nd_ctx* c) {
       EncLayer& L = c->enc[i];
       AL(L.ln_g, D); AL(L.ln_b, D); AL(L.wqkv, 3 * D * D); AL(L.bqkv, 3 * D); AL(L.wo, D * D); AL(L.bo, D);
       AL(L.fln_g, D); AL(L.fln_b, D); AL(L.w1, (size_t)F * D); AL(L.b1, F); AL(L.w2, (size_t)D * F); AL(L.b2, D);
+      AL(L.nwqkv, 3 * D * D); AL(L.nbqkv, 3 * D); AL(L.nw1, (size_t)F * D); AL(L.nb1, F);
       const std::string p = "encoder.transformer." + std::to_string(i);
       add_slot(c, p + ".layer_norm.weight", L.ln_g, {D});
       add_slot(c, p + ".layer_norm.bias", L.ln_b, {D});
@@ -202,11 +207,17 @@ static int build_registry(nd_ctx* c) {
   c->dec.resize(cfg.dec_layers);
   AL(c->ctxkv_w, (size_t)cfg.dec_layers * 2 * D * D);
   AL(c->ctxkv_b, (size_t)cfg.dec_layers * 2 * D);
+  if (cfg.encoder_type == ND_ENC_TRANSFORMER) {
+    AL(c->nctxkv_w, (size_t)cfg.dec_layers * 2 * D * D);
+    AL(c->nctxkv_b, (size_t)cfg.dec_layers * 2 * D);
+  }
   for (int i = 0; i < cfg.dec_layers; ++i) {
     DecLayer& L = c->dec[i];
     AL(L.ln1_g, D); AL(L.ln1_b, D); AL(L.wqkv, 3 * D * D); AL(L.bqkv, 3 * D); AL(L.wo, D * D); AL(L.bo, D);
     AL(L.ln2_g, D); AL(L.ln2_b, D); AL(L.cwq, D * D); AL(L.cbq, D); AL(L.cwo, D * D); AL(L.cbo, D);
     AL(L.fln_g, D); AL(L.fln_b, D); AL(L.w1, (size_t)F * D); AL(L.b1, F); AL(L.w2, (size_t)D * F); AL(L.b2, D);
+    AL(L.nwqkv, 3 * D * D); AL(L.nbqkv, 3 * D); AL(L.ncwq, D * D); AL(L.ncbq, D); AL(L.nw1, (size_t)F * D);
+    AL(L.nb1, F);
     const std::string p = "decoder.transformer_layers." + std::to_string(i);
     add_slot(c, p + ".layer_norm_1.weight", L.ln1_g, {D});
     add_slot(c, p + ".layer_norm_1.bias", L.ln1_b, {D});
@@ -323,11 +334,11 @@ static int alloc_workspaces(nd_ctx* c) {
   } while (0)
 
 static hipError_t gemm(const float* A, int lda, const float* W, int N, int K, const float* bias, float* C, int ldc,
-                       int M, hipStream_t s, const float* ln_g = nullptr, const float* ln_b = nullptr,
-                       bool relu = false, const float* R = nullptr, int ldr = 0) {
+                       int M, hipStream_t s, bool norm = false, bool relu = false, const float* R = nullptr,
+                       int ldr = 0) {
   nd::GemmArgs g;
   g.A = A; g.lda = lda; g.W = W; g.ldw = K; g.bias = bias; g.R = R; g.ldr = ldr; g.C = C; g.ldc = ldc;
-  g.ln_g = ln_g; g.ln_b = ln_b; g.M = M; g.N = N; g.K = K; g.relu = relu;
+  g.norm = norm; g.M = M; g.N = N; g.K = K; g.relu = relu;
   return nd::launch_gemm(g, s);
 }
 
@@ -337,8 +348,9 @@ struct G {
   G(const float* A, int lda, const float* W, int N, int K, const float* bias, float* C, int ldc, int M) {
     a.A = A; a.lda = lda; a.W = W; a.ldw = K; a.bias = bias; a.C = C; a.ldc = ldc; a.M = M; a.N = N; a.K = K;
   }
-  G& ln(const float* g, const float* b, const float* part, int pn) {
-    a.ln_g = g; a.ln_b = b; a.part_in = part; a.part_n_in = pn;
+  // LayerNorm prologue (affine already folded into W / bias)
+  G& ln(const float* part, int pn) {
+    a.norm = true; a.part_in = part; a.part_n_in = pn;
     return *this;
   }
   G& relu() { a.relu = true; return *this; }
@@ -359,10 +371,10 @@ static hipError_t enqueue_encode_transformer(nd_ctx* c, int B, int T, hipStream_
   int pnx = 1, pny = 0;
   for (auto& L : c->enc) {
     // encoder/transformer.py:36-54
-    LCHK(G(c->x, D, L.wqkv, 3 * D, D, L.bqkv, c->big, 3 * D, M).ln(L.ln_g, L.ln_b, c->x_part, pnx).run(s));
+    LCHK(G(c->x, D, L.nwqkv, 3 * D, D, L.nbqkv, c->big, 3 * D, M).ln(c->x_part, pnx).run(s));
     LCHK(nd::launch_enc_attention(c->big, c->sig, c->span, c->att, B, T, s));
     LCHK(G(c->att, D, L.wo, D, D, L.bo, c->y, D, M).res(c->x, D).stats(c->y_part).run(s, &pny));
-    LCHK(G(c->y, D, L.w1, F, D, L.b1, c->big, F, M).ln(L.fln_g, L.fln_b, c->y_part, pny).relu().run(s));
+    LCHK(G(c->y, D, L.nw1, F, D, L.nb1, c->big, F, M).ln(c->y_part, pny).relu().run(s));
     LCHK(G(c->big, F, L.w2, D, F, L.b2, c->x, D, M).res(c->y, D).stats(c->x_part).run(s, &pnx));
   }
   c->x_pn = pnx;
@@ -372,33 +384,46 @@ static hipError_t enqueue_encode_transformer(nd_ctx* c, int B, int T, hipStream_
 static hipError_t enqueue_ctxkv(nd_ctx* c, int B, int T, hipStream_t s) {
   const int M = B * T, D = c->D, N = (int)c->dec.size() * 2 * D;
   if (c->cfg.encoder_type == ND_ENC_TRANSFORMER)
-    return G(c->x, D, c->ctxkv_w, N, D, c->ctxkv_b, c->ctxkv, N, M).ln(c->enc_ln_g, c->enc_ln_b, c->x_part, c->x_pn)
-        .run(s);
+    return G(c->x, D, c->nctxkv_w, N, D, c->nctxkv_b, c->ctxkv, N, M).ln(c->x_part, c->x_pn).run(s);
   return G(c->x, D, c->ctxkv_w, N, D, c->ctxkv_b, c->ctxkv, N, M).run(s);
 }
 
 static hipError_t enqueue_encode(nd_ctx* c, int B, int T, hipStream_t s);
 
-// One decoder step for R = C*rpc rows: tok -> dx (pre final LN).
+static nd::NextEmbed next_embed(nd_ctx* c) {
+  nd::NextEmbed ne;
+  ne.emb = c->emb;
+  ne.pe = c->cfg.position_encoding ? c->pe : nullptr;
+  ne.x = c->dx;
+  ne.part = c->dx_part;
+  return ne;
+}
+
+// Step-0 decoder input (later steps' inputs are written by the search
+// kernel that picks their token).
+static hipError_t enqueue_first_embed(nd_ctx* c, int R, hipStream_t s) {
+  return nd::launch_dec_embed(c->tok, c->emb, c->cfg.position_encoding ? c->pe : nullptr, 0, c->dx, c->dx_part, R, s);
+}
+
+// One decoder step for R = C*rpc rows: dx (embedded input, row stats in
+// dx_part) -> dx (pre final LN).
 static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, const int* anc, int anc_ld,
                                    hipStream_t s) {
   const int R = C * rpc, D = c->D, F = c->F, S = c->cfg.max_steps;
   const int Ld = (int)c->dec.size();
-  LCHK(nd::launch_dec_embed(c->tok, c->emb, c->cfg.position_encoding ? c->pe : nullptr, step, c->dx, c->dx_part, R,
-                            s));
   int pnx = 1, pnq = 0, pnm = 0;
   for (int i = 0; i < Ld; ++i) {
     DecLayer& L = c->dec[i];
     float* cache = c->cache + (size_t)i * R * S * 2 * D;
     // decoder/transformer.py:53-95
-    LCHK(G(c->dx, D, L.wqkv, 3 * D, D, L.bqkv, c->dqkv, 3 * D, R).ln(L.ln1_g, L.ln1_b, c->dx_part, pnx).run(s));
+    LCHK(G(c->dx, D, L.nwqkv, 3 * D, D, L.nbqkv, c->dqkv, 3 * D, R).ln(c->dx_part, pnx).run(s));
     LCHK(nd::launch_dec_self_attention(c->dqkv, cache, anc, anc_ld, step, S, c->datt, R, s));
     LCHK(G(c->datt, D, L.wo, D, D, L.bo, c->dq1, D, R).res(c->dx, D).stats(c->dq1_part).run(s, &pnq));
-    LCHK(G(c->dq1, D, L.cwq, D, D, L.cbq, c->dcq, D, R).ln(L.ln2_g, L.ln2_b, c->dq1_part, pnq).run(s));
+    LCHK(G(c->dq1, D, L.ncwq, D, D, L.ncbq, c->dcq, D, R).ln(c->dq1_part, pnq).run(s));
     LCHK(nd::launch_dec_ctx_attention(c->dcq, c->ctxkv, Ld * 2 * D, i * 2 * D, c->sig, c->span,
                                       (float)c->cfg.pad_idx, c->datt, C, rpc, T, s));
     LCHK(G(c->datt, D, L.cwo, D, D, L.cbo, c->dmid, D, R).res(c->dq1, D).stats(c->dmid_part).run(s, &pnm));
-    LCHK(G(c->dmid, D, L.w1, F, D, L.b1, c->dhid, F, R).ln(L.fln_g, L.fln_b, c->dmid_part, pnm).relu().run(s));
+    LCHK(G(c->dmid, D, L.nw1, F, D, L.nb1, c->dhid, F, R).ln(c->dmid_part, pnm).relu().run(s));
     LCHK(G(c->dhid, F, L.w2, D, F, L.b2, c->dx, D, R).res(c->dmid, D).stats(c->dx_part).run(s, &pnx));
   }
   return hipSuccess;
@@ -408,10 +433,13 @@ static hipError_t enqueue_greedy(nd_ctx* c, int B, int T, int S, int min_len, bo
   LCHK(enqueue_encode(c, B, T, s));
   LCHK(enqueue_ctxkv(c, B, T, s));
   LCHK(nd::launch_fill_i32(c->tok, c->cfg.bos_idx, B, s));
+  LCHK(enqueue_first_embed(c, B, s));
+  const nd::NextEmbed ne = next_embed(c);
   for (int step = 0; step < S; ++step) {
     LCHK(enqueue_dec_step(c, B, 1, T, step, nullptr, 0, s));
     LCHK(nd::launch_dec_greedy_head(c->dx, c->dec_ln_g, c->dec_ln_b, c->gen_w, c->gen_b, c->V, step, S, min_len,
-                                    c->cfg.eos_idx, c->tok, c->gtok, c->gscore, logp ? c->glogp : nullptr, B, s));
+                                    c->cfg.eos_idx, c->tok, c->gtok, c->gscore, logp ? c->glogp : nullptr, ne, B,
+                                    s));
   }
   return hipSuccess;
 }
@@ -422,7 +450,7 @@ static hipError_t enqueue_beam_steps(nd_ctx* c, int B, int T, int beam, int n_be
     const int cur = step & 1;
     LCHK(enqueue_dec_step(c, B, beam, T, step, c->bs.anc[cur], S, s));
     const float lenpen = (float)std::pow((5.0 + (step + 1)) / 6.0, (double)alpha);
-    LCHK(nd::launch_beam_step(c->dx, c->dec_ln_g, c->dec_ln_b, c->gen_w, c->gen_b, c->V, c->bs, B, beam, n_best,
+    LCHK(nd::launch_beam_step(next_embed(c), c->dx, c->dec_ln_g, c->dec_ln_b, c->gen_w, c->gen_b, c->V, c->bs, B, beam, n_best,
                               step, S, min_len, c->cfg.eos_idx, lenpen, s));
   }
   return hipSuccess;
@@ -565,6 +593,25 @@ int nd_finalize(nd_ctx* c) {
       HIPCHK(hipMemcpy(L.bn_shift, sh.data(), sh.size() * 4, hipMemcpyHostToDevice));
     }
   }
+  // LayerNorm affines folded into the Linear that consumes them
+  {
+    const int D = c->D, F = c->F;
+    auto fold = [&](const float* W, const float* b, const float* g, const float* be, float* Wo, float* bo, int N,
+                    int K) { return nd::launch_fold_layernorm(W, b, g, be, Wo, bo, N, K, c->es); };
+    for (auto& L : c->enc) {
+      HIPCHK(fold(L.wqkv, L.bqkv, L.ln_g, L.ln_b, L.nwqkv, L.nbqkv, 3 * D, D));
+      HIPCHK(fold(L.w1, L.b1, L.fln_g, L.fln_b, L.nw1, L.nb1, F, D));
+    }
+    if (c->nctxkv_w)
+      HIPCHK(fold(c->ctxkv_w, c->ctxkv_b, c->enc_ln_g, c->enc_ln_b, c->nctxkv_w, c->nctxkv_b,
+                  (int)c->dec.size() * 2 * D, D));
+    for (auto& L : c->dec) {
+      HIPCHK(fold(L.wqkv, L.bqkv, L.ln1_g, L.ln1_b, L.nwqkv, L.nbqkv, 3 * D, D));
+      HIPCHK(fold(L.cwq, L.cbq, L.ln2_g, L.ln2_b, L.ncwq, L.ncbq, D, D));
+      HIPCHK(fold(L.w1, L.b1, L.fln_g, L.fln_b, L.nw1, L.nb1, F, D));
+    }
+    HIPCHK(hipStreamSynchronize(c->es));
+  }
   for (auto& kv : c->graphs) (void)hipGraphExecDestroy(kv.second);
   c->graphs.clear();
   c->finalized = true;
@@ -643,6 +690,7 @@ int nd_translate_beam(nd_ctx* c, const float* d_signal, const int32_t* d_len, co
     LCHK(enqueue_encode(c, B, T, s));
     LCHK(enqueue_ctxkv(c, B, T, s));
     LCHK(nd::launch_beam_init(c->bs, B, beam, n_best, max_len, c->cfg.bos_idx, s));
+    LCHK(enqueue_first_embed(c, B * beam, s));
     LCHK(nd::launch_fill_i32(c->steps_done, max_len, 1, s));
     return hipSuccess;
   });
@@ -722,9 +770,16 @@ void nd_destroy(nd_ctx* c) {
 }
 
 int nd_op_gemm(const float* A, const float* W, const float* bias, const float* R, float* C, int32_t M, int32_t N,
-               int32_t K, const float* ln_g, const float* ln_b, int32_t relu, void* stream) {
-  hipError_t e = gemm(A, K, W, N, K, bias, C, N, M, (hipStream_t)stream, ln_g, ln_b, relu != 0, R, N);
+               int32_t K, int32_t norm, int32_t relu, void* stream) {
+  hipError_t e = gemm(A, K, W, N, K, bias, C, N, M, (hipStream_t)stream, norm != 0, relu != 0, R, N);
   if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("gemm: ") + hipGetErrorString(e));
+  return ND_OK;
+}
+
+int nd_op_fold_layernorm(const float* W, const float* bias, const float* ln_g, const float* ln_b, float* W_out,
+                         float* b_out, int32_t N, int32_t K, void* stream) {
+  hipError_t e = nd::launch_fold_layernorm(W, bias, ln_g, ln_b, W_out, b_out, N, K, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("fold_layernorm: ") + hipGetErrorString(e));
   return ND_OK;
 }
 

@@ -9,7 +9,9 @@
 // v_mfma_f32_16x16x4_f32 (exact fp32 FMA chains at the fp32 peak).
 //
 //   C[M,N] = epi( pro(A)[M,K] . W[N,K]^T + bias[N] )
-//   pro(A) = LN(A) = (A - mean) * rstd * g + b over K          (LN)
+//   pro(A) = (A - mean) * rstd over K                            (LN)
+//   (the LayerNorm's gamma/beta are folded into W and bias at load time,
+//    fold_layernorm_kernel below)
 //   epi(v) = relu(v) (RELU); v + R[M,N] (RESID)
 //
 // LayerNorm fusion across kernels: every producer of a LayerNorm input (the
@@ -22,19 +24,39 @@
 
 namespace nd {
 
-// Merge P equal-width partials {mean_j, M2_j} of a 256-wide row.
+// Merge P equal-width partials {mean_j, M2_j} of a 256-wide row.  All
+// ND_PART_LD slots are loaded unconditionally (the buffer always holds them)
+// so the loads issue together; slots j >= P are discarded by selects.
 __device__ __forceinline__ void merge_stats(const float* __restrict__ p, int P, float& mu, float& rs) {
+  f32x4 v[ND_PART_LD / 2];  // {mean_2i, M2_2i, mean_2i+1, M2_2i+1}
+#pragma unroll
+  for (int i = 0; i < ND_PART_LD / 2; ++i) v[i] = ld4(p + 4 * i);
   const float w = 256.0f / (float)P;
   float m = 0.f;
-  for (int j = 0; j < P; ++j) m += p[2 * j];
+#pragma unroll
+  for (int i = 0; i < ND_PART_LD / 2; ++i) {
+    m += 2 * i < P ? v[i].x : 0.f;
+    m += 2 * i + 1 < P ? v[i].z : 0.f;
+  }
   m /= (float)P;
   float m2 = 0.f;
-  for (int j = 0; j < P; ++j) {
-    const float d = p[2 * j] - m;
-    m2 += p[2 * j + 1] + w * d * d;
+#pragma unroll
+  for (int i = 0; i < ND_PART_LD / 2; ++i) {
+    const float d0 = v[i].x - m, d1 = v[i].z - m;
+    m2 += 2 * i < P ? v[i].y + w * d0 * d0 : 0.f;
+    m2 += 2 * i + 1 < P ? v[i].w + w * d1 * d1 : 0.f;
   }
   mu = m;
   rs = 1.0f / sqrtf(m2 * (1.0f / 256.0f) + ND_LN_EPS);
+}
+
+// Sum over aligned groups of TPR lanes (16 or 32).
+template <int TPR>
+__device__ __forceinline__ float group_sum(float v) {
+  static_assert(TPR == 16 || TPR == 32, "group of 16 or 32 lanes");
+  v = sum16(v);
+  if constexpr (TPR == 32) v += __shfl_xor(v, 16, 64);
+  return v;
 }
 
 // ---------------------------------------------------------------------------
@@ -108,7 +130,7 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
       if (gr < M) {
         v = ld4(A + (size_t)gr * g.lda + k0 + c);
-        if constexpr (LN) v = (v - s_mu[row]) * s_rs[row] * ld4(g.ln_g + k0 + c) + ld4(g.ln_b + k0 + c);
+        if constexpr (LN) v = (v - s_mu[row]) * s_rs[row];
       }
       ra[i] = v;
     }
@@ -186,7 +208,6 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
   __syncthreads();
   // epilogue 2: coalesced float4 rows (+ residual), row statistics
   constexpr int TPR = BN / 4, RPP = NT / TPR;
-  static_assert(TPR <= 64 && (TPR & (TPR - 1)) == 0, "threads per row must be a power of two <= 64");
   const int c4 = (tid % TPR) * 4;
   for (int r0 = 0; r0 < BM; r0 += RPP) {
     const int rl = r0 + tid / TPR, row = m0 + rl;
@@ -196,14 +217,9 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
       st4(g.C + (size_t)row * g.ldc + n0 + c4, v);
     }
     if (g.part_out) {
-      float s = v.x + v.y + v.z + v.w;
-#pragma unroll
-      for (int o = 1; o < TPR; o <<= 1) s += __shfl_xor(s, o, 64);
-      const float mu = s * (1.0f / BN);
+      const float mu = group_sum<TPR>(v.x + v.y + v.z + v.w) * (1.0f / BN);
       const f32x4 d = v - mu;
-      float q = d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w;
-#pragma unroll
-      for (int o = 1; o < TPR; o <<= 1) q += __shfl_xor(q, o, 64);
+      const float q = group_sum<TPR>(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w);
       if ((tid % TPR) == 0 && row < M) {
         float* p = g.part_out + ((size_t)row * ND_PART_LD + blockIdx.x) * 2;
         p[0] = mu;
@@ -250,17 +266,24 @@ __global__ void __launch_bounds__(NT* KS * 64) gemm_f32_small_kernel(const GemmA
     a[f] = ld4(arow + 16 * f);
     w[f] = ld4(wrow + 16 * f);
   }
-  // keep every fragment load in flight before the first MFMA waits
+  // epilogue operands ride with the fragments: no dependent round trip
+  // after the MFMAs (rows clamped instead of branching around the loads)
+  const int col = n0 + li;
+  const float bv = g.bias ? g.bias[col] : 0.f;
+  float rv[4] = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (RESID) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) rv[r] = g.R[(size_t)min(m0 + lq * 4 + r, M - 1) * g.ldr + col];
+  }
+  float mu = 0.f, rs = 1.f;
+  if constexpr (LN) {
+    // every lane merges its own row's partial statistics (no barrier)
+    if (g.part_in) merge_stats(g.part_in + (size_t)(row_ok ? row : M - 1) * ND_PART_LD * 2, g.part_n_in, mu, rs);
+  }
+  // keep every load in flight before the first MFMA waits
   __builtin_amdgcn_sched_barrier(0);
   if constexpr (LN) {
-    if (g.part_in) {
-      if (tid < 16) {
-        float mu, rs;
-        merge_stats(g.part_in + (size_t)min(m0 + tid, M - 1) * ND_PART_LD * 2, g.part_n_in, mu, rs);
-        s_mu[tid] = mu;
-        s_rs[tid] = rs;
-      }
-    } else {
+    if (!g.part_in) {
       constexpr int RPW = (16 + WAVES - 1) / WAVES;
       f32x4 v[RPW];
 #pragma unroll
@@ -271,19 +294,20 @@ __global__ void __launch_bounds__(NT* KS * 64) gemm_f32_small_kernel(const GemmA
 #pragma unroll
       for (int i = 0; i < RPW; ++i) {
         const int r = wave + i * WAVES;
-        const float mu = wave_sum(v[i].x + v[i].y + v[i].z + v[i].w) * (1.0f / 256.0f);
-        const f32x4 d = v[i] - mu;
+        const float m_ = wave_sum(v[i].x + v[i].y + v[i].z + v[i].w) * (1.0f / 256.0f);
+        const f32x4 d = v[i] - m_;
         const float var = wave_sum(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w) * (1.0f / 256.0f);
         if (lane == 0 && r < 16) {
-          s_mu[r] = mu;
+          s_mu[r] = m_;
           s_rs[r] = 1.0f / sqrtf(var + ND_LN_EPS);
         }
       }
+      __syncthreads();
+      mu = s_mu[li];
+      rs = s_rs[li];
     }
-    __syncthreads();
-    const float mu = s_mu[li], rs = s_rs[li];
 #pragma unroll
-    for (int f = 0; f < NF; ++f) a[f] = (a[f] - mu) * rs * ld4(g.ln_g + kb + 16 * f) + ld4(g.ln_b + kb + 16 * f);
+    for (int f = 0; f < NF; ++f) a[f] = (a[f] - mu) * rs;
   }
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -307,41 +331,57 @@ __global__ void __launch_bounds__(NT* KS * 64) gemm_f32_small_kernel(const GemmA
       acc[r] = v;
     }
   }
-  const int col = n0 + li;
-  const float bv = g.bias ? g.bias[col] : 0.f;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int orow = m0 + lq * 4 + r;
     float v = acc[r] + bv;
     if constexpr (RELU) v = fmaxf(v, 0.f);
-    if constexpr (RESID) v += orow < M ? g.R[(size_t)orow * g.ldr + col] : 0.f;
+    if constexpr (RESID) v += rv[r];
     if (orow < M) g.C[(size_t)orow * g.ldc + col] = v;
     if (g.part_out) {
       // row statistics over this tile's 16 columns (lanes lq*16 .. lq*16+15)
-      float s = v;
-      s += __shfl_xor(s, 1, 64);
-      s += __shfl_xor(s, 2, 64);
-      s += __shfl_xor(s, 4, 64);
-      s += __shfl_xor(s, 8, 64);
-      const float mu = s * (1.0f / 16.0f);
-      float q = (v - mu) * (v - mu);
-      q += __shfl_xor(q, 1, 64);
-      q += __shfl_xor(q, 2, 64);
-      q += __shfl_xor(q, 4, 64);
-      q += __shfl_xor(q, 8, 64);
+      const float m_ = sum16(v) * (1.0f / 16.0f);
+      const float q = sum16((v - m_) * (v - m_));
       if (li == 0 && orow < M) {
         float* p = g.part_out + ((size_t)orow * ND_PART_LD + n0 / 16) * 2;
-        p[0] = mu;
+        p[0] = m_;
         p[1] = q;
       }
     }
   }
 }
 
+// LayerNorm affine folded into the following Linear (done once per weight
+// set): W'[n][k] = W[n][k] g[k], b'[n] = b[n] + sum_k W[n][k] beta[k]
+// (accumulated in f64).  One wave per output row.
+__global__ void __launch_bounds__(256)
+fold_layernorm_kernel(const float* __restrict__ W, const float* __restrict__ bias, const float* __restrict__ lg,
+                      const float* __restrict__ lb, float* __restrict__ Wo, float* __restrict__ bo, int N, int K) {
+  const int n = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (n >= N) return;
+  double s = 0.0;
+  for (int k = lane; k < K; k += 64) {
+    const float w = W[(size_t)n * K + k];
+    Wo[(size_t)n * K + k] = w * lg[k];
+    s += (double)w * (double)lb[k];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (lane == 0) bo[n] = (float)((bias ? (double)bias[n] : 0.0) + s);
+}
+
+hipError_t launch_fold_layernorm(const float* W, const float* bias, const float* ln_g, const float* ln_b,
+                                 float* W_out, float* b_out, int N, int K, hipStream_t s) {
+  if (N <= 0 || K <= 0 || !W || !ln_g || !ln_b || !W_out || !b_out) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(fold_layernorm_kernel, dim3((N + 3) / 4), dim3(256), 0, s, W, bias, ln_g, ln_b, W_out, b_out, N,
+                     K);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------
 #define ND_DISPATCH_FLAGS(KERNEL, ...)                                                          \
   do {                                                                                          \
-    const bool ln_ = g.ln_g != nullptr, re_ = g.relu, rs_ = g.R != nullptr;                     \
+    const bool ln_ = g.norm, re_ = g.relu, rs_ = g.R != nullptr;                     \
     if (!ln_ && !re_ && !rs_) hipLaunchKernelGGL((KERNEL<__VA_ARGS__, false, false, false>), grid, block, 0, s, g); \
     if (!ln_ && !re_ && rs_) hipLaunchKernelGGL((KERNEL<__VA_ARGS__, false, false, true>), grid, block, 0, s, g);   \
     if (!ln_ && re_ && !rs_) hipLaunchKernelGGL((KERNEL<__VA_ARGS__, false, true, false>), grid, block, 0, s, g);   \
@@ -371,7 +411,7 @@ static hipError_t launch_small(GemmArgs& g, hipStream_t s) {
 
 hipError_t launch_gemm(GemmArgs& g, hipStream_t s) {
   if (g.M <= 0) return hipSuccess;
-  if (g.K % 32 != 0 || (g.ln_g && g.K != ND_D)) return hipErrorInvalidValue;
+  if (g.K % 32 != 0 || (g.norm && g.K != ND_D)) return hipErrorInvalidValue;
   if (g.part_in && (g.part_n_in < 1 || g.part_n_in > ND_PART_LD || (ND_D % g.part_n_in) != 0))
     return hipErrorInvalidValue;
   if (g.part_out && g.N != ND_D) return hipErrorInvalidValue;  // statistics of whole 256-wide rows
@@ -382,8 +422,8 @@ hipError_t launch_gemm(GemmArgs& g, hipStream_t s) {
   if (g.N % 16 != 0) return hipErrorInvalidValue;
   if (g.K == 256) {
     // LN consumers: share the row statistics across many column tiles
-    if (g.ln_g && g.N % 128 == 0 && (long)(g.N / 128) * ((g.M + 15) / 16) >= 128) return launch_small<8, 1, 256>(g, s);
-    if (g.ln_g && g.N % 64 == 0) return launch_small<4, 2, 128>(g, s);
+    if (g.norm && g.N % 128 == 0 && (long)(g.N / 128) * ((g.M + 15) / 16) >= 128) return launch_small<8, 1, 256>(g, s);
+    if (g.norm && g.N % 64 == 0) return launch_small<4, 2, 128>(g, s);
     return launch_small<1, 4, 64>(g, s);
   }
   if (g.K == 2048) return launch_small<1, 8, 256>(g, s);

@@ -15,8 +15,10 @@ struct GemmArgs {
   int ldr = 0;
   float* C = nullptr;
   int ldc = 0;
-  const float* ln_g = nullptr;  // LayerNorm prologue over K (K == 256)
-  const float* ln_b = nullptr;
+  // LayerNorm prologue over K (K == 256): rows of A are normalised,
+  // (a - mean) * rstd; the LayerNorm's affine (gamma, beta) is folded into
+  // W and bias once at load time (launch_fold_layernorm).
+  bool norm = false;
   int M = 0, N = 0, K = 0;
   bool relu = false;
   // Row statistics hand-off (LayerNorm fusion across kernels):
@@ -32,6 +34,10 @@ struct GemmArgs {
 };
 #define ND_PART_LD 16  // partial-stat slots per row (max column tiles of a 256-wide row)
 hipError_t launch_gemm(GemmArgs& g, hipStream_t s);
+// W_out[n][k] = W[n][k] * ln_g[k];  b_out[n] = bias[n] + sum_k W[n][k] * ln_b[k]
+// (LayerNorm(x) W^T + b == xhat (W diag(g))^T + (W beta + b)); bias may be null.
+hipError_t launch_fold_layernorm(const float* W, const float* bias, const float* ln_g, const float* ln_b,
+                                 float* W_out, float* b_out, int N, int K, hipStream_t s);
 
 // ---- encoder -------------------------------------------------------------
 // x[b*T+t][:] = signal[b][t] * w_in + b_in (Linear(1, d)); part: full-row stats
@@ -62,11 +68,23 @@ hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* 
 hipError_t launch_dec_ctx_attention(const float* q, const float* kv, int ld, int koff, const float* signal,
                                     const int* span, float pad_val, float* out, int C, int rpc, int T,
                                     hipStream_t s);
+// Next step's decoder input, written by the search kernel that picks the
+// token (the embedding of step+1 fused into the head: one launch fewer per
+// step): x[row] = emb[tok] (* 16 + pe[step+1] with position encoding) and
+// its row statistics.  Skipped after the last step.
+struct NextEmbed {
+  const float* emb = nullptr;
+  const float* pe = nullptr;  // null: no position encoding (and no sqrt(d) scale)
+  float* x = nullptr;
+  float* part = nullptr;
+};
 // greedy head: LN_dec -> generator -> log_softmax -> argmax; writes token
-// (next input + output [R, S] at column step), score, optional logp dump.
+// (next input + output [R, S] at column step), score, optional logp dump,
+// and the next step's embedded input (ne).
 hipError_t launch_dec_greedy_head(const float* x, const float* ln_g, const float* ln_b, const float* gw,
                                   const float* gb, int V, int step, int S, int min_len, int eos, int* tok,
-                                  int* out_tokens, float* score, float* logp_dump, int R, hipStream_t s);
+                                  int* out_tokens, float* score, float* logp_dump, const NextEmbed& ne, int R,
+                                  hipStream_t s);
 
 struct BeamState {
   float* cum;        // [C, beam] topk_log_probs
@@ -83,7 +101,7 @@ struct BeamState {
   int* steps_done;   // [1] decoder steps until the last chunk finished
 };
 hipError_t launch_beam_init(const BeamState& st, int C, int beam, int n_best, int S, int bos, hipStream_t s);
-hipError_t launch_beam_step(const float* x, const float* ln_g, const float* ln_b, const float* gw, const float* gb,
+hipError_t launch_beam_step(const NextEmbed& ne, const float* x, const float* ln_g, const float* ln_b, const float* gw, const float* gb,
                             int V, const BeamState& st, int C, int beam, int n_best, int step, int S, int min_len,
                             int eos, float lenpen, hipStream_t s);
 hipError_t launch_beam_finish(const BeamState& st, int C, int n_best, int S, int* tokens, float* scores, int* lens,

@@ -34,40 +34,60 @@ __device__ __forceinline__ void head_row(const float* __restrict__ x, const floa
   for (int k = 0; k < V; ++k) lp[k] = (lp[k] - mx) - ls;
 }
 
+// Writes the embedded input row of step `step_next` for token `tk` (one wave;
+// onmt/modules/embeddings.py:189-207, PositionalEncoding :36-43).
+__device__ __forceinline__ void embed_row(const NextEmbed& ne, int tk, int step_next, int row, int lane) {
+  f32x4 e = ld4(ne.emb + (size_t)tk * ND_D + lane * 4);
+  if (ne.pe) e = e * 16.0f + ld4(ne.pe + (size_t)step_next * ND_D + lane * 4);  // sqrt(256) = 16
+  st4(ne.x + (size_t)row * ND_D + lane * 4, e);
+  const float mu = wave_sum(e.x + e.y + e.z + e.w) * (1.0f / ND_D);
+  const f32x4 d = e - mu;
+  const float q = wave_sum(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w);
+  if (lane == 0) {
+    ne.part[(size_t)row * ND_PART_LD * 2] = mu;  // one partial per row
+    ne.part[(size_t)row * ND_PART_LD * 2 + 1] = q;
+  }
+}
+
 __global__ void __launch_bounds__(256)
 greedy_head_kernel(const float* __restrict__ x, const float* __restrict__ ln_g, const float* __restrict__ ln_b,
                    const float* __restrict__ gw, const float* __restrict__ gb, int V, int step, int S, int min_len,
                    int eos, int* __restrict__ tok, int* __restrict__ out_tokens, float* __restrict__ score,
-                   float* __restrict__ logp_dump, int R) {
+                   float* __restrict__ logp_dump, NextEmbed ne, int R) {
   __shared__ float lps[4][ND_MAXV];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = blockIdx.x * 4 + w;
   if (r >= R) return;
   float* lp = lps[w];
   head_row(x + (size_t)r * ND_D, ln_g, ln_b, gw, gb, V, lane, lp);
+  if (lane == 0 && logp_dump)
+    for (int k = 0; k < V; ++k) logp_dump[((size_t)r * S + step) * V + k] = lp[k];
+  // every lane runs the (tiny) argmax so the token needs no broadcast
+  const bool no_eos = step < min_len;
+  int best = 0;
+  float bv = (no_eos && eos == 0) ? -1e20f : lp[0];
+  for (int k = 1; k < V; ++k) {
+    const float v = (no_eos && k == eos) ? -1e20f : lp[k];
+    if (v > bv) {  // first index wins ties (topk(1))
+      bv = v;
+      best = k;
+    }
+  }
   if (lane == 0) {
-    if (logp_dump)
-      for (int k = 0; k < V; ++k) logp_dump[((size_t)r * S + step) * V + k] = lp[k];
-    if (step < min_len) lp[eos] = -1e20f;
-    int best = 0;
-    float bv = lp[0];
-    for (int k = 1; k < V; ++k)
-      if (lp[k] > bv) {  // first index wins ties (topk(1))
-        bv = lp[k];
-        best = k;
-      }
     tok[r] = best;
     out_tokens[(size_t)r * S + step] = best;
     score[r] = bv;
   }
+  if (step + 1 < S) embed_row(ne, best, step + 1, r, lane);
 }
 
 hipError_t launch_dec_greedy_head(const float* x, const float* ln_g, const float* ln_b, const float* gw,
                                   const float* gb, int V, int step, int S, int min_len, int eos, int* tok,
-                                  int* out_tokens, float* score, float* logp_dump, int R, hipStream_t s) {
-  if (V > ND_MAXV) return hipErrorInvalidValue;
+                                  int* out_tokens, float* score, float* logp_dump, const NextEmbed& ne, int R,
+                                  hipStream_t s) {
+  if (V > ND_MAXV || !ne.emb || !ne.x || !ne.part) return hipErrorInvalidValue;
   hipLaunchKernelGGL(greedy_head_kernel, dim3((R + 3) / 4), dim3(256), 0, s, x, ln_g, ln_b, gw, gb, V, step, S,
-                     min_len, eos, tok, out_tokens, score, logp_dump, R);
+                     min_len, eos, tok, out_tokens, score, logp_dump, ne, R);
   return hipGetLastError();
 }
 
@@ -97,7 +117,7 @@ hipError_t launch_beam_init(const BeamState& st, int C, int beam, int n_best, in
 
 // One workgroup (256 threads = 4 waves) per chunk.
 __global__ void __launch_bounds__(256)
-beam_step_kernel(const float* __restrict__ x, const float* __restrict__ ln_g, const float* __restrict__ ln_b,
+beam_step_kernel(NextEmbed ne, const float* __restrict__ x, const float* __restrict__ ln_g, const float* __restrict__ ln_b,
                  const float* __restrict__ gw, const float* __restrict__ gb, int V, BeamState st, int beam,
                  int n_best, int step, int S, int min_len, int eos, float lenpen) {
   __shared__ float lp[BEAM_MAX][ND_MAXV];
@@ -171,6 +191,9 @@ beam_step_kernel(const float* __restrict__ x, const float* __restrict__ ln_g, co
     st.tok[row0 + tid] = tok;
     st.cum[row0 + tid] = fin[tid] ? -1e10f : tsc[tid] * lenpen;  // :728, :756
   }
+  // next step's input rows (x was fully read by head_row before the first barrier)
+  if (step + 1 < S)
+    for (int j = w; j < beam; j += 4) embed_row(ne, tid_sel[j] % V, step + 1, row0 + j, lane);
   __syncthreads();
   if (tid == 0) {
     bool any = false;
@@ -209,11 +232,11 @@ beam_step_kernel(const float* __restrict__ x, const float* __restrict__ ln_g, co
   }
 }
 
-hipError_t launch_beam_step(const float* x, const float* ln_g, const float* ln_b, const float* gw, const float* gb,
+hipError_t launch_beam_step(const NextEmbed& ne, const float* x, const float* ln_g, const float* ln_b, const float* gw, const float* gb,
                             int V, const BeamState& st, int C, int beam, int n_best, int step, int S, int min_len,
                             int eos, float lenpen, hipStream_t s) {
-  if (beam > BEAM_MAX || beam * V > 256 || V > ND_MAXV) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(beam_step_kernel, dim3(C), dim3(256), 0, s, x, ln_g, ln_b, gw, gb, V, st, beam, n_best, step,
+  if (beam > BEAM_MAX || beam * V > 256 || V > ND_MAXV || !ne.emb || !ne.x || !ne.part) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(beam_step_kernel, dim3(C), dim3(256), 0, s, ne, x, ln_g, ln_b, gw, gb, V, st, beam, n_best, step,
                      S, min_len, eos, lenpen);
   return hipGetLastError();
 }

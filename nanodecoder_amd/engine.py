@@ -131,13 +131,30 @@ class Engine:
 # op-level entry points (kernel unit tests)
 # ---------------------------------------------------------------------------
 
-def op_gemm(A: torch.Tensor, W: torch.Tensor, bias=None, R=None, ln_g=None, ln_b=None, relu=False):
+def op_fold_layernorm(W: torch.Tensor, bias, ln_g: torch.Tensor, ln_b: torch.Tensor):
+    """(W diag(ln_g), bias + W ln_b): the LayerNorm affine folded into the Linear."""
+    N, K = W.shape
+    Wo = torch.empty_like(W)
+    bo = torch.empty(N, dtype=torch.float32, device=W.device)
+    s = ctypes.c_void_p(torch.cuda.current_stream(W.device).cuda_stream)
+    _lib.check(_lib.lib().nd_op_fold_layernorm(_ptr(W), _ptr(bias), _ptr(ln_g), _ptr(ln_b), _ptr(Wo), _ptr(bo), N, K,
+                                               s), "nd_op_fold_layernorm")
+    return Wo, bo
+
+
+def op_gemm(A: torch.Tensor, W: torch.Tensor, bias=None, R=None, ln_g=None, ln_b=None, relu=False, norm=False):
+    """C = relu?(LN?(A) W^T + bias) (+ R).  With ln_g/ln_b the affine is folded
+    first (nd_op_fold_layernorm) and the GEMM runs with norm=1, as the engine
+    does; norm=True alone means W/bias are already folded."""
     M, K = A.shape
     N = W.shape[0]
+    if ln_g is not None:
+        W, bias = op_fold_layernorm(W, bias, ln_g, ln_b)
+        norm = True
     C = torch.empty(M, N, dtype=torch.float32, device=A.device)
     s = ctypes.c_void_p(torch.cuda.current_stream(A.device).cuda_stream)
-    _lib.check(_lib.lib().nd_op_gemm(_ptr(A), _ptr(W), _ptr(bias), _ptr(R), _ptr(C), M, N, K, _ptr(ln_g), _ptr(ln_b),
-                                     int(relu), s), "nd_op_gemm")
+    _lib.check(_lib.lib().nd_op_gemm(_ptr(A), _ptr(W), _ptr(bias), _ptr(R), _ptr(C), M, N, K, int(norm), int(relu),
+                                     s), "nd_op_gemm")
     return C
 
 

@@ -12,9 +12,17 @@ dev = torch.device("cuda", 0)
 ONLY = sys.argv[1] if len(sys.argv) > 1 else ""
 
 
+EAGER = os.environ.get("MB_EAGER") == "1"  # plain launches (for PMC counter passes)
+
+
 def timeit(fn, n=50):
     """Per-launch time inside a captured graph of n back-to-back launches
     (the way the engine runs them), in microseconds."""
+    if EAGER:
+        for _ in range(n):
+            fn()
+        torch.cuda.synchronize()
+        return float("nan")
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
@@ -41,9 +49,9 @@ def gemm_case(M, N, K, ln, relu, res):
     W = torch.randn(N, K, device=dev) / K ** 0.5
     b = torch.randn(N, device=dev)
     R = torch.randn(M, N, device=dev) if res else None
-    g = torch.ones(K, device=dev) if ln else None
-    bb = torch.zeros(K, device=dev) if ln else None
-    us = timeit(lambda: E.op_gemm(A, W, b, R, g, bb, relu))
+    if ln:  # the engine folds the LayerNorm affine once at load time
+        W, b = E.op_fold_layernorm(W, b, torch.rand(K, device=dev) + 0.5, torch.randn(K, device=dev))
+    us = timeit(lambda: E.op_gemm(A, W, b, R, relu=relu, norm=ln))
     tf = 2 * M * N * K / (us * 1e-6) / 1e12
     print(f"gemm M={M:6d} N={N:5d} K={K:5d} ln={int(ln)} relu={int(relu)} res={int(res)}: {us:9.2f} us  {tf:6.1f} TF/s")
 
@@ -56,6 +64,14 @@ if ONLY == "dec256":
     cache = torch.randn(256, 100, 512, device=dev)
     us = timeit(lambda: E.op_dec_self_attention(qkv, cache, 60))
     print(f"self-attn R=256 step=60: {us:8.2f} us")
+    for C, rpc in ((256, 1), (256, 5)):
+        T = 512
+        q = torch.randn(C * rpc, 256, device=dev)
+        kv = torch.randn(C * T, 1536, device=dev)
+        sig = torch.randn(C, T, device=dev)
+        span = torch.full((C,), T, dtype=torch.int32, device=dev)
+        us = timeit(lambda: E.op_dec_ctx_attention(q, kv, 1536, 0, sig, span, 1.0, rpc))
+        print(f"ctx-attn C={C} rpc={rpc}: {us:8.2f} us  {C * T * 512 * 4 / (us * 1e-6) / 1e9:7.1f} GB/s (K+V bytes)")
     sys.exit(0)
 for M in (256, 1280, 5120):
     gemm_case(M, 768, 256, True, False, False)
@@ -79,7 +95,7 @@ for R in (256, 5120):
         print(f"self-attn R={R} step={step}: {us:8.2f} us")
 
 # decoder context attention
-for C, rpc in ((256, 1), (1024, 5)):
+for C, rpc in ((256, 1), (256, 5)):
     T = 512
     q = torch.randn(C * rpc, 256, device=dev)
     kv = torch.randn(C * T, 1536, device=dev)
