@@ -108,15 +108,16 @@ def kernel_roofline(eng, B, mode, beam):
     with HIP events, on the engine's shapes, cycling the three layers' K/V
     column offsets as the decode loop does.  Algorithmic bytes per launch =
     K+V (2 x 512 keys x 256 f32 per chunk) + q, signal and output rows."""
-    from nanodecoder_amd.engine import op_dec_ctx_attention, op_gemm
+    from nanodecoder_amd.engine import op_dec_ctx_attention, op_fold_layernorm, op_gemm, pack_p16
     dev = eng.device
     rpc = 1 if mode == "greedy" else beam
     T, D = 512, 256
     kv = torch.randn(B * T, 3 * 2 * D, device=dev)
-    q = torch.randn(B * rpc, D, device=dev)
+    q = pack_p16(torch.randn(B * rpc, D, device=dev))  # decoder activations live P16-packed
     sig = torch.randn(B, T, device=dev)
     span = torch.full((B,), T, dtype=torch.int32, device=dev)
-    fn = lambda i: op_dec_ctx_attention(q, kv, 3 * 2 * D, (i % 3) * 2 * D, sig, span, 1.0, rpc)  # noqa: E731
+    fn = lambda i: op_dec_ctx_attention(q, kv, 3 * 2 * D, (i % 3) * 2 * D, sig, span, 1.0, rpc,  # noqa: E731
+                                        packed=True)
     for i in range(6):
         fn(i)
     ms = _time(fn, 30)
@@ -130,10 +131,10 @@ def kernel_roofline(eng, B, mode, beam):
     A = torch.randn(M, K, device=dev)
     Wt = torch.randn(N, K, device=dev) / 16
     b = torch.randn(N, device=dev)
-    g1, b1 = torch.ones(K, device=dev), torch.zeros(K, device=dev)
+    Wf, bf = op_fold_layernorm(Wt, b, torch.ones(K, device=dev), torch.zeros(K, device=dev))  # as at load time
     for _ in range(3):
-        op_gemm(A, Wt, b, None, g1, b1, True)
-    gms = _time(lambda i: op_gemm(A, Wt, b, None, g1, b1, True), 10)
+        op_gemm(A, Wf, bf, None, relu=True, norm=True)
+    gms = _time(lambda i: op_gemm(A, Wf, bf, None, relu=True, norm=True), 10)
     tf = 2.0 * M * N * K / (gms * 1e-3) / 1e12
     out["mfma_kernel"] = {"kernel": "gemm_f32_kernel<128,128,2,2,LN,RELU> (encoder FFN1)", "achieved": round(tf, 2),
                           "peak": 157.3, "unit": "TFLOP/s", "frac": round(tf / 157.3, 4),

@@ -110,6 +110,14 @@ int nd_encode(nd_ctx* ctx, const float* d_signal, const int32_t* d_len, const in
 /* Enables/disables hipGraph capture of the translate calls (default on). */
 int nd_set_graphs(nd_ctx* ctx, int enable);
 
+/* Context-attention form: 0 (default) = the memory-bank form for greedy
+ * decoding (ctx K/V projections folded into the query / output GEMMs, one
+ * shared 256-float memory row per source position) and the per-layer K/V
+ * form for beam search; 1 = the K/V form always.  Same results to fp32
+ * rounding; replaces decoder/transformer.py:82-86 + multi_headed_attn.py:
+ * 142-177's context path. */
+int nd_set_ctx_path(nd_ctx* ctx, int path);
+
 /* Kernel statistics of the last translate call (ms of device time per
  * phase, measured with HIP events on the engine stream when enabled). */
 int nd_set_timing(nd_ctx* ctx, int enable);
@@ -131,6 +139,22 @@ const char* nd_version(void);
 int nd_op_gemm(const float* A, const float* W, const float* bias, const float* R, float* C, int32_t M,
                int32_t N, int32_t K, int32_t norm, int32_t relu, void* stream);
 
+/* The decoder-step form of the same GEMM, on the fragment-packed "P16"
+ * layout the engine keeps decoder activations and step weights in: an
+ * [M, N] matrix (M, N multiples of 16) stored as 16x16 blocks in row-major
+ * block order, each block 64 float4 entries, entry e = (m%16) + 16*((n%16)/4)
+ * holding columns n&~3..+3 of row m (nd_op_pack_p16 converts).  A, W, R, C
+ * packed.  LayerNorm prologue when part_in != NULL: per-row partial
+ * statistics {mean_j, M2_j} of part_n_in equal column tiles at
+ * part_in[(row*16 + j)*2]; part_out (nullable, N == 256) receives this
+ * GEMM's output row partials, their count in *part_n_out. */
+int nd_op_gemm_p16(const float* A, const float* W, const float* bias, const float* R, float* C, int32_t M,
+                   int32_t N, int32_t K, const float* part_in, int32_t part_n_in, float* part_out, int32_t relu,
+                   int32_t* part_n_out, void* stream);
+
+/* row-major [M, N] -> P16 packed (M, N multiples of 16). */
+int nd_op_pack_p16(const float* src, float* dst, int32_t M, int32_t N, void* stream);
+
 /* Fold a LayerNorm's affine into the Linear that consumes it:
  * W_out = W diag(ln_g), b_out = bias + W ln_b (bias may be NULL), so that
  * Linear(LayerNorm(x)) == nd_op_gemm(x, W_out, b_out, norm = 1).  W [N,K]. */
@@ -143,15 +167,32 @@ int nd_op_enc_attention(const float* qkv, const float* signal, const int32_t* sp
                         int32_t T, void* stream);
 
 /* Decoder self-attention for one step (multi_headed_attn.py:124-141):
- * qkv [R, 3*d]; cache [R, max_steps, 2*d] (this step's k|v is appended at
- * [r][step]); anc nullable [R, anc_ld] slot ancestry (NULL = identity);
- * out [R, d]. */
+ * qkv [R, 3*d] and out [R, d] P16-packed (R padded to a multiple of 16);
+ * cache [R, max_steps, 2*d] row-major (this step's k|v is appended at
+ * [r][step]); anc nullable [R, anc_ld] slot ancestry (NULL = identity). */
 int nd_op_dec_self_attention(const float* qkv, float* cache, const int32_t* anc, int32_t anc_ld, int32_t step,
                              int32_t max_steps, float* out, int32_t R, void* stream);
 
+/* Memory-bank context attention (greedy form, engine.hip
+ * derive_memory_bank_weights): rows r = c*rpc+j (rpc*8 <= 16) of
+ * qp = Q' [C*rpc, 8*256] (P16; column block h = head h's query mapped into
+ * memory space) attend over the P16 memory bank mem (T16 rows per chunk,
+ * T16 a multiple of 16 >= T) with keys t < span[c] and key mask
+ * signal[c*T+t] == pad_val; out = U [C*rpc, 8*256] P16 (head h: the
+ * softmax-weighted sum of memory rows). */
+int nd_op_dec_mem_attention(const float* qp, const float* mem, const float* signal, const int32_t* span, float pad_val,
+                            float* out, int32_t C, int32_t rpc, int32_t T, int32_t T16, void* stream);
+
+/* Encoder output x [B*T, 256] row-major -> P16 memory bank with T16 rows per
+ * chunk (LayerNorm with ln_g/ln_b when ln_g != NULL, encoder/transformer.py:
+ * 126; rows t >= T zero). */
+int nd_op_memory_pack(const float* x, const float* ln_g, const float* ln_b, float* out, int32_t B, int32_t T,
+                      int32_t T16, void* stream);
+
 /* Decoder context attention (multi_headed_attn.py:142-177): rows r = c*rpc+j
  * of q [C*rpc, d] attend over K at kv[(c*T+t)*ld + koff] and V at +d, keys
- * t < span[c], key mask signal == pad_val; out [C*rpc, d]. */
+ * t < span[c], key mask signal == pad_val; out [C*rpc, d].  q and out are
+ * P16-packed (rows padded to a multiple of 16), kv row-major. */
 int nd_op_dec_ctx_attention(const float* q, const float* kv, int32_t ld, int32_t koff, const float* signal,
                             const int32_t* span, float pad_val, float* out, int32_t C, int32_t rpc, int32_t T,
                             void* stream);

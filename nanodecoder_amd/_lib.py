@@ -40,12 +40,17 @@ SIGNATURES = {
     "nd_encode": (_I, [_P, _P, _P, _P, _I, _I, _P, _P]),
     "nd_set_graphs": (_I, [_P, _I]),
     "nd_set_timing": (_I, [_P, _I]),
+    "nd_set_ctx_path": (_I, [_P, _I]),
     "nd_last_timing": (_I, [_P, ctypes.POINTER(_F), ctypes.POINTER(_F)]),
     "nd_destroy": (None, [_P]),
     "nd_last_error": (ctypes.c_char_p, []),
     "nd_version": (ctypes.c_char_p, []),
     "nd_op_gemm": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "nd_op_fold_layernorm": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _P]),
+    "nd_op_gemm_p16": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _P, _I, _P, _I, _P, _P]),
+    "nd_op_pack_p16": (_I, [_P, _P, _I, _I, _P]),
+    "nd_op_dec_mem_attention": (_I, [_P, _P, _P, _P, ctypes.c_float, _P, _I, _I, _I, _I, _P]),
+    "nd_op_memory_pack": (_I, [_P, _P, _P, _P, _I, _I, _I, _P]),
     "nd_op_enc_attention": (_I, [_P, _P, _P, _P, _I, _I, _P]),
     "nd_op_dec_self_attention": (_I, [_P, _P, _P, _I, _I, _I, _P, _I, _P]),
     "nd_op_dec_ctx_attention": (_I, [_P, _P, _I, _I, _P, _P, _F, _P, _I, _I, _I, _P]),

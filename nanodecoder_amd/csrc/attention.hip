@@ -195,7 +195,7 @@ dec_embed_kernel(const int* __restrict__ tok, const float* __restrict__ emb, con
   if (row >= R) return;
   f32x4 e = ld4(emb + (size_t)tok[row] * ND_D + lane * 4);
   if (pe) e = e * 16.0f + ld4(pe + (size_t)step * ND_D + lane * 4);  // sqrt(256) = 16
-  st4(x + (size_t)row * ND_D + lane * 4, e);
+  st4(x + pk(row, lane * 4, ND_D), e);  // decoder activations are P16-packed
   if (part) row_part(e, lane, part + (size_t)row * ND_PART_LD * 2);
 }
 
@@ -234,11 +234,12 @@ __device__ __forceinline__ void online_update(const float (&s)[RPC][U], const f3
   }
 }
 
-// LDS image: accs [NW][RPC][256], ms / ls [NW][RPC][8].  out rows j at out + j*256.
+// LDS image: accs [NW][RPC][256], ms / ls [NW][RPC][8].  Output rows
+// row0 .. row0+RPC-1 of the P16-packed [*, 256] matrix out.
 template <int RPC, int NW>
 __device__ __forceinline__ void merge_waves(float* accs, float* ms, float* ls, const float (&m)[RPC],
                                             const float (&l)[RPC], const f32x4 (&acc)[RPC], int wave, int lane,
-                                            int tid, float* __restrict__ out) {
+                                            int tid, float* __restrict__ out, int row0) {
 #pragma unroll
   for (int j = 0; j < RPC; ++j) {
     st4(accs + ((size_t)wave * RPC + j) * ND_D + lane * 4, acc[j]);
@@ -261,7 +262,7 @@ __device__ __forceinline__ void merge_waves(float* accs, float* ms, float* ls, c
       num += f * accs[((size_t)w * RPC + j) * ND_D + d];
       den += f * ls[(w * RPC + j) * ND_H + h];
     }
-    out[e] = den > 0.f ? num / den : 0.f;
+    out[pk(row0 + j, d & ~3, ND_D) + (d & 3)] = den > 0.f ? num / den : 0.f;
   }
 }
 
@@ -280,9 +281,9 @@ dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cac
   __shared__ float accs[SELF_NW * ND_D];
   __shared__ float ms[SELF_NW * ND_H], ls[SELF_NW * ND_H];
   const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const float* qrow = qkv + (size_t)r * 3 * ND_D;
-  const f32x4 qv[1] = {ld4(qrow + lane * 4) / ND_SQRT_DH};
-  const f32x4 kme = ld4(qrow + ND_D + lane * 4), vme = ld4(qrow + 2 * ND_D + lane * 4);
+  // qkv is P16-packed [R, 768]
+  const f32x4 qv[1] = {ld4(qkv + pk(r, lane * 4, 3 * ND_D)) / ND_SQRT_DH};
+  const f32x4 kme = ld4(qkv + pk(r, ND_D + lane * 4, 3 * ND_D)), vme = ld4(qkv + pk(r, 2 * ND_D + lane * 4, 3 * ND_D));
   if (wave == 0) {
     float* mine = cache + ((size_t)r * S + step) * 2 * ND_D;
     st4(mine + lane * 4, kme);
@@ -321,7 +322,7 @@ dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cac
     }
     online_update<1, SELF_U>(sc, v, m, l, acc);
   }
-  merge_waves<1, SELF_NW>(accs, ms, ls, m, l, acc, wave, lane, tid, out + (size_t)r * ND_D);
+  merge_waves<1, SELF_NW>(accs, ms, ls, m, l, acc, wave, lane, tid, out, r);
 }
 
 hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* anc, int anc_ld, int step,
@@ -369,7 +370,7 @@ dec_ctx_attention_kernel(const float* __restrict__ q, const float* __restrict__ 
   float m[RPC], l[RPC];
 #pragma unroll
   for (int j = 0; j < RPC; ++j) {
-    qv[j] = ld4(q + ((size_t)c * RPC + j) * ND_D + lane * 4) / ND_SQRT_DH;
+    qv[j] = ld4(q + pk(c * RPC + j, lane * 4, ND_D)) / ND_SQRT_DH;  // q, out P16-packed
     acc[j] = {0.f, 0.f, 0.f, 0.f};
     m[j] = -INFINITY;
     l[j] = 0.f;
@@ -413,7 +414,7 @@ dec_ctx_attention_kernel(const float* __restrict__ q, const float* __restrict__ 
       }
     }
   }
-  merge_waves<RPC, CTX_NW>(accs, ms, ls, m, l, acc, wave, lane, tid, out + (size_t)c * RPC * ND_D);
+  merge_waves<RPC, CTX_NW>(accs, ms, ls, m, l, acc, wave, lane, tid, out, c * RPC);
 }
 
 static size_t ctx_lds_bytes(int rpc) { return (size_t)CTX_NW * rpc * (ND_D + 2 * ND_H) * sizeof(float); }
@@ -440,6 +441,193 @@ hipError_t launch_dec_ctx_attention(const float* q, const float* kv, int ld, int
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Memory-bank form of the context attention (greedy decoding).
+//
+// With the decoder's ctx K/V projections folded into the query and output
+// sides (engine finalize: W_qk[h] = W_k,h^T W_q,h / sqrt(d_h),
+// W_vo[:, h] = W_o,h W_v,h), head h of row r needs only the encoder memory
+// bank m_t (256 floats per source position, shared by all three decoder
+// layers) instead of a per-layer K and V:
+//   s_h(t) = q'_h . m_t        (q'_h = W_qk[h] LN(x) + b_qk[h]; the dropped
+//                               q_h . b_k,h is constant in t: softmax-exact)
+//   U_h    = sum_t softmax_t(s_h)(t) m_t,   out = W_vo U + b_vo
+// which halves the bytes the decode loop streams per step and lets the bank
+// (128 MB at 256 chunks x 512 positions) stay in the MALL across layers.
+//
+// One workgroup (8 waves) per chunk; the chunk's 8 (head) query rows form
+// one 16-row MFMA tile (rows 8..15 zero).  Per 16-key tile a wave computes
+// S^T = M Q'^T (A = the P16 memory tile, coalesced), runs the online
+// softmax on its row (lane l: row l&15, keys 4(l>>4)..+3), transposes the
+// memory tile through its private LDS slab, and accumulates
+// U^T += M^T P^T, whose fragments are P16 entries of U (lane l: row l&15,
+// dims 4(l>>4)..+3 of each 16-dim tile).  The 8 waves' states merge through
+// LDS.  Mask: src == pad -> -1e18 (multi_headed_attn.py:172), t >= span:
+// absent.
+#define MEM_NW 8
+__device__ __forceinline__ f32x4 mfma16x4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__global__ void __launch_bounds__(MEM_NW * 64)
+dec_mem_attention_kernel(const float* __restrict__ qp, const float* __restrict__ mem, const float* __restrict__ signal,
+                         const int* __restrict__ span, float pad_val, float* __restrict__ out, int rpc, int T,
+                         int T16) {
+  extern __shared__ f32x4 lds4[];
+  f32x4* Qs = lds4;                                // [16 dim blocks][64 lanes] Q' B-fragments
+  float* Mt = reinterpret_cast<float*>(lds4 + 16 * 64);  // [NW][256 dims][16 keys], swizzled
+  float* ms = Mt + MEM_NW * 256 * 16;              // [NW][16 rows]
+  float* ls = ms + MEM_NW * 16;
+  const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int L = min(span[c], T);
+  const int rows = rpc * ND_H;  // <= 16
+  const int ri = lane & 15, lq = lane >> 4;
+  for (int e = tid; e < 16 * 64; e += MEM_NW * 64) {
+    const int f = e >> 6, l = e & 63, rho = l & 15;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (rho < rows) v = ld4(qp + pk(c * rpc + rho / ND_H, (rho % ND_H) * ND_D + 16 * f + 4 * (l >> 4), ND_H * ND_D));
+    Qs[e] = v;
+  }
+  __syncthreads();
+  float mrun = -INFINITY, lrun = 0.f;
+  f32x4 u[16];
+#pragma unroll
+  for (int d = 0; d < 16; ++d) u[d] = {0.f, 0.f, 0.f, 0.f};
+  float* mt = Mt + wave * 256 * 16;
+  const int nkt = (L + 15) >> 4;
+  const f32x4* mbase = reinterpret_cast<const f32x4*>(mem) + (size_t)c * (T16 >> 4) * 16 * 64 + lane;
+  const float* sgc = signal + (size_t)c * T;
+  for (int kt = wave; kt < nkt; kt += MEM_NW) {
+    const int t0 = kt * 16;
+    const f32x4* mp = mbase + (size_t)kt * 16 * 64;  // P16 row block kt of the chunk: 16 col blocks
+    f32x4 a[16];
+#pragma unroll
+    for (int f = 0; f < 16; ++f) a[f] = mp[f * 64];
+    float sg[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sg[r] = sgc[min(t0 + 4 * lq + r, L - 1)];
+    // all 16 KB of the tile in flight before the first MFMA waits
+    __builtin_amdgcn_sched_barrier(0);
+    // S^T = M Q'^T: lane l, reg r = S[row l&15][key t0 + 4(l>>4) + r]
+    f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int f = 0; f < 16; ++f) {
+      const f32x4 q = Qs[f * 64 + lane];
+      s0 = mfma16x4(a[f][0], q[0], s0);
+      s1 = mfma16x4(a[f][1], q[1], s1);
+      s0 = mfma16x4(a[f][2], q[2], s0);
+      s1 = mfma16x4(a[f][3], q[3], s1);
+    }
+    const f32x4 sv = s0 + s1;
+    float sc[4], mx = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int t = t0 + 4 * lq + r;
+      sc[r] = t < L ? (sg[r] == pad_val ? ND_MASK_FILL : sv[r]) : -INFINITY;
+      mx = fmaxf(mx, sc[r]);
+    }
+    mx = xor32_max(xor16_max(mx));  // over the tile's 16 keys
+    const float mnew = fmaxf(mrun, mx);  // finite: key t0 < L exists
+    const float scale = __expf(mrun - mnew);
+    float p[4], psum = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      p[r] = __expf(sc[r] - mnew);
+      psum += p[r];
+    }
+    lrun = lrun * scale + xor32_sum(xor16_sum(psum));
+    mrun = mnew;
+    // memory tile -> LDS transposed: mt[dim][key ^ 4((dim>>2)&3)] (b128 reads conflict-free)
+#pragma unroll
+    for (int f = 0; f < 16; ++f)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) mt[(16 * f + 4 * lq + i) * 16 + (ri ^ (4 * lq))] = a[f][i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // U^T += M^T P^T: A = mt[16d + (l&15)][keys 4(l>>4)..+3], B = p (lane's own keys)
+#pragma unroll
+    for (int d = 0; d < 16; ++d) {
+      const f32x4 mv = ld4(mt + (16 * d + ri) * 16 + ((4 * lq) ^ (4 * ((ri >> 2) & 3))));
+      f32x4 acc = u[d] * scale;
+      acc = mfma16x4(mv[0], p[0], acc);
+      acc = mfma16x4(mv[1], p[1], acc);
+      acc = mfma16x4(mv[2], p[2], acc);
+      acc = mfma16x4(mv[3], p[3], acc);
+      u[d] = acc;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // reads done before the next tile's writes
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  // merge the waves' partial states (the transposition slabs are reused)
+  __syncthreads();
+  float* red = Mt;  // [NW][16 d][64 lanes][4]
+#pragma unroll
+  for (int d = 0; d < 16; ++d) st4(red + ((size_t)(wave * 16 + d) * 64 + lane) * 4, u[d]);
+  if (lq == 0) {
+    ms[wave * 16 + ri] = mrun;
+    ls[wave * 16 + ri] = lrun;
+  }
+  __syncthreads();
+  float M = -INFINITY;
+#pragma unroll
+  for (int w = 0; w < MEM_NW; ++w) M = fmaxf(M, ms[w * 16 + ri]);
+  float fw[MEM_NW], den = 0.f;
+#pragma unroll
+  for (int w = 0; w < MEM_NW; ++w) {
+    const float mw = ms[w * 16 + ri];
+    fw[w] = mw == -INFINITY ? 0.f : __expf(mw - M);  // waves that owned no key
+    den += fw[w] * ls[w * 16 + ri];
+  }
+  const float inv = den > 0.f ? 1.0f / den : 0.f;
+  for (int d = wave; d < 16; d += MEM_NW) {
+    f32x4 num = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int w = 0; w < MEM_NW; ++w) num += fw[w] * ld4(red + ((size_t)(w * 16 + d) * 64 + lane) * 4);
+    if (ri < rows)
+      st4(out + pk(c * rpc + ri / ND_H, (ri % ND_H) * ND_D + 16 * d + 4 * lq, ND_H * ND_D), num * inv);
+  }
+}
+
+static size_t mem_lds_bytes() { return (16 * 64) * sizeof(f32x4) + (size_t)MEM_NW * (256 * 16 + 32) * sizeof(float); }
+
+hipError_t launch_dec_mem_attention(const float* qp, const float* mem, const float* signal, const int* span,
+                                    float pad_val, float* out, int C, int rpc, int T, int T16, hipStream_t s) {
+  if (rpc < 1 || rpc * ND_H > 16 || T < 1 || T > T16 || (T16 & 15)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(dec_mem_attention_kernel, dim3(C), dim3(MEM_NW * 64), mem_lds_bytes(), s, qp, mem, signal, span,
+                     pad_val, out, rpc, T, T16);
+  return hipGetLastError();
+}
+
+// Encoder output -> the decoder's memory bank, P16-packed with T16 rows per
+// chunk: row b*T16 + t = LN(x[b*T + t]) (transformer: encoder.layer_norm,
+// encoder/transformer.py:126) or x itself (NanoEncoder); rows t >= T zero.
+__global__ void __launch_bounds__(256)
+memory_pack_kernel(const float* __restrict__ x, const float* __restrict__ g, const float* __restrict__ b,
+                   float* __restrict__ out, int B, int T, int T16) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= B * T16) return;
+  const int bb = row / T16, t = row - bb * T16;
+  f32x4 v = {0.f, 0.f, 0.f, 0.f};
+  if (t < T) {
+    v = ld4(x + ((size_t)bb * T + t) * ND_D + lane * 4);
+    if (g) {
+      const float mu = wave_sum(v.x + v.y + v.z + v.w) * (1.0f / ND_D);
+      const f32x4 d = v - mu;
+      const float var = wave_sum(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w) * (1.0f / ND_D);
+      v = d * (1.0f / sqrtf(var + ND_LN_EPS)) * ld4(g + lane * 4) + ld4(b + lane * 4);
+    }
+  }
+  st4(out + pk(row, lane * 4, ND_D), v);
+}
+
+hipError_t launch_memory_pack(const float* x, const float* ln_g, const float* ln_b, float* out, int B, int T, int T16,
+                              hipStream_t s) {
+  if (T16 & 15 || T > T16) return hipErrorInvalidValue;
+  const int rows = B * T16;
+  hipLaunchKernelGGL(memory_pack_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, x, ln_g, ln_b, out, B, T, T16);
+  return hipGetLastError();
+}
+
 }  // namespace nd
 
 namespace nd {
@@ -462,7 +650,8 @@ hipError_t init_kernel_attributes() {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
   }
-  return hipSuccess;
+  return hipFuncSetAttribute((const void*)dec_mem_attention_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             160 * 1024);
 }
 
 }  // namespace nd

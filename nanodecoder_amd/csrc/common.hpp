@@ -54,16 +54,56 @@ __device__ __forceinline__ float max16(float v) {
   return fmaxf(v, dpp_mov<ND_DPP_MIRROR>(v));
 }
 
-__device__ __forceinline__ float wave_sum(float v) {
-  v = sum16(v);
-  v += __shfl_xor(v, 16, 64);
-  return v + __shfl_xor(v, 32, 64);
+// gfx950 cross-row lane swaps (VALU, no LDS): v_permlane16_swap exchanges
+// the odd 16-lane rows of one operand with the even rows of the other,
+// v_permlane32_swap the upper half with the lower half.  Fed the same value
+// twice, the two results hold the partner lanes' values (probe:
+// tools/probe_permlane.hip).  Inline asm: hipcc 7.2's builtin reads both
+// results from the first operand's register (r[0] + r[1] becomes 2 * r[0]).
+// The s_nop covers the VALU-write -> permlane-read hazard.
+template <bool ROW32>
+__device__ __forceinline__ void lane_swap(float v, float& a, float& b) {
+  a = v;
+  b = v;
+  if constexpr (ROW32)
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+  else
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+}
+__device__ __forceinline__ float xor16_sum(float v) {
+  float a, b;
+  lane_swap<false>(v, a, b);
+  return a + b;
+}
+__device__ __forceinline__ float xor32_sum(float v) {
+  float a, b;
+  lane_swap<true>(v, a, b);
+  return a + b;
+}
+__device__ __forceinline__ float xor16_max(float v) {
+  float a, b;
+  lane_swap<false>(v, a, b);
+  return fmaxf(a, b);
+}
+__device__ __forceinline__ float xor32_max(float v) {
+  float a, b;
+  lane_swap<true>(v, a, b);
+  return fmaxf(a, b);
 }
 
-__device__ __forceinline__ float wave_max(float v) {
-  v = max16(v);
-  v = fmaxf(v, __shfl_xor(v, 16, 64));
-  return fmaxf(v, __shfl_xor(v, 32, 64));
+__device__ __forceinline__ float wave_sum(float v) { return xor32_sum(xor16_sum(sum16(v))); }
+
+__device__ __forceinline__ float wave_max(float v) { return xor32_max(xor16_max(max16(v))); }
+
+// Fragment-packed ("P16") layout of an [M, N] fp32 matrix (M, N multiples of
+// 16): 16x16 blocks in row-major block order; inside a block, 64 float4
+// entries, entry e = (m & 15) + 16 * ((n & 15) >> 2) holding columns
+// n & ~3 .. +3 of row m.  Entry e is exactly what lane e supplies to (and
+// receives from) v_mfma_f32_16x16x4_f32 under the 4-k permutation, so a
+// wave moves a whole block with one coalesced 1 KB access.  Float offset of
+// element (m, n) with n % 4 == 0:
+__device__ __forceinline__ size_t pk(int m, int n, int N) {
+  return (((size_t)(m >> 4) * (N >> 4) + (n >> 4)) * 64 + (m & 15) + 16 * ((n >> 2) & 3)) * 4;
 }
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }

@@ -60,6 +60,11 @@ struct DecLayer {
   float *ln1_g, *ln1_b, *wqkv, *bqkv, *wo, *bo, *ln2_g, *ln2_b, *cwq, *cbq, *cwo, *cbo, *fln_g, *fln_b, *w1, *b1,
       *w2, *b2;
   float *nwqkv, *nbqkv, *ncwq, *ncbq, *nw1, *nb1;
+  // P16-packed step weights (kernels.hpp launch_gemm_p16), derived at finalize
+  float *pwqkv, *pwo, *pcwq, *pcwo, *pw1, *pw2;
+  // memory-bank context attention (greedy): ctx K folded into the query
+  // projection, ctx V into the output projection (derived at finalize, f64)
+  float *pwqk, *bqk, *pwvo, *bvo;
 };
 struct NanoLayer {
   float *wih, *bih, *bhh, *whh, *bn_g, *bn_b, *bn_rm, *bn_rv;  // raw
@@ -83,6 +88,7 @@ struct nd_ctx {
   std::vector<void*> allocs;
   bool finalized = false;
   bool use_graphs = true;
+  int ctx_path = 0;  // 0: memory-bank form for greedy, K/V form for beam; 1: always K/V
   bool timing = false;
   float t_enc = 0.f, t_dec = 0.f;
 
@@ -99,6 +105,8 @@ struct nd_ctx {
   float* sig = nullptr;
   int *len = nullptr, *span = nullptr;
   float *x = nullptr, *y = nullptr, *att = nullptr, *big = nullptr, *ctxkv = nullptr;
+  float* mem_p = nullptr;                 // P16 memory bank [B * T16, 256]
+  float *dqk = nullptr, *dU = nullptr;    // [R, 8*256] P16 (memory-bank path)
   float *nano_xp = nullptr, *nano_h = nullptr;
   float *x_part = nullptr, *y_part = nullptr, *dx_part = nullptr, *dq1_part = nullptr, *dmid_part = nullptr;
   int x_pn = 1;
@@ -218,6 +226,9 @@ static int build_registry(nd_ctx* c) {
     AL(L.fln_g, D); AL(L.fln_b, D); AL(L.w1, (size_t)F * D); AL(L.b1, F); AL(L.w2, (size_t)D * F); AL(L.b2, D);
     AL(L.nwqkv, 3 * D * D); AL(L.nbqkv, 3 * D); AL(L.ncwq, D * D); AL(L.ncbq, D); AL(L.nw1, (size_t)F * D);
     AL(L.nb1, F);
+    AL(L.pwqkv, 3 * D * D); AL(L.pwo, D * D); AL(L.pcwq, D * D); AL(L.pcwo, D * D); AL(L.pw1, (size_t)F * D);
+    AL(L.pw2, (size_t)D * F);
+    AL(L.pwqk, (size_t)ND_H * D * D); AL(L.bqk, ND_H * D); AL(L.pwvo, (size_t)D * ND_H * D); AL(L.bvo, D);
     const std::string p = "decoder.transformer_layers." + std::to_string(i);
     add_slot(c, p + ".layer_norm_1.weight", L.ln1_g, {D});
     add_slot(c, p + ".layer_norm_1.bias", L.ln1_b, {D});
@@ -266,7 +277,8 @@ static int build_registry(nd_ctx* c) {
 static int alloc_workspaces(nd_ctx* c) {
   const auto& cfg = c->cfg;
   const size_t B = cfg.max_batch, T = cfg.max_src_len, S = cfg.max_steps;
-  const size_t R = B * (size_t)std::max(1, cfg.max_beam);
+  // decoder rows, padded to whole 16-row P16 blocks
+  const size_t R = (B * (size_t)std::max(1, cfg.max_beam) + 15) / 16 * 16;
   const size_t D = c->D, F = c->F, Ld = cfg.dec_layers;
   hipError_t e;
 #define WS(ptr, n)                                          \
@@ -280,6 +292,7 @@ static int alloc_workspaces(nd_ctx* c) {
   WS(c->att, B * T * D);
   WS(c->big, B * T * std::max(F, 3 * D));
   WS(c->ctxkv, B * T * Ld * 2 * D);
+  WS(c->mem_p, B * ((T + 15) / 16 * 16) * D);
   WS(c->x_part, B * T * ND_PART_LD * 2);
   WS(c->y_part, B * T * ND_PART_LD * 2);
   WS(c->dx_part, R * ND_PART_LD * 2);
@@ -296,6 +309,8 @@ static int alloc_workspaces(nd_ctx* c) {
   WS(c->datt, R * D);
   WS(c->dqkv, R * 3 * D);
   WS(c->dhid, R * F);
+  WS(c->dqk, R * ND_H * D);
+  WS(c->dU, R * ND_H * D);
   WS(c->cache, Ld * R * S * 2 * D);
   WS(c->tok, R);
   WS(c->gtok, B * S);
@@ -356,8 +371,10 @@ struct G {
   G& relu() { a.relu = true; return *this; }
   G& res(const float* R, int ldr) { a.R = R; a.ldr = ldr; return *this; }
   G& stats(float* part) { a.part_out = part; return *this; }
+  bool packed = false;
+  G& p16() { packed = true; return *this; }  // decoder-step operands in the P16 layout
   hipError_t run(hipStream_t s, int* pn_out = nullptr) {
-    hipError_t e = nd::launch_gemm(a, s);
+    hipError_t e = packed ? nd::launch_gemm_p16(a, s) : nd::launch_gemm(a, s);
     if (pn_out) *pn_out = a.part_n_out;
     return e;
   }
@@ -407,31 +424,53 @@ static hipError_t enqueue_first_embed(nd_ctx* c, int R, hipStream_t s) {
 
 // One decoder step for R = C*rpc rows: dx (embedded input, row stats in
 // dx_part) -> dx (pre final LN).
+static bool use_memory_bank(nd_ctx* c, int rpc) { return c->ctx_path == 0 && rpc * ND_H <= 16 && rpc == 1; }
+
 static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, const int* anc, int anc_ld,
                                    hipStream_t s) {
   const int R = C * rpc, D = c->D, F = c->F, S = c->cfg.max_steps;
   const int Ld = (int)c->dec.size();
+  const bool mb = use_memory_bank(c, rpc);
+  const int T16 = (T + 15) / 16 * 16;
   int pnx = 1, pnq = 0, pnm = 0;
   for (int i = 0; i < Ld; ++i) {
     DecLayer& L = c->dec[i];
     float* cache = c->cache + (size_t)i * R * S * 2 * D;
     // decoder/transformer.py:53-95
-    LCHK(G(c->dx, D, L.nwqkv, 3 * D, D, L.nbqkv, c->dqkv, 3 * D, R).ln(c->dx_part, pnx).run(s));
+    // all step activations are P16-packed (kernels.hpp)
+    LCHK(G(c->dx, D, L.pwqkv, 3 * D, D, L.nbqkv, c->dqkv, 3 * D, R).p16().ln(c->dx_part, pnx).run(s));
     LCHK(nd::launch_dec_self_attention(c->dqkv, cache, anc, anc_ld, step, S, c->datt, R, s));
-    LCHK(G(c->datt, D, L.wo, D, D, L.bo, c->dq1, D, R).res(c->dx, D).stats(c->dq1_part).run(s, &pnq));
-    LCHK(G(c->dq1, D, L.ncwq, D, D, L.ncbq, c->dcq, D, R).ln(c->dq1_part, pnq).run(s));
-    LCHK(nd::launch_dec_ctx_attention(c->dcq, c->ctxkv, Ld * 2 * D, i * 2 * D, c->sig, c->span,
-                                      (float)c->cfg.pad_idx, c->datt, C, rpc, T, s));
-    LCHK(G(c->datt, D, L.cwo, D, D, L.cbo, c->dmid, D, R).res(c->dq1, D).stats(c->dmid_part).run(s, &pnm));
-    LCHK(G(c->dmid, D, L.nw1, F, D, L.nb1, c->dhid, F, R).ln(c->dmid_part, pnm).relu().run(s));
-    LCHK(G(c->dhid, F, L.w2, D, F, L.b2, c->dx, D, R).res(c->dmid, D).stats(c->dx_part).run(s, &pnx));
+    LCHK(G(c->datt, D, L.pwo, D, D, L.bo, c->dq1, D, R).p16().res(c->dx, D).stats(c->dq1_part).run(s, &pnq));
+    if (mb) {  // memory-bank form (attention.hip)
+      const int HD = ND_H * D;
+      LCHK(G(c->dq1, D, L.pwqk, HD, D, L.bqk, c->dqk, HD, R).p16().ln(c->dq1_part, pnq).run(s));
+      LCHK(nd::launch_dec_mem_attention(c->dqk, c->mem_p, c->sig, c->span, (float)c->cfg.pad_idx, c->dU, C, rpc, T,
+                                        T16, s));
+      LCHK(G(c->dU, HD, L.pwvo, D, HD, L.bvo, c->dmid, D, R).p16().res(c->dq1, D).stats(c->dmid_part).run(s, &pnm));
+    } else {
+      LCHK(G(c->dq1, D, L.pcwq, D, D, L.ncbq, c->dcq, D, R).p16().ln(c->dq1_part, pnq).run(s));
+      LCHK(nd::launch_dec_ctx_attention(c->dcq, c->ctxkv, Ld * 2 * D, i * 2 * D, c->sig, c->span,
+                                        (float)c->cfg.pad_idx, c->datt, C, rpc, T, s));
+      LCHK(G(c->datt, D, L.pcwo, D, D, L.cbo, c->dmid, D, R).p16().res(c->dq1, D).stats(c->dmid_part).run(s, &pnm));
+    }
+    LCHK(G(c->dmid, D, L.pw1, F, D, L.nb1, c->dhid, F, R).p16().ln(c->dmid_part, pnm).relu().run(s));
+    LCHK(G(c->dhid, F, L.pw2, D, F, L.b2, c->dx, D, R).p16().res(c->dmid, D).stats(c->dx_part).run(s, &pnx));
   }
   return hipSuccess;
 }
 
+// The decoder's view of the encoder output: the memory bank (greedy) or the
+// per-layer context K/V (beam).
+static hipError_t enqueue_memory(nd_ctx* c, int B, int T, int rpc, hipStream_t s) {
+  if (!use_memory_bank(c, rpc)) return enqueue_ctxkv(c, B, T, s);
+  const bool tr = c->cfg.encoder_type == ND_ENC_TRANSFORMER;
+  return nd::launch_memory_pack(c->x, tr ? c->enc_ln_g : nullptr, tr ? c->enc_ln_b : nullptr, c->mem_p, B, T,
+                                (T + 15) / 16 * 16, s);
+}
+
 static hipError_t enqueue_greedy(nd_ctx* c, int B, int T, int S, int min_len, bool logp, hipStream_t s) {
   LCHK(enqueue_encode(c, B, T, s));
-  LCHK(enqueue_ctxkv(c, B, T, s));
+  LCHK(enqueue_memory(c, B, T, 1, s));
   LCHK(nd::launch_fill_i32(c->tok, c->cfg.bos_idx, B, s));
   LCHK(enqueue_first_embed(c, B, s));
   const nd::NextEmbed ne = next_embed(c);
@@ -564,6 +603,89 @@ int nd_load_weight(nd_ctx* c, const char* name, const float* host, const int64_t
   return ND_OK;
 }
 
+// Memory-bank form of the context attention (attention.hip): per decoder
+// layer, in f64 on the host from the reference weights,
+//   W_qk[h*256+i][k] = sum_a W_k[32h+a][i] W_q'[32h+a][k] / sqrt(32)
+//   b_qk[h*256+i]    = sum_a W_k[32h+a][i] b_q'[32h+a]     / sqrt(32)
+//   W_vo[n][h*256+i] = sum_a W_o[n][32h+a] W_v[32h+a][i]
+//   b_vo[n]          = W_o[n] . b_v + b_o[n]
+// with W_q' = W_q diag(ln2_g), b_q' = W_q ln2_b + b_q (layer_norm_2 folded).
+// q_h . b_k,h is constant over keys and drops out of the softmax exactly.
+static int derive_memory_bank_weights(nd_ctx* c) {
+  const int D = c->D, H = ND_H, DH = ND_DH, Ld = (int)c->dec.size();
+  auto down = [&](const float* d, size_t n, std::vector<float>& h) {
+    h.resize(n);
+    return hipMemcpy(h.data(), d, n * 4, hipMemcpyDeviceToHost);
+  };
+  float* scratch = nullptr;
+  HIPCHK(hipMalloc(&scratch, (size_t)H * D * D * sizeof(float)));
+  std::vector<float> Wq, bq, g2, b2, Wk, Wv, bv, Wo, bo;
+  std::vector<float> wqk((size_t)H * D * D), bqk((size_t)H * D), wvo((size_t)D * H * D), bvo(D);
+  int rc = ND_OK;
+  for (int i = 0; i < Ld && rc == ND_OK; ++i) {
+    DecLayer& L = c->dec[i];
+    hipError_t e = hipSuccess;
+    if ((e = down(L.cwq, (size_t)D * D, Wq)) != hipSuccess || (e = down(L.cbq, D, bq)) != hipSuccess ||
+        (e = down(L.ln2_g, D, g2)) != hipSuccess || (e = down(L.ln2_b, D, b2)) != hipSuccess ||
+        (e = down(c->ctxkv_w + (size_t)(2 * i) * D * D, (size_t)D * D, Wk)) != hipSuccess ||
+        (e = down(c->ctxkv_w + (size_t)(2 * i + 1) * D * D, (size_t)D * D, Wv)) != hipSuccess ||
+        (e = down(c->ctxkv_b + (size_t)(2 * i + 1) * D, D, bv)) != hipSuccess ||
+        (e = down(L.cwo, (size_t)D * D, Wo)) != hipSuccess || (e = down(L.cbo, D, bo)) != hipSuccess) {
+      rc = fail(ND_ERR_HIP, std::string("memory-bank weights: ") + hipGetErrorString(e));
+      break;
+    }
+    const double inv = 1.0 / std::sqrt((double)DH);
+    std::vector<double> wq2((size_t)D * D), bq2(D);
+    for (int a = 0; a < D; ++a) {
+      double sb = bq[a];
+      for (int k = 0; k < D; ++k) {
+        wq2[(size_t)a * D + k] = (double)Wq[(size_t)a * D + k] * g2[k];
+        sb += (double)Wq[(size_t)a * D + k] * b2[k];
+      }
+      bq2[a] = sb;
+    }
+    std::vector<double> row(D);
+    for (int h = 0; h < H; ++h)
+      for (int ii = 0; ii < D; ++ii) {
+        std::fill(row.begin(), row.end(), 0.0);
+        double sb = 0.0;
+        for (int a = 0; a < DH; ++a) {
+          const double wk = Wk[(size_t)(h * DH + a) * D + ii];
+          const double* wr = &wq2[(size_t)(h * DH + a) * D];
+          for (int k = 0; k < D; ++k) row[k] += wk * wr[k];
+          sb += wk * bq2[h * DH + a];
+        }
+        for (int k = 0; k < D; ++k) wqk[((size_t)h * D + ii) * D + k] = (float)(row[k] * inv);
+        bqk[(size_t)h * D + ii] = (float)(sb * inv);
+      }
+    for (int n = 0; n < D; ++n) {
+      double sb = bo[n];
+      for (int j = 0; j < D; ++j) sb += (double)Wo[(size_t)n * D + j] * bv[j];
+      bvo[n] = (float)sb;
+      for (int h = 0; h < H; ++h) {
+        std::fill(row.begin(), row.end(), 0.0);
+        for (int a = 0; a < DH; ++a) {
+          const double wo = Wo[(size_t)n * D + h * DH + a];
+          const float* vr = &Wv[(size_t)(h * DH + a) * D];
+          for (int ii = 0; ii < D; ++ii) row[ii] += wo * vr[ii];
+        }
+        for (int ii = 0; ii < D; ++ii) wvo[(size_t)n * H * D + h * D + ii] = (float)row[ii];
+      }
+    }
+    if ((e = hipMemcpy(scratch, wqk.data(), wqk.size() * 4, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = nd::launch_pack_p16(scratch, D, L.pwqk, H * D, D, c->es)) != hipSuccess ||
+        (e = hipStreamSynchronize(c->es)) != hipSuccess ||
+        (e = hipMemcpy(scratch, wvo.data(), wvo.size() * 4, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = nd::launch_pack_p16(scratch, H * D, L.pwvo, D, H * D, c->es)) != hipSuccess ||
+        (e = hipStreamSynchronize(c->es)) != hipSuccess ||
+        (e = hipMemcpy(L.bqk, bqk.data(), bqk.size() * 4, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(L.bvo, bvo.data(), bvo.size() * 4, hipMemcpyHostToDevice)) != hipSuccess)
+      rc = fail(ND_ERR_HIP, std::string("memory-bank weights: ") + hipGetErrorString(e));
+  }
+  (void)hipFree(scratch);
+  return rc;
+}
+
 int nd_finalize(nd_ctx* c) {
   if (!c) return fail(ND_ERR_ARG, "null ctx");
   std::string missing;
@@ -609,8 +731,18 @@ int nd_finalize(nd_ctx* c) {
       HIPCHK(fold(L.wqkv, L.bqkv, L.ln1_g, L.ln1_b, L.nwqkv, L.nbqkv, 3 * D, D));
       HIPCHK(fold(L.cwq, L.cbq, L.ln2_g, L.ln2_b, L.ncwq, L.ncbq, D, D));
       HIPCHK(fold(L.w1, L.b1, L.fln_g, L.fln_b, L.nw1, L.nb1, F, D));
+      HIPCHK(nd::launch_pack_p16(L.nwqkv, D, L.pwqkv, 3 * D, D, c->es));
+      HIPCHK(nd::launch_pack_p16(L.wo, D, L.pwo, D, D, c->es));
+      HIPCHK(nd::launch_pack_p16(L.ncwq, D, L.pcwq, D, D, c->es));
+      HIPCHK(nd::launch_pack_p16(L.cwo, D, L.pcwo, D, D, c->es));
+      HIPCHK(nd::launch_pack_p16(L.nw1, D, L.pw1, F, D, c->es));
+      HIPCHK(nd::launch_pack_p16(L.w2, F, L.pw2, D, F, c->es));
     }
     HIPCHK(hipStreamSynchronize(c->es));
+  }
+  {
+    int rc = derive_memory_bank_weights(c);
+    if (rc) return rc;
   }
   for (auto& kv : c->graphs) (void)hipGraphExecDestroy(kv.second);
   c->graphs.clear();
@@ -743,6 +875,17 @@ int nd_set_graphs(nd_ctx* c, int enable) {
   return ND_OK;
 }
 
+int nd_set_ctx_path(nd_ctx* c, int path) {
+  if (!c) return fail(ND_ERR_ARG, "null ctx");
+  if (path < 0 || path > 1) return fail(ND_ERR_ARG, "path must be 0 (auto) or 1 (K/V form)");
+  if (c->ctx_path != path) {
+    for (auto& kv : c->graphs) (void)hipGraphExecDestroy(kv.second);
+    c->graphs.clear();
+  }
+  c->ctx_path = path;
+  return ND_OK;
+}
+
 int nd_set_timing(nd_ctx* c, int enable) {
   if (!c) return fail(ND_ERR_ARG, "null ctx");
   c->timing = enable != 0;
@@ -776,6 +919,24 @@ int nd_op_gemm(const float* A, const float* W, const float* bias, const float* R
   return ND_OK;
 }
 
+int nd_op_gemm_p16(const float* A, const float* W, const float* bias, const float* R, float* C, int32_t M,
+                   int32_t N, int32_t K, const float* part_in, int32_t part_n_in, float* part_out, int32_t relu,
+                   int32_t* part_n_out, void* stream) {
+  nd::GemmArgs g;
+  g.A = A; g.W = W; g.bias = bias; g.R = R; g.C = C; g.M = M; g.N = N; g.K = K; g.relu = relu != 0;
+  g.norm = part_in != nullptr; g.part_in = part_in; g.part_n_in = part_n_in; g.part_out = part_out;
+  hipError_t e = nd::launch_gemm_p16(g, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("gemm_p16: ") + hipGetErrorString(e));
+  if (part_n_out) *part_n_out = g.part_n_out;
+  return ND_OK;
+}
+
+int nd_op_pack_p16(const float* src, float* dst, int32_t M, int32_t N, void* stream) {
+  hipError_t e = nd::launch_pack_p16(src, N, dst, M, N, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("pack_p16: ") + hipGetErrorString(e));
+  return ND_OK;
+}
+
 int nd_op_fold_layernorm(const float* W, const float* bias, const float* ln_g, const float* ln_b, float* W_out,
                          float* b_out, int32_t N, int32_t K, void* stream) {
   hipError_t e = nd::launch_fold_layernorm(W, bias, ln_g, ln_b, W_out, b_out, N, K, (hipStream_t)stream);
@@ -794,6 +955,25 @@ int nd_op_dec_self_attention(const float* qkv, float* cache, const int32_t* anc,
                              int32_t max_steps, float* out, int32_t R, void* stream) {
   hipError_t e = nd::launch_dec_self_attention(qkv, cache, anc, anc_ld, step, max_steps, out, R, (hipStream_t)stream);
   if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("dec_self_attention: ") + hipGetErrorString(e));
+  return ND_OK;
+}
+
+int nd_op_dec_mem_attention(const float* qp, const float* mem, const float* signal, const int32_t* span, float pad_val,
+                            float* out, int32_t C, int32_t rpc, int32_t T, int32_t T16, void* stream) {
+  static bool attr = false;
+  if (!attr) {
+    if (nd::init_kernel_attributes() != hipSuccess) return fail(ND_ERR_HIP, "hipFuncSetAttribute failed");
+    attr = true;
+  }
+  hipError_t e = nd::launch_dec_mem_attention(qp, mem, signal, span, pad_val, out, C, rpc, T, T16, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("dec_mem_attention: ") + hipGetErrorString(e));
+  return ND_OK;
+}
+
+int nd_op_memory_pack(const float* x, const float* ln_g, const float* ln_b, float* out, int32_t B, int32_t T,
+                      int32_t T16, void* stream) {
+  hipError_t e = nd::launch_memory_pack(x, ln_g, ln_b, out, B, T, T16, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("memory_pack: ") + hipGetErrorString(e));
   return ND_OK;
 }
 

@@ -230,125 +230,101 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
 }
 
 // ---------------------------------------------------------------------------
-// Small-M kernel (decoder steps: M = rows of the batch, 256 for greedy).
-// Workgroup = 16 rows x (NT*16) columns on v_mfma_f32_16x16x4_f32; wave (t, s)
-// owns column tile t and K slice s (K = KS*KW).  Each wave issues ALL of its
-// A/W fragment loads up front (L2 -> registers; every fragment is used by one
-// wave), runs two interleaved accumulator chains (40-cycle dependent latency
-// vs 32-cycle issue); K slices are summed through LDS.
+// Decoder-step kernel (small M: the batch's rows) on the fragment-packed
+// layout (common.hpp, pk()).  A [M,K], W [N,K], R and C [M,N] are all P16
+// packed, so every operand fragment, the residual and the output tile move
+// as ONE coalesced 1 KB wave access (row-major fragments touch 16 rows per
+// instruction and keep the address path ~3x busier).  The product runs
+// transposed, C^T = W A^T, because the 16x16x4 MFMA's D fragment of W A^T is
+// exactly a P16 entry of C (lane l: row l&15, columns 4(l>>4)..+3).
 //
-// 16x16x4 fragments: lane l supplies A[l&15][k = l>>4] and B[k = l>>4][l&15];
-// lane l holds D[(l>>4)*4 + r][l&15].  With one float4 per lane covering
-// k0 + 4*(l>>4) + {0..3}, MFMA step s sums k in {k0+s, k0+4+s, k0+8+s, k0+12+s}.
+// Workgroup = 16 rows x (NT*16) columns; wave (t, s) owns column block t and
+// K slice s (K = KS*KW).  Each wave issues all of its loads up front (fragments,
+// bias, residual, the LayerNorm row statistics) before the first MFMA; two
+// interleaved accumulator chains; K slices are summed through LDS.
+// LN: rows are normalised with statistics merged from the producer's
+// partials (part_in); gamma/beta are folded into W / bias.
 __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
 template <int NT, int KS, int KW, bool LN, bool RELU, bool RESID>
-__global__ void __launch_bounds__(NT* KS * 64) gemm_f32_small_kernel(const GemmArgs g) {
+__global__ void __launch_bounds__(NT* KS * 64) gemm_p16_kernel(const GemmArgs g) {
   constexpr int WAVES = NT * KS;
-  constexpr int NF = KW / 16;  // float4 fragments per lane per operand
-  __shared__ float red[KS > 1 ? WAVES : 1][256];
-  __shared__ float s_mu[16], s_rs[16];
+  constexpr int NF = KW / 16;  // 16-k blocks per wave
+  __shared__ f32x4 red[KS > 1 ? WAVES : 1][64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wt = wave % NT, ws = wave / NT;
-  const int n0 = blockIdx.x * (NT * 16) + wt * 16, m0 = blockIdx.y * 16;
-  const int li = lane & 15, lq = lane >> 4;
-  const int M = g.M;
-  const int row = m0 + li;
-  const bool row_ok = row < M;
-  const int kb = ws * KW + 4 * lq;
-  const float* arow = g.A + (size_t)(row_ok ? row : 0) * g.lda + kb;
-  const float* wrow = g.W + (size_t)(n0 + li) * g.ldw + kb;
+  const int nb = blockIdx.x * NT + wt, mb = blockIdx.y;
+  const int KB = g.K >> 4, NB = g.N >> 4;
+  const f32x4* __restrict__ ap = reinterpret_cast<const f32x4*>(g.A) + ((size_t)mb * KB + ws * NF) * 64 + lane;
+  const f32x4* __restrict__ wp = reinterpret_cast<const f32x4*>(g.W) + ((size_t)nb * KB + ws * NF) * 64 + lane;
   f32x4 a[NF], w[NF];
 #pragma unroll
   for (int f = 0; f < NF; ++f) {
-    a[f] = ld4(arow + 16 * f);
-    w[f] = ld4(wrow + 16 * f);
+    a[f] = ap[f * 64];
+    w[f] = wp[f * 64];
   }
-  // epilogue operands ride with the fragments: no dependent round trip
-  // after the MFMAs (rows clamped instead of branching around the loads)
-  const int col = n0 + li;
-  const float bv = g.bias ? g.bias[col] : 0.f;
-  float rv[4] = {0.f, 0.f, 0.f, 0.f};
-  if constexpr (RESID) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) rv[r] = g.R[(size_t)min(m0 + lq * 4 + r, M - 1) * g.ldr + col];
-  }
+  const size_t ct = ((size_t)mb * NB + nb) * 64 + lane;  // this lane's output entry
+  const f32x4 bv = g.bias ? ld4(g.bias + nb * 16 + 4 * (lane >> 4)) : f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 rv = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (RESID) rv = reinterpret_cast<const f32x4*>(g.R)[ct];
   float mu = 0.f, rs = 1.f;
-  if constexpr (LN) {
-    // every lane merges its own row's partial statistics (no barrier)
-    if (g.part_in) merge_stats(g.part_in + (size_t)(row_ok ? row : M - 1) * ND_PART_LD * 2, g.part_n_in, mu, rs);
-  }
+  if constexpr (LN) merge_stats(g.part_in + (size_t)(mb * 16 + (lane & 15)) * ND_PART_LD * 2, g.part_n_in, mu, rs);
   // keep every load in flight before the first MFMA waits
   __builtin_amdgcn_sched_barrier(0);
   if constexpr (LN) {
-    if (!g.part_in) {
-      constexpr int RPW = (16 + WAVES - 1) / WAVES;
-      f32x4 v[RPW];
-#pragma unroll
-      for (int i = 0; i < RPW; ++i) {
-        const int r = wave + i * WAVES;
-        v[i] = ld4(g.A + (size_t)min(m0 + min(r, 15), M - 1) * g.lda + lane * 4);
-      }
-#pragma unroll
-      for (int i = 0; i < RPW; ++i) {
-        const int r = wave + i * WAVES;
-        const float m_ = wave_sum(v[i].x + v[i].y + v[i].z + v[i].w) * (1.0f / 256.0f);
-        const f32x4 d = v[i] - m_;
-        const float var = wave_sum(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w) * (1.0f / 256.0f);
-        if (lane == 0 && r < 16) {
-          s_mu[r] = m_;
-          s_rs[r] = 1.0f / sqrtf(var + ND_LN_EPS);
-        }
-      }
-      __syncthreads();
-      mu = s_mu[li];
-      rs = s_rs[li];
-    }
 #pragma unroll
     for (int f = 0; f < NF; ++f) a[f] = (a[f] - mu) * rs;
   }
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int f = 0; f < NF; ++f) {
-    acc0 = mfma16(a[f][0], w[f][0], acc0);
-    acc1 = mfma16(a[f][1], w[f][1], acc1);
-    acc0 = mfma16(a[f][2], w[f][2], acc0);
-    acc1 = mfma16(a[f][3], w[f][3], acc1);
+    acc0 = mfma16(w[f][0], a[f][0], acc0);
+    acc1 = mfma16(w[f][1], a[f][1], acc1);
+    acc0 = mfma16(w[f][2], a[f][2], acc0);
+    acc1 = mfma16(w[f][3], a[f][3], acc1);
   }
-  f32x4 acc = acc0 + acc1;
+  f32x4 v = acc0 + acc1;
   if constexpr (KS > 1) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) red[wave][r * 64 + lane] = acc[r];
+    red[wave][lane] = v;
     __syncthreads();
     if (ws != 0) return;
+    v = red[wt][lane];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float v = 0.f;
-#pragma unroll
-      for (int s2 = 0; s2 < KS; ++s2) v += red[s2 * NT + wt][r * 64 + lane];
-      acc[r] = v;
+    for (int s2 = 1; s2 < KS; ++s2) v += red[s2 * NT + wt][lane];
+  }
+  v += bv;
+  if constexpr (RELU) v = {fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
+  if constexpr (RESID) v += rv;
+  reinterpret_cast<f32x4*>(g.C)[ct] = v;
+  if (g.part_out) {
+    // row statistics over this block's 16 columns: lanes l, l^16, l^32, l^48
+    const float m_ = xor32_sum(xor16_sum(v.x + v.y + v.z + v.w)) * (1.0f / 16.0f);
+    const f32x4 d = v - m_;
+    const float q = xor32_sum(xor16_sum(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w));
+    if (lane < 16) {
+      float* p = g.part_out + ((size_t)(mb * 16 + lane) * ND_PART_LD + nb) * 2;
+      p[0] = m_;
+      p[1] = q;
     }
   }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int orow = m0 + lq * 4 + r;
-    float v = acc[r] + bv;
-    if constexpr (RELU) v = fmaxf(v, 0.f);
-    if constexpr (RESID) v += rv[r];
-    if (orow < M) g.C[(size_t)orow * g.ldc + col] = v;
-    if (g.part_out) {
-      // row statistics over this tile's 16 columns (lanes lq*16 .. lq*16+15)
-      const float m_ = sum16(v) * (1.0f / 16.0f);
-      const float q = sum16((v - m_) * (v - m_));
-      if (li == 0 && orow < M) {
-        float* p = g.part_out + ((size_t)orow * ND_PART_LD + n0 / 16) * 2;
-        p[0] = m_;
-        p[1] = q;
-      }
-    }
-  }
+}
+
+// row-major [M, N] (leading dim ld) -> P16 packed, one thread per float4
+__global__ void __launch_bounds__(256)
+pack_p16_kernel(const float* __restrict__ src, int ld, float* __restrict__ dst, int M, int N) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (size_t)M * (N / 4)) return;
+  const int m = (int)(i / (N / 4)), n = (int)(i % (N / 4)) * 4;
+  st4(dst + pk(m, n, N), ld4(src + (size_t)m * ld + n));
+}
+
+hipError_t launch_pack_p16(const float* src, int ld, float* dst, int M, int N, hipStream_t s) {
+  if (M % 16 || N % 16 || ld < N) return hipErrorInvalidValue;
+  const size_t n4 = (size_t)M * (N / 4);
+  hipLaunchKernelGGL(pack_p16_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, src, ld, dst, M, N);
+  return hipGetLastError();
 }
 
 // LayerNorm affine folded into the following Linear (done once per weight
@@ -401,37 +377,47 @@ static hipError_t launch_cfg(GemmArgs& g, hipStream_t s) {
 }
 
 template <int NT, int KS, int KW>
-static hipError_t launch_small(GemmArgs& g, hipStream_t s) {
+static hipError_t launch_p16(GemmArgs& g, hipStream_t s) {
   if (g.N % (NT * 16) != 0 || g.K != KS * KW) return hipErrorInvalidValue;
   dim3 grid(g.N / (NT * 16), (g.M + 15) / 16), block(NT * KS * 64);
   g.part_n_out = g.N / 16;
-  ND_DISPATCH_FLAGS(gemm_f32_small_kernel, NT, KS, KW);
+  ND_DISPATCH_FLAGS(gemm_p16_kernel, NT, KS, KW);
   return hipGetLastError();
 }
 
-hipError_t launch_gemm(GemmArgs& g, hipStream_t s) {
-  if (g.M <= 0) return hipSuccess;
+static hipError_t check_args(const GemmArgs& g) {
   if (g.K % 32 != 0 || (g.norm && g.K != ND_D)) return hipErrorInvalidValue;
   if (g.part_in && (g.part_n_in < 1 || g.part_n_in > ND_PART_LD || (ND_D % g.part_n_in) != 0))
     return hipErrorInvalidValue;
   if (g.part_out && g.N != ND_D) return hipErrorInvalidValue;  // statistics of whole 256-wide rows
+  return hipSuccess;
+}
+
+hipError_t launch_gemm(GemmArgs& g, hipStream_t s) {
+  if (g.M <= 0) return hipSuccess;
+  hipError_t e = check_args(g);
+  if (e != hipSuccess) return e;
   const long t128 = (long)((g.M + 127) / 128) * (g.N / 128);
-  const long t64 = (long)((g.M + 63) / 64) * (g.N / 64);
   if (g.N % 128 == 0 && t128 >= 512) return launch_cfg<128, 128, 2, 2>(g, s);
-  if (g.N % 64 == 0 && t64 >= 256) return launch_cfg<64, 64, 2, 2>(g, s);
-  if (g.N % 16 != 0) return hipErrorInvalidValue;
-  if (g.K == 256) {
-    // LN consumers: share the row statistics across many column tiles
-    if (g.norm && g.N % 128 == 0 && (long)(g.N / 128) * ((g.M + 15) / 16) >= 128) return launch_small<8, 1, 256>(g, s);
-    if (g.norm && g.N % 64 == 0) return launch_small<4, 2, 128>(g, s);
-    return launch_small<1, 4, 64>(g, s);
-  }
-  if (g.K == 2048) return launch_small<1, 8, 256>(g, s);
-  if (g.K == 64) return launch_small<1, 1, 64>(g, s);
-  if (g.K == 128) return launch_small<1, 2, 64>(g, s);
-  if (g.K == 512) return launch_small<1, 8, 64>(g, s);
-  if (g.K == 1024) return launch_small<1, 8, 128>(g, s);
+  if (g.N % 64 != 0) return hipErrorInvalidValue;
   return launch_cfg<64, 64, 2, 2>(g, s);
+}
+
+hipError_t launch_gemm_p16(GemmArgs& g, hipStream_t s) {
+  if (g.M <= 0) return hipSuccess;
+  hipError_t e = check_args(g);
+  if (e != hipSuccess) return e;
+  if (g.N % 16 != 0 || (g.norm && !g.part_in)) return hipErrorInvalidValue;
+  if (g.K == 256) {
+    // LN consumers share the row statistics across many column blocks
+    if (g.norm && g.N % 128 == 0 && (long)(g.N / 128) * ((g.M + 15) / 16) >= 128) return launch_p16<8, 1, 256>(g, s);
+    if (g.N % 64 == 0 && (long)(g.N / 64) * ((g.M + 15) / 16) >= 128) return launch_p16<4, 2, 128>(g, s);
+    return launch_p16<1, 4, 64>(g, s);
+  }
+  if (g.K == 2048) return launch_p16<1, 8, 256>(g, s);
+  if (g.K == 1024) return launch_p16<1, 8, 128>(g, s);
+  if (g.K == 512) return launch_p16<1, 8, 64>(g, s);
+  return hipErrorInvalidValue;
 }
 
 }  // namespace nd

@@ -33,7 +33,14 @@ struct GemmArgs {
   int part_n_out = 0;  // set by launch_gemm
 };
 #define ND_PART_LD 16  // partial-stat slots per row (max column tiles of a 256-wide row)
+// row-major operands (encoder, large M): LDS-tiled MFMA kernel
 hipError_t launch_gemm(GemmArgs& g, hipStream_t s);
+// P16-packed operands (decoder steps, small M; common.hpp pk()): A, W, R, C
+// packed, lda/ldw/ldr/ldc ignored, rows padded to a multiple of 16 in every
+// buffer (part buffers included); LN requires part_in.
+hipError_t launch_gemm_p16(GemmArgs& g, hipStream_t s);
+// row-major [M, N] with leading dimension ld -> P16 (M, N multiples of 16)
+hipError_t launch_pack_p16(const float* src, int ld, float* dst, int M, int N, hipStream_t s);
 // W_out[n][k] = W[n][k] * ln_g[k];  b_out[n] = bias[n] + sum_k W[n][k] * ln_b[k]
 // (LayerNorm(x) W^T + b == xhat (W diag(g))^T + (W beta + b)); bias may be null.
 hipError_t launch_fold_layernorm(const float* W, const float* bias, const float* ln_g, const float* ln_b,
@@ -78,6 +85,15 @@ struct NextEmbed {
   float* x = nullptr;
   float* part = nullptr;
 };
+// memory-bank context attention (greedy; rpc*8 <= 16 rows per chunk):
+// qp = Q' [C*rpc, 8*256] P16 (row r = c*rpc+j, column block h = head h's
+// 256-dim query in memory space), mem = P16 memory bank with T16 rows per
+// chunk; out = U [C*rpc, 8*256] P16 (head h's softmax-weighted memory sum).
+hipError_t launch_dec_mem_attention(const float* qp, const float* mem, const float* signal, const int* span,
+                                    float pad_val, float* out, int C, int rpc, int T, int T16, hipStream_t s);
+// encoder output rows x[b*T+t] -> P16 memory bank rows b*T16+t (LN when ln_g)
+hipError_t launch_memory_pack(const float* x, const float* ln_g, const float* ln_b, float* out, int B, int T, int T16,
+                              hipStream_t s);
 // greedy head: LN_dec -> generator -> log_softmax -> argmax; writes token
 // (next input + output [R, S] at column step), score, optional logp dump,
 // and the next step's embedded input (ne).

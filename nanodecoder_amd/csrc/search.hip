@@ -9,12 +9,13 @@
 
 namespace nd {
 
-// LN + generator + log_softmax for one 256-float row held by one wave
-// (lane owns dims 4*lane..4*lane+3).  Writes logp[0..V) to `lp` (LDS or regs via lane-uniform values).
-__device__ __forceinline__ void head_row(const float* __restrict__ x, const float* __restrict__ ln_g,
+// LN + generator + log_softmax for row `row` of the P16-packed decoder
+// output x, held by one wave (lane owns dims 4*lane..4*lane+3).  Writes
+// logp[0..V) to `lp` (LDS; every lane writes the same values).
+__device__ __forceinline__ void head_row(const float* __restrict__ x, int row, const float* __restrict__ ln_g,
                                          const float* __restrict__ ln_b, const float* __restrict__ gw,
                                          const float* __restrict__ gb, int V, int lane, float* lp) {
-  f32x4 v = ld4(x + lane * 4);
+  f32x4 v = ld4(x + pk(row, lane * 4, ND_D));
   const float mu = wave_sum(v.x + v.y + v.z + v.w) * (1.0f / ND_D);
   const f32x4 d = v - mu;
   const float var = wave_sum(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w) * (1.0f / ND_D);
@@ -39,7 +40,7 @@ __device__ __forceinline__ void head_row(const float* __restrict__ x, const floa
 __device__ __forceinline__ void embed_row(const NextEmbed& ne, int tk, int step_next, int row, int lane) {
   f32x4 e = ld4(ne.emb + (size_t)tk * ND_D + lane * 4);
   if (ne.pe) e = e * 16.0f + ld4(ne.pe + (size_t)step_next * ND_D + lane * 4);  // sqrt(256) = 16
-  st4(ne.x + (size_t)row * ND_D + lane * 4, e);
+  st4(ne.x + pk(row, lane * 4, ND_D), e);
   const float mu = wave_sum(e.x + e.y + e.z + e.w) * (1.0f / ND_D);
   const f32x4 d = e - mu;
   const float q = wave_sum(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w);
@@ -59,7 +60,7 @@ greedy_head_kernel(const float* __restrict__ x, const float* __restrict__ ln_g, 
   const int r = blockIdx.x * 4 + w;
   if (r >= R) return;
   float* lp = lps[w];
-  head_row(x + (size_t)r * ND_D, ln_g, ln_b, gw, gb, V, lane, lp);
+  head_row(x, r, ln_g, ln_b, gw, gb, V, lane, lp);
   if (lane == 0 && logp_dump)
     for (int k = 0; k < V; ++k) logp_dump[((size_t)r * S + step) * V + k] = lp[k];
   // every lane runs the (tiny) argmax so the token needs no broadcast
@@ -129,7 +130,7 @@ beam_step_kernel(NextEmbed ne, const float* __restrict__ x, const float* __restr
   const int cur = step & 1, nxt = cur ^ 1;
   const int row0 = c * beam;
   for (int j = w; j < beam; j += 4) {
-    head_row(x + (size_t)(row0 + j) * ND_D, ln_g, ln_b, gw, gb, V, lane, lp[j]);
+    head_row(x, row0 + j, ln_g, ln_b, gw, gb, V, lane, lp[j]);
     if (lane == 0) {
       if (step < min_len) lp[j][eos] = -1e20f;          // :712-713
       const float cj = st.cum[row0 + j];

@@ -73,6 +73,10 @@ class Engine:
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
+    def set_ctx_path(self, path: int):
+        """0: memory-bank context attention for greedy (default), 1: per-layer K/V always."""
+        _lib.check(self._L.nd_set_ctx_path(self._h, int(path)), "nd_set_ctx_path")
+
     def set_timing(self, on: bool):
         _lib.check(self._L.nd_set_timing(self._h, int(on)), "nd_set_timing")
 
@@ -167,22 +171,90 @@ def op_enc_attention(qkv: torch.Tensor, signal: torch.Tensor, span: torch.Tensor
     return out
 
 
-def op_dec_self_attention(qkv, cache, step, anc=None, anc_ld=0):
+def pack_p16(x: torch.Tensor) -> torch.Tensor:
+    """Row-major [M, N] -> the engine's P16 layout (include/nanodec.h,
+    nd_op_gemm_p16), rows zero-padded to a multiple of 16.  Returned flat
+    with shape [M16, N] for bookkeeping (the memory order is P16)."""
+    M, N = x.shape
+    M16 = (M + 15) // 16 * 16
+    if M16 != M:
+        x = torch.cat([x, x.new_zeros(M16 - M, N)])
+    return x.reshape(M16 // 16, 16, N // 16, 4, 4).permute(0, 2, 3, 1, 4).contiguous().view(M16, N)
+
+
+def unpack_p16(p: torch.Tensor, M: Optional[int] = None) -> torch.Tensor:
+    """Inverse of pack_p16 (first M rows)."""
+    M16, N = p.shape
+    x = p.reshape(M16 // 16, N // 16, 4, 16, 4).permute(0, 3, 1, 2, 4).reshape(M16, N)
+    return x[: (M16 if M is None else M)]
+
+
+def row_partials(x: torch.Tensor) -> torch.Tensor:
+    """Per-row {mean, M2} of the 16 column tiles of a [M, 256] matrix in the
+    engine's part layout [M, 16, 2] (what a producing GEMM hands over)."""
+    t = x.view(x.shape[0], 16, 16)
+    mu = t.mean(dim=2)
+    m2 = ((t - mu[:, :, None]) ** 2).sum(dim=2)
+    return torch.stack([mu, m2], dim=2).contiguous()
+
+
+def op_gemm_p16(Ap, Wp, bias, M, N, K, Rp=None, part_in=None, relu=False, part_out=None):
+    """The decoder-step GEMM on packed operands (see pack_p16).  Returns the
+    packed C [M16, N] and the number of output row partials."""
+    Cp = torch.empty(Ap.shape[0], N, dtype=torch.float32, device=Ap.device)
+    pn = ctypes.c_int32(0)
+    pn_in = 16 if part_in is not None else 0
+    s = ctypes.c_void_p(torch.cuda.current_stream(Ap.device).cuda_stream)
+    _lib.check(_lib.lib().nd_op_gemm_p16(_ptr(Ap), _ptr(Wp), _ptr(bias), _ptr(Rp), _ptr(Cp), M, N, K, _ptr(part_in),
+                                         pn_in, _ptr(part_out), int(relu), ctypes.byref(pn), s), "nd_op_gemm_p16")
+    return Cp, pn.value
+
+
+def op_dec_self_attention(qkv, cache, step, anc=None, anc_ld=0, packed=False):
+    """qkv [R, 768] row-major (or P16-packed with packed=True); returns out
+    [R, 256] in the same convention."""
     R = qkv.shape[0]
     S = cache.shape[1]
-    out = torch.empty(R, qkv.shape[1] // 3, dtype=torch.float32, device=qkv.device)
+    qp = qkv if packed else pack_p16(qkv)
+    out = torch.empty(qp.shape[0], qkv.shape[1] // 3, dtype=torch.float32, device=qkv.device)
     s = ctypes.c_void_p(torch.cuda.current_stream(qkv.device).cuda_stream)
-    _lib.check(_lib.lib().nd_op_dec_self_attention(_ptr(qkv), _ptr(cache), _ptr(anc), anc_ld, step, S, _ptr(out), R, s),
+    _lib.check(_lib.lib().nd_op_dec_self_attention(_ptr(qp), _ptr(cache), _ptr(anc), anc_ld, step, S, _ptr(out), R, s),
                "nd_op_dec_self_attention")
+    return out if packed else unpack_p16(out, R)
+
+
+def op_dec_ctx_attention(q, kv, ld, koff, signal, span, pad_val, rpc, packed=False):
+    """q [C*rpc, 256] row-major (or P16-packed with packed=True); returns out
+    in the same convention."""
+    C, T = signal.shape
+    R = C * rpc
+    qp = q if packed else pack_p16(q)
+    out = torch.empty(qp.shape[0], qp.shape[1], dtype=torch.float32, device=q.device)
+    s = ctypes.c_void_p(torch.cuda.current_stream(q.device).cuda_stream)
+    _lib.check(_lib.lib().nd_op_dec_ctx_attention(_ptr(qp), _ptr(kv), ld, koff, _ptr(signal), _ptr(span), float(pad_val),
+                                                  _ptr(out), C, rpc, T, s), "nd_op_dec_ctx_attention")
+    return out if packed else unpack_p16(out, R)
+
+
+def op_memory_pack(x, B, T, ln_g=None, ln_b=None):
+    """Encoder output x [B*T, 256] -> P16 memory bank [B*T16, 256]."""
+    T16 = (T + 15) // 16 * 16
+    out = torch.empty(B * T16, x.shape[1], dtype=torch.float32, device=x.device)
+    s = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+    _lib.check(_lib.lib().nd_op_memory_pack(_ptr(x), _ptr(ln_g), _ptr(ln_b), _ptr(out), B, T, T16, s),
+               "nd_op_memory_pack")
     return out
 
 
-def op_dec_ctx_attention(q, kv, ld, koff, signal, span, pad_val, rpc):
+def op_dec_mem_attention(qp, mem_p, signal, span, pad_val, rpc):
+    """Memory-bank context attention on packed operands: qp [R16, 2048],
+    mem_p [C*T16, 256] (op_memory_pack); returns U [R16, 2048] packed."""
     C, T = signal.shape
-    out = torch.empty(q.shape[0], q.shape[1], dtype=torch.float32, device=q.device)
-    s = ctypes.c_void_p(torch.cuda.current_stream(q.device).cuda_stream)
-    _lib.check(_lib.lib().nd_op_dec_ctx_attention(_ptr(q), _ptr(kv), ld, koff, _ptr(signal), _ptr(span), float(pad_val),
-                                                  _ptr(out), C, rpc, T, s), "nd_op_dec_ctx_attention")
+    T16 = mem_p.shape[0] // C
+    out = torch.zeros(qp.shape[0], qp.shape[1], dtype=torch.float32, device=qp.device)
+    s = ctypes.c_void_p(torch.cuda.current_stream(qp.device).cuda_stream)
+    _lib.check(_lib.lib().nd_op_dec_mem_attention(_ptr(qp), _ptr(mem_p), _ptr(signal), _ptr(span), float(pad_val),
+                                                  _ptr(out), C, rpc, T, T16, s), "nd_op_dec_mem_attention")
     return out
 
 

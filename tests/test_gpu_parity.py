@@ -58,6 +58,53 @@ def test_gemm_vs_fp64(M, N, K, ln, relu, res):
     assert (out - ref).abs().max().item() < 2e-4
 
 
+@pytest.mark.parametrize("M,N,K,ln,relu,res,stats", [(256, 768, 256, True, False, False, False),
+                                                      (256, 256, 256, False, False, True, True),
+                                                      (256, 256, 256, True, False, False, False),
+                                                      (256, 2048, 256, True, True, False, False),
+                                                      (256, 256, 2048, False, False, True, True),
+                                                      (1280, 768, 256, True, False, False, False),
+                                                      (1280, 2048, 256, True, True, False, False),
+                                                      (40, 256, 2048, False, False, True, True)])
+def test_gemm_p16_vs_fp64(M, N, K, ln, relu, res, stats):
+    """The decoder-step GEMM on the P16 layout: LN from handed-over row
+    partials (affine folded on the device), relu, residual, and the output
+    row partials it hands to the next LayerNorm."""
+    from nanodecoder_amd.engine import op_fold_layernorm, op_gemm_p16, pack_p16, row_partials, unpack_p16
+    g = torch.Generator().manual_seed(7 * M + N + K)
+    A = torch.randn(M, K, generator=g)
+    W = torch.randn(N, K, generator=g) / K ** 0.5
+    b = torch.randn(N, generator=g)
+    R = torch.randn(M, N, generator=g)
+    lg = 1 + 0.1 * torch.randn(K, generator=g)
+    lb = 0.1 * torch.randn(K, generator=g)
+    dev = torch.device("cuda", 0)
+    Wd, bd = W.to(dev), b.to(dev)
+    part_in = None
+    if ln:
+        Wd, bd = op_fold_layernorm(Wd, bd, lg.to(dev), lb.to(dev))
+        part_in = row_partials(torch.cat([A, A.new_zeros((-M) % 16, K)]).to(dev))  # producer's hand-off
+    part_out = torch.full(((M + 15) // 16 * 16, 16, 2), float("nan"), device=dev) if stats else None
+    Cp, pn = op_gemm_p16(pack_p16(A.to(dev)), pack_p16(Wd), bd, M, N, K, pack_p16(R.to(dev)) if res else None,
+                         part_in, relu, part_out)
+    out = unpack_p16(Cp, M).cpu().double()
+    a = A.double()
+    if ln:
+        a = torch.nn.functional.layer_norm(a, (K,), lg.double(), lb.double(), 1e-6)
+    ref = a @ W.double().t() + b.double()
+    if relu:
+        ref = ref.clamp_min(0)
+    if res:
+        ref = ref + R.double()
+    assert (out - ref).abs().max().item() < 2e-4
+    if stats:
+        assert pn == N // 16
+        want = row_partials(out.float())
+        got = part_out[:M].cpu()
+        assert torch.allclose(got[:, :, 0], want[:, :, 0], atol=1e-5)
+        assert torch.allclose(got[:, :, 1], want[:, :, 1], rtol=1e-4, atol=1e-4)
+
+
 def test_enc_attention_vs_oracle():
     from nanodecoder_amd.engine import op_enc_attention
     ref = _oracle()
@@ -99,12 +146,14 @@ def test_encoder_memory_vs_golden(name):
 
 
 @pytest.mark.parametrize("name", ["transformer_greedy", "transformer_pe_short", "nano_greedy"])
-@pytest.mark.parametrize("graphs", [True, False])
-def test_greedy_vs_golden(name, graphs):
+@pytest.mark.parametrize("graphs,ctx_path", [(True, 0), (False, 0), (True, 1)])
+def test_greedy_vs_golden(name, graphs, ctx_path):
+    """ctx_path 0: memory-bank context attention, 1: per-layer K/V form."""
     z, meta = gu.load(name)
     cfg, W = gu.model_for(meta)
     g = meta["greedy"]
     eng = _engine(cfg, W, max_batch=8, max_steps=g["max_length"], graphs=graphs)
+    eng.set_ctx_path(ctx_path)
     from nanodecoder_amd.engine import pad_chunks
     chunks = gu.chunks_of(z)
     T = int(z["T"])
@@ -196,3 +245,28 @@ def test_nano_greedy_vs_oracle_ragged():
     n_tie = _compare_tokens(r["tokens"].cpu().numpy(), o["tokens"], o["logp"])
     assert n_tie == 0
     assert gu.logp_close(r["logp"].cpu().numpy(), o["logp"], atol=LOGP_ATOL).all()
+
+
+def test_memory_bank_path_matches_kv_path_ragged_spans():
+    """Greedy with cross-read packing (per-chunk spans < T, T not a multiple
+    of 16): the memory-bank context attention and the per-layer K/V form give
+    the same log-probs (fp32 rounding) and tokens."""
+    cfg = synth.ModelConfig()
+    W = synth.make_weights(cfg, seed=5, eos_bias=-3.0)
+    B, T = 24, 200
+    rng = np.random.default_rng(17)
+    sig = synth.synth_chunk_batch(B, T, seed=21)
+    spans = rng.integers(1, T + 1, B).astype(np.int32)
+    spans[0], spans[1] = T, 1
+    lens = np.minimum(spans, rng.integers(1, T + 1, B)).astype(np.int32)
+    for i in range(B):
+        sig[i, lens[i]:] = 0.0
+    eng = _engine(cfg, W, max_batch=B, max_src_len=T, max_steps=40)
+    out = []
+    for path in (0, 1):
+        eng.set_ctx_path(path)
+        r = eng.translate_greedy(sig, lens, spans, max_len=40, return_logp=True)
+        out.append((r["tokens"].cpu().numpy(), r["logp"].cpu().numpy()))
+    assert (out[0][0] == out[1][0]).all()
+    # generator biases put some log-probs near -1e4, where one fp32 ulp is 1e-3
+    assert np.allclose(out[0][1], out[1][1], rtol=2e-6, atol=1e-4)

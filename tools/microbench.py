@@ -57,21 +57,41 @@ def gemm_case(M, N, K, ln, relu, res):
 
 
 if ONLY == "dec256":
-    for args in ((256, 768, 256, True, False, False), (256, 256, 256, False, False, True),
-                 (256, 2048, 256, True, True, False), (256, 256, 2048, False, False, True)):
-        gemm_case(*args)
-    qkv = torch.randn(256, 768, device=dev)
+    # decoder-step shapes on the engine's P16 layout (greedy R=256, beam R=1280)
+    for M in (256, 1280):
+        for N, K, ln, relu, res in ((768, 256, True, False, False), (256, 256, False, False, True),
+                                    (256, 256, True, False, False), (2048, 256, True, True, False),
+                                    (256, 2048, False, False, True)):
+            Ap = E.pack_p16(torch.randn(M, K, device=dev))
+            Wp = E.pack_p16(torch.randn(N, K, device=dev) / K ** 0.5)
+            b = torch.randn(N, device=dev)
+            Rp = E.pack_p16(torch.randn(M, N, device=dev)) if res else None
+            part = E.row_partials(torch.randn(M, K, device=dev)) if ln else None
+            pout = torch.empty(M, 16, 2, device=dev) if N == 256 else None
+            us = timeit(lambda: E.op_gemm_p16(Ap, Wp, b, M, N, K, Rp, part, relu, pout))
+            tf = 2 * M * N * K / (us * 1e-6) / 1e12
+            print(f"gemm_p16 M={M:5d} N={N:5d} K={K:5d} ln={int(ln)} relu={int(relu)} res={int(res)}: "
+                  f"{us:8.2f} us  {tf:6.1f} TF/s")
+    qkv = E.pack_p16(torch.randn(256, 768, device=dev))
     cache = torch.randn(256, 100, 512, device=dev)
-    us = timeit(lambda: E.op_dec_self_attention(qkv, cache, 60))
+    us = timeit(lambda: E.op_dec_self_attention(qkv, cache, 60, packed=True))
     print(f"self-attn R=256 step=60: {us:8.2f} us")
     for C, rpc in ((256, 1), (256, 5)):
         T = 512
-        q = torch.randn(C * rpc, 256, device=dev)
+        q = E.pack_p16(torch.randn(C * rpc, 256, device=dev))
         kv = torch.randn(C * T, 1536, device=dev)
         sig = torch.randn(C, T, device=dev)
         span = torch.full((C,), T, dtype=torch.int32, device=dev)
-        us = timeit(lambda: E.op_dec_ctx_attention(q, kv, 1536, 0, sig, span, 1.0, rpc))
+        us = timeit(lambda: E.op_dec_ctx_attention(q, kv, 1536, 0, sig, span, 1.0, rpc, packed=True))
         print(f"ctx-attn C={C} rpc={rpc}: {us:8.2f} us  {C * T * 512 * 4 / (us * 1e-6) / 1e9:7.1f} GB/s (K+V bytes)")
+    C, T = 256, 512
+    qp = E.pack_p16(torch.randn(C, 2048, device=dev))
+    memp = E.op_memory_pack(torch.randn(C * T, 256, device=dev), C, T)
+    sig = torch.randn(C, T, device=dev)
+    span = torch.full((C,), T, dtype=torch.int32, device=dev)
+    us = timeit(lambda: E.op_dec_mem_attention(qp, memp, sig, span, 1.0, 1))
+    print(f"mem-attn C={C} rpc=1: {us:8.2f} us  {C * T * 256 * 4 / (us * 1e-6) / 1e9:7.1f} GB/s (bank bytes)  "
+          f"{2 * 2 * 16 * C * T * 256 / (us * 1e-6) / 1e12:6.1f} TF/s (16-row tiles)")
     sys.exit(0)
 for M in (256, 1280, 5120):
     gemm_case(M, 768, 256, True, False, False)
