@@ -102,31 +102,58 @@ def _pmc_traffic(name):
 
 
 def kernel_roofline(eng, B, mode, beam):
-    """Dominant kernel of the translate step: the decoder context attention
-    (HBM-bound: every step streams each chunk's context K and V).  Timed
-    standalone through the C-ABI op entry point on the current torch stream
-    with HIP events, on the engine's shapes, cycling the three layers' K/V
-    column offsets as the decode loop does.  Algorithmic bytes per launch =
-    K+V (2 x 512 keys x 256 f32 per chunk) + q, signal and output rows."""
-    from nanodecoder_amd.engine import op_dec_ctx_attention, op_fold_layernorm, op_gemm, pack_p16
+    """Dominant kernel of the translate step, timed standalone through the
+    C-ABI op entry point on the current torch stream with HIP events, on the
+    engine's shapes.
+
+    greedy: the memory-bank context attention (dec_mem_attention_kernel),
+      MFMA-issue-bound.  Algorithmic FLOPs per launch = 2 products (scores,
+      weighted sum) x 2 x 8 query rows (heads) x 512 keys x 256 dims per
+      chunk; the MFMA tiles carry 16 rows (8 padding), reported as
+      "tile_tflops".  Its HBM view (the 512 x 1 KB memory bank per chunk) is
+      reported too.
+    beam: the per-layer K/V context attention (dec_ctx_attention_kernel),
+      HBM-bound: K+V 2 x 512 keys x 256 f32 per chunk + q, signal, out."""
+    from nanodecoder_amd.engine import (op_dec_ctx_attention, op_dec_mem_attention, op_fold_layernorm, op_gemm,
+                                        op_memory_pack, pack_p16)
     dev = eng.device
-    rpc = 1 if mode == "greedy" else beam
     T, D = 512, 256
-    kv = torch.randn(B * T, 3 * 2 * D, device=dev)
-    q = pack_p16(torch.randn(B * rpc, D, device=dev))  # decoder activations live P16-packed
     sig = torch.randn(B, T, device=dev)
     span = torch.full((B,), T, dtype=torch.int32, device=dev)
-    fn = lambda i: op_dec_ctx_attention(q, kv, 3 * 2 * D, (i % 3) * 2 * D, sig, span, 1.0, rpc,  # noqa: E731
-                                        packed=True)
-    for i in range(6):
-        fn(i)
-    ms = _time(fn, 30)
-    nbytes = B * T * 2 * D * 4 + B * T * 4 + 2 * B * rpc * D * 4
-    ach = nbytes / (ms * 1e-3) / 1e9
-    out = {"bound": "hbm", "kernel": f"dec_ctx_attention_kernel<{rpc}>", "achieved": round(ach, 1), "peak": 8000.0,
-           "unit": "GB/s", "frac": round(ach / 8000.0, 4), "traffic": _pmc_traffic(f"dec_ctx_attention_kernel<{rpc}>"),
-           "algorithmic_bytes_per_launch": nbytes, "avg_launch_ms": round(ms, 5)}
-    # secondary: the dominant MFMA kernel (encoder FFN1 GEMM, LN prologue + bias + ReLU)
+    if mode == "greedy":
+        qp = pack_p16(torch.randn(B, 8 * D, device=dev))
+        memp = op_memory_pack(torch.randn(B * T, D, device=dev), B, T)
+        outp = torch.empty_like(qp)
+        fn = lambda i: op_dec_mem_attention(qp, memp, sig, span, 1.0, 1, out=outp)  # noqa: E731
+        for i in range(6):
+            fn(i)
+        ms = _time(fn, 30)
+        flops = 2 * 2 * 8 * T * D * B
+        ach = flops / (ms * 1e-3) / 1e12
+        nbytes = B * T * D * 4 + B * T * 4 + 2 * B * 8 * D * 4
+        name = "dec_mem_attention_kernel<8, 0>"
+        out = {"bound": "mfma", "kernel": name, "achieved": round(ach, 2), "peak": 157.3, "unit": "TFLOP/s",
+               "frac": round(ach / 157.3, 4), "traffic": _pmc_traffic(name),
+               "algorithmic_flops_per_launch": flops, "avg_launch_ms": round(ms, 5),
+               "tile_tflops": round(2 * ach, 2),
+               "hbm_view": {"algorithmic_bytes_per_launch": nbytes,
+                            "achieved_gbs": round(nbytes / (ms * 1e-3) / 1e9, 1), "peak_gbs": 8000.0}}
+    else:
+        rpc = beam
+        kv = torch.randn(B * T, 3 * 2 * D, device=dev)
+        q = pack_p16(torch.randn(B * rpc, D, device=dev))  # decoder activations live P16-packed
+        fn = lambda i: op_dec_ctx_attention(q, kv, 3 * 2 * D, (i % 3) * 2 * D, sig, span, 1.0, rpc,  # noqa: E731
+                                            packed=True)
+        for i in range(6):
+            fn(i)
+        ms = _time(fn, 30)
+        nbytes = B * T * 2 * D * 4 + B * T * 4 + 2 * B * rpc * D * 4
+        ach = nbytes / (ms * 1e-3) / 1e9
+        out = {"bound": "hbm", "kernel": f"dec_ctx_attention_kernel<{rpc}>", "achieved": round(ach, 1),
+               "peak": 8000.0, "unit": "GB/s", "frac": round(ach / 8000.0, 4),
+               "traffic": _pmc_traffic(f"dec_ctx_attention_kernel<{rpc}>"),
+               "algorithmic_bytes_per_launch": nbytes, "avg_launch_ms": round(ms, 5)}
+    # secondary: the dominant encoder MFMA kernel (FFN1 GEMM, LN prologue + bias + ReLU)
     M, K, N = B * T, 256, 2048
     A = torch.randn(M, K, device=dev)
     Wt = torch.randn(N, K, device=dev) / 16

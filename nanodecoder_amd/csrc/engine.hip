@@ -919,9 +919,15 @@ int nd_op_gemm(const float* A, const float* W, const float* bias, const float* R
   return ND_OK;
 }
 
+static int ensure_attributes() {
+  static hipError_t e = nd::init_kernel_attributes();
+  return e == hipSuccess ? ND_OK : fail(ND_ERR_HIP, "hipFuncSetAttribute failed");
+}
+
 int nd_op_gemm_p16(const float* A, const float* W, const float* bias, const float* R, float* C, int32_t M,
                    int32_t N, int32_t K, const float* part_in, int32_t part_n_in, float* part_out, int32_t relu,
                    int32_t* part_n_out, void* stream) {
+  if (int rc = ensure_attributes()) return rc;
   nd::GemmArgs g;
   g.A = A; g.W = W; g.bias = bias; g.R = R; g.C = C; g.M = M; g.N = N; g.K = K; g.relu = relu != 0;
   g.norm = part_in != nullptr; g.part_in = part_in; g.part_n_in = part_n_in; g.part_out = part_out;
@@ -960,11 +966,7 @@ int nd_op_dec_self_attention(const float* qkv, float* cache, const int32_t* anc,
 
 int nd_op_dec_mem_attention(const float* qp, const float* mem, const float* signal, const int32_t* span, float pad_val,
                             float* out, int32_t C, int32_t rpc, int32_t T, int32_t T16, void* stream) {
-  static bool attr = false;
-  if (!attr) {
-    if (nd::init_kernel_attributes() != hipSuccess) return fail(ND_ERR_HIP, "hipFuncSetAttribute failed");
-    attr = true;
-  }
+  if (int rc = ensure_attributes()) return rc;
   hipError_t e = nd::launch_dec_mem_attention(qp, mem, signal, span, pad_val, out, C, rpc, T, T16, (hipStream_t)stream);
   if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("dec_mem_attention: ") + hipGetErrorString(e));
   return ND_OK;
@@ -980,11 +982,7 @@ int nd_op_memory_pack(const float* x, const float* ln_g, const float* ln_b, floa
 int nd_op_dec_ctx_attention(const float* q, const float* kv, int32_t ld, int32_t koff, const float* signal,
                             const int32_t* span, float pad_val, float* out, int32_t C, int32_t rpc, int32_t T,
                             void* stream) {
-  static bool attr = false;
-  if (!attr) {
-    if (nd::init_kernel_attributes() != hipSuccess) return fail(ND_ERR_HIP, "hipFuncSetAttribute failed");
-    attr = true;
-  }
+  if (int rc = ensure_attributes()) return rc;
   hipError_t e = nd::launch_dec_ctx_attention(q, kv, ld, koff, signal, span, pad_val, out, C, rpc, T,
                                               (hipStream_t)stream);
   if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("dec_ctx_attention: ") + hipGetErrorString(e));

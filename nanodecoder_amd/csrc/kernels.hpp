@@ -39,6 +39,8 @@ hipError_t launch_gemm(GemmArgs& g, hipStream_t s);
 // packed, lda/ldw/ldr/ldc ignored, rows padded to a multiple of 16 in every
 // buffer (part buffers included); LN requires part_in.
 hipError_t launch_gemm_p16(GemmArgs& g, hipStream_t s);
+// raises the dynamic-LDS limit of the LDS-staged GEMM kernels (once per process)
+hipError_t init_gemm_attributes();
 // row-major [M, N] with leading dimension ld -> P16 (M, N multiples of 16)
 hipError_t launch_pack_p16(const float* src, int ld, float* dst, int M, int N, hipStream_t s);
 // W_out[n][k] = W[n][k] * ln_g[k];  b_out[n] = bias[n] + sum_k W[n][k] * ln_b[k]

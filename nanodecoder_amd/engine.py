@@ -246,12 +246,14 @@ def op_memory_pack(x, B, T, ln_g=None, ln_b=None):
     return out
 
 
-def op_dec_mem_attention(qp, mem_p, signal, span, pad_val, rpc):
+def op_dec_mem_attention(qp, mem_p, signal, span, pad_val, rpc, out=None):
     """Memory-bank context attention on packed operands: qp [R16, 2048],
-    mem_p [C*T16, 256] (op_memory_pack); returns U [R16, 2048] packed."""
+    mem_p [C*T16, 256] (op_memory_pack); returns U [R16, 2048] packed (rows of
+    chunks c < C written)."""
     C, T = signal.shape
     T16 = mem_p.shape[0] // C
-    out = torch.zeros(qp.shape[0], qp.shape[1], dtype=torch.float32, device=qp.device)
+    if out is None:
+        out = torch.empty(qp.shape[0], qp.shape[1], dtype=torch.float32, device=qp.device)
     s = ctypes.c_void_p(torch.cuda.current_stream(qp.device).cuda_stream)
     _lib.check(_lib.lib().nd_op_dec_mem_attention(_ptr(qp), _ptr(mem_p), _ptr(signal), _ptr(span), float(pad_val),
                                                   _ptr(out), C, rpc, T, T16, s), "nd_op_dec_mem_attention")

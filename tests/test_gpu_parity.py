@@ -65,6 +65,10 @@ def test_gemm_vs_fp64(M, N, K, ln, relu, res):
                                                       (256, 256, 2048, False, False, True, True),
                                                       (1280, 768, 256, True, False, False, False),
                                                       (1280, 2048, 256, True, True, False, False),
+                                                      (1280, 256, 256, False, False, True, True),
+                                                      (1280, 256, 256, True, False, True, True),
+                                                      (112, 2048, 256, True, True, False, False),
+                                                      (200, 768, 256, True, False, False, False),
                                                       (40, 256, 2048, False, False, True, True)])
 def test_gemm_p16_vs_fp64(M, N, K, ln, relu, res, stats):
     """The decoder-step GEMM on the P16 layout: LN from handed-over row

@@ -56,6 +56,17 @@ def gemm_case(M, N, K, ln, relu, res):
     print(f"gemm M={M:6d} N={N:5d} K={K:5d} ln={int(ln)} relu={int(relu)} res={int(res)}: {us:9.2f} us  {tf:6.1f} TF/s")
 
 
+if ONLY == "mem":
+    # memory-bank attention: scaling in the chunk count and the key count
+    for C, T in ((64, 512), (128, 512), (256, 512), (512, 512), (256, 256), (256, 128)):
+        qp = E.pack_p16(torch.randn(C, 2048, device=dev))
+        memp = E.op_memory_pack(torch.randn(C * T, 256, device=dev), C, T)
+        sig = torch.randn(C, T, device=dev)
+        span = torch.full((C,), T, dtype=torch.int32, device=dev)
+        us = timeit(lambda: E.op_dec_mem_attention(qp, memp, sig, span, 1.0, 1))
+        print(f"mem-attn C={C:4d} T={T}: {us:8.2f} us  {C * T * 256 * 4 / (us * 1e-6) / 1e9:7.1f} GB/s  "
+              f"{2 * 2 * 16 * C * T * 256 / (us * 1e-6) / 1e12:6.1f} TF/s (16-row tiles)")
+    sys.exit(0)
 if ONLY == "dec256":
     # decoder-step shapes on the engine's P16 layout (greedy R=256, beam R=1280)
     for M in (256, 1280):
