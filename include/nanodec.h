@@ -174,20 +174,21 @@ int nd_op_dec_self_attention(const float* qkv, float* cache, const int32_t* anc,
                              int32_t max_steps, float* out, int32_t R, void* stream);
 
 /* Memory-bank context attention (greedy form, engine.hip
- * derive_memory_bank_weights): rows r = c*rpc+j (rpc*8 <= 16) of
- * qp = Q' [C*rpc, 8*256] (P16; column block h = head h's query mapped into
- * memory space) attend over the P16 memory bank mem (T16 rows per chunk,
- * T16 a multiple of 16 >= T) with keys t < span[c] and key mask
- * signal[c*T+t] == pad_val; out = U [C*rpc, 8*256] P16 (head h: the
+ * derive_memory_bank_weights; replaces the context MultiHeadedAttention of
+ * decoder/transformer.py:88-92 for one row per chunk, rpc == 1): row c of
+ * qp = Q' [C, 8*256] (P16; column block h = head h's query mapped into
+ * memory space) attends over the row-major memory bank mem (chunk c's
+ * position t at row c*ldT + t, T <= ldT) with keys t < span[c] and key mask
+ * signal[c*T+t] == pad_val; out = U [C, 8*256] P16 (head h: the
  * softmax-weighted sum of memory rows). */
 int nd_op_dec_mem_attention(const float* qp, const float* mem, const float* signal, const int32_t* span, float pad_val,
-                            float* out, int32_t C, int32_t rpc, int32_t T, int32_t T16, void* stream);
+                            float* out, int32_t C, int32_t rpc, int32_t T, int32_t ldT, void* stream);
 
-/* Encoder output x [B*T, 256] row-major -> P16 memory bank with T16 rows per
- * chunk (LayerNorm with ln_g/ln_b when ln_g != NULL, encoder/transformer.py:
- * 126; rows t >= T zero). */
+/* Encoder output x [B*T, 256] row-major -> memory bank, row-major with ldT
+ * rows per chunk (LayerNorm with ln_g/ln_b when ln_g != NULL,
+ * encoder/transformer.py:125; rows t >= T zero). */
 int nd_op_memory_pack(const float* x, const float* ln_g, const float* ln_b, float* out, int32_t B, int32_t T,
-                      int32_t T16, void* stream);
+                      int32_t ldT, void* stream);
 
 /* Decoder context attention (multi_headed_attn.py:142-177): rows r = c*rpc+j
  * of q [C*rpc, d] attend over K at kv[(c*T+t)*ld + koff] and V at +d, keys

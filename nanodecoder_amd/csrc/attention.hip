@@ -443,224 +443,6 @@ hipError_t launch_dec_ctx_attention(const float* q, const float* kv, int ld, int
   return hipGetLastError();
 }
 
-// ---------------------------------------------------------------------------
-// Memory-bank form of the context attention (greedy decoding).
-//
-// With the decoder's ctx K/V projections folded into the query and output
-// sides (engine finalize: W_qk[h] = W_k,h^T W_q,h / sqrt(d_h),
-// W_vo[:, h] = W_o,h W_v,h), head h of row r needs only the encoder memory
-// bank m_t (256 floats per source position, shared by all three decoder
-// layers) instead of a per-layer K and V:
-//   s_h(t) = q'_h . m_t        (q'_h = W_qk[h] LN(x) + b_qk[h]; the dropped
-//                               q_h . b_k,h is constant in t: softmax-exact)
-//   U_h    = sum_t softmax_t(s_h)(t) m_t,   out = W_vo U + b_vo
-// which halves the bytes the decode loop streams per step and lets the bank
-// (128 MB at 256 chunks x 512 positions) stay in the MALL across layers.
-//
-// One workgroup (8 waves) per chunk; the chunk's 8 (head) query rows form
-// one 16-row MFMA tile (rows 8..15 zero).  Per 16-key tile a wave computes
-// S^T = M Q'^T (A = the P16 memory tile, coalesced), runs the online
-// softmax on its row (lane l: row l&15, keys 4(l>>4)..+3), transposes the
-// memory tile through its private LDS slab, and accumulates
-// U^T += M^T P^T, whose fragments are P16 entries of U (lane l: row l&15,
-// dims 4(l>>4)..+3 of each 16-dim tile).  The 8 waves' states merge through
-// LDS.  Mask: src == pad -> -1e18 (multi_headed_attn.py:172), t >= span:
-// absent.
-#define MEM_NW 8
-__device__ __forceinline__ f32x4 mfma16x4(float a, float b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
-
-// NW = 8 waves per chunk, a 16 KB transposition slab each; the partial
-// states merge in two halves of 8 dim tiles through the same slabs.
-template <int NW, int EXPT = 0>
-__global__ void __launch_bounds__(NW * 64)
-dec_mem_attention_kernel(const float* __restrict__ qp, const float* __restrict__ mem, const float* __restrict__ signal,
-                         const int* __restrict__ span, float pad_val, float* __restrict__ out, int rpc, int T,
-                         int T16) {
-  extern __shared__ f32x4 lds4[];
-  f32x4* Qs = lds4;                                      // [16 dim blocks][64 lanes] Q' B-fragments
-  float* Mt = reinterpret_cast<float*>(lds4 + 16 * 64);  // [NW][256 dims][16 keys] swizzled; merge: [NW][8][64][4]
-  float* ms = Mt + NW * 256 * 16;                        // [NW][16 rows]
-  float* ls = ms + NW * 16;
-  const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int L = min(span[c], T);
-  const int rows = rpc * ND_H;  // <= 16
-  const int ri = lane & 15, lq = lane >> 4;
-  const int nkt = (L + 15) >> 4;
-  const f32x4* mbase = reinterpret_cast<const f32x4*>(mem) + (size_t)c * (T16 >> 4) * 16 * 64 + lane;
-  const float* sgc = signal + (size_t)c * T;
-  // the wave's first memory tile is in flight while the query image is staged
-  f32x4 a[16];
-  float sg[4];
-  auto load_tile = [&](int kt) {
-    const f32x4* mp = mbase + (size_t)kt * 16 * 64;  // P16 row block kt of the chunk: 16 col blocks
-#pragma unroll
-    for (int f = 0; f < 16; ++f) a[f] = (EXPT & 4) ? mbase[f * 64] : mp[f * 64];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) sg[r] = sgc[min(kt * 16 + 4 * lq + r, L - 1)];
-  };
-  if (wave < nkt) load_tile(wave);
-  for (int e = tid; e < 16 * 64; e += NW * 64) {
-    const int f = e >> 6, l = e & 63, rho = l & 15;
-    f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (rho < rows) v = ld4(qp + pk(c * rpc + rho / ND_H, (rho % ND_H) * ND_D + 16 * f + 4 * (l >> 4), ND_H * ND_D));
-    Qs[e] = v;
-  }
-  __syncthreads();
-  float mrun = -INFINITY, lrun = 0.f;
-  f32x4 u[16];
-#pragma unroll
-  for (int d = 0; d < 16; ++d) u[d] = {0.f, 0.f, 0.f, 0.f};
-  float* mt = Mt + wave * 256 * 16;
-  for (int kt = wave; kt < nkt; kt += NW) {
-    const int t0 = kt * 16;
-    // S^T = M Q'^T: lane l, reg r = S[row l&15][key t0 + 4(l>>4) + r]
-    f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int f = 0; f < 16 && !(EXPT & 2); ++f) {
-      const f32x4 q = Qs[f * 64 + lane];
-      s0 = mfma16x4(a[f][0], q[0], s0);
-      s1 = mfma16x4(a[f][1], q[1], s1);
-      s0 = mfma16x4(a[f][2], q[2], s0);
-      s1 = mfma16x4(a[f][3], q[3], s1);
-    }
-    const f32x4 sv = s0 + s1;
-    float sc[4], mx = -INFINITY;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int t = t0 + 4 * lq + r;
-      sc[r] = t < L ? (sg[r] == pad_val ? ND_MASK_FILL : sv[r]) : -INFINITY;
-      mx = fmaxf(mx, sc[r]);
-    }
-    mx = xor32_max(xor16_max(mx));  // over the tile's 16 keys
-    const float mnew = fmaxf(mrun, mx);  // finite: key t0 < L exists
-    const float scale = __expf(mrun - mnew);
-    float p[4], psum = 0.f;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      p[r] = __expf(sc[r] - mnew);
-      psum += p[r];
-    }
-    lrun = lrun * scale + xor32_sum(xor16_sum(psum));
-    mrun = mnew;
-    if (!(EXPT & 1)) {
-      // memory tile -> LDS transposed: mt[dim][key ^ 4((dim>>2)&3)] (b128 reads conflict-free)
-#pragma unroll
-      for (int f = 0; f < 16; ++f)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) mt[(16 * f + 4 * lq + i) * 16 + (ri ^ (4 * lq))] = a[f][i];
-    }
-    // the next tile's loads overlap this tile's P.V MFMAs
-    if (kt + NW < nkt) load_tile(kt + NW);
-    if (!(EXPT & 1)) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      // U^T += M^T P^T: A = mt[16d + (l&15)][keys 4(l>>4)..+3], B = p (lane's own keys)
-#pragma unroll
-      for (int d = 0; d < 16; ++d) {
-        const f32x4 mv = ld4(mt + (16 * d + ri) * 16 + ((4 * lq) ^ (4 * ((ri >> 2) & 3))));
-        f32x4 acc = u[d] * scale;
-        acc = mfma16x4(mv[0], p[0], acc);
-        acc = mfma16x4(mv[1], p[1], acc);
-        acc = mfma16x4(mv[2], p[2], acc);
-        acc = mfma16x4(mv[3], p[3], acc);
-        u[d] = acc;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // reads done before the slab is rewritten
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-  }
-  // merge the waves' partial states in two halves of 8 dim tiles (slabs reused)
-  if (lq == 0) {
-    ms[wave * 16 + ri] = mrun;
-    ls[wave * 16 + ri] = lrun;
-  }
-  __syncthreads();
-  float M = -INFINITY;
-#pragma unroll
-  for (int w = 0; w < NW; ++w) M = fmaxf(M, ms[w * 16 + ri]);
-  float fw[NW], den = 0.f;
-#pragma unroll
-  for (int w = 0; w < NW; ++w) {
-    const float mw = ms[w * 16 + ri];
-    fw[w] = mw == -INFINITY ? 0.f : __expf(mw - M);  // waves that owned no key
-    den += fw[w] * ls[w * 16 + ri];
-  }
-  const float inv = den > 0.f ? 1.0f / den : 0.f;
-  float* red = Mt;  // [NW][8 d][64 lanes][4]
-#pragma unroll
-  for (int hf = 0; hf < 2; ++hf) {
-#pragma unroll
-    for (int d = 0; d < 8; ++d) st4(red + ((size_t)(wave * 8 + d) * 64 + lane) * 4, u[8 * hf + d]);
-    __syncthreads();
-    for (int d = wave; d < 8; d += NW) {
-      f32x4 num = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int w = 0; w < NW; ++w) num += fw[w] * ld4(red + ((size_t)(w * 8 + d) * 64 + lane) * 4);
-      if (ri < rows)
-        st4(out + pk(c * rpc + ri / ND_H, (ri % ND_H) * ND_D + 16 * (8 * hf + d) + 4 * lq, ND_H * ND_D), num * inv);
-    }
-    __syncthreads();
-  }
-}
-
-template <int NW>
-static size_t mem_lds_bytes() {
-  return (16 * 64) * sizeof(f32x4) + (size_t)NW * (256 * 16 + 32) * sizeof(float);
-}
-
-hipError_t launch_dec_mem_attention(const float* qp, const float* mem, const float* signal, const int* span,
-                                    float pad_val, float* out, int C, int rpc, int T, int T16, hipStream_t s) {
-  if (rpc < 1 || rpc * ND_H > 16 || T < 1 || T > T16 || (T16 & 15)) return hipErrorInvalidValue;
-  static const int expt = [] {
-    const char* e = getenv("ND_MEM_EXPT");  // timing experiments only (wrong results): 1 no U, 2 no S, 4 no loads
-    return e ? atoi(e) : 0;
-  }();
-  if (expt) {
-#define ND_MEM_X(X)                                                                                              \
-  if (expt == X)                                                                                                 \
-    hipLaunchKernelGGL((dec_mem_attention_kernel<8, X>), dim3(C), dim3(8 * 64), mem_lds_bytes<8>(), s, qp, mem, \
-                       signal, span, pad_val, out, rpc, T, T16);
-    ND_MEM_X(1) ND_MEM_X(2) ND_MEM_X(3) ND_MEM_X(4)
-#undef ND_MEM_X
-    return hipGetLastError();
-  }
-  hipLaunchKernelGGL((dec_mem_attention_kernel<MEM_NW, 0>), dim3(C), dim3(MEM_NW * 64), mem_lds_bytes<MEM_NW>(), s, qp,
-                     mem, signal, span, pad_val, out, rpc, T, T16);
-  return hipGetLastError();
-}
-
-// Encoder output -> the decoder's memory bank, P16-packed with T16 rows per
-// chunk: row b*T16 + t = LN(x[b*T + t]) (transformer: encoder.layer_norm,
-// encoder/transformer.py:126) or x itself (NanoEncoder); rows t >= T zero.
-__global__ void __launch_bounds__(256)
-memory_pack_kernel(const float* __restrict__ x, const float* __restrict__ g, const float* __restrict__ b,
-                   float* __restrict__ out, int B, int T, int T16) {
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (row >= B * T16) return;
-  const int bb = row / T16, t = row - bb * T16;
-  f32x4 v = {0.f, 0.f, 0.f, 0.f};
-  if (t < T) {
-    v = ld4(x + ((size_t)bb * T + t) * ND_D + lane * 4);
-    if (g) {
-      const float mu = wave_sum(v.x + v.y + v.z + v.w) * (1.0f / ND_D);
-      const f32x4 d = v - mu;
-      const float var = wave_sum(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w) * (1.0f / ND_D);
-      v = d * (1.0f / sqrtf(var + ND_LN_EPS)) * ld4(g + lane * 4) + ld4(b + lane * 4);
-    }
-  }
-  st4(out + pk(row, lane * 4, ND_D), v);
-}
-
-hipError_t launch_memory_pack(const float* x, const float* ln_g, const float* ln_b, float* out, int B, int T, int T16,
-                              hipStream_t s) {
-  if (T16 & 15 || T > T16) return hipErrorInvalidValue;
-  const int rows = B * T16;
-  hipLaunchKernelGGL(memory_pack_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, x, ln_g, ln_b, out, B, T, T16);
-  return hipGetLastError();
-}
-
 }  // namespace nd
 
 namespace nd {
@@ -683,11 +465,8 @@ hipError_t init_kernel_attributes() {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
   }
-  const void* mf[] = {(const void*)dec_mem_attention_kernel<MEM_NW, 0>, (const void*)dec_mem_attention_kernel<MEM_NW, 1>,
-                      (const void*)dec_mem_attention_kernel<MEM_NW, 2>, (const void*)dec_mem_attention_kernel<MEM_NW, 3>,
-                      (const void*)dec_mem_attention_kernel<MEM_NW, 4>};
-  for (const void* f : mf) {
-    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  {
+    hipError_t e = init_mem_attributes();
     if (e != hipSuccess) return e;
   }
   return init_gemm_attributes();

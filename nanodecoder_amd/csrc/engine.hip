@@ -105,7 +105,8 @@ struct nd_ctx {
   float* sig = nullptr;
   int *len = nullptr, *span = nullptr;
   float *x = nullptr, *y = nullptr, *att = nullptr, *big = nullptr, *ctxkv = nullptr;
-  float* mem_p = nullptr;                 // P16 memory bank [B * T16, 256]
+  float* mem_p = nullptr;                 // memory bank [B * T, 256] row-major (LN'd encoder output)
+  const float* mem = nullptr;             // the bank the decoder reads: mem_p, or x (NanoEncoder)
   float *dqk = nullptr, *dU = nullptr;    // [R, 8*256] P16 (memory-bank path)
   float *nano_xp = nullptr, *nano_h = nullptr;
   float *x_part = nullptr, *y_part = nullptr, *dx_part = nullptr, *dq1_part = nullptr, *dmid_part = nullptr;
@@ -292,7 +293,7 @@ static int alloc_workspaces(nd_ctx* c) {
   WS(c->att, B * T * D);
   WS(c->big, B * T * std::max(F, 3 * D));
   WS(c->ctxkv, B * T * Ld * 2 * D);
-  WS(c->mem_p, B * ((T + 15) / 16 * 16) * D);
+  WS(c->mem_p, B * T * D);
   WS(c->x_part, B * T * ND_PART_LD * 2);
   WS(c->y_part, B * T * ND_PART_LD * 2);
   WS(c->dx_part, R * ND_PART_LD * 2);
@@ -431,7 +432,6 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
   const int R = C * rpc, D = c->D, F = c->F, S = c->cfg.max_steps;
   const int Ld = (int)c->dec.size();
   const bool mb = use_memory_bank(c, rpc);
-  const int T16 = (T + 15) / 16 * 16;
   int pnx = 1, pnq = 0, pnm = 0;
   for (int i = 0; i < Ld; ++i) {
     DecLayer& L = c->dec[i];
@@ -444,8 +444,8 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
     if (mb) {  // memory-bank form (attention.hip)
       const int HD = ND_H * D;
       LCHK(G(c->dq1, D, L.pwqk, HD, D, L.bqk, c->dqk, HD, R).p16().ln(c->dq1_part, pnq).run(s));
-      LCHK(nd::launch_dec_mem_attention(c->dqk, c->mem_p, c->sig, c->span, (float)c->cfg.pad_idx, c->dU, C, rpc, T,
-                                        T16, s));
+      LCHK(nd::launch_dec_mem_attention(c->dqk, c->mem, c->sig, c->span, (float)c->cfg.pad_idx, c->dU, C, rpc, T, T,
+                                        s));
       LCHK(G(c->dU, HD, L.pwvo, D, HD, L.bvo, c->dmid, D, R).p16().res(c->dq1, D).stats(c->dmid_part).run(s, &pnm));
     } else {
       LCHK(G(c->dq1, D, L.pcwq, D, D, L.ncbq, c->dcq, D, R).p16().ln(c->dq1_part, pnq).run(s));
@@ -463,9 +463,12 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
 // per-layer context K/V (beam).
 static hipError_t enqueue_memory(nd_ctx* c, int B, int T, int rpc, hipStream_t s) {
   if (!use_memory_bank(c, rpc)) return enqueue_ctxkv(c, B, T, s);
-  const bool tr = c->cfg.encoder_type == ND_ENC_TRANSFORMER;
-  return nd::launch_memory_pack(c->x, tr ? c->enc_ln_g : nullptr, tr ? c->enc_ln_b : nullptr, c->mem_p, B, T,
-                                (T + 15) / 16 * 16, s);
+  if (c->cfg.encoder_type != ND_ENC_TRANSFORMER) {  // the NanoEncoder's output is the bank as it stands
+    c->mem = c->x;
+    return hipSuccess;
+  }
+  c->mem = c->mem_p;
+  return nd::launch_memory_pack(c->x, c->enc_ln_g, c->enc_ln_b, c->mem_p, B, T, T, s);
 }
 
 static hipError_t enqueue_greedy(nd_ctx* c, int B, int T, int S, int min_len, bool logp, hipStream_t s) {
@@ -965,16 +968,16 @@ int nd_op_dec_self_attention(const float* qkv, float* cache, const int32_t* anc,
 }
 
 int nd_op_dec_mem_attention(const float* qp, const float* mem, const float* signal, const int32_t* span, float pad_val,
-                            float* out, int32_t C, int32_t rpc, int32_t T, int32_t T16, void* stream) {
+                            float* out, int32_t C, int32_t rpc, int32_t T, int32_t ldT, void* stream) {
   if (int rc = ensure_attributes()) return rc;
-  hipError_t e = nd::launch_dec_mem_attention(qp, mem, signal, span, pad_val, out, C, rpc, T, T16, (hipStream_t)stream);
+  hipError_t e = nd::launch_dec_mem_attention(qp, mem, signal, span, pad_val, out, C, rpc, T, ldT, (hipStream_t)stream);
   if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("dec_mem_attention: ") + hipGetErrorString(e));
   return ND_OK;
 }
 
 int nd_op_memory_pack(const float* x, const float* ln_g, const float* ln_b, float* out, int32_t B, int32_t T,
-                      int32_t T16, void* stream) {
-  hipError_t e = nd::launch_memory_pack(x, ln_g, ln_b, out, B, T, T16, (hipStream_t)stream);
+                      int32_t ldT, void* stream) {
+  hipError_t e = nd::launch_memory_pack(x, ln_g, ln_b, out, B, T, ldT, (hipStream_t)stream);
   if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("memory_pack: ") + hipGetErrorString(e));
   return ND_OK;
 }

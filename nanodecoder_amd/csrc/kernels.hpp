@@ -87,15 +87,18 @@ struct NextEmbed {
   float* x = nullptr;
   float* part = nullptr;
 };
-// memory-bank context attention (greedy; rpc*8 <= 16 rows per chunk):
-// qp = Q' [C*rpc, 8*256] P16 (row r = c*rpc+j, column block h = head h's
-// 256-dim query in memory space), mem = P16 memory bank with T16 rows per
-// chunk; out = U [C*rpc, 8*256] P16 (head h's softmax-weighted memory sum).
+// memory-bank context attention (greedy, one row per chunk: rpc == 1):
+// qp = Q' [C, 8*256] P16 (column block h = head h's 256-dim query in memory
+// space), mem = row-major memory bank [C * ldT, 256] (chunk c's position t at
+// row c*ldT + t, t < T <= ldT); out = U [C, 8*256] P16 (head h's
+// softmax-weighted memory sum).
 hipError_t launch_dec_mem_attention(const float* qp, const float* mem, const float* signal, const int* span,
-                                    float pad_val, float* out, int C, int rpc, int T, int T16, hipStream_t s);
-// encoder output rows x[b*T+t] -> P16 memory bank rows b*T16+t (LN when ln_g)
-hipError_t launch_memory_pack(const float* x, const float* ln_g, const float* ln_b, float* out, int B, int T, int T16,
+                                    float pad_val, float* out, int C, int rpc, int T, int ldT, hipStream_t s);
+// encoder output rows x[b*T+t] -> memory bank rows b*ldT+t, row-major (LN when
+// ln_g; rows t >= T of each chunk zero)
+hipError_t launch_memory_pack(const float* x, const float* ln_g, const float* ln_b, float* out, int B, int T, int ldT,
                               hipStream_t s);
+hipError_t init_mem_attributes();
 // greedy head: LN_dec -> generator -> log_softmax -> argmax; writes token
 // (next input + output [R, S] at column step), score, optional logp dump,
 // and the next step's embedded input (ne).

@@ -1,0 +1,307 @@
+// Memory-bank form of the decoder's context attention (greedy decoding), gfx950.
+//
+// With the decoder's ctx K/V projections folded into the query and output
+// sides (engine finalize: W_qk[h] = W_k,h^T W_q,h / sqrt(d_h),
+// W_vo[:, h] = W_o,h W_v,h), head h of a decoder row needs only the encoder
+// memory bank m_t (256 floats per source position, shared by all three
+// decoder layers) instead of a per-layer K and V
+// (onmt/modules/multi_headed_attn.py:142-179, decoder/transformer.py:88-92):
+//   s_h(t) = q'_h . m_t        (q'_h = W_qk[h] LN(x) + b_qk[h]; the dropped
+//                               q_h . b_k,h is constant in t: softmax-exact)
+//   U_h    = sum_t softmax_t(s_h)(t) m_t,   out = W_vo U + b_vo
+// Mask: src == pad -> -1e18 (multi_headed_attn.py:172); t >= span: absent.
+//
+// Per chunk the work is two skinny products over the chunk's [T, 256] bank,
+// S = M Q'^T (8 heads) and U = P^T M.  With only 8 query rows a 16-wide MFMA
+// tile would be half padding, so both run on v_mfma_f32_4x4x1_16b_f32
+// (16 independent 4x4 outer products per instruction, f32 in / f32 acc,
+// probe: tools/probe_mfma4x4.hip), whose 4-wide blocks tile 8 heads exactly.
+//
+// One workgroup (8 waves) per chunk.  Keys are split over the waves, 8 per
+// wave per 64-key tile, so every wave works on its own keys only and runs its
+// own online softmax; the waves meet once, at the end, to merge (m, l, U).
+//  - Staging: each of the wave's 8 key rows (1 KB, contiguous in HBM) is one
+//    global_load_lds_dwordx4 into the wave's private LDS slab, double
+//    buffered, the next tile in flight while this one computes.  Row k is
+//    stored rotated by 4k floats (rotation applied on the per-lane source
+//    address, the LDS side stays lane-linear), which makes both read
+//    patterns below bank-conflict-free.
+//  - S: block b of the 4x4x1 instruction = (dim class dp, key quad kg,
+//    head quad hg); dp is the ds_read_b128 lane group the block sits in, so
+//    the 16 lanes of a group read 8 distinct rows at distinct bank quads.
+//    Lane (b, x) supplies A = m[key 4kg+x][d] and B = q'[head 4hg+x][d] for
+//    the 64 dims d of class dp (its q' slice lives in 64 VGPRs for the whole
+//    launch).  The 4 class partials meet through a 1 KB LDS slab.
+//  - U: block b = (dim octet dg, head quad hg), one key per instruction:
+//    A = p[key][4hg+i], B = m[key][dims of the lane] (two 16 B reads of the
+//    key's row), 8 accumulators of 4 = the wave's U for all 8 x 256 outputs.
+#include "common.hpp"
+#include "kernels.hpp"
+
+#include <cstdlib>
+
+namespace nd {
+
+#define MB_NW 8                      // waves per chunk (2 per SIMD)
+#define MB_KW 8                      // keys per wave per tile
+#define MB_TILE (MB_NW * MB_KW)      // keys per tile
+#define MB_WAVE (2 * MB_KW * ND_D + 2 * 256 + 64)  // floats of LDS per wave: 2 tile slabs, 2 S-partial slabs, P
+#define MB_U (MB_NW * MB_WAVE)       // q' image [8 heads][256], row h rotated by 4h floats
+#define MB_ML (MB_U + ND_H * ND_D)   // merge: per wave and head (m, l)
+#define MB_LDS_FLOATS (MB_ML + MB_NW * 16)
+
+__device__ __forceinline__ f32x4 mfma4x4(float a, float b, f32x4 c) {
+  // lane 4b+i supplies A_b[i], lane 4b+j supplies B_b[j]; lane 4b+j, reg i
+  // accumulates A_b[i] * B_b[j]
+  return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 0, 0, 0);
+}
+
+#define ND_DPP_ROR8 0x128  // row_ror:8 inside a 16-lane row == lane ^ 8
+
+// over the 8 lanes sharing lane & 7
+__device__ __forceinline__ float max_by8(float v) {
+  v = fmaxf(v, dpp_mov<ND_DPP_ROR8>(v));
+  return xor32_max(xor16_max(v));
+}
+__device__ __forceinline__ float sum_by8(float v) {
+  v += dpp_mov<ND_DPP_ROR8>(v);
+  return xor32_sum(xor16_sum(v));
+}
+
+template <int EXPT>
+__global__ void __launch_bounds__(MB_NW * 64)
+dec_mem_attention_kernel(const float* __restrict__ qp, const float* __restrict__ mem,
+                         const float* __restrict__ signal, const int* __restrict__ span, float pad_val,
+                         float* __restrict__ out, int T, int ldT) {
+  extern __shared__ float lds[];
+  const int c = blockIdx.x, lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (scalar addressing)
+  float* slab = lds + w * MB_WAVE;            // [2][8 keys][256], row k rotated by 4k floats
+  float* spart = slab + 2 * MB_KW * ND_D;     // [2][4 dp][8 heads][8 keys]
+  float* pbuf = spart + 2 * 256;              // [8 heads][8 keys]
+  const float* ub = lds + MB_U;
+  const int L = min(span[c], T);
+  const int ntile = (L + MB_TILE - 1) / MB_TILE;
+  const float* mc = mem + (size_t)c * ldT * ND_D;
+
+  // ---- lane roles
+  // S: block b = lane >> 2, x = lane & 3
+  const int b = lane >> 2, x = lane & 3;
+  const int dp = 2 * (b >> 3) + (__builtin_popcount(b & 7) & 1);  // ds_read_b128 lane group of block b
+  const int kg = (b >> 2) & 1, hg = (b >> 1) & 1;                   // rank within the group
+  const int skey = 4 * kg + x, shead = 4 * hg + x;
+  // softmax: lane -> (key sk, head sh)
+  const int sk = lane >> 3, sh = lane & 7;
+  // U: lane's dims 4zm..4zm+3 and 128+4zm..+3; A operand head = sh
+  const int zm = 4 * (lane >> 3) + (lane & 3);
+
+  // Staging through registers, four tiles in flight (two in registers, two
+  // in LDS): lane l loads 16 B of each of the wave's 8 rows (one coalesced
+  // 1 KB row per instruction) and writes them to a slab at the row's rotation.
+  auto fetch = [&](int r, f32x4(&dst)[MB_KW]) {
+#pragma unroll
+    for (int k = 0; k < MB_KW; ++k) {
+      const int t = min(r * MB_TILE + w * MB_KW + k, T - 1);
+      dst[k] = (EXPT & 1) ? f32x4{0.f, 0.f, 0.f, 0.f} : ld4(mc + (size_t)t * ND_D + 4 * lane);
+    }
+  };
+  auto put = [&](int r, const f32x4(&src)[MB_KW]) {
+    float* dst = slab + (r & 1) * (MB_KW * ND_D);
+#pragma unroll
+    for (int k = 0; k < MB_KW; ++k) st4(dst + k * ND_D + ((4 * lane + 4 * k) & (ND_D - 1)), src[k]);
+  };
+  // S partial of tile r over dim class dp: lane 4b+j, reg i = s[key 4kg+i][head 4hg+j]
+  auto scores = [&](int r) {
+    const float* arow = slab + (r & 1) * (MB_KW * ND_D) + skey * ND_D;
+    const float* urow = ub + shead * ND_D;
+    f32x4 s4[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s4[e] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 16 && !(EXPT & 2); ++kk) {
+      const f32x4 a = ld4(arow + ((64 * dp + 4 * kk + 4 * skey) & (ND_D - 1)));
+      const f32x4 u = ld4(urow + ((64 * dp + 4 * kk + 4 * shead) & (ND_D - 1)));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s4[e] = mfma4x4(a[e], u[e], s4[e]);
+    }
+    return (s4[0] + s4[1]) + (s4[2] + s4[3]);
+  };
+  auto put_scores = [&](int r, f32x4 v) { st4(spart + (r & 1) * 256 + (dp * 8 + shead) * 8 + 4 * kg, v); };
+
+  f32x4 R0[MB_KW], R1[MB_KW];
+  if (ntile > 0) fetch(0, R0);
+  if (ntile > 1) fetch(1, R1);
+  // q' image (all heads; 512 threads x 16 B) and the source samples of this
+  // wave's keys (lane l -> tile l >> 3, key l & 7)
+  {
+    const int h = threadIdx.x >> 6, q = threadIdx.x & 63;
+    st4(lds + MB_U + h * ND_D + ((4 * q + 4 * h) & (ND_D - 1)), ld4(qp + pk(c, h * ND_D + 4 * q, ND_H * ND_D)));
+  }
+  const float sgv = signal[(size_t)c * T + min((lane >> 3) * MB_TILE + w * MB_KW + (lane & 7), T - 1)];
+  if (ntile > 0) put(0, R0);
+  if (ntile > 1) put(1, R1);
+  if (ntile > 2) fetch(2, R0);
+  if (ntile > 3) fetch(3, R1);
+  __syncthreads();  // q' image
+  if (ntile > 0) put_scores(0, scores(0));
+
+  f32x4 acc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] = {0.f, 0.f, 0.f, 0.f};
+  float mrun = -INFINITY, lrun = 0.f;  // online-softmax state of head sh over this wave's keys
+
+  // Iteration r: the scores of tile r + 1 (MFMA) overlap the softmax of tile r
+  // (LDS/VALU latency), then U += P^T M for tile r; then tile r + 2 (in R,
+  // fetched two iterations earlier) goes to the freed slab and R refills with
+  // tile r + 4.
+  auto body = [&](int r, f32x4(&R)[MB_KW]) {
+    const f32x4 snext = scores(r + 1);  // tile r + 1's slab (garbage past the last tile, unused)
+
+    // ---- online softmax of head sh over the tile's 8 keys of this wave
+    const float* sp = spart + (r & 1) * 256 + sh * 8 + sk;
+    float s = (sp[0] + sp[64]) + (sp[128] + sp[192]);
+    const int t = r * MB_TILE + w * MB_KW + sk;
+    const float sg = __shfl(sgv, r * 8 + sk);
+    s = t < L ? (sg == pad_val ? ND_MASK_FILL : s) : -INFINITY;
+    const float mnew = fmaxf(mrun, max_by8(s));
+    const float scale = mnew == -INFINITY ? 1.f : __expf(mrun - mnew);
+    const float p = s == -INFINITY ? 0.f : __expf(s - mnew);
+    lrun = lrun * scale + sum_by8(p);
+    mrun = mnew;
+    pbuf[sh * 8 + sk] = p;
+    {
+      // acc reg i belongs to head 4((lane>>2)&1) + i = the softmax head of quad lane i
+      const float sc0 = dpp_mov<0x00>(scale), sc1 = dpp_mov<0x55>(scale);
+      const float sc2 = dpp_mov<0xAA>(scale), sc3 = dpp_mov<0xFF>(scale);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        acc[e][0] *= sc0;
+        acc[e][1] *= sc1;
+        acc[e][2] *= sc2;
+        acc[e][3] *= sc3;
+      }
+    }
+
+    // ---- U += P^T M over the tile's 8 keys of this wave
+    const f32x4 p0 = ld4(pbuf + sh * 8), p1 = ld4(pbuf + sh * 8 + 4);
+    const float* tile = slab + (r & 1) * (MB_KW * ND_D);
+#pragma unroll
+    for (int k = 0; k < MB_KW && !(EXPT & 2); ++k) {
+      const float* row = tile + k * ND_D;
+      const f32x4 b0 = ld4(row + ((4 * zm + 4 * k) & (ND_D - 1)));
+      const f32x4 b1 = ld4(row + ((128 + 4 * zm + 4 * k) & (ND_D - 1)));
+      const float pk_ = k < 4 ? p0[k] : p1[k - 4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        acc[e] = mfma4x4(pk_, b0[e], acc[e]);
+        acc[4 + e] = mfma4x4(pk_, b1[e], acc[4 + e]);
+      }
+    }
+    put_scores(r + 1, snext);
+    // the wave's LDS accesses retire in order: tile r + 2 lands after tile r's reads
+    if (r + 2 < ntile) put(r + 2, R);
+    if (r + 4 < ntile) fetch(r + 4, R);
+  };
+  for (int r = 0; r < ntile; r += 2) {
+    body(r, R0);
+    if (r + 1 < ntile) body(r + 1, R1);
+  }
+
+  // ---- merge the waves: head h's slots are combined by wave h
+  __syncthreads();  // every wave is done with its slabs
+  float* red = lds;               // [NW][512 slots][4]; slot = head * 64 + dim quad
+  float* ml = lds + MB_ML;        // [NW][8 heads][2]
+  if (lane < 8) {
+    ml[(w * 8 + lane) * 2] = mrun;  // lane < 8: sh == lane
+    ml[(w * 8 + lane) * 2 + 1] = lrun;
+  }
+  {
+    const int hb = 4 * ((lane >> 2) & 1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const f32x4 lo = {acc[0][i], acc[1][i], acc[2][i], acc[3][i]};
+      const f32x4 hi = {acc[4][i], acc[5][i], acc[6][i], acc[7][i]};
+      st4(red + ((size_t)w * 512 + (hb + i) * 64 + zm) * 4, lo);
+      st4(red + ((size_t)w * 512 + (hb + i) * 64 + 32 + zm) * 4, hi);
+    }
+  }
+  __syncthreads();
+  const int h = w;  // this wave finishes head h: dims 4 lane .. 4 lane + 3
+  float M = -INFINITY;
+#pragma unroll
+  for (int v = 0; v < MB_NW; ++v) M = fmaxf(M, ml[(v * 8 + h) * 2]);
+  f32x4 num = {0.f, 0.f, 0.f, 0.f};
+  float den = 0.f;
+#pragma unroll
+  for (int v = 0; v < MB_NW; ++v) {
+    const float mv = ml[(v * 8 + h) * 2];
+    const float f = mv == -INFINITY ? 0.f : __expf(mv - M);  // waves that owned no key
+    den += f * ml[(v * 8 + h) * 2 + 1];
+    num += f * ld4(red + ((size_t)v * 512 + h * 64 + lane) * 4);
+  }
+  st4(out + pk(c, h * ND_D + 4 * lane, ND_H * ND_D), num * (den > 0.f ? 1.0f / den : 0.f));
+}
+
+static constexpr size_t mem_lds_bytes() { return (size_t)MB_LDS_FLOATS * sizeof(float); }
+static_assert(MB_LDS_FLOATS * 4 <= 160 * 1024, "LDS");
+static_assert(MB_NW * 512 * 4 <= MB_U, "merge slots overlap the q' image");
+
+hipError_t launch_dec_mem_attention(const float* qp, const float* mem, const float* signal, const int* span,
+                                    float pad_val, float* out, int C, int rpc, int T, int ldT, hipStream_t s) {
+  if (rpc != 1 || T < 1 || T > 512 || ldT < T || C < 1) return hipErrorInvalidValue;
+  static const int expt = [] {
+    const char* e = getenv("ND_MEM_EXPT");  // timing experiments only (wrong results): 1 no loads, 2 no MFMA
+    return e ? atoi(e) : 0;
+  }();
+#define ND_MB_LAUNCH(X)                                                                                         \
+  hipLaunchKernelGGL(dec_mem_attention_kernel<X>, dim3(C), dim3(MB_NW * 64), mem_lds_bytes(), s, qp, mem, signal, \
+                     span, pad_val, out, T, ldT)
+  if (expt == 1) ND_MB_LAUNCH(1);
+  else if (expt == 2) ND_MB_LAUNCH(2);
+  else if (expt == 3) ND_MB_LAUNCH(3);
+  else ND_MB_LAUNCH(0);
+#undef ND_MB_LAUNCH
+  return hipGetLastError();
+}
+
+// Encoder output -> the decoder's memory bank, row-major with ldT rows per
+// chunk: row b*ldT + t = LN(x[b*T + t]) (transformer: encoder.layer_norm,
+// encoder/transformer.py:125) or x itself; rows t >= T zero.
+__global__ void __launch_bounds__(256)
+memory_pack_kernel(const float* __restrict__ x, const float* __restrict__ g, const float* __restrict__ b,
+                   float* __restrict__ out, int B, int T, int ldT) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= B * ldT) return;
+  const int bb = row / ldT, t = row - bb * ldT;
+  f32x4 v = {0.f, 0.f, 0.f, 0.f};
+  if (t < T) {
+    v = ld4(x + ((size_t)bb * T + t) * ND_D + lane * 4);
+    if (g) {
+      const float mu = wave_sum(v.x + v.y + v.z + v.w) * (1.0f / ND_D);
+      const f32x4 d = v - mu;
+      const float var = wave_sum(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w) * (1.0f / ND_D);
+      v = d * (1.0f / sqrtf(var + ND_LN_EPS)) * ld4(g + lane * 4) + ld4(b + lane * 4);
+    }
+  }
+  st4(out + (size_t)row * ND_D + lane * 4, v);
+}
+
+hipError_t launch_memory_pack(const float* x, const float* ln_g, const float* ln_b, float* out, int B, int T, int ldT,
+                              hipStream_t s) {
+  if (T > ldT || T < 1) return hipErrorInvalidValue;
+  const int rows = B * ldT;
+  hipLaunchKernelGGL(memory_pack_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, x, ln_g, ln_b, out, B, T, ldT);
+  return hipGetLastError();
+}
+
+hipError_t init_mem_attributes() {
+  const void* fns[] = {(const void*)dec_mem_attention_kernel<0>, (const void*)dec_mem_attention_kernel<1>,
+                       (const void*)dec_mem_attention_kernel<2>, (const void*)dec_mem_attention_kernel<3>};
+  for (const void* f : fns) {
+    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mem_lds_bytes());
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+}  // namespace nd

@@ -236,27 +236,28 @@ def op_dec_ctx_attention(q, kv, ld, koff, signal, span, pad_val, rpc, packed=Fal
     return out if packed else unpack_p16(out, R)
 
 
-def op_memory_pack(x, B, T, ln_g=None, ln_b=None):
-    """Encoder output x [B*T, 256] -> P16 memory bank [B*T16, 256]."""
-    T16 = (T + 15) // 16 * 16
-    out = torch.empty(B * T16, x.shape[1], dtype=torch.float32, device=x.device)
+def op_memory_pack(x, B, T, ln_g=None, ln_b=None, ldT=None):
+    """Encoder output x [B*T, 256] -> row-major memory bank [B*ldT, 256]
+    (LayerNorm'd when ln_g is given; rows t >= T of each chunk zero)."""
+    ldT = ldT or T
+    out = torch.empty(B * ldT, x.shape[1], dtype=torch.float32, device=x.device)
     s = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
-    _lib.check(_lib.lib().nd_op_memory_pack(_ptr(x), _ptr(ln_g), _ptr(ln_b), _ptr(out), B, T, T16, s),
+    _lib.check(_lib.lib().nd_op_memory_pack(_ptr(x), _ptr(ln_g), _ptr(ln_b), _ptr(out), B, T, ldT, s),
                "nd_op_memory_pack")
     return out
 
 
 def op_dec_mem_attention(qp, mem_p, signal, span, pad_val, rpc, out=None):
-    """Memory-bank context attention on packed operands: qp [R16, 2048],
-    mem_p [C*T16, 256] (op_memory_pack); returns U [R16, 2048] packed (rows of
-    chunks c < C written)."""
+    """Memory-bank context attention: qp [R16, 2048] packed, mem_p the
+    row-major bank [C*ldT, 256] (op_memory_pack); returns U [R16, 2048] packed
+    (rows of chunks c < C written).  rpc must be 1."""
     C, T = signal.shape
-    T16 = mem_p.shape[0] // C
+    ldT = mem_p.shape[0] // C
     if out is None:
         out = torch.empty(qp.shape[0], qp.shape[1], dtype=torch.float32, device=qp.device)
     s = ctypes.c_void_p(torch.cuda.current_stream(qp.device).cuda_stream)
     _lib.check(_lib.lib().nd_op_dec_mem_attention(_ptr(qp), _ptr(mem_p), _ptr(signal), _ptr(span), float(pad_val),
-                                                  _ptr(out), C, rpc, T, T16, s), "nd_op_dec_mem_attention")
+                                                  _ptr(out), C, rpc, T, ldT, s), "nd_op_dec_mem_attention")
     return out
 
 

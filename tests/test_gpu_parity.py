@@ -133,6 +133,38 @@ def test_enc_attention_vs_oracle():
         assert (out[b * T: b * T + L] - exp).abs().max().item() < 1e-4, b
 
 
+@pytest.mark.parametrize("T", [512, 200, 37])
+def test_mem_attention_vs_fp64(T):
+    """Memory-bank context attention (dec_mem_attention_kernel) against an
+    fp64 softmax(q' M^T) M per head, with ragged spans (tile/wave boundaries,
+    single key, waves owning no key), pad-masked keys and an all-masked chunk."""
+    from nanodecoder_amd.engine import op_dec_mem_attention, op_memory_pack, pack_p16, unpack_p16
+    rng = np.random.default_rng(3)
+    C, PAD = 12, 1.0
+    spans = np.array([T, 1, min(T, 64), min(T, 65), min(T, 70), min(T, 8), min(T, 9), T, max(1, T - 3),
+                      min(T, 130), T, T], np.int32)
+    sig = rng.standard_normal((C, T)).astype(np.float32)
+    sig[2, ::5] = PAD                      # pad-masked keys
+    sig[7, :] = PAD                        # every key masked -> uniform over the span
+    x = rng.standard_normal((C * T, 256)).astype(np.float32)
+    q = (rng.standard_normal((C, 2048)) * 0.3).astype(np.float32)
+    dev = torch.device("cuda", 0)
+    mem = op_memory_pack(torch.from_numpy(x).to(dev), C, T)
+    out = op_dec_mem_attention(pack_p16(torch.from_numpy(q).to(dev)), mem, torch.from_numpy(sig).to(dev),
+                               torch.from_numpy(spans).to(dev), PAD, 1)
+    got = unpack_p16(out, C).cpu().numpy()
+    for c in range(C):
+        L = int(spans[c])
+        M = x[c * T: c * T + L].astype(np.float64)
+        for h in range(8):
+            s = M @ q[c, h * 256:(h + 1) * 256].astype(np.float64)
+            s[sig[c, :L] == PAD] = -1e18
+            p = np.exp(s - s.max())
+            want = (p / p.sum()) @ M
+            err = np.abs(got[c, h * 256:(h + 1) * 256] - want).max()
+            assert err < 2e-5, (c, h, L, err)
+
+
 # ----------------------------------------------------------------- golden
 @pytest.mark.parametrize("name", ["transformer_greedy", "transformer_pe_short", "nano_greedy"])
 def test_encoder_memory_vs_golden(name):
