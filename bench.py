@@ -50,6 +50,14 @@ def parse():
     return ap.parse_args()
 
 
+def workload(args):
+    idx = 3 if args.mode == "beam" else (2 if args.encoder == "nano" else 1)
+    enc = "3-layer transformer encoder" if args.encoder == "transformer" else "NanoEncoder (3x BiLSTM)"
+    dec = "greedy" if args.mode == "greedy" else f"--fast beam {args.beam}"
+    return (f"configs[{idx}]: {enc} + 3-layer transformer decoder, d_model 256, src_seq_length 512, "
+            f"batch {args.batch}, {dec}, max_length {args.max_length}")
+
+
 def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -102,57 +110,40 @@ def _pmc_traffic(name):
 
 
 def kernel_roofline(eng, B, mode, beam):
-    """Dominant kernel of the translate step, timed standalone through the
-    C-ABI op entry point on the current torch stream with HIP events, on the
-    engine's shapes.
+    """Dominant kernel of the translate step, timed LIVE: every launch of it
+    inside the timed graph replays carries in-kernel wall-clock stamps
+    (first workgroup start, last workgroup end; Engine.set_kernel_stamps), and
+    the mean over the last timed call's launches is the launch duration.
 
     greedy: the memory-bank context attention (dec_mem_attention_kernel),
-      MFMA-issue-bound.  Algorithmic FLOPs per launch = 2 products (scores,
-      weighted sum) x 2 x 8 query rows (heads) x 512 keys x 256 dims per
-      chunk; the MFMA tiles carry 16 rows (8 padding), reported as
-      "tile_tflops".  Its HBM view (the 512 x 1 KB memory bank per chunk) is
-      reported too.
+      bounded by HBM: per launch it streams the B x 512 x 256 f32 memory bank
+      once (+ q' in, U out, the signal for the key mask).  Its MFMA view
+      (2 products x 2 x 8 heads x 512 keys x 256 dims per chunk, on
+      v_mfma_f32_4x4x1_16b) is reported beside it.
     beam: the per-layer K/V context attention (dec_ctx_attention_kernel),
       HBM-bound: K+V 2 x 512 keys x 256 f32 per chunk + q, signal, out."""
-    from nanodecoder_amd.engine import (op_dec_ctx_attention, op_dec_mem_attention, op_fold_layernorm, op_gemm,
-                                        op_memory_pack, pack_p16)
-    dev = eng.device
+    us, n = eng.kernel_stamps()
     T, D = 512, 256
-    sig = torch.randn(B, T, device=dev)
-    span = torch.full((B,), T, dtype=torch.int32, device=dev)
+    ms = us * 1e-3
     if mode == "greedy":
-        qp = pack_p16(torch.randn(B, 8 * D, device=dev))
-        memp = op_memory_pack(torch.randn(B * T, D, device=dev), B, T)
-        outp = torch.empty_like(qp)
-        fn = lambda i: op_dec_mem_attention(qp, memp, sig, span, 1.0, 1, out=outp)  # noqa: E731
-        for i in range(6):
-            fn(i)
-        ms = _time(fn, 30)
-        flops = 2 * 2 * 8 * T * D * B
-        ach = flops / (ms * 1e-3) / 1e12
+        name = "dec_mem_attention_kernel<0>"
         nbytes = B * T * D * 4 + B * T * 4 + 2 * B * 8 * D * 4
-        name = "dec_mem_attention_kernel<8, 0>"
-        out = {"bound": "mfma", "kernel": name, "achieved": round(ach, 2), "peak": 157.3, "unit": "TFLOP/s",
-               "frac": round(ach / 157.3, 4), "traffic": _pmc_traffic(name),
-               "algorithmic_flops_per_launch": flops, "avg_launch_ms": round(ms, 5),
-               "tile_tflops": round(2 * ach, 2),
-               "hbm_view": {"algorithmic_bytes_per_launch": nbytes,
-                            "achieved_gbs": round(nbytes / (ms * 1e-3) / 1e9, 1), "peak_gbs": 8000.0}}
+        flops = 2 * 2 * 8 * T * D * B
+        tf = flops / (ms * 1e-3) / 1e12
+        extra = {"mfma_view": {"algorithmic_flops_per_launch": flops, "achieved": round(tf, 2), "peak": 157.3,
+                               "unit": "TFLOP/s", "frac": round(tf / 157.3, 4)}}
     else:
-        rpc = beam
-        kv = torch.randn(B * T, 3 * 2 * D, device=dev)
-        q = pack_p16(torch.randn(B * rpc, D, device=dev))  # decoder activations live P16-packed
-        fn = lambda i: op_dec_ctx_attention(q, kv, 3 * 2 * D, (i % 3) * 2 * D, sig, span, 1.0, rpc,  # noqa: E731
-                                            packed=True)
-        for i in range(6):
-            fn(i)
-        ms = _time(fn, 30)
-        nbytes = B * T * 2 * D * 4 + B * T * 4 + 2 * B * rpc * D * 4
-        ach = nbytes / (ms * 1e-3) / 1e9
-        out = {"bound": "hbm", "kernel": f"dec_ctx_attention_kernel<{rpc}>", "achieved": round(ach, 1),
-               "peak": 8000.0, "unit": "GB/s", "frac": round(ach / 8000.0, 4),
-               "traffic": _pmc_traffic(f"dec_ctx_attention_kernel<{rpc}>"),
-               "algorithmic_bytes_per_launch": nbytes, "avg_launch_ms": round(ms, 5)}
+        name = f"dec_ctx_attention_kernel<{beam}>"
+        nbytes = B * T * 2 * D * 4 + B * T * 4 + 2 * B * beam * D * 4
+        extra = {}
+    ach = nbytes / (ms * 1e-3) / 1e9
+    out = {"bound": "hbm", "kernel": name, "achieved": round(ach, 1), "peak": 8000.0, "unit": "GB/s",
+           "frac": round(ach / 8000.0, 4), "traffic": _pmc_traffic(name), "algorithmic_bytes_per_launch": nbytes,
+           "avg_launch_ms": round(ms, 5), "timed_launches": n,
+           "timing": "in-kernel wall-clock stamps, launches of the last timed call"}
+    out.update(extra)
+    dev = eng.device
+    from nanodecoder_amd.engine import op_fold_layernorm, op_gemm
     # secondary: the dominant encoder MFMA kernel (FFN1 GEMM, LN prologue + bias + ReLU)
     M, K, N = B * T, 256, 2048
     A = torch.randn(M, K, device=dev)
@@ -198,6 +189,7 @@ def main():
         return eng.translate_beam(sig, lens, lens, beam=args.beam, max_len=args.max_length,
                                   min_len=args.min_length)
 
+    eng.set_kernel_stamps(not args.no_roofline)  # live launch timing of the roofline kernel (in the graphs)
     for _ in range(args.warmup):
         out = step()
     torch.cuda.synchronize()
@@ -232,9 +224,7 @@ def main():
         "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic reads, random-init weights",
-        "config": {"workload": f"configs[1]: 3+3 {args.encoder} d256, T512, {args.mode}"
-                               f"{'' if args.mode == 'greedy' else ' beam ' + str(args.beam)}, max_length "
-                               f"{args.max_length}", "chunks_per_gpu_per_step": args.batch,
+        "config": {"workload": workload(args), "chunks_per_gpu_per_step": args.batch,
                    "global_batch": args.batch * world, "seq_len": 512, "parallelism": f"read-shard x{world}"},
         "samples_per_sec_per_gpu": round(value / world, 1),
         "bases_per_sec": round(bases_per_step * args.steps * world / dt, 1),

@@ -118,6 +118,16 @@ int nd_set_graphs(nd_ctx* ctx, int enable);
  * 142-177's context path. */
 int nd_set_ctx_path(nd_ctx* ctx, int path);
 
+/* Launch-duration stamps of the decoder's context attention (the bench's
+ * roofline kernel: dec_mem_attention_kernel for greedy, dec_ctx_attention_kernel
+ * for beam), taken inside the kernels with the constant-rate wall clock while
+ * enable != 0 (part of the captured graphs, so they time graph replays).
+ * nd_kernel_stamps waits for the context's stream and returns the mean
+ * duration (first workgroup start to last workgroup end) of the launches of
+ * the last call. */
+int nd_set_kernel_stamps(nd_ctx* c, int enable);
+int nd_kernel_stamps(nd_ctx* c, float* avg_us, int32_t* launches);
+
 /* Kernel statistics of the last translate call (ms of device time per
  * phase, measured with HIP events on the engine stream when enabled). */
 int nd_set_timing(nd_ctx* ctx, int enable);

@@ -42,6 +42,8 @@ SIGNATURES = {
     "nd_set_timing": (_I, [_P, _I]),
     "nd_set_ctx_path": (_I, [_P, _I]),
     "nd_last_timing": (_I, [_P, ctypes.POINTER(_F), ctypes.POINTER(_F)]),
+    "nd_set_kernel_stamps": (_I, [_P, _I]),
+    "nd_kernel_stamps": (_I, [_P, ctypes.POINTER(_F), ctypes.POINTER(_I)]),
     "nd_destroy": (None, [_P]),
     "nd_last_error": (ctypes.c_char_p, []),
     "nd_version": (ctypes.c_char_p, []),

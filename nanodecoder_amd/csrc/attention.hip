@@ -356,7 +356,8 @@ template <int RPC>
 __global__ void __launch_bounds__(CTX_NW * 64)
 dec_ctx_attention_kernel(const float* __restrict__ q, const float* __restrict__ kv, int ld, int koff,
                          const float* __restrict__ signal, const int* __restrict__ span, float pad_val,
-                         float* __restrict__ out, int T) {
+                         float* __restrict__ out, int T, unsigned long long* stamp) {
+  stamp_begin(stamp);
   constexpr int U = CtxTile<RPC>::U;
   extern __shared__ float sm[];
   float* accs = sm;                              // [NW][RPC][256]
@@ -417,20 +418,21 @@ dec_ctx_attention_kernel(const float* __restrict__ q, const float* __restrict__ 
     }
   }
   merge_waves<RPC, CTX_NW>(accs, ms, ls, m, l, acc, wave, lane, tid, out, c * RPC);
+  stamp_end(stamp);
 }
 
 static size_t ctx_lds_bytes(int rpc) { return (size_t)CTX_NW * rpc * (ND_D + 2 * ND_H) * sizeof(float); }
 
 hipError_t launch_dec_ctx_attention(const float* q, const float* kv, int ld, int koff, const float* signal,
                                     const int* span, float pad_val, float* out, int C, int rpc, int T,
-                                    hipStream_t s) {
+                                    hipStream_t s, unsigned long long* stamp) {
   if (rpc < 1 || rpc > CTX_MAXR || T > 512) return hipErrorInvalidValue;
   const size_t lds = ctx_lds_bytes(rpc);
   switch (rpc) {
 #define ND_CTX_CASE(R)                                                                                            \
   case R:                                                                                                         \
     hipLaunchKernelGGL(dec_ctx_attention_kernel<R>, dim3(C), dim3(CTX_NW * 64), lds, s, q, kv, ld, koff, signal,  \
-                       span, pad_val, out, T);                                                                    \
+                       span, pad_val, out, T, stamp);                                                             \
     break;
     ND_CTX_CASE(1)
     ND_CTX_CASE(2)

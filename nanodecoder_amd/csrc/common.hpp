@@ -108,3 +108,16 @@ __device__ __forceinline__ size_t pk(int m, int n, int N) {
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+
+// Launch-duration stamps (bench roofline, measured inside the timed graph):
+// stamp[0] = earliest workgroup start, stamp[1] = latest workgroup end, in
+// wall_clock64() ticks (s_memrealtime, constant rate).  stamp == nullptr: off.
+__device__ __forceinline__ void stamp_begin(unsigned long long* stamp) {
+  if (stamp && threadIdx.x == 0) atomicMin(stamp, (unsigned long long)wall_clock64());
+}
+__device__ __forceinline__ void stamp_end(unsigned long long* stamp) {
+  if (stamp) {
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(stamp + 1, (unsigned long long)wall_clock64());
+  }
+}

@@ -75,9 +75,10 @@ struct NanoLayer {
 struct GraphKey {
   int mode, B, T, S, min_len, beam, n_best, seg, logp;
   float alpha;
+  int stamp = 0;
   bool operator<(const GraphKey& o) const {
-    return std::tie(mode, B, T, S, min_len, beam, n_best, seg, logp, alpha) <
-           std::tie(o.mode, o.B, o.T, o.S, o.min_len, o.beam, o.n_best, o.seg, o.logp, o.alpha);
+    return std::tie(mode, B, T, S, min_len, beam, n_best, seg, logp, alpha, stamp) <
+           std::tie(o.mode, o.B, o.T, o.S, o.min_len, o.beam, o.n_best, o.seg, o.logp, o.alpha, o.stamp);
   }
 };
 
@@ -89,6 +90,8 @@ struct nd_ctx {
   bool finalized = false;
   bool use_graphs = true;
   int ctx_path = 0;  // 0: memory-bank form for greedy, K/V form for beam; 1: always K/V
+  bool kstamp_on = false;                 // stamp every context-attention launch (bench roofline)
+  unsigned long long* kstamp = nullptr;   // [dec_layers * max_steps][2] (start, end) wall-clock ticks
   bool timing = false;
   float t_enc = 0.f, t_dec = 0.f;
 
@@ -333,6 +336,7 @@ static int alloc_workspaces(nd_ctx* c) {
   WS(c->bs.n_alive, 4);
   WS(c->steps_done, 4);
   c->bs.steps_done = c->steps_done;
+  WS(c->kstamp, Ld * S * 2);
 #undef WS
   if ((e = hipHostMalloc((void**)&c->h_alive, 16, hipHostMallocDefault)) != hipSuccess)
     return fail(ND_ERR_HIP, std::string("hipHostMalloc: ") + hipGetErrorString(e));
@@ -436,6 +440,7 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
   for (int i = 0; i < Ld; ++i) {
     DecLayer& L = c->dec[i];
     float* cache = c->cache + (size_t)i * R * S * 2 * D;
+    unsigned long long* stamp = c->kstamp_on ? c->kstamp + 2 * ((size_t)step * Ld + i) : nullptr;
     // decoder/transformer.py:53-95
     // all step activations are P16-packed (kernels.hpp)
     LCHK(G(c->dx, D, L.pwqkv, 3 * D, D, L.nbqkv, c->dqkv, 3 * D, R).p16().ln(c->dx_part, pnx).run(s));
@@ -445,12 +450,12 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
       const int HD = ND_H * D;
       LCHK(G(c->dq1, D, L.pwqk, HD, D, L.bqk, c->dqk, HD, R).p16().ln(c->dq1_part, pnq).run(s));
       LCHK(nd::launch_dec_mem_attention(c->dqk, c->mem, c->sig, c->span, (float)c->cfg.pad_idx, c->dU, C, rpc, T, T,
-                                        s));
+                                        s, stamp));
       LCHK(G(c->dU, HD, L.pwvo, D, HD, L.bvo, c->dmid, D, R).p16().res(c->dq1, D).stats(c->dmid_part).run(s, &pnm));
     } else {
       LCHK(G(c->dq1, D, L.pcwq, D, D, L.ncbq, c->dcq, D, R).p16().ln(c->dq1_part, pnq).run(s));
       LCHK(nd::launch_dec_ctx_attention(c->dcq, c->ctxkv, Ld * 2 * D, i * 2 * D, c->sig, c->span,
-                                        (float)c->cfg.pad_idx, c->datt, C, rpc, T, s));
+                                        (float)c->cfg.pad_idx, c->datt, C, rpc, T, s, stamp));
       LCHK(G(c->datt, D, L.pcwo, D, D, L.cbo, c->dmid, D, R).p16().res(c->dq1, D).stats(c->dmid_part).run(s, &pnm));
     }
     LCHK(G(c->dmid, D, L.pw1, F, D, L.nb1, c->dhid, F, R).p16().ln(c->dmid_part, pnm).relu().run(s));
@@ -472,6 +477,7 @@ static hipError_t enqueue_memory(nd_ctx* c, int B, int T, int rpc, hipStream_t s
 }
 
 static hipError_t enqueue_greedy(nd_ctx* c, int B, int T, int S, int min_len, bool logp, hipStream_t s) {
+  if (c->kstamp_on) LCHK(nd::launch_stamp_reset(c->kstamp, (int)c->dec.size() * c->cfg.max_steps, s));
   LCHK(enqueue_encode(c, B, T, s));
   LCHK(enqueue_memory(c, B, T, 1, s));
   LCHK(nd::launch_fill_i32(c->tok, c->cfg.bos_idx, B, s));
@@ -788,7 +794,7 @@ int nd_translate_greedy(nd_ctx* c, const float* d_signal, const int32_t* d_len, 
   hipStream_t cs = (hipStream_t)stream;
   if ((rc = stage_inputs(c, d_signal, d_len, d_span, B, T, cs))) return rc;
   const bool lp = d_logp != nullptr;
-  GraphKey key{0, B, T, max_len, min_len, 1, 1, 0, lp ? 1 : 0, 0.f};
+  GraphKey key{0, B, T, max_len, min_len, 1, 1, 0, lp ? 1 : 0, 0.f, c->kstamp_on ? 1 : 0};
   if (c->timing) HIPCHK(hipEventRecord(c->ev_a, c->es));
   rc = run_graph(c, key, [&](hipStream_t s) { return enqueue_greedy(c, B, T, max_len, min_len, lp, s); });
   if (rc) return rc;
@@ -819,9 +825,11 @@ int nd_translate_beam(nd_ctx* c, const float* d_signal, const int32_t* d_len, co
   if ((rc = stage_inputs(c, d_signal, d_len, d_span, B, T, cs))) return rc;
   // n_best hypothesis storage is sized by max_beam
   const int SEG = 10;
-  GraphKey k0{1, B, T, max_len, min_len, beam, n_best, -1, 0, alpha};
+  const int st = c->kstamp_on ? 1 : 0;
+  GraphKey k0{1, B, T, max_len, min_len, beam, n_best, -1, 0, alpha, st};
   if (c->timing) HIPCHK(hipEventRecord(c->ev_a, c->es));
   rc = run_graph(c, k0, [&](hipStream_t s) -> hipError_t {
+    if (c->kstamp_on) LCHK(nd::launch_stamp_reset(c->kstamp, (int)c->dec.size() * c->cfg.max_steps, s));
     LCHK(enqueue_encode(c, B, T, s));
     LCHK(enqueue_ctxkv(c, B, T, s));
     LCHK(nd::launch_beam_init(c->bs, B, beam, n_best, max_len, c->cfg.bos_idx, s));
@@ -833,7 +841,7 @@ int nd_translate_beam(nd_ctx* c, const float* d_signal, const int32_t* d_len, co
   if (c->timing) HIPCHK(hipEventRecord(c->ev_b, c->es));
   for (int s0 = 0; s0 < max_len; s0 += SEG) {
     const int s1 = std::min(max_len, s0 + SEG);
-    GraphKey k{1, B, T, max_len, min_len, beam, n_best, s0, 0, alpha};
+    GraphKey k{1, B, T, max_len, min_len, beam, n_best, s0, 0, alpha, st};
     rc = run_graph(c, k, [&](hipStream_t s) {
       return enqueue_beam_steps(c, B, T, beam, n_best, alpha, max_len, min_len, s0, s1, s);
     });
@@ -892,6 +900,33 @@ int nd_set_ctx_path(nd_ctx* c, int path) {
 int nd_set_timing(nd_ctx* c, int enable) {
   if (!c) return fail(ND_ERR_ARG, "null ctx");
   c->timing = enable != 0;
+  return ND_OK;
+}
+
+int nd_set_kernel_stamps(nd_ctx* c, int enable) {
+  if (!c) return fail(ND_ERR_ARG, "null ctx");
+  c->kstamp_on = enable != 0;
+  return ND_OK;
+}
+
+int nd_kernel_stamps(nd_ctx* c, float* avg_us, int32_t* launches) {
+  if (!c || !avg_us || !launches) return fail(ND_ERR_ARG, "null argument");
+  const size_t n = c->dec.size() * (size_t)c->cfg.max_steps;
+  std::vector<unsigned long long> h(2 * n);
+  HIPCHK(hipSetDevice(c->cfg.device));
+  HIPCHK(hipStreamSynchronize(c->es));
+  HIPCHK(hipMemcpy(h.data(), c->kstamp, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  int rate_khz = 0;
+  HIPCHK(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, c->cfg.device));
+  double sum = 0.0;
+  int cnt = 0;
+  for (size_t i = 0; i < n; ++i)
+    if (h[2 * i] != ~0ull && h[2 * i + 1] >= h[2 * i]) {
+      sum += (double)(h[2 * i + 1] - h[2 * i]);
+      ++cnt;
+    }
+  *launches = cnt;
+  *avg_us = cnt && rate_khz > 0 ? (float)(sum / cnt / rate_khz * 1e3) : 0.f;
   return ND_OK;
 }
 

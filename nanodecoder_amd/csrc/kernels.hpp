@@ -76,7 +76,7 @@ hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* 
 // (K at kv[(c*T+t)*ld + koff], V at +256), mask signal == pad_val, keys < span.
 hipError_t launch_dec_ctx_attention(const float* q, const float* kv, int ld, int koff, const float* signal,
                                     const int* span, float pad_val, float* out, int C, int rpc, int T,
-                                    hipStream_t s);
+                                    hipStream_t s, unsigned long long* stamp = nullptr);
 // Next step's decoder input, written by the search kernel that picks the
 // token (the embedding of step+1 fused into the head: one launch fewer per
 // step): x[row] = emb[tok] (* 16 + pe[step+1] with position encoding) and
@@ -93,7 +93,10 @@ struct NextEmbed {
 // row c*ldT + t, t < T <= ldT); out = U [C, 8*256] P16 (head h's
 // softmax-weighted memory sum).
 hipError_t launch_dec_mem_attention(const float* qp, const float* mem, const float* signal, const int* span,
-                                    float pad_val, float* out, int C, int rpc, int T, int ldT, hipStream_t s);
+                                    float pad_val, float* out, int C, int rpc, int T, int ldT, hipStream_t s,
+                                    unsigned long long* stamp = nullptr);
+// stamp pairs (earliest start, latest end) <- (UINT64_MAX, 0)
+hipError_t launch_stamp_reset(unsigned long long* stamps, int pairs, hipStream_t s);
 // encoder output rows x[b*T+t] -> memory bank rows b*ldT+t, row-major (LN when
 // ln_g; rows t >= T of each chunk zero)
 hipError_t launch_memory_pack(const float* x, const float* ln_g, const float* ln_b, float* out, int B, int T, int ldT,

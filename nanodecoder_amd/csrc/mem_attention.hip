@@ -72,7 +72,8 @@ template <int EXPT>
 __global__ void __launch_bounds__(MB_NW * 64)
 dec_mem_attention_kernel(const float* __restrict__ qp, const float* __restrict__ mem,
                          const float* __restrict__ signal, const int* __restrict__ span, float pad_val,
-                         float* __restrict__ out, int T, int ldT) {
+                         float* __restrict__ out, int T, int ldT, unsigned long long* stamp) {
+  stamp_begin(stamp);
   extern __shared__ float lds[];
   const int c = blockIdx.x, lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (scalar addressing)
@@ -240,6 +241,7 @@ dec_mem_attention_kernel(const float* __restrict__ qp, const float* __restrict__
     num += f * ld4(red + ((size_t)v * 512 + h * 64 + lane) * 4);
   }
   st4(out + pk(c, h * ND_D + 4 * lane, ND_H * ND_D), num * (den > 0.f ? 1.0f / den : 0.f));
+  stamp_end(stamp);
 }
 
 static constexpr size_t mem_lds_bytes() { return (size_t)MB_LDS_FLOATS * sizeof(float); }
@@ -247,7 +249,8 @@ static_assert(MB_LDS_FLOATS * 4 <= 160 * 1024, "LDS");
 static_assert(MB_NW * 512 * 4 <= MB_U, "merge slots overlap the q' image");
 
 hipError_t launch_dec_mem_attention(const float* qp, const float* mem, const float* signal, const int* span,
-                                    float pad_val, float* out, int C, int rpc, int T, int ldT, hipStream_t s) {
+                                    float pad_val, float* out, int C, int rpc, int T, int ldT, hipStream_t s,
+                                    unsigned long long* stamp) {
   if (rpc != 1 || T < 1 || T > 512 || ldT < T || C < 1) return hipErrorInvalidValue;
   static const int expt = [] {
     const char* e = getenv("ND_MEM_EXPT");  // timing experiments only (wrong results): 1 no loads, 2 no MFMA
@@ -255,7 +258,7 @@ hipError_t launch_dec_mem_attention(const float* qp, const float* mem, const flo
   }();
 #define ND_MB_LAUNCH(X)                                                                                         \
   hipLaunchKernelGGL(dec_mem_attention_kernel<X>, dim3(C), dim3(MB_NW * 64), mem_lds_bytes(), s, qp, mem, signal, \
-                     span, pad_val, out, T, ldT)
+                     span, pad_val, out, T, ldT, stamp)
   if (expt == 1) ND_MB_LAUNCH(1);
   else if (expt == 2) ND_MB_LAUNCH(2);
   else if (expt == 3) ND_MB_LAUNCH(3);
@@ -291,6 +294,19 @@ hipError_t launch_memory_pack(const float* x, const float* ln_g, const float* ln
   if (T > ldT || T < 1) return hipErrorInvalidValue;
   const int rows = B * ldT;
   hipLaunchKernelGGL(memory_pack_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, x, ln_g, ln_b, out, B, T, ldT);
+  return hipGetLastError();
+}
+
+__global__ void stamp_reset_kernel(unsigned long long* p, int pairs) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < pairs) {
+    p[2 * i] = ~0ull;
+    p[2 * i + 1] = 0ull;
+  }
+}
+
+hipError_t launch_stamp_reset(unsigned long long* stamps, int pairs, hipStream_t s) {
+  hipLaunchKernelGGL(stamp_reset_kernel, dim3((pairs + 255) / 256), dim3(256), 0, s, stamps, pairs);
   return hipGetLastError();
 }
 

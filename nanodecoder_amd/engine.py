@@ -85,6 +85,17 @@ class Engine:
         _lib.check(self._L.nd_last_timing(self._h, ctypes.byref(e), ctypes.byref(d)), "nd_last_timing")
         return e.value, d.value
 
+    def set_kernel_stamps(self, on: bool):
+        """Stamp every decoder context-attention launch (in-kernel wall clock,
+        part of the graphs) — the bench's live roofline timing."""
+        _lib.check(self._L.nd_set_kernel_stamps(self._h, int(on)), "nd_set_kernel_stamps")
+
+    def kernel_stamps(self):
+        """(mean launch duration in us, launches) of the last call's context attention."""
+        a, n = ctypes.c_float(), ctypes.c_int32()
+        _lib.check(self._L.nd_kernel_stamps(self._h, ctypes.byref(a), ctypes.byref(n)), "nd_kernel_stamps")
+        return a.value, n.value
+
     def _inputs(self, signal, lengths, spans):
         dev = self.device
         signal = torch.as_tensor(signal, dtype=torch.float32).to(dev).contiguous()
