@@ -11,7 +11,7 @@ timeout -k 10 600 python bench.py --steps 10 --warmup 2 > $O/bench_greedy.json 2
 rc=$?; echo "bench greedy rc=$rc"; if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 600 python bench.py --mode beam --batch 1024 --steps 3 --warmup 1 > $O/bench_beam.json 2> $O/bench_beam.err
 rc=$?; echo "bench beam rc=$rc"; if [ $rc -ne 0 ]; then exit $rc; fi
-timeout -k 10 600 python bench.py --encoder nano --steps 5 --warmup 1 --cpu-chunks 16 > $O/bench_nano.json 2> $O/bench_nano.err
+timeout -k 10 600 python bench.py --encoder nano --steps 5 --warmup 1 --cpu-chunks 256 > $O/bench_nano.json 2> $O/bench_nano.err
 rc=$?; echo "bench nano rc=$rc"; if [ $rc -ne 0 ]; then exit $rc; fi
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 $R/bench.py --steps 5 --warmup 1 --cpu-baseline 0 > $O/trace.log 2>&1
