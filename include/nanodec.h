@@ -32,6 +32,8 @@ extern "C" {
 
 #define ND_ENC_TRANSFORMER 0  /* encoder/transformer.py */
 #define ND_ENC_NANO 1         /* encoder/nano_encoder.py (3x BiLSTM) */
+#define ND_SELF_SCALED_DOT 0
+#define ND_SELF_AVERAGE 1
 
 typedef struct nd_ctx nd_ctx;
 
@@ -53,6 +55,8 @@ typedef struct nd_config {
   int32_t max_steps;          /* max_length (100) */
   int32_t max_beam;           /* beam_size upper bound (1 = greedy only) */
   int32_t device;             /* HIP device ordinal */
+  int32_t self_attn_type;     /* decoder self-attention: ND_SELF_SCALED_DOT | ND_SELF_AVERAGE
+                                 (decoder/transformer.py:33-37, onmt/modules/average_attn.py) */
 } nd_config;
 
 /* Replaces models/model_builder.py:load_test_model (:217-233) +

@@ -16,10 +16,12 @@ LIB_PATH = os.environ.get("NANODEC_LIB", os.path.join(HERE, "libnanodec_hip.so")
 
 ND_ENC_TRANSFORMER = 0
 ND_ENC_NANO = 1
+ND_SELF_SCALED_DOT = 0
+ND_SELF_AVERAGE = 1
 
 _CFG_FIELDS = ["encoder_type", "enc_layers", "dec_layers", "d_model", "heads", "d_ff", "vocab", "rnn_hidden",
                "position_encoding", "pad_idx", "bos_idx", "eos_idx", "max_batch", "max_src_len", "max_steps",
-               "max_beam", "device"]
+               "max_beam", "device", "self_attn_type"]
 
 
 class NdConfig(ctypes.Structure):

@@ -121,8 +121,9 @@ def config_from_opt(opt: Dict, itos: List[str]) -> ModelConfig:
                                   "MI355X path (SURVEY.md §2)")
     if o["encoder_type"] not in ("transformer", "nano"):
         raise NotImplementedError(f"encoder_type {o['encoder_type']!r} is not on the MI355X path")
-    if o["self_attn_type"] != "scaled-dot":
-        raise NotImplementedError("self_attn_type 'average' is not supported yet")
+    if o["self_attn_type"] not in ("scaled-dot", "average"):
+        raise NotImplementedError(f"self_attn_type {o['self_attn_type']!r} (decoder/transformer.py:33-37 "
+                                  "knows scaled-dot and average)")
     if o["copy_attn"]:
         raise NotImplementedError("copy_attn models are not supported")
     if o["generator_function"] != "softmax":
@@ -135,7 +136,8 @@ def config_from_opt(opt: Dict, itos: List[str]) -> ModelConfig:
     return ModelConfig(encoder_type=o["encoder_type"], enc_layers=int(o["enc_layers"]),
                        dec_layers=int(o["dec_layers"]), d_model=int(o["dec_rnn_size"]), heads=int(o["heads"]),
                        d_ff=int(o["transformer_ff"]), rnn_hidden=int(o["enc_rnn_size"]) // 2,
-                       position_encoding=bool(o["position_encoding"]), itos=itos)
+                       position_encoding=bool(o["position_encoding"]), self_attn_type=o["self_attn_type"],
+                       itos=itos)
 
 
 def _np(t) -> np.ndarray:
@@ -171,7 +173,7 @@ def save_synthetic(path: str, cfg: ModelConfig, W: Dict[str, np.ndarray]):
                dec_layers=cfg.dec_layers, enc_rnn_size=(2 * cfg.rnn_hidden if cfg.encoder_type == "nano"
                                                         else cfg.d_model),
                dec_rnn_size=cfg.d_model, rnn_size=-1, heads=cfg.heads, transformer_ff=cfg.d_ff,
-               position_encoding=cfg.position_encoding, self_attn_type="scaled-dot", copy_attn=False,
+               position_encoding=cfg.position_encoding, self_attn_type=cfg.self_attn_type, copy_attn=False,
                generator_function="softmax", rnn_type="LSTM", audio_enc_pooling="1")
     model = {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in W.items() if not k.startswith("generator.")}
     gen = {k[len("generator."):]: torch.from_numpy(np.ascontiguousarray(v)) for k, v in W.items()

@@ -65,6 +65,12 @@ struct DecLayer {
   // memory-bank context attention (greedy): ctx K folded into the query
   // projection, ctx V into the output projection (derived at finalize, f64)
   float *pwqk, *bqk, *pwvo, *bvo;
+  // average self-attention (onmt/modules/average_attn.py): average_layer FFN
+  // (LN + 256 -> 256 -> 256) and gating Linear(512, 512); derived: LN-folded
+  // P16 w_1, P16 w_2, the gate's xn / a column halves P16
+  float *aln_g = nullptr, *aln_b = nullptr, *aw1 = nullptr, *ab1 = nullptr, *aw2 = nullptr, *ab2 = nullptr,
+        *gw = nullptr, *gb = nullptr;
+  float *naw1 = nullptr, *nab1 = nullptr, *paw1 = nullptr, *paw2 = nullptr, *pgwx = nullptr, *pgwa = nullptr;
 };
 struct NanoLayer {
   float *wih, *bih, *bhh, *whh, *bn_g, *bn_b, *bn_rm, *bn_rv;  // raw
@@ -111,6 +117,9 @@ struct nd_ctx {
   float* mem_p = nullptr;                 // memory bank [B * T, 256] row-major (LN'd encoder output)
   const float* mem = nullptr;             // the bank the decoder reads: mem_p, or x (NanoEncoder)
   float *dqk = nullptr, *dU = nullptr;    // [R, 8*256] P16 (memory-bank path)
+  // average self-attention step buffers (P16): xn, avg (+ its row stats), the
+  // average_layer hidden, a = FFN(avg), the gate pre-activations [R, 512]
+  float *axn = nullptr, *aavg = nullptr, *aavg_part = nullptr, *ah = nullptr, *aa = nullptr, *ag = nullptr;
   float *nano_xp = nullptr, *nano_h = nullptr;
   float *x_part = nullptr, *y_part = nullptr, *dx_part = nullptr, *dq1_part = nullptr, *dmid_part = nullptr;
   int x_pn = 1;
@@ -238,13 +247,29 @@ static int build_registry(nd_ctx* c) {
     add_slot(c, p + ".layer_norm_1.bias", L.ln1_b, {D});
     add_slot(c, p + ".layer_norm_2.weight", L.ln2_g, {D});
     add_slot(c, p + ".layer_norm_2.bias", L.ln2_b, {D});
-    const char* qkv[3] = {"linear_query", "linear_keys", "linear_values"};
-    for (int k = 0; k < 3; ++k) {
-      add_slot(c, p + ".self_attn." + qkv[k] + ".weight", L.wqkv + (size_t)k * D * D, {D, D});
-      add_slot(c, p + ".self_attn." + qkv[k] + ".bias", L.bqkv + k * D, {D});
+    if (cfg.self_attn_type == ND_SELF_AVERAGE) {
+      AL(L.aln_g, D); AL(L.aln_b, D); AL(L.aw1, D * D); AL(L.ab1, D); AL(L.aw2, D * D); AL(L.ab2, D);
+      AL(L.gw, 4 * D * D); AL(L.gb, 2 * D);
+      AL(L.naw1, D * D); AL(L.nab1, D); AL(L.paw1, D * D); AL(L.paw2, D * D); AL(L.pgwx, 2 * D * D);
+      AL(L.pgwa, 2 * D * D);
+      const std::string a = p + ".self_attn.";
+      add_slot(c, a + "average_layer.layer_norm.weight", L.aln_g, {D});
+      add_slot(c, a + "average_layer.layer_norm.bias", L.aln_b, {D});
+      add_slot(c, a + "average_layer.w_1.weight", L.aw1, {D, D});
+      add_slot(c, a + "average_layer.w_1.bias", L.ab1, {D});
+      add_slot(c, a + "average_layer.w_2.weight", L.aw2, {D, D});
+      add_slot(c, a + "average_layer.w_2.bias", L.ab2, {D});
+      add_slot(c, a + "gating_layer.weight", L.gw, {2 * D, 2 * D});
+      add_slot(c, a + "gating_layer.bias", L.gb, {2 * D});
+    } else {
+      const char* qkv[3] = {"linear_query", "linear_keys", "linear_values"};
+      for (int k = 0; k < 3; ++k) {
+        add_slot(c, p + ".self_attn." + qkv[k] + ".weight", L.wqkv + (size_t)k * D * D, {D, D});
+        add_slot(c, p + ".self_attn." + qkv[k] + ".bias", L.bqkv + k * D, {D});
+      }
+      add_slot(c, p + ".self_attn.final_linear.weight", L.wo, {D, D});
+      add_slot(c, p + ".self_attn.final_linear.bias", L.bo, {D});
     }
-    add_slot(c, p + ".self_attn.final_linear.weight", L.wo, {D, D});
-    add_slot(c, p + ".self_attn.final_linear.bias", L.bo, {D});
     add_slot(c, p + ".context_attn.linear_query.weight", L.cwq, {D, D});
     add_slot(c, p + ".context_attn.linear_query.bias", L.cbq, {D});
     add_slot(c, p + ".context_attn.linear_keys.weight", c->ctxkv_w + (size_t)(2 * i) * D * D, {D, D});
@@ -315,6 +340,14 @@ static int alloc_workspaces(nd_ctx* c) {
   WS(c->dhid, R * F);
   WS(c->dqk, R * ND_H * D);
   WS(c->dU, R * ND_H * D);
+  if (cfg.self_attn_type == ND_SELF_AVERAGE) {
+    WS(c->axn, R * D);
+    WS(c->aavg, R * D);
+    WS(c->aavg_part, R * ND_PART_LD * 2);
+    WS(c->ah, R * D);
+    WS(c->aa, R * D);
+    WS(c->ag, R * 2 * D);
+  }
   WS(c->cache, Ld * R * S * 2 * D);
   WS(c->tok, R);
   WS(c->gtok, B * S);
@@ -443,9 +476,21 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
     unsigned long long* stamp = c->kstamp_on ? c->kstamp + 2 * ((size_t)step * Ld + i) : nullptr;
     // decoder/transformer.py:53-95
     // all step activations are P16-packed (kernels.hpp)
-    LCHK(G(c->dx, D, L.pwqkv, 3 * D, D, L.nbqkv, c->dqkv, 3 * D, R).p16().ln(c->dx_part, pnx).run(s));
-    LCHK(nd::launch_dec_self_attention(c->dqkv, cache, anc, anc_ld, step, S, c->datt, R, s));
-    LCHK(G(c->datt, D, L.pwo, D, D, L.bo, c->dq1, D, R).p16().res(c->dx, D).stats(c->dq1_part).run(s, &pnq));
+    if (c->cfg.self_attn_type == ND_SELF_AVERAGE) {
+      // average_attn.py:55-106 + the layer residual (decoder/transformer.py:82-86)
+      LCHK(nd::launch_aan_prep(c->dx, L.ln1_g, L.ln1_b, cache, anc, anc_ld, step, S, c->axn, c->aavg, c->aavg_part,
+                               R, s));
+      LCHK(G(c->aavg, D, L.paw1, D, D, L.nab1, c->ah, D, R).p16().ln(c->aavg_part, 1).relu().run(s));
+      LCHK(G(c->ah, D, L.paw2, D, D, L.ab2, c->aa, D, R).p16().res(c->aavg, D).run(s));
+      LCHK(G(c->axn, D, L.pgwx, 2 * D, D, L.gb, c->ag, 2 * D, R).p16().run(s));
+      LCHK(G(c->aa, D, L.pgwa, 2 * D, D, nullptr, c->ag, 2 * D, R).p16().res(c->ag, 2 * D).run(s));
+      LCHK(nd::launch_aan_gate(c->ag, c->axn, c->aa, c->dx, c->dq1, c->dq1_part, R, s));
+      pnq = 1;
+    } else {
+      LCHK(G(c->dx, D, L.pwqkv, 3 * D, D, L.nbqkv, c->dqkv, 3 * D, R).p16().ln(c->dx_part, pnx).run(s));
+      LCHK(nd::launch_dec_self_attention(c->dqkv, cache, anc, anc_ld, step, S, c->datt, R, s));
+      LCHK(G(c->datt, D, L.pwo, D, D, L.bo, c->dq1, D, R).p16().res(c->dx, D).stats(c->dq1_part).run(s, &pnq));
+    }
     if (mb) {  // memory-bank form (attention.hip)
       const int HD = ND_H * D;
       LCHK(G(c->dq1, D, L.pwqk, HD, D, L.bqk, c->dqk, HD, R).p16().ln(c->dq1_part, pnq).run(s));
@@ -553,6 +598,8 @@ int nd_create(const nd_config* cfg, nd_ctx** out) {
   if (cfg->encoder_type != ND_ENC_TRANSFORMER && cfg->encoder_type != ND_ENC_NANO)
     return fail(ND_ERR_ARG, "unknown encoder_type");
   if (cfg->encoder_type == ND_ENC_NANO && cfg->rnn_hidden != 128) return fail(ND_ERR_ARG, "rnn_hidden must be 128");
+  if (cfg->self_attn_type != ND_SELF_SCALED_DOT && cfg->self_attn_type != ND_SELF_AVERAGE)
+    return fail(ND_ERR_ARG, "unknown self_attn_type");
   HIPCHK(hipSetDevice(cfg->device));
   nd_ctx* c = new nd_ctx();
   c->cfg = *cfg;
@@ -737,11 +784,19 @@ int nd_finalize(nd_ctx* c) {
       HIPCHK(fold(c->ctxkv_w, c->ctxkv_b, c->enc_ln_g, c->enc_ln_b, c->nctxkv_w, c->nctxkv_b,
                   (int)c->dec.size() * 2 * D, D));
     for (auto& L : c->dec) {
-      HIPCHK(fold(L.wqkv, L.bqkv, L.ln1_g, L.ln1_b, L.nwqkv, L.nbqkv, 3 * D, D));
+      if (c->cfg.self_attn_type == ND_SELF_AVERAGE) {
+        HIPCHK(fold(L.aw1, L.ab1, L.aln_g, L.aln_b, L.naw1, L.nab1, D, D));
+        HIPCHK(nd::launch_pack_p16(L.naw1, D, L.paw1, D, D, c->es));
+        HIPCHK(nd::launch_pack_p16(L.aw2, D, L.paw2, D, D, c->es));
+        HIPCHK(nd::launch_pack_p16(L.gw, 2 * D, L.pgwx, 2 * D, D, c->es));      // gate columns of xn
+        HIPCHK(nd::launch_pack_p16(L.gw + D, 2 * D, L.pgwa, 2 * D, D, c->es));  // gate columns of a
+      } else {
+        HIPCHK(fold(L.wqkv, L.bqkv, L.ln1_g, L.ln1_b, L.nwqkv, L.nbqkv, 3 * D, D));
+        HIPCHK(nd::launch_pack_p16(L.nwqkv, D, L.pwqkv, 3 * D, D, c->es));
+        HIPCHK(nd::launch_pack_p16(L.wo, D, L.pwo, D, D, c->es));
+      }
       HIPCHK(fold(L.cwq, L.cbq, L.ln2_g, L.ln2_b, L.ncwq, L.ncbq, D, D));
       HIPCHK(fold(L.w1, L.b1, L.fln_g, L.fln_b, L.nw1, L.nb1, F, D));
-      HIPCHK(nd::launch_pack_p16(L.nwqkv, D, L.pwqkv, 3 * D, D, c->es));
-      HIPCHK(nd::launch_pack_p16(L.wo, D, L.pwo, D, D, c->es));
       HIPCHK(nd::launch_pack_p16(L.ncwq, D, L.pcwq, D, D, c->es));
       HIPCHK(nd::launch_pack_p16(L.cwo, D, L.pcwo, D, D, c->es));
       HIPCHK(nd::launch_pack_p16(L.nw1, D, L.pw1, F, D, c->es));

@@ -102,6 +102,14 @@ hipError_t launch_stamp_reset(unsigned long long* stamps, int pairs, hipStream_t
 hipError_t launch_memory_pack(const float* x, const float* ln_g, const float* ln_b, float* out, int B, int T, int ldT,
                               hipStream_t s);
 hipError_t init_mem_attributes();
+// average self-attention (aan.hip): xn = LN_1(x), avg = (xn + step prev) / (step + 1)
+// (prev from hist[anc[r][step-1]][step-1], avg stored at hist[r][step]), avg's
+// row statistics (one partial); then q1 = sig(g_in) xn + sig(g_f) a + x (+ stats)
+hipError_t launch_aan_prep(const float* x, const float* ln_g, const float* ln_b, float* hist, const int* anc,
+                           int anc_ld, int step, int max_steps, float* xn, float* avg, float* avg_part, int R,
+                           hipStream_t s);
+hipError_t launch_aan_gate(const float* g, const float* xn, const float* a, const float* x, float* out, float* part,
+                           int R, hipStream_t s);
 // greedy head: LN_dec -> generator -> log_softmax -> argmax; writes token
 // (next input + output [R, S] at column step), score, optional logp dump,
 // and the next step's embedded input (ne).

@@ -34,6 +34,7 @@ class Engine:
         L = _lib.lib()
         c = _lib.NdConfig()
         c.encoder_type = _lib.ND_ENC_TRANSFORMER if cfg.encoder_type == "transformer" else _lib.ND_ENC_NANO
+        c.self_attn_type = _lib.ND_SELF_AVERAGE if cfg.self_attn_type == "average" else _lib.ND_SELF_SCALED_DOT
         c.enc_layers, c.dec_layers = cfg.enc_layers, cfg.dec_layers
         c.d_model, c.heads, c.d_ff, c.vocab = cfg.d_model, cfg.heads, cfg.d_ff, cfg.vocab
         c.rnn_hidden = cfg.rnn_hidden

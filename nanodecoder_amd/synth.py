@@ -38,6 +38,7 @@ class ModelConfig:
     d_ff: int = 2048
     rnn_hidden: int = 128               # per direction, NanoEncoder only
     position_encoding: bool = False     # models/opts.py:41-44 (off by default)
+    self_attn_type: str = "scaled-dot"  # decoder self-attention: "scaled-dot" | "average" (AAN)
     itos: List[str] = dataclasses.field(default_factory=lambda: list(DEFAULT_ITOS))
 
     @property
@@ -145,7 +146,12 @@ def make_weights(cfg: ModelConfig, seed: int = 0, eos_bias: float = 0.0) -> Dict
         W["decoder.embeddings.make_embedding.pe.pe"] = positional_table(d)
     for i in range(cfg.dec_layers):
         p = f"decoder.transformer_layers.{i}"
-        _mha(rng, W, p + ".self_attn", d)
+        if cfg.self_attn_type == "average":
+            # onmt/modules/average_attn.py:26-29: PositionwiseFeedForward(d, d) + Linear(2d, 2d)
+            _ffn(rng, W, p + ".self_attn.average_layer", d, d)
+            _linear(rng, W, p + ".self_attn.gating_layer", 2 * d, 2 * d)
+        else:
+            _mha(rng, W, p + ".self_attn", d)
         _mha(rng, W, p + ".context_attn", d)
         W[p + ".layer_norm_1.weight"], W[p + ".layer_norm_1.bias"] = _ln(rng, d)
         W[p + ".layer_norm_2.weight"], W[p + ".layer_norm_2.bias"] = _ln(rng, d)

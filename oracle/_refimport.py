@@ -58,6 +58,8 @@ def load_reference():
     mha = _load("onmt.modules.multi_headed_attn", "onmt/modules/multi_headed_attn.py")
     sys.modules["onmt.modules"].MultiHeadedAttention = mha.MultiHeadedAttention
     _load("onmt.modules.position_ffn", "onmt/modules/position_ffn.py")
+    aan = _load("onmt.modules.average_attn", "onmt/modules/average_attn.py")
+    sys.modules["onmt.modules"].AverageAttention = aan.AverageAttention
     util_class = _load("onmt.modules.util_class", "onmt/modules/util_class.py")
     sys.modules["onmt.modules"].Elementwise = util_class.Elementwise
     emb = _load("onmt.modules.embeddings", "onmt/modules/embeddings.py")

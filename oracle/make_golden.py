@@ -57,7 +57,7 @@ def build_reference_model(ns, cfg: synth.ModelConfig, W):
                              0.0, 4000, 0.075, 1)
     emb = ns.Embeddings(d, cfg.vocab, cfg.pad_idx, position_encoding=cfg.position_encoding)
     dec = ns.TransformerDecoder(cfg.dec_layers, d, cfg.heads, cfg.d_ff, "general", False,
-                                "scaled-dot", 0.0, emb)
+                                cfg.self_attn_type, 0.0, emb)
     gen = nn.Sequential(nn.Linear(d, cfg.vocab), nn.LogSoftmax(dim=-1))
     model = nn.Module()
     model.encoder, model.decoder = enc, dec
@@ -194,6 +194,10 @@ SCENARIOS = [
          beam2=dict(beam_size=5, n_best=3, max_length=60, min_length=10)),
     dict(name="nano_greedy", cfg=dict(encoder_type="nano"), seed=14, eos_bias=-2.0,
          chunks=dict(kind="mixed"), greedy=dict(max_length=60)),
+    # decoder with average self-attention (onmt/modules/average_attn.py), greedy and --fast beam
+    dict(name="transformer_aan", cfg=dict(encoder_type="transformer", self_attn_type="average"), seed=15,
+         eos_bias=1.5, chunks=dict(kind="mixed"), greedy=dict(max_length=60),
+         beam=dict(beam_size=4, n_best=2, max_length=50, min_length=5)),
 ]
 
 
@@ -215,13 +219,20 @@ def scenario_chunks(kind, seed):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=GOLDEN_DIR)
+    ap.add_argument("--only", nargs="*", help="regenerate only these scenarios (index.json is merged)")
     args = ap.parse_args()
     os.makedirs(args.out, exist_ok=True)
     torch.manual_seed(0)
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     ns = load_reference()
     index = {}
+    ipath = os.path.join(args.out, "index.json")
+    if args.only and os.path.exists(ipath):
+        with open(ipath) as f:
+            index = json.load(f)
     for sc in SCENARIOS:
+        if args.only and sc["name"] not in args.only:
+            continue
         cfg = synth.ModelConfig(**sc["cfg"])
         W = synth.make_weights(cfg, seed=sc["seed"], eos_bias=sc["eos_bias"])
         model = build_reference_model(ns, cfg, W)
@@ -251,7 +262,7 @@ def main():
         np.savez_compressed(path, **out)
         index[sc["name"]] = meta
         print(f"wrote {path} ({os.path.getsize(path)} B)")
-    with open(os.path.join(args.out, "index.json"), "w") as f:
+    with open(ipath, "w") as f:
         json.dump(index, f, indent=1, sort_keys=True)
 
 

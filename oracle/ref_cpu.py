@@ -147,14 +147,29 @@ class RefModel:
         """decoder/transformer.py:173-176,248-266 + context K/V projected at
         step 0 (multi_headed_attn.py:142-153)."""
         st = {"src": src, "memory": memory, "ctx_k": [], "ctx_v": [], "self_k": [], "self_v": [],
-              "len": 0}
+              "prev_g": [], "len": 0}
         for i in range(self.cfg.dec_layers):
             a = f"decoder.transformer_layers.{i}.context_attn"
             st["ctx_k"].append(self._heads(self.lin(memory, a + ".linear_keys")))
             st["ctx_v"].append(self._heads(self.lin(memory, a + ".linear_values")))
             st["self_k"].append(None)
             st["self_v"].append(None)
+            # average self-attention cache (decoder/transformer.py:262-263)
+            st["prev_g"].append(torch.zeros(memory.shape[0], 1, self.d))
         return st
+
+    def average_attention(self, st, i, h, step):
+        """onmt/modules/average_attn.py:55-106 with a layer cache:
+        avg = (h + step * prev_g) / (step + 1); a = FFN(avg);
+        out = sigmoid(g_in) * h + sigmoid(g_forget) * a, [g_in; g_forget] =
+        gating_layer([h; a])."""
+        a = f"decoder.transformer_layers.{i}.self_attn"
+        avg = (h + step * st["prev_g"][i]) / (step + 1)
+        st["prev_g"][i] = avg
+        ao = self.ffn(avg, a + ".average_layer")
+        g = self.lin(torch.cat((h, ao), -1), a + ".gating_layer")
+        gi, gf = torch.chunk(g, 2, dim=2)
+        return torch.sigmoid(gi) * h + torch.sigmoid(gf) * ao
 
     def decode_step(self, st, tok, step):
         """decoder/transformer.py:194-246 for one step + generator
@@ -169,15 +184,18 @@ class RefModel:
             p = f"decoder.transformer_layers.{i}"
             h = self.ln(x, p + ".layer_norm_1")
             a = p + ".self_attn"
-            q = self._heads(self.lin(h, a + ".linear_query"))
-            k = self._heads(self.lin(h, a + ".linear_keys"))
-            v = self._heads(self.lin(h, a + ".linear_values"))
-            if st["self_k"][i] is not None:                         # cache cat (mha.py:132-141)
-                k = torch.cat([st["self_k"][i], k], dim=2)
-                v = torch.cat([st["self_v"][i], v], dim=2)
-            st["self_k"][i], st["self_v"][i] = k, v
-            c, _ = self.attend(q, k, v, None)
-            q1 = self.lin(self._unheads(c), a + ".final_linear") + x
+            if cfg.self_attn_type == "average":                     # (:82-84)
+                q1 = self.average_attention(st, i, h, step) + x
+            else:
+                q = self._heads(self.lin(h, a + ".linear_query"))
+                k = self._heads(self.lin(h, a + ".linear_keys"))
+                v = self._heads(self.lin(h, a + ".linear_values"))
+                if st["self_k"][i] is not None:                     # cache cat (mha.py:132-141)
+                    k = torch.cat([st["self_k"][i], k], dim=2)
+                    v = torch.cat([st["self_v"][i], v], dim=2)
+                st["self_k"][i], st["self_v"][i] = k, v
+                c, _ = self.attend(q, k, v, None)
+                q1 = self.lin(self._unheads(c), a + ".final_linear") + x
             h2 = self.ln(q1, p + ".layer_norm_2")
             ca = p + ".context_attn"
             qc = self._heads(self.lin(h2, ca + ".linear_query"))
@@ -191,7 +209,7 @@ class RefModel:
     def reorder(self, st, idx):
         """map_state(index_select) (decoder/transformer.py:178-189)."""
         st["src"] = st["src"].index_select(0, idx)
-        for key in ("ctx_k", "ctx_v", "self_k", "self_v"):
+        for key in ("ctx_k", "ctx_v", "self_k", "self_v", "prev_g"):
             st[key] = [t.index_select(0, idx) if t is not None else None for t in st[key]]
 
 

@@ -5,7 +5,7 @@ import os
 import numpy as np
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-NAMES = ["transformer_greedy", "transformer_pe_short", "transformer_beam", "nano_greedy"]
+NAMES = ["transformer_greedy", "transformer_pe_short", "transformer_beam", "nano_greedy", "transformer_aan"]
 
 
 def load(name):

@@ -90,7 +90,13 @@ def test_unsupported_model_opts_raise():
         checkpoint.config_from_opt({"encoder_type": "transformer", "decoder_type": "rnn"}, synth.DEFAULT_ITOS)
     with pytest.raises(NotImplementedError):
         checkpoint.config_from_opt({"encoder_type": "transformer", "decoder_type": "transformer",
-                                    "self_attn_type": "average"}, synth.DEFAULT_ITOS)
+                                    "self_attn_type": "relative"}, synth.DEFAULT_ITOS)
+
+
+def test_average_self_attention_opt_maps_to_config():
+    cfg = checkpoint.config_from_opt({"encoder_type": "transformer", "decoder_type": "transformer",
+                                      "self_attn_type": "average"}, synth.DEFAULT_ITOS)
+    assert cfg.self_attn_type == "average"
 
 
 def test_window_matches_labelop_rules():

@@ -181,7 +181,7 @@ def test_encoder_memory_vs_golden(name):
     assert np.abs(sub - z["memory_sub"]).max() < 1e-4
 
 
-@pytest.mark.parametrize("name", ["transformer_greedy", "transformer_pe_short", "nano_greedy"])
+@pytest.mark.parametrize("name", ["transformer_greedy", "transformer_pe_short", "nano_greedy", "transformer_aan"])
 @pytest.mark.parametrize("graphs,ctx_path", [(True, 0), (False, 0), (True, 1)])
 def test_greedy_vs_golden(name, graphs, ctx_path):
     """ctx_path 0: memory-bank context attention, 1: per-layer K/V form."""
@@ -203,9 +203,12 @@ def test_greedy_vs_golden(name, graphs, ctx_path):
     assert np.abs(r["scores"].cpu().numpy() - z["scores"]).max() < LOGP_ATOL
 
 
-@pytest.mark.parametrize("which", ["", "2"])
-def test_beam_vs_golden(which):
-    z, meta = gu.load("transformer_beam")
+@pytest.mark.parametrize("name,which", [("transformer_beam", ""), ("transformer_beam", "2"),
+                                        ("transformer_aan", "")])
+def test_beam_vs_golden(name, which):
+    """--fast beam (average self-attention included: its running average
+    follows the beam ancestry)."""
+    z, meta = gu.load(name)
     cfg, W = gu.model_for(meta)
     kw = meta["beam" + which]
     eng = _engine(cfg, W, max_batch=8, max_steps=kw["max_length"], max_beam=kw["beam_size"])

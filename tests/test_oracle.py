@@ -20,7 +20,7 @@ def test_weights_regenerate_identically(name):
     assert weights_digest(W) == meta["weights_sha256"]
 
 
-@pytest.mark.parametrize("name", ["transformer_greedy", "transformer_pe_short", "nano_greedy"])
+@pytest.mark.parametrize("name", ["transformer_greedy", "transformer_pe_short", "nano_greedy", "transformer_aan"])
 def test_greedy_matches_reference(name):
     z, meta = gu.load(name)
     cfg, W = gu.model_for(meta)
@@ -36,9 +36,10 @@ def test_greedy_matches_reference(name):
     np.testing.assert_allclose(mem, z["memory_sub"], atol=1e-5)
 
 
-@pytest.mark.parametrize("which", ["", "2"])
-def test_fast_beam_matches_reference(which):
-    z, meta = gu.load("transformer_beam")
+@pytest.mark.parametrize("name,which", [("transformer_beam", ""), ("transformer_beam", "2"),
+                                        ("transformer_aan", "")])
+def test_fast_beam_matches_reference(name, which):
+    z, meta = gu.load(name)
     cfg, W = gu.model_for(meta)
     m = ref_cpu.RefModel(cfg, W)
     chunks = gu.chunks_of(z)
