@@ -80,9 +80,18 @@ def load_reference():
         sys.modules[name] = m
         return m
 
+    # onmt/translate/{penalties,beam}.py for the classic (non --fast) Beam path
+    _pkg("onmt.translate", os.path.join(REF, "onmt/translate"))
+    sys.modules["onmt"].translate = sys.modules["onmt.translate"]
+    pen = _load("onmt.translate.penalties", "onmt/translate/penalties.py")
+    sys.modules["onmt.translate"].penalties = pen
+    beam = _load("onmt.translate.beam", "onmt/translate/beam.py")
+    sys.modules["onmt.translate"].beam = beam
+    sys.modules["onmt.translate"].Beam = beam.Beam
+    sys.modules["onmt.translate"].GNMTGlobalScorer = beam.GNMTGlobalScorer
     for name in ("configargparse", "matplotlib", "matplotlib.pyplot", "models", "models.model_builder",
                  "models.opts", "utils", "utils.labelop", "translate", "translate.translation",
-                 "onmt.translate", "onmt.translate.beam", "onmt.decoders", "onmt.decoders.ensemble"):
+                 "onmt.decoders", "onmt.decoders.ensemble"):
         if name not in sys.modules:
             stub(name)
     sys.modules["utils.labelop"].extract_fast5_raw = None
@@ -90,9 +99,6 @@ def load_reference():
     stub("inputters.inputter", make_features=lambda b, side, data_type="text": getattr(b, side))
     sys.modules["inputters"].inputter = sys.modules["inputters.inputter"]
     sys.modules["translate.translation"].TranslationBuilder = object
-    sys.modules["onmt.translate.beam"].GNMTGlobalScorer = object
-    sys.modules["onmt.translate"].beam = sys.modules["onmt.translate.beam"]
-    sys.modules["onmt.translate"].GNMTGlobalScorer = object
     translator = _load("translate.translator", "translate/translator.py")
 
     ns = types.SimpleNamespace(
@@ -101,6 +107,7 @@ def load_reference():
         TransformerDecoder=dec_t.TransformerDecoder,
         Embeddings=emb.Embeddings,
         Translator=translator.Translator,
+        GNMTGlobalScorer=beam.GNMTGlobalScorer,
         tile=misc.tile,
     )
     _LOADED["ns"] = ns

@@ -83,15 +83,20 @@ class _Field:
         self.pad_token, self.unk_token = "<blank>", "<unk>"
 
 
-def make_translator(ns, model, cfg, beam_size, n_best=1, max_length=100, min_length=0, alpha=0.0):
+def make_translator(ns, model, cfg, beam_size, n_best=1, max_length=100, min_length=0, alpha=0.0, fast=True,
+                    length_penalty="none"):
     opt = types.SimpleNamespace(
         gpu=-1, n_best=n_best, max_length=max_length, beam_size=beam_size,
         random_sampling_temp=1.0, random_sampling_topk=1, min_length=min_length,
         stepwise_penalty=False, dump_beam="", block_ngram_repeat=0, ignore_when_blocking=[],
         fft=False, sample_rate=4000, window_size=0.075, window_stride=0.015, window="hamming",
-        replace_unk=False, data_type="nano", verbose=False, fast=True)
+        replace_unk=False, data_type="nano", verbose=False, fast=fast)
     model_opt = types.SimpleNamespace(copy_attn=False)
-    scorer = types.SimpleNamespace(alpha=alpha, beta=0.0)
+    if fast:
+        scorer = types.SimpleNamespace(alpha=alpha, beta=0.0)
+    else:  # onmt/translate/beam.py:181-199 (the real scorer drives the classic Beam)
+        scorer = ns.GNMTGlobalScorer(types.SimpleNamespace(alpha=alpha, beta=0.0, coverage_penalty="none",
+                                                           length_penalty=length_penalty))
     return ns.Translator(model, {"tgt": _Field(cfg.itos)}, opt, model_opt, global_scorer=scorer,
                          report_score=False, logger=None)
 
@@ -183,6 +188,46 @@ def run_beam(ns, model, cfg, chunks, beam_size=5, n_best=1, max_length=100, min_
     return dict(beam_tokens=tokens[inv], beam_lens=lens[inv], beam_scores=scores[inv])
 
 
+@contextlib.contextmanager
+def floor_int_truediv():
+    """onmt/translate/beam.py:129 divides LongTensors with '/', integer
+    division in torch 1.0 (true division since torch 1.5)."""
+    orig = torch.Tensor.__truediv__
+
+    def truediv(self, other):
+        if not self.is_floating_point() and isinstance(other, int):
+            return torch.div(self, other, rounding_mode="floor")
+        return orig(self, other)
+
+    torch.Tensor.__truediv__ = truediv
+    try:
+        yield
+    finally:
+        torch.Tensor.__truediv__ = orig
+
+
+def run_classic_beam(ns, model, cfg, chunks, beam_size=5, n_best=1, max_length=100, min_length=0, alpha=0.0,
+                     length_penalty="none"):
+    """translate/translator.py:827-926 (_translate_batch, the onmt Beam)."""
+    tr = make_translator(ns, model, cfg, beam_size=beam_size, n_best=n_best, max_length=max_length,
+                         min_length=min_length, alpha=alpha, fast=False, length_penalty=length_penalty)
+    batch, order = make_batch(chunks)
+    with torch.no_grad(), floor_int_div(), floor_int_truediv():
+        res = tr._translate_batch(batch, types.SimpleNamespace(data_type="nano"))
+    B = len(chunks)
+    inv = np.argsort(order)
+    tokens = np.full((B, n_best, max_length), -1, np.int32)
+    lens = np.zeros((B, n_best), np.int32)
+    scores = np.zeros((B, n_best), np.float32)
+    for j in range(B):
+        for n in range(n_best):
+            p = np.array([int(t) for t in res["predictions"][j][n]], np.int32)
+            tokens[j, n, : len(p)] = p
+            lens[j, n] = len(p)
+            scores[j, n] = float(res["scores"][j][n])
+    return dict(beam_tokens=tokens[inv], beam_lens=lens[inv], beam_scores=scores[inv])
+
+
 SCENARIOS = [
     # name, model config kwargs, weight seed, eos_bias, chunk spec, runs
     dict(name="transformer_greedy", cfg=dict(encoder_type="transformer"), seed=11, eos_bias=-3.0,
@@ -195,6 +240,13 @@ SCENARIOS = [
     dict(name="nano_greedy", cfg=dict(encoder_type="nano"), seed=14, eos_bias=-2.0,
          chunks=dict(kind="mixed"), greedy=dict(max_length=60)),
     # decoder with average self-attention (onmt/modules/average_attn.py), greedy and --fast beam
+    # the classic onmt Beam (no --fast): length penalties none / wu, n_best 1 and 3
+    dict(name="transformer_classic_beam", cfg=dict(encoder_type="transformer"), seed=16, eos_bias=2.5,
+         chunks=dict(kind="mixed"), classic=dict(beam_size=5, n_best=1, max_length=100),
+         classic2=dict(beam_size=4, n_best=3, max_length=60, min_length=10, alpha=0.6, length_penalty="wu")),
+    dict(name="transformer_classic_beam_mid", cfg=dict(encoder_type="transformer"), seed=17, eos_bias=1.0,
+         chunks=dict(kind="mixed"), classic=dict(beam_size=5, n_best=2, max_length=60, min_length=8,
+                                                 length_penalty="avg")),
     dict(name="transformer_aan", cfg=dict(encoder_type="transformer", self_attn_type="average"), seed=15,
          eos_bias=1.5, chunks=dict(kind="mixed"), greedy=dict(max_length=60),
          beam=dict(beam_size=4, n_best=2, max_length=50, min_length=5)),
@@ -253,8 +305,13 @@ def main():
         if "beam2" in sc:
             b = run_beam(ns, model, cfg, chunks, **sc["beam2"])
             out.update({k + "2": v for k, v in b.items()})
+        for key in ("classic", "classic2"):
+            if key in sc:
+                b = run_classic_beam(ns, model, cfg, chunks, **sc[key])
+                out.update({k.replace("beam", key): v for k, v in b.items()})
         meta = dict(name=sc["name"], cfg=sc["cfg"], seed=sc["seed"], eos_bias=sc["eos_bias"],
                     greedy=sc.get("greedy"), beam=sc.get("beam"), beam2=sc.get("beam2"),
+                    classic=sc.get("classic"), classic2=sc.get("classic2"),
                     mem_stride=MEM_STRIDE, weights_sha256=weights_digest(W),
                     torch=torch.__version__, numpy=np.__version__)
         out["meta"] = np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8)

@@ -307,6 +307,109 @@ def fast_beam(model: RefModel, src, lengths, beam_size=5, n_best=1, max_length=1
     return results
 
 
+def _length_penalty(kind, n_ys, alpha):
+    """onmt/translate/penalties.py:57-78 (the divisor applied to log-probs;
+    n_ys = len(beam.next_ys))."""
+    if kind == "wu":
+        return ((5 + n_ys) ** alpha) / ((5 + 1) ** alpha)
+    if kind == "avg":
+        return float(n_ys)
+    return 1.0
+
+
+class ClassicBeam:
+    """onmt/translate/beam.py:6-178 (``Beam``) with GNMTGlobalScorer
+    (:181-199), coverage penalty 'none', no stepwise penalty, no n-gram
+    blocking."""
+
+    def __init__(self, size, pad, bos, eos, n_best, min_length, length_penalty, alpha):
+        self.size, self._eos, self.n_best, self.min_length = size, eos, n_best, min_length
+        self.lp, self.alpha = length_penalty, alpha
+        self.scores = torch.zeros(size)                       # (:34)
+        self.prev_ks = []
+        self.next_ys = [torch.full((size,), pad, dtype=torch.long)]
+        self.next_ys[0][0] = bos                              # (:41-43)
+        self.eos_top = False
+        self.finished = []
+
+    def global_score(self, scores):                           # (:200-212)
+        return scores / _length_penalty(self.lp, len(self.next_ys), self.alpha)
+
+    def advance(self, word_probs):                            # (:73-150)
+        V = word_probs.size(1)
+        word_probs = word_probs.clone()
+        if len(self.next_ys) < self.min_length:               # (:88-91)
+            word_probs[:, self._eos] = -1e20
+        if len(self.prev_ks) > 0:                             # (:93-99)
+            beam_scores = word_probs + self.scores.unsqueeze(1)
+            for i in range(self.next_ys[-1].size(0)):
+                if int(self.next_ys[-1][i]) == self._eos:
+                    beam_scores[i] = -1e20
+        else:
+            beam_scores = word_probs[0]
+        best_scores, best_ids = beam_scores.reshape(-1).topk(self.size, 0, True, True)   # (:122-123)
+        self.scores = best_scores
+        prev_k = torch.div(best_ids, V, rounding_mode="floor")   # (:129, integer division in torch 1.0)
+        self.prev_ks.append(prev_k)
+        self.next_ys.append(best_ids - prev_k * V)
+        for i in range(self.next_ys[-1].size(0)):             # (:135-139)
+            if int(self.next_ys[-1][i]) == self._eos:
+                s = self.global_score(self.scores)[i]
+                self.finished.append((float(s), len(self.next_ys) - 1, i))
+        if int(self.next_ys[-1][0]) == self._eos:             # (:142-144)
+            self.eos_top = True
+
+    def done(self):                                           # (:146-147)
+        return self.eos_top and len(self.finished) >= self.n_best
+
+    def sort_finished(self, minimum=None):                    # (:149-161)
+        if minimum is not None:
+            i = 0
+            while len(self.finished) < minimum:
+                s = self.global_score(self.scores)[i]
+                self.finished.append((float(s), len(self.next_ys) - 1, i))
+                i += 1
+        self.finished.sort(key=lambda a: -a[0])
+        return [sc for sc, _, _ in self.finished], [(t, k) for _, t, k in self.finished]
+
+    def get_hyp(self, timestep, k):                           # (:163-173)
+        hyp = []
+        for j in range(len(self.prev_ks[:timestep]) - 1, -1, -1):
+            hyp.append(int(self.next_ys[j + 1][k]))
+            k = int(self.prev_ks[j][k])
+        return hyp[::-1]
+
+
+def classic_beam(model: RefModel, src, lengths, beam_size=5, n_best=1, max_length=100, min_length=0,
+                 alpha=0.0, length_penalty="none"):
+    """translate/translator.py:827-926 (``_translate_batch``, beam_size > 1
+    without --fast): one Beam per chunk, the whole batch advances until every
+    beam is done.  Returns per chunk n_best (score, tokens) best-first."""
+    src = _t(src)
+    cfg = model.cfg
+    with torch.no_grad():
+        memory = model.encode(src, lengths)
+        B = src.shape[0]
+        beams = [ClassicBeam(beam_size, cfg.pad_idx, cfg.bos_idx, cfg.eos_idx, n_best, min_length,
+                             length_penalty, alpha) for _ in range(B)]
+        st = model.decoder_state(tile(memory, beam_size), tile(src, beam_size))
+        for i in range(max_length):
+            if all(b.done() for b in beams):                   # (:884-885)
+                break
+            inp = torch.stack([b.next_ys[-1] for b in beams]).view(-1)
+            lp = model.decode_step(st, inp, i).view(B, beam_size, -1)
+            sel = []
+            for j, b in enumerate(beams):
+                b.advance(lp[j])
+                sel.append(b.prev_ks[-1] + j * beam_size)
+            model.reorder(st, torch.cat(sel))
+        out = []
+        for b in beams:                                        # (:914-924)
+            scores, ks = b.sort_finished(minimum=n_best)
+            out.append([(scores[n], np.array(b.get_hyp(t, k), np.int32)) for n, (t, k) in enumerate(ks[:n_best])])
+    return out
+
+
 # ---------------------------------------------------------------------------
 # Translator.translate semantics (batching, ordering, EOS truncation)
 # ---------------------------------------------------------------------------
@@ -336,7 +439,7 @@ def tokens_to_string(tokens, itos, eos_idx):
 
 
 def translate(model: RefModel, chunks: Sequence[np.ndarray], batch_size: int, beam_size=1, n_best=1,
-              max_length=100, min_length=0, alpha=0.0):
+              max_length=100, min_length=0, alpha=0.0, fast=True, length_penalty="none"):
     """translate/translator.py:181-369: consecutive batches of ``batch_size``
     chunks (never across reads), results in input order.  Returns
     (all_scores, all_predictions) like the reference."""
@@ -351,7 +454,11 @@ def translate(model: RefModel, chunks: Sequence[np.ndarray], batch_size: int, be
             for j, i in enumerate(order):
                 per[i] = ([float(r["scores"][j])], [tokens_to_string(r["tokens"][j], itos, eos)])
         else:
-            r = fast_beam(model, src, lengths, beam_size, n_best, max_length, min_length, alpha)
+            if fast:
+                r = fast_beam(model, src, lengths, beam_size, n_best, max_length, min_length, alpha)
+            else:
+                r = classic_beam(model, src, lengths, beam_size, n_best, max_length, min_length, alpha,
+                                 length_penalty)
             for j, i in enumerate(order):
                 per[i] = ([s for s, _ in r[j]], [tokens_to_string(p, itos, eos) for _, p in r[j]])
         for s, p in per:

@@ -5,7 +5,8 @@ import os
 import numpy as np
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-NAMES = ["transformer_greedy", "transformer_pe_short", "transformer_beam", "nano_greedy", "transformer_aan"]
+NAMES = ["transformer_greedy", "transformer_pe_short", "transformer_beam", "nano_greedy", "transformer_aan",
+         "transformer_classic_beam", "transformer_classic_beam_mid"]
 
 
 def load(name):

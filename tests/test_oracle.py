@@ -55,6 +55,27 @@ def test_fast_beam_matches_reference(name, which):
             assert abs(s - z["beam_scores" + which][i, nb]) < 1e-4
 
 
+@pytest.mark.parametrize("name,which", [("transformer_classic_beam", "classic"), ("transformer_classic_beam", "classic2"),
+                                        ("transformer_classic_beam_mid", "classic")])
+def test_classic_beam_matches_reference(name, which):
+    """The onmt Beam path (translate/translator.py:827-926), restated in
+    ref_cpu.ClassicBeam, against the reference's own _translate_batch."""
+    z, meta = gu.load(name)
+    cfg, W = gu.model_for(meta)
+    m = ref_cpu.RefModel(cfg, W)
+    chunks = gu.chunks_of(z)
+    src, lens, order = ref_cpu.make_batch(chunks)
+    kw = meta[which]
+    res = ref_cpu.classic_beam(m, src, lens, **kw)
+    for j, i in enumerate(order):
+        assert len(res[j]) == kw["n_best"]
+        for nb, (s, p) in enumerate(res[j]):
+            L = z[which + "_lens"][i, nb]
+            assert len(p) == L
+            assert (p == z[which + "_tokens"][i, nb, :L]).all()
+            assert abs(s - z[which + "_scores"][i, nb]) < 1e-4
+
+
 def test_translate_batching_and_strings():
     """Translator.translate semantics: batches of batch_size consecutive chunks
     padded to their own longest chunk; strings cut at the first EOS."""
