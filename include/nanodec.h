@@ -105,6 +105,21 @@ int nd_translate_beam(nd_ctx* ctx, const float* d_signal, const int32_t* d_len, 
                       int32_t min_len, int32_t* d_tokens, float* d_scores, int32_t* d_lens, int32_t* d_steps,
                       void* stream);
 
+/* Classic beam search: replaces Translator._translate_batch with the onmt
+ * Beam (translate/translator.py:827-926, onmt/translate/beam.py:6-199; the
+ * path the reference takes for beam_size > 1 without --fast).  d_group [B]
+ * is the reference batch of every chunk (translate() batches batch_size
+ * consecutive chunks of one read): a batch advances all its beams until each
+ * is done, exactly as the reference loop does, however the chunks are packed
+ * into this call.  length_penalty: 0 none, 1 wu, 2 avg (alpha for wu);
+ * coverage penalty none.  Outputs as nd_translate_beam: tokens [B, n_best,
+ * max_len] (-1 padded, EOS included when the hypothesis finished), scores
+ * and lens [B, n_best]; d_steps (nullable) = steps run. */
+int nd_translate_beam_classic(nd_ctx* ctx, const float* d_signal, const int32_t* d_len, const int32_t* d_span,
+                              const int32_t* d_group, int32_t B, int32_t T, int32_t beam, int32_t n_best,
+                              int32_t length_penalty, float alpha, int32_t max_len, int32_t min_len,
+                              int32_t* d_tokens, float* d_scores, int32_t* d_lens, int32_t* d_steps, void* stream);
+
 /* Encoder forward only; writes the memory bank [B, T, d_model] (rows
  * t >= span are unspecified).  Replaces Translator._run_encoder
  * (translate/translator.py:542-559).  Used by parity tests. */

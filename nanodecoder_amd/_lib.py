@@ -39,6 +39,7 @@ SIGNATURES = {
     "nd_finalize": (_I, [_P]),
     "nd_translate_greedy": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P]),
     "nd_translate_beam": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _F, _I, _I, _P, _P, _P, _P, _P]),
+    "nd_translate_beam_classic": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _F, _I, _I, _P, _P, _P, _P, _P]),
     "nd_encode": (_I, [_P, _P, _P, _P, _I, _I, _P, _P]),
     "nd_set_graphs": (_I, [_P, _I]),
     "nd_set_timing": (_I, [_P, _I]),

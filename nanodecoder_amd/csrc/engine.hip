@@ -129,6 +129,7 @@ struct nd_ctx {
   float *gscore = nullptr, *glogp = nullptr;
   nd::BeamState bs{};
   int* steps_done = nullptr;
+  int* group_in = nullptr;  // classic Beam: staged reference-batch ids
   int* h_alive = nullptr;  // pinned
 
   hipStream_t es = nullptr;
@@ -369,6 +370,11 @@ static int alloc_workspaces(nd_ctx* c) {
   WS(c->bs.n_alive, 4);
   WS(c->steps_done, 4);
   c->bs.steps_done = c->steps_done;
+  WS(c->bs.group, B);
+  WS(c->bs.grp_left, B);
+  WS(c->bs.grp_done, B);
+  WS(c->bs.steps_run, B);
+  WS(c->group_in, B);
   WS(c->kstamp, Ld * S * 2);
 #undef WS
   if ((e = hipHostMalloc((void**)&c->h_alive, 16, hipHostMallocDefault)) != hipSuccess)
@@ -545,6 +551,16 @@ static hipError_t enqueue_beam_steps(nd_ctx* c, int B, int T, int beam, int n_be
     const float lenpen = (float)std::pow((5.0 + (step + 1)) / 6.0, (double)alpha);
     LCHK(nd::launch_beam_step(next_embed(c), c->dx, c->dec_ln_g, c->dec_ln_b, c->gen_w, c->gen_b, c->V, c->bs, B, beam, n_best,
                               step, S, min_len, c->cfg.eos_idx, lenpen, s));
+  }
+  return hipSuccess;
+}
+
+static hipError_t enqueue_classic_steps(nd_ctx* c, int B, int T, int beam, int n_best, int lpk, float alpha, int S,
+                                        int min_len, int s0, int s1, hipStream_t s) {
+  for (int step = s0; step < s1; ++step) {
+    LCHK(enqueue_dec_step(c, B, beam, T, step, c->bs.anc[step & 1], S, s));
+    LCHK(nd::launch_beam_classic_step(next_embed(c), c->dx, c->dec_ln_g, c->dec_ln_b, c->gen_w, c->gen_b, c->V, c->bs,
+                                      B, beam, n_best, step, S, min_len, c->cfg.eos_idx, lpk, alpha, s));
   }
   return hipSuccess;
 }
@@ -915,6 +931,54 @@ int nd_translate_beam(nd_ctx* c, const float* d_signal, const int32_t* d_len, co
     HIPCHK(hipEventElapsedTime(&c->t_enc, c->ev_a, c->ev_b));
     HIPCHK(hipEventElapsedTime(&c->t_dec, c->ev_b, c->ev_c));
   }
+  return release_to(c, cs);
+}
+
+int nd_translate_beam_classic(nd_ctx* c, const float* d_signal, const int32_t* d_len, const int32_t* d_span,
+                              const int32_t* d_group, int32_t B, int32_t T, int32_t beam, int32_t n_best,
+                              int32_t length_penalty, float alpha, int32_t max_len, int32_t min_len,
+                              int32_t* d_tokens, float* d_scores, int32_t* d_lens, int32_t* d_steps, void* stream) {
+  int rc = check_call(c, B, T, max_len);
+  if (rc) return rc;
+  if (beam < 1 || beam > c->cfg.max_beam) return fail(ND_ERR_ARG, "beam out of range [1, max_beam]");
+  if (n_best < 1 || n_best > beam) return fail(ND_ERR_ARG, "n_best out of range [1, beam]");
+  if (c->V < beam) return fail(ND_ERR_ARG, "vocab smaller than beam");
+  if (length_penalty < 0 || length_penalty > 2) return fail(ND_ERR_ARG, "length_penalty must be 0 (none), 1 (wu), 2 (avg)");
+  if (!d_signal || !d_len || !d_span || !d_group || !d_tokens || !d_scores || !d_lens)
+    return fail(ND_ERR_ARG, "null buffer");
+  hipStream_t cs = (hipStream_t)stream;
+  if ((rc = stage_inputs(c, d_signal, d_len, d_span, B, T, cs))) return rc;
+  HIPCHK(hipMemcpyAsync(c->group_in, d_group, (size_t)B * 4, hipMemcpyDeviceToDevice, c->es));
+  const int SEG = 10;
+  const int st = c->kstamp_on ? 1 : 0;
+  // graph keys: mode 2, alpha and the penalty kind folded into (alpha, n_best) slots
+  GraphKey k0{2, B, T, max_len, min_len, beam, n_best, -1, length_penalty, alpha, st};
+  rc = run_graph(c, k0, [&](hipStream_t s) -> hipError_t {
+    if (c->kstamp_on) LCHK(nd::launch_stamp_reset(c->kstamp, (int)c->dec.size() * c->cfg.max_steps, s));
+    LCHK(enqueue_encode(c, B, T, s));
+    LCHK(enqueue_ctxkv(c, B, T, s));
+    LCHK(nd::launch_beam_classic_init(c->bs, c->group_in, B, beam, c->cfg.bos_idx, s));
+    LCHK(enqueue_first_embed(c, B * beam, s));
+    LCHK(nd::launch_fill_i32(c->steps_done, max_len, 1, s));
+    return hipSuccess;
+  });
+  if (rc) return rc;
+  for (int s0 = 0; s0 < max_len; s0 += SEG) {
+    const int s1 = std::min(max_len, s0 + SEG);
+    GraphKey k{2, B, T, max_len, min_len, beam, n_best, s0, length_penalty, alpha, st};
+    rc = run_graph(c, k, [&](hipStream_t s) {
+      return enqueue_classic_steps(c, B, T, beam, n_best, length_penalty, alpha, max_len, min_len, s0, s1, s);
+    });
+    if (rc) return rc;
+    if (s1 < max_len) {
+      HIPCHK(hipMemcpyAsync(c->h_alive, c->bs.n_alive, 4, hipMemcpyDeviceToHost, c->es));
+      HIPCHK(hipStreamSynchronize(c->es));
+      if (*c->h_alive == 0) break;
+    }
+  }
+  HIPCHK(nd::launch_beam_classic_finish(c->bs, B, beam, n_best, max_len, length_penalty, alpha, d_tokens, d_scores,
+                                        d_lens, c->es));
+  if (d_steps) HIPCHK(hipMemcpyAsync(d_steps, c->steps_done, 4, hipMemcpyDeviceToDevice, c->es));
   return release_to(c, cs);
 }
 

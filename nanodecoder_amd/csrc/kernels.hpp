@@ -129,8 +129,15 @@ struct BeamState {
   float* hyp_score;  // [C, n_best]
   int* hyp_len;      // [C, n_best]
   int* hyp_tok;      // [C, n_best, S]
-  int* n_alive;      // [1] chunks not done
+  int* n_alive;      // [1] chunks (classic: reference batches) not done
   int* steps_done;   // [1] decoder steps until the last chunk finished
+  // classic onmt Beam (translate/translator.py:827-926): the reference batch
+  // each chunk belongs to; a batch keeps advancing all of its beams until
+  // every one of them is done
+  int* group;        // [C] reference batch id
+  int* grp_left;     // [C] chunks of the batch not done yet
+  int* grp_done;     // [C] batch finished (its beams stop advancing)
+  int* steps_run;    // [C] advance() calls made on the chunk's beam
 };
 hipError_t launch_beam_init(const BeamState& st, int C, int beam, int n_best, int S, int bos, hipStream_t s);
 hipError_t launch_beam_step(const NextEmbed& ne, const float* x, const float* ln_g, const float* ln_b, const float* gw, const float* gb,
@@ -138,5 +145,13 @@ hipError_t launch_beam_step(const NextEmbed& ne, const float* x, const float* ln
                             int eos, float lenpen, hipStream_t s);
 hipError_t launch_beam_finish(const BeamState& st, int C, int n_best, int S, int* tokens, float* scores, int* lens,
                               hipStream_t s);
+// classic Beam: length_penalty 0 none, 1 wu, 2 avg (onmt/translate/penalties.py)
+hipError_t launch_beam_classic_init(const BeamState& st, const int* group, int C, int beam, int bos, hipStream_t s);
+hipError_t launch_beam_classic_step(const NextEmbed& ne, const float* x, const float* ln_g, const float* ln_b,
+                                    const float* gw, const float* gb, int V, const BeamState& st, int C, int beam,
+                                    int n_best, int step, int S, int min_len, int eos, int length_penalty, float alpha,
+                                    hipStream_t s);
+hipError_t launch_beam_classic_finish(const BeamState& st, int C, int beam, int n_best, int S, int length_penalty,
+                                      float alpha, int* tokens, float* scores, int* lens, hipStream_t s);
 
 }  // namespace nd

@@ -263,4 +263,211 @@ hipError_t launch_beam_finish(const BeamState& st, int C, int n_best, int S, int
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------ classic Beam
+// onmt/translate/beam.py:6-178 driven by translate/translator.py:827-926:
+// scores start at 0 for every beam, step 0 expands beam 0 only, EOS beams get
+// -1e20 rows (no children), every EOS is a finished hypothesis scored by the
+// GNMT global scorer (length penalty none / wu / avg, coverage none), and a
+// reference batch advances all its beams until each is done
+// (eos_top && finished >= n_best).  Finished lists keep the n_best best
+// entries in stable order, which is what sort_finished's stable sort reads.
+
+// global scorer divisor for len(next_ys) = n_ys (penalties.py:57-78); the
+// Python float the reference computes is rounded to fp32 by torch.
+__device__ __forceinline__ float classic_lp_div(int kind, int n_ys, float alpha) {
+  if (kind == 1) return (float)(pow(5.0 + n_ys, (double)alpha) / pow(6.0, (double)alpha));
+  if (kind == 2) return (float)n_ys;
+  return 1.0f;
+}
+
+// stable insertion of (sc, tokens src[0..len)) into chunk c's best-first list
+__device__ void classic_insert(const BeamState& st, int c, int n_best, int S, float sc, int len, const int* src) {
+  const int nh = st.n_hyp[c];
+  const int kept = min(nh, n_best);
+  int pos = 0;
+  while (pos < kept && st.hyp_score[c * n_best + pos] >= sc) ++pos;
+  if (pos < n_best) {
+    const int last = min(kept, n_best - 1);
+    for (int q = last; q > pos; --q) {
+      st.hyp_score[c * n_best + q] = st.hyp_score[c * n_best + q - 1];
+      st.hyp_len[c * n_best + q] = st.hyp_len[c * n_best + q - 1];
+      for (int t = 0; t < S; ++t)
+        st.hyp_tok[((size_t)c * n_best + q) * S + t] = st.hyp_tok[((size_t)c * n_best + q - 1) * S + t];
+    }
+    st.hyp_score[c * n_best + pos] = sc;
+    st.hyp_len[c * n_best + pos] = len;
+    for (int t = 0; t < len; ++t) st.hyp_tok[((size_t)c * n_best + pos) * S + t] = src[t];
+  }
+  st.n_hyp[c] = nh + 1;
+}
+
+__global__ void __launch_bounds__(64)
+beam_classic_init_kernel(BeamState st, const int* __restrict__ group, int C, int beam, int bos) {
+  const int c = blockIdx.x * 64 + threadIdx.x;
+  if (c >= C) return;
+  for (int j = 0; j < beam; ++j) {
+    st.cum[c * beam + j] = 0.f;  // beam.py:34
+    // beams 1.. start from <blank> (:41-43); their step-0 output is never
+    // read (step 0 expands beam 0 only and every beam then descends from it)
+    st.tok[c * beam + j] = bos;
+  }
+  st.done[c] = 0;
+  st.top_fin[c] = 0;
+  st.n_hyp[c] = 0;
+  st.steps_run[c] = 0;
+  st.group[c] = group[c];
+  st.grp_done[c] = 0;
+  if (atomicAdd(&st.grp_left[group[c]], 1) == 0) atomicAdd(st.n_alive, 1);  // first chunk of its batch
+}
+
+hipError_t launch_beam_classic_init(const BeamState& st, const int* group, int C, int beam, int bos, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(st.grp_left, 0, (size_t)C * sizeof(int), s);
+  if (e == hipSuccess) e = hipMemsetAsync(st.n_alive, 0, sizeof(int), s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(beam_classic_init_kernel, dim3((C + 63) / 64), dim3(64), 0, s, st, group, C, beam, bos);
+  return hipGetLastError();
+}
+
+// One workgroup (256 threads = 4 waves) per chunk.
+__global__ void __launch_bounds__(256)
+beam_classic_step_kernel(NextEmbed ne, const float* __restrict__ x, const float* __restrict__ ln_g,
+                         const float* __restrict__ ln_b, const float* __restrict__ gw, const float* __restrict__ gb,
+                         int V, BeamState st, int beam, int n_best, int step, int S, int min_len, int eos,
+                         int lp_kind, float alpha) {
+  __shared__ float lp[BEAM_MAX][ND_MAXV];
+  __shared__ float tsc[BEAM_MAX];
+  __shared__ int tid_sel[BEAM_MAX];
+  __shared__ int fin[BEAM_MAX];
+  const int c = blockIdx.x, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int g = st.group[c];
+  if (st.grp_done[g]) return;  // translator.py:884-885: the whole batch is done
+  const int cur = step & 1, nxt = cur ^ 1;
+  const int row0 = c * beam;
+  for (int j = w; j < beam; j += 4) {
+    head_row(x, row0 + j, ln_g, ln_b, gw, gb, V, lane, lp[j]);
+    if (lane == 0) {
+      if (step + 1 < min_len) lp[j][eos] = -1e20f;  // beam.py:88-91 (cur_len = step + 1)
+      if (step > 0) {                               // :93-99
+        const float cj = st.cum[row0 + j];
+        const bool dead = st.tok[row0 + j] == eos;  // EOS has no children
+        for (int k = 0; k < V; ++k) lp[j][k] = dead ? -1e20f : lp[j][k] + cj;
+      }
+    }
+  }
+  __syncthreads();
+  if (w == 0) {
+    // topk(beam) over beam*V candidates (step 0: beam 0's V), ties -> lower index
+    const int n = step == 0 ? V : beam * V;
+    bool tk[4] = {false, false, false, false};
+    for (int sel = 0; sel < beam; ++sel) {
+      float bv = -INFINITY;
+      int bi = 0x7fffffff;
+      for (int q = 0; q < 4; ++q) {
+        const int idx = lane + 64 * q;
+        if (idx < n && !tk[q]) {
+          const float v = lp[idx / V][idx % V];
+          if (v > bv || (v == bv && idx < bi)) {
+            bv = v;
+            bi = idx;
+          }
+        }
+      }
+      for (int o = 32; o > 0; o >>= 1) {
+        const float ov = __shfl_xor(bv, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (ov > bv || (ov == bv && oi < bi)) {
+          bv = ov;
+          bi = oi;
+        }
+      }
+      if (bi != 0x7fffffff && (bi & 63) == lane) tk[bi >> 6] = true;
+      if (lane == 0) {
+        tsc[sel] = bv;
+        tid_sel[sel] = bi;
+      }
+    }
+  }
+  __syncthreads();
+  // next_ys / prev_ks (beam.py:125-131) as the reordered histories
+  for (int e = tid; e < beam * (step + 1); e += 256) {
+    const int j = e / (step + 1), t = e - j * (step + 1);
+    const int par = tid_sel[j] / V;
+    const int src = row0 + par, dst = row0 + j;
+    if (t < step) {
+      st.seq[nxt][(size_t)dst * S + t] = st.seq[cur][(size_t)src * S + t];
+      st.anc[nxt][(size_t)dst * S + t] = st.anc[cur][(size_t)src * S + t];
+    } else {
+      st.seq[nxt][(size_t)dst * S + t] = tid_sel[j] % V;
+      st.anc[nxt][(size_t)dst * S + t] = src;
+    }
+  }
+  if (tid < beam) {
+    const int tok = tid_sel[tid] % V;
+    fin[tid] = tok == eos ? 1 : 0;
+    st.tok[row0 + tid] = tok;
+    st.cum[row0 + tid] = tsc[tid];  // self.scores = best_scores (:126)
+  }
+  if (step + 1 < S)
+    for (int j = w; j < beam; j += 4) embed_row(ne, tid_sel[j] % V, step + 1, row0 + j, lane);
+  __syncthreads();
+  if (tid == 0) {
+    const float div = classic_lp_div(lp_kind, step + 2, alpha);  // len(next_ys) after the append
+    for (int j = 0; j < beam; ++j)                                 // :135-139
+      if (fin[j]) classic_insert(st, c, n_best, S, tsc[j] / div, step + 1, st.seq[nxt] + (size_t)(row0 + j) * S);
+    if (fin[0]) st.top_fin[c] = 1;  // eos_top (:142-144)
+    st.steps_run[c] = step + 1;
+    if (!st.done[c] && st.top_fin[c] && st.n_hyp[c] >= n_best) {  // done() (:146-147)
+      st.done[c] = 1;
+      if (atomicSub(&st.grp_left[g], 1) == 1) {
+        st.grp_done[g] = 1;
+        if (atomicSub(st.n_alive, 1) == 1) *st.steps_done = step + 1;
+      }
+    }
+  }
+}
+
+hipError_t launch_beam_classic_step(const NextEmbed& ne, const float* x, const float* ln_g, const float* ln_b,
+                                    const float* gw, const float* gb, int V, const BeamState& st, int C, int beam,
+                                    int n_best, int step, int S, int min_len, int eos, int length_penalty, float alpha,
+                                    hipStream_t s) {
+  if (beam > BEAM_MAX || beam * V > 256 || V > ND_MAXV || V < beam || !ne.emb || !ne.x || !ne.part)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(beam_classic_step_kernel, dim3(C), dim3(256), 0, s, ne, x, ln_g, ln_b, gw, gb, V, st, beam,
+                     n_best, step, S, min_len, eos, length_penalty, alpha);
+  return hipGetLastError();
+}
+
+// sort_finished(minimum=n_best) (beam.py:149-161): beams still alive top the
+// list up in beam order, scored at the chunk's last step; then the n_best
+// best (score, tokens) go out like the --fast path's.
+__global__ void __launch_bounds__(256)
+beam_classic_finish_kernel(BeamState st, int beam, int n_best, int S, int lp_kind, float alpha,
+                           int* __restrict__ tokens, float* __restrict__ scores, int* __restrict__ lens) {
+  const int c = blockIdx.x;
+  if (threadIdx.x == 0 && st.n_hyp[c] < n_best) {
+    const int t = st.steps_run[c], fb = t & 1;
+    const float div = classic_lp_div(lp_kind, t + 1, alpha);
+    for (int i = 0; st.n_hyp[c] < n_best; ++i)
+      classic_insert(st, c, n_best, S, st.cum[c * beam + i] / div, t, st.seq[fb] + (size_t)(c * beam + i) * S);
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < n_best * S; e += 256) {
+    const int nb = e / S, t = e - nb * S;
+    const int len = st.hyp_len[c * n_best + nb];
+    tokens[((size_t)c * n_best + nb) * S + t] = t < len ? st.hyp_tok[((size_t)c * n_best + nb) * S + t] : -1;
+  }
+  if (threadIdx.x < n_best) {
+    scores[c * n_best + threadIdx.x] = st.hyp_score[c * n_best + threadIdx.x];
+    lens[c * n_best + threadIdx.x] = st.hyp_len[c * n_best + threadIdx.x];
+  }
+}
+
+hipError_t launch_beam_classic_finish(const BeamState& st, int C, int beam, int n_best, int S, int length_penalty,
+                                      float alpha, int* tokens, float* scores, int* lens, hipStream_t s) {
+  if (n_best > beam) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(beam_classic_finish_kernel, dim3(C), dim3(256), 0, s, st, beam, n_best, S, length_penalty, alpha,
+                     tokens, scores, lens);
+  return hipGetLastError();
+}
+
 }  // namespace nd

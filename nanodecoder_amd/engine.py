@@ -134,6 +134,27 @@ class Engine:
                                              self._stream()), "nd_translate_beam")
         return dict(tokens=tok, scores=sc, lens=ln, steps=st)
 
+    def translate_beam_classic(self, signal, lengths, spans=None, groups=None, beam: int = 5, n_best: int = 1,
+                               length_penalty: str = "none", alpha: float = 0.0, max_len: Optional[int] = None,
+                               min_len: int = 0):
+        """Classic onmt Beam search (no --fast).  groups [B]: the reference
+        batch of every chunk (default: one batch).  Returns dict like
+        translate_beam."""
+        signal, lengths, spans, B, T = self._inputs(signal, lengths, spans)
+        S = self.max_steps if max_len is None else max_len
+        g = torch.zeros(B, dtype=torch.int32) if groups is None else torch.as_tensor(groups)
+        g = g.to(self.device, torch.int32).contiguous()
+        lpk = {"none": 0, "wu": 1, "avg": 2}[length_penalty]
+        tok = torch.empty(B, n_best, S, dtype=torch.int32, device=self.device)
+        sc = torch.empty(B, n_best, dtype=torch.float32, device=self.device)
+        ln = torch.empty(B, n_best, dtype=torch.int32, device=self.device)
+        st = torch.empty(1, dtype=torch.int32, device=self.device)
+        _lib.check(self._L.nd_translate_beam_classic(self._h, _ptr(signal), _ptr(lengths), _ptr(spans), _ptr(g), B,
+                                                     T, beam, n_best, lpk, float(alpha), S, min_len, _ptr(tok),
+                                                     _ptr(sc), _ptr(ln), _ptr(st), self._stream()),
+                   "nd_translate_beam_classic")
+        return dict(tokens=tok, scores=sc, lens=ln, steps=st)
+
     def encode(self, signal, lengths, spans=None):
         """Memory bank [B, T, d] of the encoder (rows >= span unspecified)."""
         signal, lengths, spans, B, T = self._inputs(signal, lengths, spans)

@@ -34,11 +34,14 @@ from .engine import Engine
 
 
 class GNMTGlobalScorer:
-    """onmt/translate/beam.py:181-199 — only alpha/beta reach --fast beam."""
+    """onmt/translate/beam.py:181-199: alpha/beta, and the length / coverage
+    penalty kinds (onmt/translate/penalties.py) the classic Beam applies."""
 
     def __init__(self, opt):
         self.alpha = float(getattr(opt, "alpha", 0.0))
         self.beta = float(getattr(opt, "beta", 0.0))
+        self.length_penalty = str(getattr(opt, "length_penalty", "none") or "none")
+        self.coverage_penalty = str(getattr(opt, "coverage_penalty", "none") or "none")
 
 
 def parse_chunk(c) -> np.ndarray:
@@ -96,6 +99,7 @@ class Translator(object):
         self.replace_unk = bool(getattr(opt, "replace_unk", False))
         self.verbose = bool(getattr(opt, "verbose", False))
         self.fast = bool(getattr(opt, "fast", False))
+        self.stepwise_penalty = bool(getattr(opt, "stepwise_penalty", False))
         self.global_scorer = global_scorer or GNMTGlobalScorer(opt)
         self.report_score = report_score
         self.logger = logger
@@ -118,10 +122,20 @@ class Translator(object):
                 raise NotImplementedError("random sampling (-random_sampling_topk != 1) is not supported")
             if self.block_ngram_repeat != 0:
                 raise AssertionError("block_ngram_repeat is not supported (translator.py:430)")
+        elif not self.fast:
+            # the classic onmt Beam (translator.py:827-926, onmt/translate/beam.py)
+            if self.dump_beam:
+                raise NotImplementedError("-dump_beam (beam trace JSON) is not produced on the MI355X path")
+            if self.block_ngram_repeat != 0:
+                raise NotImplementedError("-block_ngram_repeat is not supported on the MI355X path")
+            if self.stepwise_penalty or (self.global_scorer.coverage_penalty != "none"
+                                         and self.global_scorer.beta != 0):
+                raise NotImplementedError("coverage penalties need attention sums, not produced on the MI355X path")
+            if self.global_scorer.length_penalty not in ("none", "wu", "avg"):
+                raise ValueError(f"unknown length_penalty {self.global_scorer.length_penalty!r}")
+            if self.n_best > self.beam_size:
+                raise ValueError("n_best must be <= beam_size")
         else:
-            if not self.fast:
-                raise NotImplementedError("the non --fast Beam path (translator.py:827-926) is not on the MI355X "
-                                          "path; pass --fast")
             if self.dump_beam:
                 raise AssertionError("dump_beam is not supported with --fast (translator.py:631)")
             if self.block_ngram_repeat != 0:
@@ -137,9 +151,10 @@ class Translator(object):
         self.out_file_attn = out_file_attn
 
     # ------------------------------------------------------------------ core
-    def _run(self, chunks: List[np.ndarray], spans: Sequence[int]):
+    def _run(self, chunks: List[np.ndarray], spans: Sequence[int], groups: Optional[Sequence[int]] = None):
         """Run the engine on up to max_batch chunks with their reference
-        spans.  Returns per chunk (scores[n_best], token lists[n_best])."""
+        spans (and, for the classic Beam, their reference batch ids).
+        Returns per chunk (scores[n_best], token lists[n_best])."""
         n = len(chunks)
         lens = np.array([len(c) for c in chunks], np.int32)
         if (lens < 1).any():
@@ -163,9 +178,21 @@ class Translator(object):
             for i in range(n):
                 out.append(([float(sc[i])], [tok[i].tolist()]))
         else:
-            r = self.engine.translate_beam(sig, L, S, beam=self.beam_size, n_best=self.n_best,
-                                           alpha=self.global_scorer.alpha, max_len=self.max_length,
-                                           min_len=self.min_length)
+            if self.fast:
+                r = self.engine.translate_beam(sig, L, S, beam=self.beam_size, n_best=self.n_best,
+                                               alpha=self.global_scorer.alpha, max_len=self.max_length,
+                                               min_len=self.min_length)
+            else:
+                # dense reference-batch ids; the engine's padding rows are batches of their own
+                g = np.zeros(B, np.int32)
+                if groups is not None:
+                    g[:n] = np.unique(np.asarray(groups), return_inverse=True)[1]
+                base = int(g[:n].max()) + 1
+                g[n:] = np.arange(base, base + B - n)
+                r = self.engine.translate_beam_classic(sig, L, S, groups=g, beam=self.beam_size, n_best=self.n_best,
+                                                       length_penalty=self.global_scorer.length_penalty,
+                                                       alpha=self.global_scorer.alpha, max_len=self.max_length,
+                                                       min_len=self.min_length)
             tok = r["tokens"].cpu().numpy()
             sc = r["scores"].cpu().numpy()
             ln = r["lens"].cpu().numpy()
@@ -201,20 +228,22 @@ class Translator(object):
         batches of up to max_batch.  Each chunk keeps the span of the
         reference batch it would belong to (consecutive ``batch_size`` chunks
         of its own read), so results equal per-read translate()."""
-        items = []  # (read idx, chunk idx, array, span)
+        items = []  # (read idx, chunk idx, array, span, reference batch id)
+        nb = 0
         for ri, read in enumerate(reads):
             chunks = [parse_chunk(c) for c in read]
             for b0 in range(0, len(chunks), batch_size):
                 part = chunks[b0: b0 + batch_size]
                 span = max(len(c) for c in part)
                 for k, c in enumerate(part):
-                    items.append((ri, b0 + k, c, span))
+                    items.append((ri, b0 + k, c, span, nb))
+                nb += 1
         results = [[None] * len(r) for r in reads]
         cap = self.engine.max_batch
         for s0 in range(0, len(items), cap):
             grp = items[s0: s0 + cap]
-            outs = self._run([g[2] for g in grp], [g[3] for g in grp])
-            for (ri, ci, _, _), o in zip(grp, outs):
+            outs = self._run([g[2] for g in grp], [g[3] for g in grp], [g[4] for g in grp])
+            for (ri, ci, _, _, _), o in zip(grp, outs):
                 results[ri][ci] = o
         ret = []
         counter = 0
@@ -256,7 +285,13 @@ class Translator(object):
         T, B = src.shape[0], src.shape[1]
         lens = batch.src_lengths.detach().cpu().numpy().astype(np.int32)
         chunks = [src[: lens[i], i, 0].numpy() for i in range(B)]
-        outs = self._run(chunks, [T] * B)
+        saved, self.fast = self.fast, bool(fast)  # translator.py:523-540 dispatches on the argument
+        try:
+            if self.beam_size > 1:
+                self._check_supported()
+            outs = self._run(chunks, [T] * B)
+        finally:
+            self.fast = saved
         return {"predictions": [[torch.tensor(t, dtype=torch.long) for t in toks] for _, toks in outs],
                 "scores": [list(sc) for sc, _ in outs], "attention": [[[]] * len(o[0]) for o in outs],
                 "gold_score": [0] * B, "batch": batch}

@@ -227,6 +227,65 @@ def test_beam_vs_golden(name, which):
     assert np.abs(sc - z["beam_scores" + which]).max() < 1e-3
 
 
+@pytest.mark.parametrize("name,which", [("transformer_classic_beam", "classic"),
+                                        ("transformer_classic_beam", "classic2"),
+                                        ("transformer_classic_beam_mid", "classic")])
+def test_classic_beam_vs_golden(name, which):
+    """The classic onmt Beam (no --fast) against the reference's own
+    _translate_batch: tokens, lengths (EOS included) and global scores."""
+    z, meta = gu.load(name)
+    cfg, W = gu.model_for(meta)
+    kw = meta[which]
+    eng = _engine(cfg, W, max_batch=8, max_steps=kw["max_length"], max_beam=kw["beam_size"])
+    from nanodecoder_amd.engine import pad_chunks
+    chunks = gu.chunks_of(z)
+    sig, lens = pad_chunks(chunks, 512)
+    spans = np.full(len(chunks), 512, np.int32)
+    r = eng.translate_beam_classic(sig, lens, spans, beam=kw["beam_size"], n_best=kw["n_best"],
+                                   length_penalty=kw.get("length_penalty", "none"), alpha=kw.get("alpha", 0.0),
+                                   max_len=kw["max_length"], min_len=kw.get("min_length", 0))
+    tok, sc, ln = (r[k].cpu().numpy() for k in ("tokens", "scores", "lens"))
+    assert (ln == z[which + "_lens"]).all(), (ln, z[which + "_lens"])
+    for i in range(len(chunks)):
+        for nb in range(kw["n_best"]):
+            L = ln[i, nb]
+            assert (tok[i, nb, :L] == z[which + "_tokens"][i, nb, :L]).all()
+    assert np.abs(sc - z[which + "_scores"]).max() < 1e-3
+
+
+def test_classic_beam_packed_batches_vs_oracle():
+    """Several reference batches packed into one engine call keep their own
+    stopping points: equal to the oracle run batch by batch."""
+    ref = _oracle()
+    z, meta = gu.load("transformer_classic_beam_mid")
+    cfg, W = gu.model_for(meta)
+    kw = dict(meta["classic"])
+    m = ref.RefModel(cfg, W)
+    chunks = gu.chunks_of(z) + [c[::-1].copy() for c in gu.chunks_of(z)[:3]]
+    groups = [0, 0, 1, 1, 2, 2, 2]          # reference batches of 2 / 2 / 3 chunks
+    exp = {}
+    for g in sorted(set(groups)):
+        idx = [i for i, gg in enumerate(groups) if gg == g]
+        part = [chunks[i] for i in idx]
+        src, lens, order = ref.make_batch(part)
+        res = ref.classic_beam(m, src, lens, **kw)
+        for j, o in enumerate(order):
+            exp[idx[o]] = (res[j], src.shape[1])
+    from nanodecoder_amd.engine import pad_chunks
+    sig, lens = pad_chunks(chunks, 512)
+    spans = np.array([exp[i][1] for i in range(len(chunks))], np.int32)
+    eng = _engine(cfg, W, max_batch=8, max_steps=kw["max_length"], max_beam=kw["beam_size"])
+    r = eng.translate_beam_classic(sig, lens, spans, groups=groups, beam=kw["beam_size"], n_best=kw["n_best"],
+                                   length_penalty=kw["length_penalty"], max_len=kw["max_length"],
+                                   min_len=kw["min_length"])
+    tok, sc, ln = (r[k].cpu().numpy() for k in ("tokens", "scores", "lens"))
+    for i in range(len(chunks)):
+        for nb, (s, p) in enumerate(exp[i][0]):
+            assert ln[i, nb] == len(p), (i, nb)
+            assert (tok[i, nb, : len(p)] == p).all(), (i, nb)
+            assert abs(sc[i, nb] - s) < 1e-3
+
+
 # ----------------------------------------------------------------- oracle, larger
 def _compare_tokens(got, exp_tokens, exp_logp):
     """Exact tokens, except after a genuine oracle near-tie."""

@@ -41,6 +41,11 @@ class FakeEngine:
                 sc[i, k] = -float(k)
         return {"tokens": tok, "scores": sc, "lens": lens, "steps": torch.tensor([4])}
 
+    def translate_beam_classic(self, sig, L, S, groups, beam, n_best, length_penalty, alpha, max_len, min_len=0):
+        out = self.translate_beam(sig, L, S, beam, n_best, alpha, max_len, min_len)
+        self.calls[-1] = ("classic", sig.shape, L.copy(), S.copy(), np.asarray(groups).copy(), length_penalty)
+        return out
+
 
 def make_tr(**over):
     opt = dict(gpu=0, n_best=1, max_length=10, min_length=0, beam_size=1, random_sampling_temp=1.0,
@@ -102,12 +107,29 @@ def test_beam_n_best():
     assert sc[0] == [0.0, -1.0]
 
 
+def test_classic_beam_reference_batches():
+    """The classic onmt Beam advances a reference batch until all of its beams
+    are done, so every chunk carries its reference batch id (batch_size
+    consecutive chunks of one read) however the engine packs reads."""
+    reads = [chunks([512, 512, 77], seed=1), chunks([512, 300], seed=2), chunks([60], seed=3)]
+    tr, eng = make_tr(beam_size=4, fast=False, n_best=2, length_penalty="wu", alpha=0.6)
+    tr.translate_reads(reads, batch_size=2)
+    (kind, shape, L, S, groups, lp), = eng.calls
+    assert kind == "classic" and lp == "wu"
+    # chunks: read0 -> batches {0,1},{2}; read1 -> {0,1}; read2 -> {0}
+    assert list(groups[:6]) == [0, 0, 1, 2, 2, 3]
+    assert len(set(groups[6:])) == len(groups) - 6 and min(groups[6:]) > 3   # padding rows: own batches
+
+
 def test_reference_errors():
     tr, _ = make_tr()
     with pytest.raises(ValueError):
         tr.translate(chunks([10]), batch_size=None)
+    make_tr(beam_size=5, fast=False)  # the classic onmt Beam is on the path
     with pytest.raises(NotImplementedError):
-        make_tr(beam_size=5, fast=False)
+        make_tr(beam_size=5, fast=False, block_ngram_repeat=2)
+    with pytest.raises(NotImplementedError):
+        make_tr(beam_size=5, fast=False, coverage_penalty="wu", beta=0.2)
     with pytest.raises(NotImplementedError):
         make_tr(random_sampling_topk=5)
     with pytest.raises(AssertionError):
