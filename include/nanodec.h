@@ -93,6 +93,15 @@ int nd_translate_greedy(nd_ctx* ctx, const float* d_signal, const int32_t* d_len
                         int32_t B, int32_t T, int32_t max_len, int32_t min_len,
                         int32_t* d_tokens, float* d_score, float* d_logp, void* stream);
 
+/* Greedy decode that also returns -attn_debug attention (translate/
+ * translator.py:285-336, return_attention at :396-503): d_attn [B, max_len, T]
+ * = per step the last decoder layer's context attention of head 0
+ * (attn["std"], onmt/modules/multi_headed_attn.py:187-192) over source
+ * positions t < span (zero beyond).  Otherwise as nd_translate_greedy. */
+int nd_translate_greedy_attn(nd_ctx* ctx, const float* d_signal, const int32_t* d_len, const int32_t* d_span,
+                             int32_t B, int32_t T, int32_t max_len, int32_t min_len, int32_t* d_tokens, float* d_score,
+                             float* d_logp, float* d_attn, void* stream);
+
 /* --fast beam search.  Replaces Translator._fast_translate_batch
  * (translate/translator.py:619-825) with GNMTGlobalScorer.alpha
  * (onmt/translate/beam.py:181-199; beta must be 0).  Per chunk the n_best

@@ -38,6 +38,7 @@ SIGNATURES = {
     "nd_load_weight": (_I, [_P, ctypes.c_char_p, _P, ctypes.POINTER(ctypes.c_int64), _I]),
     "nd_finalize": (_I, [_P]),
     "nd_translate_greedy": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P]),
+    "nd_translate_greedy_attn": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
     "nd_translate_beam": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _F, _I, _I, _P, _P, _P, _P, _P]),
     "nd_translate_beam_classic": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _F, _I, _I, _P, _P, _P, _P, _P]),
     "nd_encode": (_I, [_P, _P, _P, _P, _I, _I, _P, _P]),

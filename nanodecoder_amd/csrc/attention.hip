@@ -356,7 +356,8 @@ template <int RPC>
 __global__ void __launch_bounds__(CTX_NW * 64)
 dec_ctx_attention_kernel(const float* __restrict__ q, const float* __restrict__ kv, int ld, int koff,
                          const float* __restrict__ signal, const int* __restrict__ span, float pad_val,
-                         float* __restrict__ out, int T, unsigned long long* stamp) {
+                         float* __restrict__ out, int T, unsigned long long* stamp, float* __restrict__ dbg,
+                         size_t dbg_stride) {
   stamp_begin(stamp);
   constexpr int U = CtxTile<RPC>::U;
   extern __shared__ float sm[];
@@ -406,6 +407,8 @@ dec_ctx_attention_kernel(const float* __restrict__ q, const float* __restrict__ 
         const float d = sum8(qv[j].x * kc[u].x + qv[j].y * kc[u].y + qv[j].z * kc[u].z + qv[j].w * kc[u].w);
         sc[j][u] = valid ? (masked ? ND_MASK_FILL : d) : -INFINITY;
       }
+      // -attn_debug: head 0 (lanes 0..7 after sum8) of the chunk's first row
+      if (dbg && lane == 0 && valid) dbg[(size_t)c * dbg_stride + blk * U + u] = sc[0][u];
     }
     online_update<RPC, U>(sc, vc, m, l, acc);
     if (more) {
@@ -425,14 +428,14 @@ static size_t ctx_lds_bytes(int rpc) { return (size_t)CTX_NW * rpc * (ND_D + 2 *
 
 hipError_t launch_dec_ctx_attention(const float* q, const float* kv, int ld, int koff, const float* signal,
                                     const int* span, float pad_val, float* out, int C, int rpc, int T,
-                                    hipStream_t s, unsigned long long* stamp) {
+                                    hipStream_t s, unsigned long long* stamp, float* attn_dbg, size_t dbg_stride) {
   if (rpc < 1 || rpc > CTX_MAXR || T > 512) return hipErrorInvalidValue;
   const size_t lds = ctx_lds_bytes(rpc);
   switch (rpc) {
 #define ND_CTX_CASE(R)                                                                                            \
   case R:                                                                                                         \
     hipLaunchKernelGGL(dec_ctx_attention_kernel<R>, dim3(C), dim3(CTX_NW * 64), lds, s, q, kv, ld, koff, signal,  \
-                       span, pad_val, out, T, stamp);                                                             \
+                       span, pad_val, out, T, stamp, attn_dbg, dbg_stride);                                       \
     break;
     ND_CTX_CASE(1)
     ND_CTX_CASE(2)

@@ -130,6 +130,8 @@ struct nd_ctx {
   nd::BeamState bs{};
   int* steps_done = nullptr;
   int* group_in = nullptr;  // classic Beam: staged reference-batch ids
+  float* attn_raw = nullptr;  // -attn_debug: [max_batch][max_steps][max_src_len] head-0 scores -> probabilities
+  bool attn_on = false;       // set while a greedy call with an attention dump is enqueued
   int* h_alive = nullptr;  // pinned
 
   hipStream_t es = nullptr;
@@ -480,6 +482,9 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
     DecLayer& L = c->dec[i];
     float* cache = c->cache + (size_t)i * R * S * 2 * D;
     unsigned long long* stamp = c->kstamp_on ? c->kstamp + 2 * ((size_t)step * Ld + i) : nullptr;
+    // -attn_debug (greedy): the last layer's head-0 context scores, [B][S][T]
+    float* dbg = (c->attn_on && i == Ld - 1) ? c->attn_raw + (size_t)step * T : nullptr;
+    const size_t dbg_stride = (size_t)S * T;
     // decoder/transformer.py:53-95
     // all step activations are P16-packed (kernels.hpp)
     if (c->cfg.self_attn_type == ND_SELF_AVERAGE) {
@@ -501,12 +506,12 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
       const int HD = ND_H * D;
       LCHK(G(c->dq1, D, L.pwqk, HD, D, L.bqk, c->dqk, HD, R).p16().ln(c->dq1_part, pnq).run(s));
       LCHK(nd::launch_dec_mem_attention(c->dqk, c->mem, c->sig, c->span, (float)c->cfg.pad_idx, c->dU, C, rpc, T, T,
-                                        s, stamp));
+                                        s, stamp, dbg, dbg_stride));
       LCHK(G(c->dU, HD, L.pwvo, D, HD, L.bvo, c->dmid, D, R).p16().res(c->dq1, D).stats(c->dmid_part).run(s, &pnm));
     } else {
       LCHK(G(c->dq1, D, L.pcwq, D, D, L.ncbq, c->dcq, D, R).p16().ln(c->dq1_part, pnq).run(s));
       LCHK(nd::launch_dec_ctx_attention(c->dcq, c->ctxkv, Ld * 2 * D, i * 2 * D, c->sig, c->span,
-                                        (float)c->cfg.pad_idx, c->datt, C, rpc, T, s, stamp));
+                                        (float)c->cfg.pad_idx, c->datt, C, rpc, T, s, stamp, dbg, dbg_stride));
       LCHK(G(c->datt, D, L.pcwo, D, D, L.cbo, c->dmid, D, R).p16().res(c->dq1, D).stats(c->dmid_part).run(s, &pnm));
     }
     LCHK(G(c->dmid, D, L.pw1, F, D, L.nb1, c->dhid, F, R).p16().ln(c->dmid_part, pnm).relu().run(s));
@@ -540,6 +545,7 @@ static hipError_t enqueue_greedy(nd_ctx* c, int B, int T, int S, int min_len, bo
                                     c->cfg.eos_idx, c->tok, c->gtok, c->gscore, logp ? c->glogp : nullptr, ne, B,
                                     s));
   }
+  if (c->attn_on) LCHK(nd::launch_attn_rows_softmax(c->attn_raw, c->span, B, c->cfg.max_steps, T, s));
   return hipSuccess;
 }
 
@@ -856,23 +862,33 @@ static int release_to(nd_ctx* c, hipStream_t cs) {
   return ND_OK;
 }
 
-int nd_translate_greedy(nd_ctx* c, const float* d_signal, const int32_t* d_len, const int32_t* d_span, int32_t B,
-                        int32_t T, int32_t max_len, int32_t min_len, int32_t* d_tokens, float* d_score, float* d_logp,
-                        void* stream) {
+static int translate_greedy(nd_ctx* c, const float* d_signal, const int32_t* d_len, const int32_t* d_span, int32_t B,
+                            int32_t T, int32_t max_len, int32_t min_len, int32_t* d_tokens, float* d_score,
+                            float* d_logp, float* d_attn, void* stream) {
   int rc = check_call(c, B, T, max_len);
   if (rc) return rc;
   if (!d_signal || !d_len || !d_span || !d_tokens || !d_score) return fail(ND_ERR_ARG, "null buffer");
+  if (d_attn && !c->attn_raw) {
+    const size_t n = (size_t)c->cfg.max_batch * c->cfg.max_steps * c->cfg.max_src_len;
+    hipError_t e = dalloc(c, &c->attn_raw, n);
+    if (e != hipSuccess) return fail(ND_ERR_HIP, std::string("hipMalloc attention dump: ") + hipGetErrorString(e));
+  }
   hipStream_t cs = (hipStream_t)stream;
   if ((rc = stage_inputs(c, d_signal, d_len, d_span, B, T, cs))) return rc;
   const bool lp = d_logp != nullptr;
-  GraphKey key{0, B, T, max_len, min_len, 1, 1, 0, lp ? 1 : 0, 0.f, c->kstamp_on ? 1 : 0};
+  GraphKey key{0, B, T, max_len, min_len, 1, 1, d_attn ? 1 : 0, lp ? 1 : 0, 0.f, c->kstamp_on ? 1 : 0};
   if (c->timing) HIPCHK(hipEventRecord(c->ev_a, c->es));
+  c->attn_on = d_attn != nullptr;
   rc = run_graph(c, key, [&](hipStream_t s) { return enqueue_greedy(c, B, T, max_len, min_len, lp, s); });
+  c->attn_on = false;
   if (rc) return rc;
   if (c->timing) HIPCHK(hipEventRecord(c->ev_b, c->es));
   HIPCHK(hipMemcpyAsync(d_tokens, c->gtok, (size_t)B * max_len * 4, hipMemcpyDeviceToDevice, c->es));
   HIPCHK(hipMemcpyAsync(d_score, c->gscore, (size_t)B * 4, hipMemcpyDeviceToDevice, c->es));
   if (lp) HIPCHK(hipMemcpyAsync(d_logp, c->glogp, (size_t)B * max_len * c->V * 4, hipMemcpyDeviceToDevice, c->es));
+  if (d_attn)  // [B][max_steps][T] -> [B][max_len][T]
+    HIPCHK(hipMemcpy2DAsync(d_attn, (size_t)max_len * T * 4, c->attn_raw, (size_t)c->cfg.max_steps * T * 4,
+                            (size_t)max_len * T * 4, B, hipMemcpyDeviceToDevice, c->es));
   if (c->timing) {
     HIPCHK(hipEventSynchronize(c->ev_b));
     float ms = 0.f;
@@ -881,6 +897,21 @@ int nd_translate_greedy(nd_ctx* c, const float* d_signal, const int32_t* d_len, 
     c->t_dec = ms;
   }
   return release_to(c, cs);
+}
+
+int nd_translate_greedy(nd_ctx* c, const float* d_signal, const int32_t* d_len, const int32_t* d_span, int32_t B,
+                        int32_t T, int32_t max_len, int32_t min_len, int32_t* d_tokens, float* d_score, float* d_logp,
+                        void* stream) {
+  return translate_greedy(c, d_signal, d_len, d_span, B, T, max_len, min_len, d_tokens, d_score, d_logp, nullptr,
+                          stream);
+}
+
+int nd_translate_greedy_attn(nd_ctx* c, const float* d_signal, const int32_t* d_len, const int32_t* d_span,
+                             int32_t B, int32_t T, int32_t max_len, int32_t min_len, int32_t* d_tokens, float* d_score,
+                             float* d_logp, float* d_attn, void* stream) {
+  if (!d_attn) return fail(ND_ERR_ARG, "null attention buffer");
+  return translate_greedy(c, d_signal, d_len, d_span, B, T, max_len, min_len, d_tokens, d_score, d_logp, d_attn,
+                          stream);
 }
 
 int nd_translate_beam(nd_ctx* c, const float* d_signal, const int32_t* d_len, const int32_t* d_span, int32_t B,

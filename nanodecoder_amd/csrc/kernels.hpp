@@ -76,7 +76,8 @@ hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* 
 // (K at kv[(c*T+t)*ld + koff], V at +256), mask signal == pad_val, keys < span.
 hipError_t launch_dec_ctx_attention(const float* q, const float* kv, int ld, int koff, const float* signal,
                                     const int* span, float pad_val, float* out, int C, int rpc, int T,
-                                    hipStream_t s, unsigned long long* stamp = nullptr);
+                                    hipStream_t s, unsigned long long* stamp = nullptr, float* attn_dbg = nullptr,
+                                    size_t dbg_stride = 0);
 // Next step's decoder input, written by the search kernel that picks the
 // token (the embedding of step+1 fused into the head: one launch fewer per
 // step): x[row] = emb[tok] (* 16 + pe[step+1] with position encoding) and
@@ -94,7 +95,10 @@ struct NextEmbed {
 // softmax-weighted memory sum).
 hipError_t launch_dec_mem_attention(const float* qp, const float* mem, const float* signal, const int* span,
                                     float pad_val, float* out, int C, int rpc, int T, int ldT, hipStream_t s,
-                                    unsigned long long* stamp = nullptr);
+                                    unsigned long long* stamp = nullptr, float* attn_dbg = nullptr,
+                                    size_t dbg_stride = 0);
+// -attn_debug: raw head-0 score rows [B*S][T] (keys < span[c]) -> probabilities
+hipError_t launch_attn_rows_softmax(float* a, const int* span, int B, int S, int T, hipStream_t s);
 // stamp pairs (earliest start, latest end) <- (UINT64_MAX, 0)
 hipError_t launch_stamp_reset(unsigned long long* stamps, int pairs, hipStream_t s);
 // encoder output rows x[b*T+t] -> memory bank rows b*ldT+t, row-major (LN when

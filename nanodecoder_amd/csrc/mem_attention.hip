@@ -72,7 +72,8 @@ template <int EXPT>
 __global__ void __launch_bounds__(MB_NW * 64)
 dec_mem_attention_kernel(const float* __restrict__ qp, const float* __restrict__ mem,
                          const float* __restrict__ signal, const int* __restrict__ span, float pad_val,
-                         float* __restrict__ out, int T, int ldT, unsigned long long* stamp) {
+                         float* __restrict__ out, int T, int ldT, unsigned long long* stamp,
+                         float* __restrict__ dbg, size_t dbg_stride) {
   stamp_begin(stamp);
   extern __shared__ float lds[];
   const int c = blockIdx.x, lane = threadIdx.x & 63;
@@ -164,6 +165,7 @@ dec_mem_attention_kernel(const float* __restrict__ qp, const float* __restrict__
     const int t = r * MB_TILE + w * MB_KW + sk;
     const float sg = __shfl(sgv, r * 8 + sk);
     s = t < L ? (sg == pad_val ? ND_MASK_FILL : s) : -INFINITY;
+    if (dbg && sh == 0 && t < L) dbg[(size_t)c * dbg_stride + t] = s;  // -attn_debug: head 0's scores
     const float mnew = fmaxf(mrun, max_by8(s));
     const float scale = mnew == -INFINITY ? 1.f : __expf(mrun - mnew);
     const float p = s == -INFINITY ? 0.f : __expf(s - mnew);
@@ -250,7 +252,7 @@ static_assert(MB_NW * 512 * 4 <= MB_U, "merge slots overlap the q' image");
 
 hipError_t launch_dec_mem_attention(const float* qp, const float* mem, const float* signal, const int* span,
                                     float pad_val, float* out, int C, int rpc, int T, int ldT, hipStream_t s,
-                                    unsigned long long* stamp) {
+                                    unsigned long long* stamp, float* attn_dbg, size_t dbg_stride) {
   if (rpc != 1 || T < 1 || T > 512 || ldT < T || C < 1) return hipErrorInvalidValue;
   static const int expt = [] {
     const char* e = getenv("ND_MEM_EXPT");  // timing experiments only (wrong results): 1 no loads, 2 no MFMA
@@ -258,7 +260,7 @@ hipError_t launch_dec_mem_attention(const float* qp, const float* mem, const flo
   }();
 #define ND_MB_LAUNCH(X)                                                                                         \
   hipLaunchKernelGGL(dec_mem_attention_kernel<X>, dim3(C), dim3(MB_NW * 64), mem_lds_bytes(), s, qp, mem, signal, \
-                     span, pad_val, out, T, ldT, stamp)
+                     span, pad_val, out, T, ldT, stamp, attn_dbg, dbg_stride)
   if (expt == 1) ND_MB_LAUNCH(1);
   else if (expt == 2) ND_MB_LAUNCH(2);
   else if (expt == 3) ND_MB_LAUNCH(3);
@@ -294,6 +296,29 @@ hipError_t launch_memory_pack(const float* x, const float* ln_g, const float* ln
   if (T > ldT || T < 1) return hipErrorInvalidValue;
   const int rows = B * ldT;
   hipLaunchKernelGGL(memory_pack_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, x, ln_g, ln_b, out, B, T, ldT);
+  return hipGetLastError();
+}
+
+// -attn_debug: rows of raw head-0 scores (keys t < span) -> softmax in place
+// (the reference's attn["std"]: the last layer's context attention, head 0,
+// onmt/modules/multi_headed_attn.py:175,187-192).  One wave per row.
+__global__ void __launch_bounds__(256)
+attn_rows_softmax_kernel(float* __restrict__ a, const int* __restrict__ span, int B, int S, int T) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= B * S) return;
+  const int c = row / S, L = min(span[c], T);
+  float* r = a + (size_t)row * T;
+  float mx = -INFINITY;
+  for (int t = lane; t < L; t += 64) mx = fmaxf(mx, r[t]);
+  mx = wave_max(mx);
+  float sum = 0.f;
+  for (int t = lane; t < L; t += 64) sum += __expf(r[t] - mx);
+  sum = wave_sum(sum);
+  for (int t = lane; t < T; t += 64) r[t] = t < L ? __expf(r[t] - mx) / sum : 0.f;
+}
+
+hipError_t launch_attn_rows_softmax(float* a, const int* span, int B, int S, int T, hipStream_t s) {
+  hipLaunchKernelGGL(attn_rows_softmax_kernel, dim3((B * S + 3) / 4), dim3(256), 0, s, a, span, B, S, T);
   return hipGetLastError();
 }
 

@@ -107,17 +107,24 @@ class Engine:
         return signal, lengths, spans, B, T
 
     def translate_greedy(self, signal, lengths, spans=None, max_len: Optional[int] = None, min_len: int = 0,
-                         return_logp: bool = False):
+                         return_logp: bool = False, return_attn: bool = False):
         """Greedy decode.  signal [B,T] f32 (zero padded), lengths/spans [B].
-        Returns dict(tokens [B,S] i32, scores [B] f32, logp [B,S,V] or None)."""
+        Returns dict(tokens [B,S] i32, scores [B] f32, logp [B,S,V] or None,
+        attn [B,S,T] or None: the last layer's head-0 context attention)."""
         signal, lengths, spans, B, T = self._inputs(signal, lengths, spans)
         S = self.max_steps if max_len is None else max_len
         tok = torch.empty(B, S, dtype=torch.int32, device=self.device)
         sc = torch.empty(B, dtype=torch.float32, device=self.device)
         lp = torch.empty(B, S, self.cfg.vocab, dtype=torch.float32, device=self.device) if return_logp else None
+        if return_attn:
+            at = torch.empty(B, S, T, dtype=torch.float32, device=self.device)
+            _lib.check(self._L.nd_translate_greedy_attn(self._h, _ptr(signal), _ptr(lengths), _ptr(spans), B, T, S,
+                                                        min_len, _ptr(tok), _ptr(sc), _ptr(lp), _ptr(at),
+                                                        self._stream()), "nd_translate_greedy_attn")
+            return dict(tokens=tok, scores=sc, logp=lp, attn=at)
         _lib.check(self._L.nd_translate_greedy(self._h, _ptr(signal), _ptr(lengths), _ptr(spans), B, T, S, min_len,
                                                _ptr(tok), _ptr(sc), _ptr(lp), self._stream()), "nd_translate_greedy")
-        return dict(tokens=tok, scores=sc, logp=lp)
+        return dict(tokens=tok, scores=sc, logp=lp, attn=None)
 
     def translate_beam(self, signal, lengths, spans=None, beam: int = 5, n_best: int = 1, alpha: float = 0.0,
                        max_len: Optional[int] = None, min_len: int = 0):

@@ -144,17 +144,20 @@ class Translator(object):
                 raise AssertionError("beta must be 0 with --fast (translator.py:634)")
             if self.n_best > self.beam_size:
                 raise ValueError("n_best must be <= beam_size")
-        if self.replace_unk:
-            raise NotImplementedError("-replace_unk needs attention dumps, not produced on the MI355X path")
+        # -replace_unk is accepted: TranslationBuilder only replaces when the
+        # batch carries text src (translation.py:42-47), which nano data never
+        # does (src is None, :73-81), so predictions are unchanged
 
     def setAttnFile(self, out_file_attn):
         self.out_file_attn = out_file_attn
 
     # ------------------------------------------------------------------ core
-    def _run(self, chunks: List[np.ndarray], spans: Sequence[int], groups: Optional[Sequence[int]] = None):
+    def _run(self, chunks: List[np.ndarray], spans: Sequence[int], groups: Optional[Sequence[int]] = None,
+             attn: bool = False):
         """Run the engine on up to max_batch chunks with their reference
         spans (and, for the classic Beam, their reference batch ids).
-        Returns per chunk (scores[n_best], token lists[n_best])."""
+        Returns per chunk (scores[n_best], token lists[n_best]) and, with
+        ``attn`` (greedy), the per-step attention rows [steps, chunk length]."""
         n = len(chunks)
         lens = np.array([len(c) for c in chunks], np.int32)
         if (lens < 1).any():
@@ -172,11 +175,19 @@ class Translator(object):
         L[:n], S[:n] = lens, spans
         out = []
         if self.beam_size == 1:
-            r = self.engine.translate_greedy(sig, L, S, max_len=self.max_length, min_len=self.min_length)
+            if attn:
+                r = self.engine.translate_greedy(sig, L, S, max_len=self.max_length, min_len=self.min_length,
+                                                 return_attn=True)
+                at = r["attn"].cpu().numpy()
+            else:
+                r = self.engine.translate_greedy(sig, L, S, max_len=self.max_length, min_len=self.min_length)
             tok = r["tokens"].cpu().numpy()
             sc = r["scores"].cpu().numpy()
             for i in range(n):
-                out.append(([float(sc[i])], [tok[i].tolist()]))
+                if attn:  # results["attention"]: rows cut at the chunk's length (translator.py:491-501)
+                    out.append(([float(sc[i])], [tok[i].tolist()], at[i, :, : lens[i]]))
+                else:
+                    out.append(([float(sc[i])], [tok[i].tolist()]))
         else:
             if self.fast:
                 r = self.engine.translate_beam(sig, L, S, beam=self.beam_size, n_best=self.n_best,
@@ -217,13 +228,28 @@ class Translator(object):
         assert src is not None
         if batch_size is None:
             raise ValueError("batch_size must be set")
-        if attn_debug:
-            raise NotImplementedError("-attn_debug attention dumps are not produced on the MI355X path")
+        if attn_debug and self.beam_size != 1:
+            raise NotImplementedError("-attn_debug is produced for greedy decoding (beam_size 1) only")
         chunks = [parse_chunk(c) for c in src]
-        res = self.translate_reads([chunks], batch_size=batch_size)[0]
+        res = self.translate_reads([chunks], batch_size=batch_size, attn_debug=attn_debug)[0]
         return res
 
-    def translate_reads(self, reads: Sequence[Sequence], batch_size: int):
+    def _write_attn(self, chunk: np.ndarray, sent: List[str], attn: np.ndarray):
+        """translate/translator.py:285-336: the source samples and the
+        prediction (+ </s>) as headers, then one row of attention weights per
+        decoder step, into the file set by setAttnFile."""
+        preds = list(sent) + ["</s>"]
+        srcs = [str(x) for x in np.asarray(chunk, np.float32).reshape(-1)]
+        header_format = "{:>8.7} " + "{:>8.7} " * len(srcs)
+        row_format = "{:>8.5f} " * len(srcs)
+        output = header_format.format(">", *srcs)
+        header_format = "{:>8.7} " + "{:>8.7} " * len(preds)
+        output += header_format.format("|", *preds) + "\n"
+        for row in attn.tolist():
+            output += row_format.format(*row) + "\n"
+        self.out_file_attn.write(output)
+
+    def translate_reads(self, reads: Sequence[Sequence], batch_size: int, attn_debug: bool = False):
         """Translate many reads; chunks are packed across reads into engine
         batches of up to max_batch.  Each chunk keeps the span of the
         reference batch it would belong to (consecutive ``batch_size`` chunks
@@ -242,16 +268,19 @@ class Translator(object):
         cap = self.engine.max_batch
         for s0 in range(0, len(items), cap):
             grp = items[s0: s0 + cap]
-            outs = self._run([g[2] for g in grp], [g[3] for g in grp], [g[4] for g in grp])
-            for (ri, ci, _, _, _), o in zip(grp, outs):
-                results[ri][ci] = o
+            outs = self._run([g[2] for g in grp], [g[3] for g in grp], [g[4] for g in grp], attn=attn_debug)
+            for (ri, ci, c, _, _), o in zip(grp, outs):
+                results[ri][ci] = o + (c,) if attn_debug else o
         ret = []
         counter = 0
         pred_score_total, pred_words_total = 0.0, 0
         for r in results:
             all_scores, all_predictions = [], []
-            for scores, toks in r:
+            for res in r:
+                scores, toks = res[0], res[1]
                 sents = [self._tokens_to_sent(t) for t in toks]
+                if attn_debug:
+                    self._write_attn(res[3], sents[0], res[2])
                 all_scores.append(scores[: self.n_best])
                 all_predictions.append([" ".join(s) for s in sents[: self.n_best]])
                 pred_score_total += scores[0]
@@ -289,9 +318,11 @@ class Translator(object):
         try:
             if self.beam_size > 1:
                 self._check_supported()
-            outs = self._run(chunks, [T] * B)
+            want = bool(attn_debug or self.replace_unk) and self.beam_size == 1  # return_attention (:521-529)
+            outs = self._run(chunks, [T] * B, attn=want)
         finally:
             self.fast = saved
-        return {"predictions": [[torch.tensor(t, dtype=torch.long) for t in toks] for _, toks in outs],
-                "scores": [list(sc) for sc, _ in outs], "attention": [[[]] * len(o[0]) for o in outs],
+        att = [[torch.from_numpy(np.ascontiguousarray(o[2]))] if want else [[]] * len(o[0]) for o in outs]
+        return {"predictions": [[torch.tensor(t, dtype=torch.long) for t in o[1]] for o in outs],
+                "scores": [list(o[0]) for o in outs], "attention": att,
                 "gold_score": [0] * B, "batch": batch}

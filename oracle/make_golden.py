@@ -131,7 +131,7 @@ def floor_int_div():
         torch.Tensor.div = orig
 
 
-def run_greedy(ns, model, cfg, chunks, max_length=100, min_length=0):
+def run_greedy(ns, model, cfg, chunks, max_length=100, min_length=0, attention=False):
     tr = make_translator(ns, model, cfg, beam_size=1, max_length=max_length, min_length=min_length)
     batch, order = make_batch(chunks)
     rec = []
@@ -154,7 +154,8 @@ def run_greedy(ns, model, cfg, chunks, max_length=100, min_length=0):
     model.encoder.forward = enc_wrap
     with torch.no_grad():
         res = tr._translate_random_sampling(batch, types.SimpleNamespace(data_type="nano"), max_length,
-                                            min_length=min_length, sampling_temp=1.0, keep_topk=1)
+                                            min_length=min_length, sampling_temp=1.0, keep_topk=1,
+                                            return_attention=attention)
     model.encoder.forward = enc_fwd
     B = len(chunks)
     inv = np.argsort(order)  # batch row j holds chunk order[j]
@@ -162,9 +163,18 @@ def run_greedy(ns, model, cfg, chunks, max_length=100, min_length=0):
     tokens = np.stack([res["predictions"][j][0].numpy() for j in range(B)])[inv].astype(np.int32)
     scores = np.array([float(res["scores"][j][0]) for j in range(B)], np.float32)[inv]
     memory = mem_box["memory"].numpy()[:, inv, :]              # [T, B, d]
-    return dict(logp=logp.astype(np.float32), tokens=tokens, scores=scores,
-                memory_sub=np.ascontiguousarray(memory[::MEM_STRIDE]).astype(np.float32),
-                T=np.int32(memory.shape[0]))
+    out = dict(logp=logp.astype(np.float32), tokens=tokens, scores=scores,
+               memory_sub=np.ascontiguousarray(memory[::MEM_STRIDE]).astype(np.float32),
+               T=np.int32(memory.shape[0]))
+    if attention:
+        # -attn_debug: results["attention"][b][0] = [steps, src_length of chunk b]
+        T = memory.shape[0]
+        att = np.zeros((B, max_length, T), np.float32)
+        for j in range(B):
+            a = res["attention"][j][0].numpy()
+            att[j, :, : a.shape[1]] = a
+        out["attn"] = att[inv]
+    return out
 
 
 def run_beam(ns, model, cfg, chunks, beam_size=5, n_best=1, max_length=100, min_length=0, alpha=0.0):
@@ -233,7 +243,7 @@ SCENARIOS = [
     dict(name="transformer_greedy", cfg=dict(encoder_type="transformer"), seed=11, eos_bias=-3.0,
          chunks=dict(kind="mixed"), greedy=dict(max_length=100)),
     dict(name="transformer_pe_short", cfg=dict(encoder_type="transformer", position_encoding=True),
-         seed=12, eos_bias=0.0, chunks=dict(kind="short"), greedy=dict(max_length=40, min_length=5)),
+         seed=12, eos_bias=0.0, chunks=dict(kind="short"), greedy=dict(max_length=40, min_length=5, attention=True)),
     dict(name="transformer_beam", cfg=dict(encoder_type="transformer"), seed=13, eos_bias=2.5,
          chunks=dict(kind="mixed"), beam=dict(beam_size=5, n_best=1, max_length=100),
          beam2=dict(beam_size=5, n_best=3, max_length=60, min_length=10)),

@@ -199,7 +199,8 @@ class RefModel:
             h2 = self.ln(q1, p + ".layer_norm_2")
             ca = p + ".context_attn"
             qc = self._heads(self.lin(h2, ca + ".linear_query"))
-            cc, _ = self.attend(qc, st["ctx_k"][i], st["ctx_v"][i], src_mask)
+            cc, pc = self.attend(qc, st["ctx_k"][i], st["ctx_v"][i], src_mask)
+            st["attn"] = pc[:, 0, 0, :]   # attn["std"]: the last layer's head 0 (mha.py:187-192, :238-246)
             mid = self.lin(self._unheads(cc), ca + ".final_linear")
             x = self.ffn(mid + q1, p + ".feed_forward")
         out = self.ln(x, "decoder.layer_norm").squeeze(1)
@@ -226,18 +227,19 @@ def greedy(model: RefModel, src, lengths, max_length=100, min_length=0):
         st = model.decoder_state(memory, src)
         B = src.shape[0]
         tok = torch.full((B,), model.cfg.bos_idx, dtype=torch.long)
-        toks, lps = [], []
+        toks, lps, attns = [], [], []
         score = None
         for step in range(max_length):
             lp = model.decode_step(st, tok, step)
             lps.append(lp.clone())                                # model output (parity surface)
+            attns.append(st["attn"].clone())                      # return_attention (:491-501)
             if step < min_length:
                 lp[:, model.cfg.eos_idx] = -1e20                  # (:469-470)
             score, tok = lp.topk(1, dim=-1)                       # (:375)
             score, tok = score[:, 0], tok[:, 0]
             toks.append(tok)
     return dict(tokens=torch.stack(toks, 1).numpy().astype(np.int32), scores=score.numpy(),
-                logp=torch.stack(lps, 1).numpy(), memory=memory.numpy())
+                logp=torch.stack(lps, 1).numpy(), memory=memory.numpy(), attn=torch.stack(attns, 1).numpy())
 
 
 def tile(x, count, dim=0):

@@ -203,6 +203,29 @@ def test_greedy_vs_golden(name, graphs, ctx_path):
     assert np.abs(r["scores"].cpu().numpy() - z["scores"]).max() < LOGP_ATOL
 
 
+@pytest.mark.parametrize("graphs,ctx_path", [(True, 0), (False, 0), (True, 1)])
+def test_greedy_attention_vs_golden(graphs, ctx_path):
+    """-attn_debug attention (the last layer's head-0 context attention per
+    step) against the reference's return_attention output, memory-bank and
+    K/V forms."""
+    z, meta = gu.load("transformer_pe_short")
+    cfg, W = gu.model_for(meta)
+    g = meta["greedy"]
+    eng = _engine(cfg, W, max_batch=8, max_steps=g["max_length"], graphs=graphs)
+    eng.set_ctx_path(ctx_path)
+    from nanodecoder_amd.engine import pad_chunks
+    chunks = gu.chunks_of(z)
+    T = int(z["T"])
+    sig, lens = pad_chunks(chunks, T)
+    spans = np.full(len(chunks), T, np.int32)
+    r = eng.translate_greedy(sig, lens, spans, max_len=g["max_length"], min_len=g.get("min_length", 0),
+                             return_attn=True)
+    at = r["attn"].cpu().numpy()
+    assert (r["tokens"].cpu().numpy() == z["tokens"]).all()
+    for i, L in enumerate(z["lengths"]):
+        assert np.abs(at[i, :, :L] - z["attn"][i, :, :L]).max() < 1e-4, i
+
+
 @pytest.mark.parametrize("name,which", [("transformer_beam", ""), ("transformer_beam", "2"),
                                         ("transformer_aan", "")])
 def test_beam_vs_golden(name, which):

@@ -28,12 +28,16 @@ def test_greedy_matches_reference(name):
     chunks = gu.chunks_of(z)
     src, lens, order = ref_cpu.make_batch(chunks)
     inv = np.argsort(order)
-    r = ref_cpu.greedy(m, src, lens, **meta["greedy"])
+    r = ref_cpu.greedy(m, src, lens, **{k: v for k, v in meta["greedy"].items() if k != "attention"})
     assert gu.logp_close(r["logp"][inv], z["logp"], atol=1e-5, rtol=1e-6).all()
     assert (r["tokens"][inv] == z["tokens"]).all()
     np.testing.assert_allclose(r["scores"][inv], z["scores"], atol=1e-5)
     mem = r["memory"][inv].transpose(1, 0, 2)[:: meta["mem_stride"]]
     np.testing.assert_allclose(mem, z["memory_sub"], atol=1e-5)
+    if "attn" in z:  # -attn_debug attention (return_attention): rows cut at each chunk's length
+        att = r["attn"][inv]
+        for i, L in enumerate(z["lengths"]):
+            np.testing.assert_allclose(att[i, :, :L], z["attn"][i, :, :L], atol=1e-6)
 
 
 @pytest.mark.parametrize("name,which", [("transformer_beam", ""), ("transformer_beam", "2"),

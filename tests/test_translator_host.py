@@ -22,10 +22,16 @@ class FakeEngine:
         row = [4 + (L % 4), 4 + (S % 4), 5, 3] + [6] * (n - 4)
         return row[:n]
 
-    def translate_greedy(self, sig, L, S, max_len, min_len=0):
+    def translate_greedy(self, sig, L, S, max_len, min_len=0, return_attn=False):
         self.calls.append(("greedy", sig.shape, L.copy(), S.copy()))
         tok = torch.tensor([self._tok(int(a), int(b), max_len) for a, b in zip(L, S)], dtype=torch.int32)
-        return {"tokens": tok, "scores": torch.tensor(L, dtype=torch.float32) * -0.01, "logp": None}
+        out = {"tokens": tok, "scores": torch.tensor(L, dtype=torch.float32) * -0.01, "logp": None, "attn": None}
+        if return_attn:  # row t: uniform over the first t + 1 positions
+            a = torch.zeros(len(L), max_len, sig.shape[1])
+            for t in range(max_len):
+                a[:, t, : t + 1] = 1.0 / (t + 1)
+            out["attn"] = a
+        return out
 
     def translate_beam(self, sig, L, S, beam, n_best, alpha, max_len, min_len=0):
         self.calls.append(("beam", sig.shape, L.copy(), S.copy()))
@@ -105,6 +111,28 @@ def test_beam_n_best():
     sc, preds = tr.translate(chunks([512, 300]), batch_size=2)
     assert [len(p) for p in preds] == [2, 2]
     assert sc[0] == [0.0, -1.0]
+
+
+def test_attn_debug_dump_format():
+    """-attn_debug (translate/translator.py:285-336): '>' + the source samples
+    and '|' + the prediction + '</s>' as one header line, then one row of
+    weights per step, cut at the chunk length."""
+    import io
+    tr, eng = make_tr(max_length=6)
+    f = io.StringIO()
+    tr.setAttnFile(f)
+    src = chunks([5, 3])
+    sc, preds = tr.translate(src, batch_size=2, attn_debug=True)
+    lines = f.getvalue().split("\n")
+    assert lines[0].startswith("       > ") and "       | " in lines[0]
+    assert lines[0].split("|")[1].split() == preds[0][0].split() + ["</s>"]
+    assert lines[0].split()[1] == str(src[0][0])[:7]
+    rows = lines[1:7]
+    assert [len(r.split()) for r in rows] == [5] * 6
+    assert rows[1].split() == ["{:.5f}".format(0.5)] * 2 + ["{:.5f}".format(0.0)] * 3
+    assert len(lines[7].split("|")[0].split()) == 1 + 3       # second chunk: 3 samples
+    with pytest.raises(NotImplementedError):
+        make_tr(beam_size=5, fast=True)[0].translate(src, batch_size=2, attn_debug=True)
 
 
 def test_classic_beam_reference_batches():
