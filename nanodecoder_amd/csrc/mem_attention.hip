@@ -68,7 +68,11 @@ __device__ __forceinline__ float sum_by8(float v) {
   return xor32_sum(xor16_sum(v));
 }
 
-template <int EXPT>
+// NT > 0: the tile count is the compile-time NT (T in (64 (NT-1), 64 NT]);
+// every tile is processed (keys >= span masked), so the tile loop unrolls to
+// straight-line code and the compiler's wait counts on the in-flight tile
+// loads stay exact (a runtime loop makes it drain them every iteration).
+template <int EXPT, int NT>
 __global__ void __launch_bounds__(MB_NW * 64)
 dec_mem_attention_kernel(const float* __restrict__ qp, const float* __restrict__ mem,
                          const float* __restrict__ signal, const int* __restrict__ span, float pad_val,
@@ -83,7 +87,7 @@ dec_mem_attention_kernel(const float* __restrict__ qp, const float* __restrict__
   float* pbuf = spart + 2 * 256;              // [8 heads][8 keys]
   const float* ub = lds + MB_U;
   const int L = min(span[c], T);
-  const int ntile = (L + MB_TILE - 1) / MB_TILE;
+  const int ntile = NT > 0 ? NT : (L + MB_TILE - 1) / MB_TILE;
   const float* mc = mem + (size_t)c * ldT * ND_D;
 
   // ---- lane roles
@@ -130,16 +134,19 @@ dec_mem_attention_kernel(const float* __restrict__ qp, const float* __restrict__
   };
   auto put_scores = [&](int r, f32x4 v) { st4(spart + (r & 1) * 256 + (dp * 8 + shead) * 8 + 4 * kg, v); };
 
+  // The source samples of this wave's keys (lane l -> tile l >> 3, key l & 7)
+  // load FIRST: the waits that retire the tile loads below then retire it
+  // too, so no wait for it is left inside the loop (where it would drain
+  // the prefetched tiles every iteration).
+  const float sgv = signal[(size_t)c * T + min((lane >> 3) * MB_TILE + w * MB_KW + (lane & 7), T - 1)];
   f32x4 R0[MB_KW], R1[MB_KW];
   if (ntile > 0) fetch(0, R0);
   if (ntile > 1) fetch(1, R1);
-  // q' image (all heads; 512 threads x 16 B) and the source samples of this
-  // wave's keys (lane l -> tile l >> 3, key l & 7)
+  // q' image (all heads; 512 threads x 16 B)
   {
     const int h = threadIdx.x >> 6, q = threadIdx.x & 63;
     st4(lds + MB_U + h * ND_D + ((4 * q + 4 * h) & (ND_D - 1)), ld4(qp + pk(c, h * ND_D + 4 * q, ND_H * ND_D)));
   }
-  const float sgv = signal[(size_t)c * T + min((lane >> 3) * MB_TILE + w * MB_KW + (lane & 7), T - 1)];
   if (ntile > 0) put(0, R0);
   if (ntile > 1) put(1, R1);
   if (ntile > 2) fetch(2, R0);
@@ -205,9 +212,17 @@ dec_mem_attention_kernel(const float* __restrict__ qp, const float* __restrict__
     if (r + 2 < ntile) put(r + 2, R);
     if (r + 4 < ntile) fetch(r + 4, R);
   };
-  for (int r = 0; r < ntile; r += 2) {
-    body(r, R0);
-    if (r + 1 < ntile) body(r + 1, R1);
+  if constexpr (NT > 0) {
+#pragma unroll
+    for (int r = 0; r < NT; r += 2) {
+      body(r, R0);
+      if (r + 1 < NT) body(r + 1, R1);
+    }
+  } else {
+    for (int r = 0; r < ntile; r += 2) {
+      body(r, R0);
+      if (r + 1 < ntile) body(r + 1, R1);
+    }
   }
 
   // ---- merge the waves: head h's slots are combined by wave h
@@ -258,9 +273,16 @@ hipError_t launch_dec_mem_attention(const float* qp, const float* mem, const flo
     const char* e = getenv("ND_MEM_EXPT");  // timing experiments only (wrong results): 1 no loads, 2 no MFMA
     return e ? atoi(e) : 0;
   }();
-#define ND_MB_LAUNCH(X)                                                                                         \
-  hipLaunchKernelGGL(dec_mem_attention_kernel<X>, dim3(C), dim3(MB_NW * 64), mem_lds_bytes(), s, qp, mem, signal, \
-                     span, pad_val, out, T, ldT, stamp, attn_dbg, dbg_stride)
+  const bool full = (T + MB_TILE - 1) / MB_TILE == 8;  // the 512-sample chunks of every bench / translate batch
+#define ND_MB_LAUNCH(X)                                                                                           \
+  do {                                                                                                            \
+    if (full)                                                                                                     \
+      hipLaunchKernelGGL((dec_mem_attention_kernel<X, 8>), dim3(C), dim3(MB_NW * 64), mem_lds_bytes(), s, qp, mem, \
+                         signal, span, pad_val, out, T, ldT, stamp, attn_dbg, dbg_stride);                        \
+    else                                                                                                          \
+      hipLaunchKernelGGL((dec_mem_attention_kernel<X, 0>), dim3(C), dim3(MB_NW * 64), mem_lds_bytes(), s, qp, mem, \
+                         signal, span, pad_val, out, T, ldT, stamp, attn_dbg, dbg_stride);                        \
+  } while (0)
   if (expt == 1) ND_MB_LAUNCH(1);
   else if (expt == 2) ND_MB_LAUNCH(2);
   else if (expt == 3) ND_MB_LAUNCH(3);
@@ -336,8 +358,10 @@ hipError_t launch_stamp_reset(unsigned long long* stamps, int pairs, hipStream_t
 }
 
 hipError_t init_mem_attributes() {
-  const void* fns[] = {(const void*)dec_mem_attention_kernel<0>, (const void*)dec_mem_attention_kernel<1>,
-                       (const void*)dec_mem_attention_kernel<2>, (const void*)dec_mem_attention_kernel<3>};
+  const void* fns[] = {(const void*)dec_mem_attention_kernel<0, 0>, (const void*)dec_mem_attention_kernel<1, 0>,
+                       (const void*)dec_mem_attention_kernel<2, 0>, (const void*)dec_mem_attention_kernel<3, 0>,
+                       (const void*)dec_mem_attention_kernel<0, 8>, (const void*)dec_mem_attention_kernel<1, 8>,
+                       (const void*)dec_mem_attention_kernel<2, 8>, (const void*)dec_mem_attention_kernel<3, 8>};
   for (const void* f : fns) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mem_lds_bytes());
     if (e != hipSuccess) return e;
