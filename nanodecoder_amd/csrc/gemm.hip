@@ -22,6 +22,9 @@
 #include "common.hpp"
 #include "kernels.hpp"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace nd {
 
 // Merge P equal-width partials {mean_j, M2_j} of a 256-wide row.  All
@@ -50,10 +53,11 @@ __device__ __forceinline__ void merge_stats(const float* __restrict__ p, int P, 
   rs = 1.0f / sqrtf(m2 * (1.0f / 256.0f) + ND_LN_EPS);
 }
 
-// Sum over aligned groups of TPR lanes (16 or 32).
+// Sum over aligned groups of TPR lanes (16, 32 or the whole wave).
 template <int TPR>
 __device__ __forceinline__ float group_sum(float v) {
-  static_assert(TPR == 16 || TPR == 32, "group of 16 or 32 lanes");
+  static_assert(TPR == 16 || TPR == 32 || TPR == 64, "group of 16, 32 or 64 lanes");
+  if constexpr (TPR == 64) return wave_sum(v);
   v = sum16(v);
   if constexpr (TPR == 32) v += __shfl_xor(v, 16, 64);
   return v;
@@ -76,7 +80,10 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
   constexpr int FM = BM / WM / 32, FN = BN / WN / 32;
   constexpr int A4 = BM * BK / 4 / NT;
   constexpr int W4 = BN * BK / 4 / NT;
-  constexpr int SMEM = (2 * (BM + BN) * LDK > BM * LDC) ? 2 * (BM + BN) * LDK : BM * LDC;
+  // the epilogue stages the C tile through LDS in EP passes of BM / EP rows
+  // (one wave row group per pass when the whole tile would not fit)
+  constexpr int EP = (BM * LDC > 2 * (BM + BN) * LDK) ? WM : 1, RP = BM / EP;
+  constexpr int SMEM = (2 * (BM + BN) * LDK > RP * LDC) ? 2 * (BM + BN) * LDK : RP * LDC;
   static_assert(A4 >= 1 && W4 >= 1, "tile too small for the thread count");
   __shared__ __attribute__((aligned(16))) float smem[SMEM];
   __shared__ float s_mu[LN ? BM : 1], s_rs[LN ? BM : 1];
@@ -85,7 +92,8 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
   float* Cs = smem;                  // [BM][LDC] after the main loop
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+  const int nbt = blockIdx.x;
+  const int n0 = nbt * BN, m0 = blockIdx.y * BM;
   const int M = g.M, K = g.K;
   const float* __restrict__ A = g.A;
 
@@ -170,9 +178,9 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
   __syncthreads();
   for (int kt = 0; kt < KT; ++kt) {
     const int buf = kt & 1;
-    if (kt + 1 < KT) load_tile((kt + 1) * BK);
+    if (kt + 1 < KT && !(g.expt & 4)) load_tile((kt + 1) * BK);
 #pragma unroll
-    for (int kb = 0; kb < BK / 8; ++kb) {
+    for (int kb = 0; kb < BK / 8 && !(g.expt & 2); ++kb) {
       f32x4 af[FM], bf[FN];
 #pragma unroll
       for (int a = 0; a < FM; ++a)
@@ -191,41 +199,48 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
     __syncthreads();
   }
 
-  // epilogue 1: bias (+relu) into the LDS C tile
-#pragma unroll
-  for (int a = 0; a < FM; ++a)
-#pragma unroll
-    for (int b = 0; b < FN; ++b) {
-      const int cl = wn * FN * 32 + b * 32 + lr;
-      const float bv = g.bias ? g.bias[n0 + cl] : 0.f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float v = acc[a][b][r] + bv;
-        if constexpr (RELU) v = fmaxf(v, 0.f);
-        Cs[(wm * FM * 32 + a * 32 + mfma32_row(r, lane)) * LDC + cl] = v;
-      }
-    }
-  __syncthreads();
-  // epilogue 2: coalesced float4 rows (+ residual), row statistics
+  if (g.expt & 1) return;
   constexpr int TPR = BN / 4, RPP = NT / TPR;
   const int c4 = (tid % TPR) * 4;
-  for (int r0 = 0; r0 < BM; r0 += RPP) {
-    const int rl = r0 + tid / TPR, row = m0 + rl;
-    f32x4 v = ld4(&Cs[rl * LDC + c4]);
-    if (row < M) {
-      if constexpr (RESID) v += ld4(g.R + (size_t)row * g.ldr + n0 + c4);
-      st4(g.C + (size_t)row * g.ldc + n0 + c4, v);
+#pragma unroll
+  for (int ep = 0; ep < EP; ++ep) {
+    // epilogue 1: bias (+relu) into the LDS C tile (rows ep*RP .. +RP)
+    if (EP == 1 || wm == ep) {
+#pragma unroll
+      for (int a = 0; a < FM; ++a)
+#pragma unroll
+        for (int b = 0; b < FN; ++b) {
+          const int cl = wn * FN * 32 + b * 32 + lr;
+          const float bv = g.bias ? g.bias[n0 + cl] : 0.f;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            float v = acc[a][b][r] + bv;
+            if constexpr (RELU) v = fmaxf(v, 0.f);
+            Cs[(wm * FM * 32 + a * 32 + mfma32_row(r, lane) - ep * RP) * LDC + cl] = v;
+          }
+        }
     }
-    if (g.part_out) {
-      const float mu = group_sum<TPR>(v.x + v.y + v.z + v.w) * (1.0f / BN);
-      const f32x4 d = v - mu;
-      const float q = group_sum<TPR>(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w);
-      if ((tid % TPR) == 0 && row < M) {
-        float* p = g.part_out + ((size_t)row * ND_PART_LD + blockIdx.x) * 2;
-        p[0] = mu;
-        p[1] = q;
+    __syncthreads();
+    // epilogue 2: coalesced float4 rows (+ residual), row statistics
+    for (int r0 = 0; r0 < RP; r0 += RPP) {
+      const int rl = r0 + tid / TPR, row = m0 + ep * RP + rl;
+      f32x4 v = ld4(&Cs[rl * LDC + c4]);
+      if (row < M) {
+        if constexpr (RESID) v += ld4(g.R + (size_t)row * g.ldr + n0 + c4);
+        st4(g.C + (size_t)row * g.ldc + n0 + c4, v);
+      }
+      if (g.part_out) {
+        const float mu = group_sum<TPR>(v.x + v.y + v.z + v.w) * (1.0f / BN);
+        const f32x4 d = v - mu;
+        const float q = group_sum<TPR>(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w);
+        if ((tid % TPR) == 0 && row < M) {
+          float* p = g.part_out + ((size_t)row * ND_PART_LD + nbt) * 2;
+          p[0] = mu;
+          p[1] = q;
+        }
       }
     }
+    if (EP > 1) __syncthreads();
   }
 }
 
@@ -525,8 +540,21 @@ static hipError_t check_args(const GemmArgs& g) {
 
 hipError_t launch_gemm(GemmArgs& g, hipStream_t s) {
   if (g.M <= 0) return hipSuccess;
+  static const int expt = [] {
+    const char* e = getenv("ND_GEMM_EXPT");
+    return e ? atoi(e) : 0;
+  }();
+  g.expt = expt;
   hipError_t e = check_args(g);
   if (e != hipSuccess) return e;
+  static const int big = [] {
+    const char* e = getenv("ND_GEMM_TILE");  // 128: force the 128x128 tiles (A/B timing)
+    return !(e && atoi(e) == 128);
+  }();
+  // 256x256 tiles, 8 waves of 128x64: half the global->LDS bytes per flop and
+  // half the per-tile prologue/epilogue share of the 128x128 tile
+  const long t256 = (long)((g.M + 255) / 256) * (g.N / 256);
+  if (big && g.N % 256 == 0 && t256 >= 256) return launch_cfg<256, 256, 2, 4>(g, s);
   const long t128 = (long)((g.M + 127) / 128) * (g.N / 128);
   if (g.N % 128 == 0 && t128 >= 512) return launch_cfg<128, 128, 2, 2>(g, s);
   if (g.N % 64 != 0) return hipErrorInvalidValue;

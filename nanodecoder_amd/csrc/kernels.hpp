@@ -31,6 +31,7 @@ struct GemmArgs {
   const float* part_in = nullptr;
   int part_n_in = 0;
   int part_n_out = 0;  // set by launch_gemm
+  int expt = 0;        // timing experiments only (ND_GEMM_EXPT; wrong results): 1 no epilogue, 2 no MFMA, 4 no loads
 };
 #define ND_PART_LD 16  // partial-stat slots per row (max column tiles of a 256-wide row)
 // row-major operands (encoder, large M): LDS-tiled MFMA kernel

@@ -34,7 +34,9 @@ def _oracle():
                                                 (16384, 512, 2048, False, False, True),
                                                 (5000, 256, 2048, False, False, True),
                                                 (256, 2048, 256, True, True, False),
-                                                (37, 256, 256, False, False, True)])
+                                                (37, 256, 256, False, False, True),
+                                                (65536, 256, 256, True, True, True),      # 256x256 tiles
+                                                (65529, 256, 2048, False, False, True)])  # ragged last tile
 def test_gemm_vs_fp64(M, N, K, ln, relu, res):
     from nanodecoder_amd.engine import op_gemm
     g = torch.Generator().manual_seed(M + N + K)

@@ -56,6 +56,13 @@ def gemm_case(M, N, K, ln, relu, res):
     print(f"gemm M={M:6d} N={N:5d} K={K:5d} ln={int(ln)} relu={int(relu)} res={int(res)}: {us:9.2f} us  {tf:6.1f} TF/s")
 
 
+if ONLY == "enc":
+    # the encoder's GEMM shapes at B = 256 chunks x 512 samples
+    gemm_case(131072, 768, 256, True, False, False)    # QKV (LN)
+    gemm_case(131072, 256, 256, False, False, True)    # Wo (+res)
+    gemm_case(131072, 2048, 256, True, True, False)    # FFN1 (LN, relu)
+    gemm_case(131072, 256, 2048, False, False, True)   # FFN2 (+res)
+    sys.exit(0)
 if ONLY == "mem":
     # memory-bank attention: scaling in the chunk count and the key count
     for C, T in ((64, 512), (128, 512), (256, 512), (512, 512), (256, 256), (256, 128)):
