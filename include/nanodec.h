@@ -177,6 +177,18 @@ const char* nd_version(void);
 int nd_op_gemm(const float* A, const float* W, const float* bias, const float* R, float* C, int32_t M,
                int32_t N, int32_t K, int32_t norm, int32_t relu, void* stream);
 
+/* Split-fp16 image of a weight for nd_op_gemm_split (the engine's encoder
+ * GEMMs): Wh [N][K/8][hi 8 | lo 8] fp16 halves of W * 2^s with hi = fp16(x),
+ * lo = fp16(x - hi); *wscale receives 2^-s.  K % 32 == 0.  Synchronises the
+ * stream (load-time operation). */
+int nd_op_split_weight(const float* W, int32_t N, int32_t K, uint16_t* Wh, float* wscale, void* stream);
+
+/* nd_op_gemm on a split weight: A is split the same way as it is staged and
+ * the product summed as hi*hi + hi*lo + lo*hi on fp16 MFMAs with fp32
+ * accumulation (22-bit operands; fp32-class results). */
+int nd_op_gemm_split(const float* A, const uint16_t* Wh, float wscale, const float* bias, const float* R, float* C,
+                     int32_t M, int32_t N, int32_t K, int32_t norm, int32_t relu, void* stream);
+
 /* The decoder-step form of the same GEMM, on the fragment-packed "P16"
  * layout the engine keeps decoder activations and step weights in: an
  * [M, N] matrix (M, N multiples of 16) stored as 16x16 blocks in row-major
@@ -189,6 +201,16 @@ int nd_op_gemm(const float* A, const float* W, const float* bias, const float* R
 int nd_op_gemm_p16(const float* A, const float* W, const float* bias, const float* R, float* C, int32_t M,
                    int32_t N, int32_t K, const float* part_in, int32_t part_n_in, float* part_out, int32_t relu,
                    int32_t* part_n_out, void* stream);
+
+/* Split-fp16 decoder-step GEMM: W as its P16H image (nd_op_pack_p16h:
+ * [N/16][K/32][hi | lo][64 lanes][8 halves] of W * 2^s, *wscale = 2^-s from
+ * a row-major W [N, K]; synchronises the stream), A split on the fly, the
+ * product hi*hi + hi*lo + lo*hi on 16x16x32 f16 MFMAs into fp32.  Otherwise
+ * exactly nd_op_gemm_p16. */
+int nd_op_pack_p16h(const float* W, int32_t N, int32_t K, uint16_t* out, float* wscale, void* stream);
+int nd_op_gemm_p16_split(const float* A, const uint16_t* Wh, float wscale, const float* bias, const float* R, float* C,
+                         int32_t M, int32_t N, int32_t K, const float* part_in, int32_t part_n_in, float* part_out,
+                         int32_t relu, int32_t* part_n_out, void* stream);
 
 /* row-major [M, N] -> P16 packed (M, N multiples of 16). */
 int nd_op_pack_p16(const float* src, float* dst, int32_t M, int32_t N, void* stream);

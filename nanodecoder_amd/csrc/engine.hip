@@ -109,6 +109,9 @@ struct nd_ctx {
   std::vector<DecLayer> dec;
   float *ctxkv_w = nullptr, *ctxkv_b = nullptr, *nctxkv_w = nullptr, *nctxkv_b = nullptr;
   float *emb = nullptr, *pe = nullptr, *dec_ln_g = nullptr, *dec_ln_b = nullptr, *gen_w = nullptr, *gen_b = nullptr;
+  // split-fp16 images of the row-major GEMM weights (gemm.hip, H3), keyed by
+  // the fp32 weight they were made from (built at finalize)
+  std::map<const float*, std::pair<uint16_t*, float>> split;
 
   // workspaces
   float* sig = nullptr;
@@ -415,6 +418,15 @@ struct G {
     return *this;
   }
   G& relu() { a.relu = true; return *this; }
+  // use the weight's split-fp16 image when finalize made one
+  G& h3(const nd_ctx* c) {
+    auto it = c->split.find(a.W);
+    if (it != c->split.end()) {
+      a.Wh = it->second.first;
+      a.wscale = it->second.second;
+    }
+    return *this;
+  }
   G& res(const float* R, int ldr) { a.R = R; a.ldr = ldr; return *this; }
   G& stats(float* part) { a.part_out = part; return *this; }
   bool packed = false;
@@ -434,11 +446,11 @@ static hipError_t enqueue_encode_transformer(nd_ctx* c, int B, int T, hipStream_
   int pnx = 1, pny = 0;
   for (auto& L : c->enc) {
     // encoder/transformer.py:36-54
-    LCHK(G(c->x, D, L.nwqkv, 3 * D, D, L.nbqkv, c->big, 3 * D, M).ln(c->x_part, pnx).run(s));
+    LCHK(G(c->x, D, L.nwqkv, 3 * D, D, L.nbqkv, c->big, 3 * D, M).h3(c).ln(c->x_part, pnx).run(s));
     LCHK(nd::launch_enc_attention(c->big, c->sig, c->span, c->att, B, T, s));
-    LCHK(G(c->att, D, L.wo, D, D, L.bo, c->y, D, M).res(c->x, D).stats(c->y_part).run(s, &pny));
-    LCHK(G(c->y, D, L.nw1, F, D, L.nb1, c->big, F, M).ln(c->y_part, pny).relu().run(s));
-    LCHK(G(c->big, F, L.w2, D, F, L.b2, c->x, D, M).res(c->y, D).stats(c->x_part).run(s, &pnx));
+    LCHK(G(c->att, D, L.wo, D, D, L.bo, c->y, D, M).h3(c).res(c->x, D).stats(c->y_part).run(s, &pny));
+    LCHK(G(c->y, D, L.nw1, F, D, L.nb1, c->big, F, M).h3(c).ln(c->y_part, pny).relu().run(s));
+    LCHK(G(c->big, F, L.w2, D, F, L.b2, c->x, D, M).h3(c).res(c->y, D).stats(c->x_part).run(s, &pnx));
   }
   c->x_pn = pnx;
   return hipSuccess;
@@ -447,8 +459,8 @@ static hipError_t enqueue_encode_transformer(nd_ctx* c, int B, int T, hipStream_
 static hipError_t enqueue_ctxkv(nd_ctx* c, int B, int T, hipStream_t s) {
   const int M = B * T, D = c->D, N = (int)c->dec.size() * 2 * D;
   if (c->cfg.encoder_type == ND_ENC_TRANSFORMER)
-    return G(c->x, D, c->nctxkv_w, N, D, c->nctxkv_b, c->ctxkv, N, M).ln(c->x_part, c->x_pn).run(s);
-  return G(c->x, D, c->ctxkv_w, N, D, c->ctxkv_b, c->ctxkv, N, M).run(s);
+    return G(c->x, D, c->nctxkv_w, N, D, c->nctxkv_b, c->ctxkv, N, M).h3(c).ln(c->x_part, c->x_pn).run(s);
+  return G(c->x, D, c->ctxkv_w, N, D, c->ctxkv_b, c->ctxkv, N, M).h3(c).run(s);
 }
 
 static hipError_t enqueue_encode(nd_ctx* c, int B, int T, hipStream_t s);
@@ -491,31 +503,31 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
       // average_attn.py:55-106 + the layer residual (decoder/transformer.py:82-86)
       LCHK(nd::launch_aan_prep(c->dx, L.ln1_g, L.ln1_b, cache, anc, anc_ld, step, S, c->axn, c->aavg, c->aavg_part,
                                R, s));
-      LCHK(G(c->aavg, D, L.paw1, D, D, L.nab1, c->ah, D, R).p16().ln(c->aavg_part, 1).relu().run(s));
-      LCHK(G(c->ah, D, L.paw2, D, D, L.ab2, c->aa, D, R).p16().res(c->aavg, D).run(s));
-      LCHK(G(c->axn, D, L.pgwx, 2 * D, D, L.gb, c->ag, 2 * D, R).p16().run(s));
-      LCHK(G(c->aa, D, L.pgwa, 2 * D, D, nullptr, c->ag, 2 * D, R).p16().res(c->ag, 2 * D).run(s));
+      LCHK(G(c->aavg, D, L.paw1, D, D, L.nab1, c->ah, D, R).p16().h3(c).ln(c->aavg_part, 1).relu().run(s));
+      LCHK(G(c->ah, D, L.paw2, D, D, L.ab2, c->aa, D, R).p16().h3(c).res(c->aavg, D).run(s));
+      LCHK(G(c->axn, D, L.pgwx, 2 * D, D, L.gb, c->ag, 2 * D, R).p16().h3(c).run(s));
+      LCHK(G(c->aa, D, L.pgwa, 2 * D, D, nullptr, c->ag, 2 * D, R).p16().h3(c).res(c->ag, 2 * D).run(s));
       LCHK(nd::launch_aan_gate(c->ag, c->axn, c->aa, c->dx, c->dq1, c->dq1_part, R, s));
       pnq = 1;
     } else {
-      LCHK(G(c->dx, D, L.pwqkv, 3 * D, D, L.nbqkv, c->dqkv, 3 * D, R).p16().ln(c->dx_part, pnx).run(s));
+      LCHK(G(c->dx, D, L.pwqkv, 3 * D, D, L.nbqkv, c->dqkv, 3 * D, R).p16().h3(c).ln(c->dx_part, pnx).run(s));
       LCHK(nd::launch_dec_self_attention(c->dqkv, cache, anc, anc_ld, step, S, c->datt, R, s));
-      LCHK(G(c->datt, D, L.pwo, D, D, L.bo, c->dq1, D, R).p16().res(c->dx, D).stats(c->dq1_part).run(s, &pnq));
+      LCHK(G(c->datt, D, L.pwo, D, D, L.bo, c->dq1, D, R).p16().h3(c).res(c->dx, D).stats(c->dq1_part).run(s, &pnq));
     }
     if (mb) {  // memory-bank form (attention.hip)
       const int HD = ND_H * D;
-      LCHK(G(c->dq1, D, L.pwqk, HD, D, L.bqk, c->dqk, HD, R).p16().ln(c->dq1_part, pnq).run(s));
+      LCHK(G(c->dq1, D, L.pwqk, HD, D, L.bqk, c->dqk, HD, R).p16().h3(c).ln(c->dq1_part, pnq).run(s));
       LCHK(nd::launch_dec_mem_attention(c->dqk, c->mem, c->sig, c->span, (float)c->cfg.pad_idx, c->dU, C, rpc, T, T,
                                         s, stamp, dbg, dbg_stride));
-      LCHK(G(c->dU, HD, L.pwvo, D, HD, L.bvo, c->dmid, D, R).p16().res(c->dq1, D).stats(c->dmid_part).run(s, &pnm));
+      LCHK(G(c->dU, HD, L.pwvo, D, HD, L.bvo, c->dmid, D, R).p16().h3(c).res(c->dq1, D).stats(c->dmid_part).run(s, &pnm));
     } else {
-      LCHK(G(c->dq1, D, L.pcwq, D, D, L.ncbq, c->dcq, D, R).p16().ln(c->dq1_part, pnq).run(s));
+      LCHK(G(c->dq1, D, L.pcwq, D, D, L.ncbq, c->dcq, D, R).p16().h3(c).ln(c->dq1_part, pnq).run(s));
       LCHK(nd::launch_dec_ctx_attention(c->dcq, c->ctxkv, Ld * 2 * D, i * 2 * D, c->sig, c->span,
                                         (float)c->cfg.pad_idx, c->datt, C, rpc, T, s, stamp, dbg, dbg_stride));
-      LCHK(G(c->datt, D, L.pcwo, D, D, L.cbo, c->dmid, D, R).p16().res(c->dq1, D).stats(c->dmid_part).run(s, &pnm));
+      LCHK(G(c->datt, D, L.pcwo, D, D, L.cbo, c->dmid, D, R).p16().h3(c).res(c->dq1, D).stats(c->dmid_part).run(s, &pnm));
     }
-    LCHK(G(c->dmid, D, L.pw1, F, D, L.nb1, c->dhid, F, R).p16().ln(c->dmid_part, pnm).relu().run(s));
-    LCHK(G(c->dhid, F, L.pw2, D, F, L.b2, c->dx, D, R).p16().res(c->dmid, D).stats(c->dx_part).run(s, &pnx));
+    LCHK(G(c->dmid, D, L.pw1, F, D, L.nb1, c->dhid, F, R).p16().h3(c).ln(c->dmid_part, pnm).relu().run(s));
+    LCHK(G(c->dhid, F, L.pw2, D, F, L.b2, c->dx, D, R).p16().h3(c).res(c->dmid, D).stats(c->dx_part).run(s, &pnx));
   }
   return hipSuccess;
 }
@@ -681,6 +693,22 @@ int nd_load_weight(nd_ctx* c, const char* name, const float* host, const int64_t
   return ND_OK;
 }
 
+// P16 step weight (fp32, for the fp32 kernels) and its split-fp16 P16H image
+// (gemm.hip H3), registered under the P16 pointer for G::h3
+static hipError_t pack_step_weight(nd_ctx* c, const float* src, int ld, float* dst, int rows, int cols) {
+  hipError_t e = nd::launch_pack_p16(src, ld, dst, rows, cols, c->es);
+  if (e != hipSuccess) return e;
+  uint16_t* h = nullptr;
+  auto it = c->split.find(dst);
+  if (it != c->split.end()) h = it->second.first;  // finalize called again: refresh in place
+  // hi and lo halves: two per element
+  if (!h && (e = dalloc(c, &h, (size_t)2 * rows * cols)) != hipSuccess) return e;
+  float sc = 1.f;
+  if ((e = nd::launch_pack_p16h(src, ld, rows, cols, h, &sc, c->es)) != hipSuccess) return e;
+  c->split[dst] = {h, sc};
+  return hipSuccess;
+}
+
 // Memory-bank form of the context attention (attention.hip): per decoder
 // layer, in f64 on the host from the reference weights,
 //   W_qk[h*256+i][k] = sum_a W_k[32h+a][i] W_q'[32h+a][k] / sqrt(32)
@@ -751,10 +779,10 @@ static int derive_memory_bank_weights(nd_ctx* c) {
       }
     }
     if ((e = hipMemcpy(scratch, wqk.data(), wqk.size() * 4, hipMemcpyHostToDevice)) != hipSuccess ||
-        (e = nd::launch_pack_p16(scratch, D, L.pwqk, H * D, D, c->es)) != hipSuccess ||
+        (e = pack_step_weight(c, scratch, D, L.pwqk, H * D, D)) != hipSuccess ||
         (e = hipStreamSynchronize(c->es)) != hipSuccess ||
         (e = hipMemcpy(scratch, wvo.data(), wvo.size() * 4, hipMemcpyHostToDevice)) != hipSuccess ||
-        (e = nd::launch_pack_p16(scratch, H * D, L.pwvo, D, H * D, c->es)) != hipSuccess ||
+        (e = pack_step_weight(c, scratch, H * D, L.pwvo, D, H * D)) != hipSuccess ||
         (e = hipStreamSynchronize(c->es)) != hipSuccess ||
         (e = hipMemcpy(L.bqk, bqk.data(), bqk.size() * 4, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(L.bvo, bvo.data(), bvo.size() * 4, hipMemcpyHostToDevice)) != hipSuccess)
@@ -808,22 +836,47 @@ int nd_finalize(nd_ctx* c) {
     for (auto& L : c->dec) {
       if (c->cfg.self_attn_type == ND_SELF_AVERAGE) {
         HIPCHK(fold(L.aw1, L.ab1, L.aln_g, L.aln_b, L.naw1, L.nab1, D, D));
-        HIPCHK(nd::launch_pack_p16(L.naw1, D, L.paw1, D, D, c->es));
-        HIPCHK(nd::launch_pack_p16(L.aw2, D, L.paw2, D, D, c->es));
-        HIPCHK(nd::launch_pack_p16(L.gw, 2 * D, L.pgwx, 2 * D, D, c->es));      // gate columns of xn
-        HIPCHK(nd::launch_pack_p16(L.gw + D, 2 * D, L.pgwa, 2 * D, D, c->es));  // gate columns of a
+        HIPCHK(pack_step_weight(c, L.naw1, D, L.paw1, D, D));
+        HIPCHK(pack_step_weight(c, L.aw2, D, L.paw2, D, D));
+        HIPCHK(pack_step_weight(c, L.gw, 2 * D, L.pgwx, 2 * D, D));      // gate columns of xn
+        HIPCHK(pack_step_weight(c, L.gw + D, 2 * D, L.pgwa, 2 * D, D));  // gate columns of a
       } else {
         HIPCHK(fold(L.wqkv, L.bqkv, L.ln1_g, L.ln1_b, L.nwqkv, L.nbqkv, 3 * D, D));
-        HIPCHK(nd::launch_pack_p16(L.nwqkv, D, L.pwqkv, 3 * D, D, c->es));
-        HIPCHK(nd::launch_pack_p16(L.wo, D, L.pwo, D, D, c->es));
+        HIPCHK(pack_step_weight(c, L.nwqkv, D, L.pwqkv, 3 * D, D));
+        HIPCHK(pack_step_weight(c, L.wo, D, L.pwo, D, D));
       }
       HIPCHK(fold(L.cwq, L.cbq, L.ln2_g, L.ln2_b, L.ncwq, L.ncbq, D, D));
       HIPCHK(fold(L.w1, L.b1, L.fln_g, L.fln_b, L.nw1, L.nb1, F, D));
-      HIPCHK(nd::launch_pack_p16(L.ncwq, D, L.pcwq, D, D, c->es));
-      HIPCHK(nd::launch_pack_p16(L.cwo, D, L.pcwo, D, D, c->es));
-      HIPCHK(nd::launch_pack_p16(L.nw1, D, L.pw1, F, D, c->es));
-      HIPCHK(nd::launch_pack_p16(L.w2, F, L.pw2, D, F, c->es));
+      HIPCHK(pack_step_weight(c, L.ncwq, D, L.pcwq, D, D));
+      HIPCHK(pack_step_weight(c, L.cwo, D, L.pcwo, D, D));
+      HIPCHK(pack_step_weight(c, L.nw1, D, L.pw1, F, D));
+      HIPCHK(pack_step_weight(c, L.w2, F, L.pw2, D, F));
     }
+    HIPCHK(hipStreamSynchronize(c->es));
+  }
+  {
+    // split-fp16 images of the encoder-side row-major GEMM weights
+    // (gemm.hip H3); ND_GEMM_F32=1 at run time keeps the fp32 kernels
+    const int D = c->D, F = c->F, L2 = (int)c->dec.size() * 2 * D;
+    auto mk = [&](const float* W, int N, int K) -> hipError_t {
+      uint16_t* h = nullptr;
+      float sc = 1.f;
+      auto it = c->split.find(W);
+      if (it != c->split.end()) h = it->second.first;  // finalize called again: refresh in place
+      hipError_t e = h ? hipSuccess : dalloc(c, &h, (size_t)2 * N * K);
+      if (e == hipSuccess) e = nd::launch_split_weight(W, N, K, h, &sc, c->es);
+      if (e == hipSuccess) c->split[W] = {h, sc};
+      return e;
+    };
+    for (auto& L : c->enc) {
+      HIPCHK(mk(L.nwqkv, 3 * D, D));
+      HIPCHK(mk(L.wo, D, D));
+      HIPCHK(mk(L.nw1, F, D));
+      HIPCHK(mk(L.w2, D, F));
+    }
+    HIPCHK(mk(c->cfg.encoder_type == ND_ENC_TRANSFORMER ? c->nctxkv_w : c->ctxkv_w, L2, D));
+    for (size_t l = 1; l < c->nano.size(); ++l) HIPCHK(mk(c->nano[l].wih, 8 * c->H, 2 * c->H));
+    if (c->nano_W) HIPCHK(mk(c->nano_W, D, 2 * c->H));
     HIPCHK(hipStreamSynchronize(c->es));
   }
   {
@@ -1107,6 +1160,26 @@ int nd_op_gemm(const float* A, const float* W, const float* bias, const float* R
   return ND_OK;
 }
 
+int nd_op_split_weight(const float* W, int32_t N, int32_t K, uint16_t* Wh, float* wscale, void* stream) {
+  hipError_t e = nd::launch_split_weight(W, N, K, Wh, wscale, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("split_weight: ") + hipGetErrorString(e));
+  return ND_OK;
+}
+
+int nd_op_gemm_split(const float* A, const uint16_t* Wh, float wscale, const float* bias, const float* R, float* C,
+                     int32_t M, int32_t N, int32_t K, int32_t norm, int32_t relu, void* stream) {
+  if (!Wh) return fail(ND_ERR_ARG, "gemm_split: null Wh");
+  G g(A, K, nullptr, N, K, bias, C, N, M);
+  g.a.Wh = Wh;
+  g.a.wscale = wscale;
+  g.a.norm = norm != 0;
+  g.a.relu = relu != 0;
+  if (R) g.res(R, N);
+  hipError_t e = g.run((hipStream_t)stream);
+  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("gemm_split: ") + hipGetErrorString(e));
+  return ND_OK;
+}
+
 static int ensure_attributes() {
   static hipError_t e = nd::init_kernel_attributes();
   return e == hipSuccess ? ND_OK : fail(ND_ERR_HIP, "hipFuncSetAttribute failed");
@@ -1121,6 +1194,27 @@ int nd_op_gemm_p16(const float* A, const float* W, const float* bias, const floa
   g.norm = part_in != nullptr; g.part_in = part_in; g.part_n_in = part_n_in; g.part_out = part_out;
   hipError_t e = nd::launch_gemm_p16(g, (hipStream_t)stream);
   if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("gemm_p16: ") + hipGetErrorString(e));
+  if (part_n_out) *part_n_out = g.part_n_out;
+  return ND_OK;
+}
+
+int nd_op_pack_p16h(const float* W, int32_t N, int32_t K, uint16_t* out, float* wscale, void* stream) {
+  hipError_t e = nd::launch_pack_p16h(W, K, N, K, out, wscale, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("pack_p16h: ") + hipGetErrorString(e));
+  return ND_OK;
+}
+
+int nd_op_gemm_p16_split(const float* A, const uint16_t* Wh, float wscale, const float* bias, const float* R, float* C,
+                         int32_t M, int32_t N, int32_t K, const float* part_in, int32_t part_n_in, float* part_out,
+                         int32_t relu, int32_t* part_n_out, void* stream) {
+  if (int rc = ensure_attributes()) return rc;
+  if (!Wh) return fail(ND_ERR_ARG, "gemm_p16_split: null Wh");
+  nd::GemmArgs g;
+  g.A = A; g.Wh = Wh; g.wscale = wscale; g.bias = bias; g.R = R; g.C = C; g.M = M; g.N = N; g.K = K;
+  g.relu = relu != 0; g.norm = part_in != nullptr; g.part_in = part_in; g.part_n_in = part_n_in;
+  g.part_out = part_out;
+  hipError_t e = nd::launch_gemm_p16(g, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("gemm_p16_split: ") + hipGetErrorString(e));
   if (part_n_out) *part_n_out = g.part_n_out;
   return ND_OK;
 }
@@ -1190,12 +1284,12 @@ static hipError_t enqueue_encode_nano(nd_ctx* c, int B, int T, hipStream_t s) {
     float* out = bufs[l & 1];
     const bool last = l == Lz - 1;
     if (l > 0)
-      LCHK(gemm(bufs[(l - 1) & 1], 2 * c->H, L.wih, 8 * c->H, 2 * c->H, L.bsum, c->nano_xp, 8 * c->H, M, s));
+      LCHK(G(bufs[(l - 1) & 1], 2 * c->H, L.wih, 8 * c->H, 2 * c->H, L.bsum, c->nano_xp, 8 * c->H, M).h3(c).run(s));
     if (last) LCHK(hipMemsetAsync(out, 0, (size_t)M * 2 * c->H * sizeof(float), s));
     LCHK(nd::launch_lstm_layer(c->nano_xp, c->sig, L.wih, L.bsum, L.whh, c->len, B, T, out,
                                last ? nullptr : L.bn_scale, last ? nullptr : L.bn_shift, l == 0, s));
   }
-  return gemm(bufs[(Lz - 1) & 1], 2 * c->H, c->nano_W, D, 2 * c->H, nullptr, c->x, D, M, s);
+  return G(bufs[(Lz - 1) & 1], 2 * c->H, c->nano_W, D, 2 * c->H, nullptr, c->x, D, M).h3(c).run(s);
 }
 
 static hipError_t enqueue_encode(nd_ctx* c, int B, int T, hipStream_t s) {

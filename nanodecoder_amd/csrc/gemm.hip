@@ -23,7 +23,9 @@
 #include "kernels.hpp"
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
+#include <cstring>
 
 namespace nd {
 
@@ -73,7 +75,31 @@ __device__ __forceinline__ float group_sum(float v) {
 // sums k = {i, 4+i}: a permutation of K that A and W share).  The epilogue
 // stages the C tile through LDS so output / residual traffic is coalesced
 // float4 rows, and row statistics fall out of the same pass.
-template <int BM, int BN, int WM, int WN, bool LN, bool RELU, bool RESID>
+// Split-fp16 operands (H3): a fp32 value x is carried as hi = fp16(x) and
+// lo = fp16(x - hi), 22 significant bits, and a product as
+// hi*hi + hi*lo + lo*hi (the dropped lo*lo is below 2^-22 relative) on
+// v_mfma_f32_32x32x16_f16, which multiplies exactly into an fp32
+// accumulator: fp32-class accuracy at 16/3 of the fp32 MFMA rate.  W is
+// split once at load time (scaled by 2^s so its lo plane stays out of the
+// fp16 subnormals); A is split while it is staged into LDS (after the
+// LayerNorm), so every element is converted once per workgroup.  The LDS
+// row image is [k/8][hi 8 | lo 8] halves: the same 144-byte rows as the
+// fp32 tile, and each lane's MFMA operand (8 consecutive k of one row) is a
+// single ds_read_b128 per plane.
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ f32x16 mfma32h(h8 a, h8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void split4(f32x4 v, h4& hi, h4& lo) {
+  hi = {(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
+  lo = {(_Float16)(v.x - (float)hi.x), (_Float16)(v.y - (float)hi.y), (_Float16)(v.z - (float)hi.z),
+        (_Float16)(v.w - (float)hi.w)};
+}
+
+template <int BM, int BN, int WM, int WN, bool H3, bool LN, bool RELU, bool RESID>
 __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g) {
   constexpr int NT = WM * WN * 64;
   constexpr int BK = 32, LDK = BK + 4, LDC = BN + 4;
@@ -145,14 +171,25 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
 #pragma unroll
     for (int i = 0; i < W4; ++i) {
       const int f = tid + i * NT, row = f >> 3, c = (f & 7) * 4;
-      rw[i] = ld4(g.W + (size_t)(n0 + row) * g.ldw + k0 + c);
+      if constexpr (H3)  // 16-byte chunk c/4 of the row's [k0, k0+32) image: 8-k group c/8, plane (c/4)&1
+        rw[i] = *reinterpret_cast<const f32x4*>(g.Wh + (size_t)(n0 + row) * 2 * K + 2 * k0 + 2 * c);
+      else
+        rw[i] = ld4(g.W + (size_t)(n0 + row) * g.ldw + k0 + c);
     }
   };
   auto store_tile = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < A4; ++i) {
       const int f = tid + i * NT, row = f >> 3, c = (f & 7) * 4;
-      st4(&As[buf * BM * LDK + row * LDK + c], ra[i]);
+      if constexpr (H3) {
+        h4 hi, lo;
+        split4(ra[i], hi, lo);
+        float* p = &As[buf * BM * LDK + row * LDK + (c >> 3) * 8 + ((c >> 2) & 1) * 2];
+        *reinterpret_cast<h4*>(p) = hi;
+        *reinterpret_cast<h4*>(p + 4) = lo;
+      } else {
+        st4(&As[buf * BM * LDK + row * LDK + c], ra[i]);
+      }
     }
 #pragma unroll
     for (int i = 0; i < W4; ++i) {
@@ -179,6 +216,33 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
   for (int kt = 0; kt < KT; ++kt) {
     const int buf = kt & 1;
     if (kt + 1 < KT && !(g.expt & 4)) load_tile((kt + 1) * BK);
+    if constexpr (H3) {
+#pragma unroll
+      for (int ks = 0; ks < BK / 16 && !(g.expt & 2); ++ks) {
+        h8 ah[FM], al[FM], bh[FN], bl[FN];
+        const int o = (2 * ks + lh) * 8;  // this lane's 8-k group: hi at o, lo at o + 4 (words)
+#pragma unroll
+        for (int a = 0; a < FM; ++a) {
+          const float* p = &As[buf * BM * LDK + (wm * FM * 32 + a * 32 + lr) * LDK + o];
+          ah[a] = *reinterpret_cast<const h8*>(p);
+          al[a] = *reinterpret_cast<const h8*>(p + 4);
+        }
+#pragma unroll
+        for (int b = 0; b < FN; ++b) {
+          const float* p = &Ws[buf * BN * LDK + (wn * FN * 32 + b * 32 + lr) * LDK + o];
+          bh[b] = *reinterpret_cast<const h8*>(p);
+          bl[b] = *reinterpret_cast<const h8*>(p + 4);
+        }
+#pragma unroll
+        for (int a = 0; a < FM; ++a)
+#pragma unroll
+          for (int b = 0; b < FN; ++b) {
+            acc[a][b] = mfma32h(ah[a], bl[b], acc[a][b]);
+            acc[a][b] = mfma32h(al[a], bh[b], acc[a][b]);
+            acc[a][b] = mfma32h(ah[a], bh[b], acc[a][b]);
+          }
+      }
+    } else
 #pragma unroll
     for (int kb = 0; kb < BK / 8 && !(g.expt & 2); ++kb) {
       f32x4 af[FM], bf[FN];
@@ -214,7 +278,7 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
           const float bv = g.bias ? g.bias[n0 + cl] : 0.f;
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            float v = acc[a][b][r] + bv;
+            float v = (H3 ? acc[a][b][r] * g.wscale : acc[a][b][r]) + bv;
             if constexpr (RELU) v = fmaxf(v, 0.f);
             Cs[(wm * FM * 32 + a * 32 + mfma32_row(r, lane) - ep * RP) * LDC + cl] = v;
           }
@@ -263,7 +327,26 @@ __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-template <int NT, int KS, int KW, bool LN, bool RELU, bool RESID>
+// Split-fp16 form on the P16 layout (H3, see the row-major kernel): the
+// 16x16x32 f16 MFMA takes 8 k per lane; lane l supplies the 4 k of its P16
+// entry in k-block 2p followed by the 4 of k-block 2p+1, for the weight and
+// the activation alike (one shared permutation of the pair's 32 k), and its D
+// fragment is the P16 entry of C as with 16x16x4.  The weight image (P16H,
+// launch_pack_p16h) holds per column block and k pair a hi plane and a lo
+// plane, each one 1 KB wave access: [nb][K/32][hi | lo][64 lanes][8 halves].
+__device__ __forceinline__ f32x4 mfma16h(h8 a, h8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void split8(f32x4 x0, f32x4 x1, h8& hi, h8& lo) {
+  h4 h0, l0, h1, l1;
+  split4(x0, h0, l0);
+  split4(x1, h1, l1);
+  hi = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+  lo = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
+}
+
+template <int NT, int KS, int KW, bool H3, bool LN, bool RELU, bool RESID>
 __global__ void __launch_bounds__(NT* KS * 64) gemm_p16_kernel(const GemmArgs g) {
   constexpr int WAVES = NT * KS;
   constexpr int NF = KW / 16;  // 16-k blocks per wave
@@ -273,7 +356,9 @@ __global__ void __launch_bounds__(NT* KS * 64) gemm_p16_kernel(const GemmArgs g)
   const int nb = blockIdx.x * NT + wt, mb = blockIdx.y;
   const int KB = g.K >> 4, NB = g.N >> 4;
   const f32x4* __restrict__ ap = reinterpret_cast<const f32x4*>(g.A) + ((size_t)mb * KB + ws * NF) * 64 + lane;
-  const f32x4* __restrict__ wp = reinterpret_cast<const f32x4*>(g.W) + ((size_t)nb * KB + ws * NF) * 64 + lane;
+  // fp32 P16 blocks, or (H3) the P16H image: per 32-k pair a hi and a lo 1 KB plane
+  const f32x4* __restrict__ wp = H3 ? reinterpret_cast<const f32x4*>(g.Wh) + ((size_t)nb * KB + ws * NF) * 64 + lane
+                                    : reinterpret_cast<const f32x4*>(g.W) + ((size_t)nb * KB + ws * NF) * 64 + lane;
   f32x4 a[NF], w[NF];
 #pragma unroll
   for (int f = 0; f < NF; ++f) {
@@ -293,14 +378,27 @@ __global__ void __launch_bounds__(NT* KS * 64) gemm_p16_kernel(const GemmArgs g)
     for (int f = 0; f < NF; ++f) a[f] = (a[f] - mu) * rs;
   }
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (H3) {
 #pragma unroll
-  for (int f = 0; f < NF; ++f) {
-    acc0 = mfma16(w[f][0], a[f][0], acc0);
-    acc1 = mfma16(w[f][1], a[f][1], acc1);
-    acc0 = mfma16(w[f][2], a[f][2], acc0);
-    acc1 = mfma16(w[f][3], a[f][3], acc1);
+    for (int p = 0; p < NF / 2; ++p) {
+      h8 ah, al;
+      split8(a[2 * p], a[2 * p + 1], ah, al);
+      const h8 wh = __builtin_bit_cast(h8, w[2 * p]), wl = __builtin_bit_cast(h8, w[2 * p + 1]);
+      acc0 = mfma16h(wh, ah, acc0);
+      acc1 = mfma16h(wh, al, acc1);
+      acc1 = mfma16h(wl, ah, acc1);
+    }
+  } else {
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      acc0 = mfma16(w[f][0], a[f][0], acc0);
+      acc1 = mfma16(w[f][1], a[f][1], acc1);
+      acc0 = mfma16(w[f][2], a[f][2], acc0);
+      acc1 = mfma16(w[f][3], a[f][3], acc1);
+    }
   }
   f32x4 v = acc0 + acc1;
+  if constexpr (H3) v *= g.wscale;
   if constexpr (KS > 1) {
     red[wave][lane] = v;
     __syncthreads();
@@ -332,24 +430,28 @@ __global__ void __launch_bounds__(NT* KS * 64) gemm_p16_kernel(const GemmArgs g)
 // (coalesced 1 KB P16 blocks, the LayerNorm applied on the way in) instead
 // of once per wave, which cuts the L2 -> CU traffic that bounds these
 // small-M GEMMs (FFN1 / query projections: 256 -> 96 KB per workgroup).
-template <int BMB, int BNB, bool LN, bool RELU, bool RESID>
+template <int BMB, int BNB, bool H3, bool LN, bool RELU, bool RESID>
 __global__ void __launch_bounds__(BMB* BNB * 64) gemm_p16s_kernel(const GemmArgs g) {
   constexpr int NW = BMB * BNB, KB = ND_D / 16;
   extern __shared__ f32x4 sh[];
-  f32x4* As = sh;                  // [BMB][KB][64]
-  f32x4* Ws = sh + BMB * KB * 64;  // [BNB][KB][64]
+  f32x4* As = sh;                  // [BMB][KB][64]  (H3: [BMB][KB/2][hi | lo][64])
+  f32x4* Ws = sh + BMB * KB * 64;  // [BNB][KB][64]  (H3: the P16H image)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nb0 = blockIdx.x * BNB, mb0 = blockIdx.y * BMB, NB = g.N >> 4;
   const int MB = (g.M + 15) >> 4;  // row blocks that exist (buffers are padded to 16 rows, not 16*BMB)
   const f32x4* __restrict__ A4 = reinterpret_cast<const f32x4*>(g.A);
-  const f32x4* __restrict__ W4 = reinterpret_cast<const f32x4*>(g.W);
-  // stage: block j of A = (row block mb0 + j / KB, k block j % KB), likewise W
+  const f32x4* __restrict__ W4 = reinterpret_cast<const f32x4*>(H3 ? (const void*)g.Wh : (const void*)g.W);
+  // stage: block j of A = (row block mb0 + j / KB, k block j % KB), likewise W.
+  // H3 stages A in k-block pairs (i even / odd = blocks 2 jp, 2 jp + 1) so a
+  // thread holds both halves of each 32-k operand it splits.
   constexpr int AJ = BMB * KB / NW, WJ = BNB * KB / NW;
   static_assert(AJ * NW == BMB * KB && WJ * NW == BNB * KB, "blocks per wave");
+  static_assert(!H3 || AJ % 2 == 0, "H3 stages A block pairs");
+  auto aj = [&](int i) { return H3 ? 2 * (wave + (i >> 1) * NW) + (i & 1) : wave + i * NW; };
   f32x4 av[AJ], wv[WJ];
 #pragma unroll
   for (int i = 0; i < AJ; ++i) {
-    const int j = wave + i * NW;
+    const int j = aj(i);
     av[i] = A4[((size_t)min(mb0 + j / KB, MB - 1) * KB + j % KB) * 64 + lane];
   }
 #pragma unroll
@@ -374,30 +476,63 @@ __global__ void __launch_bounds__(BMB* BNB * 64) gemm_p16s_kernel(const GemmArgs
       st[2 * tid + 1] = rs;
     }
   }
+  if constexpr (H3) {
+    // normalise and split while staging: every A element converted once per workgroup
+    if constexpr (LN) __syncthreads();
 #pragma unroll
-  for (int i = 0; i < AJ; ++i) As[(wave + i * NW) * 64 + lane] = av[i];
+    for (int i = 0; i < AJ; i += 2) {
+      const int j = aj(i);
+      f32x4 x0 = av[i], x1 = av[i + 1];
+      if constexpr (LN) {
+        const int r = (j / KB) * 16 + (lane & 15);
+        const float m_ = st[2 * r], r_ = st[2 * r + 1];
+        x0 = (x0 - m_) * r_;
+        x1 = (x1 - m_) * r_;
+      }
+      h8 hi, lo;
+      split8(x0, x1, hi, lo);
+      As[j * 64 + lane] = __builtin_bit_cast(f32x4, hi);
+      As[(j + 1) * 64 + lane] = __builtin_bit_cast(f32x4, lo);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < AJ; ++i) As[(wave + i * NW) * 64 + lane] = av[i];
+  }
 #pragma unroll
   for (int i = 0; i < WJ; ++i) Ws[(wave + i * NW) * 64 + lane] = wv[i];
   __syncthreads();
-  float mu = 0.f, rs = 1.f;
-  if constexpr (LN) {
-    mu = st[2 * (rb * 16 + (lane & 15))];
-    rs = st[2 * (rb * 16 + (lane & 15)) + 1];
-  }
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
   const f32x4* ar = As + rb * KB * 64 + lane;
   const f32x4* wr = Ws + cb * KB * 64 + lane;
+  if constexpr (H3) {
 #pragma unroll
-  for (int f = 0; f < KB; ++f) {
-    f32x4 a = ar[f * 64];
-    const f32x4 w = wr[f * 64];
-    if constexpr (LN) a = (a - mu) * rs;
-    acc0 = mfma16(w[0], a[0], acc0);
-    acc1 = mfma16(w[1], a[1], acc1);
-    acc0 = mfma16(w[2], a[2], acc0);
-    acc1 = mfma16(w[3], a[3], acc1);
+    for (int p = 0; p < KB / 2; ++p) {
+      const h8 ah = __builtin_bit_cast(h8, ar[2 * p * 64]), al = __builtin_bit_cast(h8, ar[(2 * p + 1) * 64]);
+      const h8 wh = __builtin_bit_cast(h8, wr[2 * p * 64]), wl = __builtin_bit_cast(h8, wr[(2 * p + 1) * 64]);
+      acc0 = mfma16h(wh, ah, acc0);
+      acc1 = mfma16h(wh, al, acc1);
+      acc1 = mfma16h(wl, ah, acc1);
+    }
+  } else {
+    float mu = 0.f, rs = 1.f;
+    if constexpr (LN) {
+      mu = st[2 * (rb * 16 + (lane & 15))];
+      rs = st[2 * (rb * 16 + (lane & 15)) + 1];
+    }
+#pragma unroll
+    for (int f = 0; f < KB; ++f) {
+      f32x4 a = ar[f * 64];
+      const f32x4 w = wr[f * 64];
+      if constexpr (LN) a = (a - mu) * rs;
+      acc0 = mfma16(w[0], a[0], acc0);
+      acc1 = mfma16(w[1], a[1], acc1);
+      acc0 = mfma16(w[2], a[2], acc0);
+      acc1 = mfma16(w[3], a[3], acc1);
+    }
   }
-  f32x4 v = acc0 + acc1 + bv;
+  f32x4 v = acc0 + acc1;
+  if constexpr (H3) v *= g.wscale;
+  v += bv;
   if constexpr (RELU) v = {fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
   if constexpr (RESID) v += rv;
   if (!live) return;
@@ -427,6 +562,105 @@ hipError_t launch_pack_p16(const float* src, int ld, float* dst, int M, int N, h
   if (M % 16 || N % 16 || ld < N) return hipErrorInvalidValue;
   const size_t n4 = (size_t)M * (N / 4);
   hipLaunchKernelGGL(pack_p16_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, src, ld, dst, M, N);
+  return hipGetLastError();
+}
+
+// max |W| as float bits (non-negative floats order like their bit patterns)
+__global__ void __launch_bounds__(256) absmax_kernel(const float* __restrict__ W, size_t n, unsigned* __restrict__ out) {
+  float m = 0.f;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) m = fmaxf(m, fabsf(W[i]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+}
+
+// one thread per 8-k group of a row: 8 hi halves then 8 lo halves (32 bytes)
+__global__ void __launch_bounds__(256)
+split_weight_kernel(const float* __restrict__ W, size_t groups, float scale, uint16_t* __restrict__ Wh) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= groups) return;
+  const f32x4 v0 = ld4(W + 8 * i) * scale, v1 = ld4(W + 8 * i + 4) * scale;
+  h4 h0, l0, h1, l1;
+  split4(v0, h0, l0);
+  split4(v1, h1, l1);
+  h4* o = reinterpret_cast<h4*>(Wh + 16 * i);
+  o[0] = h0;
+  o[1] = h1;
+  o[2] = l0;
+  o[3] = l1;
+}
+
+hipError_t launch_split_weight(const float* W, int N, int K, uint16_t* Wh, float* wscale, hipStream_t s);
+
+// P16H image (see mfma16h): thread = (column block, k pair, lane)
+__global__ void __launch_bounds__(256) pack_p16h_kernel(const float* __restrict__ W, int ld, int N, int K, float scale,
+                                                        uint16_t* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const int KP = K / 32;
+  if (i >= (size_t)(N / 16) * KP * 64) return;
+  const int lane = (int)(i & 63), kp = (int)((i >> 6) % KP), nb = (int)((i >> 6) / KP);
+  const float* r = W + (size_t)(nb * 16 + (lane & 15)) * ld + kp * 32 + 4 * (lane >> 4);
+  h8 hi, lo;
+  split8(ld4(r) * scale, ld4(r + 16) * scale, hi, lo);
+  f32x4* o = reinterpret_cast<f32x4*>(out) + ((size_t)(nb * KP + kp) * 2) * 64 + lane;
+  o[0] = __builtin_bit_cast(f32x4, hi);
+  o[64] = __builtin_bit_cast(f32x4, lo);
+}
+
+// power-of-two exponent s with max|W| 2^s in [2^13, 2^14) (0 for an all-zero
+// or non-finite W); synchronises the stream
+static hipError_t weight_scale_exp(const float* W, int ld, int N, int K, hipStream_t s, int* s_exp) {
+  unsigned* d = nullptr;
+  hipError_t e = hipMallocAsync((void**)&d, sizeof(unsigned), s);
+  if (e != hipSuccess) return e;
+  unsigned bits = 0;
+  if ((e = hipMemsetAsync(d, 0, sizeof(unsigned), s)) == hipSuccess) {
+    for (int n = 0; n < N && e == hipSuccess; n += 1024) {  // rows in slabs: ld may exceed K
+      const size_t cnt = (size_t)std::min(1024, N - n) * ld - (ld - K);
+      hipLaunchKernelGGL(absmax_kernel, dim3((unsigned)std::min<size_t>((cnt + 255) / 256, 1024)), dim3(256), 0, s,
+                         W + (size_t)n * ld, cnt, d);
+      e = hipGetLastError();
+    }
+    if (e == hipSuccess && (e = hipMemcpyAsync(&bits, d, 4, hipMemcpyDeviceToHost, s)) == hipSuccess)
+      e = hipStreamSynchronize(s);
+  }
+  (void)hipFreeAsync(d, s);
+  if (e != hipSuccess) return e;
+  float mx;
+  memcpy(&mx, &bits, 4);
+  *s_exp = 0;
+  if (mx > 0.f && std::isfinite(mx)) {
+    int ex;
+    (void)std::frexp(mx, &ex);  // mx in [2^(ex-1), 2^ex)
+    *s_exp = 14 - ex;
+  }
+  return hipSuccess;
+}
+
+hipError_t launch_pack_p16h(const float* W, int ld, int N, int K, uint16_t* out, float* wscale, hipStream_t s) {
+  if (N % 16 || K % 32 || ld < K || !W || !out || !wscale) return hipErrorInvalidValue;
+  int s_exp = 0;
+  hipError_t e = weight_scale_exp(W, ld, N, K, s, &s_exp);
+  if (e != hipSuccess) return e;
+  const size_t n = (size_t)(N / 16) * (K / 32) * 64;
+  hipLaunchKernelGGL(pack_p16h_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, W, ld, N, K,
+                     std::ldexp(1.0f, s_exp), out);
+  *wscale = std::ldexp(1.0f, -s_exp);
+  return hipGetLastError();
+}
+
+// 2^s puts max|W| 2^s in [2^13, 2^14): hi stays far from the fp16 maximum
+// (65504) and lo (about 2^-11 of its element) stays normal for elements
+// above about 2^-14 of the largest.
+hipError_t launch_split_weight(const float* W, int N, int K, uint16_t* Wh, float* wscale, hipStream_t s) {
+  if (N <= 0 || K % 32 != 0 || !W || !Wh || !wscale) return hipErrorInvalidValue;
+  int s_exp = 0;
+  hipError_t e = weight_scale_exp(W, K, N, K, s, &s_exp);
+  if (e != hipSuccess) return e;
+  const size_t groups = (size_t)N * K / 8;
+  hipLaunchKernelGGL(split_weight_kernel, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, s, W, groups,
+                     std::ldexp(1.0f, s_exp), Wh);
+  *wscale = std::ldexp(1.0f, -s_exp);
   return hipGetLastError();
 }
 
@@ -475,7 +709,10 @@ template <int BM, int BN, int WM, int WN>
 static hipError_t launch_cfg(GemmArgs& g, hipStream_t s) {
   dim3 grid(g.N / BN, (g.M + BM - 1) / BM), block(WM * WN * 64);
   g.part_n_out = g.N / BN;
-  ND_DISPATCH_FLAGS(gemm_f32_kernel, BM, BN, WM, WN);
+  if (g.Wh)
+    ND_DISPATCH_FLAGS(gemm_f32_kernel, BM, BN, WM, WN, true);
+  else
+    ND_DISPATCH_FLAGS(gemm_f32_kernel, BM, BN, WM, WN, false);
   return hipGetLastError();
 }
 
@@ -484,7 +721,10 @@ static hipError_t launch_p16(GemmArgs& g, hipStream_t s) {
   if (g.N % (NT * 16) != 0 || g.K != KS * KW) return hipErrorInvalidValue;
   dim3 grid(g.N / (NT * 16), (g.M + 15) / 16), block(NT * KS * 64);
   g.part_n_out = g.N / 16;
-  ND_DISPATCH_FLAGS(gemm_p16_kernel, NT, KS, KW);
+  if (g.Wh)
+    ND_DISPATCH_FLAGS(gemm_p16_kernel, NT, KS, KW, true);
+  else
+    ND_DISPATCH_FLAGS(gemm_p16_kernel, NT, KS, KW, false);
   return hipGetLastError();
 }
 
@@ -499,25 +739,30 @@ static hipError_t launch_p16s(GemmArgs& g, hipStream_t s) {
   dim3 grid(g.N / (BNB * 16), (g.M + 16 * BMB - 1) / (16 * BMB)), block(BMB * BNB * 64);
   g.part_n_out = g.N / 16;
   const size_t lds = p16s_lds<BMB, BNB>();
-  const bool ln_ = g.norm, re_ = g.relu, rs_ = g.R != nullptr;
-#define ND_P16S(L, RE, RS) \
-  if (ln_ == L && re_ == RE && rs_ == RS) hipLaunchKernelGGL((gemm_p16s_kernel<BMB, BNB, L, RE, RS>), grid, block, lds, s, g);
-  ND_P16S(false, false, false) ND_P16S(false, false, true) ND_P16S(false, true, false) ND_P16S(false, true, true)
-  ND_P16S(true, false, false) ND_P16S(true, false, true) ND_P16S(true, true, false) ND_P16S(true, true, true)
+  const bool h3_ = g.Wh != nullptr, ln_ = g.norm, re_ = g.relu, rs_ = g.R != nullptr;
+#define ND_P16S(H, L, RE, RS)                                        \
+  if (h3_ == H && ln_ == L && re_ == RE && rs_ == RS)                \
+    hipLaunchKernelGGL((gemm_p16s_kernel<BMB, BNB, H, L, RE, RS>), grid, block, lds, s, g);
+#define ND_P16S_H(H)                                                                                   \
+  ND_P16S(H, false, false, false) ND_P16S(H, false, false, true) ND_P16S(H, false, true, false)        \
+  ND_P16S(H, false, true, true) ND_P16S(H, true, false, false) ND_P16S(H, true, false, true)           \
+  ND_P16S(H, true, true, false) ND_P16S(H, true, true, true)
+  ND_P16S_H(false) ND_P16S_H(true)
+#undef ND_P16S_H
 #undef ND_P16S
   return hipGetLastError();
 }
 
-template <int BMB, int BNB>
-static hipError_t set_p16s_attr() {
-  const void* fns[] = {(const void*)gemm_p16s_kernel<BMB, BNB, false, false, false>,
-                       (const void*)gemm_p16s_kernel<BMB, BNB, false, false, true>,
-                       (const void*)gemm_p16s_kernel<BMB, BNB, false, true, false>,
-                       (const void*)gemm_p16s_kernel<BMB, BNB, false, true, true>,
-                       (const void*)gemm_p16s_kernel<BMB, BNB, true, false, false>,
-                       (const void*)gemm_p16s_kernel<BMB, BNB, true, false, true>,
-                       (const void*)gemm_p16s_kernel<BMB, BNB, true, true, false>,
-                       (const void*)gemm_p16s_kernel<BMB, BNB, true, true, true>};
+template <int BMB, int BNB, bool H>
+static hipError_t set_p16s_attr_h() {
+  const void* fns[] = {(const void*)gemm_p16s_kernel<BMB, BNB, H, false, false, false>,
+                       (const void*)gemm_p16s_kernel<BMB, BNB, H, false, false, true>,
+                       (const void*)gemm_p16s_kernel<BMB, BNB, H, false, true, false>,
+                       (const void*)gemm_p16s_kernel<BMB, BNB, H, false, true, true>,
+                       (const void*)gemm_p16s_kernel<BMB, BNB, H, true, false, false>,
+                       (const void*)gemm_p16s_kernel<BMB, BNB, H, true, false, true>,
+                       (const void*)gemm_p16s_kernel<BMB, BNB, H, true, true, false>,
+                       (const void*)gemm_p16s_kernel<BMB, BNB, H, true, true, true>};
   for (const void* f : fns) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p16s_lds<BMB, BNB>());
     if (e != hipSuccess) return e;
@@ -525,9 +770,23 @@ static hipError_t set_p16s_attr() {
   return hipSuccess;
 }
 
+template <int BMB, int BNB>
+static hipError_t set_p16s_attr() {
+  hipError_t e = set_p16s_attr_h<BMB, BNB, false>();
+  return e != hipSuccess ? e : set_p16s_attr_h<BMB, BNB, true>();
+}
+
 hipError_t init_gemm_attributes() {
   hipError_t e = set_p16s_attr<2, 4>();
   return e != hipSuccess ? e : set_p16s_attr<2, 2>();
+}
+
+static bool gemm_f32_only() {
+  static const bool f32only = [] {
+    const char* e = getenv("ND_GEMM_F32");  // 1: fp32 MFMA kernels even where a split weight exists
+    return e && atoi(e) != 0;
+  }();
+  return f32only;
 }
 
 static hipError_t check_args(const GemmArgs& g) {
@@ -545,6 +804,8 @@ hipError_t launch_gemm(GemmArgs& g, hipStream_t s) {
     return e ? atoi(e) : 0;
   }();
   g.expt = expt;
+  if (gemm_f32_only() && g.W) g.Wh = nullptr;
+  if (!g.W && !g.Wh) return hipErrorInvalidValue;
   hipError_t e = check_args(g);
   if (e != hipSuccess) return e;
   static const int big = [] {
@@ -563,6 +824,8 @@ hipError_t launch_gemm(GemmArgs& g, hipStream_t s) {
 
 hipError_t launch_gemm_p16(GemmArgs& g, hipStream_t s) {
   if (g.M <= 0) return hipSuccess;
+  if (gemm_f32_only() && g.W) g.Wh = nullptr;
+  if (!g.W && !g.Wh) return hipErrorInvalidValue;
   hipError_t e = check_args(g);
   if (e != hipSuccess) return e;
   if (g.N % 16 != 0 || (g.norm && !g.part_in)) return hipErrorInvalidValue;

@@ -31,6 +31,12 @@ struct GemmArgs {
   const float* part_in = nullptr;
   int part_n_in = 0;
   int part_n_out = 0;  // set by launch_gemm
+  // split-fp16 operand path (row-major kernel only): W pre-split by
+  // launch_split_weight into fp16 hi/lo planes scaled by 2^s; the product is
+  // computed as hi*hi + hi*lo + lo*hi on v_mfma_f32_32x32x16_f16 and the
+  // accumulator scaled back by wscale = 2^-s (exact).
+  const uint16_t* Wh = nullptr;
+  float wscale = 1.0f;
   int expt = 0;        // timing experiments only (ND_GEMM_EXPT; wrong results): 1 no epilogue, 2 no MFMA, 4 no loads
 };
 #define ND_PART_LD 16  // partial-stat slots per row (max column tiles of a 256-wide row)
@@ -40,6 +46,14 @@ hipError_t launch_gemm(GemmArgs& g, hipStream_t s);
 // packed, lda/ldw/ldr/ldc ignored, rows padded to a multiple of 16 in every
 // buffer (part buffers included); LN requires part_in.
 hipError_t launch_gemm_p16(GemmArgs& g, hipStream_t s);
+// W [N, K] fp32 -> Wh (split-fp16, [N][K/8][hi 8 | lo 8] halves) with the
+// power-of-two scale that puts max|W| just under 2^14; returns 2^-s in
+// *wscale (synchronises the stream: load-time only).  K % 32 == 0.
+hipError_t launch_split_weight(const float* W, int N, int K, uint16_t* Wh, float* wscale, hipStream_t s);
+// P16H image of a row-major weight [N, K] (leading dim ld) for the split-fp16
+// P16 kernels: [N/16][K/32][hi | lo][64 lanes][8 halves] of W * 2^s (scale as
+// launch_split_weight; synchronises the stream).  N % 16 == 0, K % 32 == 0.
+hipError_t launch_pack_p16h(const float* W, int ld, int N, int K, uint16_t* out, float* wscale, hipStream_t s);
 // raises the dynamic-LDS limit of the LDS-staged GEMM kernels (once per process)
 hipError_t init_gemm_attributes();
 // row-major [M, N] with leading dimension ld -> P16 (M, N multiples of 16)

@@ -186,10 +186,22 @@ def op_fold_layernorm(W: torch.Tensor, bias, ln_g: torch.Tensor, ln_b: torch.Ten
     return Wo, bo
 
 
-def op_gemm(A: torch.Tensor, W: torch.Tensor, bias=None, R=None, ln_g=None, ln_b=None, relu=False, norm=False):
+def op_split_weight(W: torch.Tensor):
+    """(Wh, wscale): the split-fp16 image of W [N, K] (nd_op_split_weight)."""
+    N, K = W.shape
+    Wh = torch.empty(N, 2 * K, dtype=torch.int16, device=W.device)
+    sc = ctypes.c_float(0.0)
+    s = ctypes.c_void_p(torch.cuda.current_stream(W.device).cuda_stream)
+    _lib.check(_lib.lib().nd_op_split_weight(_ptr(W), N, K, _ptr(Wh), ctypes.byref(sc), s), "nd_op_split_weight")
+    return Wh, sc.value
+
+
+def op_gemm(A: torch.Tensor, W: torch.Tensor, bias=None, R=None, ln_g=None, ln_b=None, relu=False, norm=False,
+            split=False):
     """C = relu?(LN?(A) W^T + bias) (+ R).  With ln_g/ln_b the affine is folded
     first (nd_op_fold_layernorm) and the GEMM runs with norm=1, as the engine
-    does; norm=True alone means W/bias are already folded."""
+    does; norm=True alone means W/bias are already folded.  split=True runs
+    the engine's split-fp16 form (nd_op_split_weight + nd_op_gemm_split)."""
     M, K = A.shape
     N = W.shape[0]
     if ln_g is not None:
@@ -197,6 +209,11 @@ def op_gemm(A: torch.Tensor, W: torch.Tensor, bias=None, R=None, ln_g=None, ln_b
         norm = True
     C = torch.empty(M, N, dtype=torch.float32, device=A.device)
     s = ctypes.c_void_p(torch.cuda.current_stream(A.device).cuda_stream)
+    if split:
+        Wh, sc = op_split_weight(W)
+        _lib.check(_lib.lib().nd_op_gemm_split(_ptr(A), _ptr(Wh), sc, _ptr(bias), _ptr(R), _ptr(C), M, N, K,
+                                               int(norm), int(relu), s), "nd_op_gemm_split")
+        return C
     _lib.check(_lib.lib().nd_op_gemm(_ptr(A), _ptr(W), _ptr(bias), _ptr(R), _ptr(C), M, N, K, int(norm), int(relu),
                                      s), "nd_op_gemm")
     return C
@@ -238,13 +255,29 @@ def row_partials(x: torch.Tensor) -> torch.Tensor:
     return torch.stack([mu, m2], dim=2).contiguous()
 
 
-def op_gemm_p16(Ap, Wp, bias, M, N, K, Rp=None, part_in=None, relu=False, part_out=None):
+def op_pack_p16h(W: torch.Tensor):
+    """(Wh, wscale): the split-fp16 P16H image of a row-major W [N, K]."""
+    N, K = W.shape
+    Wh = torch.empty(N, 2 * K, dtype=torch.int16, device=W.device)
+    sc = ctypes.c_float(0.0)
+    s = ctypes.c_void_p(torch.cuda.current_stream(W.device).cuda_stream)
+    _lib.check(_lib.lib().nd_op_pack_p16h(_ptr(W), N, K, _ptr(Wh), ctypes.byref(sc), s), "nd_op_pack_p16h")
+    return Wh, sc.value
+
+
+def op_gemm_p16(Ap, Wp, bias, M, N, K, Rp=None, part_in=None, relu=False, part_out=None, Wh=None, wscale=1.0):
     """The decoder-step GEMM on packed operands (see pack_p16).  Returns the
-    packed C [M16, N] and the number of output row partials."""
+    packed C [M16, N] and the number of output row partials.  With Wh (an
+    op_pack_p16h image) the split-fp16 kernels run instead of the fp32 ones."""
     Cp = torch.empty(Ap.shape[0], N, dtype=torch.float32, device=Ap.device)
     pn = ctypes.c_int32(0)
     pn_in = 16 if part_in is not None else 0
     s = ctypes.c_void_p(torch.cuda.current_stream(Ap.device).cuda_stream)
+    if Wh is not None:
+        _lib.check(_lib.lib().nd_op_gemm_p16_split(_ptr(Ap), _ptr(Wh), wscale, _ptr(bias), _ptr(Rp), _ptr(Cp), M, N, K,
+                                                   _ptr(part_in), pn_in, _ptr(part_out), int(relu), ctypes.byref(pn),
+                                                   s), "nd_op_gemm_p16_split")
+        return Cp, pn.value
     _lib.check(_lib.lib().nd_op_gemm_p16(_ptr(Ap), _ptr(Wp), _ptr(bias), _ptr(Rp), _ptr(Cp), M, N, K, _ptr(part_in),
                                          pn_in, _ptr(part_out), int(relu), ctypes.byref(pn), s), "nd_op_gemm_p16")
     return Cp, pn.value

@@ -37,7 +37,10 @@ def _oracle():
                                                 (37, 256, 256, False, False, True),
                                                 (65536, 256, 256, True, True, True),      # 256x256 tiles
                                                 (65529, 256, 2048, False, False, True)])  # ragged last tile
-def test_gemm_vs_fp64(M, N, K, ln, relu, res):
+@pytest.mark.parametrize("split", [False, True])
+def test_gemm_vs_fp64(M, N, K, ln, relu, res, split):
+    """fp32 MFMA kernels and the split-fp16 form (hi*hi + hi*lo + lo*hi on
+    fp16 MFMAs) against fp64, both to the same 2e-4 absolute bound."""
     from nanodecoder_amd.engine import op_gemm
     g = torch.Generator().manual_seed(M + N + K)
     A = torch.randn(M, K, generator=g)
@@ -48,7 +51,7 @@ def test_gemm_vs_fp64(M, N, K, ln, relu, res):
     lb = 0.1 * torch.randn(K, generator=g) if ln else None
     dev = torch.device("cuda", 0)
     out = op_gemm(A.to(dev), W.to(dev), b.to(dev), R.to(dev) if res else None, lg.to(dev) if ln else None,
-                  lb.to(dev) if ln else None, relu).cpu().double()
+                  lb.to(dev) if ln else None, relu, split=split).cpu().double()
     a = A.double()
     if ln:
         a = torch.nn.functional.layer_norm(a, (K,), lg.double(), lb.double(), 1e-6)
@@ -58,6 +61,26 @@ def test_gemm_vs_fp64(M, N, K, ln, relu, res):
     if res:
         ref = ref + R.double()
     assert (out - ref).abs().max().item() < 2e-4
+
+
+@pytest.mark.parametrize("N,K,mag", [(256, 256, 1.0), (768, 256, 3e-4), (256, 2048, 40.0)])
+def test_split_weight_image(N, K, mag):
+    """nd_op_split_weight: hi + lo reproduces W * 2^s to 2^-21 relative (half
+    an fp16 ulp of the residual), max|W| 2^s sits in [2^13, 2^14), and the
+    image layout is [N][K/8][hi 8 | lo 8]."""
+    from nanodecoder_amd.engine import op_split_weight
+    g = torch.Generator().manual_seed(N + K)
+    W = torch.randn(N, K, generator=g) * mag
+    W[0, :8] = torch.tensor([0.0, -0.0, 1e-30, -1e-12, 1e-7, mag, -2 * mag, 0.5 * mag])
+    Wh, sc = op_split_weight(W.to(torch.device("cuda", 0)))
+    h = Wh.cpu().view(torch.float16).float().view(N, K // 8, 2, 8)
+    s = 1.0 / sc
+    assert 2 ** 13 <= W.abs().max().item() * s < 2 ** 14
+    rec = (h[:, :, 0] + h[:, :, 1]).reshape(N, K).double() / s
+    err = (rec - W.double()).abs()
+    # relative to each element, with an absolute floor for the elements whose
+    # residual falls into the fp16 subnormals (2^-25 of the scaled image)
+    assert (err <= W.double().abs() * 2.0 ** -21 + 2.0 ** -25 / s).all(), err.max().item()
 
 
 @pytest.mark.parametrize("M,N,K,ln,relu,res,stats", [(256, 768, 256, True, False, False, False),
@@ -72,11 +95,14 @@ def test_gemm_vs_fp64(M, N, K, ln, relu, res):
                                                       (112, 2048, 256, True, True, False, False),
                                                       (200, 768, 256, True, False, False, False),
                                                       (40, 256, 2048, False, False, True, True)])
-def test_gemm_p16_vs_fp64(M, N, K, ln, relu, res, stats):
+@pytest.mark.parametrize("split", [False, True])
+def test_gemm_p16_vs_fp64(M, N, K, ln, relu, res, stats, split):
     """The decoder-step GEMM on the P16 layout: LN from handed-over row
     partials (affine folded on the device), relu, residual, and the output
-    row partials it hands to the next LayerNorm."""
-    from nanodecoder_amd.engine import op_fold_layernorm, op_gemm_p16, pack_p16, row_partials, unpack_p16
+    row partials it hands to the next LayerNorm; fp32 MFMA and split-fp16
+    kernels to the same bound."""
+    from nanodecoder_amd.engine import (op_fold_layernorm, op_gemm_p16, op_pack_p16h, pack_p16, row_partials,
+                                        unpack_p16)
     g = torch.Generator().manual_seed(7 * M + N + K)
     A = torch.randn(M, K, generator=g)
     W = torch.randn(N, K, generator=g) / K ** 0.5
@@ -91,8 +117,9 @@ def test_gemm_p16_vs_fp64(M, N, K, ln, relu, res, stats):
         Wd, bd = op_fold_layernorm(Wd, bd, lg.to(dev), lb.to(dev))
         part_in = row_partials(torch.cat([A, A.new_zeros((-M) % 16, K)]).to(dev))  # producer's hand-off
     part_out = torch.full(((M + 15) // 16 * 16, 16, 2), float("nan"), device=dev) if stats else None
+    Wh, sc = op_pack_p16h(Wd) if split else (None, 1.0)
     Cp, pn = op_gemm_p16(pack_p16(A.to(dev)), pack_p16(Wd), bd, M, N, K, pack_p16(R.to(dev)) if res else None,
-                         part_in, relu, part_out)
+                         part_in, relu, part_out, Wh=Wh, wscale=sc)
     out = unpack_p16(Cp, M).cpu().double()
     a = A.double()
     if ln:

@@ -44,24 +44,37 @@ def timeit(fn, n=50):
     return e0.elapsed_time(e1) / (5 * n) * 1e3  # us
 
 
-def gemm_case(M, N, K, ln, relu, res):
+def gemm_case(M, N, K, ln, relu, res, split=False):
     A = torch.randn(M, K, device=dev)
     W = torch.randn(N, K, device=dev) / K ** 0.5
     b = torch.randn(N, device=dev)
     R = torch.randn(M, N, device=dev) if res else None
     if ln:  # the engine folds the LayerNorm affine once at load time
         W, b = E.op_fold_layernorm(W, b, torch.rand(K, device=dev) + 0.5, torch.randn(K, device=dev))
-    us = timeit(lambda: E.op_gemm(A, W, b, R, relu=relu, norm=ln))
+    C = torch.empty(M, N, device=dev)
+    if split:
+        import ctypes
+        from nanodecoder_amd import _lib
+        Wh, sc = E.op_split_weight(W)
+        st = lambda: ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)  # noqa: E731
+        fn = lambda: _lib.lib().nd_op_gemm_split(A.data_ptr(), Wh.data_ptr(), sc, b.data_ptr(),  # noqa: E731
+                                                 R.data_ptr() if res else None, C.data_ptr(), M, N, K, int(ln),
+                                                 int(relu), st())
+    else:
+        fn = lambda: E.op_gemm(A, W, b, R, relu=relu, norm=ln)  # noqa: E731
+    us = timeit(fn)
     tf = 2 * M * N * K / (us * 1e-6) / 1e12
-    print(f"gemm M={M:6d} N={N:5d} K={K:5d} ln={int(ln)} relu={int(relu)} res={int(res)}: {us:9.2f} us  {tf:6.1f} TF/s")
+    print(f"gemm{'-split' if split else '      '} M={M:6d} N={N:5d} K={K:5d} ln={int(ln)} relu={int(relu)} "
+          f"res={int(res)}: {us:9.2f} us  {tf:6.1f} TF/s")
 
 
 if ONLY == "enc":
-    # the encoder's GEMM shapes at B = 256 chunks x 512 samples
-    gemm_case(131072, 768, 256, True, False, False)    # QKV (LN)
-    gemm_case(131072, 256, 256, False, False, True)    # Wo (+res)
-    gemm_case(131072, 2048, 256, True, True, False)    # FFN1 (LN, relu)
-    gemm_case(131072, 256, 2048, False, False, True)   # FFN2 (+res)
+    # the encoder's GEMM shapes at B = 256 chunks x 512 samples, fp32 MFMA and split-fp16
+    for sp in (False, True):
+        gemm_case(131072, 768, 256, True, False, False, sp)    # QKV (LN)
+        gemm_case(131072, 256, 256, False, False, True, sp)    # Wo (+res)
+        gemm_case(131072, 2048, 256, True, True, False, sp)    # FFN1 (LN, relu)
+        gemm_case(131072, 256, 2048, False, False, True, sp)   # FFN2 (+res)
     sys.exit(0)
 if ONLY == "mem":
     # memory-bank attention: scaling in the chunk count and the key count
@@ -86,10 +99,14 @@ if ONLY == "dec256":
             Rp = E.pack_p16(torch.randn(M, N, device=dev)) if res else None
             part = E.row_partials(torch.randn(M, K, device=dev)) if ln else None
             pout = torch.empty(M, 16, 2, device=dev) if N == 256 else None
-            us = timeit(lambda: E.op_gemm_p16(Ap, Wp, b, M, N, K, Rp, part, relu, pout))
-            tf = 2 * M * N * K / (us * 1e-6) / 1e12
-            print(f"gemm_p16 M={M:5d} N={N:5d} K={K:5d} ln={int(ln)} relu={int(relu)} res={int(res)}: "
-                  f"{us:8.2f} us  {tf:6.1f} TF/s")
+            Wr = torch.randn(N, K, device=dev) / K ** 0.5
+            Wh, sc = E.op_pack_p16h(Wr)
+            for sp in (False, True):
+                kw = dict(Wh=Wh, wscale=sc) if sp else {}
+                us = timeit(lambda: E.op_gemm_p16(Ap, Wp, b, M, N, K, Rp, part, relu, pout, **kw))
+                tf = 2 * M * N * K / (us * 1e-6) / 1e12
+                print(f"gemm_p16{'-split' if sp else '      '} M={M:5d} N={N:5d} K={K:5d} ln={int(ln)} "
+                      f"relu={int(relu)} res={int(res)}: {us:8.2f} us  {tf:6.1f} TF/s")
     qkv = E.pack_p16(torch.randn(256, 768, device=dev))
     cache = torch.randn(256, 100, 512, device=dev)
     us = timeit(lambda: E.op_dec_self_attention(qkv, cache, 60, packed=True))
