@@ -268,70 +268,77 @@ __device__ __forceinline__ void merge_waves(float* accs, float* ms, float* ls, c
   }
 }
 
-// Decoder self-attention, one workgroup (8 waves) per row, single pass.
+// Decoder self-attention, one workgroup per row, single pass.
 // cache layout: [slot][t][512] = k (256) | v (256), one slot per row; key t
 // of row r lives in slot anc[r][t] (beam ancestry; identity when anc is
 // null), so beam reordering never moves the cache.  This step's k, v come
 // from registers and are appended to the row's own slot
-// (multi_headed_attn.py:124-141).  Wave w owns key blocks w, w+8, ... of 4.
+// (multi_headed_attn.py:124-141).  Wave w owns the KW consecutive keys
+// w*KW .. w*KW+KW-1 and issues every one of their loads before the first
+// score (one memory round trip per step; a loop over key blocks would pay
+// one per block), then the NW partial states merge through LDS.
 #define SELF_MAXS 256
-#define SELF_NW 8
-#define SELF_U 4
-__global__ void __launch_bounds__(SELF_NW * 64)
+template <int NW, int KW>
+__global__ void __launch_bounds__(NW * 64)
 dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cache, const int* __restrict__ anc,
                           int anc_ld, int step, int S, float* __restrict__ out) {
-  __shared__ float accs[SELF_NW * ND_D];
-  __shared__ float ms[SELF_NW * ND_H], ls[SELF_NW * ND_H];
+  __shared__ float accs[NW * ND_D];
+  __shared__ float ms[NW * ND_H], ls[NW * ND_H];
   const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n = step + 1;
   // qkv is P16-packed [R, 768]
-  const f32x4 qv[1] = {ld4(qkv + pk(r, lane * 4, 3 * ND_D)) / ND_SQRT_DH};
+  const f32x4 qv = ld4(qkv + pk(r, lane * 4, 3 * ND_D)) / ND_SQRT_DH;
   const f32x4 kme = ld4(qkv + pk(r, ND_D + lane * 4, 3 * ND_D)), vme = ld4(qkv + pk(r, 2 * ND_D + lane * 4, 3 * ND_D));
+  float m[1] = {-INFINITY}, l[1] = {0.f};
+  f32x4 acc[1] = {{0.f, 0.f, 0.f, 0.f}};
+  // one pass covers NW * KW keys (every step of max_length <= 128 in one)
+  for (int base = 0; base < n; base += NW * KW) {
+    const int t0 = base + wave * KW;
+    // slots of this wave's keys (lane u < KW: key t0 + u)
+    int sv = r;
+    if (anc) sv = anc[(size_t)r * anc_ld + max(min(t0 + (lane % KW), step - 1), 0)];
+    f32x4 k[KW], v[KW];
+#pragma unroll
+    for (int u = 0; u < KW; ++u) {
+      const int t = t0 + u;  // wave-uniform
+      k[u] = kme;
+      v[u] = vme;
+      if (t < step) {
+        const int slot = __builtin_amdgcn_readlane(sv, u);
+        const float* row = cache + ((size_t)slot * S + t) * 2 * ND_D + lane * 4;
+        k[u] = ld4(row);
+        v[u] = ld4(row + ND_D);
+      }
+    }
+    if (t0 < n) {
+      float sc[1][KW];
+#pragma unroll
+      for (int u = 0; u < KW; ++u) {
+        const float d = sum8(qv.x * k[u].x + qv.y * k[u].y + qv.z * k[u].z + qv.w * k[u].w);
+        sc[0][u] = t0 + u < n ? d : -INFINITY;
+      }
+      online_update<1, KW>(sc, v, m, l, acc);
+    }
+  }
   if (wave == 0) {
     float* mine = cache + ((size_t)r * S + step) * 2 * ND_D;
     st4(mine + lane * 4, kme);
     st4(mine + ND_D + lane * 4, vme);
   }
-  // ancestry of keys < step: lane l holds the slot of key 64*i + l
-  int av[SELF_MAXS / 64];
-#pragma unroll
-  for (int i = 0; i < SELF_MAXS / 64; ++i)
-    av[i] = anc ? anc[(size_t)r * anc_ld + max(min(i * 64 + lane, step - 1), 0)] : r;
-  const int n = step + 1;
-  float m[1] = {-INFINITY}, l[1] = {0.f};
-  f32x4 acc[1] = {{0.f, 0.f, 0.f, 0.f}};
-  for (int blk = wave; blk * SELF_U < n; blk += SELF_NW) {
-    f32x4 k[SELF_U], v[SELF_U];
-#pragma unroll
-    for (int u = 0; u < SELF_U; ++u) {
-      const int t = min(blk * SELF_U + u, step);  // wave-uniform
-      if (t < step) {
-        const int a = t >> 6;
-        const int sv = a == 0 ? av[0] : a == 1 ? av[1] : a == 2 ? av[2] : av[3];
-        const int slot = __builtin_amdgcn_readlane(sv, t & 63);
-        const float* row = cache + ((size_t)slot * S + t) * 2 * ND_D + lane * 4;
-        k[u] = ld4(row);
-        v[u] = ld4(row + ND_D);
-      } else {
-        k[u] = kme;
-        v[u] = vme;
-      }
-    }
-    float sc[1][SELF_U];
-#pragma unroll
-    for (int u = 0; u < SELF_U; ++u) {
-      const float d = sum8(qv[0].x * k[u].x + qv[0].y * k[u].y + qv[0].z * k[u].z + qv[0].w * k[u].w);
-      sc[0][u] = blk * SELF_U + u < n ? d : -INFINITY;
-    }
-    online_update<1, SELF_U>(sc, v, m, l, acc);
-  }
-  merge_waves<1, SELF_NW>(accs, ms, ls, m, l, acc, wave, lane, tid, out, r);
+  merge_waves<1, NW>(accs, ms, ls, m, l, acc, wave, lane, tid, out, r);
 }
 
 hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* anc, int anc_ld, int step,
                                      int max_steps, float* out, int R, hipStream_t s) {
   if (step >= max_steps || step >= SELF_MAXS) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(dec_self_attention_kernel, dim3(R), dim3(SELF_NW * 64), 0, s, qkv, cache, anc, anc_ld, step,
-                     max_steps, out);
+  const int n = step + 1;
+#define ND_SELF(NW, KW)                                                                                             \
+  hipLaunchKernelGGL((dec_self_attention_kernel<NW, KW>), dim3(R), dim3(NW * 64), 0, s, qkv, cache, anc, anc_ld, step, \
+                     max_steps, out)
+  if (n <= 32) ND_SELF(8, 4);
+  else if (n <= 64) ND_SELF(16, 4);
+  else ND_SELF(16, 8);  // two passes beyond 128 keys
+#undef ND_SELF
   return hipGetLastError();
 }
 

@@ -11,22 +11,47 @@ namespace nd {
 
 // LN + generator + log_softmax for row `row` of the P16-packed decoder
 // output x, held by one wave (lane owns dims 4*lane..4*lane+3).  Writes
-// logp[0..V) to `lp` (LDS; every lane writes the same values).
+// logp[0..V) to `lp` (LDS; every lane writes the same values).  The
+// generator rows are read 8 at a time, all loads issued together and the 8
+// cross-lane sums interleaved, so a step pays one load latency, not V.
 __device__ __forceinline__ void head_row(const float* __restrict__ x, int row, const float* __restrict__ ln_g,
                                          const float* __restrict__ ln_b, const float* __restrict__ gw,
                                          const float* __restrict__ gb, int V, int lane, float* lp) {
+  f32x4 wr[8];
+  float br[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {  // first 8 rows in flight with x
+    wr[k] = ld4(gw + (size_t)min(k, V - 1) * ND_D + lane * 4);
+    br[k] = gb[min(k, V - 1)];
+  }
   f32x4 v = ld4(x + pk(row, lane * 4, ND_D));
+  const f32x4 g = ld4(ln_g + lane * 4), bt = ld4(ln_b + lane * 4);
   const float mu = wave_sum(v.x + v.y + v.z + v.w) * (1.0f / ND_D);
   const f32x4 d = v - mu;
   const float var = wave_sum(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w) * (1.0f / ND_D);
   const float rs = 1.0f / sqrtf(var + ND_LN_EPS);
-  const f32x4 y = d * rs * ld4(ln_g + lane * 4) + ld4(ln_b + lane * 4);
+  const f32x4 y = d * rs * g + bt;
   float mx = -INFINITY;
-  for (int k = 0; k < V; ++k) {
-    const f32x4 w = ld4(gw + (size_t)k * ND_D + lane * 4);
-    const float logit = wave_sum(y.x * w.x + y.y * w.y + y.z * w.z + y.w * w.w) + gb[k];
-    lp[k] = logit;
-    mx = fmaxf(mx, logit);
+  for (int k0 = 0; k0 < V; k0 += 8) {
+    if (k0 > 0) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        wr[k] = ld4(gw + (size_t)min(k0 + k, V - 1) * ND_D + lane * 4);
+        br[k] = gb[min(k0 + k, V - 1)];
+      }
+    }
+    float dt[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dt[k] = y.x * wr[k].x + y.y * wr[k].y + y.z * wr[k].z + y.w * wr[k].w;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dt[k] = wave_sum(dt[k]);
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (k0 + k < V) {
+        const float logit = dt[k] + br[k];
+        lp[k0 + k] = logit;
+        mx = fmaxf(mx, logit);
+      }
   }
   // torch log_softmax: (x - max) - log(sum(exp(x - max)))
   float s = 0.f;
@@ -37,8 +62,16 @@ __device__ __forceinline__ void head_row(const float* __restrict__ x, int row, c
 
 // Writes the embedded input row of step `step_next` for token `tk` (one wave;
 // onmt/modules/embeddings.py:189-207, PositionalEncoding :36-43).
-__device__ __forceinline__ void embed_row(const NextEmbed& ne, int tk, int step_next, int row, int lane) {
-  f32x4 e = ld4(ne.emb + (size_t)tk * ND_D + lane * 4);
+__device__ __forceinline__ void embed_row(const NextEmbed& ne, int tk, int step_next, int row, int lane,
+                                          const f32x4* pre = nullptr, int npre = 0) {
+  // pre: the lane's slice of embedding rows 0..npre-1, loaded ahead of the
+  // argmax (greedy) so the chosen row needs no dependent load
+  f32x4 e = tk < npre ? pre[0] : ld4(ne.emb + (size_t)tk * ND_D + lane * 4);
+  if (tk < npre) {
+#pragma unroll
+    for (int k = 1; k < 8; ++k)
+      if (k == tk) e = pre[k];
+  }
   if (ne.pe) e = e * 16.0f + ld4(ne.pe + (size_t)step_next * ND_D + lane * 4);  // sqrt(256) = 16
   st4(ne.x + pk(row, lane * 4, ND_D), e);
   const float mu = wave_sum(e.x + e.y + e.z + e.w) * (1.0f / ND_D);
@@ -60,6 +93,10 @@ greedy_head_kernel(const float* __restrict__ x, const float* __restrict__ ln_g, 
   const int r = blockIdx.x * 4 + w;
   if (r >= R) return;
   float* lp = lps[w];
+  // the embedding rows of tokens 0..7, in flight with the head's own loads
+  f32x4 er[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) er[k] = ld4(ne.emb + (size_t)min(k, V - 1) * ND_D + lane * 4);
   head_row(x, r, ln_g, ln_b, gw, gb, V, lane, lp);
   if (lane == 0 && logp_dump)
     for (int k = 0; k < V; ++k) logp_dump[((size_t)r * S + step) * V + k] = lp[k];
@@ -79,7 +116,7 @@ greedy_head_kernel(const float* __restrict__ x, const float* __restrict__ ln_g, 
     out_tokens[(size_t)r * S + step] = best;
     score[r] = bv;
   }
-  if (step + 1 < S) embed_row(ne, best, step + 1, r, lane);
+  if (step + 1 < S) embed_row(ne, best, step + 1, r, lane, er, min(V, 8));
 }
 
 hipError_t launch_dec_greedy_head(const float* x, const float* ln_g, const float* ln_b, const float* gw,

@@ -138,6 +138,37 @@ def test_gemm_p16_vs_fp64(M, N, K, ln, relu, res, stats, split):
         assert torch.allclose(got[:, :, 1], want[:, :, 1], rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("step", [0, 1, 31, 32, 63, 64, 99, 127, 128, 200])
+@pytest.mark.parametrize("beam", [False, True])
+def test_dec_self_attention_vs_fp64(step, beam):
+    """Decoder self-attention step (multi_headed_attn.py:124-141 + :167-179):
+    keys 0..step-1 from the cache through the ancestry table (beam) or the
+    row's own slot, key `step` from this step's k/v, which is also appended
+    to the row's slot."""
+    from nanodecoder_amd.engine import op_dec_self_attention
+    R, S = 37, 256
+    g = torch.Generator().manual_seed(step + 1000 * beam)
+    qkv = torch.randn(R, 768, generator=g)
+    cache = torch.randn(R, S, 512, generator=g)
+    anc = torch.randint(0, R, (R, S), generator=g, dtype=torch.int32) if beam else None
+    dev = torch.device("cuda", 0)
+    cd = cache.to(dev)
+    out = op_dec_self_attention(qkv.to(dev), cd, step, anc=anc.to(dev) if beam else None,
+                                anc_ld=S if beam else 0).cpu().double()
+    q = qkv[:, :256].double().view(R, 8, 32) / np.float32(np.sqrt(32.0))
+    ref = torch.empty(R, 256, dtype=torch.float64)
+    for r in range(R):
+        slots = anc[r, :step].long() if beam else torch.full((step,), r, dtype=torch.long)
+        kv = cache[slots, torch.arange(step)].double()                       # [step, 512]
+        k = torch.cat([kv[:, :256], qkv[r:r + 1, 256:512].double()]).view(-1, 8, 32)
+        v = torch.cat([kv[:, 256:], qkv[r:r + 1, 512:].double()]).view(-1, 8, 32)
+        p = torch.softmax(torch.einsum("hd,thd->ht", q[r], k), dim=-1)
+        ref[r] = torch.einsum("ht,thd->hd", p, v).reshape(256)
+    assert (out - ref).abs().max().item() < 1e-5
+    appended = cd[torch.arange(R), step].cpu()
+    assert torch.equal(appended, qkv[:, 256:])
+
+
 def test_enc_attention_vs_oracle():
     from nanodecoder_amd.engine import op_enc_attention
     ref = _oracle()

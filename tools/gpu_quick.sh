@@ -1,10 +1,10 @@
-# quick iteration: GPU parity tests, decoder-shape microbench, short bench
+# GPU suite + quick greedy bench with kernel stats
 set -u
-R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/quick; mkdir -p $O; cd $R
-timeout -k 10 900 python -m pytest tests -q -m gpu -p no:cacheprovider -x > $O/tests.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -2 $O/tests.log
-if [ $rc -gt 1 ]; then exit $rc; fi
-timeout -k 10 300 python tools/microbench.py ${MICRO:-dec256} > $O/micro.log 2>&1; echo "micro rc=$?"
-if [ $? -gt 1 ]; then exit 1; fi
-timeout -k 10 300 python bench.py --steps 5 --warmup 2 --cpu-baseline 0 --no-roofline > $O/bench.json 2> $O/bench.err
-echo "bench rc=$?"
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/q; mkdir -p $O; cd $R
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1
+rc=$?; tail -4 $O/tests.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python bench.py --steps 10 --warmup 2 --cpu-baseline 0 > $O/bench.json 2> $O/bench.err
+rc=$?; echo "bench rc=$rc"; cut -c1-300 $O/bench.json; [ $rc -ne 0 ] && { tail -5 $O/bench.err; exit $rc; }
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 $R/bench.py --steps 3 --warmup 1 --cpu-baseline 0 --no-roofline > $O/trace.log 2>&1
+rc=$?; echo "trace rc=$rc"; exit $rc
