@@ -118,8 +118,22 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
   float* Cs = smem;                  // [BM][LDC] after the main loop
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int nbt = blockIdx.x;
-  const int n0 = nbt * BN, m0 = blockIdx.y * BM;
+  // XCD-aware tile order: consecutive workgroups land on the 8 XCDs in turn,
+  // so workgroup b runs on XCD b % 8; giving XCD x the row blocks x, x+8, ...
+  // with all their column tiles keeps each A row block in ONE XCD's L2 (read
+  // from HBM once instead of once per column tile), while the whole weight
+  // (<= 2 MB) is cached by every XCD.  g.xcd_map == 0: column tile fastest.
+  const int ntn = g.N / BN, nmb = (g.M + BM - 1) / BM;
+  int nbt, mbk;
+  if (g.xcd_map) {
+    const int b = blockIdx.x, j = b >> 3;
+    nbt = j % ntn;
+    mbk = (j / ntn) * 8 + (b & 7);
+  } else {
+    nbt = blockIdx.x % ntn;
+    mbk = blockIdx.x / ntn;
+  }
+  const int n0 = nbt * BN, m0 = mbk * BM;
   const int M = g.M, K = g.K;
   const float* __restrict__ A = g.A;
 
@@ -707,7 +721,13 @@ hipError_t launch_fold_layernorm(const float* W, const float* bias, const float*
 
 template <int BM, int BN, int WM, int WN>
 static hipError_t launch_cfg(GemmArgs& g, hipStream_t s) {
-  dim3 grid(g.N / BN, (g.M + BM - 1) / BM), block(WM * WN * 64);
+  static const int xcd = [] {
+    const char* e = getenv("ND_GEMM_XCD");  // 0: column tile fastest (A/B timing)
+    return e ? atoi(e) : 1;
+  }();
+  const int nmb = (g.M + BM - 1) / BM;
+  g.xcd_map = xcd && nmb % 8 == 0;
+  dim3 grid((g.N / BN) * nmb), block(WM * WN * 64);
   g.part_n_out = g.N / BN;
   if (g.Wh)
     ND_DISPATCH_FLAGS(gemm_f32_kernel, BM, BN, WM, WN, true);

@@ -37,6 +37,7 @@ struct GemmArgs {
   // accumulator scaled back by wscale = 2^-s (exact).
   const uint16_t* Wh = nullptr;
   float wscale = 1.0f;
+  int xcd_map = 0;     // row-major kernel: XCD-aware tile order (set by launch_gemm)
   int expt = 0;        // timing experiments only (ND_GEMM_EXPT; wrong results): 1 no epilogue, 2 no MFMA, 4 no loads
 };
 #define ND_PART_LD 16  // partial-stat slots per row (max column tiles of a 256-wide row)

@@ -76,6 +76,9 @@ if ONLY == "enc":
         gemm_case(131072, 2048, 256, True, True, False, sp)    # FFN1 (LN, relu)
         gemm_case(131072, 256, 2048, False, False, True, sp)   # FFN2 (+res)
     sys.exit(0)
+if ONLY == "ffn1s":  # one encoder GEMM in the split-fp16 form (PMC passes: MB_EAGER=1)
+    gemm_case(131072, 2048, 256, True, True, False, True)
+    sys.exit(0)
 if ONLY == "mem":
     # memory-bank attention: scaling in the chunk count and the key count
     for C, T in ((64, 512), (128, 512), (256, 512), (512, 512), (256, 256), (256, 128)):
