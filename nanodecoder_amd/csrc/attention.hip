@@ -181,10 +181,168 @@ enc_attention_kernel(const float* __restrict__ qkv, const float* __restrict__ si
   }
 }
 
+// Split-fp16 form of enc_attention_kernel (same work split, same accumulator
+// layouts): K, V^T are staged into LDS already split into fp16 hi / lo planes
+// and Q is split in registers, so every product is hi*hi + hi*lo + lo*hi on
+// v_mfma_f32_32x32x16_f16 into the fp32 accumulators (the GEMM's H3 scheme,
+// gemm.hip) — 6 MFMAs of 32 cycles per 32 x 32 x 32 product instead of 16 of
+// 64 cycles.  Scores S^T = K Q^T: A = K rows (lane: key l&31, dims
+// 16 s + 8 (l>>5) + j), B = Q^T.  P.V: O^T += V^T P^T with the 16 keys of
+// k-step s taken in the order the score accumulator hands them to a lane
+// (registers 8 s .. 8 s + 7 = keys 4 h + {0..3, 8..11} + 16 s), which V^T's
+// LDS image stores contiguously (key k of a 16-group at position
+// (k & 3) + 4 ((k >> 3) & 1) + 8 ((k >> 2) & 1)).
+typedef _Float16 eh8 __attribute__((ext_vector_type(8)));
+#define ENC_KH 20      // K plane row stride (dwords): 32 halves + 8 pad, conflict-free ds_read_b128
+#define ENC_VH 260     // V^T plane row stride (dwords): 512 halves + 8 pad
+
+__device__ __forceinline__ f32x16 mfma32h(eh8 a, eh8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void esplit8(const float (&x)[8], eh8& hi, eh8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    hi[j] = (_Float16)x[j];
+    lo[j] = (_Float16)(x[j] - (float)hi[j]);
+  }
+}
+
+__global__ void __launch_bounds__(1024)
+enc_attention_h3_kernel(const float* __restrict__ qkv, const float* __restrict__ signal, const int* __restrict__ span,
+                        float* __restrict__ out, int T) {
+  __shared__ __attribute__((aligned(16))) unsigned Kp[2][ENC_MAXT * ENC_KH];  // [hi|lo][key][32 halves + pad]
+  __shared__ __attribute__((aligned(16))) unsigned Vp[2][ND_DH * ENC_VH];     // [hi|lo][dim][512 halves + pad]
+  __shared__ int kflag[ENC_MAXT];  // 0 = key, 1 = masked (signal == 0), 2 = absent (t >= span)
+
+  const int h = blockIdx.x, b = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int L = min(span[b], T);
+  const int nkt = (L + 31) >> 5;
+  const size_t base = (size_t)b * T;
+
+  for (int idx = tid; idx < nkt * 32 * 8; idx += 1024) {
+    const int t = idx >> 3, c = (idx & 7) * 4;
+    f32x4 k = {0.f, 0.f, 0.f, 0.f}, v = {0.f, 0.f, 0.f, 0.f};
+    if (t < L) {
+      const float* row = qkv + (base + t) * (3 * ND_D) + h * ND_DH + c;
+      k = ld4(row + ND_D);
+      v = ld4(row + 2 * ND_D);
+    }
+    _Float16* kh = reinterpret_cast<_Float16*>(&Kp[0][t * ENC_KH]) + c;
+    _Float16* kl = reinterpret_cast<_Float16*>(&Kp[1][t * ENC_KH]) + c;
+    const int pos = (t & ~15) + (t & 3) + 4 * ((t >> 3) & 1) + 8 * ((t >> 2) & 1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const _Float16 a = (_Float16)k[i], vv = (_Float16)v[i];
+      kh[i] = a;
+      kl[i] = (_Float16)(k[i] - (float)a);
+      reinterpret_cast<_Float16*>(&Vp[0][(c + i) * ENC_VH])[pos] = vv;
+      reinterpret_cast<_Float16*>(&Vp[1][(c + i) * ENC_VH])[pos] = (_Float16)(v[i] - (float)vv);
+    }
+  }
+  for (int t = tid; t < nkt * 32; t += 1024) kflag[t] = t < L ? (signal[base + t] == 0.0f ? 1 : 0) : 2;
+  __syncthreads();
+
+  const int q0 = wave * 32;
+  if (q0 >= L) return;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int q = q0 + lr;
+  const int qc = min(q, T - 1);
+
+  // Q^T operand of k-step s: dims 16 s + 8 lh .. + 7 of query q, pre-scaled
+  // like ``query / math.sqrt(dim_per_head)`` (multi_headed_attn.py:167)
+  eh8 qh[2], ql[2];
+  {
+    const float* qrow = qkv + (base + qc) * (3 * ND_D) + h * ND_DH + 8 * lh;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const f32x4 x0 = ld4(qrow + 16 * s2) / ND_SQRT_DH, x1 = ld4(qrow + 16 * s2 + 4) / ND_SQRT_DH;
+      const float x[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+      esplit8(x, qh[s2], ql[s2]);
+    }
+  }
+
+  f32x16 o;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) o[r] = 0.f;
+  float m = -INFINITY, l = 0.f;
+
+  for (int kt = 0; kt < nkt; ++kt) {
+    f32x16 sacc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int off = (kt * 32 + lr) * ENC_KH + 8 * s2 + 4 * lh;  // dwords: dims 16 s2 + 8 lh
+      const eh8 kh = __builtin_bit_cast(eh8, *reinterpret_cast<const f32x4*>(&Kp[0][off]));
+      const eh8 kl = __builtin_bit_cast(eh8, *reinterpret_cast<const f32x4*>(&Kp[1][off]));
+      sacc = mfma32h(kh, ql[s2], sacc);
+      sacc = mfma32h(kl, qh[s2], sacc);
+      sacc = mfma32h(kh, qh[s2], sacc);
+    }
+    // sacc[r] = score(query q, key kt*32 + mfma32_row(r, lane))
+    float mx = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int f = kflag[kt * 32 + mfma32_row(r, lane)];
+      float sv = sacc[r];
+      sv = f == 1 ? ND_MASK_FILL : sv;
+      sv = f == 2 ? -INFINITY : sv;
+      sacc[r] = sv;
+      mx = fmaxf(mx, sv);
+    }
+    mx = xor32_max(mx);
+    const float mn = fmaxf(m, mx);
+    const float alpha = __expf(m - mn);
+    float rsum = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      sacc[r] = __expf(sacc[r] - mn);
+      rsum += sacc[r];
+    }
+    rsum = xor32_sum(rsum);
+    l = l * alpha + rsum;
+    m = mn;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[r] *= alpha;
+    // O^T[d][q] += V^T[d][key] P^T[key][q] over the tile's two 16-key k-steps
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const float pv[8] = {sacc[8 * s2 + 0], sacc[8 * s2 + 1], sacc[8 * s2 + 2], sacc[8 * s2 + 3],
+                           sacc[8 * s2 + 4], sacc[8 * s2 + 5], sacc[8 * s2 + 6], sacc[8 * s2 + 7]};
+      eh8 ph, pl;
+      esplit8(pv, ph, pl);
+      const int off = lr * ENC_VH + (kt * 32 + 16 * s2 + 8 * lh) / 2;  // dwords
+      const eh8 vh = __builtin_bit_cast(eh8, *reinterpret_cast<const f32x4*>(&Vp[0][off]));
+      const eh8 vl = __builtin_bit_cast(eh8, *reinterpret_cast<const f32x4*>(&Vp[1][off]));
+      o = mfma32h(vh, pl, o);
+      o = mfma32h(vl, ph, o);
+      o = mfma32h(vh, ph, o);
+    }
+  }
+  if (q < L) {
+    const float inv = 1.0f / l;
+    float* orow = out + (base + q) * ND_D + h * ND_DH + 4 * lh;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      f32x4 v = {o[4 * g + 0] * inv, o[4 * g + 1] * inv, o[4 * g + 2] * inv, o[4 * g + 3] * inv};
+      st4(orow + 8 * g, v);
+    }
+  }
+}
+
 hipError_t launch_enc_attention(const float* qkv, const float* signal, const int* span, float* out, int B, int T,
                                 hipStream_t s) {
   if (T > ENC_MAXT || T <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(enc_attention_kernel, dim3(ND_H, B), dim3(1024), 0, s, qkv, signal, span, out, T);
+  static const bool f32 = [] {
+    const char* e = getenv("ND_ENC_ATTN_F32");  // 1: the fp32-MFMA kernel
+    return e && atoi(e) != 0;
+  }();
+  if (f32)
+    hipLaunchKernelGGL(enc_attention_kernel, dim3(ND_H, B), dim3(1024), 0, s, qkv, signal, span, out, T);
+  else
+    hipLaunchKernelGGL(enc_attention_h3_kernel, dim3(ND_H, B), dim3(1024), 0, s, qkv, signal, span, out, T);
   return hipGetLastError();
 }
 

@@ -79,6 +79,14 @@ if ONLY == "enc":
 if ONLY == "ffn1s":  # one encoder GEMM in the split-fp16 form (PMC passes: MB_EAGER=1)
     gemm_case(131072, 2048, 256, True, True, False, True)
     sys.exit(0)
+if ONLY == "eattn":  # encoder self-attention at B = 256 x 512
+    B, T = 256, 512
+    qkv = torch.randn(B * T, 768, device=dev)
+    sig = torch.randn(B, T, device=dev)
+    span = torch.full((B,), T, dtype=torch.int32, device=dev)
+    us = timeit(lambda: E.op_enc_attention(qkv, sig, span), n=10)
+    print(f"enc-attn B={B}: {us:9.2f} us  {4*B*8*T*T*32/(us*1e-6)/1e12:6.1f} TF/s")
+    sys.exit(0)
 if ONLY == "mem":
     # memory-bank attention: scaling in the chunk count and the key count
     for C, T in ((64, 512), (128, 512), (256, 512), (512, 512), (256, 256), (256, 128)):
