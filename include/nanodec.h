@@ -211,6 +211,13 @@ int nd_op_pack_p16h(const float* W, int32_t N, int32_t K, uint16_t* out, float* 
 int nd_op_gemm_p16_split(const float* A, const uint16_t* Wh, float wscale, const float* bias, const float* R, float* C,
                          int32_t M, int32_t N, int32_t K, const float* part_in, int32_t part_n_in, float* part_out,
                          int32_t relu, int32_t* part_n_out, void* stream);
+/* The same GEMM with the weight's row-major split image too (nd_op_split_weight
+ * of the row-major W): from M >= 2048 rows (beam search over large batches)
+ * the engine runs it on the LDS-tiled kernel with P16 operands. */
+int nd_op_gemm_p16_split_rm(const float* A, const uint16_t* Wh, float wscale, const uint16_t* Wh_rm, float wscale_rm,
+                            const float* bias, const float* R, float* C, int32_t M, int32_t N, int32_t K,
+                            const float* part_in, int32_t part_n_in, float* part_out, int32_t relu,
+                            int32_t* part_n_out, void* stream);
 
 /* row-major [M, N] -> P16 packed (M, N multiples of 16). */
 int nd_op_pack_p16(const float* src, float* dst, int32_t M, int32_t N, void* stream);

@@ -112,6 +112,8 @@ struct nd_ctx {
   // split-fp16 images of the row-major GEMM weights (gemm.hip, H3), keyed by
   // the fp32 weight they were made from (built at finalize)
   std::map<const float*, std::pair<uint16_t*, float>> split;
+  // row-major split images of the P16 step weights (large-M route), keyed by the P16 weight
+  std::map<const float*, std::pair<uint16_t*, float>> split_rm;
 
   // workspaces
   float* sig = nullptr;
@@ -425,6 +427,11 @@ struct G {
       a.Wh = it->second.first;
       a.wscale = it->second.second;
     }
+    auto jt = c->split_rm.find(a.W);
+    if (jt != c->split_rm.end()) {
+      a.Wh_rm = jt->second.first;
+      a.wscale_rm = jt->second.second;
+    }
     return *this;
   }
   G& res(const float* R, int ldr) { a.R = R; a.ldr = ldr; return *this; }
@@ -706,6 +713,13 @@ static hipError_t pack_step_weight(nd_ctx* c, const float* src, int ld, float* d
   float sc = 1.f;
   if ((e = nd::launch_pack_p16h(src, ld, rows, cols, h, &sc, c->es)) != hipSuccess) return e;
   c->split[dst] = {h, sc};
+  // and the row-major image for the LDS-tiled kernel (many rows)
+  uint16_t* hr = nullptr;
+  auto jt = c->split_rm.find(dst);
+  if (jt != c->split_rm.end()) hr = jt->second.first;
+  if (!hr && (e = dalloc(c, &hr, (size_t)2 * rows * cols)) != hipSuccess) return e;
+  if ((e = nd::launch_split_weight(src, rows, cols, hr, &sc, c->es, ld)) != hipSuccess) return e;
+  c->split_rm[dst] = {hr, sc};
   return hipSuccess;
 }
 
@@ -1215,6 +1229,22 @@ int nd_op_gemm_p16_split(const float* A, const uint16_t* Wh, float wscale, const
   g.part_out = part_out;
   hipError_t e = nd::launch_gemm_p16(g, (hipStream_t)stream);
   if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("gemm_p16_split: ") + hipGetErrorString(e));
+  if (part_n_out) *part_n_out = g.part_n_out;
+  return ND_OK;
+}
+
+int nd_op_gemm_p16_split_rm(const float* A, const uint16_t* Wh, float wscale, const uint16_t* Wh_rm, float wscale_rm,
+                            const float* bias, const float* R, float* C, int32_t M, int32_t N, int32_t K,
+                            const float* part_in, int32_t part_n_in, float* part_out, int32_t relu,
+                            int32_t* part_n_out, void* stream) {
+  if (int rc = ensure_attributes()) return rc;
+  if (!Wh || !Wh_rm) return fail(ND_ERR_ARG, "gemm_p16_split_rm: null weight image");
+  nd::GemmArgs g;
+  g.A = A; g.Wh = Wh; g.wscale = wscale; g.Wh_rm = Wh_rm; g.wscale_rm = wscale_rm; g.bias = bias; g.R = R; g.C = C;
+  g.M = M; g.N = N; g.K = K; g.relu = relu != 0; g.norm = part_in != nullptr; g.part_in = part_in;
+  g.part_n_in = part_n_in; g.part_out = part_out;
+  hipError_t e = nd::launch_gemm_p16(g, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("gemm_p16_split_rm: ") + hipGetErrorString(e));
   if (part_n_out) *part_n_out = g.part_n_out;
   return ND_OK;
 }

@@ -170,14 +170,30 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
   }
 
   f32x4 ra[A4], rw[W4];
+  // A staging piece i of this thread: (row, c) of the BM x BK tile.  Row-major
+  // A: 8 threads per 128-B row segment.  P16 A (g.p16io, the decoder's packed
+  // activations): one whole 1 KB P16 block per wave instruction, lane e =
+  // row e & 15, columns 4 (e >> 4) .. + 3 of the block.
+  auto amap = [&](int i, int& row, int& c) {
+    if (g.p16io) {
+      const int j = wave + (NT / 64) * i;
+      row = (j >> 1) * 16 + (lane & 15);
+      c = (j & 1) * 16 + 4 * (lane >> 4);
+    } else {
+      const int f = tid + i * NT;
+      row = f >> 3;
+      c = (f & 7) * 4;
+    }
+  };
   auto load_tile = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < A4; ++i) {
-      const int f = tid + i * NT, row = f >> 3, c = (f & 7) * 4;
+      int row, c;
+      amap(i, row, c);
       const int gr = m0 + row;
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
       if (gr < M) {
-        v = ld4(A + (size_t)gr * g.lda + k0 + c);
+        v = ld4(g.p16io ? A + pk(gr, k0 + c, K) : A + (size_t)gr * g.lda + k0 + c);
         if constexpr (LN) v = (v - s_mu[row]) * s_rs[row];
       }
       ra[i] = v;
@@ -194,7 +210,8 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
   auto store_tile = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < A4; ++i) {
-      const int f = tid + i * NT, row = f >> 3, c = (f & 7) * 4;
+      int row, c;
+      amap(i, row, c);
       if constexpr (H3) {
         h4 hi, lo;
         split4(ra[i], hi, lo);
@@ -304,8 +321,10 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
       const int rl = r0 + tid / TPR, row = m0 + ep * RP + rl;
       f32x4 v = ld4(&Cs[rl * LDC + c4]);
       if (row < M) {
-        if constexpr (RESID) v += ld4(g.R + (size_t)row * g.ldr + n0 + c4);
-        st4(g.C + (size_t)row * g.ldc + n0 + c4, v);
+        const size_t ro = g.p16io ? pk(row, n0 + c4, g.N) : (size_t)row * g.ldr + n0 + c4;
+        const size_t co = g.p16io ? pk(row, n0 + c4, g.N) : (size_t)row * g.ldc + n0 + c4;
+        if constexpr (RESID) v += ld4(g.R + ro);
+        st4(g.C + co, v);
       }
       if (g.part_out) {
         const float mu = group_sum<TPR>(v.x + v.y + v.z + v.w) * (1.0f / BN);
@@ -590,10 +609,12 @@ __global__ void __launch_bounds__(256) absmax_kernel(const float* __restrict__ W
 
 // one thread per 8-k group of a row: 8 hi halves then 8 lo halves (32 bytes)
 __global__ void __launch_bounds__(256)
-split_weight_kernel(const float* __restrict__ W, size_t groups, float scale, uint16_t* __restrict__ Wh) {
+split_weight_kernel(const float* __restrict__ W, int ld, int K, size_t groups, float scale,
+                    uint16_t* __restrict__ Wh) {
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= groups) return;
-  const f32x4 v0 = ld4(W + 8 * i) * scale, v1 = ld4(W + 8 * i + 4) * scale;
+  const size_t n = i / (K / 8), k = (i % (K / 8)) * 8;
+  const f32x4 v0 = ld4(W + n * ld + k) * scale, v1 = ld4(W + n * ld + k + 4) * scale;
   h4 h0, l0, h1, l1;
   split4(v0, h0, l0);
   split4(v1, h1, l1);
@@ -604,7 +625,7 @@ split_weight_kernel(const float* __restrict__ W, size_t groups, float scale, uin
   o[3] = l1;
 }
 
-hipError_t launch_split_weight(const float* W, int N, int K, uint16_t* Wh, float* wscale, hipStream_t s);
+hipError_t launch_split_weight(const float* W, int N, int K, uint16_t* Wh, float* wscale, hipStream_t s, int ld);
 
 // P16H image (see mfma16h): thread = (column block, k pair, lane)
 __global__ void __launch_bounds__(256) pack_p16h_kernel(const float* __restrict__ W, int ld, int N, int K, float scale,
@@ -666,13 +687,14 @@ hipError_t launch_pack_p16h(const float* W, int ld, int N, int K, uint16_t* out,
 // 2^s puts max|W| 2^s in [2^13, 2^14): hi stays far from the fp16 maximum
 // (65504) and lo (about 2^-11 of its element) stays normal for elements
 // above about 2^-14 of the largest.
-hipError_t launch_split_weight(const float* W, int N, int K, uint16_t* Wh, float* wscale, hipStream_t s) {
-  if (N <= 0 || K % 32 != 0 || !W || !Wh || !wscale) return hipErrorInvalidValue;
+hipError_t launch_split_weight(const float* W, int N, int K, uint16_t* Wh, float* wscale, hipStream_t s, int ld) {
+  if (ld == 0) ld = K;
+  if (N <= 0 || K % 32 != 0 || ld < K || ld % 4 || !W || !Wh || !wscale) return hipErrorInvalidValue;
   int s_exp = 0;
-  hipError_t e = weight_scale_exp(W, K, N, K, s, &s_exp);
+  hipError_t e = weight_scale_exp(W, ld, N, K, s, &s_exp);
   if (e != hipSuccess) return e;
   const size_t groups = (size_t)N * K / 8;
-  hipLaunchKernelGGL(split_weight_kernel, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, s, W, groups,
+  hipLaunchKernelGGL(split_weight_kernel, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, s, W, ld, K, groups,
                      std::ldexp(1.0f, s_exp), Wh);
   *wscale = std::ldexp(1.0f, -s_exp);
   return hipGetLastError();
@@ -848,6 +870,25 @@ hipError_t launch_gemm_p16(GemmArgs& g, hipStream_t s) {
   if (!g.W && !g.Wh) return hipErrorInvalidValue;
   hipError_t e = check_args(g);
   if (e != hipSuccess) return e;
+  static const int big_min = [] {
+    const char* e = getenv("ND_P16_BIG_MIN");  // rows from which the LDS-tiled kernel takes P16 GEMMs
+    return e ? atoi(e) : 2048;
+  }();
+  if (g.M >= big_min && g.Wh_rm && !gemm_f32_only() && g.N % 64 == 0 && (g.N >= 512 || g.K >= 1024)) {
+    // many rows (beam search over large batches): the encoder's LDS-tiled
+    // split-fp16 kernel on P16 activations, with the row-major weight image
+    // (measured at M = 5120: QKV 25 -> 18 us, FFN1 59 -> 50, FFN2 71 -> 50;
+    // the 256 x 256, K = 256 shapes stay on gemm_p16s, 8 -> 10 us there)
+    GemmArgs r = g;
+    r.W = nullptr;
+    r.Wh = g.Wh_rm;
+    r.wscale = g.wscale_rm;
+    r.p16io = 1;
+    r.lda = r.ldr = r.ldc = 0;
+    e = launch_gemm(r, s);
+    g.part_n_out = r.part_n_out;
+    return e;
+  }
   if (g.N % 16 != 0 || (g.norm && !g.part_in)) return hipErrorInvalidValue;
   if (g.K == 256) {
     // LN consumers share the row statistics across many column blocks

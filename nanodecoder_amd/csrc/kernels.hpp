@@ -37,6 +37,12 @@ struct GemmArgs {
   // accumulator scaled back by wscale = 2^-s (exact).
   const uint16_t* Wh = nullptr;
   float wscale = 1.0f;
+  // P16 GEMMs: the weight's row-major split image too (large-M route through
+  // the LDS-tiled kernel, launch_gemm_p16), and the P16 operand mode of the
+  // row-major kernel (A, R, C in P16; lda / ldr / ldc unused)
+  const uint16_t* Wh_rm = nullptr;
+  float wscale_rm = 1.0f;
+  int p16io = 0;
   int xcd_map = 0;     // row-major kernel: XCD-aware tile order (set by launch_gemm)
   int expt = 0;        // timing experiments only (ND_GEMM_EXPT; wrong results): 1 no epilogue, 2 no MFMA, 4 no loads
 };
@@ -47,10 +53,10 @@ hipError_t launch_gemm(GemmArgs& g, hipStream_t s);
 // packed, lda/ldw/ldr/ldc ignored, rows padded to a multiple of 16 in every
 // buffer (part buffers included); LN requires part_in.
 hipError_t launch_gemm_p16(GemmArgs& g, hipStream_t s);
-// W [N, K] fp32 -> Wh (split-fp16, [N][K/8][hi 8 | lo 8] halves) with the
+// W [N, K] fp32 (leading dimension ld, 0 = K) -> Wh (split-fp16, [N][K/8][hi 8 | lo 8] halves) with the
 // power-of-two scale that puts max|W| just under 2^14; returns 2^-s in
 // *wscale (synchronises the stream: load-time only).  K % 32 == 0.
-hipError_t launch_split_weight(const float* W, int N, int K, uint16_t* Wh, float* wscale, hipStream_t s);
+hipError_t launch_split_weight(const float* W, int N, int K, uint16_t* Wh, float* wscale, hipStream_t s, int ld = 0);
 // P16H image of a row-major weight [N, K] (leading dim ld) for the split-fp16
 // P16 kernels: [N/16][K/32][hi | lo][64 lanes][8 halves] of W * 2^s (scale as
 // launch_split_weight; synchronises the stream).  N % 16 == 0, K % 32 == 0.

@@ -246,13 +246,16 @@ def unpack_p16(p: torch.Tensor, M: Optional[int] = None) -> torch.Tensor:
     return x[: (M16 if M is None else M)]
 
 
-def row_partials(x: torch.Tensor) -> torch.Tensor:
-    """Per-row {mean, M2} of the 16 column tiles of a [M, 256] matrix in the
-    engine's part layout [M, 16, 2] (what a producing GEMM hands over)."""
-    t = x.view(x.shape[0], 16, 16)
+def row_partials(x: torch.Tensor, n: int = 16) -> torch.Tensor:
+    """Per-row {mean, M2} of the n equal column tiles of a [M, 256] matrix in
+    the engine's part layout [M, 16, 2] (what a producing GEMM hands over;
+    slots >= n zero)."""
+    t = x.view(x.shape[0], n, 256 // n)
     mu = t.mean(dim=2)
     m2 = ((t - mu[:, :, None]) ** 2).sum(dim=2)
-    return torch.stack([mu, m2], dim=2).contiguous()
+    out = torch.zeros(x.shape[0], 16, 2, dtype=x.dtype, device=x.device)
+    out[:, :n] = torch.stack([mu, m2], dim=2)
+    return out
 
 
 def op_pack_p16h(W: torch.Tensor):
@@ -265,14 +268,23 @@ def op_pack_p16h(W: torch.Tensor):
     return Wh, sc.value
 
 
-def op_gemm_p16(Ap, Wp, bias, M, N, K, Rp=None, part_in=None, relu=False, part_out=None, Wh=None, wscale=1.0):
+def op_gemm_p16(Ap, Wp, bias, M, N, K, Rp=None, part_in=None, relu=False, part_out=None, Wh=None, wscale=1.0,
+                Wh_rm=None, wscale_rm=1.0):
     """The decoder-step GEMM on packed operands (see pack_p16).  Returns the
     packed C [M16, N] and the number of output row partials.  With Wh (an
-    op_pack_p16h image) the split-fp16 kernels run instead of the fp32 ones."""
+    op_pack_p16h image) the split-fp16 kernels run instead of the fp32 ones;
+    with Wh_rm too (op_split_weight of the row-major W) large M takes the
+    LDS-tiled kernel as in the engine."""
     Cp = torch.empty(Ap.shape[0], N, dtype=torch.float32, device=Ap.device)
     pn = ctypes.c_int32(0)
     pn_in = 16 if part_in is not None else 0
     s = ctypes.c_void_p(torch.cuda.current_stream(Ap.device).cuda_stream)
+    if Wh_rm is not None:
+        _lib.check(_lib.lib().nd_op_gemm_p16_split_rm(_ptr(Ap), _ptr(Wh), wscale, _ptr(Wh_rm), wscale_rm, _ptr(bias),
+                                                      _ptr(Rp), _ptr(Cp), M, N, K, _ptr(part_in), pn_in,
+                                                      _ptr(part_out), int(relu), ctypes.byref(pn), s),
+                   "nd_op_gemm_p16_split_rm")
+        return Cp, pn.value
     if Wh is not None:
         _lib.check(_lib.lib().nd_op_gemm_p16_split(_ptr(Ap), _ptr(Wh), wscale, _ptr(bias), _ptr(Rp), _ptr(Cp), M, N, K,
                                                    _ptr(part_in), pn_in, _ptr(part_out), int(relu), ctypes.byref(pn),

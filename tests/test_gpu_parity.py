@@ -94,15 +94,19 @@ def test_split_weight_image(N, K, mag):
                                                       (1280, 256, 256, True, False, True, True),
                                                       (112, 2048, 256, True, True, False, False),
                                                       (200, 768, 256, True, False, False, False),
-                                                      (40, 256, 2048, False, False, True, True)])
-@pytest.mark.parametrize("split", [False, True])
+                                                      (40, 256, 2048, False, False, True, True),
+                                                      (5120, 2048, 256, True, True, False, False),   # beam 5 x 1024
+                                                      (5120, 256, 2048, False, False, True, True),
+                                                      (5120, 768, 256, True, False, False, False),
+                                                      (2560, 256, 256, True, False, True, True)])
+@pytest.mark.parametrize("split", [False, True, "rm"])
 def test_gemm_p16_vs_fp64(M, N, K, ln, relu, res, stats, split):
     """The decoder-step GEMM on the P16 layout: LN from handed-over row
     partials (affine folded on the device), relu, residual, and the output
     row partials it hands to the next LayerNorm; fp32 MFMA and split-fp16
     kernels to the same bound."""
-    from nanodecoder_amd.engine import (op_fold_layernorm, op_gemm_p16, op_pack_p16h, pack_p16, row_partials,
-                                        unpack_p16)
+    from nanodecoder_amd.engine import (op_fold_layernorm, op_gemm_p16, op_pack_p16h, op_split_weight, pack_p16,
+                                        row_partials, unpack_p16)
     g = torch.Generator().manual_seed(7 * M + N + K)
     A = torch.randn(M, K, generator=g)
     W = torch.randn(N, K, generator=g) / K ** 0.5
@@ -118,8 +122,9 @@ def test_gemm_p16_vs_fp64(M, N, K, ln, relu, res, stats, split):
         part_in = row_partials(torch.cat([A, A.new_zeros((-M) % 16, K)]).to(dev))  # producer's hand-off
     part_out = torch.full(((M + 15) // 16 * 16, 16, 2), float("nan"), device=dev) if stats else None
     Wh, sc = op_pack_p16h(Wd) if split else (None, 1.0)
+    Wr, sr = op_split_weight(Wd) if split == "rm" else (None, 1.0)  # large M: the LDS-tiled kernel on P16 operands
     Cp, pn = op_gemm_p16(pack_p16(A.to(dev)), pack_p16(Wd), bd, M, N, K, pack_p16(R.to(dev)) if res else None,
-                         part_in, relu, part_out, Wh=Wh, wscale=sc)
+                         part_in, relu, part_out, Wh=Wh, wscale=sc, Wh_rm=Wr, wscale_rm=sr)
     out = unpack_p16(Cp, M).cpu().double()
     a = A.double()
     if ln:
@@ -131,9 +136,9 @@ def test_gemm_p16_vs_fp64(M, N, K, ln, relu, res, stats, split):
         ref = ref + R.double()
     assert (out - ref).abs().max().item() < 2e-4
     if stats:
-        assert pn == N // 16
-        want = row_partials(out.float())
-        got = part_out[:M].cpu()
+        assert pn in (N // 16, N // 64, N // 128, N // 256)   # one partial per column tile of the kernel taken
+        want = row_partials(out.float(), pn)[:, :pn]
+        got = part_out[:M, :pn].cpu()
         assert torch.allclose(got[:, :, 0], want[:, :, 0], atol=1e-5)
         assert torch.allclose(got[:, :, 1], want[:, :, 1], rtol=1e-4, atol=1e-4)
 

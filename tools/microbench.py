@@ -100,7 +100,7 @@ if ONLY == "mem":
     sys.exit(0)
 if ONLY == "dec256":
     # decoder-step shapes on the engine's P16 layout (greedy R=256, beam R=1280)
-    for M in (256, 1280):
+    for M in (256, 1280, 5120):
         for N, K, ln, relu, res in ((768, 256, True, False, False), (256, 256, False, False, True),
                                     (256, 256, True, False, False), (2048, 256, True, True, False),
                                     (256, 2048, False, False, True)):
@@ -112,11 +112,14 @@ if ONLY == "dec256":
             pout = torch.empty(M, 16, 2, device=dev) if N == 256 else None
             Wr = torch.randn(N, K, device=dev) / K ** 0.5
             Wh, sc = E.op_pack_p16h(Wr)
-            for sp in (False, True):
+            Wm, sm = E.op_split_weight(Wr)
+            for sp in ("", "-split", "-rm"):
                 kw = dict(Wh=Wh, wscale=sc) if sp else {}
+                if sp == "-rm":
+                    kw.update(Wh_rm=Wm, wscale_rm=sm)
                 us = timeit(lambda: E.op_gemm_p16(Ap, Wp, b, M, N, K, Rp, part, relu, pout, **kw))
                 tf = 2 * M * N * K / (us * 1e-6) / 1e12
-                print(f"gemm_p16{'-split' if sp else '      '} M={M:5d} N={N:5d} K={K:5d} ln={int(ln)} "
+                print(f"gemm_p16{sp:6s} M={M:5d} N={N:5d} K={K:5d} ln={int(ln)} "
                       f"relu={int(relu)} res={int(res)}: {us:8.2f} us  {tf:6.1f} TF/s")
     qkv = E.pack_p16(torch.randn(256, 768, device=dev))
     cache = torch.randn(256, 100, 512, device=dev)
