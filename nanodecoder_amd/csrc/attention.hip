@@ -439,10 +439,19 @@ __device__ __forceinline__ void merge_waves(float* accs, float* ms, float* ls, c
 template <int NW, int KW>
 __global__ void __launch_bounds__(NW * 64)
 dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cache, const int* __restrict__ anc,
-                          int anc_ld, int step, int S, float* __restrict__ out) {
+                          int anc_ld, int step, int S, float* __restrict__ out, int rpc) {
   __shared__ float accs[NW * ND_D];
   __shared__ float ms[NW * ND_H], ls[NW * ND_H];
-  const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // beam rows of a chunk mostly read the same ancestor slots: with rpc > 1
+  // (and a chunk count that is a multiple of 8) workgroup b runs chunk
+  // 8 (b / 8 / rpc) + b % 8, beam (b / 8) % rpc, so one chunk's rows share an
+  // XCD and its L2 serves their common history once
+  int r = blockIdx.x;
+  if (rpc > 1) {
+    const int j = r >> 3;
+    r = ((j / rpc) * 8 + (r & 7)) * rpc + j % rpc;
+  }
   const int n = step + 1;
   // qkv is P16-packed [R, 768]
   const f32x4 qv = ld4(qkv + pk(r, lane * 4, 3 * ND_D)) / ND_SQRT_DH;
@@ -487,12 +496,17 @@ dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cac
 }
 
 hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* anc, int anc_ld, int step,
-                                     int max_steps, float* out, int R, hipStream_t s) {
+                                     int max_steps, float* out, int R, hipStream_t s, int rpc) {
+  static const int xcd = [] {
+    const char* e = getenv("ND_SELF_XCD");  // 0: row order (A/B timing)
+    return e ? atoi(e) : 1;
+  }();
+  if (!xcd || rpc < 2 || R % (8 * rpc)) rpc = 1;
   if (step >= max_steps || step >= SELF_MAXS) return hipErrorInvalidValue;
   const int n = step + 1;
 #define ND_SELF(NW, KW)                                                                                             \
   hipLaunchKernelGGL((dec_self_attention_kernel<NW, KW>), dim3(R), dim3(NW * 64), 0, s, qkv, cache, anc, anc_ld, step, \
-                     max_steps, out)
+                     max_steps, out, rpc)
   if (n <= 32) ND_SELF(8, 4);
   else if (n <= 64) ND_SELF(16, 4);
   else ND_SELF(16, 8);  // two passes beyond 128 keys

@@ -518,7 +518,7 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
       pnq = 1;
     } else {
       LCHK(G(c->dx, D, L.pwqkv, 3 * D, D, L.nbqkv, c->dqkv, 3 * D, R).p16().h3(c).ln(c->dx_part, pnx).run(s));
-      LCHK(nd::launch_dec_self_attention(c->dqkv, cache, anc, anc_ld, step, S, c->datt, R, s));
+      LCHK(nd::launch_dec_self_attention(c->dqkv, cache, anc, anc_ld, step, S, c->datt, R, s, rpc));
       LCHK(G(c->datt, D, L.pwo, D, D, L.bo, c->dq1, D, R).p16().h3(c).res(c->dx, D).stats(c->dq1_part).run(s, &pnq));
     }
     if (mb) {  // memory-bank form (attention.hip)

@@ -93,7 +93,7 @@ hipError_t launch_dec_embed(const int* tok, const float* emb, const float* pe, i
 // self attention: writes k,v of this step into cache[slot=r][step], attends
 // over the row's history cache[anc[r][t]][t] (anc == nullptr: identity).
 hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* anc, int anc_ld, int step,
-                                     int max_steps, float* out, int R, hipStream_t s);
+                                     int max_steps, float* out, int R, hipStream_t s, int rpc = 1);
 // context attention: rows r = c*rpc + j attend over ctxkv rows of chunk c
 // (K at kv[(c*T+t)*ld + koff], V at +256), mask signal == pad_val, keys < span.
 hipError_t launch_dec_ctx_attention(const float* q, const float* kv, int ld, int koff, const float* signal,
