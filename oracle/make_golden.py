@@ -84,18 +84,20 @@ class _Field:
 
 
 def make_translator(ns, model, cfg, beam_size, n_best=1, max_length=100, min_length=0, alpha=0.0, fast=True,
-                    length_penalty="none"):
+                    length_penalty="none", beta=0.0, coverage_penalty="none", stepwise_penalty=False,
+                    block_ngram_repeat=0, ignore_when_blocking=()):
     opt = types.SimpleNamespace(
         gpu=-1, n_best=n_best, max_length=max_length, beam_size=beam_size,
         random_sampling_temp=1.0, random_sampling_topk=1, min_length=min_length,
-        stepwise_penalty=False, dump_beam="", block_ngram_repeat=0, ignore_when_blocking=[],
+        stepwise_penalty=stepwise_penalty, dump_beam="", block_ngram_repeat=block_ngram_repeat,
+        ignore_when_blocking=list(ignore_when_blocking),
         fft=False, sample_rate=4000, window_size=0.075, window_stride=0.015, window="hamming",
         replace_unk=False, data_type="nano", verbose=False, fast=fast)
     model_opt = types.SimpleNamespace(copy_attn=False)
     if fast:
         scorer = types.SimpleNamespace(alpha=alpha, beta=0.0)
     else:  # onmt/translate/beam.py:181-199 (the real scorer drives the classic Beam)
-        scorer = ns.GNMTGlobalScorer(types.SimpleNamespace(alpha=alpha, beta=0.0, coverage_penalty="none",
+        scorer = ns.GNMTGlobalScorer(types.SimpleNamespace(alpha=alpha, beta=beta, coverage_penalty=coverage_penalty,
                                                            length_penalty=length_penalty))
     return ns.Translator(model, {"tgt": _Field(cfg.itos)}, opt, model_opt, global_scorer=scorer,
                          report_score=False, logger=None)
@@ -177,13 +179,29 @@ def run_greedy(ns, model, cfg, chunks, max_length=100, min_length=0, attention=F
     return out
 
 
-def run_beam(ns, model, cfg, chunks, beam_size=5, n_best=1, max_length=100, min_length=0, alpha=0.0):
+def _hyp_attention(res, B, n_best, max_length, T):
+    """results["attention"][b][n]: [steps, cut] rows along the hypothesis,
+    cut = memory_lengths[i] as the reference indexes it -> zero-padded
+    [B, n_best, max_length, T] plus the cut per hypothesis."""
+    att = np.zeros((B, n_best, max_length, T), np.float32)
+    cut = np.zeros((B, n_best), np.int32)
+    for j in range(B):
+        for n in range(n_best):
+            a = res["attention"][j][n]
+            a = a.numpy() if hasattr(a, "numpy") else np.asarray(a)
+            att[j, n, : a.shape[0], : a.shape[1]] = a
+            cut[j, n] = a.shape[1]
+    return att, cut
+
+
+def run_beam(ns, model, cfg, chunks, beam_size=5, n_best=1, max_length=100, min_length=0, alpha=0.0,
+             attention=False):
     tr = make_translator(ns, model, cfg, beam_size=beam_size, n_best=n_best, max_length=max_length,
                          min_length=min_length, alpha=alpha)
     batch, order = make_batch(chunks)
     with torch.no_grad(), floor_int_div():
         res = tr._fast_translate_batch(batch, types.SimpleNamespace(data_type="nano"), max_length,
-                                       min_length=min_length, n_best=n_best)
+                                       min_length=min_length, n_best=n_best, return_attention=attention)
     B = len(chunks)
     inv = np.argsort(order)
     tokens = np.full((B, n_best, max_length), -1, np.int32)
@@ -195,7 +213,11 @@ def run_beam(ns, model, cfg, chunks, beam_size=5, n_best=1, max_length=100, min_
             tokens[j, n, : len(p)] = p
             lens[j, n] = len(p)
             scores[j, n] = float(res["scores"][j][n])
-    return dict(beam_tokens=tokens[inv], beam_lens=lens[inv], beam_scores=scores[inv])
+    out = dict(beam_tokens=tokens[inv], beam_lens=lens[inv], beam_scores=scores[inv])
+    if attention:
+        att, cut = _hyp_attention(res, B, n_best, max_length, batch.src.shape[0])
+        out.update(beam_attn=att[inv], beam_attn_cut=cut[inv])
+    return out
 
 
 @contextlib.contextmanager
@@ -217,10 +239,12 @@ def floor_int_truediv():
 
 
 def run_classic_beam(ns, model, cfg, chunks, beam_size=5, n_best=1, max_length=100, min_length=0, alpha=0.0,
-                     length_penalty="none"):
-    """translate/translator.py:827-926 (_translate_batch, the onmt Beam)."""
+                     length_penalty="none", attention=False, **extra):
+    """translate/translator.py:827-926 (_translate_batch, the onmt Beam);
+    ``extra``: beta, coverage_penalty, stepwise_penalty, block_ngram_repeat,
+    ignore_when_blocking (token strings)."""
     tr = make_translator(ns, model, cfg, beam_size=beam_size, n_best=n_best, max_length=max_length,
-                         min_length=min_length, alpha=alpha, fast=False, length_penalty=length_penalty)
+                         min_length=min_length, alpha=alpha, fast=False, length_penalty=length_penalty, **extra)
     batch, order = make_batch(chunks)
     with torch.no_grad(), floor_int_div(), floor_int_truediv():
         res = tr._translate_batch(batch, types.SimpleNamespace(data_type="nano"))
@@ -235,7 +259,11 @@ def run_classic_beam(ns, model, cfg, chunks, beam_size=5, n_best=1, max_length=1
             tokens[j, n, : len(p)] = p
             lens[j, n] = len(p)
             scores[j, n] = float(res["scores"][j][n])
-    return dict(beam_tokens=tokens[inv], beam_lens=lens[inv], beam_scores=scores[inv])
+    out = dict(beam_tokens=tokens[inv], beam_lens=lens[inv], beam_scores=scores[inv])
+    if attention:
+        att, cut = _hyp_attention(res, B, n_best, max_length, batch.src.shape[0])
+        out.update(beam_attn=att[inv], beam_attn_cut=cut[inv])
+    return out
 
 
 SCENARIOS = [
@@ -260,6 +288,28 @@ SCENARIOS = [
     dict(name="transformer_aan", cfg=dict(encoder_type="transformer", self_attn_type="average"), seed=15,
          eos_bias=1.5, chunks=dict(kind="mixed"), greedy=dict(max_length=60),
          beam=dict(beam_size=4, n_best=2, max_length=50, min_length=5)),
+    # -attn_debug with beam search (attention along each hypothesis, cut at
+    # memory_lengths[i] as the reference indexes it) on a batch of six chunks
+    # of distinct lengths, for --fast and for the classic Beam
+    dict(name="transformer_beam_attn", cfg=dict(encoder_type="transformer"), seed=18, eos_bias=1.0,
+         chunks=dict(kind="ragged"), beam=dict(beam_size=4, n_best=2, max_length=40, min_length=3, attention=True),
+         classic=dict(beam_size=4, n_best=2, max_length=40, min_length=3, attention=True)),
+    # the classic Beam's n-gram blocking (with an exclusion token, and without)
+    dict(name="transformer_classic_ext", cfg=dict(encoder_type="transformer"), seed=18, eos_bias=1.0,
+         chunks=dict(kind="mixed"),
+         classic=dict(beam_size=4, n_best=2, max_length=40, min_length=3, attention=True,
+                      block_ngram_repeat=4, ignore_when_blocking=["A"]),
+         classic2=dict(beam_size=4, n_best=2, max_length=30, min_length=3, block_ngram_repeat=7)),
+    # coverage penalties: wu at scoring time with length penalty none (the
+    # scorer then subtracts in place from beam.scores, penalties.py:74-78 +
+    # beam.py:200-212), summary stepwise, summary at scoring time with avg
+    dict(name="transformer_classic_cov", cfg=dict(encoder_type="transformer"), seed=18, eos_bias=1.0,
+         chunks=dict(kind="ragged"),
+         classic=dict(beam_size=4, n_best=2, max_length=40, min_length=3, coverage_penalty="wu", beta=0.2),
+         classic2=dict(beam_size=4, n_best=2, max_length=40, min_length=3, coverage_penalty="summary", beta=0.3,
+                       stepwise_penalty=True, attention=True),
+         classic3=dict(beam_size=4, n_best=3, max_length=40, min_length=3, coverage_penalty="summary", beta=0.1,
+                       length_penalty="avg")),
 ]
 
 
@@ -272,6 +322,11 @@ def scenario_chunks(kind, seed):
         assert len(tail) == 300
         zero = np.zeros(512, np.float32)
         return [full[0], tail, full[1], zero]
+    if kind == "ragged":
+        # six chunks of distinct lengths in unsorted order (T_max = 512)
+        full = synth.synth_chunk_batch(1, 512, seed=seed, inject_masks=False)[0]
+        tails = {n: synth.synth_read_chunks(seed + 700 + n, 512 + n)[-1] for n in (300, 200, 150, 100, 77)}
+        return [tails[150], full, tails[77], tails[300], tails[100], tails[200]]
     if kind == "short":
         # a batch made only of short chunks: T_max < 512 (reference batching quirk)
         return [synth.synth_read_chunks(seed + 600 + i, 512 + n)[-1] for i, n in enumerate((200, 150, 77))]
@@ -315,13 +370,13 @@ def main():
         if "beam2" in sc:
             b = run_beam(ns, model, cfg, chunks, **sc["beam2"])
             out.update({k + "2": v for k, v in b.items()})
-        for key in ("classic", "classic2"):
+        for key in ("classic", "classic2", "classic3"):
             if key in sc:
                 b = run_classic_beam(ns, model, cfg, chunks, **sc[key])
                 out.update({k.replace("beam", key): v for k, v in b.items()})
         meta = dict(name=sc["name"], cfg=sc["cfg"], seed=sc["seed"], eos_bias=sc["eos_bias"],
                     greedy=sc.get("greedy"), beam=sc.get("beam"), beam2=sc.get("beam2"),
-                    classic=sc.get("classic"), classic2=sc.get("classic2"),
+                    classic=sc.get("classic"), classic2=sc.get("classic2"), classic3=sc.get("classic3"),
                     mem_stride=MEM_STRIDE, weights_sha256=weights_digest(W),
                     torch=torch.__version__, numpy=np.__version__)
         out["meta"] = np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8)

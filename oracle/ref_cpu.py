@@ -248,9 +248,12 @@ def tile(x, count, dim=0):
 
 
 def fast_beam(model: RefModel, src, lengths, beam_size=5, n_best=1, max_length=100, min_length=0,
-              alpha=0.0):
+              alpha=0.0, return_attention=False):
     """translate/translator.py:619-825 (``--fast``).  Returns per chunk a list
-    of n_best (score, tokens) best-first."""
+    of n_best (score, tokens) best-first; with ``return_attention`` each entry
+    also carries the hypothesis' attention rows [steps, cut] (:745-751,
+    :780-790), cut = memory_lengths[i] with i the chunk's index among the
+    batches still alive (the reference indexes the beam-tiled lengths by it)."""
     src = _t(src)
     cfg = model.cfg
     V = cfg.vocab
@@ -258,15 +261,18 @@ def fast_beam(model: RefModel, src, lengths, beam_size=5, n_best=1, max_length=1
         memory = model.encode(src, lengths)
         B = src.shape[0]
         st = model.decoder_state(tile(memory, beam_size), tile(src, beam_size))
+        memory_lengths = tile(torch.as_tensor(np.asarray(lengths), dtype=torch.long), beam_size)
         top_beam_finished = torch.zeros(B, dtype=torch.bool)
         batch_offset = torch.arange(B)
         beam_offset = torch.arange(0, B * beam_size, beam_size)
         alive_seq = torch.full((B * beam_size, 1), cfg.bos_idx, dtype=torch.long)
+        alive_attn = None
         topk_log_probs = torch.tensor([0.0] + [float("-inf")] * (beam_size - 1)).repeat(B)
         hyps = [[] for _ in range(B)]
         results = [[] for _ in range(B)]
         for step in range(max_length):
             lp = model.decode_step(st, alive_seq[:, -1], step)
+            attn = st["attn"].unsqueeze(0)                          # [1, R, T]
             if step < min_length:
                 lp[:, cfg.eos_idx] = -1e20
             lp = lp + topk_log_probs.view(-1, 1)
@@ -279,6 +285,10 @@ def fast_beam(model: RefModel, src, lengths, beam_size=5, n_best=1, max_length=1
             batch_index = topk_beam_index + beam_offset[: topk_beam_index.size(0)].unsqueeze(1)
             select = batch_index.view(-1)
             alive_seq = torch.cat([alive_seq.index_select(0, select), topk_ids.view(-1, 1)], -1)
+            if return_attention:                                    # (:745-751)
+                cur_attn = attn.index_select(1, select)
+                alive_attn = cur_attn if alive_attn is None else \
+                    torch.cat([alive_attn.index_select(1, select), cur_attn], 0)
             is_finished = topk_ids.eq(cfg.eos_idx)
             if step + 1 == max_length:
                 is_finished.fill_(True)
@@ -286,14 +296,18 @@ def fast_beam(model: RefModel, src, lengths, beam_size=5, n_best=1, max_length=1
                 topk_log_probs = topk_log_probs.masked_fill(is_finished, -1e10)
                 top_beam_finished |= is_finished[:, 0]
                 preds = alive_seq.view(-1, beam_size, alive_seq.size(-1))
+                attention = (alive_attn.view(alive_attn.size(0), -1, beam_size, alive_attn.size(-1))
+                             if alive_attn is not None else None)
                 non_finished = []
                 for i in range(is_finished.size(0)):
                     b = int(batch_offset[i])
                     for j in torch.nonzero(is_finished[i]).view(-1).tolist():
-                        hyps[b].append((float(topk_scores[i, j]), preds[i, j, 1:].clone()))
+                        a = attention[:, i, j, : int(memory_lengths[i])].clone() if attention is not None else None
+                        hyps[b].append((float(topk_scores[i, j]), preds[i, j, 1:].clone(), a))
                     if bool(top_beam_finished[i]) and len(hyps[b]) >= n_best:
                         best = sorted(hyps[b], key=lambda x: x[0], reverse=True)
-                        results[b] = [(s, p.numpy().astype(np.int32)) for s, p in best[:n_best]]
+                        results[b] = [(sc, p.numpy().astype(np.int32)) + ((a.numpy(),) if return_attention else ())
+                                      for sc, p, a in best[:n_best]]
                     else:
                         non_finished.append(i)
                 if not non_finished:
@@ -305,7 +319,10 @@ def fast_beam(model: RefModel, src, lengths, beam_size=5, n_best=1, max_length=1
                 batch_index = batch_index.index_select(0, nf)
                 select = batch_index.view(-1)
                 alive_seq = preds.index_select(0, nf).view(-1, alive_seq.size(-1))
+                if alive_attn is not None:
+                    alive_attn = attention.index_select(1, nf).view(alive_attn.size(0), -1, alive_attn.size(-1))
             model.reorder(st, select)
+            memory_lengths = memory_lengths.index_select(0, select)
     return results
 
 
@@ -319,27 +336,89 @@ def _length_penalty(kind, n_ys, alpha):
     return 1.0
 
 
+def _coverage_penalty(kind, cov, beta):
+    """onmt/translate/penalties.py:34-53: beta * penalty per beam, cov [beam, cut]."""
+    if kind == "wu":
+        return beta * (-torch.min(cov, cov.clone().fill_(1.0)).log().sum(1))
+    if kind == "summary":
+        return beta * (torch.max(cov, cov.clone().fill_(1.0)).sum(1) - cov.size(1))
+    return torch.zeros(cov.size(0))
+
+
 class ClassicBeam:
     """onmt/translate/beam.py:6-178 (``Beam``) with GNMTGlobalScorer
-    (:181-199), coverage penalty 'none', no stepwise penalty, no n-gram
-    blocking."""
+    (:181-243): length penalty none / wu / avg, coverage penalty none / wu /
+    summary (at scoring time, or stepwise), n-gram blocking with exclusion
+    tokens, per-step attention kept for get_hyp."""
 
-    def __init__(self, size, pad, bos, eos, n_best, min_length, length_penalty, alpha):
+    def __init__(self, size, pad, bos, eos, n_best, min_length, length_penalty, alpha, beta=0.0,
+                 coverage_penalty="none", stepwise_penalty=False, block_ngram_repeat=0, exclusion_tokens=()):
         self.size, self._eos, self.n_best, self.min_length = size, eos, n_best, min_length
         self.lp, self.alpha = length_penalty, alpha
+        self.beta, self.cov = beta, coverage_penalty
+        self.stepwise_penalty = stepwise_penalty
+        self.block_ngram_repeat = block_ngram_repeat
+        self.exclusion_tokens = set(exclusion_tokens)
         self.scores = torch.zeros(size)                       # (:34)
         self.prev_ks = []
         self.next_ys = [torch.full((size,), pad, dtype=torch.long)]
         self.next_ys[0][0] = bos                              # (:41-43)
+        self.attn = []
         self.eos_top = False
         self.finished = []
+        self.global_state = {}
 
-    def global_score(self, scores):                           # (:200-212)
-        return scores / _length_penalty(self.lp, len(self.next_ys), self.alpha)
+    def _cov_pen(self, cov):
+        if self.cov == "none":                                # coverage_none: beam.scores zeros
+            return torch.zeros(self.size)
+        return _coverage_penalty(self.cov, cov, self.beta)
 
-    def advance(self, word_probs):                            # (:73-150)
+    def global_score(self, scores):                           # GNMTGlobalScorer.score (:200-212)
+        """length_none returns ``scores`` itself (penalties.py:74-78), so the
+        in-place ``normalized_probs -= penalty`` then also lowers beam.scores:
+        with length penalty none and a coverage penalty at scoring time, every
+        call (one per finished beam, and per top-up in sort_finished) moves
+        the live scores."""
+        if self.lp == "none":
+            normalized = scores
+        else:
+            normalized = scores / _length_penalty(self.lp, len(self.next_ys), self.alpha)
+        if not self.stepwise_penalty:
+            normalized -= self._cov_pen(self.global_state["coverage"])
+        return normalized
+
+    def _update_score(self, attn):                            # (:214-223)
+        if "prev_penalty" in self.global_state:
+            self.scores.add_(self.global_state["prev_penalty"])
+            self.scores.sub_(self._cov_pen(self.global_state["coverage"] + attn))
+
+    def _update_global_state(self):                           # (:225-243)
+        if len(self.prev_ks) == 1:
+            self.global_state["prev_penalty"] = self.scores.clone().fill_(0.0)
+            self.global_state["coverage"] = self.attn[-1]
+        else:
+            self.global_state["coverage"] = self.global_state["coverage"].index_select(
+                0, self.prev_ks[-1]).add(self.attn[-1])
+            self.global_state["prev_penalty"] = self._cov_pen(self.global_state["coverage"])
+
+    def _blocked(self, j):                                    # (:100-119)
+        le = len(self.next_ys)
+        hyp = self.get_hyp(le - 1, j)
+        ngrams, gram = set(), []
+        for i in range(le - 1):
+            gram = (gram + [hyp[i]])[-self.block_ngram_repeat:]
+            if set(gram) & self.exclusion_tokens:
+                continue
+            if tuple(gram) in ngrams:
+                return True
+            ngrams.add(tuple(gram))
+        return False
+
+    def advance(self, word_probs, attn_out):                  # (:73-150)
         V = word_probs.size(1)
         word_probs = word_probs.clone()
+        if self.stepwise_penalty:
+            self._update_score(attn_out)
         if len(self.next_ys) < self.min_length:               # (:88-91)
             word_probs[:, self._eos] = -1e20
         if len(self.prev_ks) > 0:                             # (:93-99)
@@ -347,6 +426,10 @@ class ClassicBeam:
             for i in range(self.next_ys[-1].size(0)):
                 if int(self.next_ys[-1][i]) == self._eos:
                     beam_scores[i] = -1e20
+            if self.block_ngram_repeat > 0:
+                for j in range(self.next_ys[-1].size(0)):
+                    if self._blocked(j):
+                        beam_scores[j] = -10e20
         else:
             beam_scores = word_probs[0]
         best_scores, best_ids = beam_scores.reshape(-1).topk(self.size, 0, True, True)   # (:122-123)
@@ -354,6 +437,8 @@ class ClassicBeam:
         prev_k = torch.div(best_ids, V, rounding_mode="floor")   # (:129, integer division in torch 1.0)
         self.prev_ks.append(prev_k)
         self.next_ys.append(best_ids - prev_k * V)
+        self.attn.append(attn_out.index_select(0, prev_k))
+        self._update_global_state()
         for i in range(self.next_ys[-1].size(0)):             # (:135-139)
             if int(self.next_ys[-1][i]) == self._eos:
                 s = self.global_score(self.scores)[i]
@@ -381,34 +466,49 @@ class ClassicBeam:
             k = int(self.prev_ks[j][k])
         return hyp[::-1]
 
+    def get_hyp_attn(self, timestep, k):
+        att = []
+        for j in range(len(self.prev_ks[:timestep]) - 1, -1, -1):
+            att.append(self.attn[j][k])
+            k = int(self.prev_ks[j][k])
+        return torch.stack(att[::-1])
+
 
 def classic_beam(model: RefModel, src, lengths, beam_size=5, n_best=1, max_length=100, min_length=0,
-                 alpha=0.0, length_penalty="none"):
+                 alpha=0.0, length_penalty="none", beta=0.0, coverage_penalty="none", stepwise_penalty=False,
+                 block_ngram_repeat=0, exclusion_tokens=(), return_attention=False):
     """translate/translator.py:827-926 (``_translate_batch``, beam_size > 1
     without --fast): one Beam per chunk, the whole batch advances until every
-    beam is done.  Returns per chunk n_best (score, tokens) best-first."""
+    beam is done.  Beam j's attention rows are cut at memory_lengths[j] of the
+    beam-tiled lengths (:902-907), i.e. at lengths[j // beam_size].  Returns
+    per chunk n_best (score, tokens[, attention [steps, cut]]) best-first."""
     src = _t(src)
     cfg = model.cfg
     with torch.no_grad():
         memory = model.encode(src, lengths)
         B = src.shape[0]
         beams = [ClassicBeam(beam_size, cfg.pad_idx, cfg.bos_idx, cfg.eos_idx, n_best, min_length,
-                             length_penalty, alpha) for _ in range(B)]
+                             length_penalty, alpha, beta, coverage_penalty, stepwise_penalty, block_ngram_repeat,
+                             exclusion_tokens) for _ in range(B)]
         st = model.decoder_state(tile(memory, beam_size), tile(src, beam_size))
+        memory_lengths = tile(torch.as_tensor(np.asarray(lengths), dtype=torch.long), beam_size)
         for i in range(max_length):
             if all(b.done() for b in beams):                   # (:884-885)
                 break
             inp = torch.stack([b.next_ys[-1] for b in beams]).view(-1)
             lp = model.decode_step(st, inp, i).view(B, beam_size, -1)
+            attn = st["attn"].view(B, beam_size, -1)
             sel = []
             for j, b in enumerate(beams):
-                b.advance(lp[j])
+                b.advance(lp[j], attn[j, :, : int(memory_lengths[j])])
                 sel.append(b.prev_ks[-1] + j * beam_size)
             model.reorder(st, torch.cat(sel))
         out = []
         for b in beams:                                        # (:914-924)
             scores, ks = b.sort_finished(minimum=n_best)
-            out.append([(scores[n], np.array(b.get_hyp(t, k), np.int32)) for n, (t, k) in enumerate(ks[:n_best])])
+            out.append([(scores[n], np.array(b.get_hyp(t, k), np.int32))
+                        + ((b.get_hyp_attn(t, k).numpy(),) if return_attention else ())
+                        for n, (t, k) in enumerate(ks[:n_best])])
     return out
 
 

@@ -40,8 +40,37 @@ def test_greedy_matches_reference(name):
             np.testing.assert_allclose(att[i, :, :L], z["attn"][i, :, :L], atol=1e-6)
 
 
+def _search_kwargs(kw, cfg):
+    """golden run options -> ref_cpu keyword arguments (token strings of
+    ignore_when_blocking -> ids, as translator.py:836 builds them)."""
+    out = {k: v for k, v in kw.items() if k not in ("attention", "ignore_when_blocking")}
+    out["return_attention"] = bool(kw.get("attention", False))
+    if "ignore_when_blocking" in kw:
+        out["exclusion_tokens"] = {cfg.itos.index(t) for t in kw["ignore_when_blocking"]}
+    return out
+
+
+def _score_close(a, b, tol=1e-4):
+    return (np.isinf(a) and a == b) or abs(a - b) < tol
+
+
+def _check_hyps(res, z, order, kw, tok_key, len_key, sc_key, att_key=None, cut_key=None):
+    for j, i in enumerate(order):
+        assert len(res[j]) == kw["n_best"]
+        for nb, h in enumerate(res[j]):
+            s, p = h[0], h[1]
+            L = z[len_key][i, nb]
+            assert len(p) == L
+            assert (p == z[tok_key][i, nb, :L]).all()
+            assert _score_close(s, z[sc_key][i, nb]), (s, z[sc_key][i, nb])
+            if att_key is not None:
+                a = h[2]
+                assert a.shape == (L, z[cut_key][i, nb])
+                np.testing.assert_allclose(a, z[att_key][i, nb, :L, : a.shape[1]], atol=1e-6)
+
+
 @pytest.mark.parametrize("name,which", [("transformer_beam", ""), ("transformer_beam", "2"),
-                                        ("transformer_aan", "")])
+                                        ("transformer_aan", ""), ("transformer_beam_attn", "")])
 def test_fast_beam_matches_reference(name, which):
     z, meta = gu.load(name)
     cfg, W = gu.model_for(meta)
@@ -49,35 +78,31 @@ def test_fast_beam_matches_reference(name, which):
     chunks = gu.chunks_of(z)
     src, lens, order = ref_cpu.make_batch(chunks)
     kw = meta["beam" + which]
-    res = ref_cpu.fast_beam(m, src, lens, **kw)
-    for j, i in enumerate(order):
-        assert len(res[j]) == kw["n_best"]
-        for nb, (s, p) in enumerate(res[j]):
-            L = z["beam_lens" + which][i, nb]
-            assert len(p) == L
-            assert (p == z["beam_tokens" + which][i, nb, :L]).all()
-            assert abs(s - z["beam_scores" + which][i, nb]) < 1e-4
+    res = ref_cpu.fast_beam(m, src, lens, **_search_kwargs(kw, cfg))
+    att = ("beam_attn" + which, "beam_attn_cut" + which) if kw.get("attention") else (None, None)
+    _check_hyps(res, z, order, kw, "beam_tokens" + which, "beam_lens" + which, "beam_scores" + which, *att)
 
 
 @pytest.mark.parametrize("name,which", [("transformer_classic_beam", "classic"), ("transformer_classic_beam", "classic2"),
-                                        ("transformer_classic_beam_mid", "classic")])
+                                        ("transformer_classic_beam_mid", "classic"),
+                                        ("transformer_beam_attn", "classic"), ("transformer_classic_ext", "classic"),
+                                        ("transformer_classic_ext", "classic2"),
+                                        ("transformer_classic_cov", "classic"), ("transformer_classic_cov", "classic2"),
+                                        ("transformer_classic_cov", "classic3")])
 def test_classic_beam_matches_reference(name, which):
     """The onmt Beam path (translate/translator.py:827-926), restated in
-    ref_cpu.ClassicBeam, against the reference's own _translate_batch."""
+    ref_cpu.ClassicBeam, against the reference's own _translate_batch:
+    length / coverage penalties, stepwise penalty, n-gram blocking and the
+    per-hypothesis attention."""
     z, meta = gu.load(name)
     cfg, W = gu.model_for(meta)
     m = ref_cpu.RefModel(cfg, W)
     chunks = gu.chunks_of(z)
     src, lens, order = ref_cpu.make_batch(chunks)
     kw = meta[which]
-    res = ref_cpu.classic_beam(m, src, lens, **kw)
-    for j, i in enumerate(order):
-        assert len(res[j]) == kw["n_best"]
-        for nb, (s, p) in enumerate(res[j]):
-            L = z[which + "_lens"][i, nb]
-            assert len(p) == L
-            assert (p == z[which + "_tokens"][i, nb, :L]).all()
-            assert abs(s - z[which + "_scores"][i, nb]) < 1e-4
+    res = ref_cpu.classic_beam(m, src, lens, **_search_kwargs(kw, cfg))
+    att = (which + "_attn", which + "_attn_cut") if kw.get("attention") else (None, None)
+    _check_hyps(res, z, order, kw, which + "_tokens", which + "_lens", which + "_scores", *att)
 
 
 def test_translate_batching_and_strings():
