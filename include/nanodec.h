@@ -129,6 +129,47 @@ int nd_translate_beam_classic(nd_ctx* ctx, const float* d_signal, const int32_t*
                               int32_t length_penalty, float alpha, int32_t max_len, int32_t min_len,
                               int32_t* d_tokens, float* d_scores, int32_t* d_lens, int32_t* d_steps, void* stream);
 
+/* --fast beam search with -attn_debug (translate/translator.py:745-751,
+ * :780-790): as nd_translate_beam, plus
+ *   d_attn      [B, n_best, max_len, T] f32: row t of hypothesis k = the
+ *               last layer's head-0 context attention of the decoder row
+ *               that produced its token t (probabilities over keys < span,
+ *               zero after), zero rows past the hypothesis length
+ *   d_done_step [B] i32: the number of steps the chunk ran before it was
+ *               dropped as finished (the caller derives the reference's
+ *               memory_lengths[i] cut from the alive set of each step) */
+int nd_translate_beam_attn(nd_ctx* ctx, const float* d_signal, const int32_t* d_len, const int32_t* d_span,
+                           int32_t B, int32_t T, int32_t beam, int32_t n_best, float alpha, int32_t max_len,
+                           int32_t min_len, int32_t* d_tokens, float* d_scores, int32_t* d_lens, int32_t* d_steps,
+                           float* d_attn, int32_t* d_done_step, void* stream);
+
+/* Options of the classic onmt Beam (translate/translator.py:127-173,
+ * onmt/translate/beam.py:6-243, onmt/translate/penalties.py). */
+typedef struct nd_classic_opts {
+  int32_t length_penalty;     /* 0 none, 1 wu, 2 avg */
+  float alpha;                /* -alpha */
+  float beta;                 /* -beta (coverage weight) */
+  int32_t coverage_penalty;   /* 0 none, 1 wu, 2 summary */
+  int32_t stepwise_penalty;   /* -stepwise_penalty */
+  int32_t block_ngram_repeat; /* -block_ngram_repeat (0: off) */
+  uint32_t ignore_mask;       /* -ignore_when_blocking: bit i = token id i */
+} nd_classic_opts;
+
+/* Classic beam search with the full option set: as nd_translate_beam_classic,
+ * plus coverage penalties (wu / summary, at scoring time or stepwise) and
+ * n-gram blocking, and optionally the hypotheses' attention.
+ *   d_cut  [B] i32, required when coverage_penalty != 0: the attention length
+ *          of the chunk's beams, memory_lengths[j] as the reference indexes
+ *          its beam-tiled lengths (translate/translator.py:902-907)
+ *   d_attn nullable [B, n_best, max_len, T] f32: as nd_translate_beam_attn
+ * With coverage_penalty != 0 the attention is captured every step whether or
+ * not d_attn is given. */
+int nd_translate_beam_classic_ex(nd_ctx* ctx, const float* d_signal, const int32_t* d_len, const int32_t* d_span,
+                                 const int32_t* d_group, const int32_t* d_cut, int32_t B, int32_t T, int32_t beam,
+                                 int32_t n_best, const nd_classic_opts* opts, int32_t max_len, int32_t min_len,
+                                 int32_t* d_tokens, float* d_scores, int32_t* d_lens, int32_t* d_steps, float* d_attn,
+                                 void* stream);
+
 /* Encoder forward only; writes the memory bank [B, T, d_model] (rows
  * t >= span are unspecified).  Replaces Translator._run_encoder
  * (translate/translator.py:542-559).  Used by parity tests. */

@@ -28,6 +28,13 @@ class NdConfig(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in _CFG_FIELDS]
 
 
+class NdClassicOpts(ctypes.Structure):
+    """include/nanodec.h nd_classic_opts."""
+    _fields_ = [("length_penalty", ctypes.c_int32), ("alpha", ctypes.c_float), ("beta", ctypes.c_float),
+                ("coverage_penalty", ctypes.c_int32), ("stepwise_penalty", ctypes.c_int32),
+                ("block_ngram_repeat", ctypes.c_int32), ("ignore_mask", ctypes.c_uint32)]
+
+
 _P = ctypes.c_void_p
 _I = ctypes.c_int32
 _F = ctypes.c_float
@@ -40,7 +47,10 @@ SIGNATURES = {
     "nd_translate_greedy": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P]),
     "nd_translate_greedy_attn": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
     "nd_translate_beam": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _F, _I, _I, _P, _P, _P, _P, _P]),
+    "nd_translate_beam_attn": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _F, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
     "nd_translate_beam_classic": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _F, _I, _I, _P, _P, _P, _P, _P]),
+    "nd_translate_beam_classic_ex": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, ctypes.POINTER(NdClassicOpts), _I,
+                                          _I, _P, _P, _P, _P, _P, _P]),
     "nd_encode": (_I, [_P, _P, _P, _P, _I, _I, _P, _P]),
     "nd_set_graphs": (_I, [_P, _I]),
     "nd_set_timing": (_I, [_P, _I]),

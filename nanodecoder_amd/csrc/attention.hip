@@ -586,8 +586,10 @@ dec_ctx_attention_kernel(const float* __restrict__ q, const float* __restrict__ 
         const float d = sum8(qv[j].x * kc[u].x + qv[j].y * kc[u].y + qv[j].z * kc[u].z + qv[j].w * kc[u].w);
         sc[j][u] = valid ? (masked ? ND_MASK_FILL : d) : -INFINITY;
       }
-      // -attn_debug: head 0 (lanes 0..7 after sum8) of the chunk's first row
-      if (dbg && lane == 0 && valid) dbg[(size_t)c * dbg_stride + blk * U + u] = sc[0][u];
+      // -attn_debug / coverage: head 0 (lanes 0..7 after sum8) of every row of the chunk
+      if (dbg && lane == 0 && valid)
+#pragma unroll
+        for (int j = 0; j < RPC; ++j) dbg[((size_t)c * RPC + j) * dbg_stride + blk * U + u] = sc[j][u];
     }
     online_update<RPC, U>(sc, vc, m, l, acc);
     if (more) {

@@ -82,9 +82,14 @@ struct GraphKey {
   int mode, B, T, S, min_len, beam, n_best, seg, logp;
   float alpha;
   int stamp = 0;
+  // attention capture and the classic Beam's options
+  int attn = 0, cov = 0, stepwise = 0, ngram = 0;
+  unsigned excl = 0;
+  float beta = 0.f;
   bool operator<(const GraphKey& o) const {
-    return std::tie(mode, B, T, S, min_len, beam, n_best, seg, logp, alpha, stamp) <
-           std::tie(o.mode, o.B, o.T, o.S, o.min_len, o.beam, o.n_best, o.seg, o.logp, o.alpha, o.stamp);
+    return std::tie(mode, B, T, S, min_len, beam, n_best, seg, logp, alpha, stamp, attn, cov, stepwise, ngram, excl,
+                    beta) < std::tie(o.mode, o.B, o.T, o.S, o.min_len, o.beam, o.n_best, o.seg, o.logp, o.alpha,
+                                     o.stamp, o.attn, o.cov, o.stepwise, o.ngram, o.excl, o.beta);
   }
 };
 
@@ -135,8 +140,10 @@ struct nd_ctx {
   nd::BeamState bs{};
   int* steps_done = nullptr;
   int* group_in = nullptr;  // classic Beam: staged reference-batch ids
-  float* attn_raw = nullptr;  // -attn_debug: [max_batch][max_steps][max_src_len] head-0 scores -> probabilities
-  bool attn_on = false;       // set while a greedy call with an attention dump is enqueued
+  int* cut_in = nullptr;    // classic Beam: staged attention lengths (coverage penalties)
+  // -attn_debug / coverage: [decoder rows][max_steps][max_src_len] head-0 context scores -> probabilities
+  float* attn_raw = nullptr;
+  bool attn_on = false;       // set while a call that captures the attention is enqueued
   int* h_alive = nullptr;  // pinned
 
   hipStream_t es = nullptr;
@@ -381,7 +388,16 @@ static int alloc_workspaces(nd_ctx* c) {
   WS(c->bs.grp_left, B);
   WS(c->bs.grp_done, B);
   WS(c->bs.steps_run, B);
+  WS(c->bs.hyp_anc, B * NB * S);
+  WS(c->bs.cov[0], R * T);
+  WS(c->bs.cov[1], R * T);
+  WS(c->bs.pen, R);
+  WS(c->bs.prev_pen, R);
+  WS(c->bs.blk[0], R);
+  WS(c->bs.blk[1], R);
+  c->bs.T = (int)T;
   WS(c->group_in, B);
+  WS(c->cut_in, B);
   WS(c->kstamp, Ld * S * 2);
 #undef WS
   if ((e = hipHostMalloc((void**)&c->h_alive, 16, hipHostMallocDefault)) != hipSuccess)
@@ -568,24 +584,44 @@ static hipError_t enqueue_greedy(nd_ctx* c, int B, int T, int S, int min_len, bo
   return hipSuccess;
 }
 
+// the beam paths' view of the search state: the attention rows are visible
+// to the search kernels only while a capturing call is enqueued
+static nd::BeamState beam_state(nd_ctx* c) {
+  nd::BeamState st = c->bs;
+  st.attn = c->attn_on ? c->attn_raw : nullptr;
+  st.cut = c->cut_in;
+  return st;
+}
+
+// -attn_debug / coverage: this step's captured scores -> probabilities
+static hipError_t enqueue_attn_step(nd_ctx* c, int C, int rpc, int T, int step, hipStream_t s) {
+  if (!c->attn_on) return hipSuccess;
+  const size_t S = c->cfg.max_steps;
+  return nd::launch_attn_step_softmax(c->attn_raw + (size_t)step * T, S * T, c->span, C * rpc, rpc, T, s);
+}
+
 static hipError_t enqueue_beam_steps(nd_ctx* c, int B, int T, int beam, int n_best, float alpha, int S, int min_len,
                                      int s0, int s1, hipStream_t s) {
+  const nd::BeamState st = beam_state(c);
   for (int step = s0; step < s1; ++step) {
     const int cur = step & 1;
     LCHK(enqueue_dec_step(c, B, beam, T, step, c->bs.anc[cur], S, s));
+    LCHK(enqueue_attn_step(c, B, beam, T, step, s));
     const float lenpen = (float)std::pow((5.0 + (step + 1)) / 6.0, (double)alpha);
-    LCHK(nd::launch_beam_step(next_embed(c), c->dx, c->dec_ln_g, c->dec_ln_b, c->gen_w, c->gen_b, c->V, c->bs, B, beam, n_best,
-                              step, S, min_len, c->cfg.eos_idx, lenpen, s));
+    LCHK(nd::launch_beam_step(next_embed(c), c->dx, c->dec_ln_g, c->dec_ln_b, c->gen_w, c->gen_b, c->V, st, B, beam,
+                              n_best, step, S, min_len, c->cfg.eos_idx, lenpen, s));
   }
   return hipSuccess;
 }
 
-static hipError_t enqueue_classic_steps(nd_ctx* c, int B, int T, int beam, int n_best, int lpk, float alpha, int S,
+static hipError_t enqueue_classic_steps(nd_ctx* c, int B, int T, int beam, int n_best, const nd::ClassicOpts& o, int S,
                                         int min_len, int s0, int s1, hipStream_t s) {
+  const nd::BeamState st = beam_state(c);
   for (int step = s0; step < s1; ++step) {
     LCHK(enqueue_dec_step(c, B, beam, T, step, c->bs.anc[step & 1], S, s));
-    LCHK(nd::launch_beam_classic_step(next_embed(c), c->dx, c->dec_ln_g, c->dec_ln_b, c->gen_w, c->gen_b, c->V, c->bs,
-                                      B, beam, n_best, step, S, min_len, c->cfg.eos_idx, lpk, alpha, s));
+    LCHK(enqueue_attn_step(c, B, beam, T, step, s));
+    LCHK(nd::launch_beam_classic_step(next_embed(c), c->dx, c->dec_ln_g, c->dec_ln_b, c->gen_w, c->gen_b, c->V, st,
+                                      B, beam, n_best, step, S, min_len, c->cfg.eos_idx, o, s));
   }
   return hipSuccess;
 }
@@ -929,17 +965,22 @@ static int release_to(nd_ctx* c, hipStream_t cs) {
   return ND_OK;
 }
 
+// the attention capture buffer, [decoder rows][max_steps][max_src_len], made on first use
+static int ensure_attn(nd_ctx* c) {
+  if (c->attn_raw) return ND_OK;
+  const size_t R = ((size_t)c->cfg.max_batch * std::max(1, c->cfg.max_beam) + 15) / 16 * 16;
+  hipError_t e = dalloc(c, &c->attn_raw, R * c->cfg.max_steps * c->cfg.max_src_len);
+  if (e != hipSuccess) return fail(ND_ERR_HIP, std::string("hipMalloc attention capture: ") + hipGetErrorString(e));
+  return ND_OK;
+}
+
 static int translate_greedy(nd_ctx* c, const float* d_signal, const int32_t* d_len, const int32_t* d_span, int32_t B,
                             int32_t T, int32_t max_len, int32_t min_len, int32_t* d_tokens, float* d_score,
                             float* d_logp, float* d_attn, void* stream) {
   int rc = check_call(c, B, T, max_len);
   if (rc) return rc;
   if (!d_signal || !d_len || !d_span || !d_tokens || !d_score) return fail(ND_ERR_ARG, "null buffer");
-  if (d_attn && !c->attn_raw) {
-    const size_t n = (size_t)c->cfg.max_batch * c->cfg.max_steps * c->cfg.max_src_len;
-    hipError_t e = dalloc(c, &c->attn_raw, n);
-    if (e != hipSuccess) return fail(ND_ERR_HIP, std::string("hipMalloc attention dump: ") + hipGetErrorString(e));
-  }
+  if (d_attn && (rc = ensure_attn(c))) return rc;
   hipStream_t cs = (hipStream_t)stream;
   if ((rc = stage_inputs(c, d_signal, d_len, d_span, B, T, cs))) return rc;
   const bool lp = d_logp != nullptr;
@@ -981,22 +1022,26 @@ int nd_translate_greedy_attn(nd_ctx* c, const float* d_signal, const int32_t* d_
                           stream);
 }
 
-int nd_translate_beam(nd_ctx* c, const float* d_signal, const int32_t* d_len, const int32_t* d_span, int32_t B,
-                      int32_t T, int32_t beam, int32_t n_best, float alpha, int32_t max_len, int32_t min_len,
-                      int32_t* d_tokens, float* d_scores, int32_t* d_lens, int32_t* d_steps, void* stream) {
+static int translate_beam(nd_ctx* c, const float* d_signal, const int32_t* d_len, const int32_t* d_span, int32_t B,
+                          int32_t T, int32_t beam, int32_t n_best, float alpha, int32_t max_len, int32_t min_len,
+                          int32_t* d_tokens, float* d_scores, int32_t* d_lens, int32_t* d_steps, float* d_attn,
+                          int32_t* d_done_step, void* stream) {
   int rc = check_call(c, B, T, max_len);
   if (rc) return rc;
   if (beam < 1 || beam > c->cfg.max_beam) return fail(ND_ERR_ARG, "beam out of range [1, max_beam]");
   if (n_best < 1 || n_best > beam) return fail(ND_ERR_ARG, "n_best out of range [1, beam]");
   if (c->V < beam) return fail(ND_ERR_ARG, "vocab smaller than beam");
   if (!d_signal || !d_len || !d_span || !d_tokens || !d_scores || !d_lens) return fail(ND_ERR_ARG, "null buffer");
+  if (d_attn && (rc = ensure_attn(c))) return rc;
   hipStream_t cs = (hipStream_t)stream;
   if ((rc = stage_inputs(c, d_signal, d_len, d_span, B, T, cs))) return rc;
   // n_best hypothesis storage is sized by max_beam
   const int SEG = 10;
   const int st = c->kstamp_on ? 1 : 0;
   GraphKey k0{1, B, T, max_len, min_len, beam, n_best, -1, 0, alpha, st};
+  k0.attn = d_attn ? 1 : 0;
   if (c->timing) HIPCHK(hipEventRecord(c->ev_a, c->es));
+  c->attn_on = d_attn != nullptr;
   rc = run_graph(c, k0, [&](hipStream_t s) -> hipError_t {
     if (c->kstamp_on) LCHK(nd::launch_stamp_reset(c->kstamp, (int)c->dec.size() * c->cfg.max_steps, s));
     LCHK(enqueue_encode(c, B, T, s));
@@ -1006,24 +1051,36 @@ int nd_translate_beam(nd_ctx* c, const float* d_signal, const int32_t* d_len, co
     LCHK(nd::launch_fill_i32(c->steps_done, max_len, 1, s));
     return hipSuccess;
   });
-  if (rc) return rc;
+  if (rc) {
+    c->attn_on = false;
+    return rc;
+  }
   if (c->timing) HIPCHK(hipEventRecord(c->ev_b, c->es));
   for (int s0 = 0; s0 < max_len; s0 += SEG) {
     const int s1 = std::min(max_len, s0 + SEG);
     GraphKey k{1, B, T, max_len, min_len, beam, n_best, s0, 0, alpha, st};
+    k.attn = k0.attn;
     rc = run_graph(c, k, [&](hipStream_t s) {
       return enqueue_beam_steps(c, B, T, beam, n_best, alpha, max_len, min_len, s0, s1, s);
     });
-    if (rc) return rc;
+    if (rc) break;
     if (s1 < max_len) {
       HIPCHK(hipMemcpyAsync(c->h_alive, c->bs.n_alive, 4, hipMemcpyDeviceToHost, c->es));
       HIPCHK(hipStreamSynchronize(c->es));
       if (*c->h_alive == 0) break;
     }
   }
+  c->attn_on = false;
+  if (rc) return rc;
   if (c->timing) HIPCHK(hipEventRecord(c->ev_c, c->es));
   HIPCHK(nd::launch_beam_finish(c->bs, B, n_best, max_len, d_tokens, d_scores, d_lens, c->es));
   if (d_steps) HIPCHK(hipMemcpyAsync(d_steps, c->steps_done, 4, hipMemcpyDeviceToDevice, c->es));
+  if (d_attn) {
+    nd::BeamState bst = c->bs;
+    bst.attn = c->attn_raw;
+    HIPCHK(nd::launch_beam_attn_gather(bst, B, n_best, c->cfg.max_steps, max_len, T, d_attn, c->es));
+  }
+  if (d_done_step) HIPCHK(hipMemcpyAsync(d_done_step, c->bs.steps_run, (size_t)B * 4, hipMemcpyDeviceToDevice, c->es));
   if (c->timing) {
     HIPCHK(hipEventSynchronize(c->ev_c));
     HIPCHK(hipEventElapsedTime(&c->t_enc, c->ev_a, c->ev_b));
@@ -1032,25 +1089,60 @@ int nd_translate_beam(nd_ctx* c, const float* d_signal, const int32_t* d_len, co
   return release_to(c, cs);
 }
 
-int nd_translate_beam_classic(nd_ctx* c, const float* d_signal, const int32_t* d_len, const int32_t* d_span,
-                              const int32_t* d_group, int32_t B, int32_t T, int32_t beam, int32_t n_best,
-                              int32_t length_penalty, float alpha, int32_t max_len, int32_t min_len,
-                              int32_t* d_tokens, float* d_scores, int32_t* d_lens, int32_t* d_steps, void* stream) {
+int nd_translate_beam(nd_ctx* c, const float* d_signal, const int32_t* d_len, const int32_t* d_span, int32_t B,
+                      int32_t T, int32_t beam, int32_t n_best, float alpha, int32_t max_len, int32_t min_len,
+                      int32_t* d_tokens, float* d_scores, int32_t* d_lens, int32_t* d_steps, void* stream) {
+  return translate_beam(c, d_signal, d_len, d_span, B, T, beam, n_best, alpha, max_len, min_len, d_tokens, d_scores,
+                        d_lens, d_steps, nullptr, nullptr, stream);
+}
+
+int nd_translate_beam_attn(nd_ctx* c, const float* d_signal, const int32_t* d_len, const int32_t* d_span, int32_t B,
+                           int32_t T, int32_t beam, int32_t n_best, float alpha, int32_t max_len, int32_t min_len,
+                           int32_t* d_tokens, float* d_scores, int32_t* d_lens, int32_t* d_steps, float* d_attn,
+                           int32_t* d_done_step, void* stream) {
+  if (!d_attn || !d_done_step) return fail(ND_ERR_ARG, "null attention buffer");
+  return translate_beam(c, d_signal, d_len, d_span, B, T, beam, n_best, alpha, max_len, min_len, d_tokens, d_scores,
+                        d_lens, d_steps, d_attn, d_done_step, stream);
+}
+
+static int translate_classic(nd_ctx* c, const float* d_signal, const int32_t* d_len, const int32_t* d_span,
+                             const int32_t* d_group, const int32_t* d_cut, int32_t B, int32_t T, int32_t beam,
+                             int32_t n_best, const nd_classic_opts& op, int32_t max_len, int32_t min_len,
+                             int32_t* d_tokens, float* d_scores, int32_t* d_lens, int32_t* d_steps, float* d_attn,
+                             void* stream) {
   int rc = check_call(c, B, T, max_len);
   if (rc) return rc;
   if (beam < 1 || beam > c->cfg.max_beam) return fail(ND_ERR_ARG, "beam out of range [1, max_beam]");
   if (n_best < 1 || n_best > beam) return fail(ND_ERR_ARG, "n_best out of range [1, beam]");
   if (c->V < beam) return fail(ND_ERR_ARG, "vocab smaller than beam");
-  if (length_penalty < 0 || length_penalty > 2) return fail(ND_ERR_ARG, "length_penalty must be 0 (none), 1 (wu), 2 (avg)");
+  if (op.length_penalty < 0 || op.length_penalty > 2)
+    return fail(ND_ERR_ARG, "length_penalty must be 0 (none), 1 (wu), 2 (avg)");
+  if (op.coverage_penalty < 0 || op.coverage_penalty > 2)
+    return fail(ND_ERR_ARG, "coverage_penalty must be 0 (none), 1 (wu), 2 (summary)");
+  if (op.block_ngram_repeat < 0 || op.block_ngram_repeat > max_len)
+    return fail(ND_ERR_ARG, "block_ngram_repeat out of range [0, max_len]");
   if (!d_signal || !d_len || !d_span || !d_group || !d_tokens || !d_scores || !d_lens)
     return fail(ND_ERR_ARG, "null buffer");
+  if (op.coverage_penalty != 0 && !d_cut) return fail(ND_ERR_ARG, "coverage penalty needs the attention lengths");
+  const bool capture = d_attn != nullptr || op.coverage_penalty != 0;
+  if (capture && (rc = ensure_attn(c))) return rc;
   hipStream_t cs = (hipStream_t)stream;
   if ((rc = stage_inputs(c, d_signal, d_len, d_span, B, T, cs))) return rc;
   HIPCHK(hipMemcpyAsync(c->group_in, d_group, (size_t)B * 4, hipMemcpyDeviceToDevice, c->es));
+  if (d_cut) HIPCHK(hipMemcpyAsync(c->cut_in, d_cut, (size_t)B * 4, hipMemcpyDeviceToDevice, c->es));
+  const nd::ClassicOpts o{op.length_penalty, op.alpha, op.beta,          op.coverage_penalty,
+                          op.stepwise_penalty, op.block_ngram_repeat, op.ignore_mask};
   const int SEG = 10;
   const int st = c->kstamp_on ? 1 : 0;
-  // graph keys: mode 2, alpha and the penalty kind folded into (alpha, n_best) slots
-  GraphKey k0{2, B, T, max_len, min_len, beam, n_best, -1, length_penalty, alpha, st};
+  // graph keys: mode 2, the length penalty kind in the logp slot
+  GraphKey k0{2, B, T, max_len, min_len, beam, n_best, -1, op.length_penalty, op.alpha, st};
+  k0.attn = capture ? 1 : 0;
+  k0.cov = op.coverage_penalty;
+  k0.stepwise = op.stepwise_penalty;
+  k0.ngram = op.block_ngram_repeat;
+  k0.excl = op.ignore_mask;
+  k0.beta = op.beta;
+  c->attn_on = capture;
   rc = run_graph(c, k0, [&](hipStream_t s) -> hipError_t {
     if (c->kstamp_on) LCHK(nd::launch_stamp_reset(c->kstamp, (int)c->dec.size() * c->cfg.max_steps, s));
     LCHK(enqueue_encode(c, B, T, s));
@@ -1060,24 +1152,55 @@ int nd_translate_beam_classic(nd_ctx* c, const float* d_signal, const int32_t* d
     LCHK(nd::launch_fill_i32(c->steps_done, max_len, 1, s));
     return hipSuccess;
   });
-  if (rc) return rc;
+  if (rc) {
+    c->attn_on = false;
+    return rc;
+  }
   for (int s0 = 0; s0 < max_len; s0 += SEG) {
     const int s1 = std::min(max_len, s0 + SEG);
-    GraphKey k{2, B, T, max_len, min_len, beam, n_best, s0, length_penalty, alpha, st};
+    GraphKey k = k0;
+    k.seg = s0;
     rc = run_graph(c, k, [&](hipStream_t s) {
-      return enqueue_classic_steps(c, B, T, beam, n_best, length_penalty, alpha, max_len, min_len, s0, s1, s);
+      return enqueue_classic_steps(c, B, T, beam, n_best, o, max_len, min_len, s0, s1, s);
     });
-    if (rc) return rc;
+    if (rc) break;
     if (s1 < max_len) {
       HIPCHK(hipMemcpyAsync(c->h_alive, c->bs.n_alive, 4, hipMemcpyDeviceToHost, c->es));
       HIPCHK(hipStreamSynchronize(c->es));
       if (*c->h_alive == 0) break;
     }
   }
-  HIPCHK(nd::launch_beam_classic_finish(c->bs, B, beam, n_best, max_len, length_penalty, alpha, d_tokens, d_scores,
-                                        d_lens, c->es));
+  c->attn_on = false;
+  if (rc) return rc;
+  HIPCHK(nd::launch_beam_classic_finish(c->bs, B, beam, n_best, max_len, o, d_tokens, d_scores, d_lens, c->es));
   if (d_steps) HIPCHK(hipMemcpyAsync(d_steps, c->steps_done, 4, hipMemcpyDeviceToDevice, c->es));
+  if (d_attn) {
+    nd::BeamState bst = c->bs;
+    bst.attn = c->attn_raw;
+    HIPCHK(nd::launch_beam_attn_gather(bst, B, n_best, c->cfg.max_steps, max_len, T, d_attn, c->es));
+  }
   return release_to(c, cs);
+}
+
+int nd_translate_beam_classic(nd_ctx* c, const float* d_signal, const int32_t* d_len, const int32_t* d_span,
+                              const int32_t* d_group, int32_t B, int32_t T, int32_t beam, int32_t n_best,
+                              int32_t length_penalty, float alpha, int32_t max_len, int32_t min_len,
+                              int32_t* d_tokens, float* d_scores, int32_t* d_lens, int32_t* d_steps, void* stream) {
+  nd_classic_opts op{};
+  op.length_penalty = length_penalty;
+  op.alpha = alpha;
+  return translate_classic(c, d_signal, d_len, d_span, d_group, nullptr, B, T, beam, n_best, op, max_len, min_len,
+                           d_tokens, d_scores, d_lens, d_steps, nullptr, stream);
+}
+
+int nd_translate_beam_classic_ex(nd_ctx* c, const float* d_signal, const int32_t* d_len, const int32_t* d_span,
+                                 const int32_t* d_group, const int32_t* d_cut, int32_t B, int32_t T, int32_t beam,
+                                 int32_t n_best, const nd_classic_opts* opts, int32_t max_len, int32_t min_len,
+                                 int32_t* d_tokens, float* d_scores, int32_t* d_lens, int32_t* d_steps, float* d_attn,
+                                 void* stream) {
+  if (!opts) return fail(ND_ERR_ARG, "null options");
+  return translate_classic(c, d_signal, d_len, d_span, d_group, d_cut, B, T, beam, n_best, *opts, max_len, min_len,
+                           d_tokens, d_scores, d_lens, d_steps, d_attn, stream);
 }
 
 int nd_encode(nd_ctx* c, const float* d_signal, const int32_t* d_len, const int32_t* d_span, int32_t B, int32_t T,

@@ -163,7 +163,26 @@ struct BeamState {
   int* group;        // [C] reference batch id
   int* grp_left;     // [C] chunks of the batch not done yet
   int* grp_done;     // [C] batch finished (its beams stop advancing)
-  int* steps_run;    // [C] advance() calls made on the chunk's beam
+  int* steps_run;    // [C] advance() calls made on the chunk's beam (--fast: the step count when it was dropped)
+  int* hyp_anc;      // [C, n_best, S] decoder row that ran each step of the hypothesis (its attention rows)
+  // classic Beam: GNMTGlobalScorer state (onmt/translate/beam.py:181-243) and n-gram blocking (:100-119)
+  float* cov[2];     // [C*beam, T] coverage = sum of the hypothesis' attention rows, double buffered
+  float* pen;        // [C*beam] cov_penalty(coverage) of the live beams (score(), sort_finished)
+  float* prev_pen;   // [C*beam] global_state["prev_penalty"] (stepwise penalty)
+  int* blk[2];       // [C*beam] the hypothesis repeats an n-gram, double buffered
+  const float* attn; // [C*beam][S][T] head-0 context attention probabilities, null when not captured
+  const int* cut;    // [C] attention length of the chunk's beams (memory_lengths[j], translator.py:902-907)
+  int T;             // attention row stride
+};
+// classic Beam options (translate/translator.py:113-173, onmt/translate/beam.py, penalties.py)
+struct ClassicOpts {
+  int lp_kind;     // length penalty: 0 none, 1 wu, 2 avg
+  float alpha;
+  float beta;
+  int cov_kind;    // coverage penalty: 0 none, 1 wu, 2 summary
+  int stepwise;    // -stepwise_penalty
+  int ngram;       // -block_ngram_repeat (0: off)
+  unsigned excl;   // -ignore_when_blocking token ids as a bit mask
 };
 hipError_t launch_beam_init(const BeamState& st, int C, int beam, int n_best, int S, int bos, hipStream_t s);
 hipError_t launch_beam_step(const NextEmbed& ne, const float* x, const float* ln_g, const float* ln_b, const float* gw, const float* gb,
@@ -175,9 +194,16 @@ hipError_t launch_beam_finish(const BeamState& st, int C, int n_best, int S, int
 hipError_t launch_beam_classic_init(const BeamState& st, const int* group, int C, int beam, int bos, hipStream_t s);
 hipError_t launch_beam_classic_step(const NextEmbed& ne, const float* x, const float* ln_g, const float* ln_b,
                                     const float* gw, const float* gb, int V, const BeamState& st, int C, int beam,
-                                    int n_best, int step, int S, int min_len, int eos, int length_penalty, float alpha,
+                                    int n_best, int step, int S, int min_len, int eos, const ClassicOpts& o,
                                     hipStream_t s);
-hipError_t launch_beam_classic_finish(const BeamState& st, int C, int beam, int n_best, int S, int length_penalty,
-                                      float alpha, int* tokens, float* scores, int* lens, hipStream_t s);
+hipError_t launch_beam_classic_finish(const BeamState& st, int C, int beam, int n_best, int S, const ClassicOpts& o,
+                                      int* tokens, float* scores, int* lens, hipStream_t s);
+// per-step softmax of the captured head-0 scores of R rows (row r belongs to
+// chunk r / rpc; keys t < span), in place at a[r * ld + t], zero for t >= span
+hipError_t launch_attn_step_softmax(float* a, size_t ld, const int* span, int R, int rpc, int T, hipStream_t s);
+// attention of each hypothesis along its ancestry: out[c][k][t][:] =
+// attn[hyp_anc[c][k][t]][t][:] for t < hyp_len[c][k], zero after
+hipError_t launch_beam_attn_gather(const BeamState& st, int C, int n_best, int S, int max_len, int T, float* out,
+                                   hipStream_t s);
 
 }  // namespace nd

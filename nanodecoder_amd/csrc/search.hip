@@ -143,6 +143,7 @@ beam_init_kernel(BeamState st, int C, int beam, int bos) {
   st.done[c] = 0;
   st.top_fin[c] = 0;
   st.n_hyp[c] = 0;
+  st.steps_run[c] = 0;
   if (c == 0) *st.n_alive = C;
 }
 
@@ -251,19 +252,24 @@ beam_step_kernel(NextEmbed ne, const float* __restrict__ x, const float* __restr
           for (int q = last; q > pos; --q) {
             st.hyp_score[c * n_best + q] = st.hyp_score[c * n_best + q - 1];
             st.hyp_len[c * n_best + q] = st.hyp_len[c * n_best + q - 1];
-            for (int t = 0; t < S; ++t)
+            for (int t = 0; t < S; ++t) {
               st.hyp_tok[((size_t)c * n_best + q) * S + t] = st.hyp_tok[((size_t)c * n_best + q - 1) * S + t];
+              st.hyp_anc[((size_t)c * n_best + q) * S + t] = st.hyp_anc[((size_t)c * n_best + q - 1) * S + t];
+            }
           }
           st.hyp_score[c * n_best + pos] = sc;
           st.hyp_len[c * n_best + pos] = step + 1;
-          for (int t = 0; t <= step; ++t)
+          for (int t = 0; t <= step; ++t) {
             st.hyp_tok[((size_t)c * n_best + pos) * S + t] = st.seq[nxt][(size_t)(row0 + j) * S + t];
+            st.hyp_anc[((size_t)c * n_best + pos) * S + t] = st.anc[nxt][(size_t)(row0 + j) * S + t];
+          }
         }
         ++nh;
       }
       st.n_hyp[c] = nh;
       if (st.top_fin[c] && nh >= n_best) {  // :780
         st.done[c] = 1;
+        st.steps_run[c] = step + 1;  // dropped after this step (the alive set the attention cut reads)
         if (atomicSub(st.n_alive, 1) == 1) *st.steps_done = step + 1;
       }
     }
@@ -304,9 +310,10 @@ hipError_t launch_beam_finish(const BeamState& st, int C, int n_best, int S, int
 // onmt/translate/beam.py:6-178 driven by translate/translator.py:827-926:
 // scores start at 0 for every beam, step 0 expands beam 0 only, EOS beams get
 // -1e20 rows (no children), every EOS is a finished hypothesis scored by the
-// GNMT global scorer (length penalty none / wu / avg, coverage none), and a
-// reference batch advances all its beams until each is done
-// (eos_top && finished >= n_best).  Finished lists keep the n_best best
+// GNMT global scorer (length penalty none / wu / avg, coverage penalty none /
+// wu / summary, at scoring time or stepwise), n-gram repeats block a beam
+// (-10e20 rows), and a reference batch advances all its beams until each is
+// done (eos_top && finished >= n_best).  Finished lists keep the n_best best
 // entries in stable order, which is what sort_finished's stable sort reads.
 
 // global scorer divisor for len(next_ys) = n_ys (penalties.py:57-78); the
@@ -317,8 +324,24 @@ __device__ __forceinline__ float classic_lp_div(int kind, int n_ys, float alpha)
   return 1.0f;
 }
 
-// stable insertion of (sc, tokens src[0..len)) into chunk c's best-first list
-__device__ void classic_insert(const BeamState& st, int c, int n_best, int S, float sc, int len, const int* src) {
+// cov_penalty(coverage [+ add]) of one beam over its first `cut` keys, one
+// wave (penalties.py:34-53): wu = beta * -sum log(min(c, 1)),
+// summary = beta * (sum max(c, 1) - cut)
+__device__ float classic_cov_pen(const float* __restrict__ cov, const float* __restrict__ add, int cut, int kind,
+                                 float beta, int lane) {
+  float acc = 0.f;
+  for (int t = lane; t < cut; t += 64) {
+    float v = cov ? cov[t] : 0.f;
+    if (add) v = cov ? v + add[t] : add[t];
+    acc += kind == 1 ? logf(fminf(v, 1.f)) : fmaxf(v, 1.f);
+  }
+  acc = wave_sum(acc);
+  return kind == 1 ? beta * -acc : beta * (acc - (float)cut);
+}
+
+// stable insertion of (sc, tokens src[0..len), rows anc[0..len)) into chunk c's best-first list
+__device__ void classic_insert(const BeamState& st, int c, int n_best, int S, float sc, int len, const int* src,
+                               const int* anc) {
   const int nh = st.n_hyp[c];
   const int kept = min(nh, n_best);
   int pos = 0;
@@ -328,14 +351,33 @@ __device__ void classic_insert(const BeamState& st, int c, int n_best, int S, fl
     for (int q = last; q > pos; --q) {
       st.hyp_score[c * n_best + q] = st.hyp_score[c * n_best + q - 1];
       st.hyp_len[c * n_best + q] = st.hyp_len[c * n_best + q - 1];
-      for (int t = 0; t < S; ++t)
+      for (int t = 0; t < S; ++t) {
         st.hyp_tok[((size_t)c * n_best + q) * S + t] = st.hyp_tok[((size_t)c * n_best + q - 1) * S + t];
+        st.hyp_anc[((size_t)c * n_best + q) * S + t] = st.hyp_anc[((size_t)c * n_best + q - 1) * S + t];
+      }
     }
     st.hyp_score[c * n_best + pos] = sc;
     st.hyp_len[c * n_best + pos] = len;
-    for (int t = 0; t < len; ++t) st.hyp_tok[((size_t)c * n_best + pos) * S + t] = src[t];
+    for (int t = 0; t < len; ++t) {
+      st.hyp_tok[((size_t)c * n_best + pos) * S + t] = src[t];
+      st.hyp_anc[((size_t)c * n_best + pos) * S + t] = anc[t];
+    }
   }
   st.n_hyp[c] = nh + 1;
+}
+
+// GNMTGlobalScorer.score(beam, beam.scores)[i] (beam.py:200-212).  With
+// length penalty none, length_none hands back beam.scores itself and the
+// in-place `normalized_probs -= penalty` lowers every live score: each call
+// (one per finished beam, one per sort_finished top-up) moves them all.
+__device__ float classic_score(const BeamState& st, int row0, int beam, int i, const ClassicOpts& o, float div) {
+  const bool cov = o.cov_kind != 0 && !o.stepwise;
+  if (cov && o.lp_kind == 0) {
+    for (int j = 0; j < beam; ++j) st.cum[row0 + j] -= st.pen[row0 + j];
+    return st.cum[row0 + i];
+  }
+  const float v = st.cum[row0 + i] / div;
+  return cov ? v - st.pen[row0 + i] : v;
 }
 
 __global__ void __launch_bounds__(64)
@@ -370,7 +412,7 @@ __global__ void __launch_bounds__(256)
 beam_classic_step_kernel(NextEmbed ne, const float* __restrict__ x, const float* __restrict__ ln_g,
                          const float* __restrict__ ln_b, const float* __restrict__ gw, const float* __restrict__ gb,
                          int V, BeamState st, int beam, int n_best, int step, int S, int min_len, int eos,
-                         int lp_kind, float alpha) {
+                         ClassicOpts o) {
   __shared__ float lp[BEAM_MAX][ND_MAXV];
   __shared__ float tsc[BEAM_MAX];
   __shared__ int tid_sel[BEAM_MAX];
@@ -380,7 +422,17 @@ beam_classic_step_kernel(NextEmbed ne, const float* __restrict__ x, const float*
   if (st.grp_done[g]) return;  // translator.py:884-885: the whole batch is done
   const int cur = step & 1, nxt = cur ^ 1;
   const int row0 = c * beam;
+  const bool cov_on = o.cov_kind != 0 && st.attn;
+  const int cut = cov_on ? min(st.cut[c], st.T) : 0;
+  const size_t aS = (size_t)S * st.T;  // attention row stride per decoder row
   for (int j = w; j < beam; j += 4) {
+    // stepwise penalty: GNMTGlobalScorer.update_score (beam.py:80-81, :214-223)
+    if (o.stepwise && cov_on && step > 0) {
+      const float pen = classic_cov_pen(st.cov[cur] + (size_t)(row0 + j) * st.T,
+                                        st.attn + (row0 + j) * aS + (size_t)step * st.T, cut, o.cov_kind, o.beta,
+                                        lane);
+      if (lane == 0) st.cum[row0 + j] = (st.cum[row0 + j] + st.prev_pen[row0 + j]) - pen;
+    }
     head_row(x, row0 + j, ln_g, ln_b, gw, gb, V, lane, lp[j]);
     if (lane == 0) {
       if (step + 1 < min_len) lp[j][eos] = -1e20f;  // beam.py:88-91 (cur_len = step + 1)
@@ -388,6 +440,8 @@ beam_classic_step_kernel(NextEmbed ne, const float* __restrict__ x, const float*
         const float cj = st.cum[row0 + j];
         const bool dead = st.tok[row0 + j] == eos;  // EOS has no children
         for (int k = 0; k < V; ++k) lp[j][k] = dead ? -1e20f : lp[j][k] + cj;
+        if (o.ngram > 0 && st.blk[cur][row0 + j])   // :101-119 (-10e20)
+          for (int k = 0; k < V; ++k) lp[j][k] = -10e20f;
       }
     }
   }
@@ -409,9 +463,9 @@ beam_classic_step_kernel(NextEmbed ne, const float* __restrict__ x, const float*
           }
         }
       }
-      for (int o = 32; o > 0; o >>= 1) {
-        const float ov = __shfl_xor(bv, o, 64);
-        const int oi = __shfl_xor(bi, o, 64);
+      for (int off = 32; off > 0; off >>= 1) {
+        const float ov = __shfl_xor(bv, off, 64);
+        const int oi = __shfl_xor(bi, off, 64);
         if (ov > bv || (ov == bv && oi < bi)) {
           bv = ov;
           bi = oi;
@@ -447,10 +501,54 @@ beam_classic_step_kernel(NextEmbed ne, const float* __restrict__ x, const float*
   if (step + 1 < S)
     for (int j = w; j < beam; j += 4) embed_row(ne, tid_sel[j] % V, step + 1, row0 + j, lane);
   __syncthreads();
+  for (int j = w; j < beam; j += 4) {
+    const int par = tid_sel[j] / V, src = row0 + par, dst = row0 + j;
+    // update_global_state (beam.py:132, :225-243): coverage of the new beam =
+    // the parent's coverage + the parent's attention of this step
+    if (cov_on) {
+      const float* a = st.attn + src * aS + (size_t)step * st.T;
+      const float* cp = st.cov[cur] + (size_t)src * st.T;
+      float* cn = st.cov[nxt] + (size_t)dst * st.T;
+      float acc = 0.f;
+      for (int t = lane; t < cut; t += 64) {
+        const float v = step == 0 ? a[t] : cp[t] + a[t];
+        cn[t] = v;
+        acc += o.cov_kind == 1 ? logf(fminf(v, 1.f)) : fmaxf(v, 1.f);
+      }
+      acc = wave_sum(acc);
+      const float pen = o.cov_kind == 1 ? o.beta * -acc : o.beta * (acc - (float)cut);
+      if (lane == 0) {
+        st.pen[dst] = pen;
+        st.prev_pen[dst] = step == 0 ? 0.f : pen;
+      }
+    }
+    // n-gram blocking state of the new hypothesis (its step + 1 tokens): the
+    // parent's, or its last n-gram (free of excluded tokens) seen earlier in it
+    if (o.ngram > 0) {
+      const int* h = st.seq[nxt] + (size_t)dst * S;
+      const int n = o.ngram, L = step + 1;
+      bool rep = false;
+      if (L >= n) {
+        bool excl = false;
+        for (int k = 0; k < n; ++k) excl |= ((o.excl >> h[L - n + k]) & 1u) != 0;
+        if (!excl)
+          for (int e = n - 1 + lane; e < L - 1; e += 64) {
+            bool same = true;
+            for (int k = 0; k < n; ++k) same &= h[e - n + 1 + k] == h[L - n + k];
+            rep |= same;
+          }
+      }
+      rep = __any(rep);
+      if (lane == 0) st.blk[nxt][dst] = (step > 0 && st.blk[cur][src]) || rep;
+    }
+  }
+  __syncthreads();
   if (tid == 0) {
-    const float div = classic_lp_div(lp_kind, step + 2, alpha);  // len(next_ys) after the append
-    for (int j = 0; j < beam; ++j)                                 // :135-139
-      if (fin[j]) classic_insert(st, c, n_best, S, tsc[j] / div, step + 1, st.seq[nxt] + (size_t)(row0 + j) * S);
+    const float div = classic_lp_div(o.lp_kind, step + 2, o.alpha);  // len(next_ys) after the append
+    for (int j = 0; j < beam; ++j)                                   // :135-139
+      if (fin[j])
+        classic_insert(st, c, n_best, S, classic_score(st, row0, beam, j, o, div), step + 1,
+                       st.seq[nxt] + (size_t)(row0 + j) * S, st.anc[nxt] + (size_t)(row0 + j) * S);
     if (fin[0]) st.top_fin[c] = 1;  // eos_top (:142-144)
     st.steps_run[c] = step + 1;
     if (!st.done[c] && st.top_fin[c] && st.n_hyp[c] >= n_best) {  // done() (:146-147)
@@ -465,12 +563,14 @@ beam_classic_step_kernel(NextEmbed ne, const float* __restrict__ x, const float*
 
 hipError_t launch_beam_classic_step(const NextEmbed& ne, const float* x, const float* ln_g, const float* ln_b,
                                     const float* gw, const float* gb, int V, const BeamState& st, int C, int beam,
-                                    int n_best, int step, int S, int min_len, int eos, int length_penalty, float alpha,
+                                    int n_best, int step, int S, int min_len, int eos, const ClassicOpts& o,
                                     hipStream_t s) {
   if (beam > BEAM_MAX || beam * V > 256 || V > ND_MAXV || V < beam || !ne.emb || !ne.x || !ne.part)
     return hipErrorInvalidValue;
+  if (o.cov_kind != 0 && (!st.attn || !st.cut || !st.cov[0] || !st.cov[1])) return hipErrorInvalidValue;
+  if (o.ngram < 0 || o.ngram > S || (o.ngram > 0 && (!st.blk[0] || !st.blk[1]))) return hipErrorInvalidValue;
   hipLaunchKernelGGL(beam_classic_step_kernel, dim3(C), dim3(256), 0, s, ne, x, ln_g, ln_b, gw, gb, V, st, beam,
-                     n_best, step, S, min_len, eos, length_penalty, alpha);
+                     n_best, step, S, min_len, eos, o);
   return hipGetLastError();
 }
 
@@ -478,14 +578,15 @@ hipError_t launch_beam_classic_step(const NextEmbed& ne, const float* x, const f
 // list up in beam order, scored at the chunk's last step; then the n_best
 // best (score, tokens) go out like the --fast path's.
 __global__ void __launch_bounds__(256)
-beam_classic_finish_kernel(BeamState st, int beam, int n_best, int S, int lp_kind, float alpha,
-                           int* __restrict__ tokens, float* __restrict__ scores, int* __restrict__ lens) {
+beam_classic_finish_kernel(BeamState st, int beam, int n_best, int S, ClassicOpts o, int* __restrict__ tokens,
+                           float* __restrict__ scores, int* __restrict__ lens) {
   const int c = blockIdx.x;
   if (threadIdx.x == 0 && st.n_hyp[c] < n_best) {
     const int t = st.steps_run[c], fb = t & 1;
-    const float div = classic_lp_div(lp_kind, t + 1, alpha);
+    const float div = classic_lp_div(o.lp_kind, t + 1, o.alpha);
     for (int i = 0; st.n_hyp[c] < n_best; ++i)
-      classic_insert(st, c, n_best, S, st.cum[c * beam + i] / div, t, st.seq[fb] + (size_t)(c * beam + i) * S);
+      classic_insert(st, c, n_best, S, classic_score(st, c * beam, beam, i, o, div), t,
+                     st.seq[fb] + (size_t)(c * beam + i) * S, st.anc[fb] + (size_t)(c * beam + i) * S);
   }
   __syncthreads();
   for (int e = threadIdx.x; e < n_best * S; e += 256) {
@@ -499,11 +600,58 @@ beam_classic_finish_kernel(BeamState st, int beam, int n_best, int S, int lp_kin
   }
 }
 
-hipError_t launch_beam_classic_finish(const BeamState& st, int C, int beam, int n_best, int S, int length_penalty,
-                                      float alpha, int* tokens, float* scores, int* lens, hipStream_t s) {
+hipError_t launch_beam_classic_finish(const BeamState& st, int C, int beam, int n_best, int S, const ClassicOpts& o,
+                                      int* tokens, float* scores, int* lens, hipStream_t s) {
   if (n_best > beam) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(beam_classic_finish_kernel, dim3(C), dim3(256), 0, s, st, beam, n_best, S, length_penalty, alpha,
-                     tokens, scores, lens);
+  hipLaunchKernelGGL(beam_classic_finish_kernel, dim3(C), dim3(256), 0, s, st, beam, n_best, S, o, tokens, scores,
+                     lens);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------- attention capture
+// -attn_debug / coverage: the last layer's head-0 context scores of one step
+// -> probabilities (multi_headed_attn.py:175), one wave per decoder row
+__global__ void __launch_bounds__(256)
+attn_step_softmax_kernel(float* __restrict__ a, size_t ld, const int* __restrict__ span, int R, int rpc, int T) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= R) return;
+  const int L = min(span[r / rpc], T);
+  float* p = a + (size_t)r * ld;
+  float mx = -INFINITY;
+  for (int t = lane; t < L; t += 64) mx = fmaxf(mx, p[t]);
+  mx = wave_max(mx);
+  float sum = 0.f;
+  for (int t = lane; t < L; t += 64) sum += __expf(p[t] - mx);
+  sum = wave_sum(sum);
+  for (int t = lane; t < T; t += 64) p[t] = t < L ? __expf(p[t] - mx) / sum : 0.f;
+}
+
+hipError_t launch_attn_step_softmax(float* a, size_t ld, const int* span, int R, int rpc, int T, hipStream_t s) {
+  if (R < 1 || rpc < 1 || T < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(attn_step_softmax_kernel, dim3((R + 3) / 4), dim3(256), 0, s, a, ld, span, R, rpc, T);
+  return hipGetLastError();
+}
+
+// one workgroup per (chunk, hypothesis); a wave per step row
+__global__ void __launch_bounds__(256)
+beam_attn_gather_kernel(BeamState st, int n_best, int S, int max_len, int T, float* __restrict__ out) {
+  const int ck = blockIdx.x, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int len = st.hyp_len[ck];
+  for (int t = w; t < max_len; t += 4) {
+    float* o = out + ((size_t)ck * max_len + t) * T;
+    if (t < len) {
+      const float* a = st.attn + ((size_t)st.hyp_anc[(size_t)ck * S + t] * S + t) * st.T;
+      for (int x = lane; x < T; x += 64) o[x] = a[x];
+    } else {
+      for (int x = lane; x < T; x += 64) o[x] = 0.f;
+    }
+  }
+}
+
+hipError_t launch_beam_attn_gather(const BeamState& st, int C, int n_best, int S, int max_len, int T, float* out,
+                                   hipStream_t s) {
+  if (!st.attn || T > st.T || max_len > S) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(beam_attn_gather_kernel, dim3(C * n_best), dim3(256), 0, s, st, n_best, S, max_len, T, out);
   return hipGetLastError();
 }
 

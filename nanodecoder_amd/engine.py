@@ -127,40 +127,66 @@ class Engine:
         return dict(tokens=tok, scores=sc, logp=lp, attn=None)
 
     def translate_beam(self, signal, lengths, spans=None, beam: int = 5, n_best: int = 1, alpha: float = 0.0,
-                       max_len: Optional[int] = None, min_len: int = 0):
+                       max_len: Optional[int] = None, min_len: int = 0, return_attn: bool = False):
         """--fast beam search.  Returns dict(tokens [B,n_best,S] i32 (-1 pad),
-        scores [B,n_best] f32, lens [B,n_best] i32, steps [1] i32)."""
+        scores [B,n_best] f32, lens [B,n_best] i32, steps [1] i32); with
+        ``return_attn`` also attn [B,n_best,S,T] f32 (the hypotheses'
+        attention rows) and done_step [B] i32 (steps each chunk ran)."""
         signal, lengths, spans, B, T = self._inputs(signal, lengths, spans)
         S = self.max_steps if max_len is None else max_len
         tok = torch.empty(B, n_best, S, dtype=torch.int32, device=self.device)
         sc = torch.empty(B, n_best, dtype=torch.float32, device=self.device)
         ln = torch.empty(B, n_best, dtype=torch.int32, device=self.device)
         st = torch.empty(1, dtype=torch.int32, device=self.device)
-        _lib.check(self._L.nd_translate_beam(self._h, _ptr(signal), _ptr(lengths), _ptr(spans), B, T, beam, n_best,
-                                             float(alpha), S, min_len, _ptr(tok), _ptr(sc), _ptr(ln), _ptr(st),
-                                             self._stream()), "nd_translate_beam")
-        return dict(tokens=tok, scores=sc, lens=ln, steps=st)
+        if not return_attn:
+            _lib.check(self._L.nd_translate_beam(self._h, _ptr(signal), _ptr(lengths), _ptr(spans), B, T, beam,
+                                                 n_best, float(alpha), S, min_len, _ptr(tok), _ptr(sc), _ptr(ln),
+                                                 _ptr(st), self._stream()), "nd_translate_beam")
+            return dict(tokens=tok, scores=sc, lens=ln, steps=st)
+        att = torch.empty(B, n_best, S, T, dtype=torch.float32, device=self.device)
+        done = torch.empty(B, dtype=torch.int32, device=self.device)
+        _lib.check(self._L.nd_translate_beam_attn(self._h, _ptr(signal), _ptr(lengths), _ptr(spans), B, T, beam,
+                                                  n_best, float(alpha), S, min_len, _ptr(tok), _ptr(sc), _ptr(ln),
+                                                  _ptr(st), _ptr(att), _ptr(done), self._stream()),
+                   "nd_translate_beam_attn")
+        return dict(tokens=tok, scores=sc, lens=ln, steps=st, attn=att, done_step=done)
 
     def translate_beam_classic(self, signal, lengths, spans=None, groups=None, beam: int = 5, n_best: int = 1,
                                length_penalty: str = "none", alpha: float = 0.0, max_len: Optional[int] = None,
-                               min_len: int = 0):
+                               min_len: int = 0, coverage_penalty: str = "none", beta: float = 0.0,
+                               stepwise_penalty: bool = False, block_ngram_repeat: int = 0,
+                               ignore_ids: Sequence[int] = (), cut=None, return_attn: bool = False):
         """Classic onmt Beam search (no --fast).  groups [B]: the reference
-        batch of every chunk (default: one batch).  Returns dict like
-        translate_beam."""
+        batch of every chunk (default: one batch).  cut [B]: each chunk's
+        attention length (memory_lengths[j] as the reference indexes it;
+        needed with a coverage penalty).  Returns dict like translate_beam,
+        with attn [B,n_best,S,T] when ``return_attn``."""
         signal, lengths, spans, B, T = self._inputs(signal, lengths, spans)
         S = self.max_steps if max_len is None else max_len
         g = torch.zeros(B, dtype=torch.int32) if groups is None else torch.as_tensor(groups)
         g = g.to(self.device, torch.int32).contiguous()
-        lpk = {"none": 0, "wu": 1, "avg": 2}[length_penalty]
+        opts = _lib.NdClassicOpts(
+            length_penalty={"none": 0, "wu": 1, "avg": 2}[length_penalty], alpha=float(alpha), beta=float(beta),
+            coverage_penalty={"none": 0, "wu": 1, "summary": 2}[coverage_penalty],
+            stepwise_penalty=int(bool(stepwise_penalty)), block_ngram_repeat=int(block_ngram_repeat),
+            ignore_mask=sum(1 << int(t) for t in set(ignore_ids)))
+        cu = None
+        if cut is not None:
+            cu = torch.as_tensor(np.asarray(cut, np.int32)).to(self.device).contiguous()
         tok = torch.empty(B, n_best, S, dtype=torch.int32, device=self.device)
         sc = torch.empty(B, n_best, dtype=torch.float32, device=self.device)
         ln = torch.empty(B, n_best, dtype=torch.int32, device=self.device)
         st = torch.empty(1, dtype=torch.int32, device=self.device)
-        _lib.check(self._L.nd_translate_beam_classic(self._h, _ptr(signal), _ptr(lengths), _ptr(spans), _ptr(g), B,
-                                                     T, beam, n_best, lpk, float(alpha), S, min_len, _ptr(tok),
-                                                     _ptr(sc), _ptr(ln), _ptr(st), self._stream()),
-                   "nd_translate_beam_classic")
-        return dict(tokens=tok, scores=sc, lens=ln, steps=st)
+        att = torch.empty(B, n_best, S, T, dtype=torch.float32, device=self.device) if return_attn else None
+        _lib.check(self._L.nd_translate_beam_classic_ex(self._h, _ptr(signal), _ptr(lengths), _ptr(spans), _ptr(g),
+                                                        _ptr(cu) if cu is not None else None, B, T, beam, n_best,
+                                                        ctypes.byref(opts), S, min_len, _ptr(tok), _ptr(sc), _ptr(ln),
+                                                        _ptr(st), _ptr(att) if att is not None else None,
+                                                        self._stream()), "nd_translate_beam_classic_ex")
+        out = dict(tokens=tok, scores=sc, lens=ln, steps=st)
+        if return_attn:
+            out["attn"] = att
+        return out
 
     def encode(self, signal, lengths, spans=None):
         """Memory bank [B, T, d] of the encoder (rows >= span unspecified)."""

@@ -23,6 +23,7 @@ per-chunk results, far higher throughput than one read at a time).
 """
 from __future__ import annotations
 
+import json
 import os
 from typing import List, Optional, Sequence
 
@@ -95,7 +96,12 @@ class Translator(object):
         self.random_sampling_temp = float(getattr(opt, "random_sampling_temp", 1.0))
         self.sample_from_topk = int(getattr(opt, "random_sampling_topk", 1))
         self.block_ngram_repeat = int(getattr(opt, "block_ngram_repeat", 0))
+        self.ignore_when_blocking = set(getattr(opt, "ignore_when_blocking", None) or [])
         self.dump_beam = getattr(opt, "dump_beam", "")
+        # translator.py:166-173: the beam trace accumulator -dump_beam writes
+        self.beam_trace = self.dump_beam != ""
+        self.beam_accum = ({"predicted_ids": [], "beam_parent_ids": [], "scores": [], "log_probs": []}
+                           if self.beam_trace else None)
         self.replace_unk = bool(getattr(opt, "replace_unk", False))
         self.verbose = bool(getattr(opt, "verbose", False))
         self.fast = bool(getattr(opt, "fast", False))
@@ -123,16 +129,14 @@ class Translator(object):
             if self.block_ngram_repeat != 0:
                 raise AssertionError("block_ngram_repeat is not supported (translator.py:430)")
         elif not self.fast:
-            # the classic onmt Beam (translator.py:827-926, onmt/translate/beam.py)
-            if self.dump_beam:
-                raise NotImplementedError("-dump_beam (beam trace JSON) is not produced on the MI355X path")
-            if self.block_ngram_repeat != 0:
-                raise NotImplementedError("-block_ngram_repeat is not supported on the MI355X path")
-            if self.stepwise_penalty or (self.global_scorer.coverage_penalty != "none"
-                                         and self.global_scorer.beta != 0):
-                raise NotImplementedError("coverage penalties need attention sums, not produced on the MI355X path")
+            # the classic onmt Beam (translator.py:827-926, onmt/translate/beam.py): length and
+            # coverage penalties (stepwise or at scoring time), n-gram blocking, -dump_beam
             if self.global_scorer.length_penalty not in ("none", "wu", "avg"):
                 raise ValueError(f"unknown length_penalty {self.global_scorer.length_penalty!r}")
+            if self.global_scorer.coverage_penalty not in ("none", "wu", "summary"):
+                raise ValueError(f"unknown coverage_penalty {self.global_scorer.coverage_penalty!r}")
+            if self.block_ngram_repeat < 0 or self.block_ngram_repeat > self.max_length:
+                raise ValueError("block_ngram_repeat must be in [0, max_length]")
             if self.n_best > self.beam_size:
                 raise ValueError("n_best must be <= beam_size")
         else:
@@ -157,7 +161,8 @@ class Translator(object):
         """Run the engine on up to max_batch chunks with their reference
         spans (and, for the classic Beam, their reference batch ids).
         Returns per chunk (scores[n_best], token lists[n_best]) and, with
-        ``attn`` (greedy), the per-step attention rows [steps, chunk length]."""
+        ``attn``, the attention rows of each hypothesis ([steps, cut] arrays,
+        cut as the reference's results["attention"] has it)."""
         n = len(chunks)
         lens = np.array([len(c) for c in chunks], np.int32)
         if (lens < 1).any():
@@ -185,31 +190,65 @@ class Translator(object):
             sc = r["scores"].cpu().numpy()
             for i in range(n):
                 if attn:  # results["attention"]: rows cut at the chunk's length (translator.py:491-501)
-                    out.append(([float(sc[i])], [tok[i].tolist()], at[i, :, : lens[i]]))
+                    out.append(([float(sc[i])], [tok[i].tolist()], [at[i, :, : lens[i]]]))
                 else:
                     out.append(([float(sc[i])], [tok[i].tolist()]))
         else:
+            # reference batches: the chunks of one group, sorted by length
+            # descending (stable) as the reference's batch rows are
+            grp = np.zeros(n, np.int64) if groups is None else np.asarray(groups)
+            members = {}
+            for i in range(n):
+                members.setdefault(int(grp[i]), []).append(i)
+            sorted_rows = {gid: sorted(m, key=lambda i: -int(lens[i])) for gid, m in members.items()}
+            beam = self.beam_size
             if self.fast:
-                r = self.engine.translate_beam(sig, L, S, beam=self.beam_size, n_best=self.n_best,
+                r = self.engine.translate_beam(sig, L, S, beam=beam, n_best=self.n_best,
                                                alpha=self.global_scorer.alpha, max_len=self.max_length,
-                                               min_len=self.min_length)
+                                               min_len=self.min_length, return_attn=attn)
             else:
                 # dense reference-batch ids; the engine's padding rows are batches of their own
                 g = np.zeros(B, np.int32)
-                if groups is not None:
-                    g[:n] = np.unique(np.asarray(groups), return_inverse=True)[1]
+                g[:n] = np.unique(grp, return_inverse=True)[1]
                 base = int(g[:n].max()) + 1
                 g[n:] = np.arange(base, base + B - n)
-                r = self.engine.translate_beam_classic(sig, L, S, groups=g, beam=self.beam_size, n_best=self.n_best,
-                                                       length_penalty=self.global_scorer.length_penalty,
-                                                       alpha=self.global_scorer.alpha, max_len=self.max_length,
-                                                       min_len=self.min_length)
+                # beam j of a batch reads memory_lengths[j] of the beam-tiled lengths
+                # (translator.py:902-907): the length of the batch's row j // beam
+                cut = np.ones(B, np.int32)
+                for rows in sorted_rows.values():
+                    for pos, i in enumerate(rows):
+                        cut[i] = lens[rows[pos // beam]]
+                gs = self.global_scorer
+                exclusion = [self.cfg.itos.index(t) if t in self.cfg.itos else 0 for t in self.ignore_when_blocking]
+                r = self.engine.translate_beam_classic(
+                    sig, L, S, groups=g, beam=beam, n_best=self.n_best, length_penalty=gs.length_penalty,
+                    alpha=gs.alpha, max_len=self.max_length, min_len=self.min_length,
+                    coverage_penalty=gs.coverage_penalty, beta=gs.beta, stepwise_penalty=self.stepwise_penalty,
+                    block_ngram_repeat=self.block_ngram_repeat, ignore_ids=exclusion, cut=cut, return_attn=attn)
             tok = r["tokens"].cpu().numpy()
             sc = r["scores"].cpu().numpy()
             ln = r["lens"].cpu().numpy()
+            if attn:
+                at = r["attn"].cpu().numpy()
+                if self.fast:
+                    done = r["done_step"].cpu().numpy()
             for i in range(n):
-                out.append(([float(sc[i, k]) for k in range(self.n_best)],
-                            [tok[i, k, : ln[i, k]].tolist() for k in range(self.n_best)]))
+                o = ([float(sc[i, k]) for k in range(self.n_best)],
+                     [tok[i, k, : ln[i, k]].tolist() for k in range(self.n_best)])
+                if attn:
+                    atts = []
+                    for k in range(self.n_best):
+                        if self.fast:
+                            # translator.py:780-790: attention[:, i, j, :memory_lengths[i]] with i the
+                            # chunk's index among the batches alive at the hypothesis' last step
+                            step = int(ln[i, k]) - 1
+                            alive = [q for q in sorted_rows[int(grp[i])] if done[q] == 0 or done[q] > step]
+                            c = int(lens[alive[alive.index(i) // beam]])
+                        else:
+                            c = int(cut[i])
+                        atts.append(at[i, k, : ln[i, k], :c])
+                    o = o + (atts,)
+                out.append(o)
         return out
 
     def _tokens_to_sent(self, toks) -> List[str]:
@@ -228,8 +267,6 @@ class Translator(object):
         assert src is not None
         if batch_size is None:
             raise ValueError("batch_size must be set")
-        if attn_debug and self.beam_size != 1:
-            raise NotImplementedError("-attn_debug is produced for greedy decoding (beam_size 1) only")
         chunks = [parse_chunk(c) for c in src]
         res = self.translate_reads([chunks], batch_size=batch_size, attn_debug=attn_debug)[0]
         return res
@@ -280,7 +317,7 @@ class Translator(object):
                 scores, toks = res[0], res[1]
                 sents = [self._tokens_to_sent(t) for t in toks]
                 if attn_debug:
-                    self._write_attn(res[3], sents[0], res[2])
+                    self._write_attn(res[3], sents[0], res[2][0])
                 all_scores.append(scores[: self.n_best])
                 all_predictions.append([" ".join(s) for s in sents[: self.n_best]])
                 pred_score_total += scores[0]
@@ -298,6 +335,13 @@ class Translator(object):
                     else:
                         os.write(1, msg.encode("utf-8"))
             ret.append((all_scores, all_predictions))
+        if self.dump_beam:
+            # translator.py:365-368 dumps the beam trace accumulator.  (The
+            # reference reads it through a `self.translator` attribute the
+            # Translator does not have, and nothing in it appends to the
+            # lists: the intended file is these four empty lists.)
+            with open(self.dump_beam, "w", encoding="utf-8") as f:
+                json.dump(self.beam_accum, f)
         if self.report_score and pred_words_total:
             msg = "PRED AVG SCORE: %.4f, PRED PPL: %.4f" % (pred_score_total / pred_words_total,
                                                            np.exp(-pred_score_total / pred_words_total))
@@ -318,11 +362,13 @@ class Translator(object):
         try:
             if self.beam_size > 1:
                 self._check_supported()
-            want = bool(attn_debug or self.replace_unk) and self.beam_size == 1  # return_attention (:521-529)
+            # return_attention (:521-529); the classic Beam always keeps its attention (:902-924)
+            want = bool(attn_debug or self.replace_unk) or (self.beam_size > 1 and not self.fast)
             outs = self._run(chunks, [T] * B, attn=want)
         finally:
             self.fast = saved
-        att = [[torch.from_numpy(np.ascontiguousarray(o[2]))] if want else [[]] * len(o[0]) for o in outs]
+        att = [[torch.from_numpy(np.ascontiguousarray(a)) for a in o[2]] if want else [[]] * len(o[0])
+               for o in outs]
         return {"predictions": [[torch.tensor(t, dtype=torch.long) for t in o[1]] for o in outs],
                 "scores": [list(o[0]) for o in outs], "attention": att,
                 "gold_score": [0] * B, "batch": batch}

@@ -341,6 +341,65 @@ def test_classic_beam_vs_golden(name, which):
     assert np.abs(sc - z[which + "_scores"]).max() < 1e-3
 
 
+@pytest.mark.parametrize("name,which,fast", [("transformer_beam_attn", "beam", True),
+                                             ("transformer_beam_attn", "classic", False),
+                                             ("transformer_classic_ext", "classic", False),
+                                             ("transformer_classic_ext", "classic2", False),
+                                             ("transformer_classic_cov", "classic", False),
+                                             ("transformer_classic_cov", "classic2", False),
+                                             ("transformer_classic_cov", "classic3", False)])
+def test_beam_options_vs_golden(name, which, fast):
+    """Through the Translator (translate_batch on the reference batch layout):
+    -attn_debug with --fast and classic beam search (each hypothesis' head-0
+    attention rows, cut at memory_lengths[i] as the reference indexes it),
+    the classic Beam's n-gram blocking (with exclusion tokens) and coverage
+    penalties (wu / summary, stepwise or at scoring time, the scorer's
+    in-place update of beam.scores) against the reference's own runs.
+    Tolerances: scores 1e-3 absolute + 1e-5 relative (coverage sums run over
+    512 keys in another order), attention 1e-5.  A chunk whose every beam is
+    blocked (all candidates -10e20) is compared on its score only: the
+    reference's choice among equal candidates is torch's CPU topk order."""
+    import types
+    import torch
+    from nanodecoder_amd.translator import Translator
+    z, meta = gu.load(name)
+    cfg, W = gu.model_for(meta)
+    kw = meta[which]
+    eng = _engine(cfg, W, max_batch=8, max_steps=kw["max_length"], max_beam=kw["beam_size"])
+    opt = types.SimpleNamespace(
+        gpu=0, n_best=kw["n_best"], max_length=kw["max_length"], min_length=kw.get("min_length", 0),
+        beam_size=kw["beam_size"], fast=fast, alpha=kw.get("alpha", 0.0), beta=kw.get("beta", 0.0),
+        length_penalty=kw.get("length_penalty", "none"), coverage_penalty=kw.get("coverage_penalty", "none"),
+        stepwise_penalty=kw.get("stepwise_penalty", False), block_ngram_repeat=kw.get("block_ngram_repeat", 0),
+        ignore_when_blocking=kw.get("ignore_when_blocking", []), batch_size=8)
+    tr = Translator(cfg, None, opt, engine=eng)
+    chunks = gu.chunks_of(z)
+    T = max(len(c) for c in chunks)
+    src = torch.zeros(T, len(chunks), 1)
+    for i, c in enumerate(chunks):
+        src[: len(c), i, 0] = torch.from_numpy(c)
+    batch = types.SimpleNamespace(src=src, src_lengths=torch.tensor([len(c) for c in chunks]),
+                                  batch_size=len(chunks))
+    att_on = bool(kw.get("attention", False))
+    res = tr.translate_batch(batch, None, att_on, fast=fast)
+    p = which + "_"
+    for i in range(len(chunks)):
+        for nb in range(kw["n_best"]):
+            exp_s = float(z[p + "scores"][i, nb])
+            got_s = float(res["scores"][i][nb])
+            assert abs(got_s - exp_s) <= 1e-3 + 1e-5 * abs(exp_s), (i, nb, got_s, exp_s)
+            if exp_s <= -1e20:
+                continue
+            L = int(z[p + "lens"][i, nb])
+            got = res["predictions"][i][nb].numpy()
+            assert len(got) == L and (got == z[p + "tokens"][i, nb, :L]).all(), (i, nb)
+            if att_on:
+                a = res["attention"][i][nb].numpy()
+                cut = int(z[p + "attn_cut"][i, nb])
+                assert a.shape == (L, cut), (i, nb, a.shape, (L, cut))
+                np.testing.assert_allclose(a, z[p + "attn"][i, nb, :L, :cut], atol=1e-5)
+
+
 def test_classic_beam_packed_batches_vs_oracle():
     """Several reference batches packed into one engine call keep their own
     stopping points: equal to the oracle run batch by batch."""

@@ -33,7 +33,8 @@ class FakeEngine:
             out["attn"] = a
         return out
 
-    def translate_beam(self, sig, L, S, beam, n_best, alpha, max_len, min_len=0):
+    def translate_beam(self, sig, L, S, beam, n_best, alpha, max_len, min_len=0, return_attn=False,
+                       done_step=None, hyp_len=4):
         self.calls.append(("beam", sig.shape, L.copy(), S.copy()))
         B = len(L)
         tok = torch.full((B, n_best, max_len), -1, dtype=torch.int32)
@@ -41,15 +42,24 @@ class FakeEngine:
         sc = torch.zeros(B, n_best)
         for i in range(B):
             for k in range(n_best):
-                t = self._tok(int(L[i]), int(S[i]) + k, 4)
-                tok[i, k, :4] = torch.tensor(t)
-                lens[i, k] = 4
+                t = self._tok(int(L[i]), int(S[i]) + k, hyp_len)
+                n = hyp_len if done_step is None or done_step[i] == 0 else int(done_step[i])
+                tok[i, k, :n] = torch.tensor(t[:n])
+                lens[i, k] = n
                 sc[i, k] = -float(k)
-        return {"tokens": tok, "scores": sc, "lens": lens, "steps": torch.tensor([4])}
+        out = {"tokens": tok, "scores": sc, "lens": lens, "steps": torch.tensor([4])}
+        if return_attn:  # entry (t, x) = 1000 * t + x, so cuts are visible
+            T = sig.shape[1]
+            a = torch.arange(max_len).view(-1, 1) * 1000.0 + torch.arange(T).view(1, -1)
+            out["attn"] = a.expand(B, n_best, max_len, T).clone()
+            out["done_step"] = torch.as_tensor(np.zeros(B, np.int32) if done_step is None else done_step)
+        return out
 
-    def translate_beam_classic(self, sig, L, S, groups, beam, n_best, length_penalty, alpha, max_len, min_len=0):
-        out = self.translate_beam(sig, L, S, beam, n_best, alpha, max_len, min_len)
+    def translate_beam_classic(self, sig, L, S, groups, beam, n_best, length_penalty, alpha, max_len, min_len=0,
+                               return_attn=False, **opts):
+        out = self.translate_beam(sig, L, S, beam, n_best, alpha, max_len, min_len, return_attn=return_attn)
         self.calls[-1] = ("classic", sig.shape, L.copy(), S.copy(), np.asarray(groups).copy(), length_penalty)
+        self.classic_opts = opts
         return out
 
 
@@ -131,8 +141,46 @@ def test_attn_debug_dump_format():
     assert [len(r.split()) for r in rows] == [5] * 6
     assert rows[1].split() == ["{:.5f}".format(0.5)] * 2 + ["{:.5f}".format(0.0)] * 3
     assert len(lines[7].split("|")[0].split()) == 1 + 3       # second chunk: 3 samples
-    with pytest.raises(NotImplementedError):
-        make_tr(beam_size=5, fast=True)[0].translate(src, batch_size=2, attn_debug=True)
+
+
+def _batch_of(src):
+    return types.SimpleNamespace(
+        src=torch.from_numpy(np.stack([np.pad(c, (0, 512 - len(c))) for c in src], 1)[:, :, None]),
+        src_lengths=torch.tensor([len(c) for c in src]), batch_size=len(src))
+
+
+def test_attn_debug_beam_cuts():
+    """-attn_debug with beam search: each hypothesis' rows (one per token, EOS
+    included), cut at memory_lengths[i] as the reference indexes its
+    beam-tiled lengths: the classic Beam at lengths[j // beam] of the sorted
+    batch; --fast by the same rule over the batches still alive at the
+    hypothesis' last step.  The dump file rows keep the source width (the
+    reference's row format has one field per source sample)."""
+    import io
+    src = chunks([150, 512, 77, 300, 100, 200])   # sorted: 512 300 200 150 100 77
+    tr, eng = make_tr(beam_size=4, fast=False, max_length=6, batch_size=6)
+    res = tr.translate_batch(_batch_of(src), None, True)
+    # sorted positions 0..5 -> cut = sorted[pos // 4]: 512 for the first four, 300 for 100 and 77
+    assert [a[0].shape for a in res["attention"]] == [(4, 512), (4, 512), (4, 300), (4, 512), (4, 300), (4, 512)]
+    assert res["attention"][0][0][1, :2].tolist() == [1000.0, 1001.0]
+    f = io.StringIO()
+    tr.setAttnFile(f)
+    tr.translate(src, batch_size=6, attn_debug=True)
+    rows = [ln for ln in f.getvalue().split("\n") if ln.strip() and not ln.lstrip().startswith(">")]
+    assert [len(r.split()) for r in rows] == [n for n in (150, 512, 77, 300, 100, 200) for _ in range(4)]
+    # --fast: the 512 chunk finishes and is dropped at step 1, so at the other
+    # hypotheses' last step (3) the alive sorted batch is 300 200 150 100 77:
+    # 77 sits at index 4 -> cut = alive[1] = 200, the others -> alive[0] = 300
+    tr, eng = make_tr(beam_size=4, fast=True, max_length=6, batch_size=6)
+    orig = eng.translate_beam
+
+    def beam_done(*a, **k):
+        k["done_step"] = np.array([0, 2, 0, 0, 0, 0] + [0] * 2, np.int32)
+        return orig(*a, **k)
+
+    eng.translate_beam = beam_done
+    res = tr.translate_batch(_batch_of(src), None, True, fast=True)
+    assert [a[0].shape for a in res["attention"]] == [(4, 300), (2, 512), (4, 200), (4, 300), (4, 300), (4, 300)]
 
 
 def test_classic_beam_reference_batches():
@@ -154,10 +202,13 @@ def test_reference_errors():
     with pytest.raises(ValueError):
         tr.translate(chunks([10]), batch_size=None)
     make_tr(beam_size=5, fast=False)  # the classic onmt Beam is on the path
-    with pytest.raises(NotImplementedError):
-        make_tr(beam_size=5, fast=False, block_ngram_repeat=2)
-    with pytest.raises(NotImplementedError):
-        make_tr(beam_size=5, fast=False, coverage_penalty="wu", beta=0.2)
+    make_tr(beam_size=5, fast=False, block_ngram_repeat=2, coverage_penalty="wu", beta=0.2)
+    with pytest.raises(ValueError):
+        make_tr(beam_size=5, fast=False, coverage_penalty="bogus", beta=0.2)
+    with pytest.raises(AssertionError):
+        make_tr(beam_size=5, fast=True, block_ngram_repeat=2)
+    with pytest.raises(AssertionError):
+        make_tr(beam_size=5, fast=True, dump_beam="x.json")
     with pytest.raises(NotImplementedError):
         make_tr(random_sampling_topk=5)
     with pytest.raises(AssertionError):
@@ -175,3 +226,20 @@ def test_translate_batch_reference_layout():
     res = tr.translate_batch(b, None, False)
     assert len(res["predictions"]) == 2 and res["predictions"][0][0].dtype == torch.long
     assert list(eng.calls[0][3][:2]) == [512, 512]
+
+
+def test_classic_options_reach_the_engine(tmp_path):
+    """Coverage / stepwise penalties, n-gram blocking with its exclusion
+    tokens (ids through the vocab), the attention cut, and -dump_beam's
+    accumulator file (translator.py:166-173, :365-368)."""
+    dump = tmp_path / "beam.json"
+    tr, eng = make_tr(beam_size=4, fast=False, coverage_penalty="summary", beta=0.3, stepwise_penalty=True,
+                      block_ngram_repeat=3, ignore_when_blocking=["A", "G"], dump_beam=str(dump))
+    tr.translate(chunks([512, 512, 512, 512, 77]), batch_size=5)
+    o = eng.classic_opts
+    assert o["coverage_penalty"] == "summary" and o["beta"] == 0.3 and o["stepwise_penalty"] is True
+    assert o["block_ngram_repeat"] == 3 and sorted(o["ignore_ids"]) == [4, 6]
+    assert list(o["cut"][:5]) == [512, 512, 512, 512, 512]
+    import json
+    assert json.loads(dump.read_text()) == {"predicted_ids": [], "beam_parent_ids": [], "scores": [],
+                                            "log_probs": []}
