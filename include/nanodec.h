@@ -102,6 +102,19 @@ int nd_translate_greedy_attn(nd_ctx* ctx, const float* d_signal, const int32_t* 
                              int32_t B, int32_t T, int32_t max_len, int32_t min_len, int32_t* d_tokens, float* d_score,
                              float* d_logp, float* d_attn, void* stream);
 
+/* Random sampling: Translator._translate_random_sampling with
+ * sample_with_temperature (translate/translator.py:371-503).  Every step
+ * draws the next token from softmax(log_probs / temp), restricted to the
+ * keep_topk most likely tokens when keep_topk > 0 (the others set to -10000);
+ * the score is the tempered (masked) value of the drawn token.  temp == 0 or
+ * keep_topk == 1 is the argmax of nd_translate_greedy.  The draws come from a
+ * counter-based generator keyed by (seed, chunk, step): equal seeds give
+ * equal outputs (the reference draws from torch's global generator).
+ * Outputs as nd_translate_greedy; d_attn nullable as nd_translate_greedy_attn. */
+int nd_translate_sample(nd_ctx* ctx, const float* d_signal, const int32_t* d_len, const int32_t* d_span, int32_t B,
+                        int32_t T, int32_t max_len, int32_t min_len, float temp, int32_t keep_topk, uint64_t seed,
+                        int32_t* d_tokens, float* d_score, float* d_logp, float* d_attn, void* stream);
+
 /* --fast beam search.  Replaces Translator._fast_translate_batch
  * (translate/translator.py:619-825) with GNMTGlobalScorer.alpha
  * (onmt/translate/beam.py:181-199; beta must be 0).  Per chunk the n_best

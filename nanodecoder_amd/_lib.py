@@ -46,6 +46,7 @@ SIGNATURES = {
     "nd_finalize": (_I, [_P]),
     "nd_translate_greedy": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P]),
     "nd_translate_greedy_attn": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
+    "nd_translate_sample": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _F, _I, ctypes.c_uint64, _P, _P, _P, _P, _P]),
     "nd_translate_beam": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _F, _I, _I, _P, _P, _P, _P, _P]),
     "nd_translate_beam_attn": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _F, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
     "nd_translate_beam_classic": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _F, _I, _I, _P, _P, _P, _P, _P]),

@@ -86,10 +86,14 @@ struct GraphKey {
   int attn = 0, cov = 0, stepwise = 0, ngram = 0;
   unsigned excl = 0;
   float beta = 0.f;
+  // random sampling (greedy path): top-k (1 = argmax) and temperature
+  int topk = 1;
+  float temp = 0.f;
   bool operator<(const GraphKey& o) const {
     return std::tie(mode, B, T, S, min_len, beam, n_best, seg, logp, alpha, stamp, attn, cov, stepwise, ngram, excl,
-                    beta) < std::tie(o.mode, o.B, o.T, o.S, o.min_len, o.beam, o.n_best, o.seg, o.logp, o.alpha,
-                                     o.stamp, o.attn, o.cov, o.stepwise, o.ngram, o.excl, o.beta);
+                    beta, topk, temp) < std::tie(o.mode, o.B, o.T, o.S, o.min_len, o.beam, o.n_best, o.seg, o.logp,
+                                                 o.alpha, o.stamp, o.attn, o.cov, o.stepwise, o.ngram, o.excl, o.beta,
+                                                 o.topk, o.temp);
   }
 };
 
@@ -141,6 +145,7 @@ struct nd_ctx {
   int* steps_done = nullptr;
   int* group_in = nullptr;  // classic Beam: staged reference-batch ids
   int* cut_in = nullptr;    // classic Beam: staged attention lengths (coverage penalties)
+  unsigned long long* seed_dev = nullptr;  // random sampling: the call's seed (read by the captured graph)
   // -attn_debug / coverage: [decoder rows][max_steps][max_src_len] head-0 context scores -> probabilities
   float* attn_raw = nullptr;
   bool attn_on = false;       // set while a call that captures the attention is enqueued
@@ -398,6 +403,7 @@ static int alloc_workspaces(nd_ctx* c) {
   c->bs.T = (int)T;
   WS(c->group_in, B);
   WS(c->cut_in, B);
+  WS(c->seed_dev, 2);
   WS(c->kstamp, Ld * S * 2);
 #undef WS
   if ((e = hipHostMalloc((void**)&c->h_alive, 16, hipHostMallocDefault)) != hipSuccess)
@@ -567,7 +573,8 @@ static hipError_t enqueue_memory(nd_ctx* c, int B, int T, int rpc, hipStream_t s
   return nd::launch_memory_pack(c->x, c->enc_ln_g, c->enc_ln_b, c->mem_p, B, T, T, s);
 }
 
-static hipError_t enqueue_greedy(nd_ctx* c, int B, int T, int S, int min_len, bool logp, hipStream_t s) {
+static hipError_t enqueue_greedy(nd_ctx* c, int B, int T, int S, int min_len, bool logp, hipStream_t s,
+                                 const nd::Sampling& smp = nd::Sampling()) {
   if (c->kstamp_on) LCHK(nd::launch_stamp_reset(c->kstamp, (int)c->dec.size() * c->cfg.max_steps, s));
   LCHK(enqueue_encode(c, B, T, s));
   LCHK(enqueue_memory(c, B, T, 1, s));
@@ -578,7 +585,7 @@ static hipError_t enqueue_greedy(nd_ctx* c, int B, int T, int S, int min_len, bo
     LCHK(enqueue_dec_step(c, B, 1, T, step, nullptr, 0, s));
     LCHK(nd::launch_dec_greedy_head(c->dx, c->dec_ln_g, c->dec_ln_b, c->gen_w, c->gen_b, c->V, step, S, min_len,
                                     c->cfg.eos_idx, c->tok, c->gtok, c->gscore, logp ? c->glogp : nullptr, ne, B,
-                                    s));
+                                    s, smp));
   }
   if (c->attn_on) LCHK(nd::launch_attn_rows_softmax(c->attn_raw, c->span, B, c->cfg.max_steps, T, s));
   return hipSuccess;
@@ -976,7 +983,8 @@ static int ensure_attn(nd_ctx* c) {
 
 static int translate_greedy(nd_ctx* c, const float* d_signal, const int32_t* d_len, const int32_t* d_span, int32_t B,
                             int32_t T, int32_t max_len, int32_t min_len, int32_t* d_tokens, float* d_score,
-                            float* d_logp, float* d_attn, void* stream) {
+                            float* d_logp, float* d_attn, void* stream, float temp = 0.f, int topk = 1,
+                            unsigned long long seed = 0) {
   int rc = check_call(c, B, T, max_len);
   if (rc) return rc;
   if (!d_signal || !d_len || !d_span || !d_tokens || !d_score) return fail(ND_ERR_ARG, "null buffer");
@@ -985,9 +993,18 @@ static int translate_greedy(nd_ctx* c, const float* d_signal, const int32_t* d_l
   if ((rc = stage_inputs(c, d_signal, d_len, d_span, B, T, cs))) return rc;
   const bool lp = d_logp != nullptr;
   GraphKey key{0, B, T, max_len, min_len, 1, 1, d_attn ? 1 : 0, lp ? 1 : 0, 0.f, c->kstamp_on ? 1 : 0};
+  nd::Sampling smp;
+  if (temp != 0.f && topk != 1) {  // sample_with_temperature's random branch (translator.py:376-393)
+    smp.temp = temp;
+    smp.topk = topk;
+    smp.seed = c->seed_dev;
+    key.topk = topk;
+    key.temp = temp;
+    HIPCHK(hipMemcpyAsync(c->seed_dev, &seed, sizeof(seed), hipMemcpyHostToDevice, c->es));
+  }
   if (c->timing) HIPCHK(hipEventRecord(c->ev_a, c->es));
   c->attn_on = d_attn != nullptr;
-  rc = run_graph(c, key, [&](hipStream_t s) { return enqueue_greedy(c, B, T, max_len, min_len, lp, s); });
+  rc = run_graph(c, key, [&](hipStream_t s) { return enqueue_greedy(c, B, T, max_len, min_len, lp, s, smp); });
   c->attn_on = false;
   if (rc) return rc;
   if (c->timing) HIPCHK(hipEventRecord(c->ev_b, c->es));
@@ -1087,6 +1104,14 @@ static int translate_beam(nd_ctx* c, const float* d_signal, const int32_t* d_len
     HIPCHK(hipEventElapsedTime(&c->t_dec, c->ev_b, c->ev_c));
   }
   return release_to(c, cs);
+}
+
+int nd_translate_sample(nd_ctx* c, const float* d_signal, const int32_t* d_len, const int32_t* d_span, int32_t B,
+                        int32_t T, int32_t max_len, int32_t min_len, float temp, int32_t keep_topk, uint64_t seed,
+                        int32_t* d_tokens, float* d_score, float* d_logp, float* d_attn, void* stream) {
+  if (keep_topk > c->V) return fail(ND_ERR_ARG, "random_sampling_topk larger than the vocabulary");
+  return translate_greedy(c, d_signal, d_len, d_span, B, T, max_len, min_len, d_tokens, d_score, d_logp, d_attn,
+                          stream, temp, keep_topk, (unsigned long long)seed);
 }
 
 int nd_translate_beam(nd_ctx* c, const float* d_signal, const int32_t* d_len, const int32_t* d_span, int32_t B,

@@ -136,13 +136,21 @@ hipError_t launch_aan_prep(const float* x, const float* ln_g, const float* ln_b,
                            hipStream_t s);
 hipError_t launch_aan_gate(const float* g, const float* xn, const float* a, const float* x, float* out, float* part,
                            int R, hipStream_t s);
-// greedy head: LN_dec -> generator -> log_softmax -> argmax; writes token
-// (next input + output [R, S] at column step), score, optional logp dump,
-// and the next step's embedded input (ne).
+// random sampling (translate/translator.py:371-394): temperature, top-k
+// (-1: the full distribution), and the draw's seed (device word, so one
+// captured graph serves every seed); temp == 0 or topk == 1 is argmax
+struct Sampling {
+  float temp = 1.f;
+  int topk = 1;
+  const unsigned long long* seed = nullptr;
+};
+// greedy head: LN_dec -> generator -> log_softmax -> argmax (or a sample);
+// writes token (next input + output [R, S] at column step), score, optional
+// logp dump, and the next step's embedded input (ne).
 hipError_t launch_dec_greedy_head(const float* x, const float* ln_g, const float* ln_b, const float* gw,
                                   const float* gb, int V, int step, int S, int min_len, int eos, int* tok,
                                   int* out_tokens, float* score, float* logp_dump, const NextEmbed& ne, int R,
-                                  hipStream_t s);
+                                  hipStream_t s, const Sampling& smp = Sampling());
 
 struct BeamState {
   float* cum;        // [C, beam] topk_log_probs

@@ -83,11 +83,60 @@ __device__ __forceinline__ void embed_row(const NextEmbed& ne, int tk, int step_
   }
 }
 
+// counter-based uniform in [0, 1) for (seed, row, step): splitmix64 finaliser
+__device__ __forceinline__ float draw_uniform(unsigned long long seed, int row, int step) {
+  unsigned long long z = seed + 0x9E3779B97F4A7C15ull * (((unsigned long long)row << 32) + (unsigned)step + 1ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (float)(z >> 40) * (1.0f / 16777216.0f);  // 24 random bits
+}
+
+// sample_with_temperature (translate/translator.py:371-394) for one row's
+// log-probs lp[0..V) (EOS already masked): l = lp / temp; with topk > 0 the
+// logits below the k-th largest become -10000 (keep * l + (1 - keep) * -10000);
+// one draw from softmax(l); the score is l at the drawn token.  Every lane
+// computes the same draw (deterministic), so no broadcast is needed.
+__device__ int sample_token(const float* lp, int V, float temp, int topk, float u, float& score) {
+  float l[ND_MAXV];
+  for (int k = 0; k < V; ++k) l[k] = lp[k] / temp;
+  if (topk > 0) {
+    // k-th largest value (torch.topk(...)[0][:, -1]); ties at it are kept (torch.ge)
+    float kth = INFINITY;
+    for (int q = 0; q < topk; ++q) {
+      float m = -INFINITY;
+      int cnt = 0;
+      for (int k = 0; k < V; ++k)
+        if (l[k] < kth) m = fmaxf(m, l[k]);
+      for (int k = 0; k < V; ++k) cnt += l[k] == m ? 1 : 0;
+      kth = m;
+      q += cnt - 1;  // a tie block counts once per member
+    }
+    for (int k = 0; k < V; ++k) l[k] = l[k] >= kth ? l[k] : -10000.0f;
+  }
+  float mx = -INFINITY;
+  for (int k = 0; k < V; ++k) mx = fmaxf(mx, l[k]);
+  float sum = 0.f;
+  for (int k = 0; k < V; ++k) sum += __expf(l[k] - mx);
+  const float target = u * sum;
+  float acc = 0.f;
+  int pick = V - 1;
+  for (int k = 0; k < V; ++k) {
+    acc += __expf(l[k] - mx);
+    if (target < acc) {
+      pick = k;
+      break;
+    }
+  }
+  score = l[pick];
+  return pick;
+}
+
 __global__ void __launch_bounds__(256)
 greedy_head_kernel(const float* __restrict__ x, const float* __restrict__ ln_g, const float* __restrict__ ln_b,
                    const float* __restrict__ gw, const float* __restrict__ gb, int V, int step, int S, int min_len,
                    int eos, int* __restrict__ tok, int* __restrict__ out_tokens, float* __restrict__ score,
-                   float* __restrict__ logp_dump, NextEmbed ne, int R) {
+                   float* __restrict__ logp_dump, NextEmbed ne, int R, Sampling smp) {
   __shared__ float lps[4][ND_MAXV];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = blockIdx.x * 4 + w;
@@ -103,12 +152,19 @@ greedy_head_kernel(const float* __restrict__ x, const float* __restrict__ ln_g, 
   // every lane runs the (tiny) argmax so the token needs no broadcast
   const bool no_eos = step < min_len;
   int best = 0;
-  float bv = (no_eos && eos == 0) ? -1e20f : lp[0];
-  for (int k = 1; k < V; ++k) {
-    const float v = (no_eos && k == eos) ? -1e20f : lp[k];
-    if (v > bv) {  // first index wins ties (topk(1))
-      bv = v;
-      best = k;
+  float bv;
+  if (smp.seed) {  // random sampling (translator.py:469-475)
+    float m[ND_MAXV];
+    for (int k = 0; k < V; ++k) m[k] = (no_eos && k == eos) ? -1e20f : lp[k];
+    best = sample_token(m, V, smp.temp, smp.topk, draw_uniform(*smp.seed, r, step), bv);
+  } else {
+    bv = (no_eos && eos == 0) ? -1e20f : lp[0];
+    for (int k = 1; k < V; ++k) {
+      const float v = (no_eos && k == eos) ? -1e20f : lp[k];
+      if (v > bv) {  // first index wins ties (topk(1))
+        bv = v;
+        best = k;
+      }
     }
   }
   if (lane == 0) {
@@ -122,10 +178,11 @@ greedy_head_kernel(const float* __restrict__ x, const float* __restrict__ ln_g, 
 hipError_t launch_dec_greedy_head(const float* x, const float* ln_g, const float* ln_b, const float* gw,
                                   const float* gb, int V, int step, int S, int min_len, int eos, int* tok,
                                   int* out_tokens, float* score, float* logp_dump, const NextEmbed& ne, int R,
-                                  hipStream_t s) {
+                                  hipStream_t s, const Sampling& smp) {
   if (V > ND_MAXV || !ne.emb || !ne.x || !ne.part) return hipErrorInvalidValue;
+  if (smp.seed && (smp.temp == 0.f || smp.topk == 1 || smp.topk > V)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(greedy_head_kernel, dim3((R + 3) / 4), dim3(256), 0, s, x, ln_g, ln_b, gw, gb, V, step, S,
-                     min_len, eos, tok, out_tokens, score, logp_dump, ne, R);
+                     min_len, eos, tok, out_tokens, score, logp_dump, ne, R, smp);
   return hipGetLastError();
 }
 

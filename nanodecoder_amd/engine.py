@@ -126,6 +126,23 @@ class Engine:
                                                _ptr(tok), _ptr(sc), _ptr(lp), self._stream()), "nd_translate_greedy")
         return dict(tokens=tok, scores=sc, logp=lp, attn=None)
 
+    def translate_sample(self, signal, lengths, spans=None, temp: float = 1.0, keep_topk: int = -1, seed: int = 0,
+                         max_len: Optional[int] = None, min_len: int = 0, return_logp: bool = False,
+                         return_attn: bool = False):
+        """Random sampling (translator.py:371-503): as translate_greedy, the
+        token of every step drawn from softmax(logp / temp) over the
+        keep_topk most likely tokens (-1: all); draws keyed by ``seed``."""
+        signal, lengths, spans, B, T = self._inputs(signal, lengths, spans)
+        S = self.max_steps if max_len is None else max_len
+        tok = torch.empty(B, S, dtype=torch.int32, device=self.device)
+        sc = torch.empty(B, dtype=torch.float32, device=self.device)
+        lp = torch.empty(B, S, self.cfg.vocab, dtype=torch.float32, device=self.device) if return_logp else None
+        at = torch.empty(B, S, T, dtype=torch.float32, device=self.device) if return_attn else None
+        _lib.check(self._L.nd_translate_sample(self._h, _ptr(signal), _ptr(lengths), _ptr(spans), B, T, S, min_len,
+                                               float(temp), int(keep_topk), int(seed) & (2 ** 64 - 1), _ptr(tok),
+                                               _ptr(sc), _ptr(lp), _ptr(at), self._stream()), "nd_translate_sample")
+        return dict(tokens=tok, scores=sc, logp=lp, attn=at)
+
     def translate_beam(self, signal, lengths, spans=None, beam: int = 5, n_best: int = 1, alpha: float = 0.0,
                        max_len: Optional[int] = None, min_len: int = 0, return_attn: bool = False):
         """--fast beam search.  Returns dict(tokens [B,n_best,S] i32 (-1 pad),

@@ -106,6 +106,11 @@ class Translator(object):
         self.verbose = bool(getattr(opt, "verbose", False))
         self.fast = bool(getattr(opt, "fast", False))
         self.stepwise_penalty = bool(getattr(opt, "stepwise_penalty", False))
+        # random sampling draws: keyed by -seed when given (>= 0), else by fresh entropy;
+        # successive calls advance like a generator
+        seed = getattr(opt, "seed", -1)
+        self._seed = int(seed) if seed is not None and int(seed) >= 0 else int.from_bytes(os.urandom(8), "little")
+        self._draws = 0
         self.global_scorer = global_scorer or GNMTGlobalScorer(opt)
         self.report_score = report_score
         self.logger = logger
@@ -123,9 +128,9 @@ class Translator(object):
 
     def _check_supported(self):
         if self.beam_size == 1:
-            # translator.py:371-394: keep_topk == 1 (or temp == 0) is argmax
-            if not (self.random_sampling_temp == 0.0 or self.sample_from_topk == 1):
-                raise NotImplementedError("random sampling (-random_sampling_topk != 1) is not supported")
+            # translator.py:371-394: keep_topk == 1 (or temp == 0) is argmax, anything else samples
+            if self.sample_from_topk > self.cfg.vocab:
+                raise ValueError("random_sampling_topk larger than the vocabulary")
             if self.block_ngram_repeat != 0:
                 raise AssertionError("block_ngram_repeat is not supported (translator.py:430)")
         elif not self.fast:
@@ -180,12 +185,18 @@ class Translator(object):
         L[:n], S[:n] = lens, spans
         out = []
         if self.beam_size == 1:
-            if attn:
-                r = self.engine.translate_greedy(sig, L, S, max_len=self.max_length, min_len=self.min_length,
-                                                 return_attn=True)
-                at = r["attn"].cpu().numpy()
+            if not (self.random_sampling_temp == 0.0 or self.sample_from_topk == 1):
+                # sample_with_temperature's random branch (translator.py:376-393)
+                self._draws += 1
+                seed = (self._seed * 0x9E3779B97F4A7C15 + self._draws) & (2 ** 64 - 1)
+                r = self.engine.translate_sample(sig, L, S, temp=self.random_sampling_temp,
+                                                 keep_topk=self.sample_from_topk, seed=seed, max_len=self.max_length,
+                                                 min_len=self.min_length, return_attn=attn)
             else:
-                r = self.engine.translate_greedy(sig, L, S, max_len=self.max_length, min_len=self.min_length)
+                r = self.engine.translate_greedy(sig, L, S, max_len=self.max_length, min_len=self.min_length,
+                                                 return_attn=attn)
+            if attn:
+                at = r["attn"].cpu().numpy()
             tok = r["tokens"].cpu().numpy()
             sc = r["scores"].cpu().numpy()
             for i in range(n):

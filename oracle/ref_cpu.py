@@ -242,6 +242,21 @@ def greedy(model: RefModel, src, lengths, max_length=100, min_length=0):
                 logp=torch.stack(lps, 1).numpy(), memory=memory.numpy(), attn=torch.stack(attns, 1).numpy())
 
 
+def sampling_logits(logp, temp, keep_topk):
+    """translate/translator.py:376-389 (sample_with_temperature's random
+    branch up to the draw): logits / temp, and with keep_topk > 0 every
+    logit below the k-th largest replaced by -10000.  The draw is
+    Multinomial(logits=...) (:391-393); the score is the returned logit of
+    the drawn token."""
+    logp = torch.as_tensor(logp, dtype=torch.float32)
+    lg = torch.div(logp, temp)
+    if keep_topk > 0:
+        kth = torch.topk(lg, keep_topk, dim=1)[0][:, -1].view(-1, 1).repeat(1, lg.shape[1])
+        keep = torch.ge(lg, kth).float()
+        lg = (keep * lg) + ((1 - keep) * -10000)
+    return lg
+
+
 def tile(x, count, dim=0):
     """onmt/utils/misc.py:28-47 (batch-major repeat_interleave)."""
     return x.repeat_interleave(count, dim=dim)

@@ -400,6 +400,52 @@ def test_beam_options_vs_golden(name, which, fast):
                 np.testing.assert_allclose(a, z[p + "attn"][i, nb, :L, :cut], atol=1e-5)
 
 
+@pytest.mark.parametrize("temp,topk", [(1.0, -1), (0.7, 2), (1.5, 3)])
+def test_random_sampling_distribution(temp, topk):
+    """-random_sampling_temp / -random_sampling_topk (translator.py:371-394).
+    The draws cannot match torch's generator, so parity is distributional:
+    64 copies of each golden chunk, 8 seeds, and the step-0 tokens tested
+    (chi-square, p > 1e-4) against softmax of the oracle's sampling logits
+    built from the reference's own step-0 log-probs; tokens outside the top-k
+    never drawn; the score is the drawn token's tempered log-prob; equal seeds
+    repeat."""
+    from scipy import stats
+    from nanodecoder_amd.engine import pad_chunks
+    ref = _oracle()
+    z, meta = gu.load("transformer_greedy")
+    cfg, W = gu.model_for(meta)
+    chunks = gu.chunks_of(z)
+    rep = 64
+    eng = _engine(cfg, W, max_batch=len(chunks) * rep, max_steps=2)
+    sig, lens = pad_chunks([c for c in chunks for _ in range(rep)], 512)
+    spans = np.full(len(chunks) * rep, 512, np.int32)
+    lg = ref.sampling_logits(z["logp"][:, 0, :], temp, topk)
+    p = torch.softmax(lg, -1).numpy()
+    counts = np.zeros_like(p)
+    for seed in range(8):
+        r = eng.translate_sample(sig, lens, spans, temp=temp, keep_topk=topk, seed=1000 + seed, max_len=1,
+                                 return_logp=True)
+        tok = r["tokens"].cpu().numpy()[:, 0]
+        lp = r["logp"].cpu().numpy()[:, 0, :]
+        sc = r["scores"].cpu().numpy()
+        np.testing.assert_allclose(sc, lp[np.arange(len(tok)), tok] / temp, rtol=1e-6, atol=1e-6)
+        for i in range(len(chunks)):
+            np.add.at(counts[i], tok[i * rep:(i + 1) * rep], 1)
+        if seed == 0:
+            r2 = eng.translate_sample(sig, lens, spans, temp=temp, keep_topk=topk, seed=1000, max_len=1)
+            assert (r2["tokens"].cpu().numpy()[:, 0] == tok).all()
+    for i in range(len(chunks)):
+        assert counts[i][p[i] == 0].sum() == 0
+        exp = p[i] * counts[i].sum()
+        big = exp >= 5
+        f_obs = np.append(counts[i][big], counts[i][~big].sum())
+        f_exp = np.append(exp[big], exp[~big].sum())
+        if f_exp[-1] < 1e-9:
+            f_obs, f_exp = f_obs[:-1], f_exp[:-1]
+        if len(f_obs) > 1:
+            assert stats.chisquare(f_obs, f_exp * f_obs.sum() / f_exp.sum()).pvalue > 1e-4, (i, counts[i], exp)
+
+
 def test_classic_beam_packed_batches_vs_oracle():
     """Several reference batches packed into one engine call keep their own
     stopping points: equal to the oracle run batch by batch."""

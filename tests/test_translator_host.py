@@ -33,6 +33,11 @@ class FakeEngine:
             out["attn"] = a
         return out
 
+    def translate_sample(self, sig, L, S, temp, keep_topk, seed, max_len, min_len=0, return_attn=False):
+        out = self.translate_greedy(sig, L, S, max_len, min_len, return_attn)
+        self.calls[-1] = ("sample", sig.shape, L.copy(), S.copy(), temp, keep_topk, seed)
+        return out
+
     def translate_beam(self, sig, L, S, beam, n_best, alpha, max_len, min_len=0, return_attn=False,
                        done_step=None, hyp_len=4):
         self.calls.append(("beam", sig.shape, L.copy(), S.copy()))
@@ -209,8 +214,8 @@ def test_reference_errors():
         make_tr(beam_size=5, fast=True, block_ngram_repeat=2)
     with pytest.raises(AssertionError):
         make_tr(beam_size=5, fast=True, dump_beam="x.json")
-    with pytest.raises(NotImplementedError):
-        make_tr(random_sampling_topk=5)
+    with pytest.raises(ValueError):
+        make_tr(random_sampling_topk=9)
     with pytest.raises(AssertionError):
         make_tr(beam_size=5, fast=True, beta=0.5)
     with pytest.raises(RuntimeError):
@@ -243,3 +248,23 @@ def test_classic_options_reach_the_engine(tmp_path):
     import json
     assert json.loads(dump.read_text()) == {"predicted_ids": [], "beam_parent_ids": [], "scores": [],
                                             "log_probs": []}
+
+
+def test_random_sampling_reaches_the_engine():
+    """-random_sampling_topk / -random_sampling_temp (translator.py:371-394):
+    keep_topk 1 or temp 0 stay on the argmax path; otherwise the sampling
+    entry point runs with a seed that advances per call and repeats with -seed."""
+    tr, eng = make_tr(random_sampling_topk=1, random_sampling_temp=0.5)
+    tr.translate(chunks([100]), batch_size=1)
+    assert eng.calls[-1][0] == "greedy"
+    tr, eng = make_tr(random_sampling_topk=3, random_sampling_temp=0.0)
+    tr.translate(chunks([100]), batch_size=1)
+    assert eng.calls[-1][0] == "greedy"
+    tr, eng = make_tr(random_sampling_topk=3, random_sampling_temp=0.7, seed=5)
+    tr.translate(chunks([100]), batch_size=1)
+    tr.translate(chunks([100]), batch_size=1)
+    (k1, _, _, _, t1, top1, s1), (k2, _, _, _, _, _, s2) = eng.calls
+    assert k1 == k2 == "sample" and t1 == 0.7 and top1 == 3 and s1 != s2
+    tr2, eng2 = make_tr(random_sampling_topk=3, random_sampling_temp=0.7, seed=5)
+    tr2.translate(chunks([100]), batch_size=1)
+    assert eng2.calls[0][6] == s1
