@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import logging
 import multiprocessing
+import codecs
 import os
 import sys
 import time
@@ -79,10 +80,8 @@ def write_output(opt, file_src, all_predictions, time_translate):
 def main(opt=None):
     opt = opt or parse_translate_opts()
     logger = init_logger(opt.log_file)
-    for sub in ("", "result", "segment"):
+    for sub in ("", "result", "segment") + (("attention",) if opt.attn_debug else ()):  # translate.py:64-71
         os.makedirs(os.path.join(opt.save_data, sub), exist_ok=True)
-    if opt.attn_debug:
-        raise NotImplementedError("-attn_debug is not supported on the MI355X path")
     from .translator import build_translator
     translator = build_translator(opt, report_score=False, logger=logger)
     todo, done = list_reads(opt)
@@ -109,10 +108,24 @@ def main(opt=None):
     return n_done
 
 
+def _translate_attn(opt, translator, group):
+    """-attn_debug (translate.py:110-120): read by read, each into its own
+    save_data/attention/<read> file (appended)."""
+    outs = []
+    for g in group:
+        with codecs.open(os.path.join(opt.save_data, "attention", g[0]), "a+", "utf-8") as f:
+            translator.setAttnFile(f)
+            outs.append(translator.translate(src=list(g[1:]), batch_size=opt.batch_size, attn_debug=True))
+    return outs
+
+
 def _translate_group(opt, translator, group):
     t0 = time.time()
     try:
-        outs = translator.translate_reads([g[1:] for g in group], batch_size=opt.batch_size)
+        if opt.attn_debug:
+            outs = _translate_attn(opt, translator, group)
+        else:
+            outs = translator.translate_reads([g[1:] for g in group], batch_size=opt.batch_size)
     except Exception as e:
         for g in group:
             print("!!!error!!!data src: " + g[0].split(".txt")[0] + " (%r)" % (e,))

@@ -64,6 +64,7 @@ def translate_parser() -> argparse.ArgumentParser:
     _add(g, "pack_reads", type=int, default=1,
          help="translate this many reads per engine pass (chunks packed across reads; same outputs)")
     _add(g, "engine_max_batch", type=int, default=0, help="engine batch capacity (0 = max(batch_size, 8))")
+    _add(g, "seed", type=int, default=-1, help="random sampling seed (-1: fresh entropy per run)")
     return p
 
 

@@ -41,3 +41,30 @@ def test_cli_end_to_end(tmp_path, monkeypatch):
     assert len(speed) == 3 and all(len(l.split("\t")) == 4 for l in speed)
     # resume: nothing left to do
     assert cli.main(o) == 0
+
+
+def test_cli_attn_debug_and_beam_flags(tmp_path, monkeypatch):
+    """-attn_debug writes save_data/attention/<read> per read (translate.py:64-71,
+    110-120); the classic Beam's flags parse and reach the translator."""
+    import nanodecoder_amd.translator as T
+    monkeypatch.setattr(T, "Engine", _Eng)
+    monkeypatch.setattr(torch.cuda, "current_device", lambda: 0)
+    cfg = synth.ModelConfig()
+    ck = tmp_path / "m.pt"
+    checkpoint.save_synthetic(str(ck), cfg, synth.make_weights(cfg, seed=1))
+    src = tmp_path / "reads"
+    src.mkdir()
+    for i, n in enumerate((700, 400)):
+        raw = synth.synth_raw_read(i, n)
+        (src / f"read{i}.signal").write_text(" ".join(str(int(v)) for v in raw))
+    out = tmp_path / "out"
+    o = opts.parse_translate_opts(["-model", str(ck), "-src_dir", str(src), "-save_data", str(out), "-gpu", "0",
+                                   "-beam_size", "4", "-batch_size", "2", "-thread", "1", "-max_length", "6",
+                                   "-attn_debug", "-coverage_penalty", "summary", "-beta", "0.2",
+                                   "-stepwise_penalty", "-block_ngram_repeat", "3", "-ignore_when_blocking", "A",
+                                   "-pack_reads", "2"])
+    assert cli.main(o) == 2
+    for i, n_chunks in enumerate((2, 1)):
+        lines = [ln for ln in (out / "attention" / f"read{i}.txt").read_text().splitlines() if ln.strip()]
+        headers = [ln for ln in lines if ln.lstrip().startswith(">")]
+        assert len(headers) == n_chunks
