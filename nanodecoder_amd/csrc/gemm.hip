@@ -99,10 +99,13 @@ __device__ __forceinline__ void split4(f32x4 v, h4& hi, h4& lo) {
         (_Float16)(v.w - (float)hi.w)};
 }
 
-template <int BM, int BN, int WM, int WN, bool H3, bool LN, bool RELU, bool RESID>
+// BK: k depth of a main-loop step (32; 64 for the small-tile, long-K shapes,
+// whose steps are otherwise too short to cover the next step's load latency)
+template <int BM, int BN, int WM, int WN, int BK, bool H3, bool LN, bool RELU, bool RESID>
 __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g) {
   constexpr int NT = WM * WN * 64;
-  constexpr int BK = 32, LDK = BK + 4, LDC = BN + 4;
+  constexpr int LDK = BK + 4, LDC = BN + 4;
+  constexpr int TPK = BK / 4;  // threads per row of a row-major BK-wide slice
   constexpr int FM = BM / WM / 32, FN = BN / WN / 32;
   constexpr int A4 = BM * BK / 4 / NT;
   constexpr int W4 = BN * BK / 4 / NT;
@@ -177,12 +180,12 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
   auto amap = [&](int i, int& row, int& c) {
     if (g.p16io) {
       const int j = wave + (NT / 64) * i;
-      row = (j >> 1) * 16 + (lane & 15);
-      c = (j & 1) * 16 + 4 * (lane >> 4);
+      row = (j / (BK / 16)) * 16 + (lane & 15);
+      c = (j % (BK / 16)) * 16 + 4 * (lane >> 4);
     } else {
       const int f = tid + i * NT;
-      row = f >> 3;
-      c = (f & 7) * 4;
+      row = f / TPK;
+      c = (f % TPK) * 4;
     }
   };
   auto load_tile = [&](int k0) {
@@ -200,7 +203,7 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
     }
 #pragma unroll
     for (int i = 0; i < W4; ++i) {
-      const int f = tid + i * NT, row = f >> 3, c = (f & 7) * 4;
+      const int f = tid + i * NT, row = f / TPK, c = (f % TPK) * 4;
       if constexpr (H3)  // 16-byte chunk c/4 of the row's [k0, k0+32) image: 8-k group c/8, plane (c/4)&1
         rw[i] = *reinterpret_cast<const f32x4*>(g.Wh + (size_t)(n0 + row) * 2 * K + 2 * k0 + 2 * c);
       else
@@ -224,7 +227,7 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
     }
 #pragma unroll
     for (int i = 0; i < W4; ++i) {
-      const int f = tid + i * NT, row = f >> 3, c = (f & 7) * 4;
+      const int f = tid + i * NT, row = f / TPK, c = (f % TPK) * 4;
       st4(&Ws[buf * BN * LDK + row * LDK + c], rw[i]);
     }
   };
@@ -741,8 +744,9 @@ hipError_t launch_fold_layernorm(const float* W, const float* bias, const float*
     if (ln_ && re_ && rs_) hipLaunchKernelGGL((KERNEL<__VA_ARGS__, true, true, true>), grid, block, 0, s, g);       \
   } while (0)
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int BK = 32>
 static hipError_t launch_cfg(GemmArgs& g, hipStream_t s) {
+  if (g.K % BK != 0) return hipErrorInvalidValue;
   static const int xcd = [] {
     const char* e = getenv("ND_GEMM_XCD");  // 0: column tile fastest (A/B timing)
     return e ? atoi(e) : 1;
@@ -752,9 +756,9 @@ static hipError_t launch_cfg(GemmArgs& g, hipStream_t s) {
   dim3 grid((g.N / BN) * nmb), block(WM * WN * 64);
   g.part_n_out = g.N / BN;
   if (g.Wh)
-    ND_DISPATCH_FLAGS(gemm_f32_kernel, BM, BN, WM, WN, true);
+    ND_DISPATCH_FLAGS(gemm_f32_kernel, BM, BN, WM, WN, BK, true);
   else
-    ND_DISPATCH_FLAGS(gemm_f32_kernel, BM, BN, WM, WN, false);
+    ND_DISPATCH_FLAGS(gemm_f32_kernel, BM, BN, WM, WN, BK, false);
   return hipGetLastError();
 }
 
@@ -861,6 +865,19 @@ hipError_t launch_gemm(GemmArgs& g, hipStream_t s) {
   const long t128 = (long)((g.M + 127) / 128) * (g.N / 128);
   if (g.N % 128 == 0 && t128 >= 512) return launch_cfg<128, 128, 2, 2>(g, s);
   if (g.N % 64 != 0) return hipErrorInvalidValue;
+  static const int bkl = [] {
+    const char* e = getenv("ND_GEMM_BKL");  // k step of the 64x64 tiles at K >= 1024 (32, 64, 128)
+    const int v = e ? atoi(e) : 64;
+    return v == 32 || v == 128 ? v : 64;
+  }();
+  // long K on few small tiles (the beam decoder's K = 2048 products at M = 5120):
+  // deeper k steps keep more of the next step's operands in flight.  Measured
+  // at M = 5120, N = 256, K = 2048: BK 32 / 64 / 128 = 49.1 / 45.8 / 71.7 us
+  // (128: 135 KB of LDS, one workgroup per CU); beam B = 1024 168.9 -> 164.7 ms
+  if (g.K >= 1024 && g.K % 128 == 0) {
+    if (bkl == 128) return launch_cfg<64, 64, 2, 2, 128>(g, s);
+    if (bkl == 64) return launch_cfg<64, 64, 2, 2, 64>(g, s);
+  }
   return launch_cfg<64, 64, 2, 2>(g, s);
 }
 
