@@ -333,6 +333,28 @@ def scenario_chunks(kind, seed):
     raise ValueError(kind)
 
 
+def make_sampling_fixture(ns, out_dir):
+    """translate/translator.py:371-394, the random branch with keep_topk = -1
+    (the top-k branch casts to torch.cuda.FloatTensor and cannot run on a
+    CPU): the reference's own draws from seeded torch generators on the
+    reference's step-0 log-probs of transformer_greedy (64 copies of each
+    chunk's row)."""
+    z = np.load(os.path.join(out_dir, "transformer_greedy.npz"))
+    logits = torch.from_numpy(np.repeat(z["logp"][:, 0, :], 64, axis=0)).float()
+    temps = np.array([1.0, 0.7, 1.6], np.float32)
+    seeds = np.array([11, 12, 13], np.int64)
+    ids, scores = [], []
+    for t, sd in zip(temps, seeds):
+        torch.manual_seed(int(sd))
+        i, sc = ns.Translator.sample_with_temperature(None, logits.clone(), float(t), -1)
+        ids.append(i[:, 0].numpy().astype(np.int32))
+        scores.append(sc[:, 0].numpy().astype(np.float32))
+    path = os.path.join(out_dir, "sampling.npz")
+    np.savez_compressed(path, logits=logits.numpy(), temps=temps, seeds=seeds, ids=np.stack(ids),
+                        scores=np.stack(scores), torch=np.frombuffer(torch.__version__.encode(), np.uint8))
+    print(f"wrote {path} ({os.path.getsize(path)} B)")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=GOLDEN_DIR)
@@ -386,6 +408,8 @@ def main():
         print(f"wrote {path} ({os.path.getsize(path)} B)")
     with open(ipath, "w") as f:
         json.dump(index, f, indent=1, sort_keys=True)
+    if not args.only or "sampling" in args.only:
+        make_sampling_fixture(ns, args.out)
 
 
 if __name__ == "__main__":

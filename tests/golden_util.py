@@ -6,7 +6,8 @@ import numpy as np
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 NAMES = ["transformer_greedy", "transformer_pe_short", "transformer_beam", "nano_greedy", "transformer_aan",
-         "transformer_classic_beam", "transformer_classic_beam_mid"]
+         "transformer_classic_beam", "transformer_classic_beam_mid", "transformer_beam_attn",
+         "transformer_classic_ext", "transformer_classic_cov"]
 
 
 def load(name):

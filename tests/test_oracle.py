@@ -117,3 +117,20 @@ def test_translate_batching_and_strings():
         s = ref_cpu.tokens_to_string(z["tokens"][i], cfg.itos, cfg.eos_idx)
         assert preds[i] == [s]
         assert abs(scores[i][0] - z["scores"][i]) < 1e-5
+
+
+def test_sampling_matches_reference_draws():
+    """ref_cpu.sampling_logits + torch's Multinomial draw reproduce the
+    reference's own sample_with_temperature (translator.py:371-394,
+    keep_topk = -1) draw for draw on the same seeds: ids and scores."""
+    import os
+    import torch
+    z = np.load(os.path.join(gu.GOLDEN, "sampling.npz"))
+    logits = torch.from_numpy(z["logits"])
+    for k, (t, sd) in enumerate(zip(z["temps"], z["seeds"])):
+        torch.manual_seed(int(sd))
+        lg = ref_cpu.sampling_logits(logits, float(t), -1)
+        ids = torch.argmax(torch.distributions.Multinomial(logits=lg, total_count=1).sample(), dim=1, keepdim=True)
+        sc = lg.gather(dim=1, index=ids)
+        assert (ids[:, 0].numpy() == z["ids"][k]).all()
+        np.testing.assert_array_equal(sc[:, 0].numpy(), z["scores"][k])
