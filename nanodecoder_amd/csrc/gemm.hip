@@ -140,6 +140,79 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
   const int M = g.M, K = g.K;
   const float* __restrict__ A = g.A;
 
+  f32x4 ra[A4], rw[W4];
+  // A staging piece i of this thread: (row, c) of the BM x BK tile.  Row-major
+  // A: 8 threads per 128-B row segment.  P16 A (g.p16io, the decoder's packed
+  // activations): one whole 1 KB P16 block per wave instruction, lane e =
+  // row e & 15, columns 4 (e >> 4) .. + 3 of the block.
+  auto amap = [&](int i, int& row, int& c) {
+    if (g.p16io) {
+      const int j = wave + (NT / 64) * i;
+      row = (j / (BK / 16)) * 16 + (lane & 15);
+      c = (j % (BK / 16)) * 16 + 4 * (lane >> 4);
+    } else {
+      const int f = tid + i * NT;
+      row = f / TPK;
+      c = (f % TPK) * 4;
+    }
+  };
+  auto load_tile = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < A4; ++i) {
+      int row, c;
+      amap(i, row, c);
+      const int gr = m0 + row;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (gr < M) v = ld4(g.p16io ? A + pk(gr, k0 + c, K) : A + (size_t)gr * g.lda + k0 + c);
+      ra[i] = v;  // raw: the LayerNorm is applied at the LDS store, once the row statistics are in
+    }
+#pragma unroll
+    for (int i = 0; i < W4; ++i) {
+      const int f = tid + i * NT, row = f / TPK, c = (f % TPK) * 4;
+      if constexpr (H3)  // 16-byte chunk c/4 of the row's [k0, k0+32) image: 8-k group c/8, plane (c/4)&1
+        rw[i] = *reinterpret_cast<const f32x4*>(g.Wh + (size_t)(n0 + row) * 2 * K + 2 * k0 + 2 * c);
+      else
+        rw[i] = ld4(g.W + (size_t)(n0 + row) * g.ldw + k0 + c);
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < A4; ++i) {
+      int row, c;
+      amap(i, row, c);
+      if constexpr (LN) ra[i] = (ra[i] - s_mu[row]) * s_rs[row];
+      if constexpr (H3) {
+        h4 hi, lo;
+        split4(ra[i], hi, lo);
+        float* p = &As[buf * BM * LDK + row * LDK + (c >> 3) * 8 + ((c >> 2) & 1) * 2];
+        *reinterpret_cast<h4*>(p) = hi;
+        *reinterpret_cast<h4*>(p + 4) = lo;
+      } else {
+        st4(&As[buf * BM * LDK + row * LDK + c], ra[i]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < W4; ++i) {
+      const int f = tid + i * NT, row = f / TPK, c = (f % TPK) * 4;
+      st4(&Ws[buf * BN * LDK + row * LDK + c], rw[i]);
+    }
+  };
+
+  f32x16 acc[FM][FN];
+#pragma unroll
+  for (int a = 0; a < FM; ++a)
+#pragma unroll
+    for (int b = 0; b < FN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+  const int wm = wave / WN, wn = wave % WN;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int KT = K / BK;
+
+  // the first step's operands are in flight while the row statistics load
+  // (QKV at M = 131072: 271.6 -> 266 us)
+  load_tile(0);
   if constexpr (LN) {
     if (g.part_in) {
       for (int r = tid; r < BM; r += NT) {
@@ -171,80 +244,6 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
     }
     __syncthreads();
   }
-
-  f32x4 ra[A4], rw[W4];
-  // A staging piece i of this thread: (row, c) of the BM x BK tile.  Row-major
-  // A: 8 threads per 128-B row segment.  P16 A (g.p16io, the decoder's packed
-  // activations): one whole 1 KB P16 block per wave instruction, lane e =
-  // row e & 15, columns 4 (e >> 4) .. + 3 of the block.
-  auto amap = [&](int i, int& row, int& c) {
-    if (g.p16io) {
-      const int j = wave + (NT / 64) * i;
-      row = (j / (BK / 16)) * 16 + (lane & 15);
-      c = (j % (BK / 16)) * 16 + 4 * (lane >> 4);
-    } else {
-      const int f = tid + i * NT;
-      row = f / TPK;
-      c = (f % TPK) * 4;
-    }
-  };
-  auto load_tile = [&](int k0) {
-#pragma unroll
-    for (int i = 0; i < A4; ++i) {
-      int row, c;
-      amap(i, row, c);
-      const int gr = m0 + row;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (gr < M) {
-        v = ld4(g.p16io ? A + pk(gr, k0 + c, K) : A + (size_t)gr * g.lda + k0 + c);
-        if constexpr (LN) v = (v - s_mu[row]) * s_rs[row];
-      }
-      ra[i] = v;
-    }
-#pragma unroll
-    for (int i = 0; i < W4; ++i) {
-      const int f = tid + i * NT, row = f / TPK, c = (f % TPK) * 4;
-      if constexpr (H3)  // 16-byte chunk c/4 of the row's [k0, k0+32) image: 8-k group c/8, plane (c/4)&1
-        rw[i] = *reinterpret_cast<const f32x4*>(g.Wh + (size_t)(n0 + row) * 2 * K + 2 * k0 + 2 * c);
-      else
-        rw[i] = ld4(g.W + (size_t)(n0 + row) * g.ldw + k0 + c);
-    }
-  };
-  auto store_tile = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < A4; ++i) {
-      int row, c;
-      amap(i, row, c);
-      if constexpr (H3) {
-        h4 hi, lo;
-        split4(ra[i], hi, lo);
-        float* p = &As[buf * BM * LDK + row * LDK + (c >> 3) * 8 + ((c >> 2) & 1) * 2];
-        *reinterpret_cast<h4*>(p) = hi;
-        *reinterpret_cast<h4*>(p + 4) = lo;
-      } else {
-        st4(&As[buf * BM * LDK + row * LDK + c], ra[i]);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < W4; ++i) {
-      const int f = tid + i * NT, row = f / TPK, c = (f % TPK) * 4;
-      st4(&Ws[buf * BN * LDK + row * LDK + c], rw[i]);
-    }
-  };
-
-  f32x16 acc[FM][FN];
-#pragma unroll
-  for (int a = 0; a < FM; ++a)
-#pragma unroll
-    for (int b = 0; b < FN; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-
-  const int wm = wave / WN, wn = wave % WN;
-  const int lr = lane & 31, lh = lane >> 5;
-  const int KT = K / BK;
-
-  load_tile(0);
   store_tile(0);
   __syncthreads();
   for (int kt = 0; kt < KT; ++kt) {
