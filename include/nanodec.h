@@ -183,6 +183,23 @@ int nd_translate_beam_classic_ex(nd_ctx* ctx, const float* d_signal, const int32
                                  int32_t* d_tokens, float* d_scores, int32_t* d_lens, int32_t* d_steps, float* d_attn,
                                  void* stream);
 
+/* Signal front end (utils/labelop.py:194-243, extract_fast5_raw): R raw
+ * reads concatenated in d_raw (float64, read r at d_offsets[r] ..
+ * d_offsets[r+1]) normalised per read into d_out (float32, same offsets).
+ * method: 0 none, 1 median (x - median) / MAD with statsmodels' robust.mad
+ * (median(|x - median| / 0.6744897501960817)), 2 mean ((x - median) / std,
+ * as the reference centres it).  fp64 arithmetic and exact medians, so the
+ * float32 chunks equal the reference's (method 2: within 1 ulp, the std is a
+ * reduction).  No context needed. */
+int nd_normalize_reads(const double* d_raw, const int64_t* d_offsets, int32_t R, int32_t method, float* d_out,
+                       void* stream);
+
+/* Windowing (utils/labelop.py:225-233) straight into a signal batch: chunk c
+ * = d_len[c] samples of read d_read[c] from d_start[c], zero padded to T, is
+ * row c of d_signal [C, T].  The caller lists the windows (stride, length). */
+int nd_window_reads(const float* d_sig, const int64_t* d_offsets, const int32_t* d_read, const int32_t* d_start,
+                    const int32_t* d_len, int32_t C, int32_t T, float* d_signal, void* stream);
+
 /* Encoder forward only; writes the memory bank [B, T, d_model] (rows
  * t >= span are unspecified).  Replaces Translator._run_encoder
  * (translate/translator.py:542-559).  Used by parity tests. */

@@ -52,6 +52,8 @@ SIGNATURES = {
     "nd_translate_beam_classic": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _F, _I, _I, _P, _P, _P, _P, _P]),
     "nd_translate_beam_classic_ex": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, ctypes.POINTER(NdClassicOpts), _I,
                                           _I, _P, _P, _P, _P, _P, _P]),
+    "nd_normalize_reads": (_I, [_P, _P, _I, _I, _P, _P]),
+    "nd_window_reads": (_I, [_P, _P, _P, _P, _P, _I, _I, _P, _P]),
     "nd_encode": (_I, [_P, _P, _P, _P, _I, _I, _P, _P]),
     "nd_set_graphs": (_I, [_P, _I]),
     "nd_set_timing": (_I, [_P, _I]),

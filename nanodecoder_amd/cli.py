@@ -52,6 +52,26 @@ def list_reads(opt):
     return todo, done
 
 
+def _read_only(args):
+    """-frontend gpu: the worker only reads the raw samples."""
+    path, prefix, suffix, norm, length, stride = args
+    try:
+        return [prefix, frontend.read_raw(path, suffix)]
+    except Exception:
+        return ["!" + prefix]
+
+
+def _gpu_chunks(opt, group):
+    """[prefix, raw] reads -> [prefix, chunk, ...] with the device front end."""
+    sig, lens, rd = frontend.normalize_window_gpu([g[1] for g in group], opt.normalization_raw,
+                                                  opt.src_seq_length, opt.src_seq_stride)
+    host = sig.cpu().numpy()
+    out = [[g[0]] for g in group]
+    for c in range(len(rd)):
+        out[rd[c]].append(host[c, : lens[c]].copy())
+    return out
+
+
 def _extract(args):
     path, prefix, suffix, norm, length, stride = args
     try:
@@ -90,9 +110,10 @@ def main(opt=None):
     ctx = multiprocessing.get_context("spawn")
     t_start = time.time()
     n_done = 0
+    gpu_fe = getattr(opt, "frontend", "cpu") == "gpu"
     with ctx.Pool(max(1, opt.thread)) as pool:
         pending = []
-        for src in pool.imap(_extract, jobs):
+        for src in pool.imap(_read_only if gpu_fe else _extract, jobs):
             if src and src[0].startswith("!"):
                 print("!!!error!!!data src: " + src[0][1:].split(".txt")[0])
                 continue
@@ -100,10 +121,10 @@ def main(opt=None):
                 continue
             pending.append(src)
             if len(pending) >= max(1, opt.pack_reads):
-                n_done += _translate_group(opt, translator, pending)
+                n_done += _translate_group(opt, translator, _gpu_chunks(opt, pending) if gpu_fe else pending)
                 pending = []
         if pending:
-            n_done += _translate_group(opt, translator, pending)
+            n_done += _translate_group(opt, translator, _gpu_chunks(opt, pending) if gpu_fe else pending)
     logger.info("translated %d reads in %.1f s" % (n_done, time.time() - t_start))
     return n_done
 

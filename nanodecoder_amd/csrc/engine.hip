@@ -1432,6 +1432,21 @@ int nd_op_dec_mem_attention(const float* qp, const float* mem, const float* sign
   return ND_OK;
 }
 
+int nd_normalize_reads(const double* d_raw, const int64_t* d_offsets, int32_t R, int32_t method, float* d_out,
+                       void* stream) {
+  hipError_t e = nd::launch_read_normalize(d_raw, (const long long*)d_offsets, R, method, d_out, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("normalize_reads: ") + hipGetErrorString(e));
+  return ND_OK;
+}
+
+int nd_window_reads(const float* d_sig, const int64_t* d_offsets, const int32_t* d_read, const int32_t* d_start,
+                    const int32_t* d_len, int32_t C, int32_t T, float* d_signal, void* stream) {
+  hipError_t e = nd::launch_read_window(d_sig, (const long long*)d_offsets, d_read, d_start, d_len, C, T, d_signal,
+                                        (hipStream_t)stream);
+  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("window_reads: ") + hipGetErrorString(e));
+  return ND_OK;
+}
+
 int nd_op_memory_pack(const float* x, const float* ln_g, const float* ln_b, float* out, int32_t B, int32_t T,
                       int32_t ldT, void* stream) {
   hipError_t e = nd::launch_memory_pack(x, ln_g, ln_b, out, B, T, ldT, (hipStream_t)stream);

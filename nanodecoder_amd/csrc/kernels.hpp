@@ -128,6 +128,13 @@ hipError_t launch_stamp_reset(unsigned long long* stamps, int pairs, hipStream_t
 hipError_t launch_memory_pack(const float* x, const float* ln_g, const float* ln_b, float* out, int B, int T, int ldT,
                               hipStream_t s);
 hipError_t init_mem_attributes();
+// signal front end (frontend.hip): per-read normalisation (method 0 none, 1
+// median/MAD, 2 median/std; fp64 math, float32 out) of reads concatenated at
+// off[0..R], and windowing of chunks (read, start, len) into a [C, T] batch
+hipError_t launch_read_normalize(const double* raw, const long long* off, int R, int method, float* out,
+                                 hipStream_t s);
+hipError_t launch_read_window(const float* sig, const long long* off, const int* rd, const int* start,
+                              const int* len, int C, int T, float* out, hipStream_t s);
 // average self-attention (aan.hip): xn = LN_1(x), avg = (xn + step prev) / (step + 1)
 // (prev from hist[anc[r][step-1]][step-1], avg stored at hist[r][step]), avg's
 // row statistics (one partial); then q1 = sig(g_in) xn + sig(g_f) a + x (+ stats)

@@ -71,6 +71,66 @@ def extract_raw(input_file_path: str, output_prefix: str, normalization: str, ma
                            "identified.") from e
 
 
+NORM_METHOD = {"none": 0, "None": 0, "median": 1, "mean": 2}
+
+
+def windows(n: int, max_length: int, stride: int):
+    """(start, length) of each chunk window() cuts from an n-sample read
+    (utils/labelop.py:225-233)."""
+    out = []
+    for i in range(0, math.ceil(n / stride)):
+        st = i * stride
+        e = min(st + max_length, n)
+        out.append((st, e - st))
+        if e >= n:
+            break
+    return out
+
+
+def normalize_window_gpu(raws, normalization: str, max_length: int, stride: int, device=0, T: int = None):
+    """extract_fast5_raw's normalisation and windowing for many reads on the
+    GPU (nd_normalize_reads + nd_window_reads, frontend.hip): one host-to-
+    device copy of the concatenated float64 reads, fp64 medians by radix
+    select, chunks written straight into a zero-padded [C, T] float32 batch.
+    Returns (signal [C, T] device tensor, chunk lengths [C] int32,
+    chunk -> read index [C] int32)."""
+    import ctypes
+
+    import torch
+
+    from . import _lib
+    method = NORM_METHOD.get(normalization, 0)  # anything else: the raw read, as labelop.py:220-223
+    raws = [np.asarray(r, dtype=np.float64).reshape(-1) for r in raws]
+    lens = np.array([r.size for r in raws], np.int64)
+    if (lens < 1).any():
+        raise ValueError("empty read")
+    off = np.zeros(len(raws) + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    rd, st, ln = [], [], []
+    for r, n in enumerate(lens):
+        for a, b in windows(int(n), max_length, stride):
+            rd.append(r)
+            st.append(a)
+            ln.append(b)
+    T = T or max_length
+    dev = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+    raw_d = torch.from_numpy(np.concatenate(raws)).to(dev)
+    off_d = torch.from_numpy(off).to(dev)
+    norm_d = torch.empty(int(off[-1]), dtype=torch.float32, device=dev)
+    L = _lib.lib()
+    stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    _lib.check(L.nd_normalize_reads(p(raw_d), p(off_d), len(raws), method, p(norm_d), stream), "nd_normalize_reads")
+    C = len(rd)
+    rd_d = torch.tensor(rd, dtype=torch.int32, device=dev)
+    st_d = torch.tensor(st, dtype=torch.int32, device=dev)
+    ln_d = torch.tensor(ln, dtype=torch.int32, device=dev)
+    sig = torch.empty(C, T, dtype=torch.float32, device=dev)
+    _lib.check(L.nd_window_reads(p(norm_d), p(off_d), p(rd_d), p(st_d), p(ln_d), C, T, p(sig), stream),
+               "nd_window_reads")
+    return sig, np.array(ln, np.int32), np.array(rd, np.int32)
+
+
 def index2base(read) -> str:
     """utils/labelop.py:295-307."""
     return "".join(BASE_KEYS[x] for x in read)

@@ -65,6 +65,8 @@ def translate_parser() -> argparse.ArgumentParser:
          help="translate this many reads per engine pass (chunks packed across reads; same outputs)")
     _add(g, "engine_max_batch", type=int, default=0, help="engine batch capacity (0 = max(batch_size, 8))")
     _add(g, "seed", type=int, default=-1, help="random sampling seed (-1: fresh entropy per run)")
+    _add(g, "frontend", default="cpu", choices=["cpu", "gpu"],
+         help="gpu: normalise and window the reads on the GPU (frontend.hip) instead of in the worker pool")
     return p
 
 

@@ -132,3 +132,17 @@ def test_extract_raw_signal_file(tmp_path):
     out = frontend.extract_raw(str(p), "r.txt", "median", 512, 512, "signal")
     assert out[0] == "r.txt" and [len(c) for c in out[1:]] == [512, 512, 76]
     np.testing.assert_array_equal(np.concatenate(out[1:]), frontend.normalize(raw, "median").astype(np.float32))
+
+
+def test_windows_match_window():
+    """frontend.windows (the GPU front end's chunk list) cuts exactly what
+    window() (utils/labelop.py:225-233) cuts."""
+    from nanodecoder_amd import frontend
+    for n in (1, 2, 299, 300, 512, 513, 1024, 1300, 4000):
+        for L, st in ((512, 512), (300, 60), (512, 256)):
+            x = np.arange(n, dtype=np.float64)
+            exp = frontend.window(x, L, st)
+            got = frontend.windows(n, L, st)
+            assert len(got) == len(exp)
+            for (a, b), e in zip(got, exp):
+                assert b == len(e) and (x[a: a + b].astype(np.float32) == e).all()

@@ -561,3 +561,72 @@ def test_memory_bank_path_matches_kv_path_ragged_spans():
     assert (out[0][0] == out[1][0]).all()
     # generator biases put some log-probs near -1e4, where one fp32 ulp is 1e-3
     assert np.allclose(out[0][1], out[1][1], rtol=2e-6, atol=1e-4)
+
+
+# ----------------------------------------------------------------- front end
+@pytest.mark.parametrize("method", ["median", "mean", "None"])
+def test_frontend_normalize_window_vs_host(method):
+    """nd_normalize_reads + nd_window_reads against the host restatement of
+    extract_fast5_raw (frontend.normalize + window, numpy float64): DAC-like
+    integer reads (ties everywhere), float reads, odd / even / tiny / long
+    lengths.  Bit-exact float32 chunks for median and None; mean within 1
+    ulp (its std is a reduction in another order)."""
+    from nanodecoder_amd import frontend, synth
+    rng = np.random.default_rng(7)
+    raws = [synth.synth_raw_read(i, n) for i, n in enumerate((1300, 700, 512, 513, 511, 100_003))]
+    raws += [np.array([5.0]), np.array([3.0, 9.0]), np.array([1.0, 1.0, 2.0]),
+             rng.normal(size=1001) * 50 - 20, rng.integers(-100, 100, size=2048).astype(np.float64)]
+    sig, lens, rd = frontend.normalize_window_gpu(raws, method, 512, 512)
+    got = sig.cpu().numpy()
+    c = 0
+    for r, raw in enumerate(raws):
+        exp = frontend.window(frontend.normalize(raw, method), 512, 512)
+        for e in exp:
+            assert rd[c] == r and lens[c] == len(e)
+            g = got[c, : len(e)]
+            if method == "mean":
+                np.testing.assert_array_max_ulp(g, e, maxulp=1)
+            else:
+                assert (g.view(np.uint32) == e.view(np.uint32)).all(), (r, c)
+            assert (got[c, len(e):] == 0).all()
+            c += 1
+    assert c == len(rd)
+
+
+def test_cli_gpu_frontend_matches_host(tmp_path, monkeypatch):
+    """translate.py with -frontend gpu hands the translator the same float32
+    chunks, read by read, as the worker-pool front end (median/MAD)."""
+    import torch
+    from nanodecoder_amd import checkpoint, cli, opts, synth
+    import nanodecoder_amd.translator as T
+    from tests.test_cli import _Eng
+    monkeypatch.setattr(T, "Engine", _Eng)
+    seen = {}
+
+    def capture(self, reads, batch_size, attn_debug=False):
+        seen.setdefault(mode[0], []).extend(reads)
+        return [([[0.0]] * len(r), [["A"]] * len(r)) for r in reads]
+
+    monkeypatch.setattr(T.Translator, "translate_reads", capture)
+    cfg = synth.ModelConfig()
+    ck = tmp_path / "m.pt"
+    checkpoint.save_synthetic(str(ck), cfg, synth.make_weights(cfg, seed=1))
+    src = tmp_path / "reads"
+    src.mkdir()
+    for i, n in enumerate((1300, 700, 400, 2049)):
+        raw = synth.synth_raw_read(i, n)
+        (src / f"read{i}.signal").write_text(" ".join(str(int(v)) for v in raw))
+    mode = ["cpu"]
+    for m in ("cpu", "gpu"):
+        mode[0] = m
+        out = tmp_path / ("out_" + m)
+        o = opts.parse_translate_opts(["-model", str(ck), "-src_dir", str(src), "-save_data", str(out), "-gpu", "0",
+                                       "-beam_size", "1", "-batch_size", "2", "-thread", "2", "-max_length", "10",
+                                       "-pack_reads", "2", "-frontend", m])
+        assert cli.main(o) == 4
+    a, b = seen["cpu"], seen["gpu"]
+    assert len(a) == len(b) == 4
+    for ra, rb in zip(a, b):
+        assert len(ra) == len(rb)
+        for ca, cb in zip(ra, rb):
+            assert ca.dtype == cb.dtype == np.float32 and (ca.view(np.uint32) == cb.view(np.uint32)).all()
