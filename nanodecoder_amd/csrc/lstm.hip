@@ -22,6 +22,8 @@
 #include "common.hpp"
 #include "kernels.hpp"
 
+#include <cstdlib>
+
 namespace nd {
 
 __device__ __forceinline__ f32x4 mfma16x4(float a, float b, f32x4 c) {
@@ -30,12 +32,29 @@ __device__ __forceinline__ f32x4 mfma16x4(float a, float b, f32x4 c) {
 
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
 
+typedef _Float16 lh8 __attribute__((ext_vector_type(8)));
+// split-fp16 (gemm.hip): hi = fp16(x), lo = fp16(x - hi), 22 significant bits
+__device__ __forceinline__ void lsplit8(const float (&x)[8], lh8& hi, lh8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    hi[j] = (_Float16)x[j];
+    lo[j] = (_Float16)(x[j] - (float)hi[j]);
+  }
+}
+__device__ __forceinline__ f32x4 mfma16x32h(lh8 a, lh8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+#define LSTM_HSCALE 1024.0f  // h (|h| < 1) enters the split at 2^10: lo stays clear of the fp16 subnormals
+
 #define LSTM_H 128
 #define LSTM_G 512
 #define LSTM_HS_LD (LSTM_H + 4)
 #define LSTM_GS_LD (LSTM_G + 4)
 
-template <bool LAYER0>
+// H3: the recurrent product on v_mfma_f32_16x16x32_f16 in the split-fp16
+// form (hi*lo + lo*hi + hi*hi), W_hh scaled by a power of two per direction
+// (max |W| in [2^13, 2^14)) and h by 2^10; otherwise fp32 16x16x4 MFMAs.
+template <bool LAYER0, bool H3>
 __global__ void __launch_bounds__(1024)
 lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projections (fwd | bwd), !LAYER0
                 const float* __restrict__ signal,  // [B, T] (LAYER0)
@@ -53,20 +72,51 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
   const int li = lane & 15, lq = lane >> 4;
 
   // W_hh^T fragments for this wave's two 16-column tiles, k order matching
-  // the A fragment: block kb, step s <-> k = 16*kb + 4*lq + s
+  // the A fragment: fp32, block kb, step s <-> k = 16*kb + 4*lq + s; H3,
+  // block kb (32 k), slot j <-> k = 32*kb + 8*lq + j
   float wr[2][32];
+  lh8 whi[2][4], wlo[2][4];
+  float unscale = 1.f;
   {
     const float* W = whh + (size_t)dir * LSTM_G * LSTM_H;
+    float wsc = 1.f;
+    if constexpr (H3) {
+      __shared__ float s_max[16];
+      float m = 0.f;
+      for (int e = tid; e < LSTM_G * LSTM_H; e += 1024) m = fmaxf(m, fabsf(W[e]));
+      m = wave_max(m);
+      if (lane == 0) s_max[wave] = m;
+      __syncthreads();
+      m = 0.f;
+#pragma unroll
+      for (int w = 0; w < 16; ++w) m = fmaxf(m, s_max[w]);
+      int ex = 0;
+      frexpf(m, &ex);  // m = f * 2^ex, f in [0.5, 1)
+      const int sh = m > 0.f ? 14 - ex : 0;
+      wsc = ldexpf(1.f, sh);
+      unscale = ldexpf(1.f, -sh) / LSTM_HSCALE;
+    }
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int n = wave * 32 + t * 16 + li;
+      if constexpr (H3) {
 #pragma unroll
-      for (int kb = 0; kb < 8; ++kb) {
-        const f32x4 v = ld4(W + (size_t)n * LSTM_H + kb * 16 + 4 * lq);
-        wr[t][kb * 4 + 0] = v.x;
-        wr[t][kb * 4 + 1] = v.y;
-        wr[t][kb * 4 + 2] = v.z;
-        wr[t][kb * 4 + 3] = v.w;
+        for (int kb = 0; kb < 4; ++kb) {
+          const f32x4 v0 = ld4(W + (size_t)n * LSTM_H + kb * 32 + 8 * lq);
+          const f32x4 v1 = ld4(W + (size_t)n * LSTM_H + kb * 32 + 8 * lq + 4);
+          const float x[8] = {v0.x * wsc, v0.y * wsc, v0.z * wsc, v0.w * wsc,
+                              v1.x * wsc, v1.y * wsc, v1.z * wsc, v1.w * wsc};
+          lsplit8(x, whi[t][kb], wlo[t][kb]);
+        }
+      } else {
+#pragma unroll
+        for (int kb = 0; kb < 8; ++kb) {
+          const f32x4 v = ld4(W + (size_t)n * LSTM_H + kb * 16 + 4 * lq);
+          wr[t][kb * 4 + 0] = v.x;
+          wr[t][kb * 4 + 1] = v.y;
+          wr[t][kb * 4 + 2] = v.z;
+          wr[t][kb * 4 + 3] = v.w;
+        }
       }
     }
   }
@@ -136,14 +186,34 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
 
     // gates = h_{t-1} W_hh^T on MFMA
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-    const float* hrow = &hs[cur][li * LSTM_HS_LD + 4 * lq];
+    if constexpr (H3) {
+      const float* hrow = &hs[cur][li * LSTM_HS_LD + 8 * lq];
 #pragma unroll
-    for (int kb = 0; kb < 8; ++kb) {
-      const f32x4 a = ld4(hrow + kb * 16);
+      for (int kb = 0; kb < 4; ++kb) {
+        const f32x4 a0 = ld4(hrow + kb * 32), a1 = ld4(hrow + kb * 32 + 4);
+        const float x[8] = {a0.x * LSTM_HSCALE, a0.y * LSTM_HSCALE, a0.z * LSTM_HSCALE, a0.w * LSTM_HSCALE,
+                            a1.x * LSTM_HSCALE, a1.y * LSTM_HSCALE, a1.z * LSTM_HSCALE, a1.w * LSTM_HSCALE};
+        lh8 ah, al;
+        lsplit8(x, ah, al);
+        acc0 = mfma16x32h(ah, wlo[0][kb], acc0);
+        acc1 = mfma16x32h(ah, wlo[1][kb], acc1);
+        acc0 = mfma16x32h(al, whi[0][kb], acc0);
+        acc1 = mfma16x32h(al, whi[1][kb], acc1);
+        acc0 = mfma16x32h(ah, whi[0][kb], acc0);
+        acc1 = mfma16x32h(ah, whi[1][kb], acc1);
+      }
+      acc0 *= unscale;
+      acc1 *= unscale;
+    } else {
+      const float* hrow = &hs[cur][li * LSTM_HS_LD + 4 * lq];
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        acc0 = mfma16x4(a[s], wr[0][kb * 4 + s], acc0);
-        acc1 = mfma16x4(a[s], wr[1][kb * 4 + s], acc1);
+      for (int kb = 0; kb < 8; ++kb) {
+        const f32x4 a = ld4(hrow + kb * 16);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          acc0 = mfma16x4(a[s], wr[0][kb * 4 + s], acc0);
+          acc1 = mfma16x4(a[s], wr[1][kb * 4 + s], acc1);
+        }
       }
     }
 #pragma unroll
@@ -181,12 +251,23 @@ hipError_t launch_lstm_layer(const float* xp, const float* signal, const float* 
                              const float* whh, const int* len, int B, int T, float* out, const float* bn_scale,
                              const float* bn_shift, bool layer0, hipStream_t s) {
   dim3 grid((B + 15) / 16, 2), block(1024);
-  if (layer0)
-    hipLaunchKernelGGL(lstm_dir_kernel<true>, grid, block, 0, s, xp, signal, wih0, bsum, whh, len, B, T, out,
-                       bn_scale, bn_shift);
+  static const bool f32 = [] {
+    const char* e = getenv("ND_LSTM_F32");  // 1: fp32 MFMAs for the recurrence
+    const char* g = getenv("ND_GEMM_F32");
+    return (e && atoi(e) != 0) || (g && atoi(g) != 0);
+  }();
+#define ND_LSTM_GO(L0, H)                                                                                       \
+  hipLaunchKernelGGL((lstm_dir_kernel<L0, H>), grid, block, 0, s, xp, signal, wih0, bsum, whh, len, B, T, out, \
+                     bn_scale, bn_shift)
+  if (layer0 && f32)
+    ND_LSTM_GO(true, false);
+  else if (layer0)
+    ND_LSTM_GO(true, true);
+  else if (f32)
+    ND_LSTM_GO(false, false);
   else
-    hipLaunchKernelGGL(lstm_dir_kernel<false>, grid, block, 0, s, xp, signal, wih0, bsum, whh, len, B, T, out,
-                       bn_scale, bn_shift);
+    ND_LSTM_GO(false, true);
+#undef ND_LSTM_GO
   return hipGetLastError();
 }
 
