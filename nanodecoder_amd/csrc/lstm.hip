@@ -163,9 +163,7 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
       const int pos = act ? pos_of(q, step) : 0;
       const size_t row = (size_t)(b0 + q) * T + pos;
       if constexpr (LAYER0) {
-        const float s = act ? signal[row] : 0.f;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) x[u][g] = s * w0[u][g] + bb[u][g];
+        x[u][0] = act ? signal[row] : 0.f;  // the sample; its projection is formed at use (no wait here)
       } else {
 #pragma unroll
         for (int g = 0; g < 4; ++g) x[u][g] = act ? xp[row * 1024 + dir * LSTM_G + g * LSTM_H + punit[u]] : 0.f;
@@ -181,7 +179,7 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) xc[u][g] = xn[u][g];
+      for (int g = 0; g < 4; ++g) xc[u][g] = LAYER0 ? xn[u][0] * w0[u][g] + bb[u][g] : xn[u][g];
     if (step + 1 < maxlen) load_x(step + 1, xn);  // prefetch next step's projections
 
     // gates = h_{t-1} W_hh^T on MFMA
