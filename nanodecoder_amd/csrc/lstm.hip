@@ -136,13 +136,11 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
     pseq[u] = p >> 7;
     punit[u] = p & 127;
   }
-  float bnsc[2] = {1.f, 1.f}, bnsh[2] = {0.f, 0.f};
-  if (bn_scale) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      bnsc[u] = bn_scale[dir * LSTM_H + punit[u]];
-      bnsh[u] = bn_shift[dir * LSTM_H + punit[u]];
-    }
+  // eval BatchNorm of the next layer's input, per unit, kept in LDS (registers are the limit here)
+  __shared__ float s_bn[2][LSTM_H];
+  if (bn_scale && tid < LSTM_H) {
+    s_bn[0][tid] = bn_scale[dir * LSTM_H + tid];
+    s_bn[1][tid] = bn_shift[dir * LSTM_H + tid];
   }
   float w0[2][4], bb[2][4];
   if constexpr (LAYER0) {
@@ -235,7 +233,7 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
         c[u] = fg * c[u] + ig * gg;
         h = og * tanhf(c[u]);
         const size_t row = (size_t)(b0 + q) * T + pos_of(q, step);
-        out[row * 2 * LSTM_H + dir * LSTM_H + j] = bn_scale ? h * bnsc[u] + bnsh[u] : h;
+        out[row * 2 * LSTM_H + dir * LSTM_H + j] = bn_scale ? h * s_bn[0][j] + s_bn[1][j] : h;
       } else {
         h = hs[cur][q * LSTM_HS_LD + j];
       }
