@@ -2,14 +2,16 @@
 // nn.LSTM through onmt/utils/rnn_factory.py:8-17, packed sequences).
 //
 // One workgroup = 16 sequences x one direction, for ALL time steps: the
-// recurrence never leaves the CU, so a step costs one 16x512x128 MFMA
-// product + one LDS exchange instead of a kernel launch.  W_hh^T (512 x 128
-// fp32 = 256 KB per direction, too big for LDS) is held in REGISTERS across
-// the 16 waves: wave w owns gate columns [32w, 32w+32) as two 16x16 tiles of
-// v_mfma_f32_16x16x4_f32 B operands (64 floats per lane).  h_{t-1} is the A
-// operand, read from LDS.  Gates go through LDS so every thread can apply
-// the PyTorch cell (i, f, g, o order) to 2 (sequence, unit) pairs.
-//
+// recurrence never leaves the CU, so a step costs one 16x512x128 product + one
+// LDS exchange of h instead of a kernel launch.  W_hh^T (512 x 128) is held in
+// REGISTERS across the 16 waves: wave w owns the four gates (i, f, g, o) of
+// units 8w .. 8w + 7 as two 16-column tiles (i | f, g | o) of MFMA B
+// operands, split-fp16 hi/lo on v_mfma_f32_16x16x32_f16 (or fp32 on
+// v_mfma_f32_16x16x4_f32 with ND_LSTM_F32=1).  h_{t-1} is the A operand, read
+// from LDS.  A lane finds the other half of its unit's gates in lane ^ 8 (one
+// DPP move), applies the PyTorch cell (i, f, g, o order) to 2 (sequence,
+// unit) pairs and writes h to LDS: one workgroup barrier per step.
+
 // Packing semantics (pack_padded_sequence / pad_packed_sequence):
 // sequence b only processes its valid steps; the reverse direction starts
 // at t = len_b - 1.  Outputs at t >= len_b are left as the caller zeroed them.
@@ -49,7 +51,7 @@ __device__ __forceinline__ f32x4 mfma16x32h(lh8 a, lh8 b, f32x4 c) {
 #define LSTM_H 128
 #define LSTM_G 512
 #define LSTM_HS_LD (LSTM_H + 4)
-#define LSTM_GS_LD (LSTM_G + 4)
+#define LSTM_DPP_ROR8 0x128  // DPP row_ror:8: lane ^ 8 within a 16-lane row
 
 // H3: the recurrent product on v_mfma_f32_16x16x32_f16 in the split-fp16
 // form (hi*lo + lo*hi + hi*hi), W_hh scaled by a power of two per direction
@@ -64,7 +66,6 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
                 const int* __restrict__ len, int B, int T, float* __restrict__ out,  // [B*T, 256]
                 const float* __restrict__ bn_scale, const float* __restrict__ bn_shift) {
   __shared__ __attribute__((aligned(16))) float hs[2][16 * LSTM_HS_LD];
-  __shared__ float gs[16 * LSTM_GS_LD];
   __shared__ int s_len[16];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int dir = blockIdx.y;
@@ -98,7 +99,7 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
     }
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      const int n = wave * 32 + t * 16 + li;
+      const int n = (2 * t + (li >> 3)) * LSTM_H + wave * 8 + (li & 7);  // gate (2t + li/8) of unit 8w + li%8
       if constexpr (H3) {
 #pragma unroll
         for (int kb = 0; kb < 4; ++kb) {
@@ -127,14 +128,16 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
 #pragma unroll
   for (int q = 0; q < 16; ++q) maxlen = max(maxlen, s_len[q]);
 
-  // elementwise ownership: pairs p = tid and tid + 1024 -> (seq, unit)
+  // cell ownership: the lane's accumulator rows 2 (li / 8) + u (sequences
+  // 4 lq + 2 (li / 8) + u) of unit 8 wave + li % 8, whose four gates this wave
+  // produced (i | f in tile 0, g | o in tile 1; the partner lane li ^ 8 holds
+  // the other half of each), so the cell needs no exchange through LDS
   int pseq[2], punit[2];
   float c[2] = {0.f, 0.f};
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
-    const int p = tid + u * 1024;
-    pseq[u] = p >> 7;
-    punit[u] = p & 127;
+    pseq[u] = 4 * lq + 2 * (li >> 3) + u;
+    punit[u] = wave * 8 + (li & 7);
   }
   // eval BatchNorm of the next layer's input, per unit, kept in LDS (registers are the limit here)
   __shared__ float s_bn[2][LSTM_H];
@@ -212,24 +215,24 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
         }
       }
     }
+    // the partner lane's half of each tile (row_ror:8 within 16 lanes = lane ^ 8)
+    f32x4 p0, p1;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int q = lq * 4 + r;
-      gs[q * LSTM_GS_LD + wave * 32 + li] = acc0[r];
-      gs[q * LSTM_GS_LD + wave * 32 + 16 + li] = acc1[r];
+      p0[r] = dpp_mov<LSTM_DPP_ROR8>(acc0[r]);
+      p1[r] = dpp_mov<LSTM_DPP_ROR8>(acc1[r]);
     }
-    __syncthreads();
+    const bool lo = li < 8;
     // PyTorch LSTM cell (gates i, f, g, o)
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const int q = pseq[u], j = punit[u];
+      const int q = pseq[u], j = punit[u], r = 2 * (li >> 3) + u;
       float h;
       if (step < s_len[q]) {
-        const float* g = &gs[q * LSTM_GS_LD];
-        const float ig = sigm(g[j] + xc[u][0]);
-        const float fg = sigm(g[LSTM_H + j] + xc[u][1]);
-        const float gg = tanhf(g[2 * LSTM_H + j] + xc[u][2]);
-        const float og = sigm(g[3 * LSTM_H + j] + xc[u][3]);
+        const float ig = sigm((lo ? acc0[r] : p0[r]) + xc[u][0]);
+        const float fg = sigm((lo ? p0[r] : acc0[r]) + xc[u][1]);
+        const float gg = tanhf((lo ? acc1[r] : p1[r]) + xc[u][2]);
+        const float og = sigm((lo ? p1[r] : acc1[r]) + xc[u][3]);
         c[u] = fg * c[u] + ig * gg;
         h = og * tanhf(c[u]);
         const size_t row = (size_t)(b0 + q) * T + pos_of(q, step);
