@@ -33,6 +33,17 @@ __device__ __forceinline__ f32x4 mfma16x4(float a, float b, f32x4 c) {
 }
 
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+// the cell's activations on the hardware exp (v_exp_f32) and reciprocal
+// (a few ulp from the libm forms; ND_LSTM_LIBM=1 keeps expf / tanhf)
+__device__ __forceinline__ float sigm_fast(float x) { return __frcp_rn(1.0f + __expf(-x)); }
+__device__ __forceinline__ float tanh_fast(float x) {
+  const float t = __expf(-2.0f * fabsf(x));
+  return copysignf((1.0f - t) * __frcp_rn(1.0f + t), x);
+}
+template <bool FAST>
+__device__ __forceinline__ float act_sig(float x) { return FAST ? sigm_fast(x) : sigm(x); }
+template <bool FAST>
+__device__ __forceinline__ float act_tanh(float x) { return FAST ? tanh_fast(x) : tanhf(x); }
 
 typedef _Float16 lh8 __attribute__((ext_vector_type(8)));
 // split-fp16 (gemm.hip): hi = fp16(x), lo = fp16(x - hi), 22 significant bits
@@ -56,7 +67,7 @@ __device__ __forceinline__ f32x4 mfma16x32h(lh8 a, lh8 b, f32x4 c) {
 // H3: the recurrent product on v_mfma_f32_16x16x32_f16 in the split-fp16
 // form (hi*lo + lo*hi + hi*hi), W_hh scaled by a power of two per direction
 // (max |W| in [2^13, 2^14)) and h by 2^10; otherwise fp32 16x16x4 MFMAs.
-template <bool LAYER0, bool H3>
+template <bool LAYER0, bool H3, bool FAST = false>
 __global__ void __launch_bounds__(1024)
 lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projections (fwd | bwd), !LAYER0
                 const float* __restrict__ signal,  // [B, T] (LAYER0)
@@ -229,12 +240,12 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
       const int q = pseq[u], j = punit[u], r = 2 * (li >> 3) + u;
       float h;
       if (step < s_len[q]) {
-        const float ig = sigm((lo ? acc0[r] : p0[r]) + xc[u][0]);
-        const float fg = sigm((lo ? p0[r] : acc0[r]) + xc[u][1]);
-        const float gg = tanhf((lo ? acc1[r] : p1[r]) + xc[u][2]);
-        const float og = sigm((lo ? p1[r] : acc1[r]) + xc[u][3]);
+        const float ig = act_sig<FAST>((lo ? acc0[r] : p0[r]) + xc[u][0]);
+        const float fg = act_sig<FAST>((lo ? p0[r] : acc0[r]) + xc[u][1]);
+        const float gg = act_tanh<FAST>((lo ? acc1[r] : p1[r]) + xc[u][2]);
+        const float og = act_sig<FAST>((lo ? p1[r] : acc1[r]) + xc[u][3]);
         c[u] = fg * c[u] + ig * gg;
-        h = og * tanhf(c[u]);
+        h = og * act_tanh<FAST>(c[u]);
         const size_t row = (size_t)(b0 + q) * T + pos_of(q, step);
         out[row * 2 * LSTM_H + dir * LSTM_H + j] = bn_scale ? h * s_bn[0][j] + s_bn[1][j] : h;
       } else {
@@ -255,17 +266,29 @@ hipError_t launch_lstm_layer(const float* xp, const float* signal, const float* 
     const char* g = getenv("ND_GEMM_F32");
     return (e && atoi(e) != 0) || (g && atoi(g) != 0);
   }();
-#define ND_LSTM_GO(L0, H)                                                                                       \
-  hipLaunchKernelGGL((lstm_dir_kernel<L0, H>), grid, block, 0, s, xp, signal, wih0, bsum, whh, len, B, T, out, \
+  static const bool fast = [] {
+    const char* e = getenv("ND_LSTM_LIBM");  // 1: libm expf / tanhf in the cell
+    return !(e && atoi(e) != 0);
+  }();
+#define ND_LSTM_GO(L0, H, F)                                                                                       \
+  hipLaunchKernelGGL((lstm_dir_kernel<L0, H, F>), grid, block, 0, s, xp, signal, wih0, bsum, whh, len, B, T, out, \
                      bn_scale, bn_shift)
-  if (layer0 && f32)
-    ND_LSTM_GO(true, false);
-  else if (layer0)
-    ND_LSTM_GO(true, true);
-  else if (f32)
-    ND_LSTM_GO(false, false);
-  else
-    ND_LSTM_GO(false, true);
+  if (f32) {
+    if (layer0)
+      ND_LSTM_GO(true, false, false);
+    else
+      ND_LSTM_GO(false, false, false);
+  } else if (fast) {
+    if (layer0)
+      ND_LSTM_GO(true, true, true);
+    else
+      ND_LSTM_GO(false, true, true);
+  } else {
+    if (layer0)
+      ND_LSTM_GO(true, true, false);
+    else
+      ND_LSTM_GO(false, true, false);
+  }
 #undef ND_LSTM_GO
   return hipGetLastError();
 }
