@@ -1000,7 +1000,10 @@ static int translate_greedy(nd_ctx* c, const float* d_signal, const int32_t* d_l
     smp.seed = c->seed_dev;
     key.topk = topk;
     key.temp = temp;
-    HIPCHK(hipMemcpyAsync(c->seed_dev, &seed, sizeof(seed), hipMemcpyHostToDevice, c->es));
+    // the seed travels as kernel arguments (captured at launch), not through host memory
+    int* sw = reinterpret_cast<int*>(c->seed_dev);
+    HIPCHK(nd::launch_fill_i32(sw, (int)(unsigned)(seed & 0xffffffffull), 1, c->es));
+    HIPCHK(nd::launch_fill_i32(sw + 1, (int)(unsigned)(seed >> 32), 1, c->es));
   }
   if (c->timing) HIPCHK(hipEventRecord(c->ev_a, c->es));
   c->attn_on = d_attn != nullptr;
