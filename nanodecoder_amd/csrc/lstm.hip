@@ -62,6 +62,7 @@ __device__ __forceinline__ f32x4 mfma16x32h(lh8 a, lh8 b, f32x4 c) {
 #define LSTM_H 128
 #define LSTM_G 512
 #define LSTM_HS_LD (LSTM_H + 4)
+#define LSTM_HP_LD (LSTM_H + 8)  // halves
 #define LSTM_DPP_ROR8 0x128  // DPP row_ror:8: lane ^ 8 within a 16-lane row
 
 // H3: the recurrent product on v_mfma_f32_16x16x32_f16 in the split-fp16
@@ -76,7 +77,11 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
                 const float* __restrict__ whh,     // [2][512][128]
                 const int* __restrict__ len, int B, int T, float* __restrict__ out,  // [B*T, 256]
                 const float* __restrict__ bn_scale, const float* __restrict__ bn_shift) {
-  __shared__ __attribute__((aligned(16))) float hs[2][16 * LSTM_HS_LD];
+  __shared__ __attribute__((aligned(16))) float hs[H3 ? 1 : 2][16 * LSTM_HS_LD];
+  // H3: h_{t-1} 2^10 as split-fp16 planes, written once by the lane that
+  // produced it (the 16 waves read it without re-splitting); row stride 136
+  // halves = 68 banks, so the 16 rows a ds_read_b128 group reads are disjoint
+  __shared__ __attribute__((aligned(16))) _Float16 hp[H3 ? 2 : 1][2][16 * LSTM_HP_LD];
   __shared__ int s_len[16];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int dir = blockIdx.y;
@@ -133,7 +138,11 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
     }
   }
   if (tid < 16) s_len[tid] = (b0 + tid < B) ? len[b0 + tid] : 0;
-  for (int e = tid; e < 16 * LSTM_HS_LD; e += 1024) hs[0][e] = 0.f;
+  if constexpr (H3) {
+    for (int e = tid; e < 16 * LSTM_HP_LD; e += 1024) hp[0][0][e] = hp[0][1][e] = (_Float16)0.f;
+  } else {
+    for (int e = tid; e < 16 * LSTM_HS_LD; e += 1024) hs[0][e] = 0.f;
+  }
   __syncthreads();
   int maxlen = 0;
 #pragma unroll
@@ -197,14 +206,12 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
     // gates = h_{t-1} W_hh^T on MFMA
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
     if constexpr (H3) {
-      const float* hrow = &hs[cur][li * LSTM_HS_LD + 8 * lq];
+      const _Float16* hhi = &hp[cur][0][li * LSTM_HP_LD + 8 * lq];
+      const _Float16* hlo = &hp[cur][1][li * LSTM_HP_LD + 8 * lq];
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) {
-        const f32x4 a0 = ld4(hrow + kb * 32), a1 = ld4(hrow + kb * 32 + 4);
-        const float x[8] = {a0.x * LSTM_HSCALE, a0.y * LSTM_HSCALE, a0.z * LSTM_HSCALE, a0.w * LSTM_HSCALE,
-                            a1.x * LSTM_HSCALE, a1.y * LSTM_HSCALE, a1.z * LSTM_HSCALE, a1.w * LSTM_HSCALE};
-        lh8 ah, al;
-        lsplit8(x, ah, al);
+        const lh8 ah = *reinterpret_cast<const lh8*>(hhi + kb * 32);
+        const lh8 al = *reinterpret_cast<const lh8*>(hlo + kb * 32);
         acc0 = mfma16x32h(ah, wlo[0][kb], acc0);
         acc1 = mfma16x32h(ah, wlo[1][kb], acc1);
         acc0 = mfma16x32h(al, whi[0][kb], acc0);
@@ -248,10 +255,20 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
         h = og * act_tanh<FAST>(c[u]);
         const size_t row = (size_t)(b0 + q) * T + pos_of(q, step);
         out[row * 2 * LSTM_H + dir * LSTM_H + j] = bn_scale ? h * s_bn[0][j] + s_bn[1][j] : h;
+        if constexpr (H3) {
+          // the split the consumers used to form from the fp32 h (lsplit8 of h 2^10)
+          const float x = h * LSTM_HSCALE;
+          const _Float16 hi = (_Float16)x;
+          hp[cur ^ 1][0][q * LSTM_HP_LD + j] = hi;
+          hp[cur ^ 1][1][q * LSTM_HP_LD + j] = (_Float16)(x - (float)hi);
+        }
+      } else if constexpr (H3) {  // past the sequence's end: h carries over
+        hp[cur ^ 1][0][q * LSTM_HP_LD + j] = hp[cur][0][q * LSTM_HP_LD + j];
+        hp[cur ^ 1][1][q * LSTM_HP_LD + j] = hp[cur][1][q * LSTM_HP_LD + j];
       } else {
         h = hs[cur][q * LSTM_HS_LD + j];
       }
-      hs[cur ^ 1][q * LSTM_HS_LD + j] = h;
+      if constexpr (!H3) hs[cur ^ 1][q * LSTM_HS_LD + j] = h;
     }
     __syncthreads();
   }
