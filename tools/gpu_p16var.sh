@@ -1,4 +1,5 @@
-# decoder P16 GEMM slicing A/B (ND_P16_VARIANT bits, gemm.hip): GEMM parity
+# decoder P16 GEMM slicing A/B (ND_P16_VARIANT bits; the knob was removed from
+# gemm.hip after this A/B showed no change): GEMM parity
 # under each variant, then the greedy bench alternating variants, then a
 # kernel trace of the best guess
 set -u
