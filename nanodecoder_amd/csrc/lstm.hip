@@ -68,7 +68,11 @@ __device__ __forceinline__ f32x4 mfma16x32h(lh8 a, lh8 b, f32x4 c) {
 // H3: the recurrent product on v_mfma_f32_16x16x32_f16 in the split-fp16
 // form (hi*lo + lo*hi + hi*hi), W_hh scaled by a power of two per direction
 // (max |W| in [2^13, 2^14)) and h by 2^10; otherwise fp32 16x16x4 MFMAs.
-template <bool LAYER0, bool H3, bool FAST = false>
+// S8 (H3 only): 8 sequences per workgroup (twice the workgroups).  MFMA rows
+// 8-15 are zero padding, so only lanes 0-31 hold gate sums; a lower lane
+// hands the gates of its second row to lane + 32 by one v_permlane32_swap
+// per gate, and every lane runs ONE cell per step instead of two.
+template <bool LAYER0, bool H3, bool FAST = false, bool S8 = false>
 __global__ void __launch_bounds__(1024)
 lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projections (fwd | bwd), !LAYER0
                 const float* __restrict__ signal,  // [B, T] (LAYER0)
@@ -85,7 +89,9 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
   __shared__ int s_len[16];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int dir = blockIdx.y;
-  const int b0 = blockIdx.x * 16;
+  static_assert(H3 || !S8, "S8 is a split-fp16 mapping");
+  constexpr int NSEQ = S8 ? 8 : 16, NP = S8 ? 1 : 2;  // sequences per workgroup, cells per lane
+  const int b0 = blockIdx.x * NSEQ;
   const int li = lane & 15, lq = lane >> 4;
 
   // W_hh^T fragments for this wave's two 16-column tiles, k order matching
@@ -137,7 +143,7 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
       }
     }
   }
-  if (tid < 16) s_len[tid] = (b0 + tid < B) ? len[b0 + tid] : 0;
+  if (tid < 16) s_len[tid] = (tid < NSEQ && b0 + tid < B) ? len[b0 + tid] : 0;
   if constexpr (H3) {
     for (int e = tid; e < 16 * LSTM_HP_LD; e += 1024) hp[0][0][e] = hp[0][1][e] = (_Float16)0.f;
   } else {
@@ -155,8 +161,9 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
   int pseq[2], punit[2];
   float c[2] = {0.f, 0.f};
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    pseq[u] = 4 * lq + 2 * (li >> 3) + u;
+  for (int u = 0; u < NP; ++u) {
+    // S8: lane x < 32 owns the row pair's first row, lane x + 32 the second
+    pseq[u] = S8 ? 4 * ((lane & 31) >> 4) + 2 * (li >> 3) + (lane >> 5) : 4 * lq + 2 * (li >> 3) + u;
     punit[u] = wave * 8 + (li & 7);
   }
   // eval BatchNorm of the next layer's input, per unit, kept in LDS (registers are the limit here)
@@ -168,7 +175,7 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
   float w0[2][4], bb[2][4];
   if constexpr (LAYER0) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < NP; ++u)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         w0[u][g] = wih0[dir * LSTM_G + g * LSTM_H + punit[u]];
@@ -178,7 +185,7 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
   auto pos_of = [&](int q, int step) { return dir == 0 ? step : s_len[q] - 1 - step; };
   auto load_x = [&](int step, float (&x)[2][4]) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < NP; ++u) {
       const int q = pseq[u];
       const bool act = step < s_len[q];
       const int pos = act ? pos_of(q, step) : 0;
@@ -198,7 +205,7 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
     const int cur = step & 1;
     float xc[2][4];
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < NP; ++u)
 #pragma unroll
       for (int g = 0; g < 4; ++g) xc[u][g] = LAYER0 ? xn[u][0] * w0[u][g] + bb[u][g] : xn[u][g];
     if (step + 1 < maxlen) load_x(step + 1, xn);  // prefetch next step's projections
@@ -241,16 +248,43 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
       p1[r] = dpp_mov<LSTM_DPP_ROR8>(acc1[r]);
     }
     const bool lo = li < 8;
+    // gate sums (i, f, g, o) of accumulator row r of this lane's unit
+    auto gates = [&](int r, float (&z)[4]) {
+      z[0] = lo ? acc0[r] : p0[r];
+      z[1] = lo ? p0[r] : acc0[r];
+      z[2] = lo ? acc1[r] : p1[r];
+      z[3] = lo ? p1[r] : acc1[r];
+    };
+    float zg[NP][4];
+    if constexpr (S8) {
+      // lower lane: row 2 (li / 8) itself, row 2 (li / 8) + 1 to lane + 32
+      float za[4], zb[4];
+      gates(0, za);
+      gates(2, zb);
+      float zc[4], zd[4];
+      gates(1, zc);
+      gates(3, zd);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float own = lo ? za[g] : zb[g], send = lo ? zc[g] : zd[g];
+        float a_, b_;
+        lane_swap<true>(send, a_, b_);  // upper lanes: a_ = the lower partner's send
+        zg[0][g] = (lane >> 5) ? a_ : own;
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < NP; ++u) gates(2 * (li >> 3) + u, zg[u]);
+    }
     // PyTorch LSTM cell (gates i, f, g, o)
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int q = pseq[u], j = punit[u], r = 2 * (li >> 3) + u;
+    for (int u = 0; u < NP; ++u) {
+      const int q = pseq[u], j = punit[u];
       float h;
       if (step < s_len[q]) {
-        const float ig = act_sig<FAST>((lo ? acc0[r] : p0[r]) + xc[u][0]);
-        const float fg = act_sig<FAST>((lo ? p0[r] : acc0[r]) + xc[u][1]);
-        const float gg = act_tanh<FAST>((lo ? acc1[r] : p1[r]) + xc[u][2]);
-        const float og = act_sig<FAST>((lo ? p1[r] : acc1[r]) + xc[u][3]);
+        const float ig = act_sig<FAST>(zg[u][0] + xc[u][0]);
+        const float fg = act_sig<FAST>(zg[u][1] + xc[u][1]);
+        const float gg = act_tanh<FAST>(zg[u][2] + xc[u][2]);
+        const float og = act_sig<FAST>(zg[u][3] + xc[u][3]);
         c[u] = fg * c[u] + ig * gg;
         h = og * act_tanh<FAST>(c[u]);
         const size_t row = (size_t)(b0 + q) * T + pos_of(q, step);
@@ -277,7 +311,6 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
 hipError_t launch_lstm_layer(const float* xp, const float* signal, const float* wih0, const float* bsum,
                              const float* whh, const int* len, int B, int T, float* out, const float* bn_scale,
                              const float* bn_shift, bool layer0, hipStream_t s) {
-  dim3 grid((B + 15) / 16, 2), block(1024);
   static const bool f32 = [] {
     const char* e = getenv("ND_LSTM_F32");  // 1: fp32 MFMAs for the recurrence
     const char* g = getenv("ND_GEMM_F32");
@@ -287,25 +320,39 @@ hipError_t launch_lstm_layer(const float* xp, const float* signal, const float* 
     const char* e = getenv("ND_LSTM_LIBM");  // 1: libm expf / tanhf in the cell
     return !(e && atoi(e) != 0);
   }();
-#define ND_LSTM_GO(L0, H, F)                                                                                       \
-  hipLaunchKernelGGL((lstm_dir_kernel<L0, H, F>), grid, block, 0, s, xp, signal, wih0, bsum, whh, len, B, T, out, \
+  static const bool s16 = [] {
+    const char* e = getenv("ND_LSTM_SEQ16");  // 1: 16 sequences per workgroup on the split-fp16 path
+    return e && atoi(e) != 0;
+  }();
+  const bool s8 = !f32 && !s16;
+  dim3 grid(s8 ? (B + 7) / 8 : (B + 15) / 16, 2), block(1024);
+#define ND_LSTM_GO(L0, H, F, S)                                                                                       \
+  hipLaunchKernelGGL((lstm_dir_kernel<L0, H, F, S>), grid, block, 0, s, xp, signal, wih0, bsum, whh, len, B, T, out, \
                      bn_scale, bn_shift)
+#define ND_LSTM_H3(F)                  \
+  do {                                 \
+    if (s8) {                          \
+      if (layer0)                      \
+        ND_LSTM_GO(true, true, F, true);  \
+      else                             \
+        ND_LSTM_GO(false, true, F, true); \
+    } else if (layer0) {               \
+      ND_LSTM_GO(true, true, F, false);   \
+    } else {                           \
+      ND_LSTM_GO(false, true, F, false);  \
+    }                                  \
+  } while (0)
   if (f32) {
     if (layer0)
-      ND_LSTM_GO(true, false, false);
+      ND_LSTM_GO(true, false, false, false);
     else
-      ND_LSTM_GO(false, false, false);
+      ND_LSTM_GO(false, false, false, false);
   } else if (fast) {
-    if (layer0)
-      ND_LSTM_GO(true, true, true);
-    else
-      ND_LSTM_GO(false, true, true);
+    ND_LSTM_H3(true);
   } else {
-    if (layer0)
-      ND_LSTM_GO(true, true, false);
-    else
-      ND_LSTM_GO(false, true, false);
+    ND_LSTM_H3(false);
   }
+#undef ND_LSTM_H3
 #undef ND_LSTM_GO
   return hipGetLastError();
 }
