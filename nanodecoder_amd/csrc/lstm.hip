@@ -68,12 +68,17 @@ __device__ __forceinline__ f32x4 mfma16x32h(lh8 a, lh8 b, f32x4 c) {
 // H3: the recurrent product on v_mfma_f32_16x16x32_f16 in the split-fp16
 // form (hi*lo + lo*hi + hi*hi), W_hh scaled by a power of two per direction
 // (max |W| in [2^13, 2^14)) and h by 2^10; otherwise fp32 16x16x4 MFMAs.
-// S8 (H3 only): 8 sequences per workgroup (twice the workgroups).  MFMA rows
-// 8-15 are zero padding, so only lanes 0-31 hold gate sums; a lower lane
-// hands the gates of its second row to lane + 32 by one v_permlane32_swap
-// per gate, and every lane runs ONE cell per step instead of two.
-template <bool LAYER0, bool H3, bool FAST = false, bool S8 = false>
-__global__ void __launch_bounds__(1024)
+// NS < 16 (H3 only): fewer sequences per workgroup, more workgroups.  MFMA
+// rows NS..15 are zero padding, so only the lanes of the first NS/4 16-lane
+// rows hold gate sums; they hand them to the other rows by
+// v_permlane16/32_swap, and every lane runs ONE cell per step instead of two.
+//  NS = 8: 16 waves x 8 units; a lower lane keeps its row 2 (li / 8) and
+//          hands row 2 (li / 8) + 1 to lane + 32.
+//  NS = 4: 8 waves x 16 units (four tiles: i|f, g|o of units 0-7, then 8-15);
+//          row-0 lane li holds all 8 (unit group, sequence) combinations of
+//          unit li % 8 and sends combination k to 16-lane row k >> 1.
+template <bool LAYER0, bool H3, bool FAST = false, int NS = 16>
+__global__ void __launch_bounds__(NS == 4 ? 512 : 1024)
 lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projections (fwd | bwd), !LAYER0
                 const float* __restrict__ signal,  // [B, T] (LAYER0)
                 const float* __restrict__ wih0,    // [2][512] (LAYER0, input_size 1)
@@ -89,16 +94,19 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
   __shared__ int s_len[16];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int dir = blockIdx.y;
-  static_assert(H3 || !S8, "S8 is a split-fp16 mapping");
-  constexpr int NSEQ = S8 ? 8 : 16, NP = S8 ? 1 : 2;  // sequences per workgroup, cells per lane
-  const int b0 = blockIdx.x * NSEQ;
+  static_assert(H3 || NS == 16, "NS < 16 is a split-fp16 mapping");
+  static_assert(NS == 16 || NS == 8 || NS == 4, "sequences per workgroup");
+  constexpr int NWAVE = NS == 4 ? 8 : 16, NTH = NWAVE * 64;
+  constexpr int UPW = LSTM_H / NWAVE, NT = UPW / 4;  // units and 16-column tiles per wave
+  constexpr int NP = NS == 16 ? 2 : 1;               // cells per lane
+  const int b0 = blockIdx.x * NS;
   const int li = lane & 15, lq = lane >> 4;
 
   // W_hh^T fragments for this wave's two 16-column tiles, k order matching
   // the A fragment: fp32, block kb, step s <-> k = 16*kb + 4*lq + s; H3,
   // block kb (32 k), slot j <-> k = 32*kb + 8*lq + j
   float wr[2][32];
-  lh8 whi[2][4], wlo[2][4];
+  lh8 whi[NT][4], wlo[NT][4];
   float unscale = 1.f;
   {
     const float* W = whh + (size_t)dir * LSTM_G * LSTM_H;
@@ -106,13 +114,13 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
     if constexpr (H3) {
       __shared__ float s_max[16];
       float m = 0.f;
-      for (int e = tid; e < LSTM_G * LSTM_H; e += 1024) m = fmaxf(m, fabsf(W[e]));
+      for (int e = tid; e < LSTM_G * LSTM_H; e += NTH) m = fmaxf(m, fabsf(W[e]));
       m = wave_max(m);
       if (lane == 0) s_max[wave] = m;
       __syncthreads();
       m = 0.f;
 #pragma unroll
-      for (int w = 0; w < 16; ++w) m = fmaxf(m, s_max[w]);
+      for (int w = 0; w < NWAVE; ++w) m = fmaxf(m, s_max[w]);
       int ex = 0;
       frexpf(m, &ex);  // m = f * 2^ex, f in [0.5, 1)
       const int sh = m > 0.f ? 14 - ex : 0;
@@ -120,8 +128,9 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
       unscale = ldexpf(1.f, -sh) / LSTM_HSCALE;
     }
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int n = (2 * t + (li >> 3)) * LSTM_H + wave * 8 + (li & 7);  // gate (2t + li/8) of unit 8w + li%8
+    for (int t = 0; t < NT; ++t) {
+      // gate 2 (t % 2) + li / 8 of unit UPW w + 8 (t / 2) + li % 8
+      const int n = (2 * (t & 1) + (li >> 3)) * LSTM_H + wave * UPW + 8 * (t >> 1) + (li & 7);
       if constexpr (H3) {
 #pragma unroll
         for (int kb = 0; kb < 4; ++kb) {
@@ -143,11 +152,11 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
       }
     }
   }
-  if (tid < 16) s_len[tid] = (tid < NSEQ && b0 + tid < B) ? len[b0 + tid] : 0;
+  if (tid < 16) s_len[tid] = (tid < NS && b0 + tid < B) ? len[b0 + tid] : 0;
   if constexpr (H3) {
-    for (int e = tid; e < 16 * LSTM_HP_LD; e += 1024) hp[0][0][e] = hp[0][1][e] = (_Float16)0.f;
+    for (int e = tid; e < 16 * LSTM_HP_LD; e += NTH) hp[0][0][e] = hp[0][1][e] = (_Float16)0.f;
   } else {
-    for (int e = tid; e < 16 * LSTM_HS_LD; e += 1024) hs[0][e] = 0.f;
+    for (int e = tid; e < 16 * LSTM_HS_LD; e += NTH) hs[0][e] = 0.f;
   }
   __syncthreads();
   int maxlen = 0;
@@ -162,9 +171,16 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
   float c[2] = {0.f, 0.f};
 #pragma unroll
   for (int u = 0; u < NP; ++u) {
-    // S8: lane x < 32 owns the row pair's first row, lane x + 32 the second
-    pseq[u] = S8 ? 4 * ((lane & 31) >> 4) + 2 * (li >> 3) + (lane >> 5) : 4 * lq + 2 * (li >> 3) + u;
-    punit[u] = wave * 8 + (li & 7);
+    if constexpr (NS == 16) {
+      pseq[u] = 4 * lq + 2 * (li >> 3) + u;
+      punit[u] = wave * 8 + (li & 7);
+    } else if constexpr (NS == 8) {  // lane x < 32 owns its row pair's first row, lane x + 32 the second
+      pseq[u] = 4 * ((lane & 31) >> 4) + 2 * (li >> 3) + (lane >> 5);
+      punit[u] = wave * 8 + (li & 7);
+    } else {  // 16-lane row k >> 1 = lq: combination k = 2 lq + li / 8
+      pseq[u] = 2 * (lq & 1) + (li >> 3);
+      punit[u] = wave * UPW + 8 * (lq >> 1) + (li & 7);
+    }
   }
   // eval BatchNorm of the next layer's input, per unit, kept in LDS (registers are the limit here)
   __shared__ float s_bn[2][LSTM_H];
@@ -211,7 +227,9 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
     if (step + 1 < maxlen) load_x(step + 1, xn);  // prefetch next step's projections
 
     // gates = h_{t-1} W_hh^T on MFMA
-    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    f32x4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = {0.f, 0.f, 0.f, 0.f};
     if constexpr (H3) {
       const _Float16* hhi = &hp[cur][0][li * LSTM_HP_LD + 8 * lq];
       const _Float16* hlo = &hp[cur][1][li * LSTM_HP_LD + 8 * lq];
@@ -219,15 +237,15 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
       for (int kb = 0; kb < 4; ++kb) {
         const lh8 ah = *reinterpret_cast<const lh8*>(hhi + kb * 32);
         const lh8 al = *reinterpret_cast<const lh8*>(hlo + kb * 32);
-        acc0 = mfma16x32h(ah, wlo[0][kb], acc0);
-        acc1 = mfma16x32h(ah, wlo[1][kb], acc1);
-        acc0 = mfma16x32h(al, whi[0][kb], acc0);
-        acc1 = mfma16x32h(al, whi[1][kb], acc1);
-        acc0 = mfma16x32h(ah, whi[0][kb], acc0);
-        acc1 = mfma16x32h(ah, whi[1][kb], acc1);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = mfma16x32h(ah, wlo[t][kb], acc[t]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = mfma16x32h(al, whi[t][kb], acc[t]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = mfma16x32h(ah, whi[t][kb], acc[t]);
       }
-      acc0 *= unscale;
-      acc1 *= unscale;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] *= unscale;
     } else {
       const float* hrow = &hs[cur][li * LSTM_HS_LD + 4 * lq];
 #pragma unroll
@@ -235,28 +253,54 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
         const f32x4 a = ld4(hrow + kb * 16);
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          acc0 = mfma16x4(a[s], wr[0][kb * 4 + s], acc0);
-          acc1 = mfma16x4(a[s], wr[1][kb * 4 + s], acc1);
+          acc[0] = mfma16x4(a[s], wr[0][kb * 4 + s], acc[0]);
+          acc[1] = mfma16x4(a[s], wr[1][kb * 4 + s], acc[1]);
         }
       }
     }
     // the partner lane's half of each tile (row_ror:8 within 16 lanes = lane ^ 8)
-    f32x4 p0, p1;
+    f32x4 pt[NT];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      p0[r] = dpp_mov<LSTM_DPP_ROR8>(acc0[r]);
-      p1[r] = dpp_mov<LSTM_DPP_ROR8>(acc1[r]);
-    }
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pt[t][r] = dpp_mov<LSTM_DPP_ROR8>(acc[t][r]);
     const bool lo = li < 8;
-    // gate sums (i, f, g, o) of accumulator row r of this lane's unit
-    auto gates = [&](int r, float (&z)[4]) {
-      z[0] = lo ? acc0[r] : p0[r];
-      z[1] = lo ? p0[r] : acc0[r];
-      z[2] = lo ? acc1[r] : p1[r];
-      z[3] = lo ? p1[r] : acc1[r];
+    // gate sums (i, f, g, o) of accumulator row r of this lane's unit in unit group ug
+    auto gates_g = [&](int ug, int r, float (&z)[4]) {
+      z[0] = lo ? acc[2 * ug][r] : pt[2 * ug][r];
+      z[1] = lo ? pt[2 * ug][r] : acc[2 * ug][r];
+      z[2] = lo ? acc[2 * ug + 1][r] : pt[2 * ug + 1][r];
+      z[3] = lo ? pt[2 * ug + 1][r] : acc[2 * ug + 1][r];
     };
+    auto gates = [&](int r, float (&z)[4]) { gates_g(0, r, z); };
     float zg[NP][4];
-    if constexpr (S8) {
+    if constexpr (NS == 4) {
+      // row-0 lane li: v_q = the gate sums 16-lane row q will own
+      float v0[4], v1[4], v2[4], v3[4], t_[4];
+      gates_g(0, 0, v0);  // per target row q: (ug = q >> 1, r = 2 (q & 1) + li / 8)
+      gates_g(0, 1, t_);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) v0[g] = lo ? v0[g] : t_[g];
+      gates_g(0, 2, v1);
+      gates_g(0, 3, t_);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) v1[g] = lo ? v1[g] : t_[g];
+      gates_g(1, 0, v2);
+      gates_g(1, 1, t_);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) v2[g] = lo ? v2[g] : t_[g];
+      gates_g(1, 2, v3);
+      gates_g(1, 3, t_);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        v3[g] = lo ? v3[g] : t_[g];
+        float a1, b1, a3, b3, a23, b23;
+        lane_swap<false>(v1[g], a1, b1);  // odd rows: the value of the row below
+        lane_swap<false>(v3[g], a3, b3);
+        lane_swap<true>(lq == 0 ? v2[g] : a3, a23, b23);  // upper half: rows 0, 1 -> 2, 3
+        zg[0][g] = lq == 0 ? v0[g] : lq == 1 ? a1 : a23;
+      }
+    } else if constexpr (NS == 8) {
       // lower lane: row 2 (li / 8) itself, row 2 (li / 8) + 1 to lane + 32
       float za[4], zb[4];
       gates(0, za);
@@ -320,38 +364,43 @@ hipError_t launch_lstm_layer(const float* xp, const float* signal, const float* 
     const char* e = getenv("ND_LSTM_LIBM");  // 1: libm expf / tanhf in the cell
     return !(e && atoi(e) != 0);
   }();
-  static const bool s16 = [] {
-    const char* e = getenv("ND_LSTM_SEQ16");  // 1: 16 sequences per workgroup on the split-fp16 path
-    return e && atoi(e) != 0;
+  static const int ns_env = [] {
+    const char* e = getenv("ND_LSTM_SEQ");  // sequences per workgroup on the split-fp16 path: 16, 8 or 4
+    const int v = e ? atoi(e) : 4;  // measured: 0.95 ms per layer at 4, 1.04 at 8, 1.52 at 16
+    return v == 16 || v == 8 ? v : 4;
   }();
-  const bool s8 = !f32 && !s16;
-  dim3 grid(s8 ? (B + 7) / 8 : (B + 15) / 16, 2), block(1024);
+  const int ns = f32 ? 16 : ns_env;
+  dim3 grid((B + ns - 1) / ns, 2), block(ns == 4 ? 512 : 1024);
 #define ND_LSTM_GO(L0, H, F, S)                                                                                       \
   hipLaunchKernelGGL((lstm_dir_kernel<L0, H, F, S>), grid, block, 0, s, xp, signal, wih0, bsum, whh, len, B, T, out, \
                      bn_scale, bn_shift)
-#define ND_LSTM_H3(F)                  \
-  do {                                 \
-    if (s8) {                          \
-      if (layer0)                      \
-        ND_LSTM_GO(true, true, F, true);  \
-      else                             \
-        ND_LSTM_GO(false, true, F, true); \
-    } else if (layer0) {               \
-      ND_LSTM_GO(true, true, F, false);   \
-    } else {                           \
-      ND_LSTM_GO(false, true, F, false);  \
-    }                                  \
+#define ND_LSTM_NS(F, S)                \
+  do {                                  \
+    if (layer0)                         \
+      ND_LSTM_GO(true, true, F, S);     \
+    else                                \
+      ND_LSTM_GO(false, true, F, S);    \
+  } while (0)
+#define ND_LSTM_H3(F)                   \
+  do {                                  \
+    if (ns == 4)                        \
+      ND_LSTM_NS(F, 4);                 \
+    else if (ns == 8)                   \
+      ND_LSTM_NS(F, 8);                 \
+    else                                \
+      ND_LSTM_NS(F, 16);                \
   } while (0)
   if (f32) {
     if (layer0)
-      ND_LSTM_GO(true, false, false, false);
+      ND_LSTM_GO(true, false, false, 16);
     else
-      ND_LSTM_GO(false, false, false, false);
+      ND_LSTM_GO(false, false, false, 16);
   } else if (fast) {
     ND_LSTM_H3(true);
   } else {
     ND_LSTM_H3(false);
   }
+#undef ND_LSTM_NS
 #undef ND_LSTM_H3
 #undef ND_LSTM_GO
   return hipGetLastError();
