@@ -1,16 +1,19 @@
 // NanoEncoder BiLSTM recurrence on gfx950 (encoder/nano_encoder.py:79-124,
 // nn.LSTM through onmt/utils/rnn_factory.py:8-17, packed sequences).
 //
-// One workgroup = 16 sequences x one direction, for ALL time steps: the
-// recurrence never leaves the CU, so a step costs one 16x512x128 product + one
-// LDS exchange of h instead of a kernel launch.  W_hh^T (512 x 128) is held in
-// REGISTERS across the 16 waves: wave w owns the four gates (i, f, g, o) of
-// units 8w .. 8w + 7 as two 16-column tiles (i | f, g | o) of MFMA B
-// operands, split-fp16 hi/lo on v_mfma_f32_16x16x32_f16 (or fp32 on
-// v_mfma_f32_16x16x4_f32 with ND_LSTM_F32=1).  h_{t-1} is the A operand, read
-// from LDS.  A lane finds the other half of its unit's gates in lane ^ 8 (one
-// DPP move), applies the PyTorch cell (i, f, g, o order) to 2 (sequence,
-// unit) pairs and writes h to LDS: one workgroup barrier per step.
+// One workgroup = NS sequences (16, 8 or 4; default 4, ND_LSTM_SEQ) x one
+// direction, for ALL time steps: the recurrence never leaves the CU, so a
+// step costs one 16x512x128 product + one LDS exchange of h instead of a
+// kernel launch.  W_hh^T (512 x 128) is held in REGISTERS across the waves:
+// with 16 waves, wave w owns the four gates (i, f, g, o) of units
+// 8w .. 8w + 7 as two 16-column tiles (i | f, g | o) of MFMA B operands (8
+// waves: 16 units, four tiles), split-fp16 hi/lo on v_mfma_f32_16x16x32_f16
+// (or fp32 on v_mfma_f32_16x16x4_f32 with ND_LSTM_F32=1, NS = 16).  h_{t-1}
+// is the A operand, read from LDS (rows NS..15 zero).  A lane finds the other
+// half of its unit's gates in lane ^ 8 (one DPP move); with NS < 16 the gate
+// sums then fan out to the lanes of the padding rows (permlane swaps), and
+// each lane applies the PyTorch cell (i, f, g, o order) to 1 (NS < 16) or 2
+// (sequence, unit) pairs and writes h to LDS: one workgroup barrier per step.
 
 // Packing semantics (pack_padded_sequence / pad_packed_sequence):
 // sequence b only processes its valid steps; the reverse direction starts
