@@ -109,7 +109,7 @@ def _pmc_traffic(name):
         return None
 
 
-def kernel_roofline(eng, B, mode, beam):
+def kernel_roofline(eng, B, mode, beam, encoder="transformer"):
     """Dominant kernel of the translate step, timed LIVE: every launch of it
     inside the timed graph replays carries in-kernel wall-clock stamps
     (first workgroup start, last workgroup end; Engine.set_kernel_stamps), and
@@ -143,6 +143,9 @@ def kernel_roofline(eng, B, mode, beam):
            "timing": "in-kernel wall-clock stamps, launches of the last timed call"}
     out.update(extra)
     dev = eng.device
+    if encoder == "nano":
+        out["lstm_kernel"] = lstm_view(dev, B, T)
+        return out
     import ctypes
     from nanodecoder_amd import _lib
     from nanodecoder_amd.engine import op_fold_layernorm, op_split_weight
@@ -171,6 +174,32 @@ def kernel_roofline(eng, B, mode, beam):
                           "unit": "TFLOP/s fp32-equivalent (fp16 MFMA peak / 3 products)",
                           "frac": round(tf / peak, 4), "avg_launch_ms": round(gms, 4)}
     return out
+
+
+def lstm_view(dev, B, T):
+    """The NanoEncoder's recurrence (lstm_dir_kernel, one BiLSTM layer in
+    its layer-1 form) timed alone: latency-bound (T sequential steps, one
+    workgroup barrier each), so the figure of merit is the time per step; the
+    MFMA rate counts the algorithmic recurrent product 2 x 2 directions x B x
+    512 gates x 128 per step against the dense fp16 peak / 3 (split-fp16)."""
+    from nanodecoder_amd.engine import op_lstm_layer
+    g = torch.Generator(device="cpu").manual_seed(3)
+    whh = ((torch.rand(2, 512, 128, generator=g) - 0.5) * 0.2).to(dev)
+    xp = torch.randn(B * T, 1024, generator=g).to(dev)
+    lens = torch.full((B,), T, dtype=torch.int32, device=dev)
+    out = torch.zeros(B * T, 256, device=dev)
+
+    def layer(i):
+        op_lstm_layer(whh, lens, T, xp=xp, out=out)
+    for i in range(2):
+        layer(i)
+    ms = _time(layer, 5)
+    flops = 2.0 * 2 * B * 512 * 128 * T
+    tf = flops / (ms * 1e-3) / 1e12
+    return {"kernel": "lstm_dir_kernel (BiLSTM layer, split-fp16)", "bound": "latency",
+            "avg_launch_ms": round(ms, 4), "us_per_step": round(ms * 1e3 / T, 3),
+            "achieved": round(tf, 2), "peak": round(2516.6 / 3, 1),
+            "unit": "TFLOP/s fp32-equivalent (fp16 MFMA peak / 3 products)", "frac": round(tf / (2516.6 / 3), 4)}
 
 
 def main():
@@ -247,7 +276,7 @@ def main():
         res["decoder_steps_executed"] = int(out["steps"].cpu().item())
     if rank == 0:
         if not args.no_roofline:
-            res["roofline"] = kernel_roofline(eng, args.batch, args.mode, beam)
+            res["roofline"] = kernel_roofline(eng, args.batch, args.mode, beam, args.encoder)
         if args.cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(cfg, W, sig_np, lens_np, args)
         print(json.dumps(res), flush=True)

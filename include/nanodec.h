@@ -322,6 +322,19 @@ int nd_op_dec_self_attention(const float* qkv, float* cache, const int32_t* anc,
 int nd_op_dec_mem_attention(const float* qp, const float* mem, const float* signal, const int32_t* span, float pad_val,
                             float* out, int32_t C, int32_t rpc, int32_t T, int32_t ldT, void* stream);
 
+/* One NanoEncoder BiLSTM layer, both directions (encoder/nano_encoder.py:92-111,
+ * nn.LSTM(in, 128, bidirectional) over packed sequences): out [B*T, 256]
+ * (fwd | bwd per row b*T + t) for t < len[b]; rows t >= len[b] are left as
+ * the caller set them (pad_packed_sequence zeros).  layer0 != 0: input_size
+ * 1, xp unused, the projection signal[b*T+t] * wih0[dir][g] + bsum[dir][g]
+ * ([2][512] each) is formed in-kernel; otherwise xp [B*T, 1024] holds
+ * x W_ih^T + b_ih + b_hh (fwd | bwd).  whh [2][512][128] (gates i, f, g, o).
+ * bn_scale/bn_shift ([2][128], nullable): eval BatchNorm applied to the
+ * written h. */
+int nd_op_lstm_layer(const float* xp, const float* signal, const float* wih0, const float* bsum, const float* whh,
+                     const int32_t* len, int32_t B, int32_t T, float* out, const float* bn_scale,
+                     const float* bn_shift, int32_t layer0, void* stream);
+
 /* Encoder output x [B*T, 256] row-major -> memory bank, row-major with ldT
  * rows per chunk (LayerNorm with ln_g/ln_b when ln_g != NULL,
  * encoder/transformer.py:125; rows t >= T zero). */

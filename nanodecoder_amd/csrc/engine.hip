@@ -1435,6 +1435,17 @@ int nd_op_dec_mem_attention(const float* qp, const float* mem, const float* sign
   return ND_OK;
 }
 
+int nd_op_lstm_layer(const float* xp, const float* signal, const float* wih0, const float* bsum, const float* whh,
+                     const int32_t* len, int32_t B, int32_t T, float* out, const float* bn_scale,
+                     const float* bn_shift, int32_t layer0, void* stream) {
+  if (B < 1 || T < 1 || !whh || !len || !out || (layer0 ? (!signal || !wih0 || !bsum) : !xp))
+    return fail(ND_ERR_ARG, "lstm_layer: bad arguments");
+  hipError_t e = nd::launch_lstm_layer(xp, signal, wih0, bsum, whh, len, B, T, out, bn_scale, bn_shift, layer0 != 0,
+                                       (hipStream_t)stream);
+  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("lstm_layer: ") + hipGetErrorString(e));
+  return ND_OK;
+}
+
 int nd_normalize_reads(const double* d_raw, const int64_t* d_offsets, int32_t R, int32_t method, float* d_out,
                        void* stream) {
   hipError_t e = nd::launch_read_normalize(d_raw, (const long long*)d_offsets, R, method, d_out, (hipStream_t)stream);

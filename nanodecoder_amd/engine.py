@@ -389,6 +389,23 @@ def op_dec_mem_attention(qp, mem_p, signal, span, pad_val, rpc, out=None):
     return out
 
 
+def op_lstm_layer(whh, lens, T, xp=None, signal=None, wih0=None, bsum=None, bn_scale=None, bn_shift=None,
+                  out=None):
+    """One BiLSTM layer (both directions) through nd_op_lstm_layer:
+    whh [2, 512, 128], lens [B] int32 on the device.  Layer 0: signal [B, T],
+    wih0 / bsum [2, 512]; otherwise xp [B*T, 1024] = x W_ih^T + b_ih + b_hh
+    (fwd | bwd).  Returns out [B*T, 256] (zeros at t >= len)."""
+    B = lens.shape[0]
+    dev = whh.device
+    if out is None:
+        out = torch.zeros(B * T, 256, dtype=torch.float32, device=dev)
+    s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    _lib.check(_lib.lib().nd_op_lstm_layer(_ptr(xp), _ptr(signal), _ptr(wih0), _ptr(bsum), _ptr(whh), _ptr(lens), B,
+                                           T, _ptr(out), _ptr(bn_scale), _ptr(bn_shift), int(xp is None), s),
+               "nd_op_lstm_layer")
+    return out
+
+
 def pad_chunks(chunks: Sequence[np.ndarray], T: Optional[int] = None):
     """make_nano (inputters/inputter.py:86-95): zero pad to [B, T]."""
     lens = np.array([len(c) for c in chunks], np.int32)

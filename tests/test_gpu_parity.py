@@ -630,3 +630,56 @@ def test_cli_gpu_frontend_matches_host(tmp_path, monkeypatch):
         assert len(ra) == len(rb)
         for ca, cb in zip(ra, rb):
             assert ca.dtype == cb.dtype == np.float32 and (ca.view(np.uint32) == cb.view(np.uint32)).all()
+
+
+@pytest.mark.parametrize("layer0,bn", [(True, False), (False, False), (False, True)])
+def test_nano_lstm_layer_vs_torch_lstm(layer0, bn):
+    """One BiLSTM layer through nd_op_lstm_layer against torch.nn.LSTM (CPU,
+    fp32) over packed ragged sequences (encoder/nano_encoder.py:92-111: pack,
+    bidirectional LSTM, unpack with zeros past each length, eval BatchNorm).
+    B = 6 leaves a partly filled last workgroup at every sequences-per-
+    workgroup setting (ND_LSTM_SEQ 16 / 8 / 4).  Tolerance 1e-4 absolute:
+    split-fp16 recurrent products (22-bit operands) and the hardware exp /
+    reciprocal in the cell, over 48 steps."""
+    from torch.nn.utils.rnn import pack_padded_sequence, pad_packed_sequence
+
+    from nanodecoder_amd.engine import op_lstm_layer
+    g = torch.Generator().manual_seed(7 + 2 * layer0 + bn)
+    B, T, H = 6, 48, 128
+    insz = 1 if layer0 else 256
+    lstm = torch.nn.LSTM(insz, H, bidirectional=True)
+    with torch.no_grad():
+        for p in lstm.parameters():
+            p.uniform_(-0.15, 0.15, generator=g)
+        lens = torch.tensor([48, 48, 40, 33, 17, 5])
+        x = torch.randn(T, B, insz, generator=g)
+        y, _ = lstm(pack_padded_sequence(x, lens))
+        y, _ = pad_packed_sequence(y, total_length=T)
+    ref = y.transpose(0, 1).reshape(B * T, 2 * H)
+    whh = torch.stack([lstm.weight_hh_l0, lstm.weight_hh_l0_reverse]).detach()
+    bsum = torch.stack([lstm.bias_ih_l0 + lstm.bias_hh_l0,
+                        lstm.bias_ih_l0_reverse + lstm.bias_hh_l0_reverse]).detach()
+    wih = [lstm.weight_ih_l0.detach(), lstm.weight_ih_l0_reverse.detach()]
+    dev = torch.device("cuda", 0)
+    kw = {}
+    if bn:
+        scale = torch.rand(2, H, generator=g) + 0.5
+        shift = torch.randn(2, H, generator=g) * 0.1
+        kw = {"bn_scale": scale.to(dev), "bn_shift": shift.to(dev)}
+        valid = (torch.arange(T)[None, :] < lens[:, None]).reshape(B * T, 1)
+        ref = torch.where(valid, ref * scale.reshape(1, -1) + shift.reshape(1, -1), ref)
+    if layer0:
+        signal = x[:, :, 0].T.contiguous()
+        wih0 = torch.stack([w[:, 0] for w in wih])
+        out = op_lstm_layer(whh.to(dev), lens.int().to(dev), T, signal=signal.to(dev), wih0=wih0.to(dev),
+                            bsum=bsum.to(dev), **kw)
+    else:
+        xb = x.transpose(0, 1).reshape(B * T, insz)
+        xp = torch.cat([xb @ wih[0].T + bsum[0], xb @ wih[1].T + bsum[1]], dim=1).contiguous()
+        out = op_lstm_layer(whh.to(dev), lens.int().to(dev), T, xp=xp.to(dev), **kw)
+    torch.cuda.synchronize()
+    got = out.cpu()
+    pad = ~(torch.arange(T)[None, :] < lens[:, None]).reshape(B * T)
+    assert (got[pad] == 0).all(), "rows past a sequence's length must stay zero"
+    err = float((got - ref).abs().max())
+    assert err < 1e-4, err
