@@ -7,9 +7,26 @@ workload = BASELINE.json configs[1]: 3+3 transformer, d_model 256, T 512,
 batch 256 chunks per GPU, greedy, max_length 100, random-init weights of the
 reference architecture (no trained checkpoint exists offline).
 
-Multi-GPU (``torch.distributed.run``): reads shard across ranks with no
-collective in the hot loop ("scaling": "weak" — every rank translates its own
-batch); rank 0 loads/creates the weights and broadcasts them once over RCCL.
+Multi-GPU: ``--gpus N`` starts N rank processes itself (torch.distributed.run,
+spawned before this process touches the GPU) unless it already runs under a
+launcher (WORLD_SIZE set).  Reads shard across ranks with no collective in the
+hot loop ("scaling": "weak"); rank 0 creates the weights and broadcasts them
+once over RCCL.
+
+Beside the headline ``value`` the line carries, on every run:
+  roofline      the dominant kernel against its HBM roofline (live in-kernel
+                timing) + the encoder FFN1 GEMM against the MFMA peak;
+  mfma          algorithmic MFMA utilisation, path-level and encoder-only,
+                against the fp32 peak and the split-fp16 fp32-equivalent peak
+                (and the committed rocprof counter pass, profiles/);
+  exact_fp32    the same workload with every product in exact fp32;
+  host_inclusive the same batches through Translator (host packing, H2D,
+                token D2H) — PCIe-inclusive, never ``value``;
+  read_shard    BASELINE configs[4]: the synthetic read set sharded over the
+                ranks (front end + packing + engine), samples/s, bases/s,
+                per-rank load, world size;
+  cpu_baseline  the CPU oracle at configs[0]'s batch 50 (rank 0, N=1).
+``--workload reads`` makes configs[4] the headline.
 
 Prints ONE JSON line on rank 0.
 """
@@ -18,6 +35,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -28,13 +47,20 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "signal-samples/sec/GPU (512-sample chunks) + bases/sec at 1/2/4/8 MI355X"
+FP32_PEAK = 157.3            # TFLOP/s, dense fp32 MFMA (MI355X_MICROARCH.md)
+SPLIT_PEAK = 2516.6 / 3      # TFLOP/s fp32-equivalent: dense fp16 MFMA peak / 3 split products
+HBM_PEAK = 8000.0            # GB/s
+FLOP_PER_CHUNK = 6_273_038_336          # SURVEY.md §8d, greedy, 100 steps (12.25 MFLOP/sample)
+ENC_FLOP_PER_CHUNK = 4_832_100_352      # transformer encoder term
+NANO_ENC_FLOP_PER_CHUNK = 1_007_681_536  # NanoEncoder term
+DEC_FLOP_PER_CHUNK = 1_440_937_984      # decoder term (greedy, 100 steps)
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=200, help="timed steps (200 x ~29 ms: a timed region of ~6 s)")
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=256, help="chunks per GPU per step")
     ap.add_argument("--mode", default="greedy", choices=["greedy", "beam"])
     ap.add_argument("--beam", type=int, default=5)
@@ -44,18 +70,41 @@ def parse():
                     help="-min_length: EOS masked before this step.  The random-init model is EOS-prone, so this "
                          "sets its decode length to a trained basecaller's ~57 bases per 512 samples (greedy cost "
                          "is unaffected: all max_length steps always run)")
+    ap.add_argument("--eos-bias", type=float, default=-3.0, help="generator EOS logit shift of the random-init model")
+    ap.add_argument("--workload", default="batch", choices=["batch", "reads"],
+                    help="batch: configs[1..3] fixed batches resident in HBM; reads: configs[4] read sharding")
+    ap.add_argument("--reads", type=int, default=16384, help="synthetic reads PER GPU for the read-shard workload")
+    ap.add_argument("--read-shard", type=int, default=1, help="append the configs[4] read-shard measurement")
+    ap.add_argument("--exact", type=int, default=1, help="append the exact-fp32 throughput")
+    ap.add_argument("--host-inclusive", type=int, default=1, help="append the Translator (host-inclusive) rate")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 (0 = skip)")
-    ap.add_argument("--cpu-chunks", type=int, default=0, help="CPU baseline sample size (0: 128 greedy / 24 beam)")
+    ap.add_argument("--cpu-chunks", type=int, default=50, help="CPU baseline batch (configs[0]: 50)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline: repeat batches for at least this")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
+    ap.add_argument("--selftest-cpu", action="store_true",
+                    help="launcher/rank plumbing self-test on CPU (gloo, no engine, no measurement)")
     return ap.parse_args()
 
 
-def workload(args):
-    idx = 3 if args.mode == "beam" else (2 if args.encoder == "nano" else 1)
-    enc = "3-layer transformer encoder" if args.encoder == "transformer" else "NanoEncoder (3x BiLSTM)"
-    dec = "greedy" if args.mode == "greedy" else f"--fast beam {args.beam}"
-    return (f"configs[{idx}]: {enc} + 3-layer transformer decoder, d_model 256, src_seq_length 512, "
-            f"batch {args.batch}, {dec}, max_length {args.max_length}")
+# ----------------------------------------------------------------- launcher
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch(args) -> int:
+    """--gpus N outside a launcher: N rank processes under torch.distributed.run,
+    started as CHILDREN of this process before it has made any GPU call
+    (pipeline.evaluate.sh:114-115 runs one process per GPU the same way)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
 def dist_setup(args):
@@ -63,52 +112,128 @@ def dist_setup(args):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            torch.cuda.set_device(local)
+            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            torch.distributed.init_process_group("gloo")
     return world, rank, local
+
+
+def workload(args):
+    if args.workload == "reads":
+        return (f"configs[4]: 3+3 transformer, d_model 256, src_seq_length 512, synthetic read set "
+                f"({args.reads} reads/GPU, lengths U[256,1024]) sharded by LPT over the ranks, greedy, "
+                f"engine batch {args.batch}, max_length {args.max_length}")
+    idx = 3 if args.mode == "beam" else (2 if args.encoder == "nano" else 1)
+    enc = "3-layer transformer encoder" if args.encoder == "transformer" else "NanoEncoder (3x BiLSTM)"
+    dec = "greedy" if args.mode == "greedy" else f"--fast beam {args.beam}"
+    return (f"configs[{idx}]: {enc} + 3-layer transformer decoder, d_model 256, src_seq_length 512, "
+            f"batch {args.batch}, {dec}, max_length {args.max_length}")
+
+
+# ----------------------------------------------------------------- CPU baseline
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_threads() -> int:
+    """Threads the CPU baseline may use: the cores this process is given
+    (OMP_NUM_THREADS where the box sets it, else the affinity mask)."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
 
 
 def cpu_baseline(cfg, W, sig, lens, args):
     from oracle import ref_cpu
-    n = min(args.cpu_chunks or (128 if args.mode == "greedy" else 24), sig.shape[0])
-    threads = min(16, os.cpu_count() or 1)
+    n = min(args.cpu_chunks, sig.shape[0])
+    threads = cpu_threads()
     torch.set_num_threads(threads)
     m = ref_cpu.RefModel(cfg, W)
+    done, dt, batches = 0, 0.0, 0
     t0 = time.perf_counter()
-    if args.mode == "greedy":
-        ref_cpu.greedy(m, sig[:n], lens[:n], max_length=args.max_length, min_length=args.min_length)
-    else:
-        ref_cpu.fast_beam(m, sig[:n], lens[:n], beam_size=args.beam, max_length=args.max_length,
-                          min_length=args.min_length)
-    dt = time.perf_counter() - t0
-    return {"value": float(lens[:n].sum() / dt), "unit": "samples/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/ref_cpu.py {args.mode} on {n} chunks x 512 samples, max_length {args.max_length}, "
-                      f"torch CPU fp32, {threads} threads, {dt:.1f} s"}
+    while dt < args.cpu_seconds or batches == 0:
+        s, l = sig[done % sig.shape[0]:][:n], lens[done % sig.shape[0]:][:n]
+        if s.shape[0] < n:
+            s, l = sig[:n], lens[:n]
+        if args.mode == "greedy":
+            ref_cpu.greedy(m, s, l, max_length=args.max_length, min_length=args.min_length)
+        else:
+            ref_cpu.fast_beam(m, s, l, beam_size=args.beam, max_length=args.max_length, min_length=args.min_length)
+        done += n
+        batches += 1
+        dt = time.perf_counter() - t0
+        if args.mode == "beam":
+            break
+    return {"value": round(float(done * 512 / dt), 1), "unit": "samples/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(), "machine_cpus": os.cpu_count(),
+            "sample": f"oracle/ref_cpu.py {args.mode} (the reference's algorithm in torch CPU fp32, pinned to the "
+                      f"reference's own outputs by tests/golden) on {batches} batch(es) of {n} chunks x 512 "
+                      f"samples (configs[0] batch), max_length {args.max_length}, {threads} threads, {dt:.1f} s"}
 
 
-def _time(fn, n):
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for i in range(n):
-        fn(i)
-    e1.record()
-    e1.synchronize()
-    return e0.elapsed_time(e1) / n
+# ----------------------------------------------------------------- helpers
+class _StreamTimer:
+    """HIP events on the stream the engine's kernels run on (the engine's own
+    stream is joined to the current stream by events, so bracketing the
+    current stream covers the whole call)."""
+
+    def __init__(self, dev):
+        self.dev = dev
+
+    def time(self, fn, n):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(torch.cuda.current_stream(self.dev))
+        for i in range(n):
+            fn(i)
+        e1.record(torch.cuda.current_stream(self.dev))
+        e1.synchronize()
+        return e0.elapsed_time(e1) / n
 
 
-def _pmc_traffic(name):
-    """HBM bytes per launch for `name` from the committed PMC summary
-    (profiles/pmc_summary.json, written by tools/pmc_summary.py from
-    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes with the gfx950 x2
-    FETCH_SIZE correction), or None."""
+def _pmc(name, key="kernels"):
+    """HBM bytes per launch for kernel `name` from the committed PMC summary
+    (profiles/pmc_summary.json, tools/pmc_summary.py: rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes with the gfx950 x2 FETCH_SIZE correction)."""
     p = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(p) as f:
-            return json.load(f)["kernels"][name]["hbm_bytes_per_launch"]
+            return json.load(f)[key][name]["hbm_bytes_per_launch"]
     except Exception:
         return None
 
 
+def _mfma_counters():
+    """The committed rocprof MFMA counter pass (profiles/mfma_summary.json,
+    tools/mfma_summary.py), or None."""
+    p = os.path.join(ROOT, "profiles", "mfma_summary.json")
+    try:
+        with open(p) as f:
+            return json.load(f)
+    except Exception:
+        return None
+
+
+def count_bases(tok: np.ndarray, eos: int) -> int:
+    """Base tokens (ids >= 4: not <unk>/<blank>/<s>/</s>) before the first EOS."""
+    is_eos = tok == eos
+    first = np.where(is_eos.any(1), is_eos.argmax(1), tok.shape[1])
+    return int(((np.arange(tok.shape[1])[None, :] < first[:, None]) & (tok >= 4)).sum())
+
+
+# ----------------------------------------------------------------- roofline
 def kernel_roofline(eng, B, mode, beam, encoder="transformer"):
     """Dominant kernel of the translate step, timed LIVE: every launch of it
     inside the timed graph replays carries in-kernel wall-clock stamps
@@ -126,19 +251,19 @@ def kernel_roofline(eng, B, mode, beam, encoder="transformer"):
     T, D = 512, 256
     ms = us * 1e-3
     if mode == "greedy":
-        name = "dec_mem_attention_kernel<0, 8>"
+        name = "dec_mem_attention_kernel<8>"
         nbytes = B * T * D * 4 + B * T * 4 + 2 * B * 8 * D * 4
         flops = 2 * 2 * 8 * T * D * B
         tf = flops / (ms * 1e-3) / 1e12
-        extra = {"mfma_view": {"algorithmic_flops_per_launch": flops, "achieved": round(tf, 2), "peak": 157.3,
-                               "unit": "TFLOP/s", "frac": round(tf / 157.3, 4)}}
+        extra = {"mfma_view": {"algorithmic_flops_per_launch": flops, "achieved": round(tf, 2), "peak": FP32_PEAK,
+                               "unit": "TFLOP/s", "frac": round(tf / FP32_PEAK, 4)}}
     else:
         name = f"dec_ctx_attention_kernel<{beam}>"
         nbytes = B * T * 2 * D * 4 + B * T * 4 + 2 * B * beam * D * 4
         extra = {}
     ach = nbytes / (ms * 1e-3) / 1e9
-    out = {"bound": "hbm", "kernel": name, "achieved": round(ach, 1), "peak": 8000.0, "unit": "GB/s",
-           "frac": round(ach / 8000.0, 4), "traffic": _pmc_traffic(name), "algorithmic_bytes_per_launch": nbytes,
+    out = {"bound": "hbm", "kernel": name, "achieved": round(ach, 1), "peak": HBM_PEAK, "unit": "GB/s",
+           "frac": round(ach / HBM_PEAK, 4), "traffic": _pmc(name), "algorithmic_bytes_per_launch": nbytes,
            "avg_launch_ms": round(ms, 5), "timed_launches": n,
            "timing": "in-kernel wall-clock stamps, launches of the last timed call"}
     out.update(extra)
@@ -166,13 +291,13 @@ def kernel_roofline(eng, B, mode, beam, encoder="transformer"):
                                                M, N, K, 1, 1, st), "nd_op_gemm_split")
     for i in range(3):
         ffn1(i)
-    gms = _time(ffn1, 10)
+    gms = _StreamTimer(dev).time(ffn1, 10)
     tf = 2.0 * M * N * K / (gms * 1e-3) / 1e12
-    peak = 2516.6 / 3
     out["mfma_kernel"] = {"kernel": "gemm_f32_kernel<256,256,2,4,H3,LN,RELU> (encoder FFN1, split-fp16)",
-                          "achieved": round(tf, 2), "peak": round(peak, 1),
+                          "achieved": round(tf, 2), "peak": round(SPLIT_PEAK, 1),
                           "unit": "TFLOP/s fp32-equivalent (fp16 MFMA peak / 3 products)",
-                          "frac": round(tf / peak, 4), "avg_launch_ms": round(gms, 4)}
+                          "frac": round(tf / SPLIT_PEAK, 4), "avg_launch_ms": round(gms, 4)}
+    del A, C, Wh, Wf
     return out
 
 
@@ -193,31 +318,51 @@ def lstm_view(dev, B, T):
         op_lstm_layer(whh, lens, T, xp=xp, out=out)
     for i in range(2):
         layer(i)
-    ms = _time(layer, 5)
+    ms = _StreamTimer(dev).time(layer, 5)
     flops = 2.0 * 2 * B * 512 * 128 * T
     tf = flops / (ms * 1e-3) / 1e12
     return {"kernel": "lstm_dir_kernel (BiLSTM layer, split-fp16)", "bound": "latency",
             "avg_launch_ms": round(ms, 4), "us_per_step": round(ms * 1e3 / T, 3),
-            "achieved": round(tf, 2), "peak": round(2516.6 / 3, 1),
-            "unit": "TFLOP/s fp32-equivalent (fp16 MFMA peak / 3 products)", "frac": round(tf / (2516.6 / 3), 4)}
+            "achieved": round(tf, 2), "peak": round(SPLIT_PEAK, 1),
+            "unit": "TFLOP/s fp32-equivalent (fp16 MFMA peak / 3 products)", "frac": round(tf / SPLIT_PEAK, 4)}
 
 
-def main():
-    args = parse()
-    world, rank, local = dist_setup(args)
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
+def mfma_view(args, eng, sig, lens, ms_per_step):
+    """Algorithmic MFMA utilisation (SURVEY §8d FLOP counts) of the whole
+    path and of the encoder alone (nd_encode timed by itself), against the
+    fp32 MFMA peak and the split-fp16 fp32-equivalent peak."""
+    B = args.batch
+    enc_flop = ENC_FLOP_PER_CHUNK if args.encoder == "transformer" else NANO_ENC_FLOP_PER_CHUNK
+    path_flop = (enc_flop + DEC_FLOP_PER_CHUNK) * B
+    if args.mode != "greedy":
+        return None
+    timer = _StreamTimer(eng.device)
+    for _ in range(2):
+        eng.encode(sig, lens, lens)
+    enc_ms = timer.time(lambda i: eng.encode(sig, lens, lens), 10)
+    path_tf = path_flop / (ms_per_step * 1e-3) / 1e12
+    enc_tf = enc_flop * B / (enc_ms * 1e-3) / 1e12
+    out = {"algorithmic_flop_per_chunk": enc_flop + DEC_FLOP_PER_CHUNK,
+           "path": {"tflops": round(path_tf, 2), "frac_fp32_peak": round(path_tf / FP32_PEAK, 4),
+                    "frac_split_peak": round(path_tf / SPLIT_PEAK, 4)},
+           "encoder_only": {"ms": round(enc_ms, 4), "tflops": round(enc_tf, 2),
+                            "frac_fp32_peak": round(enc_tf / FP32_PEAK, 4),
+                            "frac_split_peak": round(enc_tf / SPLIT_PEAK, 4),
+                            "note": "nd_encode incl. its memory-bank LayerNorm copy"},
+           "peaks": {"fp32": FP32_PEAK, "split_fp16_fp32_equiv": round(SPLIT_PEAK, 1), "unit": "TFLOP/s"}}
+    cnt = _mfma_counters()
+    if cnt is not None:
+        out["rocprof_counters"] = cnt.get("bench", cnt)
+    return out
+
+
+# ----------------------------------------------------------------- workloads
+def run_batch(args, world, rank, dev, cfg, W):
     from nanodecoder_amd import synth
     from nanodecoder_amd.engine import Engine
 
-    cfg = synth.ModelConfig(encoder_type=args.encoder)
-    # rank 0 owns the weights; one RCCL broadcast of the packed blob reaches the others
-    W = synth.make_weights(cfg, seed=11, eos_bias=-3.0) if rank == 0 else None
-    if world > 1:
-        from nanodecoder_amd.shard import broadcast_weights
-        W = broadcast_weights(W, dev)
     beam = args.beam if args.mode == "beam" else 1
-    eng = Engine(cfg, W, device=local, max_batch=args.batch, max_src_len=512, max_steps=args.max_length,
+    eng = Engine(cfg, W, device=dev.index, max_batch=args.batch, max_src_len=512, max_steps=args.max_length,
                  max_beam=beam)
     # each rank gets its own shard of synthetic reads
     sig_np = synth.synth_chunk_batch(args.batch, 512, seed=1000 + rank, inject_masks=False)
@@ -239,7 +384,6 @@ def main():
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    bases = 0
     for _ in range(args.steps):
         out = step()
     torch.cuda.synchronize()
@@ -251,11 +395,7 @@ def main():
     tok = out["tokens"].cpu().numpy()
     if args.mode == "beam":
         tok = tok[:, 0]
-    eos = cfg.eos_idx
-    is_eos = tok == eos
-    first = np.where(is_eos.any(1), is_eos.argmax(1), tok.shape[1])
-    base_mask = (np.arange(tok.shape[1])[None, :] < first[:, None]) & (tok >= 4)
-    bases_per_step = int(base_mask.sum())
+    bases_per_step = count_bases(tok, cfg.eos_idx)
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
     if world > 1:
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -265,23 +405,158 @@ def main():
     res = {
         "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic reads, random-init weights",
+        "scaling": "weak", "vs_baseline": None,
+        "dtype": "f32 (fp32 values; products as split-fp16 x3 on fp16 MFMA: 22-bit operands, fp32 accumulate)",
+        "data": "synthetic reads, random-init weights",
         "config": {"workload": workload(args), "chunks_per_gpu_per_step": args.batch,
                    "global_batch": args.batch * world, "seq_len": 512, "parallelism": f"read-shard x{world}"},
         "samples_per_sec_per_gpu": round(value / world, 1),
         "bases_per_sec": round(bases_per_step * args.steps * world / dt, 1),
+        "timed_seconds": round(dt, 3),
         "min_length": args.min_length,
     }
     if args.mode == "beam":
         res["decoder_steps_executed"] = int(out["steps"].cpu().item())
+    extras = {}
     if rank == 0:
         if not args.no_roofline:
-            res["roofline"] = kernel_roofline(eng, args.batch, args.mode, beam, args.encoder)
+            extras["roofline"] = kernel_roofline(eng, args.batch, args.mode, beam, args.encoder)
+        eng.set_kernel_stamps(False)
+        mv = None if args.no_roofline else mfma_view(args, eng, sig, lens, dt / args.steps * 1e3)
+        if mv is not None:
+            extras["mfma"] = mv
+    if args.exact:
+        # the same workload with exact fp32 products (nd_set_exact_fp32)
+        eng.set_exact_fp32(True)
+        n_ex = max(5, min(40, args.steps // 4))
+        for _ in range(2):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n_ex):
+            step()
+        torch.cuda.synchronize()
+        dte = time.perf_counter() - t0
+        eng.set_exact_fp32(False)
+        extras["exact_fp32"] = {"value_per_gpu": round(float(lens_np.sum()) * n_ex / dte, 1), "unit": "samples/s",
+                                "ms_per_step": round(dte / n_ex * 1e3, 3), "steps": n_ex,
+                                "note": "every GEMM, the encoder attention and the BiLSTM on fp32 MFMAs"}
+    if args.host_inclusive and args.mode == "greedy":
+        extras["host_inclusive"] = host_inclusive(args, cfg, eng, sig_np, lens_np)
+    res.update(extras)
+    return res, eng, sig_np, lens_np
+
+
+def host_inclusive(args, cfg, eng, sig_np, lens_np):
+    """The same batches through the Translator drop-in: float32 chunks on the
+    host -> pinned staging -> H2D -> engine -> tokens D2H -> strings, with one
+    batch in flight while the next is packed (Translator.stream_reads)."""
+    import types
+    from nanodecoder_amd.translator import Translator
+    opt = types.SimpleNamespace(gpu=eng.device.index, n_best=1, max_length=args.max_length,
+                                min_length=args.min_length, beam_size=1, batch_size=args.batch,
+                                engine_max_batch=args.batch)
+    tr = Translator(cfg, None, opt, engine=eng)
+    n = max(4, min(40, args.steps // 4))
+    # each "read" is one chunk here: batches are exactly the timed batch
+    reads = [[sig_np[i % args.batch]] for i in range(args.batch * n)]
+    list(tr.stream_reads(reads[: 2 * args.batch], batch_size=1))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    done = sum(1 for _ in tr.stream_reads(reads, batch_size=1))
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return {"value_per_gpu": round(done * 512 / dt, 1), "unit": "samples/s", "batches": n,
+            "ms_per_batch": round(dt / n * 1e3, 3),
+            "path": "Translator.stream_reads: host packing + pinned H2D + engine + token D2H + EOS cut"}
+
+
+def run_reads(args, world, rank, dev, cfg, W, n_reads_per_gpu):
+    """configs[4]: the synthetic read set (lengths U[256,1024], 1-2 chunks per
+    read) sharded over the ranks by LPT on sample count; every rank packs its
+    reads into full engine batches; host front end (median/MAD + windowing)
+    in a producer thread; timed region = max over ranks (shard.run_distributed)."""
+    import types
+    from nanodecoder_amd import shard
+    from nanodecoder_amd.engine import Engine
+    from nanodecoder_amd.translator import Translator
+
+    def translator_factory(Wr):
+        opt = types.SimpleNamespace(gpu=dev.index, n_best=1, max_length=args.max_length, min_length=args.min_length,
+                                    beam_size=1, batch_size=100, engine_max_batch=args.batch)
+        eng = Engine(cfg, Wr, device=dev.index, max_batch=args.batch, max_src_len=512, max_steps=args.max_length)
+        return Translator(cfg, Wr, opt, engine=eng)
+
+    g, _ = shard.run_distributed(n_reads_per_gpu * world, translator_factory, lambda: W, dev, batch_size=100,
+                                 pregenerate=True, warmup_reads=min(2048, n_reads_per_gpu))
+    return {"value": round(g["samples"] / g["seconds"], 1), "unit": "samples/s", "n_gpus": world,
+            "samples_per_sec_per_gpu": round(g["samples"] / g["seconds"] / world, 1),
+            "bases_per_sec": round(g["bases"] / g["seconds"], 1), "reads": g["reads"], "chunks": g["chunks"],
+            "seconds": round(g["seconds"], 3), "samples_per_rank": g["samples_per_rank"],
+            "load_imbalance_max_over_mean": round(g["load_imbalance"], 4),
+            "scaling": "weak" if args.workload == "batch" else "weak (reads per GPU fixed)",
+            "workload": (f"configs[4]: {n_reads_per_gpu} synthetic reads per GPU, lengths U[256,1024], LPT shard, "
+                         f"engine batch {args.batch}, reference batch_size 100, greedy, max_length "
+                         f"{args.max_length}; front end (median/MAD + windowing) in a host producer thread, "
+                         f"raw traces pre-generated (stand-in for the files read)")}
+
+
+def selftest_cpu(args):
+    """Launcher plumbing on CPU: every rank joins a gloo group, rank 0 prints
+    the line with the world size it saw (no engine, no measurement)."""
+    world, rank, _ = dist_setup(args)
+    t = torch.tensor([float(rank)])
+    if world > 1:
+        torch.distributed.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"selftest": True, "n_gpus": world, "rank_sum": float(t.item())}), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(args))
+    if args.selftest_cpu:
+        return selftest_cpu(args)
+    world, rank, local = dist_setup(args)
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    from nanodecoder_amd import synth
+
+    cfg = synth.ModelConfig(encoder_type=args.encoder)
+    # rank 0 owns the weights; one RCCL broadcast of the packed blob reaches the others
+    W = synth.make_weights(cfg, seed=11, eos_bias=args.eos_bias) if rank == 0 else None
+    if world > 1:
+        from nanodecoder_amd.shard import broadcast_weights
+        W = broadcast_weights(W, dev)
+
+    if args.workload == "reads":
+        rs = run_reads(args, world, rank, dev, cfg, W, args.reads)
+        res = {"metric": METRIC, "value": rs["value"], "unit": "samples/s", "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": None, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+               "dtype": "f32 (fp32 values; products as split-fp16 x3 on fp16 MFMA)",
+               "data": "synthetic reads, random-init weights",
+               "config": {"workload": workload(args), "seq_len": 512, "parallelism": f"read-shard x{world}"},
+               "read_shard": rs}
+        if rank == 0:
+            print(json.dumps(res), flush=True)
+        if torch.distributed.is_initialized():
+            torch.distributed.destroy_process_group()
+        return
+
+    res, eng, sig_np, lens_np = run_batch(args, world, rank, dev, cfg, W)
+    if args.read_shard and args.mode == "greedy" and args.encoder == "transformer":
+        eng.close()  # the read-shard engine replaces it
+        res["read_shard"] = run_reads(args, world, rank, dev, cfg, W, max(1024, args.reads // 4))
+    if rank == 0:
         if args.cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(cfg, W, sig_np, lens_np, args)
         print(json.dumps(res), flush=True)
     eng.close()
-    if world > 1:
+    if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
 
 

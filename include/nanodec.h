@@ -217,6 +217,14 @@ int nd_set_graphs(nd_ctx* ctx, int enable);
  * 142-177's context path. */
 int nd_set_ctx_path(nd_ctx* ctx, int path);
 
+/* Arithmetic of the products: 0 (default) = split-fp16 (each fp32 operand as
+ * an fp16 hi/lo pair, 22 significant bits, three fp16 MFMA products summed in
+ * fp32 accumulators); 1 = exact fp32 (fp32-MFMA kernels for every GEMM, the
+ * encoder attention and the BiLSTM recurrence), the reference's own fp32
+ * arithmetic (nn.Linear / bmm in fp32).  Default from ND_GEMM_F32.  Clears
+ * the context's captured graphs when it changes. */
+int nd_set_exact_fp32(nd_ctx* ctx, int enable);
+
 /* Launch-duration stamps of the decoder's context attention (the bench's
  * roofline kernel: dec_mem_attention_kernel for greedy, dec_ctx_attention_kernel
  * for beam), taken inside the kernels with the constant-rate wall clock while

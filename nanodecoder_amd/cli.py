@@ -53,23 +53,47 @@ def list_reads(opt):
 
 
 def _read_only(args):
-    """-frontend gpu: the worker only reads the raw samples."""
+    """-frontend gpu: the worker only reads the raw samples.  An empty read
+    yields [prefix] alone and is skipped like the reference's
+    (translate.py:102-103)."""
     path, prefix, suffix, norm, length, stride = args
     try:
-        return [prefix, frontend.read_raw(path, suffix)]
+        raw = frontend.read_raw(path, suffix)
+        return [prefix, raw] if len(raw) else [prefix]
     except Exception:
         return ["!" + prefix]
 
 
 def _gpu_chunks(opt, group):
-    """[prefix, raw] reads -> [prefix, chunk, ...] with the device front end."""
+    """[prefix, raw] reads -> [prefix, chunk, ...] with the device front end,
+    on the translator's GPU (-gpu)."""
     sig, lens, rd = frontend.normalize_window_gpu([g[1] for g in group], opt.normalization_raw,
-                                                  opt.src_seq_length, opt.src_seq_stride)
+                                                  opt.src_seq_length, opt.src_seq_stride, device=max(0, opt.gpu))
     host = sig.cpu().numpy()
     out = [[g[0]] for g in group]
     for c in range(len(rd)):
         out[rd[c]].append(host[c, : lens[c]].copy())
     return out
+
+
+def _n_chunks(opt, src, gpu_fe):
+    """Chunks a pending read will contribute (for -pack_reads 0)."""
+    if not gpu_fe:
+        return len(src) - 1
+    return len(frontend.windows(len(src[1]), opt.src_seq_length, opt.src_seq_stride))
+
+
+def _run_group(opt, translator, pending, gpu_fe):
+    """Front end (device) + translate for one packed group, with the
+    per-group error isolation of translate.py:97-98."""
+    if gpu_fe:
+        try:
+            pending = _gpu_chunks(opt, pending)
+        except Exception as e:
+            for g in pending:
+                print("!!!error!!!data src: " + g[0].split(".txt")[0] + " (%r)" % (e,))
+            return 0
+    return _translate_group(opt, translator, pending)
 
 
 def _extract(args):
@@ -111,8 +135,10 @@ def main(opt=None):
     t_start = time.time()
     n_done = 0
     gpu_fe = getattr(opt, "frontend", "cpu") == "gpu"
+    # -pack_reads 0: flush once the pending reads fill the engine batch
+    cap = int(getattr(translator, "max_batch", 0) or 256)
     with ctx.Pool(max(1, opt.thread)) as pool:
-        pending = []
+        pending, n_chunks = [], 0
         for src in pool.imap(_read_only if gpu_fe else _extract, jobs):
             if src and src[0].startswith("!"):
                 print("!!!error!!!data src: " + src[0][1:].split(".txt")[0])
@@ -120,11 +146,13 @@ def main(opt=None):
             if not src or len(src) == 1:   # translate.py:102-103
                 continue
             pending.append(src)
-            if len(pending) >= max(1, opt.pack_reads):
-                n_done += _translate_group(opt, translator, _gpu_chunks(opt, pending) if gpu_fe else pending)
-                pending = []
+            n_chunks += _n_chunks(opt, src, gpu_fe)
+            full = len(pending) >= opt.pack_reads if opt.pack_reads > 0 else n_chunks >= cap
+            if full:
+                n_done += _run_group(opt, translator, pending, gpu_fe)
+                pending, n_chunks = [], 0
         if pending:
-            n_done += _translate_group(opt, translator, _gpu_chunks(opt, pending) if gpu_fe else pending)
+            n_done += _run_group(opt, translator, pending, gpu_fe)
     logger.info("translated %d reads in %.1f s" % (n_done, time.time() - t_start))
     return n_done
 

@@ -333,13 +333,13 @@ enc_attention_h3_kernel(const float* __restrict__ qkv, const float* __restrict__
 }
 
 hipError_t launch_enc_attention(const float* qkv, const float* signal, const int* span, float* out, int B, int T,
-                                hipStream_t s) {
+                                hipStream_t s, bool exact) {
   if (T > ENC_MAXT || T <= 0) return hipErrorInvalidValue;
   static const bool f32 = [] {
     const char* e = getenv("ND_ENC_ATTN_F32");  // 1: the fp32-MFMA kernel
     return e && atoi(e) != 0;
   }();
-  if (f32)
+  if (f32 || exact)
     hipLaunchKernelGGL(enc_attention_kernel, dim3(ND_H, B), dim3(1024), 0, s, qkv, signal, span, out, T);
   else
     hipLaunchKernelGGL(enc_attention_h3_kernel, dim3(ND_H, B), dim3(1024), 0, s, qkv, signal, span, out, T);

@@ -12,6 +12,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -109,6 +110,9 @@ struct nd_ctx {
   unsigned long long* kstamp = nullptr;   // [dec_layers * max_steps][2] (start, end) wall-clock ticks
   bool timing = false;
   float t_enc = 0.f, t_dec = 0.f;
+  // exact fp32: plain fp32-MFMA kernels everywhere (no split-fp16 products);
+  // nd_set_exact_fp32, default from ND_GEMM_F32
+  bool exact = false;
 
   // weights
   float *enc_lin_w = nullptr, *enc_lin_b = nullptr, *enc_ln_g = nullptr, *enc_ln_b = nullptr;
@@ -444,6 +448,7 @@ struct G {
   G& relu() { a.relu = true; return *this; }
   // use the weight's split-fp16 image when finalize made one
   G& h3(const nd_ctx* c) {
+    if (c->exact) return *this;  // fp32 weights only: the fp32-MFMA kernels
     auto it = c->split.find(a.W);
     if (it != c->split.end()) {
       a.Wh = it->second.first;
@@ -476,7 +481,7 @@ static hipError_t enqueue_encode_transformer(nd_ctx* c, int B, int T, hipStream_
   for (auto& L : c->enc) {
     // encoder/transformer.py:36-54
     LCHK(G(c->x, D, L.nwqkv, 3 * D, D, L.nbqkv, c->big, 3 * D, M).h3(c).ln(c->x_part, pnx).run(s));
-    LCHK(nd::launch_enc_attention(c->big, c->sig, c->span, c->att, B, T, s));
+    LCHK(nd::launch_enc_attention(c->big, c->sig, c->span, c->att, B, T, s, c->exact));
     LCHK(G(c->att, D, L.wo, D, D, L.bo, c->y, D, M).h3(c).res(c->x, D).stats(c->y_part).run(s, &pny));
     LCHK(G(c->y, D, L.nw1, F, D, L.nb1, c->big, F, M).h3(c).ln(c->y_part, pny).relu().run(s));
     LCHK(G(c->big, F, L.w2, D, F, L.b2, c->x, D, M).h3(c).res(c->y, D).stats(c->x_part).run(s, &pnx));
@@ -687,6 +692,10 @@ int nd_create(const nd_config* cfg, nd_ctx** out) {
   HIPCHK(hipSetDevice(cfg->device));
   nd_ctx* c = new nd_ctx();
   c->cfg = *cfg;
+  {
+    const char* e = getenv("ND_GEMM_F32");
+    c->exact = e && atoi(e) != 0;
+  }
   c->F = cfg->d_ff;
   c->V = cfg->vocab;
   c->H = cfg->rnn_hidden;
@@ -1265,6 +1274,16 @@ int nd_set_ctx_path(nd_ctx* c, int path) {
   return ND_OK;
 }
 
+int nd_set_exact_fp32(nd_ctx* c, int enable) {
+  if (!c) return fail(ND_ERR_ARG, "null ctx");
+  if (c->exact != (enable != 0)) {
+    for (auto& kv : c->graphs) (void)hipGraphExecDestroy(kv.second);
+    c->graphs.clear();
+  }
+  c->exact = enable != 0;
+  return ND_OK;
+}
+
 int nd_set_timing(nd_ctx* c, int enable) {
   if (!c) return fail(ND_ERR_ARG, "null ctx");
   c->timing = enable != 0;
@@ -1440,6 +1459,8 @@ int nd_op_lstm_layer(const float* xp, const float* signal, const float* wih0, co
                      const float* bn_shift, int32_t layer0, void* stream) {
   if (B < 1 || T < 1 || !whh || !len || !out || (layer0 ? (!signal || !wih0 || !bsum) : !xp))
     return fail(ND_ERR_ARG, "lstm_layer: bad arguments");
+  if ((bn_scale == nullptr) != (bn_shift == nullptr))
+    return fail(ND_ERR_ARG, "lstm_layer: bn_scale and bn_shift must both be set or both be null");
   hipError_t e = nd::launch_lstm_layer(xp, signal, wih0, bsum, whh, len, B, T, out, bn_scale, bn_shift, layer0 != 0,
                                        (hipStream_t)stream);
   if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("lstm_layer: ") + hipGetErrorString(e));
@@ -1494,7 +1515,7 @@ static hipError_t enqueue_encode_nano(nd_ctx* c, int B, int T, hipStream_t s) {
       LCHK(G(bufs[(l - 1) & 1], 2 * c->H, L.wih, 8 * c->H, 2 * c->H, L.bsum, c->nano_xp, 8 * c->H, M).h3(c).run(s));
     if (last) LCHK(hipMemsetAsync(out, 0, (size_t)M * 2 * c->H * sizeof(float), s));
     LCHK(nd::launch_lstm_layer(c->nano_xp, c->sig, L.wih, L.bsum, L.whh, c->len, B, T, out,
-                               last ? nullptr : L.bn_scale, last ? nullptr : L.bn_shift, l == 0, s));
+                               last ? nullptr : L.bn_scale, last ? nullptr : L.bn_shift, l == 0, s, c->exact));
   }
   return G(bufs[(Lz - 1) & 1], 2 * c->H, c->nano_W, D, 2 * c->H, nullptr, c->x, D, M).h3(c).run(s);
 }

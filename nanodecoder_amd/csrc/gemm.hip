@@ -248,10 +248,10 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
   __syncthreads();
   for (int kt = 0; kt < KT; ++kt) {
     const int buf = kt & 1;
-    if (kt + 1 < KT && !(g.expt & 4)) load_tile((kt + 1) * BK);
+    if (kt + 1 < KT) load_tile((kt + 1) * BK);
     if constexpr (H3) {
 #pragma unroll
-      for (int ks = 0; ks < BK / 16 && !(g.expt & 2); ++ks) {
+      for (int ks = 0; ks < BK / 16; ++ks) {
         h8 ah[FM], al[FM], bh[FN], bl[FN];
         const int o = (2 * ks + lh) * 8;  // this lane's 8-k group: hi at o, lo at o + 4 (words)
 #pragma unroll
@@ -277,7 +277,7 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
       }
     } else
 #pragma unroll
-    for (int kb = 0; kb < BK / 8 && !(g.expt & 2); ++kb) {
+    for (int kb = 0; kb < BK / 8; ++kb) {
       f32x4 af[FM], bf[FN];
 #pragma unroll
       for (int a = 0; a < FM; ++a)
@@ -296,7 +296,6 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
     __syncthreads();
   }
 
-  if (g.expt & 1) return;
   constexpr int TPR = BN / 4, RPP = NT / TPR;
   const int c4 = (tid % TPR) * 4;
 #pragma unroll
@@ -844,11 +843,6 @@ static hipError_t check_args(const GemmArgs& g) {
 
 hipError_t launch_gemm(GemmArgs& g, hipStream_t s) {
   if (g.M <= 0) return hipSuccess;
-  static const int expt = [] {
-    const char* e = getenv("ND_GEMM_EXPT");
-    return e ? atoi(e) : 0;
-  }();
-  g.expt = expt;
   if (gemm_f32_only() && g.W) g.Wh = nullptr;
   if (!g.W && !g.Wh) return hipErrorInvalidValue;
   hipError_t e = check_args(g);

@@ -44,7 +44,6 @@ struct GemmArgs {
   float wscale_rm = 1.0f;
   int p16io = 0;
   int xcd_map = 0;     // row-major kernel: XCD-aware tile order (set by launch_gemm)
-  int expt = 0;        // timing experiments only (ND_GEMM_EXPT; wrong results): 1 no epilogue, 2 no MFMA, 4 no loads
 };
 #define ND_PART_LD 16  // partial-stat slots per row (max column tiles of a 256-wide row)
 // row-major operands (encoder, large M): LDS-tiled MFMA kernel
@@ -75,14 +74,15 @@ hipError_t launch_fold_layernorm(const float* W, const float* bias, const float*
 hipError_t launch_enc_embed(const float* signal, const float* w_in, const float* b_in, float* x, float* part, int B,
                             int T, hipStream_t s);
 // flash attention over qkv [B*T, 768]; mask signal==0; keys >= span excluded
+// exact: the fp32-MFMA kernel instead of split-fp16 (also forced by ND_ENC_ATTN_F32=1)
 hipError_t launch_enc_attention(const float* qkv, const float* signal, const int* span, float* out, int B, int T,
-                                hipStream_t s);
+                                hipStream_t s, bool exact = false);
 // NanoEncoder BiLSTM layer (both directions): xp [B*T, 1024] projections
 // (or, layer0, computed from signal with wih0/bsum [2][512]); whh [2][512][128];
 // out [B*T, 256] (h, or BatchNorm(h) when bn_scale != nullptr).
 hipError_t launch_lstm_layer(const float* xp, const float* signal, const float* wih0, const float* bsum,
                              const float* whh, const int* len, int B, int T, float* out, const float* bn_scale,
-                             const float* bn_shift, bool layer0, hipStream_t s);
+                             const float* bn_shift, bool layer0, hipStream_t s, bool exact = false);
 // out[r] = LN(x[r]) (rows of 256)
 hipError_t launch_layernorm(const float* x, const float* g, const float* b, float* out, int rows, hipStream_t s);
 

@@ -156,6 +156,14 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
     }
   }
   if (tid < 16) s_len[tid] = (tid < NS && b0 + tid < B) ? len[b0 + tid] : 0;
+  // eval BatchNorm of the next layer's input, per unit, kept in LDS (registers
+  // are the limit here); filled before the barrier below, which publishes it
+  // to every wave before the first step's output
+  __shared__ float s_bn[2][LSTM_H];
+  if (bn_scale && tid < LSTM_H) {
+    s_bn[0][tid] = bn_scale[dir * LSTM_H + tid];
+    s_bn[1][tid] = bn_shift[dir * LSTM_H + tid];
+  }
   if constexpr (H3) {
     for (int e = tid; e < 16 * LSTM_HP_LD; e += NTH) hp[0][0][e] = hp[0][1][e] = (_Float16)0.f;
   } else {
@@ -184,12 +192,6 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
       pseq[u] = 2 * (lq & 1) + (li >> 3);
       punit[u] = wave * UPW + 8 * (lq >> 1) + (li & 7);
     }
-  }
-  // eval BatchNorm of the next layer's input, per unit, kept in LDS (registers are the limit here)
-  __shared__ float s_bn[2][LSTM_H];
-  if (bn_scale && tid < LSTM_H) {
-    s_bn[0][tid] = bn_scale[dir * LSTM_H + tid];
-    s_bn[1][tid] = bn_shift[dir * LSTM_H + tid];
   }
   float w0[2][4], bb[2][4];
   if constexpr (LAYER0) {
@@ -357,12 +359,13 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
 
 hipError_t launch_lstm_layer(const float* xp, const float* signal, const float* wih0, const float* bsum,
                              const float* whh, const int* len, int B, int T, float* out, const float* bn_scale,
-                             const float* bn_shift, bool layer0, hipStream_t s) {
-  static const bool f32 = [] {
+                             const float* bn_shift, bool layer0, hipStream_t s, bool exact) {
+  static const bool f32_env = [] {
     const char* e = getenv("ND_LSTM_F32");  // 1: fp32 MFMAs for the recurrence
     const char* g = getenv("ND_GEMM_F32");
     return (e && atoi(e) != 0) || (g && atoi(g) != 0);
   }();
+  const bool f32 = f32_env || exact;
   static const bool fast = [] {
     const char* e = getenv("ND_LSTM_LIBM");  // 1: libm expf / tanhf in the cell
     return !(e && atoi(e) != 0);

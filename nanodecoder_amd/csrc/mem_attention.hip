@@ -72,7 +72,7 @@ __device__ __forceinline__ float sum_by8(float v) {
 // every tile is processed (keys >= span masked), so the tile loop unrolls to
 // straight-line code and the compiler's wait counts on the in-flight tile
 // loads stay exact (a runtime loop makes it drain them every iteration).
-template <int EXPT, int NT>
+template <int NT>
 __global__ void __launch_bounds__(MB_NW * 64)
 dec_mem_attention_kernel(const float* __restrict__ qp, const float* __restrict__ mem,
                          const float* __restrict__ signal, const int* __restrict__ span, float pad_val,
@@ -108,7 +108,7 @@ dec_mem_attention_kernel(const float* __restrict__ qp, const float* __restrict__
 #pragma unroll
     for (int k = 0; k < MB_KW; ++k) {
       const int t = min(r * MB_TILE + w * MB_KW + k, T - 1);
-      dst[k] = (EXPT & 1) ? f32x4{0.f, 0.f, 0.f, 0.f} : ld4(mc + (size_t)t * ND_D + 4 * lane);
+      dst[k] = ld4(mc + (size_t)t * ND_D + 4 * lane);
     }
   };
   auto put = [&](int r, const f32x4(&src)[MB_KW]) {
@@ -124,7 +124,7 @@ dec_mem_attention_kernel(const float* __restrict__ qp, const float* __restrict__
 #pragma unroll
     for (int e = 0; e < 4; ++e) s4[e] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int kk = 0; kk < 16 && !(EXPT & 2); ++kk) {
+    for (int kk = 0; kk < 16; ++kk) {
       const f32x4 a = ld4(arow + ((64 * dp + 4 * kk + 4 * skey) & (ND_D - 1)));
       const f32x4 u = ld4(urow + ((64 * dp + 4 * kk + 4 * shead) & (ND_D - 1)));
 #pragma unroll
@@ -196,7 +196,7 @@ dec_mem_attention_kernel(const float* __restrict__ qp, const float* __restrict__
     const f32x4 p0 = ld4(pbuf + sh * 8), p1 = ld4(pbuf + sh * 8 + 4);
     const float* tile = slab + (r & 1) * (MB_KW * ND_D);
 #pragma unroll
-    for (int k = 0; k < MB_KW && !(EXPT & 2); ++k) {
+    for (int k = 0; k < MB_KW; ++k) {
       const float* row = tile + k * ND_D;
       const f32x4 b0 = ld4(row + ((4 * zm + 4 * k) & (ND_D - 1)));
       const f32x4 b1 = ld4(row + ((128 + 4 * zm + 4 * k) & (ND_D - 1)));
@@ -269,25 +269,13 @@ hipError_t launch_dec_mem_attention(const float* qp, const float* mem, const flo
                                     float pad_val, float* out, int C, int rpc, int T, int ldT, hipStream_t s,
                                     unsigned long long* stamp, float* attn_dbg, size_t dbg_stride) {
   if (rpc != 1 || T < 1 || T > 512 || ldT < T || C < 1) return hipErrorInvalidValue;
-  static const int expt = [] {
-    const char* e = getenv("ND_MEM_EXPT");  // timing experiments only (wrong results): 1 no loads, 2 no MFMA
-    return e ? atoi(e) : 0;
-  }();
   const bool full = (T + MB_TILE - 1) / MB_TILE == 8;  // the 512-sample chunks of every bench / translate batch
-#define ND_MB_LAUNCH(X)                                                                                           \
-  do {                                                                                                            \
-    if (full)                                                                                                     \
-      hipLaunchKernelGGL((dec_mem_attention_kernel<X, 8>), dim3(C), dim3(MB_NW * 64), mem_lds_bytes(), s, qp, mem, \
-                         signal, span, pad_val, out, T, ldT, stamp, attn_dbg, dbg_stride);                        \
-    else                                                                                                          \
-      hipLaunchKernelGGL((dec_mem_attention_kernel<X, 0>), dim3(C), dim3(MB_NW * 64), mem_lds_bytes(), s, qp, mem, \
-                         signal, span, pad_val, out, T, ldT, stamp, attn_dbg, dbg_stride);                        \
-  } while (0)
-  if (expt == 1) ND_MB_LAUNCH(1);
-  else if (expt == 2) ND_MB_LAUNCH(2);
-  else if (expt == 3) ND_MB_LAUNCH(3);
-  else ND_MB_LAUNCH(0);
-#undef ND_MB_LAUNCH
+  if (full)
+    hipLaunchKernelGGL((dec_mem_attention_kernel<8>), dim3(C), dim3(MB_NW * 64), mem_lds_bytes(), s, qp, mem, signal,
+                       span, pad_val, out, T, ldT, stamp, attn_dbg, dbg_stride);
+  else
+    hipLaunchKernelGGL((dec_mem_attention_kernel<0>), dim3(C), dim3(MB_NW * 64), mem_lds_bytes(), s, qp, mem, signal,
+                       span, pad_val, out, T, ldT, stamp, attn_dbg, dbg_stride);
   return hipGetLastError();
 }
 
@@ -358,10 +346,7 @@ hipError_t launch_stamp_reset(unsigned long long* stamps, int pairs, hipStream_t
 }
 
 hipError_t init_mem_attributes() {
-  const void* fns[] = {(const void*)dec_mem_attention_kernel<0, 0>, (const void*)dec_mem_attention_kernel<1, 0>,
-                       (const void*)dec_mem_attention_kernel<2, 0>, (const void*)dec_mem_attention_kernel<3, 0>,
-                       (const void*)dec_mem_attention_kernel<0, 8>, (const void*)dec_mem_attention_kernel<1, 8>,
-                       (const void*)dec_mem_attention_kernel<2, 8>, (const void*)dec_mem_attention_kernel<3, 8>};
+  const void* fns[] = {(const void*)dec_mem_attention_kernel<0>, (const void*)dec_mem_attention_kernel<8>};
   for (const void* f : fns) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mem_lds_bytes());
     if (e != hipSuccess) return e;

@@ -78,6 +78,11 @@ class Engine:
         """0: memory-bank context attention for greedy (default), 1: per-layer K/V always."""
         _lib.check(self._L.nd_set_ctx_path(self._h, int(path)), "nd_set_ctx_path")
 
+    def set_exact_fp32(self, on: bool):
+        """Exact fp32 (fp32-MFMA kernels for every product) instead of the
+        default split-fp16 products (22-bit operands, fp32 accumulation)."""
+        _lib.check(self._L.nd_set_exact_fp32(self._h, int(on)), "nd_set_exact_fp32")
+
     def set_timing(self, on: bool):
         _lib.check(self._L.nd_set_timing(self._h, int(on)), "nd_set_timing")
 
@@ -99,10 +104,12 @@ class Engine:
 
     def _inputs(self, signal, lengths, spans):
         dev = self.device
-        signal = torch.as_tensor(signal, dtype=torch.float32).to(dev).contiguous()
+        # pinned host inputs (the Translator's staging ring) copy asynchronously
+        signal = torch.as_tensor(signal, dtype=torch.float32).to(dev, non_blocking=True).contiguous()
         B, T = signal.shape
-        lengths = torch.as_tensor(lengths).to(dev, torch.int32).contiguous()
-        spans = lengths.clone() if spans is None else torch.as_tensor(spans).to(dev, torch.int32).contiguous()
+        lengths = torch.as_tensor(lengths).to(dev, torch.int32, non_blocking=True).contiguous()
+        spans = lengths.clone() if spans is None else \
+            torch.as_tensor(spans).to(dev, torch.int32, non_blocking=True).contiguous()
         assert lengths.shape == (B,) and spans.shape == (B,)
         return signal, lengths, spans, B, T
 

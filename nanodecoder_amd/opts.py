@@ -61,9 +61,11 @@ def translate_parser() -> argparse.ArgumentParser:
     _add(g, "window_stride", type=float, default=0.015)
     _add(g, "window", default="hamming")
     g = p.add_argument_group("MI355X engine (additions)")
-    _add(g, "pack_reads", type=int, default=1,
-         help="translate this many reads per engine pass (chunks packed across reads; same outputs)")
-    _add(g, "engine_max_batch", type=int, default=0, help="engine batch capacity (0 = max(batch_size, 8))")
+    _add(g, "pack_reads", type=int, default=0,
+         help="translate this many reads per engine pass (chunks packed across reads; same outputs); "
+              "0 = as many reads as fill the engine batch")
+    _add(g, "engine_max_batch", type=int, default=0,
+         help="engine batch capacity in chunks (0 = max(batch_size, 256): a full MI355X batch)")
     _add(g, "seed", type=int, default=-1, help="random sampling seed (-1: fresh entropy per run)")
     _add(g, "frontend", default="cpu", choices=["cpu", "gpu"],
          help="gpu: normalise and window the reads on the GPU (frontend.hip) instead of in the worker pool")

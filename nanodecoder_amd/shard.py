@@ -47,14 +47,17 @@ def read_lengths(n_reads: int, seed: int = 0, lo: int = 256, hi: int = 1024) -> 
     return np.random.default_rng(seed).integers(lo, hi + 1, size=n_reads)
 
 
-def synth_read(read_id: int, n: int) -> np.ndarray:
-    """Vectorised synthetic read (same model as synth.synth_raw_read),
-    median/MAD normalised, float64."""
+def synth_raw(read_id: int, n: int) -> np.ndarray:
+    """Vectorised synthetic raw DAC trace (same model as synth.synth_raw_read)."""
     rng = np.random.default_rng(1234 + read_id)
     dw = rng.geometric(1.0 / 9.0, size=n // 2 + 16)
     lv = rng.normal(90.0, 15.0, size=dw.size)
-    raw = np.round(np.repeat(lv, dw)[:n] + rng.normal(0.0, 2.0, size=n))
-    return synth.normalize_median(raw)
+    return np.round(np.repeat(lv, dw)[:n] + rng.normal(0.0, 2.0, size=n))
+
+
+def synth_read(read_id: int, n: int) -> np.ndarray:
+    """synth_raw, median/MAD normalised, float64."""
+    return synth.normalize_median(synth_raw(read_id, n))
 
 
 def pack_weights(W: Dict[str, np.ndarray]):
@@ -90,49 +93,129 @@ def broadcast_weights(W, device) -> Dict[str, np.ndarray]:
 
 class ReadShard:
     """Translates one rank's reads with a Translator-like object exposing
-    ``translate_reads(list_of_chunk_lists, batch_size)``."""
+    ``stream_reads(iterable_of_chunk_lists, batch_size)``.
+
+    The host front end (median/MAD normalisation + windowing,
+    utils/labelop.py:194-233) runs in a producer thread and overlaps the
+    device: the Translator keeps one engine batch in flight while it packs
+    the next, and the producer stays up to ``prefetch`` reads ahead."""
 
     def __init__(self, translator, batch_size: int = 100, src_seq_length: int = 512, src_seq_stride: int = 512,
-                 reads_per_pass: int = 256):
+                 prefetch: int = 2048):
         self.tr = translator
         self.batch_size = batch_size
         self.L, self.stride = src_seq_length, src_seq_stride
-        self.reads_per_pass = reads_per_pass
+        self.prefetch = prefetch
 
-    def run(self, read_ids: Sequence[int], lengths: Sequence[int], keep_predictions: bool = False):
+    def _produce(self, read_ids, lengths, raws, q, stop):
+        try:
+            for k, rid in enumerate(read_ids):
+                if stop.is_set():
+                    return
+                if raws is not None:
+                    sig = synth.normalize_median(raws[k])
+                else:
+                    sig = synth_read(int(rid), int(lengths[rid]))
+                q.put(synth.window(sig, self.L, self.stride))
+            q.put(None)
+        except BaseException as e:  # surfaced in the consumer
+            q.put(e)
+
+    def run(self, read_ids: Sequence[int], lengths: Sequence[int], keep_predictions: bool = False, raws=None):
+        """Translate the reads ``read_ids`` (lengths indexed by read id).  With
+        ``raws`` (raw DAC traces, one per read id in order) only the front end
+        is timed; otherwise the synthetic reads are generated on the fly."""
+        import queue
+        import threading
+        q: "queue.Queue" = queue.Queue(maxsize=max(1, self.prefetch))
+        stop = threading.Event()
+        th = threading.Thread(target=self._produce, args=(list(read_ids), lengths, raws, q, stop), daemon=True)
         samples = bases = chunks = 0
         preds = {}
+        specials = {self.tr.cfg.unk_idx, self.tr.cfg.pad_idx, self.tr.cfg.bos_idx}
+        eos = self.tr.cfg.eos_idx
+        n_samples = {}
+
+        def reads():
+            k = 0
+            while True:
+                item = q.get()
+                if item is None:
+                    return
+                if isinstance(item, BaseException):
+                    raise item
+                n_samples[k] = (sum(len(c) for c in item), len(item))
+                k += 1
+                yield item
+
         t0 = time.perf_counter()
-        for g0 in range(0, len(read_ids), self.reads_per_pass):
-            ids = read_ids[g0: g0 + self.reads_per_pass]
-            reads = [synth.window(synth_read(int(i), int(lengths[i])), self.L, self.stride) for i in ids]
-            outs = self.tr.translate_reads(reads, batch_size=self.batch_size)
-            for rid, rd, (_, p) in zip(ids, reads, outs):
-                samples += sum(len(c) for c in rd)
-                chunks += len(rd)
-                bases += sum(len(x[0].replace(" ", "")) for x in p)
+        th.start()
+        try:
+            for k, res in self.tr.stream_reads(reads(), self.batch_size):
+                ns, nc = n_samples.pop(k)
+                samples += ns
+                chunks += nc
+                for r in res:
+                    toks = r[1][0]
+                    for t in toks:
+                        if t == eos:
+                            break
+                        bases += t not in specials
                 if keep_predictions:
-                    preds[int(rid)] = p
-        return dict(samples=samples, bases=bases, chunks=chunks, seconds=time.perf_counter() - t0), preds
+                    preds[int(read_ids[k])] = [[" ".join(self.tr._tokens_to_sent(t)) for t in r[1]] for r in res]
+        finally:
+            stop.set()
+            while th.is_alive():  # unblock a producer waiting on a full queue
+                try:
+                    q.get_nowait()
+                except Exception:
+                    pass
+                th.join(timeout=0.01)
+        return dict(samples=samples, bases=bases, chunks=chunks, seconds=time.perf_counter() - t0,
+                    reads=len(read_ids)), preds
 
 
 def run_distributed(n_reads: int, translator_factory: Callable, weights_factory: Callable, device,
-                    batch_size: int = 100, seed: int = 0, keep_predictions: bool = False):
-    """Rank-local part of the sharded job; returns (global stats, local preds)."""
-    rank, world = dist.get_rank(), dist.get_world_size()
+                    batch_size: int = 100, seed: int = 0, keep_predictions: bool = False, pregenerate: bool = False,
+                    warmup_reads: int = 0):
+    """Rank-local part of the sharded job; returns (global stats, local preds).
+    The timed region (max over ranks) covers the front end, packing, the
+    engine and the token copies of the rank's reads."""
+    multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    rank, world = (dist.get_rank(), dist.get_world_size()) if multi else (0, 1)
     lengths = read_lengths(n_reads, seed)
     mine = lpt_assign(lengths.tolist(), world)[rank]
     W = weights_factory() if rank == 0 else None
-    W = broadcast_weights(W, device)
+    if multi:
+        W = broadcast_weights(W, device)
     tr = translator_factory(W)
-    dist.barrier()
-    stats, preds = ReadShard(tr, batch_size=batch_size).run(mine, lengths, keep_predictions)
-    dist.barrier()
+    raws = None
+    if pregenerate:  # the raw traces stand in for files already read (untimed); the front end is timed
+        raws = [synth_raw(int(i), int(lengths[i])) for i in mine]
+    if warmup_reads:  # graphs captured and pinned buffers made outside the timed region
+        ReadShard(tr, batch_size=batch_size).run(mine[:warmup_reads], lengths)
+    on_gpu = device.type == "cuda" and torch.cuda.is_available()
+    if multi:
+        dist.barrier()
+    if on_gpu:
+        torch.cuda.synchronize(device)
+    stats, preds = ReadShard(tr, batch_size=batch_size).run(mine, lengths, keep_predictions, raws=raws)
+    if on_gpu:
+        torch.cuda.synchronize(device)
+    if multi:
+        dist.barrier()
     red = torch.tensor([stats["samples"], stats["bases"], stats["chunks"]], dtype=torch.float64, device=device)
     secs = torch.tensor([stats["seconds"]], dtype=torch.float64, device=device)
-    dist.all_reduce(red)
-    dist.all_reduce(secs, op=dist.ReduceOp.MAX)
-    g = dict(samples=int(red[0]), bases=int(red[1]), chunks=int(red[2]), seconds=float(secs[0]), world=world)
+    per_rank = torch.zeros(world, dtype=torch.float64, device=device)
+    per_rank[rank] = stats["samples"]
+    if multi:
+        dist.all_reduce(red)
+        dist.all_reduce(per_rank)
+        dist.all_reduce(secs, op=dist.ReduceOp.MAX)
+    loads = per_rank.cpu().numpy()
+    g = dict(samples=int(red[0]), bases=int(red[1]), chunks=int(red[2]), seconds=float(secs[0]), world=world,
+             reads=int(n_reads), samples_per_rank=[int(x) for x in loads],
+             load_imbalance=float(loads.max() / max(loads.mean(), 1.0)))
     return g, preds
 
 

@@ -25,13 +25,14 @@ from __future__ import annotations
 
 import json
 import os
-from typing import List, Optional, Sequence
+from typing import Iterable, List, Optional, Sequence
 
 import numpy as np
 import torch
 
 from . import checkpoint
 from .engine import Engine
+from .engine import Engine as _HipEngine  # the real engine class (tests substitute Engine)
 
 
 class GNMTGlobalScorer:
@@ -117,7 +118,7 @@ class Translator(object):
         self.out_file_attn = None
         self._check_supported()
         batch_cap = max(1, int(getattr(opt, "batch_size", 100)))
-        self.max_batch = int(getattr(opt, "engine_max_batch", 0)) or max(batch_cap, 8)
+        self.max_batch = int(getattr(opt, "engine_max_batch", 0) or 0) or max(batch_cap, 256)
         if engine is None:
             dev = torch.cuda.current_device()  # the reference moves tensors to the default "cuda" device
             engine = Engine(cfg, weights, device=dev, max_batch=self.max_batch,
@@ -125,6 +126,7 @@ class Translator(object):
                             int(getattr(opt, "src_seq_length", 512)) <= 512 else 512,
                             max_steps=self.max_length, max_beam=max(1, self.beam_size))
         self.engine = engine
+        self._pinned, self._pin_i, self._copy_stream = None, 0, None
 
     def _check_supported(self):
         if self.beam_size == 1:
@@ -161,13 +163,32 @@ class Translator(object):
         self.out_file_attn = out_file_attn
 
     # ------------------------------------------------------------------ core
-    def _run(self, chunks: List[np.ndarray], spans: Sequence[int], groups: Optional[Sequence[int]] = None,
-             attn: bool = False):
-        """Run the engine on up to max_batch chunks with their reference
-        spans (and, for the classic Beam, their reference batch ids).
-        Returns per chunk (scores[n_best], token lists[n_best]) and, with
-        ``attn``, the attention rows of each hypothesis ([steps, cut] arrays,
-        cut as the reference's results["attention"] has it)."""
+    def _stage(self, B: int, T: int):
+        """Host staging of one engine batch: views into a ring of pinned
+        buffers (real engine; the host-to-device copies then run async, so the
+        next batch is packed while the device works on this one), or plain
+        numpy arrays (stand-in engines)."""
+        if not isinstance(self.engine, _HipEngine):
+            return np.zeros((B, T), np.float32), np.ones(B, np.int32), np.ones(B, np.int32), None
+        if self._pinned is None:
+            cap, tl = self.engine.max_batch, self.engine.max_src_len
+            self._pinned = [(torch.empty(cap * tl, dtype=torch.float32).pin_memory(),
+                             torch.empty(2 * cap, dtype=torch.int32).pin_memory()) for _ in range(3)]
+        fbuf, ibuf = self._pinned[self._pin_i % len(self._pinned)]
+        self._pin_i += 1
+        sig_t = fbuf[: B * T].view(B, T)
+        sig_t.zero_()
+        L_t, S_t = ibuf[:B], ibuf[B: 2 * B]
+        L_t.fill_(1)
+        S_t.fill_(1)
+        return sig_t.numpy(), L_t.numpy(), S_t.numpy(), (sig_t, L_t, S_t)
+
+    def _submit(self, chunks: List[np.ndarray], spans: Sequence[int], groups: Optional[Sequence[int]] = None,
+                attn: bool = False):
+        """Stage up to max_batch chunks with their reference spans (and, for
+        the classic Beam, their reference batch ids) and enqueue the engine
+        call.  Greedy and sampling calls return before the device finishes;
+        ``_finish`` collects the results."""
         n = len(chunks)
         lens = np.array([len(c) for c in chunks], np.int32)
         if (lens < 1).any():
@@ -177,13 +198,13 @@ class Translator(object):
             raise ValueError(f"chunk longer than {self.engine.max_src_len} samples (src_seq_length) is not supported")
         T = min(self.engine.max_src_len, ((int(spans.max()) + 63) // 64) * 64)
         B = _bucket(n, self.engine.max_batch)
-        sig = np.zeros((B, T), np.float32)
+        sig, L, S, dev_in = self._stage(B, T)
         for i, c in enumerate(chunks):
             sig[i, : len(c)] = c
-        L = np.ones(B, np.int32)
-        S = np.ones(B, np.int32)
         L[:n], S[:n] = lens, spans
-        out = []
+        if dev_in is not None:
+            sig, L, S = dev_in
+        job = dict(n=n, lens=lens, attn=attn, B=B, inputs=dev_in)
         if self.beam_size == 1:
             if not (self.random_sampling_temp == 0.0 or self.sample_from_topk == 1):
                 # sample_with_temperature's random branch (translator.py:376-393)
@@ -195,15 +216,7 @@ class Translator(object):
             else:
                 r = self.engine.translate_greedy(sig, L, S, max_len=self.max_length, min_len=self.min_length,
                                                  return_attn=attn)
-            if attn:
-                at = r["attn"].cpu().numpy()
-            tok = r["tokens"].cpu().numpy()
-            sc = r["scores"].cpu().numpy()
-            for i in range(n):
-                if attn:  # results["attention"]: rows cut at the chunk's length (translator.py:491-501)
-                    out.append(([float(sc[i])], [tok[i].tolist()], [at[i, :, : lens[i]]]))
-                else:
-                    out.append(([float(sc[i])], [tok[i].tolist()]))
+            job.update(kind="greedy", r=r)
         else:
             # reference batches: the chunks of one group, sorted by length
             # descending (stable) as the reference's batch rows are
@@ -213,6 +226,7 @@ class Translator(object):
                 members.setdefault(int(grp[i]), []).append(i)
             sorted_rows = {gid: sorted(m, key=lambda i: -int(lens[i])) for gid, m in members.items()}
             beam = self.beam_size
+            cut = None
             if self.fast:
                 r = self.engine.translate_beam(sig, L, S, beam=beam, n_best=self.n_best,
                                                alpha=self.global_scorer.alpha, max_len=self.max_length,
@@ -236,31 +250,70 @@ class Translator(object):
                     alpha=gs.alpha, max_len=self.max_length, min_len=self.min_length,
                     coverage_penalty=gs.coverage_penalty, beta=gs.beta, stepwise_penalty=self.stepwise_penalty,
                     block_ngram_repeat=self.block_ngram_repeat, ignore_ids=exclusion, cut=cut, return_attn=attn)
-            tok = r["tokens"].cpu().numpy()
-            sc = r["scores"].cpu().numpy()
-            ln = r["lens"].cpu().numpy()
-            if attn:
-                at = r["attn"].cpu().numpy()
-                if self.fast:
-                    done = r["done_step"].cpu().numpy()
-            for i in range(n):
-                o = ([float(sc[i, k]) for k in range(self.n_best)],
-                     [tok[i, k, : ln[i, k]].tolist() for k in range(self.n_best)])
-                if attn:
-                    atts = []
-                    for k in range(self.n_best):
-                        if self.fast:
-                            # translator.py:780-790: attention[:, i, j, :memory_lengths[i]] with i the
-                            # chunk's index among the batches alive at the hypothesis' last step
-                            step = int(ln[i, k]) - 1
-                            alive = [q for q in sorted_rows[int(grp[i])] if done[q] == 0 or done[q] > step]
-                            c = int(lens[alive[alive.index(i) // beam]])
-                        else:
-                            c = int(cut[i])
-                        atts.append(at[i, k, : ln[i, k], :c])
-                    o = o + (atts,)
-                out.append(o)
+            job.update(kind="beam", r=r, grp=grp, sorted_rows=sorted_rows, cut=cut)
+        if isinstance(self.engine, _HipEngine):
+            # fires when this call's outputs are written (the engine's release
+            # event is ordered before it on the current stream)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.engine.device))
+            job["event"] = ev
+        return job
+
+    def _host(self, job, *names):
+        """Results of a submitted call on the host.  The copies wait only for
+        THIS call (its event, on a side stream), not for calls submitted after
+        it on the current stream."""
+        r = job["r"]
+        ev = job.get("event")
+        if ev is None:
+            return [None if r.get(k) is None else r[k].cpu().numpy() for k in names]
+        if self._copy_stream is None:
+            self._copy_stream = torch.cuda.Stream(self.engine.device)
+        cs = self._copy_stream
+        with torch.cuda.stream(cs):
+            cs.wait_event(ev)
+            out = [None if r.get(k) is None else r[k].cpu().numpy() for k in names]
         return out
+
+    def _finish(self, job):
+        """Per chunk (scores[n_best], token lists[n_best]) and, with ``attn``,
+        the attention rows of each hypothesis ([steps, cut] arrays, cut as the
+        reference's results["attention"] has it)."""
+        n, lens, attn = job["n"], job["lens"], job["attn"]
+        out = []
+        if job["kind"] == "greedy":
+            tok, sc, at = self._host(job, "tokens", "scores", "attn")
+            for i in range(n):
+                if attn:  # results["attention"]: rows cut at the chunk's length (translator.py:491-501)
+                    out.append(([float(sc[i])], [tok[i].tolist()], [at[i, :, : lens[i]]]))
+                else:
+                    out.append(([float(sc[i])], [tok[i].tolist()]))
+            return out
+        grp, sorted_rows, cut, beam = job["grp"], job["sorted_rows"], job["cut"], self.beam_size
+        tok, sc, ln, at, done = self._host(job, "tokens", "scores", "lens", "attn", "done_step")
+        for i in range(n):
+            o = ([float(sc[i, k]) for k in range(self.n_best)],
+                 [tok[i, k, : ln[i, k]].tolist() for k in range(self.n_best)])
+            if attn:
+                atts = []
+                for k in range(self.n_best):
+                    if self.fast:
+                        # translator.py:780-790: attention[:, i, j, :memory_lengths[i]] with i the
+                        # chunk's index among the batches alive at the hypothesis' last step
+                        step = int(ln[i, k]) - 1
+                        alive = [q for q in sorted_rows[int(grp[i])] if done[q] == 0 or done[q] > step]
+                        c = int(lens[alive[alive.index(i) // beam]])
+                    else:
+                        c = int(cut[i])
+                    atts.append(at[i, k, : ln[i, k], :c])
+                o = o + (atts,)
+            out.append(o)
+        return out
+
+    def _run(self, chunks: List[np.ndarray], spans: Sequence[int], groups: Optional[Sequence[int]] = None,
+             attn: bool = False):
+        """One engine batch, synchronously (see _submit / _finish)."""
+        return self._finish(self._submit(chunks, spans, groups, attn))
 
     def _tokens_to_sent(self, toks) -> List[str]:
         """translate/translation.py:31-47."""
@@ -297,28 +350,68 @@ class Translator(object):
             output += row_format.format(*row) + "\n"
         self.out_file_attn.write(output)
 
-    def translate_reads(self, reads: Sequence[Sequence], batch_size: int, attn_debug: bool = False):
-        """Translate many reads; chunks are packed across reads into engine
-        batches of up to max_batch.  Each chunk keeps the span of the
-        reference batch it would belong to (consecutive ``batch_size`` chunks
-        of its own read), so results equal per-read translate()."""
-        items = []  # (read idx, chunk idx, array, span, reference batch id)
+    def stream_reads(self, reads: Iterable[Sequence], batch_size: int, attn_debug: bool = False):
+        """Generator over many reads (any iterable of chunk lists): chunks are
+        packed across reads into engine batches of max_batch, one batch stays
+        in flight on the device while the next is packed on the host, and
+        (read index, per-chunk results) is yielded as each read completes.
+        Each chunk keeps the span of the reference batch it would belong to
+        (consecutive ``batch_size`` chunks of its own read), so results equal
+        per-read translate()."""
+        cap = self.engine.max_batch
+        pending, inflight = [], None
+        results, remaining = {}, {}
         nb = 0
+
+        def collect(jb):
+            job, items = jb
+            done = []
+            for (ri, ci, c, _, _), o in zip(items, self._finish(job)):
+                results[ri][ci] = o + (c,) if attn_debug else o
+                remaining[ri] -= 1
+                if remaining[ri] == 0:
+                    done.append(ri)
+            return done
+
+        def submit(items):
+            return self._submit([g[2] for g in items], [g[3] for g in items], [g[4] for g in items],
+                                attn=attn_debug), items
+
         for ri, read in enumerate(reads):
             chunks = [parse_chunk(c) for c in read]
+            if not chunks:
+                yield ri, []
+                continue
+            results[ri], remaining[ri] = [None] * len(chunks), len(chunks)
             for b0 in range(0, len(chunks), batch_size):
                 part = chunks[b0: b0 + batch_size]
                 span = max(len(c) for c in part)
                 for k, c in enumerate(part):
-                    items.append((ri, b0 + k, c, span, nb))
+                    pending.append((ri, b0 + k, c, span, nb))
+                    if len(pending) == cap:
+                        nxt = submit(pending)
+                        pending = []
+                        if inflight is not None:
+                            for r in collect(inflight):
+                                yield r, results.pop(r)
+                        inflight = nxt
                 nb += 1
-        results = [[None] * len(r) for r in reads]
-        cap = self.engine.max_batch
-        for s0 in range(0, len(items), cap):
-            grp = items[s0: s0 + cap]
-            outs = self._run([g[2] for g in grp], [g[3] for g in grp], [g[4] for g in grp], attn=attn_debug)
-            for (ri, ci, c, _, _), o in zip(grp, outs):
-                results[ri][ci] = o + (c,) if attn_debug else o
+        if pending:
+            nxt = submit(pending)
+            if inflight is not None:
+                for r in collect(inflight):
+                    yield r, results.pop(r)
+            inflight = nxt
+        if inflight is not None:
+            for r in collect(inflight):
+                yield r, results.pop(r)
+
+    def translate_reads(self, reads: Sequence[Sequence], batch_size: int, attn_debug: bool = False):
+        """Translate many reads (stream_reads); returns per read
+        (all_scores, all_predictions) as translate() does."""
+        results = [None] * len(reads)
+        for ri, res in self.stream_reads(reads, batch_size, attn_debug):
+            results[ri] = res
         ret = []
         counter = 0
         pred_score_total, pred_words_total = 0.0, 0

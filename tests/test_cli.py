@@ -68,3 +68,33 @@ def test_cli_attn_debug_and_beam_flags(tmp_path, monkeypatch):
         lines = [ln for ln in (out / "attention" / f"read{i}.txt").read_text().splitlines() if ln.strip()]
         headers = [ln for ln in lines if ln.lstrip().startswith(">")]
         assert len(headers) == n_chunks
+
+
+def test_cli_empty_read_and_auto_pack(tmp_path, monkeypatch):
+    """An empty .signal read is skipped, not fatal (translate.py:102-103), on
+    both front ends' worker paths; -pack_reads 0 (default) packs reads until
+    the engine batch is full and writes every read."""
+    import nanodecoder_amd.translator as T
+    monkeypatch.setattr(T, "Engine", _Eng)
+    monkeypatch.setattr(torch.cuda, "current_device", lambda: 0)
+    cfg = synth.ModelConfig()
+    ck = tmp_path / "m.pt"
+    checkpoint.save_synthetic(str(ck), cfg, synth.make_weights(cfg, seed=1))
+    src = tmp_path / "reads"
+    src.mkdir()
+    for i, n in enumerate((1300, 700, 400, 2100)):
+        raw = synth.synth_raw_read(i, n)
+        (src / f"read{i}.signal").write_text(" ".join(str(int(v)) for v in raw))
+    (src / "empty.signal").write_text("")
+    # the -frontend gpu worker: an empty read is [prefix] alone (skipped), not [prefix, empty]
+    job = (str(src / "empty.signal"), "empty.txt", "signal", "median", 512, 512)
+    assert cli._read_only(job) == ["empty.txt"]
+    out = tmp_path / "out"
+    o = opts.parse_translate_opts(["-model", str(ck), "-src_dir", str(src), "-save_data", str(out), "-gpu", "0",
+                                   "-beam_size", "1", "-batch_size", "2", "-thread", "2", "-max_length", "10",
+                                   "-engine_max_batch", "4"])
+    assert o.pack_reads == 0
+    assert cli.main(o) == 4
+    for i in range(4):
+        assert (out / "result" / f"read{i}.fasta").exists()
+    assert not (out / "result" / "empty.fasta").exists()

@@ -632,7 +632,7 @@ def test_cli_gpu_frontend_matches_host(tmp_path, monkeypatch):
             assert ca.dtype == cb.dtype == np.float32 and (ca.view(np.uint32) == cb.view(np.uint32)).all()
 
 
-@pytest.mark.parametrize("layer0,bn", [(True, False), (False, False), (False, True)])
+@pytest.mark.parametrize("layer0,bn", [(True, False), (False, False), (False, True), (True, True)])
 def test_nano_lstm_layer_vs_torch_lstm(layer0, bn):
     """One BiLSTM layer through nd_op_lstm_layer against torch.nn.LSTM (CPU,
     fp32) over packed ragged sequences (encoder/nano_encoder.py:92-111: pack,
@@ -683,3 +683,8 @@ def test_nano_lstm_layer_vs_torch_lstm(layer0, bn):
     assert (got[pad] == 0).all(), "rows past a sequence's length must stay zero"
     err = float((got - ref).abs().max())
     assert err < 1e-4, err
+    # step 0 of each direction (forward pos 0, reverse pos len - 1): the rows
+    # written before the first in-loop barrier, BatchNorm table included
+    for b in range(B):
+        for row, cols in ((b * T, slice(0, H)), (b * T + int(lens[b]) - 1, slice(H, 2 * H))):
+            assert float((got[row, cols] - ref[row, cols]).abs().max()) < 1e-4, (b, row)

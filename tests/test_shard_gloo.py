@@ -32,13 +32,24 @@ def test_pack_unpack_roundtrip():
 
 
 class FakeTranslator:
-    """Per chunk: 'A' * (len % 7) — depends only on the chunk."""
+    """Per chunk: 'A' * (len % 7) then EOS — depends only on the chunk."""
 
     def __init__(self, W):
         self.W = W
+        from nanodecoder_amd import synth
+        self.cfg = synth.ModelConfig()
 
-    def translate_reads(self, reads, batch_size):
-        return [([[0.0]] * len(r), [[" ".join("A" * (len(c) % 7))] for c in r]) for r in reads]
+    def _tokens_to_sent(self, toks):
+        out = []
+        for t in toks:
+            if t == self.cfg.eos_idx:
+                break
+            out.append(self.cfg.itos[t])
+        return out
+
+    def stream_reads(self, reads, batch_size):
+        for ri, r in enumerate(reads):
+            yield ri, [([0.0], [[4] * (len(c) % 7) + [3, 5]]) for c in r]
 
 
 def _free_port():
