@@ -277,6 +277,11 @@ SCENARIOS = [
          beam2=dict(beam_size=5, n_best=3, max_length=60, min_length=10)),
     dict(name="nano_greedy", cfg=dict(encoder_type="nano"), seed=14, eos_bias=-2.0,
          chunks=dict(kind="mixed"), greedy=dict(max_length=60)),
+    # -cpg models (models/opts.py:254): the methylated-C label 'M' is a fifth base, V = 9
+    dict(name="transformer_cpg", cfg=dict(encoder_type="transformer",
+                                          itos=["<unk>", "<blank>", "<s>", "</s>", "A", "C", "G", "T", "M"]),
+         seed=19, eos_bias=-1.0, chunks=dict(kind="ragged"), greedy=dict(max_length=60, min_length=5),
+         beam=dict(beam_size=5, n_best=2, max_length=50, min_length=5)),
     # decoder with average self-attention (onmt/modules/average_attn.py), greedy and --fast beam
     # the classic onmt Beam (no --fast): length penalties none / wu, n_best 1 and 3
     dict(name="transformer_classic_beam", cfg=dict(encoder_type="transformer"), seed=16, eos_bias=2.5,

@@ -146,3 +146,44 @@ def test_windows_match_window():
             assert len(got) == len(exp)
             for (a, b), e in zip(got, exp):
                 assert b == len(e) and (x[a: a + b].astype(np.float32) == e).all()
+
+
+# ---------------------------------------------------------------- pinned to the reference's labelop.py
+def _golden_frontend():
+    from tests import golden_util as gu
+    return gu, *gu.load_frontend()
+
+
+def test_extract_raw_vs_reference_labelop(tmp_path):
+    """frontend.extract_raw on .signal files against the chunks the
+    reference's own extract_fast5_raw cut from the same files
+    (tests/golden/frontend.npz, oracle/make_golden_frontend.py): median / mean
+    / None normalisation at 512/512 and the 300/60 overlap setting; bit-exact
+    float32, NaN where the reference divides by a zero MAD or std."""
+    gu, z, meta = _golden_frontend()
+    for i in range(meta["reads"]):
+        raw = z[f"raw{i}"]
+        path = tmp_path / f"read{i}.signal"
+        path.write_text(" ".join(str(int(v)) if float(v).is_integer() else repr(float(v)) for v in raw))
+        for si, (norm, ml, st) in enumerate(meta["settings"]):
+            with np.errstate(divide="ignore", invalid="ignore"):
+                got = frontend.extract_raw(str(path), f"read{i}.txt", norm, ml, st, "signal")
+            exp = gu.frontend_chunks(z, i, si)
+            assert got[0] == f"read{i}.txt" and len(got) - 1 == len(exp), (i, si)
+            for g, e in zip(got[1:], exp):
+                assert gu.same_f32(g, e), (i, si)
+
+
+def test_simple_assembly_vs_reference_labelop():
+    """frontend.simple_assembly / index2base against the reference's own
+    simple_assembly on overlapping-window predictions with substitutions,
+    indels, an empty chunk and a read that grows the consensus past 1000
+    columns: identical count matrices and base strings, both branches."""
+    gu, z, meta = _golden_frontend()
+    for j in range(len(meta["assembly"])):
+        preds = [[str(p)] for p in z[f"asm_preds{j}"]]
+        cons = frontend.simple_assembly(preds)
+        assert cons.shape == z[f"asm_cons{j}"].shape and (cons == z[f"asm_cons{j}"]).all(), j
+        assert frontend.index2base(np.argmax(cons, axis=0)) == str(z[f"asm_seq{j}"]), j
+        assert frontend.simple_assembly(preds, flag_intersection=False) == str(z[f"asm_concat{j}"]), j
+        assert frontend.assemble_read(preds, 300, 60) == str(z[f"asm_seq{j}"])

@@ -246,7 +246,8 @@ def test_encoder_memory_vs_golden(name):
     assert np.abs(sub - z["memory_sub"]).max() < 1e-4
 
 
-@pytest.mark.parametrize("name", ["transformer_greedy", "transformer_pe_short", "nano_greedy", "transformer_aan"])
+@pytest.mark.parametrize("name", ["transformer_greedy", "transformer_pe_short", "nano_greedy", "transformer_aan",
+                                  "transformer_cpg"])
 @pytest.mark.parametrize("graphs,ctx_path", [(True, 0), (False, 0), (True, 1)])
 def test_greedy_vs_golden(name, graphs, ctx_path):
     """ctx_path 0: memory-bank context attention, 1: per-layer K/V form."""
@@ -292,7 +293,7 @@ def test_greedy_attention_vs_golden(graphs, ctx_path):
 
 
 @pytest.mark.parametrize("name,which", [("transformer_beam", ""), ("transformer_beam", "2"),
-                                        ("transformer_aan", "")])
+                                        ("transformer_aan", ""), ("transformer_cpg", "")])
 def test_beam_vs_golden(name, which):
     """--fast beam (average self-attention included: its running average
     follows the beam ancestry)."""
@@ -513,6 +514,75 @@ def test_greedy_vs_oracle_batch32():
     assert gu.logp_close(got_lp[same], o["logp"][same], atol=LOGP_ATOL).all()
 
 
+def _reads_for_packing():
+    """Median/MAD-normalised synthetic reads windowed at 512: short last
+    chunks, one-chunk reads, a read shorter than a chunk."""
+    from nanodecoder_amd import frontend
+    reads = []
+    for i, n in enumerate((1300, 700, 512, 2049, 300, 1100, 1536, 90)):
+        reads.append(frontend.window(frontend.normalize(synth.synth_raw_read(50 + i, n), "median"), 512, 512))
+    return reads
+
+
+@pytest.mark.parametrize("beam", [1, 5])
+def test_translate_reads_packed_vs_oracle(beam):
+    """Translator.translate_reads, the CLI / read-shard production path: the
+    chunks of many reads packed into engine batches of 8 (so one call mixes
+    reads and reference batches, and a reference batch of 3 can straddle two
+    calls), each chunk keeping its reference batch's padded length as its
+    span.  Against the oracle run read by read in the reference's own
+    batching (ref_cpu.translate, translate/translator.py:181-369): identical
+    strings, scores within 1e-3."""
+    import types
+    from nanodecoder_amd.translator import Translator
+    ref = _oracle()
+    cfg = synth.ModelConfig()
+    W = synth.make_weights(cfg, seed=11, eos_bias=-1.0 if beam == 1 else 1.0)
+    S, bs = 40, 3
+    eng = _engine(cfg, W, max_batch=8, max_steps=S, max_beam=beam)
+    opt = types.SimpleNamespace(gpu=0, n_best=1, max_length=S, min_length=4, beam_size=beam, fast=True,
+                                batch_size=bs, engine_max_batch=8)
+    tr = Translator(cfg, None, opt, engine=eng)
+    reads = _reads_for_packing()
+    got = tr.translate_reads(reads, batch_size=bs)
+    m = ref.RefModel(cfg, W)
+    n_chunks = 0
+    for ri, chunks in enumerate(reads):
+        es, ep = ref.translate(m, chunks, bs, beam_size=beam, n_best=1, max_length=S, min_length=4)
+        gs, gp = got[ri]
+        assert len(gp) == len(ep) == len(chunks)
+        for ci in range(len(chunks)):
+            assert gp[ci] == ep[ci], (ri, ci, gp[ci], ep[ci])
+            assert abs(gs[ci][0] - es[ci][0]) < 1e-3, (ri, ci)
+            n_chunks += 1
+    assert n_chunks > 16
+
+
+def test_beam_large_batch_vs_oracle():
+    """--fast beam 5 on 416 chunks (2080 decoder rows: the LDS-tiled
+    split-fp16 GEMMs of ND_P16_BIG_MIN's large-M path, as configs[3]'s
+    B = 1024 runs) against the oracle on a sample of the chunks.  Every
+    chunk is a full 512-sample window, so its padded length (and result) does
+    not depend on the rest of its batch: the sample runs as its own batch."""
+    ref = _oracle()
+    cfg = synth.ModelConfig()
+    W = synth.make_weights(cfg, seed=13, eos_bias=1.0)
+    B, S = 416, 30
+    sig = synth.synth_chunk_batch(B, 512, seed=77, inject_masks=False)
+    lens = np.full(B, 512, np.int32)
+    eng = _engine(cfg, W, max_batch=B, max_steps=S, max_beam=5)
+    r = eng.translate_beam(sig, lens, lens, beam=5, n_best=2, max_len=S, min_len=3)
+    tok, sc, ln = (r[k].cpu().numpy() for k in ("tokens", "scores", "lens"))
+    pick = [0, 1, 97, 203, 204, 333, 414, 415]
+    exp = ref.fast_beam(ref.RefModel(cfg, W), sig[pick], lens[pick], beam_size=5, n_best=2, max_length=S,
+                        min_length=3)
+    for j, i in enumerate(pick):
+        for nb, (s, p) in enumerate(exp[j]):
+            assert ln[i, nb] == len(p), (i, nb)
+            assert (tok[i, nb, : len(p)] == p).all(), (i, nb)
+            assert abs(sc[i, nb] - s) < 1e-3, (i, nb)
+
+
 def test_nano_greedy_vs_oracle_ragged():
     """NanoEncoder packing: ragged lengths inside one batch (reverse LSTM
     starts at len-1), B not a multiple of the 16-sequence LSTM group."""
@@ -591,6 +661,31 @@ def test_frontend_normalize_window_vs_host(method):
             assert (got[c, len(e):] == 0).all()
             c += 1
     assert c == len(rd)
+
+
+def test_frontend_gpu_vs_reference_labelop():
+    """nd_normalize_reads + nd_window_reads against the chunks the
+    reference's own extract_fast5_raw cut (tests/golden/frontend.npz): every
+    normalisation at 512/512 and the 300/60 overlap windows.  Bit-exact
+    float32 for median and None (NaN where the reference divides by a zero
+    MAD); mean within 1 ulp (its std is a reduction in another order)."""
+    from nanodecoder_amd import frontend
+    z, meta = gu.load_frontend()
+    raws = [z[f"raw{i}"] for i in range(meta["reads"])]
+    for si, (norm, ml, st) in enumerate(meta["settings"]):
+        sig, lens, rd = frontend.normalize_window_gpu(raws, norm, ml, st)
+        got = sig.cpu().numpy()
+        c = 0
+        for i in range(len(raws)):
+            for e in gu.frontend_chunks(z, i, si):
+                assert rd[c] == i and lens[c] == len(e), (si, i, c)
+                g = got[c, : len(e)]
+                if norm == "mean" and not np.isnan(e).any():
+                    np.testing.assert_array_max_ulp(g, e, maxulp=1)
+                else:
+                    assert gu.same_f32(g, e), (si, i, c)
+                c += 1
+        assert c == len(rd)
 
 
 def test_cli_gpu_frontend_matches_host(tmp_path, monkeypatch):

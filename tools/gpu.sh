@@ -7,6 +7,7 @@
 #   bash tools/gpu.sh bench TAG [bench args]    one bench line -> gpurun_out/TAG.json
 #   bash tools/gpu.sh prof TAG [bench args]     rocprofv3 --kernel-trace --stats of a short bench
 #   bash tools/gpu.sh pmc TAG "CTRS" [args]     one rocprofv3 --pmc pass (one counter group)
+#   bash tools/gpu.sh mfma TAG [args]          rocprofv3 MFMA counter pass -> gpurun_out/TAG_mfma.json
 #   bash tools/gpu.sh list                      rocprofv3 -L (available counters)
 #   bash tools/gpu.sh py TAG script.py [args]   any python tool (probes, microbenches)
 # Steps chain with &&:  bash tools/gpu.sh test && bash tools/gpu.sh bench r02_greedy
@@ -43,6 +44,16 @@ case $step in
       python3 $R/bench.py --steps 1 --warmup 1 --cpu-baseline 0 --exact 0 --host-inclusive 0 --read-shard 0 \
       --no-roofline "$@" > $O/$tag.log 2>&1
     rc=$?; echo "pmc $tag rc=$rc"; exit $rc ;;
+  mfma)
+    # MFMA utilisation counters (one pass: 4 SQ + 1 GRBM), summarised per kernel
+    tag=$1; shift
+    cd /tmp && export TMPDIR=/tmp
+    timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F16 SQ_INSTS_VALU_MFMA_MOPS_F32 \
+      SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d $O/$tag -o run --output-format csv -- \
+      python3 $R/bench.py --steps 1 --warmup 1 --cpu-baseline 0 --exact 0 --host-inclusive 0 --read-shard 0 \
+      --no-roofline "$@" > $O/$tag.log 2>&1
+    rc=$?; echo "mfma $tag rc=$rc"; [ $rc -ne 0 ] && exit $rc
+    python3 $R/tools/mfma_summary.py $O/$tag/run_counter_collection.csv $tag $O/${tag}_mfma.json | head -40; exit 0 ;;
   list)
     cd /tmp && export TMPDIR=/tmp
     timeout -s KILL 60 rocprofv3 -L > $O/counters.txt 2>&1
