@@ -215,15 +215,20 @@ def _pmc(name, key="kernels"):
         return None
 
 
-def _mfma_counters():
-    """The committed rocprof MFMA counter pass (profiles/mfma_summary.json,
-    tools/mfma_summary.py), or None."""
-    p = os.path.join(ROOT, "profiles", "mfma_summary.json")
+def _mfma_counters(which):
+    """The committed rocprof MFMA counter pass of this workload
+    (profiles/r02_mfma_summary.json: tools/gpu.sh mfma -> tools/mfma_summary.py;
+    which = greedy | beam | nano), or None."""
+    p = os.path.join(ROOT, "profiles", "r02_mfma_summary.json")
     try:
         with open(p) as f:
-            return json.load(f)
+            d = json.load(f)[which]
     except Exception:
         return None
+    k = d["kernels"]
+    top = sorted(k.items(), key=lambda kv: -kv[1]["launches"] * kv[1]["avg_us"])[:4]
+    return {"source": "profiles/r02_mfma_summary.json (" + d["tag"] + ")", "path": d["path"],
+            "top_kernels": {n: {x: v[x] for x in ("avg_us", "f16_tflops", "f32_tflops", "mfma_util")} for n, v in top}}
 
 
 def count_bases(tok: np.ndarray, eos: int) -> int:
@@ -234,7 +239,7 @@ def count_bases(tok: np.ndarray, eos: int) -> int:
 
 
 # ----------------------------------------------------------------- roofline
-def kernel_roofline(eng, B, mode, beam, encoder="transformer"):
+def kernel_roofline(eng, B, mode, beam, encoder="transformer", alive=None):
     """Dominant kernel of the translate step, timed LIVE: every launch of it
     inside the timed graph replays carries in-kernel wall-clock stamps
     (first workgroup start, last workgroup end; Engine.set_kernel_stamps), and
@@ -246,7 +251,10 @@ def kernel_roofline(eng, B, mode, beam, encoder="transformer"):
       (2 products x 2 x 8 heads x 512 keys x 256 dims per chunk, on
       v_mfma_f32_4x4x1_16b) is reported beside it.
     beam: the per-layer K/V context attention (dec_ctx_attention_kernel),
-      HBM-bound: K+V 2 x 512 keys x 256 f32 per chunk + q, signal, out."""
+      HBM-bound: K+V 2 x 512 keys x 256 f32 per chunk + q, signal, out, for
+      the chunks still in the decode loop (finished chunks' workgroups exit
+      at once; launches with none alive carry no stamp): achieved = the
+      alive chunks' bytes over all stamped launches / their summed time."""
     us, n = eng.kernel_stamps()
     T, D = 512, 256
     ms = us * 1e-3
@@ -259,11 +267,17 @@ def kernel_roofline(eng, B, mode, beam, encoder="transformer"):
                                "unit": "TFLOP/s", "frac": round(tf / FP32_PEAK, 4)}}
     else:
         name = f"dec_ctx_attention_kernel<{beam}>"
-        nbytes = B * T * 2 * D * 4 + B * T * 4 + 2 * B * beam * D * 4
+        per_chunk = T * 2 * D * 4 + T * 4 + 2 * beam * D * 4
+        nbytes = B * per_chunk
         extra = {}
+        if alive is not None and n > 0:
+            # mean bytes of a stamped launch (3 layers per step with >= 1 alive chunk)
+            nbytes = int(3 * sum(alive) * per_chunk / n)
+            extra = {"alive_chunks_per_launch": round(3 * sum(alive) / n, 1)}
     ach = nbytes / (ms * 1e-3) / 1e9
     out = {"bound": "hbm", "kernel": name, "achieved": round(ach, 1), "peak": HBM_PEAK, "unit": "GB/s",
-           "frac": round(ach / HBM_PEAK, 4), "traffic": _pmc(name), "algorithmic_bytes_per_launch": nbytes,
+           "frac": round(ach / HBM_PEAK, 4), "traffic": _pmc(name, "kernels" if mode == "greedy" else "kernels_beam"),
+           "algorithmic_bytes_per_launch": nbytes,
            "avg_launch_ms": round(ms, 5), "timed_launches": n,
            "timing": "in-kernel wall-clock stamps, launches of the last timed call"}
     out.update(extra)
@@ -350,9 +364,9 @@ def mfma_view(args, eng, sig, lens, ms_per_step):
                             "frac_split_peak": round(enc_tf / SPLIT_PEAK, 4),
                             "note": "nd_encode incl. its memory-bank LayerNorm copy"},
            "peaks": {"fp32": FP32_PEAK, "split_fp16_fp32_equiv": round(SPLIT_PEAK, 1), "unit": "TFLOP/s"}}
-    cnt = _mfma_counters()
+    cnt = _mfma_counters("nano" if args.encoder == "nano" else "greedy")
     if cnt is not None:
-        out["rocprof_counters"] = cnt.get("bench", cnt)
+        out["rocprof_counters"] = cnt
     return out
 
 
@@ -415,12 +429,39 @@ def run_batch(args, world, rank, dev, cfg, W):
         "timed_seconds": round(dt, 3),
         "min_length": args.min_length,
     }
+    alive = None
     if args.mode == "beam":
         res["decoder_steps_executed"] = int(out["steps"].cpu().item())
+        # the steps each chunk ran (the reference drops a finished chunk's batch
+        # at that step, translate/translator.py:793-823); same inputs, same search
+        rr = eng.translate_beam(sig, lens, lens, beam=args.beam, max_len=args.max_length, min_len=args.min_length,
+                                return_attn=True)
+        done = rr["done_step"].cpu().numpy()
+        alive = [int((done > s_).sum()) for s_ in range(res["decoder_steps_executed"])]
+        res["chunk_steps"] = {"executed_share": round(sum(alive) / (args.batch * len(alive)), 4),
+                              "done_step_percentiles_0_50_99_100": np.percentile(done, [0, 50, 99, 100]).tolist(),
+                              "note": "finished chunks' attention workgroups and GEMM row tiles exit at once"}
+        del rr
+        # the forced-100-step worst case: EOS masked at every step (-min_length = max_length)
+        n_wc = max(2, min(10, args.steps // 10))
+        for _ in range(2):
+            eng.translate_beam(sig, lens, lens, beam=args.beam, max_len=args.max_length, min_len=args.max_length)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n_wc):
+            eng.translate_beam(sig, lens, lens, beam=args.beam, max_len=args.max_length, min_len=args.max_length)
+        torch.cuda.synchronize()
+        wc = (time.perf_counter() - t0) / n_wc
+        res["worst_case_all_steps"] = {"ms_per_step": round(wc * 1e3, 3),
+                                       "samples_per_sec_per_gpu": round(float(lens_np.sum()) / wc, 1),
+                                       "note": f"min_length {args.max_length}: no chunk finishes before step "
+                                               f"{args.max_length}, {n_wc} calls"}
+        step()  # the timed workload's graphs again (kernel stamps below come from this call)
+        torch.cuda.synchronize()
     extras = {}
     if rank == 0:
         if not args.no_roofline:
-            extras["roofline"] = kernel_roofline(eng, args.batch, args.mode, beam, args.encoder)
+            extras["roofline"] = kernel_roofline(eng, args.batch, args.mode, beam, args.encoder, alive)
         eng.set_kernel_stamps(False)
         mv = None if args.no_roofline else mfma_view(args, eng, sig, lens, dt / args.steps * 1e3)
         if mv is not None:

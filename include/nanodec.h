@@ -221,9 +221,22 @@ int nd_set_ctx_path(nd_ctx* ctx, int path);
  * an fp16 hi/lo pair, 22 significant bits, three fp16 MFMA products summed in
  * fp32 accumulators); 1 = exact fp32 (fp32-MFMA kernels for every GEMM, the
  * encoder attention and the BiLSTM recurrence), the reference's own fp32
- * arithmetic (nn.Linear / bmm in fp32).  Default from ND_GEMM_F32.  Clears
- * the context's captured graphs when it changes. */
+ * arithmetic (nn.Linear / bmm in fp32).  Default from ND_GEMM_F32.  The
+ * captured graphs of both forms are kept (keyed by it). */
 int nd_set_exact_fp32(nd_ctx* ctx, int enable);
+
+/* Split-fp16 range guard.  An activation operand the split form carries as
+ * fp16 hi/lo leaves the fp16 range from |x| = 65504 on, where the
+ * reference's fp32 arithmetic is still finite.  Every kernel that splits an
+ * activation it does not normalise itself (GEMMs without a LayerNorm
+ * prologue, the encoder attention's Q/K/V) raises the context's overflow
+ * word when it sees one.  nd_take_overflow enqueues, on `stream`, a copy of
+ * that word to d_out (one int32: nonzero = some product of the calls
+ * enqueued since the last take saw an out-of-range operand) and clears it.
+ * Call it right after each translate call, as the Python Translator does,
+ * and rerun a flagged call after nd_set_exact_fp32(ctx, 1).  No reference
+ * counterpart: the reference computes in fp32 (nn.Linear / bmm). */
+int nd_take_overflow(nd_ctx* ctx, int32_t* d_out, void* stream);
 
 /* Launch-duration stamps of the decoder's context attention (the bench's
  * roofline kernel: dec_mem_attention_kernel for greedy, dec_ctx_attention_kernel

@@ -210,7 +210,7 @@ __device__ __forceinline__ void esplit8(const float (&x)[8], eh8& hi, eh8& lo) {
 
 __global__ void __launch_bounds__(1024)
 enc_attention_h3_kernel(const float* __restrict__ qkv, const float* __restrict__ signal, const int* __restrict__ span,
-                        float* __restrict__ out, int T) {
+                        float* __restrict__ out, int T, int* ovf) {
   __shared__ __attribute__((aligned(16))) unsigned Kp[2][ENC_MAXT * ENC_KH];  // [hi|lo][key][32 halves + pad]
   __shared__ __attribute__((aligned(16))) unsigned Vp[2][ND_DH * ENC_VH];     // [hi|lo][dim][512 halves + pad]
   __shared__ int kflag[ENC_MAXT];  // 0 = key, 1 = masked (signal == 0), 2 = absent (t >= span)
@@ -228,6 +228,7 @@ enc_attention_h3_kernel(const float* __restrict__ qkv, const float* __restrict__
       const float* row = qkv + (base + t) * (3 * ND_D) + h * ND_DH + c;
       k = ld4(row + ND_D);
       v = ld4(row + 2 * ND_D);
+      flag_overflow(ovf, fmaxf(absmax4(k), absmax4(v)));
     }
     _Float16* kh = reinterpret_cast<_Float16*>(&Kp[0][t * ENC_KH]) + c;
     _Float16* kl = reinterpret_cast<_Float16*>(&Kp[1][t * ENC_KH]) + c;
@@ -258,6 +259,7 @@ enc_attention_h3_kernel(const float* __restrict__ qkv, const float* __restrict__
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       const f32x4 x0 = ld4(qrow + 16 * s2) / ND_SQRT_DH, x1 = ld4(qrow + 16 * s2 + 4) / ND_SQRT_DH;
+      flag_overflow(ovf, fmaxf(absmax4(x0), absmax4(x1)));
       const float x[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
       esplit8(x, qh[s2], ql[s2]);
     }
@@ -333,7 +335,7 @@ enc_attention_h3_kernel(const float* __restrict__ qkv, const float* __restrict__
 }
 
 hipError_t launch_enc_attention(const float* qkv, const float* signal, const int* span, float* out, int B, int T,
-                                hipStream_t s, bool exact) {
+                                hipStream_t s, bool exact, int* ovf) {
   if (T > ENC_MAXT || T <= 0) return hipErrorInvalidValue;
   static const bool f32 = [] {
     const char* e = getenv("ND_ENC_ATTN_F32");  // 1: the fp32-MFMA kernel
@@ -342,7 +344,7 @@ hipError_t launch_enc_attention(const float* qkv, const float* signal, const int
   if (f32 || exact)
     hipLaunchKernelGGL(enc_attention_kernel, dim3(ND_H, B), dim3(1024), 0, s, qkv, signal, span, out, T);
   else
-    hipLaunchKernelGGL(enc_attention_h3_kernel, dim3(ND_H, B), dim3(1024), 0, s, qkv, signal, span, out, T);
+    hipLaunchKernelGGL(enc_attention_h3_kernel, dim3(ND_H, B), dim3(1024), 0, s, qkv, signal, span, out, T, ovf);
   return hipGetLastError();
 }
 
@@ -439,7 +441,8 @@ __device__ __forceinline__ void merge_waves(float* accs, float* ms, float* ls, c
 template <int NW, int KW>
 __global__ void __launch_bounds__(NW * 64)
 dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cache, const int* __restrict__ anc,
-                          int anc_ld, int step, int S, float* __restrict__ out, int rpc) {
+                          int anc_ld, int step, int S, float* __restrict__ out, int rpc, const int* __restrict__ skip,
+                          int skip_rpc) {
   __shared__ float accs[NW * ND_D];
   __shared__ float ms[NW * ND_H], ls[NW * ND_H];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -452,6 +455,9 @@ dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cac
     const int j = r >> 3;
     r = ((j / rpc) * 8 + (r & 7)) * rpc + j % rpc;
   }
+  // --fast beam: rows of finished chunks are out of the decode loop
+  // (translate/translator.py:793-823 drops their batches)
+  if (skip && skip[r / skip_rpc]) return;
   const int n = step + 1;
   // qkv is P16-packed [R, 768]
   const f32x4 qv = ld4(qkv + pk(r, lane * 4, 3 * ND_D)) / ND_SQRT_DH;
@@ -496,7 +502,8 @@ dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cac
 }
 
 hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* anc, int anc_ld, int step,
-                                     int max_steps, float* out, int R, hipStream_t s, int rpc) {
+                                     int max_steps, float* out, int R, hipStream_t s, int rpc, const int* skip) {
+  const int skip_rpc = rpc;
   static const int xcd = [] {
     const char* e = getenv("ND_SELF_XCD");  // 0: row order (A/B timing)
     return e ? atoi(e) : 1;
@@ -506,7 +513,7 @@ hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* 
   const int n = step + 1;
 #define ND_SELF(NW, KW)                                                                                             \
   hipLaunchKernelGGL((dec_self_attention_kernel<NW, KW>), dim3(R), dim3(NW * 64), 0, s, qkv, cache, anc, anc_ld, step, \
-                     max_steps, out, rpc)
+                     max_steps, out, rpc, skip, skip_rpc)
   if (n <= 32) ND_SELF(8, 4);
   else if (n <= 64) ND_SELF(16, 4);
   else ND_SELF(16, 8);  // two passes beyond 128 keys
@@ -536,7 +543,8 @@ __global__ void __launch_bounds__(CTX_NW * 64)
 dec_ctx_attention_kernel(const float* __restrict__ q, const float* __restrict__ kv, int ld, int koff,
                          const float* __restrict__ signal, const int* __restrict__ span, float pad_val,
                          float* __restrict__ out, int T, unsigned long long* stamp, float* __restrict__ dbg,
-                         size_t dbg_stride) {
+                         size_t dbg_stride, const int* __restrict__ skip) {
+  if (skip && skip[blockIdx.x]) return;  // finished chunk (--fast beam, translator.py:793-823)
   stamp_begin(stamp);
   constexpr int U = CtxTile<RPC>::U;
   extern __shared__ float sm[];
@@ -609,14 +617,15 @@ static size_t ctx_lds_bytes(int rpc) { return (size_t)CTX_NW * rpc * (ND_D + 2 *
 
 hipError_t launch_dec_ctx_attention(const float* q, const float* kv, int ld, int koff, const float* signal,
                                     const int* span, float pad_val, float* out, int C, int rpc, int T,
-                                    hipStream_t s, unsigned long long* stamp, float* attn_dbg, size_t dbg_stride) {
+                                    hipStream_t s, unsigned long long* stamp, float* attn_dbg, size_t dbg_stride,
+                                    const int* skip) {
   if (rpc < 1 || rpc > CTX_MAXR || T > 512) return hipErrorInvalidValue;
   const size_t lds = ctx_lds_bytes(rpc);
   switch (rpc) {
 #define ND_CTX_CASE(R)                                                                                            \
   case R:                                                                                                         \
     hipLaunchKernelGGL(dec_ctx_attention_kernel<R>, dim3(C), dim3(CTX_NW * 64), lds, s, q, kv, ld, koff, signal,  \
-                       span, pad_val, out, T, stamp, attn_dbg, dbg_stride);                                       \
+                       span, pad_val, out, T, stamp, attn_dbg, dbg_stride, skip);                                 \
     break;
     ND_CTX_CASE(1)
     ND_CTX_CASE(2)

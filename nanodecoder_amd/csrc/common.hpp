@@ -109,6 +109,21 @@ __device__ __forceinline__ size_t pk(int m, int n, int N) {
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
 
+// Split-fp16 range guard.  An activation split as hi = fp16(x), lo =
+// fp16(x - hi) leaves the fp16 range from |x| = 65504 on (hi becomes inf
+// where the fp32 reference is finite).  Every kernel that splits an
+// activation it did not normalise itself records the largest |x| it split
+// and raises the ctx's overflow word (plain vector store of 1 from the lanes
+// that saw one; all writers store the same value); the host reads the word
+// per call (nd_take_overflow) and reruns that call on the exact fp32 path.
+#define ND_F16_LIMIT 65504.0f
+__device__ __forceinline__ float absmax4(f32x4 v) {
+  return fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+}
+__device__ __forceinline__ void flag_overflow(int* ovf, float amax) {
+  if (amax >= ND_F16_LIMIT && ovf != nullptr) ovf[0] = 1;
+}
+
 // Launch-duration stamps (bench roofline, measured inside the timed graph):
 // stamp[0] = earliest workgroup start, stamp[1] = latest workgroup end, in
 // wall_clock64() ticks (s_memrealtime, constant rate).  stamp == nullptr: off.

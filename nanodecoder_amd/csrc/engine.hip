@@ -90,11 +90,14 @@ struct GraphKey {
   // random sampling (greedy path): top-k (1 = argmax) and temperature
   int topk = 1;
   float temp = 0.f;
+  int exact = 0;  // exact fp32 products (set by run_graph from the ctx)
+  int tail = 0;   // --fast beam tail segments (nd_ctx.beam_tail)
   bool operator<(const GraphKey& o) const {
     return std::tie(mode, B, T, S, min_len, beam, n_best, seg, logp, alpha, stamp, attn, cov, stepwise, ngram, excl,
-                    beta, topk, temp) < std::tie(o.mode, o.B, o.T, o.S, o.min_len, o.beam, o.n_best, o.seg, o.logp,
-                                                 o.alpha, o.stamp, o.attn, o.cov, o.stepwise, o.ngram, o.excl, o.beta,
-                                                 o.topk, o.temp);
+                    beta, topk, temp, exact, tail) < std::tie(o.mode, o.B, o.T, o.S, o.min_len, o.beam, o.n_best,
+                                                              o.seg, o.logp, o.alpha, o.stamp, o.attn, o.cov,
+                                                              o.stepwise, o.ngram, o.excl, o.beta, o.topk, o.temp,
+                                                              o.exact, o.tail);
   }
 };
 
@@ -113,6 +116,12 @@ struct nd_ctx {
   // exact fp32: plain fp32-MFMA kernels everywhere (no split-fp16 products);
   // nd_set_exact_fp32, default from ND_GEMM_F32
   bool exact = false;
+  // split-fp16 range guard word (common.hpp flag_overflow), read and cleared
+  // per call by nd_take_overflow
+  int* ovf = nullptr;
+  // --fast beam: few chunks alive (seen at a segment poll): the decoder GEMMs
+  // stay on the small-M P16 kernels (GraphKey.tail)
+  bool beam_tail = false;
 
   // weights
   float *enc_lin_w = nullptr, *enc_lin_b = nullptr, *enc_ln_g = nullptr, *enc_ln_b = nullptr;
@@ -409,6 +418,7 @@ static int alloc_workspaces(nd_ctx* c) {
   WS(c->cut_in, B);
   WS(c->seed_dev, 2);
   WS(c->kstamp, Ld * S * 2);
+  WS(c->ovf, 4);
 #undef WS
   if ((e = hipHostMalloc((void**)&c->h_alive, 16, hipHostMallocDefault)) != hipSuccess)
     return fail(ND_ERR_HIP, std::string("hipHostMalloc: ") + hipGetErrorString(e));
@@ -453,6 +463,7 @@ struct G {
     if (it != c->split.end()) {
       a.Wh = it->second.first;
       a.wscale = it->second.second;
+      a.ovf = c->ovf;
     }
     auto jt = c->split_rm.find(a.W);
     if (jt != c->split_rm.end()) {
@@ -463,6 +474,8 @@ struct G {
   }
   G& res(const float* R, int ldr) { a.R = R; a.ldr = ldr; return *this; }
   G& stats(float* part) { a.part_out = part; return *this; }
+  G& skip(const int* done, int rpc) { a.skip = done; a.skip_rpc = rpc; return *this; }
+  G& small_m(bool on) { a.prefer_p16 = on ? 1 : 0; return *this; }
   bool packed = false;
   G& p16() { packed = true; return *this; }  // decoder-step operands in the P16 layout
   hipError_t run(hipStream_t s, int* pn_out = nullptr) {
@@ -481,7 +494,7 @@ static hipError_t enqueue_encode_transformer(nd_ctx* c, int B, int T, hipStream_
   for (auto& L : c->enc) {
     // encoder/transformer.py:36-54
     LCHK(G(c->x, D, L.nwqkv, 3 * D, D, L.nbqkv, c->big, 3 * D, M).h3(c).ln(c->x_part, pnx).run(s));
-    LCHK(nd::launch_enc_attention(c->big, c->sig, c->span, c->att, B, T, s, c->exact));
+    LCHK(nd::launch_enc_attention(c->big, c->sig, c->span, c->att, B, T, s, c->exact, c->ovf));
     LCHK(G(c->att, D, L.wo, D, D, L.bo, c->y, D, M).h3(c).res(c->x, D).stats(c->y_part).run(s, &pny));
     LCHK(G(c->y, D, L.nw1, F, D, L.nb1, c->big, F, M).h3(c).ln(c->y_part, pny).relu().run(s));
     LCHK(G(c->big, F, L.w2, D, F, L.b2, c->x, D, M).h3(c).res(c->y, D).stats(c->x_part).run(s, &pnx));
@@ -518,12 +531,18 @@ static hipError_t enqueue_first_embed(nd_ctx* c, int R, hipStream_t s) {
 // dx_part) -> dx (pre final LN).
 static bool use_memory_bank(nd_ctx* c, int rpc) { return c->ctx_path == 0 && rpc * ND_H <= 16 && rpc == 1; }
 
+// done: per chunk, nonzero = finished (--fast beam; null otherwise): its rows'
+// tiles and attention workgroups exit without work
 static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, const int* anc, int anc_ld,
-                                   hipStream_t s) {
+                                   hipStream_t s, const int* done = nullptr) {
   const int R = C * rpc, D = c->D, F = c->F, S = c->cfg.max_steps;
   const int Ld = (int)c->dec.size();
   const bool mb = use_memory_bank(c, rpc);
   int pnx = 1, pnq = 0, pnm = 0;
+  // a decoder-step GEMM over the R rows: P16 operands, split-fp16 weights, dead chunks skipped
+  auto dg = [&](const float* A, int lda, const float* W, int N, int K, const float* bias, float* out, int ldc) {
+    return G(A, lda, W, N, K, bias, out, ldc, R).p16().h3(c).skip(done, rpc).small_m(c->beam_tail);
+  };
   for (int i = 0; i < Ld; ++i) {
     DecLayer& L = c->dec[i];
     float* cache = c->cache + (size_t)i * R * S * 2 * D;
@@ -537,31 +556,31 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
       // average_attn.py:55-106 + the layer residual (decoder/transformer.py:82-86)
       LCHK(nd::launch_aan_prep(c->dx, L.ln1_g, L.ln1_b, cache, anc, anc_ld, step, S, c->axn, c->aavg, c->aavg_part,
                                R, s));
-      LCHK(G(c->aavg, D, L.paw1, D, D, L.nab1, c->ah, D, R).p16().h3(c).ln(c->aavg_part, 1).relu().run(s));
-      LCHK(G(c->ah, D, L.paw2, D, D, L.ab2, c->aa, D, R).p16().h3(c).res(c->aavg, D).run(s));
-      LCHK(G(c->axn, D, L.pgwx, 2 * D, D, L.gb, c->ag, 2 * D, R).p16().h3(c).run(s));
-      LCHK(G(c->aa, D, L.pgwa, 2 * D, D, nullptr, c->ag, 2 * D, R).p16().h3(c).res(c->ag, 2 * D).run(s));
+      LCHK(dg(c->aavg, D, L.paw1, D, D, L.nab1, c->ah, D).ln(c->aavg_part, 1).relu().run(s));
+      LCHK(dg(c->ah, D, L.paw2, D, D, L.ab2, c->aa, D).res(c->aavg, D).run(s));
+      LCHK(dg(c->axn, D, L.pgwx, 2 * D, D, L.gb, c->ag, 2 * D).run(s));
+      LCHK(dg(c->aa, D, L.pgwa, 2 * D, D, nullptr, c->ag, 2 * D).res(c->ag, 2 * D).run(s));
       LCHK(nd::launch_aan_gate(c->ag, c->axn, c->aa, c->dx, c->dq1, c->dq1_part, R, s));
       pnq = 1;
     } else {
-      LCHK(G(c->dx, D, L.pwqkv, 3 * D, D, L.nbqkv, c->dqkv, 3 * D, R).p16().h3(c).ln(c->dx_part, pnx).run(s));
-      LCHK(nd::launch_dec_self_attention(c->dqkv, cache, anc, anc_ld, step, S, c->datt, R, s, rpc));
-      LCHK(G(c->datt, D, L.pwo, D, D, L.bo, c->dq1, D, R).p16().h3(c).res(c->dx, D).stats(c->dq1_part).run(s, &pnq));
+      LCHK(dg(c->dx, D, L.pwqkv, 3 * D, D, L.nbqkv, c->dqkv, 3 * D).ln(c->dx_part, pnx).run(s));
+      LCHK(nd::launch_dec_self_attention(c->dqkv, cache, anc, anc_ld, step, S, c->datt, R, s, rpc, done));
+      LCHK(dg(c->datt, D, L.pwo, D, D, L.bo, c->dq1, D).res(c->dx, D).stats(c->dq1_part).run(s, &pnq));
     }
     if (mb) {  // memory-bank form (attention.hip)
       const int HD = ND_H * D;
-      LCHK(G(c->dq1, D, L.pwqk, HD, D, L.bqk, c->dqk, HD, R).p16().h3(c).ln(c->dq1_part, pnq).run(s));
+      LCHK(dg(c->dq1, D, L.pwqk, HD, D, L.bqk, c->dqk, HD).ln(c->dq1_part, pnq).run(s));
       LCHK(nd::launch_dec_mem_attention(c->dqk, c->mem, c->sig, c->span, (float)c->cfg.pad_idx, c->dU, C, rpc, T, T,
                                         s, stamp, dbg, dbg_stride));
-      LCHK(G(c->dU, HD, L.pwvo, D, HD, L.bvo, c->dmid, D, R).p16().h3(c).res(c->dq1, D).stats(c->dmid_part).run(s, &pnm));
+      LCHK(dg(c->dU, HD, L.pwvo, D, HD, L.bvo, c->dmid, D).res(c->dq1, D).stats(c->dmid_part).run(s, &pnm));
     } else {
-      LCHK(G(c->dq1, D, L.pcwq, D, D, L.ncbq, c->dcq, D, R).p16().h3(c).ln(c->dq1_part, pnq).run(s));
+      LCHK(dg(c->dq1, D, L.pcwq, D, D, L.ncbq, c->dcq, D).ln(c->dq1_part, pnq).run(s));
       LCHK(nd::launch_dec_ctx_attention(c->dcq, c->ctxkv, Ld * 2 * D, i * 2 * D, c->sig, c->span,
-                                        (float)c->cfg.pad_idx, c->datt, C, rpc, T, s, stamp, dbg, dbg_stride));
-      LCHK(G(c->datt, D, L.pcwo, D, D, L.cbo, c->dmid, D, R).p16().h3(c).res(c->dq1, D).stats(c->dmid_part).run(s, &pnm));
+                                        (float)c->cfg.pad_idx, c->datt, C, rpc, T, s, stamp, dbg, dbg_stride, done));
+      LCHK(dg(c->datt, D, L.pcwo, D, D, L.cbo, c->dmid, D).res(c->dq1, D).stats(c->dmid_part).run(s, &pnm));
     }
-    LCHK(G(c->dmid, D, L.pw1, F, D, L.nb1, c->dhid, F, R).p16().h3(c).ln(c->dmid_part, pnm).relu().run(s));
-    LCHK(G(c->dhid, F, L.pw2, D, F, L.b2, c->dx, D, R).p16().h3(c).res(c->dmid, D).stats(c->dx_part).run(s, &pnx));
+    LCHK(dg(c->dmid, D, L.pw1, F, D, L.nb1, c->dhid, F).ln(c->dmid_part, pnm).relu().run(s));
+    LCHK(dg(c->dhid, F, L.pw2, D, F, L.b2, c->dx, D).res(c->dmid, D).stats(c->dx_part).run(s, &pnx));
   }
   return hipSuccess;
 }
@@ -617,7 +636,7 @@ static hipError_t enqueue_beam_steps(nd_ctx* c, int B, int T, int beam, int n_be
   const nd::BeamState st = beam_state(c);
   for (int step = s0; step < s1; ++step) {
     const int cur = step & 1;
-    LCHK(enqueue_dec_step(c, B, beam, T, step, c->bs.anc[cur], S, s));
+    LCHK(enqueue_dec_step(c, B, beam, T, step, c->bs.anc[cur], S, s, c->bs.done));
     LCHK(enqueue_attn_step(c, B, beam, T, step, s));
     const float lenpen = (float)std::pow((5.0 + (step + 1)) / 6.0, (double)alpha);
     LCHK(nd::launch_beam_step(next_embed(c), c->dx, c->dec_ln_g, c->dec_ln_b, c->gen_w, c->gen_b, c->V, st, B, beam,
@@ -646,7 +665,10 @@ static int run_graph(nd_ctx* c, const GraphKey& key, F&& enqueue) {
     if (e != hipSuccess) return fail(ND_ERR_HIP, g_err.empty() ? hipGetErrorString(e) : g_err);
     return ND_OK;
   }
-  auto it = c->graphs.find(key);
+  GraphKey k = key;
+  k.exact = c->exact ? 1 : 0;  // both product forms keep their graphs (the overflow rerun switches)
+  k.tail = c->beam_tail ? 1 : 0;
+  auto it = c->graphs.find(k);
   if (it == c->graphs.end()) {
     hipGraph_t g = nullptr;
     HIPCHK(hipStreamBeginCapture(c->es, hipStreamCaptureModeRelaxed));
@@ -661,7 +683,7 @@ static int run_graph(nd_ctx* c, const GraphKey& key, F&& enqueue) {
     e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
     (void)hipGraphDestroy(g);
     if (e != hipSuccess) return fail(ND_ERR_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
-    it = c->graphs.emplace(key, ex).first;
+    it = c->graphs.emplace(k, ex).first;
   }
   HIPCHK(hipGraphLaunch(it->second, c->es));
   return ND_OK;
@@ -1085,6 +1107,7 @@ static int translate_beam(nd_ctx* c, const float* d_signal, const int32_t* d_len
     return rc;
   }
   if (c->timing) HIPCHK(hipEventRecord(c->ev_b, c->es));
+  c->beam_tail = false;
   for (int s0 = 0; s0 < max_len; s0 += SEG) {
     const int s1 = std::min(max_len, s0 + SEG);
     GraphKey k{1, B, T, max_len, min_len, beam, n_best, s0, 0, alpha, st};
@@ -1097,8 +1120,12 @@ static int translate_beam(nd_ctx* c, const float* d_signal, const int32_t* d_len
       HIPCHK(hipMemcpyAsync(c->h_alive, c->bs.n_alive, 4, hipMemcpyDeviceToHost, c->es));
       HIPCHK(hipStreamSynchronize(c->es));
       if (*c->h_alive == 0) break;
+      // a sixteenth of the chunks or fewer left (a trained model's stragglers):
+      // the remaining segments' GEMMs run on the latency-bound small-M kernels
+      c->beam_tail = (long)*c->h_alive * 16 <= (long)B;
     }
   }
+  c->beam_tail = false;
   c->attn_on = false;
   if (rc) return rc;
   if (c->timing) HIPCHK(hipEventRecord(c->ev_c, c->es));
@@ -1276,11 +1303,16 @@ int nd_set_ctx_path(nd_ctx* c, int path) {
 
 int nd_set_exact_fp32(nd_ctx* c, int enable) {
   if (!c) return fail(ND_ERR_ARG, "null ctx");
-  if (c->exact != (enable != 0)) {
-    for (auto& kv : c->graphs) (void)hipGraphExecDestroy(kv.second);
-    c->graphs.clear();
-  }
-  c->exact = enable != 0;
+  c->exact = enable != 0;  // graphs are keyed by it
+  return ND_OK;
+}
+
+int nd_take_overflow(nd_ctx* c, int32_t* d_out, void* stream) {
+  if (!c || !d_out) return fail(ND_ERR_ARG, "null argument");
+  HIPCHK(hipSetDevice(c->cfg.device));
+  const hipStream_t s = (hipStream_t)stream;
+  HIPCHK(hipMemcpyAsync(d_out, c->ovf, sizeof(int), hipMemcpyDeviceToDevice, s));
+  HIPCHK(hipMemsetAsync(c->ovf, 0, sizeof(int), s));
   return ND_OK;
 }
 

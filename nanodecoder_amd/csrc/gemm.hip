@@ -55,6 +55,17 @@ __device__ __forceinline__ void merge_stats(const float* __restrict__ p, int P, 
   rs = 1.0f / sqrtf(m2 * (1.0f / 256.0f) + ND_LN_EPS);
 }
 
+// --fast beam: every row of [r0, r0 + n) (rows < M) belongs to a finished
+// chunk (skip[row / rpc] != 0).  Wave-uniform; each wave of a workgroup
+// computes the same answer, so a dead tile returns before any barrier.
+__device__ __forceinline__ bool rows_dead(const int* __restrict__ skip, int rpc, int r0, int n, int M) {
+  if (skip == nullptr) return false;
+  const int c0 = r0 / rpc, c1 = (min(r0 + n, M) - 1) / rpc;
+  bool alive = false;
+  for (int c = c0 + (int)(threadIdx.x & 63); c <= c1; c += 64) alive |= skip[c] == 0;
+  return __ballot(alive) == 0;
+}
+
 // Sum over aligned groups of TPR lanes (16, 32 or the whole wave).
 template <int TPR>
 __device__ __forceinline__ float group_sum(float v) {
@@ -175,6 +186,7 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
         rw[i] = ld4(g.W + (size_t)(n0 + row) * g.ldw + k0 + c);
     }
   };
+  float amax = 0.f;  // split-fp16 range guard (H3, no LN prologue)
   auto store_tile = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < A4; ++i) {
@@ -182,6 +194,7 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
       amap(i, row, c);
       if constexpr (LN) ra[i] = (ra[i] - s_mu[row]) * s_rs[row];
       if constexpr (H3) {
+        if constexpr (!LN) amax = fmaxf(amax, absmax4(ra[i]));
         h4 hi, lo;
         split4(ra[i], hi, lo);
         float* p = &As[buf * BM * LDK + row * LDK + (c >> 3) * 8 + ((c >> 2) & 1) * 2];
@@ -213,6 +226,7 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
   // the first step's operands are in flight while the row statistics load
   // (QKV at M = 131072: 271.6 -> 266 us)
   load_tile(0);
+  if (rows_dead(g.skip, g.skip_rpc, m0, BM, M)) return;
   if constexpr (LN) {
     if (g.part_in) {
       for (int r = tid; r < BM; r += NT) {
@@ -295,6 +309,7 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
     if (kt + 1 < KT) store_tile(buf ^ 1);
     __syncthreads();
   }
+  if constexpr (H3 && !LN) flag_overflow(g.ovf, amax);
 
   constexpr int TPR = BN / 4, RPP = NT / TPR;
   const int c4 = (tid % TPR) * 4;
@@ -389,6 +404,7 @@ __global__ void __launch_bounds__(NT* KS * 64) gemm_p16_kernel(const GemmArgs g)
   const int wt = wave % NT, ws = wave / NT;
   const int nb = blockIdx.x * NT + wt, mb = blockIdx.y;
   const int KB = g.K >> 4, NB = g.N >> 4;
+  if (rows_dead(g.skip, g.skip_rpc, mb * 16, 16, g.M)) return;
   const f32x4* __restrict__ ap = reinterpret_cast<const f32x4*>(g.A) + ((size_t)mb * KB + ws * NF) * 64 + lane;
   // fp32 P16 blocks, or (H3) the P16H image: per 32-k pair a hi and a lo 1 KB plane
   const f32x4* __restrict__ wp = H3 ? reinterpret_cast<const f32x4*>(g.Wh) + ((size_t)nb * KB + ws * NF) * 64 + lane
@@ -410,6 +426,12 @@ __global__ void __launch_bounds__(NT* KS * 64) gemm_p16_kernel(const GemmArgs g)
   if constexpr (LN) {
 #pragma unroll
     for (int f = 0; f < NF; ++f) a[f] = (a[f] - mu) * rs;
+  }
+  if constexpr (H3 && !LN) {
+    float amax = 0.f;
+#pragma unroll
+    for (int f = 0; f < NF; ++f) amax = fmaxf(amax, absmax4(a[f]));
+    flag_overflow(g.ovf, amax);
   }
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
   if constexpr (H3) {
@@ -473,6 +495,7 @@ __global__ void __launch_bounds__(BMB* BNB * 64) gemm_p16s_kernel(const GemmArgs
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nb0 = blockIdx.x * BNB, mb0 = blockIdx.y * BMB, NB = g.N >> 4;
   const int MB = (g.M + 15) >> 4;  // row blocks that exist (buffers are padded to 16 rows, not 16*BMB)
+  if (rows_dead(g.skip, g.skip_rpc, mb0 * 16, BMB * 16, g.M)) return;
   const f32x4* __restrict__ A4 = reinterpret_cast<const f32x4*>(g.A);
   const f32x4* __restrict__ W4 = reinterpret_cast<const f32x4*>(H3 ? (const void*)g.Wh : (const void*)g.W);
   // stage: block j of A = (row block mb0 + j / KB, k block j % KB), likewise W.
@@ -513,6 +536,12 @@ __global__ void __launch_bounds__(BMB* BNB * 64) gemm_p16s_kernel(const GemmArgs
   if constexpr (H3) {
     // normalise and split while staging: every A element converted once per workgroup
     if constexpr (LN) __syncthreads();
+    if constexpr (!LN) {
+      float amax = 0.f;
+#pragma unroll
+      for (int i = 0; i < AJ; ++i) amax = fmaxf(amax, absmax4(av[i]));
+      flag_overflow(g.ovf, amax);
+    }
 #pragma unroll
     for (int i = 0; i < AJ; i += 2) {
       const int j = aj(i);
@@ -884,7 +913,8 @@ hipError_t launch_gemm_p16(GemmArgs& g, hipStream_t s) {
     const char* e = getenv("ND_P16_BIG_MIN");  // rows from which the LDS-tiled kernel takes P16 GEMMs
     return e ? atoi(e) : 2048;
   }();
-  if (g.M >= big_min && g.Wh_rm && !gemm_f32_only() && g.N % 64 == 0 && (g.N >= 512 || g.K >= 1024)) {
+  if (g.M >= big_min && !g.prefer_p16 && g.Wh_rm && !gemm_f32_only() && g.N % 64 == 0 &&
+      (g.N >= 512 || g.K >= 1024)) {
     // many rows (beam search over large batches): the encoder's LDS-tiled
     // split-fp16 kernel on P16 activations, with the row-major weight image
     // (measured at M = 5120: QKV 25 -> 18 us, FFN1 59 -> 50, FFN2 71 -> 50;

@@ -44,6 +44,16 @@ struct GemmArgs {
   float wscale_rm = 1.0f;
   int p16io = 0;
   int xcd_map = 0;     // row-major kernel: XCD-aware tile order (set by launch_gemm)
+  // split-fp16 range guard (common.hpp flag_overflow): set to 1 when a split
+  // activation operand (no LN prologue) reaches |x| >= 65504; nullable
+  int* ovf = nullptr;
+  // --fast beam: row r belongs to chunk r / skip_rpc; a tile whose rows all
+  // belong to finished chunks (skip[chunk] != 0) exits without work; nullable
+  const int* skip = nullptr;
+  int skip_rpc = 1;
+  // P16 GEMMs: stay on the small-M kernels at any M (the beam loop's tail,
+  // when few chunks are alive: a 16-row block's latency, not a 64-row tile's)
+  int prefer_p16 = 0;
 };
 #define ND_PART_LD 16  // partial-stat slots per row (max column tiles of a 256-wide row)
 // row-major operands (encoder, large M): LDS-tiled MFMA kernel
@@ -74,9 +84,10 @@ hipError_t launch_fold_layernorm(const float* W, const float* bias, const float*
 hipError_t launch_enc_embed(const float* signal, const float* w_in, const float* b_in, float* x, float* part, int B,
                             int T, hipStream_t s);
 // flash attention over qkv [B*T, 768]; mask signal==0; keys >= span excluded
-// exact: the fp32-MFMA kernel instead of split-fp16 (also forced by ND_ENC_ATTN_F32=1)
+// exact: the fp32-MFMA kernel instead of split-fp16 (also forced by ND_ENC_ATTN_F32=1);
+// ovf: split-fp16 range guard word (nullable)
 hipError_t launch_enc_attention(const float* qkv, const float* signal, const int* span, float* out, int B, int T,
-                                hipStream_t s, bool exact = false);
+                                hipStream_t s, bool exact = false, int* ovf = nullptr);
 // NanoEncoder BiLSTM layer (both directions): xp [B*T, 1024] projections
 // (or, layer0, computed from signal with wih0/bsum [2][512]); whh [2][512][128];
 // out [B*T, 256] (h, or BatchNorm(h) when bn_scale != nullptr).
@@ -92,14 +103,16 @@ hipError_t launch_dec_embed(const int* tok, const float* emb, const float* pe, i
                             int R, hipStream_t s);
 // self attention: writes k,v of this step into cache[slot=r][step], attends
 // over the row's history cache[anc[r][t]][t] (anc == nullptr: identity).
+// skip (nullable): per chunk (row / rpc), nonzero = finished, its rows do nothing
 hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* anc, int anc_ld, int step,
-                                     int max_steps, float* out, int R, hipStream_t s, int rpc = 1);
+                                     int max_steps, float* out, int R, hipStream_t s, int rpc = 1,
+                                     const int* skip = nullptr);
 // context attention: rows r = c*rpc + j attend over ctxkv rows of chunk c
 // (K at kv[(c*T+t)*ld + koff], V at +256), mask signal == pad_val, keys < span.
 hipError_t launch_dec_ctx_attention(const float* q, const float* kv, int ld, int koff, const float* signal,
                                     const int* span, float pad_val, float* out, int C, int rpc, int T,
                                     hipStream_t s, unsigned long long* stamp = nullptr, float* attn_dbg = nullptr,
-                                    size_t dbg_stride = 0);
+                                    size_t dbg_stride = 0, const int* skip = nullptr);
 // Next step's decoder input, written by the search kernel that picks the
 // token (the embedding of step+1 fused into the head: one launch fewer per
 // step): x[row] = emb[tok] (* 16 + pe[step+1] with position encoding) and

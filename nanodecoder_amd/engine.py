@@ -102,6 +102,14 @@ class Engine:
         _lib.check(self._L.nd_kernel_stamps(self._h, ctypes.byref(a), ctypes.byref(n)), "nd_kernel_stamps")
         return a.value, n.value
 
+    def _take_overflow(self):
+        """The split-fp16 range guard word of the calls enqueued so far
+        (nd_take_overflow): a [1] int32 device tensor, nonzero when some split
+        activation reached |x| >= 65504 (rerun the call with set_exact_fp32)."""
+        ov = torch.empty(1, dtype=torch.int32, device=self.device)
+        _lib.check(self._L.nd_take_overflow(self._h, _ptr(ov), self._stream()), "nd_take_overflow")
+        return ov
+
     def _inputs(self, signal, lengths, spans):
         dev = self.device
         # pinned host inputs (the Translator's staging ring) copy asynchronously
@@ -128,10 +136,10 @@ class Engine:
             _lib.check(self._L.nd_translate_greedy_attn(self._h, _ptr(signal), _ptr(lengths), _ptr(spans), B, T, S,
                                                         min_len, _ptr(tok), _ptr(sc), _ptr(lp), _ptr(at),
                                                         self._stream()), "nd_translate_greedy_attn")
-            return dict(tokens=tok, scores=sc, logp=lp, attn=at)
+            return dict(tokens=tok, scores=sc, logp=lp, attn=at, overflow=self._take_overflow())
         _lib.check(self._L.nd_translate_greedy(self._h, _ptr(signal), _ptr(lengths), _ptr(spans), B, T, S, min_len,
                                                _ptr(tok), _ptr(sc), _ptr(lp), self._stream()), "nd_translate_greedy")
-        return dict(tokens=tok, scores=sc, logp=lp, attn=None)
+        return dict(tokens=tok, scores=sc, logp=lp, attn=None, overflow=self._take_overflow())
 
     def translate_sample(self, signal, lengths, spans=None, temp: float = 1.0, keep_topk: int = -1, seed: int = 0,
                          max_len: Optional[int] = None, min_len: int = 0, return_logp: bool = False,
@@ -148,7 +156,7 @@ class Engine:
         _lib.check(self._L.nd_translate_sample(self._h, _ptr(signal), _ptr(lengths), _ptr(spans), B, T, S, min_len,
                                                float(temp), int(keep_topk), int(seed) & (2 ** 64 - 1), _ptr(tok),
                                                _ptr(sc), _ptr(lp), _ptr(at), self._stream()), "nd_translate_sample")
-        return dict(tokens=tok, scores=sc, logp=lp, attn=at)
+        return dict(tokens=tok, scores=sc, logp=lp, attn=at, overflow=self._take_overflow())
 
     def translate_beam(self, signal, lengths, spans=None, beam: int = 5, n_best: int = 1, alpha: float = 0.0,
                        max_len: Optional[int] = None, min_len: int = 0, return_attn: bool = False):
@@ -166,14 +174,15 @@ class Engine:
             _lib.check(self._L.nd_translate_beam(self._h, _ptr(signal), _ptr(lengths), _ptr(spans), B, T, beam,
                                                  n_best, float(alpha), S, min_len, _ptr(tok), _ptr(sc), _ptr(ln),
                                                  _ptr(st), self._stream()), "nd_translate_beam")
-            return dict(tokens=tok, scores=sc, lens=ln, steps=st)
+            return dict(tokens=tok, scores=sc, lens=ln, steps=st, overflow=self._take_overflow())
         att = torch.empty(B, n_best, S, T, dtype=torch.float32, device=self.device)
         done = torch.empty(B, dtype=torch.int32, device=self.device)
         _lib.check(self._L.nd_translate_beam_attn(self._h, _ptr(signal), _ptr(lengths), _ptr(spans), B, T, beam,
                                                   n_best, float(alpha), S, min_len, _ptr(tok), _ptr(sc), _ptr(ln),
                                                   _ptr(st), _ptr(att), _ptr(done), self._stream()),
                    "nd_translate_beam_attn")
-        return dict(tokens=tok, scores=sc, lens=ln, steps=st, attn=att, done_step=done)
+        return dict(tokens=tok, scores=sc, lens=ln, steps=st, attn=att, done_step=done,
+                    overflow=self._take_overflow())
 
     def translate_beam_classic(self, signal, lengths, spans=None, groups=None, beam: int = 5, n_best: int = 1,
                                length_penalty: str = "none", alpha: float = 0.0, max_len: Optional[int] = None,
@@ -207,7 +216,7 @@ class Engine:
                                                         ctypes.byref(opts), S, min_len, _ptr(tok), _ptr(sc), _ptr(ln),
                                                         _ptr(st), _ptr(att) if att is not None else None,
                                                         self._stream()), "nd_translate_beam_classic_ex")
-        out = dict(tokens=tok, scores=sc, lens=ln, steps=st)
+        out = dict(tokens=tok, scores=sc, lens=ln, steps=st, overflow=self._take_overflow())
         if return_attn:
             out["attn"] = att
         return out

@@ -204,7 +204,7 @@ class Translator(object):
         L[:n], S[:n] = lens, spans
         if dev_in is not None:
             sig, L, S = dev_in
-        job = dict(n=n, lens=lens, attn=attn, B=B, inputs=dev_in)
+        job = dict(n=n, lens=lens, attn=attn, B=B, inputs=dev_in, args=(chunks, spans, groups, attn))
         if self.beam_size == 1:
             if not (self.random_sampling_temp == 0.0 or self.sample_from_topk == 1):
                 # sample_with_temperature's random branch (translator.py:376-393)
@@ -275,6 +275,22 @@ class Translator(object):
             out = [None if r.get(k) is None else r[k].cpu().numpy() for k in names]
         return out
 
+    def _rerun_exact(self, job):
+        """Split-fp16 range guard (nd_take_overflow): a call in which some
+        split activation reached |x| >= 65504 (fp16's range; the reference's
+        fp32 is still finite there) runs again with every product in exact
+        fp32, and its results replace the flagged ones."""
+        self.engine.set_exact_fp32(True)
+        try:
+            again = self._submit(*job["args"])
+            again["exact"] = True
+            return self._finish(again)
+        finally:
+            self.engine.set_exact_fp32(False)
+
+    def _overflowed(self, job, ov):
+        return ov is not None and int(ov.reshape(-1)[0]) != 0 and not job.get("exact")
+
     def _finish(self, job):
         """Per chunk (scores[n_best], token lists[n_best]) and, with ``attn``,
         the attention rows of each hypothesis ([steps, cut] arrays, cut as the
@@ -282,7 +298,9 @@ class Translator(object):
         n, lens, attn = job["n"], job["lens"], job["attn"]
         out = []
         if job["kind"] == "greedy":
-            tok, sc, at = self._host(job, "tokens", "scores", "attn")
+            tok, sc, at, ov = self._host(job, "tokens", "scores", "attn", "overflow")
+            if self._overflowed(job, ov):
+                return self._rerun_exact(job)
             for i in range(n):
                 if attn:  # results["attention"]: rows cut at the chunk's length (translator.py:491-501)
                     out.append(([float(sc[i])], [tok[i].tolist()], [at[i, :, : lens[i]]]))
@@ -290,7 +308,9 @@ class Translator(object):
                     out.append(([float(sc[i])], [tok[i].tolist()]))
             return out
         grp, sorted_rows, cut, beam = job["grp"], job["sorted_rows"], job["cut"], self.beam_size
-        tok, sc, ln, at, done = self._host(job, "tokens", "scores", "lens", "attn", "done_step")
+        tok, sc, ln, at, done, ov = self._host(job, "tokens", "scores", "lens", "attn", "done_step", "overflow")
+        if self._overflowed(job, ov):
+            return self._rerun_exact(job)
         for i in range(n):
             o = ([float(sc[i, k]) for k in range(self.n_best)],
                  [tok[i, k, : ln[i, k]].tolist() for k in range(self.n_best)])

@@ -558,6 +558,42 @@ def test_translate_reads_packed_vs_oracle(beam):
     assert n_chunks > 16
 
 
+def test_split_fp16_range_guard():
+    """Activations beyond fp16's range (|x| >= 65504) in a split-fp16
+    product: the FFN hiddens of encoder layer 0 and decoder layer 1 scaled
+    up 1e5x (their W_2 down 1e5x, so the model's function is unchanged).
+    The engine's split path flags the call (nd_take_overflow) instead of
+    returning infs, the Translator reruns it on exact fp32, and the strings
+    and scores equal the fp32 oracle's.  The unscaled model never trips it."""
+    import types
+    from nanodecoder_amd.translator import Translator
+    ref = _oracle()
+    cfg = synth.ModelConfig()
+    W0 = synth.make_weights(cfg, seed=11, eos_bias=-1.0)
+    W = dict(W0)
+    for p in ("encoder.transformer.0.feed_forward", "decoder.transformer_layers.1.feed_forward"):
+        W[p + ".w_1.weight"] = W0[p + ".w_1.weight"] * np.float32(1e5)
+        W[p + ".w_1.bias"] = W0[p + ".w_1.bias"] * np.float32(1e5)
+        W[p + ".w_2.weight"] = W0[p + ".w_2.weight"] * np.float32(1e-5)
+    S = 30
+    reads = _reads_for_packing()[:4]
+    chunks = [c for r in reads for c in r]
+    from nanodecoder_amd.engine import pad_chunks
+    sig, lens = pad_chunks(chunks, 512)
+    for w, expect in ((W0, 0), (W, 1)):
+        eng = _engine(cfg, w, max_batch=16, max_steps=S)
+        r = eng.translate_greedy(sig, lens, np.full(len(chunks), 512, np.int32), max_len=S)
+        assert int(r["overflow"].cpu()[0]) == expect
+    opt = types.SimpleNamespace(gpu=0, n_best=1, max_length=S, min_length=4, beam_size=1, batch_size=3,
+                                engine_max_batch=16)
+    got = Translator(cfg, None, opt, engine=eng).translate_reads(reads, batch_size=3)
+    m = ref.RefModel(cfg, W)
+    for ri, chunks in enumerate(reads):
+        es, ep = ref.translate(m, chunks, 3, max_length=S, min_length=4)
+        assert got[ri][1] == ep, ri
+        assert np.abs(np.array(got[ri][0]) - np.array(es)).max() < 1e-3
+
+
 def test_beam_large_batch_vs_oracle():
     """--fast beam 5 on 416 chunks (2080 decoder rows: the LDS-tiled
     split-fp16 GEMMs of ND_P16_BIG_MIN's large-M path, as configs[3]'s
