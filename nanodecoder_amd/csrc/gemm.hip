@@ -402,7 +402,19 @@ __global__ void __launch_bounds__(NT* KS * 64) gemm_p16_kernel(const GemmArgs g)
   __shared__ f32x4 red[KS > 1 ? WAVES : 1][64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wt = wave % NT, ws = wave / NT;
-  const int nb = blockIdx.x * NT + wt, mb = blockIdx.y;
+  // XCD-aware block order: consecutive workgroups go to the 8 XCDs in turn
+  // (b % 8 share one), so XCD x is given a rectangle of (GY / a) row blocks x
+  // (GX / (8 / a)) column groups; each XCD's L2 then fetches 1 / a of A and
+  // a / 8 of W instead of all of A (grid order: x fastest, every XCD saw
+  // every row block; measured 4.2x the algorithmic fabric bytes at K = 2048)
+  int bx = blockIdx.x, by = blockIdx.y;
+  if (g.xcd_a) {
+    const int GX = gridDim.x, GY = gridDim.y, a = g.xcd_a, lc = GX / (8 / a);
+    const int lin = by * GX + bx, x = lin & 7, j = lin >> 3;
+    by = (x / (8 / a)) * (GY / a) + j / lc;
+    bx = (x % (8 / a)) * lc + j % lc;
+  }
+  const int nb = bx * NT + wt, mb = by;
   const int KB = g.K >> 4, NB = g.N >> 4;
   if (rows_dead(g.skip, g.skip_rpc, mb * 16, 16, g.M)) return;
   const f32x4* __restrict__ ap = reinterpret_cast<const f32x4*>(g.A) + ((size_t)mb * KB + ws * NF) * 64 + lane;
@@ -789,10 +801,30 @@ static hipError_t launch_cfg(GemmArgs& g, hipStream_t s) {
   return hipGetLastError();
 }
 
+// Row split a (a x 8/a rectangle of XCDs) that minimises the operand blocks
+// each XCD's L2 fetches: GY / a row blocks of A plus GX / (8 / a) column
+// groups of W (NT column blocks each); 0 when no split divides the grid.
+static int p16_xcd_rows(int GX, int GY, int NT) {
+  static const bool on = [] {
+    const char* e = getenv("ND_P16_XCD");  // 0: grid order (A/B timing)
+    return !(e && atoi(e) == 0);
+  }();
+  int best = 0;
+  long cost = 0;
+  for (int a = 1; a <= 8 && on; a *= 2) {
+    const int b = 8 / a;
+    if (GY % a || GX % b) continue;
+    const long c = (long)GY / a + (long)NT * GX / b;
+    if (!best || c < cost) best = a, cost = c;
+  }
+  return best;
+}
+
 template <int NT, int KS, int KW>
 static hipError_t launch_p16(GemmArgs& g, hipStream_t s) {
   if (g.N % (NT * 16) != 0 || g.K != KS * KW) return hipErrorInvalidValue;
   dim3 grid(g.N / (NT * 16), (g.M + 15) / 16), block(NT * KS * 64);
+  g.xcd_a = p16_xcd_rows((int)grid.x, (int)grid.y, NT);
   g.part_n_out = g.N / 16;
   if (g.Wh)
     ND_DISPATCH_FLAGS(gemm_p16_kernel, NT, KS, KW, true);

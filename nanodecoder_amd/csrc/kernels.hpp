@@ -44,6 +44,7 @@ struct GemmArgs {
   float wscale_rm = 1.0f;
   int p16io = 0;
   int xcd_map = 0;     // row-major kernel: XCD-aware tile order (set by launch_gemm)
+  int xcd_a = 0;       // P16 kernel: row-block split over the 8 XCDs (0: grid order; set by launch_p16)
   // split-fp16 range guard (common.hpp flag_overflow): set to 1 when a split
   // activation operand (no LN prologue) reaches |x| >= 65504; nullable
   int* ovf = nullptr;
