@@ -300,6 +300,17 @@ int nd_op_gemm_p16(const float* A, const float* W, const float* bias, const floa
  * product hi*hi + hi*lo + lo*hi on 16x16x32 f16 MFMAs into fp32.  Otherwise
  * exactly nd_op_gemm_p16. */
 int nd_op_pack_p16h(const float* W, int32_t N, int32_t K, uint16_t* out, float* wscale, void* stream);
+/* The encoder's fused position-wise FFN block (onmt/modules/position_ffn.py:
+ * 27-40 as encoder/transformer.py:36-54 runs it): x = y + W2 relu(W1' LN(y)
+ * + b1') + b2 over M rows of 256, y and x row-major [M, 256] (x != y), with
+ * the LayerNorm affine folded into W1' / b1' (nd_op_fold_layernorm).  w1h /
+ * w2h: P16H images (nd_op_pack_p16h) of W1' [F, 256] and W2 [256, F] with
+ * their scales; F % 64 == 0, F <= 2048.  xpart (nullable) gets each row's
+ * {mean, M2} at xpart[row * 32]; overflow (nullable) is set to 1 when a
+ * hidden value leaves the fp16 range. */
+int nd_op_enc_ffn(const float* y, const uint16_t* w1h, float w1s, const float* b1, const uint16_t* w2h, float w2s,
+                  const float* b2, float* x, float* xpart, int32_t M, int32_t F, int32_t* overflow, void* stream);
+
 int nd_op_gemm_p16_split(const float* A, const uint16_t* Wh, float wscale, const float* bias, const float* R, float* C,
                          int32_t M, int32_t N, int32_t K, const float* part_in, int32_t part_n_in, float* part_out,
                          int32_t relu, int32_t* part_n_out, void* stream);

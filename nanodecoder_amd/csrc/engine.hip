@@ -56,6 +56,9 @@ struct Slot {
 struct EncLayer {
   float *ln_g, *ln_b, *wqkv, *bqkv, *wo, *bo, *fln_g, *fln_b, *w1, *b1, *w2, *b2;
   float *nwqkv, *nbqkv, *nw1, *nb1;
+  // P16H images of W1' (LN folded) and W2 for the fused FFN block (ffn.hip)
+  uint16_t *w1h = nullptr, *w2h = nullptr;
+  float w1s = 1.f, w2s = 1.f;
 };
 struct DecLayer {
   float *ln1_g, *ln1_b, *wqkv, *bqkv, *wo, *bo, *ln2_g, *ln2_b, *cwq, *cbq, *cwo, *cbo, *fln_g, *fln_b, *w1, *b1,
@@ -487,6 +490,16 @@ struct G {
 
 // Encoder forward (transformer): x <- memory before the final LayerNorm (its
 // row statistics in x_part); the final LN is the ctx-K/V GEMM's prologue.
+// fused FFN block (ffn.hip) on the split-fp16 path; ND_ENC_FFN=0 keeps the
+// two GEMMs (A/B timing; same arithmetic)
+static bool enc_ffn_fused(const nd_ctx* c, const EncLayer& L) {
+  static const bool on = [] {
+    const char* e = getenv("ND_ENC_FFN");
+    return !(e && atoi(e) == 0);
+  }();
+  return on && !c->exact && L.w1h != nullptr && !nd::gemm_f32_forced();
+}
+
 static hipError_t enqueue_encode_transformer(nd_ctx* c, int B, int T, hipStream_t s) {
   const int M = B * T, D = c->D, F = c->F;
   LCHK(nd::launch_enc_embed(c->sig, c->enc_lin_w, c->enc_lin_b, c->x, c->x_part, B, T, s));
@@ -496,6 +509,11 @@ static hipError_t enqueue_encode_transformer(nd_ctx* c, int B, int T, hipStream_
     LCHK(G(c->x, D, L.nwqkv, 3 * D, D, L.nbqkv, c->big, 3 * D, M).h3(c).ln(c->x_part, pnx).run(s));
     LCHK(nd::launch_enc_attention(c->big, c->sig, c->span, c->att, B, T, s, c->exact, c->ovf));
     LCHK(G(c->att, D, L.wo, D, D, L.bo, c->y, D, M).h3(c).res(c->x, D).stats(c->y_part).run(s, &pny));
+    if (enc_ffn_fused(c, L)) {  // position_ffn.py:27-40 in one launch: the hidden stays on chip
+      LCHK(nd::launch_enc_ffn(c->y, L.w1h, L.w1s, L.nb1, L.w2h, L.w2s, L.b2, c->x, c->x_part, M, F, c->ovf, s));
+      pnx = 1;
+      continue;
+    }
     LCHK(G(c->y, D, L.nw1, F, D, L.nb1, c->big, F, M).h3(c).ln(c->y_part, pny).relu().run(s));
     LCHK(G(c->big, F, L.w2, D, F, L.b2, c->x, D, M).h3(c).res(c->y, D).stats(c->x_part).run(s, &pnx));
   }
@@ -946,6 +964,7 @@ int nd_finalize(nd_ctx* c) {
     // split-fp16 images of the encoder-side row-major GEMM weights
     // (gemm.hip H3); ND_GEMM_F32=1 at run time keeps the fp32 kernels
     const int D = c->D, F = c->F, L2 = (int)c->dec.size() * 2 * D;
+    hipError_t e_ = hipSuccess;
     auto mk = [&](const float* W, int N, int K) -> hipError_t {
       uint16_t* h = nullptr;
       float sc = 1.f;
@@ -961,6 +980,12 @@ int nd_finalize(nd_ctx* c) {
       HIPCHK(mk(L.wo, D, D));
       HIPCHK(mk(L.nw1, F, D));
       HIPCHK(mk(L.w2, D, F));
+      if (F % 64 == 0 && F <= 2048) {  // the fused FFN block's weight images
+        if (!L.w1h && (e_ = dalloc(c, &L.w1h, (size_t)2 * F * D)) != hipSuccess) return fail(ND_ERR_HIP, "alloc");
+        if (!L.w2h && (e_ = dalloc(c, &L.w2h, (size_t)2 * F * D)) != hipSuccess) return fail(ND_ERR_HIP, "alloc");
+        HIPCHK(nd::launch_pack_p16h(L.nw1, D, F, D, L.w1h, &L.w1s, c->es));
+        HIPCHK(nd::launch_pack_p16h(L.w2, F, D, F, L.w2h, &L.w2s, c->es));
+      }
     }
     HIPCHK(mk(c->cfg.encoder_type == ND_ENC_TRANSFORMER ? c->nctxkv_w : c->ctxkv_w, L2, D));
     for (size_t l = 1; l < c->nano.size(); ++l) HIPCHK(mk(c->nano[l].wih, 8 * c->H, 2 * c->H));
@@ -1417,6 +1442,14 @@ int nd_op_gemm_p16(const float* A, const float* W, const float* bias, const floa
 int nd_op_pack_p16h(const float* W, int32_t N, int32_t K, uint16_t* out, float* wscale, void* stream) {
   hipError_t e = nd::launch_pack_p16h(W, K, N, K, out, wscale, (hipStream_t)stream);
   if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("pack_p16h: ") + hipGetErrorString(e));
+  return ND_OK;
+}
+
+int nd_op_enc_ffn(const float* y, const uint16_t* w1h, float w1s, const float* b1, const uint16_t* w2h, float w2s,
+                  const float* b2, float* x, float* xpart, int32_t M, int32_t F, int32_t* overflow, void* stream) {
+  if (int rc = ensure_attributes()) return rc;
+  hipError_t e = nd::launch_enc_ffn(y, w1h, w1s, b1, w2h, w2s, b2, x, xpart, M, F, overflow, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("enc_ffn: ") + hipGetErrorString(e));
   return ND_OK;
 }
 

@@ -167,15 +167,17 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
       c = (f % TPK) * 4;
     }
   };
+  // straight-line loads: the row is clamped into the matrix and rows >= M
+  // are zeroed at the LDS store (a guarded load per element made hipcc
+  // branch around each one and wait for the previous before issuing it)
   auto load_tile = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < A4; ++i) {
       int row, c;
       amap(i, row, c);
-      const int gr = m0 + row;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (gr < M) v = ld4(g.p16io ? A + pk(gr, k0 + c, K) : A + (size_t)gr * g.lda + k0 + c);
-      ra[i] = v;  // raw: the LayerNorm is applied at the LDS store, once the row statistics are in
+      const int gr = min(m0 + row, M - 1);
+      const size_t off = g.p16io ? pk(gr, k0 + c, K) : (size_t)gr * g.lda + k0 + c;
+      ra[i] = ld4(A + off);  // raw: the LayerNorm is applied at the LDS store, once the row statistics are in
     }
 #pragma unroll
     for (int i = 0; i < W4; ++i) {
@@ -193,6 +195,7 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
       int row, c;
       amap(i, row, c);
       if constexpr (LN) ra[i] = (ra[i] - s_mu[row]) * s_rs[row];
+      if (m0 + row >= M) ra[i] = f32x4{0.f, 0.f, 0.f, 0.f};
       if constexpr (H3) {
         if constexpr (!LN) amax = fmaxf(amax, absmax4(ra[i]));
         h4 hi, lo;
@@ -893,6 +896,8 @@ static bool gemm_f32_only() {
   }();
   return f32only;
 }
+
+bool gemm_f32_forced() { return gemm_f32_only(); }
 
 static hipError_t check_args(const GemmArgs& g) {
   if (g.K % 32 != 0 || (g.norm && g.K != ND_D)) return hipErrorInvalidValue;

@@ -71,6 +71,8 @@ hipError_t launch_split_weight(const float* W, int N, int K, uint16_t* Wh, float
 // P16 kernels: [N/16][K/32][hi | lo][64 lanes][8 halves] of W * 2^s (scale as
 // launch_split_weight; synchronises the stream).  N % 16 == 0, K % 32 == 0.
 hipError_t launch_pack_p16h(const float* W, int ld, int N, int K, uint16_t* out, float* wscale, hipStream_t s);
+// ND_GEMM_F32=1: the fp32-MFMA kernels everywhere (split images unused)
+bool gemm_f32_forced();
 // raises the dynamic-LDS limit of the LDS-staged GEMM kernels (once per process)
 hipError_t init_gemm_attributes();
 // row-major [M, N] with leading dimension ld -> P16 (M, N multiples of 16)
@@ -95,6 +97,12 @@ hipError_t launch_enc_attention(const float* qkv, const float* signal, const int
 hipError_t launch_lstm_layer(const float* xp, const float* signal, const float* wih0, const float* bsum,
                              const float* whh, const int* len, int B, int T, float* out, const float* bn_scale,
                              const float* bn_shift, bool layer0, hipStream_t s, bool exact = false);
+// fused encoder FFN block (ffn.hip): x = y + W2 relu(W1' LN(y) + b1') + b2 with
+// the LN affine folded into W1' / b1'; w1h = P16H image of W1' [F, 256], w2h =
+// P16H image of W2 [256, F] (launch_pack_p16h), w*s their scales; xpart gets
+// each row's exact {mean, M2} in slot 0 (one partial).  F % 64 == 0, F <= 2048.
+hipError_t launch_enc_ffn(const float* y, const uint16_t* w1h, float w1s, const float* b1, const uint16_t* w2h,
+                          float w2s, const float* b2, float* x, float* xpart, int M, int F, int* ovf, hipStream_t s);
 // out[r] = LN(x[r]) (rows of 256)
 hipError_t launch_layernorm(const float* x, const float* g, const float* b, float* out, int rows, hipStream_t s);
 

@@ -327,6 +327,24 @@ def op_pack_p16h(W: torch.Tensor):
     return Wh, sc.value
 
 
+def op_enc_ffn(y, W1, b1, W2, b2, ln_g, ln_b):
+    """The encoder's fused FFN block (nd_op_enc_ffn): x = y + W2 relu(W1
+    LN(y) + b1) + b2 for row-major y [M, 256], the LN affine folded and both
+    weights packed to P16H images here as the engine does at load time.
+    Returns (x, row stats [M, 2] = {mean, M2}, overflow flag)."""
+    M, F = y.shape[0], W1.shape[0]
+    W1f, b1f = op_fold_layernorm(W1, b1, ln_g, ln_b)
+    w1h, w1s = op_pack_p16h(W1f)
+    w2h, w2s = op_pack_p16h(W2)
+    x = torch.empty_like(y)
+    part = torch.zeros(M, 16, 2, dtype=torch.float32, device=y.device)
+    ov = torch.zeros(1, dtype=torch.int32, device=y.device)
+    s = ctypes.c_void_p(torch.cuda.current_stream(y.device).cuda_stream)
+    _lib.check(_lib.lib().nd_op_enc_ffn(_ptr(y), _ptr(w1h), w1s, _ptr(b1f), _ptr(w2h), w2s, _ptr(b2), _ptr(x),
+                                        _ptr(part), M, F, _ptr(ov), s), "nd_op_enc_ffn")
+    return x, part[:, 0, :], ov
+
+
 def op_gemm_p16(Ap, Wp, bias, M, N, K, Rp=None, part_in=None, relu=False, part_out=None, Wh=None, wscale=1.0,
                 Wh_rm=None, wscale_rm=1.0):
     """The decoder-step GEMM on packed operands (see pack_p16).  Returns the

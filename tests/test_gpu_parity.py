@@ -63,6 +63,37 @@ def test_gemm_vs_fp64(M, N, K, ln, relu, res, split):
     assert (out - ref).abs().max().item() < 2e-4
 
 
+@pytest.mark.parametrize("M,F", [(1000, 2048), (256, 2048), (131, 64), (384, 512)])
+def test_enc_ffn_fused_vs_fp64(M, F):
+    """The encoder's fused FFN block (nd_op_enc_ffn: LayerNorm, W1, ReLU, W2
+    and the residual in one launch, the hidden kept on chip) against fp64,
+    with a ragged last 128-row block (M = 1000, 131), d_ff 64..2048: the same
+    2e-4 absolute bound as the split GEMMs, and the exact row statistics it
+    hands to the next LayerNorm."""
+    from nanodecoder_amd.engine import op_enc_ffn
+    g = torch.Generator().manual_seed(M + F)
+    y = torch.randn(M, 256, generator=g) * 2 + 0.5
+    W1 = torch.randn(F, 256, generator=g) / 16
+    b1 = torch.randn(F, generator=g) * 0.1
+    W2 = torch.randn(256, F, generator=g) / F ** 0.5
+    b2 = torch.randn(256, generator=g) * 0.1
+    lg = 1 + 0.1 * torch.randn(256, generator=g)
+    lb = 0.1 * torch.randn(256, generator=g)
+    dev = torch.device("cuda", 0)
+    x, st, ov = op_enc_ffn(*(t.to(dev) for t in (y, W1, b1, W2, b2, lg, lb)))
+    torch.cuda.synchronize()
+    yd = y.double()
+    h = torch.relu(torch.nn.functional.layer_norm(yd, (256,), lg.double(), lb.double(), 1e-6) @ W1.double().t()
+                   + b1.double())
+    ref = yd + h @ W2.double().t() + b2.double()
+    got = x.cpu().double()
+    assert (got - ref).abs().max().item() < 2e-4
+    st = st.cpu().double()
+    assert torch.allclose(st[:, 0], got.mean(1), atol=1e-5)
+    assert torch.allclose(st[:, 1], ((got - got.mean(1, keepdim=True)) ** 2).sum(1), rtol=1e-4, atol=1e-3)
+    assert int(ov.cpu()[0]) == 0
+
+
 @pytest.mark.parametrize("N,K,mag", [(256, 256, 1.0), (768, 256, 3e-4), (256, 2048, 40.0)])
 def test_split_weight_image(N, K, mag):
     """nd_op_split_weight: hi + lo reproduces W * 2^s to 2^-21 relative (half

@@ -76,6 +76,28 @@ if ONLY == "enc":
         gemm_case(131072, 2048, 256, True, True, False, sp)    # FFN1 (LN, relu)
         gemm_case(131072, 256, 2048, False, False, True, sp)   # FFN2 (+res)
     sys.exit(0)
+if ONLY == "encffn":  # the fused FFN block against the two split GEMMs it replaces
+    M = 131072
+    y = torch.randn(M, 256, device=dev)
+    W1 = torch.randn(2048, 256, device=dev) / 16
+    W2 = torch.randn(256, 2048, device=dev) / 45
+    b1, b2 = torch.randn(2048, device=dev), torch.randn(256, device=dev)
+    lg, lb = torch.rand(256, device=dev) + 0.5, torch.randn(256, device=dev)
+    import ctypes
+    from nanodecoder_amd import _lib
+    W1f, b1f = E.op_fold_layernorm(W1, b1, lg, lb)
+    w1h, w1s = E.op_pack_p16h(W1f)
+    w2h, w2s = E.op_pack_p16h(W2)
+    x = torch.empty_like(y)
+    part = torch.empty(M, 16, 2, device=dev)
+    st = lambda: ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)  # noqa: E731
+    us = timeit(lambda: _lib.lib().nd_op_enc_ffn(y.data_ptr(), w1h.data_ptr(), w1s, b1f.data_ptr(), w2h.data_ptr(),
+                                                  w2s, b2.data_ptr(), x.data_ptr(), part.data_ptr(), M, 2048, None,
+                                                  st()), n=5)
+    print(f"enc-ffn fused M={M}: {us:9.2f} us  {2 * 2 * M * 2048 * 256 / (us * 1e-6) / 1e12:6.1f} TF/s (fp32-equiv)")
+    gemm_case(M, 2048, 256, True, True, False, True)
+    gemm_case(M, 256, 2048, False, False, True, True)
+    sys.exit(0)
 if ONLY == "ffn1s":  # one encoder GEMM in the split-fp16 form (PMC passes: MB_EAGER=1)
     gemm_case(131072, 2048, 256, True, True, False, True)
     sys.exit(0)
