@@ -305,7 +305,7 @@ int nd_op_pack_p16h(const float* W, int32_t N, int32_t K, uint16_t* out, float* 
  * + b1') + b2 over M rows of 256, y and x row-major [M, 256] (x != y), with
  * the LayerNorm affine folded into W1' / b1' (nd_op_fold_layernorm).  w1h /
  * w2h: P16H images (nd_op_pack_p16h) of W1' [F, 256] and W2 [256, F] with
- * their scales; F % 64 == 0, F <= 2048.  xpart (nullable) gets each row's
+ * their scales; F % 32 == 0, F <= 2048.  xpart (nullable) gets each row's
  * {mean, M2} at xpart[row * 32]; overflow (nullable) is set to 1 when a
  * hidden value leaves the fp16 range. */
 int nd_op_enc_ffn(const float* y, const uint16_t* w1h, float w1s, const float* b1, const uint16_t* w2h, float w2s,

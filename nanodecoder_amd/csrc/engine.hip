@@ -980,7 +980,7 @@ int nd_finalize(nd_ctx* c) {
       HIPCHK(mk(L.wo, D, D));
       HIPCHK(mk(L.nw1, F, D));
       HIPCHK(mk(L.w2, D, F));
-      if (F % 64 == 0 && F <= 2048) {  // the fused FFN block's weight images
+      if (F % 32 == 0 && F <= 2048) {  // the fused FFN block's weight images
         if (!L.w1h && (e_ = dalloc(c, &L.w1h, (size_t)2 * F * D)) != hipSuccess) return fail(ND_ERR_HIP, "alloc");
         if (!L.w2h && (e_ = dalloc(c, &L.w2h, (size_t)2 * F * D)) != hipSuccess) return fail(ND_ERR_HIP, "alloc");
         HIPCHK(nd::launch_pack_p16h(L.nw1, D, F, D, L.w1h, &L.w1s, c->es));

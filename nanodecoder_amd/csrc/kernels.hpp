@@ -100,7 +100,7 @@ hipError_t launch_lstm_layer(const float* xp, const float* signal, const float* 
 // fused encoder FFN block (ffn.hip): x = y + W2 relu(W1' LN(y) + b1') + b2 with
 // the LN affine folded into W1' / b1'; w1h = P16H image of W1' [F, 256], w2h =
 // P16H image of W2 [256, F] (launch_pack_p16h), w*s their scales; xpart gets
-// each row's exact {mean, M2} in slot 0 (one partial).  F % 64 == 0, F <= 2048.
+// each row's exact {mean, M2} in slot 0 (one partial).  F % 32 == 0, F <= 2048.
 hipError_t launch_enc_ffn(const float* y, const uint16_t* w1h, float w1s, const float* b1, const uint16_t* w2h,
                           float w2s, const float* b2, float* x, float* xpart, int M, int F, int* ovf, hipStream_t s);
 // out[r] = LN(x[r]) (rows of 256)

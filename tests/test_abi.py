@@ -55,3 +55,20 @@ def test_code_object_targets_gfx950(lib):
     so = os.path.join(ROOT, "nanodecoder_amd", "libnanodec_hip.so")
     blob = open(so, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in blob
+
+
+def test_inline_asm_lds_ring_has_no_hazard(tmp_path):
+    """ffn.hip's inline-asm LDS read ring: in the compiled gfx950 code no
+    instruction touches a ring destination register between its ds_read and
+    the s_waitcnt that retires it (tools/lds_ring_check.py)."""
+    import subprocess
+    import sys
+    from nanodecoder_amd import build
+    if not os.path.exists(build.HIPCC):
+        pytest.skip("no hipcc")
+    out = tmp_path / "ffn.s"
+    subprocess.run([build.HIPCC] + build.CFLAGS + ["--cuda-device-only", "-S", os.path.join(build.CSRC, "ffn.hip"),
+                    "-o", str(out)], check=True, capture_output=True)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "lds_ring_check.py"), str(out), "enc_ffn"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0 and "0 hazards" in r.stdout, r.stdout + r.stderr

@@ -8,6 +8,7 @@
 #   bash tools/gpu.sh prof TAG [bench args]     rocprofv3 --kernel-trace --stats of a short bench
 #   bash tools/gpu.sh pmc TAG "CTRS" [args]     one rocprofv3 --pmc pass (one counter group)
 #   bash tools/gpu.sh mfma TAG [args]          rocprofv3 MFMA counter pass -> gpurun_out/TAG_mfma.json
+#   bash tools/gpu.sh pmcmb TAG "CTRS" CASE   one --pmc pass over a microbench case
 #   bash tools/gpu.sh list                      rocprofv3 -L (available counters)
 #   bash tools/gpu.sh py TAG script.py [args]   any python tool (probes, microbenches)
 # Steps chain with &&:  bash tools/gpu.sh test && bash tools/gpu.sh bench r02_greedy
@@ -54,6 +55,13 @@ case $step in
       --no-roofline "$@" > $O/$tag.log 2>&1
     rc=$?; echo "mfma $tag rc=$rc"; [ $rc -ne 0 ] && exit $rc
     python3 $R/tools/mfma_summary.py $O/$tag/run_counter_collection.csv $tag $O/${tag}_mfma.json | head -40; exit 0 ;;
+  pmcmb)
+    # one --pmc pass over a tools/microbench.py case (plain launches)
+    tag=$1; ctrs=$2; shift 2
+    cd /tmp && export TMPDIR=/tmp
+    MB_EAGER=1 timeout -s KILL 180 rocprofv3 --pmc $ctrs --kernel-trace -d $O/$tag -o run --output-format csv -- \
+      python3 $R/tools/microbench.py "$@" > $O/$tag.log 2>&1
+    rc=$?; echo "pmcmb $tag rc=$rc"; exit $rc ;;
   list)
     cd /tmp && export TMPDIR=/tmp
     timeout -s KILL 60 rocprofv3 -L > $O/counters.txt 2>&1
