@@ -15,7 +15,7 @@ once over RCCL.
 
 Beside the headline ``value`` the line carries, on every run:
   roofline      the dominant kernel against its HBM roofline (live in-kernel
-                timing) + the encoder FFN1 GEMM against the MFMA peak;
+                timing) + the fused encoder FFN block against the MFMA peak;
   mfma          algorithmic MFMA utilisation, path-level and encoder-only,
                 against the fp32 peak and the split-fp16 fp32-equivalent peak
                 (and the committed rocprof counter pass, profiles/);
@@ -287,31 +287,38 @@ def kernel_roofline(eng, B, mode, beam, encoder="transformer", alive=None):
         return out
     import ctypes
     from nanodecoder_amd import _lib
-    from nanodecoder_amd.engine import op_fold_layernorm, op_split_weight
-    # secondary: the dominant encoder MFMA kernel (FFN1 GEMM, LN prologue + bias
-    # + ReLU) in the split-fp16 form the engine runs: 3 fp16 MFMA products per
-    # fp32 multiply-add, so its fp32-equivalent peak is the dense fp16 peak / 3
-    M, K, N = B * T, 256, 2048
-    A = torch.randn(M, K, device=dev)
-    Wt = torch.randn(N, K, device=dev) / 16
-    b = torch.randn(N, device=dev)
-    Wf, bf = op_fold_layernorm(Wt, b, torch.ones(K, device=dev), torch.zeros(K, device=dev))  # as at load time
-    Wh, sc = op_split_weight(Wf)
-    C = torch.empty(M, N, device=dev)
+    from nanodecoder_amd.engine import op_fold_layernorm, op_pack_p16h
+    # secondary: the dominant encoder MFMA kernel, the fused FFN block
+    # (enc_ffn_kernel: LN + W1 + bias + ReLU + W2 + bias + residual, the hidden
+    # kept on chip) in the split-fp16 form the engine runs: 3 fp16 MFMA
+    # products per fp32 multiply-add, so its fp32-equivalent peak is the dense
+    # fp16 peak / 3.  Algorithmic work: the two products, 2 x 2 M F D.
+    M, D, F = B * T, 256, 2048
+    Y = torch.randn(M, D, device=dev)
+    W1, b1 = op_fold_layernorm(torch.randn(F, D, device=dev) / 16, torch.randn(F, device=dev) * 0.1,
+                               torch.ones(D, device=dev), torch.zeros(D, device=dev))  # as at load time
+    w1h, w1s = op_pack_p16h(W1)
+    w2h, w2s = op_pack_p16h(torch.randn(D, F, device=dev) / F ** 0.5)
+    b2 = torch.randn(D, device=dev) * 0.1
+    X = torch.empty_like(Y)
+    part = torch.empty(M, 16, 2, device=dev)
+    ov = torch.zeros(1, dtype=torch.int32, device=dev)
     st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
 
-    def ffn1(i):
-        _lib.check(_lib.lib().nd_op_gemm_split(A.data_ptr(), Wh.data_ptr(), sc, bf.data_ptr(), None, C.data_ptr(),
-                                               M, N, K, 1, 1, st), "nd_op_gemm_split")
+    def ffn(i):
+        _lib.check(_lib.lib().nd_op_enc_ffn(Y.data_ptr(), w1h.data_ptr(), w1s, b1.data_ptr(), w2h.data_ptr(), w2s,
+                                            b2.data_ptr(), X.data_ptr(), part.data_ptr(), M, F, ov.data_ptr(), st),
+                   "nd_op_enc_ffn")
     for i in range(3):
-        ffn1(i)
-    gms = _StreamTimer(dev).time(ffn1, 10)
-    tf = 2.0 * M * N * K / (gms * 1e-3) / 1e12
-    out["mfma_kernel"] = {"kernel": "gemm_f32_kernel<256,256,2,4,H3,LN,RELU> (encoder FFN1, split-fp16)",
+        ffn(i)
+    gms = _StreamTimer(dev).time(ffn, 10)
+    tf = 4.0 * M * F * D / (gms * 1e-3) / 1e12
+    out["mfma_kernel"] = {"kernel": "enc_ffn_kernel (encoder FFN block: W1 and W2 products fused, split-fp16)",
                           "achieved": round(tf, 2), "peak": round(SPLIT_PEAK, 1),
                           "unit": "TFLOP/s fp32-equivalent (fp16 MFMA peak / 3 products)",
-                          "frac": round(tf / SPLIT_PEAK, 4), "avg_launch_ms": round(gms, 4)}
-    del A, C, Wh, Wf
+                          "frac": round(tf / SPLIT_PEAK, 4), "avg_launch_ms": round(gms, 4),
+                          "algorithmic_flops_per_launch": int(4 * M * F * D)}
+    del Y, X, W1, w1h, w2h
     return out
 
 
