@@ -28,6 +28,7 @@
 #include "kernels.hpp"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace nd {
 
@@ -37,11 +38,13 @@ __device__ __forceinline__ f32x4 mfma16x4(float a, float b, f32x4 c) {
 
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
 // the cell's activations on the hardware exp (v_exp_f32) and reciprocal
-// (a few ulp from the libm forms; ND_LSTM_LIBM=1 keeps expf / tanhf)
-__device__ __forceinline__ float sigm_fast(float x) { return __frcp_rn(1.0f + __expf(-x)); }
+// (v_rcp_f32, 1 ulp; __frcp_rn lowers to the ~10-instruction IEEE division
+// sequence, and five of them sat on every step's dependent chain); a few ulp
+// from the libm forms; ND_LSTM_LIBM=1 keeps expf / tanhf
+__device__ __forceinline__ float sigm_fast(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 __device__ __forceinline__ float tanh_fast(float x) {
   const float t = __expf(-2.0f * fabsf(x));
-  return copysignf((1.0f - t) * __frcp_rn(1.0f + t), x);
+  return copysignf((1.0f - t) * __builtin_amdgcn_rcpf(1.0f + t), x);
 }
 template <bool FAST>
 __device__ __forceinline__ float act_sig(float x) { return FAST ? sigm_fast(x) : sigm(x); }
@@ -203,33 +206,49 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
         bb[u][g] = bsum[dir * LSTM_G + g * LSTM_H + punit[u]];
       }
   }
-  auto pos_of = [&](int q, int step) { return dir == 0 ? step : s_len[q] - 1 - step; };
+  // lengths in registers (the step loop's raw barrier clobbers LDS-held values)
+  int mylen[2];
+#pragma unroll
+  for (int u = 0; u < NP; ++u) mylen[u] = s_len[pseq[u]];
+  // Global traffic inside the step loop is straight-line: every x load and
+  // every h store is issued unconditionally (clamped rows; past a sequence's
+  // end the lane re-writes 0 into a padding row), so the compiler's vmcnt
+  // waits count exactly and a step waits only for its own x, which was
+  // loaded PD steps earlier.  A branch around any of them made it wait
+  // vmcnt(0), i.e. for this step's h store and the prefetch, every step.
+  // Workgroups with fewer than NS live sequences run a second copy of the
+  // loop with the guarded forms (FULL = false).
+  auto pos_of = [&](int u, int step) { return dir == 0 ? step : mylen[u] - 1 - step; };
   auto load_x = [&](int step, float (&x)[2][4]) {
 #pragma unroll
     for (int u = 0; u < NP; ++u) {
       const int q = pseq[u];
-      const bool act = step < s_len[q];
-      const int pos = act ? pos_of(q, step) : 0;
-      const size_t row = (size_t)(b0 + q) * T + pos;
+      const bool act = step < mylen[u];
+      const int pos = act ? pos_of(u, step) : 0;
+      const size_t row = (size_t)min(b0 + q, B - 1) * T + pos;
       if constexpr (LAYER0) {
-        x[u][0] = act ? signal[row] : 0.f;  // the sample; its projection is formed at use (no wait here)
+        x[u][0] = signal[row];  // the sample; its projection is formed at use
       } else {
 #pragma unroll
-        for (int g = 0; g < 4; ++g) x[u][g] = act ? xp[row * 1024 + dir * LSTM_G + g * LSTM_H + punit[u]] : 0.f;
+        for (int g = 0; g < 4; ++g) x[u][g] = xp[row * 1024 + dir * LSTM_G + g * LSTM_H + punit[u]];
       }
     }
   };
 
-  float xn[2][4];
-  load_x(0, xn);
-  for (int step = 0; step < maxlen; ++step) {
+  // PD named x buffers (the step loop unrolled by PD): NS = 16 has no
+  // registers to spare and keeps one
+  constexpr int PD = NS == 16 ? 1 : 2;
+  float xa[2][4], xb[2][4];
+  load_x(0, xa);
+  if (PD > 1) load_x(1, xb);
+  auto step_body = [&](auto full_c, const int step, float (&xn)[2][4]) {
+    constexpr bool FULL = decltype(full_c)::value;
     const int cur = step & 1;
     float xc[2][4];
 #pragma unroll
     for (int u = 0; u < NP; ++u)
 #pragma unroll
       for (int g = 0; g < 4; ++g) xc[u][g] = LAYER0 ? xn[u][0] * w0[u][g] + bb[u][g] : xn[u][g];
-    if (step + 1 < maxlen) load_x(step + 1, xn);  // prefetch next step's projections
 
     // gates = h_{t-1} W_hh^T on MFMA
     f32x4 acc[NT];
@@ -249,8 +268,8 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
 #pragma unroll
         for (int t = 0; t < NT; ++t) acc[t] = mfma16x32h(ah, whi[t][kb], acc[t]);
       }
-#pragma unroll
-      for (int t = 0; t < NT; ++t) acc[t] *= unscale;
+      // (the 2^-s / 2^10 unscale is applied to the four gate sums a lane keeps,
+      // in the cell: 4 FMAs instead of 4 NT multiplies here)
     } else {
       const float* hrow = &hs[cur][li * LSTM_HS_LD + 4 * lq];
 #pragma unroll
@@ -328,16 +347,15 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
 #pragma unroll
     for (int u = 0; u < NP; ++u) {
       const int q = pseq[u], j = punit[u];
-      float h;
-      if (step < s_len[q]) {
-        const float ig = act_sig<FAST>(zg[u][0] + xc[u][0]);
-        const float fg = act_sig<FAST>(zg[u][1] + xc[u][1]);
-        const float gg = act_tanh<FAST>(zg[u][2] + xc[u][2]);
-        const float og = act_sig<FAST>(zg[u][3] + xc[u][3]);
+      const bool act = step < mylen[u];
+      float h = 0.f;
+      if (act) {
+        const float ig = act_sig<FAST>(fmaf(zg[u][0], unscale, xc[u][0]));
+        const float fg = act_sig<FAST>(fmaf(zg[u][1], unscale, xc[u][1]));
+        const float gg = act_tanh<FAST>(fmaf(zg[u][2], unscale, xc[u][2]));
+        const float og = act_sig<FAST>(fmaf(zg[u][3], unscale, xc[u][3]));
         c[u] = fg * c[u] + ig * gg;
         h = og * act_tanh<FAST>(c[u]);
-        const size_t row = (size_t)(b0 + q) * T + pos_of(q, step);
-        out[row * 2 * LSTM_H + dir * LSTM_H + j] = bn_scale ? h * s_bn[0][j] + s_bn[1][j] : h;
         if constexpr (H3) {
           // the split the consumers used to form from the fp32 h (lsplit8 of h 2^10)
           const float x = h * LSTM_HSCALE;
@@ -352,8 +370,38 @@ lstm_dir_kernel(const float* __restrict__ xp,      // [B*T, 1024] input projecti
         h = hs[cur][q * LSTM_HS_LD + j];
       }
       if constexpr (!H3) hs[cur ^ 1][q * LSTM_HS_LD + j] = h;
+      const float ov = act ? (bn_scale ? h * s_bn[0][j] + s_bn[1][j] : h) : 0.f;
+      if constexpr (FULL) {  // unconditional: past the end, 0 into padding row `step`
+        const size_t row = (size_t)(b0 + q) * T + (act ? pos_of(u, step) : step);
+        out[row * 2 * LSTM_H + dir * LSTM_H + j] = ov;
+      } else if (act) {
+        const size_t row = (size_t)(b0 + q) * T + pos_of(u, step);
+        out[row * 2 * LSTM_H + dir * LSTM_H + j] = ov;
+      }
     }
-    __syncthreads();
+    load_x(step + PD, xn);  // this buffer's next use: step + PD (past maxlen: a clamped, unused load)
+    // publish h_t (LDS) to every wave: a raw barrier behind an LDS-only wait
+    // (__syncthreads() would also wait vmcnt(0): the h stores and the x
+    // prefetch, one global round trip every step)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  };
+  auto run = [&](auto full_c) {
+    if constexpr (PD == 1) {
+      for (int step = 0; step < maxlen; ++step) step_body(full_c, step, xa);
+    } else {
+      for (int step = 0; step < maxlen; step += 2) {
+        step_body(full_c, step, xa);
+        if (step + 1 < maxlen) step_body(full_c, step + 1, xb);
+      }
+    }
+  };
+  if constexpr (NS == 16) {  // (registers: one guarded copy of the loop)
+    run(std::false_type{});
+  } else {
+    if (b0 + NS <= B)
+      run(std::true_type{});
+    else
+      run(std::false_type{});
   }
 }
 
