@@ -30,7 +30,7 @@ aan_prep_kernel(const float* __restrict__ x, const float* __restrict__ g1, const
   const float mu = wave_sum(v.x + v.y + v.z + v.w) * (1.0f / ND_D);
   const f32x4 d = v - mu;
   const float var = wave_sum(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w) * (1.0f / ND_D);
-  const f32x4 xn = d * (1.0f / sqrtf(var + ND_LN_EPS)) * ld4(g1 + 4 * lane) + ld4(b1 + 4 * lane);
+  const f32x4 xn = d * ln_rsqrt(var + ND_LN_EPS) * ld4(g1 + 4 * lane) + ld4(b1 + 4 * lane);
   f32x4 prev = {0.f, 0.f, 0.f, 0.f};
   if (step > 0) {
     const int slot = anc ? anc[(size_t)r * anc_ld + step - 1] : r;

@@ -61,7 +61,7 @@ layernorm_kernel(const float* __restrict__ x, const float* __restrict__ g, const
   const float mu = wave_sum(v.x + v.y + v.z + v.w) * (1.0f / ND_D);
   const f32x4 d = v - mu;
   const float var = wave_sum(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w) * (1.0f / ND_D);
-  const float rs = 1.0f / sqrtf(var + ND_LN_EPS);
+  const float rs = ln_rsqrt(var + ND_LN_EPS);
   st4(out + (size_t)row * ND_D + lane * 4, d * rs * ld4(g + lane * 4) + ld4(b + lane * 4));
 }
 
@@ -410,7 +410,7 @@ __device__ __forceinline__ void merge_waves(float* accs, float* ms, float* ls, c
       ls[(wave * RPC + j) * ND_H + (lane >> 3)] = l[j];
     }
   }
-  __syncthreads();
+  lds_barrier();  // (the self-attention's cache append may still be in flight)
   for (int e = tid; e < RPC * ND_D; e += NW * 64) {
     const int j = e / ND_D, d = e % ND_D, h = d / ND_DH;
     float M = -INFINITY;
@@ -424,7 +424,7 @@ __device__ __forceinline__ void merge_waves(float* accs, float* ms, float* ls, c
       num += f * accs[((size_t)w * RPC + j) * ND_D + d];
       den += f * ls[(w * RPC + j) * ND_H + h];
     }
-    out[pk(row0 + j, d & ~3, ND_D) + (d & 3)] = den > 0.f ? num / den : 0.f;
+    out[pk(row0 + j, d & ~3, ND_D) + (d & 3)] = den > 0.f ? num * __builtin_amdgcn_rcpf(den) : 0.f;
   }
 }
 

@@ -107,6 +107,17 @@ __device__ __forceinline__ size_t pk(int m, int n, int N) {
 }
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+
+// LayerNorm 1 / sqrt(var + eps): v_rsq_f32 (1 ulp; the argument is >= eps,
+// never denormal).  1.0f / sqrtf() lowers to an IEEE sqrt plus an IEEE
+// division, ~20 dependent instructions on the path of every LN consumer.
+__device__ __forceinline__ float ln_rsqrt(float x) { return __builtin_amdgcn_rsqf(x); }
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS
+// operations, not for its outstanding global loads and stores
+// (__syncthreads() also waits vmcnt(0), which drains every prefetch in
+// flight and every store just issued).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
 
 // Split-fp16 range guard.  An activation split as hi = fp16(x), lo =

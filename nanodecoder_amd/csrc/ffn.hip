@@ -147,7 +147,7 @@ enc_ffn_kernel(const float* __restrict__ y, const uint16_t* __restrict__ w1h, fl
     }
     v2 += __shfl_xor(v2, 16, 64);
     v2 += __shfl_xor(v2, 32, 64);
-    const float rs = 1.0f / sqrtf(v2 * (1.0f / ND_D) + ND_LN_EPS);
+    const float rs = ln_rsqrt(v2 * (1.0f / ND_D) + ND_LN_EPS);
 #pragma unroll
     for (int kb = 0; kb < 8; ++kb) ff_split((ya[kb] - mu) * rs, (yb[kb] - mu) * rs, yh[g][kb], yl[g][kb]);
   }

@@ -52,7 +52,7 @@ __device__ __forceinline__ void merge_stats(const float* __restrict__ p, int P, 
     m2 += 2 * i + 1 < P ? v[i].w + w * d1 * d1 : 0.f;
   }
   mu = m;
-  rs = 1.0f / sqrtf(m2 * (1.0f / 256.0f) + ND_LN_EPS);
+  rs = ln_rsqrt(m2 * (1.0f / 256.0f) + ND_LN_EPS);
 }
 
 // --fast beam: every row of [r0, r0 + n) (rows < M) belongs to a finished
@@ -254,7 +254,7 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
           const float var = wave_sum(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w) * (1.0f / 256.0f);
           if (lane == 0) {
             s_mu[r] = mu;
-            s_rs[r] = 1.0f / sqrtf(var + ND_LN_EPS);
+            s_rs[r] = ln_rsqrt(var + ND_LN_EPS);
           }
         }
       }

@@ -151,7 +151,7 @@ dec_mem_attention_kernel(const float* __restrict__ qp, const float* __restrict__
   if (ntile > 1) put(1, R1);
   if (ntile > 2) fetch(2, R0);
   if (ntile > 3) fetch(3, R1);
-  __syncthreads();  // q' image
+  lds_barrier();  // q' image (tiles 2 and 3 stay in flight)
   if (ntile > 0) put_scores(0, scores(0));
 
   f32x4 acc[8];
@@ -257,7 +257,7 @@ dec_mem_attention_kernel(const float* __restrict__ qp, const float* __restrict__
     den += f * ml[(v * 8 + h) * 2 + 1];
     num += f * ld4(red + ((size_t)v * 512 + h * 64 + lane) * 4);
   }
-  st4(out + pk(c, h * ND_D + 4 * lane, ND_H * ND_D), num * (den > 0.f ? 1.0f / den : 0.f));
+  st4(out + pk(c, h * ND_D + 4 * lane, ND_H * ND_D), num * (den > 0.f ? __builtin_amdgcn_rcpf(den) : 0.f));
   stamp_end(stamp);
 }
 
@@ -295,7 +295,7 @@ memory_pack_kernel(const float* __restrict__ x, const float* __restrict__ g, con
       const float mu = wave_sum(v.x + v.y + v.z + v.w) * (1.0f / ND_D);
       const f32x4 d = v - mu;
       const float var = wave_sum(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w) * (1.0f / ND_D);
-      v = d * (1.0f / sqrtf(var + ND_LN_EPS)) * ld4(g + lane * 4) + ld4(b + lane * 4);
+      v = d * ln_rsqrt(var + ND_LN_EPS) * ld4(g + lane * 4) + ld4(b + lane * 4);
     }
   }
   st4(out + (size_t)row * ND_D + lane * 4, v);

@@ -29,7 +29,7 @@ __device__ __forceinline__ void head_row(const float* __restrict__ x, int row, c
   const float mu = wave_sum(v.x + v.y + v.z + v.w) * (1.0f / ND_D);
   const f32x4 d = v - mu;
   const float var = wave_sum(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w) * (1.0f / ND_D);
-  const float rs = 1.0f / sqrtf(var + ND_LN_EPS);
+  const float rs = ln_rsqrt(var + ND_LN_EPS);
   const f32x4 y = d * rs * g + bt;
   float mx = -INFINITY;
   for (int k0 = 0; k0 < V; k0 += 8) {
