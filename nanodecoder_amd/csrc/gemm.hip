@@ -36,14 +36,16 @@ __device__ __forceinline__ void merge_stats(const float* __restrict__ p, int P, 
   f32x4 v[ND_PART_LD / 2];  // {mean_2i, M2_2i, mean_2i+1, M2_2i+1}
 #pragma unroll
   for (int i = 0; i < ND_PART_LD / 2; ++i) v[i] = ld4(p + 4 * i);
-  const float w = 256.0f / (float)P;
+  // P is a power of two (the producer's column tiles, or 1): v_rcp_f32 is
+  // exact there, and no IEEE division sits on the LN consumer's path
+  const float invP = __builtin_amdgcn_rcpf((float)P), w = 256.0f * invP;
   float m = 0.f;
 #pragma unroll
   for (int i = 0; i < ND_PART_LD / 2; ++i) {
     m += 2 * i < P ? v[i].x : 0.f;
     m += 2 * i + 1 < P ? v[i].z : 0.f;
   }
-  m /= (float)P;
+  m *= invP;
   float m2 = 0.f;
 #pragma unroll
   for (int i = 0; i < ND_PART_LD / 2; ++i) {
