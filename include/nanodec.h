@@ -373,6 +373,20 @@ int nd_op_lstm_layer(const float* xp, const float* signal, const float* wih0, co
 int nd_op_memory_pack(const float* x, const float* ln_g, const float* ln_b, float* out, int32_t B, int32_t T,
                       int32_t ldT, void* stream);
 
+/* Split-fp16 memory bank (the greedy decoder's context attention at T in
+ * (448, 512]; multi_headed_attn.py:142-177 in the memory-bank form of
+ * nd_op_dec_mem_attention).  nd_op_bank_pack_h3: x [B*T, 256] row-major ->
+ * out, B x 512 rows as fp16 hi / lo planes in the v_mfma_f32_16x16x32_f16
+ * A-operand fragment order (B * 512 * 256 * 4 bytes; LayerNorm with
+ * ln_g/ln_b when set; rows t >= T zero).  nd_op_dec_bank_h3: qp [C16, 2048]
+ * P16 as nd_op_dec_mem_attention, bank from nd_op_bank_pack_h3, T in
+ * (448, 512]; out U [C16, 2048] P16.  ovf (nullable): set to 1 when an
+ * operand reaches the fp16 range (|x| >= 65504). */
+int nd_op_bank_pack_h3(const float* x, const float* ln_g, const float* ln_b, uint16_t* out, int32_t B, int32_t T,
+                       int32_t* ovf, void* stream);
+int nd_op_dec_bank_h3(const float* qp, const uint16_t* bank, const float* signal, const int32_t* span, float pad_val,
+                      float* out, int32_t C, int32_t T, int32_t* ovf, void* stream);
+
 /* Decoder context attention (multi_headed_attn.py:142-177): rows r = c*rpc+j
  * of q [C*rpc, d] attend over K at kv[(c*T+t)*ld + koff] and V at +d, keys
  * t < span[c], key mask signal == pad_val; out [C*rpc, d].  q and out are

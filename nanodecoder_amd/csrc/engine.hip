@@ -146,6 +146,7 @@ struct nd_ctx {
   float *x = nullptr, *y = nullptr, *att = nullptr, *big = nullptr, *ctxkv = nullptr;
   float* mem_p = nullptr;                 // memory bank [B * T, 256] row-major (LN'd encoder output)
   const float* mem = nullptr;             // the bank the decoder reads: mem_p, or x (NanoEncoder)
+  bool bank_h3 = false;                   // mem_p holds the split-fp16 fragment bank (dec_bank_h3_kernel)
   float *dqk = nullptr, *dU = nullptr;    // [R, 8*256] P16 (memory-bank path)
   // average self-attention step buffers (P16): xn, avg (+ its row stats), the
   // average_layer hidden, a = FFN(avg), the gate pre-activations [R, 512]
@@ -588,8 +589,12 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
     if (mb) {  // memory-bank form (attention.hip)
       const int HD = ND_H * D;
       LCHK(dg(c->dq1, D, L.pwqk, HD, D, L.bqk, c->dqk, HD).ln(c->dq1_part, pnq).run(s));
-      LCHK(nd::launch_dec_mem_attention(c->dqk, c->mem, c->sig, c->span, (float)c->cfg.pad_idx, c->dU, C, rpc, T, T,
-                                        s, stamp, dbg, dbg_stride));
+      if (c->bank_h3)
+        LCHK(nd::launch_dec_bank_h3(c->dqk, reinterpret_cast<const uint16_t*>(c->mem_p), c->sig, c->span,
+                                    (float)c->cfg.pad_idx, c->dU, C, T, s, stamp, dbg, dbg_stride, c->ovf));
+      else
+        LCHK(nd::launch_dec_mem_attention(c->dqk, c->mem, c->sig, c->span, (float)c->cfg.pad_idx, c->dU, C, rpc, T,
+                                          T, s, stamp, dbg, dbg_stride));
       LCHK(dg(c->dU, HD, L.pwvo, D, HD, L.bvo, c->dmid, D).res(c->dq1, D).stats(c->dmid_part).run(s, &pnm));
     } else {
       LCHK(dg(c->dq1, D, L.pcwq, D, D, L.ncbq, c->dcq, D).ln(c->dq1_part, pnq).run(s));
@@ -606,8 +611,18 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
 // The decoder's view of the encoder output: the memory bank (greedy) or the
 // per-layer context K/V (beam).
 static hipError_t enqueue_memory(nd_ctx* c, int B, int T, int rpc, hipStream_t s) {
+  c->bank_h3 = false;
   if (!use_memory_bank(c, rpc)) return enqueue_ctxkv(c, B, T, s);
-  if (c->cfg.encoder_type != ND_ENC_TRANSFORMER) {  // the NanoEncoder's output is the bank as it stands
+  const bool tf = c->cfg.encoder_type == ND_ENC_TRANSFORMER;
+  if (!c->exact && nd::bank_h3_eligible(T, c->cfg.max_src_len)) {
+    // 512-sample chunks: the split-fp16 fragment bank (LN'd for the transformer,
+    // the NanoEncoder's output as it stands)
+    c->bank_h3 = true;
+    c->mem = c->mem_p;
+    return nd::launch_bank_pack_h3(c->x, tf ? c->enc_ln_g : nullptr, tf ? c->enc_ln_b : nullptr,
+                                   reinterpret_cast<uint16_t*>(c->mem_p), B, T, c->ovf, s);
+  }
+  if (!tf) {  // the NanoEncoder's output is the bank as it stands
     c->mem = c->x;
     return hipSuccess;
   }
@@ -1121,7 +1136,7 @@ static int translate_beam(nd_ctx* c, const float* d_signal, const int32_t* d_len
   rc = run_graph(c, k0, [&](hipStream_t s) -> hipError_t {
     if (c->kstamp_on) LCHK(nd::launch_stamp_reset(c->kstamp, (int)c->dec.size() * c->cfg.max_steps, s));
     LCHK(enqueue_encode(c, B, T, s));
-    LCHK(enqueue_ctxkv(c, B, T, s));
+    LCHK(enqueue_memory(c, B, T, beam, s));  // K/V per layer (memory bank at beam 1)
     LCHK(nd::launch_beam_init(c->bs, B, beam, n_best, max_len, c->cfg.bos_idx, s));
     LCHK(enqueue_first_embed(c, B * beam, s));
     LCHK(nd::launch_fill_i32(c->steps_done, max_len, 1, s));
@@ -1235,7 +1250,7 @@ static int translate_classic(nd_ctx* c, const float* d_signal, const int32_t* d_
   rc = run_graph(c, k0, [&](hipStream_t s) -> hipError_t {
     if (c->kstamp_on) LCHK(nd::launch_stamp_reset(c->kstamp, (int)c->dec.size() * c->cfg.max_steps, s));
     LCHK(enqueue_encode(c, B, T, s));
-    LCHK(enqueue_ctxkv(c, B, T, s));
+    LCHK(enqueue_memory(c, B, T, beam, s));  // K/V per layer (memory bank at beam 1)
     LCHK(nd::launch_beam_classic_init(c->bs, c->group_in, B, beam, c->cfg.bos_idx, s));
     LCHK(enqueue_first_embed(c, B * beam, s));
     LCHK(nd::launch_fill_i32(c->steps_done, max_len, 1, s));
@@ -1551,6 +1566,24 @@ int nd_op_memory_pack(const float* x, const float* ln_g, const float* ln_b, floa
                       int32_t ldT, void* stream) {
   hipError_t e = nd::launch_memory_pack(x, ln_g, ln_b, out, B, T, ldT, (hipStream_t)stream);
   if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("memory_pack: ") + hipGetErrorString(e));
+  return ND_OK;
+}
+
+int nd_op_bank_pack_h3(const float* x, const float* ln_g, const float* ln_b, uint16_t* out, int32_t B, int32_t T,
+                       int32_t* ovf, void* stream) {
+  if (!x || !out || (ln_g == nullptr) != (ln_b == nullptr)) return fail(ND_ERR_ARG, "bank_pack_h3: bad arguments");
+  hipError_t e = nd::launch_bank_pack_h3(x, ln_g, ln_b, out, B, T, ovf, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("bank_pack_h3: ") + hipGetErrorString(e));
+  return ND_OK;
+}
+
+int nd_op_dec_bank_h3(const float* qp, const uint16_t* bank, const float* signal, const int32_t* span, float pad_val,
+                      float* out, int32_t C, int32_t T, int32_t* ovf, void* stream) {
+  if (int rc = ensure_attributes()) return rc;
+  if (!qp || !bank || !signal || !span || !out) return fail(ND_ERR_ARG, "dec_bank_h3: bad arguments");
+  hipError_t e = nd::launch_dec_bank_h3(qp, bank, signal, span, pad_val, out, C, T, (hipStream_t)stream, nullptr,
+                                        nullptr, 0, ovf);
+  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("dec_bank_h3: ") + hipGetErrorString(e));
   return ND_OK;
 }
 

@@ -261,6 +261,323 @@ dec_mem_attention_kernel(const float* __restrict__ qp, const float* __restrict__
   stamp_end(stamp);
 }
 
+// ---------------------------------------------------------------------------
+// Split-fp16 form (T in (448, 512] with 512-row bank buffers: every bench and
+// translate batch of 512-sample chunks).  The kernel above runs both
+// products on fp32 4x4x1 MFMAs (8192 per chunk, ~9 us of matrix-core time per
+// CU) and stages every bank tile through LDS three times; its compute side
+// alone takes ~22 us against a ~17-20 us bank stream.  Here:
+//  - the bank is packed ONCE per call (bank_pack_h3_kernel) as fp16 hi / lo
+//    planes in the A-operand fragment order of v_mfma_f32_16x16x32_f16:
+//    fragment (chunk, key block kb of 16 keys, dim block db of 32, plane) is
+//    1 KB, lane l holding key 16 kb + (l & 15), dims 32 db + 8 (l >> 4) .. +7.
+//    Same 4 bytes per element as fp32; every wave load is one coalesced 1 KB.
+//  - S = M Q'^T straight from the load registers: B = q' with its 16 columns
+//    [q'_hi of heads 0-7 | q'_lo of heads 0-7], so A_hi B + A_lo B holds all
+//    four split products of a head in columns h and h + 8 (one DPP add):
+//    16 MFMAs per 16 keys.
+//  - U = P^T M on v_mfma_f32_16x16x16_f16 with A = [P_hi | P_lo] (rows =
+//    heads, k = keys): the S accumulator hands every lane exactly its A
+//    operand (4 keys of its column's head), so P never moves.  B = the key
+//    block transposed: the fragments are written once to a per-wave 16 KB
+//    LDS image [plane][dim block k of 16][16 keys][16 dims] and read back by
+//    ds_read_b64_tr_b16.  A key's 32-byte row holds two 16-byte halves,
+//    swapped on rows with bit 2 set: the transposed reads of a 32-lane half
+//    cover 256 contiguous bytes (conflict-free), the b128 stores of 8 rows
+//    hit 8 distinct bank groups, and every address is a per-lane base plus a
+//    compile-time offset (no per-block address registers).  32 MFMAs per 16
+//    keys; 64 fp32 accumulators (rows 0-7 P_hi, 8-15 P_lo, summed at the
+//    end).  The fragments load through a buffer descriptor: one offset
+//    register for every load (a register spill in this loop is a vmcnt(0)
+//    drain of every prefetch in flight).
+//  - Online softmax with a lazy maximum: p = exp(s - m) <= e^6 and P is
+//    split at 2^7 (< 65504; its lo plane out of the fp16 subnormals down to
+//    p ~ 5e-7); U and l are rescaled (4 shuffles + 64 multiplies, a
+//    wave-uniform branch) only when a head's block maximum exceeds m by
+//    more than 6.
+//  - One workgroup of 8 waves (two per SIMD) per chunk, wave w owning keys
+//    [64 w, 64 w + 64) = 4 key blocks; loads run in half blocks (8 fragments,
+//    4 dim blocks x 2 planes), two half blocks ahead of the one computed;
+//    the 8 waves' (m, l, U) merge through LDS at the end.
+// Matrix-core time per CU: 64 x 16 + 128 x 8 cycles per wave, ~1.8 us.
+#define BH_NW 8                          // waves per chunk (64 keys each)
+#define BH_KB 32                         // key blocks per chunk (512 keys)
+#define BH_THR 6.0f                      // lazy-rescale threshold (natural log units)
+#define BH_PSCALE 128.0f                 // P split at 2^7
+#define BH_IMG 16384                     // bytes: one wave's transposed image (2 planes x 16 keys x 512 B)
+#define BH_ML (BH_NW * BH_IMG)           // merge (m, l) [wave][8 heads][2] floats, behind the images
+#define BH_LDS (BH_ML + BH_NW * 16 * 4)
+static_assert(BH_NW * ND_H * ND_D * 4 <= BH_ML, "merge image overlaps (m, l)");
+
+typedef _Float16 bh4 __attribute__((ext_vector_type(4)));
+typedef _Float16 bh8 __attribute__((ext_vector_type(8)));
+typedef short bs4 __attribute__((vector_size(8)));
+typedef __attribute__((address_space(3))) bs4 lds_bs4;
+
+__device__ __forceinline__ f32x4 mfma_h32(bh8 a, bh8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma_h16(bh4 a, bh4 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c, 0, 0, 0);
+}
+// byte offset of the 16-byte half hf (dims 8 hf .. +7 of a 16-dim block) of
+// key row r in a dim block of one plane of the transposed image
+__device__ __forceinline__ int bh_row(int r, int hf) { return 32 * r + 16 * (hf ^ ((r >> 2) & 1)); }
+
+__global__ void __launch_bounds__(BH_NW * 64)
+dec_bank_h3_kernel(const float* __restrict__ qp, const f32x4* __restrict__ bank, const float* __restrict__ signal,
+                   const int* __restrict__ span, float pad_val, float* __restrict__ out, int T,
+                   unsigned long long* stamp, float* __restrict__ dbg, size_t dbg_stride, int* ovf) {
+  stamp_begin(stamp);
+  extern __shared__ float lds[];
+  const int c = blockIdx.x, lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int L = min(span[c], T);
+  const int col = lane & 15, g = lane >> 4;
+  char* img = reinterpret_cast<char*>(lds) + w * BH_IMG;  // [plane][dim block][16 keys][32 B]
+  // this wave's fragments: key blocks 4w .. 4w + 3 (64 KB from the descriptor base)
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<f32x4*>(bank + ((size_t)c * BH_KB + 4 * w) * 8 * 2 * 64), 0, 65536, 0x00020000);
+  const int voff = lane * 16;
+
+  // half block h (0..7): key block 4w + (h >> 1), dim blocks 4 (h & 1) .. +3, both planes
+  auto hload = [&](int h, f32x4(&f)[8]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      f[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                           rsrc, voff, ((h >> 1) * 16 + 8 * (h & 1) + i) * 1024, 0));
+  };
+  // this lane's image addresses: write (row col, dim block 2 db + (g >> 1), half g & 1);
+  // transposed read (row 4g + q, dims 4p .. 4p + 3 of a dim block)
+  char* wimg = img + 512 * (g >> 1) + bh_row(col, g & 1);
+  const int q4 = (lane >> 2) & 3, p4 = lane & 3;
+  const char* rimg = img + bh_row(4 * g + q4, p4 >> 1) + 8 * (p4 & 1);
+  // q' and the signal load FIRST, then three half blocks: the wait that
+  // retires q' (for its split) leaves all 24 bank loads in flight
+  f32x4 qv[8][2];
+  const int hd = col & 7;
+#pragma unroll
+  for (int db = 0; db < 8; ++db) {
+    const int d0 = hd * ND_D + 32 * db + 8 * g;
+    qv[db][0] = ld4(qp + pk(c, d0, ND_H * ND_D));
+    qv[db][1] = ld4(qp + pk(c, d0 + 4, ND_H * ND_D));
+  }
+  const float sg = signal[(size_t)c * T + min(64 * w + lane, T - 1)];
+  f32x4 F[3][8];
+  hload(0, F[0]);
+  hload(1, F[1]);
+  hload(2, F[2]);
+  __builtin_amdgcn_sched_barrier(0);  // every load issued before the q' split waits on q'
+  // q' as the B operand: column col = (plane col >> 3, head col & 7), dims 32 db + 8 g .. +7
+  bh8 qb[8];
+  {
+    float amax = 0.f;
+#pragma unroll
+    for (int db = 0; db < 8; ++db) {
+      amax = fmaxf(amax, fmaxf(absmax4(qv[db][0]), absmax4(qv[db][1])));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float x = qv[db][j >> 2][j & 3];
+        const _Float16 hi = (_Float16)x;
+        qb[db][j] = col < 8 ? hi : (_Float16)(x - (float)hi);
+      }
+    }
+    flag_overflow(ovf, amax);
+  }
+  const unsigned long long padm = __ballot(sg == pad_val);
+
+  f32x4 ua[16];  // U^T... rows 4g + i = (P plane, head), column col of dim block: lane holds rows 4g .. 4g + 3
+#pragma unroll
+  for (int k = 0; k < 16; ++k) ua[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;  // head col & 7 (l: this lane's keys)
+
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb) {
+    f32x4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = d0;
+#pragma unroll
+    for (int part = 0; part < 2; ++part) {
+      const int h = 2 * kb + part;
+      f32x4(&f)[8] = F[h % 3];
+      // ---- S partial over dim blocks 4 part .. +3: D[key 4g + i][col]
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        d0 = mfma_h32(__builtin_bit_cast(bh8, f[2 * i]), qb[4 * part + i], d0);
+        d1 = mfma_h32(__builtin_bit_cast(bh8, f[2 * i + 1]), qb[4 * part + i], d1);
+      }
+      // ---- the fragments into the transposed image: dims 32 db + 8 g .. +7 of key col
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int db = 4 * part + (i >> 1), pl = i & 1;
+        *reinterpret_cast<f32x4*>(wimg + pl * 8192 + 1024 * db) = f[i];
+      }
+      __builtin_amdgcn_sched_barrier(0);  // the next loads reuse f's registers
+      if (h + 3 < 8) hload(h + 3, F[h % 3]);
+    }
+    // ---- scores: columns h and h + 8 hold the hi and lo halves of q'_h
+    f32x4 s = d0 + d1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s[i] += dpp_mov<ND_DPP_ROR8>(s[i]);
+    const int kbase = 64 * w + 16 * kb + 4 * g;  // key of row i: kbase + i
+    const unsigned pb = (unsigned)(padm >> (16 * kb + 4 * g)) & 0xFu;
+    float gm = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      s[i] = kbase + i < L ? (((pb >> i) & 1u) ? ND_MASK_FILL : s[i]) : -INFINITY;
+      gm = fmaxf(gm, s[i]);
+    }
+    if (dbg && col == 0) {  // -attn_debug: head 0's scores
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (kbase + i < L) dbg[(size_t)c * dbg_stride + kbase + i] = s[i];
+    }
+    gm = xor32_max(xor16_max(gm));
+    if (__any(gm > m + BH_THR)) {
+      const float nm = fmaxf(m, gm);
+      const float sc = nm == m ? 1.f : __expf(m - nm);
+      m = nm;
+      l *= sc;
+      // U row 4g + i belongs to head 4 (g & 1) + i: that column's scale
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float si = __shfl(sc, (lane & 48) | (4 * (g & 1) + i));
+#pragma unroll
+        for (int k = 0; k < 16; ++k) ua[k][i] *= si;
+      }
+    }
+    f32x4 p;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) p[i] = s[i] == -INFINITY ? 0.f : __expf(s[i] - m);
+    l += (p[0] + p[1]) + (p[2] + p[3]);
+    // ---- A operand of U: row col = (plane col >> 3, head col & 7), keys 4g .. 4g + 3
+    bh4 pa;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float x = p[i] * BH_PSCALE;
+      const _Float16 hi = (_Float16)x;
+      pa[i] = col < 8 ? hi : (_Float16)(x - (float)hi);
+    }
+    // ---- U += P^T M: B = key rows 4g + q, dims 16 k + col (transposed reads)
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+#pragma unroll
+      for (int pl = 0; pl < 2; ++pl) {
+        const bs4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bs4*)(rimg + pl * 8192 + 512 * k));
+        ua[k] = mfma_h16(pa, __builtin_bit_cast(bh4, b), ua[k]);
+      }
+  }
+
+  // ---- rows 4g + i: g 0, 1 = P_hi of heads 4g + i, g 2, 3 = P_lo of the same heads.
+  //      permlane32 swap-add of dim-block pairs (2j, 2j + 1): lanes < 32 end with
+  //      block 2j, lanes >= 32 with block 2j + 1, both for heads 4 (g & 1) + i
+  f32x4 u8[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      // unscale first: a VALU op the compiler sees between the MFMA results and
+      // the swap (inline asm gets no MFMA -> VALU wait states of its own)
+      float a = ua[2 * j][i] * (1.0f / BH_PSCALE), b = ua[2 * j + 1][i] * (1.0f / BH_PSCALE);
+      asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+      u8[j][i] = a + b;
+    }
+  l = xor32_sum(xor16_sum(l));  // over the 4 key rows of the column's head
+
+  // ---- merge the 8 waves
+  __syncthreads();  // every wave is done with its image (the merge image overlays them)
+  float* red = lds;                         // [wave][8 heads][256]
+  float* ml = lds + BH_ML / 4;              // [wave][8 heads][2]
+  {
+    const int hb = 4 * (g & 1), dsel = lane >> 5;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[(w * ND_H + hb + i) * ND_D + 16 * (2 * j + dsel) + col] = u8[j][i];
+  }
+  if (lane < 8) {
+    ml[(w * ND_H + lane) * 2] = m;
+    ml[(w * ND_H + lane) * 2 + 1] = l;
+  }
+  __syncthreads();
+  const int oh = threadIdx.x >> 6, o0 = 4 * (threadIdx.x & 63);
+  float M = -INFINITY;
+#pragma unroll
+  for (int v = 0; v < BH_NW; ++v) M = fmaxf(M, ml[(v * ND_H + oh) * 2]);
+  f32x4 num = {0.f, 0.f, 0.f, 0.f};
+  float den = 0.f;
+#pragma unroll
+  for (int v = 0; v < BH_NW; ++v) {
+    const float mv = ml[(v * ND_H + oh) * 2];
+    const float f = mv == -INFINITY ? 0.f : __expf(mv - M);  // waves that owned no key
+    den += f * ml[(v * ND_H + oh) * 2 + 1];
+    num += f * ld4(red + (v * ND_H + oh) * ND_D + o0);
+  }
+  st4(out + pk(c, oh * ND_D + o0, ND_H * ND_D), num * (den > 0.f ? __builtin_amdgcn_rcpf(den) : 0.f));
+  stamp_end(stamp);
+}
+
+// Encoder output -> the split-fp16 fragment bank of dec_bank_h3_kernel: one
+// workgroup per (chunk, key block of 16 rows): LayerNorm (as
+// memory_pack_kernel) into LDS, then the 16 fragments (8 dim blocks x hi /
+// lo) written as coalesced 1 KB blocks.  Rows t >= T are zero.
+__global__ void __launch_bounds__(256)
+bank_pack_h3_kernel(const float* __restrict__ x, const float* __restrict__ g, const float* __restrict__ b,
+                    uint16_t* __restrict__ out, int T, int* ovf) {
+  __shared__ float rows[16 * ND_D];
+  const int c = blockIdx.x / BH_KB, kb = blockIdx.x % BH_KB, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int r = wv + 4 * rr, t = 16 * kb + r;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (t < T) {
+      v = ld4(x + ((size_t)c * T + t) * ND_D + lane * 4);
+      if (g) {
+        const float mu = wave_sum(v.x + v.y + v.z + v.w) * (1.0f / ND_D);
+        const f32x4 d = v - mu;
+        const float var = wave_sum(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w) * (1.0f / ND_D);
+        v = d * ln_rsqrt(var + ND_LN_EPS) * ld4(g + lane * 4) + ld4(b + lane * 4);
+      }
+    }
+    st4(rows + r * ND_D + lane * 4, v);
+  }
+  __syncthreads();
+  float amax = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int item = threadIdx.x + 256 * j, fr = item >> 6, ln = item & 63, db = fr >> 1, pl = fr & 1;
+    const float* src = rows + (ln & 15) * ND_D + 32 * db + 8 * (ln >> 4);
+    const f32x4 v0 = ld4(src), v1 = ld4(src + 4);
+    amax = fmaxf(amax, fmaxf(absmax4(v0), absmax4(v1)));
+    bh8 o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float v = k < 4 ? v0[k] : v1[k - 4];
+      const _Float16 hi = (_Float16)v;
+      o[k] = pl == 0 ? hi : (_Float16)(v - (float)hi);
+    }
+    *reinterpret_cast<bh8*>(out + ((((size_t)c * BH_KB + kb) * 8 + db) * 2 + pl) * 512 + ln * 8) = o;
+  }
+  flag_overflow(ovf, amax);
+}
+
+bool bank_h3_eligible(int T, int ldT) { return T > 448 && T <= 512 && ldT >= 512; }
+
+hipError_t launch_bank_pack_h3(const float* x, const float* ln_g, const float* ln_b, uint16_t* out, int B, int T,
+                               int* ovf, hipStream_t s) {
+  if (T < 1 || T > 512 || B < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(bank_pack_h3_kernel, dim3(B * BH_KB), dim3(256), 0, s, x, ln_g, ln_b, out, T, ovf);
+  return hipGetLastError();
+}
+
+hipError_t launch_dec_bank_h3(const float* qp, const uint16_t* bank, const float* signal, const int* span,
+                              float pad_val, float* out, int C, int T, hipStream_t s, unsigned long long* stamp,
+                              float* attn_dbg, size_t dbg_stride, int* ovf) {
+  if (T < 1 || T > 512 || C < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(dec_bank_h3_kernel, dim3(C), dim3(BH_NW * 64), BH_LDS, s, qp,
+                     reinterpret_cast<const f32x4*>(bank), signal, span, pad_val, out, T, stamp, attn_dbg,
+                     dbg_stride, ovf);
+  return hipGetLastError();
+}
+
 static constexpr size_t mem_lds_bytes() { return (size_t)MB_LDS_FLOATS * sizeof(float); }
 static_assert(MB_LDS_FLOATS * 4 <= 160 * 1024, "LDS");
 static_assert(MB_NW * 512 * 4 <= MB_U, "merge slots overlap the q' image");
@@ -351,7 +668,7 @@ hipError_t init_mem_attributes() {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mem_lds_bytes());
     if (e != hipSuccess) return e;
   }
-  return hipSuccess;
+  return hipFuncSetAttribute((const void*)dec_bank_h3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, BH_LDS);
 }
 
 }  // namespace nd

@@ -423,6 +423,28 @@ def op_dec_mem_attention(qp, mem_p, signal, span, pad_val, rpc, out=None):
     return out
 
 
+def op_bank_pack_h3(x, B, T, ln_g=None, ln_b=None, ovf=None):
+    """Split-fp16 fragment bank (nd_op_bank_pack_h3): x [B*T, 256] -> uint16
+    [B * 512 * 512] (hi / lo planes of 512 rows per chunk)."""
+    out = torch.empty(B * 512 * 512, dtype=torch.int16, device=x.device)
+    s = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+    _lib.check(_lib.lib().nd_op_bank_pack_h3(_ptr(x), _ptr(ln_g), _ptr(ln_b), _ptr(out), B, T, _ptr(ovf), s),
+               "nd_op_bank_pack_h3")
+    return out
+
+
+def op_dec_bank_h3(qp, bank, signal, span, pad_val, out=None, ovf=None):
+    """Memory-bank context attention on the split-fp16 bank (nd_op_dec_bank_h3):
+    qp [R16, 2048] packed, T in (448, 512]; returns U [R16, 2048] packed."""
+    C, T = signal.shape
+    if out is None:
+        out = torch.empty(qp.shape[0], qp.shape[1], dtype=torch.float32, device=qp.device)
+    s = ctypes.c_void_p(torch.cuda.current_stream(qp.device).cuda_stream)
+    _lib.check(_lib.lib().nd_op_dec_bank_h3(_ptr(qp), _ptr(bank), _ptr(signal), _ptr(span), float(pad_val),
+                                            _ptr(out), C, T, _ptr(ovf), s), "nd_op_dec_bank_h3")
+    return out
+
+
 def op_lstm_layer(whh, lens, T, xp=None, signal=None, wih0=None, bsum=None, bn_scale=None, bn_shift=None,
                   out=None):
     """One BiLSTM layer (both directions) through nd_op_lstm_layer:

@@ -261,6 +261,53 @@ def test_mem_attention_vs_fp64(T):
             assert err < 2e-5, (c, h, L, err)
 
 
+@pytest.mark.parametrize("T,ln", [(512, True), (480, False), (449, True)])
+def test_bank_h3_vs_fp64(T, ln):
+    """Split-fp16 memory-bank attention (bank_pack_h3 + dec_bank_h3_kernel, the
+    greedy path at 512-sample chunks) against an fp64 softmax(q' M^T) M per
+    head: ragged spans (key-block / wave boundaries, single key, waves owning
+    no key), pad-masked keys, an all-masked chunk, a peaked chunk whose scores
+    climb past the lazy-rescale threshold, with and without the LayerNorm."""
+    from nanodecoder_amd.engine import op_bank_pack_h3, op_dec_bank_h3, pack_p16, unpack_p16
+    rng = np.random.default_rng(7)
+    C, PAD = 12, 1.0
+    spans = np.array([T, 1, 64, 65, 16, 17, 8, T, T - 3, 130, 300, T], np.int32)
+    sig = rng.standard_normal((C, T)).astype(np.float32)
+    sig[2, ::5] = PAD                      # pad-masked keys
+    sig[7, :] = PAD                        # every key masked -> uniform over the span
+    x = rng.standard_normal((C * T, 256)).astype(np.float32)
+    q = (rng.standard_normal((C, 2048)) * 0.3).astype(np.float32)
+    q[11] *= 8.0                           # scores spread ~+-50: running-maximum rescales
+    x[11 * T + 400] *= 4.0                 # a late key far above the first blocks' maximum
+    g = (rng.random(256) + 0.5).astype(np.float32)
+    b = (rng.standard_normal(256) * 0.1).astype(np.float32)
+    dev = torch.device("cuda", 0)
+    xt = torch.from_numpy(x).to(dev)
+    ovf = torch.zeros(1, dtype=torch.int32, device=dev)
+    if ln:
+        bank = op_bank_pack_h3(xt, C, T, torch.from_numpy(g).to(dev), torch.from_numpy(b).to(dev), ovf=ovf)
+        mu = x.mean(1, keepdims=True)
+        var = ((x - mu) ** 2).mean(1, keepdims=True)
+        xm = ((x - mu) / np.sqrt(var + 1e-6) * g + b).astype(np.float64)
+    else:
+        bank = op_bank_pack_h3(xt, C, T, ovf=ovf)
+        xm = x.astype(np.float64)
+    out = op_dec_bank_h3(pack_p16(torch.from_numpy(q).to(dev)), bank, torch.from_numpy(sig).to(dev),
+                         torch.from_numpy(spans).to(dev), PAD, ovf=ovf)
+    got = unpack_p16(out, C).cpu().numpy()
+    assert int(ovf.item()) == 0
+    for c in range(C):
+        L = int(spans[c])
+        M = xm[c * T: c * T + L]
+        for h in range(8):
+            s = M @ q[c, h * 256:(h + 1) * 256].astype(np.float64)
+            s[sig[c, :L] == PAD] = -1e18
+            p = np.exp(s - s.max())
+            want = (p / p.sum()) @ M
+            err = np.abs(got[c, h * 256:(h + 1) * 256] - want).max()
+            assert err < 2e-5 * max(1.0, np.abs(want).max()), (c, h, L, err)
+
+
 # ----------------------------------------------------------------- golden
 @pytest.mark.parametrize("name", ["transformer_greedy", "transformer_pe_short", "nano_greedy"])
 def test_encoder_memory_vs_golden(name):

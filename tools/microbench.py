@@ -119,6 +119,10 @@ if ONLY == "mem":
         us = timeit(lambda: E.op_dec_mem_attention(qp, memp, sig, span, 1.0, 1))
         print(f"mem-attn C={C:4d} T={T}: {us:8.2f} us  {C * T * 256 * 4 / (us * 1e-6) / 1e9:7.1f} GB/s  "
               f"{2 * 2 * 8 * C * T * 256 / (us * 1e-6) / 1e12:6.1f} TF/s (algorithmic, 8 heads)")
+        if T == 512:  # the split-fp16 fragment bank (the greedy path at 512-sample chunks)
+            bank = E.op_bank_pack_h3(torch.randn(C * T, 256, device=dev), C, T)
+            us = timeit(lambda: E.op_dec_bank_h3(qp, bank, sig, span, 1.0))
+            print(f"bank-h3  C={C:4d} T={T}: {us:8.2f} us  {C * T * 256 * 4 / (us * 1e-6) / 1e9:7.1f} GB/s")
     sys.exit(0)
 if ONLY == "dec256":
     # decoder-step shapes on the engine's P16 layout (greedy R=256, beam R=1280)

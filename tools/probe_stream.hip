@@ -7,12 +7,15 @@
 // chunk.  Build: hipcc -O3 --offload-arch=gfx950 tools/probe_stream.hip -o tools/probe_stream
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <cstdlib>
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); return 1; } } while (0)
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 // SPLIT workgroups per chunk, each over T / SPLIT consecutive rows
 template <int NW, int KW, int DEPTH, int SPLIT>
 __global__ void __launch_bounds__(NW * 64) stream(const float* __restrict__ mem, float* out, int T) {
+  extern __shared__ float lds_pad[];  // PROBE_LDS: dynamic LDS per workgroup (occupancy as the attention kernels)
+  if (T < 0) lds_pad[threadIdx.x] = 0.f;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x / SPLIT, part = blockIdx.x % SPLIT;
   const int rows = T / SPLIT, tile = NW * KW, nt = rows / tile;
@@ -40,16 +43,27 @@ __global__ void __launch_bounds__(NW * 64) stream(const float* __restrict__ mem,
   if (acc.x + acc.y + acc.z + acc.w == 12345.f) out[threadIdx.x] = acc.x;
 }
 
+__global__ void fill_random(unsigned* p, size_t n) {
+  for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+    unsigned x = (unsigned)i * 2654435761u + 12345u;
+    x ^= x >> 13;
+    x *= 0x5bd1e995u;
+    p[i] = (x & 0x807FFFFFu) | 0x3F000000u;  // finite floats in [0.5, 1) with random sign
+  }
+}
+
 template <int NW, int KW, int DEPTH, int SPLIT>
 int run(const char* name, const float* mem, float* out, int C, int T) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((stream<NW, KW, DEPTH, SPLIT>), dim3(C * SPLIT), dim3(NW * 64), 0, 0, mem, out, T);
+  const int lb = getenv("PROBE_LDS") ? atoi(getenv("PROBE_LDS")) : 0;
+  CK(hipFuncSetAttribute((const void*)stream<NW, KW, DEPTH, SPLIT>, hipFuncAttributeMaxDynamicSharedMemorySize, lb));
+  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((stream<NW, KW, DEPTH, SPLIT>), dim3(C * SPLIT), dim3(NW * 64), lb, 0, mem, out, T);
   CK(hipDeviceSynchronize());
   const int n = 50;
   CK(hipEventRecord(e0));
-  for (int i = 0; i < n; ++i) hipLaunchKernelGGL((stream<NW, KW, DEPTH, SPLIT>), dim3(C * SPLIT), dim3(NW * 64), 0, 0, mem, out, T);
+  for (int i = 0; i < n; ++i) hipLaunchKernelGGL((stream<NW, KW, DEPTH, SPLIT>), dim3(C * SPLIT), dim3(NW * 64), lb, 0, mem, out, T);
   CK(hipEventRecord(e1));
   CK(hipEventSynchronize(e1));
   float ms;
@@ -65,6 +79,11 @@ int main() {
   CK(hipMalloc(&mem, (size_t)Cmax * T * 1024));
   CK(hipMalloc(&out, 4096));
   CK(hipMemset(mem, 0, (size_t)Cmax * T * 1024));
+  if (getenv("PROBE_RANDOM")) {  // random bits instead of zeros (zero lines may stream faster)
+    hipLaunchKernelGGL(fill_random, dim3(4096), dim3(256), 0, 0, reinterpret_cast<unsigned*>(mem),
+                       (size_t)Cmax * T * 256);
+    CK(hipDeviceSynchronize());
+  }
   for (int C : {64, 256, 512}) {
     run<8, 8, 2, 1>("nw8 kw8 depth2 (engine-like)", mem, out, C, T);
     run<8, 8, 4, 1>("nw8 kw8 depth4", mem, out, C, T);
