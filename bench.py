@@ -245,11 +245,12 @@ def kernel_roofline(eng, B, mode, beam, encoder="transformer", alive=None):
     (first workgroup start, last workgroup end; Engine.set_kernel_stamps), and
     the mean over the last timed call's launches is the launch duration.
 
-    greedy: the memory-bank context attention (dec_mem_attention_kernel),
-      bounded by HBM: per launch it streams the B x 512 x 256 f32 memory bank
-      once (+ q' in, U out, the signal for the key mask).  Its MFMA view
-      (2 products x 2 x 8 heads x 512 keys x 256 dims per chunk, on
-      v_mfma_f32_4x4x1_16b) is reported beside it.
+    greedy: the memory-bank context attention (dec_bank_h3_kernel at
+      512-sample chunks), bounded by HBM: per launch it streams the B x 512 x
+      256 memory bank once (fp16 hi/lo planes, 4 bytes per element as fp32;
+      + q' in, U out, the signal for the key mask).  Its MFMA view (2
+      products x 2 x 8 heads x 512 keys x 256 dims per chunk, split-fp16 on
+      fp16 MFMAs) is reported beside it.
     beam: the per-layer K/V context attention (dec_ctx_attention_kernel),
       HBM-bound: K+V 2 x 512 keys x 256 f32 per chunk + q, signal, out, for
       the chunks still in the decode loop (finished chunks' workgroups exit
@@ -259,12 +260,14 @@ def kernel_roofline(eng, B, mode, beam, encoder="transformer", alive=None):
     T, D = 512, 256
     ms = us * 1e-3
     if mode == "greedy":
-        name = "dec_mem_attention_kernel<8>"
+        # 512-sample chunks run the split-fp16 form (dec_bank_h3_kernel: the bank as
+        # fp16 hi/lo fragments, same 4 bytes per element); exact fp32 runs the other
+        name = "dec_bank_h3_kernel" if T == 512 else "dec_mem_attention_kernel<8>"
         nbytes = B * T * D * 4 + B * T * 4 + 2 * B * 8 * D * 4
         flops = 2 * 2 * 8 * T * D * B
         tf = flops / (ms * 1e-3) / 1e12
-        extra = {"mfma_view": {"algorithmic_flops_per_launch": flops, "achieved": round(tf, 2), "peak": FP32_PEAK,
-                               "unit": "TFLOP/s", "frac": round(tf / FP32_PEAK, 4)}}
+        extra = {"mfma_view": {"algorithmic_flops_per_launch": flops, "achieved": round(tf, 2), "peak": round(SPLIT_PEAK, 1),
+                               "unit": "TFLOP/s fp32-equivalent (split-fp16 on fp16 MFMA)", "frac": round(tf / SPLIT_PEAK, 4)}}
     else:
         name = f"dec_ctx_attention_kernel<{beam}>"
         per_chunk = T * 2 * D * 4 + T * 4 + 2 * beam * D * 4

@@ -304,9 +304,22 @@ dec_mem_attention_kernel(const float* __restrict__ qp, const float* __restrict__
 #define BH_KB 32                         // key blocks per chunk (512 keys)
 #define BH_THR 6.0f                      // lazy-rescale threshold (natural log units)
 #define BH_PSCALE 128.0f                 // P split at 2^7
+#ifndef BH_AHEAD
+#define BH_AHEAD 1                       // half blocks in flight beyond the one computed (2: slower)
+#endif
+#ifndef BH_INTERLEAVE
+#define BH_INTERLEAVE 1                  // key blocks w + 8 kb (1) or 4 w + kb (0)
+#endif
+#ifndef BH_GLOBAL
+#define BH_GLOBAL 0
+#endif
+#ifndef BH_EXPT
+#define BH_EXPT 0                        // timing probes only (bit 0 no U, 1 no S, 2 no image writes, 3 no softmax)
+#endif
 #define BH_IMG 16384                     // bytes: one wave's transposed image (2 planes x 16 keys x 512 B)
 #define BH_ML (BH_NW * BH_IMG)           // merge (m, l) [wave][8 heads][2] floats, behind the images
-#define BH_LDS (BH_ML + BH_NW * 16 * 4)
+#define BH_Q (BH_ML + BH_NW * 16 * 4)    // q' image [8 heads][260] floats
+#define BH_LDS (BH_Q + ND_H * 260 * 4)
 static_assert(BH_NW * ND_H * ND_D * 4 <= BH_ML, "merge image overlaps (m, l)");
 
 typedef _Float16 bh4 __attribute__((ext_vector_type(4)));
@@ -336,38 +349,56 @@ dec_bank_h3_kernel(const float* __restrict__ qp, const f32x4* __restrict__ bank,
   const int col = lane & 15, g = lane >> 4;
   char* img = reinterpret_cast<char*>(lds) + w * BH_IMG;  // [plane][dim block][16 keys][32 B]
   // this wave's fragments: key blocks 4w .. 4w + 3 (64 KB from the descriptor base)
+#if BH_INTERLEAVE
+  // key block kb of this wave = w + 8 kb: the 8 waves stream one contiguous 128 KB window per step
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<f32x4*>(bank + (size_t)c * BH_KB * 8 * 2 * 64), 0,
+                                                      BH_KB * 16384, 0x00020000);
+  const int kb0 = w, kbs = 8;
+#else
   const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<f32x4*>(bank + ((size_t)c * BH_KB + 4 * w) * 8 * 2 * 64), 0, 65536, 0x00020000);
+  const int kb0 = 0, kbs = 1;
+#endif
   const int voff = lane * 16;
 
   // half block h (0..7): key block 4w + (h >> 1), dim blocks 4 (h & 1) .. +3, both planes
   auto hload = [&](int h, f32x4(&f)[8]) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 8; ++i) {
+#if BH_GLOBAL
+      f[i] = bank[((size_t)c * BH_KB * 16 + (kb0 + kbs * (h >> 1)) * 16 + 8 * (h & 1) + i) * 64 + lane];
+#else
       f[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                           rsrc, voff, ((h >> 1) * 16 + 8 * (h & 1) + i) * 1024, 0));
+                                           rsrc, voff, ((kb0 + kbs * (h >> 1)) * 16 + 8 * (h & 1) + i) * 1024, 0));
+#endif
+    }
   };
   // this lane's image addresses: write (row col, dim block 2 db + (g >> 1), half g & 1);
   // transposed read (row 4g + q, dims 4p .. 4p + 3 of a dim block)
   char* wimg = img + 512 * (g >> 1) + bh_row(col, g & 1);
   const int q4 = (lane >> 2) & 3, p4 = lane & 3;
   const char* rimg = img + bh_row(4 * g + q4, p4 >> 1) + 8 * (p4 & 1);
-  // q' and the signal load FIRST, then three half blocks: the wait that
-  // retires q' (for its split) leaves all 24 bank loads in flight
+  // q' (one 16 B load per thread, staged in LDS) and the signal FIRST, then
+  // the first half blocks: the wait that retires q' leaves them in flight
+  float* qimg = lds + BH_Q / 4;  // [8 heads][260] (rows padded: the b128 reads of 8 heads hit 8 bank groups)
+  const f32x4 qld = ld4(qp + pk(c, (threadIdx.x >> 6) * ND_D + 4 * lane, ND_H * ND_D));
+  // lane l: row l & 15 of the wave's key block l >> 4
+  const int bkey = BH_INTERLEAVE ? 16 * (w + 8 * (lane >> 4)) + (lane & 15) : 64 * w + lane;
+  const float sg = signal[(size_t)c * T + min(bkey, T - 1)];
+  f32x4 F[3][8];
+  hload(0, F[0]);
+  hload(1, F[1]);
+  if (BH_AHEAD == 2) hload(2, F[2]);
+  __builtin_amdgcn_sched_barrier(0);
+  st4(qimg + (threadIdx.x >> 6) * 260 + 4 * lane, qld);
+  lds_barrier();  // LDS only: the bank loads stay in flight
   f32x4 qv[8][2];
   const int hd = col & 7;
 #pragma unroll
   for (int db = 0; db < 8; ++db) {
-    const int d0 = hd * ND_D + 32 * db + 8 * g;
-    qv[db][0] = ld4(qp + pk(c, d0, ND_H * ND_D));
-    qv[db][1] = ld4(qp + pk(c, d0 + 4, ND_H * ND_D));
+    qv[db][0] = ld4(qimg + hd * 260 + 32 * db + 8 * g);
+    qv[db][1] = ld4(qimg + hd * 260 + 32 * db + 8 * g + 4);
   }
-  const float sg = signal[(size_t)c * T + min(64 * w + lane, T - 1)];
-  f32x4 F[3][8];
-  hload(0, F[0]);
-  hload(1, F[1]);
-  hload(2, F[2]);
-  __builtin_amdgcn_sched_barrier(0);  // every load issued before the q' split waits on q'
   // q' as the B operand: column col = (plane col >> 3, head col & 7), dims 32 db + 8 g .. +7
   bh8 qb[8];
   {
@@ -401,23 +432,29 @@ dec_bank_h3_kernel(const float* __restrict__ qp, const f32x4* __restrict__ bank,
       // ---- S partial over dim blocks 4 part .. +3: D[key 4g + i][col]
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
+#if BH_EXPT & 2
+        d0 += f[2 * i] + f[2 * i + 1];
+#else
         d0 = mfma_h32(__builtin_bit_cast(bh8, f[2 * i]), qb[4 * part + i], d0);
         d1 = mfma_h32(__builtin_bit_cast(bh8, f[2 * i + 1]), qb[4 * part + i], d1);
+#endif
       }
       // ---- the fragments into the transposed image: dims 32 db + 8 g .. +7 of key col
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const int db = 4 * part + (i >> 1), pl = i & 1;
+#if !(BH_EXPT & 4)
         *reinterpret_cast<f32x4*>(wimg + pl * 8192 + 1024 * db) = f[i];
+#endif
       }
       __builtin_amdgcn_sched_barrier(0);  // the next loads reuse f's registers
-      if (h + 3 < 8) hload(h + 3, F[h % 3]);
+      if (h + BH_AHEAD + 1 < 8) hload(h + BH_AHEAD + 1, F[(h + BH_AHEAD + 1) % 3]);
     }
     // ---- scores: columns h and h + 8 hold the hi and lo halves of q'_h
     f32x4 s = d0 + d1;
 #pragma unroll
     for (int i = 0; i < 4; ++i) s[i] += dpp_mov<ND_DPP_ROR8>(s[i]);
-    const int kbase = 64 * w + 16 * kb + 4 * g;  // key of row i: kbase + i
+    const int kbase = BH_INTERLEAVE ? 16 * (w + 8 * kb) + 4 * g : 64 * w + 16 * kb + 4 * g;  // key of row i
     const unsigned pb = (unsigned)(padm >> (16 * kb + 4 * g)) & 0xFu;
     float gm = -INFINITY;
 #pragma unroll
@@ -430,8 +467,13 @@ dec_bank_h3_kernel(const float* __restrict__ qp, const f32x4* __restrict__ bank,
       for (int i = 0; i < 4; ++i)
         if (kbase + i < L) dbg[(size_t)c * dbg_stride + kbase + i] = s[i];
     }
+#if BH_EXPT & 8
+    m = 0.f;
+    if (false) {
+#else
     gm = xor32_max(xor16_max(gm));
     if (__any(gm > m + BH_THR)) {
+#endif
       const float nm = fmaxf(m, gm);
       const float sc = nm == m ? 1.f : __expf(m - nm);
       m = nm;
@@ -461,8 +503,12 @@ dec_bank_h3_kernel(const float* __restrict__ qp, const f32x4* __restrict__ bank,
     for (int k = 0; k < 16; ++k)
 #pragma unroll
       for (int pl = 0; pl < 2; ++pl) {
+#if BH_EXPT & 1
+        ua[k][pl] += (float)pa[pl];
+#else
         const bs4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bs4*)(rimg + pl * 8192 + 512 * k));
         ua[k] = mfma_h16(pa, __builtin_bit_cast(bh4, b), ua[k]);
+#endif
       }
   }
 
@@ -482,6 +528,10 @@ dec_bank_h3_kernel(const float* __restrict__ qp, const f32x4* __restrict__ bank,
     }
   l = xor32_sum(xor16_sum(l));  // over the 4 key rows of the column's head
 
+#if BH_EXPT & 16  // timing probe only: no merge (each wave stores its own partial)
+  if (l == 12345.f) out[threadIdx.x] = u8[0][0] + u8[7][3] + m;
+  return;
+#endif
   // ---- merge the 8 waves
   __syncthreads();  // every wave is done with its image (the merge image overlays them)
   float* red = lds;                         // [wave][8 heads][256]
@@ -559,7 +609,12 @@ bank_pack_h3_kernel(const float* __restrict__ x, const float* __restrict__ g, co
   flag_overflow(ovf, amax);
 }
 
-bool bank_h3_eligible(int T, int ldT) { return T > 448 && T <= 512 && ldT >= 512; }
+bool bank_h3_eligible(int T, int ldT) {
+#ifdef ND_NO_BANK_H3  // A/B builds only (tools/ab_lib.sh): the fp32 LDS-slab kernel everywhere
+  return false;
+#endif
+  return T > 448 && T <= 512 && ldT >= 512;
+}
 
 hipError_t launch_bank_pack_h3(const float* x, const float* ln_g, const float* ln_b, uint16_t* out, int B, int T,
                                int* ovf, hipStream_t s) {
