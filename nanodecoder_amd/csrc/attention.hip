@@ -208,12 +208,23 @@ __device__ __forceinline__ void esplit8(const float (&x)[8], eh8& hi, eh8& lo) {
   }
 }
 
+// Softmax in log2 units (Q pre-scaled by log2(e) / sqrt(dh): p = 2^(s - m)
+// on v_exp_f32 with no multiply) with a lazy running maximum: O and l are
+// rescaled only when a query's tile maximum exceeds m by more than
+// ENC_THR (p <= 2^8, far inside fp16 once split).  Tiles with no masked or
+// absent key (the common case) skip the per-element mask selects; the row
+// sum stays per lane until the end.  These cut the loop's VALU work, which
+// (at head dim 32) is what bounds this kernel, not the MFMAs.
+#define ENC_THR 8.0f
+typedef float ef2 __attribute__((ext_vector_type(2)));
+
 __global__ void __launch_bounds__(1024)
 enc_attention_h3_kernel(const float* __restrict__ qkv, const float* __restrict__ signal, const int* __restrict__ span,
                         float* __restrict__ out, int T, int* ovf) {
   __shared__ __attribute__((aligned(16))) unsigned Kp[2][ENC_MAXT * ENC_KH];  // [hi|lo][key][32 halves + pad]
   __shared__ __attribute__((aligned(16))) unsigned Vp[2][ND_DH * ENC_VH];     // [hi|lo][dim][512 halves + pad]
-  __shared__ int kflag[ENC_MAXT];  // 0 = key, 1 = masked (signal == 0), 2 = absent (t >= span)
+  __shared__ int kflag[ENC_MAXT];          // 0 = key, 1 = masked (signal == 0), 2 = absent (t >= span)
+  __shared__ int tdirty[ENC_MAXT / 32];    // 32-key tile holds a masked or absent key
 
   const int h = blockIdx.x, b = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -242,7 +253,21 @@ enc_attention_h3_kernel(const float* __restrict__ qkv, const float* __restrict__
       reinterpret_cast<_Float16*>(&Vp[1][(c + i) * ENC_VH])[pos] = (_Float16)(v[i] - (float)vv);
     }
   }
-  for (int t = tid; t < nkt * 32; t += 1024) kflag[t] = t < L ? (signal[base + t] == 0.0f ? 1 : 0) : 2;
+  {
+    // ENC_MAXT <= 1024 threads: one key per thread; wave w covers tiles 2w, 2w + 1
+    static_assert(ENC_MAXT <= 1024, "one key per thread");
+    const bool have = tid < nkt * 32;
+    int f = 0;
+    if (have) {
+      f = tid < L ? (signal[base + tid] == 0.0f ? 1 : 0) : 2;
+      kflag[tid] = f;
+    }
+    const unsigned long long bal = __ballot(have && f != 0);
+    if (lane == 0 && 64 * wave < nkt * 32) {
+      tdirty[2 * wave] = (unsigned)bal != 0u;
+      tdirty[2 * wave + 1] = (unsigned)(bal >> 32) != 0u;
+    }
+  }
   __syncthreads();
 
   const int q0 = wave * 32;
@@ -252,14 +277,17 @@ enc_attention_h3_kernel(const float* __restrict__ qkv, const float* __restrict__
   const int qc = min(q, T - 1);
 
   // Q^T operand of k-step s: dims 16 s + 8 lh .. + 7 of query q, pre-scaled
-  // like ``query / math.sqrt(dim_per_head)`` (multi_headed_attn.py:167)
+  // like ``query / math.sqrt(dim_per_head)`` (multi_headed_attn.py:167) and
+  // by log2(e) (scores in log2 units)
   eh8 qh[2], ql[2];
   {
+    const float qs = 1.4426950408889634f / ND_SQRT_DH;
     const float* qrow = qkv + (base + qc) * (3 * ND_D) + h * ND_DH + 8 * lh;
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      const f32x4 x0 = ld4(qrow + 16 * s2) / ND_SQRT_DH, x1 = ld4(qrow + 16 * s2 + 4) / ND_SQRT_DH;
-      flag_overflow(ovf, fmaxf(absmax4(x0), absmax4(x1)));
+      const f32x4 r0 = ld4(qrow + 16 * s2), r1 = ld4(qrow + 16 * s2 + 4);
+      flag_overflow(ovf, fmaxf(absmax4(r0), absmax4(r1)) * (1.0f / ND_SQRT_DH));
+      const f32x4 x0 = r0 * qs, x1 = r1 * qs;
       const float x[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
       esplit8(x, qh[s2], ql[s2]);
     }
@@ -268,7 +296,7 @@ enc_attention_h3_kernel(const float* __restrict__ qkv, const float* __restrict__
   f32x16 o;
 #pragma unroll
   for (int r = 0; r < 16; ++r) o[r] = 0.f;
-  float m = -INFINITY, l = 0.f;
+  float m = -INFINITY, l = 0.f;  // l: this lane's 16 keys of each tile
 
   for (int kt = 0; kt < nkt; ++kt) {
     f32x16 sacc;
@@ -283,31 +311,39 @@ enc_attention_h3_kernel(const float* __restrict__ qkv, const float* __restrict__
       sacc = mfma32h(kl, qh[s2], sacc);
       sacc = mfma32h(kh, qh[s2], sacc);
     }
-    // sacc[r] = score(query q, key kt*32 + mfma32_row(r, lane))
-    float mx = -INFINITY;
+    // sacc[r] = score(query q, key kt*32 + mfma32_row(r, lane)), log2 units
+    if (tdirty[kt]) {  // wave-uniform
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int f = kflag[kt * 32 + mfma32_row(r, lane)];
-      float sv = sacc[r];
-      sv = f == 1 ? ND_MASK_FILL : sv;
-      sv = f == 2 ? -INFINITY : sv;
-      sacc[r] = sv;
-      mx = fmaxf(mx, sv);
+      for (int r = 0; r < 16; ++r) {
+        const int f = kflag[kt * 32 + mfma32_row(r, lane)];
+        float sv = sacc[r];
+        sv = f == 1 ? ND_MASK_FILL : sv;
+        sv = f == 2 ? -INFINITY : sv;
+        sacc[r] = sv;
+      }
     }
+    float mx = sacc[0];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, sacc[r]);
     mx = xor32_max(mx);
-    const float mn = fmaxf(m, mx);
-    const float alpha = __expf(m - mn);
-    float rsum = 0.f;
+    if (__any(mx > m + ENC_THR)) {
+      const float mn = fmaxf(m, mx);
+      const float alpha = __builtin_amdgcn_exp2f(m - mn);  // m = -inf: 0
+      m = mn;
+      l *= alpha;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      sacc[r] = __expf(sacc[r] - mn);
-      rsum += sacc[r];
+      for (int r = 0; r < 16; ++r) o[r] *= alpha;
     }
-    rsum = xor32_sum(rsum);
-    l = l * alpha + rsum;
-    m = mn;
+    ef2 ls = {0.f, 0.f};
 #pragma unroll
-    for (int r = 0; r < 16; ++r) o[r] *= alpha;
+    for (int r = 0; r < 16; r += 2) {
+      const ef2 d = ef2{sacc[r], sacc[r + 1]} - m;
+      const ef2 p = {__builtin_amdgcn_exp2f(d.x), __builtin_amdgcn_exp2f(d.y)};
+      sacc[r] = p.x;
+      sacc[r + 1] = p.y;
+      ls += p;
+    }
+    l += ls.x + ls.y;
     // O^T[d][q] += V^T[d][key] P^T[key][q] over the tile's two 16-key k-steps
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
@@ -323,6 +359,7 @@ enc_attention_h3_kernel(const float* __restrict__ qkv, const float* __restrict__
       o = mfma32h(vh, ph, o);
     }
   }
+  l = xor32_sum(l);  // both lane halves of query q
   if (q < L) {
     const float inv = 1.0f / l;
     float* orow = out + (base + q) * ND_D + h * ND_DH + 4 * lh;
@@ -364,6 +401,31 @@ dec_embed_kernel(const int* __restrict__ tok, const float* __restrict__ emb, con
 hipError_t launch_dec_embed(const int* tok, const float* emb, const float* pe, int step, float* x, float* part,
                             int R, hipStream_t s) {
   hipLaunchKernelGGL(dec_embed_kernel, dim3((R + 3) / 4), dim3(256), 0, s, tok, emb, pe, step, x, part, R);
+  return hipGetLastError();
+}
+
+// the layer-0 QKV table's input: row s * V + v = emb[v] (* 16 + pe[s]), the
+// same arithmetic as dec_embed_kernel / embed_row (search.hip) for token v
+// at step s; rows past S * V are zero (the GEMM's padded row block)
+__global__ void __launch_bounds__(256)
+dec_embed_table_kernel(const float* __restrict__ emb, const float* __restrict__ pe, int V, int S,
+                       float* __restrict__ x, float* __restrict__ part, int rows) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  f32x4 e = {0.f, 0.f, 0.f, 0.f};
+  if (row < S * V) {
+    const int st = row / V, tk = row - st * V;
+    e = ld4(emb + (size_t)tk * ND_D + lane * 4);
+    if (pe) e = e * 16.0f + ld4(pe + (size_t)st * ND_D + lane * 4);
+  }
+  st4(x + pk(row, lane * 4, ND_D), e);
+  row_part(e, lane, part + (size_t)row * ND_PART_LD * 2);
+}
+
+hipError_t launch_dec_embed_table(const float* emb, const float* pe, int V, int S, float* x, float* part, int rows,
+                                  hipStream_t s) {
+  if (V < 1 || S < 1 || rows < S * V || rows % 16) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(dec_embed_table_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, emb, pe, V, S, x, part, rows);
   return hipGetLastError();
 }
 
@@ -438,11 +500,11 @@ __device__ __forceinline__ void merge_waves(float* accs, float* ms, float* ls, c
 // score (one memory round trip per step; a loop over key blocks would pay
 // one per block), then the NW partial states merge through LDS.
 #define SELF_MAXS 256
-template <int NW, int KW>
+template <int NW, int KW, bool ANC>
 __global__ void __launch_bounds__(NW * 64)
 dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cache, const int* __restrict__ anc,
                           int anc_ld, int step, int S, float* __restrict__ out, int rpc, const int* __restrict__ skip,
-                          int skip_rpc) {
+                          int skip_rpc, QkvRows qr) {
   __shared__ float accs[NW * ND_D];
   __shared__ float ms[NW * ND_H], ls[NW * ND_H];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -459,30 +521,45 @@ dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cac
   // (translate/translator.py:793-823 drops their batches)
   if (skip && skip[r / skip_rpc]) return;
   const int n = step + 1;
-  // qkv is P16-packed [R, 768]
-  const f32x4 qv = ld4(qkv + pk(r, lane * 4, 3 * ND_D)) / ND_SQRT_DH;
-  const f32x4 kme = ld4(qkv + pk(r, ND_D + lane * 4, 3 * ND_D)), vme = ld4(qkv + pk(r, 2 * ND_D + lane * 4, 3 * ND_D));
+  // this wave's keys of pass `base`: the cached history (t < step); the
+  // step's own key (t == step) and keys past it are patched in below.  The
+  // loads are straight-line (t clamped into the history; a branch around
+  // each made hipcc wait vmcnt(0) before the next, one round trip per key)
+  f32x4 k[KW], v[KW];
+  auto load_pass = [&](int base) {
+    const int t0 = base + wave * KW, tmax = max(step - 1, 0);
+    // slots of this wave's keys (lane u < KW: key t0 + u; beam ancestry)
+    int sv = r;
+    if constexpr (ANC) sv = anc[(size_t)r * anc_ld + min(t0 + (lane % KW), tmax)];
+#pragma unroll
+    for (int u = 0; u < KW; ++u) {
+      const int t = min(t0 + u, tmax);  // wave-uniform
+      const int slot = ANC ? __builtin_amdgcn_readlane(sv, u) : r;
+      const float* row = cache + ((size_t)slot * S + t) * 2 * ND_D + lane * 4;
+      k[u] = ld4(row);
+      v[u] = ld4(row + ND_D);
+    }
+  };
+  // the first pass's cache loads go out before the row's q | k | v, whose
+  // address (table mode) waits on the row's token
+  load_pass(0);
+  // qkv is P16-packed [R, 768], or the layer-0 table [S * V, 768] (QkvRows)
+  const int qrow = qr.tok ? step * qr.V + (step == 0 ? qr.tok0 : qr.tok[r]) : r;
+  const f32x4 qv = ld4(qkv + pk(qrow, lane * 4, 3 * ND_D)) / ND_SQRT_DH;
+  const f32x4 kme = ld4(qkv + pk(qrow, ND_D + lane * 4, 3 * ND_D));
+  const f32x4 vme = ld4(qkv + pk(qrow, 2 * ND_D + lane * 4, 3 * ND_D));
   float m[1] = {-INFINITY}, l[1] = {0.f};
   f32x4 acc[1] = {{0.f, 0.f, 0.f, 0.f}};
   // one pass covers NW * KW keys (every step of max_length <= 128 in one)
   for (int base = 0; base < n; base += NW * KW) {
+    if (base > 0) load_pass(base);
     const int t0 = base + wave * KW;
-    // slots of this wave's keys (lane u < KW: key t0 + u)
-    int sv = r;
-    if (anc) sv = anc[(size_t)r * anc_ld + max(min(t0 + (lane % KW), step - 1), 0)];
-    f32x4 k[KW], v[KW];
 #pragma unroll
-    for (int u = 0; u < KW; ++u) {
-      const int t = t0 + u;  // wave-uniform
-      k[u] = kme;
-      v[u] = vme;
-      if (t < step) {
-        const int slot = __builtin_amdgcn_readlane(sv, u);
-        const float* row = cache + ((size_t)slot * S + t) * 2 * ND_D + lane * 4;
-        k[u] = ld4(row);
-        v[u] = ld4(row + ND_D);
+    for (int u = 0; u < KW; ++u)
+      if (t0 + u >= step) {
+        k[u] = kme;
+        v[u] = vme;
       }
-    }
     if (t0 < n) {
       float sc[1][KW];
 #pragma unroll
@@ -502,7 +579,9 @@ dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cac
 }
 
 hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* anc, int anc_ld, int step,
-                                     int max_steps, float* out, int R, hipStream_t s, int rpc, const int* skip) {
+                                     int max_steps, float* out, int R, hipStream_t s, int rpc, const int* skip,
+                                     const QkvRows& qr) {
+  if (qr.tok && (qr.V < 1 || qr.tok0 < 0 || qr.tok0 >= qr.V)) return hipErrorInvalidValue;
   const int skip_rpc = rpc;
   static const int xcd = [] {
     const char* e = getenv("ND_SELF_XCD");  // 0: row order (A/B timing)
@@ -511,13 +590,19 @@ hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* 
   if (!xcd || rpc < 2 || R % (8 * rpc)) rpc = 1;
   if (step >= max_steps || step >= SELF_MAXS) return hipErrorInvalidValue;
   const int n = step + 1;
-#define ND_SELF(NW, KW)                                                                                             \
-  hipLaunchKernelGGL((dec_self_attention_kernel<NW, KW>), dim3(R), dim3(NW * 64), 0, s, qkv, cache, anc, anc_ld, step, \
-                     max_steps, out, rpc, skip, skip_rpc)
+#define ND_SELF2(NW, KW, A)                                                                                    \
+  hipLaunchKernelGGL((dec_self_attention_kernel<NW, KW, A>), dim3(R), dim3(NW * 64), 0, s, qkv, cache, anc, anc_ld, \
+                     step, max_steps, out, rpc, skip, skip_rpc, qr)
+#define ND_SELF(NW, KW)      \
+  if (anc)                   \
+    ND_SELF2(NW, KW, true);  \
+  else                       \
+    ND_SELF2(NW, KW, false)
   if (n <= 32) ND_SELF(8, 4);
   else if (n <= 64) ND_SELF(16, 4);
   else ND_SELF(16, 8);  // two passes beyond 128 keys
 #undef ND_SELF
+#undef ND_SELF2
   return hipGetLastError();
 }
 

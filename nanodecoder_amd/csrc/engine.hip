@@ -157,6 +157,10 @@ struct nd_ctx {
   float *dx = nullptr, *dq1 = nullptr, *dmid = nullptr, *dcq = nullptr, *datt = nullptr, *dqkv = nullptr,
         *dhid = nullptr, *cache = nullptr;
   int *tok = nullptr, *gtok = nullptr;
+  // layer-0 QKV table (QkvRows): input rows, their statistics, the table
+  // [round16(max_steps * V), 768] P16, and each row's token of the step
+  float *qtab_x = nullptr, *qtab_part = nullptr, *qtab = nullptr;
+  int* rtok = nullptr;
   float *gscore = nullptr, *glogp = nullptr;
   nd::BeamState bs{};
   int* steps_done = nullptr;
@@ -387,6 +391,13 @@ static int alloc_workspaces(nd_ctx* c) {
   }
   WS(c->cache, Ld * R * S * 2 * D);
   WS(c->tok, R);
+  if (cfg.self_attn_type != ND_SELF_AVERAGE) {
+    const size_t QR = (S * (size_t)c->V + 15) / 16 * 16;
+    WS(c->qtab_x, QR * D);
+    WS(c->qtab_part, QR * ND_PART_LD * 2);
+    WS(c->qtab, QR * 3 * D);
+    WS(c->rtok, R);
+  }
   WS(c->gtok, B * S);
   WS(c->gscore, B);
   WS(c->glogp, B * S * (size_t)c->V);
@@ -531,13 +542,39 @@ static hipError_t enqueue_ctxkv(nd_ctx* c, int B, int T, hipStream_t s) {
 
 static hipError_t enqueue_encode(nd_ctx* c, int B, int T, hipStream_t s);
 
+// Layer 0 of a scaled-dot decoder reads q | k | v from the per-call table
+// QKV0[step][token] (kernels.hpp, QkvRows) instead of running its QKV GEMM
+// every step; ND_QKV_TABLE=0 keeps the per-step GEMM (A/B timing).
+static bool use_qkv_table(const nd_ctx* c) {
+  static const bool on = [] {
+    const char* e = getenv("ND_QKV_TABLE");
+    return !(e && atoi(e) == 0);
+  }();
+  return on && c->qtab != nullptr;
+}
+
 static nd::NextEmbed next_embed(nd_ctx* c) {
   nd::NextEmbed ne;
   ne.emb = c->emb;
   ne.pe = c->cfg.position_encoding ? c->pe : nullptr;
   ne.x = c->dx;
   ne.part = c->dx_part;
+  ne.tok = use_qkv_table(c) ? c->rtok : nullptr;
   return ne;
+}
+
+// QKV0[s][v] = LN(emb[v] (* 16 + pe[s])) W_qkv + b for the S steps of the
+// call: the layer-0 projection of every input a step can see (V of them),
+// through the same split-fp16 GEMM the step would run (decoder/transformer.py:
+// 76-78, the embedding as onmt/modules/embeddings.py:189-207)
+static hipError_t enqueue_qkv_table(nd_ctx* c, int S, hipStream_t s) {
+  if (!use_qkv_table(c)) return hipSuccess;
+  if (S < 1 || S > c->cfg.max_steps) return hipErrorInvalidValue;
+  const int D = c->D, rows = (S * c->V + 15) / 16 * 16;
+  LCHK(nd::launch_dec_embed_table(c->emb, c->cfg.position_encoding ? c->pe : nullptr, c->V, S, c->qtab_x,
+                                  c->qtab_part, rows, s));
+  const DecLayer& L = c->dec[0];
+  return G(c->qtab_x, D, L.pwqkv, 3 * D, D, L.nbqkv, c->qtab, 3 * D, rows).p16().h3(c).ln(c->qtab_part, 1).run(s);
 }
 
 // Step-0 decoder input (later steps' inputs are written by the search
@@ -582,8 +619,16 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
       LCHK(nd::launch_aan_gate(c->ag, c->axn, c->aa, c->dx, c->dq1, c->dq1_part, R, s));
       pnq = 1;
     } else {
-      LCHK(dg(c->dx, D, L.pwqkv, 3 * D, D, L.nbqkv, c->dqkv, 3 * D).ln(c->dx_part, pnx).run(s));
-      LCHK(nd::launch_dec_self_attention(c->dqkv, cache, anc, anc_ld, step, S, c->datt, R, s, rpc, done));
+      if (i == 0 && use_qkv_table(c)) {  // the row's q | k | v from the call's table
+        nd::QkvRows qr;
+        qr.tok = c->rtok;
+        qr.V = c->V;
+        qr.tok0 = c->cfg.bos_idx;
+        LCHK(nd::launch_dec_self_attention(c->qtab, cache, anc, anc_ld, step, S, c->datt, R, s, rpc, done, qr));
+      } else {
+        LCHK(dg(c->dx, D, L.pwqkv, 3 * D, D, L.nbqkv, c->dqkv, 3 * D).ln(c->dx_part, pnx).run(s));
+        LCHK(nd::launch_dec_self_attention(c->dqkv, cache, anc, anc_ld, step, S, c->datt, R, s, rpc, done));
+      }
       LCHK(dg(c->datt, D, L.pwo, D, D, L.bo, c->dq1, D).res(c->dx, D).stats(c->dq1_part).run(s, &pnq));
     }
     if (mb) {  // memory-bank form (attention.hip)
@@ -636,6 +681,7 @@ static hipError_t enqueue_greedy(nd_ctx* c, int B, int T, int S, int min_len, bo
   LCHK(enqueue_encode(c, B, T, s));
   LCHK(enqueue_memory(c, B, T, 1, s));
   LCHK(nd::launch_fill_i32(c->tok, c->cfg.bos_idx, B, s));
+  LCHK(enqueue_qkv_table(c, S, s));
   LCHK(enqueue_first_embed(c, B, s));
   const nd::NextEmbed ne = next_embed(c);
   for (int step = 0; step < S; ++step) {
@@ -1138,6 +1184,7 @@ static int translate_beam(nd_ctx* c, const float* d_signal, const int32_t* d_len
     LCHK(enqueue_encode(c, B, T, s));
     LCHK(enqueue_memory(c, B, T, beam, s));  // K/V per layer (memory bank at beam 1)
     LCHK(nd::launch_beam_init(c->bs, B, beam, n_best, max_len, c->cfg.bos_idx, s));
+    LCHK(enqueue_qkv_table(c, max_len, s));
     LCHK(enqueue_first_embed(c, B * beam, s));
     LCHK(nd::launch_fill_i32(c->steps_done, max_len, 1, s));
     return hipSuccess;
@@ -1252,6 +1299,7 @@ static int translate_classic(nd_ctx* c, const float* d_signal, const int32_t* d_
     LCHK(enqueue_encode(c, B, T, s));
     LCHK(enqueue_memory(c, B, T, beam, s));  // K/V per layer (memory bank at beam 1)
     LCHK(nd::launch_beam_classic_init(c->bs, c->group_in, B, beam, c->cfg.bos_idx, s));
+    LCHK(enqueue_qkv_table(c, max_len, s));
     LCHK(enqueue_first_embed(c, B * beam, s));
     LCHK(nd::launch_fill_i32(c->steps_done, max_len, 1, s));
     return hipSuccess;

@@ -107,6 +107,19 @@ hipError_t launch_enc_ffn(const float* y, const uint16_t* w1h, float w1s, const 
 hipError_t launch_layernorm(const float* x, const float* g, const float* b, float* out, int rows, hipStream_t s);
 
 // ---- decoder -------------------------------------------------------------
+// Layer 0's self-attention reads its row's q | k | v from a per-call table
+// QKV0[step][token] (P16 [S * V, 768]; launch_dec_embed_table + one GEMM)
+// instead of a per-step GEMM: its input LN(emb[tok] * 16 + pe[step]) takes
+// only V values per step.  tok == nullptr: the per-step qkv matrix.
+struct QkvRows {
+  const int* tok = nullptr;  // row -> token of this step (steps > 0)
+  int V = 0;
+  int tok0 = 0;  // every row's step-0 token (BOS)
+};
+// rows s * V + v (s < S, v < V) of the layer-0 QKV table's input, P16, with
+// one row-statistics partial per row; rows S * V .. rows_alloc - 1 zero
+hipError_t launch_dec_embed_table(const float* emb, const float* pe, int V, int S, float* x, float* part, int rows_alloc,
+                                  hipStream_t s);
 struct DecStepArgs;
 hipError_t launch_dec_embed(const int* tok, const float* emb, const float* pe, int step, float* x, float* part,
                             int R, hipStream_t s);
@@ -115,7 +128,7 @@ hipError_t launch_dec_embed(const int* tok, const float* emb, const float* pe, i
 // skip (nullable): per chunk (row / rpc), nonzero = finished, its rows do nothing
 hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* anc, int anc_ld, int step,
                                      int max_steps, float* out, int R, hipStream_t s, int rpc = 1,
-                                     const int* skip = nullptr);
+                                     const int* skip = nullptr, const QkvRows& qr = QkvRows());
 // context attention: rows r = c*rpc + j attend over ctxkv rows of chunk c
 // (K at kv[(c*T+t)*ld + koff], V at +256), mask signal == pad_val, keys < span.
 hipError_t launch_dec_ctx_attention(const float* q, const float* kv, int ld, int koff, const float* signal,
@@ -131,6 +144,7 @@ struct NextEmbed {
   const float* pe = nullptr;  // null: no position encoding (and no sqrt(d) scale)
   float* x = nullptr;
   float* part = nullptr;
+  int* tok = nullptr;  // optional: the row's token (the layer-0 QKV table's row index)
 };
 // memory-bank context attention (greedy, one row per chunk: rpc == 1):
 // qp = Q' [C, 8*256] P16 (column block h = head h's 256-dim query in memory

@@ -74,6 +74,7 @@ __device__ __forceinline__ void embed_row(const NextEmbed& ne, int tk, int step_
   }
   if (ne.pe) e = e * 16.0f + ld4(ne.pe + (size_t)step_next * ND_D + lane * 4);  // sqrt(256) = 16
   st4(ne.x + pk(row, lane * 4, ND_D), e);
+  if (ne.tok && lane == 0) ne.tok[row] = tk;
   const float mu = wave_sum(e.x + e.y + e.z + e.w) * (1.0f / ND_D);
   const f32x4 d = e - mu;
   const float q = wave_sum(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w);

@@ -205,12 +205,23 @@ def test_dec_self_attention_vs_fp64(step, beam):
     assert torch.equal(appended, qkv[:, 256:])
 
 
-def test_enc_attention_vs_oracle():
+@pytest.mark.parametrize("scale", [1.0, 4.0, "rising"])
+def test_enc_attention_vs_oracle(scale):
+    """Split-fp16 encoder attention against the oracle's attend: masked keys,
+    an all-masked chunk, a ragged span; ``scale`` 4 spreads the scores over
+    ~±60 so the lazy running maximum rescales mid-row, ``rising`` makes every
+    query's scores grow along the keys (a rescale in most tiles)."""
     from nanodecoder_amd.engine import op_enc_attention
     ref = _oracle()
     B, T = 3, 512
     g = torch.Generator().manual_seed(5)
     qkv = torch.randn(B * T, 768, generator=g)
+    if scale == "rising":
+        qkv[:, :256] = qkv[:, :256].abs() * 0.5 + 1.0                       # queries > 0
+        ramp = torch.linspace(0.0, 3.0, T).repeat(B)[:, None]
+        qkv[:, 256:512] = qkv[:, 256:512] * 0.2 + ramp                      # keys rise with t
+    else:
+        qkv = qkv * scale
     sig = torch.randn(B, T, generator=g)
     sig[0, ::7] = 0.0          # masked keys
     sig[2, :] = 0.0            # every key masked -> uniform attention
@@ -226,7 +237,8 @@ def test_enc_attention_vs_oracle():
         mask = (sig[b, :L] == 0).view(1, 1, L)
         c, _ = m.attend(q, k, v, mask)
         exp = m._unheads(c)[0]
-        assert (out[b * T: b * T + L] - exp).abs().max().item() < 1e-4, b
+        tol = 1e-4 * (4.0 if scale == 4.0 else 1.0) * max(1.0, exp.abs().max().item() / 4.0)
+        assert (out[b * T: b * T + L] - exp).abs().max().item() < tol, b
 
 
 @pytest.mark.parametrize("T", [512, 200, 37])
