@@ -32,10 +32,12 @@ namespace nd {
 // Merge P equal-width partials {mean_j, M2_j} of a 256-wide row.  All
 // ND_PART_LD slots are loaded unconditionally (the buffer always holds them)
 // so the loads issue together; slots j >= P are discarded by selects.
-__device__ __forceinline__ void merge_stats(const float* __restrict__ p, int P, float& mu, float& rs) {
-  f32x4 v[ND_PART_LD / 2];  // {mean_2i, M2_2i, mean_2i+1, M2_2i+1}
+typedef f32x4 PartRow[ND_PART_LD / 2];  // {mean_2i, M2_2i, mean_2i+1, M2_2i+1}
+__device__ __forceinline__ void load_stats(const float* __restrict__ p, PartRow& v) {
 #pragma unroll
   for (int i = 0; i < ND_PART_LD / 2; ++i) v[i] = ld4(p + 4 * i);
+}
+__device__ __forceinline__ void merge_loaded(const PartRow& v, int P, float& mu, float& rs) {
   // P is a power of two (the producer's column tiles, or 1): v_rcp_f32 is
   // exact there, and no IEEE division sits on the LN consumer's path
   const float invP = __builtin_amdgcn_rcpf((float)P), w = 256.0f * invP;
@@ -55,6 +57,11 @@ __device__ __forceinline__ void merge_stats(const float* __restrict__ p, int P, 
   }
   mu = m;
   rs = ln_rsqrt(m2 * (1.0f / 256.0f) + ND_LN_EPS);
+}
+__device__ __forceinline__ void merge_stats(const float* __restrict__ p, int P, float& mu, float& rs) {
+  PartRow v;
+  load_stats(p, v);
+  merge_loaded(v, P, mu, rs);
 }
 
 // --fast beam: every row of [r0, r0 + n) (rows < M) belongs to a finished
@@ -377,6 +384,11 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
 // interleaved accumulator chains; K slices are summed through LDS.
 // LN: rows are normalised with statistics merged from the producer's
 // partials (part_in); gamma/beta are folded into W / bias.
+// the bias operand of a GEMM without one: its load stays unconditional (a
+// branch around it made hipcc wait vmcnt(0) there, draining every A / W
+// load in flight before the epilogue operands were even requested)
+__device__ __attribute__((aligned(16))) float nd_zero16[16];
+
 __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
@@ -426,6 +438,10 @@ __global__ void __launch_bounds__(NT* KS * 64) gemm_p16_kernel(const GemmArgs g)
   // fp32 P16 blocks, or (H3) the P16H image: per 32-k pair a hi and a lo 1 KB plane
   const f32x4* __restrict__ wp = H3 ? reinterpret_cast<const f32x4*>(g.Wh) + ((size_t)nb * KB + ws * NF) * 64 + lane
                                     : reinterpret_cast<const f32x4*>(g.W) + ((size_t)nb * KB + ws * NF) * 64 + lane;
+  // every load straight-line, in the order of use: LN partials, A / W, then
+  // the epilogue's bias and residual (the waits below count down in order)
+  PartRow pr;
+  if constexpr (LN) load_stats(g.part_in + (size_t)(mb * 16 + (lane & 15)) * ND_PART_LD * 2, pr);
   f32x4 a[NF], w[NF];
 #pragma unroll
   for (int f = 0; f < NF; ++f) {
@@ -433,11 +449,11 @@ __global__ void __launch_bounds__(NT* KS * 64) gemm_p16_kernel(const GemmArgs g)
     w[f] = wp[f * 64];
   }
   const size_t ct = ((size_t)mb * NB + nb) * 64 + lane;  // this lane's output entry
-  const f32x4 bv = g.bias ? ld4(g.bias + nb * 16 + 4 * (lane >> 4)) : f32x4{0.f, 0.f, 0.f, 0.f};
+  const f32x4 bv = ld4((g.bias ? g.bias + nb * 16 : nd_zero16) + 4 * (lane >> 4));
   f32x4 rv = {0.f, 0.f, 0.f, 0.f};
   if constexpr (RESID) rv = reinterpret_cast<const f32x4*>(g.R)[ct];
   float mu = 0.f, rs = 1.f;
-  if constexpr (LN) merge_stats(g.part_in + (size_t)(mb * 16 + (lane & 15)) * ND_PART_LD * 2, g.part_n_in, mu, rs);
+  if constexpr (LN) merge_loaded(pr, g.part_n_in, mu, rs);
   // keep every load in flight before the first MFMA waits
   __builtin_amdgcn_sched_barrier(0);
   if constexpr (LN) {
@@ -522,6 +538,13 @@ __global__ void __launch_bounds__(BMB* BNB * 64) gemm_p16s_kernel(const GemmArgs
   static_assert(AJ * NW == BMB * KB && WJ * NW == BNB * KB, "blocks per wave");
   static_assert(!H3 || AJ % 2 == 0, "H3 stages A block pairs");
   auto aj = [&](int i) { return H3 ? 2 * (wave + (i >> 1) * NW) + (i & 1) : wave + i * NW; };
+  // LN partials first (wave 0: one row per lane of the BMB * 16 staged rows),
+  // then A / W, then bias and residual: straight-line, waits in order
+  static_assert(BMB * 16 <= 64, "one staged row per lane of wave 0");
+  PartRow pr;
+  if constexpr (LN)
+    if (wave == 0)
+      load_stats(g.part_in + (size_t)min(mb0 * 16 + (lane & (BMB * 16 - 1)), MB * 16 - 1) * ND_PART_LD * 2, pr);
   f32x4 av[AJ], wv[WJ];
 #pragma unroll
   for (int i = 0; i < AJ; ++i) {
@@ -537,7 +560,7 @@ __global__ void __launch_bounds__(BMB* BNB * 64) gemm_p16s_kernel(const GemmArgs
   const int rb = wave / BNB, cb = wave % BNB, nb = nb0 + cb, mb = mb0 + rb;
   const bool live = mb < MB;
   const size_t ct = ((size_t)min(mb, MB - 1) * NB + nb) * 64 + lane;
-  const f32x4 bv = g.bias ? ld4(g.bias + nb * 16 + 4 * (lane >> 4)) : f32x4{0.f, 0.f, 0.f, 0.f};
+  const f32x4 bv = ld4((g.bias ? g.bias + nb * 16 : nd_zero16) + 4 * (lane >> 4));
   f32x4 rv = {0.f, 0.f, 0.f, 0.f};
   if constexpr (RESID) rv = reinterpret_cast<const f32x4*>(g.R)[ct];
   // LayerNorm row statistics: one thread per staged row, into LDS
@@ -545,7 +568,7 @@ __global__ void __launch_bounds__(BMB* BNB * 64) gemm_p16s_kernel(const GemmArgs
   if constexpr (LN) {
     if (tid < BMB * 16) {
       float mu, rs;
-      merge_stats(g.part_in + (size_t)min(mb0 * 16 + tid, MB * 16 - 1) * ND_PART_LD * 2, g.part_n_in, mu, rs);
+      merge_loaded(pr, g.part_n_in, mu, rs);
       st[2 * tid] = mu;
       st[2 * tid + 1] = rs;
     }
