@@ -216,6 +216,9 @@ __device__ __forceinline__ void esplit8(const float (&x)[8], eh8& hi, eh8& lo) {
 // sum stays per lane until the end.  These cut the loop's VALU work, which
 // (at head dim 32) is what bounds this kernel, not the MFMAs.
 #define ENC_THR 8.0f
+#ifndef EA_EXPT
+#define EA_EXPT 0  // timing probes only (tools/build_variant.sh): 1 no loop, 2 no softmax, 4 no P.V MFMAs, 8 no LDS staging writes
+#endif
 typedef float ef2 __attribute__((ext_vector_type(2)));
 
 __global__ void __launch_bounds__(1024)
@@ -232,15 +235,42 @@ enc_attention_h3_kernel(const float* __restrict__ qkv, const float* __restrict__
   const int nkt = (L + 31) >> 5;
   const size_t base = (size_t)b * T;
 
-  for (int idx = tid; idx < nkt * 32 * 8; idx += 1024) {
-    const int t = idx >> 3, c = (idx & 7) * 4;
-    f32x4 k = {0.f, 0.f, 0.f, 0.f}, v = {0.f, 0.f, 0.f, 0.f};
-    if (t < L) {
-      const float* row = qkv + (base + t) * (3 * ND_D) + h * ND_DH + c;
-      k = ld4(row + ND_D);
-      v = ld4(row + 2 * ND_D);
-      flag_overflow(ovf, fmaxf(absmax4(k), absmax4(v)));
+  // staging: every K / V load of the workgroup's 512 keys (4 x 2 per
+  // thread, rows clamped into the span) and the key flags' signal load go
+  // out together before the first conversion (a load under `t < L` in each
+  // pass of a loop made hipcc drain them pass by pass: 4 round trips)
+  static_assert(ENC_MAXT * 8 % 1024 == 0 && ENC_MAXT <= 1024, "staging passes / one key per thread");
+  constexpr int IT = ENC_MAXT * 8 / 1024;
+  f32x4 kr[IT], vr[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int idx = tid + it * 1024, t = min(idx >> 3, L - 1), c = (idx & 7) * 4;
+    const float* row = qkv + (base + t) * (3 * ND_D) + h * ND_DH + c;
+    kr[it] = ld4(row + ND_D);
+    vr[it] = ld4(row + 2 * ND_D);
+  }
+  const float sgv = signal[base + min(tid, L - 1)];
+  // this lane's query row (see the Q^T operand below), loaded with the rest
+  const int lr = lane & 31, lh = lane >> 5;
+  f32x4 qraw[4];
+  {
+    const float* qrow = qkv + (base + min(wave * 32 + lr, T - 1)) * (3 * ND_D) + h * ND_DH + 8 * lh;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      qraw[2 * s2] = ld4(qrow + 16 * s2);
+      qraw[2 * s2 + 1] = ld4(qrow + 16 * s2 + 4);
     }
+  }
+  float amax = 0.f;
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int idx = tid + it * 1024, t = idx >> 3, c = (idx & 7) * 4;
+    const bool in = t < L;
+    const f32x4 k = in ? kr[it] : f32x4{0.f, 0.f, 0.f, 0.f}, v = in ? vr[it] : f32x4{0.f, 0.f, 0.f, 0.f};
+    amax = fmaxf(amax, fmaxf(absmax4(k), absmax4(v)));
+#if EA_EXPT & 8
+    continue;
+#endif
     _Float16* kh = reinterpret_cast<_Float16*>(&Kp[0][t * ENC_KH]) + c;
     _Float16* kl = reinterpret_cast<_Float16*>(&Kp[1][t * ENC_KH]) + c;
     const int pos = (t & ~15) + (t & 3) + 4 * ((t >> 3) & 1) + 8 * ((t >> 2) & 1);
@@ -253,13 +283,13 @@ enc_attention_h3_kernel(const float* __restrict__ qkv, const float* __restrict__
       reinterpret_cast<_Float16*>(&Vp[1][(c + i) * ENC_VH])[pos] = (_Float16)(v[i] - (float)vv);
     }
   }
+  flag_overflow(ovf, amax);
   {
-    // ENC_MAXT <= 1024 threads: one key per thread; wave w covers tiles 2w, 2w + 1
-    static_assert(ENC_MAXT <= 1024, "one key per thread");
+    // one key per thread; wave w covers tiles 2w, 2w + 1
     const bool have = tid < nkt * 32;
     int f = 0;
     if (have) {
-      f = tid < L ? (signal[base + tid] == 0.0f ? 1 : 0) : 2;
+      f = tid < L ? (sgv == 0.0f ? 1 : 0) : 2;
       kflag[tid] = f;
     }
     const unsigned long long bal = __ballot(have && f != 0);
@@ -272,9 +302,7 @@ enc_attention_h3_kernel(const float* __restrict__ qkv, const float* __restrict__
 
   const int q0 = wave * 32;
   if (q0 >= L) return;
-  const int lr = lane & 31, lh = lane >> 5;
   const int q = q0 + lr;
-  const int qc = min(q, T - 1);
 
   // Q^T operand of k-step s: dims 16 s + 8 lh .. + 7 of query q, pre-scaled
   // like ``query / math.sqrt(dim_per_head)`` (multi_headed_attn.py:167) and
@@ -282,10 +310,9 @@ enc_attention_h3_kernel(const float* __restrict__ qkv, const float* __restrict__
   eh8 qh[2], ql[2];
   {
     const float qs = 1.4426950408889634f / ND_SQRT_DH;
-    const float* qrow = qkv + (base + qc) * (3 * ND_D) + h * ND_DH + 8 * lh;
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      const f32x4 r0 = ld4(qrow + 16 * s2), r1 = ld4(qrow + 16 * s2 + 4);
+      const f32x4 r0 = qraw[2 * s2], r1 = qraw[2 * s2 + 1];
       flag_overflow(ovf, fmaxf(absmax4(r0), absmax4(r1)) * (1.0f / ND_SQRT_DH));
       const f32x4 x0 = r0 * qs, x1 = r1 * qs;
       const float x[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
@@ -298,7 +325,7 @@ enc_attention_h3_kernel(const float* __restrict__ qkv, const float* __restrict__
   for (int r = 0; r < 16; ++r) o[r] = 0.f;
   float m = -INFINITY, l = 0.f;  // l: this lane's 16 keys of each tile
 
-  for (int kt = 0; kt < nkt; ++kt) {
+  for (int kt = 0; kt < (EA_EXPT & 1 ? 0 : nkt); ++kt) {
     f32x16 sacc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
@@ -312,6 +339,7 @@ enc_attention_h3_kernel(const float* __restrict__ qkv, const float* __restrict__
       sacc = mfma32h(kh, qh[s2], sacc);
     }
     // sacc[r] = score(query q, key kt*32 + mfma32_row(r, lane)), log2 units
+#if !(EA_EXPT & 2)
     if (tdirty[kt]) {  // wave-uniform
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -344,6 +372,7 @@ enc_attention_h3_kernel(const float* __restrict__ qkv, const float* __restrict__
       ls += p;
     }
     l += ls.x + ls.y;
+#endif
     // O^T[d][q] += V^T[d][key] P^T[key][q] over the tile's two 16-key k-steps
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
@@ -354,9 +383,13 @@ enc_attention_h3_kernel(const float* __restrict__ qkv, const float* __restrict__
       const int off = lr * ENC_VH + (kt * 32 + 16 * s2 + 8 * lh) / 2;  // dwords
       const eh8 vh = __builtin_bit_cast(eh8, *reinterpret_cast<const f32x4*>(&Vp[0][off]));
       const eh8 vl = __builtin_bit_cast(eh8, *reinterpret_cast<const f32x4*>(&Vp[1][off]));
+#if EA_EXPT & 4
+      o[0] += (float)vh[0] + (float)vl[1] + (float)ph[0] + (float)pl[1];
+#else
       o = mfma32h(vh, pl, o);
       o = mfma32h(vl, ph, o);
       o = mfma32h(vh, ph, o);
+#endif
     }
   }
   l = xor32_sum(l);  // both lane halves of query q

@@ -109,6 +109,15 @@ if ONLY == "eattn":  # encoder self-attention at B = 256 x 512
     us = timeit(lambda: E.op_enc_attention(qkv, sig, span), n=10)
     print(f"enc-attn B={B}: {us:9.2f} us  {4*B*8*T*T*32/(us*1e-6)/1e12:6.1f} TF/s")
     sys.exit(0)
+if ONLY == "bank":  # the split-fp16 bank kernel alone at the bench shape (C = 256, T = 512)
+    C, T = 256, 512
+    qp = E.pack_p16(torch.randn(C, 2048, device=dev) * 0.05)
+    sig = torch.randn(C, T, device=dev)
+    span = torch.full((C,), T, dtype=torch.int32, device=dev)
+    bank = E.op_bank_pack_h3(torch.randn(C * T, 256, device=dev), C, T)
+    us = timeit(lambda: E.op_dec_bank_h3(qp, bank, sig, span, 1.0))
+    print(f"bank-h3  C={C:4d} T={T}: {us:8.2f} us  {C * T * 256 * 4 / (us * 1e-6) / 1e9:7.1f} GB/s")
+    sys.exit(0)
 if ONLY == "mem":
     # memory-bank attention: scaling in the chunk count and the key count
     for C, T in ((64, 512), (128, 512), (256, 512), (512, 512), (256, 256), (256, 128)):
