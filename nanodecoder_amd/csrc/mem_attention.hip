@@ -320,7 +320,7 @@ dec_mem_attention_kernel(const float* __restrict__ qp, const float* __restrict__
 #define BH_ML (BH_NW * BH_IMG)           // merge (m, l) [wave][8 heads][2] floats, behind the images
 #define BH_Q (BH_ML + BH_NW * 16 * 4)    // q' image [8 heads][260] floats
 #define BH_LDS (BH_Q + ND_H * 260 * 4)
-static_assert(BH_NW * ND_H * ND_D * 4 <= BH_ML, "merge image overlaps (m, l)");
+static_assert(ND_H * ND_D * 4 <= BH_IMG, "a wave's partial U fits its own image");
 
 typedef _Float16 bh4 __attribute__((ext_vector_type(4)));
 typedef _Float16 bh8 __attribute__((ext_vector_type(8)));
@@ -532,16 +532,17 @@ dec_bank_h3_kernel(const float* __restrict__ qp, const f32x4* __restrict__ bank,
   if (l == 12345.f) out[threadIdx.x] = u8[0][0] + u8[7][3] + m;
   return;
 #endif
-  // ---- merge the 8 waves
-  __syncthreads();  // every wave is done with its image (the merge image overlays them)
-  float* red = lds;                         // [wave][8 heads][256]
+  // ---- merge the 8 waves.  Wave w's partial U [8 heads][256] goes into its
+  // OWN image (16 KB, no longer read once its keys are done: a wave's LDS
+  // operations retire in order), so no barrier is needed before the writes
   float* ml = lds + BH_ML / 4;              // [wave][8 heads][2]
   {
+    float* red = lds + w * (BH_IMG / 4);
     const int hb = 4 * (g & 1), dsel = lane >> 5;
 #pragma unroll
     for (int j = 0; j < 8; ++j)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) red[(w * ND_H + hb + i) * ND_D + 16 * (2 * j + dsel) + col] = u8[j][i];
+      for (int i = 0; i < 4; ++i) red[(hb + i) * ND_D + 16 * (2 * j + dsel) + col] = u8[j][i];
   }
   if (lane < 8) {
     ml[(w * ND_H + lane) * 2] = m;
@@ -559,7 +560,7 @@ dec_bank_h3_kernel(const float* __restrict__ qp, const f32x4* __restrict__ bank,
     const float mv = ml[(v * ND_H + oh) * 2];
     const float f = mv == -INFINITY ? 0.f : __expf(mv - M);  // waves that owned no key
     den += f * ml[(v * ND_H + oh) * 2 + 1];
-    num += f * ld4(red + (v * ND_H + oh) * ND_D + o0);
+    num += f * ld4(lds + v * (BH_IMG / 4) + oh * ND_D + o0);
   }
   st4(out + pk(c, oh * ND_D + o0, ND_H * ND_D), num * (den > 0.f ? __builtin_amdgcn_rcpf(den) : 0.f));
   stamp_end(stamp);
