@@ -141,6 +141,12 @@ __device__ __forceinline__ void flag_overflow(int* ovf, float amax) {
 __device__ __forceinline__ void stamp_begin(unsigned long long* stamp) {
   if (stamp && threadIdx.x == 0) atomicMin(stamp, (unsigned long long)wall_clock64());
 }
+// the same with the clock read at kernel entry (t0 = wall_clock64() as the
+// first statement) and published later, so the stamp's branch and atomic do
+// not sit ahead of the kernel's first loads
+__device__ __forceinline__ void stamp_begin_at(unsigned long long* stamp, unsigned long long t0) {
+  if (stamp && threadIdx.x == 0) atomicMin(stamp, t0);
+}
 __device__ __forceinline__ void stamp_end(unsigned long long* stamp) {
   if (stamp) {
     __syncthreads();

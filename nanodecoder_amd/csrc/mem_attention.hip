@@ -341,11 +341,10 @@ __global__ void __launch_bounds__(BH_NW * 64)
 dec_bank_h3_kernel(const float* __restrict__ qp, const f32x4* __restrict__ bank, const float* __restrict__ signal,
                    const int* __restrict__ span, float pad_val, float* __restrict__ out, int T,
                    unsigned long long* stamp, float* __restrict__ dbg, size_t dbg_stride, int* ovf) {
-  stamp_begin(stamp);
+  const unsigned long long t_entry = wall_clock64();  // the timing stamp's start (published below)
   extern __shared__ float lds[];
   const int c = blockIdx.x, lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int L = min(span[c], T);
   const int col = lane & 15, g = lane >> 4;
   char* img = reinterpret_cast<char*>(lds) + w * BH_IMG;  // [plane][dim block][16 keys][32 B]
   // this wave's fragments: key blocks 4w .. 4w + 3 (64 KB from the descriptor base)
@@ -390,6 +389,11 @@ dec_bank_h3_kernel(const float* __restrict__ qp, const f32x4* __restrict__ bank,
   hload(1, F[1]);
   if (BH_AHEAD == 2) hload(2, F[2]);
   __builtin_amdgcn_sched_barrier(0);
+  // the timing stamp (clock read at entry) and the span after every first
+  // load is out (a branch or a scalar load ahead of them split the
+  // kernel-argument loads: one more scalar round trip before the stream)
+  stamp_begin_at(stamp, t_entry);
+  const int L = min(span[c], T);
   st4(qimg + (threadIdx.x >> 6) * 260 + 4 * lane, qld);
   lds_barrier();  // LDS only: the bank loads stay in flight
   f32x4 qv[8][2];
