@@ -287,9 +287,10 @@ dec_mem_attention_kernel(const float* __restrict__ qp, const float* __restrict__
 //    hit 8 distinct bank groups, and every address is a per-lane base plus a
 //    compile-time offset (no per-block address registers).  32 MFMAs per 16
 //    keys; 64 fp32 accumulators (rows 0-7 P_hi, 8-15 P_lo, summed at the
-//    end).  The fragments load through a buffer descriptor: one offset
-//    register for every load (a register spill in this loop is a vmcnt(0)
-//    drain of every prefetch in flight).
+//    end).  The fragments are plain global loads at constant offsets from
+//    one per-wave base (BH_GLOBAL; the buffer-descriptor form, once needed
+//    to avoid a spill, is 0.5 us slower now): a register spill here would
+//    be a vmcnt(0) drain of every prefetch in flight, so check the .s.
 //  - Online softmax with a lazy maximum: p = exp(s - m) <= e^6 and P is
 //    split at 2^7 (< 65504; its lo plane out of the fp16 subnormals down to
 //    p ~ 5e-7); U and l are rescaled (4 shuffles + 64 multiplies, a
@@ -311,7 +312,8 @@ dec_mem_attention_kernel(const float* __restrict__ qp, const float* __restrict__
 #define BH_INTERLEAVE 1                  // key blocks w + 8 kb (1) or 4 w + kb (0)
 #endif
 #ifndef BH_GLOBAL
-#define BH_GLOBAL 0
+#define BH_GLOBAL 1  // global loads (0: buffer loads through one descriptor; 0.5 us slower since the
+                     // prologue and merge changes, same box, tools/microbench.py bank; neither spills)
 #endif
 #ifndef BH_EXPT
 #define BH_EXPT 0                        // timing probes only (bit 0 no U, 1 no S, 2 no image writes, 3 no softmax)
