@@ -72,3 +72,41 @@ def test_inline_asm_lds_ring_has_no_hazard(tmp_path):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "lds_ring_check.py"), str(out), "enc_ffn"],
                        capture_output=True, text=True)
     assert r.returncode == 0 and "0 hazards" in r.stdout, r.stdout + r.stderr
+
+
+def test_hot_path_kernels_do_not_drain_loads(tmp_path):
+    """The greedy decoder's kernels issue their loads straight-line: no
+    `s_waitcnt vmcnt(0)` followed by more loads (hipcc's lowering of a load
+    under a runtime condition drains every load in flight; DESIGN.md §3,
+    "Straight-line loads").  The P16 GEMMs keep one: the `--fast` beam's
+    finished-chunk probe (rows_dead), which runs only with a skip list."""
+    import concurrent.futures as cf
+    import subprocess
+    import sys
+    from nanodecoder_amd import build
+    if not os.path.exists(build.HIPCC):
+        pytest.skip("no hipcc")
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from isa_loops import drains
+
+    def asm(name):
+        out = tmp_path / (name + ".s")
+        subprocess.run([build.HIPCC] + build.CFLAGS + ["--cuda-device-only", "-S", os.path.join(build.CSRC, name + ".hip"),
+                        "-o", str(out)], check=True, capture_output=True)
+        return out.read_text()
+
+    with cf.ThreadPoolExecutor(4) as ex:
+        src = dict(zip(["attention", "mem_attention", "search", "gemm"],
+                       ex.map(asm, ["attention", "mem_attention", "search", "gemm"])))
+    want = [("attention", r"dec_self_attention_kernel.*Lb0E", 0),  # no beam ancestry
+            ("mem_attention", r"dec_bank_h3_kernel", 0),
+            ("search", r"greedy_head_kernel", 0),
+            ("gemm", r"gemm_p16_kernelILi1ELi8ELi256ELb1ELb0ELb0ELb1E", 1),  # VO / FFN2 (K = 2048)
+            ("gemm", r"gemm_p16_kernelILi1ELi4ELi64ELb1ELb0ELb0ELb1E", 1),  # Wo
+            ("gemm", r"gemm_p16s_kernelILi2ELi4ELb1ELb1E", 1),  # QK / FFN1
+            ("gemm", r"gemm_p16s_kernelILi2ELi2ELb1ELb1ELb0ELb0E", 1)]  # QKV (layers 1, 2)
+    for f, rx, most in want:
+        found = drains(src[f], rx)
+        assert found, rx
+        bad = {k: v for k, v in found.items() if v > most}
+        assert not bad, bad

@@ -2,10 +2,15 @@
 
   hipcc --offload-arch=gfx950 -O3 -std=c++17 --cuda-device-only -S -o x.s file.hip
   python tools/isa_loops.py x.s enc_attention_h3_kernel
+  python tools/isa_loops.py --drains x.s REGEX
 
 Prints, per backward branch (a loop), its length, VALU / MFMA / LDS / VMEM
 counts and the most common opcodes, plus the kernel's register and spill
-counts from the .amdhsa metadata.
+counts from the .amdhsa metadata.  --drains lists, for every kernel whose
+symbol matches REGEX, the `s_waitcnt vmcnt(0)` followed by another vector
+load: a drain of every load in flight before more are issued (hipcc emits
+one after a load under a runtime condition whose result is used in the
+branch, DESIGN.md §3 "Straight-line loads").
 """
 import re
 import sys
@@ -43,5 +48,32 @@ def main(path, name):
             print(f"{key} {mm.group(1)}")
 
 
+def drains(asm, regex, window=80):
+    """{kernel symbol: number of vmcnt(0) waits followed by a vector load}"""
+    out = {}
+    for m in re.finditer(r"^(_Z\S+):", asm, re.M):
+        name = m.group(1)
+        if not re.search(regex, name):
+            continue
+        body = asm[m.end():asm.index(".Lfunc_end", m.end())]
+        lines = [l.split(";")[0].strip() for l in body.split("\n")]
+        lines = [l for l in lines if l]
+        n = 0
+        for i, l in enumerate(lines):
+            if l.startswith("s_waitcnt") and "vmcnt(0)" in l:
+                for nxt in lines[i + 1:i + window]:
+                    if nxt.startswith(("global_load", "buffer_load")):
+                        n += 1
+                        break
+                    if nxt.startswith("s_endpgm"):
+                        break
+        out[name] = n
+    return out
+
+
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    if sys.argv[1] == "--drains":
+        for k, v in sorted(drains(open(sys.argv[2]).read(), sys.argv[3]).items()):
+            print(v, k)
+    else:
+        main(sys.argv[1], sys.argv[2])
