@@ -533,6 +533,9 @@ __device__ __forceinline__ void merge_waves(float* accs, float* ms, float* ls, c
 // score (one memory round trip per step; a loop over key blocks would pay
 // one per block), then the NW partial states merge through LDS.
 #define SELF_MAXS 256
+#ifndef SA_EXPT
+#define SA_EXPT 0  // timing probes only (tools/build_variant.sh): 1 no cache loads, 2 no merge
+#endif
 template <int NW, int KW, bool ANC>
 __global__ void __launch_bounds__(NW * 64)
 dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cache, const int* __restrict__ anc,
@@ -569,8 +572,14 @@ dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cac
       const int t = min(t0 + u, tmax);  // wave-uniform
       const int slot = ANC ? __builtin_amdgcn_readlane(sv, u) : r;
       const float* row = cache + ((size_t)slot * S + t) * 2 * ND_D + lane * 4;
+#if SA_EXPT & 1
+      k[u] = f32x4{0.01f * u, 0.f, 0.f, 0.f};
+      v[u] = k[u];
+      (void)row;
+#else
       k[u] = ld4(row);
       v[u] = ld4(row + ND_D);
+#endif
     }
   };
   // the first pass's cache loads go out before the row's q | k | v, whose
@@ -589,7 +598,7 @@ dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cac
     const int t0 = base + wave * KW;
 #pragma unroll
     for (int u = 0; u < KW; ++u)
-      if (t0 + u >= step) {
+      if (t0 + u >= step) {  // this step's own key (and masked keys past it)
         k[u] = kme;
         v[u] = vme;
       }
@@ -608,6 +617,10 @@ dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cac
     st4(mine + lane * 4, kme);
     st4(mine + ND_D + lane * 4, vme);
   }
+#if SA_EXPT & 2
+  if (wave == 0 && l[0] == 12345.f) st4(out + pk(r, lane * 4, ND_D), acc[0]);
+  return;
+#endif
   merge_waves<1, NW>(accs, ms, ls, m, l, acc, wave, lane, tid, out, r);
 }
 

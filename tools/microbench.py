@@ -109,6 +109,14 @@ if ONLY == "eattn":  # encoder self-attention at B = 256 x 512
     us = timeit(lambda: E.op_enc_attention(qkv, sig, span), n=10)
     print(f"enc-attn B={B}: {us:9.2f} us  {4*B*8*T*T*32/(us*1e-6)/1e12:6.1f} TF/s")
     sys.exit(0)
+if ONLY == "self":  # decoder self-attention at the greedy shape (R = 256, P16 q | k | v)
+    R, S = 256, 100
+    qkv = E.pack_p16(torch.randn(R, 768, device=dev))
+    cache = torch.randn(R, S, 512, device=dev)
+    for step in (20, 50, 90):
+        us = timeit(lambda: E.op_dec_self_attention(qkv, cache, step, packed=True))
+        print(f"self-attn R={R} step={step:3d}: {us:7.2f} us  {R * step * 2048 / (us * 1e-6) / 1e9:7.1f} GB/s")
+    sys.exit(0)
 if ONLY == "bank":  # the split-fp16 bank kernel alone at the bench shape (C = 256, T = 512)
     C, T = 256, 512
     qp = E.pack_p16(torch.randn(C, 2048, device=dev) * 0.05)
