@@ -15,6 +15,7 @@
 #include <cstdlib>
 
 #include "common.hpp"
+#include "head.hpp"
 #include "kernels.hpp"
 
 namespace nd {
@@ -536,11 +537,15 @@ __device__ __forceinline__ void merge_waves(float* accs, float* ms, float* ls, c
 #ifndef SA_EXPT
 #define SA_EXPT 0  // timing probes only (tools/build_variant.sh): 1 no cache loads, 2 no merge
 #endif
-template <int NW, int KW, bool ANC>
+// HEAD (greedy, layer 0 in table mode, step > 0): wave 0 first runs the
+// previous step's greedy head for the row (head.hpp), whose token picks the
+// row's q | k | v in the table; the other waves' cache loads are in flight
+// meanwhile.  One launch per step fewer than a standalone head kernel.
+template <int NW, int KW, bool ANC, bool HEAD>
 __global__ void __launch_bounds__(NW * 64)
 dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cache, const int* __restrict__ anc,
                           int anc_ld, int step, int S, float* __restrict__ out, int rpc, const int* __restrict__ skip,
-                          int skip_rpc, QkvRows qr) {
+                          int skip_rpc, QkvRows qr, GreedyHead hd) {
   __shared__ float accs[NW * ND_D];
   __shared__ float ms[NW * ND_H], ls[NW * ND_H];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -584,9 +589,26 @@ dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cac
   };
   // the first pass's cache loads go out before the row's q | k | v, whose
   // address (table mode) waits on the row's token
-  load_pass(0);
+  // HEAD: wave 0 runs the head before its own cache loads (its registers are
+  // then free of the keys: no spill), the other waves' loads go out first
+  const int wu = __builtin_amdgcn_readfirstlane(wave);
+  if (!HEAD || wu != 0) load_pass(0);
+  int tk = 0;
+  if constexpr (HEAD) {
+    __shared__ float hlp[ND_MAXV];
+    __shared__ int htok;
+    if (wu == 0) {
+      const int b = greedy_head_row(hd, r, step - 1, lane, hlp);
+      if (lane == 0) htok = b;
+      load_pass(0);
+    }
+    lds_barrier();  // LDS only: the cache loads stay in flight
+    tk = htok;
+  } else if (qr.tok) {
+    tk = step == 0 ? qr.tok0 : qr.tok[r];
+  }
   // qkv is P16-packed [R, 768], or the layer-0 table [S * V, 768] (QkvRows)
-  const int qrow = qr.tok ? step * qr.V + (step == 0 ? qr.tok0 : qr.tok[r]) : r;
+  const int qrow = qr.tok ? step * qr.V + tk : r;
   const f32x4 qv = ld4(qkv + pk(qrow, lane * 4, 3 * ND_D)) / ND_SQRT_DH;
   const f32x4 kme = ld4(qkv + pk(qrow, ND_D + lane * 4, 3 * ND_D));
   const f32x4 vme = ld4(qkv + pk(qrow, 2 * ND_D + lane * 4, 3 * ND_D));
@@ -626,8 +648,15 @@ dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cac
 
 hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* anc, int anc_ld, int step,
                                      int max_steps, float* out, int R, hipStream_t s, int rpc, const int* skip,
-                                     const QkvRows& qr) {
+                                     const QkvRows& qr, const GreedyHead* head) {
   if (qr.tok && (qr.V < 1 || qr.tok0 < 0 || qr.tok0 >= qr.V)) return hipErrorInvalidValue;
+  if (head) {
+    if (!qr.tok || anc || skip || rpc != 1 || step < 1 || head->V != qr.V || head->S != max_steps)
+      return hipErrorInvalidValue;
+    const hipError_t e = check_greedy_head(*head);
+    if (e != hipSuccess) return e;
+  }
+  const GreedyHead hd = head ? *head : GreedyHead();
   const int skip_rpc = rpc;
   static const int xcd = [] {
     const char* e = getenv("ND_SELF_XCD");  // 0: row order (A/B timing)
@@ -636,14 +665,16 @@ hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* 
   if (!xcd || rpc < 2 || R % (8 * rpc)) rpc = 1;
   if (step >= max_steps || step >= SELF_MAXS) return hipErrorInvalidValue;
   const int n = step + 1;
-#define ND_SELF2(NW, KW, A)                                                                                    \
-  hipLaunchKernelGGL((dec_self_attention_kernel<NW, KW, A>), dim3(R), dim3(NW * 64), 0, s, qkv, cache, anc, anc_ld, \
-                     step, max_steps, out, rpc, skip, skip_rpc, qr)
-#define ND_SELF(NW, KW)      \
-  if (anc)                   \
-    ND_SELF2(NW, KW, true);  \
-  else                       \
-    ND_SELF2(NW, KW, false)
+#define ND_SELF2(NW, KW, A, HD)                                                                                  \
+  hipLaunchKernelGGL((dec_self_attention_kernel<NW, KW, A, HD>), dim3(R), dim3(NW * 64), 0, s, qkv, cache, anc,     \
+                     anc_ld, step, max_steps, out, rpc, skip, skip_rpc, qr, hd)
+#define ND_SELF(NW, KW)                \
+  if (anc)                             \
+    ND_SELF2(NW, KW, true, false);     \
+  else if (head)                       \
+    ND_SELF2(NW, KW, false, true);     \
+  else                                 \
+    ND_SELF2(NW, KW, false, false)
   if (n <= 32) ND_SELF(8, 4);
   else if (n <= 64) ND_SELF(16, 4);
   else ND_SELF(16, 8);  // two passes beyond 128 keys

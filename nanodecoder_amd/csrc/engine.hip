@@ -553,6 +553,16 @@ static bool use_qkv_table(const nd_ctx* c) {
   return on && c->qtab != nullptr;
 }
 
+// the greedy head fused into the next step's layer-0 self-attention (table
+// mode, scaled-dot layer 0); ND_HEAD_FUSE=0 keeps one head launch per step (A/B timing)
+static bool head_fused(const nd_ctx* c) {
+  static const bool on = [] {
+    const char* e = getenv("ND_HEAD_FUSE");
+    return !(e && atoi(e) == 0);
+  }();
+  return on && use_qkv_table(c) && c->cfg.self_attn_type != ND_SELF_AVERAGE;
+}
+
 static nd::NextEmbed next_embed(nd_ctx* c) {
   nd::NextEmbed ne;
   ne.emb = c->emb;
@@ -590,7 +600,7 @@ static bool use_memory_bank(nd_ctx* c, int rpc) { return c->ctx_path == 0 && rpc
 // done: per chunk, nonzero = finished (--fast beam; null otherwise): its rows'
 // tiles and attention workgroups exit without work
 static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, const int* anc, int anc_ld,
-                                   hipStream_t s, const int* done = nullptr) {
+                                   hipStream_t s, const int* done = nullptr, const nd::GreedyHead* head = nullptr) {
   const int R = C * rpc, D = c->D, F = c->F, S = c->cfg.max_steps;
   const int Ld = (int)c->dec.size();
   const bool mb = use_memory_bank(c, rpc);
@@ -624,7 +634,7 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
         qr.tok = c->rtok;
         qr.V = c->V;
         qr.tok0 = c->cfg.bos_idx;
-        LCHK(nd::launch_dec_self_attention(c->qtab, cache, anc, anc_ld, step, S, c->datt, R, s, rpc, done, qr));
+        LCHK(nd::launch_dec_self_attention(c->qtab, cache, anc, anc_ld, step, S, c->datt, R, s, rpc, done, qr, head));
       } else {
         LCHK(dg(c->dx, D, L.pwqkv, 3 * D, D, L.nbqkv, c->dqkv, 3 * D).ln(c->dx_part, pnx).run(s));
         LCHK(nd::launch_dec_self_attention(c->dqkv, cache, anc, anc_ld, step, S, c->datt, R, s, rpc, done));
@@ -684,11 +694,18 @@ static hipError_t enqueue_greedy(nd_ctx* c, int B, int T, int S, int min_len, bo
   LCHK(enqueue_qkv_table(c, S, s));
   LCHK(enqueue_first_embed(c, B, s));
   const nd::NextEmbed ne = next_embed(c);
+  // step k's head runs inside step k + 1's layer-0 self-attention (table
+  // mode); only the last step's head is a launch of its own
+  const bool fuse = head_fused(c);
+  const nd::GreedyHead hd = nd::make_greedy_head(c->dx, c->dec_ln_g, c->dec_ln_b, c->gen_w, c->gen_b, c->V, S, min_len,
+                                                 c->cfg.eos_idx, c->tok, c->gtok, c->gscore,
+                                                 logp ? c->glogp : nullptr, ne, smp);
   for (int step = 0; step < S; ++step) {
-    LCHK(enqueue_dec_step(c, B, 1, T, step, nullptr, 0, s));
-    LCHK(nd::launch_dec_greedy_head(c->dx, c->dec_ln_g, c->dec_ln_b, c->gen_w, c->gen_b, c->V, step, S, min_len,
-                                    c->cfg.eos_idx, c->tok, c->gtok, c->gscore, logp ? c->glogp : nullptr, ne, B,
-                                    s, smp));
+    LCHK(enqueue_dec_step(c, B, 1, T, step, nullptr, 0, s, nullptr, fuse && step > 0 ? &hd : nullptr));
+    if (!fuse || step == S - 1)
+      LCHK(nd::launch_dec_greedy_head(c->dx, c->dec_ln_g, c->dec_ln_b, c->gen_w, c->gen_b, c->V, step, S, min_len,
+                                      c->cfg.eos_idx, c->tok, c->gtok, c->gscore, logp ? c->glogp : nullptr, ne, B,
+                                      s, smp));
   }
   if (c->attn_on) LCHK(nd::launch_attn_rows_softmax(c->attn_raw, c->span, B, c->cfg.max_steps, T, s));
   return hipSuccess;

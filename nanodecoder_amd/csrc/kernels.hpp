@@ -125,10 +125,15 @@ hipError_t launch_dec_embed(const int* tok, const float* emb, const float* pe, i
                             int R, hipStream_t s);
 // self attention: writes k,v of this step into cache[slot=r][step], attends
 // over the row's history cache[anc[r][t]][t] (anc == nullptr: identity).
-// skip (nullable): per chunk (row / rpc), nonzero = finished, its rows do nothing
+// skip (nullable): per chunk (row / rpc), nonzero = finished, its rows do nothing.
+// head (greedy, table mode, step > 0, no anc / skip): the workgroup of row r first
+// runs the previous step's greedy head for r (its token is this step's input),
+// so the standalone head kernel runs only after the last step
+struct GreedyHead;
 hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* anc, int anc_ld, int step,
                                      int max_steps, float* out, int R, hipStream_t s, int rpc = 1,
-                                     const int* skip = nullptr, const QkvRows& qr = QkvRows());
+                                     const int* skip = nullptr, const QkvRows& qr = QkvRows(),
+                                     const GreedyHead* head = nullptr);
 // context attention: rows r = c*rpc + j attend over ctxkv rows of chunk c
 // (K at kv[(c*T+t)*ld + koff], V at +256), mask signal == pad_val, keys < span.
 hipError_t launch_dec_ctx_attention(const float* q, const float* kv, int ld, int koff, const float* signal,
@@ -195,6 +200,29 @@ struct Sampling {
   int topk = 1;
   const unsigned long long* seed = nullptr;
 };
+// One greedy head (search.hip / head.hpp greedy_head_row): LN_dec ->
+// generator -> log_softmax -> argmax (or a sample) for a row, its token into
+// tok / out_tokens[row][step], score, optional logp dump [R][S][V], and the
+// next step's embedded input (ne).  Run by greedy_head_kernel, or by the
+// layer-0 self-attention of the next step (launch_dec_self_attention's head).
+struct GreedyHead {
+  const float* x = nullptr;
+  const float* ln_g = nullptr;
+  const float* ln_b = nullptr;
+  const float* gw = nullptr;
+  const float* gb = nullptr;
+  int V = 0, S = 0, min_len = 0, eos = 0;
+  int* tok = nullptr;
+  int* out_tokens = nullptr;
+  float* score = nullptr;
+  float* logp_dump = nullptr;
+  NextEmbed ne;
+  Sampling smp;
+};
+GreedyHead make_greedy_head(const float* x, const float* ln_g, const float* ln_b, const float* gw, const float* gb,
+                            int V, int S, int min_len, int eos, int* tok, int* out_tokens, float* score,
+                            float* logp_dump, const NextEmbed& ne, const Sampling& smp);
+hipError_t check_greedy_head(const GreedyHead& h);
 // greedy head: LN_dec -> generator -> log_softmax -> argmax (or a sample);
 // writes token (next input + output [R, S] at column step), score, optional
 // logp dump, and the next step's embedded input (ne).

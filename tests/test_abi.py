@@ -98,9 +98,14 @@ def test_hot_path_kernels_do_not_drain_loads(tmp_path):
     with cf.ThreadPoolExecutor(4) as ex:
         src = dict(zip(["attention", "mem_attention", "search", "gemm"],
                        ex.map(asm, ["attention", "mem_attention", "search", "gemm"])))
-    want = [("attention", r"dec_self_attention_kernel.*Lb0E", 0),  # no beam ancestry
+    want = [("attention", r"dec_self_attention_kernelILi\d+ELi\d+ELb0ELb0E", 0),  # no beam ancestry
+            # the form that runs the previous step's head: wave 0 waits for the
+            # head's own loads, then issues its cache loads (the one allowed)
+            ("attention", r"dec_self_attention_kernelILi\d+ELi\d+ELb0ELb1E", 1),
             ("mem_attention", r"dec_bank_h3_kernel", 0),
-            ("search", r"greedy_head_kernel", 0),
+            # the standalone head (the last step only when the head is fused):
+            # the V > 8 generator loop's loads follow the first 8 rows' wait
+            ("search", r"greedy_head_kernel", 1),
             ("gemm", r"gemm_p16_kernelILi1ELi8ELi256ELb1ELb0ELb0ELb1E", 1),  # VO / FFN2 (K = 2048)
             ("gemm", r"gemm_p16_kernelILi1ELi4ELi64ELb1ELb0ELb0ELb1E", 1),  # Wo
             ("gemm", r"gemm_p16s_kernelILi2ELi4ELb1ELb1E", 1),  # QK / FFN1
