@@ -534,6 +534,7 @@ __device__ __forceinline__ void merge_waves(float* accs, float* ms, float* ls, c
 // score (one memory round trip per step; a loop over key blocks would pay
 // one per block), then the NW partial states merge through LDS.
 #define SELF_MAXS 256
+#define SELF_TABV 8  // vocabulary bound of the head-fused form (its candidate table rows sit in LDS)
 #ifndef SA_EXPT
 #define SA_EXPT 0  // timing probes only (tools/build_variant.sh): 1 no cache loads, 2 no merge
 #endif
@@ -590,28 +591,51 @@ dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cac
   // the first pass's cache loads go out before the row's q | k | v, whose
   // address (table mode) waits on the row's token
   // HEAD: wave 0 runs the head before its own cache loads (its registers are
-  // then free of the keys: no spill), the other waves' loads go out first
+  // then free of the keys: no spill); the other waves first load the step's
+  // V candidate table rows (every token the head can pick) for LDS, then
+  // their cache loads, so the row's q | k | v is an LDS read once the token
+  // is known (not a global round trip after the barrier)
   const int wu = __builtin_amdgcn_readfirstlane(wave);
-  if (!HEAD || wu != 0) load_pass(0);
-  int tk = 0;
+  f32x4 qv, kme, vme;
   if constexpr (HEAD) {
     __shared__ float hlp[ND_MAXV];
     __shared__ int htok;
+    __shared__ __attribute__((aligned(16))) float tabs[SELF_TABV * 3 * ND_D];
     if (wu == 0) {
       const int b = greedy_head_row(hd, r, step - 1, lane, hlp);
       if (lane == 0) htok = b;
       load_pass(0);
+    } else {
+      // V x 192 float4 pieces over (NW - 1) x 64 threads, clamped (straight-line:
+      // a load under a branch would make the stores below wait for the cache loads)
+      constexpr int TPT = (SELF_TABV * 3 * ND_D / 4 + (NW - 1) * 64 - 1) / ((NW - 1) * 64);
+      const int n4 = qr.V * (3 * ND_D / 4), t0 = tid - 64;
+      f32x4 tv[TPT];
+#pragma unroll
+      for (int i = 0; i < TPT; ++i) {
+        const int e = min(t0 + i * (NW - 1) * 64, n4 - 1), v = e / (3 * ND_D / 4), c4 = e % (3 * ND_D / 4);
+        tv[i] = ld4(qkv + pk(step * qr.V + v, 4 * c4, 3 * ND_D));
+      }
+      load_pass(0);
+#pragma unroll
+      for (int i = 0; i < TPT; ++i) {
+        const int e = min(t0 + i * (NW - 1) * 64, n4 - 1);
+        st4(tabs + 4 * e, tv[i]);
+      }
     }
     lds_barrier();  // LDS only: the cache loads stay in flight
-    tk = htok;
-  } else if (qr.tok) {
-    tk = step == 0 ? qr.tok0 : qr.tok[r];
+    const float* trow = tabs + htok * (3 * ND_D);
+    qv = ld4(trow + lane * 4) / ND_SQRT_DH;
+    kme = ld4(trow + ND_D + lane * 4);
+    vme = ld4(trow + 2 * ND_D + lane * 4);
+  } else {
+    load_pass(0);
+    // qkv is P16-packed [R, 768], or the layer-0 table [S * V, 768] (QkvRows)
+    const int qrow = qr.tok ? step * qr.V + (step == 0 ? qr.tok0 : qr.tok[r]) : r;
+    qv = ld4(qkv + pk(qrow, lane * 4, 3 * ND_D)) / ND_SQRT_DH;
+    kme = ld4(qkv + pk(qrow, ND_D + lane * 4, 3 * ND_D));
+    vme = ld4(qkv + pk(qrow, 2 * ND_D + lane * 4, 3 * ND_D));
   }
-  // qkv is P16-packed [R, 768], or the layer-0 table [S * V, 768] (QkvRows)
-  const int qrow = qr.tok ? step * qr.V + tk : r;
-  const f32x4 qv = ld4(qkv + pk(qrow, lane * 4, 3 * ND_D)) / ND_SQRT_DH;
-  const f32x4 kme = ld4(qkv + pk(qrow, ND_D + lane * 4, 3 * ND_D));
-  const f32x4 vme = ld4(qkv + pk(qrow, 2 * ND_D + lane * 4, 3 * ND_D));
   float m[1] = {-INFINITY}, l[1] = {0.f};
   f32x4 acc[1] = {{0.f, 0.f, 0.f, 0.f}};
   // one pass covers NW * KW keys (every step of max_length <= 128 in one)
@@ -651,7 +675,8 @@ hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* 
                                      const QkvRows& qr, const GreedyHead* head) {
   if (qr.tok && (qr.V < 1 || qr.tok0 < 0 || qr.tok0 >= qr.V)) return hipErrorInvalidValue;
   if (head) {
-    if (!qr.tok || anc || skip || rpc != 1 || step < 1 || head->V != qr.V || head->S != max_steps)
+    if (!qr.tok || anc || skip || rpc != 1 || step < 1 || head->V != qr.V || head->V > SELF_TABV ||
+        head->S != max_steps)
       return hipErrorInvalidValue;
     const hipError_t e = check_greedy_head(*head);
     if (e != hipSuccess) return e;

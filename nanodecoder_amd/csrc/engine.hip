@@ -560,7 +560,7 @@ static bool head_fused(const nd_ctx* c) {
     const char* e = getenv("ND_HEAD_FUSE");
     return !(e && atoi(e) == 0);
   }();
-  return on && use_qkv_table(c) && c->cfg.self_attn_type != ND_SELF_AVERAGE;
+  return on && use_qkv_table(c) && c->cfg.self_attn_type != ND_SELF_AVERAGE && c->V <= 8;  // SELF_TABV
 }
 
 static nd::NextEmbed next_embed(nd_ctx* c) {
