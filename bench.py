@@ -50,6 +50,7 @@ METRIC = "signal-samples/sec/GPU (512-sample chunks) + bases/sec at 1/2/4/8 MI35
 FP32_PEAK = 157.3            # TFLOP/s, dense fp32 MFMA (MI355X_MICROARCH.md)
 SPLIT_PEAK = 2516.6 / 3      # TFLOP/s fp32-equivalent: dense fp16 MFMA peak / 3 split products
 HBM_PEAK = 8000.0            # GB/s
+HBM_MEASURED = 6290.0        # GB/s: MI355X_MICROARCH.md's measured float4 copy (79 % of the spec peak)
 FLOP_PER_CHUNK = 6_273_038_336          # SURVEY.md §8d, greedy, 100 steps (12.25 MFLOP/sample)
 ENC_FLOP_PER_CHUNK = 4_832_100_352      # transformer encoder term
 NANO_ENC_FLOP_PER_CHUNK = 1_007_681_536  # NanoEncoder term
@@ -282,7 +283,9 @@ def kernel_roofline(eng, B, mode, beam, encoder="transformer", alive=None):
            "frac": round(ach / HBM_PEAK, 4), "traffic": _pmc(name, "kernels" if mode == "greedy" else "kernels_beam"),
            "algorithmic_bytes_per_launch": nbytes,
            "avg_launch_ms": round(ms, 5), "timed_launches": n,
-           "timing": "in-kernel wall-clock stamps, launches of the last timed call"}
+           "timing": "in-kernel wall-clock stamps, launches of the last timed call",
+           "frac_of_measured_copy": round(ach / HBM_MEASURED, 4),
+           "measured_copy_gbs": HBM_MEASURED}
     out.update(extra)
     dev = eng.device
     if encoder == "nano":
