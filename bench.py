@@ -575,7 +575,12 @@ def main():
     if args.selftest_cpu:
         return selftest_cpu(args)
     world, rank, local = dist_setup(args)
-    dev = torch.device("cuda", local)
+    # rehearsal of the multi-rank flow on a one-GPU box: every rank on GPU 0
+    # over gloo (RCCL refuses two ranks on one device); the line says so
+    share = os.environ.get("ND_BENCH_SHARE_GPU") == "1"
+    if share and args.backend != "gloo":
+        raise SystemExit("ND_BENCH_SHARE_GPU=1 needs --backend gloo")
+    dev = torch.device("cuda", 0 if share else local)
     torch.cuda.set_device(dev)
     from nanodecoder_amd import synth
 
@@ -595,6 +600,8 @@ def main():
                "data": "synthetic reads, random-init weights",
                "config": {"workload": workload(args), "seq_len": 512, "parallelism": f"read-shard x{world}"},
                "read_shard": rs}
+        if share:
+            res["rehearsal"] = f"{world} ranks sharing GPU 0 over gloo (plumbing check, not a measurement)"
         if rank == 0:
             print(json.dumps(res), flush=True)
         if torch.distributed.is_initialized():
@@ -605,6 +612,8 @@ def main():
     if args.read_shard and args.mode == "greedy" and args.encoder == "transformer":
         eng.close()  # the read-shard engine replaces it
         res["read_shard"] = run_reads(args, world, rank, dev, cfg, W, max(1024, args.reads // 4))
+    if share:
+        res["rehearsal"] = f"{world} ranks sharing GPU 0 over gloo (plumbing check, not a measurement)"
     if rank == 0:
         if args.cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(cfg, W, sig_np, lens_np, args)

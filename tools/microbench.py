@@ -126,6 +126,22 @@ if ONLY == "bank":  # the split-fp16 bank kernel alone at the bench shape (C = 2
     us = timeit(lambda: E.op_dec_bank_h3(qp, bank, sig, span, 1.0))
     print(f"bank-h3  C={C:4d} T={T}: {us:8.2f} us  {C * T * 256 * 4 / (us * 1e-6) / 1e9:7.1f} GB/s")
     sys.exit(0)
+if ONLY == "bankmall":  # Infinity Cache residency: one bank re-read vs 3 banks in rotation (402 MB)
+    C, T = 256, 512
+    qp = E.pack_p16(torch.randn(C, 2048, device=dev) * 0.05)
+    sig = torch.randn(C, T, device=dev)
+    span = torch.full((C,), T, dtype=torch.int32, device=dev)
+    banks = [E.op_bank_pack_h3(torch.randn(C * T, 256, device=dev), C, T) for _ in range(3)]
+    for nb in (1, 2, 3):
+        it = [0]
+
+        def launch():
+            E.op_dec_bank_h3(qp, banks[it[0] % nb], sig, span, 1.0)
+            it[0] += 1
+        us = timeit(launch, n=48)
+        print(f"bank-h3 rotation over {nb} bank(s) ({nb * C * T * 1024 / 2**20:.0f} MiB): {us:8.2f} us  "
+              f"{C * T * 256 * 4 / (us * 1e-6) / 1e9:7.1f} GB/s")
+    sys.exit(0)
 if ONLY == "mem":
     # memory-bank attention: scaling in the chunk count and the key count
     for C, T in ((64, 512), (128, 512), (256, 512), (512, 512), (256, 256), (256, 128)):
