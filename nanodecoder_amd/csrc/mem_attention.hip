@@ -316,7 +316,7 @@ dec_mem_attention_kernel(const float* __restrict__ qp, const float* __restrict__
                      // prologue and merge changes, same box, tools/microbench.py bank; neither spills)
 #endif
 #ifndef BH_EXPT
-#define BH_EXPT 0                        // timing probes only (bit 0 no U, 1 no S, 2 no image writes, 3 no softmax)
+#define BH_EXPT 0                        // timing probes only (bit 0 no U, 1 no S, 2 no image writes, 3 no softmax, 4 no merge)
 #endif
 #define BH_IMG 16384                     // bytes: one wave's transposed image (2 planes x 16 keys x 512 B)
 #define BH_ML (BH_NW * BH_IMG)           // merge (m, l) [wave][8 heads][2] floats, behind the images
@@ -518,57 +518,61 @@ dec_bank_h3_kernel(const float* __restrict__ qp, const f32x4* __restrict__ bank,
       }
   }
 
-  // ---- rows 4g + i: g 0, 1 = P_hi of heads 4g + i, g 2, 3 = P_lo of the same heads.
-  //      permlane32 swap-add of dim-block pairs (2j, 2j + 1): lanes < 32 end with
-  //      block 2j, lanes >= 32 with block 2j + 1, both for heads 4 (g & 1) + i
-  f32x4 u8[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      // unscale first: a VALU op the compiler sees between the MFMA results and
-      // the swap (inline asm gets no MFMA -> VALU wait states of its own)
-      float a = ua[2 * j][i] * (1.0f / BH_PSCALE), b = ua[2 * j + 1][i] * (1.0f / BH_PSCALE);
-      asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
-      u8[j][i] = a + b;
-    }
+  // ---- merge the 8 waves without cross-lane work in the waves: wave w's
+  //      unmerged U^T fragments ua[k] (rows 4g .. 4g + 3: plane g >> 1, heads
+  //      4 (g & 1) .. + 3; column col: dim 16 k + col) go to its OWN image as 16
+  //      b128 writes (its image reads are done: a wave's LDS operations retire
+  //      in order), (m, l) beside; wave 0 then turns the 64 (m, l) into the
+  //      merge weights exp(m - M) and 1 / den once; every thread combines 4
+  //      heads x 1 dim from b128 reads of the hi and lo rows
   l = xor32_sum(xor16_sum(l));  // over the 4 key rows of the column's head
-
-#if BH_EXPT & 16  // timing probe only: no merge (each wave stores its own partial)
-  if (l == 12345.f) out[threadIdx.x] = u8[0][0] + u8[7][3] + m;
+#if BH_EXPT & 16  // timing probe only: no merge
+  if (l == 12345.f) out[threadIdx.x] = ua[0][0] + ua[15][3] + m;
   return;
 #endif
-  // ---- merge the 8 waves.  Wave w's partial U [8 heads][256] goes into its
-  // OWN image (16 KB, no longer read once its keys are done: a wave's LDS
-  // operations retire in order), so no barrier is needed before the writes
-  float* ml = lds + BH_ML / 4;              // [wave][8 heads][2]
+  float* ml = lds + BH_ML / 4;  // [wave][8 heads][2]
   {
-    float* red = lds + w * (BH_IMG / 4);
-    const int hb = 4 * (g & 1), dsel = lane >> 5;
+    f32x4* red = reinterpret_cast<f32x4*>(lds + w * (BH_IMG / 4));
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) red[(hb + i) * ND_D + 16 * (2 * j + dsel) + col] = u8[j][i];
+    for (int k = 0; k < 16; ++k) red[k * 64 + lane] = ua[k];
   }
   if (lane < 8) {
     ml[(w * ND_H + lane) * 2] = m;
     ml[(w * ND_H + lane) * 2 + 1] = l;
   }
   __syncthreads();
-  const int oh = threadIdx.x >> 6, o0 = 4 * (threadIdx.x & 63);
-  float M = -INFINITY;
-#pragma unroll
-  for (int v = 0; v < BH_NW; ++v) M = fmaxf(M, ml[(v * ND_H + oh) * 2]);
-  f32x4 num = {0.f, 0.f, 0.f, 0.f};
-  float den = 0.f;
-#pragma unroll
-  for (int v = 0; v < BH_NW; ++v) {
-    const float mv = ml[(v * ND_H + oh) * 2];
+  float* fw = lds + BH_Q / 4;  // [wave][8 heads] weights, then [8 heads] 1 / den (the q' image is dead)
+  if (w == 0) {
+    const int v = lane >> 3, h = lane & 7;
+    const float mv = ml[(v * ND_H + h) * 2], lv = ml[(v * ND_H + h) * 2 + 1];
+    float M = fmaxf(mv, __shfl_xor(mv, 8, 64));
+    M = fmaxf(M, __shfl_xor(M, 16, 64));
+    M = fmaxf(M, __shfl_xor(M, 32, 64));
     const float f = mv == -INFINITY ? 0.f : __expf(mv - M);  // waves that owned no key
-    den += f * ml[(v * ND_H + oh) * 2 + 1];
-    num += f * ld4(lds + v * (BH_IMG / 4) + oh * ND_D + o0);
+    float den = f * lv;
+    den += __shfl_xor(den, 8, 64);
+    den += __shfl_xor(den, 16, 64);
+    den += __shfl_xor(den, 32, 64);
+    fw[v * ND_H + h] = f;
+    if (v == 0) fw[64 + h] = den > 0.f ? __builtin_amdgcn_rcpf(den) * (1.0f / BH_PSCALE) : 0.f;
   }
-  st4(out + pk(c, oh * ND_D + o0, ND_H * ND_D), num * (den > 0.f ? __builtin_amdgcn_rcpf(den) : 0.f));
+  lds_barrier();
+  {
+    const int hs = threadIdx.x >> 8, d = threadIdx.x & 255, k = d >> 4, cl = d & 15;
+    const int lh = k * 64 + cl + 16 * hs, ll = k * 64 + cl + 16 * (2 + hs);  // hi rows g = hs, lo rows g = 2 + hs
+    f32x4 num = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int v = 0; v < BH_NW; ++v) {
+      const f32x4* red = reinterpret_cast<const f32x4*>(lds + v * (BH_IMG / 4));
+      num += ld4(fw + v * ND_H + 4 * hs) * (red[lh] + red[ll]);
+    }
+    num *= ld4(fw + 64 + 4 * hs);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int n = (4 * hs + i) * ND_D + d;
+      out[pk(c, n & ~3, ND_H * ND_D) + (n & 3)] = num[i];
+    }
+  }
   stamp_end(stamp);
 }
 
