@@ -585,9 +585,13 @@ def _compare_tokens(got, exp_tokens, exp_logp):
     return n_tie
 
 
-def test_greedy_vs_oracle_batch32():
+@pytest.mark.parametrize("itos", [None, ["<unk>", "<blank>", "<s>", "</s>", "A", "C"]])
+def test_greedy_vs_oracle_batch32(itos):
+    """V = 8 (the largest vocabulary whose head runs inside the next step's
+    self-attention, its candidate table rows in LDS) and V = 6 (fewer table
+    rows than the staging threads: clamped loads)."""
     ref = _oracle()
-    cfg = synth.ModelConfig()
+    cfg = synth.ModelConfig() if itos is None else synth.ModelConfig(itos=list(itos))
     W = synth.make_weights(cfg, seed=11, eos_bias=-3.0)
     sig = synth.synth_chunk_batch(32, 512, seed=3)
     lens = np.full(32, 512, np.int32)
