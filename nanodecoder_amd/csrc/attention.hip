@@ -12,6 +12,7 @@
 //   and the exponentiated tile is directly the B operand of the P.V MFMA.
 // * dec_self_attention / dec_ctx_attention: the decoder's q_len = 1
 //   attention (multi_headed_attn.py:124-153 cache modes), bandwidth bound.
+#include <algorithm>
 #include <cstdlib>
 
 #include "common.hpp"
@@ -222,187 +223,223 @@ __device__ __forceinline__ void esplit8(const float (&x)[8], eh8& hi, eh8& lo) {
 #endif
 typedef float ef2 __attribute__((ext_vector_type(2)));
 
+// Persistent form: one workgroup per CU walks the (chunk, head) items
+// blockIdx.x, + gridDim.x, ...; the next item's K / V loads are issued right
+// after the current item is staged into LDS and land while its key loop runs
+// (78 -> ~110 VGPRs, still 4 waves per SIMD), so the staging's HBM reads no
+// longer stand alone between two loops (one workgroup per CU: 150 KB of LDS).
 __global__ void __launch_bounds__(1024)
 enc_attention_h3_kernel(const float* __restrict__ qkv, const float* __restrict__ signal, const int* __restrict__ span,
-                        float* __restrict__ out, int T, int* ovf) {
+                        float* __restrict__ out, int T, int B, int* ovf) {
   __shared__ __attribute__((aligned(16))) unsigned Kp[2][ENC_MAXT * ENC_KH];  // [hi|lo][key][32 halves + pad]
   __shared__ __attribute__((aligned(16))) unsigned Vp[2][ND_DH * ENC_VH];     // [hi|lo][dim][512 halves + pad]
   __shared__ int kflag[ENC_MAXT];          // 0 = key, 1 = masked (signal == 0), 2 = absent (t >= span)
   __shared__ int tdirty[ENC_MAXT / 32];    // 32-key tile holds a masked or absent key
 
-  const int h = blockIdx.x, b = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int L = min(span[b], T);
-  const int nkt = (L + 31) >> 5;
-  const size_t base = (size_t)b * T;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int n_items = B * ND_H;
 
-  // staging: every K / V load of the workgroup's 512 keys (4 x 2 per
-  // thread, rows clamped into the span) and the key flags' signal load go
-  // out together before the first conversion (a load under `t < L` in each
-  // pass of a loop made hipcc drain them pass by pass: 4 round trips)
+  // staging loads of item it (head it % 8 of chunk it / 8): every K / V load
+  // of its 512 keys (4 x 2 per thread, rows clamped into the span) and the
+  // key flags' signal load, straight-line (a load under `t < L` in each pass
+  // of a loop made hipcc drain them pass by pass)
   static_assert(ENC_MAXT * 8 % 1024 == 0 && ENC_MAXT <= 1024, "staging passes / one key per thread");
   constexpr int IT = ENC_MAXT * 8 / 1024;
+  // The first PF of the IT passes are prefetched under the previous item's
+  // loop; the rest (and the signal) go out with the item's own staging (the
+  // whole prefetch would need 5 registers beyond the 128 of 4 waves per SIMD,
+  // and a spill's scratch wait would drain the prefetch)
+  constexpr int PF = 2;
   f32x4 kr[IT], vr[IT];
+  auto issue = [&](int it, int i0, int i1) {
+    const int h = it % ND_H, b = it / ND_H;
+    const int L = min(span[b], T);
+    const size_t base = (size_t)b * T;
 #pragma unroll
-  for (int it = 0; it < IT; ++it) {
-    const int idx = tid + it * 1024, t = min(idx >> 3, L - 1), c = (idx & 7) * 4;
-    const float* row = qkv + (base + t) * (3 * ND_D) + h * ND_DH + c;
-    kr[it] = ld4(row + ND_D);
-    vr[it] = ld4(row + 2 * ND_D);
-  }
-  const float sgv = signal[base + min(tid, L - 1)];
-  // this lane's query row (see the Q^T operand below), loaded with the rest
-  const int lr = lane & 31, lh = lane >> 5;
-  f32x4 qraw[4];
-  {
-    const float* qrow = qkv + (base + min(wave * 32 + lr, T - 1)) * (3 * ND_D) + h * ND_DH + 8 * lh;
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      qraw[2 * s2] = ld4(qrow + 16 * s2);
-      qraw[2 * s2 + 1] = ld4(qrow + 16 * s2 + 4);
+    for (int i = 0; i < IT; ++i) {
+      if (i < i0 || i >= i1) continue;  // compile-time after unrolling
+      const int idx = tid + i * 1024, t = min(idx >> 3, L - 1), c = (idx & 7) * 4;
+      const float* row = qkv + (base + t) * (3 * ND_D) + h * ND_DH + c;
+      kr[i] = ld4(row + ND_D);
+      vr[i] = ld4(row + 2 * ND_D);
     }
-  }
-  float amax = 0.f;
+  };
+  int item = blockIdx.x;
+  if (item < n_items) issue(item, 0, PF);
+  for (; item < n_items; item += gridDim.x) {
+    const int h = item % ND_H, b = item / ND_H;
+    const int L = min(span[b], T);
+    const int nkt = (L + 31) >> 5;
+    const size_t base = (size_t)b * T;
+    issue(item, PF, IT);
+    const float sgv = signal[base + min(tid, L - 1)];
+    // this lane's query row (see the Q^T operand below)
+    f32x4 qraw[4];
+    {
+      const float* qrow = qkv + (base + min(wave * 32 + lr, T - 1)) * (3 * ND_D) + h * ND_DH + 8 * lh;
 #pragma unroll
-  for (int it = 0; it < IT; ++it) {
-    const int idx = tid + it * 1024, t = idx >> 3, c = (idx & 7) * 4;
-    const bool in = t < L;
-    const f32x4 k = in ? kr[it] : f32x4{0.f, 0.f, 0.f, 0.f}, v = in ? vr[it] : f32x4{0.f, 0.f, 0.f, 0.f};
-    amax = fmaxf(amax, fmaxf(absmax4(k), absmax4(v)));
-#if EA_EXPT & 8
-    continue;
-#endif
-    _Float16* kh = reinterpret_cast<_Float16*>(&Kp[0][t * ENC_KH]) + c;
-    _Float16* kl = reinterpret_cast<_Float16*>(&Kp[1][t * ENC_KH]) + c;
-    const int pos = (t & ~15) + (t & 3) + 4 * ((t >> 3) & 1) + 8 * ((t >> 2) & 1);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const _Float16 a = (_Float16)k[i], vv = (_Float16)v[i];
-      kh[i] = a;
-      kl[i] = (_Float16)(k[i] - (float)a);
-      reinterpret_cast<_Float16*>(&Vp[0][(c + i) * ENC_VH])[pos] = vv;
-      reinterpret_cast<_Float16*>(&Vp[1][(c + i) * ENC_VH])[pos] = (_Float16)(v[i] - (float)vv);
-    }
-  }
-  flag_overflow(ovf, amax);
-  {
-    // one key per thread; wave w covers tiles 2w, 2w + 1
-    const bool have = tid < nkt * 32;
-    int f = 0;
-    if (have) {
-      f = tid < L ? (sgv == 0.0f ? 1 : 0) : 2;
-      kflag[tid] = f;
-    }
-    const unsigned long long bal = __ballot(have && f != 0);
-    if (lane == 0 && 64 * wave < nkt * 32) {
-      tdirty[2 * wave] = (unsigned)bal != 0u;
-      tdirty[2 * wave + 1] = (unsigned)(bal >> 32) != 0u;
-    }
-  }
-  __syncthreads();
-
-  const int q0 = wave * 32;
-  if (q0 >= L) return;
-  const int q = q0 + lr;
-
-  // Q^T operand of k-step s: dims 16 s + 8 lh .. + 7 of query q, pre-scaled
-  // like ``query / math.sqrt(dim_per_head)`` (multi_headed_attn.py:167) and
-  // by log2(e) (scores in log2 units)
-  eh8 qh[2], ql[2];
-  {
-    const float qs = 1.4426950408889634f / ND_SQRT_DH;
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      const f32x4 r0 = qraw[2 * s2], r1 = qraw[2 * s2 + 1];
-      flag_overflow(ovf, fmaxf(absmax4(r0), absmax4(r1)) * (1.0f / ND_SQRT_DH));
-      const f32x4 x0 = r0 * qs, x1 = r1 * qs;
-      const float x[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-      esplit8(x, qh[s2], ql[s2]);
-    }
-  }
-
-  f32x16 o;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) o[r] = 0.f;
-  float m = -INFINITY, l = 0.f;  // l: this lane's 16 keys of each tile
-
-  for (int kt = 0; kt < (EA_EXPT & 1 ? 0 : nkt); ++kt) {
-    f32x16 sacc;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      const int off = (kt * 32 + lr) * ENC_KH + 8 * s2 + 4 * lh;  // dwords: dims 16 s2 + 8 lh
-      const eh8 kh = __builtin_bit_cast(eh8, *reinterpret_cast<const f32x4*>(&Kp[0][off]));
-      const eh8 kl = __builtin_bit_cast(eh8, *reinterpret_cast<const f32x4*>(&Kp[1][off]));
-      sacc = mfma32h(kh, ql[s2], sacc);
-      sacc = mfma32h(kl, qh[s2], sacc);
-      sacc = mfma32h(kh, qh[s2], sacc);
-    }
-    // sacc[r] = score(query q, key kt*32 + mfma32_row(r, lane)), log2 units
-#if !(EA_EXPT & 2)
-    if (tdirty[kt]) {  // wave-uniform
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int f = kflag[kt * 32 + mfma32_row(r, lane)];
-        float sv = sacc[r];
-        sv = f == 1 ? ND_MASK_FILL : sv;
-        sv = f == 2 ? -INFINITY : sv;
-        sacc[r] = sv;
+      for (int s2 = 0; s2 < 2; ++s2) {
+        qraw[2 * s2] = ld4(qrow + 16 * s2);
+        qraw[2 * s2 + 1] = ld4(qrow + 16 * s2 + 4);
       }
     }
-    float mx = sacc[0];
+    float amax = 0.f;
 #pragma unroll
-    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, sacc[r]);
-    mx = xor32_max(mx);
-    if (__any(mx > m + ENC_THR)) {
-      const float mn = fmaxf(m, mx);
-      const float alpha = __builtin_amdgcn_exp2f(m - mn);  // m = -inf: 0
-      m = mn;
-      l *= alpha;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) o[r] *= alpha;
-    }
-    ef2 ls = {0.f, 0.f};
-#pragma unroll
-    for (int r = 0; r < 16; r += 2) {
-      const ef2 d = ef2{sacc[r], sacc[r + 1]} - m;
-      const ef2 p = {__builtin_amdgcn_exp2f(d.x), __builtin_amdgcn_exp2f(d.y)};
-      sacc[r] = p.x;
-      sacc[r + 1] = p.y;
-      ls += p;
-    }
-    l += ls.x + ls.y;
+    for (int i = 0; i < IT; ++i) {
+      const int idx = tid + i * 1024, t = idx >> 3, c = (idx & 7) * 4;
+      const bool in = t < L;
+      const f32x4 k = in ? kr[i] : f32x4{0.f, 0.f, 0.f, 0.f}, v = in ? vr[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+      amax = fmaxf(amax, fmaxf(absmax4(k), absmax4(v)));
+#if EA_EXPT & 8
+      continue;
 #endif
-    // O^T[d][q] += V^T[d][key] P^T[key][q] over the tile's two 16-key k-steps
+      _Float16* kh = reinterpret_cast<_Float16*>(&Kp[0][t * ENC_KH]) + c;
+      _Float16* kl = reinterpret_cast<_Float16*>(&Kp[1][t * ENC_KH]) + c;
+      const int pos = (t & ~15) + (t & 3) + 4 * ((t >> 3) & 1) + 8 * ((t >> 2) & 1);
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      const float pv[8] = {sacc[8 * s2 + 0], sacc[8 * s2 + 1], sacc[8 * s2 + 2], sacc[8 * s2 + 3],
-                           sacc[8 * s2 + 4], sacc[8 * s2 + 5], sacc[8 * s2 + 6], sacc[8 * s2 + 7]};
-      eh8 ph, pl;
-      esplit8(pv, ph, pl);
-      const int off = lr * ENC_VH + (kt * 32 + 16 * s2 + 8 * lh) / 2;  // dwords
-      const eh8 vh = __builtin_bit_cast(eh8, *reinterpret_cast<const f32x4*>(&Vp[0][off]));
-      const eh8 vl = __builtin_bit_cast(eh8, *reinterpret_cast<const f32x4*>(&Vp[1][off]));
+      for (int j = 0; j < 4; ++j) {
+        const _Float16 a = (_Float16)k[j], vv = (_Float16)v[j];
+        kh[j] = a;
+        kl[j] = (_Float16)(k[j] - (float)a);
+        reinterpret_cast<_Float16*>(&Vp[0][(c + j) * ENC_VH])[pos] = vv;
+        reinterpret_cast<_Float16*>(&Vp[1][(c + j) * ENC_VH])[pos] = (_Float16)(v[j] - (float)vv);
+      }
+    }
+    flag_overflow(ovf, amax);
+    {
+      // one key per thread; wave w covers tiles 2w, 2w + 1
+      const bool have = tid < nkt * 32;
+      int f = 0;
+      if (have) {
+        f = tid < L ? (sgv == 0.0f ? 1 : 0) : 2;
+        kflag[tid] = f;
+      }
+      const unsigned long long bal = __ballot(have && f != 0);
+      if (lane == 0 && 64 * wave < nkt * 32) {
+        tdirty[2 * wave] = (unsigned)bal != 0u;
+        tdirty[2 * wave + 1] = (unsigned)(bal >> 32) != 0u;
+      }
+    }
+    __syncthreads();
+    // the next item's K / V go out now and land under this item's key loop
+    if (item + (int)gridDim.x < n_items) issue(item + gridDim.x, 0, PF);
+
+    const int q0 = wave * 32;
+    const int q = q0 + lr;
+    if (q0 < L) {
+      // Q^T operand of k-step s: dims 16 s + 8 lh .. + 7 of query q, pre-scaled
+      // like ``query / math.sqrt(dim_per_head)`` (multi_headed_attn.py:167)
+      // and by log2(e) (scores in log2 units)
+      eh8 qh[2], ql[2];
+      {
+        const float qs = 1.4426950408889634f / ND_SQRT_DH;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const f32x4 r0 = qraw[2 * s2], r1 = qraw[2 * s2 + 1];
+          flag_overflow(ovf, fmaxf(absmax4(r0), absmax4(r1)) * (1.0f / ND_SQRT_DH));
+          const f32x4 x0 = r0 * qs, x1 = r1 * qs;
+          const float x[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+          esplit8(x, qh[s2], ql[s2]);
+        }
+      }
+
+      f32x16 o;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[r] = 0.f;
+      float m = -INFINITY, l = 0.f;  // l: this lane's 16 keys of each tile
+
+      for (int kt = 0; kt < (EA_EXPT & 1 ? 0 : nkt); ++kt) {
+        f32x16 sacc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int off = (kt * 32 + lr) * ENC_KH + 8 * s2 + 4 * lh;  // dwords: dims 16 s2 + 8 lh
+          const eh8 kh = __builtin_bit_cast(eh8, *reinterpret_cast<const f32x4*>(&Kp[0][off]));
+          const eh8 kl = __builtin_bit_cast(eh8, *reinterpret_cast<const f32x4*>(&Kp[1][off]));
+          sacc = mfma32h(kh, ql[s2], sacc);
+          sacc = mfma32h(kl, qh[s2], sacc);
+          sacc = mfma32h(kh, qh[s2], sacc);
+        }
+        // sacc[r] = score(query q, key kt*32 + mfma32_row(r, lane)), log2 units
+#if !(EA_EXPT & 2)
+        if (tdirty[kt]) {  // wave-uniform
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int f = kflag[kt * 32 + mfma32_row(r, lane)];
+            float sv = sacc[r];
+            sv = f == 1 ? ND_MASK_FILL : sv;
+            sv = f == 2 ? -INFINITY : sv;
+            sacc[r] = sv;
+          }
+        }
+        float mx = sacc[0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) mx = fmaxf(mx, sacc[r]);
+        mx = xor32_max(mx);
+        if (__any(mx > m + ENC_THR)) {
+          const float mn = fmaxf(m, mx);
+          const float alpha = __builtin_amdgcn_exp2f(m - mn);  // m = -inf: 0
+          m = mn;
+          l *= alpha;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[r] *= alpha;
+        }
+        ef2 ls = {0.f, 0.f};
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          const ef2 d = ef2{sacc[r], sacc[r + 1]} - m;
+          const ef2 p = {__builtin_amdgcn_exp2f(d.x), __builtin_amdgcn_exp2f(d.y)};
+          sacc[r] = p.x;
+          sacc[r + 1] = p.y;
+          ls += p;
+        }
+        l += ls.x + ls.y;
+#endif
+        // O^T[d][q] += V^T[d][key] P^T[key][q] over the tile's two 16-key k-steps
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const float pv[8] = {sacc[8 * s2 + 0], sacc[8 * s2 + 1], sacc[8 * s2 + 2], sacc[8 * s2 + 3],
+                               sacc[8 * s2 + 4], sacc[8 * s2 + 5], sacc[8 * s2 + 6], sacc[8 * s2 + 7]};
+          eh8 ph, pl;
+          esplit8(pv, ph, pl);
+          const int off = lr * ENC_VH + (kt * 32 + 16 * s2 + 8 * lh) / 2;  // dwords
+          const eh8 vh = __builtin_bit_cast(eh8, *reinterpret_cast<const f32x4*>(&Vp[0][off]));
+          const eh8 vl = __builtin_bit_cast(eh8, *reinterpret_cast<const f32x4*>(&Vp[1][off]));
 #if EA_EXPT & 4
-      o[0] += (float)vh[0] + (float)vl[1] + (float)ph[0] + (float)pl[1];
+          o[0] += (float)vh[0] + (float)vl[1] + (float)ph[0] + (float)pl[1];
 #else
-      o = mfma32h(vh, pl, o);
-      o = mfma32h(vl, ph, o);
-      o = mfma32h(vh, ph, o);
+          o = mfma32h(vh, pl, o);
+          o = mfma32h(vl, ph, o);
+          o = mfma32h(vh, ph, o);
 #endif
-    }
-  }
-  l = xor32_sum(l);  // both lane halves of query q
-  if (q < L) {
-    const float inv = 1.0f / l;
-    float* orow = out + (base + q) * ND_D + h * ND_DH + 4 * lh;
+        }
+      }
+      l = xor32_sum(l);  // both lane halves of query q
+      if (q < L) {
+        const float inv = 1.0f / l;
+        float* orow = out + (base + q) * ND_D + h * ND_DH + 4 * lh;
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      f32x4 v = {o[4 * g + 0] * inv, o[4 * g + 1] * inv, o[4 * g + 2] * inv, o[4 * g + 3] * inv};
-      st4(orow + 8 * g, v);
+        for (int g = 0; g < 4; ++g) {
+          f32x4 v = {o[4 * g + 0] * inv, o[4 * g + 1] * inv, o[4 * g + 2] * inv, o[4 * g + 3] * inv};
+          st4(orow + 8 * g, v);
+        }
+      }
     }
+    lds_barrier();  // every wave is done with this item's K / V / flags in LDS
   }
+}
+
+// persistent grid of the split-fp16 encoder attention: one workgroup per CU
+static int enc_attn_grid() {
+  static const int n = [] {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const char* e = getenv("ND_ENC_ATTN_GRID");  // workgroups (A/B timing)
+    return e && atoi(e) > 0 ? atoi(e) : (cus > 0 ? cus : 256);
+  }();
+  return n;
 }
 
 hipError_t launch_enc_attention(const float* qkv, const float* signal, const int* span, float* out, int B, int T,
@@ -415,7 +452,8 @@ hipError_t launch_enc_attention(const float* qkv, const float* signal, const int
   if (f32 || exact)
     hipLaunchKernelGGL(enc_attention_kernel, dim3(ND_H, B), dim3(1024), 0, s, qkv, signal, span, out, T);
   else
-    hipLaunchKernelGGL(enc_attention_h3_kernel, dim3(ND_H, B), dim3(1024), 0, s, qkv, signal, span, out, T, ovf);
+    hipLaunchKernelGGL(enc_attention_h3_kernel, dim3(std::min(B * ND_H, enc_attn_grid())), dim3(1024), 0, s, qkv,
+                       signal, span, out, T, B, ovf);
   return hipGetLastError();
 }
 
