@@ -226,9 +226,14 @@ typedef float ef2 __attribute__((ext_vector_type(2)));
 // Persistent form: one workgroup per CU walks the (chunk, head) items
 // blockIdx.x, + gridDim.x, ...; the next item's K / V loads are issued right
 // after the current item is staged into LDS and land while its key loop runs
-// (78 -> ~110 VGPRs, still 4 waves per SIMD), so the staging's HBM reads no
-// longer stand alone between two loops (one workgroup per CU: 150 KB of LDS).
-__global__ void __launch_bounds__(1024)
+// (one workgroup per CU: 150 KB of LDS).  NQ = query blocks of 32 per wave:
+//  - NQ = 1: 16 waves, 128 VGPRs each; only half of the next K / V fits
+//    beside the loop (the whole prefetch spills);
+//  - NQ = 2: 8 waves of 64 queries, 256 VGPRs each: the whole next item
+//    (K, V and the wave's Q rows) is prefetched, and every K / V fragment
+//    read from LDS feeds two query blocks.
+template <int NQ>
+__global__ void __launch_bounds__(1024 / NQ)
 enc_attention_h3_kernel(const float* __restrict__ qkv, const float* __restrict__ signal, const int* __restrict__ span,
                         float* __restrict__ out, int T, int B, int* ovf) {
   __shared__ __attribute__((aligned(16))) unsigned Kp[2][ENC_MAXT * ENC_KH];  // [hi|lo][key][32 halves + pad]
@@ -236,22 +241,23 @@ enc_attention_h3_kernel(const float* __restrict__ qkv, const float* __restrict__
   __shared__ int kflag[ENC_MAXT];          // 0 = key, 1 = masked (signal == 0), 2 = absent (t >= span)
   __shared__ int tdirty[ENC_MAXT / 32];    // 32-key tile holds a masked or absent key
 
+  constexpr int NT = 1024 / NQ;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 31, lh = lane >> 5;
   const int n_items = B * ND_H;
 
   // staging loads of item it (head it % 8 of chunk it / 8): every K / V load
-  // of its 512 keys (4 x 2 per thread, rows clamped into the span) and the
-  // key flags' signal load, straight-line (a load under `t < L` in each pass
-  // of a loop made hipcc drain them pass by pass)
-  static_assert(ENC_MAXT * 8 % 1024 == 0 && ENC_MAXT <= 1024, "staging passes / one key per thread");
-  constexpr int IT = ENC_MAXT * 8 / 1024;
-  // The first PF of the IT passes are prefetched under the previous item's
-  // loop; the rest (and the signal) go out with the item's own staging (the
-  // whole prefetch would need 5 registers beyond the 128 of 4 waves per SIMD,
-  // and a spill's scratch wait would drain the prefetch)
-  constexpr int PF = 2;
+  // of its 512 keys (IT x 2 per thread, rows clamped into the span),
+  // straight-line (a load under `t < L` in each pass of a loop made hipcc
+  // drain them pass by pass).  The first PF passes (and with QPF the wave's
+  // Q rows) are prefetched under the previous item's loop; the rest go out
+  // with the item's own staging.
+  static_assert(ENC_MAXT * 8 % NT == 0 && ENC_MAXT <= NT, "staging passes / one key per thread");
+  constexpr int IT = ENC_MAXT * 8 / NT;
+  constexpr int PF = NQ == 1 ? 2 : IT;
+  constexpr bool QPF = false;  // the Q rows too: 5 registers beyond 256 at NQ = 2 (a spill)
   f32x4 kr[IT], vr[IT];
+  f32x4 qraw[NQ][4];  // this lane's query rows (see the Q^T operand below)
   auto issue = [&](int it, int i0, int i1) {
     const int h = it % ND_H, b = it / ND_H;
     const int L = min(span[b], T);
@@ -259,35 +265,42 @@ enc_attention_h3_kernel(const float* __restrict__ qkv, const float* __restrict__
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
       if (i < i0 || i >= i1) continue;  // compile-time after unrolling
-      const int idx = tid + i * 1024, t = min(idx >> 3, L - 1), c = (idx & 7) * 4;
+      const int idx = tid + i * NT, t = min(idx >> 3, L - 1), c = (idx & 7) * 4;
       const float* row = qkv + (base + t) * (3 * ND_D) + h * ND_DH + c;
       kr[i] = ld4(row + ND_D);
       vr[i] = ld4(row + 2 * ND_D);
     }
   };
+  auto issue_q = [&](int it) {
+    const int h = it % ND_H, b = it / ND_H;
+    const size_t base = (size_t)b * T;
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) {
+      const float* qrow = qkv + (base + min((wave * NQ + j) * 32 + lr, T - 1)) * (3 * ND_D) + h * ND_DH + 8 * lh;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        qraw[j][2 * s2] = ld4(qrow + 16 * s2);
+        qraw[j][2 * s2 + 1] = ld4(qrow + 16 * s2 + 4);
+      }
+    }
+  };
   int item = blockIdx.x;
-  if (item < n_items) issue(item, 0, PF);
+  if (item < n_items) {
+    issue(item, 0, PF);
+    if constexpr (QPF) issue_q(item);
+  }
   for (; item < n_items; item += gridDim.x) {
     const int h = item % ND_H, b = item / ND_H;
     const int L = min(span[b], T);
     const int nkt = (L + 31) >> 5;
     const size_t base = (size_t)b * T;
     issue(item, PF, IT);
+    if constexpr (!QPF) issue_q(item);
     const float sgv = signal[base + min(tid, L - 1)];
-    // this lane's query row (see the Q^T operand below)
-    f32x4 qraw[4];
-    {
-      const float* qrow = qkv + (base + min(wave * 32 + lr, T - 1)) * (3 * ND_D) + h * ND_DH + 8 * lh;
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        qraw[2 * s2] = ld4(qrow + 16 * s2);
-        qraw[2 * s2 + 1] = ld4(qrow + 16 * s2 + 4);
-      }
-    }
     float amax = 0.f;
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
-      const int idx = tid + i * 1024, t = idx >> 3, c = (idx & 7) * 4;
+      const int idx = tid + i * NT, t = idx >> 3, c = (idx & 7) * 4;
       const bool in = t < L;
       const f32x4 k = in ? kr[i] : f32x4{0.f, 0.f, 0.f, 0.f}, v = in ? vr[i] : f32x4{0.f, 0.f, 0.f, 0.f};
       amax = fmaxf(amax, fmaxf(absmax4(k), absmax4(v)));
@@ -321,114 +334,148 @@ enc_attention_h3_kernel(const float* __restrict__ qkv, const float* __restrict__
         tdirty[2 * wave + 1] = (unsigned)(bal >> 32) != 0u;
       }
     }
-    __syncthreads();
-    // the next item's K / V go out now and land under this item's key loop
-    if (item + (int)gridDim.x < n_items) issue(item + gridDim.x, 0, PF);
-
-    const int q0 = wave * 32;
-    const int q = q0 + lr;
-    if (q0 < L) {
-      // Q^T operand of k-step s: dims 16 s + 8 lh .. + 7 of query q, pre-scaled
-      // like ``query / math.sqrt(dim_per_head)`` (multi_headed_attn.py:167)
-      // and by log2(e) (scores in log2 units)
-      eh8 qh[2], ql[2];
-      {
-        const float qs = 1.4426950408889634f / ND_SQRT_DH;
+    // Q^T operand of k-step s: dims 16 s + 8 lh .. + 7 of query q, pre-scaled
+    // like ``query / math.sqrt(dim_per_head)`` (multi_headed_attn.py:167)
+    // and by log2(e) (scores in log2 units)
+    eh8 qh[NQ][2], ql[NQ][2];
 #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const f32x4 r0 = qraw[2 * s2], r1 = qraw[2 * s2 + 1];
-          flag_overflow(ovf, fmaxf(absmax4(r0), absmax4(r1)) * (1.0f / ND_SQRT_DH));
-          const f32x4 x0 = r0 * qs, x1 = r1 * qs;
-          const float x[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-          esplit8(x, qh[s2], ql[s2]);
-        }
+    for (int j = 0; j < NQ; ++j) {
+      const float qs = 1.4426950408889634f / ND_SQRT_DH;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const f32x4 r0 = qraw[j][2 * s2], r1 = qraw[j][2 * s2 + 1];
+        flag_overflow(ovf, fmaxf(absmax4(r0), absmax4(r1)) * (1.0f / ND_SQRT_DH));
+        const f32x4 x0 = r0 * qs, x1 = r1 * qs;
+        const float x[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+        esplit8(x, qh[j][s2], ql[j][s2]);
+      }
+    }
+    __syncthreads();
+    // the next item's loads go out now and land under this item's key loop
+    if (item + (int)gridDim.x < n_items) {
+      issue(item + gridDim.x, 0, PF);
+      if constexpr (QPF) issue_q(item + gridDim.x);
+    }
+
+    const int q0 = wave * NQ * 32;
+    if (q0 < L) {
+      f32x16 o[NQ];
+      float m[NQ], l[NQ];  // l: this lane's 16 keys of each tile
+#pragma unroll
+      for (int j = 0; j < NQ; ++j) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[j][r] = 0.f;
+        m[j] = -INFINITY;
+        l[j] = 0.f;
       }
 
-      f32x16 o;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) o[r] = 0.f;
-      float m = -INFINITY, l = 0.f;  // l: this lane's 16 keys of each tile
-
       for (int kt = 0; kt < (EA_EXPT & 1 ? 0 : nkt); ++kt) {
-        f32x16 sacc;
+        f32x16 sacc[NQ];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
+        for (int j = 0; j < NQ; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) sacc[j][r] = 0.f;
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
           const int off = (kt * 32 + lr) * ENC_KH + 8 * s2 + 4 * lh;  // dwords: dims 16 s2 + 8 lh
           const eh8 kh = __builtin_bit_cast(eh8, *reinterpret_cast<const f32x4*>(&Kp[0][off]));
           const eh8 kl = __builtin_bit_cast(eh8, *reinterpret_cast<const f32x4*>(&Kp[1][off]));
-          sacc = mfma32h(kh, ql[s2], sacc);
-          sacc = mfma32h(kl, qh[s2], sacc);
-          sacc = mfma32h(kh, qh[s2], sacc);
+#pragma unroll
+          for (int j = 0; j < NQ; ++j) {
+            sacc[j] = mfma32h(kh, ql[j][s2], sacc[j]);
+            sacc[j] = mfma32h(kl, qh[j][s2], sacc[j]);
+            sacc[j] = mfma32h(kh, qh[j][s2], sacc[j]);
+          }
         }
-        // sacc[r] = score(query q, key kt*32 + mfma32_row(r, lane)), log2 units
+        // sacc[j][r] = score(query q0 + 32 j + lr, key kt*32 + mfma32_row(r, lane)), log2 units
 #if !(EA_EXPT & 2)
         if (tdirty[kt]) {  // wave-uniform
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int f = kflag[kt * 32 + mfma32_row(r, lane)];
-            float sv = sacc[r];
-            sv = f == 1 ? ND_MASK_FILL : sv;
-            sv = f == 2 ? -INFINITY : sv;
-            sacc[r] = sv;
+#pragma unroll
+            for (int j = 0; j < NQ; ++j) {
+              float sv = sacc[j][r];
+              sv = f == 1 ? ND_MASK_FILL : sv;
+              sv = f == 2 ? -INFINITY : sv;
+              sacc[j][r] = sv;
+            }
           }
         }
-        float mx = sacc[0];
 #pragma unroll
-        for (int r = 1; r < 16; ++r) mx = fmaxf(mx, sacc[r]);
-        mx = xor32_max(mx);
-        if (__any(mx > m + ENC_THR)) {
-          const float mn = fmaxf(m, mx);
-          const float alpha = __builtin_amdgcn_exp2f(m - mn);  // m = -inf: 0
-          m = mn;
-          l *= alpha;
+        for (int j = 0; j < NQ; ++j) {
+          float mx = sacc[j][0];
 #pragma unroll
-          for (int r = 0; r < 16; ++r) o[r] *= alpha;
+          for (int r = 1; r < 16; ++r) mx = fmaxf(mx, sacc[j][r]);
+          mx = xor32_max(mx);
+          if (__any(mx > m[j] + ENC_THR)) {
+            const float mn = fmaxf(m[j], mx);
+            const float alpha = __builtin_amdgcn_exp2f(m[j] - mn);  // m = -inf: 0
+            m[j] = mn;
+            l[j] *= alpha;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) o[j][r] *= alpha;
+          }
+          ef2 ls = {0.f, 0.f};
+#pragma unroll
+          for (int r = 0; r < 16; r += 2) {
+            const ef2 d = ef2{sacc[j][r], sacc[j][r + 1]} - m[j];
+            const ef2 p = {__builtin_amdgcn_exp2f(d.x), __builtin_amdgcn_exp2f(d.y)};
+            sacc[j][r] = p.x;
+            sacc[j][r + 1] = p.y;
+            ls += p;
+          }
+          l[j] += ls.x + ls.y;
         }
-        ef2 ls = {0.f, 0.f};
-#pragma unroll
-        for (int r = 0; r < 16; r += 2) {
-          const ef2 d = ef2{sacc[r], sacc[r + 1]} - m;
-          const ef2 p = {__builtin_amdgcn_exp2f(d.x), __builtin_amdgcn_exp2f(d.y)};
-          sacc[r] = p.x;
-          sacc[r + 1] = p.y;
-          ls += p;
-        }
-        l += ls.x + ls.y;
 #endif
         // O^T[d][q] += V^T[d][key] P^T[key][q] over the tile's two 16-key k-steps
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
-          const float pv[8] = {sacc[8 * s2 + 0], sacc[8 * s2 + 1], sacc[8 * s2 + 2], sacc[8 * s2 + 3],
-                               sacc[8 * s2 + 4], sacc[8 * s2 + 5], sacc[8 * s2 + 6], sacc[8 * s2 + 7]};
-          eh8 ph, pl;
-          esplit8(pv, ph, pl);
           const int off = lr * ENC_VH + (kt * 32 + 16 * s2 + 8 * lh) / 2;  // dwords
           const eh8 vh = __builtin_bit_cast(eh8, *reinterpret_cast<const f32x4*>(&Vp[0][off]));
           const eh8 vl = __builtin_bit_cast(eh8, *reinterpret_cast<const f32x4*>(&Vp[1][off]));
+#pragma unroll
+          for (int j = 0; j < NQ; ++j) {
+            const float pv[8] = {sacc[j][8 * s2 + 0], sacc[j][8 * s2 + 1], sacc[j][8 * s2 + 2], sacc[j][8 * s2 + 3],
+                                 sacc[j][8 * s2 + 4], sacc[j][8 * s2 + 5], sacc[j][8 * s2 + 6], sacc[j][8 * s2 + 7]};
+            eh8 ph, pl;
+            esplit8(pv, ph, pl);
 #if EA_EXPT & 4
-          o[0] += (float)vh[0] + (float)vl[1] + (float)ph[0] + (float)pl[1];
+            o[j][0] += (float)vh[0] + (float)vl[1] + (float)ph[0] + (float)pl[1];
 #else
-          o = mfma32h(vh, pl, o);
-          o = mfma32h(vl, ph, o);
-          o = mfma32h(vh, ph, o);
+            o[j] = mfma32h(vh, pl, o[j]);
+            o[j] = mfma32h(vl, ph, o[j]);
+            o[j] = mfma32h(vh, ph, o[j]);
 #endif
+          }
         }
       }
-      l = xor32_sum(l);  // both lane halves of query q
-      if (q < L) {
-        const float inv = 1.0f / l;
-        float* orow = out + (base + q) * ND_D + h * ND_DH + 4 * lh;
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          f32x4 v = {o[4 * g + 0] * inv, o[4 * g + 1] * inv, o[4 * g + 2] * inv, o[4 * g + 3] * inv};
-          st4(orow + 8 * g, v);
+      for (int j = 0; j < NQ; ++j) {
+        const float lj = xor32_sum(l[j]);  // both lane halves of query q
+        const int q = q0 + 32 * j + lr;
+        if (q < L) {
+          const float inv = 1.0f / lj;
+          float* orow = out + (base + q) * ND_D + h * ND_DH + 4 * lh;
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            f32x4 v = {o[j][4 * g + 0] * inv, o[j][4 * g + 1] * inv, o[j][4 * g + 2] * inv, o[j][4 * g + 3] * inv};
+            st4(orow + 8 * g, v);
+          }
         }
       }
     }
     lds_barrier();  // every wave is done with this item's K / V / flags in LDS
   }
+}
+
+// query blocks per wave of the split-fp16 encoder attention (ND_ENC_ATTN_NQ=1|2, A/B timing)
+static int enc_attn_nq() {
+  static const int n = [] {
+    const char* e = getenv("ND_ENC_ATTN_NQ");
+    return e && atoi(e) == 1 ? 1 : 2;
+  }();
+  return n;
 }
 
 // persistent grid of the split-fp16 encoder attention: one workgroup per CU
@@ -451,8 +498,11 @@ hipError_t launch_enc_attention(const float* qkv, const float* signal, const int
   }();
   if (f32 || exact)
     hipLaunchKernelGGL(enc_attention_kernel, dim3(ND_H, B), dim3(1024), 0, s, qkv, signal, span, out, T);
+  else if (enc_attn_nq() == 1)
+    hipLaunchKernelGGL(enc_attention_h3_kernel<1>, dim3(std::min(B * ND_H, enc_attn_grid())), dim3(1024), 0, s, qkv,
+                       signal, span, out, T, B, ovf);
   else
-    hipLaunchKernelGGL(enc_attention_h3_kernel, dim3(std::min(B * ND_H, enc_attn_grid())), dim3(1024), 0, s, qkv,
+    hipLaunchKernelGGL(enc_attention_h3_kernel<2>, dim3(std::min(B * ND_H, enc_attn_grid())), dim3(512), 0, s, qkv,
                        signal, span, out, T, B, ovf);
   return hipGetLastError();
 }
