@@ -219,7 +219,7 @@ __device__ __forceinline__ void esplit8(const float (&x)[8], eh8& hi, eh8& lo) {
 // (at head dim 32) is what bounds this kernel, not the MFMAs.
 #define ENC_THR 8.0f
 #ifndef EA_EXPT
-#define EA_EXPT 0  // timing probes only (tools/build_variant.sh): 1 no loop, 2 no softmax, 4 no P.V MFMAs, 8 no LDS staging writes
+#define EA_EXPT 0  // timing probes only (tools/build_variant.sh): 1 no loop, 2 no softmax, 4 no P.V MFMAs, 8 no LDS staging writes, 32 no K / V loads
 #endif
 typedef float ef2 __attribute__((ext_vector_type(2)));
 
@@ -267,8 +267,14 @@ enc_attention_h3_kernel(const float* __restrict__ qkv, const float* __restrict__
       if (i < i0 || i >= i1) continue;  // compile-time after unrolling
       const int idx = tid + i * NT, t = min(idx >> 3, L - 1), c = (idx & 7) * 4;
       const float* row = qkv + (base + t) * (3 * ND_D) + h * ND_DH + c;
+#if EA_EXPT & 32
+      kr[i] = f32x4{0.01f * (t & 7), 0.02f, -0.01f * (c & 3), 0.f};
+      vr[i] = kr[i];
+      (void)row;
+#else
       kr[i] = ld4(row + ND_D);
       vr[i] = ld4(row + 2 * ND_D);
+#endif
     }
   };
   auto issue_q = [&](int it) {
@@ -482,7 +488,9 @@ static int enc_attn_nq() {
 static int enc_attn_grid() {
   static const int n = [] {
     int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
     const char* e = getenv("ND_ENC_ATTN_GRID");  // workgroups (A/B timing)
     return e && atoi(e) > 0 ? atoi(e) : (cus > 0 ? cus : 256);
   }();
