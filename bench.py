@@ -65,6 +65,9 @@ def parse():
     ap.add_argument("--batch", type=int, default=256, help="chunks per GPU per step")
     ap.add_argument("--mode", default="greedy", choices=["greedy", "beam"])
     ap.add_argument("--beam", type=int, default=5)
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="translate calls on the device at once (EnginePool lanes: one engine context and HIP "
+                         "stream each); 1 = one call at a time")
     ap.add_argument("--encoder", default="transformer", choices=["transformer", "nano"])
     ap.add_argument("--max-length", type=int, default=100)
     ap.add_argument("--min-length", type=int, default=57,
@@ -76,12 +79,18 @@ def parse():
                     help="batch: configs[1..3] fixed batches resident in HBM; reads: configs[4] read sharding")
     ap.add_argument("--reads", type=int, default=16384, help="synthetic reads PER GPU for the read-shard workload")
     ap.add_argument("--read-shard", type=int, default=1, help="append the configs[4] read-shard measurement")
+    ap.add_argument("--config-legs", type=int, default=1,
+                    help="append configs[2] (NanoEncoder greedy) and configs[3] (--fast beam, batch 1024) measured "
+                         "in the same run")
     ap.add_argument("--exact", type=int, default=1, help="append the exact-fp32 throughput")
     ap.add_argument("--host-inclusive", type=int, default=1, help="append the Translator (host-inclusive) rate")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 (0 = skip)")
     ap.add_argument("--cpu-chunks", type=int, default=50, help="CPU baseline batch (configs[0]: 50)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline: repeat batches for at least this")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--allow-switches", action="store_true",
+                    help="run even when an ND_* A/B switch of the library is set to a non-default value (the line "
+                         "then carries headline: false)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
     ap.add_argument("--selftest-cpu", action="store_true",
                     help="launcher/rank plumbing self-test on CPU (gloo, no engine, no measurement)")
@@ -384,49 +393,99 @@ def mfma_view(args, eng, sig, lens, ms_per_step):
 
 
 # ----------------------------------------------------------------- workloads
-def run_batch(args, world, rank, dev, cfg, W):
-    from nanodecoder_amd import synth
-    from nanodecoder_amd.engine import Engine
+def run_calls(pool, n, call):
+    """n translate calls, `pool.lanes` of them on the device at once; returns
+    the last call's outputs (complete: every lane is joined to the current
+    stream).  ``call(engine_or_pool)`` issues one call.  Greedy calls are
+    asynchronous, so one host thread keeps every lane busy; a beam call polls
+    its alive count between 10-step graph segments (host-synchronous), so each
+    lane gets a host thread of its own there."""
+    import threading
+    outs = [None] * pool.lanes
+    if not getattr(call, "blocking", False) or pool.lanes == 1:
+        for k in range(n):
+            outs[k % pool.lanes] = call(pool)
+        pool.synchronize()
+        return outs[(n - 1) % pool.lanes]
+    cur = torch.cuda.current_stream(pool.device)
+    errs = []
 
-    beam = args.beam if args.mode == "beam" else 1
-    eng = Engine(cfg, W, device=dev.index, max_batch=args.batch, max_src_len=512, max_steps=args.max_length,
-                 max_beam=beam)
-    # each rank gets its own shard of synthetic reads
-    sig_np = synth.synth_chunk_batch(args.batch, 512, seed=1000 + rank, inject_masks=False)
-    lens_np = np.full(args.batch, 512, np.int32)
-    sig = torch.from_numpy(sig_np).to(dev)
-    lens = torch.from_numpy(lens_np).to(dev)
+    def lane(i):
+        try:
+            e = pool.engines[i]
+            with torch.cuda.stream(e.stream):
+                for _ in range(i, n, pool.lanes):
+                    outs[i] = call(e)
+        except BaseException as ex:  # surfaced below
+            errs.append(ex)
+    for e in pool.engines:
+        e.stream.wait_stream(cur)
+    th = [threading.Thread(target=lane, args=(i,)) for i in range(min(pool.lanes, n))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    if errs:
+        raise errs[0]
+    pool.synchronize()
+    return outs[(n - 1) % pool.lanes]
 
-    def step():
-        if args.mode == "greedy":
-            return eng.translate_greedy(sig, lens, lens, max_len=args.max_length, min_len=args.min_length)
-        return eng.translate_beam(sig, lens, lens, beam=args.beam, max_len=args.max_length,
-                                  min_len=args.min_length)
 
-    eng.set_kernel_stamps(not args.no_roofline)  # live launch timing of the roofline kernel (in the graphs)
-    for _ in range(args.warmup):
-        out = step()
+def make_call(args, mode, sig, lens, min_len=None):
+    ml = args.min_length if min_len is None else min_len
+    if mode == "greedy":
+        def call(e):
+            return e.translate_greedy(sig, lens, lens, max_len=args.max_length, min_len=ml)
+        return call
+
+    def call(e):
+        return e.translate_beam(sig, lens, lens, beam=args.beam, max_len=args.max_length, min_len=ml)
+    call.blocking = True
+    return call
+
+
+def timed(pool, n, call, world):
+    """Seconds for n calls between a barrier + device sync on both sides, max over ranks."""
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        out = step()
+    out = run_calls(pool, n, call)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=pool.device)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt, out
+
+
+def run_batch(args, world, rank, dev, cfg, W):
+    from nanodecoder_amd import synth
+    from nanodecoder_amd.engine import EnginePool
+
+    beam = args.beam if args.mode == "beam" else 1
+    eng = EnginePool(cfg, W, device=dev.index, lanes=args.inflight, max_batch=args.batch, max_src_len=512,
+                     max_steps=args.max_length, max_beam=beam)
+    # each rank gets its own shard of synthetic reads
+    sig_np = synth.synth_chunk_batch(args.batch, 512, seed=1000 + rank, inject_masks=False)
+    lens_np = np.full(args.batch, 512, np.int32)
+    sig = torch.from_numpy(sig_np).to(dev)
+    lens = torch.from_numpy(lens_np).to(dev)
+    call = make_call(args, args.mode, sig, lens)
+
+    eng.set_kernel_stamps(not args.no_roofline)  # live launch timing of the roofline kernel (in the graphs)
+    run_calls(eng, max(args.warmup, eng.lanes), call)  # every lane captures its graphs
+    dt, out = timed(eng, args.steps, call, world)
     # bases = base tokens before the first EOS (outside the timed region)
     tok = out["tokens"].cpu().numpy()
     if args.mode == "beam":
         tok = tok[:, 0]
     bases_per_step = count_bases(tok, cfg.eos_idx)
-    t = torch.tensor([dt], dtype=torch.float64, device=dev)
-    if world > 1:
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-    dt = float(t.item())
     samples = float(lens_np.sum()) * args.steps * world
     value = samples / dt
     res = {
@@ -436,19 +495,31 @@ def run_batch(args, world, rank, dev, cfg, W):
         "dtype": "f32 (fp32 values; products as split-fp16 x3 on fp16 MFMA: 22-bit operands, fp32 accumulate)",
         "data": "synthetic reads, random-init weights",
         "config": {"workload": workload(args), "chunks_per_gpu_per_step": args.batch,
-                   "global_batch": args.batch * world, "seq_len": 512, "parallelism": f"read-shard x{world}"},
+                   "global_batch": args.batch * world, "seq_len": 512, "parallelism": f"read-shard x{world}",
+                   "calls_in_flight_per_gpu": eng.lanes},
         "samples_per_sec_per_gpu": round(value / world, 1),
         "bases_per_sec": round(bases_per_step * args.steps * world / dt, 1),
         "timed_seconds": round(dt, 3),
         "min_length": args.min_length,
     }
+    if eng.lanes > 1:
+        # the same calls one at a time (lane 0 only, each joined before the next): per-call latency
+        one = eng.subset(1)
+        n1 = max(3, min(40, args.steps // 4))
+        run_calls(one, 2, call)
+        dt1, _ = timed(one, n1, call, world)
+        res["one_call_in_flight"] = {"value": round(float(lens_np.sum()) * n1 * world / dt1, 1),
+                                     "ms_per_step": round(dt1 / n1 * 1e3, 3), "steps": n1,
+                                     "note": "the same calls with one call on the device at a time: the latency "
+                                             "of one 256-chunk call"}
     alive = None
     if args.mode == "beam":
+        e0 = eng.engines[0]
         res["decoder_steps_executed"] = int(out["steps"].cpu().item())
         # the steps each chunk ran (the reference drops a finished chunk's batch
         # at that step, translate/translator.py:793-823); same inputs, same search
-        rr = eng.translate_beam(sig, lens, lens, beam=args.beam, max_len=args.max_length, min_len=args.min_length,
-                                return_attn=True)
+        rr = e0.translate_beam(sig, lens, lens, beam=args.beam, max_len=args.max_length, min_len=args.min_length,
+                               return_attn=True)
         done = rr["done_step"].cpu().numpy()
         alive = [int((done > s_).sum()) for s_ in range(res["decoder_steps_executed"])]
         res["chunk_steps"] = {"executed_share": round(sum(alive) / (args.batch * len(alive)), 4),
@@ -457,19 +528,15 @@ def run_batch(args, world, rank, dev, cfg, W):
         del rr
         # the forced-100-step worst case: EOS masked at every step (-min_length = max_length)
         n_wc = max(2, min(10, args.steps // 10))
-        for _ in range(2):
-            eng.translate_beam(sig, lens, lens, beam=args.beam, max_len=args.max_length, min_len=args.max_length)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(n_wc):
-            eng.translate_beam(sig, lens, lens, beam=args.beam, max_len=args.max_length, min_len=args.max_length)
-        torch.cuda.synchronize()
-        wc = (time.perf_counter() - t0) / n_wc
+        wcall = make_call(args, "beam", sig, lens, min_len=args.max_length)
+        run_calls(eng, eng.lanes, wcall)
+        wc, _ = timed(eng, n_wc, wcall, world)
+        wc /= n_wc
         res["worst_case_all_steps"] = {"ms_per_step": round(wc * 1e3, 3),
                                        "samples_per_sec_per_gpu": round(float(lens_np.sum()) / wc, 1),
                                        "note": f"min_length {args.max_length}: no chunk finishes before step "
                                                f"{args.max_length}, {n_wc} calls"}
-        step()  # the timed workload's graphs again (kernel stamps below come from this call)
+        run_calls(eng, eng.lanes, call)  # the timed workload's graphs again (kernel stamps below come from these)
         torch.cuda.synchronize()
     extras = {}
     if rank == 0:
@@ -483,14 +550,8 @@ def run_batch(args, world, rank, dev, cfg, W):
         # the same workload with exact fp32 products (nd_set_exact_fp32)
         eng.set_exact_fp32(True)
         n_ex = max(5, min(40, args.steps // 4))
-        for _ in range(2):
-            step()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(n_ex):
-            step()
-        torch.cuda.synchronize()
-        dte = time.perf_counter() - t0
+        run_calls(eng, max(2, eng.lanes), call)
+        dte, _ = timed(eng, n_ex, call, world)
         eng.set_exact_fp32(False)
         extras["exact_fp32"] = {"value_per_gpu": round(float(lens_np.sum()) * n_ex / dte, 1), "unit": "samples/s",
                                 "ms_per_step": round(dte / n_ex * 1e3, 3), "steps": n_ex,
@@ -499,6 +560,43 @@ def run_batch(args, world, rank, dev, cfg, W):
         extras["host_inclusive"] = host_inclusive(args, cfg, eng, sig_np, lens_np)
     res.update(extras)
     return res, eng, sig_np, lens_np
+
+
+def config_legs(args, world, rank, dev):
+    """BASELINE configs[2] and configs[3] in the same run as the headline
+    (fewer calls each): the NanoEncoder model greedy at batch 256, and --fast
+    beam 5 at batch 1024 (random-init weights, -min_length as the headline)."""
+    from nanodecoder_amd import synth
+    from nanodecoder_amd.engine import EnginePool
+    legs = {}
+    n = max(3, args.steps // 4)
+    for key, enc, mode, B in (("configs[2]", "nano", "greedy", 256), ("configs[3]", "transformer", "beam", 1024)):
+        cfg = synth.ModelConfig(encoder_type=enc)
+        W = synth.make_weights(cfg, seed=11, eos_bias=args.eos_bias)
+        beam = args.beam if mode == "beam" else 1
+        pool = EnginePool(cfg, W, device=dev.index, lanes=args.inflight, max_batch=B, max_src_len=512,
+                          max_steps=args.max_length, max_beam=beam)
+        sig = torch.from_numpy(synth.synth_chunk_batch(B, 512, seed=2000 + rank, inject_masks=False)).to(dev)
+        lens = torch.full((B,), 512, dtype=torch.int32, device=dev)
+        call = make_call(args, mode, sig, lens)
+        run_calls(pool, max(2, pool.lanes), call)
+        dt, out = timed(pool, n, call, world)
+        tok = out["tokens"].cpu().numpy()
+        tok = tok[:, 0] if mode == "beam" else tok
+        legs[key] = {"workload": f"{'NanoEncoder (3x BiLSTM)' if enc == 'nano' else '3-layer transformer'} encoder "
+                                 f"+ 3-layer transformer decoder, d_model 256, src_seq_length 512, batch {B}, "
+                                 f"{'greedy' if mode == 'greedy' else f'--fast beam {beam}'}, max_length "
+                                 f"{args.max_length}",
+                     "value": round(B * 512 * n * world / dt, 1), "unit": "samples/s", "n_gpus": world,
+                     "samples_per_sec_per_gpu": round(B * 512 * n / dt, 1),
+                     "bases_per_sec": round(count_bases(tok, cfg.eos_idx) * n * world / dt, 1),
+                     "ms_per_step": round(dt / n * 1e3, 3), "steps": n, "calls_in_flight_per_gpu": pool.lanes}
+        if mode == "beam":
+            legs[key]["decoder_steps_executed"] = int(out["steps"].cpu().item())
+        pool.close()
+        del pool, sig, lens
+        torch.cuda.empty_cache()
+    return legs
 
 
 def host_inclusive(args, cfg, eng, sig_np, lens_np):
@@ -532,13 +630,14 @@ def run_reads(args, world, rank, dev, cfg, W, n_reads_per_gpu):
     in a producer thread; timed region = max over ranks (shard.run_distributed)."""
     import types
     from nanodecoder_amd import shard
-    from nanodecoder_amd.engine import Engine
+    from nanodecoder_amd.engine import EnginePool
     from nanodecoder_amd.translator import Translator
 
     def translator_factory(Wr):
         opt = types.SimpleNamespace(gpu=dev.index, n_best=1, max_length=args.max_length, min_length=args.min_length,
                                     beam_size=1, batch_size=100, engine_max_batch=args.batch)
-        eng = Engine(cfg, Wr, device=dev.index, max_batch=args.batch, max_src_len=512, max_steps=args.max_length)
+        eng = EnginePool(cfg, Wr, device=dev.index, lanes=args.inflight, max_batch=args.batch, max_src_len=512,
+                         max_steps=args.max_length)
         return Translator(cfg, Wr, opt, engine=eng)
 
     g, _ = shard.run_distributed(n_reads_per_gpu * world, translator_factory, lambda: W, dev, batch_size=100,
@@ -575,6 +674,13 @@ def main():
     if args.selftest_cpu:
         return selftest_cpu(args)
     world, rank, local = dist_setup(args)
+    # the library's A/B switches (ND_* environment variables) change the kernel
+    # mix; a headline is only printed with all of them at their defaults
+    from nanodecoder_amd import _lib
+    switches = _lib.switches()
+    if switches and not args.allow_switches:
+        raise SystemExit(f"non-default ND_* switches set: {switches} (unset them, or pass --allow-switches for a "
+                         f"non-headline line)")
     # rehearsal of the multi-rank flow on a one-GPU box: every rank on GPU 0
     # over gloo (RCCL refuses two ranks on one device); the line says so
     share = os.environ.get("ND_BENCH_SHARE_GPU") == "1"
@@ -609,11 +715,16 @@ def main():
         return
 
     res, eng, sig_np, lens_np = run_batch(args, world, rank, dev, cfg, W)
+    if args.config_legs and args.mode == "greedy" and args.encoder == "transformer" and args.batch == 256:
+        res["config_legs"] = config_legs(args, world, rank, dev)
     if args.read_shard and args.mode == "greedy" and args.encoder == "transformer":
         eng.close()  # the read-shard engine replaces it
         res["read_shard"] = run_reads(args, world, rank, dev, cfg, W, max(1024, args.reads // 4))
     if share:
         res["rehearsal"] = f"{world} ranks sharing GPU 0 over gloo (plumbing check, not a measurement)"
+    res["switches"] = switches
+    if switches:
+        res["headline"] = False
     if rank == 0:
         if args.cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(cfg, W, sig_np, lens_np, args)

@@ -206,6 +206,11 @@ int nd_window_reads(const float* d_sig, const int64_t* d_offsets, const int32_t*
 int nd_encode(nd_ctx* ctx, const float* d_signal, const int32_t* d_len, const int32_t* d_span, int32_t B,
               int32_t T, float* d_memory, void* stream);
 
+/* The context's own HIP stream (non-blocking; the translate graphs run on
+ * it).  A caller that enqueues its inputs and reads
+ * its outputs on this stream needs no cross-stream join per call. */
+void* nd_stream(nd_ctx* ctx);
+
 /* Enables/disables hipGraph capture of the translate calls (default on). */
 int nd_set_graphs(nd_ctx* ctx, int enable);
 
@@ -256,6 +261,33 @@ int nd_last_timing(nd_ctx* ctx, float* encode_ms, float* decode_ms);
 void nd_destroy(nd_ctx* ctx);
 const char* nd_last_error(void);
 const char* nd_version(void);
+
+/* ---- diagnostics (no reference counterpart) ----------------------------- */
+
+/* GEMM kernel routes, counted per process each time a GEMM is enqueued (a
+ * graph capture enqueues once; replays are not counted).  Lets a test check
+ * which kernels a workload of a given size runs (gemm.hip launch_gemm_p16 /
+ * launch_gemm pick the kernel from M, N, K). */
+#define ND_ROUTE_P16_SMALL 0   /* gemm_p16_kernel<1,4,64>  (K = 256, few row blocks) */
+#define ND_ROUTE_P16_N64 1     /* gemm_p16_kernel<4,2,128> (K = 256) */
+#define ND_ROUTE_P16_LN128 2   /* gemm_p16_kernel<8,1,256> (K = 256, LN prologue) */
+#define ND_ROUTE_P16S_2X4 3    /* gemm_p16s_kernel<2,4>    (K = 256, LDS-staged, 32-row blocks) */
+#define ND_ROUTE_P16S_2X2 4    /* gemm_p16s_kernel<2,2> */
+#define ND_ROUTE_P16_LONGK 5   /* gemm_p16_kernel<1,8,*>   (K = 512 / 1024 / 2048) */
+#define ND_ROUTE_P16_BIG 6     /* P16 operands on the LDS-tiled row-major kernel (large M) */
+#define ND_ROUTE_TILE256 7     /* gemm_f32_kernel 256x256 tiles */
+#define ND_ROUTE_TILE128 8     /* gemm_f32_kernel 128x128 tiles */
+#define ND_ROUTE_TILE64 9      /* gemm_f32_kernel 64x64 tiles */
+#define ND_ROUTE_N 10
+/* counts[0 .. min(n, ND_ROUTE_N) - 1] <- launches per route since the last
+ * reset; reset != 0 zeroes the counters afterwards. */
+int nd_gemm_routes(int64_t* counts, int32_t n, int32_t reset);
+
+/* The library's run-time switches (ND_* environment variables read by the
+ * kernels' launchers, A/B timing knobs): writes "NAME=value" pairs separated
+ * by ';' for every switch whose environment value differs from its default
+ * into buf (NUL-terminated, truncated to len) and returns their number. */
+int nd_switches(char* buf, int32_t len);
 
 /* ---- op-level entry points (unit tests of individual kernels) ---------- */
 

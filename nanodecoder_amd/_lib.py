@@ -63,6 +63,9 @@ SIGNATURES = {
     "nd_last_timing": (_I, [_P, ctypes.POINTER(_F), ctypes.POINTER(_F)]),
     "nd_set_kernel_stamps": (_I, [_P, _I]),
     "nd_kernel_stamps": (_I, [_P, ctypes.POINTER(_F), ctypes.POINTER(_I)]),
+    "nd_stream": (_P, [_P]),
+    "nd_gemm_routes": (_I, [ctypes.POINTER(ctypes.c_int64), _I, _I]),
+    "nd_switches": (_I, [ctypes.c_char_p, _I]),
     "nd_destroy": (None, [_P]),
     "nd_last_error": (ctypes.c_char_p, []),
     "nd_version": (ctypes.c_char_p, []),
@@ -109,6 +112,24 @@ def lib():
         fn.argtypes = args
     _lib = L
     return L
+
+
+ROUTES = ["p16_small", "p16_n64", "p16_ln128", "p16s_2x4", "p16s_2x2", "p16_longk", "p16_big", "tile256",
+          "tile128", "tile64"]  # include/nanodec.h ND_ROUTE_*
+
+
+def gemm_routes(reset: bool = False):
+    """{route: launches enqueued since the last reset} (nd_gemm_routes)."""
+    c = (ctypes.c_int64 * len(ROUTES))()
+    check(lib().nd_gemm_routes(c, len(ROUTES), int(reset)), "nd_gemm_routes")
+    return dict(zip(ROUTES, list(c)))
+
+
+def switches():
+    """{name: value} of the library's A/B switches set to a non-default value (nd_switches)."""
+    buf = ctypes.create_string_buffer(4096)
+    lib().nd_switches(buf, len(buf))
+    return dict(kv.split("=", 1) for kv in buf.value.decode().split(";") if kv)
 
 
 def check(rc: int, what: str = ""):

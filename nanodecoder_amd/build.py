@@ -63,5 +63,42 @@ def build(force: bool = False, verbose: bool = False) -> str:
     return LIB
 
 
+# Host-side AddressSanitizer build of the C-ABI: engine.hip's host
+# code instrumented, device code not (GPU ASan is unavailable); linked with the
+# regular objects of the other kernels into tests/asan_driver.cpp's driver.
+ASAN_HOST = "-g -Xarch_host -fsanitize=address -Xarch_host -fno-omit-frame-pointer -fno-gpu-sanitize".split()
+ASAN_LINK = "-fsanitize=address -fno-gpu-sanitize".split()
+ASAN_BIN = os.path.join(BUILD, "asan_driver")
+ASAN_SRC = os.path.join(os.path.dirname(HERE), "tests", "asan_driver.cpp")
+
+
+def build_asan(verbose: bool = False) -> str:
+    build(verbose=verbose)
+    objs = [os.path.join(BUILD, os.path.basename(p)[:-4] + ".o") for p in sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+            if os.path.basename(p) != "engine.hip"]
+    eng_src, eng_obj = os.path.join(CSRC, "engine.hip"), os.path.join(BUILD, "asan_engine.o")
+    drv_obj = os.path.join(BUILD, "asan_driver.o")
+    dep_t = _newest_dep()
+    jobs = []
+    if not os.path.exists(eng_obj) or os.path.getmtime(eng_obj) < max(os.path.getmtime(eng_src), dep_t):
+        jobs.append((eng_src, eng_obj))
+    if not os.path.exists(drv_obj) or os.path.getmtime(drv_obj) < max(os.path.getmtime(ASAN_SRC), dep_t):
+        jobs.append((ASAN_SRC, drv_obj))
+    for src, obj in jobs:
+        cmd = [HIPCC] + CFLAGS + ASAN_HOST + ["-c", src, "-o", obj]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc (asan) failed for {os.path.basename(src)}:\n{r.stdout}\n{r.stderr}")
+    deps = [eng_obj, drv_obj] + objs
+    if jobs or not os.path.exists(ASAN_BIN) or os.path.getmtime(ASAN_BIN) < max(os.path.getmtime(o) for o in deps):
+        cmd = [HIPCC, f"--offload-arch={ARCH}"] + ASAN_LINK + ["-o", ASAN_BIN] + deps
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"asan link failed:\n{r.stdout}\n{r.stderr}")
+    return ASAN_BIN
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
+    if "--asan" in sys.argv:
+        print(build_asan(verbose=True))

@@ -350,8 +350,8 @@ enc_attention_h3_kernel(const float* __restrict__ qkv, const float* __restrict__
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         const f32x4 r0 = qraw[j][2 * s2], r1 = qraw[j][2 * s2 + 1];
-        flag_overflow(ovf, fmaxf(absmax4(r0), absmax4(r1)) * (1.0f / ND_SQRT_DH));
         const f32x4 x0 = r0 * qs, x1 = r1 * qs;
+        flag_overflow(ovf, fmaxf(absmax4(x0), absmax4(x1)));  // the values split, log2(e) included
         const float x[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
         esplit8(x, qh[j][s2], ql[j][s2]);
       }

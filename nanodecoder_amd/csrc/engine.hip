@@ -10,6 +10,7 @@
 //   * instantiated hipGraphs of whole translate calls, keyed by shape.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -597,6 +598,21 @@ static hipError_t enqueue_first_embed(nd_ctx* c, int R, hipStream_t s) {
 // dx_part) -> dx (pre final LN).
 static bool use_memory_bank(nd_ctx* c, int rpc) { return c->ctx_path == 0 && rpc * ND_H <= 16 && rpc == 1; }
 
+// The decoder's view of the encoder output: a pure function of (ctx path,
+// exact, T, rpc, encoder type).  Set on the host before every call's graphs
+// run or are captured: a replayed encoder graph does not re-enter
+// enqueue_memory, but the step graphs captured after it read these fields.
+static void set_memory_view(nd_ctx* c, int T, int rpc) {
+  c->bank_h3 = false;
+  c->mem = nullptr;
+  if (!use_memory_bank(c, rpc)) return;
+  const bool tf = c->cfg.encoder_type == ND_ENC_TRANSFORMER;
+  // 512-sample chunks: the split-fp16 fragment bank (LN'd for the transformer,
+  // the NanoEncoder's output as it stands)
+  c->bank_h3 = !c->exact && nd::bank_h3_eligible(T, c->cfg.max_src_len);
+  c->mem = (c->bank_h3 || tf) ? c->mem_p : c->x;  // the NanoEncoder's fp32 output is the bank as it stands
+}
+
 // done: per chunk, nonzero = finished (--fast beam; null otherwise): its rows'
 // tiles and attention workgroups exit without work
 static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, const int* anc, int anc_ld,
@@ -666,22 +682,13 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
 // The decoder's view of the encoder output: the memory bank (greedy) or the
 // per-layer context K/V (beam).
 static hipError_t enqueue_memory(nd_ctx* c, int B, int T, int rpc, hipStream_t s) {
-  c->bank_h3 = false;
+  set_memory_view(c, T, rpc);
   if (!use_memory_bank(c, rpc)) return enqueue_ctxkv(c, B, T, s);
   const bool tf = c->cfg.encoder_type == ND_ENC_TRANSFORMER;
-  if (!c->exact && nd::bank_h3_eligible(T, c->cfg.max_src_len)) {
-    // 512-sample chunks: the split-fp16 fragment bank (LN'd for the transformer,
-    // the NanoEncoder's output as it stands)
-    c->bank_h3 = true;
-    c->mem = c->mem_p;
+  if (c->bank_h3)
     return nd::launch_bank_pack_h3(c->x, tf ? c->enc_ln_g : nullptr, tf ? c->enc_ln_b : nullptr,
                                    reinterpret_cast<uint16_t*>(c->mem_p), B, T, c->ovf, s);
-  }
-  if (!tf) {  // the NanoEncoder's output is the bank as it stands
-    c->mem = c->x;
-    return hipSuccess;
-  }
-  c->mem = c->mem_p;
+  if (!tf) return hipSuccess;  // the NanoEncoder's output is the bank as it stands
   return nd::launch_memory_pack(c->x, c->enc_ln_g, c->enc_ln_b, c->mem_p, B, T, T, s);
 }
 
@@ -1141,6 +1148,7 @@ static int translate_greedy(nd_ctx* c, const float* d_signal, const int32_t* d_l
   }
   if (c->timing) HIPCHK(hipEventRecord(c->ev_a, c->es));
   c->attn_on = d_attn != nullptr;
+  set_memory_view(c, T, 1);
   rc = run_graph(c, key, [&](hipStream_t s) { return enqueue_greedy(c, B, T, max_len, min_len, lp, s, smp); });
   c->attn_on = false;
   if (rc) return rc;
@@ -1196,6 +1204,7 @@ static int translate_beam(nd_ctx* c, const float* d_signal, const int32_t* d_len
   k0.attn = d_attn ? 1 : 0;
   if (c->timing) HIPCHK(hipEventRecord(c->ev_a, c->es));
   c->attn_on = d_attn != nullptr;
+  set_memory_view(c, T, beam);
   rc = run_graph(c, k0, [&](hipStream_t s) -> hipError_t {
     if (c->kstamp_on) LCHK(nd::launch_stamp_reset(c->kstamp, (int)c->dec.size() * c->cfg.max_steps, s));
     LCHK(enqueue_encode(c, B, T, s));
@@ -1311,6 +1320,7 @@ static int translate_classic(nd_ctx* c, const float* d_signal, const int32_t* d_
   k0.excl = op.ignore_mask;
   k0.beta = op.beta;
   c->attn_on = capture;
+  set_memory_view(c, T, beam);
   rc = run_graph(c, k0, [&](hipStream_t s) -> hipError_t {
     if (c->kstamp_on) LCHK(nd::launch_stamp_reset(c->kstamp, (int)c->dec.size() * c->cfg.max_steps, s));
     LCHK(enqueue_encode(c, B, T, s));
@@ -1387,6 +1397,44 @@ int nd_encode(nd_ctx* c, const float* d_signal, const int32_t* d_len, const int3
     HIPCHK(hipMemcpyAsync(d_memory, c->x, (size_t)B * T * c->D * 4, hipMemcpyDeviceToDevice, c->es));
   }
   return release_to(c, cs);
+}
+
+void* nd_stream(nd_ctx* c) { return c ? (void*)c->es : nullptr; }
+
+int nd_gemm_routes(int64_t* counts, int32_t n, int32_t reset) {
+  if (!counts || n < 0) return fail(ND_ERR_ARG, "null argument");
+  for (int r = 0; r < ND_ROUTE_N; ++r) {
+    const long long v = nd::gemm_route_count(r, reset != 0);
+    if (r < n) counts[r] = v;
+  }
+  return ND_OK;
+}
+
+// the A/B switches the launchers read (name, default); nd_switches reports the
+// ones set to something else
+static const struct {
+  const char* name;
+  int def;
+} kSwitches[] = {{"ND_GEMM_F32", 0},   {"ND_GEMM_TILE", 0},    {"ND_GEMM_BKL", 64},     {"ND_GEMM_XCD", 1},
+                 {"ND_P16_XCD", 1},    {"ND_P16_BIG_MIN", 2048}, {"ND_ENC_FFN", 1},     {"ND_QKV_TABLE", 1},
+                 {"ND_HEAD_FUSE", 1},  {"ND_LSTM_F32", 0},     {"ND_LSTM_LIBM", 0},     {"ND_LSTM_SEQ", 4},
+                 {"ND_ENC_ATTN_NQ", 2}, {"ND_ENC_ATTN_GRID", 0}, {"ND_ENC_ATTN_F32", 0}, {"ND_SELF_XCD", 1}};
+
+int nd_switches(char* buf, int32_t len) {
+  std::string out;
+  int n = 0;
+  for (const auto& sw : kSwitches) {
+    const char* e = getenv(sw.name);
+    if (!e || atoi(e) == sw.def) continue;
+    out += (n ? ";" : "") + std::string(sw.name) + "=" + e;
+    ++n;
+  }
+  if (buf && len > 0) {
+    const size_t k = std::min(out.size(), (size_t)len - 1);
+    memcpy(buf, out.data(), k);
+    buf[k] = 0;
+  }
+  return n;
 }
 
 int nd_set_graphs(nd_ctx* c, int enable) {

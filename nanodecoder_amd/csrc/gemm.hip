@@ -19,10 +19,12 @@
 // {mean_j, M2_j} of its column tile; the consuming GEMM merges them (Chan's
 // parallel-variance formula, exact and stable) instead of re-reading whole
 // rows in every column workgroup.
+#include "../../include/nanodec.h"
 #include "common.hpp"
 #include "kernels.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -811,9 +813,19 @@ hipError_t launch_fold_layernorm(const float* W, const float* bias, const float*
     if (ln_ && re_ && rs_) hipLaunchKernelGGL((KERNEL<__VA_ARGS__, true, true, true>), grid, block, 0, s, g);       \
   } while (0)
 
+// kernel routes taken (include/nanodec.h ND_ROUTE_*), counted at enqueue time
+static std::atomic<long long> g_routes[ND_ROUTE_N];
+static void count_route(int r) { g_routes[r].fetch_add(1, std::memory_order_relaxed); }
+
+long long gemm_route_count(int r, bool reset) {
+  if (r < 0 || r >= ND_ROUTE_N) return 0;
+  return reset ? g_routes[r].exchange(0) : g_routes[r].load();
+}
+
 template <int BM, int BN, int WM, int WN, int BK = 32>
 static hipError_t launch_cfg(GemmArgs& g, hipStream_t s) {
   if (g.K % BK != 0) return hipErrorInvalidValue;
+  count_route(BM == 256 ? ND_ROUTE_TILE256 : BM == 128 ? ND_ROUTE_TILE128 : ND_ROUTE_TILE64);
   static const int xcd = [] {
     const char* e = getenv("ND_GEMM_XCD");  // 0: column tile fastest (A/B timing)
     return e ? atoi(e) : 1;
@@ -852,6 +864,8 @@ template <int NT, int KS, int KW>
 static hipError_t launch_p16(GemmArgs& g, hipStream_t s) {
   if (g.N % (NT * 16) != 0 || g.K != KS * KW) return hipErrorInvalidValue;
   dim3 grid(g.N / (NT * 16), (g.M + 15) / 16), block(NT * KS * 64);
+  count_route(g.K != 256 ? ND_ROUTE_P16_LONGK : NT == 1 ? ND_ROUTE_P16_SMALL : NT == 4 ? ND_ROUTE_P16_N64
+                                                                                        : ND_ROUTE_P16_LN128);
   g.xcd_a = p16_xcd_rows((int)grid.x, (int)grid.y, NT);
   g.part_n_out = g.N / 16;
   if (g.Wh)
@@ -870,6 +884,7 @@ template <int BMB, int BNB>
 static hipError_t launch_p16s(GemmArgs& g, hipStream_t s) {
   if (g.K != ND_D || g.N % (BNB * 16) != 0) return hipErrorInvalidValue;
   dim3 grid(g.N / (BNB * 16), (g.M + 16 * BMB - 1) / (16 * BMB)), block(BMB * BNB * 64);
+  count_route(BNB == 4 ? ND_ROUTE_P16S_2X4 : ND_ROUTE_P16S_2X2);
   g.part_n_out = g.N / 16;
   const size_t lds = p16s_lds<BMB, BNB>();
   const bool h3_ = g.Wh != nullptr, ln_ = g.norm, re_ = g.relu, rs_ = g.R != nullptr;
@@ -981,6 +996,7 @@ hipError_t launch_gemm_p16(GemmArgs& g, hipStream_t s) {
     // split-fp16 kernel on P16 activations, with the row-major weight image
     // (measured at M = 5120: QKV 25 -> 18 us, FFN1 59 -> 50, FFN2 71 -> 50;
     // the 256 x 256, K = 256 shapes stay on gemm_p16s, 8 -> 10 us there)
+    count_route(ND_ROUTE_P16_BIG);  // the tile it runs on is counted too
     GemmArgs r = g;
     r.W = nullptr;
     r.Wh = g.Wh_rm;

@@ -73,6 +73,8 @@ hipError_t launch_split_weight(const float* W, int N, int K, uint16_t* Wh, float
 hipError_t launch_pack_p16h(const float* W, int ld, int N, int K, uint16_t* out, float* wscale, hipStream_t s);
 // ND_GEMM_F32=1: the fp32-MFMA kernels everywhere (split images unused)
 bool gemm_f32_forced();
+// launches per GEMM route (include/nanodec.h ND_ROUTE_*) since the last reset
+long long gemm_route_count(int route, bool reset);
 // raises the dynamic-LDS limit of the LDS-staged GEMM kernels (once per process)
 hipError_t init_gemm_attributes();
 // row-major [M, N] with leading dimension ld -> P16 (M, N multiples of 16)

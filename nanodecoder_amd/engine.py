@@ -74,6 +74,14 @@ class Engine:
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
+    @property
+    def stream(self) -> torch.cuda.ExternalStream:
+        """The context's own HIP stream (nd_stream), as a torch stream.  Work
+        enqueued with it current needs no cross-stream join per call."""
+        if getattr(self, "_ext", None) is None:
+            self._ext = torch.cuda.ExternalStream(self._L.nd_stream(self._h), device=self.device)
+        return self._ext
+
     def set_ctx_path(self, path: int):
         """0: memory-bank context attention for greedy (default), 1: per-layer K/V always."""
         _lib.check(self._L.nd_set_ctx_path(self._h, int(path)), "nd_set_ctx_path")
@@ -228,6 +236,123 @@ class Engine:
         _lib.check(self._L.nd_encode(self._h, _ptr(signal), _ptr(lengths), _ptr(spans), B, T, _ptr(mem),
                                      self._stream()), "nd_encode")
         return mem
+
+
+class EnginePool:
+    """Several translate calls in flight on one GPU: ``lanes`` engine contexts
+    of the same model, each on its own HIP stream (its own hardware queue),
+    used round robin.
+
+    One call is a chain of ~2,300 dependent launches, most of them latency
+    bound (decoder steps at 256 rows); a second call's chain on another
+    hardware queue fills the gaps (measured on MI355X, greedy configs[1]:
+    26.8 ms per 256-chunk call alone, 42.1 ms per two calls in flight).
+
+    Interface as Engine's translate_* / encode, with one difference: a call
+    returns before its outputs exist and does NOT join the caller's stream
+    (that join would order the next call behind this one).  The result dict
+    carries ``event`` (recorded on the lane's stream when the outputs are
+    written); wait on it (``wait``) before using the outputs on another stream.
+    A lane waits for the caller's current stream at submission, so inputs
+    produced there are safe; the lane reuses its workspaces in call order, so
+    call k + lanes waits for call k on the same lane."""
+
+    def __init__(self, cfg: ModelConfig, weights: Dict[str, np.ndarray], device: int = 0, lanes: int = 2, **kw):
+        if lanes < 1:
+            raise ValueError("lanes must be >= 1")
+        self.engines = [Engine(cfg, weights, device=device, **kw) for _ in range(lanes)]
+        e0 = self.engines[0]
+        self.cfg, self.device = cfg, e0.device
+        self.max_batch, self.max_src_len, self.max_steps, self.max_beam = (e0.max_batch, e0.max_src_len,
+                                                                           e0.max_steps, e0.max_beam)
+        self._next = 0
+
+    @property
+    def lanes(self) -> int:
+        return len(self.engines)
+
+    def subset(self, n: int) -> "EnginePool":
+        """A pool over the first n lanes (same contexts; e.g. n = 1: one call at a time)."""
+        p = EnginePool.__new__(EnginePool)
+        p.__dict__.update(self.__dict__)
+        p.engines = self.engines[:n]
+        p._next = 0
+        return p
+
+    def _call(self, name, signal, lengths, spans=None, **kw):
+        i = self._next
+        self._next = (i + 1) % len(self.engines)
+        eng = self.engines[i]
+        st = eng.stream
+        st.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(st):
+            r = getattr(eng, name)(signal, lengths, spans, **kw)
+            for t in (signal, lengths, spans):
+                if isinstance(t, torch.Tensor) and t.is_cuda:
+                    t.record_stream(st)  # the caching allocator keeps caller inputs alive for the lane
+            ev = torch.cuda.Event()
+            ev.record(st)
+        r["event"], r["lane"] = ev, i
+        return r
+
+    @staticmethod
+    def wait(result, stream=None):
+        """Order ``stream`` (default: the current stream) after ``result``'s call."""
+        (stream or torch.cuda.current_stream()).wait_event(result["event"])
+        return result
+
+    def translate_greedy(self, signal, lengths, spans=None, **kw):
+        return self._call("translate_greedy", signal, lengths, spans, **kw)
+
+    def translate_sample(self, signal, lengths, spans=None, **kw):
+        return self._call("translate_sample", signal, lengths, spans, **kw)
+
+    def translate_beam(self, signal, lengths, spans=None, **kw):
+        return self._call("translate_beam", signal, lengths, spans, **kw)
+
+    def translate_beam_classic(self, signal, lengths, spans=None, **kw):
+        return self._call("translate_beam_classic", signal, lengths, spans, **kw)
+
+    def encode(self, signal, lengths, spans=None):
+        """Engine.encode on the next lane, joined to the current stream (the memory bank is a tensor)."""
+        eng = self.engines[self._next]
+        self._next = (self._next + 1) % len(self.engines)
+        cur = torch.cuda.current_stream(self.device)
+        eng.stream.wait_stream(cur)
+        with torch.cuda.stream(eng.stream):
+            mem = eng.encode(signal, lengths, spans)
+        cur.wait_stream(eng.stream)
+        mem.record_stream(cur)
+        return mem
+
+    def synchronize(self):
+        """Order the current stream after every lane's calls so far."""
+        cur = torch.cuda.current_stream(self.device)
+        for e in self.engines:
+            cur.wait_stream(e.stream)
+
+    def _each(self, name, *a):
+        for e in self.engines:
+            getattr(e, name)(*a)
+
+    def set_ctx_path(self, path: int):
+        self._each("set_ctx_path", path)
+
+    def set_exact_fp32(self, on: bool):
+        self._each("set_exact_fp32", on)
+
+    def set_kernel_stamps(self, on: bool):
+        self._each("set_kernel_stamps", on)
+
+    def kernel_stamps(self):
+        """Launch durations of the last call's roofline kernel, averaged over the lanes."""
+        st = [e.kernel_stamps() for e in self.engines]
+        n = sum(k for _, k in st)
+        return (sum(u * k for u, k in st) / n if n else 0.0), n
+
+    def close(self):
+        for e in self.engines:
+            e.close()
 
 
 # ---------------------------------------------------------------------------

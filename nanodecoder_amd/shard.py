@@ -227,12 +227,13 @@ def main(argv=None):
     ap.add_argument("--max-length", type=int, default=100)
     ap.add_argument("--min-length", type=int, default=0)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--inflight", type=int, default=2, help="translate calls on the device at once (EnginePool lanes)")
     args = ap.parse_args(argv)
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist.init_process_group("nccl", device_id=dev)
-    from .engine import Engine
+    from .engine import EnginePool
     from .translator import Translator
     cfg = synth.ModelConfig()
 
@@ -242,7 +243,8 @@ def main(argv=None):
     def translator_factory(W):
         opt = argparse.Namespace(gpu=local, n_best=1, max_length=args.max_length, min_length=args.min_length,
                                  beam_size=1, batch_size=args.batch_size, engine_max_batch=args.engine_batch)
-        eng = Engine(cfg, W, device=local, max_batch=args.engine_batch, max_steps=args.max_length)
+        eng = EnginePool(cfg, W, device=local, lanes=args.inflight, max_batch=args.engine_batch,
+                         max_steps=args.max_length)
         return Translator(cfg, W, opt, engine=eng)
 
     g, _ = run_distributed(args.reads, translator_factory, weights_factory, dev, batch_size=args.batch_size,

@@ -33,6 +33,7 @@ import torch
 from . import checkpoint
 from .engine import Engine
 from .engine import Engine as _HipEngine  # the real engine class (tests substitute Engine)
+from .engine import EnginePool
 
 
 class GNMTGlobalScorer:
@@ -168,12 +169,13 @@ class Translator(object):
         buffers (real engine; the host-to-device copies then run async, so the
         next batch is packed while the device works on this one), or plain
         numpy arrays (stand-in engines)."""
-        if not isinstance(self.engine, _HipEngine):
+        if not self._real_engine():
             return np.zeros((B, T), np.float32), np.ones(B, np.int32), np.ones(B, np.int32), None
         if self._pinned is None:
+            # one buffer per call in flight, one being packed, one spare
             cap, tl = self.engine.max_batch, self.engine.max_src_len
             self._pinned = [(torch.empty(cap * tl, dtype=torch.float32).pin_memory(),
-                             torch.empty(2 * cap, dtype=torch.int32).pin_memory()) for _ in range(3)]
+                             torch.empty(2 * cap, dtype=torch.int32).pin_memory()) for _ in range(self._depth() + 2)]
         fbuf, ibuf = self._pinned[self._pin_i % len(self._pinned)]
         self._pin_i += 1
         sig_t = fbuf[: B * T].view(B, T)
@@ -182,6 +184,13 @@ class Translator(object):
         L_t.fill_(1)
         S_t.fill_(1)
         return sig_t.numpy(), L_t.numpy(), S_t.numpy(), (sig_t, L_t, S_t)
+
+    def _real_engine(self) -> bool:
+        return isinstance(self.engine, (_HipEngine, EnginePool))
+
+    def _depth(self) -> int:
+        """Engine calls kept in flight by stream_reads: one per EnginePool lane."""
+        return max(1, int(getattr(self.engine, "lanes", 1)))
 
     def _submit(self, chunks: List[np.ndarray], spans: Sequence[int], groups: Optional[Sequence[int]] = None,
                 attn: bool = False):
@@ -251,7 +260,9 @@ class Translator(object):
                     coverage_penalty=gs.coverage_penalty, beta=gs.beta, stepwise_penalty=self.stepwise_penalty,
                     block_ngram_repeat=self.block_ngram_repeat, ignore_ids=exclusion, cut=cut, return_attn=attn)
             job.update(kind="beam", r=r, grp=grp, sorted_rows=sorted_rows, cut=cut)
-        if isinstance(self.engine, _HipEngine):
+        if "event" in r:  # EnginePool: recorded on the call's lane stream
+            job["event"] = r["event"]
+        elif self._real_engine():
             # fires when this call's outputs are written (the engine's release
             # event is ordered before it on the current stream)
             ev = torch.cuda.Event()
@@ -372,14 +383,17 @@ class Translator(object):
 
     def stream_reads(self, reads: Iterable[Sequence], batch_size: int, attn_debug: bool = False):
         """Generator over many reads (any iterable of chunk lists): chunks are
-        packed across reads into engine batches of max_batch, one batch stays
-        in flight on the device while the next is packed on the host, and
+        packed across reads into engine batches of max_batch, one batch (one
+        per EnginePool lane) stays in flight on the device while the next is
+        packed on the host, and
         (read index, per-chunk results) is yielded as each read completes.
         Each chunk keeps the span of the reference batch it would belong to
         (consecutive ``batch_size`` chunks of its own read), so results equal
         per-read translate()."""
+        import collections
         cap = self.engine.max_batch
-        pending, inflight = [], None
+        depth = self._depth()
+        pending, inflight = [], collections.deque()
         results, remaining = {}, {}
         nb = 0
 
@@ -409,21 +423,17 @@ class Translator(object):
                 for k, c in enumerate(part):
                     pending.append((ri, b0 + k, c, span, nb))
                     if len(pending) == cap:
-                        nxt = submit(pending)
+                        inflight.append(submit(pending))
                         pending = []
-                        if inflight is not None:
-                            for r in collect(inflight):
+                        # `depth` calls stay on the device while the next batch is packed
+                        while len(inflight) > depth:
+                            for r in collect(inflight.popleft()):
                                 yield r, results.pop(r)
-                        inflight = nxt
                 nb += 1
         if pending:
-            nxt = submit(pending)
-            if inflight is not None:
-                for r in collect(inflight):
-                    yield r, results.pop(r)
-            inflight = nxt
-        if inflight is not None:
-            for r in collect(inflight):
+            inflight.append(submit(pending))
+        while inflight:
+            for r in collect(inflight.popleft()):
                 yield r, results.pop(r)
 
     def translate_reads(self, reads: Sequence[Sequence], batch_size: int, attn_debug: bool = False):

@@ -1,0 +1,224 @@
+"""BASELINE.json configs at their real sizes, end to end, against the oracle
+(needs an MI355X).
+
+Which kernels a call runs depends on the batch: at 256 chunks the decoder
+GEMMs take the LDS-staged ``gemm_p16s_kernel`` and the K = 2048 products the
+long-K P16 kernel; at 1024 chunks x beam 5 the LDS-tiled large-M route, and
+the --fast beam's tail segments (few chunks alive) the small-M kernels again.
+The smaller parity tests in test_gpu_parity.py run none of the first.  Each
+test here asserts the route it covers (nd_gemm_routes) and compares with
+oracle/ref_cpu.py (the reference's algorithm, pinned to its own outputs):
+log-probs within 1e-3, identical tokens except after a genuine oracle
+near-tie (top-2 margin < 1e-4).  Reference: translate/translator.py:396-503
+(greedy), :619-825 (--fast beam).
+
+Also here: the EnginePool (several calls in flight on one GPU) against the
+single engine, and a graph-cache regression (the decoder's memory view after
+an exact-fp32 call).
+"""
+import types
+
+import numpy as np
+import pytest
+
+from nanodecoder_amd import synth
+from tests import golden_util as gu
+
+pytestmark = pytest.mark.gpu
+
+LOGP_ATOL = 1e-3
+TIE_MARGIN = 1e-4
+
+
+def _oracle():
+    from oracle import ref_cpu
+    return ref_cpu
+
+
+def _engine(cfg, W, **kw):
+    from nanodecoder_amd.engine import Engine
+    return Engine(cfg, W, device=0, **kw)
+
+
+def _routes(reset=True):
+    from nanodecoder_amd import _lib
+    return _lib.gemm_routes(reset=reset)
+
+
+def _tie_rows(got, exp_tokens, exp_logp):
+    """Rows whose tokens differ from the oracle's; each first difference must
+    be a genuine oracle near-tie.  Returns the set of such rows."""
+    rows = set()
+    for b in range(exp_tokens.shape[0]):
+        d = np.nonzero(got[b] != exp_tokens[b])[0]
+        if d.size:
+            s = int(d[0])
+            top2 = np.sort(exp_logp[b, s])[-2:]
+            assert top2[1] - top2[0] < TIE_MARGIN, (b, s, got[b, s], exp_tokens[b, s], top2)
+            rows.add(b)
+    return rows
+
+
+@pytest.mark.parametrize("encoder", ["transformer", "nano"])
+def test_greedy_config_batch256_vs_oracle(encoder):
+    """configs[1] (3+3 transformer) and configs[2] (NanoEncoder + transformer
+    decoder): 256 chunks x 512 samples, greedy, max_length 100, -min_length 57
+    (the bench's workload, mask samples injected), every chunk against the
+    oracle.  Asserts the M = 256 GEMM kernels ran (gemm_p16s, long-K P16)."""
+    ref = _oracle()
+    cfg = synth.ModelConfig(encoder_type=encoder)
+    W = synth.make_weights(cfg, seed=11, eos_bias=-3.0)
+    B, S, MINL = 256, 100, 57
+    sig = synth.synth_chunk_batch(B, 512, seed=1000)
+    lens = np.full(B, 512, np.int32)
+    eng = _engine(cfg, W, max_batch=B, max_steps=S)
+    _routes()
+    r = eng.translate_greedy(sig, lens, lens, max_len=S, min_len=MINL)  # the bench's graph (no log-prob dump)
+    routes = _routes()
+    assert routes["p16s_2x4"] > 0 and routes["p16_longk"] > 0, routes
+    assert routes["p16_small"] == 0, routes  # the small-batch kernel is not the one at 256 rows
+    rl = eng.translate_greedy(sig, lens, lens, max_len=S, min_len=MINL, return_logp=True)
+    tok = r["tokens"].cpu().numpy()
+    assert (tok == rl["tokens"].cpu().numpy()).all()
+    assert (r["scores"].cpu().numpy() == rl["scores"].cpu().numpy()).all()
+    o = ref.greedy(ref.RefModel(cfg, W), sig, lens, max_length=S, min_length=MINL)
+    ties = _tie_rows(tok, o["tokens"], o["logp"])
+    assert len(ties) <= 3, ties
+    keep = np.array([b not in ties for b in range(B)])
+    lp = rl["logp"].cpu().numpy()
+    assert gu.logp_close(lp[keep], o["logp"][keep], atol=LOGP_ATOL).all()
+    assert np.abs(r["scores"].cpu().numpy()[keep] - o["scores"][keep]).max() < LOGP_ATOL
+    assert int(r["overflow"].cpu()[0]) == 0
+
+
+def test_beam_config3_batch1024_sampled_vs_oracle():
+    """configs[3]: --fast beam 5 on 1024 chunks, max_length 100, -min_length
+    57 (the bench's workload).  Most chunks finish at step ~58; the few that
+    run on are decoded by the tail segments (GraphKey.tail: <= 1/16 of the
+    chunks alive, small-M GEMM kernels).  16 chunks are compared with the
+    oracle: every chunk that ran into the tail plus random others."""
+    ref = _oracle()
+    cfg = synth.ModelConfig()
+    W = synth.make_weights(cfg, seed=11, eos_bias=-3.0)
+    B, S, MINL = 1024, 100, 57
+    sig = synth.synth_chunk_batch(B, 512, seed=2000, inject_masks=False)
+    lens = np.full(B, 512, np.int32)
+    eng = _engine(cfg, W, max_batch=B, max_steps=S, max_beam=5)
+    _routes()
+    r = eng.translate_beam(sig, lens, lens, beam=5, n_best=1, max_len=S, min_len=MINL)  # the bench's graphs
+    routes = _routes()
+    ra = eng.translate_beam(sig, lens, lens, beam=5, n_best=1, max_len=S, min_len=MINL, return_attn=True)
+    tok, sc, ln = (r[k].cpu().numpy() for k in ("tokens", "scores", "lens"))
+    assert (tok == ra["tokens"].cpu().numpy()).all() and (ln == ra["lens"].cpu().numpy()).all()
+    done = ra["done_step"].cpu().numpy()
+    steps = int(r["steps"].cpu()[0])
+    # the segment polls see at most B / 16 chunks alive from some step on: the tail ran
+    alive_at = [int((done > s0).sum()) for s0 in range(10, steps, 10)]
+    assert any(16 * a <= B for a in alive_at), alive_at
+    assert routes["p16_big"] > 0 and routes["p16_longk"] > 0, routes  # large-M route and the tail's small-M kernels
+    tail = [int(i) for i in np.nonzero(done > 60)[0]][:8]
+    rng = np.random.default_rng(5)
+    rest = [int(i) for i in rng.choice(np.setdiff1d(np.arange(B), tail), 16 - len(tail), replace=False)]
+    pick = sorted(tail + rest)
+    exp = ref.fast_beam(ref.RefModel(cfg, W), sig[pick], lens[pick], beam_size=5, n_best=1, max_length=S,
+                        min_length=MINL)
+    for j, i in enumerate(pick):
+        s, p = exp[j][0]
+        assert ln[i, 0] == len(p), (i, ln[i, 0], len(p))
+        assert (tok[i, 0, : len(p)] == p).all(), i
+        assert abs(sc[i, 0] - s) < LOGP_ATOL, (i, sc[i, 0], s)
+
+
+def test_pool_matches_single_engine():
+    """EnginePool (two calls in flight, one engine context and stream each)
+    returns exactly what one engine returns for the same batches, in order,
+    with the lanes overlapping."""
+    import torch
+    from nanodecoder_amd.engine import EnginePool
+    cfg = synth.ModelConfig()
+    W = synth.make_weights(cfg, seed=11, eos_bias=-3.0)
+    B, S = 64, 40
+    batches = [synth.synth_chunk_batch(B, 512, seed=300 + k) for k in range(5)]
+    lens = np.full(B, 512, np.int32)
+    one = _engine(cfg, W, max_batch=B, max_steps=S)
+    exp = [one.translate_greedy(b, lens, lens, max_len=S, min_len=5, return_logp=True) for b in batches]
+    pool = EnginePool(cfg, W, device=0, lanes=2, max_batch=B, max_steps=S)
+    dev_b = [torch.from_numpy(b).cuda() for b in batches]
+    got = [pool.translate_greedy(b, lens, lens, max_len=S, min_len=5, return_logp=True) for b in dev_b]
+    assert [g["lane"] for g in got] == [0, 1, 0, 1, 0]
+    pool.synchronize()
+    for g, e in zip(got, exp):
+        for k in ("tokens", "scores", "logp"):
+            assert torch.equal(g[k].cpu(), e[k].cpu()), k
+    pool.close()
+
+
+def test_translator_reads_with_pool_vs_oracle():
+    """Translator.translate_reads on an EnginePool (two engine batches in
+    flight while the next is packed): identical strings and scores to the
+    oracle run read by read (translate/translator.py:181-369)."""
+    from nanodecoder_amd import frontend
+    from nanodecoder_amd.engine import EnginePool
+    from nanodecoder_amd.translator import Translator
+    ref = _oracle()
+    cfg = synth.ModelConfig()
+    W = synth.make_weights(cfg, seed=11, eos_bias=-1.0)
+    S, bs = 40, 3
+    reads = [frontend.window(frontend.normalize(synth.synth_raw_read(80 + i, n), "median"), 512, 512)
+             for i, n in enumerate((1300, 700, 512, 2049, 300, 1100, 1536, 90, 3000, 800))]
+    pool = EnginePool(cfg, W, device=0, lanes=2, max_batch=4, max_steps=S)
+    opt = types.SimpleNamespace(gpu=0, n_best=1, max_length=S, min_length=4, beam_size=1, batch_size=bs,
+                                engine_max_batch=4)
+    got = Translator(cfg, None, opt, engine=pool).translate_reads(reads, batch_size=bs)
+    m = ref.RefModel(cfg, W)
+    n = 0
+    for ri, chunks in enumerate(reads):
+        es, ep = ref.translate(m, chunks, bs, max_length=S, min_length=4)
+        assert got[ri][1] == ep, ri
+        assert np.abs(np.array(got[ri][0]) - np.array(es)).max() < 1e-3, ri
+        n += len(chunks)
+    assert n > 20
+    pool.close()
+
+
+def _eos_steps(cfg, W, sig, lens, S):
+    """First EOS step of every chunk under greedy (S if none)."""
+    eng = _engine(cfg, W, max_batch=sig.shape[0], max_steps=S)
+    tok = eng.translate_greedy(sig, lens, lens, max_len=S)["tokens"].cpu().numpy()
+    eng.close()
+    hit = tok == cfg.eos_idx
+    return np.where(hit.any(1), hit.argmax(1), S)
+
+
+def test_beam1_segments_captured_after_exact_call():
+    """the decoder's memory view (split-fp16 fragment bank or fp32
+    bank) must follow the call, not the last captured encoder graph.  A
+    beam-1 --fast call that stops early captures only its first 10-step
+    segment; an exact-fp32 call follows; the next split-fp16 beam-1 call
+    replays the cached encoder graph and captures its later segments for the
+    first time.  Its results must equal a fresh engine's."""
+    cfg = synth.ModelConfig()
+    S = 40
+    pool_sig = synth.synth_chunk_batch(96, 512, seed=41, inject_masks=False)
+    lens = np.full(4, 512, np.int32)
+    for eb in (0.5, 0.0, 1.0, -0.5):
+        W = synth.make_weights(cfg, seed=12, eos_bias=eb)
+        st = _eos_steps(cfg, W, pool_sig, np.full(96, 512, np.int32), S)
+        order = np.argsort(st, kind="stable")
+        early, late = order[:4], order[-4:]
+        if st[early].max() < 9 and st[late].min() >= 12:
+            break
+    else:
+        pytest.fail(f"no early/late chunk split found: {np.sort(st)}")
+    eng = _engine(cfg, W, max_batch=4, max_steps=S, max_beam=1)
+    a = eng.translate_beam(pool_sig[early], lens, lens, beam=1, max_len=S)
+    assert int(a["steps"].cpu()[0]) <= 10
+    eng.set_exact_fp32(True)
+    eng.translate_beam(pool_sig[late], lens, lens, beam=1, max_len=S)
+    eng.set_exact_fp32(False)
+    c = eng.translate_beam(pool_sig[late], lens, lens, beam=1, max_len=S)
+    fresh = _engine(cfg, W, max_batch=4, max_steps=S, max_beam=1)
+    f = fresh.translate_beam(pool_sig[late], lens, lens, beam=1, max_len=S)
+    assert int(f["steps"].cpu()[0]) > 10
+    for k in ("tokens", "scores", "lens"):
+        assert (c[k].cpu().numpy() == f[k].cpu().numpy()).all(), k

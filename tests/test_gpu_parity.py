@@ -652,20 +652,31 @@ def test_translate_reads_packed_vs_oracle(beam):
     assert n_chunks > 16
 
 
-def test_split_fp16_range_guard():
+@pytest.mark.parametrize("where", ["ffn", "attn"])
+def test_split_fp16_range_guard(where):
     """Activations beyond fp16's range (|x| >= 65504) in a split-fp16
-    product: the FFN hiddens of encoder layer 0 and decoder layer 1 scaled
-    up 1e5x (their W_2 down 1e5x, so the model's function is unchanged).
-    The engine's split path flags the call (nd_take_overflow) instead of
-    returning infs, the Translator reruns it on exact fp32, and the strings
-    and scores equal the fp32 oracle's.  The unscaled model never trips it."""
+    product.  ffn: the FFN hiddens of encoder layer 0 and decoder layer 1
+    scaled up 1e5x (their W_2 down 1e5x, so the model's function is
+    unchanged).  attn: encoder layer 1's queries scaled up 1e6x and its keys
+    down 1e6x (the scores are unchanged; the split Q * log2(e) / sqrt(32)
+    leaves fp16's range).  The engine's split path flags the call
+    (nd_take_overflow) instead of returning infs, the Translator reruns it on
+    exact fp32, and the strings and scores equal the fp32 oracle's.  The
+    unscaled model never trips it."""
     import types
     from nanodecoder_amd.translator import Translator
     ref = _oracle()
     cfg = synth.ModelConfig()
     W0 = synth.make_weights(cfg, seed=11, eos_bias=-1.0)
     W = dict(W0)
+    if where == "attn":
+        p = "encoder.transformer.1.self_attn."
+        for k, f in (("linear_query", 1e6), ("linear_keys", 1e-6)):
+            W[p + k + ".weight"] = W0[p + k + ".weight"] * np.float32(f)
+            W[p + k + ".bias"] = W0[p + k + ".bias"] * np.float32(f)
     for p in ("encoder.transformer.0.feed_forward", "decoder.transformer_layers.1.feed_forward"):
+        if where != "ffn":
+            break
         W[p + ".w_1.weight"] = W0[p + ".w_1.weight"] * np.float32(1e5)
         W[p + ".w_1.bias"] = W0[p + ".w_1.bias"] * np.float32(1e5)
         W[p + ".w_2.weight"] = W0[p + ".w_2.weight"] * np.float32(1e-5)

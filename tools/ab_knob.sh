@@ -4,7 +4,7 @@ var=$1; vals=$2; shift 2
 R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out; mkdir -p $O; cd $R
 for rep in 1 2; do
   for v in $vals; do
-    env $var=$v timeout -k 10 300 python -u bench.py --steps 60 --warmup 3 --cpu-baseline 0 --exact 0 --host-inclusive 0 \
+    env $var=$v timeout -k 10 300 python -u bench.py --allow-switches --steps 60 --warmup 3 --cpu-baseline 0 --exact 0 --host-inclusive 0 \
       --read-shard 0 "$@" > $O/ab_${var}_${v}_$rep.json 2> $O/ab_${var}_${v}_$rep.err || exit $?
     python3 -c "
 import json,sys; d=json.loads(open('$O/ab_${var}_${v}_$rep.json').read().strip().splitlines()[-1])

@@ -17,7 +17,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
 mkdir -p $O
 step=$1; shift
-SHORT="--steps 5 --warmup 2 --cpu-baseline 0 --exact 0 --host-inclusive 0 --read-shard 0 --no-roofline"
+SHORT="--config-legs 0 --steps 5 --warmup 2 --cpu-baseline 0 --exact 0 --host-inclusive 0 --read-shard 0 --no-roofline"
 case $step in
   test)
     cd $R
@@ -42,7 +42,7 @@ case $step in
     tag=$1; ctrs=$2; shift 2
     cd /tmp && export TMPDIR=/tmp
     timeout -s KILL 240 rocprofv3 --pmc $ctrs --kernel-trace -d $O/$tag -o run --output-format csv -- \
-      python3 $R/bench.py --steps 1 --warmup 1 --cpu-baseline 0 --exact 0 --host-inclusive 0 --read-shard 0 \
+      python3 $R/bench.py --config-legs 0 --steps 1 --warmup 1 --cpu-baseline 0 --exact 0 --host-inclusive 0 --read-shard 0 \
       --no-roofline "$@" > $O/$tag.log 2>&1
     rc=$?; echo "pmc $tag rc=$rc"; exit $rc ;;
   mfma)
@@ -51,7 +51,7 @@ case $step in
     cd /tmp && export TMPDIR=/tmp
     timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F16 SQ_INSTS_VALU_MFMA_MOPS_F32 \
       SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d $O/$tag -o run --output-format csv -- \
-      python3 $R/bench.py --steps 1 --warmup 1 --cpu-baseline 0 --exact 0 --host-inclusive 0 --read-shard 0 \
+      python3 $R/bench.py --config-legs 0 --steps 1 --warmup 1 --cpu-baseline 0 --exact 0 --host-inclusive 0 --read-shard 0 \
       --no-roofline "$@" > $O/$tag.log 2>&1
     rc=$?; echo "mfma $tag rc=$rc"; [ $rc -ne 0 ] && exit $rc
     python3 $R/tools/mfma_summary.py $O/$tag/run_counter_collection.csv $tag $O/${tag}_mfma.json | head -40; exit 0 ;;
@@ -70,5 +70,12 @@ case $step in
     tag=$1; shift; cd $R
     timeout -k 10 600 python -u "$@" > $O/$tag.log 2>&1
     rc=$?; echo "py $tag rc=$rc"; tail -20 $O/$tag.log; exit $rc ;;
+  ptrace)
+    # rocprofv3 --kernel-trace of any python tool (queue ids, start/end per dispatch)
+    tag=$1; shift
+    cd /tmp && export TMPDIR=/tmp
+    timeout -k 10 300 rocprofv3 --kernel-trace -d $O/$tag -o run --output-format csv -- \
+      python3 "$@" > $O/$tag.log 2>&1
+    rc=$?; echo "ptrace $tag rc=$rc"; tail -3 $O/$tag.log; exit $rc ;;
   *) echo "unknown step $step"; exit 2 ;;
 esac
