@@ -66,9 +66,9 @@ def build(force: bool = False, verbose: bool = False) -> str:
 # Host-side AddressSanitizer build of the C-ABI: engine.hip's host
 # code instrumented, device code not (GPU ASan is unavailable); linked with the
 # regular objects of the other kernels into tests/asan_driver.cpp's driver.
-ASAN_HOST = "-g -Xarch_host -fsanitize=address -Xarch_host -fno-omit-frame-pointer -fno-gpu-sanitize".split()
+ASAN_HOST = "-gline-tables-only -Xarch_host -fsanitize=address -Xarch_host -fno-omit-frame-pointer -fno-gpu-sanitize".split()
 ASAN_LINK = "-fsanitize=address -fno-gpu-sanitize".split()
-ASAN_BIN = os.path.join(BUILD, "asan_driver")
+ASAN_BIN = os.path.join(HERE, "asan_driver")  # beside the .so: built files under _build/ stay home
 ASAN_SRC = os.path.join(os.path.dirname(HERE), "tests", "asan_driver.cpp")
 
 

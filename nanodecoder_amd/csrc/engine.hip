@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <string>
 #include <tuple>
 #include <vector>
@@ -798,6 +799,32 @@ extern "C" {
 const char* nd_last_error(void) { return g_err.c_str(); }
 const char* nd_version(void) { return "nanodec_hip 0.1.0 gfx950 fp32-mfma"; }
 
+// Engine streams are recycled, never destroyed: a caller may still hold HIP
+// events recorded on a context's stream (EnginePool results carry one) after
+// the context is gone, and destroying the stream under them leaves the
+// events pointing at a freed queue.  nd_destroy parks its (synchronised)
+// stream here; nd_create takes a parked one first.
+static std::mutex g_streams_mu;
+static std::vector<std::pair<int, hipStream_t>> g_spare_streams;  // (device, stream)
+
+static hipError_t acquire_stream(int dev, hipStream_t* s) {
+  {
+    std::lock_guard<std::mutex> lk(g_streams_mu);
+    for (size_t i = 0; i < g_spare_streams.size(); ++i)
+      if (g_spare_streams[i].first == dev) {
+        *s = g_spare_streams[i].second;
+        g_spare_streams.erase(g_spare_streams.begin() + i);
+        return hipSuccess;
+      }
+  }
+  return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+}
+
+static void release_stream(int dev, hipStream_t s) {
+  std::lock_guard<std::mutex> lk(g_streams_mu);
+  g_spare_streams.emplace_back(dev, s);
+}
+
 int nd_create(const nd_config* cfg, nd_ctx** out) {
   if (!cfg || !out) return fail(ND_ERR_ARG, "null argument");
   *out = nullptr;
@@ -831,7 +858,7 @@ int nd_create(const nd_config* cfg, nd_ctx** out) {
     return rc;
   }
   hipError_t e = nd::init_kernel_attributes();
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->es, hipStreamNonBlocking);
+  if (e == hipSuccess) e = acquire_stream(cfg->device, &c->es);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_out, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreate(&c->ev_a);
@@ -1518,7 +1545,7 @@ void nd_destroy(nd_ctx* c) {
   if (c->h_alive) (void)hipHostFree(c->h_alive);
   for (hipEvent_t e : {c->ev_in, c->ev_out, c->ev_a, c->ev_b, c->ev_c})
     if (e) (void)hipEventDestroy(e);
-  if (c->es) (void)hipStreamDestroy(c->es);
+  if (c->es) release_stream(c->cfg.device, c->es);  // synchronised above; recycled, not destroyed
   delete c;
 }
 

@@ -60,6 +60,30 @@ __device__ __forceinline__ void merge_loaded(const PartRow& v, int P, float& mu,
   mu = m;
   rs = ln_rsqrt(m2 * (1.0f / 256.0f) + ND_LN_EPS);
 }
+// The same merge spread over the 4 lanes l, l ^ 16, l ^ 32, l ^ 48 that share
+// a row (lane >> 4 = q holds partials 4q .. 4q + 3: two loads per lane
+// instead of eight); every lane of the four ends with the row's statistics.
+typedef f32x4 PartQuad[2];  // {mean_4q, M2_4q, mean_4q+1, M2_4q+1}, {.. 4q+2, .. 4q+3}
+__device__ __forceinline__ void load_stats_quad(const float* __restrict__ prow, int q, PartQuad& v) {
+  v[0] = ld4(prow + 8 * q);
+  v[1] = ld4(prow + 8 * q + 4);
+}
+__device__ __forceinline__ void merge_quad(const PartQuad& v, int P, int q, float& mu, float& rs) {
+  const float invP = __builtin_amdgcn_rcpf((float)P), w = 256.0f * invP;
+  const int j = 4 * q;
+  float m = (j < P ? v[0].x : 0.f) + (j + 1 < P ? v[0].z : 0.f) + (j + 2 < P ? v[1].x : 0.f) +
+            (j + 3 < P ? v[1].z : 0.f);
+  m += __shfl_xor(m, 16, 64);
+  m += __shfl_xor(m, 32, 64);
+  m *= invP;
+  const float d0 = v[0].x - m, d1 = v[0].z - m, d2 = v[1].x - m, d3 = v[1].z - m;
+  float m2 = (j < P ? v[0].y + w * d0 * d0 : 0.f) + (j + 1 < P ? v[0].w + w * d1 * d1 : 0.f) +
+             (j + 2 < P ? v[1].y + w * d2 * d2 : 0.f) + (j + 3 < P ? v[1].w + w * d3 * d3 : 0.f);
+  m2 += __shfl_xor(m2, 16, 64);
+  m2 += __shfl_xor(m2, 32, 64);
+  mu = m;
+  rs = ln_rsqrt(m2 * (1.0f / 256.0f) + ND_LN_EPS);
+}
 __device__ __forceinline__ void merge_stats(const float* __restrict__ p, int P, float& mu, float& rs) {
   PartRow v;
   load_stats(p, v);
@@ -540,13 +564,18 @@ __global__ void __launch_bounds__(BMB* BNB * 64) gemm_p16s_kernel(const GemmArgs
   static_assert(AJ * NW == BMB * KB && WJ * NW == BNB * KB, "blocks per wave");
   static_assert(!H3 || AJ % 2 == 0, "H3 stages A block pairs");
   auto aj = [&](int i) { return H3 ? 2 * (wave + (i >> 1) * NW) + (i & 1) : wave + i * NW; };
-  // LN partials first (wave 0: one row per lane of the BMB * 16 staged rows),
-  // then A / W, then bias and residual: straight-line, waits in order
-  static_assert(BMB * 16 <= 64, "one staged row per lane of wave 0");
-  PartRow pr;
+  // LN partials first (every lane: the rows lane & 15 of the BMB row blocks,
+  // the rows its staged A blocks and its output block belong to), then A /
+  // W, then bias and residual: straight-line, waits in order.  The row
+  // statistics stay in registers: no LDS hand-off, no barrier for them (a
+  // wave-0 LDS hand-off measured a corrupted tile when another kernel's
+  // workgroups shared the CU, EnginePool)
+  PartQuad pr[LN ? BMB : 1];
   if constexpr (LN)
-    if (wave == 0)
-      load_stats(g.part_in + (size_t)min(mb0 * 16 + (lane & (BMB * 16 - 1)), MB * 16 - 1) * ND_PART_LD * 2, pr);
+#pragma unroll
+    for (int b = 0; b < BMB; ++b)
+      load_stats_quad(g.part_in + (size_t)min(mb0 * 16 + b * 16 + (lane & 15), MB * 16 - 1) * ND_PART_LD * 2,
+                      lane >> 4, pr[b]);
   f32x4 av[AJ], wv[WJ];
 #pragma unroll
   for (int i = 0; i < AJ; ++i) {
@@ -565,19 +594,13 @@ __global__ void __launch_bounds__(BMB* BNB * 64) gemm_p16s_kernel(const GemmArgs
   const f32x4 bv = ld4((g.bias ? g.bias + nb * 16 : nd_zero16) + 4 * (lane >> 4));
   f32x4 rv = {0.f, 0.f, 0.f, 0.f};
   if constexpr (RESID) rv = reinterpret_cast<const f32x4*>(g.R)[ct];
-  // LayerNorm row statistics: one thread per staged row, into LDS
-  float* st = reinterpret_cast<float*>(sh + (BMB + BNB) * KB * 64);  // [BMB*16][2]
-  if constexpr (LN) {
-    if (tid < BMB * 16) {
-      float mu, rs;
-      merge_loaded(pr, g.part_n_in, mu, rs);
-      st[2 * tid] = mu;
-      st[2 * tid + 1] = rs;
-    }
-  }
+  // LayerNorm row statistics of rows b * 16 + (lane & 15)
+  float smu[BMB], srs[BMB];
+  if constexpr (LN)
+#pragma unroll
+    for (int b = 0; b < BMB; ++b) merge_quad(pr[b], g.part_n_in, lane >> 4, smu[b], srs[b]);
   if constexpr (H3) {
     // normalise and split while staging: every A element converted once per workgroup
-    if constexpr (LN) __syncthreads();
     if constexpr (!LN) {
       float amax = 0.f;
 #pragma unroll
@@ -589,8 +612,8 @@ __global__ void __launch_bounds__(BMB* BNB * 64) gemm_p16s_kernel(const GemmArgs
       const int j = aj(i);
       f32x4 x0 = av[i], x1 = av[i + 1];
       if constexpr (LN) {
-        const int r = (j / KB) * 16 + (lane & 15);
-        const float m_ = st[2 * r], r_ = st[2 * r + 1];
+        const int b = j / KB;  // the block's row block (its row: b * 16 + (lane & 15))
+        const float m_ = smu[b], r_ = srs[b];
         x0 = (x0 - m_) * r_;
         x1 = (x1 - m_) * r_;
       }
@@ -621,8 +644,8 @@ __global__ void __launch_bounds__(BMB* BNB * 64) gemm_p16s_kernel(const GemmArgs
   } else {
     float mu = 0.f, rs = 1.f;
     if constexpr (LN) {
-      mu = st[2 * (rb * 16 + (lane & 15))];
-      rs = st[2 * (rb * 16 + (lane & 15)) + 1];
+      mu = smu[rb];
+      rs = srs[rb];
     }
 #pragma unroll
     for (int f = 0; f < KB; ++f) {
@@ -877,7 +900,7 @@ static hipError_t launch_p16(GemmArgs& g, hipStream_t s) {
 
 template <int BMB, int BNB>
 static constexpr size_t p16s_lds() {
-  return (size_t)(BMB + BNB) * (ND_D / 16) * 64 * sizeof(f32x4) + BMB * 16 * 2 * sizeof(float);
+  return (size_t)(BMB + BNB) * (ND_D / 16) * 64 * sizeof(f32x4);
 }
 
 template <int BMB, int BNB>

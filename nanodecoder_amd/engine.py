@@ -248,11 +248,13 @@ class EnginePool:
     hardware queue fills the gaps (measured on MI355X, greedy configs[1]:
     26.8 ms per 256-chunk call alone, 42.1 ms per two calls in flight).
 
-    Interface as Engine's translate_* / encode, with one difference: a call
-    returns before its outputs exist and does NOT join the caller's stream
-    (that join would order the next call behind this one).  The result dict
-    carries ``event`` (recorded on the lane's stream when the outputs are
-    written); wait on it (``wait``) before using the outputs on another stream.
+    Interface as Engine's translate_* / encode, with one difference: a
+    translate call returns before its outputs exist and does NOT join the
+    caller's stream (that join would order the next call behind this one).
+    The result dict carries ``event`` (recorded on the lane's stream when the
+    outputs are written); wait on it (``wait``) before using the outputs on
+    another stream, and keep them referenced until that use has completed
+    (they are allocated on the lane's stream).
     A lane waits for the caller's current stream at submission, so inputs
     produced there are safe; the lane reuses its workspaces in call order, so
     call k + lanes waits for call k on the same lane."""
@@ -266,6 +268,7 @@ class EnginePool:
         self.max_batch, self.max_src_len, self.max_steps, self.max_beam = (e0.max_batch, e0.max_src_len,
                                                                            e0.max_steps, e0.max_beam)
         self._next = 0
+        self._held = [None] * lanes
 
     @property
     def lanes(self) -> int:
@@ -287,12 +290,15 @@ class EnginePool:
         st.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(st):
             r = getattr(eng, name)(signal, lengths, spans, **kw)
-            for t in (signal, lengths, spans):
-                if isinstance(t, torch.Tensor) and t.is_cuda:
-                    t.record_stream(st)  # the caching allocator keeps caller inputs alive for the lane
             ev = torch.cuda.Event()
             ev.record(st)
-        r["event"], r["lane"] = ev, i
+        # the caller's input tensors stay referenced until the lane's next call
+        # and by the result (the call copies them into its own workspace first
+        # thing).  Not Tensor.record_stream: the caching allocator would record
+        # an event on the lane's stream whenever such a tensor is freed, also
+        # after the pool is closed and the stream destroyed.
+        self._held[i] = (signal, lengths, spans)
+        r["event"], r["lane"], r["inputs"] = ev, i, self._held[i]
         return r
 
     @staticmethod
@@ -314,16 +320,11 @@ class EnginePool:
         return self._call("translate_beam_classic", signal, lengths, spans, **kw)
 
     def encode(self, signal, lengths, spans=None):
-        """Engine.encode on the next lane, joined to the current stream (the memory bank is a tensor)."""
+        """Engine.encode on the next lane's context, joined to the current
+        stream as Engine.encode is (the memory bank is a tensor of the caller's stream)."""
         eng = self.engines[self._next]
         self._next = (self._next + 1) % len(self.engines)
-        cur = torch.cuda.current_stream(self.device)
-        eng.stream.wait_stream(cur)
-        with torch.cuda.stream(eng.stream):
-            mem = eng.encode(signal, lengths, spans)
-        cur.wait_stream(eng.stream)
-        mem.record_stream(cur)
-        return mem
+        return eng.encode(signal, lengths, spans)
 
     def synchronize(self):
         """Order the current stream after every lane's calls so far."""
@@ -352,7 +353,10 @@ class EnginePool:
 
     def close(self):
         for e in self.engines:
+            if getattr(e, "_h", None):
+                e.stream.synchronize()
             e.close()
+        self._held = [None] * len(self.engines)
 
 
 # ---------------------------------------------------------------------------

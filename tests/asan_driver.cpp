@@ -162,6 +162,8 @@ static void gpu_lifecycle(const char* wpath) {
   CHECK(read_weights(wpath, W));
   if (W.empty()) return;
   nd_config cfg = good_config();
+  cfg.position_encoding = 0;  // as the weights file has it
+  for (const auto& t : W) cfg.position_encoding |= t.name == "decoder.embeddings.make_embedding.pe.pe";
   nd_ctx* c = nullptr;
   CHECK(nd_create(&cfg, &c) == ND_OK && c != nullptr);
   if (!c) return;

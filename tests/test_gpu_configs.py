@@ -75,8 +75,9 @@ def test_greedy_config_batch256_vs_oracle(encoder):
     _routes()
     r = eng.translate_greedy(sig, lens, lens, max_len=S, min_len=MINL)  # the bench's graph (no log-prob dump)
     routes = _routes()
-    assert routes["p16s_2x4"] > 0 and routes["p16_longk"] > 0, routes
-    assert routes["p16_small"] == 0, routes  # the small-batch kernel is not the one at 256 rows
+    # 256 rows: the N = 2048 products (query projection, FFN1) on gemm_p16s<2,4>, the QKV products on
+    # gemm_p16s<2,2>, the K = 2048 products on the long-K kernel (Wo, N = K = 256, stays on gemm_p16<1,4,64>)
+    assert routes["p16s_2x4"] > 0 and routes["p16s_2x2"] > 0 and routes["p16_longk"] > 0, routes
     rl = eng.translate_greedy(sig, lens, lens, max_len=S, min_len=MINL, return_logp=True)
     tok = r["tokens"].cpu().numpy()
     assert (tok == rl["tokens"].cpu().numpy()).all()
@@ -129,27 +130,59 @@ def test_beam_config3_batch1024_sampled_vs_oracle():
         assert abs(sc[i, 0] - s) < LOGP_ATOL, (i, sc[i, 0], s)
 
 
-def test_pool_matches_single_engine():
-    """EnginePool (two calls in flight, one engine context and stream each)
-    returns exactly what one engine returns for the same batches, in order,
-    with the lanes overlapping."""
+@pytest.mark.parametrize("encoder,mode", [("transformer", "greedy"), ("nano", "greedy"), ("transformer", "beam")])
+def test_pool_matches_single_engine(encoder, mode):
+    """EnginePool (two calls in flight, one engine context and hardware
+    queue each, their kernels sharing the CUs) returns bit-for-bit what one
+    engine returns for the same batches.  Greedy calls are issued from one
+    host thread; --fast beam calls (host-synchronous segment polls) from one
+    thread per lane, as bench.py runs them."""
+    import threading
     import torch
     from nanodecoder_amd.engine import EnginePool
-    cfg = synth.ModelConfig()
-    W = synth.make_weights(cfg, seed=11, eos_bias=-3.0)
+    cfg = synth.ModelConfig(encoder_type=encoder)
+    W = synth.make_weights(cfg, seed=11, eos_bias=-3.0 if mode == "greedy" else 1.0)
     B, S = 64, 40
-    batches = [synth.synth_chunk_batch(B, 512, seed=300 + k) for k in range(5)]
+    beam = 5 if mode == "beam" else 1
+    batches = [synth.synth_chunk_batch(B, 512, seed=300 + k) for k in range(6)]
     lens = np.full(B, 512, np.int32)
-    one = _engine(cfg, W, max_batch=B, max_steps=S)
-    exp = [one.translate_greedy(b, lens, lens, max_len=S, min_len=5, return_logp=True) for b in batches]
-    pool = EnginePool(cfg, W, device=0, lanes=2, max_batch=B, max_steps=S)
+    keys = ("tokens", "scores", "logp") if mode == "greedy" else ("tokens", "scores", "lens")
+
+    def call(e, b):
+        if mode == "greedy":
+            return e.translate_greedy(b, lens, lens, max_len=S, min_len=5, return_logp=True)
+        return e.translate_beam(b, lens, lens, beam=beam, n_best=2, max_len=S, min_len=3)
+    one = _engine(cfg, W, max_batch=B, max_steps=S, max_beam=beam)
+    exp = [{k: v.cpu() for k, v in call(one, b).items() if k in keys} for b in batches]
+    one.close()
+    pool = EnginePool(cfg, W, device=0, lanes=2, max_batch=B, max_steps=S, max_beam=beam)
     dev_b = [torch.from_numpy(b).cuda() for b in batches]
-    got = [pool.translate_greedy(b, lens, lens, max_len=S, min_len=5, return_logp=True) for b in dev_b]
-    assert [g["lane"] for g in got] == [0, 1, 0, 1, 0]
-    pool.synchronize()
-    for g, e in zip(got, exp):
-        for k in ("tokens", "scores", "logp"):
-            assert torch.equal(g[k].cpu(), e[k].cpu()), k
+    for rnd in range(2):
+        if mode == "greedy":
+            got = [call(pool, b) for b in dev_b]
+            assert [g["lane"] for g in got] == [0, 1] * 3
+            pool.synchronize()
+        else:
+            got = [None] * len(dev_b)
+            cur = torch.cuda.current_stream()
+
+            def lane(i):
+                e = pool.engines[i]
+                with torch.cuda.stream(e.stream):
+                    for k in range(i, len(dev_b), 2):
+                        got[k] = call(e, dev_b[k])
+            for e in pool.engines:
+                e.stream.wait_stream(cur)
+            th = [threading.Thread(target=lane, args=(i,)) for i in range(2)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+            pool.synchronize()
+        torch.cuda.synchronize()
+        for k, (g, e) in enumerate(zip(got, exp)):
+            for key in keys:
+                assert torch.equal(g[key].cpu(), e[key]), (rnd, k, key)
     pool.close()
 
 
