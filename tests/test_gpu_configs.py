@@ -234,7 +234,7 @@ def test_beam1_segments_captured_after_exact_call():
     S = 40
     pool_sig = synth.synth_chunk_batch(96, 512, seed=41, inject_masks=False)
     lens = np.full(4, 512, np.int32)
-    for eb in (0.5, 0.0, 1.0, -0.5):
+    for eb in (2.0, 3.0, 4.0, 5.0, 6.0, 8.0, 10.0):
         W = synth.make_weights(cfg, seed=12, eos_bias=eb)
         st = _eos_steps(cfg, W, pool_sig, np.full(96, 512, np.int32), S)
         order = np.argsort(st, kind="stable")
