@@ -65,6 +65,9 @@ def parse():
     ap.add_argument("--batch", type=int, default=256, help="chunks per GPU per step")
     ap.add_argument("--mode", default="greedy", choices=["greedy", "beam"])
     ap.add_argument("--beam", type=int, default=5)
+    ap.add_argument("--bank-nt-lanes", default="auto",
+                    help="comma list of EnginePool lanes whose memory bank streams with non-temporal loads "
+                         "(auto: every lane when --inflight > 1; none: no lane)")
     ap.add_argument("--inflight", type=int, default=2,
                     help="translate calls on the device at once (EnginePool lanes: one engine context and HIP "
                          "stream each); 1 = one call at a time")
@@ -431,6 +434,14 @@ def run_calls(pool, n, call):
     return outs[(n - 1) % pool.lanes]
 
 
+def nt_lanes(args):
+    if args.bank_nt_lanes == "auto":
+        return None
+    if args.bank_nt_lanes == "none":
+        return []
+    return [int(x) for x in args.bank_nt_lanes.split(",") if x.strip()]
+
+
 def make_call(args, mode, sig, lens, min_len=None):
     ml = args.min_length if min_len is None else min_len
     if mode == "greedy":
@@ -470,7 +481,7 @@ def run_batch(args, world, rank, dev, cfg, W):
 
     beam = args.beam if args.mode == "beam" else 1
     eng = EnginePool(cfg, W, device=dev.index, lanes=args.inflight, max_batch=args.batch, max_src_len=512,
-                     max_steps=args.max_length, max_beam=beam)
+                     max_steps=args.max_length, max_beam=beam, bank_nt_lanes=nt_lanes(args))
     # each rank gets its own shard of synthetic reads
     sig_np = synth.synth_chunk_batch(args.batch, 512, seed=1000 + rank, inject_masks=False)
     lens_np = np.full(args.batch, 512, np.int32)
@@ -496,7 +507,7 @@ def run_batch(args, world, rank, dev, cfg, W):
         "data": "synthetic reads, random-init weights",
         "config": {"workload": workload(args), "chunks_per_gpu_per_step": args.batch,
                    "global_batch": args.batch * world, "seq_len": 512, "parallelism": f"read-shard x{world}",
-                   "calls_in_flight_per_gpu": eng.lanes},
+                   "calls_in_flight_per_gpu": eng.lanes, "bank_nontemporal_lanes": list(eng.bank_nt_lanes)},
         "samples_per_sec_per_gpu": round(value / world, 1),
         "bases_per_sec": round(bases_per_step * args.steps * world / dt, 1),
         "timed_seconds": round(dt, 3),
@@ -575,7 +586,7 @@ def config_legs(args, world, rank, dev):
         W = synth.make_weights(cfg, seed=11, eos_bias=args.eos_bias)
         beam = args.beam if mode == "beam" else 1
         pool = EnginePool(cfg, W, device=dev.index, lanes=args.inflight, max_batch=B, max_src_len=512,
-                          max_steps=args.max_length, max_beam=beam)
+                          max_steps=args.max_length, max_beam=beam, bank_nt_lanes=nt_lanes(args))
         sig = torch.from_numpy(synth.synth_chunk_batch(B, 512, seed=2000 + rank, inject_masks=False)).to(dev)
         lens = torch.full((B,), 512, dtype=torch.int32, device=dev)
         call = make_call(args, mode, sig, lens)

@@ -230,6 +230,12 @@ int nd_set_ctx_path(nd_ctx* ctx, int path);
  * captured graphs of both forms are kept (keyed by it). */
 int nd_set_exact_fp32(nd_ctx* ctx, int enable);
 
+/* Cache policy of the greedy memory bank: nontemporal != 0 streams it with
+ * non-temporal loads (it then does not stay in the Infinity Cache).  For
+ * several contexts on one GPU (EnginePool) whose banks together exceed the
+ * cache.  Default 0.  No reference counterpart. */
+int nd_set_bank_policy(nd_ctx* ctx, int nontemporal);
+
 /* Split-fp16 range guard.  An activation operand the split form carries as
  * fp16 hi/lo leaves the fp16 range from |x| = 65504 on, where the
  * reference's fp32 arithmetic is still finite.  Every kernel that splits an

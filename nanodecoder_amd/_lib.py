@@ -58,6 +58,7 @@ SIGNATURES = {
     "nd_set_graphs": (_I, [_P, _I]),
     "nd_set_timing": (_I, [_P, _I]),
     "nd_set_exact_fp32": (_I, [_P, _I]),
+    "nd_set_bank_policy": (_I, [_P, _I]),
     "nd_take_overflow": (_I, [_P, _P, _P]),
     "nd_set_ctx_path": (_I, [_P, _I]),
     "nd_last_timing": (_I, [_P, ctypes.POINTER(_F), ctypes.POINTER(_F)]),

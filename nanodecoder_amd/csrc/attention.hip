@@ -236,6 +236,9 @@ template <int NQ>
 __global__ void __launch_bounds__(1024 / NQ)
 enc_attention_h3_kernel(const float* __restrict__ qkv, const float* __restrict__ signal, const int* __restrict__ span,
                         float* __restrict__ out, int T, int B, int* ovf) {
+#ifdef ND_SKIP_EATTN  // timing probe only (tools/build_variant.sh): the kernel's marginal cost
+  if (threadIdx.x < 100000) return;
+#endif
   __shared__ __attribute__((aligned(16))) unsigned Kp[2][ENC_MAXT * ENC_KH];  // [hi|lo][key][32 halves + pad]
   __shared__ __attribute__((aligned(16))) unsigned Vp[2][ND_DH * ENC_VH];     // [hi|lo][dim][512 halves + pad]
   __shared__ int kflag[ENC_MAXT];          // 0 = key, 1 = masked (signal == 0), 2 = absent (t >= span)
@@ -643,6 +646,9 @@ __global__ void __launch_bounds__(NW * 64)
 dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cache, const int* __restrict__ anc,
                           int anc_ld, int step, int S, float* __restrict__ out, int rpc, const int* __restrict__ skip,
                           int skip_rpc, QkvRows qr, GreedyHead hd) {
+#ifdef ND_SKIP_SELF  // timing probe only (tools/build_variant.sh): the kernel's marginal cost
+  if (threadIdx.x < 100000) return;
+#endif
   __shared__ float accs[NW * ND_D];
   __shared__ float ms[NW * ND_H], ls[NW * ND_H];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;

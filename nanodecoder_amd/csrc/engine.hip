@@ -96,13 +96,13 @@ struct GraphKey {
   int topk = 1;
   float temp = 0.f;
   int exact = 0;  // exact fp32 products (set by run_graph from the ctx)
+  int bank_nt = 0;  // memory bank streamed non-temporally (set by run_graph from the ctx)
   int tail = 0;   // --fast beam tail segments (nd_ctx.beam_tail)
   bool operator<(const GraphKey& o) const {
     return std::tie(mode, B, T, S, min_len, beam, n_best, seg, logp, alpha, stamp, attn, cov, stepwise, ngram, excl,
-                    beta, topk, temp, exact, tail) < std::tie(o.mode, o.B, o.T, o.S, o.min_len, o.beam, o.n_best,
-                                                              o.seg, o.logp, o.alpha, o.stamp, o.attn, o.cov,
-                                                              o.stepwise, o.ngram, o.excl, o.beta, o.topk, o.temp,
-                                                              o.exact, o.tail);
+                    beta, topk, temp, exact, tail, bank_nt) <
+           std::tie(o.mode, o.B, o.T, o.S, o.min_len, o.beam, o.n_best, o.seg, o.logp, o.alpha, o.stamp, o.attn,
+                    o.cov, o.stepwise, o.ngram, o.excl, o.beta, o.topk, o.temp, o.exact, o.tail, o.bank_nt);
   }
 };
 
@@ -127,6 +127,10 @@ struct nd_ctx {
   // --fast beam: few chunks alive (seen at a segment poll): the decoder GEMMs
   // stay on the small-M P16 kernels (GraphKey.tail)
   bool beam_tail = false;
+  // stream the memory bank with non-temporal loads (nd_set_bank_policy): an
+  // EnginePool lane whose bank should not displace another lane's from the
+  // Infinity Cache
+  bool bank_nt = false;
 
   // weights
   float *enc_lin_w = nullptr, *enc_lin_b = nullptr, *enc_ln_g = nullptr, *enc_ln_b = nullptr;
@@ -663,7 +667,8 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
       LCHK(dg(c->dq1, D, L.pwqk, HD, D, L.bqk, c->dqk, HD).ln(c->dq1_part, pnq).run(s));
       if (c->bank_h3)
         LCHK(nd::launch_dec_bank_h3(c->dqk, reinterpret_cast<const uint16_t*>(c->mem_p), c->sig, c->span,
-                                    (float)c->cfg.pad_idx, c->dU, C, T, s, stamp, dbg, dbg_stride, c->ovf));
+                                    (float)c->cfg.pad_idx, c->dU, C, T, s, stamp, dbg, dbg_stride, c->ovf,
+                                    c->bank_nt));
       else
         LCHK(nd::launch_dec_mem_attention(c->dqk, c->mem, c->sig, c->span, (float)c->cfg.pad_idx, c->dU, C, rpc, T,
                                           T, s, stamp, dbg, dbg_stride));
@@ -772,6 +777,7 @@ static int run_graph(nd_ctx* c, const GraphKey& key, F&& enqueue) {
   GraphKey k = key;
   k.exact = c->exact ? 1 : 0;  // both product forms keep their graphs (the overflow rerun switches)
   k.tail = c->beam_tail ? 1 : 0;
+  k.bank_nt = c->bank_nt ? 1 : 0;
   auto it = c->graphs.find(k);
   if (it == c->graphs.end()) {
     hipGraph_t g = nullptr;
@@ -1478,6 +1484,12 @@ int nd_set_ctx_path(nd_ctx* c, int path) {
     c->graphs.clear();
   }
   c->ctx_path = path;
+  return ND_OK;
+}
+
+int nd_set_bank_policy(nd_ctx* c, int nontemporal) {
+  if (!c) return fail(ND_ERR_ARG, "null ctx");
+  c->bank_nt = nontemporal != 0;  // graphs are keyed by it
   return ND_OK;
 }
 

@@ -440,6 +440,9 @@ __device__ __forceinline__ void split8(f32x4 x0, f32x4 x1, h8& hi, h8& lo) {
 
 template <int NT, int KS, int KW, bool H3, bool LN, bool RELU, bool RESID>
 __global__ void __launch_bounds__(NT* KS * 64) gemm_p16_kernel(const GemmArgs g) {
+#ifdef ND_SKIP_P16  // timing probe only (tools/build_variant.sh): the kernel's marginal cost
+  if (g.M >= 0) return;
+#endif
   constexpr int WAVES = NT * KS;
   constexpr int NF = KW / 16;  // 16-k blocks per wave
   __shared__ f32x4 red[KS > 1 ? WAVES : 1][64];
@@ -547,6 +550,9 @@ __global__ void __launch_bounds__(NT* KS * 64) gemm_p16_kernel(const GemmArgs g)
 // small-M GEMMs (FFN1 / query projections: 256 -> 96 KB per workgroup).
 template <int BMB, int BNB, bool H3, bool LN, bool RELU, bool RESID>
 __global__ void __launch_bounds__(BMB* BNB * 64) gemm_p16s_kernel(const GemmArgs g) {
+#ifdef ND_SKIP_P16  // timing probe only
+  if (g.M >= 0) return;
+#endif
   constexpr int NW = BMB * BNB, KB = ND_D / 16;
   extern __shared__ f32x4 sh[];
   f32x4* As = sh;                  // [BMB][KB][64]  (H3: [BMB][KB/2][hi | lo][64])

@@ -339,10 +339,16 @@ __device__ __forceinline__ f32x4 mfma_h16(bh4 a, bh4 b, f32x4 c) {
 // key row r in a dim block of one plane of the transposed image
 __device__ __forceinline__ int bh_row(int r, int hf) { return 32 * r + 16 * (hf ^ ((r >> 2) & 1)); }
 
+// NT: the bank streamed with non-temporal loads (not kept in the Infinity
+// Cache), for an EnginePool lane whose bank should leave the cache to another
+template <bool NT>
 __global__ void __launch_bounds__(BH_NW * 64)
 dec_bank_h3_kernel(const float* __restrict__ qp, const f32x4* __restrict__ bank, const float* __restrict__ signal,
                    const int* __restrict__ span, float pad_val, float* __restrict__ out, int T,
                    unsigned long long* stamp, float* __restrict__ dbg, size_t dbg_stride, int* ovf) {
+#ifdef ND_SKIP_BANK  // timing probe only (tools/build_variant.sh): the kernel's marginal cost
+  if (threadIdx.x < 100000) return;
+#endif
   const unsigned long long t_entry = wall_clock64();  // the timing stamp's start (published below)
   extern __shared__ float lds[];
   const int c = blockIdx.x, lane = threadIdx.x & 63;
@@ -367,7 +373,11 @@ dec_bank_h3_kernel(const float* __restrict__ qp, const f32x4* __restrict__ bank,
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
 #if BH_GLOBAL
-      f[i] = bank[((size_t)c * BH_KB * 16 + (kb0 + kbs * (h >> 1)) * 16 + 8 * (h & 1) + i) * 64 + lane];
+      const f32x4* p = bank + ((size_t)c * BH_KB * 16 + (kb0 + kbs * (h >> 1)) * 16 + 8 * (h & 1) + i) * 64 + lane;
+      if constexpr (NT)
+        f[i] = __builtin_nontemporal_load(p);
+      else
+        f[i] = *p;
 #else
       f[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                            rsrc, voff, ((kb0 + kbs * (h >> 1)) * 16 + 8 * (h & 1) + i) * 1024, 0));
@@ -636,11 +646,16 @@ hipError_t launch_bank_pack_h3(const float* x, const float* ln_g, const float* l
 
 hipError_t launch_dec_bank_h3(const float* qp, const uint16_t* bank, const float* signal, const int* span,
                               float pad_val, float* out, int C, int T, hipStream_t s, unsigned long long* stamp,
-                              float* attn_dbg, size_t dbg_stride, int* ovf) {
+                              float* attn_dbg, size_t dbg_stride, int* ovf, bool nt) {
   if (T < 1 || T > 512 || C < 1) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(dec_bank_h3_kernel, dim3(C), dim3(BH_NW * 64), BH_LDS, s, qp,
-                     reinterpret_cast<const f32x4*>(bank), signal, span, pad_val, out, T, stamp, attn_dbg,
-                     dbg_stride, ovf);
+  if (nt)
+    hipLaunchKernelGGL(dec_bank_h3_kernel<true>, dim3(C), dim3(BH_NW * 64), BH_LDS, s, qp,
+                       reinterpret_cast<const f32x4*>(bank), signal, span, pad_val, out, T, stamp, attn_dbg,
+                       dbg_stride, ovf);
+  else
+    hipLaunchKernelGGL(dec_bank_h3_kernel<false>, dim3(C), dim3(BH_NW * 64), BH_LDS, s, qp,
+                       reinterpret_cast<const f32x4*>(bank), signal, span, pad_val, out, T, stamp, attn_dbg,
+                       dbg_stride, ovf);
   return hipGetLastError();
 }
 
@@ -734,7 +749,11 @@ hipError_t init_mem_attributes() {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mem_lds_bytes());
     if (e != hipSuccess) return e;
   }
-  return hipFuncSetAttribute((const void*)dec_bank_h3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, BH_LDS);
+  const hipError_t e =
+      hipFuncSetAttribute((const void*)dec_bank_h3_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, BH_LDS);
+  return e != hipSuccess ? e
+                         : hipFuncSetAttribute((const void*)dec_bank_h3_kernel<true>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, BH_LDS);
 }
 
 }  // namespace nd

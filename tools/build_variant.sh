@@ -9,6 +9,7 @@ python3 -c "import sys; sys.path.insert(0, '$R'); from nanodecoder_amd import bu
 mkdir -p $R/tools/_ab /tmp/ndvar
 objs=""
 for o in $R/nanodecoder_amd/_build/*.o; do
+  case $(basename $o) in asan_*) continue ;; esac
   if [ "$(basename $o .o).hip" = "$src" ]; then
     /opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 --offload-arch=gfx950 -munsafe-fp-atomics -I$R/nanodecoder_amd/csrc \
       -I$R/include $flags -c $R/nanodecoder_amd/csrc/$src -o /tmp/ndvar/$name.o
