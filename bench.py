@@ -68,7 +68,7 @@ def parse():
     ap.add_argument("--bank-nt-lanes", default="auto",
                     help="comma list of EnginePool lanes whose memory bank streams with non-temporal loads "
                          "(auto: every lane when --inflight > 1; none: no lane)")
-    ap.add_argument("--inflight", type=int, default=2,
+    ap.add_argument("--inflight", type=int, default=3,
                     help="translate calls on the device at once (EnginePool lanes: one engine context and HIP "
                          "stream each); 1 = one call at a time")
     ap.add_argument("--encoder", default="transformer", choices=["transformer", "nano"])
@@ -252,7 +252,7 @@ def count_bases(tok: np.ndarray, eos: int) -> int:
 
 
 # ----------------------------------------------------------------- roofline
-def kernel_roofline(eng, B, mode, beam, encoder="transformer", alive=None):
+def kernel_roofline(eng, B, mode, beam, encoder="transformer", alive=None, secondary=True):
     """Dominant kernel of the translate step, timed LIVE: every launch of it
     inside the timed graph replays carries in-kernel wall-clock stamps
     (first workgroup start, last workgroup end; Engine.set_kernel_stamps), and
@@ -300,6 +300,8 @@ def kernel_roofline(eng, B, mode, beam, encoder="transformer", alive=None):
            "measured_copy_gbs": HBM_MEASURED}
     out.update(extra)
     dev = eng.device
+    if not secondary:
+        return out
     if encoder == "nano":
         out["lstm_kernel"] = lstm_view(dev, B, T)
         return out
@@ -513,7 +515,14 @@ def run_batch(args, world, rank, dev, cfg, W):
         "timed_seconds": round(dt, 3),
         "min_length": args.min_length,
     }
+    roof_iso = None
+    greedy_roof = rank == 0 and not args.no_roofline and args.mode == "greedy"
     if eng.lanes > 1:
+        if greedy_roof:
+            # the roofline kernel's launches inside the timed region, sharing the GPU with the other lanes
+            res["roofline_pooled"] = kernel_roofline(eng, args.batch, args.mode, beam, args.encoder, secondary=False)
+            res["roofline_pooled"]["timing"] = ("in-kernel wall-clock stamps, launches of the last timed call of "
+                                                "every lane (the other lanes' kernels run beside them)")
         # the same calls one at a time (lane 0 only, each joined before the next): per-call latency
         one = eng.subset(1)
         n1 = max(3, min(40, args.steps // 4))
@@ -523,6 +532,11 @@ def run_batch(args, world, rank, dev, cfg, W):
                                      "ms_per_step": round(dt1 / n1 * 1e3, 3), "steps": n1,
                                      "note": "the same calls with one call on the device at a time: the latency "
                                              "of one 256-chunk call"}
+        if greedy_roof:
+            # the kernel with the GPU to itself (as rocprof's serialised kernel trace times it)
+            roof_iso = kernel_roofline(one, args.batch, args.mode, beam, args.encoder)
+            roof_iso["timing"] = ("in-kernel wall-clock stamps, launches of the last call of the timed "
+                                  "one-call-in-flight leg (the kernel alone on the GPU)")
     alive = None
     if args.mode == "beam":
         e0 = eng.engines[0]
@@ -551,7 +565,9 @@ def run_batch(args, world, rank, dev, cfg, W):
         torch.cuda.synchronize()
     extras = {}
     if rank == 0:
-        if not args.no_roofline:
+        if roof_iso is not None:
+            extras["roofline"] = roof_iso
+        elif not args.no_roofline:
             extras["roofline"] = kernel_roofline(eng, args.batch, args.mode, beam, args.encoder, alive)
         eng.set_kernel_stamps(False)
         mv = None if args.no_roofline else mfma_view(args, eng, sig, lens, dt / args.steps * 1e3)
