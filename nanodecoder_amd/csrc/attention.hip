@@ -778,7 +778,7 @@ hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* 
   if (qr.tok && (qr.V < 1 || qr.tok0 < 0 || qr.tok0 >= qr.V)) return hipErrorInvalidValue;
   if (head) {
     if (!qr.tok || anc || skip || rpc != 1 || step < 1 || head->V != qr.V || head->V > SELF_TABV ||
-        head->S != max_steps)
+        head->S > max_steps)
       return hipErrorInvalidValue;
     const hipError_t e = check_greedy_head(*head);
     if (e != hipSuccess) return e;

@@ -608,6 +608,25 @@ def test_greedy_vs_oracle_batch32(itos):
     assert gu.logp_close(got_lp[same], o["logp"][same], atol=LOGP_ATOL).all()
 
 
+def test_greedy_short_max_len_vs_oracle():
+    """A call with max_len below the context's max_steps: the head-fused
+    self-attention's token history has the call's max_len as its stride, the
+    layer-0 cache the context's max_steps."""
+    ref = _oracle()
+    cfg = synth.ModelConfig()
+    W = synth.make_weights(cfg, seed=11, eos_bias=-3.0)
+    sig = synth.synth_chunk_batch(32, 512, seed=5)
+    lens = np.full(32, 512, np.int32)
+    eng = _engine(cfg, W, max_batch=32, max_steps=100)
+    r = eng.translate_greedy(sig, lens, lens, max_len=37, return_logp=True)
+    o = ref.greedy(ref.RefModel(cfg, W), sig, lens, max_length=37)
+    got_tok = r["tokens"].cpu().numpy()
+    assert got_tok.shape == (32, 37)
+    assert _compare_tokens(got_tok, o["tokens"], o["logp"]) <= 1
+    same = (got_tok == o["tokens"]).all(axis=1)
+    assert gu.logp_close(r["logp"].cpu().numpy()[same], o["logp"][same], atol=LOGP_ATOL).all()
+
+
 def _reads_for_packing():
     """Median/MAD-normalised synthetic reads windowed at 512: short last
     chunks, one-chunk reads, a read shorter than a chunk."""
