@@ -348,6 +348,14 @@ int nd_op_pack_p16h(const float* W, int32_t N, int32_t K, uint16_t* out, float* 
  * hidden value leaves the fp16 range. */
 int nd_op_enc_ffn(const float* y, const uint16_t* w1h, float w1s, const float* b1, const uint16_t* w2h, float w2s,
                   const float* b2, float* x, float* xpart, int32_t M, int32_t F, int32_t* overflow, void* stream);
+/* The same block with the attention's output projection folded in front
+ * (encoder/transformer.py:45-54, one launch for the rest of the layer):
+ * y = x_in + att Wo^T + bo, then x = y + W2 relu(W1' LN(y) + b1') + b2.
+ * woh: P16H image of Wo [256, 256] with its scale wos.  x may alias x_in
+ * (the engine updates the layer's rows in place); att must not. */
+int nd_op_enc_ffn_wo(const float* att, const float* x_in, const uint16_t* woh, float wos, const float* bo,
+                     const uint16_t* w1h, float w1s, const float* b1, const uint16_t* w2h, float w2s, const float* b2,
+                     float* x, float* xpart, int32_t M, int32_t F, int32_t* overflow, void* stream);
 
 int nd_op_gemm_p16_split(const float* A, const uint16_t* Wh, float wscale, const float* bias, const float* R, float* C,
                          int32_t M, int32_t N, int32_t K, const float* part_in, int32_t part_n_in, float* part_out,

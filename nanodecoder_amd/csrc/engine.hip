@@ -61,6 +61,9 @@ struct EncLayer {
   // P16H images of W1' (LN folded) and W2 for the fused FFN block (ffn.hip)
   uint16_t *w1h = nullptr, *w2h = nullptr;
   float w1s = 1.f, w2s = 1.f;
+  // P16H image of Wo, folded into the FFN block's launch (ffn.hip WO)
+  uint16_t* woh = nullptr;
+  float wos = 1.f;
 };
 struct DecLayer {
   float *ln1_g, *ln1_b, *wqkv, *bqkv, *wo, *bo, *ln2_g, *ln2_b, *cwq, *cbq, *cwo, *cbo, *fln_g, *fln_b, *w1, *b1,
@@ -518,6 +521,16 @@ static bool enc_ffn_fused(const nd_ctx* c, const EncLayer& L) {
   return on && !c->exact && L.w1h != nullptr && !nd::gemm_f32_forced();
 }
 
+// the attention's output projection folded into the fused FFN block's launch
+// (y never written); ND_ENC_WO=0 keeps the Wo GEMM (A/B timing)
+static bool enc_wo_fused(const nd_ctx* c, const EncLayer& L) {
+  static const bool on = [] {
+    const char* e = getenv("ND_ENC_WO");
+    return !(e && atoi(e) == 0);
+  }();
+  return on && enc_ffn_fused(c, L) && L.woh != nullptr;
+}
+
 static hipError_t enqueue_encode_transformer(nd_ctx* c, int B, int T, hipStream_t s) {
   const int M = B * T, D = c->D, F = c->F;
   LCHK(nd::launch_enc_embed(c->sig, c->enc_lin_w, c->enc_lin_b, c->x, c->x_part, B, T, s));
@@ -526,6 +539,16 @@ static hipError_t enqueue_encode_transformer(nd_ctx* c, int B, int T, hipStream_
     // encoder/transformer.py:36-54
     LCHK(G(c->x, D, L.nwqkv, 3 * D, D, L.nbqkv, c->big, 3 * D, M).h3(c).ln(c->x_part, pnx).run(s));
     LCHK(nd::launch_enc_attention(c->big, c->sig, c->span, c->att, B, T, s, c->exact, c->ovf));
+    if (enc_wo_fused(c, L)) {  // Wo + residual, LN, FFN in one launch; the layer's rows updated in place
+      nd::EncWo wo;
+      wo.att = c->att;
+      wo.woh = L.woh;
+      wo.wos = L.wos;
+      wo.bo = L.bo;
+      LCHK(nd::launch_enc_ffn(c->x, L.w1h, L.w1s, L.nb1, L.w2h, L.w2s, L.b2, c->x, c->x_part, M, F, c->ovf, s, &wo));
+      pnx = 1;
+      continue;
+    }
     LCHK(G(c->att, D, L.wo, D, D, L.bo, c->y, D, M).h3(c).res(c->x, D).stats(c->y_part).run(s, &pny));
     if (enc_ffn_fused(c, L)) {  // position_ffn.py:27-40 in one launch: the hidden stays on chip
       LCHK(nd::launch_enc_ffn(c->y, L.w1h, L.w1s, L.nb1, L.w2h, L.w2s, L.b2, c->x, c->x_part, M, F, c->ovf, s));
@@ -1103,6 +1126,8 @@ int nd_finalize(nd_ctx* c) {
         if (!L.w2h && (e_ = dalloc(c, &L.w2h, (size_t)2 * F * D)) != hipSuccess) return fail(ND_ERR_HIP, "alloc");
         HIPCHK(nd::launch_pack_p16h(L.nw1, D, F, D, L.w1h, &L.w1s, c->es));
         HIPCHK(nd::launch_pack_p16h(L.w2, F, D, F, L.w2h, &L.w2s, c->es));
+        if (!L.woh && (e_ = dalloc(c, &L.woh, (size_t)2 * D * D)) != hipSuccess) return fail(ND_ERR_HIP, "alloc");
+        HIPCHK(nd::launch_pack_p16h(L.wo, D, D, D, L.woh, &L.wos, c->es));
       }
     }
     HIPCHK(mk(c->cfg.encoder_type == ND_ENC_TRANSFORMER ? c->nctxkv_w : c->ctxkv_w, L2, D));
@@ -1451,7 +1476,8 @@ static const struct {
 } kSwitches[] = {{"ND_GEMM_F32", 0},   {"ND_GEMM_TILE", 0},    {"ND_GEMM_BKL", 64},     {"ND_GEMM_XCD", 1},
                  {"ND_P16_XCD", 1},    {"ND_P16_BIG_MIN", 2048}, {"ND_ENC_FFN", 1},     {"ND_QKV_TABLE", 1},
                  {"ND_HEAD_FUSE", 1},  {"ND_LSTM_F32", 0},     {"ND_LSTM_LIBM", 0},     {"ND_LSTM_SEQ", 4},
-                 {"ND_ENC_ATTN_NQ", 2}, {"ND_ENC_ATTN_GRID", 0}, {"ND_ENC_ATTN_F32", 0}, {"ND_SELF_XCD", 1}};
+                 {"ND_ENC_ATTN_NQ", 2}, {"ND_ENC_ATTN_GRID", 0}, {"ND_ENC_ATTN_F32", 0}, {"ND_SELF_XCD", 1},
+                 {"ND_ENC_WO", 1}};
 
 int nd_switches(char* buf, int32_t len) {
   std::string out;
@@ -1617,6 +1643,21 @@ int nd_op_enc_ffn(const float* y, const uint16_t* w1h, float w1s, const float* b
   if (int rc = ensure_attributes()) return rc;
   hipError_t e = nd::launch_enc_ffn(y, w1h, w1s, b1, w2h, w2s, b2, x, xpart, M, F, overflow, (hipStream_t)stream);
   if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("enc_ffn: ") + hipGetErrorString(e));
+  return ND_OK;
+}
+
+int nd_op_enc_ffn_wo(const float* att, const float* x_in, const uint16_t* woh, float wos, const float* bo,
+                     const uint16_t* w1h, float w1s, const float* b1, const uint16_t* w2h, float w2s, const float* b2,
+                     float* x, float* xpart, int32_t M, int32_t F, int32_t* overflow, void* stream) {
+  if (int rc = ensure_attributes()) return rc;
+  nd::EncWo wo;
+  wo.att = att;
+  wo.woh = woh;
+  wo.wos = wos;
+  wo.bo = bo;
+  hipError_t e =
+      nd::launch_enc_ffn(x_in, w1h, w1s, b1, w2h, w2s, b2, x, xpart, M, F, overflow, (hipStream_t)stream, &wo);
+  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("enc_ffn_wo: ") + hipGetErrorString(e));
   return ND_OK;
 }
 

@@ -37,7 +37,19 @@
 // issued a whole step before it is read.  Raw s_barrier + explicit vmcnt
 // waits (a __syncthreads would drain the in-flight copies).  Row statistics
 // of x (for the next LayerNorm) come out of the epilogue exactly, from whole
-// rows (one partial).
+// rows (one partial).  The residual and b2 are the accumulators' initial
+// value ((y + b2) * 2^s): the epilogue reads nothing.
+//
+// WO (the attention block's output projection folded in front,
+// encoder/transformer.py:45-47): the workgroup first computes its rows of
+//
+//   y = x + att Wo^T + bo                       (the accumulators start at (x + bo) * 2^s_o)
+//
+// with Wo's P16H image streamed through the W1 slots in 8 slices of 32
+// output columns (each a phase-1 product against the split attention rows),
+// whose out^T tiles are exactly y in the P16 k-permutation: its LayerNorm and
+// split run in registers, and y never goes to HBM (the unfused form wrote it
+// from a GEMM and read it back twice).
 #include "common.hpp"
 #include "kernels.hpp"
 
@@ -89,11 +101,14 @@ __device__ __forceinline__ void ff_copy_w2(const char* w2h, int kp, int j, char*
 // RG = 1 (8 waves, two per SIMD).  RG = 2 (one wave per SIMD, each weight
 // operand read from LDS feeding 6 MFMAs) measured 1.8x slower at M = 131072:
 // its 512 registers spill and no second wave covers the LDS latency.
-template <int RG>
+// WO: y is the block's residual input (the layer input x; x may alias it:
+// a workgroup reads its rows before it writes them), att the attention
+// output.  !WO: y is the FFN's input.
+template <int RG, bool WO>
 __global__ void __launch_bounds__(FF_BM / (16 * RG) * 64)
-enc_ffn_kernel(const float* __restrict__ y, const uint16_t* __restrict__ w1h, float w1s, const float* __restrict__ b1,
-               const uint16_t* __restrict__ w2h, float w2s, const float* __restrict__ b2, float* __restrict__ x,
-               float* __restrict__ xpart, int M, int F, int* ovf) {
+enc_ffn_kernel(const float* y, const uint16_t* __restrict__ w1h, float w1s, const float* __restrict__ b1,
+               const uint16_t* __restrict__ w2h, float w2s, const float* __restrict__ b2, float* x,
+               float* __restrict__ xpart, int M, int F, int* ovf, EncWo wo) {
 #ifdef ND_SKIP_FFN  // timing probe only (tools/build_variant.sh): the kernel's marginal cost
   if (threadIdx.x < 100000) return;
 #endif
@@ -121,19 +136,16 @@ enc_ffn_kernel(const float* __restrict__ y, const uint16_t* __restrict__ w1h, fl
   // k-block kb the 8 columns 32 kb + {4q..4q+3, 16+4q..16+4q+3} (the P16
   // k-permutation), LayerNorm'd (two-pass statistics over the 4 lanes
   // q = 0..3 that hold the row, as torch) and split: phase 1's B operand,
-  // resident for the whole d_ff walk
+  // resident for the whole d_ff walk.  The lane's out^T accumulator tiles
+  // nt = 2 kb, 2 kb + 1 hold the same columns (out[row][16 nt + 4q + i])
   fh8 yh[RG][8], yl[RG][8];
+  f32x4 acc[RG][16];  // out^T tiles: lane holds out[row g][16 nt + 4q + i]
   int row[RG];
-#pragma unroll
-  for (int g = 0; g < RG; ++g) {
-    row[g] = blockIdx.x * FF_BM + (wave * RG + g) * 16 + li;
-    const float* yr = y + (size_t)min(row[g], M - 1) * ND_D + 4 * q;
-    f32x4 ya[8], yb[8];
-#pragma unroll
-    for (int kb = 0; kb < 8; ++kb) {
-      ya[kb] = ld4(yr + 32 * kb);
-      yb[kb] = ld4(yr + 32 * kb + 16);
-    }
+  const float rw2 = 1.0f / w2s;  // 2^s: exact
+  // y (pre-LN, fp32, in the accumulator layout) -> the split LN(y) and the
+  // accumulators' initial value (y + b2) 2^s (b2 from bsrc: global, or LDS
+  // once the copies are in flight: a global load then would wait for them)
+  auto ln_split = [&](int g, f32x4 (&ya)[8], f32x4 (&yb)[8], const float* bsrc) {
     float s = 0.f;
 #pragma unroll
     for (int kb = 0; kb < 8; ++kb)
@@ -152,19 +164,104 @@ enc_ffn_kernel(const float* __restrict__ y, const uint16_t* __restrict__ w1h, fl
     v2 += __shfl_xor(v2, 32, 64);
     const float rs = ln_rsqrt(v2 * (1.0f / ND_D) + ND_LN_EPS);
 #pragma unroll
-    for (int kb = 0; kb < 8; ++kb) ff_split((ya[kb] - mu) * rs, (yb[kb] - mu) * rs, yh[g][kb], yl[g][kb]);
+    for (int kb = 0; kb < 8; ++kb) {
+      ff_split((ya[kb] - mu) * rs, (yb[kb] - mu) * rs, yh[g][kb], yl[g][kb]);
+      acc[g][2 * kb] = (ya[kb] + ld4(bsrc + 32 * kb + 4 * q)) * rw2;
+      acc[g][2 * kb + 1] = (yb[kb] + ld4(bsrc + 32 * kb + 16 + 4 * q)) * rw2;
+    }
+  };
+  auto p1_mfma = [&](fh8 wh, fh8 wl, int t, int kb, f32x4 (&h)[RG][2]) {
+#pragma unroll
+    for (int g = 0; g < RG; ++g) {
+      h[g][t] = ffma16(wh, yl[g][kb], h[g][t]);
+      h[g][t] = ffma16(wl, yh[g][kb], h[g][t]);
+      h[g][t] = ffma16(wh, yh[g][kb], h[g][t]);
+    }
+  };
+#pragma unroll
+  for (int g = 0; g < RG; ++g) row[g] = blockIdx.x * FF_BM + (wave * RG + g) * 16 + li;
+
+  if constexpr (WO) {
+    // the attention rows, split (no LayerNorm: the range guard), and the
+    // accumulators' initial value (x + bo) 2^s_o
+    const float rwo = 1.0f / wo.wos;
+    float amax = 0.f;
+#pragma unroll
+    for (int g = 0; g < RG; ++g) {
+      const float* ar = wo.att + (size_t)min(row[g], M - 1) * ND_D + 4 * q;
+      const float* xr = y + (size_t)min(row[g], M - 1) * ND_D + 4 * q;
+#pragma unroll
+      for (int kb = 0; kb < 8; ++kb) {
+        const f32x4 a0 = ld4(ar + 32 * kb), a1 = ld4(ar + 32 * kb + 16);
+        amax = fmaxf(amax, fmaxf(absmax4(a0), absmax4(a1)));
+        ff_split(a0, a1, yh[g][kb], yl[g][kb]);
+        acc[g][2 * kb] = (ld4(xr + 32 * kb) + ld4(wo.bo + 32 * kb + 4 * q)) * rwo;
+        acc[g][2 * kb + 1] = (ld4(xr + 32 * kb + 16) + ld4(wo.bo + 32 * kb + 16 + 4 * q)) * rwo;
+      }
+    }
+    flag_overflow(ovf, amax);
+    __syncthreads();  // the biases in LDS (and every ordinary load retired)
+    // y = the accumulators + att Wo^T: slice j (output columns 32 j .. +31,
+    // tiles 2 j, 2 j + 1) from w1slot(j); W1_0 and W2_0 go out with the last
+    const char* WoH = reinterpret_cast<const char*>(wo.woh);
+    ff_copy_w1<NW>(WoH, 0, w1slot(0), wave, lane);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      if (j + 1 < 8) {
+        ff_copy_w1<NW>(WoH, j + 1, w1slot(j + 1), wave, lane);
+      } else {
+        ff_copy_w1<NW>(W1, 0, w1slot(0), wave, lane);
+        ff_copy_w2<NW>(W2, kp, 0, w2slot(0), wave, lane);
+      }
+      const f32x4* A = reinterpret_cast<const f32x4*>(w1slot(j)) + lane;
+      f32x4 h[RG][2];
+#pragma unroll
+      for (int g = 0; g < RG; ++g) {
+        h[g][0] = acc[g][2 * j];
+        h[g][1] = acc[g][2 * j + 1];
+      }
+#pragma unroll
+      for (int kb = 0; kb < 8; ++kb)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+          p1_mfma(__builtin_bit_cast(fh8, A[((t * 8 + kb) * 2) * 64]),
+                  __builtin_bit_cast(fh8, A[((t * 8 + kb) * 2 + 1) * 64]), t, kb, h);
+#pragma unroll
+      for (int g = 0; g < RG; ++g) {
+        acc[g][2 * j] = h[g][0];
+        acc[g][2 * j + 1] = h[g][1];
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < RG; ++g) {
+      f32x4 ya[8], yb[8];
+#pragma unroll
+      for (int kb = 0; kb < 8; ++kb) {
+        ya[kb] = acc[g][2 * kb] * wo.wos;
+        yb[kb] = acc[g][2 * kb + 1] * wo.wos;
+      }
+      ln_split(g, ya, yb, sb2);
+    }
+    asm volatile("s_barrier" ::: "memory");  // every wave is done with Wo's last slice (slot 1)
+    if (nch > 1) ff_copy_w1<NW>(W1, 1, w1slot(1), wave, lane);
+  } else {
+#pragma unroll
+    for (int g = 0; g < RG; ++g) {
+      const float* yr = y + (size_t)min(row[g], M - 1) * ND_D + 4 * q;
+      f32x4 ya[8], yb[8];
+#pragma unroll
+      for (int kb = 0; kb < 8; ++kb) {
+        ya[kb] = ld4(yr + 32 * kb);
+        yb[kb] = ld4(yr + 32 * kb + 16);
+      }
+      ln_split(g, ya, yb, b2);
+    }
+    __syncthreads();  // the biases in LDS (and every ordinary load retired)
+    ff_copy_w1<NW>(W1, 0, w1slot(0), wave, lane);
+    ff_copy_w2<NW>(W2, kp, 0, w2slot(0), wave, lane);
+    if (nch > 1) ff_copy_w1<NW>(W1, 1, w1slot(1), wave, lane);
   }
-  __syncthreads();  // biases in LDS (and every ordinary load retired)
-
-  ff_copy_w1<NW>(W1, 0, w1slot(0), wave, lane);
-  ff_copy_w2<NW>(W2, kp, 0, w2slot(0), wave, lane);
-  if (nch > 1) ff_copy_w1<NW>(W1, 1, w1slot(1), wave, lane);
-
-  f32x4 acc[RG][16];  // out^T tiles: lane holds out[row g][16 nt + 4q + i]
-#pragma unroll
-  for (int g = 0; g < RG; ++g)
-#pragma unroll
-    for (int nt = 0; nt < 16; ++nt) acc[g][nt] = {0.f, 0.f, 0.f, 0.f};
   float hmax = 0.f;  // split-fp16 range guard over the hidden
   fh8 hh[RG], hl[RG];  // H of the chunk phase 2 works on, split: its B operand
 
@@ -182,14 +279,6 @@ enc_ffn_kernel(const float* __restrict__ y, const uint16_t* __restrict__ w1h, fl
       ff_split(h[g][0], h[g][1], hh[g], hl[g]);
     }
   };
-  auto p1_mfma = [&](fh8 wh, fh8 wl, int t, int kb, f32x4 (&h)[RG][2]) {
-#pragma unroll
-    for (int g = 0; g < RG; ++g) {
-      h[g][t] = ffma16(wh, yl[g][kb], h[g][t]);
-      h[g][t] = ffma16(wl, yh[g][kb], h[g][t]);
-      h[g][t] = ffma16(wh, yh[g][kb], h[g][t]);
-    }
-  };
   auto p2_mfma = [&](fh8 wh, fh8 wl, int nt) {
 #pragma unroll
     for (int g = 0; g < RG; ++g) {
@@ -199,9 +288,12 @@ enc_ffn_kernel(const float* __restrict__ y, const uint16_t* __restrict__ w1h, fl
     }
   };
 
-  // prologue: phase 1 of chunk 0
+  // prologue: phase 1 of chunk 0 (W1_0 and W2_0 landed; W1_1 may be in flight)
   {
-    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    if (nch > 1)
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(32 / NW) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
     const f32x4* A1 = reinterpret_cast<const f32x4*>(w1slot(0)) + lane;
     f32x4 h[RG][2];
 #pragma unroll
@@ -277,16 +369,15 @@ enc_ffn_kernel(const float* __restrict__ y, const uint16_t* __restrict__ w1h, fl
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   flag_overflow(ovf, hmax);
 
-  // ---- epilogue: x = out * w2s + b2 + y, and the row's exact statistics
+  // ---- epilogue: x = out * w2s (b2 and the residual were the accumulators'
+  //      initial value), and the row's exact statistics
 #pragma unroll
   for (int g = 0; g < RG; ++g) {
-    const float* yr = y + (size_t)min(row[g], M - 1) * ND_D + 4 * q;
     f32x4 o[16];
     float s2 = 0.f;
 #pragma unroll
     for (int nt = 0; nt < 16; ++nt) {
-      const int col = 16 * nt + 4 * q;  // nt = 2 kb (+1): the lane's y columns 32 kb (+16) + 4q
-      o[nt] = acc[g][nt] * w2s + ld4(sb2 + col) + ld4(yr + 16 * nt);
+      o[nt] = acc[g][nt] * w2s;
       s2 += o[nt].x + o[nt].y + o[nt].z + o[nt].w;
     }
     s2 += __shfl_xor(s2, 16, 64);
@@ -314,12 +405,21 @@ enc_ffn_kernel(const float* __restrict__ y, const uint16_t* __restrict__ w1h, fl
 }
 
 hipError_t launch_enc_ffn(const float* y, const uint16_t* w1h, float w1s, const float* b1, const uint16_t* w2h,
-                          float w2s, const float* b2, float* x, float* xpart, int M, int F, int* ovf, hipStream_t s) {
+                          float w2s, const float* b2, float* x, float* xpart, int M, int F, int* ovf, hipStream_t s,
+                          const EncWo* wo) {
   if (M <= 0) return hipSuccess;
-  if (F % FF_HC != 0 || F > FF_MAXF || F < FF_HC || !y || !w1h || !b1 || !w2h || !b2 || !x || x == y)
+  if (F % FF_HC != 0 || F > FF_MAXF || F < FF_HC || !y || !w1h || !b1 || !w2h || !b2 || !x)
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(enc_ffn_kernel<1>, dim3((M + FF_BM - 1) / FF_BM), dim3(FF_BM / 16 * 64), 0, s, y, w1h, w1s, b1,
-                     w2h, w2s, b2, x, xpart, M, F, ovf);
+  const dim3 grid((M + FF_BM - 1) / FF_BM), block(FF_BM / 16 * 64);
+  if (wo) {  // x may alias y (the residual): each workgroup reads its rows before it writes them
+    if (!wo->att || !wo->woh || !wo->bo || wo->att == x || wo->att == y) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((enc_ffn_kernel<1, true>), grid, block, 0, s, y, w1h, w1s, b1, w2h, w2s, b2, x, xpart, M, F,
+                       ovf, *wo);
+  } else {
+    if (x == y) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((enc_ffn_kernel<1, false>), grid, block, 0, s, y, w1h, w1s, b1, w2h, w2s, b2, x, xpart, M, F,
+                       ovf, EncWo());
+  }
   return hipGetLastError();
 }
 

@@ -103,8 +103,18 @@ hipError_t launch_lstm_layer(const float* xp, const float* signal, const float* 
 // the LN affine folded into W1' / b1'; w1h = P16H image of W1' [F, 256], w2h =
 // P16H image of W2 [256, F] (launch_pack_p16h), w*s their scales; xpart gets
 // each row's exact {mean, M2} in slot 0 (one partial).  F % 32 == 0, F <= 2048.
+// wo (nullable): the attention block's output projection folded in front,
+// y = x + att Wo^T + bo with y the residual argument (x may alias it), woh
+// the P16H image of Wo [256, 256], wos its scale.
+struct EncWo {
+  const float* att = nullptr;
+  const uint16_t* woh = nullptr;
+  float wos = 1.f;
+  const float* bo = nullptr;
+};
 hipError_t launch_enc_ffn(const float* y, const uint16_t* w1h, float w1s, const float* b1, const uint16_t* w2h,
-                          float w2s, const float* b2, float* x, float* xpart, int M, int F, int* ovf, hipStream_t s);
+                          float w2s, const float* b2, float* x, float* xpart, int M, int F, int* ovf, hipStream_t s,
+                          const EncWo* wo = nullptr);
 // out[r] = LN(x[r]) (rows of 256)
 hipError_t launch_layernorm(const float* x, const float* g, const float* b, float* out, int rows, hipStream_t s);
 

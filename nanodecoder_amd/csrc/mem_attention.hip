@@ -301,8 +301,12 @@ dec_mem_attention_kernel(const float* __restrict__ qp, const float* __restrict__
 //    4 dim blocks x 2 planes), two half blocks ahead of the one computed;
 //    the 8 waves' (m, l, U) merge through LDS at the end.
 // Matrix-core time per CU: 64 x 16 + 128 x 8 cycles per wave, ~1.8 us.
-#define BH_NW 8                          // waves per chunk (64 keys each)
+#ifndef BH_NW
+#define BH_NW 8                          // waves per chunk (64 keys each; 4: 128 keys each, half the LDS)
+#endif
 #define BH_KB 32                         // key blocks per chunk (512 keys)
+#define BH_KPW (BH_KB / BH_NW)           // key blocks per wave
+static_assert(BH_NW == 4 || BH_NW == 8, "waves per chunk");
 #define BH_THR 6.0f                      // lazy-rescale threshold (natural log units)
 #define BH_PSCALE 128.0f                 // P split at 2^7
 #ifndef BH_AHEAD
@@ -360,10 +364,10 @@ dec_bank_h3_kernel(const float* __restrict__ qp, const f32x4* __restrict__ bank,
   // key block kb of this wave = w + 8 kb: the 8 waves stream one contiguous 128 KB window per step
   const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<f32x4*>(bank + (size_t)c * BH_KB * 8 * 2 * 64), 0,
                                                       BH_KB * 16384, 0x00020000);
-  const int kb0 = w, kbs = 8;
+  const int kb0 = w, kbs = BH_NW;
 #else
   const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<f32x4*>(bank + ((size_t)c * BH_KB + 4 * w) * 8 * 2 * 64), 0, 65536, 0x00020000);
+      const_cast<f32x4*>(bank + ((size_t)c * BH_KB + BH_KPW * w) * 8 * 2 * 64), 0, BH_KPW * 16384, 0x00020000);
   const int kb0 = 0, kbs = 1;
 #endif
   const int voff = lane * 16;
@@ -392,10 +396,18 @@ dec_bank_h3_kernel(const float* __restrict__ qp, const f32x4* __restrict__ bank,
   // q' (one 16 B load per thread, staged in LDS) and the signal FIRST, then
   // the first half blocks: the wait that retires q' leaves them in flight
   float* qimg = lds + BH_Q / 4;  // [8 heads][260] (rows padded: the b128 reads of 8 heads hit 8 bank groups)
-  const f32x4 qld = ld4(qp + pk(c, (threadIdx.x >> 6) * ND_D + 4 * lane, ND_H * ND_D));
-  // lane l: row l & 15 of the wave's key block l >> 4
-  const int bkey = BH_INTERLEAVE ? 16 * (w + 8 * (lane >> 4)) + (lane & 15) : 64 * w + lane;
-  const float sg = signal[(size_t)c * T + min(bkey, T - 1)];
+  constexpr int QH = ND_H / BH_NW, SGN = BH_KPW / 4;  // q' heads per thread, signal words per lane
+  f32x4 qld[QH];
+#pragma unroll
+  for (int i = 0; i < QH; ++i) qld[i] = ld4(qp + pk(c, (w + BH_NW * i) * ND_D + 4 * lane, ND_H * ND_D));
+  // lane l: row l & 15 of the wave's key block 4 j + (l >> 4)
+  float sg[SGN];
+#pragma unroll
+  for (int j = 0; j < SGN; ++j) {
+    const int kl = 4 * j + (lane >> 4);
+    const int bkey = 16 * (BH_INTERLEAVE ? w + BH_NW * kl : BH_KPW * w + kl) + (lane & 15);
+    sg[j] = signal[(size_t)c * T + min(bkey, T - 1)];
+  }
   f32x4 F[3][8];
   hload(0, F[0]);
   hload(1, F[1]);
@@ -406,7 +418,8 @@ dec_bank_h3_kernel(const float* __restrict__ qp, const f32x4* __restrict__ bank,
   // kernel-argument loads: one more scalar round trip before the stream)
   stamp_begin_at(stamp, t_entry);
   const int L = min(span[c], T);
-  st4(qimg + (threadIdx.x >> 6) * 260 + 4 * lane, qld);
+#pragma unroll
+  for (int i = 0; i < QH; ++i) st4(qimg + (w + BH_NW * i) * 260 + 4 * lane, qld[i]);
   lds_barrier();  // LDS only: the bank loads stay in flight
   f32x4 qv[8][2];
   const int hd = col & 7;
@@ -431,7 +444,9 @@ dec_bank_h3_kernel(const float* __restrict__ qp, const f32x4* __restrict__ bank,
     }
     flag_overflow(ovf, amax);
   }
-  const unsigned long long padm = __ballot(sg == pad_val);
+  unsigned long long padm[SGN];
+#pragma unroll
+  for (int j = 0; j < SGN; ++j) padm[j] = __ballot(sg[j] == pad_val);
 
   f32x4 ua[16];  // U^T... rows 4g + i = (P plane, head), column col of dim block: lane holds rows 4g .. 4g + 3
 #pragma unroll
@@ -439,7 +454,7 @@ dec_bank_h3_kernel(const float* __restrict__ qp, const f32x4* __restrict__ bank,
   float m = -INFINITY, l = 0.f;  // head col & 7 (l: this lane's keys)
 
 #pragma unroll
-  for (int kb = 0; kb < 4; ++kb) {
+  for (int kb = 0; kb < BH_KPW; ++kb) {
     f32x4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = d0;
 #pragma unroll
     for (int part = 0; part < 2; ++part) {
@@ -464,14 +479,14 @@ dec_bank_h3_kernel(const float* __restrict__ qp, const f32x4* __restrict__ bank,
 #endif
       }
       __builtin_amdgcn_sched_barrier(0);  // the next loads reuse f's registers
-      if (h + BH_AHEAD + 1 < 8) hload(h + BH_AHEAD + 1, F[(h + BH_AHEAD + 1) % 3]);
+      if (h + BH_AHEAD + 1 < 2 * BH_KPW) hload(h + BH_AHEAD + 1, F[(h + BH_AHEAD + 1) % 3]);
     }
     // ---- scores: columns h and h + 8 hold the hi and lo halves of q'_h
     f32x4 s = d0 + d1;
 #pragma unroll
     for (int i = 0; i < 4; ++i) s[i] += dpp_mov<ND_DPP_ROR8>(s[i]);
-    const int kbase = BH_INTERLEAVE ? 16 * (w + 8 * kb) + 4 * g : 64 * w + 16 * kb + 4 * g;  // key of row i
-    const unsigned pb = (unsigned)(padm >> (16 * kb + 4 * g)) & 0xFu;
+    const int kbase = 16 * (BH_INTERLEAVE ? w + BH_NW * kb : BH_KPW * w + kb) + 4 * g;  // key of row i
+    const unsigned pb = (unsigned)(padm[kb >> 2] >> (16 * (kb & 3) + 4 * g)) & 0xFu;
     float gm = -INFINITY;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -554,7 +569,7 @@ dec_bank_h3_kernel(const float* __restrict__ qp, const f32x4* __restrict__ bank,
   float* fw = lds + BH_Q / 4;  // [wave][8 heads] weights, then [8 heads] 1 / den (the q' image is dead)
   if (w == 0) {
     const int v = lane >> 3, h = lane & 7;
-    const float mv = ml[(v * ND_H + h) * 2], lv = ml[(v * ND_H + h) * 2 + 1];
+    const float mv = v < BH_NW ? ml[(v * ND_H + h) * 2] : -INFINITY, lv = v < BH_NW ? ml[(v * ND_H + h) * 2 + 1] : 0.f;
     float M = fmaxf(mv, __shfl_xor(mv, 8, 64));
     M = fmaxf(M, __shfl_xor(M, 16, 64));
     M = fmaxf(M, __shfl_xor(M, 32, 64));
@@ -563,12 +578,13 @@ dec_bank_h3_kernel(const float* __restrict__ qp, const f32x4* __restrict__ bank,
     den += __shfl_xor(den, 8, 64);
     den += __shfl_xor(den, 16, 64);
     den += __shfl_xor(den, 32, 64);
-    fw[v * ND_H + h] = f;
+    if (v < BH_NW) fw[v * ND_H + h] = f;
     if (v == 0) fw[64 + h] = den > 0.f ? __builtin_amdgcn_rcpf(den) * (1.0f / BH_PSCALE) : 0.f;
   }
   lds_barrier();
-  {
-    const int hs = threadIdx.x >> 8, d = threadIdx.x & 255, k = d >> 4, cl = d & 15;
+#pragma unroll
+  for (int e = threadIdx.x; e < 512; e += BH_NW * 64) {
+    const int hs = e >> 8, d = e & 255, k = d >> 4, cl = d & 15;
     const int lh = k * 64 + cl + 16 * hs, ll = k * 64 + cl + 16 * (2 + hs);  // hi rows g = hs, lo rows g = 2 + hs
     f32x4 num = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll

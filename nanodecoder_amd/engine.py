@@ -470,21 +470,30 @@ def op_pack_p16h(W: torch.Tensor):
     return Wh, sc.value
 
 
-def op_enc_ffn(y, W1, b1, W2, b2, ln_g, ln_b):
+def op_enc_ffn(y, W1, b1, W2, b2, ln_g, ln_b, att=None, Wo=None, bo=None, inplace=False):
     """The encoder's fused FFN block (nd_op_enc_ffn): x = y + W2 relu(W1
     LN(y) + b1) + b2 for row-major y [M, 256], the LN affine folded and both
     weights packed to P16H images here as the engine does at load time.
+    With att, Wo, bo (nd_op_enc_ffn_wo) y is first replaced by
+    y + att Wo^T + bo (the attention block's output projection and residual);
+    inplace: x is written over y, as the engine does.
     Returns (x, row stats [M, 2] = {mean, M2}, overflow flag)."""
     M, F = y.shape[0], W1.shape[0]
     W1f, b1f = op_fold_layernorm(W1, b1, ln_g, ln_b)
     w1h, w1s = op_pack_p16h(W1f)
     w2h, w2s = op_pack_p16h(W2)
-    x = torch.empty_like(y)
+    x = y if inplace else torch.empty_like(y)
     part = torch.zeros(M, 16, 2, dtype=torch.float32, device=y.device)
     ov = torch.zeros(1, dtype=torch.int32, device=y.device)
     s = ctypes.c_void_p(torch.cuda.current_stream(y.device).cuda_stream)
-    _lib.check(_lib.lib().nd_op_enc_ffn(_ptr(y), _ptr(w1h), w1s, _ptr(b1f), _ptr(w2h), w2s, _ptr(b2), _ptr(x),
-                                        _ptr(part), M, F, _ptr(ov), s), "nd_op_enc_ffn")
+    if Wo is not None:
+        woh, wos = op_pack_p16h(Wo)
+        _lib.check(_lib.lib().nd_op_enc_ffn_wo(_ptr(att), _ptr(y), _ptr(woh), wos, _ptr(bo), _ptr(w1h), w1s,
+                                               _ptr(b1f), _ptr(w2h), w2s, _ptr(b2), _ptr(x), _ptr(part), M, F,
+                                               _ptr(ov), s), "nd_op_enc_ffn_wo")
+    else:
+        _lib.check(_lib.lib().nd_op_enc_ffn(_ptr(y), _ptr(w1h), w1s, _ptr(b1f), _ptr(w2h), w2s, _ptr(b2), _ptr(x),
+                                            _ptr(part), M, F, _ptr(ov), s), "nd_op_enc_ffn")
     return x, part[:, 0, :], ov
 
 

@@ -64,12 +64,15 @@ def test_gemm_vs_fp64(M, N, K, ln, relu, res, split):
 
 
 @pytest.mark.parametrize("M,F", [(1000, 2048), (256, 2048), (131, 64), (384, 512)])
-def test_enc_ffn_fused_vs_fp64(M, F):
+@pytest.mark.parametrize("wo", ["none", "wo", "wo_inplace"])
+def test_enc_ffn_fused_vs_fp64(M, F, wo):
     """The encoder's fused FFN block (nd_op_enc_ffn: LayerNorm, W1, ReLU, W2
     and the residual in one launch, the hidden kept on chip) against fp64,
     with a ragged last 128-row block (M = 1000, 131), d_ff 64..2048: the same
     2e-4 absolute bound as the split GEMMs, and the exact row statistics it
-    hands to the next LayerNorm."""
+    hands to the next LayerNorm.  wo: the attention's output projection and
+    residual folded in front (nd_op_enc_ffn_wo: y = x + att Wo^T + bo never
+    leaves the chip), written over the input as the engine does (inplace)."""
     from nanodecoder_amd.engine import op_enc_ffn
     g = torch.Generator().manual_seed(M + F)
     y = torch.randn(M, 256, generator=g) * 2 + 0.5
@@ -79,10 +82,18 @@ def test_enc_ffn_fused_vs_fp64(M, F):
     b2 = torch.randn(256, generator=g) * 0.1
     lg = 1 + 0.1 * torch.randn(256, generator=g)
     lb = 0.1 * torch.randn(256, generator=g)
+    att = torch.randn(M, 256, generator=g)
+    Wo = torch.randn(256, 256, generator=g) / 16
+    bo = torch.randn(256, generator=g) * 0.1
     dev = torch.device("cuda", 0)
-    x, st, ov = op_enc_ffn(*(t.to(dev) for t in (y, W1, b1, W2, b2, lg, lb)))
+    kw = {}
+    if wo != "none":
+        kw = dict(att=att.to(dev), Wo=Wo.to(dev), bo=bo.to(dev), inplace=wo == "wo_inplace")
+    x, st, ov = op_enc_ffn(*(t.to(dev) for t in (y, W1, b1, W2, b2, lg, lb)), **kw)
     torch.cuda.synchronize()
     yd = y.double()
+    if wo != "none":
+        yd = yd + att.double() @ Wo.double().t() + bo.double()
     h = torch.relu(torch.nn.functional.layer_norm(yd, (256,), lg.double(), lb.double(), 1e-6) @ W1.double().t()
                    + b1.double())
     ref = yd + h @ W2.double().t() + b2.double()
