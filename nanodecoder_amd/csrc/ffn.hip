@@ -50,6 +50,8 @@
 // whose out^T tiles are exactly y in the P16 k-permutation: its LayerNorm and
 // split run in registers, and y never goes to HBM (the unfused form wrote it
 // from a GEMM and read it back twice).
+#include <utility>
+
 #include "common.hpp"
 #include "kernels.hpp"
 
@@ -62,9 +64,37 @@ typedef __attribute__((address_space(3))) void lds_void;
 #define FF_HC 32                    // hidden columns per chunk (one k-block of phase 2)
 #define FF_SLICE 32768              // bytes of one weight slice in LDS
 #define FF_MAXF 2048                // d_ff bound (b1 staged whole in LDS)
+#ifndef FF_AHEAD
+#define FF_AHEAD 2                  // units whose LDS reads are in flight beyond the one computed
+#endif
 
 __device__ __forceinline__ f32x4 ffma16(fh8 a, fh8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+// f(std::integral_constant<int, i>) for i = 0 .. N-1: a loop whose index is a
+// constant expression (inline-asm immediates)
+template <typename F, int... I>
+__device__ __forceinline__ void ff_static_for(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+
+// the inline-asm LDS read ring of the main loop (FF_AHEAD + 1 slots): unit
+// U's weight pair (hi, lo: two 1 KB lane-linear blocks 1 KB apart) at the
+// constant offset (U / 2) 2048 from its slot's base (a1: W1, odd U; a2: W2)
+template <int U, int RING>
+__device__ __forceinline__ void ff_fetch(f32x4 (&rh)[RING], f32x4 (&rl)[RING], uint32_t a1, uint32_t a2) {
+  constexpr int off = (U >> 1) * 2048;
+  asm volatile("ds_read_b128 %0, %2 offset:%3\n\tds_read_b128 %1, %2 offset:%4"
+               : "=&v"(rh[U % RING]), "=&v"(rl[U % RING])
+               : "v"((U & 1) ? a1 : a2), "n"(off), "n"(off + 1024)
+               : "memory");
+}
+// retire unit U's pair; the younger pairs (up to RING - 1, fewer at the end) stay in flight
+template <int U, int RING, int NU>
+__device__ __forceinline__ void ff_wait(f32x4 (&rh)[RING], f32x4 (&rl)[RING]) {
+  constexpr int left = NU - 1 - U < RING - 1 ? NU - 1 - U : RING - 1;
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(rh[U % RING]), "+v"(rl[U % RING]) : "n"(2 * left));
 }
 
 __device__ __forceinline__ void ff_split(f32x4 x0, f32x4 x1, fh8& hi, fh8& lo) {
@@ -326,44 +356,35 @@ enc_ffn_kernel(const float* y, const uint16_t* __restrict__ w1h, float w1s, cons
     // 32 units, even: phase 2 of chunk k on output tile u / 2, odd: phase 1
     // of chunk k + 1 on (tile, k-block) = ((u / 2) / 8, (u / 2) % 8); each is
     // a hi and a lo ds_read_b128 operand and 3 RG MFMAs.  The reads go out
-    // two units ahead into a 3-deep register ring from inline asm (left to
-    // itself hipcc sinks every LDS read to its use and waits on it: 12 %
-    // slower), and each unit waits only for its own pair (lgkmcnt(4): the two
-    // younger pairs stay in flight under this unit's MFMAs).  The "+v" ties
-    // make the data defined at the wait; tools/lds_ring_check.py verifies on
-    // the compiled code that nothing touches a ring register in between
-    // (tests/test_build.py)
+    // FF_AHEAD units ahead into a (FF_AHEAD + 1)-deep register ring from
+    // inline asm (left to itself hipcc sinks every LDS read to its use and
+    // waits on it: 12 % slower), and each unit waits only for its own pair
+    // (lgkmcnt(2 FF_AHEAD): the younger pairs stay in flight under this unit's
+    // MFMAs).  Addresses are one base register per slot plus the unit's
+    // constant offset (immediates: no per-unit address registers).  The "+v"
+    // ties make the data defined at the wait; tools/lds_ring_check.py
+    // verifies on the compiled code that nothing touches a ring register in
+    // between (tests/test_abi.py)
+    constexpr int RING = FF_AHEAD + 1;
     const uint32_t a2 = (uint32_t)(uintptr_t)A2, a1 = (uint32_t)(uintptr_t)A1;
-    auto uaddr = [&](int u) -> uint32_t {
-      const int i = u >> 1;
-      return (u & 1) ? a1 + (uint32_t)(i * 2048) : a2 + (uint32_t)(i * 2048);
-    };
-    f32x4 rh[3], rl[3];
-    auto fetch = [&](int u) {
-      asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:1024"
-                   : "=&v"(rh[u % 3]), "=&v"(rl[u % 3]) : "v"(uaddr(u)) : "memory");
-    };
+    f32x4 rh[RING], rl[RING];
     f32x4 h[RG][2];
 #pragma unroll
     for (int g = 0; g < RG; ++g) h[g][0] = h[g][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-    fetch(0);
-    fetch(1);
-#pragma unroll
-    for (int u = 0; u < 32; ++u) {
-      if (u + 2 < 32) {
-        fetch(u + 2);
-        asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(rh[u % 3]), "+v"(rl[u % 3]));
-      } else if (u + 1 < 32) {
-        asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(rh[u % 3]), "+v"(rl[u % 3]));
-      } else {
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(rh[u % 3]), "+v"(rl[u % 3]));
-      }
-      const fh8 wh = __builtin_bit_cast(fh8, rh[u % 3]), wl = __builtin_bit_cast(fh8, rl[u % 3]);
-      if (u & 1)
-        p1_mfma(wh, wl, (u >> 1) >> 3, (u >> 1) & 7, h);
-      else
-        p2_mfma(wh, wl, u >> 1);
-    }
+    ff_static_for([&](auto uc) { ff_fetch<decltype(uc)::value, RING>(rh, rl, a1, a2); },
+                  std::make_integer_sequence<int, FF_AHEAD>{});
+    ff_static_for(
+        [&](auto uc) {
+          constexpr int u = decltype(uc)::value;
+          if constexpr (u + FF_AHEAD < 32) ff_fetch<u + FF_AHEAD, RING>(rh, rl, a1, a2);
+          ff_wait<u, RING, 32>(rh, rl);
+          const fh8 wh = __builtin_bit_cast(fh8, rh[u % RING]), wl = __builtin_bit_cast(fh8, rl[u % RING]);
+          if constexpr (u & 1)
+            p1_mfma(wh, wl, (u >> 1) >> 3, (u >> 1) & 7, h);
+          else
+            p2_mfma(wh, wl, u >> 1);
+        },
+        std::make_integer_sequence<int, 32>{});
     finish_h(k + 1, h);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
