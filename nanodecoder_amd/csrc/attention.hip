@@ -34,9 +34,10 @@ __device__ __forceinline__ void row_part(f32x4 v, int lane, float* part) {
   }
 }
 
+template <bool QKV>
 __global__ void __launch_bounds__(256)
 enc_embed_kernel(const float* __restrict__ signal, const float* __restrict__ w, const float* __restrict__ b,
-                 float* __restrict__ x, float* __restrict__ part, int n_rows) {
+                 float* __restrict__ x, float* __restrict__ part, int n_rows, EmbedQkv eq) {
   // encoder/transformer.py:104,113 — Linear(1, d) applied to the scalar sample
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= n_rows) return;
@@ -45,12 +46,72 @@ enc_embed_kernel(const float* __restrict__ signal, const float* __restrict__ w, 
   const f32x4 v = s * wv + bv;
   st4(x + (size_t)row * ND_D + lane * 4, v);
   if (part) row_part(v, lane, part + (size_t)row * ND_PART_LD * 2);
+  if constexpr (QKV) {  // layer 0's q | k | v (encoder/transformer.py:44, the rank-2 form of EmbedQkv)
+    const float rs = ln_rsqrt(fmaf(s, fmaf(s, eq.mww, 2.0f * eq.mwb), eq.mbb) + ND_LN_EPS);
+    float* o = eq.qkv + (size_t)row * 3 * ND_D + lane * 4;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int n = j * ND_D + lane * 4;
+      st4(o + j * ND_D, (s * ld4(eq.ac + n) + ld4(eq.ac + 3 * ND_D + n)) * rs + ld4(eq.bias + n));
+    }
+  }
 }
 
 hipError_t launch_enc_embed(const float* signal, const float* w_in, const float* b_in, float* x, float* part, int B,
-                            int T, hipStream_t s) {
+                            int T, hipStream_t s, const EmbedQkv* eq) {
   const int rows = B * T;
-  hipLaunchKernelGGL(enc_embed_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, signal, w_in, b_in, x, part, rows);
+  if (eq) {
+    if (!eq->ac || !eq->bias || !eq->qkv) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(enc_embed_kernel<true>, dim3((rows + 3) / 4), dim3(256), 0, s, signal, w_in, b_in, x, part,
+                       rows, *eq);
+  } else {
+    hipLaunchKernelGGL(enc_embed_kernel<false>, dim3((rows + 3) / 4), dim3(256), 0, s, signal, w_in, b_in, x, part,
+                       rows, EmbedQkv());
+  }
+  return hipGetLastError();
+}
+
+// EmbedQkv's a, c (thread n of 768) and means (block 0), accumulated in double
+__global__ void __launch_bounds__(256)
+embed_qkv_prep_kernel(const float* __restrict__ w, const float* __restrict__ b, const float* __restrict__ W,
+                      float* __restrict__ ac, double* __restrict__ scal) {
+  __shared__ double wd[ND_D], bd[ND_D];
+  const int tid = threadIdx.x;
+  wd[tid] = w[tid];
+  bd[tid] = b[tid];
+  __syncthreads();
+  double wm = 0.0, bm = 0.0;
+  for (int d = 0; d < ND_D; ++d) {
+    wm += wd[d];
+    bm += bd[d];
+  }
+  wm /= ND_D;
+  bm /= ND_D;
+  const int n = blockIdx.x * 256 + tid;
+  double a = 0.0, c = 0.0;
+  for (int d = 0; d < ND_D; ++d) {
+    const double wt = W[(size_t)n * ND_D + d];
+    a += (wd[d] - wm) * wt;
+    c += (bd[d] - bm) * wt;
+  }
+  ac[n] = (float)a;
+  ac[3 * ND_D + n] = (float)c;
+  if (blockIdx.x == 0 && tid == 0) {
+    double ww = 0.0, wb = 0.0, bb = 0.0;
+    for (int d = 0; d < ND_D; ++d) {
+      ww += (wd[d] - wm) * (wd[d] - wm);
+      wb += (wd[d] - wm) * (bd[d] - bm);
+      bb += (bd[d] - bm) * (bd[d] - bm);
+    }
+    scal[0] = ww / ND_D;
+    scal[1] = wb / ND_D;
+    scal[2] = bb / ND_D;
+  }
+}
+
+hipError_t launch_embed_qkv_prep(const float* w_in, const float* b_in, const float* nwqkv, float* ac, double* scal,
+                                 hipStream_t s) {
+  hipLaunchKernelGGL(embed_qkv_prep_kernel, dim3(3), dim3(256), 0, s, w_in, b_in, nwqkv, ac, scal);
   return hipGetLastError();
 }
 

@@ -137,6 +137,12 @@ struct nd_ctx {
 
   // weights
   float *enc_lin_w = nullptr, *enc_lin_b = nullptr, *enc_ln_g = nullptr, *enc_ln_b = nullptr;
+  // encoder layer 0's QKV in the rank-2 form (kernels.hpp EmbedQkv): a | c on
+  // the device, the three means on the host (kernel arguments); set at finalize
+  float* eq_ac = nullptr;
+  double* eq_scal = nullptr;
+  float eq_m[3] = {0.f, 0.f, 0.f};
+  bool eq_ready = false;
   std::vector<EncLayer> enc;
   std::vector<NanoLayer> nano;
   float* nano_W = nullptr;
@@ -531,13 +537,34 @@ static bool enc_wo_fused(const nd_ctx* c, const EncLayer& L) {
   return on && enc_ffn_fused(c, L) && L.woh != nullptr;
 }
 
+// layer 0's QKV from the embedding in the rank-2 form (EmbedQkv); ND_ENC_QKV0=0
+// keeps its GEMM (A/B timing)
+static bool enc_qkv0_rank2(const nd_ctx* c) {
+  static const bool on = [] {
+    const char* e = getenv("ND_ENC_QKV0");
+    return !(e && atoi(e) == 0);
+  }();
+  return on && c->eq_ready;
+}
+
 static hipError_t enqueue_encode_transformer(nd_ctx* c, int B, int T, hipStream_t s) {
   const int M = B * T, D = c->D, F = c->F;
-  LCHK(nd::launch_enc_embed(c->sig, c->enc_lin_w, c->enc_lin_b, c->x, c->x_part, B, T, s));
+  nd::EmbedQkv eq;
+  const bool r2 = enc_qkv0_rank2(c);
+  if (r2) {
+    eq.ac = c->eq_ac;
+    eq.bias = c->enc[0].nbqkv;
+    eq.mww = c->eq_m[0];
+    eq.mwb = c->eq_m[1];
+    eq.mbb = c->eq_m[2];
+    eq.qkv = c->big;
+  }
+  LCHK(nd::launch_enc_embed(c->sig, c->enc_lin_w, c->enc_lin_b, c->x, c->x_part, B, T, s, r2 ? &eq : nullptr));
   int pnx = 1, pny = 0;
   for (auto& L : c->enc) {
     // encoder/transformer.py:36-54
-    LCHK(G(c->x, D, L.nwqkv, 3 * D, D, L.nbqkv, c->big, 3 * D, M).h3(c).ln(c->x_part, pnx).run(s));
+    if (!(r2 && &L == &c->enc[0]))
+      LCHK(G(c->x, D, L.nwqkv, 3 * D, D, L.nbqkv, c->big, 3 * D, M).h3(c).ln(c->x_part, pnx).run(s));
     LCHK(nd::launch_enc_attention(c->big, c->sig, c->span, c->att, B, T, s, c->exact, c->ovf));
     if (enc_wo_fused(c, L)) {  // Wo + residual, LN, FFN in one launch; the layer's rows updated in place
       nd::EncWo wo;
@@ -1077,6 +1104,16 @@ int nd_finalize(nd_ctx* c) {
       HIPCHK(fold(L.wqkv, L.bqkv, L.ln_g, L.ln_b, L.nwqkv, L.nbqkv, 3 * D, D));
       HIPCHK(fold(L.w1, L.b1, L.fln_g, L.fln_b, L.nw1, L.nb1, F, D));
     }
+    if (c->cfg.encoder_type == ND_ENC_TRANSFORMER && !c->enc.empty()) {
+      if (!c->eq_ac && dalloc(c, &c->eq_ac, (size_t)6 * D) != hipSuccess) return fail(ND_ERR_HIP, "alloc");
+      if (!c->eq_scal && dalloc(c, &c->eq_scal, 3) != hipSuccess) return fail(ND_ERR_HIP, "alloc");
+      HIPCHK(nd::launch_embed_qkv_prep(c->enc_lin_w, c->enc_lin_b, c->enc[0].nwqkv, c->eq_ac, c->eq_scal, c->es));
+      double m[3];
+      HIPCHK(hipMemcpyAsync(m, c->eq_scal, sizeof(m), hipMemcpyDeviceToHost, c->es));
+      HIPCHK(hipStreamSynchronize(c->es));
+      for (int i = 0; i < 3; ++i) c->eq_m[i] = (float)m[i];
+      c->eq_ready = true;
+    }
     if (c->nctxkv_w)
       HIPCHK(fold(c->ctxkv_w, c->ctxkv_b, c->enc_ln_g, c->enc_ln_b, c->nctxkv_w, c->nctxkv_b,
                   (int)c->dec.size() * 2 * D, D));
@@ -1477,7 +1514,7 @@ static const struct {
                  {"ND_P16_XCD", 1},    {"ND_P16_BIG_MIN", 2048}, {"ND_ENC_FFN", 1},     {"ND_QKV_TABLE", 1},
                  {"ND_HEAD_FUSE", 1},  {"ND_LSTM_F32", 0},     {"ND_LSTM_LIBM", 0},     {"ND_LSTM_SEQ", 4},
                  {"ND_ENC_ATTN_NQ", 2}, {"ND_ENC_ATTN_GRID", 0}, {"ND_ENC_ATTN_F32", 0}, {"ND_SELF_XCD", 1},
-                 {"ND_ENC_WO", 1}};
+                 {"ND_ENC_WO", 1},     {"ND_ENC_QKV0", 1}};
 
 int nd_switches(char* buf, int32_t len) {
   std::string out;

@@ -85,9 +85,26 @@ hipError_t launch_fold_layernorm(const float* W, const float* bias, const float*
                                  float* W_out, float* b_out, int N, int K, hipStream_t s);
 
 // ---- encoder -------------------------------------------------------------
-// x[b*T+t][:] = signal[b][t] * w_in + b_in (Linear(1, d)); part: full-row stats
+// Layer 0 of the Transformer encoder reads x = s w + b (Linear(1, d) of the
+// sample s): with w' = w - mean(w), b' = b - mean(b) its LayerNorm'd
+// projection is the rank-2 form
+//   LN(x) W'^T + b'' = (s a + c) / sqrt(s^2 m_ww + 2 s m_wb + m_bb + eps) + b''
+// a = W' w', c = W' b', m_.. the means of w'^2, w'b', b'^2 (W', b'': the
+// LN-folded QKV weight and bias), so the layer's QKV GEMM becomes a write of
+// the [M, 768] rows beside the embedding's.
+struct EmbedQkv {
+  const float* ac = nullptr;  // [2][768]: a, c
+  const float* bias = nullptr;
+  float mww = 0.f, mwb = 0.f, mbb = 0.f;
+  float* qkv = nullptr;       // [M, 768] row-major
+};
+// ac and the three means (double scal[3]) from the LN-folded weight [768, 256]
+hipError_t launch_embed_qkv_prep(const float* w_in, const float* b_in, const float* nwqkv, float* ac, double* scal,
+                                 hipStream_t s);
+// x[b*T+t][:] = signal[b][t] * w_in + b_in (Linear(1, d)); part: full-row stats;
+// eq: also layer 0's q | k | v rows (EmbedQkv)
 hipError_t launch_enc_embed(const float* signal, const float* w_in, const float* b_in, float* x, float* part, int B,
-                            int T, hipStream_t s);
+                            int T, hipStream_t s, const EmbedQkv* eq = nullptr);
 // flash attention over qkv [B*T, 768]; mask signal==0; keys >= span excluded
 // exact: the fp32-MFMA kernel instead of split-fp16 (also forced by ND_ENC_ATTN_F32=1);
 // ovf: split-fp16 range guard word (nullable)
