@@ -352,10 +352,14 @@ int nd_op_enc_ffn(const float* y, const uint16_t* w1h, float w1s, const float* b
  * (encoder/transformer.py:45-54, one launch for the rest of the layer):
  * y = x_in + att Wo^T + bo, then x = y + W2 relu(W1' LN(y) + b1') + b2.
  * woh: P16H image of Wo [256, 256] with its scale wos.  x may alias x_in
- * (the engine updates the layer's rows in place); att must not. */
+ * (the engine updates the layer's rows in place); att must not.  With qkvh
+ * (nullable) the next layer's projection follows in the same launch:
+ * qkv = LN(x) Wq'^T + qkvb (row-major [M, 768]; qkvh the P16H image of the
+ * LN-folded Wq' [768, 256], qkvs its scale). */
 int nd_op_enc_ffn_wo(const float* att, const float* x_in, const uint16_t* woh, float wos, const float* bo,
                      const uint16_t* w1h, float w1s, const float* b1, const uint16_t* w2h, float w2s, const float* b2,
-                     float* x, float* xpart, int32_t M, int32_t F, int32_t* overflow, void* stream);
+                     float* x, float* xpart, const uint16_t* qkvh, float qkvs, const float* qkvb, float* qkv,
+                     int32_t M, int32_t F, int32_t* overflow, void* stream);
 
 int nd_op_gemm_p16_split(const float* A, const uint16_t* Wh, float wscale, const float* bias, const float* R, float* C,
                          int32_t M, int32_t N, int32_t K, const float* part_in, int32_t part_n_in, float* part_out,

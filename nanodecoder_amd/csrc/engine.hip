@@ -64,6 +64,9 @@ struct EncLayer {
   // P16H image of Wo, folded into the FFN block's launch (ffn.hip WO)
   uint16_t* woh = nullptr;
   float wos = 1.f;
+  // P16H image of the LN-folded W_qkv, folded into the previous layer's FFN launch (ffn.hip QK)
+  uint16_t* qkvh = nullptr;
+  float qkvs = 1.f;
 };
 struct DecLayer {
   float *ln1_g, *ln1_b, *wqkv, *bqkv, *wo, *bo, *ln2_g, *ln2_b, *cwq, *cbq, *cwo, *cbo, *fln_g, *fln_b, *w1, *b1,
@@ -547,6 +550,16 @@ static bool enc_qkv0_rank2(const nd_ctx* c) {
   return on && c->eq_ready;
 }
 
+// the next layer's QKV projection folded into the FFN block's launch (q | k | v
+// from the block's registers); ND_ENC_QKV=0 keeps its GEMM (A/B timing)
+static bool enc_qkv_folded(const nd_ctx* c, const EncLayer& next) {
+  static const bool on = [] {
+    const char* e = getenv("ND_ENC_QKV");
+    return !(e && atoi(e) == 0);
+  }();
+  return on && next.qkvh != nullptr;
+}
+
 static hipError_t enqueue_encode_transformer(nd_ctx* c, int B, int T, hipStream_t s) {
   const int M = B * T, D = c->D, F = c->F;
   nd::EmbedQkv eq;
@@ -561,10 +574,12 @@ static hipError_t enqueue_encode_transformer(nd_ctx* c, int B, int T, hipStream_
   }
   LCHK(nd::launch_enc_embed(c->sig, c->enc_lin_w, c->enc_lin_b, c->x, c->x_part, B, T, s, r2 ? &eq : nullptr));
   int pnx = 1, pny = 0;
-  for (auto& L : c->enc) {
+  bool qkv_done = r2;  // this layer's q | k | v already in c->big
+  for (size_t li = 0; li < c->enc.size(); ++li) {
+    EncLayer& L = c->enc[li];
     // encoder/transformer.py:36-54
-    if (!(r2 && &L == &c->enc[0]))
-      LCHK(G(c->x, D, L.nwqkv, 3 * D, D, L.nbqkv, c->big, 3 * D, M).h3(c).ln(c->x_part, pnx).run(s));
+    if (!qkv_done) LCHK(G(c->x, D, L.nwqkv, 3 * D, D, L.nbqkv, c->big, 3 * D, M).h3(c).ln(c->x_part, pnx).run(s));
+    qkv_done = false;
     LCHK(nd::launch_enc_attention(c->big, c->sig, c->span, c->att, B, T, s, c->exact, c->ovf));
     if (enc_wo_fused(c, L)) {  // Wo + residual, LN, FFN in one launch; the layer's rows updated in place
       nd::EncWo wo;
@@ -572,7 +587,17 @@ static hipError_t enqueue_encode_transformer(nd_ctx* c, int B, int T, hipStream_
       wo.woh = L.woh;
       wo.wos = L.wos;
       wo.bo = L.bo;
-      LCHK(nd::launch_enc_ffn(c->x, L.w1h, L.w1s, L.nb1, L.w2h, L.w2s, L.b2, c->x, c->x_part, M, F, c->ovf, s, &wo));
+      nd::EncQkv qk;
+      if (li + 1 < c->enc.size() && enc_qkv_folded(c, c->enc[li + 1])) {
+        const EncLayer& N = c->enc[li + 1];
+        qk.wh = N.qkvh;
+        qk.ws = N.qkvs;
+        qk.bias = N.nbqkv;
+        qk.out = c->big;
+        qkv_done = true;
+      }
+      LCHK(nd::launch_enc_ffn(c->x, L.w1h, L.w1s, L.nb1, L.w2h, L.w2s, L.b2, c->x, c->x_part, M, F, c->ovf, s, &wo,
+                              qkv_done ? &qk : nullptr));
       pnx = 1;
       continue;
     }
@@ -1165,6 +1190,8 @@ int nd_finalize(nd_ctx* c) {
         HIPCHK(nd::launch_pack_p16h(L.w2, F, D, F, L.w2h, &L.w2s, c->es));
         if (!L.woh && (e_ = dalloc(c, &L.woh, (size_t)2 * D * D)) != hipSuccess) return fail(ND_ERR_HIP, "alloc");
         HIPCHK(nd::launch_pack_p16h(L.wo, D, D, D, L.woh, &L.wos, c->es));
+        if (!L.qkvh && (e_ = dalloc(c, &L.qkvh, (size_t)2 * 3 * D * D)) != hipSuccess) return fail(ND_ERR_HIP, "alloc");
+        HIPCHK(nd::launch_pack_p16h(L.nwqkv, D, 3 * D, D, L.qkvh, &L.qkvs, c->es));
       }
     }
     HIPCHK(mk(c->cfg.encoder_type == ND_ENC_TRANSFORMER ? c->nctxkv_w : c->ctxkv_w, L2, D));
@@ -1514,7 +1541,8 @@ static const struct {
                  {"ND_P16_XCD", 1},    {"ND_P16_BIG_MIN", 2048}, {"ND_ENC_FFN", 1},     {"ND_QKV_TABLE", 1},
                  {"ND_HEAD_FUSE", 1},  {"ND_LSTM_F32", 0},     {"ND_LSTM_LIBM", 0},     {"ND_LSTM_SEQ", 4},
                  {"ND_ENC_ATTN_NQ", 2}, {"ND_ENC_ATTN_GRID", 0}, {"ND_ENC_ATTN_F32", 0}, {"ND_SELF_XCD", 1},
-                 {"ND_ENC_WO", 1},     {"ND_ENC_QKV0", 1}};
+                 {"ND_ENC_WO", 1},     {"ND_ENC_QKV0", 1},
+                 {"ND_ENC_QKV", 1}};
 
 int nd_switches(char* buf, int32_t len) {
   std::string out;
@@ -1685,15 +1713,21 @@ int nd_op_enc_ffn(const float* y, const uint16_t* w1h, float w1s, const float* b
 
 int nd_op_enc_ffn_wo(const float* att, const float* x_in, const uint16_t* woh, float wos, const float* bo,
                      const uint16_t* w1h, float w1s, const float* b1, const uint16_t* w2h, float w2s, const float* b2,
-                     float* x, float* xpart, int32_t M, int32_t F, int32_t* overflow, void* stream) {
+                     float* x, float* xpart, const uint16_t* qkvh, float qkvs, const float* qkvb, float* qkv,
+                     int32_t M, int32_t F, int32_t* overflow, void* stream) {
   if (int rc = ensure_attributes()) return rc;
   nd::EncWo wo;
   wo.att = att;
   wo.woh = woh;
   wo.wos = wos;
   wo.bo = bo;
-  hipError_t e =
-      nd::launch_enc_ffn(x_in, w1h, w1s, b1, w2h, w2s, b2, x, xpart, M, F, overflow, (hipStream_t)stream, &wo);
+  nd::EncQkv qk;
+  qk.wh = qkvh;
+  qk.ws = qkvs;
+  qk.bias = qkvb;
+  qk.out = qkv;
+  hipError_t e = nd::launch_enc_ffn(x_in, w1h, w1s, b1, w2h, w2s, b2, x, xpart, M, F, overflow, (hipStream_t)stream,
+                                    &wo, qkvh ? &qk : nullptr);
   if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("enc_ffn_wo: ") + hipGetErrorString(e));
   return ND_OK;
 }

@@ -50,6 +50,13 @@
 // whose out^T tiles are exactly y in the P16 k-permutation: its LayerNorm and
 // split run in registers, and y never goes to HBM (the unfused form wrote it
 // from a GEMM and read it back twice).
+//
+// QK (the next layer's QKV projection folded behind,
+// encoder/transformer.py:44 of layer l + 1): the epilogue's x rows are
+// LayerNorm'd from their exact statistics and split into the registers phase
+// 1 used, and the 24 slices of 32 columns of W'_qkv stream through the W1
+// slots (the first two issued during the last step) as 24 phase-1 products;
+// q | k | v leave from the accumulators (x is not re-read by a GEMM).
 #include <utility>
 
 #include "common.hpp"
@@ -105,25 +112,48 @@ __device__ __forceinline__ void ff_split(f32x4 x0, f32x4 x1, fh8& hi, fh8& lo) {
         (_Float16)(x1.z - (float)hi[6]), (_Float16)(x1.w - (float)hi[7])};
 }
 
-// NW waves copy a slice's 32 lane-linear 1 KB blocks into LDS, 32 / NW each
+// NW waves copy a slice's 32 lane-linear 1 KB blocks into LDS, 32 / NW each,
+// as buffer_load ... lds: one buffer descriptor per weight image (SGPRs),
+// the block's byte offset in an SGPR (soffset) and lane * 16 as the only
+// vector operand (the global_load_lds form kept a 64-bit address register
+// pair per block live across the loop: spills once the QKV fold was added;
+// FF_BUFLDS=0 keeps it)
+#ifndef FF_BUFLDS
+#define FF_BUFLDS 1
+#endif
+#if FF_BUFLDS
+typedef __amdgpu_buffer_rsrc_t ff_src;
+__device__ __forceinline__ ff_src ff_source(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void ff_piece(ff_src s, int off, char* dst, int lane) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(s, (lds_void*)dst, 16, lane * 16, off, 0, 0);
+}
+#else
+typedef const char* ff_src;
+__device__ __forceinline__ ff_src ff_source(const void* p) { return reinterpret_cast<const char*>(p); }
+__device__ __forceinline__ void ff_piece(ff_src s, int off, char* dst, int lane) {
+  __builtin_amdgcn_global_load_lds((const void*)(s + off + lane * 16), (lds_void*)dst, 16, 0, 0);
+}
+#endif
 // W1 slice j: column tiles 2j, 2j + 1 (contiguous in the P16H image)
 template <int NW>
-__device__ __forceinline__ void ff_copy_w1(const char* w1h, int j, char* dst, int wave, int lane) {
-  const char* src = w1h + (size_t)j * FF_SLICE + lane * 16;
+__device__ __forceinline__ void ff_copy_w1(ff_src w1h, int j, char* dst, int wave, int lane) {
+  const int wu = __builtin_amdgcn_readfirstlane(wave);
 #pragma unroll
   for (int i = 0; i < 32 / NW; ++i) {
-    const int blk = wave * (32 / NW) + i;
-    __builtin_amdgcn_global_load_lds((const void*)(src + blk * 1024), (lds_void*)(dst + blk * 1024), 16, 0, 0);
+    const int blk = wu * (32 / NW) + i;
+    ff_piece(w1h, j * FF_SLICE + blk * 1024, dst + blk * 1024, lane);
   }
 }
 // W2 slice j: output tile nt, k-block j, plane -> LDS block nt * 2 + plane
 template <int NW>
-__device__ __forceinline__ void ff_copy_w2(const char* w2h, int kp, int j, char* dst, int wave, int lane) {
+__device__ __forceinline__ void ff_copy_w2(ff_src w2h, int kp, int j, char* dst, int wave, int lane) {
+  const int wu = __builtin_amdgcn_readfirstlane(wave);
 #pragma unroll
   for (int i = 0; i < 32 / NW; ++i) {
-    const int blk = wave * (32 / NW) + i, nt = blk >> 1, pl = blk & 1;
-    const char* src = w2h + ((size_t)(nt * kp + j) * 2 + pl) * 1024 + lane * 16;
-    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(dst + blk * 1024), 16, 0, 0);
+    const int blk = wu * (32 / NW) + i, nt = blk >> 1, pl = blk & 1;
+    ff_piece(w2h, ((nt * kp + j) * 2 + pl) * 1024, dst + blk * 1024, lane);
   }
 }
 
@@ -134,33 +164,35 @@ __device__ __forceinline__ void ff_copy_w2(const char* w2h, int kp, int j, char*
 // WO: y is the block's residual input (the layer input x; x may alias it:
 // a workgroup reads its rows before it writes them), att the attention
 // output.  !WO: y is the FFN's input.
-template <int RG, bool WO>
+template <int RG, bool WO, bool QK>
 __global__ void __launch_bounds__(FF_BM / (16 * RG) * 64)
 enc_ffn_kernel(const float* y, const uint16_t* __restrict__ w1h, float w1s, const float* __restrict__ b1,
                const uint16_t* __restrict__ w2h, float w2s, const float* __restrict__ b2, float* x,
-               float* __restrict__ xpart, int M, int F, int* ovf, EncWo wo) {
+               float* __restrict__ xpart, int M, int F, int* ovf, EncWo wo, EncQkv qk) {
 #ifdef ND_SKIP_FFN  // timing probe only (tools/build_variant.sh): the kernel's marginal cost
   if (threadIdx.x < 100000) return;
 #endif
   constexpr int NW = FF_BM / (16 * RG), NT = NW * 64;
   // ONE shared array (a second __shared__ object beside LDS-DMA staging can
   // make hipcc drain vmcnt before every ds_read)
-  __shared__ __attribute__((aligned(16))) char smem[4 * FF_SLICE + (FF_MAXF + ND_D) * 4];
+  __shared__ __attribute__((aligned(16))) char smem[4 * FF_SLICE + (FF_MAXF + ND_D + (QK ? 3 * ND_D : 0)) * 4];
   // four 32 KB slots: W1 slices of even / odd chunks, then W2 slices
   auto w1slot = [&](int i) { return smem + (i & 1) * FF_SLICE; };
   auto w2slot = [&](int i) { return smem + (2 + (i & 1)) * FF_SLICE; };
   float* sb1 = reinterpret_cast<float*>(smem + 4 * FF_SLICE);
   float* sb2 = sb1 + FF_MAXF;
+  float* sqb = sb2 + ND_D;  // (QK) the next layer's q | k | v bias
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, q = lane >> 4;
   const int nch = F / FF_HC, kp = F / 32;
-  const char* W1 = reinterpret_cast<const char*>(w1h);
-  const char* W2 = reinterpret_cast<const char*>(w2h);
+  const ff_src W1 = ff_source(w1h), W2 = ff_source(w2h);
 
   // biases (ordinary loads: done before the first copy is issued, so no wait
   // on them later drains an in-flight copy)
   for (int i = tid; i < F; i += NT) sb1[i] = b1[i];
   for (int i = tid; i < ND_D; i += NT) sb2[i] = b2[i];
+  if constexpr (QK)
+    for (int i = tid; i < 3 * ND_D; i += NT) sqb[i] = qk.bias[i];
 
   // row group g's activation fragment: row r0 + 16 g + li, for every
   // k-block kb the 8 columns 32 kb + {4q..4q+3, 16+4q..16+4q+3} (the P16
@@ -233,7 +265,7 @@ enc_ffn_kernel(const float* y, const uint16_t* __restrict__ w1h, float w1s, cons
     __syncthreads();  // the biases in LDS (and every ordinary load retired)
     // y = the accumulators + att Wo^T: slice j (output columns 32 j .. +31,
     // tiles 2 j, 2 j + 1) from w1slot(j); W1_0 and W2_0 go out with the last
-    const char* WoH = reinterpret_cast<const char*>(wo.woh);
+    const ff_src WoH = ff_source(wo.woh);
     ff_copy_w1<NW>(WoH, 0, w1slot(0), wave, lane);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -347,7 +379,11 @@ enc_ffn_kernel(const float* y, const uint16_t* __restrict__ w1h, float w1s, cons
     if (k + 2 < nch) ff_copy_w1<NW>(W1, k + 2, w1slot(k), wave, lane);
     const f32x4* A2 = reinterpret_cast<const f32x4*>(w2slot(k)) + lane;
     const f32x4* A1 = reinterpret_cast<const f32x4*>(w1slot(k + 1)) + lane;
-    if (k + 1 == nch) {  // the last step: phase 2 alone
+    if (k + 1 == nch) {  // the last step: phase 2 alone (QK: the W1 slots take W'_qkv's first slices)
+      if constexpr (QK) {
+        ff_copy_w1<NW>(ff_source(qk.wh), 0, w1slot(0), wave, lane);
+        ff_copy_w1<NW>(ff_source(qk.wh), 1, w1slot(1), wave, lane);
+      }
 #pragma unroll
       for (int nt = 0; nt < 16; ++nt)
         p2_mfma(__builtin_bit_cast(fh8, A2[(nt * 2) * 64]), __builtin_bit_cast(fh8, A2[(nt * 2 + 1) * 64]), nt);
@@ -422,25 +458,73 @@ enc_ffn_kernel(const float* y, const uint16_t* __restrict__ w1h, float w1s, cons
         p[1] = q2;
       }
     }
+    if constexpr (QK) {  // LN(x) (the next layer's LayerNorm, affine folded into W'), split
+      const float rs = ln_rsqrt(q2 * (1.0f / ND_D) + ND_LN_EPS);
+#pragma unroll
+      for (int kb = 0; kb < 8; ++kb) ff_split((o[2 * kb] - m2) * rs, (o[2 * kb + 1] - m2) * rs, yh[g][kb], yl[g][kb]);
+    }
+  }
+  if constexpr (QK) {
+    // 24 slices of 32 output columns; slice j in W1 slot j & 1, the copy of
+    // slice j + 1 issued at the top of step j (slices 0 and 1: during the
+    // last main step).  Rows past M store the values of row M - 1 (their
+    // inputs were clamped to it): identical bytes, straight-line stores, so
+    // vmcnt(2 RG) at the top of a step (the previous step's stores) counts
+    // the copy exactly
+    const ff_src QH = ff_source(qk.wh);
+    for (int j = 0; j < 3 * ND_D / FF_HC; ++j) {
+      if (j == 0)
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * RG) : "memory");
+      if (j >= 1 && j + 1 < 3 * ND_D / FF_HC) ff_copy_w1<NW>(QH, j + 1, w1slot(j + 1), wave, lane);
+      const f32x4* A = reinterpret_cast<const f32x4*>(w1slot(j)) + lane;
+      f32x4 h[RG][2];
+#pragma unroll
+      for (int g = 0; g < RG; ++g) h[g][0] = h[g][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kb = 0; kb < 8; ++kb)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+          p1_mfma(__builtin_bit_cast(fh8, A[((t * 8 + kb) * 2) * 64]),
+                  __builtin_bit_cast(fh8, A[((t * 8 + kb) * 2 + 1) * 64]), t, kb, h);
+#pragma unroll
+      for (int g = 0; g < RG; ++g)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int n = FF_HC * j + 16 * t + 4 * q;
+          st4(qk.out + (size_t)min(row[g], M - 1) * 3 * ND_D + n, h[g][t] * qk.ws + ld4(sqb + n));
+        }
+    }
   }
 }
 
 hipError_t launch_enc_ffn(const float* y, const uint16_t* w1h, float w1s, const float* b1, const uint16_t* w2h,
                           float w2s, const float* b2, float* x, float* xpart, int M, int F, int* ovf, hipStream_t s,
-                          const EncWo* wo) {
+                          const EncWo* wo, const EncQkv* qk) {
   if (M <= 0) return hipSuccess;
   if (F % FF_HC != 0 || F > FF_MAXF || F < FF_HC || !y || !w1h || !b1 || !w2h || !b2 || !x)
     return hipErrorInvalidValue;
+  if (wo && (!wo->att || !wo->woh || !wo->bo || wo->att == x || wo->att == y)) return hipErrorInvalidValue;
+  if (!wo && x == y) return hipErrorInvalidValue;  // with wo, x may alias y (the residual): each
+                                                    // workgroup reads its rows before it writes them
+  if (qk && (!qk->wh || !qk->bias || !qk->out || qk->out == x || qk->out == y || (wo && qk->out == wo->att)))
+    return hipErrorInvalidValue;
   const dim3 grid((M + FF_BM - 1) / FF_BM), block(FF_BM / 16 * 64);
-  if (wo) {  // x may alias y (the residual): each workgroup reads its rows before it writes them
-    if (!wo->att || !wo->woh || !wo->bo || wo->att == x || wo->att == y) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((enc_ffn_kernel<1, true>), grid, block, 0, s, y, w1h, w1s, b1, w2h, w2s, b2, x, xpart, M, F,
-                       ovf, *wo);
-  } else {
-    if (x == y) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((enc_ffn_kernel<1, false>), grid, block, 0, s, y, w1h, w1s, b1, w2h, w2s, b2, x, xpart, M, F,
-                       ovf, EncWo());
-  }
+  const EncWo w = wo ? *wo : EncWo();
+  const EncQkv k = qk ? *qk : EncQkv();
+#define ND_FFN_GO(WO, QK)                                                                                          \
+  hipLaunchKernelGGL((enc_ffn_kernel<1, WO, QK>), grid, block, 0, s, y, w1h, w1s, b1, w2h, w2s, b2, x, xpart, M, F, \
+                     ovf, w, k)
+  if (wo && qk)
+    ND_FFN_GO(true, true);
+  else if (wo)
+    ND_FFN_GO(true, false);
+  else if (qk)
+    ND_FFN_GO(false, true);
+  else
+    ND_FFN_GO(false, false);
+#undef ND_FFN_GO
   return hipGetLastError();
 }
 

@@ -129,9 +129,18 @@ struct EncWo {
   float wos = 1.f;
   const float* bo = nullptr;
 };
+// qk (nullable): the NEXT layer's QKV projection folded behind, out = LN(x)
+// W'^T + b' (wh: P16H image of the LN-folded W' [768, 256], ws its scale;
+// out row-major [M, 768])
+struct EncQkv {
+  const uint16_t* wh = nullptr;
+  float ws = 1.f;
+  const float* bias = nullptr;
+  float* out = nullptr;
+};
 hipError_t launch_enc_ffn(const float* y, const uint16_t* w1h, float w1s, const float* b1, const uint16_t* w2h,
                           float w2s, const float* b2, float* x, float* xpart, int M, int F, int* ovf, hipStream_t s,
-                          const EncWo* wo = nullptr);
+                          const EncWo* wo = nullptr, const EncQkv* qk = nullptr);
 // out[r] = LN(x[r]) (rows of 256)
 hipError_t launch_layernorm(const float* x, const float* g, const float* b, float* out, int rows, hipStream_t s);
 

@@ -470,14 +470,17 @@ def op_pack_p16h(W: torch.Tensor):
     return Wh, sc.value
 
 
-def op_enc_ffn(y, W1, b1, W2, b2, ln_g, ln_b, att=None, Wo=None, bo=None, inplace=False):
+def op_enc_ffn(y, W1, b1, W2, b2, ln_g, ln_b, att=None, Wo=None, bo=None, inplace=False, Wq=None, bq=None,
+               lnq_g=None, lnq_b=None):
     """The encoder's fused FFN block (nd_op_enc_ffn): x = y + W2 relu(W1
     LN(y) + b1) + b2 for row-major y [M, 256], the LN affine folded and both
     weights packed to P16H images here as the engine does at load time.
     With att, Wo, bo (nd_op_enc_ffn_wo) y is first replaced by
     y + att Wo^T + bo (the attention block's output projection and residual);
-    inplace: x is written over y, as the engine does.
-    Returns (x, row stats [M, 2] = {mean, M2}, overflow flag)."""
+    inplace: x is written over y, as the engine does.  With Wq, bq, lnq_g,
+    lnq_b too the next layer's projection LN(x) Wq^T + bq is computed in the
+    same launch and returned as a fourth value.
+    Returns (x, row stats [M, 2] = {mean, M2}, overflow flag[, qkv])."""
     M, F = y.shape[0], W1.shape[0]
     W1f, b1f = op_fold_layernorm(W1, b1, ln_g, ln_b)
     w1h, w1s = op_pack_p16h(W1f)
@@ -488,9 +491,19 @@ def op_enc_ffn(y, W1, b1, W2, b2, ln_g, ln_b, att=None, Wo=None, bo=None, inplac
     s = ctypes.c_void_p(torch.cuda.current_stream(y.device).cuda_stream)
     if Wo is not None:
         woh, wos = op_pack_p16h(Wo)
+        qh, qs, qb, qkv = None, 1.0, None, None
+        if Wq is not None:
+            Wqf, qb = op_fold_layernorm(Wq, bq, lnq_g, lnq_b)
+            qh, qs = op_pack_p16h(Wqf)
+            qkv = torch.empty(M, Wq.shape[0], dtype=torch.float32, device=y.device)
         _lib.check(_lib.lib().nd_op_enc_ffn_wo(_ptr(att), _ptr(y), _ptr(woh), wos, _ptr(bo), _ptr(w1h), w1s,
-                                               _ptr(b1f), _ptr(w2h), w2s, _ptr(b2), _ptr(x), _ptr(part), M, F,
-                                               _ptr(ov), s), "nd_op_enc_ffn_wo")
+                                               _ptr(b1f), _ptr(w2h), w2s, _ptr(b2), _ptr(x), _ptr(part),
+                                               _ptr(qh) if qh is not None else None, qs,
+                                               _ptr(qb) if qb is not None else None,
+                                               _ptr(qkv) if qkv is not None else None, M, F, _ptr(ov), s),
+                   "nd_op_enc_ffn_wo")
+        if qkv is not None:
+            return x, part[:, 0, :], ov, qkv
     else:
         _lib.check(_lib.lib().nd_op_enc_ffn(_ptr(y), _ptr(w1h), w1s, _ptr(b1f), _ptr(w2h), w2s, _ptr(b2), _ptr(x),
                                             _ptr(part), M, F, _ptr(ov), s), "nd_op_enc_ffn")

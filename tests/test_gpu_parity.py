@@ -64,7 +64,7 @@ def test_gemm_vs_fp64(M, N, K, ln, relu, res, split):
 
 
 @pytest.mark.parametrize("M,F", [(1000, 2048), (256, 2048), (131, 64), (384, 512)])
-@pytest.mark.parametrize("wo", ["none", "wo", "wo_inplace"])
+@pytest.mark.parametrize("wo", ["none", "wo", "wo_inplace", "wo_qkv"])
 def test_enc_ffn_fused_vs_fp64(M, F, wo):
     """The encoder's fused FFN block (nd_op_enc_ffn: LayerNorm, W1, ReLU, W2
     and the residual in one launch, the hidden kept on chip) against fp64,
@@ -72,7 +72,9 @@ def test_enc_ffn_fused_vs_fp64(M, F, wo):
     2e-4 absolute bound as the split GEMMs, and the exact row statistics it
     hands to the next LayerNorm.  wo: the attention's output projection and
     residual folded in front (nd_op_enc_ffn_wo: y = x + att Wo^T + bo never
-    leaves the chip), written over the input as the engine does (inplace)."""
+    leaves the chip), written over the input as the engine does (inplace);
+    wo_qkv: the next layer's LN + QKV projection folded behind (its q | k | v
+    from the block's registers) against LN(x) Wq^T + bq in fp64."""
     from nanodecoder_amd.engine import op_enc_ffn
     g = torch.Generator().manual_seed(M + F)
     y = torch.randn(M, 256, generator=g) * 2 + 0.5
@@ -86,10 +88,18 @@ def test_enc_ffn_fused_vs_fp64(M, F, wo):
     Wo = torch.randn(256, 256, generator=g) / 16
     bo = torch.randn(256, generator=g) * 0.1
     dev = torch.device("cuda", 0)
+    Wq = torch.randn(768, 256, generator=g) / 16
+    bq = torch.randn(768, generator=g) * 0.1
+    lq = 1 + 0.1 * torch.randn(256, generator=g)
+    lqb = 0.1 * torch.randn(256, generator=g)
     kw = {}
     if wo != "none":
-        kw = dict(att=att.to(dev), Wo=Wo.to(dev), bo=bo.to(dev), inplace=wo == "wo_inplace")
-    x, st, ov = op_enc_ffn(*(t.to(dev) for t in (y, W1, b1, W2, b2, lg, lb)), **kw)
+        kw = dict(att=att.to(dev), Wo=Wo.to(dev), bo=bo.to(dev), inplace=wo != "wo")
+    if wo == "wo_qkv":
+        kw.update(Wq=Wq.to(dev), bq=bq.to(dev), lnq_g=lq.to(dev), lnq_b=lqb.to(dev))
+        x, st, ov, qkv = op_enc_ffn(*(t.to(dev) for t in (y, W1, b1, W2, b2, lg, lb)), **kw)
+    else:
+        x, st, ov = op_enc_ffn(*(t.to(dev) for t in (y, W1, b1, W2, b2, lg, lb)), **kw)
     torch.cuda.synchronize()
     yd = y.double()
     if wo != "none":
@@ -103,6 +113,10 @@ def test_enc_ffn_fused_vs_fp64(M, F, wo):
     assert torch.allclose(st[:, 0], got.mean(1), atol=1e-5)
     assert torch.allclose(st[:, 1], ((got - got.mean(1, keepdim=True)) ** 2).sum(1), rtol=1e-4, atol=1e-3)
     assert int(ov.cpu()[0]) == 0
+    if wo == "wo_qkv":
+        qref = torch.nn.functional.layer_norm(ref, (256,), lq.double(), lqb.double(), 1e-6) @ Wq.double().t() \
+            + bq.double()
+        assert (qkv.cpu().double() - qref).abs().max().item() < 2e-4
 
 
 @pytest.mark.parametrize("N,K,mag", [(256, 256, 1.0), (768, 256, 3e-4), (256, 2048, 40.0)])

@@ -100,10 +100,18 @@ if ONLY == "encffn":  # the fused FFN block against the two split GEMMs it repla
     att, bo = torch.randn(M, 256, device=dev), torch.randn(256, device=dev)
     us = timeit(lambda: _lib.lib().nd_op_enc_ffn_wo(att.data_ptr(), y.data_ptr(), woh.data_ptr(), wos, bo.data_ptr(),
                                                      w1h.data_ptr(), w1s, b1f.data_ptr(), w2h.data_ptr(), w2s,
-                                                     b2.data_ptr(), x.data_ptr(), part.data_ptr(), M, 2048, None,
-                                                     st()), n=5)
+                                                     b2.data_ptr(), x.data_ptr(), part.data_ptr(), None, 1.0, None,
+                                                     None, M, 2048, None, st()), n=5)
     fl = 2 * M * 256 * (2 * 2048 + 256)
     print(f"enc-ffn + Wo M={M}: {us:9.2f} us  {fl / (us * 1e-6) / 1e12:6.1f} TF/s (fp32-equiv)")
+    qh, qs = E.op_pack_p16h(torch.randn(768, 256, device=dev) / 16)
+    qb, qkv = torch.randn(768, device=dev), torch.empty(M, 768, device=dev)
+    us = timeit(lambda: _lib.lib().nd_op_enc_ffn_wo(att.data_ptr(), y.data_ptr(), woh.data_ptr(), wos, bo.data_ptr(),
+                                                     w1h.data_ptr(), w1s, b1f.data_ptr(), w2h.data_ptr(), w2s,
+                                                     b2.data_ptr(), x.data_ptr(), part.data_ptr(), qh.data_ptr(), qs,
+                                                     qb.data_ptr(), qkv.data_ptr(), M, 2048, None, st()), n=5)
+    fl = 2 * M * 256 * (2 * 2048 + 256 + 768)
+    print(f"enc-ffn + Wo + QKV M={M}: {us:9.2f} us  {fl / (us * 1e-6) / 1e12:6.1f} TF/s (fp32-equiv)")
     gemm_case(M, 2048, 256, True, True, False, True)
     gemm_case(M, 256, 2048, False, False, True, True)
     sys.exit(0)
