@@ -579,6 +579,102 @@ hipError_t launch_enc_attention(const float* qkv, const float* signal, const int
   return hipGetLastError();
 }
 
+// Layer 0's attention in closed form (kernels.hpp launch_enc_attention_rank2;
+// multi_headed_attn.py:154-177 with the key mask of encoder/transformer.py:
+// 117-121).  One workgroup per chunk, one query per thread: the unmasked keys'
+// (y, r) are compacted into LDS (a masked key's score is the -1e18 fill, whose
+// weight is exactly 0 beside any unmasked key; a chunk with no unmasked key
+// is uniform over its keys, which all share s = 0, so one representative key
+// gives the same expectations); two passes over them per (query, head):
+// the maximum, then exp2 and the three sums; the 8 heads' E[y], E[r] meet in
+// LDS and every wave writes whole 1 KB output rows.
+__global__ void __launch_bounds__(512)
+enc_attention_rank2_kernel(const float* __restrict__ signal, const int* __restrict__ span, EmbedQkv eq,
+                           const float* __restrict__ coef, float* __restrict__ out, int T) {
+  __shared__ __attribute__((aligned(16))) float2 kyr[ENC_MAXT];   // unmasked keys: (y, r)
+  __shared__ __attribute__((aligned(16))) float ex[ENC_MAXT][17];  // per query: E[y], E[r] of 8 heads (+ pad)
+  __shared__ int wcnt[8];
+  const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int L = min(span[b], T);
+  const float s = signal[(size_t)b * T + min(t, L - 1)];
+  const float r = ln_rsqrt(fmaf(s, fmaf(s, eq.mww, 2.0f * eq.mwb), eq.mbb) + ND_LN_EPS), y = s * r;
+  // compaction of the unmasked keys u < L (signal != 0), in key order
+  const bool key = t < L && s != 0.0f;
+  const unsigned long long bal = __ballot(key);
+  if (lane == 0) wcnt[wave] = __popcll(bal);
+  __syncthreads();
+  int base = 0, n_um = 0;
+#pragma unroll
+  for (int w = 0; w < 8; ++w) {
+    base += w < wave ? wcnt[w] : 0;
+    n_um += wcnt[w];
+  }
+  if (key) kyr[base + __popcll(bal & ((1ull << lane) - 1ull))] = make_float2(y, r);
+  if (n_um == 0 && t == 0) kyr[0] = make_float2(0.0f, ln_rsqrt(eq.mbb + ND_LN_EPS));  // all masked: s = 0
+  const int nk = n_um > 0 ? n_um : 1;
+  __syncthreads();
+  if (t < L) {
+    // alpha_h, beta_h of this query (log2 units); heads in pairs for packed math
+    ef2 al[4], be[4];
+#pragma unroll
+    for (int h = 0; h < 8; ++h) {
+      const float* k = coef + h * 6;
+      const float a = fmaf(k[0], y, fmaf(k[1], r, k[2])), bb = fmaf(k[3], y, fmaf(k[4], r, k[5]));
+      al[h >> 1][h & 1] = a;
+      be[h >> 1][h & 1] = bb;
+    }
+    ef2 m[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) m[p] = ef2{-INFINITY, -INFINITY};
+    for (int u = 0; u < nk; ++u) {
+      const float2 k = kyr[u];
+      const ef2 ky = {k.x, k.x}, kr = {k.y, k.y};
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const ef2 l = al[p] * ky + be[p] * kr;
+        m[p] = ef2{fmaxf(m[p].x, l.x), fmaxf(m[p].y, l.y)};
+      }
+    }
+    ef2 sp[4], sy[4], sr[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) sp[p] = sy[p] = sr[p] = ef2{0.f, 0.f};
+    for (int u = 0; u < nk; ++u) {
+      const float2 k = kyr[u];
+      const ef2 ky = {k.x, k.x}, kr = {k.y, k.y};
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const ef2 d = al[p] * ky + (be[p] * kr - m[p]);
+        const ef2 e = {__builtin_amdgcn_exp2f(d.x), __builtin_amdgcn_exp2f(d.y)};
+        sp[p] += e;
+        sy[p] += e * ky;
+        sr[p] += e * kr;
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const float inv = __builtin_amdgcn_rcpf(sp[p][j]);
+        ex[t][2 * (2 * p + j)] = sy[p][j] * inv;
+        ex[t][2 * (2 * p + j) + 1] = sr[p][j] * inv;
+      }
+  }
+  __syncthreads();
+  // out[t][32 h + d] = a_v[h][d] E[y] + c_v[h][d] E[r] + b_v[h][d]: wave w writes rows w, w + 8, ...
+  const int n = 2 * ND_D + lane * 4, h = lane >> 3;
+  const f32x4 av = ld4(eq.ac + n), cv = ld4(eq.ac + 3 * ND_D + n), bv = ld4(eq.bias + n);
+  for (int q = wave; q < L; q += 8)
+    st4(out + ((size_t)b * T + q) * ND_D + lane * 4, av * ex[q][2 * h] + cv * ex[q][2 * h + 1] + bv);
+}
+
+hipError_t launch_enc_attention_rank2(const float* signal, const int* span, const EmbedQkv& eq, const float* coef,
+                                      float* out, int B, int T, hipStream_t s) {
+  if (T > ENC_MAXT || T <= 0 || !eq.ac || !eq.bias || !coef) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(enc_attention_rank2_kernel, dim3(B), dim3(512), 0, s, signal, span, eq, coef, out, T);
+  return hipGetLastError();
+}
+
+
 // ------------------------------------------------------------------ decoder
 __global__ void __launch_bounds__(256)
 dec_embed_kernel(const int* __restrict__ tok, const float* __restrict__ emb, const float* __restrict__ pe, int step,

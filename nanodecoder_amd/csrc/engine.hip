@@ -146,6 +146,9 @@ struct nd_ctx {
   double* eq_scal = nullptr;
   float eq_m[3] = {0.f, 0.f, 0.f};
   bool eq_ready = false;
+  // layer 0's attention in the same closed form: per head the 6 coefficients
+  // of alpha_t, beta_t (launch_enc_attention_rank2), on the device
+  float* eq_coef = nullptr;
   std::vector<EncLayer> enc;
   std::vector<NanoLayer> nano;
   float* nano_W = nullptr;
@@ -560,10 +563,20 @@ static bool enc_qkv_folded(const nd_ctx* c, const EncLayer& next) {
   return on && next.qkvh != nullptr;
 }
 
+// layer 0's attention in closed form (launch_enc_attention_rank2): no q | k | v
+// rows at all for layer 0; ND_ENC_ATTN0=0 keeps the split-fp16 attention (A/B)
+static bool enc_attn0_rank2(const nd_ctx* c) {
+  static const bool on = [] {
+    const char* e = getenv("ND_ENC_ATTN0");
+    return !(e && atoi(e) == 0);
+  }();
+  return on && c->eq_ready && c->eq_coef != nullptr;
+}
+
 static hipError_t enqueue_encode_transformer(nd_ctx* c, int B, int T, hipStream_t s) {
   const int M = B * T, D = c->D, F = c->F;
   nd::EmbedQkv eq;
-  const bool r2 = enc_qkv0_rank2(c);
+  const bool r2 = enc_qkv0_rank2(c), a0 = r2 && enc_attn0_rank2(c);
   if (r2) {
     eq.ac = c->eq_ac;
     eq.bias = c->enc[0].nbqkv;
@@ -572,7 +585,8 @@ static hipError_t enqueue_encode_transformer(nd_ctx* c, int B, int T, hipStream_
     eq.mbb = c->eq_m[2];
     eq.qkv = c->big;
   }
-  LCHK(nd::launch_enc_embed(c->sig, c->enc_lin_w, c->enc_lin_b, c->x, c->x_part, B, T, s, r2 ? &eq : nullptr));
+  LCHK(nd::launch_enc_embed(c->sig, c->enc_lin_w, c->enc_lin_b, c->x, c->x_part, B, T, s,
+                            r2 && !a0 ? &eq : nullptr));
   int pnx = 1, pny = 0;
   bool qkv_done = r2;  // this layer's q | k | v already in c->big
   for (size_t li = 0; li < c->enc.size(); ++li) {
@@ -580,7 +594,10 @@ static hipError_t enqueue_encode_transformer(nd_ctx* c, int B, int T, hipStream_
     // encoder/transformer.py:36-54
     if (!qkv_done) LCHK(G(c->x, D, L.nwqkv, 3 * D, D, L.nbqkv, c->big, 3 * D, M).h3(c).ln(c->x_part, pnx).run(s));
     qkv_done = false;
-    LCHK(nd::launch_enc_attention(c->big, c->sig, c->span, c->att, B, T, s, c->exact, c->ovf));
+    if (a0 && li == 0)
+      LCHK(nd::launch_enc_attention_rank2(c->sig, c->span, eq, c->eq_coef, c->att, B, T, s));
+    else
+      LCHK(nd::launch_enc_attention(c->big, c->sig, c->span, c->att, B, T, s, c->exact, c->ovf));
     if (enc_wo_fused(c, L)) {  // Wo + residual, LN, FFN in one launch; the layer's rows updated in place
       nd::EncWo wo;
       wo.att = c->att;
@@ -1137,6 +1154,29 @@ int nd_finalize(nd_ctx* c) {
       HIPCHK(hipMemcpyAsync(m, c->eq_scal, sizeof(m), hipMemcpyDeviceToHost, c->es));
       HIPCHK(hipStreamSynchronize(c->es));
       for (int i = 0; i < 3; ++i) c->eq_m[i] = (float)m[i];
+      // per head h: alpha = k0 y + k1 r + k2, beta = k3 y + k4 r + k5 with
+      // k = (a_q, c_q, b_q) . (a_k | c_k) log2(e) / sqrt(32), in double
+      std::vector<float> ac(6 * D), nb(3 * D), coef(ND_H * 6);
+      HIPCHK(hipMemcpyAsync(ac.data(), c->eq_ac, ac.size() * 4, hipMemcpyDeviceToHost, c->es));
+      HIPCHK(hipMemcpyAsync(nb.data(), c->enc[0].nbqkv, nb.size() * 4, hipMemcpyDeviceToHost, c->es));
+      HIPCHK(hipStreamSynchronize(c->es));
+      const double sc = 1.4426950408889634 / std::sqrt((double)(D / ND_H));
+      for (int h = 0; h < ND_H; ++h) {
+        double k[6] = {0, 0, 0, 0, 0, 0};
+        for (int d = 0; d < D / ND_H; ++d) {
+          const int i = h * (D / ND_H) + d;
+          const double aq = ac[i], ak = ac[D + i], cq = ac[3 * D + i], ck = ac[4 * D + i], bq = nb[i];
+          k[0] += aq * ak;
+          k[1] += cq * ak;
+          k[2] += bq * ak;
+          k[3] += aq * ck;
+          k[4] += cq * ck;
+          k[5] += bq * ck;
+        }
+        for (int j = 0; j < 6; ++j) coef[h * 6 + j] = (float)(k[j] * sc);
+      }
+      if (!c->eq_coef && dalloc(c, &c->eq_coef, coef.size()) != hipSuccess) return fail(ND_ERR_HIP, "alloc");
+      HIPCHK(hipMemcpy(c->eq_coef, coef.data(), coef.size() * 4, hipMemcpyHostToDevice));
       c->eq_ready = true;
     }
     if (c->nctxkv_w)
@@ -1542,7 +1582,7 @@ static const struct {
                  {"ND_HEAD_FUSE", 1},  {"ND_LSTM_F32", 0},     {"ND_LSTM_LIBM", 0},     {"ND_LSTM_SEQ", 4},
                  {"ND_ENC_ATTN_NQ", 2}, {"ND_ENC_ATTN_GRID", 0}, {"ND_ENC_ATTN_F32", 0}, {"ND_SELF_XCD", 1},
                  {"ND_ENC_WO", 1},     {"ND_ENC_QKV0", 1},
-                 {"ND_ENC_QKV", 1}};
+                 {"ND_ENC_QKV", 1},    {"ND_ENC_ATTN0", 1}};
 
 int nd_switches(char* buf, int32_t len) {
   std::string out;

@@ -98,6 +98,14 @@ struct EmbedQkv {
   float mww = 0.f, mwb = 0.f, mbb = 0.f;
   float* qkv = nullptr;       // [M, 768] row-major
 };
+// Layer 0's attention in the same closed form: per head h the query, key
+// and value of position t are u_h y_t + v_h r_t + w_h (y = s r, r the LN
+// scale of the row), so a score is y_u alpha_t + r_u beta_t + (a constant
+// of t that cancels in the softmax) with alpha_t, beta_t linear in
+// (y_t, r_t, 1) (coef [8 heads][6], log2 units), and the output is
+// a_v E[y] + c_v E[r] + b_v over the softmax: out [M, 256] row-major.
+hipError_t launch_enc_attention_rank2(const float* signal, const int* span, const EmbedQkv& eq, const float* coef,
+                                      float* out, int B, int T, hipStream_t s);
 // ac and the three means (double scal[3]) from the LN-folded weight [768, 256]
 hipError_t launch_embed_qkv_prep(const float* w_in, const float* b_in, const float* nwqkv, float* ac, double* scal,
                                  hipStream_t s);

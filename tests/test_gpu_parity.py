@@ -768,6 +768,34 @@ def test_beam_large_batch_vs_oracle():
             assert abs(sc[i, nb] - s) < 1e-3, (i, nb)
 
 
+def test_transformer_encoder_vs_oracle_masks():
+    """The transformer encoder (layer 0's attention in closed form, its QKV in
+    none; layers 1-2 through the folded FFN launches) against the oracle's
+    encoder: masked keys (signal 0), an all-zero chunk (uniform attention), a
+    ragged span, a large-amplitude chunk; rows past a chunk's span are not
+    compared (no query there)."""
+    ref = _oracle()
+    cfg = synth.ModelConfig()
+    W = synth.make_weights(cfg, seed=21)
+    B = 6
+    sig = synth.synth_chunk_batch(B, 512, seed=21)
+    lens = np.full(B, 512, np.int32)
+    spans = np.full(B, 512, np.int32)
+    sig[1, ::7] = 0.0
+    sig[2, :] = 0.0
+    lens[3], spans[3] = 300, 300
+    sig[3, 300:] = 0.0
+    lens[4] = 200
+    sig[4, 200:] = 0.0          # zero padding inside the span: masked keys
+    sig[5] *= 5.0
+    eng = _engine(cfg, W, max_batch=B, max_steps=10)
+    mem = eng.encode(sig, lens, spans).cpu().numpy()
+    exp_mem = ref.RefModel(cfg, W).encode(torch.from_numpy(sig), lens).numpy()
+    for i in range(B):
+        L = spans[i]
+        assert np.abs(mem[i, :L] - exp_mem[i, :L]).max() < 1e-4, i
+
+
 def test_nano_greedy_vs_oracle_ragged():
     """NanoEncoder packing: ragged lengths inside one batch (reverse LSTM
     starts at len-1), B not a multiple of the 16-sequence LSTM group."""
