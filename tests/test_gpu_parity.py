@@ -769,8 +769,8 @@ def test_beam_large_batch_vs_oracle():
 
 
 def test_transformer_encoder_vs_oracle_masks():
-    """The transformer encoder (layer 0's attention in closed form, its QKV in
-    none; layers 1-2 through the folded FFN launches) against the oracle's
+    """The transformer encoder (layer 0's QKV in closed form from the
+    embedding; every layer through the folded FFN launches) against the oracle's
     encoder: masked keys (signal 0), an all-zero chunk (uniform attention), a
     ragged span, a large-amplitude chunk; rows past a chunk's span are not
     compared (no query there)."""
