@@ -68,6 +68,9 @@ def parse():
     ap.add_argument("--bank-nt-lanes", default="auto",
                     help="comma list of EnginePool lanes whose memory bank streams with non-temporal loads "
                          "(auto: every lane when --inflight > 1; none: no lane)")
+    ap.add_argument("--bank-grid", default="auto",
+                    help="memory-bank kernel workgroups at most per pool lane (auto: half the CUs with several "
+                         "lanes; 0: one per chunk)")
     ap.add_argument("--inflight", type=int, default=3,
                     help="translate calls on the device at once (EnginePool lanes: one engine context and HIP "
                          "stream each); 1 = one call at a time")
@@ -436,6 +439,10 @@ def run_calls(pool, n, call):
     return outs[(n - 1) % pool.lanes]
 
 
+def bank_grid(args):
+    return None if args.bank_grid == "auto" else int(args.bank_grid)
+
+
 def nt_lanes(args):
     if args.bank_nt_lanes == "auto":
         return None
@@ -483,7 +490,8 @@ def run_batch(args, world, rank, dev, cfg, W):
 
     beam = args.beam if args.mode == "beam" else 1
     eng = EnginePool(cfg, W, device=dev.index, lanes=args.inflight, max_batch=args.batch, max_src_len=512,
-                     max_steps=args.max_length, max_beam=beam, bank_nt_lanes=nt_lanes(args))
+                     max_steps=args.max_length, max_beam=beam, bank_nt_lanes=nt_lanes(args),
+                     bank_grid=bank_grid(args))
     # each rank gets its own shard of synthetic reads
     sig_np = synth.synth_chunk_batch(args.batch, 512, seed=1000 + rank, inject_masks=False)
     lens_np = np.full(args.batch, 512, np.int32)
@@ -509,7 +517,8 @@ def run_batch(args, world, rank, dev, cfg, W):
         "data": "synthetic reads, random-init weights",
         "config": {"workload": workload(args), "chunks_per_gpu_per_step": args.batch,
                    "global_batch": args.batch * world, "seq_len": 512, "parallelism": f"read-shard x{world}",
-                   "calls_in_flight_per_gpu": eng.lanes, "bank_nontemporal_lanes": list(eng.bank_nt_lanes)},
+                   "calls_in_flight_per_gpu": eng.lanes, "bank_nontemporal_lanes": list(eng.bank_nt_lanes),
+                   "bank_kernel_workgroups": eng.bank_grid or "one per chunk"},
         "samples_per_sec_per_gpu": round(value / world, 1),
         "bases_per_sec": round(bases_per_step * args.steps * world / dt, 1),
         "timed_seconds": round(dt, 3),
@@ -525,6 +534,8 @@ def run_batch(args, world, rank, dev, cfg, W):
                                                 "every lane (the other lanes' kernels run beside them)")
         # the same calls one at a time (lane 0 only, each joined before the next): per-call latency
         one = eng.subset(1)
+        # a lone call has every CU: the bank kernel at one workgroup per chunk (nd_set_bank_grid)
+        eng.engines[0].set_bank_grid(0)
         n1 = max(3, min(40, args.steps // 4))
         run_calls(one, 2, call)
         dt1, _ = timed(one, n1, call, world)
@@ -536,7 +547,8 @@ def run_batch(args, world, rank, dev, cfg, W):
             # the kernel with the GPU to itself (as rocprof's serialised kernel trace times it)
             roof_iso = kernel_roofline(one, args.batch, args.mode, beam, args.encoder)
             roof_iso["timing"] = ("in-kernel wall-clock stamps, launches of the last call of the timed "
-                                  "one-call-in-flight leg (the kernel alone on the GPU)")
+                                  "one-call-in-flight leg (the kernel alone on the GPU, one workgroup per chunk)")
+        eng.engines[0].set_bank_grid(eng.bank_grid)
     alive = None
     if args.mode == "beam":
         e0 = eng.engines[0]

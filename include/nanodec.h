@@ -236,6 +236,15 @@ int nd_set_exact_fp32(nd_ctx* ctx, int enable);
  * cache.  Default 0.  No reference counterpart. */
 int nd_set_bank_policy(nd_ctx* ctx, int nontemporal);
 
+/* Workgroups of the greedy memory-bank kernel at most: 0 (default) = one per
+ * chunk, i.e. every CU while it streams; n > 0 = n workgroups walking the
+ * chunks.  The kernel holds 137 KB of a CU's 160 KB LDS, so while it runs no
+ * other context's LDS-staged GEMM fits beside it; EnginePool lanes cap it at
+ * half the CUs (measured, 3 lanes x 256 chunks: 18.3 -> 17.6 ms per call).
+ * Same results (each chunk is one workgroup's work either way).  No reference
+ * counterpart. */
+int nd_set_bank_grid(nd_ctx* ctx, int32_t workgroups);
+
 /* Split-fp16 range guard.  An activation operand the split form carries as
  * fp16 hi/lo leaves the fp16 range from |x| = 65504 on, where the
  * reference's fp32 arithmetic is still finite.  Every kernel that splits an
@@ -431,11 +440,12 @@ int nd_op_memory_pack(const float* x, const float* ln_g, const float* ln_b, floa
  * ln_g/ln_b when set; rows t >= T zero).  nd_op_dec_bank_h3: qp [C16, 2048]
  * P16 as nd_op_dec_mem_attention, bank from nd_op_bank_pack_h3, T in
  * (448, 512]; out U [C16, 2048] P16.  ovf (nullable): set to 1 when an
- * operand reaches the fp16 range (|x| >= 65504). */
+ * operand reaches the fp16 range (|x| >= 65504).  grid: workgroups at most
+ * (0 = one per chunk; fewer walk the chunks, as nd_set_bank_grid). */
 int nd_op_bank_pack_h3(const float* x, const float* ln_g, const float* ln_b, uint16_t* out, int32_t B, int32_t T,
                        int32_t* ovf, void* stream);
 int nd_op_dec_bank_h3(const float* qp, const uint16_t* bank, const float* signal, const int32_t* span, float pad_val,
-                      float* out, int32_t C, int32_t T, int32_t* ovf, void* stream);
+                      float* out, int32_t C, int32_t T, int32_t* ovf, int32_t grid, void* stream);
 
 /* Decoder context attention (multi_headed_attn.py:142-177): rows r = c*rpc+j
  * of q [C*rpc, d] attend over K at kv[(c*T+t)*ld + koff] and V at +d, keys

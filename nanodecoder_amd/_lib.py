@@ -59,6 +59,7 @@ SIGNATURES = {
     "nd_set_timing": (_I, [_P, _I]),
     "nd_set_exact_fp32": (_I, [_P, _I]),
     "nd_set_bank_policy": (_I, [_P, _I]),
+    "nd_set_bank_grid": (_I, [_P, _I]),
     "nd_take_overflow": (_I, [_P, _P, _P]),
     "nd_set_ctx_path": (_I, [_P, _I]),
     "nd_last_timing": (_I, [_P, ctypes.POINTER(_F), ctypes.POINTER(_F)]),
@@ -84,7 +85,7 @@ SIGNATURES = {
     "nd_op_dec_mem_attention": (_I, [_P, _P, _P, _P, ctypes.c_float, _P, _I, _I, _I, _I, _P]),
     "nd_op_memory_pack": (_I, [_P, _P, _P, _P, _I, _I, _I, _P]),
     "nd_op_bank_pack_h3": (_I, [_P, _P, _P, _P, _I, _I, _P, _P]),
-    "nd_op_dec_bank_h3": (_I, [_P, _P, _P, _P, ctypes.c_float, _P, _I, _I, _P, _P]),
+    "nd_op_dec_bank_h3": (_I, [_P, _P, _P, _P, ctypes.c_float, _P, _I, _I, _P, _I, _P]),
     "nd_op_lstm_layer": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _I, _P]),
     "nd_op_enc_attention": (_I, [_P, _P, _P, _P, _I, _I, _P]),
     "nd_op_dec_self_attention": (_I, [_P, _P, _P, _I, _I, _I, _P, _I, _P]),

@@ -103,12 +103,14 @@ struct GraphKey {
   float temp = 0.f;
   int exact = 0;  // exact fp32 products (set by run_graph from the ctx)
   int bank_nt = 0;  // memory bank streamed non-temporally (set by run_graph from the ctx)
+  int bank_grid = 0;  // the bank kernel's workgroup cap (set by run_graph from the ctx)
   int tail = 0;   // --fast beam tail segments (nd_ctx.beam_tail)
   bool operator<(const GraphKey& o) const {
     return std::tie(mode, B, T, S, min_len, beam, n_best, seg, logp, alpha, stamp, attn, cov, stepwise, ngram, excl,
-                    beta, topk, temp, exact, tail, bank_nt) <
+                    beta, topk, temp, exact, tail, bank_nt, bank_grid) <
            std::tie(o.mode, o.B, o.T, o.S, o.min_len, o.beam, o.n_best, o.seg, o.logp, o.alpha, o.stamp, o.attn,
-                    o.cov, o.stepwise, o.ngram, o.excl, o.beta, o.topk, o.temp, o.exact, o.tail, o.bank_nt);
+                    o.cov, o.stepwise, o.ngram, o.excl, o.beta, o.topk, o.temp, o.exact, o.tail, o.bank_nt,
+                    o.bank_grid);
   }
 };
 
@@ -137,6 +139,8 @@ struct nd_ctx {
   // EnginePool lane whose bank should not displace another lane's from the
   // Infinity Cache
   bool bank_nt = false;
+  // workgroups of the bank kernel at most (nd_set_bank_grid; 0 = one per chunk)
+  int bank_grid = 0;
 
   // weights
   float *enc_lin_w = nullptr, *enc_lin_b = nullptr, *enc_ln_g = nullptr, *enc_ln_b = nullptr;
@@ -764,7 +768,7 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
       if (c->bank_h3)
         LCHK(nd::launch_dec_bank_h3(c->dqk, reinterpret_cast<const uint16_t*>(c->mem_p), c->sig, c->span,
                                     (float)c->cfg.pad_idx, c->dU, C, T, s, stamp, dbg, dbg_stride, c->ovf,
-                                    c->bank_nt));
+                                    c->bank_nt, c->bank_grid));
       else
         LCHK(nd::launch_dec_mem_attention(c->dqk, c->mem, c->sig, c->span, (float)c->cfg.pad_idx, c->dU, C, rpc, T,
                                           T, s, stamp, dbg, dbg_stride));
@@ -874,6 +878,7 @@ static int run_graph(nd_ctx* c, const GraphKey& key, F&& enqueue) {
   k.exact = c->exact ? 1 : 0;  // both product forms keep their graphs (the overflow rerun switches)
   k.tail = c->beam_tail ? 1 : 0;
   k.bank_nt = c->bank_nt ? 1 : 0;
+  k.bank_grid = c->bank_grid;
   auto it = c->graphs.find(k);
   if (it == c->graphs.end()) {
     hipGraph_t g = nullptr;
@@ -1628,6 +1633,13 @@ int nd_set_bank_policy(nd_ctx* c, int nontemporal) {
   return ND_OK;
 }
 
+int nd_set_bank_grid(nd_ctx* c, int32_t workgroups) {
+  if (!c) return fail(ND_ERR_ARG, "null ctx");
+  if (workgroups < 0) return fail(ND_ERR_ARG, "bank grid: workgroups must be >= 0");
+  c->bank_grid = workgroups;  // graphs are keyed by it
+  return ND_OK;
+}
+
 int nd_set_exact_fp32(nd_ctx* c, int enable) {
   if (!c) return fail(ND_ERR_ARG, "null ctx");
   c->exact = enable != 0;  // graphs are keyed by it
@@ -1886,11 +1898,11 @@ int nd_op_bank_pack_h3(const float* x, const float* ln_g, const float* ln_b, uin
 }
 
 int nd_op_dec_bank_h3(const float* qp, const uint16_t* bank, const float* signal, const int32_t* span, float pad_val,
-                      float* out, int32_t C, int32_t T, int32_t* ovf, void* stream) {
+                      float* out, int32_t C, int32_t T, int32_t* ovf, int32_t grid, void* stream) {
   if (int rc = ensure_attributes()) return rc;
-  if (!qp || !bank || !signal || !span || !out) return fail(ND_ERR_ARG, "dec_bank_h3: bad arguments");
+  if (!qp || !bank || !signal || !span || !out || grid < 0) return fail(ND_ERR_ARG, "dec_bank_h3: bad arguments");
   hipError_t e = nd::launch_dec_bank_h3(qp, bank, signal, span, pad_val, out, C, T, (hipStream_t)stream, nullptr,
-                                        nullptr, 0, ovf);
+                                        nullptr, 0, ovf, false, grid);
   if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("dec_bank_h3: ") + hipGetErrorString(e));
   return ND_OK;
 }

@@ -219,7 +219,7 @@ hipError_t launch_bank_pack_h3(const float* x, const float* ln_g, const float* l
                                int* ovf, hipStream_t s);
 hipError_t launch_dec_bank_h3(const float* qp, const uint16_t* bank, const float* signal, const int* span,
                               float pad_val, float* out, int C, int T, hipStream_t s, unsigned long long* stamp,
-                              float* attn_dbg, size_t dbg_stride, int* ovf, bool nt = false);
+                              float* attn_dbg, size_t dbg_stride, int* ovf, bool nt = false, int grid = 0);
 hipError_t launch_memory_pack(const float* x, const float* ln_g, const float* ln_b, float* out, int B, int T, int ldT,
                               hipStream_t s);
 hipError_t init_mem_attributes();

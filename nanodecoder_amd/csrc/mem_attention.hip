@@ -35,6 +35,8 @@
 //  - U: block b = (dim octet dg, head quad hg), one key per instruction:
 //    A = p[key][4hg+i], B = m[key][dims of the lane] (two 16 B reads of the
 //    key's row), 8 accumulators of 4 = the wave's U for all 8 x 256 outputs.
+#include <algorithm>
+
 #include "common.hpp"
 #include "kernels.hpp"
 
@@ -345,17 +347,15 @@ __device__ __forceinline__ int bh_row(int r, int hf) { return 32 * r + 16 * (hf 
 
 // NT: the bank streamed with non-temporal loads (not kept in the Infinity
 // Cache), for an EnginePool lane whose bank should leave the cache to another
+// one chunk c (dec_bank_h3_kernel below)
 template <bool NT>
-__global__ void __launch_bounds__(BH_NW * 64)
-dec_bank_h3_kernel(const float* __restrict__ qp, const f32x4* __restrict__ bank, const float* __restrict__ signal,
-                   const int* __restrict__ span, float pad_val, float* __restrict__ out, int T,
-                   unsigned long long* stamp, float* __restrict__ dbg, size_t dbg_stride, int* ovf) {
-#ifdef ND_SKIP_BANK  // timing probe only (tools/build_variant.sh): the kernel's marginal cost
-  if (threadIdx.x < 100000) return;
-#endif
-  const unsigned long long t_entry = wall_clock64();  // the timing stamp's start (published below)
+__device__ __forceinline__ void bank_h3_chunk(int c, const float* __restrict__ qp, const f32x4* __restrict__ bank,
+                                              const float* __restrict__ signal, const int* __restrict__ span,
+                                              float pad_val, float* __restrict__ out, int T,
+                                              unsigned long long* stamp, float* __restrict__ dbg, size_t dbg_stride,
+                                              int* ovf, unsigned long long t_entry) {
   extern __shared__ float lds[];
-  const int c = blockIdx.x, lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int col = lane & 15, g = lane >> 4;
   char* img = reinterpret_cast<char*>(lds) + w * BH_IMG;  // [plane][dim block][16 keys][32 B]
@@ -599,6 +599,30 @@ dec_bank_h3_kernel(const float* __restrict__ qp, const f32x4* __restrict__ bank,
       out[pk(c, n & ~3, ND_H * ND_D) + (n & 3)] = num[i];
     }
   }
+}
+
+// grid = C (one chunk per workgroup, every CU), or (WALK) fewer workgroups
+// walking the chunks (nd_set_bank_grid: an EnginePool lane leaves half the
+// CUs to the other lanes' kernels, whose LDS does not fit beside this
+// kernel's 137 KB).  Two forms: the loop changes the one-chunk code's load
+// schedule (a drain of the first half blocks, tests/test_abi.py)
+template <bool NT, bool WALK>
+__global__ void __launch_bounds__(BH_NW * 64)
+dec_bank_h3_kernel(const float* __restrict__ qp, const f32x4* __restrict__ bank, const float* __restrict__ signal,
+                   const int* __restrict__ span, float pad_val, float* __restrict__ out, int T, int C,
+                   unsigned long long* stamp, float* __restrict__ dbg, size_t dbg_stride, int* ovf) {
+#ifdef ND_SKIP_BANK  // timing probe only (tools/build_variant.sh): the kernel's marginal cost
+  if (threadIdx.x < 100000) return;
+#endif
+  const unsigned long long t_entry = wall_clock64();  // the timing stamp's start (published below)
+  if constexpr (WALK) {
+    for (int c = blockIdx.x; c < C; c += gridDim.x) {
+      if (c != (int)blockIdx.x) lds_barrier();  // the previous chunk's merge reads of LDS are done
+      bank_h3_chunk<NT>(c, qp, bank, signal, span, pad_val, out, T, stamp, dbg, dbg_stride, ovf, t_entry);
+    }
+  } else {
+    bank_h3_chunk<NT>(blockIdx.x, qp, bank, signal, span, pad_val, out, T, stamp, dbg, dbg_stride, ovf, t_entry);
+  }
   stamp_end(stamp);
 }
 
@@ -662,16 +686,24 @@ hipError_t launch_bank_pack_h3(const float* x, const float* ln_g, const float* l
 
 hipError_t launch_dec_bank_h3(const float* qp, const uint16_t* bank, const float* signal, const int* span,
                               float pad_val, float* out, int C, int T, hipStream_t s, unsigned long long* stamp,
-                              float* attn_dbg, size_t dbg_stride, int* ovf, bool nt) {
-  if (T < 1 || T > 512 || C < 1) return hipErrorInvalidValue;
-  if (nt)
-    hipLaunchKernelGGL(dec_bank_h3_kernel<true>, dim3(C), dim3(BH_NW * 64), BH_LDS, s, qp,
-                       reinterpret_cast<const f32x4*>(bank), signal, span, pad_val, out, T, stamp, attn_dbg,
-                       dbg_stride, ovf);
-  else
-    hipLaunchKernelGGL(dec_bank_h3_kernel<false>, dim3(C), dim3(BH_NW * 64), BH_LDS, s, qp,
-                       reinterpret_cast<const f32x4*>(bank), signal, span, pad_val, out, T, stamp, attn_dbg,
-                       dbg_stride, ovf);
+                              float* attn_dbg, size_t dbg_stride, int* ovf, bool nt, int grid) {
+  if (T < 1 || T > 512 || C < 1 || grid < 0) return hipErrorInvalidValue;
+  const int G = grid > 0 ? std::min(C, grid) : C;
+#define ND_BANK_GO(N, W)                                                                                          \
+  hipLaunchKernelGGL((dec_bank_h3_kernel<N, W>), dim3(G), dim3(BH_NW * 64), BH_LDS, s, qp,                       \
+                     reinterpret_cast<const f32x4*>(bank), signal, span, pad_val, out, T, C, stamp, attn_dbg,     \
+                     dbg_stride, ovf)
+  if (G < C) {
+    if (nt)
+      ND_BANK_GO(true, true);
+    else
+      ND_BANK_GO(false, true);
+  } else if (nt) {
+    ND_BANK_GO(true, false);
+  } else {
+    ND_BANK_GO(false, false);
+  }
+#undef ND_BANK_GO
   return hipGetLastError();
 }
 
@@ -765,11 +797,13 @@ hipError_t init_mem_attributes() {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mem_lds_bytes());
     if (e != hipSuccess) return e;
   }
-  const hipError_t e =
-      hipFuncSetAttribute((const void*)dec_bank_h3_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, BH_LDS);
-  return e != hipSuccess ? e
-                         : hipFuncSetAttribute((const void*)dec_bank_h3_kernel<true>,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, BH_LDS);
+  const void* bh[] = {(const void*)dec_bank_h3_kernel<false, false>, (const void*)dec_bank_h3_kernel<true, false>,
+                      (const void*)dec_bank_h3_kernel<false, true>, (const void*)dec_bank_h3_kernel<true, true>};
+  for (const void* f : bh) {
+    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, BH_LDS);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 }  // namespace nd

@@ -102,7 +102,10 @@ def test_hot_path_kernels_do_not_drain_loads(tmp_path):
             # the form that runs the previous step's head: wave 0 waits for the
             # head's own loads, then issues its cache loads (the one allowed)
             ("attention", r"dec_self_attention_kernelILi\d+ELi\d+ELb0ELb1E", 1),
-            ("mem_attention", r"dec_bank_h3_kernel", 0),
+            ("mem_attention", r"dec_bank_h3_kernelILb\dELb0E", 0),  # one chunk per workgroup
+            # the walking form (pool lanes): the loop's load schedule drains the
+            # first half blocks once per chunk
+            ("mem_attention", r"dec_bank_h3_kernelILb\dELb1E", 2),
             # the standalone head (the last step only when the head is fused):
             # the V > 8 generator loop's loads follow the first 8 rows' wait
             ("search", r"greedy_head_kernel", 1),

@@ -155,7 +155,8 @@ def test_pool_matches_single_engine(encoder, mode):
     one = _engine(cfg, W, max_batch=B, max_steps=S, max_beam=beam)
     exp = [{k: v.cpu() for k, v in call(one, b).items() if k in keys} for b in batches]
     one.close()
-    pool = EnginePool(cfg, W, device=0, lanes=2, max_batch=B, max_steps=S, max_beam=beam)
+    # bank_grid 16: each lane's memory-bank workgroups walk 4 of the 64 chunks (nd_set_bank_grid)
+    pool = EnginePool(cfg, W, device=0, lanes=2, max_batch=B, max_steps=S, max_beam=beam, bank_grid=16)
     dev_b = [torch.from_numpy(b).cuda() for b in batches]
     for rnd in range(2):
         if mode == "greedy":

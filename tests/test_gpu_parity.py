@@ -298,13 +298,16 @@ def test_mem_attention_vs_fp64(T):
             assert err < 2e-5, (c, h, L, err)
 
 
-@pytest.mark.parametrize("T,ln", [(512, True), (480, False), (449, True)])
-def test_bank_h3_vs_fp64(T, ln):
+@pytest.mark.parametrize("T,ln,grid", [(512, True, 0), (480, False, 0), (449, True, 0), (512, True, 5),
+                                       (512, False, 1)])
+def test_bank_h3_vs_fp64(T, ln, grid):
     """Split-fp16 memory-bank attention (bank_pack_h3 + dec_bank_h3_kernel, the
     greedy path at 512-sample chunks) against an fp64 softmax(q' M^T) M per
     head: ragged spans (key-block / wave boundaries, single key, waves owning
     no key), pad-masked keys, an all-masked chunk, a peaked chunk whose scores
-    climb past the lazy-rescale threshold, with and without the LayerNorm."""
+    climb past the lazy-rescale threshold, with and without the LayerNorm.
+    grid > 0: that many workgroups walk the 12 chunks (nd_set_bank_grid's
+    form; 5 leaves a ragged last round)."""
     from nanodecoder_amd.engine import op_bank_pack_h3, op_dec_bank_h3, pack_p16, unpack_p16
     rng = np.random.default_rng(7)
     C, PAD = 12, 1.0
@@ -330,7 +333,7 @@ def test_bank_h3_vs_fp64(T, ln):
         bank = op_bank_pack_h3(xt, C, T, ovf=ovf)
         xm = x.astype(np.float64)
     out = op_dec_bank_h3(pack_p16(torch.from_numpy(q).to(dev)), bank, torch.from_numpy(sig).to(dev),
-                         torch.from_numpy(spans).to(dev), PAD, ovf=ovf)
+                         torch.from_numpy(spans).to(dev), PAD, ovf=ovf, grid=grid)
     got = unpack_p16(out, C).cpu().numpy()
     assert int(ovf.item()) == 0
     for c in range(C):
