@@ -959,7 +959,18 @@ hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* 
     ND_SELF2(NW, KW, false, true);     \
   else                                 \
     ND_SELF2(NW, KW, false, false)
+  // 8 waves per row at every length (16 keys per wave from 65 keys on): the
+  // 16-wave forms fill a CU's whole register file (16 x 113-119 VGPRs), the
+  // 8-wave ones leave room for another pool lane's waves: pooled 17.85 ->
+  // 17.73 ms per call, one call in flight 23.72 -> 23.59 ms (two reps each,
+  // same box).  ND_SELF_NW8=0 keeps the 16-wave forms (A/B timing)
+  static const bool w8 = [] {
+    const char* e = getenv("ND_SELF_NW8");
+    return !(e && atoi(e) == 0);
+  }();
   if (n <= 32) ND_SELF(8, 4);
+  else if (w8 && n <= 64) ND_SELF(8, 8);
+  else if (w8) ND_SELF(8, 16);  // two passes beyond 128 keys
   else if (n <= 64) ND_SELF(16, 4);
   else ND_SELF(16, 8);  // two passes beyond 128 keys
 #undef ND_SELF

@@ -1591,7 +1591,7 @@ static const struct {
                  {"ND_HEAD_FUSE", 1},  {"ND_LSTM_F32", 0},     {"ND_LSTM_LIBM", 0},     {"ND_LSTM_SEQ", 4},
                  {"ND_ENC_ATTN_NQ", 2}, {"ND_ENC_ATTN_GRID", 0}, {"ND_ENC_ATTN_F32", 0}, {"ND_SELF_XCD", 1},
                  {"ND_ENC_WO", 1},     {"ND_ENC_QKV0", 1},
-                 {"ND_ENC_QKV", 1},    {"ND_ENC_ATTN0", 0}};
+                 {"ND_ENC_QKV", 1},    {"ND_ENC_ATTN0", 0},   {"ND_SELF_NW8", 1}};
 
 int nd_switches(char* buf, int32_t len) {
   std::string out;
