@@ -988,11 +988,20 @@ hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* 
 // 16 waves x 2 blocks x U x 2 KB are in flight per CU.  The 16 partial states
 // merge through LDS at the end.  softmax(QK^T/sqrt(d), mask src == pad_idx
 // -> -1e18) V as decoder/transformer.py:220-221 + modules/multi_headed_attn.py.
-#define CTX_NW 16
+// 8 waves per chunk: the 16-wave form filled a CU's register file (16 x 114
+// VGPRs at rpc 5) and shut the other pool lanes out; beam configs[3] pooled
+// 83.6 -> 82.1 ms per call, one call 102.2 -> 101.5 ms (two reps, same box,
+// tools/_g44.sh); round 2 measured the two forms equal alone
+#ifndef CTX_NW
+#define CTX_NW 8
+#endif
+#ifndef CTX_URPC
+#define CTX_URPC 2  // rows per chunk up to which a block holds 4 keys (else 2)
+#endif
 #define CTX_MAXR 6
 template <int RPC>
 struct CtxTile {
-  static constexpr int U = RPC <= 2 ? 4 : 2;  // keys per block (register budget: 128 VGPRs at 16 waves/CU)
+  static constexpr int U = RPC <= CTX_URPC ? 4 : 2;  // keys per block (register budget)
 };
 
 template <int RPC>
