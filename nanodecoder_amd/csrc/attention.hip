@@ -582,37 +582,49 @@ hipError_t launch_enc_attention(const float* qkv, const float* signal, const int
 // Layer 0's attention in closed form (kernels.hpp launch_enc_attention_rank2;
 // multi_headed_attn.py:154-177 with the key mask of encoder/transformer.py:
 // 117-121).  One workgroup per chunk, one query per thread: the unmasked keys'
-// (y, r) are compacted into LDS (a masked key's score is the -1e18 fill, whose
-// weight is exactly 0 beside any unmasked key; a chunk with no unmasked key
-// is uniform over its keys, which all share s = 0, so one representative key
-// gives the same expectations); two passes over them per (query, head):
-// the maximum, then exp2 and the three sums; the 8 heads' E[y], E[r] meet in
-// LDS and every wave writes whole 1 KB output rows.
+// (y, r) are compacted (a masked key's score is the -1e18 fill, whose weight
+// is exactly 0 beside any unmasked key; a chunk with no unmasked key is
+// uniform over its keys, which all share s = 0, so one representative key
+// gives the same expectations); two passes over them per (query, head): the
+// maximum, then exp2 and the three sums.
+// No data crosses between waves: every wave compacts all of the chunk's keys
+// into its OWN LDS slab (8 keys per lane, ballots and popcounts) and stages
+// its own 64 queries' E[y], E[r] for its coalesced row stores, so the kernel
+// has no barrier.  (The first form shared one key list and the 8 waves'
+// counts through LDS across barriers; its output went wrong by whole chunks
+// when another engine's decoder GEMMs ran beside it on the GPU)
+#define R2_SLAB (8 * ENC_MAXT + 64 * 17 * 4)  // bytes per wave: keys (y, r), then its queries' E[y], E[r]
 __global__ void __launch_bounds__(512)
 enc_attention_rank2_kernel(const float* __restrict__ signal, const int* __restrict__ span, EmbedQkv eq,
                            const float* __restrict__ coef, float* __restrict__ out, int T) {
-  __shared__ __attribute__((aligned(16))) float2 kyr[ENC_MAXT];   // unmasked keys: (y, r)
-  __shared__ __attribute__((aligned(16))) float ex[ENC_MAXT][17];  // per query: E[y], E[r] of 8 heads (+ pad)
-  __shared__ int wcnt[8];
+  __shared__ __attribute__((aligned(16))) char smem[8 * R2_SLAB];
   const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  float2* kyr = reinterpret_cast<float2*>(smem + wave * R2_SLAB);                  // [ENC_MAXT]
+  float(*ex)[17] = reinterpret_cast<float(*)[17]>(smem + wave * R2_SLAB + 8 * ENC_MAXT);  // [64][17]
   const int L = min(span[b], T);
-  const float s = signal[(size_t)b * T + min(t, L - 1)];
-  const float r = ln_rsqrt(fmaf(s, fmaf(s, eq.mww, 2.0f * eq.mwb), eq.mbb) + ND_LN_EPS), y = s * r;
-  // compaction of the unmasked keys u < L (signal != 0), in key order
-  const bool key = t < L && s != 0.0f;
-  const unsigned long long bal = __ballot(key);
-  if (lane == 0) wcnt[wave] = __popcll(bal);
-  __syncthreads();
-  int base = 0, n_um = 0;
+  const float* sig = signal + (size_t)b * T;
+  // every key of the chunk in this wave: key u = 64 j + lane
+  float ky[ENC_MAXT / 64], kr[ENC_MAXT / 64];
+  unsigned long long bal[ENC_MAXT / 64];
 #pragma unroll
-  for (int w = 0; w < 8; ++w) {
-    base += w < wave ? wcnt[w] : 0;
-    n_um += wcnt[w];
+  for (int j = 0; j < ENC_MAXT / 64; ++j) {
+    const int u = 64 * j + lane;
+    const float s = sig[max(min(u, L - 1), 0)];
+    kr[j] = ln_rsqrt(fmaf(s, fmaf(s, eq.mww, 2.0f * eq.mwb), eq.mbb) + ND_LN_EPS);
+    ky[j] = s * kr[j];
+    bal[j] = __ballot(u < L && s != 0.0f);
   }
-  if (key) kyr[base + __popcll(bal & ((1ull << lane) - 1ull))] = make_float2(y, r);
-  if (n_um == 0 && t == 0) kyr[0] = make_float2(0.0f, ln_rsqrt(eq.mbb + ND_LN_EPS));  // all masked: s = 0
+  int n_um = 0;
+#pragma unroll
+  for (int j = 0; j < ENC_MAXT / 64; ++j) {
+    if ((bal[j] >> lane) & 1ull) kyr[n_um + __popcll(bal[j] & ((1ull << lane) - 1ull))] = make_float2(ky[j], kr[j]);
+    n_um += __popcll(bal[j]);
+  }
+  if (n_um == 0 && lane == 0) kyr[0] = make_float2(0.0f, ln_rsqrt(eq.mbb + ND_LN_EPS));  // all masked: s = 0
   const int nk = n_um > 0 ? n_um : 1;
-  __syncthreads();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's slab written (its own reads follow in order)
+  // this thread's query t: its (y, r) is key t's, held by lane t % 64 as key slot t / 64
+  const float y = ky[wave], r = kr[wave];
   if (t < L) {
     // alpha_h, beta_h of this query (log2 units); heads in pairs for packed math
     ef2 al[4], be[4];
@@ -628,10 +640,10 @@ enc_attention_rank2_kernel(const float* __restrict__ signal, const int* __restri
     for (int p = 0; p < 4; ++p) m[p] = ef2{-INFINITY, -INFINITY};
     for (int u = 0; u < nk; ++u) {
       const float2 k = kyr[u];
-      const ef2 ky = {k.x, k.x}, kr = {k.y, k.y};
+      const ef2 kyv = {k.x, k.x}, krv = {k.y, k.y};
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
-        const ef2 l = al[p] * ky + be[p] * kr;
+        const ef2 l = al[p] * kyv + be[p] * krv;
         m[p] = ef2{fmaxf(m[p].x, l.x), fmaxf(m[p].y, l.y)};
       }
     }
@@ -640,14 +652,14 @@ enc_attention_rank2_kernel(const float* __restrict__ signal, const int* __restri
     for (int p = 0; p < 4; ++p) sp[p] = sy[p] = sr[p] = ef2{0.f, 0.f};
     for (int u = 0; u < nk; ++u) {
       const float2 k = kyr[u];
-      const ef2 ky = {k.x, k.x}, kr = {k.y, k.y};
+      const ef2 kyv = {k.x, k.x}, krv = {k.y, k.y};
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
-        const ef2 d = al[p] * ky + (be[p] * kr - m[p]);
+        const ef2 d = al[p] * kyv + (be[p] * krv - m[p]);
         const ef2 e = {__builtin_amdgcn_exp2f(d.x), __builtin_amdgcn_exp2f(d.y)};
         sp[p] += e;
-        sy[p] += e * ky;
-        sr[p] += e * kr;
+        sy[p] += e * kyv;
+        sr[p] += e * krv;
       }
     }
 #pragma unroll
@@ -655,16 +667,17 @@ enc_attention_rank2_kernel(const float* __restrict__ signal, const int* __restri
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const float inv = __builtin_amdgcn_rcpf(sp[p][j]);
-        ex[t][2 * (2 * p + j)] = sy[p][j] * inv;
-        ex[t][2 * (2 * p + j) + 1] = sr[p][j] * inv;
+        ex[lane][2 * (2 * p + j)] = sy[p][j] * inv;
+        ex[lane][2 * (2 * p + j) + 1] = sr[p][j] * inv;
       }
   }
-  __syncthreads();
-  // out[t][32 h + d] = a_v[h][d] E[y] + c_v[h][d] E[r] + b_v[h][d]: wave w writes rows w, w + 8, ...
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's E[y], E[r] staged
+  // out[t][32 h + d] = a_v[h][d] E[y] + c_v[h][d] E[r] + b_v[h][d]: the wave's 64 rows, 1 KB each
   const int n = 2 * ND_D + lane * 4, h = lane >> 3;
   const f32x4 av = ld4(eq.ac + n), cv = ld4(eq.ac + 3 * ND_D + n), bv = ld4(eq.bias + n);
-  for (int q = wave; q < L; q += 8)
-    st4(out + ((size_t)b * T + q) * ND_D + lane * 4, av * ex[q][2 * h] + cv * ex[q][2 * h + 1] + bv);
+  const int q1 = min(64, L - 64 * wave);
+  for (int q = 0; q < q1; ++q)
+    st4(out + ((size_t)b * T + 64 * wave + q) * ND_D + lane * 4, av * ex[q][2 * h] + cv * ex[q][2 * h + 1] + bv);
 }
 
 hipError_t launch_enc_attention_rank2(const float* signal, const int* span, const EmbedQkv& eq, const float* coef,
