@@ -437,8 +437,8 @@ int nd_op_memory_pack(const float* x, const float* ln_g, const float* ln_b, floa
  * nd_op_dec_mem_attention).  nd_op_bank_pack_h3: x [B*T, 256] row-major ->
  * out, B x 512 rows as fp16 hi / lo planes in the v_mfma_f32_16x16x32_f16
  * A-operand fragment order (B * 512 * 256 * 4 bytes; LayerNorm with
- * ln_g/ln_b when set; rows t >= T zero).  nd_op_dec_bank_h3: qp [C16, 2048]
- * P16 as nd_op_dec_mem_attention, bank from nd_op_bank_pack_h3, T in
+ * ln_g/ln_b when set; rows t >= T zero).  nd_op_dec_bank_h3: qp [C, 2048]
+ * ROW-MAJOR (one row per chunk), bank from nd_op_bank_pack_h3, T in
  * (448, 512]; out U [C16, 2048] P16.  ovf (nullable): set to 1 when an
  * operand reaches the fp16 range (|x| >= 65504).  grid: workgroups at most
  * (0 = one per chunk; fewer walk the chunks, as nd_set_bank_grid). */

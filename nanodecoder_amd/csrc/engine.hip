@@ -516,6 +516,7 @@ struct G {
   G& stats(float* part) { a.part_out = part; return *this; }
   G& skip(const int* done, int rpc) { a.skip = done; a.skip_rpc = rpc; return *this; }
   G& small_m(bool on) { a.prefer_p16 = on ? 1 : 0; return *this; }
+  G& c_rowmajor(bool on) { a.c_rm = on ? 1 : 0; return *this; }  // P16 GEMMs: C row-major
   bool packed = false;
   G& p16() { packed = true; return *this; }  // decoder-step operands in the P16 layout
   hipError_t run(hipStream_t s, int* pn_out = nullptr) {
@@ -764,7 +765,8 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
     }
     if (mb) {  // memory-bank form (attention.hip)
       const int HD = ND_H * D;
-      LCHK(dg(c->dq1, D, L.pwqk, HD, D, L.bqk, c->dqk, HD).ln(c->dq1_part, pnq).run(s));
+      // q' row-major for the split-fp16 bank kernel (one row per chunk), P16 for the fp32 one
+      LCHK(dg(c->dq1, D, L.pwqk, HD, D, L.bqk, c->dqk, HD).ln(c->dq1_part, pnq).c_rowmajor(c->bank_h3).run(s));
       if (c->bank_h3)
         LCHK(nd::launch_dec_bank_h3(c->dqk, reinterpret_cast<const uint16_t*>(c->mem_p), c->sig, c->span,
                                     (float)c->cfg.pad_idx, c->dU, C, T, s, stamp, dbg, dbg_stride, c->ovf,

@@ -528,7 +528,10 @@ __global__ void __launch_bounds__(NT* KS * 64) gemm_p16_kernel(const GemmArgs g)
   v += bv;
   if constexpr (RELU) v = {fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
   if constexpr (RESID) v += rv;
-  reinterpret_cast<f32x4*>(g.C)[ct] = v;
+  if (g.c_rm)
+    st4(g.C + (size_t)(mb * 16 + (lane & 15)) * g.N + nb * 16 + 4 * (lane >> 4), v);
+  else
+    reinterpret_cast<f32x4*>(g.C)[ct] = v;
   if (g.part_out) {
     // row statistics over this block's 16 columns: lanes l, l^16, l^32, l^48
     const float m_ = xor32_sum(xor16_sum(v.x + v.y + v.z + v.w)) * (1.0f / 16.0f);
@@ -670,7 +673,10 @@ __global__ void __launch_bounds__(BMB* BNB * 64) gemm_p16s_kernel(const GemmArgs
   if constexpr (RELU) v = {fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
   if constexpr (RESID) v += rv;
   if (!live) return;
-  reinterpret_cast<f32x4*>(g.C)[ct] = v;
+  if (g.c_rm)
+    st4(g.C + (size_t)(mb * 16 + (lane & 15)) * g.N + nb * 16 + 4 * (lane >> 4), v);
+  else
+    reinterpret_cast<f32x4*>(g.C)[ct] = v;
   if (g.part_out) {
     const float m_ = xor32_sum(xor16_sum(v.x + v.y + v.z + v.w)) * (1.0f / 16.0f);
     const f32x4 d = v - m_;
@@ -1019,7 +1025,7 @@ hipError_t launch_gemm_p16(GemmArgs& g, hipStream_t s) {
     const char* e = getenv("ND_P16_BIG_MIN");  // rows from which the LDS-tiled kernel takes P16 GEMMs
     return e ? atoi(e) : 2048;
   }();
-  if (g.M >= big_min && !g.prefer_p16 && g.Wh_rm && !gemm_f32_only() && g.N % 64 == 0 &&
+  if (g.M >= big_min && !g.prefer_p16 && !g.c_rm && g.Wh_rm && !gemm_f32_only() && g.N % 64 == 0 &&
       (g.N >= 512 || g.K >= 1024)) {
     // many rows (beam search over large batches): the encoder's LDS-tiled
     // split-fp16 kernel on P16 activations, with the row-major weight image

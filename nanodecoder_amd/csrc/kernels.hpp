@@ -55,6 +55,10 @@ struct GemmArgs {
   // P16 GEMMs: stay on the small-M kernels at any M (the beam loop's tail,
   // when few chunks are alive: a 16-row block's latency, not a 64-row tile's)
   int prefer_p16 = 0;
+  // P16 GEMMs: C written row-major [M16][N] instead of P16 (the memory-bank
+  // kernel's q': its one-row-per-chunk loads then read whole 1 KB runs, not
+  // 16 B of every 64 B line; PMC: 4x over-fetch of q' in the P16 layout)
+  int c_rm = 0;
 };
 #define ND_PART_LD 16  // partial-stat slots per row (max column tiles of a 256-wide row)
 // row-major operands (encoder, large M): LDS-tiled MFMA kernel

@@ -399,7 +399,7 @@ __device__ __forceinline__ void bank_h3_chunk(int c, const float* __restrict__ q
   constexpr int QH = ND_H / BH_NW, SGN = BH_KPW / 4;  // q' heads per thread, signal words per lane
   f32x4 qld[QH];
 #pragma unroll
-  for (int i = 0; i < QH; ++i) qld[i] = ld4(qp + pk(c, (w + BH_NW * i) * ND_D + 4 * lane, ND_H * ND_D));
+  for (int i = 0; i < QH; ++i) qld[i] = ld4(qp + (size_t)c * (ND_H * ND_D) + (w + BH_NW * i) * ND_D + 4 * lane);
   // lane l: row l & 15 of the wave's key block 4 j + (l >> 4)
   float sg[SGN];
 #pragma unroll

@@ -616,10 +616,10 @@ def op_bank_pack_h3(x, B, T, ln_g=None, ln_b=None, ovf=None):
 
 def op_dec_bank_h3(qp, bank, signal, span, pad_val, out=None, ovf=None, grid=0):
     """Memory-bank context attention on the split-fp16 bank (nd_op_dec_bank_h3):
-    qp [R16, 2048] packed, T in (448, 512]; returns U [R16, 2048] packed."""
+    qp [C, 2048] row-major, T in (448, 512]; returns U [C16, 2048] packed."""
     C, T = signal.shape
     if out is None:
-        out = torch.empty(qp.shape[0], qp.shape[1], dtype=torch.float32, device=qp.device)
+        out = torch.empty((C + 15) // 16 * 16, qp.shape[1], dtype=torch.float32, device=qp.device)
     s = ctypes.c_void_p(torch.cuda.current_stream(qp.device).cuda_stream)
     _lib.check(_lib.lib().nd_op_dec_bank_h3(_ptr(qp), _ptr(bank), _ptr(signal), _ptr(span), float(pad_val),
                                             _ptr(out), C, T, _ptr(ovf), int(grid), s), "nd_op_dec_bank_h3")

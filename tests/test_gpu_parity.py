@@ -332,7 +332,7 @@ def test_bank_h3_vs_fp64(T, ln, grid):
     else:
         bank = op_bank_pack_h3(xt, C, T, ovf=ovf)
         xm = x.astype(np.float64)
-    out = op_dec_bank_h3(pack_p16(torch.from_numpy(q).to(dev)), bank, torch.from_numpy(sig).to(dev),
+    out = op_dec_bank_h3(torch.from_numpy(q).to(dev), bank, torch.from_numpy(sig).to(dev),  # q' row-major
                          torch.from_numpy(spans).to(dev), PAD, ovf=ovf, grid=grid)
     got = unpack_p16(out, C).cpu().numpy()
     assert int(ovf.item()) == 0

@@ -24,7 +24,7 @@ print("pack max|err|", np.abs(rec.reshape(C * 512, 256) - x).max())
 
 
 def run(q, sig, spans):
-    out = op_dec_bank_h3(pack_p16(torch.from_numpy(q).to(dev)), torch.from_numpy(bank.view(np.int16)).to(dev),
+    out = op_dec_bank_h3(torch.from_numpy(q).to(dev), torch.from_numpy(bank.view(np.int16)).to(dev),
                          torch.from_numpy(sig).to(dev), torch.from_numpy(spans).to(dev), 1.0)
     return unpack_p16(out, C).cpu().numpy()
 
