@@ -886,7 +886,8 @@ dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cac
 #pragma unroll
       for (int i = 0; i < TPT; ++i) {
         const int e = min(t0 + i * (NW - 1) * 64, n4 - 1), v = e / (3 * ND_D / 4), c4 = e % (3 * ND_D / 4);
-        tv[i] = ld4(qkv + pk(step * qr.V + v, 4 * c4, 3 * ND_D));
+        const int tr = step * qr.V + v;
+        tv[i] = ld4(qkv + (qr.rm ? (size_t)tr * 3 * ND_D + 4 * c4 : pk(tr, 4 * c4, 3 * ND_D)));
       }
       load_pass(0);
 #pragma unroll
@@ -904,9 +905,11 @@ dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cac
     load_pass(0);
     // qkv is P16-packed [R, 768], or the layer-0 table [S * V, 768] (QkvRows)
     const int qrow = qr.tok ? step * qr.V + (step == 0 ? qr.tok0 : qr.tok[r]) : r;
-    qv = ld4(qkv + pk(qrow, lane * 4, 3 * ND_D)) / ND_SQRT_DH;
-    kme = ld4(qkv + pk(qrow, ND_D + lane * 4, 3 * ND_D));
-    vme = ld4(qkv + pk(qrow, 2 * ND_D + lane * 4, 3 * ND_D));
+    const float* qr0 = qkv + (qr.rm ? (size_t)qrow * 3 * ND_D + lane * 4 : pk(qrow, lane * 4, 3 * ND_D));
+    const size_t qstep = qr.rm ? (size_t)ND_D : pk(0, ND_D, 3 * ND_D);  // q -> k -> v: 256 columns on
+    qv = ld4(qr0) / ND_SQRT_DH;
+    kme = ld4(qr0 + qstep);
+    vme = ld4(qr0 + 2 * qstep);
   }
   float m[1] = {-INFINITY}, l[1] = {0.f};
   f32x4 acc[1] = {{0.f, 0.f, 0.f, 0.f}};

@@ -691,7 +691,13 @@ static hipError_t enqueue_qkv_table(nd_ctx* c, int S, hipStream_t s) {
   LCHK(nd::launch_dec_embed_table(c->emb, c->cfg.position_encoding ? c->pe : nullptr, c->V, S, c->qtab_x,
                                   c->qtab_part, rows, s));
   const DecLayer& L = c->dec[0];
-  return G(c->qtab_x, D, L.pwqkv, 3 * D, D, L.nbqkv, c->qtab, 3 * D, rows).p16().h3(c).ln(c->qtab_part, 1).run(s);
+  // row-major: the self-attention reads one table row per workgroup (QkvRows.rm)
+  return G(c->qtab_x, D, L.pwqkv, 3 * D, D, L.nbqkv, c->qtab, 3 * D, rows)
+      .p16()
+      .h3(c)
+      .ln(c->qtab_part, 1)
+      .c_rowmajor(true)
+      .run(s);
 }
 
 // Step-0 decoder input (later steps' inputs are written by the search
@@ -756,10 +762,15 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
         qr.tok = c->rtok;
         qr.V = c->V;
         qr.tok0 = c->cfg.bos_idx;
+        qr.rm = 1;  // the table is row-major (enqueue_qkv_table)
         LCHK(nd::launch_dec_self_attention(c->qtab, cache, anc, anc_ld, step, S, c->datt, R, s, rpc, done, qr, head));
       } else {
-        LCHK(dg(c->dx, D, L.pwqkv, 3 * D, D, L.nbqkv, c->dqkv, 3 * D).ln(c->dx_part, pnx).run(s));
-        LCHK(nd::launch_dec_self_attention(c->dqkv, cache, anc, anc_ld, step, S, c->datt, R, s, rpc, done));
+        // greedy rows (one workgroup each): q | k | v row-major; beam keeps P16 (its M = 5120 GEMMs
+        // take the LDS-tiled route, which writes P16)
+        nd::QkvRows q12;
+        q12.rm = (rpc == 1 && !anc && !done) ? 1 : 0;
+        LCHK(dg(c->dx, D, L.pwqkv, 3 * D, D, L.nbqkv, c->dqkv, 3 * D).ln(c->dx_part, pnx).c_rowmajor(q12.rm).run(s));
+        LCHK(nd::launch_dec_self_attention(c->dqkv, cache, anc, anc_ld, step, S, c->datt, R, s, rpc, done, q12));
       }
       LCHK(dg(c->datt, D, L.pwo, D, D, L.bo, c->dq1, D).res(c->dx, D).stats(c->dq1_part).run(s, &pnq));
     }

@@ -165,6 +165,10 @@ struct QkvRows {
   const int* tok = nullptr;  // row -> token of this step (steps > 0)
   int V = 0;
   int tok0 = 0;  // every row's step-0 token (BOS)
+  // q | k | v (the table or the per-step matrix) row-major [rows][768]
+  // instead of P16: a workgroup reads ONE row, which in P16 is 16 B of every
+  // 128 B line (GemmArgs.c_rm)
+  int rm = 0;
 };
 // rows s * V + v (s < S, v < V) of the layer-0 QKV table's input, P16, with
 // one row-statistics partial per row; rows S * V .. rows_alloc - 1 zero
