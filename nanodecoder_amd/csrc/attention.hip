@@ -594,9 +594,15 @@ hipError_t launch_enc_attention(const float* qkv, const float* signal, const int
 // counts through LDS across barriers; its output went wrong by whole chunks
 // when another engine's decoder GEMMs ran beside it on the GPU)
 #define R2_SLAB (8 * ENC_MAXT + 64 * 17 * 4)  // bytes per wave: keys (y, r), then its queries' E[y], E[r]
+template <bool DA, bool NTS>
 __global__ void __launch_bounds__(512)
-enc_attention_rank2_kernel(const float* __restrict__ signal, const int* __restrict__ span, EmbedQkv eq,
-                           const float* __restrict__ coef, float* __restrict__ out, int T) {
+enc_attention_rank2_kernel(R2Args ka, const R2Args* __restrict__ da, int T) {
+  const R2Args& A = DA ? *da : ka;  // DA: the arguments from device memory (R2Args)
+  const float* __restrict__ signal = A.signal;
+  const int* __restrict__ span = A.span;
+  const EmbedQkv eq = A.eq;
+  const float* __restrict__ coef = A.coef;
+  float* __restrict__ out = A.out;
   __shared__ __attribute__((aligned(16))) char smem[8 * R2_SLAB];
   const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
   float2* kyr = reinterpret_cast<float2*>(smem + wave * R2_SLAB);                  // [ENC_MAXT]
@@ -676,14 +682,35 @@ enc_attention_rank2_kernel(const float* __restrict__ signal, const int* __restri
   const int n = 2 * ND_D + lane * 4, h = lane >> 3;
   const f32x4 av = ld4(eq.ac + n), cv = ld4(eq.ac + 3 * ND_D + n), bv = ld4(eq.bias + n);
   const int q1 = min(64, L - 64 * wave);
-  for (int q = 0; q < q1; ++q)
-    st4(out + ((size_t)b * T + 64 * wave + q) * ND_D + lane * 4, av * ex[q][2 * h] + cv * ex[q][2 * h + 1] + bv);
+  for (int q = 0; q < q1; ++q) {
+    const f32x4 o = av * ex[q][2 * h] + cv * ex[q][2 * h + 1] + bv;
+    f32x4* dst = reinterpret_cast<f32x4*>(out + ((size_t)b * T + 64 * wave + q) * ND_D + lane * 4);
+    if constexpr (NTS)
+      __builtin_nontemporal_store(o, dst);  // probe: past the L2s
+    else
+      *dst = o;
+  }
 }
 
 hipError_t launch_enc_attention_rank2(const float* signal, const int* span, const EmbedQkv& eq, const float* coef,
-                                      float* out, int B, int T, hipStream_t s) {
+                                      float* out, int B, int T, hipStream_t s, const R2Args* dev_args) {
   if (T > ENC_MAXT || T <= 0 || !eq.ac || !eq.bias || !coef) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(enc_attention_rank2_kernel, dim3(B), dim3(512), 0, s, signal, span, eq, coef, out, T);
+  R2Args a;
+  a.signal = signal;
+  a.span = span;
+  a.eq = eq;
+  a.coef = coef;
+  a.out = out;
+  static const bool nts = [] {
+    const char* e = getenv("ND_ENC_ATTN0");
+    return e && atoi(e) == 3;  // probe: output stores non-temporal
+  }();
+  if (dev_args)
+    hipLaunchKernelGGL((enc_attention_rank2_kernel<true, false>), dim3(B), dim3(512), 0, s, a, dev_args, T);
+  else if (nts)
+    hipLaunchKernelGGL((enc_attention_rank2_kernel<false, true>), dim3(B), dim3(512), 0, s, a, dev_args, T);
+  else
+    hipLaunchKernelGGL((enc_attention_rank2_kernel<false, false>), dim3(B), dim3(512), 0, s, a, dev_args, T);
   return hipGetLastError();
 }
 
