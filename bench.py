@@ -232,18 +232,21 @@ def _pmc(name, key="kernels"):
 
 
 def _mfma_counters(which):
-    """The committed rocprof MFMA counter pass of this workload
-    (profiles/r02_mfma_summary.json: tools/gpu.sh mfma -> tools/mfma_summary.py;
-    which = greedy | beam | nano), or None."""
-    p = os.path.join(ROOT, "profiles", "r02_mfma_summary.json")
+    """The newest committed rocprof MFMA counter pass of this workload
+    (profiles/rNN_mfma_summary.json, the highest round: tools/gpu.sh mfma ->
+    tools/mfma_summary.py; which = greedy | beam | nano), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_mfma_summary.json")))
+    if not files:
+        return None
     try:
-        with open(p) as f:
+        with open(files[-1]) as f:
             d = json.load(f)[which]
     except Exception:
         return None
     k = d["kernels"]
-    top = sorted(k.items(), key=lambda kv: -kv[1]["launches"] * kv[1]["avg_us"])[:4]
-    return {"source": "profiles/r02_mfma_summary.json (" + d["tag"] + ")", "path": d["path"],
+    top = sorted(k.items(), key=lambda kv: -kv[1]["launches"] * kv[1]["avg_us"])[:6]
+    return {"source": "profiles/" + os.path.basename(files[-1]) + " (" + d["tag"] + ")", "path": d["path"],
             "top_kernels": {n: {x: v[x] for x in ("avg_us", "f16_tflops", "f32_tflops", "mfma_util")} for n, v in top}}
 
 
@@ -401,10 +404,11 @@ def mfma_view(args, eng, sig, lens, ms_per_step):
 
 
 # ----------------------------------------------------------------- workloads
-def run_calls(pool, n, call):
+def run_calls(pool, n, call, every_lane=False):
     """n translate calls, `pool.lanes` of them on the device at once; returns
     the last call's outputs (complete: every lane is joined to the current
-    stream).  ``call(engine_or_pool)`` issues one call.  Greedy calls are
+    stream), or with ``every_lane`` the last outputs of each lane.
+    ``call(engine_or_pool)`` issues one call.  Greedy calls are
     asynchronous, so one host thread keeps every lane busy; a beam call polls
     its alive count between 10-step graph segments (host-synchronous), so each
     lane gets a host thread of its own there."""
@@ -414,7 +418,7 @@ def run_calls(pool, n, call):
         for k in range(n):
             outs[k % pool.lanes] = call(pool)
         pool.synchronize()
-        return outs[(n - 1) % pool.lanes]
+        return outs if every_lane else outs[(n - 1) % pool.lanes]
     cur = torch.cuda.current_stream(pool.device)
     errs = []
 
@@ -436,7 +440,32 @@ def run_calls(pool, n, call):
     if errs:
         raise errs[0]
     pool.synchronize()
-    return outs[(n - 1) % pool.lanes]
+    return outs if every_lane else outs[(n - 1) % pool.lanes]
+
+
+def pool_check(cfg, W, args, mode, B, beam, call, outs):
+    """The timed pooled calls' outputs against one fresh single engine on the
+    same inputs (tokens and scores, + lengths for beam), bitwise: "identical"
+    or what differed.  The single engine is oracle-pinned at these sizes
+    (tests/test_gpu_configs.py)."""
+    from nanodecoder_amd.engine import Engine
+    one = Engine(cfg, W, device=torch.cuda.current_device(), max_batch=B, max_src_len=512,
+                 max_steps=args.max_length, max_beam=beam)
+    try:
+        ref = call(one)
+        keys = ("tokens", "scores") + (("lens",) if mode == "beam" else ())
+        bad = []
+        for lane, o in enumerate(outs):
+            if o is None:
+                continue
+            for k in keys:
+                if not torch.equal(o[k].cpu(), ref[k].cpu()):
+                    bad.append(f"lane {lane} {k}")
+        return {"result": "identical" if not bad else "DIFFERENT: " + ", ".join(bad),
+                "lanes_compared": sum(o is not None for o in outs),
+                "against": "a fresh single Engine (one call in flight, bank kernel one workgroup per chunk)"}
+    finally:
+        one.close()
 
 
 def bank_grid(args):
@@ -464,14 +493,14 @@ def make_call(args, mode, sig, lens, min_len=None):
     return call
 
 
-def timed(pool, n, call, world):
+def timed(pool, n, call, world, every_lane=False):
     """Seconds for n calls between a barrier + device sync on both sides, max over ranks."""
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    out = run_calls(pool, n, call)
+    out = run_calls(pool, n, call, every_lane)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -501,7 +530,8 @@ def run_batch(args, world, rank, dev, cfg, W):
 
     eng.set_kernel_stamps(not args.no_roofline)  # live launch timing of the roofline kernel (in the graphs)
     run_calls(eng, max(args.warmup, eng.lanes), call)  # every lane captures its graphs
-    dt, out = timed(eng, args.steps, call, world)
+    dt, outs = timed(eng, args.steps, call, world, every_lane=True)
+    out = outs[(args.steps - 1) % eng.lanes]
     # bases = base tokens before the first EOS (outside the timed region)
     tok = out["tokens"].cpu().numpy()
     if args.mode == "beam":
@@ -523,6 +553,7 @@ def run_batch(args, world, rank, dev, cfg, W):
         "bases_per_sec": round(bases_per_step * args.steps * world / dt, 1),
         "timed_seconds": round(dt, 3),
         "min_length": args.min_length,
+        "pool_check": pool_check(cfg, W, args, args.mode, args.batch, beam, call, outs),
     }
     roof_iso = None
     greedy_roof = rank == 0 and not args.no_roofline and args.mode == "greedy"
@@ -619,7 +650,8 @@ def config_legs(args, world, rank, dev):
         lens = torch.full((B,), 512, dtype=torch.int32, device=dev)
         call = make_call(args, mode, sig, lens)
         run_calls(pool, max(2, pool.lanes), call)
-        dt, out = timed(pool, n, call, world)
+        dt, outs = timed(pool, n, call, world, every_lane=True)
+        out = outs[(n - 1) % pool.lanes]
         tok = out["tokens"].cpu().numpy()
         tok = tok[:, 0] if mode == "beam" else tok
         legs[key] = {"workload": f"{'NanoEncoder (3x BiLSTM)' if enc == 'nano' else '3-layer transformer'} encoder "
@@ -632,6 +664,7 @@ def config_legs(args, world, rank, dev):
                      "ms_per_step": round(dt / n * 1e3, 3), "steps": n, "calls_in_flight_per_gpu": pool.lanes}
         if mode == "beam":
             legs[key]["decoder_steps_executed"] = int(out["steps"].cpu().item())
+        legs[key]["pool_check"] = pool_check(cfg, W, args, mode, B, beam, call, outs)
         pool.close()
         del pool, sig, lens
         torch.cuda.empty_cache()
@@ -665,8 +698,10 @@ def host_inclusive(args, cfg, eng, sig_np, lens_np):
 def run_reads(args, world, rank, dev, cfg, W, n_reads_per_gpu):
     """configs[4]: the synthetic read set (lengths U[256,1024], 1-2 chunks per
     read) sharded over the ranks by LPT on sample count; every rank packs its
-    reads into full engine batches; host front end (median/MAD + windowing)
-    in a producer thread; timed region = max over ranks (shard.run_distributed)."""
+    reads into full engine batches; the front end (median/MAD + windowing)
+    runs on the device on each call's lane stream (ReadShard's default,
+    Translator.stream_raw_reads); timed region = max over ranks
+    (shard.run_distributed)."""
     import types
     from nanodecoder_amd import shard
     from nanodecoder_amd.engine import EnginePool
@@ -687,10 +722,12 @@ def run_reads(args, world, rank, dev, cfg, W, n_reads_per_gpu):
             "seconds": round(g["seconds"], 3), "samples_per_rank": g["samples_per_rank"],
             "load_imbalance_max_over_mean": round(g["load_imbalance"], 4),
             "scaling": "weak" if args.workload == "batch" else "weak (reads per GPU fixed)",
+            "frontend": g.get("frontend"),
             "workload": (f"configs[4]: {n_reads_per_gpu} synthetic reads per GPU, lengths U[256,1024], LPT shard, "
                          f"engine batch {args.batch}, reference batch_size 100, greedy, max_length "
-                         f"{args.max_length}; front end (median/MAD + windowing) in a host producer thread, "
-                         f"raw traces pre-generated (stand-in for the files read)")}
+                         f"{args.max_length}; raw reads handed to the translator, median/MAD + windowing on the "
+                         f"device per engine batch (nd_normalize_reads / nd_window_reads on the call's lane "
+                         f"stream), raw traces pre-generated (stand-in for the files read)")}
 
 
 def selftest_cpu(args):

@@ -129,10 +129,14 @@ def gemm_routes(reset: bool = False):
 
 
 def switches():
-    """{name: value} of the library's A/B switches set to a non-default value (nd_switches)."""
+    """{name: value} of the library's A/B switches set to a non-default value
+    (nd_switches), plus NANODEC_LIB when it replaces the in-tree library."""
     buf = ctypes.create_string_buffer(4096)
     lib().nd_switches(buf, len(buf))
-    return dict(kv.split("=", 1) for kv in buf.value.decode().split(";") if kv)
+    out = dict(kv.split("=", 1) for kv in buf.value.decode().split(";") if kv)
+    if os.path.realpath(LIB_PATH) != os.path.realpath(os.path.join(HERE, "libnanodec_hip.so")):
+        out["NANODEC_LIB"] = LIB_PATH
+    return out
 
 
 def check(rc: int, what: str = ""):

@@ -85,7 +85,13 @@ def _n_chunks(opt, src, gpu_fe):
 
 def _run_group(opt, translator, pending, gpu_fe):
     """Front end (device) + translate for one packed group, with the
-    per-group error isolation of translate.py:97-98."""
+    per-group error isolation of translate.py:97-98.  -frontend gpu: the raw
+    reads go to the translator, which normalises and windows every engine
+    batch on the device right before its call (stream_raw_reads); with
+    -attn_debug (its file needs each chunk's samples on the host) the chunks
+    come back to the host first."""
+    if gpu_fe and not opt.attn_debug:
+        return _translate_group(opt, translator, pending, raw=True)
     if gpu_fe:
         try:
             pending = _gpu_chunks(opt, pending)
@@ -168,11 +174,16 @@ def _translate_attn(opt, translator, group):
     return outs
 
 
-def _translate_group(opt, translator, group):
+def _translate_group(opt, translator, group, raw=False):
     t0 = time.time()
     try:
         if opt.attn_debug:
             outs = _translate_attn(opt, translator, group)
+        elif raw:  # [prefix, raw samples]: the front end runs on the device
+            outs = translator.translate_raw_reads([g[1] for g in group], batch_size=opt.batch_size,
+                                                  normalization=opt.normalization_raw,
+                                                  src_seq_length=opt.src_seq_length,
+                                                  src_seq_stride=opt.src_seq_stride)
         else:
             outs = translator.translate_reads([g[1:] for g in group], batch_size=opt.batch_size)
     except Exception as e:
@@ -180,9 +191,9 @@ def _translate_group(opt, translator, group):
             print("!!!error!!!data src: " + g[0].split(".txt")[0] + " (%r)" % (e,))
         return 0
     dt = time.time() - t0
-    total = sum(len(g) - 1 for g in group)
+    total = max(1, sum(len(preds) for _, preds in outs))
     for g, (_, preds) in zip(group, outs):
-        write_output(opt, g[0], preds, dt * (len(g) - 1) / total)
+        write_output(opt, g[0], preds, dt * len(preds) / total)
     return len(group)
 
 

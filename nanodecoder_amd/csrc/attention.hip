@@ -593,20 +593,37 @@ hipError_t launch_enc_attention(const float* qkv, const float* signal, const int
 // has no barrier.  (The first form shared one key list and the 8 waves'
 // counts through LDS across barriers; its output went wrong by whole chunks
 // when another engine's decoder GEMMs ran beside it on the GPU)
-#define R2_SLAB (8 * ENC_MAXT + 64 * 17 * 4)  // bytes per wave: keys (y, r), then its queries' E[y], E[r]
-template <bool DA, bool NTS>
+// LDS: 8 wave slabs of 8 KB = exactly 64 KB.  Each slab holds the keys (y, r)
+// and then its 64 queries' E[y], E[r] as [64][16] floats, column c of row q at
+// c ^ (q & 15) (the 64 lanes' row writes hit 64 distinct banks).  The round-3
+// layout ([64][17], 67,584 B in all) put wave 7's rows q >= 34 past byte
+// 65,536 and went wrong beside other engines' kernels;
+// ND_R2_EXLD=17 / ND_R2_PAD=<bytes> / ND_R2_FRONT=<bytes> rebuild that layout,
+// pad the allocation or shift the slabs (probe builds only,
+// tools/build_variant.sh, tools/r2_lds.sh).
+#ifndef ND_R2_EXLD
+#define ND_R2_EXLD 16
+#endif
+#ifndef ND_R2_PAD
+#define ND_R2_PAD 0
+#endif
+#ifndef ND_R2_FRONT
+#define ND_R2_FRONT 0  // probe builds: the slabs start this many bytes into the allocation
+#endif
+#define R2_SLAB (8 * ENC_MAXT + 64 * ND_R2_EXLD * 4)  // bytes per wave: keys (y, r), then its queries' E[y], E[r]
+__device__ __forceinline__ int r2_col(int q, int c) { return ND_R2_EXLD == 16 ? (c ^ (q & 15)) : c; }
 __global__ void __launch_bounds__(512)
-enc_attention_rank2_kernel(R2Args ka, const R2Args* __restrict__ da, int T) {
-  const R2Args& A = DA ? *da : ka;  // DA: the arguments from device memory (R2Args)
+enc_attention_rank2_kernel(R2Args A, int T) {
   const float* __restrict__ signal = A.signal;
   const int* __restrict__ span = A.span;
   const EmbedQkv eq = A.eq;
   const float* __restrict__ coef = A.coef;
   float* __restrict__ out = A.out;
-  __shared__ __attribute__((aligned(16))) char smem[8 * R2_SLAB];
+  __shared__ __attribute__((aligned(16))) char smem_[ND_R2_FRONT + 8 * R2_SLAB + ND_R2_PAD];
+  char* smem = smem_ + ND_R2_FRONT;
   const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  float2* kyr = reinterpret_cast<float2*>(smem + wave * R2_SLAB);                  // [ENC_MAXT]
-  float(*ex)[17] = reinterpret_cast<float(*)[17]>(smem + wave * R2_SLAB + 8 * ENC_MAXT);  // [64][17]
+  float2* kyr = reinterpret_cast<float2*>(smem + wave * R2_SLAB);                                   // [ENC_MAXT]
+  float(*ex)[ND_R2_EXLD] = reinterpret_cast<float(*)[ND_R2_EXLD]>(smem + wave * R2_SLAB + 8 * ENC_MAXT);  // [64][16]
   const int L = min(span[b], T);
   const float* sig = signal + (size_t)b * T;
   // every key of the chunk in this wave: key u = 64 j + lane
@@ -673,8 +690,8 @@ enc_attention_rank2_kernel(R2Args ka, const R2Args* __restrict__ da, int T) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const float inv = __builtin_amdgcn_rcpf(sp[p][j]);
-        ex[lane][2 * (2 * p + j)] = sy[p][j] * inv;
-        ex[lane][2 * (2 * p + j) + 1] = sr[p][j] * inv;
+        ex[lane][r2_col(lane, 2 * (2 * p + j))] = sy[p][j] * inv;
+        ex[lane][r2_col(lane, 2 * (2 * p + j) + 1)] = sr[p][j] * inv;
       }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's E[y], E[r] staged
@@ -683,17 +700,13 @@ enc_attention_rank2_kernel(R2Args ka, const R2Args* __restrict__ da, int T) {
   const f32x4 av = ld4(eq.ac + n), cv = ld4(eq.ac + 3 * ND_D + n), bv = ld4(eq.bias + n);
   const int q1 = min(64, L - 64 * wave);
   for (int q = 0; q < q1; ++q) {
-    const f32x4 o = av * ex[q][2 * h] + cv * ex[q][2 * h + 1] + bv;
-    f32x4* dst = reinterpret_cast<f32x4*>(out + ((size_t)b * T + 64 * wave + q) * ND_D + lane * 4);
-    if constexpr (NTS)
-      __builtin_nontemporal_store(o, dst);  // probe: past the L2s
-    else
-      *dst = o;
+    const f32x4 o = av * ex[q][r2_col(q, 2 * h)] + cv * ex[q][r2_col(q, 2 * h + 1)] + bv;
+    *reinterpret_cast<f32x4*>(out + ((size_t)b * T + 64 * wave + q) * ND_D + lane * 4) = o;
   }
 }
 
 hipError_t launch_enc_attention_rank2(const float* signal, const int* span, const EmbedQkv& eq, const float* coef,
-                                      float* out, int B, int T, hipStream_t s, const R2Args* dev_args) {
+                                      float* out, int B, int T, hipStream_t s) {
   if (T > ENC_MAXT || T <= 0 || !eq.ac || !eq.bias || !coef) return hipErrorInvalidValue;
   R2Args a;
   a.signal = signal;
@@ -701,16 +714,7 @@ hipError_t launch_enc_attention_rank2(const float* signal, const int* span, cons
   a.eq = eq;
   a.coef = coef;
   a.out = out;
-  static const bool nts = [] {
-    const char* e = getenv("ND_ENC_ATTN0");
-    return e && atoi(e) == 3;  // probe: output stores non-temporal
-  }();
-  if (dev_args)
-    hipLaunchKernelGGL((enc_attention_rank2_kernel<true, false>), dim3(B), dim3(512), 0, s, a, dev_args, T);
-  else if (nts)
-    hipLaunchKernelGGL((enc_attention_rank2_kernel<false, true>), dim3(B), dim3(512), 0, s, a, dev_args, T);
-  else
-    hipLaunchKernelGGL((enc_attention_rank2_kernel<false, false>), dim3(B), dim3(512), 0, s, a, dev_args, T);
+  hipLaunchKernelGGL(enc_attention_rank2_kernel, dim3(B), dim3(512), 0, s, a, T);
   return hipGetLastError();
 }
 

@@ -153,7 +153,6 @@ struct nd_ctx {
   // layer 0's attention in the same closed form: per head the 6 coefficients
   // of alpha_t, beta_t (launch_enc_attention_rank2), on the device
   float* eq_coef = nullptr;
-  nd::R2Args* r2args = nullptr;  // the closed-form layer-0 attention's arguments in device memory (ND_ENC_ATTN0=2)
   std::vector<EncLayer> enc;
   std::vector<NanoLayer> nano;
   float* nano_W = nullptr;
@@ -575,15 +574,11 @@ static bool enc_qkv_folded(const nd_ctx* c, const EncLayer& next) {
 // chunks of its output came out different (max |d memory| ~0.2,
 // tools/rank2_probe.py); alone it matches the oracle.  Cause not found (not the
 // LDS size granule, not hardware-queue sharing: DESIGN.md section 5)
-static int enc_attn0_mode() {  // 0 off, 1 on, 2 on with its arguments from device memory
-  static const int m = [] {
-    const char* e = getenv("ND_ENC_ATTN0");
-    return e ? atoi(e) : 0;
-  }();
-  return m;
-}
 static bool enc_attn0_rank2(const nd_ctx* c) {
-  const bool on = enc_attn0_mode() >= 1 && enc_attn0_mode() <= 3;
+  static const bool on = [] {
+    const char* e = getenv("ND_ENC_ATTN0");
+    return e && atoi(e) == 1;
+  }();
   return on && c->eq_ready && c->eq_coef != nullptr;
 }
 
@@ -609,8 +604,7 @@ static hipError_t enqueue_encode_transformer(nd_ctx* c, int B, int T, hipStream_
     if (!qkv_done) LCHK(G(c->x, D, L.nwqkv, 3 * D, D, L.nbqkv, c->big, 3 * D, M).h3(c).ln(c->x_part, pnx).run(s));
     qkv_done = false;
     if (a0 && li == 0)
-      LCHK(nd::launch_enc_attention_rank2(c->sig, c->span, eq, c->eq_coef, c->att, B, T, s,
-                                          enc_attn0_mode() == 2 ? c->r2args : nullptr));
+      LCHK(nd::launch_enc_attention_rank2(c->sig, c->span, eq, c->eq_coef, c->att, B, T, s));
     else
       LCHK(nd::launch_enc_attention(c->big, c->sig, c->span, c->att, B, T, s, c->exact, c->ovf));
     if (enc_wo_fused(c, L)) {  // Wo + residual, LN, FFN in one launch; the layer's rows updated in place
@@ -1206,25 +1200,6 @@ int nd_finalize(nd_ctx* c) {
       if (!c->eq_coef && dalloc(c, &c->eq_coef, coef.size()) != hipSuccess) return fail(ND_ERR_HIP, "alloc");
       HIPCHK(hipMemcpy(c->eq_coef, coef.data(), coef.size() * 4, hipMemcpyHostToDevice));
       c->eq_ready = true;
-      {  // the closed-form layer-0 attention's arguments, for its device-memory form
-        nd::R2Args a;
-        a.signal = c->sig;
-        a.span = c->span;
-        a.eq.ac = c->eq_ac;
-        a.eq.bias = c->enc[0].nbqkv;
-        a.eq.mww = c->eq_m[0];
-        a.eq.mwb = c->eq_m[1];
-        a.eq.mbb = c->eq_m[2];
-        a.eq.qkv = c->big;
-        a.coef = c->eq_coef;
-        a.out = c->att;
-        if (!c->r2args) {
-          float* p = nullptr;
-          if (dalloc(c, &p, (sizeof(nd::R2Args) + 3) / 4) != hipSuccess) return fail(ND_ERR_HIP, "alloc");
-          c->r2args = reinterpret_cast<nd::R2Args*>(p);
-        }
-        HIPCHK(hipMemcpy(c->r2args, &a, sizeof(a), hipMemcpyHostToDevice));
-      }
     }
     if (c->nctxkv_w)
       HIPCHK(fold(c->ctxkv_w, c->ctxkv_b, c->enc_ln_g, c->enc_ln_b, c->nctxkv_w, c->nctxkv_b,

@@ -108,9 +108,6 @@ struct EmbedQkv {
 // of t that cancels in the softmax) with alpha_t, beta_t linear in
 // (y_t, r_t, 1) (coef [8 heads][6], log2 units), and the output is
 // a_v E[y] + c_v E[r] + b_v over the softmax: out [M, 256] row-major.
-// dev_args (nullable): the same arguments as an R2Args in device memory; the
-// kernel then reads them from there instead of its kernel-argument segment
-// (a probe of the co-residency fault)
 struct R2Args {
   const float* signal = nullptr;
   const int* span = nullptr;
@@ -119,7 +116,7 @@ struct R2Args {
   float* out = nullptr;
 };
 hipError_t launch_enc_attention_rank2(const float* signal, const int* span, const EmbedQkv& eq, const float* coef,
-                                      float* out, int B, int T, hipStream_t s, const R2Args* dev_args = nullptr);
+                                      float* out, int B, int T, hipStream_t s);
 // ac and the three means (double scal[3]) from the LN-folded weight [768, 256]
 hipError_t launch_embed_qkv_prep(const float* w_in, const float* b_in, const float* nwqkv, float* ac, double* scal,
                                  hipStream_t s);

@@ -87,47 +87,70 @@ def windows(n: int, max_length: int, stride: int):
     return out
 
 
-def normalize_window_gpu(raws, normalization: str, max_length: int, stride: int, device=0, T: int = None):
-    """extract_fast5_raw's normalisation and windowing for many reads on the
-    GPU (nd_normalize_reads + nd_window_reads, frontend.hip): one host-to-
-    device copy of the concatenated float64 reads, fp64 medians by radix
-    select, chunks written straight into a zero-padded [C, T] float32 batch.
-    Returns (signal [C, T] device tensor, chunk lengths [C] int32,
-    chunk -> read index [C] int32)."""
+def _pinned(a: np.ndarray):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).pin_memory()
+
+
+def device_batch(raws, rd, start, length, normalization: str, B: int, T: int, device):
+    """The device front end for one engine batch (nd_normalize_reads +
+    nd_window_reads, frontend.hip) on the CURRENT stream: the reads ``raws``
+    (float64 arrays) are copied to the device once (pinned, asynchronous),
+    normalised in fp64 (median/MAD, median/std or none as
+    utils/labelop.py:220-223) and cut into chunk rows c = samples
+    [start[c], start[c] + length[c]) of read rd[c] (index into ``raws``), zero
+    padded, in a [B, T] float32 batch (rows >= len(rd) zero).  Returns
+    (signal [B, T], the device tensors to keep alive until the stream has
+    used them)."""
     import ctypes
 
     import torch
 
     from . import _lib
     method = NORM_METHOD.get(normalization, 0)  # anything else: the raw read, as labelop.py:220-223
-    raws = [np.asarray(r, dtype=np.float64).reshape(-1) for r in raws]
-    lens = np.array([r.size for r in raws], np.int64)
+    lens = np.fromiter((r.size for r in raws), np.int64, len(raws))
     if (lens < 1).any():
         raise ValueError("empty read")
     off = np.zeros(len(raws) + 1, np.int64)
     off[1:] = np.cumsum(lens)
-    rd, st, ln = [], [], []
-    for r, n in enumerate(lens):
-        for a, b in windows(int(n), max_length, stride):
-            rd.append(r)
-            st.append(a)
-            ln.append(b)
-    T = T or max_length
+    C = len(rd)
+    if C > B or (C and int(np.max(length)) > T):
+        raise ValueError("chunk descriptors exceed the batch")
     dev = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
-    raw_d = torch.from_numpy(np.concatenate(raws)).to(dev)
-    off_d = torch.from_numpy(off).to(dev)
+    idx = np.zeros((len(off) * 2 + 3 * C + 1) // 2 * 2, np.int32)  # one pinned block of every index array
+    idx.view(np.int64)[: len(off)] = off
+    idx[2 * len(off): 2 * len(off) + 3 * C] = np.concatenate([np.asarray(rd, np.int32), np.asarray(start, np.int32),
+                                         np.asarray(length, np.int32)])
+    raw_d = _pinned(np.concatenate(raws) if len(raws) > 1 else raws[0]).to(dev, non_blocking=True)
+    idx_d = _pinned(idx).to(dev, non_blocking=True)
+    off_d = idx_d[: 2 * len(off)].view(torch.int64)
+    rd_d = idx_d[2 * len(off): 2 * len(off) + C]
+    st_d = idx_d[2 * len(off) + C: 2 * len(off) + 2 * C]
+    ln_d = idx_d[2 * len(off) + 2 * C: 2 * len(off) + 3 * C]
     norm_d = torch.empty(int(off[-1]), dtype=torch.float32, device=dev)
+    sig = torch.zeros(B, T, dtype=torch.float32, device=dev)
     L = _lib.lib()
     stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     _lib.check(L.nd_normalize_reads(p(raw_d), p(off_d), len(raws), method, p(norm_d), stream), "nd_normalize_reads")
-    C = len(rd)
-    rd_d = torch.tensor(rd, dtype=torch.int32, device=dev)
-    st_d = torch.tensor(st, dtype=torch.int32, device=dev)
-    ln_d = torch.tensor(ln, dtype=torch.int32, device=dev)
-    sig = torch.empty(C, T, dtype=torch.float32, device=dev)
     _lib.check(L.nd_window_reads(p(norm_d), p(off_d), p(rd_d), p(st_d), p(ln_d), C, T, p(sig), stream),
                "nd_window_reads")
+    return sig, (raw_d, idx_d, norm_d)
+
+
+def normalize_window_gpu(raws, normalization: str, max_length: int, stride: int, device=0, T: int = None):
+    """extract_fast5_raw's normalisation and windowing for many reads on the
+    GPU (device_batch over every window of every read).  Returns (signal
+    [C, T] device tensor, chunk lengths [C] int32, chunk -> read index [C]
+    int32)."""
+    raws = [np.asarray(r, dtype=np.float64).reshape(-1) for r in raws]
+    rd, st, ln = [], [], []
+    for r, x in enumerate(raws):
+        for a, b in windows(int(x.size), max_length, stride):
+            rd.append(r)
+            st.append(a)
+            ln.append(b)
+    sig, _ = device_batch(raws, rd, st, ln, normalization, len(rd), T or max_length, device)
     return sig, np.array(ln, np.int32), np.array(rd, np.int32)
 
 

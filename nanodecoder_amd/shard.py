@@ -55,11 +55,6 @@ def synth_raw(read_id: int, n: int) -> np.ndarray:
     return np.round(np.repeat(lv, dw)[:n] + rng.normal(0.0, 2.0, size=n))
 
 
-def synth_read(read_id: int, n: int) -> np.ndarray:
-    """synth_raw, median/MAD normalised, float64."""
-    return synth.normalize_median(synth_raw(read_id, n))
-
-
 def pack_weights(W: Dict[str, np.ndarray]):
     names = sorted(W)
     meta = [(n, tuple(W[n].shape)) for n in names]
@@ -91,32 +86,51 @@ def broadcast_weights(W, device) -> Dict[str, np.ndarray]:
     return unpack_weights(meta, t.cpu().numpy())
 
 
-class ReadShard:
-    """Translates one rank's reads with a Translator-like object exposing
-    ``stream_reads(iterable_of_chunk_lists, batch_size)``.
+def count_bases(tok: np.ndarray, eos: int, specials) -> int:
+    """Base tokens of [n, S] token rows: before each row's first EOS, not a
+    special (<unk>, <blank>, <s>)."""
+    if tok.size == 0:
+        return 0
+    is_eos = tok == eos
+    first = np.where(is_eos.any(1), is_eos.argmax(1), tok.shape[1])
+    keep = (np.arange(tok.shape[1])[None, :] < first[:, None]) & ~np.isin(tok, list(specials))
+    return int(keep.sum())
 
-    The host front end (median/MAD normalisation + windowing,
-    utils/labelop.py:194-233) runs in a producer thread and overlaps the
-    device: the Translator keeps one engine batch in flight while it packs
-    the next, and the producer stays up to ``prefetch`` reads ahead."""
+
+class ReadShard:
+    """Translates one rank's reads with a Translator-like object.
+
+    ``frontend="gpu"`` (default when the translator has ``stream_raw_reads``):
+    a producer thread hands RAW reads over and the translator normalises and
+    windows each engine batch on the device (nd_normalize_reads /
+    nd_window_reads, utils/labelop.py:194-233) right before the engine call,
+    on the call's stream; tokens come back as arrays.  ``frontend="cpu"``:
+    the host front end (median/MAD + windowing in numpy) runs in the producer
+    thread and chunks go through ``stream_reads``.  Either way the translator
+    keeps one engine batch per pool lane in flight while it packs the next,
+    and the producer stays up to ``prefetch`` reads ahead."""
 
     def __init__(self, translator, batch_size: int = 100, src_seq_length: int = 512, src_seq_stride: int = 512,
-                 prefetch: int = 2048):
+                 prefetch: int = 2048, frontend: str = "auto", normalization: str = "median"):
         self.tr = translator
         self.batch_size = batch_size
         self.L, self.stride = src_seq_length, src_seq_stride
         self.prefetch = prefetch
+        if frontend == "auto":
+            frontend = "gpu" if hasattr(translator, "stream_raw_reads") else "cpu"
+        self.frontend = frontend
+        self.normalization = normalization
 
     def _produce(self, read_ids, lengths, raws, q, stop):
         try:
             for k, rid in enumerate(read_ids):
                 if stop.is_set():
                     return
-                if raws is not None:
-                    sig = synth.normalize_median(raws[k])
+                raw = raws[k] if raws is not None else synth_raw(int(rid), int(lengths[rid]))
+                if self.frontend == "gpu":
+                    q.put(raw)
                 else:
-                    sig = synth_read(int(rid), int(lengths[rid]))
-                q.put(synth.window(sig, self.L, self.stride))
+                    q.put(synth.window(synth.normalize_median(raw), self.L, self.stride))
             q.put(None)
         except BaseException as e:  # surfaced in the consumer
             q.put(e)
@@ -127,6 +141,7 @@ class ReadShard:
         is timed; otherwise the synthetic reads are generated on the fly."""
         import queue
         import threading
+        from . import frontend
         q: "queue.Queue" = queue.Queue(maxsize=max(1, self.prefetch))
         stop = threading.Event()
         th = threading.Thread(target=self._produce, args=(list(read_ids), lengths, raws, q, stop), daemon=True)
@@ -135,6 +150,7 @@ class ReadShard:
         specials = {self.tr.cfg.unk_idx, self.tr.cfg.pad_idx, self.tr.cfg.bos_idx}
         eos = self.tr.cfg.eos_idx
         n_samples = {}
+        gpu = self.frontend == "gpu"
 
         def reads():
             k = 0
@@ -144,25 +160,37 @@ class ReadShard:
                     return
                 if isinstance(item, BaseException):
                     raise item
-                n_samples[k] = (sum(len(c) for c in item), len(item))
+                if gpu:
+                    w = frontend.windows(int(item.size), self.L, self.stride)
+                    n_samples[k] = (sum(ln for _, ln in w), len(w))
+                else:
+                    n_samples[k] = (sum(len(c) for c in item), len(item))
                 k += 1
                 yield item
 
         t0 = time.perf_counter()
         th.start()
         try:
-            for k, res in self.tr.stream_reads(reads(), self.batch_size):
-                ns, nc = n_samples.pop(k)
-                samples += ns
-                chunks += nc
-                for r in res:
-                    toks = r[1][0]
-                    for t in toks:
-                        if t == eos:
-                            break
-                        bases += t not in specials
-                if keep_predictions:
-                    preds[int(read_ids[k])] = [[" ".join(self.tr._tokens_to_sent(t)) for t in r[1]] for r in res]
+            if gpu:
+                it = self.tr.stream_raw_reads(reads(), self.batch_size, self.normalization, self.L, self.stride,
+                                              arrays=True)
+                for k, tok, _ in it:
+                    ns, nc = n_samples.pop(k)
+                    samples += ns
+                    chunks += nc
+                    bases += count_bases(tok, eos, specials)
+                    if keep_predictions:
+                        preds[int(read_ids[k])] = [[" ".join(self.tr._tokens_to_sent(t))] for t in tok.tolist()]
+            else:
+                for k, res in self.tr.stream_reads(reads(), self.batch_size):
+                    ns, nc = n_samples.pop(k)
+                    samples += ns
+                    chunks += nc
+                    for r in res:
+                        bases += count_bases(np.asarray([r[1][0]], np.int64), eos, specials)
+                    if keep_predictions:
+                        preds[int(read_ids[k])] = [[" ".join(self.tr._tokens_to_sent(t)) for t in r[1]]
+                                                   for r in res]
         finally:
             stop.set()
             while th.is_alive():  # unblock a producer waiting on a full queue
@@ -172,12 +200,12 @@ class ReadShard:
                     pass
                 th.join(timeout=0.01)
         return dict(samples=samples, bases=bases, chunks=chunks, seconds=time.perf_counter() - t0,
-                    reads=len(read_ids)), preds
+                    reads=len(read_ids), frontend=self.frontend), preds
 
 
 def run_distributed(n_reads: int, translator_factory: Callable, weights_factory: Callable, device,
                     batch_size: int = 100, seed: int = 0, keep_predictions: bool = False, pregenerate: bool = False,
-                    warmup_reads: int = 0):
+                    warmup_reads: int = 0, frontend: str = "auto"):
     """Rank-local part of the sharded job; returns (global stats, local preds).
     The timed region (max over ranks) covers the front end, packing, the
     engine and the token copies of the rank's reads."""
@@ -193,13 +221,14 @@ def run_distributed(n_reads: int, translator_factory: Callable, weights_factory:
     if pregenerate:  # the raw traces stand in for files already read (untimed); the front end is timed
         raws = [synth_raw(int(i), int(lengths[i])) for i in mine]
     if warmup_reads:  # graphs captured and pinned buffers made outside the timed region
-        ReadShard(tr, batch_size=batch_size).run(mine[:warmup_reads], lengths)
+        ReadShard(tr, batch_size=batch_size, frontend=frontend).run(mine[:warmup_reads], lengths)
     on_gpu = device.type == "cuda" and torch.cuda.is_available()
     if multi:
         dist.barrier()
     if on_gpu:
         torch.cuda.synchronize(device)
-    stats, preds = ReadShard(tr, batch_size=batch_size).run(mine, lengths, keep_predictions, raws=raws)
+    shard = ReadShard(tr, batch_size=batch_size, frontend=frontend)
+    stats, preds = shard.run(mine, lengths, keep_predictions, raws=raws)
     if on_gpu:
         torch.cuda.synchronize(device)
     if multi:
@@ -214,7 +243,7 @@ def run_distributed(n_reads: int, translator_factory: Callable, weights_factory:
         dist.all_reduce(secs, op=dist.ReduceOp.MAX)
     loads = per_rank.cpu().numpy()
     g = dict(samples=int(red[0]), bases=int(red[1]), chunks=int(red[2]), seconds=float(secs[0]), world=world,
-             reads=int(n_reads), samples_per_rank=[int(x) for x in loads],
+             reads=int(n_reads), samples_per_rank=[int(x) for x in loads], frontend=shard.frontend,
              load_imbalance=float(loads.max() / max(loads.mean(), 1.0)))
     return g, preds
 
@@ -227,7 +256,9 @@ def main(argv=None):
     ap.add_argument("--max-length", type=int, default=100)
     ap.add_argument("--min-length", type=int, default=0)
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--inflight", type=int, default=2, help="translate calls on the device at once (EnginePool lanes)")
+    ap.add_argument("--inflight", type=int, default=3, help="translate calls on the device at once (EnginePool lanes)")
+    ap.add_argument("--frontend", default="gpu", choices=["gpu", "cpu"],
+                    help="normalise and window the reads on the device (gpu) or in a host thread (cpu)")
     args = ap.parse_args(argv)
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
@@ -248,7 +279,7 @@ def main(argv=None):
         return Translator(cfg, W, opt, engine=eng)
 
     g, _ = run_distributed(args.reads, translator_factory, weights_factory, dev, batch_size=args.batch_size,
-                           seed=args.seed)
+                           seed=args.seed, frontend=args.frontend)
     if dist.get_rank() == 0:
         g["samples_per_sec"] = g["samples"] / g["seconds"]
         g["bases_per_sec"] = g["bases"] / g["seconds"]

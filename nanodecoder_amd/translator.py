@@ -122,12 +122,18 @@ class Translator(object):
         self.max_batch = int(getattr(opt, "engine_max_batch", 0) or 0) or max(batch_cap, 256)
         if engine is None:
             dev = torch.cuda.current_device()  # the reference moves tensors to the default "cuda" device
-            engine = Engine(cfg, weights, device=dev, max_batch=self.max_batch,
-                            max_src_len=int(getattr(opt, "src_seq_length", 512)) if
-                            int(getattr(opt, "src_seq_length", 512)) <= 512 else 512,
-                            max_steps=self.max_length, max_beam=max(1, self.beam_size))
+            kw = dict(device=dev, max_batch=self.max_batch, max_steps=self.max_length,
+                      max_src_len=min(512, int(getattr(opt, "src_seq_length", 512))),
+                      max_beam=max(1, self.beam_size))
+            # -engine_lanes (default 3): that many calls in flight on the GPU
+            # (EnginePool), stream_reads keeping every lane busy
+            lanes = int(getattr(opt, "engine_lanes", 3) or 1)
+            if lanes > 1 and Engine is _HipEngine:
+                engine = EnginePool(cfg, weights, lanes=lanes, **kw)
+            else:
+                engine = Engine(cfg, weights, **kw)
         self.engine = engine
-        self._pinned, self._pin_i, self._copy_stream = None, 0, None
+        self._pinned, self._pin_i = None, 0
 
     def _check_supported(self):
         if self.beam_size == 1:
@@ -213,7 +219,15 @@ class Translator(object):
         L[:n], S[:n] = lens, spans
         if dev_in is not None:
             sig, L, S = dev_in
-        job = dict(n=n, lens=lens, attn=attn, B=B, inputs=dev_in, args=(chunks, spans, groups, attn))
+        job = self._enqueue(sig, L, S, B, n, lens, groups, attn, dev_in)
+        job["again"] = lambda: self._submit(chunks, spans, groups, attn)
+        return job
+
+    def _enqueue(self, sig, L, S, B: int, n: int, lens: np.ndarray, groups, attn: bool, inputs):
+        """The engine call for one staged batch (signal [B, T], chunk lengths
+        and spans [B]; the first n rows are chunks), its results copied to
+        pinned host buffers on the call's own stream."""
+        job = dict(n=n, lens=lens, attn=attn, B=B, inputs=inputs)
         if self.beam_size == 1:
             if not (self.random_sampling_temp == 0.0 or self.sample_from_topk == 1):
                 # sample_with_temperature's random branch (translator.py:376-393)
@@ -260,42 +274,52 @@ class Translator(object):
                     coverage_penalty=gs.coverage_penalty, beta=gs.beta, stepwise_penalty=self.stepwise_penalty,
                     block_ngram_repeat=self.block_ngram_repeat, ignore_ids=exclusion, cut=cut, return_attn=attn)
             job.update(kind="beam", r=r, grp=grp, sorted_rows=sorted_rows, cut=cut)
-        if "event" in r:  # EnginePool: recorded on the call's lane stream
-            job["event"] = r["event"]
-        elif self._real_engine():
-            # fires when this call's outputs are written (the engine's release
-            # event is ordered before it on the current stream)
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(self.engine.device))
-            job["event"] = ev
+        if self._real_engine():
+            self._copy_out(job)
         return job
 
-    def _host(self, job, *names):
-        """Results of a submitted call on the host.  The copies wait only for
-        THIS call (its event, on a side stream), not for calls submitted after
-        it on the current stream."""
-        r = job["r"]
-        ev = job.get("event")
-        if ev is None:
-            return [None if r.get(k) is None else r[k].cpu().numpy() for k in names]
-        if self._copy_stream is None:
-            self._copy_stream = torch.cuda.Stream(self.engine.device)
-        cs = self._copy_stream
-        with torch.cuda.stream(cs):
-            cs.wait_event(ev)
-            out = [None if r.get(k) is None else r[k].cpu().numpy() for k in names]
-        return out
+    _HOST_KEYS = ("tokens", "scores", "lens", "attn", "done_step", "overflow")
 
-    def _rerun_exact(self, job):
+    def _copy_out(self, job):
+        """Enqueue the call's device-to-host copies (into pinned buffers) on
+        the stream the call ran on (its EnginePool lane, or the current
+        stream the single Engine joined), then an event: ``_host`` waits on
+        that event alone, never on calls submitted after this one."""
+        r = job["r"]
+        st = self.engine.engines[r["lane"]].stream if "lane" in r else \
+            torch.cuda.current_stream(self.engine.device)
+        host = {}
+        with torch.cuda.stream(st):
+            for k in self._HOST_KEYS:
+                t = r.get(k)
+                if isinstance(t, torch.Tensor):
+                    h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+                    h.copy_(t, non_blocking=True)
+                    host[k] = h
+            ev = torch.cuda.Event()
+            ev.record(st)
+        job["host"], job["event"] = host, ev
+
+    def _host(self, job, *names):
+        """Results of a submitted call on the host (numpy; None where the
+        call has no such output)."""
+        if "host" in job:
+            job["event"].synchronize()
+            h = job["host"]
+            return [h[k].numpy() if k in h else None for k in names]
+        r = job["r"]  # stand-in engines: host tensors
+        return [None if r.get(k) is None else r[k].cpu().numpy() for k in names]
+
+    def _rerun_exact(self, job, finish=None):
         """Split-fp16 range guard (nd_take_overflow): a call in which some
         split activation reached |x| >= 65504 (fp16's range; the reference's
         fp32 is still finite there) runs again with every product in exact
         fp32, and its results replace the flagged ones."""
         self.engine.set_exact_fp32(True)
         try:
-            again = self._submit(*job["args"])
+            again = job["again"]()
             again["exact"] = True
-            return self._finish(again)
+            return (finish or self._finish)(again)
         finally:
             self.engine.set_exact_fp32(False)
 
@@ -442,6 +466,22 @@ class Translator(object):
         results = [None] * len(reads)
         for ri, res in self.stream_reads(reads, batch_size, attn_debug):
             results[ri] = res
+        return self._report(results, attn_debug)
+
+    def translate_raw_reads(self, raws: Sequence[np.ndarray], batch_size: int, normalization: str = "median",
+                            src_seq_length: int = 512, src_seq_stride: int = 512):
+        """translate_reads on raw reads with the signal front end on the
+        device (stream_raw_reads); returns per read (all_scores,
+        all_predictions)."""
+        results = [None] * len(raws)
+        for ri, res in self.stream_raw_reads(raws, batch_size, normalization, src_seq_length, src_seq_stride):
+            results[ri] = res
+        return self._report(results, False)
+
+    def _report(self, results, attn_debug: bool):
+        """Per read (all_scores, all_predictions) from per-chunk results, with
+        the reference's verbose / -dump_beam / report_score side outputs
+        (translate/translator.py:255-369)."""
         ret = []
         counter = 0
         pred_score_total, pred_words_total = 0.0, 0
@@ -481,6 +521,128 @@ class Translator(object):
                                                            np.exp(-pred_score_total / pred_words_total))
             (self.logger.info if self.logger else print)(msg)
         return ret
+
+    # ------------------------------------------------------ device front end
+    def _next_stream(self):
+        """The stream the engine's next call will run on (its EnginePool
+        lane, or the current stream for a single Engine)."""
+        if isinstance(self.engine, EnginePool):
+            return self.engine.engines[self.engine._next].stream
+        return torch.cuda.current_stream(self.engine.device)
+
+    def _submit_raw(self, items, batch_reads, normalization: str):
+        """One engine batch from raw reads: chunk descriptors ``items`` =
+        (read, chunk, start, length, span, reference batch) and the reads
+        they cut (``batch_reads``: read -> float64 samples).  The front end
+        (frontend.device_batch) runs on the call's own stream, so the
+        normalised chunks go from HBM to the engine with no host pass."""
+        from . import frontend
+        n = len(items)
+        uniq = list(batch_reads)
+        local = {ri: j for j, ri in enumerate(uniq)}
+        lens = np.fromiter((it[3] for it in items), np.int32, n)
+        spans = np.fromiter((it[4] for it in items), np.int32, n)
+        if spans.max() > self.engine.max_src_len:
+            raise ValueError(f"chunk longer than {self.engine.max_src_len} samples (src_seq_length) is not supported")
+        T = min(self.engine.max_src_len, ((int(spans.max()) + 63) // 64) * 64)
+        B = _bucket(n, self.engine.max_batch)
+        ls = np.ones(2 * B, np.int32)
+        ls[:n], ls[B: B + n] = lens, spans
+        st = self._next_stream()
+        with torch.cuda.stream(st):
+            sig, keep = frontend.device_batch([batch_reads[r] for r in uniq],
+                                              np.fromiter((local[it[0]] for it in items), np.int32, n),
+                                              np.fromiter((it[2] for it in items), np.int32, n), lens,
+                                              normalization, B, T, self.engine.device)
+            ls_d = torch.from_numpy(ls).pin_memory().to(self.engine.device, non_blocking=True)
+            job = self._enqueue(sig, ls_d[:B], ls_d[B:], B, n, lens, [it[5] for it in items], False,
+                                (sig, ls_d, keep))
+        job["again"] = lambda: self._submit_raw(items, batch_reads, normalization)
+        return job
+
+    def stream_raw_reads(self, raws: Iterable, batch_size: int, normalization: str = "median",
+                         src_seq_length: int = 512, src_seq_stride: int = 512, arrays: bool = False):
+        """stream_reads on RAW reads (float64 sample arrays, as
+        frontend.read_raw returns them) with extract_fast5_raw's
+        normalisation and windowing (utils/labelop.py:194-243) on the device:
+        the reads of each engine batch go to HBM once and are cut into its
+        [B, T] signal batch there (nd_normalize_reads / nd_window_reads),
+        bit-identical to the host front end.  Chunks keep the span of their
+        reference batch (``batch_size`` consecutive chunks of one read), so
+        results equal per-read translate() on the host front end's chunks.
+        Yields (read index, per-chunk results) as stream_reads does; with
+        ``arrays`` (greedy and sampling only) (read index, tokens [n_chunks,
+        max_length] int32, scores [n_chunks] float32) instead."""
+        import collections
+
+        from . import frontend
+        if arrays and self.beam_size != 1:
+            raise ValueError("arrays=True is for greedy / sampling decoding")
+        cap = self.engine.max_batch
+        depth = self._depth()
+        pending, batch_reads, inflight = [], {}, collections.deque()
+        results, remaining = {}, {}
+        nb = 0
+
+        def collect(jb):
+            job, items = jb
+            if arrays:
+                tok, sc = self._finish_arrays(job)
+                outs = ((tok[i], sc[i]) for i in range(len(items)))
+            else:
+                outs = self._finish(job)
+            done = []
+            for (ri, ci, _, _, _, _), o in zip(items, outs):
+                if arrays:
+                    results[ri][0][ci] = o[0]
+                    results[ri][1][ci] = o[1]
+                else:
+                    results[ri][ci] = o
+                remaining[ri] -= 1
+                if remaining[ri] == 0:
+                    done.append(ri)
+            return done
+
+        def flush():
+            nonlocal pending, batch_reads
+            inflight.append((self._submit_raw(pending, batch_reads, normalization), pending))
+            pending, batch_reads = [], {}
+
+        for ri, raw in enumerate(raws):
+            raw = np.asarray(raw, dtype=np.float64).reshape(-1)
+            if raw.size == 0:
+                yield (ri, np.zeros((0, self.max_length), np.int32), np.zeros(0, np.float32)) if arrays else (ri, [])
+                continue
+            wins = frontend.windows(int(raw.size), src_seq_length, src_seq_stride)
+            if arrays:
+                results[ri] = (np.empty((len(wins), self.max_length), np.int32), np.empty(len(wins), np.float32))
+            else:
+                results[ri] = [None] * len(wins)
+            remaining[ri] = len(wins)
+            for b0 in range(0, len(wins), batch_size):
+                part = wins[b0: b0 + batch_size]
+                span = max(ln for _, ln in part)
+                for k, (st, ln) in enumerate(part):
+                    pending.append((ri, b0 + k, st, ln, span, nb))
+                    batch_reads[ri] = raw
+                    if len(pending) == cap:
+                        flush()
+                        while len(inflight) > depth:
+                            for r in collect(inflight.popleft()):
+                                yield (r,) + results.pop(r) if arrays else (r, results.pop(r))
+                nb += 1
+        if pending:
+            flush()
+        while inflight:
+            for r in collect(inflight.popleft()):
+                yield (r,) + results.pop(r) if arrays else (r, results.pop(r))
+
+    def _finish_arrays(self, job):
+        """(tokens [n, S], scores [n]) numpy of a greedy / sampling call."""
+        tok, sc, ov = self._host(job, "tokens", "scores", "overflow")
+        if self._overflowed(job, ov):
+            return self._rerun_exact(job, self._finish_arrays)
+        return tok[: job["n"]], sc[: job["n"]]
 
     def translate_batch(self, batch, data=None, attn_debug=False, fast=False):
         """translate/translator.py:505-540 on a batch object with

@@ -187,6 +187,93 @@ def test_pool_matches_single_engine(encoder, mode):
     pool.close()
 
 
+def _ragged(sig, seed):
+    """Half the chunks cut to 300..511 samples (zero padded, span = the
+    reference batch of 4 consecutive chunks' longest): pad-masked keys and
+    spans < T beside full chunks."""
+    rng = np.random.default_rng(seed)
+    B = sig.shape[0]
+    lens = np.full(B, 512, np.int32)
+    cut = rng.random(B) < 0.5
+    lens[cut] = rng.integers(300, 512, size=int(cut.sum()))
+    sig = sig.copy()
+    for b in np.nonzero(cut)[0]:
+        sig[b, lens[b]:] = 0.0
+    spans = lens.reshape(-1, 4).max(axis=1).repeat(4).astype(np.int32)
+    return sig, lens, spans
+
+
+@pytest.mark.parametrize("key", ["configs[1]", "configs[2]", "configs[3]"])
+def test_pool_at_bench_config_matches_single_engine(key):
+    """The bench's headline mode exactly (bench.py run_batch / config_legs):
+    EnginePool with 3 lanes, the memory-bank kernel on half the CUs (the
+    pool's default bank grid, 128 workgroups walking the chunks), every
+    lane's bank non-temporal, 256 chunks (1024 for --fast beam 5),
+    max_length 100, -min_length 57, the graphs the bench replays (no log-prob
+    dump).  Six distinct batches (every other one ragged: pad-masked chunks,
+    spans < T) go through the pool twice, three calls in flight (greedy:
+    one host thread; beam: one thread per lane, as the bench); every pooled
+    call equals a single engine's bitwise.  The single engine is pinned to
+    the oracle at these sizes by the two tests above."""
+    import threading
+    import torch
+    from nanodecoder_amd.engine import EnginePool
+    enc, mode, B = {"configs[1]": ("transformer", "greedy", 256), "configs[2]": ("nano", "greedy", 256),
+                    "configs[3]": ("transformer", "beam", 1024)}[key]
+    cfg = synth.ModelConfig(encoder_type=enc)
+    W = synth.make_weights(cfg, seed=11, eos_bias=-3.0)
+    S, MINL, beam, lanes = 100, 57, (5 if mode == "beam" else 1), 3
+    inputs = []
+    for k in range(6):
+        sig = synth.synth_chunk_batch(B, 512, seed=500 + k, inject_masks=(mode == "greedy"))
+        if k % 2:
+            inputs.append(_ragged(sig, 900 + k))
+        else:
+            inputs.append((sig, np.full(B, 512, np.int32), np.full(B, 512, np.int32)))
+    keys = ("tokens", "scores") if mode == "greedy" else ("tokens", "scores", "lens", "steps")
+
+    def call(e, inp):
+        sig, ln, sp = inp
+        if mode == "greedy":
+            return e.translate_greedy(sig, ln, sp, max_len=S, min_len=MINL)
+        return e.translate_beam(sig, ln, sp, beam=beam, n_best=1, max_len=S, min_len=MINL)
+    one = _engine(cfg, W, max_batch=B, max_steps=S, max_beam=beam)
+    exp = [{k: v.cpu() for k, v in call(one, i).items() if k in keys} for i in inputs]
+    one.close()
+    pool = EnginePool(cfg, W, device=0, lanes=lanes, max_batch=B, max_steps=S, max_beam=beam)
+    assert pool.bank_nt_lanes == (0, 1, 2)
+    assert pool.bank_grid == torch.cuda.get_device_properties(0).multi_processor_count // 2
+    dev_in = [tuple(torch.from_numpy(a).cuda() for a in i) for i in inputs]
+    for rnd in range(2):
+        if mode == "greedy":
+            got = [call(pool, i) for i in dev_in]
+            assert [g["lane"] for g in got] == [0, 1, 2] * 2
+            pool.synchronize()
+        else:
+            got = [None] * len(dev_in)
+            cur = torch.cuda.current_stream()
+
+            def lane(i):
+                e = pool.engines[i]
+                with torch.cuda.stream(e.stream):
+                    for k in range(i, len(dev_in), lanes):
+                        got[k] = call(e, dev_in[k])
+            for e in pool.engines:
+                e.stream.wait_stream(cur)
+            th = [threading.Thread(target=lane, args=(i,)) for i in range(lanes)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+            pool.synchronize()
+        torch.cuda.synchronize()
+        for k, (g, e) in enumerate(zip(got, exp)):
+            for name in keys:
+                assert torch.equal(g[name].cpu(), e[name]), (key, rnd, k, name)
+            assert int(g["overflow"].cpu()[0]) == 0
+    pool.close()
+
+
 def test_translator_reads_with_pool_vs_oracle():
     """Translator.translate_reads on an EnginePool (two engine batches in
     flight while the next is packed): identical strings and scores to the
@@ -212,6 +299,42 @@ def test_translator_reads_with_pool_vs_oracle():
         assert np.abs(np.array(got[ri][0]) - np.array(es)).max() < 1e-3, ri
         n += len(chunks)
     assert n > 20
+    pool.close()
+
+
+def test_read_shard_device_frontend_vs_oracle():
+    """configs[4]'s per-rank path (shard.ReadShard, the default device front
+    end): raw synthetic reads -> Translator.stream_raw_reads on a 3-lane
+    EnginePool (every engine batch normalised and windowed on the device, on
+    its call's stream; reads split across engine batches) -> token arrays.
+    Every read's strings equal the oracle's per-read translate on the host
+    front end's chunks, and the sample / chunk / base counts equal the host
+    front-end path's (utils/labelop.py:194-233, translator.py:181-369)."""
+    from nanodecoder_amd import frontend, shard
+    from nanodecoder_amd.engine import EnginePool
+    from nanodecoder_amd.translator import Translator
+    ref = _oracle()
+    cfg = synth.ModelConfig()
+    W = synth.make_weights(cfg, seed=11, eos_bias=-1.0)
+    S, bs = 30, 100
+    pool = EnginePool(cfg, W, device=0, lanes=3, max_batch=8, max_steps=S)
+    opt = types.SimpleNamespace(gpu=0, n_best=1, max_length=S, min_length=4, beam_size=1, batch_size=bs,
+                                engine_max_batch=8)
+    tr = Translator(cfg, None, opt, engine=pool)
+    n = 24
+    lengths = shard.read_lengths(n, seed=9, lo=100, hi=1700)
+    ids = list(range(n))
+    a, pa = shard.ReadShard(tr, batch_size=bs).run(ids, lengths, keep_predictions=True)
+    b, pb = shard.ReadShard(tr, batch_size=bs, frontend="cpu").run(ids, lengths, keep_predictions=True)
+    assert a["frontend"] == "gpu" and b["frontend"] == "cpu"
+    for k in ("samples", "chunks", "bases"):
+        assert a[k] == b[k], k
+    assert pa == pb
+    m = ref.RefModel(cfg, W)
+    for rid in ids:
+        chunks = frontend.window(frontend.normalize(shard.synth_raw(rid, int(lengths[rid])), "median"), 512, 512)
+        _, ep = ref.translate(m, chunks, bs, max_length=S, min_length=4)
+        assert pa[rid] == ep, rid
     pool.close()
 
 

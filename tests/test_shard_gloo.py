@@ -51,6 +51,33 @@ class FakeTranslator:
         for ri, r in enumerate(reads):
             yield ri, [([0.0], [[4] * (len(c) % 7) + [3, 5]]) for c in r]
 
+    def stream_raw_reads(self, raws, batch_size, normalization, L, stride, arrays=False):
+        """The device front end's contract: raw reads in, windowed here;
+        token arrays out (rows padded with EOS past the hypothesis)."""
+        from nanodecoder_amd import frontend
+        assert arrays and normalization == "median"
+        for ri, raw in enumerate(raws):
+            w = frontend.windows(int(raw.size), L, stride)
+            tok = np.full((len(w), 10), 3, np.int32)
+            for j, (_, ln) in enumerate(w):
+                tok[j, : ln % 7] = 4
+                tok[j, ln % 7 + 1] = 5
+            yield ri, tok, np.zeros(len(w), np.float32)
+
+
+def test_read_shard_frontends_agree():
+    """ReadShard's device front-end path (raw reads -> stream_raw_reads) and
+    host path (normalise + window in the producer thread -> stream_reads)
+    count the same samples, chunks and bases and give the same strings."""
+    n = 30
+    lengths = shard.read_lengths(n, seed=4)
+    a, pa = shard.ReadShard(FakeTranslator(None)).run(list(range(n)), lengths, True)
+    b, pb = shard.ReadShard(FakeTranslator(None), frontend="cpu").run(list(range(n)), lengths, True)
+    assert a["frontend"] == "gpu" and b["frontend"] == "cpu"
+    for k in ("samples", "chunks", "bases"):
+        assert a[k] == b[k], k
+    assert pa == pb
+
 
 def _free_port():
     s = socket.socket()
