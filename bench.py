@@ -264,10 +264,10 @@ def kernel_roofline(eng, B, mode, beam, encoder="transformer", alive=None, secon
     (first workgroup start, last workgroup end; Engine.set_kernel_stamps), and
     the mean over the last timed call's launches is the launch duration.
 
-    greedy: the memory-bank context attention (dec_bank_h3_kernel at
+    greedy: the memory-bank context attention (dec_bank_d8_kernel at
       512-sample chunks), bounded by HBM: per launch it streams the B x 512 x
-      256 memory bank once (fp16 hi/lo planes, 4 bytes per element as fp32;
-      + q' in, U out, the signal for the key mask).  Its MFMA view (2
+      256 memory bank once (24-bit digits: 3 bytes per element + one float
+      scale per key row; + q' in, U out, the signal for the key mask).  Its MFMA view (2
       products x 2 x 8 heads x 512 keys x 256 dims per chunk, split-fp16 on
       fp16 MFMAs) is reported beside it.
     beam: the per-layer K/V context attention (dec_ctx_attention_kernel),
@@ -279,10 +279,16 @@ def kernel_roofline(eng, B, mode, beam, encoder="transformer", alive=None, secon
     T, D = 512, 256
     ms = us * 1e-3
     if mode == "greedy":
-        # 512-sample chunks run the split-fp16 form (dec_bank_h3_kernel: the bank as
-        # fp16 hi/lo fragments, same 4 bytes per element); exact fp32 runs the other
-        name = "dec_bank_h3_kernel" if T == 512 else "dec_mem_attention_kernel<8>"
-        nbytes = B * T * D * 4 + B * T * 4 + 2 * B * 8 * D * 4
+        # 512-sample chunks stream the 24-bit digit bank (dec_bank_d8_kernel: 3 bytes per element + a
+        # float scale per key row) or, with ND_BANK_D8=0, the split-fp16 bank (dec_bank_h3_kernel: fp16
+        # hi / lo, 4 bytes per element); exact fp32 runs the fp32 bank kernel
+        form = eng.engines[0].bank_form() if hasattr(eng, "engines") else eng.bank_form()
+        if form == 2:
+            name = "dec_bank_d8_kernel"
+            nbytes = B * T * D * 3 + B * T * 4 + B * 4 + B * T * 4 + 2 * B * 8 * D * 4
+        else:
+            name = "dec_bank_h3_kernel" if form == 1 else "dec_mem_attention_kernel<8>"
+            nbytes = B * T * D * 4 + B * T * 4 + 2 * B * 8 * D * 4
         flops = 2 * 2 * 8 * T * D * B
         tf = flops / (ms * 1e-3) / 1e12
         extra = {"mfma_view": {"algorithmic_flops_per_launch": flops, "achieved": round(tf, 2), "peak": round(SPLIT_PEAK, 1),
@@ -543,7 +549,9 @@ def run_batch(args, world, rank, dev, cfg, W):
         "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None,
-        "dtype": "f32 (fp32 values; products as split-fp16 x3 on fp16 MFMA: 22-bit operands, fp32 accumulate)",
+        "dtype": ("f32 (fp32 values; products as split-fp16 x3 on fp16 MFMA: 22-bit operands, fp32 accumulate; "
+                  "the greedy memory bank as 24-bit fixed point per key row: int8 digit MFMAs summed exactly in "
+                  "int32)"),
         "data": "synthetic reads, random-init weights",
         "config": {"workload": workload(args), "chunks_per_gpu_per_step": args.batch,
                    "global_batch": args.batch * world, "seq_len": 512, "parallelism": f"read-shard x{world}",

@@ -447,6 +447,27 @@ int nd_op_bank_pack_h3(const float* x, const float* ln_g, const float* ln_b, uin
 int nd_op_dec_bank_h3(const float* qp, const uint16_t* bank, const float* signal, const int32_t* span, float pad_val,
                       float* out, int32_t C, int32_t T, int32_t* ovf, int32_t grid, void* stream);
 
+/* 24-bit fixed-point memory bank (the greedy decoder's context attention at
+ * T in (448, 512] by default; ND_BANK_D8=0 keeps the split-fp16 bank; the
+ * same reference lines).  nd_op_bank_pack_d8: x [B*T, 256] row-major -> the
+ * digit bank (B x 512 rows; every row t as 2^e_t times an integer of < 2^22
+ * in three signed 8-bit digit planes, B * 512 * 256 * 3 bytes in the
+ * v_mfma_i32_16x16x64_i8 A-operand fragment order), kscale [B * 512] floats
+ * (2^e_t) and kemax [B] ints (each chunk's largest e_t, biased by 1024);
+ * LayerNorm with ln_g/ln_b when set; rows t >= T zero.  nd_op_dec_bank_d8:
+ * as nd_op_dec_bank_h3 on that bank.  ovf (nullable): set to 1 on a
+ * non-finite operand. */
+int nd_op_bank_pack_d8(const float* x, const float* ln_g, const float* ln_b, void* bank, float* kscale,
+                       int32_t* kemax, int32_t B, int32_t T, int32_t* ovf, void* stream);
+int nd_op_dec_bank_d8(const float* qp, const void* bank, const float* kscale, const int32_t* kemax,
+                      const float* signal, const int32_t* span, float pad_val, float* out, int32_t C, int32_t T,
+                      int32_t* ovf, int32_t grid, void* stream);
+
+/* Which memory bank the context's last greedy call streamed (diagnostics,
+ * the bench's roofline accounting): 0 fp32 bank (or none), 1 split-fp16
+ * (nd_op_dec_bank_h3), 2 24-bit digits (nd_op_dec_bank_d8). */
+int nd_bank_form(nd_ctx* ctx);
+
 /* Decoder context attention (multi_headed_attn.py:142-177): rows r = c*rpc+j
  * of q [C*rpc, d] attend over K at kv[(c*T+t)*ld + koff] and V at +d, keys
  * t < span[c], key mask signal == pad_val; out [C*rpc, d].  q and out are

@@ -1177,6 +1177,10 @@ hipError_t init_kernel_attributes() {
     hipError_t e = init_mem_attributes();
     if (e != hipSuccess) return e;
   }
+  {
+    hipError_t e = init_bank8_attributes();
+    if (e != hipSuccess) return e;
+  }
   return init_gemm_attributes();
 }
 

@@ -1,0 +1,465 @@
+// 24-bit fixed-point memory bank: the greedy decoder's context attention in
+// memory-bank form (kernels.hpp launch_dec_bank_d8) on 3 bytes per bank
+// element instead of the split-fp16 bank's 4 (mem_attention.hip,
+// dec_bank_h3_kernel).  Reference: onmt/modules/multi_headed_attn.py:142-177
+// (scores, mask, softmax, context) with the context K/V projections folded
+// into the query side (W_qk) and the output side (W_vo) as in the h3 form.
+//
+// Bank (bank_pack_d8_kernel, once per call): every key row t of the LN'd
+// encoder output is m_t = 2^e_t A_t with A_t integer, |A_t| < 2^22 (e_t =
+// floor(log2 max|m_t|) - 21), held as three signed 8-bit digits
+// A = a2 2^16 + a1 2^8 + a0 (balanced: a0 = sext8(A), ...).  Error per element
+// <= 2^(e_t - 1) <= 2^-22 max|m_t|.  Layout: 1 KB fragments (chunk, key block
+// kb of 16 keys, dim block db of 64, digit plane), lane l holding key
+// 16 kb + (l & 15), dims 64 db + 16 (l >> 4) .. +15; per key the scale 2^e_t
+// (float) and per chunk max e_t.
+//
+// S = M q'^T on v_mfma_i32_16x16x64_i8: q' of head h is quantised the same
+// way per (chunk, head) in the prologue (sigma_h, digits q2 q1 q0); B1 =
+// [q2 | q1] and B2 = [q0 | 0] over the 16 columns (8 heads each); the four
+// products a2 B1, a2 B2, a1 B1, a0 B1 hold every digit product of weight
+// >= 2^8 (a1 q0 and a0 q0 dropped: <= 2^-22.4 max|m| max|q'| per dim), summed
+// exactly in int32 and combined in fp32 with their power-of-two weights.
+//
+// U = P^T M on f16 MFMAs as in the h3 form, the digits turned into exact f16
+// integers (magic-number conversion) from a per-wave transposed LDS image
+// read by ds_read_b64_tr_b8: one 16x16x32 product per dim block takes
+// [P, P] against [a2 * 2^8 (4 keys), a1 (4 keys)], one 16x16x16 product P
+// against a0 * 2^-8.  P is p * 2^(e_t - e_max + 7) (e_max: the chunk's largest
+// e_t, so <= 2^7 e^6 < 65504) split hi | lo as in the h3 form.
+//
+// 3 bytes per element: 103.9 MB per launch at 256 chunks against 138.9 MB.
+#include "common.hpp"
+#include "kernels.hpp"
+
+namespace nd {
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 d8h2 __attribute__((ext_vector_type(2)));
+typedef _Float16 d8h4 __attribute__((ext_vector_type(4)));
+typedef _Float16 d8h8 __attribute__((ext_vector_type(8)));
+typedef unsigned d8u2 __attribute__((ext_vector_type(2)));
+
+#define B8_NW 8                          // waves per chunk, 64 keys each
+#define B8_KB 32                         // key blocks of 16 per chunk
+#define B8_KPW (B8_KB / B8_NW)           // key blocks per wave
+#define B8_THR 6.0f                      // lazy-rescale threshold (natural log units), as the h3 form
+#define B8_ROW 272                       // bytes per key row of one digit plane in the image (256 + 16)
+#define B8_PLANE (16 * B8_ROW)           // one plane of a key block
+#define B8_IMG 16384                     // bytes per wave: the 3-plane image (13 KB), then its U partial (16 KB)
+#define B8_QD (B8_NW * B8_IMG)           // q' digits [3 planes][8 heads][256 dims]
+#define B8_ZERO (B8_QD + 3 * ND_H * ND_D)  // 16 zero bytes (B2 of columns 8..15)
+#define B8_SIG (B8_ZERO + 16)            // [8 heads] sigma_h * 2^16
+#define B8_ML (B8_SIG + ND_H * 4)        // merge (m, l) [wave][8 heads][2]
+#define B8_FW (B8_ML + B8_NW * 16 * 4)   // merge weights [wave][8 heads], then [8 heads] output scales
+#define B8_LDS (B8_FW + (B8_NW + 1) * ND_H * 4)
+#define B8_EBIAS 1024                    // e_max is stored biased (atomicMax over ints >= 0)
+static_assert(3 * B8_PLANE <= B8_IMG && ND_H * ND_D * 2 * 4 <= B8_IMG, "wave image");
+static_assert(B8_LDS <= 160 * 1024, "LDS");
+
+__device__ __forceinline__ int sext8(int x) { return (x << 24) >> 24; }
+
+// the three balanced digits of an integer |A| < 2^22, as bytes of three words
+__device__ __forceinline__ void digits(int A, int& d2, int& d1, int& d0) {
+  d0 = sext8(A);
+  const int A1 = (A - d0) >> 8;
+  d1 = sext8(A1);
+  d2 = (A1 - d1) >> 8;
+}
+
+// e with 2^21 <= |x| * 2^-e < 2^22 for x = the row / head maximum (0 for 0)
+__device__ __forceinline__ int fix_exp(float mx) {
+  int E = 0;
+  (void)frexpf(mx, &E);
+  return mx > 0.f ? E - 22 : 0;
+}
+
+__device__ __forceinline__ i32x4 mfma_i8(i32x4 a, i32x4 b, i32x4 c) {
+  return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma_d8h32(d8h8 a, d8h8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma_d8h16(d8h4 a, d8h4 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c, 0, 0, 0);
+}
+
+// 4 signed bytes -> 4 exact f16: f16 bits 0x64uu = 1024 + u with u = b + 128
+// (b ^ 0x80), minus 1152 (exact); then the plane weight (exact power of two)
+__device__ __forceinline__ d8h4 d8_cvt(unsigned x, int plane) {
+  const unsigned t = x ^ 0x80808080u;
+  const d8h2 lo = __builtin_bit_cast(d8h2, __builtin_amdgcn_perm(0x64646464u, t, 0x04010400u));
+  const d8h2 hi = __builtin_bit_cast(d8h2, __builtin_amdgcn_perm(0x64646464u, t, 0x04030402u));
+  d8h2 a, b;
+  if (plane == 2) {  // a2 * 2^8
+    const d8h2 k = {(_Float16)1152.0f, (_Float16)1152.0f}, s = {(_Float16)256.0f, (_Float16)256.0f};
+    a = (lo - k) * s;
+    b = (hi - k) * s;
+  } else if (plane == 1) {  // a1
+    const d8h2 k = {(_Float16)1152.0f, (_Float16)1152.0f};
+    a = lo - k;
+    b = hi - k;
+  } else {  // a0 * 2^-8: u / 256 - 4.5 (exact)
+    const d8h2 s = {(_Float16)0.00390625f, (_Float16)0.00390625f}, k = {(_Float16)4.5f, (_Float16)4.5f};
+    a = lo * s - k;
+    b = hi * s - k;
+  }
+  return d8h4{a.x, a.y, b.x, b.y};
+}
+
+// ds_read_b64_tr_b8 (tools/probe_i8.py): per 16-lane group, lane 2q + p
+// supplies the address of row q (0..7), bytes 8p .. 8p + 7 of a 16-byte
+// column run; lane i receives byte i of the 8 rows
+__device__ __forceinline__ d8u2 tr_b8(const char* p) {
+  typedef int v2i __attribute__((ext_vector_type(2)));
+  typedef __attribute__((address_space(3))) v2i lds_v2i;
+  return __builtin_bit_cast(d8u2, __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)p));
+}
+
+template <bool NT>
+__device__ __forceinline__ void bank_d8_chunk(int c, const float* __restrict__ qp, const i32x4* __restrict__ bank,
+                                              const float* __restrict__ kscale, const int* __restrict__ kemax,
+                                              const float* __restrict__ signal, const int* __restrict__ span,
+                                              float pad_val, float* __restrict__ out, int T,
+                                              unsigned long long* stamp, float* __restrict__ dbg, size_t dbg_stride,
+                                              int* ovf, unsigned long long t_entry) {
+  extern __shared__ float lds[];
+  char* lb = reinterpret_cast<char*>(lds);
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int col = lane & 15, g = lane >> 4;
+  char* img = lb + w * B8_IMG;
+  // half block h: key block w + 8 (h >> 1), dim blocks 2 (h & 1) + j (j = 0, 1), planes 2, 1, 0: f[3 j + 2 - pl]
+  auto hload = [&](int h, i32x4(&f)[6]) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const int db = 2 * (h & 1) + i / 3, pl = 2 - i % 3;
+      const i32x4* p = bank + ((((size_t)c * B8_KB + w + B8_NW * (h >> 1)) * 4 + db) * 3 + pl) * 64 + lane;
+      if constexpr (NT)
+        f[i] = __builtin_nontemporal_load(p);
+      else
+        f[i] = *p;
+    }
+  };
+  // q' of head w (4 dims per lane), this lane's key scales (keys 16 (w + 8 kb) + 4 g + i), the signal,
+  // e_max: then the first half blocks
+  const f32x4 qv = ld4(qp + (size_t)c * (ND_H * ND_D) + w * ND_D + 4 * lane);
+  f32x4 ksc[B8_KPW];
+#pragma unroll
+  for (int kb = 0; kb < B8_KPW; ++kb) ksc[kb] = ld4(kscale + (size_t)c * 512 + 16 * (w + B8_NW * kb) + 4 * g);
+  float sg;
+  {
+    const int bkey = 16 * (w + B8_NW * (lane >> 4)) + (lane & 15);  // lane l: row l & 15 of key block w + 8 (l >> 4)
+    sg = signal[(size_t)c * T + min(bkey, T - 1)];
+  }
+  const int emax = kemax[c] - B8_EBIAS;
+  i32x4 F[3][6];
+  // issue order = retire order: q' and the scales first, then half block 0, then 1 (a wait for an
+  // earlier load leaves the later ones in flight)
+  __builtin_amdgcn_sched_barrier(0);
+  hload(0, F[0]);
+  __builtin_amdgcn_sched_barrier(0);
+  hload(1, F[1]);
+  __builtin_amdgcn_sched_barrier(0);
+  stamp_begin_at(stamp, t_entry);
+  const int L = min(span[c], T);
+  // q' of head w in digits (every wave one head)
+  {
+    const float qm = wave_max(absmax4(qv));
+    if (!(qm <= 3.0e38f) && ovf != nullptr) ovf[0] = 1;  // non-finite q'
+    const int es = fix_exp(qm);
+    unsigned pw[3] = {0u, 0u, 0u};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int d2, d1, d0;
+      digits((int)rintf(ldexpf(qv[j], -es)), d2, d1, d0);
+      pw[2] |= (unsigned)(d2 & 255) << (8 * j);
+      pw[1] |= (unsigned)(d1 & 255) << (8 * j);
+      pw[0] |= (unsigned)(d0 & 255) << (8 * j);
+    }
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<unsigned*>(lb + B8_QD + pl * ND_H * ND_D + w * ND_D + 4 * lane) = pw[pl];
+    if (lane == 0) reinterpret_cast<float*>(lb + B8_SIG)[w] = ldexpf(1.0f, es + 16);
+    if (w == 0 && lane < 4) reinterpret_cast<unsigned*>(lb + B8_ZERO)[lane] = 0u;
+  }
+  lds_barrier();  // LDS only: the bank loads stay in flight
+  // B operands: column col = head col & 7; B1 = q2 (col < 8) | q1, B2 = q0 (col < 8) | 0; dims 64 db + 16 g ..
+  i32x4 qb1[4], qb2[4];
+  {
+    const char* q1p = lb + B8_QD + (col < 8 ? 2 : 1) * ND_H * ND_D + (col & 7) * ND_D + 16 * g;
+    const char* q2p = col < 8 ? lb + B8_QD + (col & 7) * ND_D + 16 * g : lb + B8_ZERO;
+    const int q2s = col < 8 ? 64 : 0;
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      qb1[db] = *reinterpret_cast<const i32x4*>(q1p + 64 * db);
+      qb2[db] = *reinterpret_cast<const i32x4*>(q2p + q2s * db);
+    }
+  }
+  const float sgm = reinterpret_cast<const float*>(lb + B8_SIG)[col & 7];
+  // digit-product weights (x 2^-16, folded into sgm): X1 = a2 [q2 | q1], X2 = a2 [q0 | 0], X3 = a1 [q2 | q1],
+  // X4 = a0 [q2 | q1]
+  const float w1 = col < 8 ? 65536.0f : 256.0f, w3 = col < 8 ? 256.0f : 1.0f, w4 = col < 8 ? 1.0f : 0.00390625f;
+  const float kp = ldexpf(1.0f, min(7 - emax, 127));  // P scale: p 2^(e_t - e_max + 7)
+  const unsigned long long padm = __ballot(sg == pad_val);
+  // transposed reads: lane 2q + p of its group supplies row q (keys 4 g + (q & 3)); planes (a2 | a1) at
+  // dim block k, or a0 at dim blocks (k | k + 1)
+  const int q8 = (lane & 15) >> 1, p8 = lane & 1;
+  const char* rb1 = img + (q8 < 4 ? 2 : 1) * B8_PLANE + (4 * g + (q8 & 3)) * B8_ROW + 8 * p8;
+  const char* rb3 = img + (4 * g + (q8 & 3)) * B8_ROW + 8 * p8 + (q8 < 4 ? 0 : 16);
+  char* wimg = img + col * B8_ROW + 16 * g;  // this lane's fragment row in the image
+
+  f32x4 ua[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) ua[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+
+#pragma unroll
+  for (int kb = 0; kb < B8_KPW; ++kb) {
+    i32x4 X1 = {0, 0, 0, 0}, X2 = X1, X3 = X1, X4 = X1;
+#pragma unroll
+    for (int part = 0; part < 2; ++part) {
+      const int h = 2 * kb + part;
+      i32x4(&f)[6] = F[h % 3];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int db = 2 * part + j;
+        X1 = mfma_i8(f[3 * j], qb1[db], X1);
+        X2 = mfma_i8(f[3 * j], qb2[db], X2);
+        X3 = mfma_i8(f[3 * j + 1], qb1[db], X3);
+        X4 = mfma_i8(f[3 * j + 2], qb1[db], X4);
+      }
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const int db = 2 * part + i / 3, pl = 2 - i % 3;
+        *reinterpret_cast<i32x4*>(wimg + pl * B8_PLANE + 64 * db) = f[i];
+      }
+      __builtin_amdgcn_sched_barrier(0);  // the next loads reuse f's registers
+      if (h + 2 < 2 * B8_KPW) hload(h + 2, F[(h + 2) % 3]);
+    }
+    // ---- scores: columns h and h + 8 hold the high and low digit products of head h
+    f32x4 s;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s[i] = (float)X1[i] * w1 + (float)X2[i] + (float)X3[i] * w3 + (float)X4[i] * w4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s[i] = (s[i] + dpp_mov<0x128>(s[i])) * (ksc[kb][i] * sgm);
+    const int kbase = 16 * (w + B8_NW * kb) + 4 * g;  // key of row i
+    const unsigned pb = (unsigned)(padm >> (16 * kb + 4 * g)) & 0xFu;
+    float gm = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      s[i] = kbase + i < L ? (((pb >> i) & 1u) ? ND_MASK_FILL : s[i]) : -INFINITY;
+      gm = fmaxf(gm, s[i]);
+    }
+    if (dbg && col == 0) {  // -attn_debug: head 0's scores
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (kbase + i < L) dbg[(size_t)c * dbg_stride + kbase + i] = s[i];
+    }
+    gm = xor32_max(xor16_max(gm));
+    if (__any(gm > m + B8_THR)) {
+      const float nm = fmaxf(m, gm);
+      const float sc = nm == m ? 1.f : __expf(m - nm);
+      m = nm;
+      l *= sc;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float si = __shfl(sc, (lane & 48) | (4 * (g & 1) + i));
+#pragma unroll
+        for (int k = 0; k < 16; ++k) ua[k][i] *= si;
+      }
+    }
+    f32x4 p;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) p[i] = s[i] == -INFINITY ? 0.f : __expf(s[i] - m);
+    l += (p[0] + p[1]) + (p[2] + p[3]);
+    // ---- A operand of U: row col = (P plane col >> 3, head col & 7), keys 4 g .. 4 g + 3
+    d8h4 pa;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float x = p[i] * (ksc[kb][i] * kp);
+      const _Float16 hi = (_Float16)x;
+      pa[i] = col < 8 ? hi : (_Float16)(x - (float)hi);
+    }
+    const d8h8 pa8 = {pa[0], pa[1], pa[2], pa[3], pa[0], pa[1], pa[2], pa[3]};
+    // ---- U += P^T M': dim blocks (2 kp, 2 kp + 1) of 16 dims, dims 16 k + col
+#pragma unroll
+    for (int kp2 = 0; kp2 < 8; ++kp2) {
+      const d8u2 r1 = tr_b8(rb1 + 32 * kp2), r2 = tr_b8(rb1 + 32 * kp2 + 16), r3 = tr_b8(rb3 + 32 * kp2);
+      const d8h4 b1a = d8_cvt(r1.x, 2), b1b = d8_cvt(r1.y, 1), b2a = d8_cvt(r2.x, 2), b2b = d8_cvt(r2.y, 1);
+      const d8h8 b1 = {b1a[0], b1a[1], b1a[2], b1a[3], b1b[0], b1b[1], b1b[2], b1b[3]};
+      const d8h8 b2 = {b2a[0], b2a[1], b2a[2], b2a[3], b2b[0], b2b[1], b2b[2], b2b[3]};
+      ua[2 * kp2] = mfma_d8h32(pa8, b1, ua[2 * kp2]);
+      ua[2 * kp2] = mfma_d8h16(pa, d8_cvt(r3.x, 0), ua[2 * kp2]);
+      ua[2 * kp2 + 1] = mfma_d8h32(pa8, b2, ua[2 * kp2 + 1]);
+      ua[2 * kp2 + 1] = mfma_d8h16(pa, d8_cvt(r3.y, 0), ua[2 * kp2 + 1]);
+    }
+  }
+
+  // ---- merge the 8 waves (as dec_bank_h3_kernel): unmerged U^T fragments to the wave's own image, (m, l)
+  //      beside, wave 0 turns them into merge weights and the output scale 2^(e_max + 1) / den
+  l = xor32_sum(xor16_sum(l));
+  float* ml = reinterpret_cast<float*>(lb + B8_ML);  // [wave][8 heads][2]
+  {
+    f32x4* red = reinterpret_cast<f32x4*>(img);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) red[k * 64 + lane] = ua[k];
+  }
+  if (lane < 8) {
+    ml[(w * ND_H + lane) * 2] = m;
+    ml[(w * ND_H + lane) * 2 + 1] = l;
+  }
+  __syncthreads();
+  float* fw = reinterpret_cast<float*>(lb + B8_FW);  // [wave][8 heads] weights, then [8 heads] output scales
+  if (w == 0) {
+    const int v = lane >> 3, hh = lane & 7;
+    const float mv = ml[(v * ND_H + hh) * 2], lv = ml[(v * ND_H + hh) * 2 + 1];
+    float M = fmaxf(mv, __shfl_xor(mv, 8, 64));
+    M = fmaxf(M, __shfl_xor(M, 16, 64));
+    M = fmaxf(M, __shfl_xor(M, 32, 64));
+    const float f = mv == -INFINITY ? 0.f : __expf(mv - M);  // waves that owned no key
+    float den = f * lv;
+    den += __shfl_xor(den, 8, 64);
+    den += __shfl_xor(den, 16, 64);
+    den += __shfl_xor(den, 32, 64);
+    fw[v * ND_H + hh] = f;
+    if (v == 0) fw[B8_NW * ND_H + hh] = den > 0.f ? __builtin_amdgcn_rcpf(den) * ldexpf(1.0f, emax + 1) : 0.f;
+  }
+  lds_barrier();
+#pragma unroll
+  for (int e = threadIdx.x; e < 512; e += B8_NW * 64) {
+    const int hs = e >> 8, d = e & 255, k = d >> 4, cl = d & 15;
+    const int lh = k * 64 + cl + 16 * hs, ll = k * 64 + cl + 16 * (2 + hs);  // P hi rows g = hs, lo rows g = 2 + hs
+    f32x4 num = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int v = 0; v < B8_NW; ++v) {
+      const f32x4* red = reinterpret_cast<const f32x4*>(lb + v * B8_IMG);
+      num += ld4(fw + v * ND_H + 4 * hs) * (red[lh] + red[ll]);
+    }
+    num *= ld4(fw + B8_NW * ND_H + 4 * hs);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int n = (4 * hs + i) * ND_D + d;
+      out[pk(c, n & ~3, ND_H * ND_D) + (n & 3)] = num[i];
+    }
+  }
+}
+
+template <bool NT, bool WALK>
+__global__ void __launch_bounds__(B8_NW * 64)
+dec_bank_d8_kernel(const float* __restrict__ qp, const i32x4* __restrict__ bank, const float* __restrict__ kscale,
+                   const int* __restrict__ kemax, const float* __restrict__ signal, const int* __restrict__ span,
+                   float pad_val, float* __restrict__ out, int T, int C, unsigned long long* stamp,
+                   float* __restrict__ dbg, size_t dbg_stride, int* ovf) {
+  const unsigned long long t_entry = wall_clock64();
+  if constexpr (WALK) {
+    for (int c = blockIdx.x; c < C; c += gridDim.x) {
+      if (c != (int)blockIdx.x) lds_barrier();  // the previous chunk's merge reads of LDS are done
+      bank_d8_chunk<NT>(c, qp, bank, kscale, kemax, signal, span, pad_val, out, T, stamp, dbg, dbg_stride, ovf,
+                        t_entry);
+    }
+  } else {
+    bank_d8_chunk<NT>(blockIdx.x, qp, bank, kscale, kemax, signal, span, pad_val, out, T, stamp, dbg, dbg_stride, ovf,
+                      t_entry);
+  }
+  stamp_end(stamp);
+}
+
+// Encoder output -> the 24-bit digit bank: one workgroup per (chunk, key
+// block of 16 rows): LayerNorm (as bank_pack_h3_kernel), per row the
+// exponent e_t and the digits into LDS, then the 12 fragments as coalesced
+// 1 KB stores; the row scales 2^e_t and the chunk's largest e_t (atomicMax,
+// biased; kemax zeroed by the caller).  Rows t >= T are zero.
+__global__ void __launch_bounds__(256)
+bank_pack_d8_kernel(const float* __restrict__ x, const float* __restrict__ gm, const float* __restrict__ bt,
+                    i32x4* __restrict__ bank, float* __restrict__ kscale, int* __restrict__ kemax, int T, int* ovf) {
+  __shared__ __attribute__((aligned(16))) unsigned char dg[3][16][ND_D];
+  const int c = blockIdx.x / B8_KB, kb = blockIdx.x % B8_KB, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int emx = B8_EBIAS - 126;  // a chunk of all-zero rows: e_max = -126 (its P scale stays finite)
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int r = wv + 4 * rr, t = 16 * kb + r;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (t < T) {
+      v = ld4(x + ((size_t)c * T + t) * ND_D + lane * 4);
+      if (gm) {
+        const float mu = wave_sum(v.x + v.y + v.z + v.w) * (1.0f / ND_D);
+        const f32x4 d = v - mu;
+        const float var = wave_sum(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w) * (1.0f / ND_D);
+        v = d * ln_rsqrt(var + ND_LN_EPS) * ld4(gm + lane * 4) + ld4(bt + lane * 4);
+      }
+    }
+    const float mx = wave_max(absmax4(v));
+    if (!(mx <= 3.0e38f) && ovf != nullptr) ovf[0] = 1;  // non-finite encoder output
+    // a zero row (t >= T) gets the smallest scale: it never sets the chunk's e_max, whose P scale
+    // 2^(e_t - e_max + 7) would otherwise push every real row's P into the fp16 subnormals
+    const int e = mx > 0.f ? fix_exp(mx) : -126;
+    unsigned pw[3] = {0u, 0u, 0u};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int d2, d1, d0;
+      digits((int)rintf(ldexpf(v[j], -e)), d2, d1, d0);
+      pw[2] |= (unsigned)(d2 & 255) << (8 * j);
+      pw[1] |= (unsigned)(d1 & 255) << (8 * j);
+      pw[0] |= (unsigned)(d0 & 255) << (8 * j);
+    }
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<unsigned*>(&dg[pl][r][4 * lane]) = pw[pl];
+    if (lane == 0) kscale[(size_t)c * 512 + t] = ldexpf(1.0f, e);
+    if (mx > 0.f) emx = max(emx, e + B8_EBIAS);
+  }
+  if (lane == 0) atomicMax(kemax + c, emx);
+  __syncthreads();
+  // fragment (db, pl): lane ln holds key ln & 15, dims 64 db + 16 (ln >> 4) .. +15
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int item = threadIdx.x + 256 * j, fr = item >> 6, ln = item & 63, db = fr / 3, pl = fr % 3;
+    bank[((((size_t)c * B8_KB + kb) * 4 + db) * 3 + pl) * 64 + ln] =
+        *reinterpret_cast<const i32x4*>(&dg[pl][ln & 15][64 * db + 16 * (ln >> 4)]);
+  }
+}
+
+hipError_t launch_bank_pack_d8(const float* x, const float* ln_g, const float* ln_b, void* bank, float* kscale,
+                               int* kemax, int B, int T, int* ovf, hipStream_t s) {
+  if (T < 1 || T > 512 || B < 1 || !bank || !kscale || !kemax) return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(kemax, 0, (size_t)B * sizeof(int), s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(bank_pack_d8_kernel, dim3(B * B8_KB), dim3(256), 0, s, x, ln_g, ln_b,
+                     reinterpret_cast<i32x4*>(bank), kscale, kemax, T, ovf);
+  return hipGetLastError();
+}
+
+hipError_t launch_dec_bank_d8(const float* qp, const void* bank, const float* kscale, const int* kemax,
+                              const float* signal, const int* span, float pad_val, float* out, int C, int T,
+                              hipStream_t s, unsigned long long* stamp, float* attn_dbg, size_t dbg_stride, int* ovf,
+                              bool nt, int grid) {
+  if (T < 1 || T > 512 || C < 1 || grid < 0 || !bank || !kscale || !kemax) return hipErrorInvalidValue;
+  const int G = grid > 0 ? std::min(C, grid) : C;
+#define ND_BANK8_GO(N, W)                                                                                         \
+  hipLaunchKernelGGL((dec_bank_d8_kernel<N, W>), dim3(G), dim3(B8_NW * 64), B8_LDS, s, qp,                       \
+                     reinterpret_cast<const i32x4*>(bank), kscale, kemax, signal, span, pad_val, out, T, C, stamp,  \
+                     attn_dbg, dbg_stride, ovf)
+  if (G < C) {
+    if (nt)
+      ND_BANK8_GO(true, true);
+    else
+      ND_BANK8_GO(false, true);
+  } else if (nt) {
+    ND_BANK8_GO(true, false);
+  } else {
+    ND_BANK8_GO(false, false);
+  }
+#undef ND_BANK8_GO
+  return hipGetLastError();
+}
+
+hipError_t init_bank8_attributes() {
+  const void* fns[] = {(const void*)dec_bank_d8_kernel<false, false>, (const void*)dec_bank_d8_kernel<true, false>,
+                       (const void*)dec_bank_d8_kernel<false, true>, (const void*)dec_bank_d8_kernel<true, true>};
+  for (const void* f : fns) {
+    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, B8_LDS);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+}  // namespace nd

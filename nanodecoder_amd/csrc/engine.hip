@@ -172,6 +172,10 @@ struct nd_ctx {
   float* mem_p = nullptr;                 // memory bank [B * T, 256] row-major (LN'd encoder output)
   const float* mem = nullptr;             // the bank the decoder reads: mem_p, or x (NanoEncoder)
   bool bank_h3 = false;                   // mem_p holds the split-fp16 fragment bank (dec_bank_h3_kernel)
+  bool bank_d8 = false;                   // ... or the 24-bit digit bank (dec_bank_d8_kernel; bank8.hip)
+  float* bank_ks = nullptr;               // digit bank: per-row scales 2^e_t [B * 512]
+  int* bank_em = nullptr;                 // digit bank: per-chunk max e_t (biased) [B]
+  int last_bank_form = 0;                 // nd_bank_form
   float *dqk = nullptr, *dU = nullptr;    // [R, 8*256] P16 (memory-bank path)
   // average self-attention step buffers (P16): xn, avg (+ its row stats), the
   // average_layer hidden, a = FFN(avg), the gate pre-activations [R, 512]
@@ -388,6 +392,12 @@ static int alloc_workspaces(nd_ctx* c) {
   WS(c->big, B * T * std::max(F, 3 * D));
   WS(c->ctxkv, B * T * Ld * 2 * D);
   WS(c->mem_p, B * T * D);
+  WS(c->bank_ks, B * 512);
+  {
+    float* em = nullptr;
+    WS(em, B);
+    c->bank_em = reinterpret_cast<int*>(em);
+  }
   WS(c->x_part, B * T * ND_PART_LD * 2);
   WS(c->y_part, B * T * ND_PART_LD * 2);
   WS(c->dx_part, R * ND_PART_LD * 2);
@@ -569,15 +579,16 @@ static bool enc_qkv_folded(const nd_ctx* c, const EncLayer& next) {
 }
 
 // layer 0's attention in closed form (launch_enc_attention_rank2): no q | k | v
-// rows at all for layer 0.  OFF by default, opt-in with ND_ENC_ATTN0=1: with a
-// second engine's decoder GEMMs running beside it on the GPU (EnginePool), whole
-// chunks of its output came out different (max |d memory| ~0.2,
-// tools/rank2_probe.py); alone it matches the oracle.  Cause not found (not the
-// LDS size granule, not hardware-queue sharing: DESIGN.md section 5)
+// rows at all for layer 0 (encoder 3.65 -> 3.40 ms per 256-chunk call).  On by
+// default since its LDS is exactly 64 KB: the round-3 layout (67,584 B, wave 7's
+// E[y] / E[r] rows read and written past byte 65,536 by ds_read2 / ds_write2)
+// returned wrong chunks whenever another engine's decoder GEMMs shared the CU;
+// every layout whose accesses stay below 65,536 is clean (tools/r2_lds.sh,
+// DESIGN.md section 5).  ND_ENC_ATTN0=0 keeps the attention kernel for layer 0.
 static bool enc_attn0_rank2(const nd_ctx* c) {
   static const bool on = [] {
     const char* e = getenv("ND_ENC_ATTN0");
-    return e && atoi(e) == 1;
+    return !(e && atoi(e) == 0);
   }();
   return on && c->eq_ready && c->eq_coef != nullptr;
 }
@@ -714,15 +725,28 @@ static bool use_memory_bank(nd_ctx* c, int rpc) { return c->ctx_path == 0 && rpc
 // exact, T, rpc, encoder type).  Set on the host before every call's graphs
 // run or are captured: a replayed encoder graph does not re-enter
 // enqueue_memory, but the step graphs captured after it read these fields.
+// the 24-bit digit bank instead of the split-fp16 one (bank8.hip); ND_BANK_D8=0
+// keeps the split-fp16 bank
+static bool use_bank_d8() {
+  static const bool on = [] {
+    const char* e = getenv("ND_BANK_D8");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
 static void set_memory_view(nd_ctx* c, int T, int rpc) {
   c->bank_h3 = false;
+  c->bank_d8 = false;
   c->mem = nullptr;
   if (!use_memory_bank(c, rpc)) return;
   const bool tf = c->cfg.encoder_type == ND_ENC_TRANSFORMER;
   // 512-sample chunks: the split-fp16 fragment bank (LN'd for the transformer,
   // the NanoEncoder's output as it stands)
   c->bank_h3 = !c->exact && nd::bank_h3_eligible(T, c->cfg.max_src_len);
+  c->bank_d8 = c->bank_h3 && use_bank_d8();
   c->mem = (c->bank_h3 || tf) ? c->mem_p : c->x;  // the NanoEncoder's fp32 output is the bank as it stands
+  c->last_bank_form = c->bank_d8 ? 2 : c->bank_h3 ? 1 : 0;
 }
 
 // done: per chunk, nonzero = finished (--fast beam; null otherwise): its rows'
@@ -778,7 +802,10 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
       const int HD = ND_H * D;
       // q' row-major for the split-fp16 bank kernel (one row per chunk), P16 for the fp32 one
       LCHK(dg(c->dq1, D, L.pwqk, HD, D, L.bqk, c->dqk, HD).ln(c->dq1_part, pnq).c_rowmajor(c->bank_h3).run(s));
-      if (c->bank_h3)
+      if (c->bank_d8)
+        LCHK(nd::launch_dec_bank_d8(c->dqk, c->mem_p, c->bank_ks, c->bank_em, c->sig, c->span, (float)c->cfg.pad_idx,
+                                    c->dU, C, T, s, stamp, dbg, dbg_stride, c->ovf, c->bank_nt, c->bank_grid));
+      else if (c->bank_h3)
         LCHK(nd::launch_dec_bank_h3(c->dqk, reinterpret_cast<const uint16_t*>(c->mem_p), c->sig, c->span,
                                     (float)c->cfg.pad_idx, c->dU, C, T, s, stamp, dbg, dbg_stride, c->ovf,
                                     c->bank_nt, c->bank_grid));
@@ -804,6 +831,9 @@ static hipError_t enqueue_memory(nd_ctx* c, int B, int T, int rpc, hipStream_t s
   set_memory_view(c, T, rpc);
   if (!use_memory_bank(c, rpc)) return enqueue_ctxkv(c, B, T, s);
   const bool tf = c->cfg.encoder_type == ND_ENC_TRANSFORMER;
+  if (c->bank_d8)
+    return nd::launch_bank_pack_d8(c->x, tf ? c->enc_ln_g : nullptr, tf ? c->enc_ln_b : nullptr, c->mem_p, c->bank_ks,
+                                   c->bank_em, B, T, c->ovf, s);
   if (c->bank_h3)
     return nd::launch_bank_pack_h3(c->x, tf ? c->enc_ln_g : nullptr, tf ? c->enc_ln_b : nullptr,
                                    reinterpret_cast<uint16_t*>(c->mem_p), B, T, c->ovf, s);
@@ -1604,7 +1634,7 @@ static const struct {
                  {"ND_HEAD_FUSE", 1},  {"ND_LSTM_F32", 0},     {"ND_LSTM_LIBM", 0},     {"ND_LSTM_SEQ", 4},
                  {"ND_ENC_ATTN_NQ", 2}, {"ND_ENC_ATTN_GRID", 0}, {"ND_ENC_ATTN_F32", 0}, {"ND_SELF_XCD", 1},
                  {"ND_ENC_WO", 1},     {"ND_ENC_QKV0", 1},
-                 {"ND_ENC_QKV", 1},    {"ND_ENC_ATTN0", 0},   {"ND_SELF_NW8", 1}};
+                 {"ND_ENC_QKV", 1},    {"ND_ENC_ATTN0", 1},   {"ND_SELF_NW8", 1},     {"ND_BANK_D8", 1}};
 
 int nd_switches(char* buf, int32_t len) {
   std::string out;
@@ -1919,6 +1949,29 @@ int nd_op_dec_bank_h3(const float* qp, const uint16_t* bank, const float* signal
   if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("dec_bank_h3: ") + hipGetErrorString(e));
   return ND_OK;
 }
+
+int nd_op_bank_pack_d8(const float* x, const float* ln_g, const float* ln_b, void* bank, float* kscale,
+                       int32_t* kemax, int32_t B, int32_t T, int32_t* ovf, void* stream) {
+  if (!x || !bank || !kscale || !kemax || (ln_g == nullptr) != (ln_b == nullptr))
+    return fail(ND_ERR_ARG, "bank_pack_d8: bad arguments");
+  hipError_t e = nd::launch_bank_pack_d8(x, ln_g, ln_b, bank, kscale, kemax, B, T, ovf, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("bank_pack_d8: ") + hipGetErrorString(e));
+  return ND_OK;
+}
+
+int nd_op_dec_bank_d8(const float* qp, const void* bank, const float* kscale, const int32_t* kemax,
+                      const float* signal, const int32_t* span, float pad_val, float* out, int32_t C, int32_t T,
+                      int32_t* ovf, int32_t grid, void* stream) {
+  if (int rc = ensure_attributes()) return rc;
+  if (!qp || !bank || !kscale || !kemax || !signal || !span || !out || grid < 0)
+    return fail(ND_ERR_ARG, "dec_bank_d8: bad arguments");
+  hipError_t e = nd::launch_dec_bank_d8(qp, bank, kscale, kemax, signal, span, pad_val, out, C, T,
+                                        (hipStream_t)stream, nullptr, nullptr, 0, ovf, false, grid);
+  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("dec_bank_d8: ") + hipGetErrorString(e));
+  return ND_OK;
+}
+
+int nd_bank_form(nd_ctx* c) { return c ? c->last_bank_form : 0; }
 
 int nd_op_dec_ctx_attention(const float* q, const float* kv, int32_t ld, int32_t koff, const float* signal,
                             const int32_t* span, float pad_val, float* out, int32_t C, int32_t rpc, int32_t T,

@@ -101,6 +101,11 @@ class Engine:
         _lib.check(self._L.nd_set_bank_grid(self._h, int(workgroups)), "nd_set_bank_grid")
         self.bank_grid = int(workgroups)
 
+    def bank_form(self) -> int:
+        """The memory bank the last greedy call streamed (nd_bank_form): 0 fp32 (or none), 1 split-fp16,
+        2 24-bit digits."""
+        return int(self._L.nd_bank_form(self._h))
+
     def set_timing(self, on: bool):
         _lib.check(self._L.nd_set_timing(self._h, int(on)), "nd_set_timing")
 
@@ -623,6 +628,34 @@ def op_dec_bank_h3(qp, bank, signal, span, pad_val, out=None, ovf=None, grid=0):
     s = ctypes.c_void_p(torch.cuda.current_stream(qp.device).cuda_stream)
     _lib.check(_lib.lib().nd_op_dec_bank_h3(_ptr(qp), _ptr(bank), _ptr(signal), _ptr(span), float(pad_val),
                                             _ptr(out), C, T, _ptr(ovf), int(grid), s), "nd_op_dec_bank_h3")
+    return out
+
+
+def op_bank_pack_d8(x, B, T, ln_g=None, ln_b=None, ovf=None):
+    """24-bit digit bank (nd_op_bank_pack_d8): x [B*T, 256] -> (digits uint8
+    [B * 512 * 256 * 3], row scales [B * 512], chunk max exponents [B] int32)."""
+    dev = x.device
+    bank = torch.empty(B * 512 * 256 * 3, dtype=torch.uint8, device=dev)
+    ks = torch.empty(B * 512, dtype=torch.float32, device=dev)
+    em = torch.empty(B, dtype=torch.int32, device=dev)
+    s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    _lib.check(_lib.lib().nd_op_bank_pack_d8(_ptr(x), _ptr(ln_g), _ptr(ln_b), _ptr(bank), _ptr(ks), _ptr(em), B, T,
+                                             _ptr(ovf), s), "nd_op_bank_pack_d8")
+    return bank, ks, em
+
+
+def op_dec_bank_d8(qp, bank, signal, span, pad_val, out=None, ovf=None, grid=0):
+    """Memory-bank context attention on the 24-bit digit bank (nd_op_dec_bank_d8):
+    qp [C, 2048] row-major, bank = op_bank_pack_d8's triple, T in (448, 512];
+    returns U [C16, 2048] packed."""
+    C, T = signal.shape
+    digits, ks, em = bank
+    if out is None:
+        out = torch.empty((C + 15) // 16 * 16, qp.shape[1], dtype=torch.float32, device=qp.device)
+    s = ctypes.c_void_p(torch.cuda.current_stream(qp.device).cuda_stream)
+    _lib.check(_lib.lib().nd_op_dec_bank_d8(_ptr(qp), _ptr(digits), _ptr(ks), _ptr(em), _ptr(signal), _ptr(span),
+                                            float(pad_val), _ptr(out), C, T, _ptr(ovf), int(grid), s),
+               "nd_op_dec_bank_d8")
     return out
 
 

@@ -5,6 +5,8 @@ tokens identical.  The only allowed token difference is a genuine near-tie in
 the oracle (top-2 log-prob margin < 1e-4), after which that row's history
 diverges and is not compared further.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -346,6 +348,79 @@ def test_bank_h3_vs_fp64(T, ln, grid):
             want = (p / p.sum()) @ M
             err = np.abs(got[c, h * 256:(h + 1) * 256] - want).max()
             assert err < 2e-5 * max(1.0, np.abs(want).max()), (c, h, L, err)
+
+
+@pytest.mark.parametrize("T,ln,grid", [(512, True, 0), (480, False, 0), (449, True, 0), (512, True, 5),
+                                       (512, False, 1)])
+def test_bank_d8_vs_fp64(T, ln, grid):
+    """24-bit digit-bank attention (bank_pack_d8 + dec_bank_d8_kernel, the
+    greedy path at 512-sample chunks) against an fp64 softmax(q' M^T) M per
+    head, on the cases of test_bank_h3_vs_fp64 (ragged spans, pad-masked keys,
+    an all-masked chunk, running-maximum rescales) plus rows of very
+    different magnitude (per-row exponents 2^e_t far below the chunk's
+    largest) and a head of q' a thousand times the others (per-head digit
+    scales).  Tolerance: 2e-5 relative to the output's magnitude, as the
+    split-fp16 bank (digits carry 22-23 bits per row)."""
+    from nanodecoder_amd.engine import op_bank_pack_d8, op_dec_bank_d8, unpack_p16
+    rng = np.random.default_rng(7)
+    C, PAD = 12, 1.0
+    spans = np.array([T, 1, 64, 65, 16, 17, 8, T, T - 3, 130, 300, T], np.int32)
+    sig = rng.standard_normal((C, T)).astype(np.float32)
+    sig[2, ::5] = PAD                      # pad-masked keys
+    sig[7, :] = PAD                        # every key masked -> uniform over the span
+    x = rng.standard_normal((C * T, 256)).astype(np.float32)
+    q = (rng.standard_normal((C, 2048)) * 0.3).astype(np.float32)
+    q[11] *= 8.0                           # scores spread ~+-50: running-maximum rescales
+    x[11 * T + 400] *= 4.0                 # a late key far above the first blocks' maximum
+    x[3 * T: 4 * T: 3] *= 1e-3             # rows of very different magnitude in one chunk
+    x[9 * T + 7] = 0.0                     # an all-zero row
+    q[5, 3 * 256:4 * 256] *= 1e3           # one head's q' far above the others
+    q[6, 5 * 256:6 * 256] = 0.0            # a zero head
+    g = (rng.random(256) + 0.5).astype(np.float32)
+    b = (rng.standard_normal(256) * 0.1).astype(np.float32)
+    dev = torch.device("cuda", 0)
+    xt = torch.from_numpy(x).to(dev)
+    ovf = torch.zeros(1, dtype=torch.int32, device=dev)
+    if ln:
+        bank = op_bank_pack_d8(xt, C, T, torch.from_numpy(g).to(dev), torch.from_numpy(b).to(dev), ovf=ovf)
+        mu = x.mean(1, keepdims=True)
+        var = ((x - mu) ** 2).mean(1, keepdims=True)
+        xm = ((x - mu) / np.sqrt(var + 1e-6) * g + b).astype(np.float64)
+    else:
+        bank = op_bank_pack_d8(xt, C, T, ovf=ovf)
+        xm = x.astype(np.float64)
+    out = op_dec_bank_d8(torch.from_numpy(q).to(dev), bank, torch.from_numpy(sig).to(dev),
+                         torch.from_numpy(spans).to(dev), PAD, ovf=ovf, grid=grid)
+    got = unpack_p16(out, C).cpu().numpy()
+    assert int(ovf.item()) == 0
+    for c in range(C):
+        L = int(spans[c])
+        M = xm[c * T: c * T + L]
+        for h in range(8):
+            s = M @ q[c, h * 256:(h + 1) * 256].astype(np.float64)
+            s[sig[c, :L] == PAD] = -1e18
+            p = np.exp(s - s.max())
+            want = (p / p.sum()) @ M
+            err = np.abs(got[c, h * 256:(h + 1) * 256] - want).max()
+            assert err < 2e-5 * max(1.0, np.abs(want).max()), (c, h, L, err)
+
+
+def test_engine_reports_bank_form():
+    """A greedy call at 512-sample chunks streams the 24-bit digit bank by
+    default (nd_bank_form 2; ND_BANK_D8=0: the split-fp16 bank, 1), exact
+    fp32 the fp32 bank (0).  The digit bank's end-to-end parity is the golden
+    and config tests, which run on it."""
+    cfg = synth.ModelConfig()
+    W = synth.make_weights(cfg, seed=11, eos_bias=-3.0)
+    sig = synth.synth_chunk_batch(8, 512, seed=5)
+    lens = np.full(8, 512, np.int32)
+    eng = _engine(cfg, W, max_batch=8, max_steps=20)
+    eng.translate_greedy(sig, lens, lens, max_len=20)
+    assert eng.bank_form() == (1 if os.environ.get("ND_BANK_D8") == "0" else 2)
+    eng.set_exact_fp32(True)
+    eng.translate_greedy(sig, lens, lens, max_len=20)
+    assert eng.bank_form() == 0
+    eng.close()
 
 
 # ----------------------------------------------------------------- golden

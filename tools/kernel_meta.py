@@ -55,7 +55,7 @@ def kernel_notes(co: str):
     """{symbol: {lds, vgpr, vgpr_spill, sgpr_spill, private}} from the metadata note."""
     txt = subprocess.run([os.path.join(LLVM, "llvm-readelf"), "--notes", co], check=True, capture_output=True,
                          text=True).stdout
-    out, cur = {}, {}
+    out, cur, sym = {}, {}, None
     fields = {".group_segment_fixed_size": "lds", ".vgpr_count": "vgpr", ".vgpr_spill_count": "vgpr_spill",
               ".sgpr_spill_count": "sgpr_spill", ".private_segment_fixed_size": "private",
               ".max_flat_workgroup_size": "max_wg", ".agpr_count": "agpr"}
@@ -70,8 +70,10 @@ def kernel_notes(co: str):
         if k in fields:
             cur[fields[k]] = int(v)
         elif k == ".symbol":
-            out[v[:-3] if v.endswith(".kd") else v] = cur
-            cur = {}
+            sym = v[:-3] if v.endswith(".kd") else v
+        elif k == ".wavefront_size" and sym:  # the last key of a kernel's (alphabetical) map
+            out[sym] = cur
+            cur, sym = {}, None
     return out
 
 
