@@ -450,10 +450,10 @@ int nd_op_dec_bank_h3(const float* qp, const uint16_t* bank, const float* signal
 /* 24-bit fixed-point memory bank (the greedy decoder's context attention at
  * T in (448, 512] by default; ND_BANK_D8=0 keeps the split-fp16 bank; the
  * same reference lines).  nd_op_bank_pack_d8: x [B*T, 256] row-major -> the
- * digit bank (B x 512 rows; every row t as 2^e_t times an integer of < 2^22
- * in three signed 8-bit digit planes, B * 512 * 256 * 3 bytes in the
- * v_mfma_i32_16x16x64_i8 A-operand fragment order), kscale [B * 512] floats
- * (2^e_t) and kemax [B] ints (each chunk's largest e_t, biased by 1024);
+ * digit bank (B x 512 rows; every row t as s_t times an integer of at most
+ * 126 * 2^16 in magnitude in three signed 8-bit digit planes, B * 512 * 256 *
+ * 3 bytes in the v_mfma_i32_16x16x64_i8 A-operand fragment order), kscale
+ * [B * 512] floats (s_t) and kemax [B] (each chunk's largest s_t, float bits);
  * LayerNorm with ln_g/ln_b when set; rows t >= T zero.  nd_op_dec_bank_d8:
  * as nd_op_dec_bank_h3 on that bank.  ovf (nullable): set to 1 on a
  * non-finite operand. */

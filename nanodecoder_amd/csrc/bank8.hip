@@ -6,27 +6,29 @@
 // into the query side (W_qk) and the output side (W_vo) as in the h3 form.
 //
 // Bank (bank_pack_d8_kernel, once per call): every key row t of the LN'd
-// encoder output is m_t = 2^e_t A_t with A_t integer, |A_t| < 2^22 (e_t =
-// floor(log2 max|m_t|) - 21), held as three signed 8-bit digits
-// A = a2 2^16 + a1 2^8 + a0 (balanced: a0 = sext8(A), ...).  Error per element
-// <= 2^(e_t - 1) <= 2^-22 max|m_t|.  Layout: 1 KB fragments (chunk, key block
-// kb of 16 keys, dim block db of 64, digit plane), lane l holding key
-// 16 kb + (l & 15), dims 64 db + 16 (l >> 4) .. +15; per key the scale 2^e_t
-// (float) and per chunk max e_t.
+// encoder output is m_t = s_t A_t with s_t = max|m_t| / (126 * 2^16) and A_t
+// integer, |A_t| <= 126 * 2^16 < 2^23, held as three signed 8-bit digits
+// A = a2 2^16 + a1 2^8 + a0 (balanced: a0 = sext8(A), ...; |a2| <= 126).
+// Error per element <= 0.75 s_t ~ 2^-23.4 max|m_t|.  Layout: 1 KB fragments
+// (chunk, key block kb of 16 keys, dim block db of 64, digit plane), lane l
+// holding key 16 kb + (l & 15), dims 64 db + 16 (l >> 4) .. +15; per key s_t,
+// per chunk max_t s_t.
 //
 // S = M q'^T on v_mfma_i32_16x16x64_i8: q' of head h is quantised the same
 // way per (chunk, head) in the prologue (sigma_h, digits q2 q1 q0); B1 =
-// [q2 | q1] and B2 = [q0 | 0] over the 16 columns (8 heads each); the four
-// products a2 B1, a2 B2, a1 B1, a0 B1 hold every digit product of weight
-// >= 2^8 (a1 q0 and a0 q0 dropped: <= 2^-22.4 max|m| max|q'| per dim), summed
-// exactly in int32 and combined in fp32 with their power-of-two weights.
+// [q2 | q1] and B2 = [0 | q0] over the 16 columns (8 heads each); five
+// products per 64 dims, a2 B1, a2 B2, a1 B1, a0 B1 + a1 B2 (one accumulator:
+// a0 q1 and a1 q0 share the weight 2^8), hold every digit product of weight
+// >= 2^8 (only a0 q0 dropped), summed exactly in int32 and combined in fp32
+// with their power-of-two weights.  Score error on LN-like rows: below a
+// plain fp32 dot product's rounding (tests/test_bank_d8_scheme.py).
 //
 // U = P^T M on f16 MFMAs as in the h3 form, the digits turned into exact f16
 // integers (magic-number conversion) from a per-wave transposed LDS image
 // read by ds_read_b64_tr_b8: one 16x16x32 product per dim block takes
 // [P, P] against [a2 * 2^8 (4 keys), a1 (4 keys)], one 16x16x16 product P
-// against a0 * 2^-8.  P is p * 2^(e_t - e_max + 7) (e_max: the chunk's largest
-// e_t, so <= 2^7 e^6 < 65504) split hi | lo as in the h3 form.
+// against a0 * 2^-8.  P is p s_t 2^7 / s_max (s_max: the chunk's largest s_t,
+// so <= 2^7 e^6 < 65504) split hi | lo as in the h3 form.
 //
 // 3 bytes per element: 103.9 MB per launch at 256 chunks against 138.9 MB.
 #include "common.hpp"
@@ -53,13 +55,13 @@ typedef unsigned d8u2 __attribute__((ext_vector_type(2)));
 #define B8_ML (B8_SIG + ND_H * 4)        // merge (m, l) [wave][8 heads][2]
 #define B8_FW (B8_ML + B8_NW * 16 * 4)   // merge weights [wave][8 heads], then [8 heads] output scales
 #define B8_LDS (B8_FW + (B8_NW + 1) * ND_H * 4)
-#define B8_EBIAS 1024                    // e_max is stored biased (atomicMax over ints >= 0)
+#define B8_AMAX (126.0f * 65536.0f)       // |A| <= 126 * 2^16: |a2| <= 126 after the balanced carries
 static_assert(3 * B8_PLANE <= B8_IMG && ND_H * ND_D * 2 * 4 <= B8_IMG, "wave image");
 static_assert(B8_LDS <= 160 * 1024, "LDS");
 
 __device__ __forceinline__ int sext8(int x) { return (x << 24) >> 24; }
 
-// the three balanced digits of an integer |A| < 2^22, as bytes of three words
+// the three balanced digits of an integer |A| <= 126 * 2^16 + 1 (|a2| <= 126)
 __device__ __forceinline__ void digits(int A, int& d2, int& d1, int& d0) {
   d0 = sext8(A);
   const int A1 = (A - d0) >> 8;
@@ -67,12 +69,9 @@ __device__ __forceinline__ void digits(int A, int& d2, int& d1, int& d0) {
   d2 = (A1 - d1) >> 8;
 }
 
-// e with 2^21 <= |x| * 2^-e < 2^22 for x = the row / head maximum (0 for 0)
-__device__ __forceinline__ int fix_exp(float mx) {
-  int E = 0;
-  (void)frexpf(mx, &E);
-  return mx > 0.f ? E - 22 : 0;
-}
+// x / s for the scale s = max|x| / (126 * 2^16) of its row (or head), rounded to an integer: |result| <=
+// 126 * 2^16 + 1 (IEEE division: the quotient's rounding is below the rint's)
+__device__ __forceinline__ int fix_q(float x, float s) { return s > 0.f ? (int)rintf(x / s) : 0; }
 
 __device__ __forceinline__ i32x4 mfma_i8(i32x4 a, i32x4 b, i32x4 c) {
   return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
@@ -152,7 +151,7 @@ __device__ __forceinline__ void bank_d8_chunk(int c, const float* __restrict__ q
     const int bkey = 16 * (w + B8_NW * (lane >> 4)) + (lane & 15);  // lane l: row l & 15 of key block w + 8 (l >> 4)
     sg = signal[(size_t)c * T + min(bkey, T - 1)];
   }
-  const int emax = kemax[c] - B8_EBIAS;
+  const float smax = __builtin_bit_cast(float, kemax[c]);  // the chunk's largest row scale
   i32x4 F[3][6];
   // issue order = retire order: q' and the scales first, then half block 0, then 1 (a wait for an
   // earlier load leaves the later ones in flight)
@@ -167,28 +166,28 @@ __device__ __forceinline__ void bank_d8_chunk(int c, const float* __restrict__ q
   {
     const float qm = wave_max(absmax4(qv));
     if (!(qm <= 3.0e38f) && ovf != nullptr) ovf[0] = 1;  // non-finite q'
-    const int es = fix_exp(qm);
+    const float qs = qm * (1.0f / B8_AMAX);
     unsigned pw[3] = {0u, 0u, 0u};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       int d2, d1, d0;
-      digits((int)rintf(ldexpf(qv[j], -es)), d2, d1, d0);
+      digits(fix_q(qv[j], qs), d2, d1, d0);
       pw[2] |= (unsigned)(d2 & 255) << (8 * j);
       pw[1] |= (unsigned)(d1 & 255) << (8 * j);
       pw[0] |= (unsigned)(d0 & 255) << (8 * j);
     }
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<unsigned*>(lb + B8_QD + pl * ND_H * ND_D + w * ND_D + 4 * lane) = pw[pl];
-    if (lane == 0) reinterpret_cast<float*>(lb + B8_SIG)[w] = ldexpf(1.0f, es + 16);
+    if (lane == 0) reinterpret_cast<float*>(lb + B8_SIG)[w] = qs * 65536.0f;  // sigma_h * 2^16 (exact)
     if (w == 0 && lane < 4) reinterpret_cast<unsigned*>(lb + B8_ZERO)[lane] = 0u;
   }
   lds_barrier();  // LDS only: the bank loads stay in flight
-  // B operands: column col = head col & 7; B1 = q2 (col < 8) | q1, B2 = q0 (col < 8) | 0; dims 64 db + 16 g ..
+  // B operands: column col = head col & 7; B1 = q2 (col < 8) | q1, B2 = 0 (col < 8) | q0; dims 64 db + 16 g ..
   i32x4 qb1[4], qb2[4];
   {
     const char* q1p = lb + B8_QD + (col < 8 ? 2 : 1) * ND_H * ND_D + (col & 7) * ND_D + 16 * g;
-    const char* q2p = col < 8 ? lb + B8_QD + (col & 7) * ND_D + 16 * g : lb + B8_ZERO;
-    const int q2s = col < 8 ? 64 : 0;
+    const char* q2p = col < 8 ? lb + B8_ZERO : lb + B8_QD + (col & 7) * ND_D + 16 * g;
+    const int q2s = col < 8 ? 0 : 64;
 #pragma unroll
     for (int db = 0; db < 4; ++db) {
       qb1[db] = *reinterpret_cast<const i32x4*>(q1p + 64 * db);
@@ -196,10 +195,11 @@ __device__ __forceinline__ void bank_d8_chunk(int c, const float* __restrict__ q
     }
   }
   const float sgm = reinterpret_cast<const float*>(lb + B8_SIG)[col & 7];
-  // digit-product weights (x 2^-16, folded into sgm): X1 = a2 [q2 | q1], X2 = a2 [q0 | 0], X3 = a1 [q2 | q1],
-  // X4 = a0 [q2 | q1]
-  const float w1 = col < 8 ? 65536.0f : 256.0f, w3 = col < 8 ? 256.0f : 1.0f, w4 = col < 8 ? 1.0f : 0.00390625f;
-  const float kp = ldexpf(1.0f, min(7 - emax, 127));  // P scale: p 2^(e_t - e_max + 7)
+  // digit-product weights (x 2^-16, folded into sgm): X1 = a2 [q2 | q1], X2 = a2 [0 | q0], X3 = a1 [q2 | q1],
+  // X4 = a0 [q2 | q1] + a1 [0 | q0]
+  const float w1 = col < 8 ? 65536.0f : 256.0f, w2 = col < 8 ? 0.0f : 1.0f, w3 = col < 8 ? 256.0f : 1.0f,
+              w4 = col < 8 ? 1.0f : 0.00390625f;
+  const float kp = smax > 0.f ? 128.0f / smax : 0.f;  // P scale: p s_t 2^7 / s_max
   const unsigned long long padm = __ballot(sg == pad_val);
   // transposed reads: lane 2q + p of its group supplies row q (keys 4 g + (q & 3)); planes (a2 | a1) at
   // dim block k, or a0 at dim blocks (k | k + 1)
@@ -227,6 +227,7 @@ __device__ __forceinline__ void bank_d8_chunk(int c, const float* __restrict__ q
         X2 = mfma_i8(f[3 * j], qb2[db], X2);
         X3 = mfma_i8(f[3 * j + 1], qb1[db], X3);
         X4 = mfma_i8(f[3 * j + 2], qb1[db], X4);
+        X4 = mfma_i8(f[3 * j + 1], qb2[db], X4);
       }
 #pragma unroll
       for (int i = 0; i < 6; ++i) {
@@ -239,7 +240,7 @@ __device__ __forceinline__ void bank_d8_chunk(int c, const float* __restrict__ q
     // ---- scores: columns h and h + 8 hold the high and low digit products of head h
     f32x4 s;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) s[i] = (float)X1[i] * w1 + (float)X2[i] + (float)X3[i] * w3 + (float)X4[i] * w4;
+    for (int i = 0; i < 4; ++i) s[i] = (float)X1[i] * w1 + (float)X2[i] * w2 + (float)X3[i] * w3 + (float)X4[i] * w4;
 #pragma unroll
     for (int i = 0; i < 4; ++i) s[i] = (s[i] + dpp_mov<0x128>(s[i])) * (ksc[kb][i] * sgm);
     const int kbase = 16 * (w + B8_NW * kb) + 4 * g;  // key of row i
@@ -296,7 +297,7 @@ __device__ __forceinline__ void bank_d8_chunk(int c, const float* __restrict__ q
   }
 
   // ---- merge the 8 waves (as dec_bank_h3_kernel): unmerged U^T fragments to the wave's own image, (m, l)
-  //      beside, wave 0 turns them into merge weights and the output scale 2^(e_max + 1) / den
+  //      beside, wave 0 turns them into merge weights and the output scale 2 s_max / den
   l = xor32_sum(xor16_sum(l));
   float* ml = reinterpret_cast<float*>(lb + B8_ML);  // [wave][8 heads][2]
   {
@@ -322,7 +323,7 @@ __device__ __forceinline__ void bank_d8_chunk(int c, const float* __restrict__ q
     den += __shfl_xor(den, 16, 64);
     den += __shfl_xor(den, 32, 64);
     fw[v * ND_H + hh] = f;
-    if (v == 0) fw[B8_NW * ND_H + hh] = den > 0.f ? __builtin_amdgcn_rcpf(den) * ldexpf(1.0f, emax + 1) : 0.f;
+    if (v == 0) fw[B8_NW * ND_H + hh] = den > 0.f ? __builtin_amdgcn_rcpf(den) * (2.0f * smax) : 0.f;
   }
   lds_barrier();
 #pragma unroll
@@ -365,16 +366,17 @@ dec_bank_d8_kernel(const float* __restrict__ qp, const i32x4* __restrict__ bank,
 }
 
 // Encoder output -> the 24-bit digit bank: one workgroup per (chunk, key
-// block of 16 rows): LayerNorm (as bank_pack_h3_kernel), per row the
-// exponent e_t and the digits into LDS, then the 12 fragments as coalesced
-// 1 KB stores; the row scales 2^e_t and the chunk's largest e_t (atomicMax,
-// biased; kemax zeroed by the caller).  Rows t >= T are zero.
+// block of 16 rows): LayerNorm (as bank_pack_h3_kernel), per row the scale
+// s_t and the digits into LDS, then the 12 fragments as coalesced 1 KB
+// stores; the row scales and the chunk's largest (atomicMax on the float's
+// bits, non-negative; kemax zeroed by the caller).  Rows t >= T are zero
+// (scale 0).
 __global__ void __launch_bounds__(256)
 bank_pack_d8_kernel(const float* __restrict__ x, const float* __restrict__ gm, const float* __restrict__ bt,
                     i32x4* __restrict__ bank, float* __restrict__ kscale, int* __restrict__ kemax, int T, int* ovf) {
   __shared__ __attribute__((aligned(16))) unsigned char dg[3][16][ND_D];
   const int c = blockIdx.x / B8_KB, kb = blockIdx.x % B8_KB, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  int emx = B8_EBIAS - 126;  // a chunk of all-zero rows: e_max = -126 (its P scale stays finite)
+  float smx = 0.f;
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) {
     const int r = wv + 4 * rr, t = 16 * kb + r;
@@ -390,24 +392,22 @@ bank_pack_d8_kernel(const float* __restrict__ x, const float* __restrict__ gm, c
     }
     const float mx = wave_max(absmax4(v));
     if (!(mx <= 3.0e38f) && ovf != nullptr) ovf[0] = 1;  // non-finite encoder output
-    // a zero row (t >= T) gets the smallest scale: it never sets the chunk's e_max, whose P scale
-    // 2^(e_t - e_max + 7) would otherwise push every real row's P into the fp16 subnormals
-    const int e = mx > 0.f ? fix_exp(mx) : -126;
+    const float st = mx * (1.0f / B8_AMAX);
     unsigned pw[3] = {0u, 0u, 0u};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       int d2, d1, d0;
-      digits((int)rintf(ldexpf(v[j], -e)), d2, d1, d0);
+      digits(fix_q(v[j], st), d2, d1, d0);
       pw[2] |= (unsigned)(d2 & 255) << (8 * j);
       pw[1] |= (unsigned)(d1 & 255) << (8 * j);
       pw[0] |= (unsigned)(d0 & 255) << (8 * j);
     }
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<unsigned*>(&dg[pl][r][4 * lane]) = pw[pl];
-    if (lane == 0) kscale[(size_t)c * 512 + t] = ldexpf(1.0f, e);
-    if (mx > 0.f) emx = max(emx, e + B8_EBIAS);
+    if (lane == 0) kscale[(size_t)c * 512 + t] = st;
+    smx = fmaxf(smx, st);
   }
-  if (lane == 0) atomicMax(kemax + c, emx);
+  if (lane == 0) atomicMax(kemax + c, __builtin_bit_cast(int, smx));  // non-negative floats order as ints
   __syncthreads();
   // fragment (db, pl): lane ln holds key ln & 15, dims 64 db + 16 (ln >> 4) .. +15
 #pragma unroll

@@ -633,7 +633,8 @@ def op_dec_bank_h3(qp, bank, signal, span, pad_val, out=None, ovf=None, grid=0):
 
 def op_bank_pack_d8(x, B, T, ln_g=None, ln_b=None, ovf=None):
     """24-bit digit bank (nd_op_bank_pack_d8): x [B*T, 256] -> (digits uint8
-    [B * 512 * 256 * 3], row scales [B * 512], chunk max exponents [B] int32)."""
+    [B * 512 * 256 * 3], row scales [B * 512], each chunk's largest row scale
+    [B] as float bits in int32)."""
     dev = x.device
     bank = torch.empty(B * 512 * 256 * 3, dtype=torch.uint8, device=dev)
     ks = torch.empty(B * 512, dtype=torch.float32, device=dev)
