@@ -9,7 +9,7 @@
 // encoder output is m_t = s_t A_t with s_t = max|m_t| / (126 * 2^16) and A_t
 // integer, |A_t| <= 126 * 2^16 < 2^23, held as three signed 8-bit digits
 // A = a2 2^16 + a1 2^8 + a0 (balanced: a0 = sext8(A), ...; |a2| <= 126).
-// Error per element <= 0.75 s_t ~ 2^-23.4 max|m_t|.  Layout: 1 KB fragments
+// Error per element <= 0.75 s_t ~ 2^-23.3 max|m_t|.  Layout: 1 KB fragments
 // (chunk, key block kb of 16 keys, dim block db of 64, digit plane), lane l
 // holding key 16 kb + (l & 15), dims 64 db + 16 (l >> 4) .. +15; per key s_t,
 // per chunk max_t s_t.
