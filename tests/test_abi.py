@@ -118,3 +118,59 @@ def test_hot_path_kernels_do_not_drain_loads(tmp_path):
         assert found, rx
         bad = {k: v for k, v in found.items() if v > most}
         assert not bad, bad
+
+
+# ----------------------------------------------------------------- LDS rule
+# DESIGN.md section 5 "Co-residency": the closed-form layer-0 encoder attention
+# returned wrong chunks beside another engine's kernels exactly when its
+# per-wave data past LDS byte 65,536 was accessed by ds_read2* / ds_write2*
+# through an address register >= 65,536 (tools/r2_lds.sh, profiles/r04_lds/).
+# Every kernel that can hold more than 64 KB of LDS and uses the paired forms
+# is listed here with the reason its paired accesses were reviewed, and the
+# most paired-form instructions it had when reviewed; a new kernel, or more
+# paired accesses in a listed one, fails until it is reviewed again.
+DYNAMIC_LDS = {  # kernels launched with dynamic LDS (metadata says 0): bytes at the launch site
+    "dec_bank_d8_kernel": 138064,        # bank8.hip B8_LDS
+    "dec_bank_h3_kernel": 139904,        # mem_attention.hip BH_LDS
+    "dec_mem_attention_kernel": 158208,  # mem_lds_bytes()
+    "dec_ctx_attention_kernel": 163840,  # up to 160 KB (init_kernel_attributes)
+    "gemm_p16s_kernel": 98304,           # 2x4 tiles
+}
+REVIEWED_PAIRED = {
+    # base name: (max paired-form DS instructions per instantiation, reason)
+    "enc_attention_h3_kernel": (9, "K / V^T staging with ds_write2st64_b64 from a base below 64 KB, read by the "
+                                   "other waves after a barrier; pool-tested bitwise"),
+    "enc_ffn_kernel": (8, "row statistics written with ds_write2st64_b32 behind the weight slots, read after a "
+                          "barrier; pool-tested"),
+    "gemm_f32_kernel": (48, "A / W tile staging (ds_write2_b32 / _b64 / 2st64) read by other waves after a "
+                            "barrier; encoder-side GEMMs of the beam / exact / NanoEncoder paths, pool-tested"),
+    "dec_ctx_attention_kernel": (18, "K / V staging and row reads in the beam context attention; pool-tested "
+                                     "(configs[3] at the bench's size)"),
+    "dec_bank_d8_kernel": (3, "the (m, l) merge and the q' digit rows (cross-wave, after a barrier); "
+                              "pool-tested at the bench's configuration"),
+    "dec_bank_h3_kernel": (2, "the (m, l) merge, as dec_bank_d8_kernel"),
+    "dec_mem_attention_kernel": (25, "the fp32 bank kernel (exact fp32 / short chunks): slab reads after "
+                                     "barriers"),
+}
+
+
+def test_lds_paired_forms_above_64k_are_reviewed():
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import kernel_meta
+    from nanodecoder_amd import build
+    build.build()
+    seen = {}
+    for r in kernel_meta.collect():
+        base = re.sub(r"\(.*$", "", re.sub(r"^void ", "", r["name"])).replace("nd::", "")
+        base = re.sub(r"<.*$", "", base)
+        lds = r.get("lds", 0) + DYNAMIC_LDS.get(base, 0)
+        pairs = sum(v for k, v in r["ds"].items() if re.match(r"ds_(read|write)2", k))
+        if lds > 65536 and pairs:
+            seen[base] = max(seen.get(base, 0), pairs)
+    for base, n in seen.items():
+        assert base in REVIEWED_PAIRED, f"{base}: {n} paired-form LDS instructions and more than 64 KB of LDS"
+        assert n <= REVIEWED_PAIRED[base][0], (base, n, REVIEWED_PAIRED[base])
+    # the closed-form layer-0 attention keeps its whole allocation at 64 KB
+    r2 = [r for r in kernel_meta.collect() if "enc_attention_rank2_kernel" in r["name"]]
+    assert r2 and all(r["lds"] <= 65536 for r in r2)

@@ -12,7 +12,7 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u2 __attribute__((ext_vector_type(2)));
 
 __global__ void tr_b8_kernel(const unsigned* addr, unsigned long long* out) {
-  __shared__ unsigned char m[256];
+  __shared__ volatile unsigned char m[256];  // volatile: the stores stay (only the asm reads them)
   const int l = threadIdx.x;
   for (int i = l; i < 256; i += 64) m[i] = (unsigned char)(((i >> 5) << 5) | (i & 31));
   __syncthreads();
