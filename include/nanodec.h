@@ -454,18 +454,33 @@ int nd_op_dec_bank_h3(const float* qp, const uint16_t* bank, const float* signal
  * 126 * 2^16 in magnitude in three signed 8-bit digit planes, B * 512 * 256 *
  * 3 bytes in the v_mfma_i32_16x16x64_i8 A-operand fragment order), kscale
  * [B * 512] floats (s_t) and kemax [B] (each chunk's largest s_t, float bits);
- * LayerNorm with ln_g/ln_b when set; rows t >= T zero.  nd_op_dec_bank_d8:
+ * LayerNorm with ln_g/ln_b when set; rows t >= T, and rows t >= span[c] when
+ * span (nullable, [B]) is given, zero with scale 0 (the engine passes the
+ * call's spans: rows past a chunk's span are never attended and must not set
+ * its largest scale).  nd_op_dec_bank_d8:
  * as nd_op_dec_bank_h3 on that bank.  ovf (nullable): set to 1 on a
  * non-finite operand. */
 int nd_op_bank_pack_d8(const float* x, const float* ln_g, const float* ln_b, void* bank, float* kscale,
-                       int32_t* kemax, int32_t B, int32_t T, int32_t* ovf, void* stream);
+                       int32_t* kemax, const int32_t* span, int32_t B, int32_t T, int32_t* ovf, void* stream);
 int nd_op_dec_bank_d8(const float* qp, const void* bank, const float* kscale, const int32_t* kemax,
                       const float* signal, const int32_t* span, float pad_val, float* out, int32_t C, int32_t T,
                       int32_t* ovf, int32_t grid, void* stream);
 
-/* Which memory bank the context's last greedy call streamed (diagnostics,
- * the bench's roofline accounting): 0 fp32 bank (or none), 1 split-fp16
- * (nd_op_dec_bank_h3), 2 24-bit digits (nd_op_dec_bank_d8). */
+/* The --fast / classic beam's context attention on the same digit bank
+ * (replaces the per-layer K/V form, nd_op_dec_ctx_attention, for beam rows;
+ * translate/translator.py:700-823 + decoder/transformer.py:178-189 over
+ * multi_headed_attn.py:142-177): rows r = c*rpc + j (rpc 2..6) of q' [C*rpc,
+ * 2048] in the P16 layout attend over chunk c's bank; out U [C*rpc, 2048]
+ * P16, as nd_op_dec_bank_d8 per row.  Chunks with done[c] != 0 are skipped
+ * (done nullable).  One pass over a chunk's bank serves all its rows. */
+int nd_op_dec_bank_d8_beam(const float* qp, const void* bank, const float* kscale, const int32_t* kemax,
+                           const float* signal, const int32_t* span, float pad_val, float* out, int32_t C,
+                           int32_t rpc, int32_t T, const int32_t* done, int32_t* ovf, void* stream);
+
+/* Which memory bank the context's last call streamed (diagnostics, the
+ * bench's roofline accounting): 0 fp32 bank, or none (a beam call on the
+ * K/V form), 1 split-fp16 (nd_op_dec_bank_h3), 2 24-bit digits
+ * (nd_op_dec_bank_d8, or nd_op_dec_bank_d8_beam for a beam call). */
 int nd_bank_form(nd_ctx* ctx);
 
 /* Decoder context attention (multi_headed_attn.py:142-177): rows r = c*rpc+j

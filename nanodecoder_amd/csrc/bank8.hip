@@ -369,19 +369,23 @@ dec_bank_d8_kernel(const float* __restrict__ qp, const i32x4* __restrict__ bank,
 // block of 16 rows): LayerNorm (as bank_pack_h3_kernel), per row the scale
 // s_t and the digits into LDS, then the 12 fragments as coalesced 1 KB
 // stores; the row scales and the chunk's largest (atomicMax on the float's
-// bits, non-negative; kemax zeroed by the caller).  Rows t >= T are zero
-// (scale 0).
+// bits, non-negative; kemax zeroed by the caller).  Rows t >= T, and rows at
+// or past the chunk's span (never attended; the encoder leaves them
+// unspecified), are zero with scale 0, so s_max is a function of the
+// attended rows alone.
 __global__ void __launch_bounds__(256)
 bank_pack_d8_kernel(const float* __restrict__ x, const float* __restrict__ gm, const float* __restrict__ bt,
-                    i32x4* __restrict__ bank, float* __restrict__ kscale, int* __restrict__ kemax, int T, int* ovf) {
+                    i32x4* __restrict__ bank, float* __restrict__ kscale, int* __restrict__ kemax,
+                    const int* __restrict__ span, int T, int* ovf) {
   __shared__ __attribute__((aligned(16))) unsigned char dg[3][16][ND_D];
   const int c = blockIdx.x / B8_KB, kb = blockIdx.x % B8_KB, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int L = span ? min(span[c], T) : T;
   float smx = 0.f;
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) {
     const int r = wv + 4 * rr, t = 16 * kb + r;
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (t < T) {
+    if (t < L) {
       v = ld4(x + ((size_t)c * T + t) * ND_D + lane * 4);
       if (gm) {
         const float mu = wave_sum(v.x + v.y + v.z + v.w) * (1.0f / ND_D);
@@ -419,12 +423,12 @@ bank_pack_d8_kernel(const float* __restrict__ x, const float* __restrict__ gm, c
 }
 
 hipError_t launch_bank_pack_d8(const float* x, const float* ln_g, const float* ln_b, void* bank, float* kscale,
-                               int* kemax, int B, int T, int* ovf, hipStream_t s) {
+                               int* kemax, const int* span, int B, int T, int* ovf, hipStream_t s) {
   if (T < 1 || T > 512 || B < 1 || !bank || !kscale || !kemax) return hipErrorInvalidValue;
   hipError_t e = hipMemsetAsync(kemax, 0, (size_t)B * sizeof(int), s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(bank_pack_d8_kernel, dim3(B * B8_KB), dim3(256), 0, s, x, ln_g, ln_b,
-                     reinterpret_cast<i32x4*>(bank), kscale, kemax, T, ovf);
+                     reinterpret_cast<i32x4*>(bank), kscale, kemax, span, T, ovf);
   return hipGetLastError();
 }
 
@@ -449,6 +453,300 @@ hipError_t launch_dec_bank_d8(const float* qp, const void* bank, const float* ks
     ND_BANK8_GO(false, false);
   }
 #undef ND_BANK8_GO
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// --fast beam rows in memory-bank form (translate/translator.py:700-823 runs
+// the decoder on beam x batch rows; decoder/transformer.py:178-189 their
+// context attention): the RPC (2..6) rows of a chunk share ONE pass over the
+// chunk's digit bank, against the K/V form's 1 MB per chunk.
+//  - The chunk's key blocks (12 KB each: 4 dim blocks x 3 planes of 1 KB
+//    fragments) stream through a 3-slot LDS ring by buffer_load ... lds
+//    (waves 0..5 copy two fragments each), two blocks ahead; slots are 1152 B
+//    apart so the a2 and a1 planes of a dim block sit on opposite bank halves
+//    for the transposed reads.
+//  - Scores: wave j < RPC owns row j (its q' digits in registers, computed
+//    straight from the P16 q' rows) and runs the greedy form's five i8
+//    products per 64 dims on the block from LDS, its lazy online softmax per
+//    head, and hands P (hi | lo f16 rows, the U A-operand layout) plus any
+//    rescale factors to LDS.
+//  - Context: every wave owns two 16-dim blocks of U for ALL rows, converts
+//    only those digits (tr_b8 + the exact f16 conversion) and runs the greedy
+//    form's two f16 products per row: no U merge across waves, the digits of
+//    a block converted once per workgroup.
+// Output U [C * RPC, 2048] P16 (row c * RPC + j), as dec_bank_d8_kernel's.
+#define BB_NW 8
+#define BB_MAXR 6
+#ifndef BB_WPE
+#define BB_WPE 4                           // waves per SIMD: two workgroups per CU (128 VGPRs)
+#endif
+#define BB_FR 1152                         // LDS bytes per 1 KB fragment slot
+#define BB_BLK (12 * BB_FR)                // one key block
+#define BB_NBUF 3                          // ring slots
+#define BB_KS (BB_NBUF * BB_BLK)           // [512] row scales s_t
+#define BB_PM (BB_KS + 512 * 4)            // [512] pad flags (bytes)
+#define BB_P (BB_PM + 512)                 // [row][64 lanes] P fragments, 8 B each
+#define BB_SC (BB_P + BB_MAXR * 512)       // [row][8 heads] rescale factors of the current block
+#define BB_FIN (BB_SC + BB_MAXR * 8 * 4)   // [row][8 heads] output scales 2 s_max / l
+#define BB_LDS (BB_FIN + BB_MAXR * 8 * 4)
+static_assert(BB_LDS <= 65536, "beam bank LDS within 64 KB (DESIGN.md section 5, co-residency rule)");
+
+template <int RPC>
+__device__ __forceinline__ void bank_d8_beam_chunk(char* lb, int c, const float* __restrict__ qp, const char* bank,
+                                                   const float* __restrict__ kscale, const int* __restrict__ kemax,
+                                                   const float* __restrict__ signal, const int* __restrict__ span,
+                                                   float pad_val, float* __restrict__ out, int T, int* ovf) {
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int col = lane & 15, g = lane >> 4;
+  const int L = min(span[c], T);
+  const int nkb = (L + 15) >> 4;  // key blocks holding a key < L
+  const float smax = __builtin_bit_cast(float, kemax[c]);
+  const __amdgpu_buffer_rsrc_t src = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<char*>(bank) + (size_t)c * (B8_KB * 12 * 1024), 0, B8_KB * 12 * 1024, 0x00020000);
+  // key block kb -> ring slot kb % 3: waves 0..5 copy fragments 2w, 2w + 1 (db * 3 + plane)
+  auto issue = [&](int kb) {
+    if (w < 6) {
+      char* dst = lb + (kb % BB_NBUF) * BB_BLK;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int f = 2 * w + i;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(src, (__attribute__((address_space(3))) void*)(dst + f * BB_FR), 16,
+                                                 lane * 16, kb * 12288 + f * 1024, 0, 0);
+      }
+    }
+  };
+  // ---- prologue: row j = w's q' (P16 [R][2048]; lane: head col & 7, dims 64 db + 16 g + 4 i ..), the
+  //      chunk's row scales and pad flags (one key per thread), then the first two key blocks
+  const int r = c * RPC + w;
+  // the first two key blocks, then every prologue load at once (one memory round trip)
+  if (nkb > 0) issue(0);
+  if (nkb > 1) issue(1);
+  const float* qrow = qp + pk(r, (col & 7) * ND_D + 16 * g, ND_H * ND_D);  // + pk offsets of 64 db + 4 i
+  f32x4 qv[16];
+  if (w < RPC) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) qv[k] = ld4(qrow + pk(0, 64 * (k >> 2) + 4 * (k & 3), ND_H * ND_D));
+  }
+  const int tk = threadIdx.x;  // 512 threads, 512 keys
+  const float ksv = kscale[(size_t)c * 512 + tk];
+  const float sgv = signal[(size_t)c * T + min(tk, T - 1)];
+  reinterpret_cast<float*>(lb + BB_KS)[tk] = ksv;
+  reinterpret_cast<unsigned char*>(lb + BB_PM)[tk] = (tk < T && sgv == pad_val) ? 1 : 0;
+  // B operands of the scores (as dec_bank_d8_kernel's qb1 / qb2): B1 = q2 (col < 8) | q1, B2 = 0 | q0
+  i32x4 qb1[4], qb2[4];
+  float sgm = 0.f;
+  if (w < RPC) {
+    float mx = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) mx = fmaxf(mx, absmax4(qv[k]));
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    if (!(mx <= 3.0e38f) && ovf != nullptr) ovf[0] = 1;  // non-finite q'
+    const float qs = mx * (1.0f / B8_AMAX);
+    const float qdiv = qs > 0.f ? qs : 1.0f;  // a zero head is all zeros: x / 1 = 0 (fix_q without its branch)
+    sgm = qs * 65536.0f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      unsigned u1 = 0u, u2 = 0u;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        int d2, d1, d0;
+        digits((int)rintf(qv[k][e] / qdiv), d2, d1, d0);
+        u1 |= (unsigned)((col < 8 ? d2 : d1) & 255) << (8 * e);
+        u2 |= (unsigned)((col < 8 ? 0 : d0) & 255) << (8 * e);
+      }
+      qb1[k >> 2][k & 3] = (int)u1;
+      qb2[k >> 2][k & 3] = (int)u2;
+      __builtin_amdgcn_sched_barrier(0);  // four values at a time (the divisions' temporaries)
+    }
+  }
+  const float w1 = col < 8 ? 65536.0f : 256.0f, w3 = col < 8 ? 256.0f : 1.0f, w4 = col < 8 ? 1.0f : 0.00390625f;
+  const float kp = smax > 0.f ? 128.0f / smax : 0.f;  // P scale: p s_t 2^7 / s_max
+  // ---- this wave's U dim blocks 2w, 2w + 1 (dim block db_u, 16-dim groups G0, G0 + 1) in the transposed
+  //      reads: lane 2q + p of its group supplies row q (keys 4 g + (q & 3); planes a2 | a1, or a0 of G0 | G0 + 1)
+  const int db_u = w >> 1, G0 = 2 * (w & 1);
+  const int q8 = (lane & 15) >> 1, p8 = lane & 1;
+  const int o1 = (db_u * 3 + (q8 < 4 ? 2 : 1)) * BB_FR + (4 * g + (q8 & 3) + 16 * G0) * 16 + 8 * p8;
+  const int o3 = db_u * 3 * BB_FR + (4 * g + (q8 & 3) + 16 * (G0 + (q8 < 4 ? 0 : 1))) * 16 + 8 * p8;
+  // U accumulators: row block b holds rows 2b (MFMA rows 0..7, head = row) and 2b + 1 (rows 8..15); P's
+  // hi and lo parts ride in the K dimension against the same digits twice
+  constexpr int NB = (RPC + 1) / 2;
+  f32x4 ua[NB][2];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) ua[b][0] = ua[b][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (RPC & 1) {  // the last block's second row does not exist: zero P rows, unit rescale factors
+    if (threadIdx.x < 32) reinterpret_cast<f32x4*>(lb + BB_P + RPC * 512)[threadIdx.x] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (threadIdx.x < 8) reinterpret_cast<float*>(lb + BB_SC)[RPC * 8 + threadIdx.x] = 1.0f;
+  }
+  float m = -INFINITY, l = 0.f;
+
+  for (int kb = 0; kb < nkb; ++kb) {
+    // block kb landed (this wave's copies; the barrier: everyone's), and every wave is done with
+    // block kb - 1 (its ring slot takes block kb + 2)
+    if (kb + 1 < nkb)
+      asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (kb + 2 < nkb) issue(kb + 2);
+    const char* buf = lb + (kb % BB_NBUF) * BB_BLK;
+    if (w < RPC) {
+      // ---- scores of row w: columns h and h + 8 hold the high and low digit products of head h
+      // X3 takes a1 B1 + a2 B2 (columns < 8: a2 B2 = 0; columns >= 8: both weight 1)
+      i32x4 X1 = {0, 0, 0, 0}, X3 = X1, X4 = X1;
+      const char* fb = buf + lane * 16;
+      // one dim block's three planes in flight beside the previous block's products (24 registers)
+      i32x4 fr[2][3];
+      auto fload = [&](int db, i32x4(&f)[3]) {
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) f[pl] = *reinterpret_cast<const i32x4*>(fb + (db * 3 + pl) * BB_FR);
+      };
+      fload(0, fr[0]);
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        if (db < 3) fload(db + 1, fr[(db + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+        const i32x4(&f)[3] = fr[db & 1];
+        X1 = mfma_i8(f[2], qb1[db], X1);
+        X3 = mfma_i8(f[2], qb2[db], X3);
+        X3 = mfma_i8(f[1], qb1[db], X3);
+        X4 = mfma_i8(f[0], qb1[db], X4);
+        X4 = mfma_i8(f[1], qb2[db], X4);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      const f32x4 ks4 = *reinterpret_cast<const f32x4*>(lb + BB_KS + (16 * kb + 4 * g) * 4);
+      const unsigned pf = *reinterpret_cast<const unsigned*>(lb + BB_PM + 16 * kb + 4 * g);
+      f32x4 s;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) s[i] = (float)X1[i] * w1 + (float)X3[i] * w3 + (float)X4[i] * w4;
+      const int kbase = 16 * kb + 4 * g;  // key of row i
+      float gm = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        s[i] = (s[i] + dpp_mov<0x128>(s[i])) * (ks4[i] * sgm);
+        s[i] = kbase + i < L ? (((pf >> (8 * i)) & 1u) ? ND_MASK_FILL : s[i]) : -INFINITY;
+        gm = fmaxf(gm, s[i]);
+      }
+      gm = xor32_max(xor16_max(gm));
+      const bool resc = __any(gm > m + B8_THR);  // wave-uniform
+      float sc = 1.f;
+      if (resc) {
+        const float nm = fmaxf(m, gm);
+        sc = nm == m ? 1.f : __expf(m - nm);
+        m = nm;
+        l *= sc;
+      }
+      // every block (1 when this row did not rescale): the row blocks rescale unconditionally
+      if (g == 0 && col < 8) reinterpret_cast<float*>(lb + BB_SC)[w * 8 + col] = sc;
+      f32x4 p;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) p[i] = s[i] == -INFINITY ? 0.f : __expf(s[i] - m);
+      l += (p[0] + p[1]) + (p[2] + p[3]);
+      // the U A operand of head col (< 8), keys 4 g .. 4 g + 3: hi x 4 | lo x 4 at P[row][g][head]
+      d8h8 pa;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float x = p[i] * (ks4[i] * kp);
+        const _Float16 hi = (_Float16)x;
+        pa[i] = hi;
+        pa[4 + i] = (_Float16)(x - (float)hi);
+      }
+      if (col < 8) *reinterpret_cast<d8h8*>(lb + BB_P + w * 512 + (g * 8 + col) * 16) = pa;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // P, rescale factors visible
+    // ---- U += P^T M' for every row on this wave's two dim blocks
+    const d8u2 r1 = tr_b8(buf + o1), r2 = tr_b8(buf + o1 + 256), r3 = tr_b8(buf + o3);
+    const d8h4 c2a = d8_cvt(r1.x, 2), c1a = d8_cvt(r1.y, 1), c2b = d8_cvt(r2.x, 2), c1b = d8_cvt(r2.y, 1);
+    const d8h8 b2a = {c2a[0], c2a[1], c2a[2], c2a[3], c2a[0], c2a[1], c2a[2], c2a[3]};  // [a2 | a2] 2^8
+    const d8h8 b1a = {c1a[0], c1a[1], c1a[2], c1a[3], c1a[0], c1a[1], c1a[2], c1a[3]};  // [a1 | a1]
+    const d8h8 b2b = {c2b[0], c2b[1], c2b[2], c2b[3], c2b[0], c2b[1], c2b[2], c2b[3]};
+    const d8h8 b1b = {c1b[0], c1b[1], c1b[2], c1b[3], c1b[0], c1b[1], c1b[2], c1b[3]};
+    const d8h4 b0a = d8_cvt(r3.x, 0), b0b = d8_cvt(r3.y, 0);  // a0 2^-8 (the hi parts only)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      // the running-maximum rescale, every block (factor 1 when the row did not rescale).  Branch-free on
+      // purpose: a branch around these multiplies gave wrong components 0, 1 of ua[b][1] on gfx950
+      // (tools/bb_debug.py; cause not isolated, the unconditional form is exact)
+      // accumulator rows 4 g + i: row 2 b + (g >> 1), head 4 (g & 1) + i
+      {
+        const f32x4 sc4 = *reinterpret_cast<const f32x4*>(lb + BB_SC + (2 * b + (g >> 1)) * 32 + 16 * (g & 1));
+        ua[b][0] *= sc4;
+        ua[b][1] *= sc4;
+      }
+      // A operand row col: row 2 b + (col >> 3), head col & 7
+      const d8h8 pa = *reinterpret_cast<const d8h8*>(lb + BB_P + (2 * b + (col >> 3)) * 512 + (g * 8 + (col & 7)) * 16);
+      const d8h4 ph = {pa[0], pa[1], pa[2], pa[3]};
+      ua[b][0] = mfma_d8h32(pa, b2a, ua[b][0]);
+      ua[b][0] = mfma_d8h32(pa, b1a, ua[b][0]);
+      ua[b][0] = mfma_d8h16(ph, b0a, ua[b][0]);
+      ua[b][1] = mfma_d8h32(pa, b2b, ua[b][1]);
+      ua[b][1] = mfma_d8h32(pa, b1b, ua[b][1]);
+      ua[b][1] = mfma_d8h16(ph, b0b, ua[b][1]);
+    }
+  }
+  // ---- output scales 2 s_max / l per (row, head); U [row][h * 256 + d] P16
+  if (w < RPC) {
+    l = xor32_sum(xor16_sum(l));
+    if (g == 0 && col < 8)
+      reinterpret_cast<float*>(lb + BB_FIN)[w * 8 + col] = l > 0.f ? __builtin_amdgcn_rcpf(l) * (2.0f * smax) : 0.f;
+  }
+  __syncthreads();
+  const int jl = 2 * 0 + (g >> 1);  // this lane's row within a block
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const int j = 2 * b + jl;
+    if (j < RPC) {
+      const f32x4 fs = *reinterpret_cast<const f32x4*>(lb + BB_FIN + j * 32 + 16 * (g & 1));
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int d = 16 * (2 * w + kk) + col;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int n = (4 * (g & 1) + i) * ND_D + d;
+          out[pk(c * RPC + j, n & ~3, ND_H * ND_D) + (n & 3)] = ua[b][kk][i] * fs[i];
+        }
+      }
+    }
+  }
+}
+
+// one workgroup per chunk (two per CU: 8 waves of <= 128 VGPRs each, 47.5 KB of LDS)
+template <int RPC>
+__global__ void __launch_bounds__(BB_NW * 64) __attribute__((amdgpu_waves_per_eu(BB_WPE)))
+dec_bank_d8_beam_kernel(const float* __restrict__ qp, const char* __restrict__ bank,
+                        const float* __restrict__ kscale, const int* __restrict__ kemax,
+                        const float* __restrict__ signal, const int* __restrict__ span, float pad_val,
+                        float* __restrict__ out, int T, const int* __restrict__ done, unsigned long long* stamp,
+                        int* ovf) {
+  // ONE shared array (a second __shared__ object beside LDS-DMA staging can make hipcc drain vmcnt
+  // before every ds_read)
+  __shared__ __attribute__((aligned(16))) char lb[BB_LDS];
+  const unsigned long long t_entry = wall_clock64();
+  stamp_begin_at(stamp, t_entry);
+  const int c = blockIdx.x;
+  if (!(done && done[c])) bank_d8_beam_chunk<RPC>(lb, c, qp, bank, kscale, kemax, signal, span, pad_val, out, T, ovf);
+  stamp_end(stamp);
+}
+
+hipError_t launch_dec_bank_d8_beam(const float* qp, const void* bank, const float* kscale, const int* kemax,
+                                   const float* signal, const int* span, float pad_val, float* out, int C, int rpc,
+                                   int T, const int* done, hipStream_t s, unsigned long long* stamp, int* ovf) {
+  if (T < 1 || T > 512 || C < 1 || rpc < 2 || rpc > BB_MAXR || !qp || !bank || !kscale || !kemax || !signal ||
+      !span || !out)
+    return hipErrorInvalidValue;
+#define ND_BANK8B_GO(R)                                                                                         \
+  hipLaunchKernelGGL((dec_bank_d8_beam_kernel<R>), dim3(C), dim3(BB_NW * 64), 0, s, qp,                       \
+                     reinterpret_cast<const char*>(bank), kscale, kemax, signal, span, pad_val, out, T, done, stamp, \
+                     ovf)
+  switch (rpc) {
+    case 2: ND_BANK8B_GO(2); break;
+    case 3: ND_BANK8B_GO(3); break;
+    case 4: ND_BANK8B_GO(4); break;
+    case 5: ND_BANK8B_GO(5); break;
+    default: ND_BANK8B_GO(6); break;
+  }
+#undef ND_BANK8B_GO
   return hipGetLastError();
 }
 

@@ -173,6 +173,7 @@ struct nd_ctx {
   const float* mem = nullptr;             // the bank the decoder reads: mem_p, or x (NanoEncoder)
   bool bank_h3 = false;                   // mem_p holds the split-fp16 fragment bank (dec_bank_h3_kernel)
   bool bank_d8 = false;                   // ... or the 24-bit digit bank (dec_bank_d8_kernel; bank8.hip)
+  bool beam_bank = false;                 // beam rows read the digit bank (dec_bank_d8_beam_kernel), not K/V
   float* bank_ks = nullptr;               // digit bank: per-row scales 2^e_t [B * 512]
   int* bank_em = nullptr;                 // digit bank: per-chunk max e_t (biased) [B]
   int last_bank_form = 0;                 // nd_bank_form
@@ -719,7 +720,9 @@ static hipError_t enqueue_first_embed(nd_ctx* c, int R, hipStream_t s) {
 
 // One decoder step for R = C*rpc rows: dx (embedded input, row stats in
 // dx_part) -> dx (pre final LN).
-static bool use_memory_bank(nd_ctx* c, int rpc) { return c->ctx_path == 0 && rpc * ND_H <= 16 && rpc == 1; }
+// greedy rows always take the memory-bank form (ctx path 0); beam rows when
+// set_memory_view chose the digit bank for them
+static bool use_memory_bank(nd_ctx* c, int rpc) { return c->ctx_path == 0 && (rpc == 1 || c->beam_bank); }
 
 // The decoder's view of the encoder output: a pure function of (ctx path,
 // exact, T, rpc, encoder type).  Set on the host before every call's graphs
@@ -735,10 +738,24 @@ static bool use_bank_d8() {
   return on;
 }
 
+// --fast / classic beam rows on the digit bank (bank8.hip dec_bank_d8_beam_kernel) instead of the
+// per-layer context K/V: ND_BEAM_BANK=1 (off by default: parity-green, but 95.7 against 86.1 ms per
+// pooled configs[3] call).  Not with a capturing call (-attn_debug, coverage
+// penalty): those read the K/V kernel's per-row scores
+static bool use_beam_bank() {
+  static const bool on = [] {
+    const char* e = getenv("ND_BEAM_BANK");
+    return e && atoi(e) != 0;
+  }();
+  return on;
+}
+
 static void set_memory_view(nd_ctx* c, int T, int rpc) {
   c->bank_h3 = false;
   c->bank_d8 = false;
   c->mem = nullptr;
+  c->beam_bank = rpc > 1 && rpc <= 6 && c->ctx_path == 0 && use_beam_bank() && use_bank_d8() && !c->exact &&
+                 !c->attn_on && nd::bank_h3_eligible(T, c->cfg.max_src_len);
   if (!use_memory_bank(c, rpc)) return;
   const bool tf = c->cfg.encoder_type == ND_ENC_TRANSFORMER;
   // 512-sample chunks: the split-fp16 fragment bank (LN'd for the transformer,
@@ -800,9 +817,13 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
     }
     if (mb) {  // memory-bank form (attention.hip)
       const int HD = ND_H * D;
-      // q' row-major for the split-fp16 bank kernel (one row per chunk), P16 for the fp32 one
-      LCHK(dg(c->dq1, D, L.pwqk, HD, D, L.bqk, c->dqk, HD).ln(c->dq1_part, pnq).c_rowmajor(c->bank_h3).run(s));
-      if (c->bank_d8)
+      // q' row-major for the split-fp16 bank kernel (one row per chunk), P16 for the fp32 one and for
+      // beam rows
+      LCHK(dg(c->dq1, D, L.pwqk, HD, D, L.bqk, c->dqk, HD).ln(c->dq1_part, pnq).c_rowmajor(c->bank_h3 && rpc == 1).run(s));
+      if (rpc > 1)
+        LCHK(nd::launch_dec_bank_d8_beam(c->dqk, c->mem_p, c->bank_ks, c->bank_em, c->sig, c->span,
+                                         (float)c->cfg.pad_idx, c->dU, C, rpc, T, done, s, stamp, c->ovf));
+      else if (c->bank_d8)
         LCHK(nd::launch_dec_bank_d8(c->dqk, c->mem_p, c->bank_ks, c->bank_em, c->sig, c->span, (float)c->cfg.pad_idx,
                                     c->dU, C, T, s, stamp, dbg, dbg_stride, c->ovf, c->bank_nt, c->bank_grid));
       else if (c->bank_h3)
@@ -833,7 +854,7 @@ static hipError_t enqueue_memory(nd_ctx* c, int B, int T, int rpc, hipStream_t s
   const bool tf = c->cfg.encoder_type == ND_ENC_TRANSFORMER;
   if (c->bank_d8)
     return nd::launch_bank_pack_d8(c->x, tf ? c->enc_ln_g : nullptr, tf ? c->enc_ln_b : nullptr, c->mem_p, c->bank_ks,
-                                   c->bank_em, B, T, c->ovf, s);
+                                   c->bank_em, c->span, B, T, c->ovf, s);
   if (c->bank_h3)
     return nd::launch_bank_pack_h3(c->x, tf ? c->enc_ln_g : nullptr, tf ? c->enc_ln_b : nullptr,
                                    reinterpret_cast<uint16_t*>(c->mem_p), B, T, c->ovf, s);
@@ -1634,7 +1655,8 @@ static const struct {
                  {"ND_HEAD_FUSE", 1},  {"ND_LSTM_F32", 0},     {"ND_LSTM_LIBM", 0},     {"ND_LSTM_SEQ", 4},
                  {"ND_ENC_ATTN_NQ", 2}, {"ND_ENC_ATTN_GRID", 0}, {"ND_ENC_ATTN_F32", 0}, {"ND_SELF_XCD", 1},
                  {"ND_ENC_WO", 1},     {"ND_ENC_QKV0", 1},
-                 {"ND_ENC_QKV", 1},    {"ND_ENC_ATTN0", 1},   {"ND_SELF_NW8", 1},     {"ND_BANK_D8", 1}};
+                 {"ND_ENC_QKV", 1},    {"ND_ENC_ATTN0", 1},   {"ND_SELF_NW8", 1},     {"ND_BANK_D8", 1},
+                 {"ND_BEAM_BANK", 0}};
 
 int nd_switches(char* buf, int32_t len) {
   std::string out;
@@ -1951,10 +1973,10 @@ int nd_op_dec_bank_h3(const float* qp, const uint16_t* bank, const float* signal
 }
 
 int nd_op_bank_pack_d8(const float* x, const float* ln_g, const float* ln_b, void* bank, float* kscale,
-                       int32_t* kemax, int32_t B, int32_t T, int32_t* ovf, void* stream) {
+                       int32_t* kemax, const int32_t* span, int32_t B, int32_t T, int32_t* ovf, void* stream) {
   if (!x || !bank || !kscale || !kemax || (ln_g == nullptr) != (ln_b == nullptr))
     return fail(ND_ERR_ARG, "bank_pack_d8: bad arguments");
-  hipError_t e = nd::launch_bank_pack_d8(x, ln_g, ln_b, bank, kscale, kemax, B, T, ovf, (hipStream_t)stream);
+  hipError_t e = nd::launch_bank_pack_d8(x, ln_g, ln_b, bank, kscale, kemax, span, B, T, ovf, (hipStream_t)stream);
   if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("bank_pack_d8: ") + hipGetErrorString(e));
   return ND_OK;
 }
@@ -1968,6 +1990,17 @@ int nd_op_dec_bank_d8(const float* qp, const void* bank, const float* kscale, co
   hipError_t e = nd::launch_dec_bank_d8(qp, bank, kscale, kemax, signal, span, pad_val, out, C, T,
                                         (hipStream_t)stream, nullptr, nullptr, 0, ovf, false, grid);
   if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("dec_bank_d8: ") + hipGetErrorString(e));
+  return ND_OK;
+}
+
+int nd_op_dec_bank_d8_beam(const float* qp, const void* bank, const float* kscale, const int32_t* kemax,
+                           const float* signal, const int32_t* span, float pad_val, float* out, int32_t C,
+                           int32_t rpc, int32_t T, const int32_t* done, int32_t* ovf, void* stream) {
+  if (!qp || !bank || !kscale || !kemax || !signal || !span || !out)
+    return fail(ND_ERR_ARG, "dec_bank_d8_beam: bad arguments");
+  hipError_t e = nd::launch_dec_bank_d8_beam(qp, bank, kscale, kemax, signal, span, pad_val, out, C, rpc, T, done,
+                                             (hipStream_t)stream, nullptr, ovf);
+  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("dec_bank_d8_beam: ") + hipGetErrorString(e));
   return ND_OK;
 }
 

@@ -241,11 +241,16 @@ hipError_t init_mem_attributes();
 // 24-bit fixed-point memory bank (bank8.hip): digits in bank (B * 512 * 256 * 3
 // bytes), per-row scales kscale [B * 512], per-chunk biased max exponent kemax [B]
 hipError_t launch_bank_pack_d8(const float* x, const float* ln_g, const float* ln_b, void* bank, float* kscale,
-                               int* kemax, int B, int T, int* ovf, hipStream_t s);
+                               int* kemax, const int* span, int B, int T, int* ovf, hipStream_t s);
 hipError_t launch_dec_bank_d8(const float* qp, const void* bank, const float* kscale, const int* kemax,
                               const float* signal, const int* span, float pad_val, float* out, int C, int T,
                               hipStream_t s, unsigned long long* stamp, float* attn_dbg, size_t dbg_stride, int* ovf,
                               bool nt = false, int grid = 0);
+// --fast beam rows on the same bank: rows c * rpc + j (rpc 2..6) of q' [C * rpc, 2048] P16 -> U P16;
+// chunks with done[c] != 0 skipped (done nullable)
+hipError_t launch_dec_bank_d8_beam(const float* qp, const void* bank, const float* kscale, const int* kemax,
+                                   const float* signal, const int* span, float pad_val, float* out, int C, int rpc,
+                                   int T, const int* done, hipStream_t s, unsigned long long* stamp, int* ovf);
 hipError_t init_bank8_attributes();
 // signal front end (frontend.hip): per-read normalisation (method 0 none, 1
 // median/MAD, 2 median/std; fp64 math, float32 out) of reads concatenated at

@@ -631,17 +631,18 @@ def op_dec_bank_h3(qp, bank, signal, span, pad_val, out=None, ovf=None, grid=0):
     return out
 
 
-def op_bank_pack_d8(x, B, T, ln_g=None, ln_b=None, ovf=None):
+def op_bank_pack_d8(x, B, T, ln_g=None, ln_b=None, ovf=None, span=None):
     """24-bit digit bank (nd_op_bank_pack_d8): x [B*T, 256] -> (digits uint8
     [B * 512 * 256 * 3], row scales [B * 512], each chunk's largest row scale
-    [B] as float bits in int32)."""
+    [B] as float bits in int32).  span [B] int32 (optional): rows at or past a
+    chunk's span are zero."""
     dev = x.device
     bank = torch.empty(B * 512 * 256 * 3, dtype=torch.uint8, device=dev)
     ks = torch.empty(B * 512, dtype=torch.float32, device=dev)
     em = torch.empty(B, dtype=torch.int32, device=dev)
     s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-    _lib.check(_lib.lib().nd_op_bank_pack_d8(_ptr(x), _ptr(ln_g), _ptr(ln_b), _ptr(bank), _ptr(ks), _ptr(em), B, T,
-                                             _ptr(ovf), s), "nd_op_bank_pack_d8")
+    _lib.check(_lib.lib().nd_op_bank_pack_d8(_ptr(x), _ptr(ln_g), _ptr(ln_b), _ptr(bank), _ptr(ks), _ptr(em),
+                                             _ptr(span), B, T, _ptr(ovf), s), "nd_op_bank_pack_d8")
     return bank, ks, em
 
 
@@ -657,6 +658,22 @@ def op_dec_bank_d8(qp, bank, signal, span, pad_val, out=None, ovf=None, grid=0):
     _lib.check(_lib.lib().nd_op_dec_bank_d8(_ptr(qp), _ptr(digits), _ptr(ks), _ptr(em), _ptr(signal), _ptr(span),
                                             float(pad_val), _ptr(out), C, T, _ptr(ovf), int(grid), s),
                "nd_op_dec_bank_d8")
+    return out
+
+
+def op_dec_bank_d8_beam(qp, bank, signal, span, pad_val, rpc, out=None, done=None, ovf=None):
+    """Beam rows on the 24-bit digit bank (nd_op_dec_bank_d8_beam): qp [C*rpc, 2048]
+    in the P16 layout (pack_p16), rows c*rpc + j of chunk c; returns U [R16, 2048] packed."""
+    C, T = signal.shape
+    digits, ks, em = bank
+    R = C * rpc
+    if out is None:
+        out = torch.zeros((R + 15) // 16 * 16, qp.shape[1], dtype=torch.float32, device=qp.device)
+    s = ctypes.c_void_p(torch.cuda.current_stream(qp.device).cuda_stream)
+    _lib.check(_lib.lib().nd_op_dec_bank_d8_beam(_ptr(qp), _ptr(digits), _ptr(ks), _ptr(em), _ptr(signal),
+                                                 _ptr(span), float(pad_val), _ptr(out), C, int(rpc), T, _ptr(done),
+                                                 _ptr(ovf), s),
+               "nd_op_dec_bank_d8_beam")
     return out
 
 

@@ -381,13 +381,15 @@ def test_bank_d8_vs_fp64(T, ln, grid):
     dev = torch.device("cuda", 0)
     xt = torch.from_numpy(x).to(dev)
     ovf = torch.zeros(1, dtype=torch.int32, device=dev)
+    span_d = torch.from_numpy(spans).to(dev)
     if ln:
-        bank = op_bank_pack_d8(xt, C, T, torch.from_numpy(g).to(dev), torch.from_numpy(b).to(dev), ovf=ovf)
+        bank = op_bank_pack_d8(xt, C, T, torch.from_numpy(g).to(dev), torch.from_numpy(b).to(dev), ovf=ovf,
+                               span=span_d)
         mu = x.mean(1, keepdims=True)
         var = ((x - mu) ** 2).mean(1, keepdims=True)
         xm = ((x - mu) / np.sqrt(var + 1e-6) * g + b).astype(np.float64)
     else:
-        bank = op_bank_pack_d8(xt, C, T, ovf=ovf)
+        bank = op_bank_pack_d8(xt, C, T, ovf=ovf, span=span_d)
         xm = x.astype(np.float64)
     out = op_dec_bank_d8(torch.from_numpy(q).to(dev), bank, torch.from_numpy(sig).to(dev),
                          torch.from_numpy(spans).to(dev), PAD, ovf=ovf, grid=grid)
@@ -403,6 +405,66 @@ def test_bank_d8_vs_fp64(T, ln, grid):
             want = (p / p.sum()) @ M
             err = np.abs(got[c, h * 256:(h + 1) * 256] - want).max()
             assert err < 2e-5 * max(1.0, np.abs(want).max()), (c, h, L, err)
+
+
+@pytest.mark.parametrize("rpc", [2, 5, 6])
+def test_bank_d8_beam_vs_fp64(rpc):
+    """Beam rows on the digit bank (dec_bank_d8_beam_kernel: the rpc rows of a
+    chunk share one pass over its bank) against fp64 softmax(q' M^T) M per row
+    and head: ragged spans (1, 15, 16, 17, a partial last key block), pad-masked
+    keys, an all-masked chunk, running-maximum rescales in some rows only, a
+    head a thousand times the others, a zero row of q', and finished chunks
+    (done != 0: their rows untouched).  Tolerance as the greedy digit bank."""
+    from nanodecoder_amd.engine import op_bank_pack_d8, op_dec_bank_d8_beam, pack_p16, unpack_p16
+    rng = np.random.default_rng(17 + rpc)
+    C, T, PAD = 10, 512, 1.0
+    spans = np.array([T, 1, 15, 16, 17, 300, T, T - 3, 200, T], np.int32)
+    sig = rng.standard_normal((C, T)).astype(np.float32)
+    sig[3, ::4] = PAD
+    sig[6, :] = PAD
+    x = rng.standard_normal((C * T, 256)).astype(np.float32)
+    x[9 * T + 450] *= 5.0                      # a late key far above the first blocks' maximum
+    x[5 * T: 6 * T: 2] *= 1e-3
+    x[4 * T + 17:5 * T] = 1e30                 # rows past a span (never attended; the encoder leaves them
+    x[8 * T + 200:9 * T] = np.nan              # unspecified) must not set the chunk's scale or trip ovf
+    R = C * rpc
+    q = (rng.standard_normal((R, 2048)) * 0.3).astype(np.float32)
+    q[9 * rpc] *= 8.0                          # this row rescales; its chunk's other rows less so
+    q[2 * rpc + 1, 2 * 256:3 * 256] *= 1e3
+    q[7 * rpc + rpc - 1] = 0.0                 # a zero row: uniform weights
+    done = np.zeros(C, np.int32)
+    done[8] = 1
+    g = (rng.random(256) + 0.5).astype(np.float32)
+    b = (rng.standard_normal(256) * 0.1).astype(np.float32)
+    dev = torch.device("cuda", 0)
+    ovf = torch.zeros(1, dtype=torch.int32, device=dev)
+    bank = op_bank_pack_d8(torch.from_numpy(x).to(dev), C, T, torch.from_numpy(g).to(dev),
+                           torch.from_numpy(b).to(dev), ovf=ovf, span=torch.from_numpy(spans).to(dev))
+    qp = pack_p16(torch.from_numpy(q).to(dev))
+    out = op_dec_bank_d8_beam(qp, bank, torch.from_numpy(sig).to(dev), torch.from_numpy(spans).to(dev), PAD, rpc,
+                              done=torch.from_numpy(done).to(dev), ovf=ovf)
+    torch.cuda.synchronize()
+    got = unpack_p16(out, R).cpu().numpy()
+    assert int(ovf.item()) == 0
+    with np.errstate(invalid="ignore", over="ignore"):
+        mu = x.mean(1, keepdims=True)
+        var = ((x - mu) ** 2).mean(1, keepdims=True)
+        xm = ((x - mu) / np.sqrt(var + 1e-6) * g + b).astype(np.float64)
+    for c in range(C):
+        L = int(spans[c])
+        M = xm[c * T: c * T + L]
+        for j in range(rpc):
+            r = c * rpc + j
+            if done[c]:
+                assert not got[r].any(), (c, j)
+                continue
+            for h in range(8):
+                s = M @ q[r, h * 256:(h + 1) * 256].astype(np.float64)
+                s[sig[c, :L] == PAD] = -1e18
+                p = np.exp(s - s.max())
+                want = (p / p.sum()) @ M
+                err = np.abs(got[r, h * 256:(h + 1) * 256] - want).max()
+                assert err < 2e-5 * max(1.0, np.abs(want).max()), (c, j, h, L, err)
 
 
 def test_engine_reports_bank_form():
