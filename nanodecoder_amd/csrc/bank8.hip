@@ -466,18 +466,25 @@ hipError_t launch_dec_bank_d8(const float* qp, const void* bank, const float* ks
 //    (waves 0..5 copy two fragments each), two blocks ahead; slots are 1152 B
 //    apart so the a2 and a1 planes of a dim block sit on opposite bank halves
 //    for the transposed reads.
-//  - Scores: wave j < RPC owns row j (its q' digits in registers, computed
-//    straight from the P16 q' rows) and runs the greedy form's five i8
-//    products per 64 dims on the block from LDS, its lazy online softmax per
-//    head, and hands P (hi | lo f16 rows, the U A-operand layout) plus any
-//    rescale factors to LDS.
-//  - Context: every wave owns two 16-dim blocks of U for ALL rows, converts
-//    only those digits (tr_b8 + the exact f16 conversion) and runs the greedy
-//    form's two f16 products per row: no U merge across waves, the digits of
-//    a block converted once per workgroup.
+//  - Scores: wave p < ceil(RPC / 2) owns the row pair (2p, 2p + 1): its 16
+//    MFMA columns are (row 2p + (col >> 3), head col & 7), so every column
+//    carries a score (the one-row form duplicates each head over a column
+//    pair).  Eight i8 products per 64 dims on the block from LDS, grouped by
+//    digit weight into four exact int32 sums: a2 q2 (2^16); a2 q1 + a1 q2
+//    (2^8); a2 q0 + a1 q1 + a0 q2 (1); a1 q0 + a0 q1 (2^-8) -- the digit
+//    products the greedy form keeps (only a0 q0 dropped).  Then the lazy
+//    online softmax per column and P (hi | lo f16, the U A-operand layout) and
+//    the rescale factors to LDS.
+//  - Context: every wave owns two 16-dim blocks of U for ALL rows (row pair
+//    b = MFMA rows 0..15 of accumulator block b), converts only those digits
+//    (tr_b8 + the exact f16 conversion) and runs two 16x16x32 products
+//    ([hi | lo] against [a2 | a2] and [a1 | a1]) and one 16x16x16 (hi against
+//    a0) per pair: no U merge across waves, the digits of a block converted
+//    once per workgroup.
 // Output U [C * RPC, 2048] P16 (row c * RPC + j), as dec_bank_d8_kernel's.
 #define BB_NW 8
 #define BB_MAXR 6
+#define BB_MAXP 3                          // row pairs
 #ifndef BB_WPE
 #define BB_WPE 4                           // waves per SIMD: two workgroups per CU (128 VGPRs)
 #endif
@@ -486,10 +493,10 @@ hipError_t launch_dec_bank_d8(const float* qp, const void* bank, const float* ks
 #define BB_NBUF 3                          // ring slots
 #define BB_KS (BB_NBUF * BB_BLK)           // [512] row scales s_t
 #define BB_PM (BB_KS + 512 * 4)            // [512] pad flags (bytes)
-#define BB_P (BB_PM + 512)                 // [row][64 lanes] P fragments, 8 B each
-#define BB_SC (BB_P + BB_MAXR * 512)       // [row][8 heads] rescale factors of the current block
-#define BB_FIN (BB_SC + BB_MAXR * 8 * 4)   // [row][8 heads] output scales 2 s_max / l
-#define BB_LDS (BB_FIN + BB_MAXR * 8 * 4)
+#define BB_P (BB_PM + 512)                 // [pair][4 key groups][16 columns] P hi x 4 | lo x 4 (16 B)
+#define BB_SC (BB_P + BB_MAXP * 1024)      // [pair][16 columns] rescale factors of the current block
+#define BB_FIN (BB_SC + BB_MAXP * 16 * 4)  // [pair][16 columns] output scales 2 s_max / l
+#define BB_LDS (BB_FIN + BB_MAXP * 16 * 4)
 static_assert(BB_LDS <= 65536, "beam bank LDS within 64 KB (DESIGN.md section 5, co-residency rule)");
 
 template <int RPC>
@@ -497,6 +504,7 @@ __device__ __forceinline__ void bank_d8_beam_chunk(char* lb, int c, const float*
                                                    const float* __restrict__ kscale, const int* __restrict__ kemax,
                                                    const float* __restrict__ signal, const int* __restrict__ span,
                                                    float pad_val, float* __restrict__ out, int T, int* ovf) {
+  constexpr int NP = (RPC + 1) / 2;  // row pairs = score waves = U accumulator blocks
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int col = lane & 15, g = lane >> 4;
@@ -517,27 +525,29 @@ __device__ __forceinline__ void bank_d8_beam_chunk(char* lb, int c, const float*
       }
     }
   };
-  // ---- prologue: row j = w's q' (P16 [R][2048]; lane: head col & 7, dims 64 db + 16 g + 4 i ..), the
-  //      chunk's row scales and pad flags (one key per thread), then the first two key blocks
-  const int r = c * RPC + w;
-  // the first two key blocks, then every prologue load at once (one memory round trip)
+  // ---- prologue: the first two key blocks, then every prologue load at once (one memory round trip):
+  //      this lane's q' (row 2 w + (col >> 3), head col & 7, dims 64 db + 16 g + 4 i ..; P16 [R][2048]),
+  //      the chunk's row scales and pad flags (one key per thread)
+  const int jq = 2 * w + (col >> 3);  // this lane's row (score waves)
+  const bool rowq = w < NP && jq < RPC;
   if (nkb > 0) issue(0);
   if (nkb > 1) issue(1);
-  const float* qrow = qp + pk(r, (col & 7) * ND_D + 16 * g, ND_H * ND_D);  // + pk offsets of 64 db + 4 i
+  const float* qrow = qp + pk(c * RPC + (rowq ? jq : 0), (col & 7) * ND_D + 16 * g, ND_H * ND_D);
   f32x4 qv[16];
-  if (w < RPC) {
+  if (w < NP) {
 #pragma unroll
-    for (int k = 0; k < 16; ++k) qv[k] = ld4(qrow + pk(0, 64 * (k >> 2) + 4 * (k & 3), ND_H * ND_D));
+    for (int k = 0; k < 16; ++k)
+      qv[k] = rowq ? ld4(qrow + pk(0, 64 * (k >> 2) + 4 * (k & 3), ND_H * ND_D)) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
   const int tk = threadIdx.x;  // 512 threads, 512 keys
   const float ksv = kscale[(size_t)c * 512 + tk];
   const float sgv = signal[(size_t)c * T + min(tk, T - 1)];
   reinterpret_cast<float*>(lb + BB_KS)[tk] = ksv;
   reinterpret_cast<unsigned char*>(lb + BB_PM)[tk] = (tk < T && sgv == pad_val) ? 1 : 0;
-  // B operands of the scores (as dec_bank_d8_kernel's qb1 / qb2): B1 = q2 (col < 8) | q1, B2 = 0 | q0
-  i32x4 qb1[4], qb2[4];
+  // B operands of the scores: the three digit planes of this lane's column
+  i32x4 qd[3][4];
   float sgm = 0.f;
-  if (w < RPC) {
+  if (w < NP) {
     float mx = 0.f;
 #pragma unroll
     for (int k = 0; k < 16; ++k) mx = fmaxf(mx, absmax4(qv[k]));
@@ -549,20 +559,21 @@ __device__ __forceinline__ void bank_d8_beam_chunk(char* lb, int c, const float*
     sgm = qs * 65536.0f;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-      unsigned u1 = 0u, u2 = 0u;
+      unsigned u2 = 0u, u1 = 0u, u0 = 0u;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         int d2, d1, d0;
         digits((int)rintf(qv[k][e] / qdiv), d2, d1, d0);
-        u1 |= (unsigned)((col < 8 ? d2 : d1) & 255) << (8 * e);
-        u2 |= (unsigned)((col < 8 ? 0 : d0) & 255) << (8 * e);
+        u2 |= (unsigned)(d2 & 255) << (8 * e);
+        u1 |= (unsigned)(d1 & 255) << (8 * e);
+        u0 |= (unsigned)(d0 & 255) << (8 * e);
       }
-      qb1[k >> 2][k & 3] = (int)u1;
-      qb2[k >> 2][k & 3] = (int)u2;
+      qd[2][k >> 2][k & 3] = (int)u2;
+      qd[1][k >> 2][k & 3] = (int)u1;
+      qd[0][k >> 2][k & 3] = (int)u0;
       __builtin_amdgcn_sched_barrier(0);  // four values at a time (the divisions' temporaries)
     }
   }
-  const float w1 = col < 8 ? 65536.0f : 256.0f, w3 = col < 8 ? 256.0f : 1.0f, w4 = col < 8 ? 1.0f : 0.00390625f;
   const float kp = smax > 0.f ? 128.0f / smax : 0.f;  // P scale: p s_t 2^7 / s_max
   // ---- this wave's U dim blocks 2w, 2w + 1 (dim block db_u, 16-dim groups G0, G0 + 1) in the transposed
   //      reads: lane 2q + p of its group supplies row q (keys 4 g + (q & 3); planes a2 | a1, or a0 of G0 | G0 + 1)
@@ -570,16 +581,11 @@ __device__ __forceinline__ void bank_d8_beam_chunk(char* lb, int c, const float*
   const int q8 = (lane & 15) >> 1, p8 = lane & 1;
   const int o1 = (db_u * 3 + (q8 < 4 ? 2 : 1)) * BB_FR + (4 * g + (q8 & 3) + 16 * G0) * 16 + 8 * p8;
   const int o3 = db_u * 3 * BB_FR + (4 * g + (q8 & 3) + 16 * (G0 + (q8 < 4 ? 0 : 1))) * 16 + 8 * p8;
-  // U accumulators: row block b holds rows 2b (MFMA rows 0..7, head = row) and 2b + 1 (rows 8..15); P's
-  // hi and lo parts ride in the K dimension against the same digits twice
-  constexpr int NB = (RPC + 1) / 2;
-  f32x4 ua[NB][2];
+  // U accumulators: block b = row pair b (MFMA rows = columns of the pair's scores); P's hi and lo parts
+  // ride in the K dimension against the same digits twice
+  f32x4 ua[NP][2];
 #pragma unroll
-  for (int b = 0; b < NB; ++b) ua[b][0] = ua[b][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (RPC & 1) {  // the last block's second row does not exist: zero P rows, unit rescale factors
-    if (threadIdx.x < 32) reinterpret_cast<f32x4*>(lb + BB_P + RPC * 512)[threadIdx.x] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (threadIdx.x < 8) reinterpret_cast<float*>(lb + BB_SC)[RPC * 8 + threadIdx.x] = 1.0f;
-  }
+  for (int b = 0; b < NP; ++b) ua[b][0] = ua[b][1] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m = -INFINITY, l = 0.f;
 
   for (int kb = 0; kb < nkb; ++kb) {
@@ -591,12 +597,12 @@ __device__ __forceinline__ void bank_d8_beam_chunk(char* lb, int c, const float*
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     if (kb + 2 < nkb) issue(kb + 2);
     const char* buf = lb + (kb % BB_NBUF) * BB_BLK;
-    if (w < RPC) {
-      // ---- scores of row w: columns h and h + 8 hold the high and low digit products of head h
-      // X3 takes a1 B1 + a2 B2 (columns < 8: a2 B2 = 0; columns >= 8: both weight 1)
-      i32x4 X1 = {0, 0, 0, 0}, X3 = X1, X4 = X1;
+    if (w < NP) {
+      // ---- scores of row pair w, grouped by digit weight (x 2^-16): X1 2^16, X2 2^8, X3 1, X4 2^-8
+      i32x4 X1 = {0, 0, 0, 0}, X2 = X1, X3 = X1, X4 = X1;
       const char* fb = buf + lane * 16;
-      // one dim block's three planes in flight beside the previous block's products (24 registers)
+      // the next dim block's fragments load under this one's products; the products alternate between
+      // the four accumulators (a dependent MFMA waits for its predecessor's result)
       i32x4 fr[2][3];
       auto fload = [&](int db, i32x4(&f)[3]) {
 #pragma unroll
@@ -606,25 +612,27 @@ __device__ __forceinline__ void bank_d8_beam_chunk(char* lb, int c, const float*
 #pragma unroll
       for (int db = 0; db < 4; ++db) {
         if (db < 3) fload(db + 1, fr[(db + 1) & 1]);
-        __builtin_amdgcn_sched_barrier(0);
         const i32x4(&f)[3] = fr[db & 1];
-        X1 = mfma_i8(f[2], qb1[db], X1);
-        X3 = mfma_i8(f[2], qb2[db], X3);
-        X3 = mfma_i8(f[1], qb1[db], X3);
-        X4 = mfma_i8(f[0], qb1[db], X4);
-        X4 = mfma_i8(f[1], qb2[db], X4);
-        __builtin_amdgcn_sched_barrier(0);
+        X1 = mfma_i8(f[2], qd[2][db], X1);
+        X2 = mfma_i8(f[2], qd[1][db], X2);
+        X3 = mfma_i8(f[2], qd[0][db], X3);
+        X4 = mfma_i8(f[1], qd[0][db], X4);
+        X2 = mfma_i8(f[1], qd[2][db], X2);
+        X3 = mfma_i8(f[1], qd[1][db], X3);
+        X4 = mfma_i8(f[0], qd[1][db], X4);
+        X3 = mfma_i8(f[0], qd[2][db], X3);
+        __builtin_amdgcn_sched_barrier(0);  // two dim blocks' fragments live at most (registers)
       }
       const f32x4 ks4 = *reinterpret_cast<const f32x4*>(lb + BB_KS + (16 * kb + 4 * g) * 4);
       const unsigned pf = *reinterpret_cast<const unsigned*>(lb + BB_PM + 16 * kb + 4 * g);
-      f32x4 s;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) s[i] = (float)X1[i] * w1 + (float)X3[i] * w3 + (float)X4[i] * w4;
       const int kbase = 16 * kb + 4 * g;  // key of row i
+      f32x4 s;
       float gm = -INFINITY;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        s[i] = (s[i] + dpp_mov<0x128>(s[i])) * (ks4[i] * sgm);
+        const float v = fmaf((float)X1[i], 65536.0f, fmaf((float)X2[i], 256.0f, fmaf((float)X4[i], 0.00390625f,
+                                                                                   (float)X3[i])));
+        s[i] = v * (ks4[i] * sgm);
         s[i] = kbase + i < L ? (((pf >> (8 * i)) & 1u) ? ND_MASK_FILL : s[i]) : -INFINITY;
         gm = fmaxf(gm, s[i]);
       }
@@ -637,13 +645,13 @@ __device__ __forceinline__ void bank_d8_beam_chunk(char* lb, int c, const float*
         m = nm;
         l *= sc;
       }
-      // every block (1 when this row did not rescale): the row blocks rescale unconditionally
-      if (g == 0 && col < 8) reinterpret_cast<float*>(lb + BB_SC)[w * 8 + col] = sc;
+      // every block (1 when this column did not rescale): the accumulators rescale unconditionally
+      if (g == 0) reinterpret_cast<float*>(lb + BB_SC)[w * 16 + col] = sc;
       f32x4 p;
 #pragma unroll
       for (int i = 0; i < 4; ++i) p[i] = s[i] == -INFINITY ? 0.f : __expf(s[i] - m);
       l += (p[0] + p[1]) + (p[2] + p[3]);
-      // the U A operand of head col (< 8), keys 4 g .. 4 g + 3: hi x 4 | lo x 4 at P[row][g][head]
+      // the U A operand of column col, keys 4 g .. 4 g + 3: hi x 4 | lo x 4 at P[pair][g][col]
       d8h8 pa;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -652,10 +660,10 @@ __device__ __forceinline__ void bank_d8_beam_chunk(char* lb, int c, const float*
         pa[i] = hi;
         pa[4 + i] = (_Float16)(x - (float)hi);
       }
-      if (col < 8) *reinterpret_cast<d8h8*>(lb + BB_P + w * 512 + (g * 8 + col) * 16) = pa;
+      *reinterpret_cast<d8h8*>(lb + BB_P + w * 1024 + (g * 16 + col) * 16) = pa;
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // P, rescale factors visible
-    // ---- U += P^T M' for every row on this wave's two dim blocks
+    // ---- U += P^T M' for every row pair on this wave's two dim blocks
     const d8u2 r1 = tr_b8(buf + o1), r2 = tr_b8(buf + o1 + 256), r3 = tr_b8(buf + o3);
     const d8h4 c2a = d8_cvt(r1.x, 2), c1a = d8_cvt(r1.y, 1), c2b = d8_cvt(r2.x, 2), c1b = d8_cvt(r2.y, 1);
     const d8h8 b2a = {c2a[0], c2a[1], c2a[2], c2a[3], c2a[0], c2a[1], c2a[2], c2a[3]};  // [a2 | a2] 2^8
@@ -664,40 +672,36 @@ __device__ __forceinline__ void bank_d8_beam_chunk(char* lb, int c, const float*
     const d8h8 b1b = {c1b[0], c1b[1], c1b[2], c1b[3], c1b[0], c1b[1], c1b[2], c1b[3]};
     const d8h4 b0a = d8_cvt(r3.x, 0), b0b = d8_cvt(r3.y, 0);  // a0 2^-8 (the hi parts only)
 #pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      // the running-maximum rescale, every block (factor 1 when the row did not rescale).  Branch-free on
-      // purpose: a branch around these multiplies gave wrong components 0, 1 of ua[b][1] on gfx950
-      // (tools/bb_debug.py; cause not isolated, the unconditional form is exact)
-      // accumulator rows 4 g + i: row 2 b + (g >> 1), head 4 (g & 1) + i
-      {
-        const f32x4 sc4 = *reinterpret_cast<const f32x4*>(lb + BB_SC + (2 * b + (g >> 1)) * 32 + 16 * (g & 1));
-        ua[b][0] *= sc4;
-        ua[b][1] *= sc4;
-      }
-      // A operand row col: row 2 b + (col >> 3), head col & 7
-      const d8h8 pa = *reinterpret_cast<const d8h8*>(lb + BB_P + (2 * b + (col >> 3)) * 512 + (g * 8 + (col & 7)) * 16);
+    for (int b = 0; b < NP; ++b) {
+      // the running-maximum rescale, every block (factor 1 when the column did not rescale).  Branch-free
+      // on purpose: a branch around these multiplies gave wrong components 0, 1 of the second dim
+      // block's accumulator on gfx950 (tools/bb_debug.py; cause not isolated, this form is exact).
+      // Accumulator rows 4 g + i = columns 4 g + i of the pair's scores
+      const f32x4 sc4 = *reinterpret_cast<const f32x4*>(lb + BB_SC + b * 64 + 16 * g);
+      ua[b][0] *= sc4;
+      ua[b][1] *= sc4;
+      const d8h8 pa = *reinterpret_cast<const d8h8*>(lb + BB_P + b * 1024 + (g * 16 + col) * 16);
       const d8h4 ph = {pa[0], pa[1], pa[2], pa[3]};
       ua[b][0] = mfma_d8h32(pa, b2a, ua[b][0]);
-      ua[b][0] = mfma_d8h32(pa, b1a, ua[b][0]);
-      ua[b][0] = mfma_d8h16(ph, b0a, ua[b][0]);
       ua[b][1] = mfma_d8h32(pa, b2b, ua[b][1]);
+      ua[b][0] = mfma_d8h32(pa, b1a, ua[b][0]);
       ua[b][1] = mfma_d8h32(pa, b1b, ua[b][1]);
+      ua[b][0] = mfma_d8h16(ph, b0a, ua[b][0]);
       ua[b][1] = mfma_d8h16(ph, b0b, ua[b][1]);
     }
   }
-  // ---- output scales 2 s_max / l per (row, head); U [row][h * 256 + d] P16
-  if (w < RPC) {
+  // ---- output scales 2 s_max / l per column; U [row][h * 256 + d] P16
+  if (w < NP) {
     l = xor32_sum(xor16_sum(l));
-    if (g == 0 && col < 8)
-      reinterpret_cast<float*>(lb + BB_FIN)[w * 8 + col] = l > 0.f ? __builtin_amdgcn_rcpf(l) * (2.0f * smax) : 0.f;
+    if (g == 0)
+      reinterpret_cast<float*>(lb + BB_FIN)[w * 16 + col] = l > 0.f ? __builtin_amdgcn_rcpf(l) * (2.0f * smax) : 0.f;
   }
   __syncthreads();
-  const int jl = 2 * 0 + (g >> 1);  // this lane's row within a block
 #pragma unroll
-  for (int b = 0; b < NB; ++b) {
-    const int j = 2 * b + jl;
+  for (int b = 0; b < NP; ++b) {
+    const int j = 2 * b + (g >> 1);  // accumulator rows 4 g + i: row 2 b + (g >> 1), head 4 (g & 1) + i
     if (j < RPC) {
-      const f32x4 fs = *reinterpret_cast<const f32x4*>(lb + BB_FIN + j * 32 + 16 * (g & 1));
+      const f32x4 fs = *reinterpret_cast<const f32x4*>(lb + BB_FIN + b * 64 + 16 * g);
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         const int d = 16 * (2 * w + kk) + col;

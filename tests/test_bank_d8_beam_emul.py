@@ -78,85 +78,79 @@ def tr_b8(img, addr):
 
 def emulate(m, q_rows, L):
     """One chunk, RPC = len(q_rows) rows (no masks): the kernel's arithmetic in float64 where it is exact,
-    float32 / float16 where the kernel rounds."""
+    float32 / float16 where the kernel rounds.  Score wave p owns rows (2p, 2p + 1): column col = (row
+    2p + (col >> 3), head col & 7)."""
     RPC = len(q_rows)
+    NP = (RPC + 1) // 2
     blocks, s = pack_bank(m)
     smax = np.float32(s.max())
     kp = np.float32(128.0) / smax
     lanes = np.arange(64)
     col, g = lanes & 15, lanes >> 4
-    # q digits, B operands per row (qb1, qb2 [db][lane] 16 bytes)
-    qb = []
-    sgm = []
-    for q in q_rows:
-        Q = np.zeros((8, 256), np.int64)
-        sg = np.zeros(8, np.float32)
-        for h in range(8):
-            qh = q[h * 256:(h + 1) * 256].astype(np.float32)
+    qd, sgm = [], []  # per pair: [plane][db][lane] 16 digit bytes; sigma per lane
+    for pr in range(NP):
+        Qd = np.zeros((3, 4, 64, 16), np.int64)
+        sg = np.zeros(64, np.float32)
+        for l in range(64):
+            j, h, gq = 2 * pr + ((l & 15) >> 3), l & 7, l >> 4
+            if j >= RPC:
+                continue
+            qh = q_rows[j, h * 256:(h + 1) * 256].astype(np.float32)
             qs = np.float32(np.abs(qh).max() * np.float32(1 / AMAX))
-            Q[h] = np.rint(qh / (qs if qs > 0 else np.float32(1))).astype(np.int64)
-            sg[h] = qs * np.float32(65536)
-        q2, q1, q0 = digits(Q)
-        b1 = np.zeros((4, 64, 16), np.int64)
-        b2 = np.zeros((4, 64, 16), np.int64)
-        for db in range(4):
-            for l in range(64):
-                h, gq = l & 7, l >> 4
+            Q = np.rint(qh / (qs if qs > 0 else np.float32(1))).astype(np.int64)
+            q2, q1, q0 = digits(Q)
+            for db in range(4):
                 sl = slice(64 * db + 16 * gq, 64 * db + 16 * gq + 16)
-                b1[db, l] = (q2 if (l & 15) < 8 else q1)[h, sl] & 255
-                b2[db, l] = 0 if (l & 15) < 8 else (q0[h, sl] & 255)
-        qb.append((b1, b2))
-        sgm.append(sg[col & 7])
-    w1 = np.where(col < 8, 65536.0, 256.0)
-    w3 = np.where(col < 8, 256.0, 1.0)
-    w4 = np.where(col < 8, 1.0, 1 / 256)
-    NB = (RPC + 1) // 2
-    U = np.zeros((NB, 16, 16, 16))  # [row block][16-dim block] D[row][col]
-    mrow = [np.full(64, -np.inf) for _ in range(RPC)]
-    lrow = [np.zeros(64) for _ in range(RPC)]
+                Qd[2, db, l], Qd[1, db, l], Qd[0, db, l] = q2[sl] & 255, q1[sl] & 255, q0[sl] & 255
+            sg[l] = qs * np.float32(65536)
+        qd.append(Qd)
+        sgm.append(sg)
+    U = np.zeros((NP, 16, 16, 16))  # [pair][16-dim block] D[row][col]
+    mrow = [np.full(64, -np.inf) for _ in range(NP)]
+    lrow = [np.zeros(64) for _ in range(NP)]
     nkb = (L + 15) // 16
     for kb in range(nkb):
         img = lds_image(blocks[kb])
-        P = np.zeros((6, 4, 8, 8))  # [row][g][head][hi x4 | lo x4]
-        SC = np.ones((6, 8))
-        FL = np.zeros(6, bool)
-        for j in range(RPC):
-            fb = lambda f: np.stack([img[f * FR + 16 * l: f * FR + 16 * l + 16] for l in range(64)])
-            X1 = sum(mfma_i8(fb(db * 3 + 2), qb[j][0][db]) for db in range(4))
-            X3 = sum(mfma_i8(fb(db * 3 + 2), qb[j][1][db]) + mfma_i8(fb(db * 3 + 1), qb[j][0][db]) for db in range(4))
-            X4 = sum(mfma_i8(fb(db * 3), qb[j][0][db]) + mfma_i8(fb(db * 3 + 1), qb[j][1][db]) for db in range(4))
+        P = np.zeros((NP, 4, 16, 8))  # [pair][g][col][hi x4 | lo x4]
+        SC = np.ones((NP, 16))
+        fb = lambda f: np.stack([img[f * FR + 16 * l: f * FR + 16 * l + 16] for l in range(64)])
+        for pr in range(NP):
+            X = np.zeros((4, 16, 16), np.int64)
+            for db in range(4):
+                a2, a1, a0 = fb(db * 3 + 2), fb(db * 3 + 1), fb(db * 3)
+                Q2, Q1, Q0 = qd[pr][2, db], qd[pr][1, db], qd[pr][0, db]
+                X[0] += mfma_i8(a2, Q2)
+                X[1] += mfma_i8(a2, Q1) + mfma_i8(a1, Q2)
+                X[2] += mfma_i8(a2, Q0) + mfma_i8(a1, Q1) + mfma_i8(a0, Q2)
+                X[3] += mfma_i8(a1, Q0) + mfma_i8(a0, Q1)
             sv = np.zeros((64, 4))
             for l in range(64):
                 for i in range(4):
                     r = 4 * (l >> 4) + i
-                    sv[l, i] = X1[r, l & 15] * w1[l] + X3[r, l & 15] * w3[l] + X4[r, l & 15] * w4[l]
+                    sv[l, i] = X[0, r, l & 15] * 65536.0 + X[1, r, l & 15] * 256.0 + X[2, r, l & 15] \
+                        + X[3, r, l & 15] / 256.0
             ks4 = np.stack([s[16 * kb + 4 * (l >> 4): 16 * kb + 4 * (l >> 4) + 4] for l in range(64)])
-            sv = (sv + sv[(lanes & 48) | ((lanes + 8) & 15)]) * (ks4 * sgm[j][:, None])
+            sv = sv * (ks4 * sgm[pr][:, None])
             keys = 16 * kb + 4 * g[:, None] + np.arange(4)[None, :]
             sv = np.where(keys < L, sv, -np.inf)
             gm = sv.max(1)
             gm = np.array([gm[(lanes & 15) == (l & 15)].max() for l in range(64)])
-            if np.any(gm > mrow[j] + 6):
-                nm = np.maximum(mrow[j], gm)
-                sc = np.where(nm == mrow[j], 1.0, np.exp(mrow[j] - nm))
-                mrow[j], lrow[j] = nm, lrow[j] * sc
-                SC[j] = sc[:8]
-                FL[j] = True
-            p = np.where(sv == -np.inf, 0.0, np.exp(sv - mrow[j][:, None]))
-            lrow[j] += p.sum(1)
+            if np.any(gm > mrow[pr] + 6):
+                nm = np.maximum(mrow[pr], gm)
+                sc = np.where(nm == mrow[pr], 1.0, np.exp(mrow[pr] - nm))
+                mrow[pr], lrow[pr] = nm, lrow[pr] * sc
+                SC[pr] = sc[:16]
+            p = np.where(sv == -np.inf, 0.0, np.exp(sv - mrow[pr][:, None]))
+            lrow[pr] += p.sum(1)
             x = (p * (ks4 * kp)).astype(np.float32)
             hi = x.astype(np.float16)
             lo = (x - hi.astype(np.float32)).astype(np.float16)
             for l in range(64):
-                if (l & 15) < 8:
-                    P[j, l >> 4, l & 15, :4] = hi[l]
-                    P[j, l >> 4, l & 15, 4:] = lo[l]
-        for b in range(NB):  # rescale each row block once (every wave does its own dim blocks)
-            j0, j1 = 2 * b, 2 * b + 1 if 2 * b + 1 < RPC else 2 * b
-            if FL[j0] or FL[j1]:
-                for r in range(16):
-                    jj = 2 * b + (r >> 3)
-                    U[b, :, r, :] *= SC[jj, r & 7] if jj < RPC else 1.0
+                P[pr, l >> 4, l & 15, :4] = hi[l]
+                P[pr, l >> 4, l & 15, 4:] = lo[l]
+        for b in range(NP):  # accumulator rows 4 g + i = columns 4 g + i of the pair
+            for r in range(16):
+                U[b, :, r, :] *= SC[b, r]
         for w in range(8):
             db_u, G0 = w >> 1, 2 * (w & 1)
             q8, p8 = (lanes & 15) >> 1, lanes & 1
@@ -165,20 +159,22 @@ def emulate(m, q_rows, L):
             r1, r2, r3 = tr_b8(img, o1), tr_b8(img, o1 + 256), tr_b8(img, o3)
             ops = ((r1[:, :4] * 256.0, r1[:, 4:] * 1.0, r3[:, :4] / 256.0),
                    (r2[:, :4] * 256.0, r2[:, 4:] * 1.0, r3[:, 4:] / 256.0))
-            for b in range(NB):
-                pa = np.stack([P[2 * b + ((l & 15) >> 3), l >> 4, l & 7] for l in range(64)])
+            for b in range(NP):
+                pa = np.stack([P[b, l >> 4, l & 15] for l in range(64)])
                 for kk, (c2, c1, b0) in enumerate(ops):
                     U[b, 2 * w + kk] += (mfma_f16(pa, np.concatenate([c2, c2], 1), 8)
                                          + mfma_f16(pa, np.concatenate([c1, c1], 1), 8)
                                          + mfma_f16(pa[:, :4], b0, 4))
     out = np.zeros((RPC, 2048))
-    for j in range(RPC):
-        lt = np.array([lrow[j][(lanes & 15) == h].sum() for h in range(8)])  # the four lanes of column h
-        for h in range(8):
-            fs = 2 * smax / lt[h]
+    for b in range(NP):
+        lt = np.array([lrow[b][(lanes & 15) == cc].sum() for cc in range(16)])  # the four lanes of a column
+        for r in range(16):
+            j, h = 2 * b + (r >> 3), r & 7
+            if j >= RPC:
+                continue
+            fs = 2 * smax / lt[r]
             for blkk in range(16):
-                r = 8 * (j & 1) + h
-                out[j, h * 256 + 16 * blkk: h * 256 + 16 * blkk + 16] = U[j // 2, blkk, r] * fs
+                out[j, h * 256 + 16 * blkk: h * 256 + 16 * blkk + 16] = U[b, blkk, r] * fs
     return out
 
 

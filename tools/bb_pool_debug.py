@@ -55,7 +55,6 @@ def main():
         r = call(e, dv[k])
         e.close()
         print(f"batch {k} alone: steps {int(r['steps'])}", flush=True)
-    return
     # (4) the pool test's pattern: 3 lanes (bank policy / grid as EnginePool sets them), six batches
     from nanodecoder_amd.engine import EnginePool
     one = mk()

@@ -37,6 +37,8 @@ case $step in
       python3 $R/bench.py $SHORT "$@" > $O/$tag.log 2>&1
     rc=$?; echo "prof $tag rc=$rc"; [ $rc -ne 0 ] && exit $rc
     python3 $R/tools/profsum.py $O/$tag/run_kernel_stats.csv 7 > $O/${tag}_kernel_stats.txt
+    # keep the stats, drop the per-dispatch trace (gpurun copies back at most 64 MiB)
+    find $O/$tag -name '*.csv' ! -name '*kernel_stats.csv' -delete
     head -30 $O/${tag}_kernel_stats.txt; exit 0 ;;
   pmc)
     tag=$1; ctrs=$2; shift 2
@@ -54,7 +56,8 @@ case $step in
       python3 $R/bench.py --config-legs 0 --steps 1 --warmup 1 --cpu-baseline 0 --exact 0 --host-inclusive 0 --read-shard 0 \
       --no-roofline "$@" > $O/$tag.log 2>&1
     rc=$?; echo "mfma $tag rc=$rc"; [ $rc -ne 0 ] && exit $rc
-    python3 $R/tools/mfma_summary.py $O/$tag/run_counter_collection.csv $tag $O/${tag}_mfma.json | head -40; exit 0 ;;
+    python3 $R/tools/mfma_summary.py $O/$tag/run_counter_collection.csv $tag $O/${tag}_mfma.json | head -40
+    rm -rf $O/$tag; exit 0 ;;
   pmcmb)
     # one --pmc pass over a tools/microbench.py case (plain launches)
     tag=$1; ctrs=$2; shift 2

@@ -8,6 +8,8 @@ bash tools/gpu.sh prof ${t}_one_call --inflight 1 && \
 bash tools/gpu.sh prof ${t}_pool3 && \
 bash tools/gpu.sh pmc ${t}_pmcF "FETCH_SIZE" --inflight 1 && \
 bash tools/gpu.sh pmc ${t}_pmcW "WRITE_SIZE" --inflight 1 && \
+python3 tools/pmc_summary.py gpurun_out/${t}_pmcF/run_counter_collection.csv gpurun_out/${t}_pmcW/run_counter_collection.csv \
+  gpurun_out/${t}_pmc_summary.json && rm -rf gpurun_out/${t}_pmcF gpurun_out/${t}_pmcW && \
 bash tools/gpu.sh mfma ${t}_mfma_greedy --inflight 1 && \
 bash tools/gpu.sh mfma ${t}_mfma_nano --inflight 1 --encoder nano && \
 bash tools/gpu.sh mfma ${t}_mfma_beam --inflight 1 --mode beam --batch 1024
