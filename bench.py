@@ -294,8 +294,13 @@ def kernel_roofline(eng, B, mode, beam, encoder="transformer", alive=None, secon
         extra = {"mfma_view": {"algorithmic_flops_per_launch": flops, "achieved": round(tf, 2), "peak": round(SPLIT_PEAK, 1),
                                "unit": "TFLOP/s fp32-equivalent (split-fp16 on fp16 MFMA)", "frac": round(tf / SPLIT_PEAK, 4)}}
     else:
-        name = f"dec_ctx_attention_kernel<{beam}>"
-        per_chunk = T * 2 * D * 4 + T * 4 + 2 * beam * D * 4
+        form = eng.engines[0].bank_form() if hasattr(eng, "engines") else eng.bank_form()
+        if form == 2:  # ND_BEAM_BANK=1: the beam rows on the digit bank (digits + row scales + signal, q' and U)
+            name = f"dec_bank_d8_beam_kernel<{beam}>"
+            per_chunk = T * D * 3 + T * 4 + T * 4 + 2 * beam * 8 * D * 4
+        else:
+            name = f"dec_ctx_attention_kernel<{beam}>"
+            per_chunk = T * 2 * D * 4 + T * 4 + 2 * beam * D * 4
         nbytes = B * per_chunk
         extra = {}
         if alive is not None and n > 0:

@@ -754,6 +754,7 @@ static void set_memory_view(nd_ctx* c, int T, int rpc) {
   c->bank_h3 = false;
   c->bank_d8 = false;
   c->mem = nullptr;
+  c->last_bank_form = 0;
   c->beam_bank = rpc > 1 && rpc <= 6 && c->ctx_path == 0 && use_beam_bank() && use_bank_d8() && !c->exact &&
                  !c->attn_on && nd::bank_h3_eligible(T, c->cfg.max_src_len);
   if (!use_memory_bank(c, rpc)) return;

@@ -102,8 +102,8 @@ class Engine:
         self.bank_grid = int(workgroups)
 
     def bank_form(self) -> int:
-        """The memory bank the last greedy call streamed (nd_bank_form): 0 fp32 (or none), 1 split-fp16,
-        2 24-bit digits."""
+        """The memory bank the last call streamed (nd_bank_form): 0 fp32 (or none: a beam call on the
+        K/V form), 1 split-fp16, 2 24-bit digits (greedy, or beam rows with ND_BEAM_BANK=1)."""
         return int(self._L.nd_bank_form(self._h))
 
     def set_timing(self, on: bool):
