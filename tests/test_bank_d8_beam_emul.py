@@ -76,7 +76,7 @@ def tr_b8(img, addr):
     return out
 
 
-def emulate(m, q_rows, L):
+def emulate(m, q_rows, L, pipe=True):
     """One chunk, RPC = len(q_rows) rows (no masks): the kernel's arithmetic in float64 where it is exact,
     float32 / float16 where the kernel rounds.  Score wave p owns rows (2p, 2p + 1): column col = (row
     2p + (col >> 3), head col & 7)."""
@@ -151,18 +151,29 @@ def emulate(m, q_rows, L):
         for b in range(NP):  # accumulator rows 4 g + i = columns 4 g + i of the pair
             for r in range(16):
                 U[b, :, r, :] *= SC[b, r]
-        for w in range(8):
-            db_u, G0 = w >> 1, 2 * (w & 1)
-            q8, p8 = (lanes & 15) >> 1, lanes & 1
-            o1 = (db_u * 3 + np.where(q8 < 4, 2, 1)) * FR + (4 * g + (q8 & 3) + 16 * G0) * 16 + 8 * p8
-            o3 = db_u * 3 * FR + (4 * g + (q8 & 3) + 16 * (G0 + np.where(q8 < 4, 0, 1))) * 16 + 8 * p8
+        # (dim-block pair, offsets): the two-phase kernel's wave w owns 16-dim blocks 2w, 2w + 1; the pipelined
+        # kernel's context wave u owns 64-dim block u as the pairs gp = 0, 1 (offsets + 512 gp)
+        q8, p8 = (lanes & 15) >> 1, lanes & 1
+        units = []
+        if pipe:
+            for uu in range(4):
+                o1 = (uu * 3 + np.where(q8 < 4, 2, 1)) * FR + (4 * g + (q8 & 3)) * 16 + 8 * p8
+                o3 = uu * 3 * FR + (4 * g + (q8 & 3) + 16 * np.where(q8 < 4, 0, 1)) * 16 + 8 * p8
+                units += [(4 * uu + 2 * gp, o1 + 512 * gp, o3 + 512 * gp) for gp in range(2)]
+        else:
+            for w in range(8):
+                db_u, G0 = w >> 1, 2 * (w & 1)
+                o1 = (db_u * 3 + np.where(q8 < 4, 2, 1)) * FR + (4 * g + (q8 & 3) + 16 * G0) * 16 + 8 * p8
+                o3 = db_u * 3 * FR + (4 * g + (q8 & 3) + 16 * (G0 + np.where(q8 < 4, 0, 1))) * 16 + 8 * p8
+                units.append((2 * w, o1, o3))
+        for k0, o1, o3 in units:
             r1, r2, r3 = tr_b8(img, o1), tr_b8(img, o1 + 256), tr_b8(img, o3)
             ops = ((r1[:, :4] * 256.0, r1[:, 4:] * 1.0, r3[:, :4] / 256.0),
                    (r2[:, :4] * 256.0, r2[:, 4:] * 1.0, r3[:, 4:] / 256.0))
             for b in range(NP):
                 pa = np.stack([P[b, l >> 4, l & 15] for l in range(64)])
                 for kk, (c2, c1, b0) in enumerate(ops):
-                    U[b, 2 * w + kk] += (mfma_f16(pa, np.concatenate([c2, c2], 1), 8)
+                    U[b, k0 + kk] += (mfma_f16(pa, np.concatenate([c2, c2], 1), 8)
                                          + mfma_f16(pa, np.concatenate([c1, c1], 1), 8)
                                          + mfma_f16(pa[:, :4], b0, 4))
     out = np.zeros((RPC, 2048))
@@ -181,14 +192,14 @@ def emulate(m, q_rows, L):
 import pytest
 
 
-@pytest.mark.parametrize("RPC,L,qscale", [(3, 40, 0.3), (2, 72, 2.4)])
-def test_beam_bank_index_math_matches_fp64(RPC, L, qscale):
+@pytest.mark.parametrize("RPC,L,qscale,pipe", [(3, 40, 0.3, True), (2, 72, 2.4, True), (3, 40, 0.3, False)])
+def test_beam_bank_index_math_matches_fp64(RPC, L, qscale, pipe):
     """Odd rows (the padded second row of the last block), a partial last key block, and (qscale 2.4) scores
     spread enough for running-maximum rescales inside the chunk."""
     rng = np.random.default_rng(5)
     m = rng.standard_normal((512, 256)).astype(np.float32)
     q_rows = (rng.standard_normal((RPC, 2048)) * qscale).astype(np.float32)
-    got = emulate(m, q_rows, L)
+    got = emulate(m, q_rows, L, pipe)
     M = m[:L].astype(np.float64)
     for j in range(RPC):
         for h in range(8):
