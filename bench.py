@@ -325,36 +325,46 @@ def kernel_roofline(eng, B, mode, beam, encoder="transformer", alive=None, secon
     import ctypes
     from nanodecoder_amd import _lib
     from nanodecoder_amd.engine import op_fold_layernorm, op_pack_p16h
-    # secondary: the dominant encoder MFMA kernel, the fused FFN block
-    # (enc_ffn_kernel: LN + W1 + bias + ReLU + W2 + bias + residual, the hidden
-    # kept on chip) in the split-fp16 form the engine runs: 3 fp16 MFMA
-    # products per fp32 multiply-add, so its fp32-equivalent peak is the dense
-    # fp16 peak / 3.  Algorithmic work: the two products, 2 x 2 M F D.
+    # secondary: the dominant encoder MFMA kernel in the form the engine launches for layers 0-1
+    # (enc_ffn_kernel<1, true, true>: the attention's output projection Wo + residual, LN + W1 + bias +
+    # ReLU + W2 + bias + residual with the hidden kept on chip, and the next layer's LN + QKV projection),
+    # split-fp16: 3 fp16 MFMA products per fp32 multiply-add, so its fp32-equivalent peak is the dense fp16
+    # peak / 3.  Algorithmic work: Wo 2 M D^2 + FFN 4 M F D + QKV 6 M D^2.
     M, D, F = B * T, 256, 2048
     Y = torch.randn(M, D, device=dev)
+    att = torch.randn(M, D, device=dev)
     W1, b1 = op_fold_layernorm(torch.randn(F, D, device=dev) / 16, torch.randn(F, device=dev) * 0.1,
                                torch.ones(D, device=dev), torch.zeros(D, device=dev))  # as at load time
     w1h, w1s = op_pack_p16h(W1)
     w2h, w2s = op_pack_p16h(torch.randn(D, F, device=dev) / F ** 0.5)
-    b2 = torch.randn(D, device=dev) * 0.1
+    woh, wos = op_pack_p16h(torch.randn(D, D, device=dev) / 16)
+    Wq, bq = op_fold_layernorm(torch.randn(3 * D, D, device=dev) / 16, torch.randn(3 * D, device=dev) * 0.1,
+                               torch.ones(D, device=dev), torch.zeros(D, device=dev))
+    qh, qs = op_pack_p16h(Wq)
+    b2, bo = torch.randn(D, device=dev) * 0.1, torch.randn(D, device=dev) * 0.1
     X = torch.empty_like(Y)
+    qkv = torch.empty(M, 3 * D, device=dev)
     part = torch.empty(M, 16, 2, device=dev)
     ov = torch.zeros(1, dtype=torch.int32, device=dev)
     st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
 
     def ffn(i):
-        _lib.check(_lib.lib().nd_op_enc_ffn(Y.data_ptr(), w1h.data_ptr(), w1s, b1.data_ptr(), w2h.data_ptr(), w2s,
-                                            b2.data_ptr(), X.data_ptr(), part.data_ptr(), M, F, ov.data_ptr(), st),
-                   "nd_op_enc_ffn")
+        _lib.check(_lib.lib().nd_op_enc_ffn_wo(att.data_ptr(), Y.data_ptr(), woh.data_ptr(), wos, bo.data_ptr(),
+                                               w1h.data_ptr(), w1s, b1.data_ptr(), w2h.data_ptr(), w2s,
+                                               b2.data_ptr(), X.data_ptr(), part.data_ptr(), qh.data_ptr(), qs,
+                                               bq.data_ptr(), qkv.data_ptr(), M, F, ov.data_ptr(), st),
+                   "nd_op_enc_ffn_wo")
     for i in range(3):
         ffn(i)
     gms = _StreamTimer(dev).time(ffn, 10)
-    tf = 4.0 * M * F * D / (gms * 1e-3) / 1e12
-    out["mfma_kernel"] = {"kernel": "enc_ffn_kernel (encoder FFN block: W1 and W2 products fused, split-fp16)",
+    flops = 2 * M * D * D + 4 * M * F * D + 6 * M * D * D
+    tf = flops / (gms * 1e-3) / 1e12
+    out["mfma_kernel"] = {"kernel": "enc_ffn_kernel<1, true, true> (the engine's form for encoder layers 0-1: "
+                                    "Wo + residual, LN + W1 + ReLU + W2 + residual, next layer's LN + QKV; split-fp16)",
                           "achieved": round(tf, 2), "peak": round(SPLIT_PEAK, 1),
                           "unit": "TFLOP/s fp32-equivalent (fp16 MFMA peak / 3 products)",
                           "frac": round(tf / SPLIT_PEAK, 4), "avg_launch_ms": round(gms, 4),
-                          "algorithmic_flops_per_launch": int(4 * M * F * D)}
+                          "algorithmic_flops_per_launch": int(flops), "rows": M}
     del Y, X, W1, w1h, w2h
     return out
 
