@@ -351,6 +351,9 @@ dec_bank_d8_kernel(const float* __restrict__ qp, const i32x4* __restrict__ bank,
                    const int* __restrict__ kemax, const float* __restrict__ signal, const int* __restrict__ span,
                    float pad_val, float* __restrict__ out, int T, int C, unsigned long long* stamp,
                    float* __restrict__ dbg, size_t dbg_stride, int* ovf) {
+#ifdef ND_SKIP_BANK  // timing probe only (tools/build_variant.sh, tools/marginal.sh): the kernel's marginal cost
+  if (threadIdx.x < 100000) return;
+#endif
   const unsigned long long t_entry = wall_clock64();
   if constexpr (WALK) {
     for (int c = blockIdx.x; c < C; c += gridDim.x) {

@@ -1054,7 +1054,14 @@ hipError_t launch_gemm_p16(GemmArgs& g, hipStream_t s) {
     if (g.N % 64 == 0 && (long)(g.N / 64) * ((g.M + 15) / 16) >= 128) return launch_p16<4, 2, 128>(g, s);
     return launch_p16<1, 4, 64>(g, s);
   }
-  if (g.K == 2048) return launch_p16<1, 8, 256>(g, s);
+  if (g.K == 2048) {
+    static const int k16 = [] {
+      const char* e = getenv("ND_P16_K2048");  // 1: 16 K-slice waves of 128 (A/B timing); 0: 8 of 256
+      return e ? atoi(e) : 0;
+    }();
+    if (k16 == 1) return launch_p16<1, 16, 128>(g, s);
+    return launch_p16<1, 8, 256>(g, s);
+  }
   if (g.K == 1024) return launch_p16<1, 8, 128>(g, s);
   if (g.K == 512) return launch_p16<1, 8, 64>(g, s);
   return hipErrorInvalidValue;
