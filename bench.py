@@ -298,8 +298,11 @@ def kernel_roofline(eng, B, mode, beam, encoder="transformer", alive=None, secon
         if form == 2:  # ND_BEAM_BANK=1: the beam rows on the digit bank (digits + row scales + signal, q' and U)
             name = f"dec_bank_d8_beam_kernel<{beam}>"
             per_chunk = T * D * 3 + T * 4 + T * 4 + 2 * beam * 8 * D * 4
+        elif form == 3:  # the 24-bit context K/V image (1600 B per key: 3-byte k, v + 8 head scales each)
+            name = f"dec_ctx_attention_kernel<{beam}, true>"
+            per_chunk = T * 1600 + T * 4 + 2 * beam * D * 4
         else:
-            name = f"dec_ctx_attention_kernel<{beam}>"
+            name = f"dec_ctx_attention_kernel<{beam}, false>"
             per_chunk = T * 2 * D * 4 + T * 4 + 2 * beam * D * 4
         nbytes = B * per_chunk
         extra = {}

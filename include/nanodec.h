@@ -478,9 +478,10 @@ int nd_op_dec_bank_d8_beam(const float* qp, const void* bank, const float* kscal
                            int32_t rpc, int32_t T, const int32_t* done, int32_t* ovf, void* stream);
 
 /* Which memory bank the context's last call streamed (diagnostics, the
- * bench's roofline accounting): 0 fp32 bank, or none (a beam call on the
- * K/V form), 1 split-fp16 (nd_op_dec_bank_h3), 2 24-bit digits
- * (nd_op_dec_bank_d8, or nd_op_dec_bank_d8_beam for a beam call). */
+ * bench's roofline accounting): 0 fp32 bank, or fp32 K/V (a beam call in
+ * exact fp32 or with ND_CTX_Q24=0), 1 split-fp16 (nd_op_dec_bank_h3), 2 24-bit
+ * digits (nd_op_dec_bank_d8, or nd_op_dec_bank_d8_beam for a beam call), 3 the
+ * 24-bit context K/V of a beam call (nd_op_dec_ctx_attention_q24). */
 int nd_bank_form(nd_ctx* ctx);
 
 /* Decoder context attention (multi_headed_attn.py:142-177): rows r = c*rpc+j
@@ -490,6 +491,24 @@ int nd_bank_form(nd_ctx* ctx);
 int nd_op_dec_ctx_attention(const float* q, const float* kv, int32_t ld, int32_t koff, const float* signal,
                             const int32_t* span, float pad_val, float* out, int32_t C, int32_t rpc, int32_t T,
                             void* stream);
+
+/* The beam's context K/V in 24-bit fixed point (the default for beam rows
+ * outside exact fp32; the same attention as nd_op_dec_ctx_attention,
+ * multi_headed_attn.py:142-177, on 0.78x the bytes).  nd_op_ctx_pack_q24:
+ * fp32 K/V kv [B*T, ld] (layer l's k at column l*512, v at l*512+256; the
+ * reference's linear_keys / linear_values outputs, multi_headed_attn.py:
+ * 142-150) -> image out [B*T][layers][1600 B]: per (key, layer) k's 256
+ * values as 24-bit integers (3 bytes each; the 12 bytes at 12*i hold dims
+ * 4i..4i+3), v's at byte 768, then per head h {2^(e_k - 23), 2^(e_v - 23)}
+ * as floats at byte 1536 + 8h, with e the head's exponent (max|x| < 2^e); an
+ * element's error is at most 2^-23 of its head's largest |x|.  Rows t >=
+ * span[c] are not written.  nd_op_dec_ctx_attention_q24: as
+ * nd_op_dec_ctx_attention with K/V of layer `layer` from that image. */
+int nd_op_ctx_pack_q24(const float* kv, int32_t ld, int32_t layers, void* out, const int32_t* span, int32_t B,
+                       int32_t T, void* stream);
+int nd_op_dec_ctx_attention_q24(const float* q, const void* kvq, int32_t layers, int32_t layer, const float* signal,
+                                const int32_t* span, float pad_val, float* out, int32_t C, int32_t rpc, int32_t T,
+                                void* stream);
 
 #ifdef __cplusplus
 }

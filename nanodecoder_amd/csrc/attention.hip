@@ -1051,9 +1051,14 @@ struct CtxTile {
   static constexpr int U = RPC <= CTX_URPC ? 4 : 2;  // keys per block (register budget)
 };
 
-template <int RPC>
+// Q24 (round 4): the chunk's K/V in 24-bit fixed point (ctx_pack_q24_kernel
+// below): per key row 1600 B instead of 2 KB, so the HBM-bound kernel streams
+// 0.78x the bytes; the integers convert exactly to fp32 and the per-(key,
+// head) power-of-two scales fold into the score (after the head's 8-lane
+// sum) and into v.  kv, ld and koff are then bytes.
+template <int RPC, bool Q24>
 __global__ void __launch_bounds__(CTX_NW * 64)
-dec_ctx_attention_kernel(const float* __restrict__ q, const float* __restrict__ kv, int ld, int koff,
+dec_ctx_attention_kernel(const float* __restrict__ q, const void* __restrict__ kv_, int ld, int koff,
                          const float* __restrict__ signal, const int* __restrict__ span, float pad_val,
                          float* __restrict__ out, int T, unsigned long long* stamp, float* __restrict__ dbg,
                          size_t dbg_stride, const int* __restrict__ skip) {
@@ -1067,7 +1072,6 @@ dec_ctx_attention_kernel(const float* __restrict__ q, const float* __restrict__ 
   const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int L = min(span[c], T);
   const size_t base = (size_t)c * T;
-  const float* kvc = kv + base * ld + koff + lane * 4;
   const float* sgc = signal + base;
   // lane owns dims 4*lane..4*lane+3 of every row; head = lane / 8
   f32x4 qv[RPC], acc[RPC];
@@ -1079,14 +1083,26 @@ dec_ctx_attention_kernel(const float* __restrict__ q, const float* __restrict__ 
     m[j] = -INFINITY;
     l[j] = 0.f;
   }
+  // a key's registers: fp32 k, v (Q24: the 12 bytes of k's and of v's four
+  // integers in .xyz, the head's k and v scales in k.w, v.w)
   f32x4 kc[U], vc[U];
   float sg[U];
   auto load = [&](int blk, f32x4* kk, f32x4* vv, float* ss) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int t = min(blk * U + u, L - 1);
-      kk[u] = ld4(kvc + (size_t)t * ld);
-      vv[u] = ld4(kvc + (size_t)t * ld + ND_D);
+      if constexpr (Q24) {
+        const uint8_t* row = static_cast<const uint8_t*>(kv_) + (base + t) * ld + koff;
+        const u32x3 kb = *reinterpret_cast<const u32x3*>(row + 12 * lane);
+        const u32x3 vb = *reinterpret_cast<const u32x3*>(row + CTXQ_V + 12 * lane);
+        const f32x2 sc = *reinterpret_cast<const f32x2*>(row + CTXQ_S + 8 * (lane >> 3));
+        kk[u] = f32x4{__uint_as_float(kb.x), __uint_as_float(kb.y), __uint_as_float(kb.z), sc.x};
+        vv[u] = f32x4{__uint_as_float(vb.x), __uint_as_float(vb.y), __uint_as_float(vb.z), sc.y};
+      } else {
+        const float* kvc = static_cast<const float*>(kv_) + (base + t) * ld + koff + lane * 4;
+        kk[u] = ld4(kvc);
+        vv[u] = ld4(kvc + ND_D);
+      }
       ss[u] = sgc[t];
     }
   };
@@ -1098,13 +1114,24 @@ dec_ctx_attention_kernel(const float* __restrict__ q, const float* __restrict__ 
     const bool more = (blk + CTX_NW) * U < L;
     if (more) load(blk + CTX_NW, kn, vn, sn);
     float sc[RPC][U];
+    f32x4 vf[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const bool valid = blk * U + u < L;
       const bool masked = sg[u] == pad_val;
+      f32x4 kf = kc[u];
+      float ks = 1.f;
+      if constexpr (Q24) {
+        kf = q24_unpack(kc[u]);
+        ks = kc[u].w;
+        vf[u] = q24_unpack(vc[u]) * vc[u].w;
+      } else {
+        vf[u] = vc[u];
+      }
 #pragma unroll
       for (int j = 0; j < RPC; ++j) {
-        const float d = sum8(qv[j].x * kc[u].x + qv[j].y * kc[u].y + qv[j].z * kc[u].z + qv[j].w * kc[u].w);
+        float d = sum8(qv[j].x * kf.x + qv[j].y * kf.y + qv[j].z * kf.z + qv[j].w * kf.w);
+        if constexpr (Q24) d *= ks;
         sc[j][u] = valid ? (masked ? ND_MASK_FILL : d) : -INFINITY;
       }
       // -attn_debug / coverage: head 0 (lanes 0..7 after sum8) of every row of the chunk
@@ -1112,7 +1139,7 @@ dec_ctx_attention_kernel(const float* __restrict__ q, const float* __restrict__ 
 #pragma unroll
         for (int j = 0; j < RPC; ++j) dbg[((size_t)c * RPC + j) * dbg_stride + blk * U + u] = sc[j][u];
     }
-    online_update<RPC, U>(sc, vc, m, l, acc);
+    online_update<RPC, U>(sc, vf, m, l, acc);
     if (more) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -1126,19 +1153,80 @@ dec_ctx_attention_kernel(const float* __restrict__ q, const float* __restrict__ 
   stamp_end(stamp);
 }
 
+// fp32 K/V [M][ld] (layer l's k | v at column koff + l * 512) -> the 24-bit
+// image [M][Ld][CTXQ_ROW] bytes: per (key, layer) k's and v's 256 integers
+// (3 bytes each, little-endian two's complement, lane-major: lane i's 12
+// bytes hold dims 4i..4i+3), then per head {2^(e_k - 23), 2^(e_v - 23)} as
+// floats.  e = the head's exponent: max|x| < 2^e, so |x| 2^(23-e) < 2^23 and
+// rounding to the nearest integer (clamped to 2^23 - 1) leaves an error of at
+// most 2^(e-24) <= 2^-23 max|x| per element (an fp32 value's own rounding is
+// 2^-24 |x|; the split-fp16 GEMM that produced K / V carries 2^-22 operands).
+// Rows t >= span of their chunk are never read and not written.
+// One wave per (key row, layer).
+__global__ void __launch_bounds__(256)
+ctx_pack_q24_kernel(const float* __restrict__ kv, int ld, int Ld, uint8_t* __restrict__ out,
+                    const int* __restrict__ span, int T, int n) {
+  const int w = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (w >= n) return;
+  const int row = w / Ld, layer = w % Ld;
+  if (row % T >= min(span[row / T], T)) return;
+  const float* src = kv + (size_t)row * ld + (size_t)layer * 2 * ND_D + lane * 4;
+  uint8_t* dst = out + ((size_t)row * Ld + layer) * CTXQ_ROW;
+  float scl[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const f32x4 x = ld4(src + h * ND_D);
+    float mx = fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w)));
+    if (!(fabsf(x.x) <= 3.4028235e38f && fabsf(x.y) <= 3.4028235e38f && fabsf(x.z) <= 3.4028235e38f &&
+          fabsf(x.w) <= 3.4028235e38f))
+      mx = INFINITY;  // NaN / inf anywhere in the head (fmaxf would drop a NaN)
+    mx = fmaxf(mx, dpp_mov<ND_DPP_XOR1>(mx));
+    mx = fmaxf(mx, dpp_mov<ND_DPP_XOR2>(mx));
+    mx = fmaxf(mx, dpp_mov<ND_DPP_HALF_MIRROR>(mx));  // the head's 8 lanes
+    int e = 0;
+    frexpf(mx, &e);  // mx = f 2^e, f in [0.5, 1): mx < 2^e (mx == 0: e = 0, the integers are 0)
+    e = max(e, -100);  // a head below 2^-100 (2^(23 - e) must stay finite): its integers round to 0
+    const float up = ldexpf(1.f, 23 - e);
+    // a non-finite head keeps a NaN scale, so its scores / values stay non-finite as in fp32
+    scl[h] = mx <= 3.4028235e38f ? ldexpf(1.f, e - 23) : __builtin_nanf("");
+    int v[4];
+    const float xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = (int)fminf(fmaxf(rintf(xs[i] * up), -8388607.f), 8388607.f);
+    u32x3 b;
+    b.x = (uint32_t)(v[0] & 0xffffff) | ((uint32_t)v[1] << 24);
+    b.y = (((uint32_t)v[1] >> 8) & 0xffff) | ((uint32_t)v[2] << 16);
+    b.z = (((uint32_t)v[2] >> 16) & 0xff) | ((uint32_t)v[3] << 8);
+    *reinterpret_cast<u32x3*>(dst + h * CTXQ_V + 12 * lane) = b;
+  }
+  if ((lane & 7) == 0) *reinterpret_cast<f32x2*>(dst + CTXQ_S + 8 * (lane >> 3)) = f32x2{scl[0], scl[1]};
+}
+
+hipError_t launch_ctx_pack_q24(const float* kv, int ld, int Ld, uint8_t* out, const int* span, int B, int T,
+                               hipStream_t s) {
+  if (Ld < 1 || ld < Ld * 2 * ND_D || B < 1 || T < 1) return hipErrorInvalidValue;
+  const int n = B * T * Ld;
+  hipLaunchKernelGGL(ctx_pack_q24_kernel, dim3((n + 3) / 4), dim3(256), 0, s, kv, ld, Ld, out, span, T, n);
+  return hipGetLastError();
+}
+
 static size_t ctx_lds_bytes(int rpc) { return (size_t)CTX_NW * rpc * (ND_D + 2 * ND_H) * sizeof(float); }
 
-hipError_t launch_dec_ctx_attention(const float* q, const float* kv, int ld, int koff, const float* signal,
+hipError_t launch_dec_ctx_attention(const float* q, const void* kv, int ld, int koff, const float* signal,
                                     const int* span, float pad_val, float* out, int C, int rpc, int T,
                                     hipStream_t s, unsigned long long* stamp, float* attn_dbg, size_t dbg_stride,
-                                    const int* skip) {
+                                    const int* skip, bool q24) {
   if (rpc < 1 || rpc > CTX_MAXR || T > 512) return hipErrorInvalidValue;
   const size_t lds = ctx_lds_bytes(rpc);
   switch (rpc) {
 #define ND_CTX_CASE(R)                                                                                            \
   case R:                                                                                                         \
-    hipLaunchKernelGGL(dec_ctx_attention_kernel<R>, dim3(C), dim3(CTX_NW * 64), lds, s, q, kv, ld, koff, signal,  \
-                       span, pad_val, out, T, stamp, attn_dbg, dbg_stride, skip);                                 \
+    if (q24)                                                                                                      \
+      hipLaunchKernelGGL((dec_ctx_attention_kernel<R, true>), dim3(C), dim3(CTX_NW * 64), lds, s, q, kv, ld, koff, \
+                         signal, span, pad_val, out, T, stamp, attn_dbg, dbg_stride, skip);                       \
+    else                                                                                                          \
+      hipLaunchKernelGGL((dec_ctx_attention_kernel<R, false>), dim3(C), dim3(CTX_NW * 64), lds, s, q, kv, ld,     \
+                         koff, signal, span, pad_val, out, T, stamp, attn_dbg, dbg_stride, skip);                 \
     break;
     ND_CTX_CASE(1)
     ND_CTX_CASE(2)
@@ -1166,9 +1254,13 @@ hipError_t launch_fill_i32(int* p, int v, int n, hipStream_t s) {
 }
 
 hipError_t init_kernel_attributes() {
-  const void* fns[] = {(const void*)dec_ctx_attention_kernel<1>, (const void*)dec_ctx_attention_kernel<2>,
-                       (const void*)dec_ctx_attention_kernel<3>, (const void*)dec_ctx_attention_kernel<4>,
-                       (const void*)dec_ctx_attention_kernel<5>, (const void*)dec_ctx_attention_kernel<6>};
+  const void* fns[] = {
+      (const void*)dec_ctx_attention_kernel<1, false>, (const void*)dec_ctx_attention_kernel<2, false>,
+      (const void*)dec_ctx_attention_kernel<3, false>, (const void*)dec_ctx_attention_kernel<4, false>,
+      (const void*)dec_ctx_attention_kernel<5, false>, (const void*)dec_ctx_attention_kernel<6, false>,
+      (const void*)dec_ctx_attention_kernel<1, true>,  (const void*)dec_ctx_attention_kernel<2, true>,
+      (const void*)dec_ctx_attention_kernel<3, true>,  (const void*)dec_ctx_attention_kernel<4, true>,
+      (const void*)dec_ctx_attention_kernel<5, true>,  (const void*)dec_ctx_attention_kernel<6, true>};
   for (const void* f : fns) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;

@@ -13,6 +13,21 @@
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+struct u32x3 {  // 12 bytes, 4-byte aligned (one dwordx3 access)
+  uint32_t x, y, z;
+};
+
+// Four 24-bit two's-complement integers packed little-endian in the bits of
+// raw.x, raw.y, raw.z (ctx_pack_q24_kernel) -> exact fp32 values.
+__device__ __forceinline__ f32x4 q24_unpack(f32x4 raw) {
+  const uint32_t w0 = __float_as_uint(raw.x), w1 = __float_as_uint(raw.y), w2 = __float_as_uint(raw.z);
+  const int i0 = (int)(w0 << 8) >> 8;
+  const int i1 = (int)(__builtin_amdgcn_alignbit(w1, w0, 24) << 8) >> 8;
+  const int i2 = (int)(__builtin_amdgcn_alignbit(w2, w1, 16) << 8) >> 8;
+  const int i3 = (int)w2 >> 8;
+  return f32x4{(float)i0, (float)i1, (float)i2, (float)i3};
+}
 
 // v_mfma_f32_32x32x2_f32: lane l supplies A[l&31][l>>5] and B[l>>5][l&31];
 // D lane l, reg r holds D[(r&3) + 8*(r>>2) + 4*(l>>5)][l&31].

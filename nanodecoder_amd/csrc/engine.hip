@@ -174,6 +174,8 @@ struct nd_ctx {
   bool bank_h3 = false;                   // mem_p holds the split-fp16 fragment bank (dec_bank_h3_kernel)
   bool bank_d8 = false;                   // ... or the 24-bit digit bank (dec_bank_d8_kernel; bank8.hip)
   bool beam_bank = false;                 // beam rows read the digit bank (dec_bank_d8_beam_kernel), not K/V
+  bool ctx_q24 = false;                   // beam rows read the 24-bit context K/V image (ctxq), not fp32 ctxkv
+  uint8_t* ctxq = nullptr;                // [B * T][layers][CTXQ_ROW] (attention.hip ctx_pack_q24_kernel)
   float* bank_ks = nullptr;               // digit bank: per-row scales 2^e_t [B * 512]
   int* bank_em = nullptr;                 // digit bank: per-chunk max e_t (biased) [B]
   int last_bank_form = 0;                 // nd_bank_form
@@ -392,6 +394,11 @@ static int alloc_workspaces(nd_ctx* c) {
   WS(c->att, B * T * D);
   WS(c->big, B * T * std::max(F, 3 * D));
   WS(c->ctxkv, B * T * Ld * 2 * D);
+  {
+    float* q = nullptr;
+    WS(q, B * T * Ld * (CTXQ_ROW / 4));
+    c->ctxq = reinterpret_cast<uint8_t*>(q);
+  }
   WS(c->mem_p, B * T * D);
   WS(c->bank_ks, B * 512);
   {
@@ -750,6 +757,16 @@ static bool use_beam_bank() {
   return on;
 }
 
+// beam rows' context K/V in 24-bit fixed point (attention.hip ctx_pack_q24_kernel: 0.78x the bytes of
+// the HBM-bound context attention); ND_CTX_Q24=0 keeps fp32 K/V.  Exact fp32 keeps fp32 K/V
+static bool use_ctx_q24() {
+  static const bool on = [] {
+    const char* e = getenv("ND_CTX_Q24");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
 static void set_memory_view(nd_ctx* c, int T, int rpc) {
   c->bank_h3 = false;
   c->bank_d8 = false;
@@ -757,6 +774,8 @@ static void set_memory_view(nd_ctx* c, int T, int rpc) {
   c->last_bank_form = 0;
   c->beam_bank = rpc > 1 && rpc <= 6 && c->ctx_path == 0 && use_beam_bank() && use_bank_d8() && !c->exact &&
                  !c->attn_on && nd::bank_h3_eligible(T, c->cfg.max_src_len);
+  c->ctx_q24 = !use_memory_bank(c, rpc) && !c->exact && use_ctx_q24();
+  if (c->ctx_q24) c->last_bank_form = 3;
   if (!use_memory_bank(c, rpc)) return;
   const bool tf = c->cfg.encoder_type == ND_ENC_TRANSFORMER;
   // 512-sample chunks: the split-fp16 fragment bank (LN'd for the transformer,
@@ -837,8 +856,13 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
       LCHK(dg(c->dU, HD, L.pwvo, D, HD, L.bvo, c->dmid, D).res(c->dq1, D).stats(c->dmid_part).run(s, &pnm));
     } else {
       LCHK(dg(c->dq1, D, L.pcwq, D, D, L.ncbq, c->dcq, D).ln(c->dq1_part, pnq).run(s));
-      LCHK(nd::launch_dec_ctx_attention(c->dcq, c->ctxkv, Ld * 2 * D, i * 2 * D, c->sig, c->span,
-                                        (float)c->cfg.pad_idx, c->datt, C, rpc, T, s, stamp, dbg, dbg_stride, done));
+      if (c->ctx_q24)
+        LCHK(nd::launch_dec_ctx_attention(c->dcq, c->ctxq, Ld * CTXQ_ROW, i * CTXQ_ROW, c->sig, c->span,
+                                          (float)c->cfg.pad_idx, c->datt, C, rpc, T, s, stamp, dbg, dbg_stride, done,
+                                          true));
+      else
+        LCHK(nd::launch_dec_ctx_attention(c->dcq, c->ctxkv, Ld * 2 * D, i * 2 * D, c->sig, c->span,
+                                          (float)c->cfg.pad_idx, c->datt, C, rpc, T, s, stamp, dbg, dbg_stride, done));
       LCHK(dg(c->datt, D, L.pcwo, D, D, L.cbo, c->dmid, D).res(c->dq1, D).stats(c->dmid_part).run(s, &pnm));
     }
     LCHK(dg(c->dmid, D, L.pw1, F, D, L.nb1, c->dhid, F).ln(c->dmid_part, pnm).relu().run(s));
@@ -851,7 +875,12 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
 // per-layer context K/V (beam).
 static hipError_t enqueue_memory(nd_ctx* c, int B, int T, int rpc, hipStream_t s) {
   set_memory_view(c, T, rpc);
-  if (!use_memory_bank(c, rpc)) return enqueue_ctxkv(c, B, T, s);
+  if (!use_memory_bank(c, rpc)) {
+    LCHK(enqueue_ctxkv(c, B, T, s));
+    if (!c->ctx_q24) return hipSuccess;
+    const int Ld = (int)c->dec.size();
+    return nd::launch_ctx_pack_q24(c->ctxkv, Ld * 2 * c->D, Ld, c->ctxq, c->span, B, T, s);
+  }
   const bool tf = c->cfg.encoder_type == ND_ENC_TRANSFORMER;
   if (c->bank_d8)
     return nd::launch_bank_pack_d8(c->x, tf ? c->enc_ln_g : nullptr, tf ? c->enc_ln_b : nullptr, c->mem_p, c->bank_ks,
@@ -1657,7 +1686,8 @@ static const struct {
                  {"ND_ENC_ATTN_NQ", 2}, {"ND_ENC_ATTN_GRID", 0}, {"ND_ENC_ATTN_F32", 0}, {"ND_SELF_XCD", 1},
                  {"ND_ENC_WO", 1},     {"ND_ENC_QKV0", 1},
                  {"ND_ENC_QKV", 1},    {"ND_ENC_ATTN0", 1},   {"ND_SELF_NW8", 1},     {"ND_BANK_D8", 1},
-                 {"ND_BEAM_BANK", 0},  {"ND_BB_PIPE", 1},     {"ND_P16_K2048", 0}};
+                 {"ND_BEAM_BANK", 0},  {"ND_BB_PIPE", 1},     {"ND_P16_K2048", 0},
+                 {"ND_CTX_Q24", 1}};
 
 int nd_switches(char* buf, int32_t len) {
   std::string out;
@@ -2014,6 +2044,26 @@ int nd_op_dec_ctx_attention(const float* q, const float* kv, int32_t ld, int32_t
   hipError_t e = nd::launch_dec_ctx_attention(q, kv, ld, koff, signal, span, pad_val, out, C, rpc, T,
                                               (hipStream_t)stream);
   if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("dec_ctx_attention: ") + hipGetErrorString(e));
+  return ND_OK;
+}
+
+int nd_op_ctx_pack_q24(const float* kv, int32_t ld, int32_t layers, void* out, const int32_t* span, int32_t B,
+                       int32_t T, void* stream) {
+  if (!kv || !out || !span) return fail(ND_ERR_ARG, "ctx_pack_q24: bad arguments");
+  hipError_t e = nd::launch_ctx_pack_q24(kv, ld, layers, static_cast<uint8_t*>(out), span, B, T, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("ctx_pack_q24: ") + hipGetErrorString(e));
+  return ND_OK;
+}
+
+int nd_op_dec_ctx_attention_q24(const float* q, const void* kvq, int32_t layers, int32_t layer, const float* signal,
+                                const int32_t* span, float pad_val, float* out, int32_t C, int32_t rpc, int32_t T,
+                                void* stream) {
+  if (int rc = ensure_attributes()) return rc;
+  if (!q || !kvq || !signal || !span || !out || layer < 0 || layer >= layers)
+    return fail(ND_ERR_ARG, "dec_ctx_attention_q24: bad arguments");
+  hipError_t e = nd::launch_dec_ctx_attention(q, kvq, layers * CTXQ_ROW, layer * CTXQ_ROW, signal, span, pad_val, out,
+                                              C, rpc, T, (hipStream_t)stream, nullptr, nullptr, 0, nullptr, true);
+  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("dec_ctx_attention_q24: ") + hipGetErrorString(e));
   return ND_OK;
 }
 

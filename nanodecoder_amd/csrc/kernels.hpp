@@ -197,10 +197,20 @@ hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* 
                                      const GreedyHead* head = nullptr);
 // context attention: rows r = c*rpc + j attend over ctxkv rows of chunk c
 // (K at kv[(c*T+t)*ld + koff], V at +256), mask signal == pad_val, keys < span.
-hipError_t launch_dec_ctx_attention(const float* q, const float* kv, int ld, int koff, const float* signal,
+// q24: kv is the 24-bit image of launch_ctx_pack_q24 (ld, koff in bytes).
+hipError_t launch_dec_ctx_attention(const float* q, const void* kv, int ld, int koff, const float* signal,
                                     const int* span, float pad_val, float* out, int C, int rpc, int T,
                                     hipStream_t s, unsigned long long* stamp = nullptr, float* attn_dbg = nullptr,
-                                    size_t dbg_stride = 0, const int* skip = nullptr);
+                                    size_t dbg_stride = 0, const int* skip = nullptr, bool q24 = false);
+// 24-bit context K/V (beam rows): per (key row, layer) CTXQ_ROW bytes = k's 256
+// integers (3 bytes each, lane i's 12 bytes = dims 4i..4i+3) | v's | per head
+// {k scale, v scale} (powers of two, f32).  Image [B*T][Ld][CTXQ_ROW] from the
+// fp32 [B*T][ld] K/V (layer l at column l*512); rows t >= span not written.
+#define CTXQ_V 768
+#define CTXQ_S 1536
+#define CTXQ_ROW 1600
+hipError_t launch_ctx_pack_q24(const float* kv, int ld, int Ld, uint8_t* out, const int* span, int B, int T,
+                               hipStream_t s);
 // Next step's decoder input, written by the search kernel that picks the
 // token (the embedding of step+1 fused into the head: one launch fewer per
 // step): x[row] = emb[tok] (* 16 + pe[step+1] with position encoding) and

@@ -584,6 +584,32 @@ def op_dec_ctx_attention(q, kv, ld, koff, signal, span, pad_val, rpc, packed=Fal
     return out if packed else unpack_p16(out, R)
 
 
+CTXQ_ROW = 1600  # bytes per (key row, layer) of the 24-bit context K/V image (kernels.hpp)
+
+
+def op_ctx_pack_q24(kv, ld, layers, span, B, T):
+    """24-bit context K/V image (nd_op_ctx_pack_q24): kv [B*T, ld] f32 (layer l's
+    k | v at columns l*512 .. l*512+511) -> uint8 [B*T, layers, 1600]; rows t >=
+    span[c] of chunk c are not written (left zero here)."""
+    out = torch.zeros(B * T, layers, CTXQ_ROW, dtype=torch.uint8, device=kv.device)
+    s = ctypes.c_void_p(torch.cuda.current_stream(kv.device).cuda_stream)
+    _lib.check(_lib.lib().nd_op_ctx_pack_q24(_ptr(kv), ld, layers, _ptr(out), _ptr(span), B, T, s),
+               "nd_op_ctx_pack_q24")
+    return out
+
+
+def op_dec_ctx_attention_q24(qp, kvq, layer, signal, span, pad_val, rpc):
+    """Context attention on the 24-bit image (nd_op_dec_ctx_attention_q24): qp
+    [R16, 256] P16-packed, kvq = op_ctx_pack_q24's image; returns out packed."""
+    C, T = signal.shape
+    out = torch.empty(qp.shape[0], qp.shape[1], dtype=torch.float32, device=qp.device)
+    s = ctypes.c_void_p(torch.cuda.current_stream(qp.device).cuda_stream)
+    _lib.check(_lib.lib().nd_op_dec_ctx_attention_q24(_ptr(qp), _ptr(kvq), kvq.shape[1], layer, _ptr(signal),
+                                                      _ptr(span), float(pad_val), _ptr(out), C, rpc, T, s),
+               "nd_op_dec_ctx_attention_q24")
+    return out
+
+
 def op_memory_pack(x, B, T, ln_g=None, ln_b=None, ldT=None):
     """Encoder output x [B*T, 256] -> row-major memory bank [B*ldT, 256]
     (LayerNorm'd when ln_g is given; rows t >= T of each chunk zero)."""

@@ -467,6 +467,90 @@ def test_bank_d8_beam_vs_fp64(rpc):
                 assert err < 2e-5 * max(1.0, np.abs(want).max()), (c, j, h, L, err)
 
 
+def test_ctx_pack_q24_bitexact():
+    """The 24-bit context K/V image (nd_op_ctx_pack_q24) equals the numpy
+    restatement byte for byte (tests/test_ctx_q24_scheme.py): heads from 1e-30
+    to 1e30, a zero head, values that round to the clamp, rows past a span
+    left unwritten; a non-finite head gets a NaN scale."""
+    from nanodecoder_amd.engine import op_ctx_pack_q24
+    from tests.test_ctx_q24_scheme import pack_q24
+    rng = np.random.default_rng(23)
+    B, T, Ld = 6, 512, 3
+    kv = rng.standard_normal((B * T, Ld * 512)).astype(np.float32)
+    kv[5, :32] = 0.0
+    kv[7] *= np.float32(1e-30)
+    kv[8] *= np.float32(1e30)
+    kv[9, 64:96] = np.float32(1.0) - np.float32(2.0 ** -24)
+    kv[10, 600:632] *= 1e-3
+    kv[10, 600] = 7e4
+    spans = np.array([T, 1, 300, T - 1, 17, T], np.int32)
+    dev = torch.device("cuda", 0)
+    got = op_ctx_pack_q24(torch.from_numpy(kv).to(dev), Ld * 512, Ld, torch.from_numpy(spans).to(dev), B, T)
+    torch.cuda.synchronize()
+    got = got.cpu().numpy()
+    want = pack_q24(kv, Ld * 512, Ld, spans, B, T)
+    bad = np.argwhere(got != want)
+    assert bad.size == 0, bad[:8]
+    kv[3 * T + 2, 256 + 40] = np.nan  # v of head 1, layer 0
+    got = op_ctx_pack_q24(torch.from_numpy(kv).to(dev), Ld * 512, Ld, torch.from_numpy(spans).to(dev), B, T)
+    sc = got[3 * T + 2, 0, 1536:1600].cpu().numpy().view(np.float32).reshape(8, 2)
+    assert np.isnan(sc[1, 1]) and np.isfinite(np.delete(sc.reshape(-1), 3)).all()
+
+
+@pytest.mark.parametrize("rpc", [1, 2, 5, 6])
+@pytest.mark.parametrize("q24", [False, True])
+def test_ctx_attention_vs_fp64(rpc, q24):
+    """The beam's context attention (dec_ctx_attention_kernel, fp32 K/V or the
+    24-bit image) against fp64 softmax(q k^T / sqrt(32), mask) v per row and
+    head (multi_headed_attn.py:142-177): ragged spans (1, a partial block,
+    512), pad-masked keys, an all-masked chunk, a late key far above the
+    first keys' maximum, heads 1e3 apart, a zero q row.  Tolerance: 1e-5 of
+    the output's magnitude (fp32 K/V), 2e-5 on the image (its elements carry
+    2^-23 of their head's largest value)."""
+    from nanodecoder_amd.engine import (op_ctx_pack_q24, op_dec_ctx_attention, op_dec_ctx_attention_q24,
+                                        pack_p16, unpack_p16)
+    rng = np.random.default_rng(31 + rpc)
+    C, T, Ld, PAD = 7, 512, 3, 1.0
+    spans = np.array([T, 1, 15, 300, T, T - 5, 77], np.int32)
+    sig = rng.standard_normal((C, T)).astype(np.float32)
+    sig[2, ::3] = PAD
+    sig[4, :] = PAD
+    kv = rng.standard_normal((C * T, Ld * 512)).astype(np.float32)
+    kv[0 * T + 450, 512:1024] *= 6.0            # layer 1: a late key past the first blocks' maximum
+    kv[5 * T: 6 * T, 512 + 64: 512 + 96] *= 1e3  # layer 1, head 2 of chunk 5
+    R = C * rpc
+    q = rng.standard_normal((R, 256)).astype(np.float32)
+    q[6 * rpc] = 0.0
+    dev = torch.device("cuda", 0)
+    kvd = torch.from_numpy(kv).to(dev)
+    sp = torch.from_numpy(spans).to(dev)
+    sg = torch.from_numpy(sig).to(dev)
+    qp = pack_p16(torch.from_numpy(q).to(dev))
+    layer = 1
+    if q24:
+        img = op_ctx_pack_q24(kvd, Ld * 512, Ld, sp, C, T)
+        out = op_dec_ctx_attention_q24(qp, img, layer, sg, sp, PAD, rpc)
+    else:
+        out = op_dec_ctx_attention(qp, kvd, Ld * 512, layer * 512, sg, sp, PAD, rpc, packed=True)
+    torch.cuda.synchronize()
+    got = unpack_p16(out, R).cpu().numpy()
+    K = kv[:, layer * 512: layer * 512 + 256].astype(np.float64)
+    V = kv[:, layer * 512 + 256: (layer + 1) * 512].astype(np.float64)
+    tol = 2e-5 if q24 else 1e-5
+    for c in range(C):
+        L = int(spans[c])
+        for j in range(rpc):
+            r = c * rpc + j
+            for h in range(8):
+                hs = slice(h * 32, (h + 1) * 32)
+                s = K[c * T: c * T + L, hs] @ q[r, hs].astype(np.float64) / np.sqrt(32)
+                s[sig[c, :L] == PAD] = -1e18
+                p = np.exp(s - s.max())
+                want = (p / p.sum()) @ V[c * T: c * T + L, hs]
+                err = np.abs(got[r, hs] - want).max()
+                assert err < tol * max(1.0, np.abs(V[c * T: c * T + L, hs]).max()), (c, j, h, L, err)
+
+
 def test_engine_reports_bank_form():
     """A greedy call at 512-sample chunks streams the 24-bit digit bank by
     default (nd_bank_form 2; ND_BANK_D8=0: the split-fp16 bank, 1), exact
@@ -476,12 +560,19 @@ def test_engine_reports_bank_form():
     W = synth.make_weights(cfg, seed=11, eos_bias=-3.0)
     sig = synth.synth_chunk_batch(8, 512, seed=5)
     lens = np.full(8, 512, np.int32)
-    eng = _engine(cfg, W, max_batch=8, max_steps=20)
+    eng = _engine(cfg, W, max_batch=8, max_steps=20, max_beam=3)
     eng.translate_greedy(sig, lens, lens, max_len=20)
     assert eng.bank_form() == (1 if os.environ.get("ND_BANK_D8") == "0" else 2)
     eng.set_exact_fp32(True)
     eng.translate_greedy(sig, lens, lens, max_len=20)
     assert eng.bank_form() == 0
+    # beam rows: the 24-bit context K/V (3) by default, fp32 K/V in exact fp32 (0)
+    eng.translate_beam(sig, lens, lens, beam=3, max_len=20)
+    assert eng.bank_form() == 0
+    eng.set_exact_fp32(False)
+    eng.translate_beam(sig, lens, lens, beam=3, max_len=20)
+    want = 2 if os.environ.get("ND_BEAM_BANK") == "1" else 0 if os.environ.get("ND_CTX_Q24") == "0" else 3
+    assert eng.bank_form() == want
     eng.close()
 
 
