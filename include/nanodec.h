@@ -510,6 +510,22 @@ int nd_op_dec_ctx_attention_q24(const float* q, const void* kvq, int32_t layers,
                                 const int32_t* span, float pad_val, float* out, int32_t C, int32_t rpc, int32_t T,
                                 void* stream);
 
+/* The --fast beam tail's forms (translate/translator.py:793-823 drops
+ * finished batches; the engine launches over the alive chunks only once at
+ * most a sixteenth of them remain).  nd_op_alive_list: chunks c < C with
+ * done[c] == 0, ascending, into list[0 .. cap), the rest -1; more than cap
+ * alive sets *ovf (nullable) to 1.  nd_op_dec_ctx_attention_list: the context
+ * attention (fp32 K/V, or the 24-bit image when q24 != 0 with ld / koff in
+ * bytes) for the listed chunks only (list entries -1 and chunks with done[c]
+ * != 0 untouched), each chunk's keys in nsplit workgroups (1..64) whose
+ * partial softmax states go to part (ccap * nsplit * rpc * 272 floats) and
+ * are combined by a second launch. */
+int nd_op_alive_list(const int32_t* done, int32_t C, int32_t* list, int32_t cap, int32_t* ovf, void* stream);
+int nd_op_dec_ctx_attention_list(const float* q, const void* kv, int32_t ld, int32_t koff, int32_t q24,
+                                 const float* signal, const int32_t* span, float pad_val, float* out, int32_t C,
+                                 int32_t rpc, int32_t T, const int32_t* clist, int32_t ccap, int32_t nsplit,
+                                 float* part, const int32_t* done, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -824,6 +824,44 @@ __device__ __forceinline__ void merge_waves(float* accs, float* ms, float* ls, c
   }
 }
 
+// merge_waves without the normalisation: per row j the workgroup's partial
+// state {num[256], max[8], den[8]} at part + j * CTX_PART (the split
+// context attention; ctx_split_merge_kernel combines the splits).
+#define CTX_PART (ND_D + 2 * ND_H)
+template <int RPC, int NW>
+__device__ __forceinline__ void merge_waves_part(float* accs, float* ms, float* ls, const float (&m)[RPC],
+                                                 const float (&l)[RPC], const f32x4 (&acc)[RPC], int wave, int lane,
+                                                 int tid, float* __restrict__ part) {
+#pragma unroll
+  for (int j = 0; j < RPC; ++j) {
+    st4(accs + ((size_t)wave * RPC + j) * ND_D + lane * 4, acc[j]);
+    if ((lane & 7) == 0) {
+      ms[(wave * RPC + j) * ND_H + (lane >> 3)] = m[j];
+      ls[(wave * RPC + j) * ND_H + (lane >> 3)] = l[j];
+    }
+  }
+  lds_barrier();
+  for (int e = tid; e < RPC * ND_D; e += NW * 64) {
+    const int j = e / ND_D, d = e % ND_D, h = d / ND_DH;
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) M = fmaxf(M, ms[(w * RPC + j) * ND_H + h]);
+    float num = 0.f, den = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const float mw = ms[(w * RPC + j) * ND_H + h];
+      const float f = mw == -INFINITY ? 0.f : __expf(mw - M);
+      num += f * accs[((size_t)w * RPC + j) * ND_D + d];
+      den += f * ls[(w * RPC + j) * ND_H + h];
+    }
+    part[j * CTX_PART + d] = num;
+    if ((d & (ND_DH - 1)) == 0) {
+      part[j * CTX_PART + ND_D + h] = M;
+      part[j * CTX_PART + ND_D + ND_H + h] = den;
+    }
+  }
+}
+
 // Decoder self-attention, one workgroup per row, single pass.
 // cache layout: [slot][t][512] = k (256) | v (256), one slot per row; key t
 // of row r lives in slot anc[r][t] (beam ancestry; identity when anc is
@@ -846,7 +884,7 @@ template <int NW, int KW, bool ANC, bool HEAD>
 __global__ void __launch_bounds__(NW * 64)
 dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cache, const int* __restrict__ anc,
                           int anc_ld, int step, int S, float* __restrict__ out, int rpc, const int* __restrict__ skip,
-                          int skip_rpc, QkvRows qr, GreedyHead hd) {
+                          int skip_rpc, QkvRows qr, GreedyHead hd, const int* __restrict__ clist) {
 #ifdef ND_SKIP_SELF  // timing probe only (tools/build_variant.sh): the kernel's marginal cost
   if (threadIdx.x < 100000) return;
 #endif
@@ -858,7 +896,11 @@ dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cac
   // 8 (b / 8 / rpc) + b % 8, beam (b / 8) % rpc, so one chunk's rows share an
   // XCD and its L2 serves their common history once
   int r = blockIdx.x;
-  if (rpc > 1) {
+  if (clist) {  // --fast beam tail: workgroups over the listed chunks only (-1: none)
+    const int cc = clist[r / skip_rpc];
+    if (cc < 0) return;
+    r = cc * skip_rpc + r % skip_rpc;
+  } else if (rpc > 1) {
     const int j = r >> 3;
     r = ((j / rpc) * 8 + (r & 7)) * rpc + j % rpc;
   }
@@ -978,7 +1020,7 @@ dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cac
 
 hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* anc, int anc_ld, int step,
                                      int max_steps, float* out, int R, hipStream_t s, int rpc, const int* skip,
-                                     const QkvRows& qr, const GreedyHead* head) {
+                                     const QkvRows& qr, const GreedyHead* head, const int* clist, int ccap) {
   if (qr.tok && (qr.V < 1 || qr.tok0 < 0 || qr.tok0 >= qr.V)) return hipErrorInvalidValue;
   if (head) {
     if (!qr.tok || anc || skip || rpc != 1 || step < 1 || head->V != qr.V || head->V > SELF_TABV ||
@@ -994,11 +1036,13 @@ hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* 
     return e ? atoi(e) : 1;
   }();
   if (!xcd || rpc < 2 || R % (8 * rpc)) rpc = 1;
+  if (clist && (ccap < 1 || (long)ccap * skip_rpc > R || head)) return hipErrorInvalidValue;
+  const int grid = clist ? ccap * skip_rpc : R;
   if (step >= max_steps || step >= SELF_MAXS) return hipErrorInvalidValue;
   const int n = step + 1;
 #define ND_SELF2(NW, KW, A, HD)                                                                                  \
-  hipLaunchKernelGGL((dec_self_attention_kernel<NW, KW, A, HD>), dim3(R), dim3(NW * 64), 0, s, qkv, cache, anc,     \
-                     anc_ld, step, max_steps, out, rpc, skip, skip_rpc, qr, hd)
+  hipLaunchKernelGGL((dec_self_attention_kernel<NW, KW, A, HD>), dim3(grid), dim3(NW * 64), 0, s, qkv, cache, anc,  \
+                     anc_ld, step, max_steps, out, rpc, skip, skip_rpc, qr, hd, clist)
 #define ND_SELF(NW, KW)                \
   if (anc)                             \
     ND_SELF2(NW, KW, true, false);     \
@@ -1061,15 +1105,20 @@ __global__ void __launch_bounds__(CTX_NW * 64)
 dec_ctx_attention_kernel(const float* __restrict__ q, const void* __restrict__ kv_, int ld, int koff,
                          const float* __restrict__ signal, const int* __restrict__ span, float pad_val,
                          float* __restrict__ out, int T, unsigned long long* stamp, float* __restrict__ dbg,
-                         size_t dbg_stride, const int* __restrict__ skip) {
-  if (skip && skip[blockIdx.x]) return;  // finished chunk (--fast beam, translator.py:793-823)
+                         size_t dbg_stride, const int* __restrict__ skip, const int* __restrict__ clist, int nsplit,
+                         float* __restrict__ part) {
+  // --fast beam tail: workgroups over the listed chunks only (-1: none), nsplit
+  // workgroups per chunk (the keys in nsplit ranges; their unnormalised states
+  // go to part and ctx_split_merge_kernel combines them)
+  const int c = clist ? clist[blockIdx.x / nsplit] : (int)blockIdx.x;
+  if (c < 0 || (skip && skip[c])) return;  // finished chunk (--fast beam, translator.py:793-823)
   stamp_begin(stamp);
   constexpr int U = CtxTile<RPC>::U;
   extern __shared__ float sm[];
   float* accs = sm;                              // [NW][RPC][256]
   float* ms = sm + CTX_NW * RPC * ND_D;          // [NW][RPC][8]
   float* ls = ms + CTX_NW * RPC * ND_H;          // [NW][RPC][8]
-  const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int L = min(span[c], T);
   const size_t base = (size_t)c * T;
   const float* sgc = signal + base;
@@ -1106,12 +1155,15 @@ dec_ctx_attention_kernel(const float* __restrict__ q, const void* __restrict__ k
       ss[u] = sgc[t];
     }
   };
-  int blk = wave;
-  if (blk * U < L) load(blk, kc, vc, sg);
-  for (; blk * U < L; blk += CTX_NW) {
+  // this workgroup's key blocks [b0, b1) (all of them unless split)
+  const int nblk = (L + U - 1) / U, bps = (nblk + nsplit - 1) / nsplit;
+  const int b0 = (blockIdx.x % nsplit) * bps, b1 = min(nblk, b0 + bps);
+  int blk = b0 + wave;
+  if (blk < b1) load(blk, kc, vc, sg);
+  for (; blk < b1; blk += CTX_NW) {
     f32x4 kn[U], vn[U];
     float sn[U];
-    const bool more = (blk + CTX_NW) * U < L;
+    const bool more = blk + CTX_NW < b1;
     if (more) load(blk + CTX_NW, kn, vn, sn);
     float sc[RPC][U];
     f32x4 vf[U];
@@ -1149,8 +1201,33 @@ dec_ctx_attention_kernel(const float* __restrict__ q, const void* __restrict__ k
       }
     }
   }
-  merge_waves<RPC, CTX_NW>(accs, ms, ls, m, l, acc, wave, lane, tid, out, c * RPC);
+  if (part)
+    merge_waves_part<RPC, CTX_NW>(accs, ms, ls, m, l, acc, wave, lane, tid, part + (size_t)blockIdx.x * RPC * CTX_PART);
+  else
+    merge_waves<RPC, CTX_NW>(accs, ms, ls, m, l, acc, wave, lane, tid, out, c * RPC);
   stamp_end(stamp);
+}
+
+// The split form's combine: row j of listed chunk b from its nsplit partial
+// states {num[256], max[8], den[8]} (one workgroup of 256 threads per row).
+__global__ void __launch_bounds__(256)
+ctx_split_merge_kernel(const float* __restrict__ part, const int* __restrict__ clist, const int* __restrict__ skip,
+                       int nsplit, int rpc, float* __restrict__ out) {
+  const int b = blockIdx.x / rpc, j = blockIdx.x % rpc, d = threadIdx.x, h = d / ND_DH;
+  const int c = clist[b];
+  if (c < 0 || (skip && skip[c])) return;
+  const float* p = part + ((size_t)b * nsplit * rpc + j) * CTX_PART;
+  const size_t ps = (size_t)rpc * CTX_PART;  // one split's states
+  float M = -INFINITY;
+  for (int s = 0; s < nsplit; ++s) M = fmaxf(M, p[s * ps + ND_D + h]);
+  float num = 0.f, den = 0.f;
+  for (int s = 0; s < nsplit; ++s) {
+    const float ms = p[s * ps + ND_D + h];
+    const float f = ms == -INFINITY ? 0.f : __expf(ms - M);  // a split with no key
+    num += f * p[s * ps + d];
+    den += f * p[s * ps + ND_D + ND_H + h];
+  }
+  out[pk(c * rpc + j, d & ~3, ND_D) + (d & 3)] = den > 0.f ? num * __builtin_amdgcn_rcpf(den) : 0.f;
 }
 
 // fp32 K/V [M][ld] (layer l's k | v at column koff + l * 512) -> the 24-bit
@@ -1215,18 +1292,25 @@ static size_t ctx_lds_bytes(int rpc) { return (size_t)CTX_NW * rpc * (ND_D + 2 *
 hipError_t launch_dec_ctx_attention(const float* q, const void* kv, int ld, int koff, const float* signal,
                                     const int* span, float pad_val, float* out, int C, int rpc, int T,
                                     hipStream_t s, unsigned long long* stamp, float* attn_dbg, size_t dbg_stride,
-                                    const int* skip, bool q24) {
+                                    const int* skip, bool q24, const int* clist, int ccap, int nsplit, float* part) {
   if (rpc < 1 || rpc > CTX_MAXR || T > 512) return hipErrorInvalidValue;
+  if (clist && (ccap < 1 || ccap > C)) return hipErrorInvalidValue;
+  if (!clist || !part || attn_dbg) nsplit = 1;  // the split form runs over a chunk list (the -attn_debug form whole)
+  if (nsplit < 1 || nsplit > 64) return hipErrorInvalidValue;
+  float* const pout = nsplit > 1 ? part : nullptr;
+  const int grid = clist ? ccap * nsplit : C;
   const size_t lds = ctx_lds_bytes(rpc);
   switch (rpc) {
 #define ND_CTX_CASE(R)                                                                                            \
   case R:                                                                                                         \
     if (q24)                                                                                                      \
-      hipLaunchKernelGGL((dec_ctx_attention_kernel<R, true>), dim3(C), dim3(CTX_NW * 64), lds, s, q, kv, ld, koff, \
-                         signal, span, pad_val, out, T, stamp, attn_dbg, dbg_stride, skip);                       \
+      hipLaunchKernelGGL((dec_ctx_attention_kernel<R, true>), dim3(grid), dim3(CTX_NW * 64), lds, s, q, kv, ld,   \
+                         koff, signal, span, pad_val, out, T, stamp, attn_dbg, dbg_stride, skip, clist, nsplit,   \
+                         pout);                                                                                   \
     else                                                                                                          \
-      hipLaunchKernelGGL((dec_ctx_attention_kernel<R, false>), dim3(C), dim3(CTX_NW * 64), lds, s, q, kv, ld,     \
-                         koff, signal, span, pad_val, out, T, stamp, attn_dbg, dbg_stride, skip);                 \
+      hipLaunchKernelGGL((dec_ctx_attention_kernel<R, false>), dim3(grid), dim3(CTX_NW * 64), lds, s, q, kv, ld,  \
+                         koff, signal, span, pad_val, out, T, stamp, attn_dbg, dbg_stride, skip, clist, nsplit,   \
+                         pout);                                                                                   \
     break;
     ND_CTX_CASE(1)
     ND_CTX_CASE(2)
@@ -1235,6 +1319,11 @@ hipError_t launch_dec_ctx_attention(const float* q, const void* kv, int ld, int 
     ND_CTX_CASE(5)
     ND_CTX_CASE(6)
 #undef ND_CTX_CASE
+  }
+  if (nsplit > 1) {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(ctx_split_merge_kernel, dim3(ccap * rpc), dim3(ND_D), 0, s, part, clist, skip, nsplit, rpc, out);
   }
   return hipGetLastError();
 }
@@ -1250,6 +1339,33 @@ __global__ void fill_i32_kernel(int* p, int v, int n) {
 
 hipError_t launch_fill_i32(int* p, int v, int n, hipStream_t s) {
   hipLaunchKernelGGL(fill_i32_kernel, dim3((n + 255) / 256), dim3(256), 0, s, p, v, n);
+  return hipGetLastError();
+}
+
+// --fast beam tail: the chunks not yet done, in ascending order, into
+// list[0 .. cap) (the rest -1).  One workgroup; a wave ballot per 64 chunks.
+// The engine builds it at the start of a tail segment, when at most cap
+// chunks are alive (chunks finishing inside the segment are skipped by their
+// done flag); more than cap alive sets *ovf (the caller's guard is violated).
+__global__ void __launch_bounds__(64)
+alive_list_kernel(const int* __restrict__ done, int C, int* __restrict__ list, int cap, int* __restrict__ ovf) {
+  const int lane = threadIdx.x;
+  int n = 0;
+  for (int c0 = 0; c0 < C; c0 += 64) {
+    const int c = c0 + lane;
+    const bool alive = c < C && done[c] == 0;
+    const unsigned long long m = __ballot(alive);
+    const int k = n + __popcll(m & ((1ull << lane) - 1ull));
+    if (alive && k < cap) list[k] = c;
+    n += __popcll(m);
+  }
+  for (int k = n + lane; k < cap; k += 64) list[k] = -1;
+  if (n > cap && lane == 0 && ovf) *ovf = 1;
+}
+
+hipError_t launch_alive_list(const int* done, int C, int* list, int cap, int* ovf, hipStream_t s) {
+  if (C < 1 || cap < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(alive_list_kernel, dim3(1), dim3(64), 0, s, done, C, list, cap, ovf);
   return hipGetLastError();
 }
 

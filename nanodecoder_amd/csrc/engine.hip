@@ -175,6 +175,8 @@ struct nd_ctx {
   bool bank_d8 = false;                   // ... or the 24-bit digit bank (dec_bank_d8_kernel; bank8.hip)
   bool beam_bank = false;                 // beam rows read the digit bank (dec_bank_d8_beam_kernel), not K/V
   bool ctx_q24 = false;                   // beam rows read the 24-bit context K/V image (ctxq), not fp32 ctxkv
+  int* clist = nullptr;                   // --fast beam tail: the alive chunks (launch_alive_list), ceil(B/16)
+  float* ctx_part = nullptr;              // ... and the split context attention's partial states
   uint8_t* ctxq = nullptr;                // [B * T][layers][CTXQ_ROW] (attention.hip ctx_pack_q24_kernel)
   float* bank_ks = nullptr;               // digit bank: per-row scales 2^e_t [B * 512]
   int* bank_em = nullptr;                 // digit bank: per-chunk max e_t (biased) [B]
@@ -398,6 +400,11 @@ static int alloc_workspaces(nd_ctx* c) {
     float* q = nullptr;
     WS(q, B * T * Ld * (CTXQ_ROW / 4));
     c->ctxq = reinterpret_cast<uint8_t*>(q);
+    float* l = nullptr;
+    WS(l, B);
+    c->clist = reinterpret_cast<int*>(l);
+    // ceil(B/16) listed chunks x up to 32 splits x rows x {num[256], max[8], den[8]}
+    WS(c->ctx_part, (B + 15) / 16 * 32 * std::max(1, cfg.max_beam) * (D + 16));
   }
   WS(c->mem_p, B * T * D);
   WS(c->bank_ks, B * 512);
@@ -767,6 +774,26 @@ static bool use_ctx_q24() {
   return on;
 }
 
+// --fast beam tail launches over the alive chunks (launch_alive_list); ND_BEAM_COMPACT=0: over all B
+static bool use_beam_compact() {
+  static const bool on = [] {
+    const char* e = getenv("ND_BEAM_COMPACT");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
+// --fast beam tail: the context attention over a chunk's keys in this many workgroups (one per CU: a lone
+// chunk's 512 keys are latency-bound on one workgroup, ~150 us); ND_CTX_SPLIT=1 keeps one per chunk
+static int ctx_split() {
+  static const int n = [] {
+    const char* e = getenv("ND_CTX_SPLIT");
+    const int v = e ? atoi(e) : 16;
+    return std::min(32, std::max(1, v));
+  }();
+  return n;
+}
+
 static void set_memory_view(nd_ctx* c, int T, int rpc) {
   c->bank_h3 = false;
   c->bank_d8 = false;
@@ -789,7 +816,8 @@ static void set_memory_view(nd_ctx* c, int T, int rpc) {
 // done: per chunk, nonzero = finished (--fast beam; null otherwise): its rows'
 // tiles and attention workgroups exit without work
 static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, const int* anc, int anc_ld,
-                                   hipStream_t s, const int* done = nullptr, const nd::GreedyHead* head = nullptr) {
+                                   hipStream_t s, const int* done = nullptr, const nd::GreedyHead* head = nullptr,
+                                   const int* clist = nullptr, int ccap = 0) {
   const int R = C * rpc, D = c->D, F = c->F, S = c->cfg.max_steps;
   const int Ld = (int)c->dec.size();
   const bool mb = use_memory_bank(c, rpc);
@@ -824,14 +852,16 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
         qr.V = c->V;
         qr.tok0 = c->cfg.bos_idx;
         qr.rm = 1;  // the table is row-major (enqueue_qkv_table)
-        LCHK(nd::launch_dec_self_attention(c->qtab, cache, anc, anc_ld, step, S, c->datt, R, s, rpc, done, qr, head));
+        LCHK(nd::launch_dec_self_attention(c->qtab, cache, anc, anc_ld, step, S, c->datt, R, s, rpc, done, qr, head,
+                                           clist, ccap));
       } else {
         // greedy rows (one workgroup each): q | k | v row-major; beam keeps P16 (its M = 5120 GEMMs
         // take the LDS-tiled route, which writes P16)
         nd::QkvRows q12;
         q12.rm = (rpc == 1 && !anc && !done) ? 1 : 0;
         LCHK(dg(c->dx, D, L.pwqkv, 3 * D, D, L.nbqkv, c->dqkv, 3 * D).ln(c->dx_part, pnx).c_rowmajor(q12.rm).run(s));
-        LCHK(nd::launch_dec_self_attention(c->dqkv, cache, anc, anc_ld, step, S, c->datt, R, s, rpc, done, q12));
+        LCHK(nd::launch_dec_self_attention(c->dqkv, cache, anc, anc_ld, step, S, c->datt, R, s, rpc, done, q12, nullptr,
+                                           clist, ccap));
       }
       LCHK(dg(c->datt, D, L.pwo, D, D, L.bo, c->dq1, D).res(c->dx, D).stats(c->dq1_part).run(s, &pnq));
     }
@@ -859,10 +889,11 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
       if (c->ctx_q24)
         LCHK(nd::launch_dec_ctx_attention(c->dcq, c->ctxq, Ld * CTXQ_ROW, i * CTXQ_ROW, c->sig, c->span,
                                           (float)c->cfg.pad_idx, c->datt, C, rpc, T, s, stamp, dbg, dbg_stride, done,
-                                          true));
+                                          true, clist, ccap, ctx_split(), c->ctx_part));
       else
         LCHK(nd::launch_dec_ctx_attention(c->dcq, c->ctxkv, Ld * 2 * D, i * 2 * D, c->sig, c->span,
-                                          (float)c->cfg.pad_idx, c->datt, C, rpc, T, s, stamp, dbg, dbg_stride, done));
+                                          (float)c->cfg.pad_idx, c->datt, C, rpc, T, s, stamp, dbg, dbg_stride, done,
+                                          false, clist, ccap, ctx_split(), c->ctx_part));
       LCHK(dg(c->datt, D, L.pcwo, D, D, L.cbo, c->dmid, D).res(c->dq1, D).stats(c->dmid_part).run(s, &pnm));
     }
     LCHK(dg(c->dmid, D, L.pw1, F, D, L.nb1, c->dhid, F).ln(c->dmid_part, pnm).relu().run(s));
@@ -937,13 +968,21 @@ static hipError_t enqueue_attn_step(nd_ctx* c, int C, int rpc, int T, int step, 
 static hipError_t enqueue_beam_steps(nd_ctx* c, int B, int T, int beam, int n_best, float alpha, int S, int min_len,
                                      int s0, int s1, hipStream_t s) {
   const nd::BeamState st = beam_state(c);
+  // the tail (at most a sixteenth of the chunks alive, translate_beam): the attention and beam-step launches
+  // run over the segment's alive chunks only (a list built at its start), not B chunks that exit at once
+  const int ccap = (B + 15) / 16;
+  const int* clist = nullptr;
+  if (c->beam_tail && use_beam_compact()) {
+    LCHK(nd::launch_alive_list(c->bs.done, B, c->clist, ccap, c->ovf, s));
+    clist = c->clist;
+  }
   for (int step = s0; step < s1; ++step) {
     const int cur = step & 1;
-    LCHK(enqueue_dec_step(c, B, beam, T, step, c->bs.anc[cur], S, s, c->bs.done));
+    LCHK(enqueue_dec_step(c, B, beam, T, step, c->bs.anc[cur], S, s, c->bs.done, nullptr, clist, ccap));
     LCHK(enqueue_attn_step(c, B, beam, T, step, s));
     const float lenpen = (float)std::pow((5.0 + (step + 1)) / 6.0, (double)alpha);
     LCHK(nd::launch_beam_step(next_embed(c), c->dx, c->dec_ln_g, c->dec_ln_b, c->gen_w, c->gen_b, c->V, st, B, beam,
-                              n_best, step, S, min_len, c->cfg.eos_idx, lenpen, s));
+                              n_best, step, S, min_len, c->cfg.eos_idx, lenpen, s, clist, ccap));
   }
   return hipSuccess;
 }
@@ -1687,7 +1726,7 @@ static const struct {
                  {"ND_ENC_WO", 1},     {"ND_ENC_QKV0", 1},
                  {"ND_ENC_QKV", 1},    {"ND_ENC_ATTN0", 1},   {"ND_SELF_NW8", 1},     {"ND_BANK_D8", 1},
                  {"ND_BEAM_BANK", 0},  {"ND_BB_PIPE", 1},     {"ND_P16_K2048", 0},
-                 {"ND_CTX_Q24", 1}};
+                 {"ND_CTX_Q24", 1},    {"ND_BEAM_COMPACT", 1}, {"ND_CTX_SPLIT", 16}};
 
 int nd_switches(char* buf, int32_t len) {
   std::string out;
@@ -2052,6 +2091,27 @@ int nd_op_ctx_pack_q24(const float* kv, int32_t ld, int32_t layers, void* out, c
   if (!kv || !out || !span) return fail(ND_ERR_ARG, "ctx_pack_q24: bad arguments");
   hipError_t e = nd::launch_ctx_pack_q24(kv, ld, layers, static_cast<uint8_t*>(out), span, B, T, (hipStream_t)stream);
   if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("ctx_pack_q24: ") + hipGetErrorString(e));
+  return ND_OK;
+}
+
+int nd_op_dec_ctx_attention_list(const float* q, const void* kv, int32_t ld, int32_t koff, int32_t q24,
+                                 const float* signal, const int32_t* span, float pad_val, float* out, int32_t C,
+                                 int32_t rpc, int32_t T, const int32_t* clist, int32_t ccap, int32_t nsplit,
+                                 float* part, const int32_t* done, void* stream) {
+  if (int rc = ensure_attributes()) return rc;
+  if (!q || !kv || !signal || !span || !out || !clist || (nsplit > 1 && !part))
+    return fail(ND_ERR_ARG, "dec_ctx_attention_list: bad arguments");
+  hipError_t e = nd::launch_dec_ctx_attention(q, kv, ld, koff, signal, span, pad_val, out, C, rpc, T,
+                                              (hipStream_t)stream, nullptr, nullptr, 0, done, q24 != 0, clist, ccap,
+                                              nsplit, part);
+  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("dec_ctx_attention_list: ") + hipGetErrorString(e));
+  return ND_OK;
+}
+
+int nd_op_alive_list(const int32_t* done, int32_t C, int32_t* list, int32_t cap, int32_t* ovf, void* stream) {
+  if (!done || !list) return fail(ND_ERR_ARG, "alive_list: bad arguments");
+  hipError_t e = nd::launch_alive_list(done, C, list, cap, ovf, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("alive_list: ") + hipGetErrorString(e));
   return ND_OK;
 }
 

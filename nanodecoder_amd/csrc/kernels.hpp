@@ -194,14 +194,20 @@ struct GreedyHead;
 hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* anc, int anc_ld, int step,
                                      int max_steps, float* out, int R, hipStream_t s, int rpc = 1,
                                      const int* skip = nullptr, const QkvRows& qr = QkvRows(),
-                                     const GreedyHead* head = nullptr);
+                                     const GreedyHead* head = nullptr, const int* clist = nullptr, int ccap = 0);
 // context attention: rows r = c*rpc + j attend over ctxkv rows of chunk c
 // (K at kv[(c*T+t)*ld + koff], V at +256), mask signal == pad_val, keys < span.
 // q24: kv is the 24-bit image of launch_ctx_pack_q24 (ld, koff in bytes).
 hipError_t launch_dec_ctx_attention(const float* q, const void* kv, int ld, int koff, const float* signal,
                                     const int* span, float pad_val, float* out, int C, int rpc, int T,
                                     hipStream_t s, unsigned long long* stamp = nullptr, float* attn_dbg = nullptr,
-                                    size_t dbg_stride = 0, const int* skip = nullptr, bool q24 = false);
+                                    size_t dbg_stride = 0, const int* skip = nullptr, bool q24 = false,
+                                    const int* clist = nullptr, int ccap = 0, int nsplit = 1, float* part = nullptr);
+// part: nsplit > 1 (with clist): scratch of ccap * nsplit * rpc * (256 + 16) floats
+// --fast beam tail: clist (nullable) lists the chunks the self / context
+// attention and the beam step run (ccap entries, -1 = none); launch_alive_list
+// builds it from the done flags (*ovf = 1 when more than cap are alive)
+hipError_t launch_alive_list(const int* done, int C, int* list, int cap, int* ovf, hipStream_t s);
 // 24-bit context K/V (beam rows): per (key row, layer) CTXQ_ROW bytes = k's 256
 // integers (3 bytes each, lane i's 12 bytes = dims 4i..4i+3) | v's | per head
 // {k scale, v scale} (powers of two, f32).  Image [B*T][Ld][CTXQ_ROW] from the
@@ -359,7 +365,7 @@ struct ClassicOpts {
 hipError_t launch_beam_init(const BeamState& st, int C, int beam, int n_best, int S, int bos, hipStream_t s);
 hipError_t launch_beam_step(const NextEmbed& ne, const float* x, const float* ln_g, const float* ln_b, const float* gw, const float* gb,
                             int V, const BeamState& st, int C, int beam, int n_best, int step, int S, int min_len,
-                            int eos, float lenpen, hipStream_t s);
+                            int eos, float lenpen, hipStream_t s, const int* clist = nullptr, int ccap = 0);
 hipError_t launch_beam_finish(const BeamState& st, int C, int n_best, int S, int* tokens, float* scores, int* lens,
                               hipStream_t s);
 // classic Beam: length_penalty 0 none, 1 wu, 2 avg (onmt/translate/penalties.py)

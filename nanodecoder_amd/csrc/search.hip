@@ -87,13 +87,13 @@ hipError_t launch_beam_init(const BeamState& st, int C, int beam, int n_best, in
 __global__ void __launch_bounds__(256)
 beam_step_kernel(NextEmbed ne, const float* __restrict__ x, const float* __restrict__ ln_g, const float* __restrict__ ln_b,
                  const float* __restrict__ gw, const float* __restrict__ gb, int V, BeamState st, int beam,
-                 int n_best, int step, int S, int min_len, int eos, float lenpen) {
+                 int n_best, int step, int S, int min_len, int eos, float lenpen, const int* __restrict__ clist) {
   __shared__ float lp[BEAM_MAX][ND_MAXV];
   __shared__ float tsc[BEAM_MAX];
   __shared__ int tid_sel[BEAM_MAX];
   __shared__ int fin[BEAM_MAX];
-  const int c = blockIdx.x, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  if (st.done[c]) return;  // finished batches are dropped (translator.py:793-810)
+  const int c = clist ? clist[blockIdx.x] : (int)blockIdx.x, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  if (c < 0 || st.done[c]) return;  // finished batches are dropped (translator.py:793-810); tail list: -1 = none
   const int cur = step & 1, nxt = cur ^ 1;
   const int row0 = c * beam;
   for (int j = w; j < beam; j += 4) {
@@ -207,10 +207,11 @@ beam_step_kernel(NextEmbed ne, const float* __restrict__ x, const float* __restr
 
 hipError_t launch_beam_step(const NextEmbed& ne, const float* x, const float* ln_g, const float* ln_b, const float* gw, const float* gb,
                             int V, const BeamState& st, int C, int beam, int n_best, int step, int S, int min_len,
-                            int eos, float lenpen, hipStream_t s) {
+                            int eos, float lenpen, hipStream_t s, const int* clist, int ccap) {
   if (beam > BEAM_MAX || beam * V > 256 || V > ND_MAXV || !ne.emb || !ne.x || !ne.part) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(beam_step_kernel, dim3(C), dim3(256), 0, s, ne, x, ln_g, ln_b, gw, gb, V, st, beam, n_best, step,
-                     S, min_len, eos, lenpen);
+  if (clist && (ccap < 1 || ccap > C)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(beam_step_kernel, dim3(clist ? ccap : C), dim3(256), 0, s, ne, x, ln_g, ln_b, gw, gb, V, st, beam,
+                     n_best, step, S, min_len, eos, lenpen, clist);
   return hipGetLastError();
 }
 

@@ -610,6 +610,31 @@ def op_dec_ctx_attention_q24(qp, kvq, layer, signal, span, pad_val, rpc):
     return out
 
 
+def op_alive_list(done, cap, ovf=None):
+    """nd_op_alive_list: the chunks with done == 0 (ascending) in cap int32 slots, -1 after."""
+    out = torch.empty(cap, dtype=torch.int32, device=done.device)
+    s = ctypes.c_void_p(torch.cuda.current_stream(done.device).cuda_stream)
+    _lib.check(_lib.lib().nd_op_alive_list(_ptr(done), done.numel(), _ptr(out), cap, _ptr(ovf), s), "nd_op_alive_list")
+    return out
+
+
+def op_dec_ctx_attention_list(qp, kv, ld, koff, signal, span, pad_val, rpc, clist, nsplit, q24=False, done=None,
+                              out=None):
+    """nd_op_dec_ctx_attention_list (the --fast beam tail's form): qp P16-packed; kv fp32 [C*T, ld] (or the
+    24-bit image, ld / koff in bytes, q24=True); only the chunks listed in clist are written into out."""
+    C, T = signal.shape
+    ccap = clist.numel()
+    if out is None:
+        out = torch.zeros(qp.shape[0], qp.shape[1], dtype=torch.float32, device=qp.device)
+    part = torch.empty(ccap * nsplit * rpc * 272, dtype=torch.float32, device=qp.device)
+    s = ctypes.c_void_p(torch.cuda.current_stream(qp.device).cuda_stream)
+    _lib.check(_lib.lib().nd_op_dec_ctx_attention_list(_ptr(qp), _ptr(kv), ld, koff, int(q24), _ptr(signal),
+                                                       _ptr(span), float(pad_val), _ptr(out), C, rpc, T, _ptr(clist),
+                                                       ccap, nsplit, _ptr(part), _ptr(done), s),
+               "nd_op_dec_ctx_attention_list")
+    return out
+
+
 def op_memory_pack(x, B, T, ln_g=None, ln_b=None, ldT=None):
     """Encoder output x [B*T, 256] -> row-major memory bank [B*ldT, 256]
     (LayerNorm'd when ln_g is given; rows t >= T of each chunk zero)."""

@@ -133,7 +133,7 @@ DYNAMIC_LDS = {  # kernels launched with dynamic LDS (metadata says 0): bytes at
     "dec_bank_d8_kernel": 138064,        # bank8.hip B8_LDS
     "dec_bank_h3_kernel": 139904,        # mem_attention.hip BH_LDS
     "dec_mem_attention_kernel": 158208,  # mem_lds_bytes()
-    "dec_ctx_attention_kernel": 163840,  # up to 160 KB (init_kernel_attributes)
+    "dec_ctx_attention_kernel": 52224,   # ctx_lds_bytes(6) (the attribute allows 160 KB; launches take this)
     "gemm_p16s_kernel": 98304,           # 2x4 tiles
 }
 REVIEWED_PAIRED = {
@@ -144,8 +144,8 @@ REVIEWED_PAIRED = {
                           "barrier; pool-tested"),
     "gemm_f32_kernel": (48, "A / W tile staging (ds_write2_b32 / _b64 / 2st64) read by other waves after a "
                             "barrier; encoder-side GEMMs of the beam / exact / NanoEncoder paths, pool-tested"),
-    "dec_ctx_attention_kernel": (18, "K / V staging and row reads in the beam context attention; pool-tested "
-                                     "(configs[3] at the bench's size)"),
+    "dec_ctx_attention_kernel": (36, "the (m, l, acc) merge of the beam context attention (and of its split "
+                                     "form); launched with at most 52 KB, listed in case that grows"),
     "dec_bank_d8_kernel": (3, "the (m, l) merge and the q' digit rows (cross-wave, after a barrier); "
                               "pool-tested at the bench's configuration"),
     "dec_bank_h3_kernel": (2, "the (m, l) merge, as dec_bank_d8_kernel"),

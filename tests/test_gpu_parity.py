@@ -551,6 +551,85 @@ def test_ctx_attention_vs_fp64(rpc, q24):
                 assert err < tol * max(1.0, np.abs(V[c * T: c * T + L, hs]).max()), (c, j, h, L, err)
 
 
+def test_alive_list():
+    """nd_op_alive_list: the chunks not done, ascending, then -1; more alive
+    than slots raises the guard word."""
+    from nanodecoder_amd.engine import op_alive_list
+    dev = torch.device("cuda", 0)
+    done = np.ones(200, np.int32)
+    alive = [0, 5, 63, 64, 65, 127, 128, 199]
+    done[alive] = 0
+    ovf = torch.zeros(1, dtype=torch.int32, device=dev)
+    got = op_alive_list(torch.from_numpy(done).to(dev), 13, ovf).cpu().numpy()
+    assert got.tolist() == alive + [-1] * 5 and int(ovf.item()) == 0
+    got = op_alive_list(torch.from_numpy(done).to(dev), 5, ovf).cpu().numpy()
+    assert got.tolist() == alive[:5] and int(ovf.item()) == 1
+
+
+@pytest.mark.parametrize("rpc,nsplit,q24", [(5, 16, True), (5, 16, False), (2, 7, True), (6, 32, True), (5, 1, True)])
+def test_ctx_attention_tail_list_split(rpc, nsplit, q24):
+    """The --fast beam tail's context attention: workgroups over a chunk list
+    only, each chunk's keys in nsplit workgroups combined by a second launch,
+    equal to the one-workgroup form within fp32 rounding and to fp64; rows of
+    unlisted and done chunks untouched.  Spans of 1 key (most splits empty),
+    a partial block, 512; an all-masked chunk; a late key far above the
+    first keys' maximum (the splits' maxima differ by far)."""
+    from nanodecoder_amd.engine import (op_ctx_pack_q24, op_dec_ctx_attention, op_dec_ctx_attention_list,
+                                        op_dec_ctx_attention_q24, pack_p16, unpack_p16)
+    rng = np.random.default_rng(41 + rpc + nsplit)
+    C, T, Ld, PAD = 12, 512, 3, 1.0
+    spans = np.array([T, 1, 15, 300, T, T - 5, 77, T, 2, 511, 40, T], np.int32)
+    sig = rng.standard_normal((C, T)).astype(np.float32)
+    sig[4, :] = PAD
+    sig[7, ::2] = PAD
+    kv = rng.standard_normal((C * T, Ld * 512)).astype(np.float32)
+    kv[0 * T + 480, 0:256] *= 8.0
+    kv[11 * T + 3, 0:256] *= 8.0
+    R = C * rpc
+    q = rng.standard_normal((R, 256)).astype(np.float32)
+    done = np.zeros(C, np.int32)
+    done[5] = 1
+    listed = [0, 1, 2, 3, 4, 5, 7, 8, 9, 11]   # 6 and 10 not listed
+    clist = np.array(listed + [-1, -1], np.int32)
+    dev = torch.device("cuda", 0)
+    kvd = torch.from_numpy(kv).to(dev)
+    sp = torch.from_numpy(spans).to(dev)
+    sg = torch.from_numpy(sig).to(dev)
+    qp = pack_p16(torch.from_numpy(q).to(dev))
+    dn = torch.from_numpy(done).to(dev)
+    if q24:
+        img = op_ctx_pack_q24(kvd, Ld * 512, Ld, sp, C, T)
+        whole = op_dec_ctx_attention_q24(qp, img, 0, sg, sp, PAD, rpc)
+        got = op_dec_ctx_attention_list(qp, img, Ld * 1600, 0, sg, sp, PAD, rpc, torch.from_numpy(clist).to(dev),
+                                        nsplit, q24=True, done=dn)
+    else:
+        whole = op_dec_ctx_attention(qp, kvd, Ld * 512, 0, sg, sp, PAD, rpc, packed=True)
+        got = op_dec_ctx_attention_list(qp, kvd, Ld * 512, 0, sg, sp, PAD, rpc, torch.from_numpy(clist).to(dev),
+                                        nsplit, done=dn)
+    torch.cuda.synchronize()
+    got = unpack_p16(got, R).cpu().numpy()
+    whole = unpack_p16(whole, R).cpu().numpy()
+    K = kv[:, 0:256].astype(np.float64)
+    V = kv[:, 256:512].astype(np.float64)
+    for c in range(C):
+        rows = slice(c * rpc, (c + 1) * rpc)
+        if c not in listed or done[c]:
+            assert not got[rows].any(), c
+            continue
+        assert np.abs(got[rows] - whole[rows]).max() <= 2e-6 * max(1.0, np.abs(whole[rows]).max()), c
+        L = int(spans[c])
+        for j in range(rpc):
+            r = c * rpc + j
+            for h in range(8):
+                hs = slice(h * 32, (h + 1) * 32)
+                s = K[c * T: c * T + L, hs] @ q[r, hs].astype(np.float64) / np.sqrt(32)
+                s[sig[c, :L] == PAD] = -1e18
+                p = np.exp(s - s.max())
+                want = (p / p.sum()) @ V[c * T: c * T + L, hs]
+                err = np.abs(got[r, hs] - want).max()
+                assert err < 2e-5 * max(1.0, np.abs(V[c * T: c * T + L, hs]).max()), (c, j, h, L, err)
+
+
 def test_engine_reports_bank_form():
     """A greedy call at 512-sample chunks streams the 24-bit digit bank by
     default (nd_bank_form 2; ND_BANK_D8=0: the split-fp16 bank, 1), exact

@@ -40,6 +40,17 @@ case $step in
     # keep the stats, drop the per-dispatch trace (gpurun copies back at most 64 MiB)
     find $O/$tag -name '*.csv' ! -name '*kernel_stats.csv' -delete
     head -30 $O/${tag}_kernel_stats.txt; exit 0 ;;
+  steps)
+    # kernel trace of a short bench, summarised per launch on the box (tools/trace_steps.py)
+    tag=$1; shift
+    cd /tmp && export TMPDIR=/tmp
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/$tag -o run --output-format csv -- \
+      python3 $R/bench.py $SHORT "$@" > $O/$tag.log 2>&1
+    rc=$?; echo "steps $tag rc=$rc"; [ $rc -ne 0 ] && exit $rc
+    python3 $R/tools/profsum.py $O/$tag/run_kernel_stats.csv 7 > $O/${tag}_kernel_stats.txt
+    python3 $R/tools/trace_steps.py $O/$tag/run_kernel_trace.csv > $O/${tag}_steps.txt
+    find $O/$tag -name '*.csv' ! -name '*kernel_stats.csv' -delete
+    head -20 $O/${tag}_steps.txt; exit 0 ;;
   pmc)
     tag=$1; ctrs=$2; shift 2
     cd /tmp && export TMPDIR=/tmp
