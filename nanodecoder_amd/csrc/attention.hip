@@ -1089,10 +1089,16 @@ hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* 
 #ifndef CTX_URPC
 #define CTX_URPC 2  // rows per chunk up to which a block holds 4 keys (else 2)
 #endif
+#ifndef CTX_UHI
+#define CTX_UHI 2  // keys per block above CTX_URPC rows
+#endif
+#ifndef CTX_WPE
+#define CTX_WPE 0  // timing variants: amdgpu_waves_per_eu hint (0: none)
+#endif
 #define CTX_MAXR 6
 template <int RPC>
 struct CtxTile {
-  static constexpr int U = RPC <= CTX_URPC ? 4 : 2;  // keys per block (register budget)
+  static constexpr int U = RPC <= CTX_URPC ? 4 : CTX_UHI;  // keys per block (register budget)
 };
 
 // Q24 (round 4): the chunk's K/V in 24-bit fixed point (ctx_pack_q24_kernel
@@ -1102,6 +1108,9 @@ struct CtxTile {
 // sum) and into v.  kv, ld and koff are then bytes.
 template <int RPC, bool Q24>
 __global__ void __launch_bounds__(CTX_NW * 64)
+#if CTX_WPE > 0
+__attribute__((amdgpu_waves_per_eu(CTX_WPE)))
+#endif
 dec_ctx_attention_kernel(const float* __restrict__ q, const void* __restrict__ kv_, int ld, int koff,
                          const float* __restrict__ signal, const int* __restrict__ span, float pad_val,
                          float* __restrict__ out, int T, unsigned long long* stamp, float* __restrict__ dbg,
