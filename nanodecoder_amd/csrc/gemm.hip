@@ -860,7 +860,7 @@ long long gemm_route_count(int r, bool reset) {
 template <int BM, int BN, int WM, int WN, int BK = 32>
 static hipError_t launch_cfg(GemmArgs& g, hipStream_t s) {
   if (g.K % BK != 0) return hipErrorInvalidValue;
-  count_route(BM == 256 ? ND_ROUTE_TILE256 : BM == 128 ? ND_ROUTE_TILE128 : ND_ROUTE_TILE64);
+  count_route(BM == 256 ? ND_ROUTE_TILE256 : BM == 128 ? ND_ROUTE_TILE128 : ND_ROUTE_TILE64);  // (32 counts as 64)
   static const int xcd = [] {
     const char* e = getenv("ND_GEMM_XCD");  // 0: column tile fastest (A/B timing)
     return e ? atoi(e) : 1;
@@ -1008,7 +1008,13 @@ hipError_t launch_gemm(GemmArgs& g, hipStream_t s) {
   // deeper k steps keep more of the next step's operands in flight.  Measured
   // at M = 5120, N = 256, K = 2048: BK 32 / 64 / 128 = 49.1 / 45.8 / 71.7 us
   // (128: 135 KB of LDS, one workgroup per CU); beam B = 1024 168.9 -> 164.7 ms
+  static const int t32 = [] {
+    const char* e = getenv("ND_GEMM_T32");  // 1: 32 x 64 tiles for the long-K products (A/B timing)
+    return e ? atoi(e) : 0;
+  }();
   if (g.K >= 1024 && g.K % 128 == 0) {
+    // fewer 64 x 64 tiles than two per CU: 32 x 64 tiles (two waves) double them
+    if (t32 && (long)((g.M + 63) / 64) * (g.N / 64) < 512) return launch_cfg<32, 64, 1, 2, 64>(g, s);
     if (bkl == 128) return launch_cfg<64, 64, 2, 2, 128>(g, s);
     if (bkl == 64) return launch_cfg<64, 64, 2, 2, 64>(g, s);
   }
