@@ -506,6 +506,12 @@ int nd_op_dec_ctx_attention(const float* q, const float* kv, int32_t ld, int32_t
  * nd_op_dec_ctx_attention with K/V of layer `layer` from that image. */
 int nd_op_ctx_pack_q24(const float* kv, int32_t ld, int32_t layers, void* out, const int32_t* span, int32_t B,
                        int32_t T, void* stream);
+/* The engine's form: the memory's K / V projection (split-fp16, as
+ * nd_op_gemm_split, N = layers * 512) whose epilogue writes that image
+ * (ld bytes per row >= layers * 1600) instead of fp32 K / V; every row is
+ * written. */
+int nd_op_gemm_split_q24(const float* A, const uint16_t* Wh, float wscale, const float* bias, void* img, int32_t ld,
+                         int32_t M, int32_t N, int32_t K, int32_t norm, void* stream);
 int nd_op_dec_ctx_attention_q24(const float* q, const void* kvq, int32_t layers, int32_t layer, const float* signal,
                                 const int32_t* span, float pad_val, float* out, int32_t C, int32_t rpc, int32_t T,
                                 void* stream);

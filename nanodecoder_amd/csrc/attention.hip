@@ -1260,31 +1260,7 @@ ctx_pack_q24_kernel(const float* __restrict__ kv, int ld, int Ld, uint8_t* __res
   uint8_t* dst = out + ((size_t)row * Ld + layer) * CTXQ_ROW;
   float scl[2];
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const f32x4 x = ld4(src + h * ND_D);
-    float mx = fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w)));
-    if (!(fabsf(x.x) <= 3.4028235e38f && fabsf(x.y) <= 3.4028235e38f && fabsf(x.z) <= 3.4028235e38f &&
-          fabsf(x.w) <= 3.4028235e38f))
-      mx = INFINITY;  // NaN / inf anywhere in the head (fmaxf would drop a NaN)
-    mx = fmaxf(mx, dpp_mov<ND_DPP_XOR1>(mx));
-    mx = fmaxf(mx, dpp_mov<ND_DPP_XOR2>(mx));
-    mx = fmaxf(mx, dpp_mov<ND_DPP_HALF_MIRROR>(mx));  // the head's 8 lanes
-    int e = 0;
-    frexpf(mx, &e);  // mx = f 2^e, f in [0.5, 1): mx < 2^e (mx == 0: e = 0, the integers are 0)
-    e = max(e, -100);  // a head below 2^-100 (2^(23 - e) must stay finite): its integers round to 0
-    const float up = ldexpf(1.f, 23 - e);
-    // a non-finite head keeps a NaN scale, so its scores / values stay non-finite as in fp32
-    scl[h] = mx <= 3.4028235e38f ? ldexpf(1.f, e - 23) : __builtin_nanf("");
-    int v[4];
-    const float xs[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = (int)fminf(fmaxf(rintf(xs[i] * up), -8388607.f), 8388607.f);
-    u32x3 b;
-    b.x = (uint32_t)(v[0] & 0xffffff) | ((uint32_t)v[1] << 24);
-    b.y = (((uint32_t)v[1] >> 8) & 0xffff) | ((uint32_t)v[2] << 16);
-    b.z = (((uint32_t)v[2] >> 16) & 0xff) | ((uint32_t)v[3] << 8);
-    *reinterpret_cast<u32x3*>(dst + h * CTXQ_V + 12 * lane) = b;
-  }
+  for (int h = 0; h < 2; ++h) scl[h] = q24_quant_store(ld4(src + h * ND_D), dst + h * CTXQ_V + 12 * lane);
   if ((lane & 7) == 0) *reinterpret_cast<f32x2*>(dst + CTXQ_S + 8 * (lane >> 3)) = f32x2{scl[0], scl[1]};
 }
 

@@ -18,6 +18,36 @@ struct u32x3 {  // 12 bytes, 4-byte aligned (one dwordx3 access)
   uint32_t x, y, z;
 };
 
+// The 24-bit context K/V quantiser (attention.hip ctx_pack_q24_kernel and the
+// GEMM epilogue that writes the image directly): x = this lane's 4 values of
+// a 32-wide head held by 8 consecutive lanes (lane & 7 = the dims' quad).
+// Stores the lane's 12 bytes at dst (little-endian 3-byte integers) and
+// returns the head's scale 2^(e-23) (NaN for a head holding a NaN / inf).
+__device__ __forceinline__ float q24_quant_store(f32x4 x, uint8_t* dst) {
+  float mx = fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w)));
+  if (!(fabsf(x.x) <= 3.4028235e38f && fabsf(x.y) <= 3.4028235e38f && fabsf(x.z) <= 3.4028235e38f &&
+        fabsf(x.w) <= 3.4028235e38f))
+    mx = INFINITY;  // NaN / inf anywhere in the head (fmaxf would drop a NaN)
+  mx = fmaxf(mx, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, mx), 0xB1, 0xF, 0xF, false)));
+  mx = fmaxf(mx, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, mx), 0x4E, 0xF, 0xF, false)));
+  mx = fmaxf(mx, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, mx), 0x141, 0xF, 0xF, false)));
+  int e = 0;
+  frexpf(mx, &e);  // mx = f 2^e, f in [0.5, 1): mx < 2^e (mx == 0: e = 0, the integers are 0)
+  e = max(e, -100);  // a head below 2^-100 (2^(23 - e) must stay finite): its integers round to 0
+  const float up = ldexpf(1.f, 23 - e);
+  int v[4];
+  const float xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = (int)fminf(fmaxf(rintf(xs[i] * up), -8388607.f), 8388607.f);
+  u32x3 b;
+  b.x = (uint32_t)(v[0] & 0xffffff) | ((uint32_t)v[1] << 24);
+  b.y = (((uint32_t)v[1] >> 8) & 0xffff) | ((uint32_t)v[2] << 16);
+  b.z = (((uint32_t)v[2] >> 16) & 0xff) | ((uint32_t)v[3] << 8);
+  *reinterpret_cast<u32x3*>(dst) = b;
+  // a non-finite head keeps a NaN scale, so its scores / values stay non-finite as in fp32
+  return mx <= 3.4028235e38f ? ldexpf(1.f, e - 23) : __builtin_nanf("");
+}
+
 // Four 24-bit two's-complement integers packed little-endian in the bits of
 // raw.x, raw.y, raw.z (ctx_pack_q24_kernel) -> exact fp32 values.
 __device__ __forceinline__ f32x4 q24_unpack(f32x4 raw) {

@@ -542,6 +542,7 @@ struct G {
   G& skip(const int* done, int rpc) { a.skip = done; a.skip_rpc = rpc; return *this; }
   G& small_m(bool on) { a.prefer_p16 = on ? 1 : 0; return *this; }
   G& c_rowmajor(bool on) { a.c_rm = on ? 1 : 0; return *this; }  // P16 GEMMs: C row-major
+  G& q24(uint8_t* img, int ld) { a.q24 = img; a.q24_ld = ld; return *this; }  // the 24-bit K/V image, not C
   bool packed = false;
   G& p16() { packed = true; return *this; }  // decoder-step operands in the P16 layout
   hipError_t run(hipStream_t s, int* pn_out = nullptr) {
@@ -666,11 +667,23 @@ static hipError_t enqueue_encode_transformer(nd_ctx* c, int B, int T, hipStream_
   return hipSuccess;
 }
 
-static hipError_t enqueue_ctxkv(nd_ctx* c, int B, int T, hipStream_t s) {
+// q24: the GEMM's epilogue writes the 24-bit image (ctxq) instead of fp32 K/V
+static hipError_t enqueue_ctxkv(nd_ctx* c, int B, int T, hipStream_t s, bool q24 = false) {
   const int M = B * T, D = c->D, N = (int)c->dec.size() * 2 * D;
+  uint8_t* img = q24 ? c->ctxq : nullptr;
+  const int ld = (int)c->dec.size() * CTXQ_ROW;
   if (c->cfg.encoder_type == ND_ENC_TRANSFORMER)
-    return G(c->x, D, c->nctxkv_w, N, D, c->nctxkv_b, c->ctxkv, N, M).h3(c).ln(c->x_part, c->x_pn).run(s);
-  return G(c->x, D, c->ctxkv_w, N, D, c->ctxkv_b, c->ctxkv, N, M).h3(c).run(s);
+    return G(c->x, D, c->nctxkv_w, N, D, c->nctxkv_b, c->ctxkv, N, M).h3(c).ln(c->x_part, c->x_pn).q24(img, ld).run(s);
+  return G(c->x, D, c->ctxkv_w, N, D, c->ctxkv_b, c->ctxkv, N, M).h3(c).q24(img, ld).run(s);
+}
+
+// the 24-bit image straight from the K/V GEMM's epilogue (ND_CTX_Q24_FUSE=0: fp32 K/V, then the pack kernel)
+static bool use_ctx_q24_fuse() {
+  static const bool on = [] {
+    const char* e = getenv("ND_CTX_Q24_FUSE");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
 }
 
 static hipError_t enqueue_encode(nd_ctx* c, int B, int T, hipStream_t s);
@@ -907,8 +920,10 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
 static hipError_t enqueue_memory(nd_ctx* c, int B, int T, int rpc, hipStream_t s) {
   set_memory_view(c, T, rpc);
   if (!use_memory_bank(c, rpc)) {
-    LCHK(enqueue_ctxkv(c, B, T, s));
-    if (!c->ctx_q24) return hipSuccess;
+    // the fused form needs the split-fp16 weights (h3): exact fp32 never takes the image
+    const bool fuse = c->ctx_q24 && use_ctx_q24_fuse() && !nd::gemm_f32_forced();
+    LCHK(enqueue_ctxkv(c, B, T, s, fuse));
+    if (!c->ctx_q24 || fuse) return hipSuccess;
     const int Ld = (int)c->dec.size();
     return nd::launch_ctx_pack_q24(c->ctxkv, Ld * 2 * c->D, Ld, c->ctxq, c->span, B, T, s);
   }
@@ -1727,7 +1742,7 @@ static const struct {
                  {"ND_ENC_QKV", 1},    {"ND_ENC_ATTN0", 1},   {"ND_SELF_NW8", 1},     {"ND_BANK_D8", 1},
                  {"ND_BEAM_BANK", 0},  {"ND_BB_PIPE", 1},     {"ND_P16_K2048", 0},
                  {"ND_CTX_Q24", 1},    {"ND_BEAM_COMPACT", 1}, {"ND_CTX_SPLIT", 16},
-                 {"ND_GEMM_T32", 0}};
+                 {"ND_GEMM_T32", 0},   {"ND_CTX_Q24_FUSE", 1}};
 
 int nd_switches(char* buf, int32_t len) {
   std::string out;
@@ -1868,6 +1883,19 @@ int nd_op_gemm_split(const float* A, const uint16_t* Wh, float wscale, const flo
   if (R) g.res(R, N);
   hipError_t e = g.run((hipStream_t)stream);
   if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("gemm_split: ") + hipGetErrorString(e));
+  return ND_OK;
+}
+
+int nd_op_gemm_split_q24(const float* A, const uint16_t* Wh, float wscale, const float* bias, void* img, int32_t ld,
+                         int32_t M, int32_t N, int32_t K, int32_t norm, void* stream) {
+  if (!Wh || !img) return fail(ND_ERR_ARG, "gemm_split_q24: null Wh / image");
+  G g(A, K, nullptr, N, K, bias, nullptr, N, M);
+  g.a.Wh = Wh;
+  g.a.wscale = wscale;
+  g.a.norm = norm != 0;
+  g.q24(static_cast<uint8_t*>(img), ld);
+  hipError_t e = g.run((hipStream_t)stream);
+  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("gemm_split_q24: ") + hipGetErrorString(e));
   return ND_OK;
 }
 

@@ -378,7 +378,18 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
         const size_t ro = g.p16io ? pk(row, n0 + c4, g.N) : (size_t)row * g.ldr + n0 + c4;
         const size_t co = g.p16io ? pk(row, n0 + c4, g.N) : (size_t)row * g.ldc + n0 + c4;
         if constexpr (RESID) v += ld4(g.R + ro);
-        st4(g.C + co, v);
+        if (!g.q24) st4(g.C + co, v);
+      }
+      if constexpr (BN % ND_D == 0 && !RESID && !RELU) {
+        // the 24-bit context K/V image (q24_quant_store: the head's 8 lanes are
+        // this row's threads c4 / 4 .. + 7, every lane of them active here)
+        // (BN >= 256: one wave = 64 threads of one row, so `row < M` is wave-uniform)
+        if (g.q24 && row < M) {
+          const int col = n0 + c4, layer = col / (2 * ND_D), half = (col / ND_D) & 1, d = col % ND_D;
+          uint8_t* dst = g.q24 + (size_t)row * g.q24_ld + (size_t)layer * CTXQ_ROW;
+          const float sc = q24_quant_store(v, dst + half * CTXQ_V + 3 * d);
+          if ((d & (ND_DH - 1)) == 0) reinterpret_cast<float*>(dst + CTXQ_S)[2 * (d / ND_DH) + half] = sc;
+        }
       }
       if (g.part_out) {
         const float mu = group_sum<TPR>(v.x + v.y + v.z + v.w) * (1.0f / BN);
@@ -988,6 +999,12 @@ hipError_t launch_gemm(GemmArgs& g, hipStream_t s) {
   if (!g.W && !g.Wh) return hipErrorInvalidValue;
   hipError_t e = check_args(g);
   if (e != hipSuccess) return e;
+  // the 24-bit context K/V image: the 256 x 256 tiles (a wave holds one row's 256 columns = k or v of a layer)
+  if (g.q24) {
+    if (g.N % (2 * ND_D) || g.p16io || g.R || g.relu || g.q24_ld < (g.N / (2 * ND_D)) * CTXQ_ROW)
+      return hipErrorInvalidValue;
+    return launch_cfg<256, 256, 2, 4>(g, s);
+  }
   static const int big = [] {
     const char* e = getenv("ND_GEMM_TILE");  // 128: force the 128x128 tiles (A/B timing)
     return !(e && atoi(e) == 128);

@@ -59,6 +59,11 @@ struct GemmArgs {
   // kernel's q': its one-row-per-chunk loads then read whole 1 KB runs, not
   // 16 B of every 64 B line; PMC: 4x over-fetch of q' in the P16 layout)
   int c_rm = 0;
+  // row-major LDS-tiled kernel, N = layers * 512 (the beam's context K / V):
+  // write the 24-bit image (CTXQ_ROW bytes per layer, q24_ld bytes per row)
+  // instead of C; nullable
+  uint8_t* q24 = nullptr;
+  int q24_ld = 0;
 };
 #define ND_PART_LD 16  // partial-stat slots per row (max column tiles of a 256-wide row)
 // row-major operands (encoder, large M): LDS-tiled MFMA kernel

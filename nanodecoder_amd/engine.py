@@ -442,6 +442,20 @@ def op_gemm(A: torch.Tensor, W: torch.Tensor, bias=None, R=None, ln_g=None, ln_b
     return C
 
 
+def op_gemm_split_q24(A: torch.Tensor, W: torch.Tensor, bias=None, norm=False):
+    """The beam's K / V projection writing the 24-bit image (nd_op_gemm_split_q24): A [M, K], W [layers*512, K]
+    (split-fp16 as op_gemm(split=True)) -> uint8 [M, layers, 1600]."""
+    M, K = A.shape
+    N = W.shape[0]
+    layers = N // 512
+    img = torch.zeros(M, layers, 1600, dtype=torch.uint8, device=A.device)
+    Wh, sc = op_split_weight(W)
+    s = ctypes.c_void_p(torch.cuda.current_stream(A.device).cuda_stream)
+    _lib.check(_lib.lib().nd_op_gemm_split_q24(_ptr(A), _ptr(Wh), sc, _ptr(bias), _ptr(img), layers * 1600, M, N, K,
+                                               int(norm), s), "nd_op_gemm_split_q24")
+    return img
+
+
 def op_enc_attention(qkv: torch.Tensor, signal: torch.Tensor, span: torch.Tensor):
     B, T = signal.shape
     out = torch.zeros(B * T, qkv.shape[1] // 3, dtype=torch.float32, device=qkv.device)

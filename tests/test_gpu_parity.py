@@ -497,6 +497,28 @@ def test_ctx_pack_q24_bitexact():
     assert np.isnan(sc[1, 1]) and np.isfinite(np.delete(sc.reshape(-1), 3)).all()
 
 
+@pytest.mark.parametrize("norm", [False, True])
+def test_gemm_q24_epilogue_equals_pack(norm):
+    """The engine's K / V projection writing the 24-bit image from its epilogue
+    (nd_op_gemm_split_q24) equals the fp32 GEMM's output packed by
+    nd_op_ctx_pack_q24, byte for byte (same 256 x 256 tiles, same quantiser);
+    M not a multiple of the tile (rows past M untouched)."""
+    from nanodecoder_amd.engine import op_ctx_pack_q24, op_gemm, op_gemm_split_q24
+    rng = np.random.default_rng(7 + int(norm))
+    M, K, Ld = 64 * 512 + 100, 256, 3
+    dev = torch.device("cuda", 0)
+    A = torch.from_numpy(rng.standard_normal((M, K)).astype(np.float32)).to(dev)
+    W = torch.from_numpy((rng.standard_normal((Ld * 512, K)) / 16).astype(np.float32)).to(dev)
+    b = torch.from_numpy((rng.standard_normal(Ld * 512) * 0.1).astype(np.float32)).to(dev)
+    C = op_gemm(A, W, b, norm=norm, split=True)
+    img = op_gemm_split_q24(A, W, b, norm=norm)
+    span = torch.full((1,), M, dtype=torch.int32, device=dev)
+    want = op_ctx_pack_q24(C, Ld * 512, Ld, span, 1, M)
+    torch.cuda.synchronize()
+    bad = (img != want).nonzero()
+    assert bad.numel() == 0, bad[:8].tolist()
+
+
 @pytest.mark.parametrize("rpc", [1, 2, 5, 6])
 @pytest.mark.parametrize("q24", [False, True])
 def test_ctx_attention_vs_fp64(rpc, q24):
