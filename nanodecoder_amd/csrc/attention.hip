@@ -771,7 +771,15 @@ hipError_t launch_dec_embed_table(const float* emb, const float* pe, int V, int 
 // through LDS at the end.  softmax is exp(s - max) / sum as torch computes
 // it; masked keys carry the reference's finite -1e18 fill, keys that do not
 // exist carry -inf (weight 0).
-template <int RPC, int U>
+// L2: scores in log2 units (q pre-scaled by log2(e)), so each weight is one
+// v_exp_f32 (exp2) without the multiply __expf adds
+template <bool L2>
+__device__ __forceinline__ float sm_exp(float x) {
+  if constexpr (L2) return __builtin_amdgcn_exp2f(x);
+  return __expf(x);
+}
+
+template <int RPC, int U, bool L2 = false>
 __device__ __forceinline__ void online_update(const float (&s)[RPC][U], const f32x4 (&v)[U], float (&m)[RPC],
                                               float (&l)[RPC], f32x4 (&acc)[RPC]) {
 #pragma unroll
@@ -779,12 +787,12 @@ __device__ __forceinline__ void online_update(const float (&s)[RPC][U], const f3
     float mx = m[j];
 #pragma unroll
     for (int u = 0; u < U; ++u) mx = fmaxf(mx, s[j][u]);  // finite: the block's first key exists
-    const float sc = __expf(m[j] - mx);
+    const float sc = sm_exp<L2>(m[j] - mx);
     acc[j] = acc[j] * sc;
     l[j] *= sc;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const float p = __expf(s[j][u] - mx);
+      const float p = sm_exp<L2>(s[j][u] - mx);
       l[j] += p;
       acc[j] += p * v[u];
     }
@@ -794,7 +802,7 @@ __device__ __forceinline__ void online_update(const float (&s)[RPC][U], const f3
 
 // LDS image: accs [NW][RPC][256], ms / ls [NW][RPC][8].  Output rows
 // row0 .. row0+RPC-1 of the P16-packed [*, 256] matrix out.
-template <int RPC, int NW>
+template <int RPC, int NW, bool L2 = false>
 __device__ __forceinline__ void merge_waves(float* accs, float* ms, float* ls, const float (&m)[RPC],
                                             const float (&l)[RPC], const f32x4 (&acc)[RPC], int wave, int lane,
                                             int tid, float* __restrict__ out, int row0) {
@@ -816,7 +824,7 @@ __device__ __forceinline__ void merge_waves(float* accs, float* ms, float* ls, c
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
       const float mw = ms[(w * RPC + j) * ND_H + h];
-      const float f = mw == -INFINITY ? 0.f : __expf(mw - M);  // waves that owned no key
+      const float f = mw == -INFINITY ? 0.f : sm_exp<L2>(mw - M);  // waves that owned no key
       num += f * accs[((size_t)w * RPC + j) * ND_D + d];
       den += f * ls[(w * RPC + j) * ND_H + h];
     }
@@ -828,7 +836,7 @@ __device__ __forceinline__ void merge_waves(float* accs, float* ms, float* ls, c
 // state {num[256], max[8], den[8]} at part + j * CTX_PART (the split
 // context attention; ctx_split_merge_kernel combines the splits).
 #define CTX_PART (ND_D + 2 * ND_H)
-template <int RPC, int NW>
+template <int RPC, int NW, bool L2 = false>
 __device__ __forceinline__ void merge_waves_part(float* accs, float* ms, float* ls, const float (&m)[RPC],
                                                  const float (&l)[RPC], const f32x4 (&acc)[RPC], int wave, int lane,
                                                  int tid, float* __restrict__ part) {
@@ -850,7 +858,7 @@ __device__ __forceinline__ void merge_waves_part(float* accs, float* ms, float* 
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
       const float mw = ms[(w * RPC + j) * ND_H + h];
-      const float f = mw == -INFINITY ? 0.f : __expf(mw - M);
+      const float f = mw == -INFINITY ? 0.f : sm_exp<L2>(mw - M);
       num += f * accs[((size_t)w * RPC + j) * ND_D + d];
       den += f * ls[(w * RPC + j) * ND_H + h];
     }
@@ -1095,6 +1103,11 @@ hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* 
 #ifndef CTX_WPE
 #define CTX_WPE 0  // timing variants: amdgpu_waves_per_eu hint (0: none)
 #endif
+#ifndef CTX_EXP2
+#define CTX_EXP2 1  // scores in log2 units (q pre-scaled by log2(e) / sqrt(32)); 0: natural units (A/B)
+#endif
+#define ND_LOG2E 1.4426950408889634f
+#define ND_LN2 0.6931471805599453f
 #define CTX_MAXR 6
 template <int RPC>
 struct CtxTile {
@@ -1136,7 +1149,9 @@ dec_ctx_attention_kernel(const float* __restrict__ q, const void* __restrict__ k
   float m[RPC], l[RPC];
 #pragma unroll
   for (int j = 0; j < RPC; ++j) {
-    qv[j] = ld4(q + pk(c * RPC + j, lane * 4, ND_D)) / ND_SQRT_DH;  // q, out P16-packed
+    // q, out P16-packed; log2 units: q / sqrt(32) * log2(e)
+    qv[j] = CTX_EXP2 ? ld4(q + pk(c * RPC + j, lane * 4, ND_D)) * (ND_LOG2E / ND_SQRT_DH)
+                     : ld4(q + pk(c * RPC + j, lane * 4, ND_D)) / ND_SQRT_DH;
     acc[j] = {0.f, 0.f, 0.f, 0.f};
     m[j] = -INFINITY;
     l[j] = 0.f;
@@ -1198,9 +1213,11 @@ dec_ctx_attention_kernel(const float* __restrict__ q, const void* __restrict__ k
       // -attn_debug / coverage: head 0 (lanes 0..7 after sum8) of every row of the chunk
       if (dbg && lane == 0 && valid)
 #pragma unroll
-        for (int j = 0; j < RPC; ++j) dbg[((size_t)c * RPC + j) * dbg_stride + blk * U + u] = sc[j][u];
+        for (int j = 0; j < RPC; ++j)  // natural units (the -1e18 fill as it stands)
+          dbg[((size_t)c * RPC + j) * dbg_stride + blk * U + u] =
+              (CTX_EXP2 && sc[j][u] != ND_MASK_FILL) ? sc[j][u] * ND_LN2 : sc[j][u];
     }
-    online_update<RPC, U>(sc, vf, m, l, acc);
+    online_update<RPC, U, CTX_EXP2>(sc, vf, m, l, acc);
     if (more) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -1211,9 +1228,10 @@ dec_ctx_attention_kernel(const float* __restrict__ q, const void* __restrict__ k
     }
   }
   if (part)
-    merge_waves_part<RPC, CTX_NW>(accs, ms, ls, m, l, acc, wave, lane, tid, part + (size_t)blockIdx.x * RPC * CTX_PART);
+    merge_waves_part<RPC, CTX_NW, CTX_EXP2>(accs, ms, ls, m, l, acc, wave, lane, tid,
+                                            part + (size_t)blockIdx.x * RPC * CTX_PART);
   else
-    merge_waves<RPC, CTX_NW>(accs, ms, ls, m, l, acc, wave, lane, tid, out, c * RPC);
+    merge_waves<RPC, CTX_NW, CTX_EXP2>(accs, ms, ls, m, l, acc, wave, lane, tid, out, c * RPC);
   stamp_end(stamp);
 }
 
@@ -1232,7 +1250,7 @@ ctx_split_merge_kernel(const float* __restrict__ part, const int* __restrict__ c
   float num = 0.f, den = 0.f;
   for (int s = 0; s < nsplit; ++s) {
     const float ms = p[s * ps + ND_D + h];
-    const float f = ms == -INFINITY ? 0.f : __expf(ms - M);  // a split with no key
+    const float f = ms == -INFINITY ? 0.f : sm_exp<CTX_EXP2>(ms - M);  // a split with no key
     num += f * p[s * ps + d];
     den += f * p[s * ps + ND_D + ND_H + h];
   }
