@@ -1104,7 +1104,7 @@ hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* 
 #define CTX_WPE 0  // timing variants: amdgpu_waves_per_eu hint (0: none)
 #endif
 #ifndef CTX_EXP2
-#define CTX_EXP2 1  // scores in log2 units (q pre-scaled by log2(e) / sqrt(32)); 0: natural units (A/B)
+#define CTX_EXP2 0  // 1: scores in log2 units (q pre-scaled by log2(e) / sqrt(32)); measured slower in the engine (A/B)
 #endif
 #define ND_LOG2E 1.4426950408889634f
 #define ND_LN2 0.6931471805599453f
