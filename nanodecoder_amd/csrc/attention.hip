@@ -800,6 +800,46 @@ __device__ __forceinline__ void online_update(const float (&s)[RPC][U], const f3
   }
 }
 
+// The same update with a lazy maximum (flash-attention style): a row's running
+// maximum moves only when a score exceeds it by more than tau = 8 (weights up
+// to e^8 relative to the kept maximum; (m, l, acc) stay mutually consistent,
+// so the merge and the final division are exact).  The rescale (one exp and
+// 5 multiplies per row) then runs only on blocks where some row of some lane
+// needs it, a wave-uniform branch: after a chunk's first keys, almost never.
+template <int RPC, int U>
+__device__ __forceinline__ void online_update_lazy(const float (&s)[RPC][U], const f32x4 (&v)[U], float (&m)[RPC],
+                                                   float (&l)[RPC], f32x4 (&acc)[RPC]) {
+  constexpr float TAU = 8.0f;
+  float mxs[RPC];
+  bool need = false;
+#pragma unroll
+  for (int j = 0; j < RPC; ++j) {
+    float mx = s[j][0];
+#pragma unroll
+    for (int u = 1; u < U; ++u) mx = fmaxf(mx, s[j][u]);
+    mxs[j] = mx;
+    need |= mx > m[j] + TAU;  // m = -inf: any existing key
+  }
+  if (__builtin_amdgcn_ballot_w64(need)) {
+#pragma unroll
+    for (int j = 0; j < RPC; ++j) {
+      const float mx = fmaxf(m[j], mxs[j]);
+      const float sc = __expf(m[j] - mx);  // m = -inf: 0 (acc, l are 0)
+      acc[j] = acc[j] * sc;
+      l[j] *= sc;
+      m[j] = mx;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < RPC; ++j)
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float p = __expf(s[j][u] - m[j]);
+      l[j] += p;
+      acc[j] += p * v[u];
+    }
+}
+
 // LDS image: accs [NW][RPC][256], ms / ls [NW][RPC][8].  Output rows
 // row0 .. row0+RPC-1 of the P16-packed [*, 256] matrix out.
 template <int RPC, int NW, bool L2 = false>
@@ -1103,6 +1143,9 @@ hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* 
 #ifndef CTX_WPE
 #define CTX_WPE 0  // timing variants: amdgpu_waves_per_eu hint (0: none)
 #endif
+#ifndef CTX_LAZY
+#define CTX_LAZY 1  // the lazy running maximum (online_update_lazy); 0: rescale every block (A/B)
+#endif
 #ifndef CTX_EXP2
 #define CTX_EXP2 0  // 1: scores in log2 units (q pre-scaled by log2(e) / sqrt(32)); measured slower in the engine (A/B)
 #endif
@@ -1217,7 +1260,10 @@ dec_ctx_attention_kernel(const float* __restrict__ q, const void* __restrict__ k
           dbg[((size_t)c * RPC + j) * dbg_stride + blk * U + u] =
               (CTX_EXP2 && sc[j][u] != ND_MASK_FILL) ? sc[j][u] * ND_LN2 : sc[j][u];
     }
-    online_update<RPC, U, CTX_EXP2>(sc, vf, m, l, acc);
+    if constexpr (CTX_LAZY && !CTX_EXP2)
+      online_update_lazy<RPC, U>(sc, vf, m, l, acc);
+    else
+      online_update<RPC, U, CTX_EXP2>(sc, vf, m, l, acc);
     if (more) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
