@@ -1107,6 +1107,19 @@ hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* 
     const char* e = getenv("ND_SELF_NW8");
     return !(e && atoi(e) == 0);
   }();
+  // 4 waves of up to 16 keys per row up to 64 keys: beam rows (ancestry) by
+  // default, configs[3] pooled 75.62 -> 74.59 ms, one call 94.28 -> 93.60 ms
+  // (two reps, one box).  ND_SELF_NW4: 0 never, 1 beam rows, 2 every row
+  static const int nw4 = [] {
+    const char* e = getenv("ND_SELF_NW4");
+    return e ? atoi(e) : 1;
+  }();
+  if ((nw4 == 2 || (nw4 == 1 && anc)) && n <= 64) {
+    if (n <= 16) ND_SELF(4, 4);
+    else if (n <= 32) ND_SELF(4, 8);
+    else ND_SELF(4, 16);
+    return hipGetLastError();
+  }
   if (n <= 32) ND_SELF(8, 4);
   else if (w8 && n <= 64) ND_SELF(8, 8);
   else if (w8) ND_SELF(8, 16);  // two passes beyond 128 keys
