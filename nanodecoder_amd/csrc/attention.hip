@@ -1107,12 +1107,13 @@ hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* 
     const char* e = getenv("ND_SELF_NW8");
     return !(e && atoi(e) == 0);
   }();
-  // 4 waves of up to 16 keys per row up to 64 keys: beam rows (ancestry) by
-  // default, configs[3] pooled 75.62 -> 74.59 ms, one call 94.28 -> 93.60 ms
-  // (two reps, one box).  ND_SELF_NW4: 0 never, 1 beam rows, 2 every row
+  // 4 waves of up to 16 keys per row up to 64 keys: beam rows (ancestry),
+  // configs[3] pooled 75.62 -> 74.59 ms, one call 94.28 -> 93.60 ms; greedy
+  // rows, pooled 16.75 / 16.84 -> 16.72 / 16.70 ms (two reps each, one box).
+  // ND_SELF_NW4: 0 never, 1 beam rows only, 2 every row (default)
   static const int nw4 = [] {
     const char* e = getenv("ND_SELF_NW4");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 2;
   }();
   if ((nw4 == 2 || (nw4 == 1 && anc)) && n <= 64) {
     if (n <= 16) ND_SELF(4, 4);

@@ -1743,7 +1743,7 @@ static const struct {
                  {"ND_BEAM_BANK", 0},  {"ND_BB_PIPE", 1},     {"ND_P16_K2048", 0},
                  {"ND_CTX_Q24", 1},    {"ND_BEAM_COMPACT", 1}, {"ND_CTX_SPLIT", 16},
                  {"ND_GEMM_T32", 0},   {"ND_CTX_Q24_FUSE", 1},
-                 {"ND_SELF_NW4", 1}};
+                 {"ND_SELF_NW4", 2}};
 
 int nd_switches(char* buf, int32_t len) {
   std::string out;
