@@ -1157,6 +1157,9 @@ hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* 
 #ifndef CTX_WPE
 #define CTX_WPE 0  // timing variants: amdgpu_waves_per_eu hint (0: none)
 #endif
+#ifndef CTX_PLAIN
+#define CTX_PLAIN 1  // select-free scores for blocks of existing unmasked keys; 0: selects always (A/B)
+#endif
 #ifndef CTX_LAZY
 #define CTX_LAZY 1  // the lazy running maximum (online_update_lazy); 0: rescale every block (A/B)
 #endif
@@ -1248,6 +1251,12 @@ dec_ctx_attention_kernel(const float* __restrict__ q, const void* __restrict__ k
     if (more) load(blk + CTX_NW, kn, vn, sn);
     float sc[RPC][U];
     f32x4 vf[U];
+    // a block of existing, unmasked keys (wave-uniform: the signal value is
+    // the same in every lane) takes its scores as they are, no selects
+    bool plain = CTX_PLAIN && (blk + 1) * U <= L;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      plain &= __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(sg[u]))) != pad_val;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const bool valid = blk * U + u < L;
@@ -1265,8 +1274,11 @@ dec_ctx_attention_kernel(const float* __restrict__ q, const void* __restrict__ k
       for (int j = 0; j < RPC; ++j) {
         float d = sum8(qv[j].x * kf.x + qv[j].y * kf.y + qv[j].z * kf.z + qv[j].w * kf.w);
         if constexpr (Q24) d *= ks;
-        sc[j][u] = valid ? (masked ? ND_MASK_FILL : d) : -INFINITY;
+        sc[j][u] = d;
       }
+      if (!plain)
+#pragma unroll
+        for (int j = 0; j < RPC; ++j) sc[j][u] = valid ? (masked ? ND_MASK_FILL : sc[j][u]) : -INFINITY;
       // -attn_debug / coverage: head 0 (lanes 0..7 after sum8) of every row of the chunk
       if (dbg && lane == 0 && valid)
 #pragma unroll
