@@ -1144,9 +1144,11 @@ hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* 
 // 8 waves per chunk: the 16-wave form filled a CU's register file (16 x 114
 // VGPRs at rpc 5) and shut the other pool lanes out; beam configs[3] pooled
 // 83.6 -> 82.1 ms per call, one call 102.2 -> 101.5 ms (two reps, same box,
-// tools/_g44.sh); round 2 measured the two forms equal alone
+// tools/_g44.sh); round 2 measured the two forms equal alone.  Round 4: 4
+// waves per chunk (more chunks' workgroups per CU beside the other lanes):
+// configs[3] pooled 77.3 -> 75.9 ms on one box (profiles/r04_beam_ab.txt)
 #ifndef CTX_NW
-#define CTX_NW 8
+#define CTX_NW 4
 #endif
 #ifndef CTX_URPC
 #define CTX_URPC 2  // rows per chunk up to which a block holds 4 keys (else 2)
@@ -1158,7 +1160,7 @@ hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* 
 #define CTX_WPE 0  // timing variants: amdgpu_waves_per_eu hint (0: none)
 #endif
 #ifndef CTX_PLAIN
-#define CTX_PLAIN 1  // select-free scores for blocks of existing unmasked keys; 0: selects always (A/B)
+#define CTX_PLAIN 0  // 1: select-free scores for blocks of existing unmasked keys (measured slower: 78.9 vs 77.3 ms)
 #endif
 #ifndef CTX_LAZY
 #define CTX_LAZY 1  // the lazy running maximum (online_update_lazy); 0: rescale every block (A/B)
