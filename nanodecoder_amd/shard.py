@@ -171,7 +171,8 @@ class ReadShard:
         t0 = time.perf_counter()
         th.start()
         try:
-            if gpu:
+            if gpu and getattr(self.tr, "beam_size", 1) == 1:
+                # greedy / sampling: tokens come back as one array per read
                 it = self.tr.stream_raw_reads(reads(), self.batch_size, self.normalization, self.L, self.stride,
                                               arrays=True)
                 for k, tok, _ in it:
@@ -181,6 +182,18 @@ class ReadShard:
                     bases += count_bases(tok, eos, specials)
                     if keep_predictions:
                         preds[int(read_ids[k])] = [[" ".join(self.tr._tokens_to_sent(t))] for t in tok.tolist()]
+            elif gpu:
+                # beam: per-chunk (scores, n_best token lists), the first hypothesis counted
+                it = self.tr.stream_raw_reads(reads(), self.batch_size, self.normalization, self.L, self.stride)
+                for k, res in it:
+                    ns, nc = n_samples.pop(k)
+                    samples += ns
+                    chunks += nc
+                    for r in res:
+                        bases += count_bases(np.asarray([r[1][0]], np.int64), eos, specials)
+                    if keep_predictions:
+                        preds[int(read_ids[k])] = [[" ".join(self.tr._tokens_to_sent(t)) for t in r[1]]
+                                                   for r in res]
             else:
                 for k, res in self.tr.stream_reads(reads(), self.batch_size):
                     ns, nc = n_samples.pop(k)
@@ -203,16 +216,48 @@ class ReadShard:
                     reads=len(read_ids), frontend=self.frontend), preds
 
 
+class ShardFailure(RuntimeError):
+    """Reads no rank could translate (their rank failed, and so did the retry)."""
+
+    def __init__(self, read_ids, causes):
+        self.read_ids = sorted(int(i) for i in read_ids)
+        head = ", ".join(str(i) for i in self.read_ids[:20]) + (" ..." if len(self.read_ids) > 20 else "")
+        super().__init__(f"{len(self.read_ids)} reads not translated (read ids {head}): {causes}")
+
+
+def _empty_stats(frontend):
+    return dict(samples=0, bases=0, chunks=0, seconds=0.0, reads=0, frontend=frontend)
+
+
+def _merge(a, b):
+    for k in ("samples", "bases", "chunks", "reads"):
+        a[k] += b[k]
+    return a
+
+
 def run_distributed(n_reads: int, translator_factory: Callable, weights_factory: Callable, device,
                     batch_size: int = 100, seed: int = 0, keep_predictions: bool = False, pregenerate: bool = False,
-                    warmup_reads: int = 0, frontend: str = "auto"):
+                    warmup_reads: int = 0, frontend: str = "auto", retry: bool = True):
     """Rank-local part of the sharded job; returns (global stats, local preds).
     The timed region (max over ranks) covers the front end, packing, the
-    engine and the token copies of the rank's reads."""
+    engine and the token copies of the rank's reads.
+
+    Rank failure (reads are independent, so a failed shard is
+    rerun): a rank whose translator raises keeps its process and its place in
+    the collectives.  After the first pass one all_reduce of per-rank failure
+    flags tells every rank which shards failed; their reads are re-assigned
+    by LPT to the ranks that did not fail and translated there (``retried``
+    in the stats).  Reads that still fail, or a job where every rank failed,
+    raise ``ShardFailure`` naming them on every rank (the launcher exits
+    non-zero).  A rank PROCESS that dies is the launcher's to report:
+    torch.distributed.run stops the other workers and exits non-zero; a
+    rerun of the CLI skips the reads already written (translate.py's
+    resume)."""
     multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
     rank, world = (dist.get_rank(), dist.get_world_size()) if multi else (0, 1)
     lengths = read_lengths(n_reads, seed)
-    mine = lpt_assign(lengths.tolist(), world)[rank]
+    parts = lpt_assign(lengths.tolist(), world)
+    mine = parts[rank]
     W = weights_factory() if rank == 0 else None
     if multi:
         W = broadcast_weights(W, device)
@@ -228,9 +273,52 @@ def run_distributed(n_reads: int, translator_factory: Callable, weights_factory:
     if on_gpu:
         torch.cuda.synchronize(device)
     shard = ReadShard(tr, batch_size=batch_size, frontend=frontend)
-    stats, preds = shard.run(mine, lengths, keep_predictions, raws=raws)
-    if on_gpu:
-        torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    failures = {}
+
+    def attempt(ids, raw_list):
+        try:
+            st, pr = shard.run(ids, lengths, keep_predictions, raws=raw_list)
+            if on_gpu:
+                torch.cuda.synchronize(device)
+            return st, pr, None
+        except Exception as e:  # this rank's shard failed; the others take its reads
+            return _empty_stats(shard.frontend), {}, f"rank {rank}: {type(e).__name__}: {e}"
+
+    stats, preds, err = attempt(mine, raws)
+    retried = 0
+    if err is not None:
+        failures[rank] = err
+    if multi:
+        flags = torch.zeros(world, dtype=torch.float64, device=device)
+        flags[rank] = 1.0 if err is not None else 0.0
+        dist.all_reduce(flags)
+        failed = [r for r in range(world) if flags[r] > 0]
+        if failed:
+            ok = [r for r in range(world) if r not in failed]
+            todo = sorted(i for r in failed for i in parts[r])
+            if not ok or not retry:
+                raise ShardFailure(todo, f"failed ranks {failed}")
+            share = lpt_assign([int(lengths[i]) for i in todo], len(ok))
+            extra = [todo[j] for j in share[ok.index(rank)]] if rank in ok else []
+            retried = len(todo)
+            err2 = None
+            if extra:
+                xraws = [synth_raw(int(i), int(lengths[i])) for i in extra] if pregenerate else None
+                st2, pr2, err2 = attempt(extra, xraws)
+                stats = _merge(stats, st2)
+                preds.update(pr2)
+            flags.zero_()
+            flags[rank] = 1.0 if err2 is not None else 0.0
+            dist.all_reduce(flags)
+            failed2 = [r for r in range(world) if flags[r] > 0]
+            if failed2:
+                lost = sorted(i for r in failed2 for i in
+                              ([todo[j] for j in share[ok.index(r)]] if r in ok else []))
+                raise ShardFailure(lost, f"failed ranks {failed} then {failed2} on retry")
+    elif err is not None:
+        raise ShardFailure(mine, err)
+    stats["seconds"] = time.perf_counter() - t0
     if multi:
         dist.barrier()
     red = torch.tensor([stats["samples"], stats["bases"], stats["chunks"]], dtype=torch.float64, device=device)
@@ -244,7 +332,7 @@ def run_distributed(n_reads: int, translator_factory: Callable, weights_factory:
     loads = per_rank.cpu().numpy()
     g = dict(samples=int(red[0]), bases=int(red[1]), chunks=int(red[2]), seconds=float(secs[0]), world=world,
              reads=int(n_reads), samples_per_rank=[int(x) for x in loads], frontend=shard.frontend,
-             load_imbalance=float(loads.max() / max(loads.mean(), 1.0)))
+             load_imbalance=float(loads.max() / max(loads.mean(), 1.0)), retried=retried)
     return g, preds
 
 

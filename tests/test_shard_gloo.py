@@ -1,6 +1,6 @@
-"""Multi-process read sharding on CPU (gloo, world_size 2): partition,
-weight broadcast and stats reduction, with the engine replaced by a
-deterministic stand-in (no GPU here)."""
+"""Multi-process read sharding on CPU (gloo, world_size 2, 4 and 8):
+partition, weight broadcast, stats reduction and the rank-failure retry, with
+the engine replaced by a deterministic stand-in (no GPU here)."""
 import os
 import socket
 import types
@@ -34,8 +34,11 @@ def test_pack_unpack_roundtrip():
 class FakeTranslator:
     """Per chunk: 'A' * (len % 7) then EOS — depends only on the chunk."""
 
-    def __init__(self, W):
+    beam_size = 1
+
+    def __init__(self, W, fail_sizes=()):
         self.W = W
+        self.fail_sizes = set(fail_sizes)
         from nanodecoder_amd import synth
         self.cfg = synth.ModelConfig()
 
@@ -57,6 +60,8 @@ class FakeTranslator:
         from nanodecoder_amd import frontend
         assert arrays and normalization == "median"
         for ri, raw in enumerate(raws):
+            if raw.size in self.fail_sizes:
+                raise RuntimeError(f"engine fault on a read of {raw.size} samples")
             w = frontend.windows(int(raw.size), L, stride)
             tok = np.full((len(w), 10), 3, np.int32)
             for j, (_, ln) in enumerate(w):
@@ -79,6 +84,35 @@ def test_read_shard_frontends_agree():
     assert pa == pb
 
 
+class FakeBeamTranslator(FakeTranslator):
+    """A beam translator's device front end returns per-chunk (scores, n_best
+    token lists), never token arrays (Translator.stream_raw_reads refuses
+    arrays=True for beam_size > 1)."""
+    beam_size = 5
+
+    def stream_raw_reads(self, raws, batch_size, normalization, L, stride, arrays=False):
+        from nanodecoder_amd import frontend
+        if arrays:
+            raise ValueError("arrays=True is for greedy / sampling decoding")
+        for ri, raw in enumerate(raws):
+            w = frontend.windows(int(raw.size), L, stride)
+            yield ri, [([0.0, -1.0], [[4] * (ln % 7) + [3], [4]]) for _, ln in w]
+
+
+def test_read_shard_beam_translator_on_device_frontend():
+    """ReadShard's "auto" front end picks the device path for a
+    beam translator too; it must read per-chunk results there (first
+    hypothesis) and count what the host path counts."""
+    n = 30
+    lengths = shard.read_lengths(n, seed=5)
+    a, pa = shard.ReadShard(FakeBeamTranslator(None)).run(list(range(n)), lengths, True)
+    b, pb = shard.ReadShard(FakeTranslator(None), frontend="cpu").run(list(range(n)), lengths, True)
+    assert a["frontend"] == "gpu"
+    for k in ("samples", "chunks", "bases"):
+        assert a[k] == b[k], k
+    assert all(len(c) == 2 for r in pa.values() for c in r)  # n_best strings per chunk
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -87,35 +121,43 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n_reads, q):
+def _worker(rank, world, port, n_reads, q, fail):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     dev = torch.device("cpu")
     W0 = {"w": np.arange(10, dtype=np.float32)}
     seen = {}
+    lengths = shard.read_lengths(n_reads)
 
     def tf(W):
         seen["W"] = W
-        return FakeTranslator(W)
+        if fail.get("rank") == rank:  # this rank's engine fails on its first read
+            return FakeTranslator(W, fail_sizes={int(x) for x in lengths})
+        return FakeTranslator(W, fail_sizes=fail.get("sizes", ()))
 
-    g, preds = shard.run_distributed(n_reads, tf, lambda: W0, dev, batch_size=100, keep_predictions=True)
-    q.put((rank, g, preds, seen["W"]["w"].tolist()))
+    try:
+        g, preds = shard.run_distributed(n_reads, tf, lambda: W0, dev, batch_size=100, keep_predictions=True)
+        q.put((rank, g, preds, seen["W"]["w"].tolist(), None))
+    except shard.ShardFailure as e:
+        q.put((rank, None, None, None, e.read_ids))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
-def test_sharded_run_matches_single_process(world):
-    n = 40
+def _run_world(world, n, fail):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, q, fail)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=120) for _ in range(world)]
+    res = [q.get(timeout=180) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    return sorted(res, key=lambda r: r[0])
+
+
+def _check_complete(res, n):
     # every rank received rank 0's weights through the broadcast
     assert all(r[3] == list(range(10)) for r in res)
     # all reads translated exactly once across ranks
@@ -130,3 +172,38 @@ def test_sharded_run_matches_single_process(world):
     g = res[0][1]
     assert g["samples"] == single["samples"] and g["bases"] == single["bases"] and g["chunks"] == single["chunks"]
     assert got == preds1
+    return g
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_sharded_run_matches_single_process(world):
+    n = 40 * world
+    res = _run_world(world, n, {})
+    g = _check_complete(res, n)
+    assert g["world"] == world and g["retried"] == 0
+    # LPT balance: no rank carries more than the mean plus one read's samples
+    lengths = shard.read_lengths(n)
+    assert max(g["samples_per_rank"]) - min(g["samples_per_rank"]) <= int(lengths.max())
+
+
+def test_failed_rank_reads_are_reassigned():
+    """World 4, rank 2's translator fails on its first read: its reads go to
+    ranks 0, 1, 3 (LPT) and the job's output equals a failure-free run."""
+    n, world = 120, 4
+    res = _run_world(world, n, {"rank": 2})
+    g = _check_complete(res, n)
+    lengths = shard.read_lengths(n)
+    assert g["retried"] == len(shard.lpt_assign(lengths.tolist(), world)[2])
+    assert res[2][2] == {}  # the failed rank kept none of the results
+
+
+def test_reads_failing_everywhere_are_named():
+    """A read no rank can translate: every rank raises ShardFailure naming the
+    reads left untranslated (the failing read among them)."""
+    n, world = 40, 2
+    lengths = shard.read_lengths(n)
+    bad = int(lengths[7])
+    res = _run_world(world, n, {"sizes": [bad]})
+    named = [r[4] for r in res]
+    assert all(x is not None for x in named) and named[0] == named[1]
+    assert 7 in named[0]
