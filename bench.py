@@ -280,14 +280,13 @@ def kernel_roofline(eng, B, mode, beam, encoder="transformer", alive=None, secon
     ms = us * 1e-3
     if mode == "greedy":
         # 512-sample chunks stream the 24-bit digit bank (dec_bank_d8_kernel: 3 bytes per element + a
-        # float scale per key row) or, with ND_BANK_D8=0, the split-fp16 bank (dec_bank_h3_kernel: fp16
-        # hi / lo, 4 bytes per element); exact fp32 runs the fp32 bank kernel
+        # float scale per key row); exact fp32 runs the fp32 bank kernel
         form = eng.engines[0].bank_form() if hasattr(eng, "engines") else eng.bank_form()
         if form == 2:
             name = "dec_bank_d8_kernel"
             nbytes = B * T * D * 3 + B * T * 4 + B * 4 + B * T * 4 + 2 * B * 8 * D * 4
         else:
-            name = "dec_bank_h3_kernel" if form == 1 else "dec_mem_attention_kernel<8>"
+            name = "dec_mem_attention_kernel<8>"
             nbytes = B * T * D * 4 + B * T * 4 + 2 * B * 8 * D * 4
         flops = 2 * 2 * 8 * T * D * B
         tf = flops / (ms * 1e-3) / 1e12
@@ -295,10 +294,7 @@ def kernel_roofline(eng, B, mode, beam, encoder="transformer", alive=None, secon
                                "unit": "TFLOP/s fp32-equivalent (split-fp16 on fp16 MFMA)", "frac": round(tf / SPLIT_PEAK, 4)}}
     else:
         form = eng.engines[0].bank_form() if hasattr(eng, "engines") else eng.bank_form()
-        if form == 2:  # ND_BEAM_BANK=1: the beam rows on the digit bank (digits + row scales + signal, q' and U)
-            name = f"dec_bank_d8_beam_kernel<{beam}>"
-            per_chunk = T * D * 3 + T * 4 + T * 4 + 2 * beam * 8 * D * 4
-        elif form == 3:  # the 24-bit context K/V image (1600 B per key: 3-byte k, v + 8 head scales each)
+        if form == 3:  # the 24-bit context K/V image (1600 B per key: 3-byte k, v + 8 head scales each)
             name = f"dec_ctx_attention_kernel<{beam}, true>"
             per_chunk = T * 1600 + T * 4 + 2 * beam * D * 4
         else:

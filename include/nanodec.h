@@ -432,24 +432,9 @@ int nd_op_lstm_layer(const float* xp, const float* signal, const float* wih0, co
 int nd_op_memory_pack(const float* x, const float* ln_g, const float* ln_b, float* out, int32_t B, int32_t T,
                       int32_t ldT, void* stream);
 
-/* Split-fp16 memory bank (the greedy decoder's context attention at T in
- * (448, 512]; multi_headed_attn.py:142-177 in the memory-bank form of
- * nd_op_dec_mem_attention).  nd_op_bank_pack_h3: x [B*T, 256] row-major ->
- * out, B x 512 rows as fp16 hi / lo planes in the v_mfma_f32_16x16x32_f16
- * A-operand fragment order (B * 512 * 256 * 4 bytes; LayerNorm with
- * ln_g/ln_b when set; rows t >= T zero).  nd_op_dec_bank_h3: qp [C, 2048]
- * ROW-MAJOR (one row per chunk), bank from nd_op_bank_pack_h3, T in
- * (448, 512]; out U [C16, 2048] P16.  ovf (nullable): set to 1 when an
- * operand reaches the fp16 range (|x| >= 65504).  grid: workgroups at most
- * (0 = one per chunk; fewer walk the chunks, as nd_set_bank_grid). */
-int nd_op_bank_pack_h3(const float* x, const float* ln_g, const float* ln_b, uint16_t* out, int32_t B, int32_t T,
-                       int32_t* ovf, void* stream);
-int nd_op_dec_bank_h3(const float* qp, const uint16_t* bank, const float* signal, const int32_t* span, float pad_val,
-                      float* out, int32_t C, int32_t T, int32_t* ovf, int32_t grid, void* stream);
-
 /* 24-bit fixed-point memory bank (the greedy decoder's context attention at
- * T in (448, 512] by default; ND_BANK_D8=0 keeps the split-fp16 bank; the
- * same reference lines).  nd_op_bank_pack_d8: x [B*T, 256] row-major -> the
+ * T in (448, 512]; multi_headed_attn.py:142-177 in the memory-bank form of
+ * nd_op_dec_mem_attention).  nd_op_bank_pack_d8: x [B*T, 256] row-major -> the
  * digit bank (B x 512 rows; every row t as s_t times an integer of at most
  * 126 * 2^16 in magnitude in three signed 8-bit digit planes, B * 512 * 256 *
  * 3 bytes in the v_mfma_i32_16x16x64_i8 A-operand fragment order), kscale
@@ -457,31 +442,21 @@ int nd_op_dec_bank_h3(const float* qp, const uint16_t* bank, const float* signal
  * LayerNorm with ln_g/ln_b when set; rows t >= T, and rows t >= span[c] when
  * span (nullable, [B]) is given, zero with scale 0 (the engine passes the
  * call's spans: rows past a chunk's span are never attended and must not set
- * its largest scale).  nd_op_dec_bank_d8:
- * as nd_op_dec_bank_h3 on that bank.  ovf (nullable): set to 1 on a
- * non-finite operand. */
+ * its largest scale).  nd_op_dec_bank_d8: qp [C, 2048] ROW-MAJOR (one row
+ * per chunk), T in (448, 512]; out U [C16, 2048] P16.  grid: workgroups at
+ * most (0 = one per chunk; fewer walk the chunks, as nd_set_bank_grid).  ovf
+ * (nullable): set to 1 on a non-finite operand. */
 int nd_op_bank_pack_d8(const float* x, const float* ln_g, const float* ln_b, void* bank, float* kscale,
                        int32_t* kemax, const int32_t* span, int32_t B, int32_t T, int32_t* ovf, void* stream);
 int nd_op_dec_bank_d8(const float* qp, const void* bank, const float* kscale, const int32_t* kemax,
                       const float* signal, const int32_t* span, float pad_val, float* out, int32_t C, int32_t T,
                       int32_t* ovf, int32_t grid, void* stream);
 
-/* The --fast / classic beam's context attention on the same digit bank
- * (replaces the per-layer K/V form, nd_op_dec_ctx_attention, for beam rows;
- * translate/translator.py:700-823 + decoder/transformer.py:178-189 over
- * multi_headed_attn.py:142-177): rows r = c*rpc + j (rpc 2..6) of q' [C*rpc,
- * 2048] in the P16 layout attend over chunk c's bank; out U [C*rpc, 2048]
- * P16, as nd_op_dec_bank_d8 per row.  Chunks with done[c] != 0 are skipped
- * (done nullable).  One pass over a chunk's bank serves all its rows. */
-int nd_op_dec_bank_d8_beam(const float* qp, const void* bank, const float* kscale, const int32_t* kemax,
-                           const float* signal, const int32_t* span, float pad_val, float* out, int32_t C,
-                           int32_t rpc, int32_t T, const int32_t* done, int32_t* ovf, void* stream);
-
 /* Which memory bank the context's last call streamed (diagnostics, the
  * bench's roofline accounting): 0 fp32 bank, or fp32 K/V (a beam call in
- * exact fp32 or with ND_CTX_Q24=0), 1 split-fp16 (nd_op_dec_bank_h3), 2 24-bit
- * digits (nd_op_dec_bank_d8, or nd_op_dec_bank_d8_beam for a beam call), 3 the
- * 24-bit context K/V of a beam call (nd_op_dec_ctx_attention_q24). */
+ * exact fp32), 2 24-bit digits (nd_op_dec_bank_d8), 3 the 24-bit context K/V
+ * of a beam call (nd_op_dec_ctx_attention_q24).  (1, the split-fp16 bank of
+ * rounds 2-3, is retired.) */
 int nd_bank_form(nd_ctx* ctx);
 
 /* Decoder context attention (multi_headed_attn.py:142-177): rows r = c*rpc+j

@@ -84,11 +84,8 @@ SIGNATURES = {
     "nd_op_gemm_p16_split_rm": (_I, [_P, _P, _F, _P, _F, _P, _P, _P, _I, _I, _I, _P, _I, _P, _I, _P, _P]),
     "nd_op_dec_mem_attention": (_I, [_P, _P, _P, _P, ctypes.c_float, _P, _I, _I, _I, _I, _P]),
     "nd_op_memory_pack": (_I, [_P, _P, _P, _P, _I, _I, _I, _P]),
-    "nd_op_bank_pack_h3": (_I, [_P, _P, _P, _P, _I, _I, _P, _P]),
-    "nd_op_dec_bank_h3": (_I, [_P, _P, _P, _P, ctypes.c_float, _P, _I, _I, _P, _I, _P]),
     "nd_op_bank_pack_d8": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P]),
     "nd_op_dec_bank_d8": (_I, [_P, _P, _P, _P, _P, _P, ctypes.c_float, _P, _I, _I, _P, _I, _P]),
-    "nd_op_dec_bank_d8_beam": (_I, [_P, _P, _P, _P, _P, _P, ctypes.c_float, _P, _I, _I, _I, _P, _P, _P]),
     "nd_bank_form": (_I, [_P]),
     "nd_op_lstm_layer": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _I, _P]),
     "nd_op_enc_attention": (_I, [_P, _P, _P, _P, _I, _I, _P]),

@@ -279,9 +279,6 @@ __device__ __forceinline__ void esplit8(const float (&x)[8], eh8& hi, eh8& lo) {
 // sum stays per lane until the end.  These cut the loop's VALU work, which
 // (at head dim 32) is what bounds this kernel, not the MFMAs.
 #define ENC_THR 8.0f
-#ifndef EA_EXPT
-#define EA_EXPT 0  // timing probes only (tools/build_variant.sh): 1 no loop, 2 no softmax, 4 no P.V MFMAs, 8 no LDS staging writes, 32 no K / V loads
-#endif
 typedef float ef2 __attribute__((ext_vector_type(2)));
 
 // Persistent form: one workgroup per CU walks the (chunk, head) items
@@ -331,14 +328,8 @@ enc_attention_h3_kernel(const float* __restrict__ qkv, const float* __restrict__
       if (i < i0 || i >= i1) continue;  // compile-time after unrolling
       const int idx = tid + i * NT, t = min(idx >> 3, L - 1), c = (idx & 7) * 4;
       const float* row = qkv + (base + t) * (3 * ND_D) + h * ND_DH + c;
-#if EA_EXPT & 32
-      kr[i] = f32x4{0.01f * (t & 7), 0.02f, -0.01f * (c & 3), 0.f};
-      vr[i] = kr[i];
-      (void)row;
-#else
       kr[i] = ld4(row + ND_D);
       vr[i] = ld4(row + 2 * ND_D);
-#endif
     }
   };
   auto issue_q = [&](int it) {
@@ -374,9 +365,6 @@ enc_attention_h3_kernel(const float* __restrict__ qkv, const float* __restrict__
       const bool in = t < L;
       const f32x4 k = in ? kr[i] : f32x4{0.f, 0.f, 0.f, 0.f}, v = in ? vr[i] : f32x4{0.f, 0.f, 0.f, 0.f};
       amax = fmaxf(amax, fmaxf(absmax4(k), absmax4(v)));
-#if EA_EXPT & 8
-      continue;
-#endif
       _Float16* kh = reinterpret_cast<_Float16*>(&Kp[0][t * ENC_KH]) + c;
       _Float16* kl = reinterpret_cast<_Float16*>(&Kp[1][t * ENC_KH]) + c;
       const int pos = (t & ~15) + (t & 3) + 4 * ((t >> 3) & 1) + 8 * ((t >> 2) & 1);
@@ -439,7 +427,7 @@ enc_attention_h3_kernel(const float* __restrict__ qkv, const float* __restrict__
         l[j] = 0.f;
       }
 
-      for (int kt = 0; kt < (EA_EXPT & 1 ? 0 : nkt); ++kt) {
+      for (int kt = 0; kt < nkt; ++kt) {
         f32x16 sacc[NQ];
 #pragma unroll
         for (int j = 0; j < NQ; ++j)
@@ -458,7 +446,6 @@ enc_attention_h3_kernel(const float* __restrict__ qkv, const float* __restrict__
           }
         }
         // sacc[j][r] = score(query q0 + 32 j + lr, key kt*32 + mfma32_row(r, lane)), log2 units
-#if !(EA_EXPT & 2)
         if (tdirty[kt]) {  // wave-uniform
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
@@ -497,7 +484,6 @@ enc_attention_h3_kernel(const float* __restrict__ qkv, const float* __restrict__
           }
           l[j] += ls.x + ls.y;
         }
-#endif
         // O^T[d][q] += V^T[d][key] P^T[key][q] over the tile's two 16-key k-steps
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
@@ -510,13 +496,9 @@ enc_attention_h3_kernel(const float* __restrict__ qkv, const float* __restrict__
                                  sacc[j][8 * s2 + 4], sacc[j][8 * s2 + 5], sacc[j][8 * s2 + 6], sacc[j][8 * s2 + 7]};
             eh8 ph, pl;
             esplit8(pv, ph, pl);
-#if EA_EXPT & 4
-            o[j][0] += (float)vh[0] + (float)vl[1] + (float)ph[0] + (float)pl[1];
-#else
             o[j] = mfma32h(vh, pl, o[j]);
             o[j] = mfma32h(vl, ph, o[j]);
             o[j] = mfma32h(vh, ph, o[j]);
-#endif
           }
         }
       }
@@ -539,15 +521,6 @@ enc_attention_h3_kernel(const float* __restrict__ qkv, const float* __restrict__
   }
 }
 
-// query blocks per wave of the split-fp16 encoder attention (ND_ENC_ATTN_NQ=1|2, A/B timing)
-static int enc_attn_nq() {
-  static const int n = [] {
-    const char* e = getenv("ND_ENC_ATTN_NQ");
-    return e && atoi(e) == 1 ? 1 : 2;
-  }();
-  return n;
-}
-
 // persistent grid of the split-fp16 encoder attention: one workgroup per CU
 static int enc_attn_grid() {
   static const int n = [] {
@@ -555,8 +528,7 @@ static int enc_attn_grid() {
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       cus = 256;
-    const char* e = getenv("ND_ENC_ATTN_GRID");  // workgroups (A/B timing)
-    return e && atoi(e) > 0 ? atoi(e) : (cus > 0 ? cus : 256);
+    return cus > 0 ? cus : 256;
   }();
   return n;
 }
@@ -570,9 +542,6 @@ hipError_t launch_enc_attention(const float* qkv, const float* signal, const int
   }();
   if (f32 || exact)
     hipLaunchKernelGGL(enc_attention_kernel, dim3(ND_H, B), dim3(1024), 0, s, qkv, signal, span, out, T);
-  else if (enc_attn_nq() == 1)
-    hipLaunchKernelGGL(enc_attention_h3_kernel<1>, dim3(std::min(B * ND_H, enc_attn_grid())), dim3(1024), 0, s, qkv,
-                       signal, span, out, T, B, ovf);
   else
     hipLaunchKernelGGL(enc_attention_h3_kernel<2>, dim3(std::min(B * ND_H, enc_attn_grid())), dim3(512), 0, s, qkv,
                        signal, span, out, T, B, ovf);
@@ -597,21 +566,10 @@ hipError_t launch_enc_attention(const float* qkv, const float* signal, const int
 // and then its 64 queries' E[y], E[r] as [64][16] floats, column c of row q at
 // c ^ (q & 15) (the 64 lanes' row writes hit 64 distinct banks).  The round-3
 // layout ([64][17], 67,584 B in all) put wave 7's rows q >= 34 past byte
-// 65,536 and went wrong beside other engines' kernels;
-// ND_R2_EXLD=17 / ND_R2_PAD=<bytes> / ND_R2_FRONT=<bytes> rebuild that layout,
-// pad the allocation or shift the slabs (probe builds only,
-// tools/build_variant.sh, tools/r2_lds.sh).
-#ifndef ND_R2_EXLD
-#define ND_R2_EXLD 16
-#endif
-#ifndef ND_R2_PAD
-#define ND_R2_PAD 0
-#endif
-#ifndef ND_R2_FRONT
-#define ND_R2_FRONT 0  // probe builds: the slabs start this many bytes into the allocation
-#endif
-#define R2_SLAB (8 * ENC_MAXT + 64 * ND_R2_EXLD * 4)  // bytes per wave: keys (y, r), then its queries' E[y], E[r]
-__device__ __forceinline__ int r2_col(int q, int c) { return ND_R2_EXLD == 16 ? (c ^ (q & 15)) : c; }
+// 65,536 and went wrong beside other engines' kernels (DESIGN.md section 5;
+// the probe layouts of that experiment live in git history, round 4).
+#define R2_SLAB (8 * ENC_MAXT + 64 * 16 * 4)  // bytes per wave: keys (y, r), then its queries' E[y], E[r]
+__device__ __forceinline__ int r2_col(int q, int c) { return c ^ (q & 15); }
 __global__ void __launch_bounds__(512)
 enc_attention_rank2_kernel(R2Args A, int T) {
   const float* __restrict__ signal = A.signal;
@@ -619,11 +577,10 @@ enc_attention_rank2_kernel(R2Args A, int T) {
   const EmbedQkv eq = A.eq;
   const float* __restrict__ coef = A.coef;
   float* __restrict__ out = A.out;
-  __shared__ __attribute__((aligned(16))) char smem_[ND_R2_FRONT + 8 * R2_SLAB + ND_R2_PAD];
-  char* smem = smem_ + ND_R2_FRONT;
+  __shared__ __attribute__((aligned(16))) char smem[8 * R2_SLAB];
   const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
   float2* kyr = reinterpret_cast<float2*>(smem + wave * R2_SLAB);                                   // [ENC_MAXT]
-  float(*ex)[ND_R2_EXLD] = reinterpret_cast<float(*)[ND_R2_EXLD]>(smem + wave * R2_SLAB + 8 * ENC_MAXT);  // [64][16]
+  float(*ex)[16] = reinterpret_cast<float(*)[16]>(smem + wave * R2_SLAB + 8 * ENC_MAXT);  // [64][16]
   const int L = min(span[b], T);
   const float* sig = signal + (size_t)b * T;
   // every key of the chunk in this wave: key u = 64 j + lane
@@ -771,15 +728,7 @@ hipError_t launch_dec_embed_table(const float* emb, const float* pe, int V, int 
 // through LDS at the end.  softmax is exp(s - max) / sum as torch computes
 // it; masked keys carry the reference's finite -1e18 fill, keys that do not
 // exist carry -inf (weight 0).
-// L2: scores in log2 units (q pre-scaled by log2(e)), so each weight is one
-// v_exp_f32 (exp2) without the multiply __expf adds
-template <bool L2>
-__device__ __forceinline__ float sm_exp(float x) {
-  if constexpr (L2) return __builtin_amdgcn_exp2f(x);
-  return __expf(x);
-}
-
-template <int RPC, int U, bool L2 = false>
+template <int RPC, int U>
 __device__ __forceinline__ void online_update(const float (&s)[RPC][U], const f32x4 (&v)[U], float (&m)[RPC],
                                               float (&l)[RPC], f32x4 (&acc)[RPC]) {
 #pragma unroll
@@ -787,12 +736,12 @@ __device__ __forceinline__ void online_update(const float (&s)[RPC][U], const f3
     float mx = m[j];
 #pragma unroll
     for (int u = 0; u < U; ++u) mx = fmaxf(mx, s[j][u]);  // finite: the block's first key exists
-    const float sc = sm_exp<L2>(m[j] - mx);
+    const float sc = __expf(m[j] - mx);
     acc[j] = acc[j] * sc;
     l[j] *= sc;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const float p = sm_exp<L2>(s[j][u] - mx);
+      const float p = __expf(s[j][u] - mx);
       l[j] += p;
       acc[j] += p * v[u];
     }
@@ -842,7 +791,7 @@ __device__ __forceinline__ void online_update_lazy(const float (&s)[RPC][U], con
 
 // LDS image: accs [NW][RPC][256], ms / ls [NW][RPC][8].  Output rows
 // row0 .. row0+RPC-1 of the P16-packed [*, 256] matrix out.
-template <int RPC, int NW, bool L2 = false>
+template <int RPC, int NW>
 __device__ __forceinline__ void merge_waves(float* accs, float* ms, float* ls, const float (&m)[RPC],
                                             const float (&l)[RPC], const f32x4 (&acc)[RPC], int wave, int lane,
                                             int tid, float* __restrict__ out, int row0) {
@@ -864,7 +813,7 @@ __device__ __forceinline__ void merge_waves(float* accs, float* ms, float* ls, c
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
       const float mw = ms[(w * RPC + j) * ND_H + h];
-      const float f = mw == -INFINITY ? 0.f : sm_exp<L2>(mw - M);  // waves that owned no key
+      const float f = mw == -INFINITY ? 0.f : __expf(mw - M);  // waves that owned no key
       num += f * accs[((size_t)w * RPC + j) * ND_D + d];
       den += f * ls[(w * RPC + j) * ND_H + h];
     }
@@ -876,7 +825,7 @@ __device__ __forceinline__ void merge_waves(float* accs, float* ms, float* ls, c
 // state {num[256], max[8], den[8]} at part + j * CTX_PART (the split
 // context attention; ctx_split_merge_kernel combines the splits).
 #define CTX_PART (ND_D + 2 * ND_H)
-template <int RPC, int NW, bool L2 = false>
+template <int RPC, int NW>
 __device__ __forceinline__ void merge_waves_part(float* accs, float* ms, float* ls, const float (&m)[RPC],
                                                  const float (&l)[RPC], const f32x4 (&acc)[RPC], int wave, int lane,
                                                  int tid, float* __restrict__ part) {
@@ -898,7 +847,7 @@ __device__ __forceinline__ void merge_waves_part(float* accs, float* ms, float* 
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
       const float mw = ms[(w * RPC + j) * ND_H + h];
-      const float f = mw == -INFINITY ? 0.f : sm_exp<L2>(mw - M);
+      const float f = mw == -INFINITY ? 0.f : __expf(mw - M);
       num += f * accs[((size_t)w * RPC + j) * ND_D + d];
       den += f * ls[(w * RPC + j) * ND_H + h];
     }
@@ -921,9 +870,6 @@ __device__ __forceinline__ void merge_waves_part(float* accs, float* ms, float* 
 // one per block), then the NW partial states merge through LDS.
 #define SELF_MAXS 256
 #define SELF_TABV 8  // vocabulary bound of the head-fused form (its candidate table rows sit in LDS)
-#ifndef SA_EXPT
-#define SA_EXPT 0  // timing probes only (tools/build_variant.sh): 1 no cache loads, 2 no merge
-#endif
 // HEAD (greedy, layer 0 in table mode, step > 0): wave 0 first runs the
 // previous step's greedy head for the row (head.hpp), whose token picks the
 // row's q | k | v in the table; the other waves' cache loads are in flight
@@ -971,14 +917,8 @@ dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cac
       const int t = min(t0 + u, tmax);  // wave-uniform
       const int slot = ANC ? __builtin_amdgcn_readlane(sv, u) : r;
       const float* row = cache + ((size_t)slot * S + t) * 2 * ND_D + lane * 4;
-#if SA_EXPT & 1
-      k[u] = f32x4{0.01f * u, 0.f, 0.f, 0.f};
-      v[u] = k[u];
-      (void)row;
-#else
       k[u] = ld4(row);
       v[u] = ld4(row + ND_D);
-#endif
     }
   };
   // the first pass's cache loads go out before the row's q | k | v, whose
@@ -1059,10 +999,6 @@ dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cac
     st4(mine + lane * 4, kme);
     st4(mine + ND_D + lane * 4, vme);
   }
-#if SA_EXPT & 2
-  if (wave == 0 && l[0] == 12345.f) st4(out + pk(r, lane * 4, ND_D), acc[0]);
-  return;
-#endif
   merge_waves<1, NW>(accs, ms, ls, m, l, acc, wave, lane, tid, out, r);
 }
 
@@ -1079,11 +1015,7 @@ hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* 
   }
   const GreedyHead hd = head ? *head : GreedyHead();
   const int skip_rpc = rpc;
-  static const int xcd = [] {
-    const char* e = getenv("ND_SELF_XCD");  // 0: row order (A/B timing)
-    return e ? atoi(e) : 1;
-  }();
-  if (!xcd || rpc < 2 || R % (8 * rpc)) rpc = 1;
+  if (rpc < 2 || R % (8 * rpc)) rpc = 1;
   if (clist && (ccap < 1 || (long)ccap * skip_rpc > R || head)) return hipErrorInvalidValue;
   const int grid = clist ? ccap * skip_rpc : R;
   if (step >= max_steps || step >= SELF_MAXS) return hipErrorInvalidValue;
@@ -1098,34 +1030,15 @@ hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* 
     ND_SELF2(NW, KW, false, true);     \
   else                                 \
     ND_SELF2(NW, KW, false, false)
-  // 8 waves per row at every length (16 keys per wave from 65 keys on): the
-  // 16-wave forms fill a CU's whole register file (16 x 113-119 VGPRs), the
-  // 8-wave ones leave room for another pool lane's waves: pooled 17.85 ->
-  // 17.73 ms per call, one call in flight 23.72 -> 23.59 ms (two reps each,
-  // same box).  ND_SELF_NW8=0 keeps the 16-wave forms (A/B timing)
-  static const bool w8 = [] {
-    const char* e = getenv("ND_SELF_NW8");
-    return !(e && atoi(e) == 0);
-  }();
-  // 4 waves of up to 16 keys per row up to 64 keys: beam rows (ancestry),
-  // configs[3] pooled 75.62 -> 74.59 ms, one call 94.28 -> 93.60 ms; greedy
-  // rows, pooled 16.75 / 16.84 -> 16.72 / 16.70 ms (two reps each, one box).
-  // ND_SELF_NW4: 0 never, 1 beam rows only, 2 every row (default)
-  static const int nw4 = [] {
-    const char* e = getenv("ND_SELF_NW4");
-    return e ? atoi(e) : 2;
-  }();
-  if ((nw4 == 2 || (nw4 == 1 && anc)) && n <= 64) {
-    if (n <= 16) ND_SELF(4, 4);
-    else if (n <= 32) ND_SELF(4, 8);
-    else ND_SELF(4, 16);
-    return hipGetLastError();
-  }
-  if (n <= 32) ND_SELF(8, 4);
-  else if (w8 && n <= 64) ND_SELF(8, 8);
-  else if (w8) ND_SELF(8, 16);  // two passes beyond 128 keys
-  else if (n <= 64) ND_SELF(16, 4);
-  else ND_SELF(16, 8);  // two passes beyond 128 keys
+  // 4 waves of up to 16 keys per row up to 64 keys (beam rows: configs[3]
+  // pooled 75.62 -> 74.59 ms, one call 94.28 -> 93.60 ms; greedy rows pooled
+  // 16.75 / 16.84 -> 16.72 / 16.70 ms), then 8 waves of 16 keys (the 16-wave
+  // forms fill a CU's whole register file and shut other pool lanes out:
+  // pooled 17.85 -> 17.73 ms per call); round 3-4 same-box A/B pairs
+  if (n <= 16) ND_SELF(4, 4);
+  else if (n <= 32) ND_SELF(4, 8);
+  else if (n <= 64) ND_SELF(4, 16);
+  else ND_SELF(8, 16);  // two passes beyond 128 keys
 #undef ND_SELF
 #undef ND_SELF2
   return hipGetLastError();
@@ -1147,29 +1060,12 @@ hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* 
 // tools/_g44.sh); round 2 measured the two forms equal alone.  Round 4: 4
 // waves per chunk (more chunks' workgroups per CU beside the other lanes):
 // configs[3] pooled 77.3 -> 75.9 ms on one box (profiles/r04_beam_ab.txt)
-#ifndef CTX_NW
+// Measured and dropped (round 4, profiles/r04_beam_ab.txt): scores in log2
+// units, a select-free path for plain key blocks, waves-per-EU hints, 2 / 8 /
+// 16 waves per chunk, 4-key blocks above 2 rows per chunk.
 #define CTX_NW 4
-#endif
-#ifndef CTX_URPC
 #define CTX_URPC 2  // rows per chunk up to which a block holds 4 keys (else 2)
-#endif
-#ifndef CTX_UHI
-#define CTX_UHI 2  // keys per block above CTX_URPC rows
-#endif
-#ifndef CTX_WPE
-#define CTX_WPE 0  // timing variants: amdgpu_waves_per_eu hint (0: none)
-#endif
-#ifndef CTX_PLAIN
-#define CTX_PLAIN 0  // 1: select-free scores for blocks of existing unmasked keys (measured slower: 78.9 vs 77.3 ms)
-#endif
-#ifndef CTX_LAZY
-#define CTX_LAZY 1  // the lazy running maximum (online_update_lazy); 0: rescale every block (A/B)
-#endif
-#ifndef CTX_EXP2
-#define CTX_EXP2 0  // 1: scores in log2 units (q pre-scaled by log2(e) / sqrt(32)); measured slower in the engine (A/B)
-#endif
-#define ND_LOG2E 1.4426950408889634f
-#define ND_LN2 0.6931471805599453f
+#define CTX_UHI 2   // keys per block above CTX_URPC rows
 #define CTX_MAXR 6
 template <int RPC>
 struct CtxTile {
@@ -1183,9 +1079,6 @@ struct CtxTile {
 // sum) and into v.  kv, ld and koff are then bytes.
 template <int RPC, bool Q24>
 __global__ void __launch_bounds__(CTX_NW * 64)
-#if CTX_WPE > 0
-__attribute__((amdgpu_waves_per_eu(CTX_WPE)))
-#endif
 dec_ctx_attention_kernel(const float* __restrict__ q, const void* __restrict__ kv_, int ld, int koff,
                          const float* __restrict__ signal, const int* __restrict__ span, float pad_val,
                          float* __restrict__ out, int T, unsigned long long* stamp, float* __restrict__ dbg,
@@ -1211,9 +1104,8 @@ dec_ctx_attention_kernel(const float* __restrict__ q, const void* __restrict__ k
   float m[RPC], l[RPC];
 #pragma unroll
   for (int j = 0; j < RPC; ++j) {
-    // q, out P16-packed; log2 units: q / sqrt(32) * log2(e)
-    qv[j] = CTX_EXP2 ? ld4(q + pk(c * RPC + j, lane * 4, ND_D)) * (ND_LOG2E / ND_SQRT_DH)
-                     : ld4(q + pk(c * RPC + j, lane * 4, ND_D)) / ND_SQRT_DH;
+    // q, out P16-packed
+    qv[j] = ld4(q + pk(c * RPC + j, lane * 4, ND_D)) / ND_SQRT_DH;
     acc[j] = {0.f, 0.f, 0.f, 0.f};
     m[j] = -INFINITY;
     l[j] = 0.f;
@@ -1253,12 +1145,6 @@ dec_ctx_attention_kernel(const float* __restrict__ q, const void* __restrict__ k
     if (more) load(blk + CTX_NW, kn, vn, sn);
     float sc[RPC][U];
     f32x4 vf[U];
-    // a block of existing, unmasked keys (wave-uniform: the signal value is
-    // the same in every lane) takes its scores as they are, no selects
-    bool plain = CTX_PLAIN && (blk + 1) * U <= L;
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      plain &= __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(sg[u]))) != pad_val;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const bool valid = blk * U + u < L;
@@ -1278,20 +1164,15 @@ dec_ctx_attention_kernel(const float* __restrict__ q, const void* __restrict__ k
         if constexpr (Q24) d *= ks;
         sc[j][u] = d;
       }
-      if (!plain)
 #pragma unroll
-        for (int j = 0; j < RPC; ++j) sc[j][u] = valid ? (masked ? ND_MASK_FILL : sc[j][u]) : -INFINITY;
+      for (int j = 0; j < RPC; ++j) sc[j][u] = valid ? (masked ? ND_MASK_FILL : sc[j][u]) : -INFINITY;
       // -attn_debug / coverage: head 0 (lanes 0..7 after sum8) of every row of the chunk
       if (dbg && lane == 0 && valid)
 #pragma unroll
         for (int j = 0; j < RPC; ++j)  // natural units (the -1e18 fill as it stands)
-          dbg[((size_t)c * RPC + j) * dbg_stride + blk * U + u] =
-              (CTX_EXP2 && sc[j][u] != ND_MASK_FILL) ? sc[j][u] * ND_LN2 : sc[j][u];
+          dbg[((size_t)c * RPC + j) * dbg_stride + blk * U + u] = sc[j][u];
     }
-    if constexpr (CTX_LAZY && !CTX_EXP2)
-      online_update_lazy<RPC, U>(sc, vf, m, l, acc);
-    else
-      online_update<RPC, U, CTX_EXP2>(sc, vf, m, l, acc);
+    online_update_lazy<RPC, U>(sc, vf, m, l, acc);
     if (more) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -1302,10 +1183,10 @@ dec_ctx_attention_kernel(const float* __restrict__ q, const void* __restrict__ k
     }
   }
   if (part)
-    merge_waves_part<RPC, CTX_NW, CTX_EXP2>(accs, ms, ls, m, l, acc, wave, lane, tid,
+    merge_waves_part<RPC, CTX_NW>(accs, ms, ls, m, l, acc, wave, lane, tid,
                                             part + (size_t)blockIdx.x * RPC * CTX_PART);
   else
-    merge_waves<RPC, CTX_NW, CTX_EXP2>(accs, ms, ls, m, l, acc, wave, lane, tid, out, c * RPC);
+    merge_waves<RPC, CTX_NW>(accs, ms, ls, m, l, acc, wave, lane, tid, out, c * RPC);
   stamp_end(stamp);
 }
 
@@ -1324,7 +1205,7 @@ ctx_split_merge_kernel(const float* __restrict__ part, const int* __restrict__ c
   float num = 0.f, den = 0.f;
   for (int s = 0; s < nsplit; ++s) {
     const float ms = p[s * ps + ND_D + h];
-    const float f = ms == -INFINITY ? 0.f : sm_exp<CTX_EXP2>(ms - M);  // a split with no key
+    const float f = ms == -INFINITY ? 0.f : __expf(ms - M);  // a split with no key
     num += f * p[s * ps + d];
     den += f * p[s * ps + ND_D + ND_H + h];
   }

@@ -171,9 +171,7 @@ struct nd_ctx {
   float *x = nullptr, *y = nullptr, *att = nullptr, *big = nullptr, *ctxkv = nullptr;
   float* mem_p = nullptr;                 // memory bank [B * T, 256] row-major (LN'd encoder output)
   const float* mem = nullptr;             // the bank the decoder reads: mem_p, or x (NanoEncoder)
-  bool bank_h3 = false;                   // mem_p holds the split-fp16 fragment bank (dec_bank_h3_kernel)
-  bool bank_d8 = false;                   // ... or the 24-bit digit bank (dec_bank_d8_kernel; bank8.hip)
-  bool beam_bank = false;                 // beam rows read the digit bank (dec_bank_d8_beam_kernel), not K/V
+  bool bank_d8 = false;                   // mem_p holds the 24-bit digit bank (dec_bank_d8_kernel; bank8.hip)
   bool ctx_q24 = false;                   // beam rows read the 24-bit context K/V image (ctxq), not fp32 ctxkv
   int* clist = nullptr;                   // --fast beam tail: the alive chunks (launch_alive_list), ceil(B/16)
   float* ctx_part = nullptr;              // ... and the split context attention's partial states
@@ -554,43 +552,30 @@ struct G {
 
 // Encoder forward (transformer): x <- memory before the final LayerNorm (its
 // row statistics in x_part); the final LN is the ctx-K/V GEMM's prologue.
-// fused FFN block (ffn.hip) on the split-fp16 path; ND_ENC_FFN=0 keeps the
-// two GEMMs (A/B timing; same arithmetic)
+// fused FFN block (ffn.hip) on the split-fp16 path (exact fp32 keeps the two
+// GEMMs; same arithmetic)
 static bool enc_ffn_fused(const nd_ctx* c, const EncLayer& L) {
-  static const bool on = [] {
-    const char* e = getenv("ND_ENC_FFN");
-    return !(e && atoi(e) == 0);
-  }();
+  constexpr bool on = true;
   return on && !c->exact && L.w1h != nullptr && !nd::gemm_f32_forced();
 }
 
 // the attention's output projection folded into the fused FFN block's launch
-// (y never written); ND_ENC_WO=0 keeps the Wo GEMM (A/B timing)
+// (y never written)
 static bool enc_wo_fused(const nd_ctx* c, const EncLayer& L) {
-  static const bool on = [] {
-    const char* e = getenv("ND_ENC_WO");
-    return !(e && atoi(e) == 0);
-  }();
+  constexpr bool on = true;
   return on && enc_ffn_fused(c, L) && L.woh != nullptr;
 }
 
-// layer 0's QKV from the embedding in the rank-2 form (EmbedQkv); ND_ENC_QKV0=0
-// keeps its GEMM (A/B timing)
+// layer 0's QKV from the embedding in the rank-2 form (EmbedQkv)
 static bool enc_qkv0_rank2(const nd_ctx* c) {
-  static const bool on = [] {
-    const char* e = getenv("ND_ENC_QKV0");
-    return !(e && atoi(e) == 0);
-  }();
+  constexpr bool on = true;
   return on && c->eq_ready;
 }
 
 // the next layer's QKV projection folded into the FFN block's launch (q | k | v
-// from the block's registers); ND_ENC_QKV=0 keeps its GEMM (A/B timing)
+// from the block's registers)
 static bool enc_qkv_folded(const nd_ctx* c, const EncLayer& next) {
-  static const bool on = [] {
-    const char* e = getenv("ND_ENC_QKV");
-    return !(e && atoi(e) == 0);
-  }();
+  constexpr bool on = true;
   return on && next.qkvh != nullptr;
 }
 
@@ -677,12 +662,9 @@ static hipError_t enqueue_ctxkv(nd_ctx* c, int B, int T, hipStream_t s, bool q24
   return G(c->x, D, c->ctxkv_w, N, D, c->ctxkv_b, c->ctxkv, N, M).h3(c).q24(img, ld).run(s);
 }
 
-// the 24-bit image straight from the K/V GEMM's epilogue (ND_CTX_Q24_FUSE=0: fp32 K/V, then the pack kernel)
+// the 24-bit image straight from the K/V GEMM's epilogue (fp32-forced GEMMs: fp32 K/V, then the pack kernel)
 static bool use_ctx_q24_fuse() {
-  static const bool on = [] {
-    const char* e = getenv("ND_CTX_Q24_FUSE");
-    return !(e && atoi(e) == 0);
-  }();
+  constexpr bool on = true;
   return on;
 }
 
@@ -690,22 +672,16 @@ static hipError_t enqueue_encode(nd_ctx* c, int B, int T, hipStream_t s);
 
 // Layer 0 of a scaled-dot decoder reads q | k | v from the per-call table
 // QKV0[step][token] (kernels.hpp, QkvRows) instead of running its QKV GEMM
-// every step; ND_QKV_TABLE=0 keeps the per-step GEMM (A/B timing).
+// every step (average-attention decoders keep the per-step GEMM).
 static bool use_qkv_table(const nd_ctx* c) {
-  static const bool on = [] {
-    const char* e = getenv("ND_QKV_TABLE");
-    return !(e && atoi(e) == 0);
-  }();
+  constexpr bool on = true;
   return on && c->qtab != nullptr;
 }
 
 // the greedy head fused into the next step's layer-0 self-attention (table
-// mode, scaled-dot layer 0); ND_HEAD_FUSE=0 keeps one head launch per step (A/B timing)
+// mode, scaled-dot layer 0)
 static bool head_fused(const nd_ctx* c) {
-  static const bool on = [] {
-    const char* e = getenv("ND_HEAD_FUSE");
-    return !(e && atoi(e) == 0);
-  }();
+  constexpr bool on = true;
   return on && use_qkv_table(c) && c->cfg.self_attn_type != ND_SELF_AVERAGE && c->V <= 8;  // SELF_TABV
 }
 
@@ -747,43 +723,18 @@ static hipError_t enqueue_first_embed(nd_ctx* c, int R, hipStream_t s) {
 
 // One decoder step for R = C*rpc rows: dx (embedded input, row stats in
 // dx_part) -> dx (pre final LN).
-// greedy rows always take the memory-bank form (ctx path 0); beam rows when
-// set_memory_view chose the digit bank for them
-static bool use_memory_bank(nd_ctx* c, int rpc) { return c->ctx_path == 0 && (rpc == 1 || c->beam_bank); }
+// greedy rows always take the memory-bank form (ctx path 0); beam rows read
+// the per-layer context K/V
+static bool use_memory_bank(nd_ctx* c, int rpc) { return c->ctx_path == 0 && rpc == 1; }
 
 // The decoder's view of the encoder output: a pure function of (ctx path,
 // exact, T, rpc, encoder type).  Set on the host before every call's graphs
 // run or are captured: a replayed encoder graph does not re-enter
 // enqueue_memory, but the step graphs captured after it read these fields.
-// the 24-bit digit bank instead of the split-fp16 one (bank8.hip); ND_BANK_D8=0
-// keeps the split-fp16 bank
-static bool use_bank_d8() {
-  static const bool on = [] {
-    const char* e = getenv("ND_BANK_D8");
-    return !(e && atoi(e) == 0);
-  }();
-  return on;
-}
-
-// --fast / classic beam rows on the digit bank (bank8.hip dec_bank_d8_beam_kernel) instead of the
-// per-layer context K/V: ND_BEAM_BANK=1 (off by default: parity-green, but 95.7 against 86.1 ms per
-// pooled configs[3] call).  Not with a capturing call (-attn_debug, coverage
-// penalty): those read the K/V kernel's per-row scores
-static bool use_beam_bank() {
-  static const bool on = [] {
-    const char* e = getenv("ND_BEAM_BANK");
-    return e && atoi(e) != 0;
-  }();
-  return on;
-}
-
 // beam rows' context K/V in 24-bit fixed point (attention.hip ctx_pack_q24_kernel: 0.78x the bytes of
-// the HBM-bound context attention); ND_CTX_Q24=0 keeps fp32 K/V.  Exact fp32 keeps fp32 K/V
+// the HBM-bound context attention).  Exact fp32 keeps fp32 K/V
 static bool use_ctx_q24() {
-  static const bool on = [] {
-    const char* e = getenv("ND_CTX_Q24");
-    return !(e && atoi(e) == 0);
-  }();
+  constexpr bool on = true;
   return on;
 }
 
@@ -808,22 +759,18 @@ static int ctx_split() {
 }
 
 static void set_memory_view(nd_ctx* c, int T, int rpc) {
-  c->bank_h3 = false;
   c->bank_d8 = false;
   c->mem = nullptr;
   c->last_bank_form = 0;
-  c->beam_bank = rpc > 1 && rpc <= 6 && c->ctx_path == 0 && use_beam_bank() && use_bank_d8() && !c->exact &&
-                 !c->attn_on && nd::bank_h3_eligible(T, c->cfg.max_src_len);
   c->ctx_q24 = !use_memory_bank(c, rpc) && !c->exact && use_ctx_q24();
   if (c->ctx_q24) c->last_bank_form = 3;
   if (!use_memory_bank(c, rpc)) return;
   const bool tf = c->cfg.encoder_type == ND_ENC_TRANSFORMER;
-  // 512-sample chunks: the split-fp16 fragment bank (LN'd for the transformer,
-  // the NanoEncoder's output as it stands)
-  c->bank_h3 = !c->exact && nd::bank_h3_eligible(T, c->cfg.max_src_len);
-  c->bank_d8 = c->bank_h3 && use_bank_d8();
-  c->mem = (c->bank_h3 || tf) ? c->mem_p : c->x;  // the NanoEncoder's fp32 output is the bank as it stands
-  c->last_bank_form = c->bank_d8 ? 2 : c->bank_h3 ? 1 : 0;
+  // 512-sample chunks: the 24-bit digit bank (LN'd for the transformer, the
+  // NanoEncoder's output as it stands)
+  c->bank_d8 = !c->exact && nd::bank_eligible(T, c->cfg.max_src_len);
+  c->mem = (c->bank_d8 || tf) ? c->mem_p : c->x;  // the NanoEncoder's fp32 output is the bank as it stands
+  c->last_bank_form = c->bank_d8 ? 2 : 0;
 }
 
 // done: per chunk, nonzero = finished (--fast beam; null otherwise): its rows'
@@ -880,19 +827,11 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
     }
     if (mb) {  // memory-bank form (attention.hip)
       const int HD = ND_H * D;
-      // q' row-major for the split-fp16 bank kernel (one row per chunk), P16 for the fp32 one and for
-      // beam rows
-      LCHK(dg(c->dq1, D, L.pwqk, HD, D, L.bqk, c->dqk, HD).ln(c->dq1_part, pnq).c_rowmajor(c->bank_h3 && rpc == 1).run(s));
-      if (rpc > 1)
-        LCHK(nd::launch_dec_bank_d8_beam(c->dqk, c->mem_p, c->bank_ks, c->bank_em, c->sig, c->span,
-                                         (float)c->cfg.pad_idx, c->dU, C, rpc, T, done, s, stamp, c->ovf));
-      else if (c->bank_d8)
+      // q' row-major for the digit-bank kernel (one row per chunk), P16 for the fp32 one
+      LCHK(dg(c->dq1, D, L.pwqk, HD, D, L.bqk, c->dqk, HD).ln(c->dq1_part, pnq).c_rowmajor(c->bank_d8).run(s));
+      if (c->bank_d8)
         LCHK(nd::launch_dec_bank_d8(c->dqk, c->mem_p, c->bank_ks, c->bank_em, c->sig, c->span, (float)c->cfg.pad_idx,
                                     c->dU, C, T, s, stamp, dbg, dbg_stride, c->ovf, c->bank_nt, c->bank_grid));
-      else if (c->bank_h3)
-        LCHK(nd::launch_dec_bank_h3(c->dqk, reinterpret_cast<const uint16_t*>(c->mem_p), c->sig, c->span,
-                                    (float)c->cfg.pad_idx, c->dU, C, T, s, stamp, dbg, dbg_stride, c->ovf,
-                                    c->bank_nt, c->bank_grid));
       else
         LCHK(nd::launch_dec_mem_attention(c->dqk, c->mem, c->sig, c->span, (float)c->cfg.pad_idx, c->dU, C, rpc, T,
                                           T, s, stamp, dbg, dbg_stride));
@@ -931,9 +870,6 @@ static hipError_t enqueue_memory(nd_ctx* c, int B, int T, int rpc, hipStream_t s
   if (c->bank_d8)
     return nd::launch_bank_pack_d8(c->x, tf ? c->enc_ln_g : nullptr, tf ? c->enc_ln_b : nullptr, c->mem_p, c->bank_ks,
                                    c->bank_em, c->span, B, T, c->ovf, s);
-  if (c->bank_h3)
-    return nd::launch_bank_pack_h3(c->x, tf ? c->enc_ln_g : nullptr, tf ? c->enc_ln_b : nullptr,
-                                   reinterpret_cast<uint16_t*>(c->mem_p), B, T, c->ovf, s);
   if (!tf) return hipSuccess;  // the NanoEncoder's output is the bank as it stands
   return nd::launch_memory_pack(c->x, c->enc_ln_g, c->enc_ln_b, c->mem_p, B, T, T, s);
 }
@@ -1734,16 +1670,8 @@ int nd_gemm_routes(int64_t* counts, int32_t n, int32_t reset) {
 static const struct {
   const char* name;
   int def;
-} kSwitches[] = {{"ND_GEMM_F32", 0},   {"ND_GEMM_TILE", 0},    {"ND_GEMM_BKL", 64},     {"ND_GEMM_XCD", 1},
-                 {"ND_P16_XCD", 1},    {"ND_P16_BIG_MIN", 2048}, {"ND_ENC_FFN", 1},     {"ND_QKV_TABLE", 1},
-                 {"ND_HEAD_FUSE", 1},  {"ND_LSTM_F32", 0},     {"ND_LSTM_LIBM", 0},     {"ND_LSTM_SEQ", 4},
-                 {"ND_ENC_ATTN_NQ", 2}, {"ND_ENC_ATTN_GRID", 0}, {"ND_ENC_ATTN_F32", 0}, {"ND_SELF_XCD", 1},
-                 {"ND_ENC_WO", 1},     {"ND_ENC_QKV0", 1},
-                 {"ND_ENC_QKV", 1},    {"ND_ENC_ATTN0", 1},   {"ND_SELF_NW8", 1},     {"ND_BANK_D8", 1},
-                 {"ND_BEAM_BANK", 0},  {"ND_BB_PIPE", 1},     {"ND_P16_K2048", 0},
-                 {"ND_CTX_Q24", 1},    {"ND_BEAM_COMPACT", 1}, {"ND_CTX_SPLIT", 16},
-                 {"ND_GEMM_T32", 0},   {"ND_CTX_Q24_FUSE", 1},
-                 {"ND_SELF_NW4", 2}};
+} kSwitches[] = {{"ND_GEMM_F32", 0},  {"ND_ENC_ATTN_F32", 0}, {"ND_LSTM_F32", 0},
+                 {"ND_ENC_ATTN0", 1}, {"ND_BEAM_COMPACT", 1}, {"ND_CTX_SPLIT", 16}};
 
 int nd_switches(char* buf, int32_t len) {
   std::string out;
@@ -2054,24 +1982,6 @@ int nd_op_memory_pack(const float* x, const float* ln_g, const float* ln_b, floa
   return ND_OK;
 }
 
-int nd_op_bank_pack_h3(const float* x, const float* ln_g, const float* ln_b, uint16_t* out, int32_t B, int32_t T,
-                       int32_t* ovf, void* stream) {
-  if (!x || !out || (ln_g == nullptr) != (ln_b == nullptr)) return fail(ND_ERR_ARG, "bank_pack_h3: bad arguments");
-  hipError_t e = nd::launch_bank_pack_h3(x, ln_g, ln_b, out, B, T, ovf, (hipStream_t)stream);
-  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("bank_pack_h3: ") + hipGetErrorString(e));
-  return ND_OK;
-}
-
-int nd_op_dec_bank_h3(const float* qp, const uint16_t* bank, const float* signal, const int32_t* span, float pad_val,
-                      float* out, int32_t C, int32_t T, int32_t* ovf, int32_t grid, void* stream) {
-  if (int rc = ensure_attributes()) return rc;
-  if (!qp || !bank || !signal || !span || !out || grid < 0) return fail(ND_ERR_ARG, "dec_bank_h3: bad arguments");
-  hipError_t e = nd::launch_dec_bank_h3(qp, bank, signal, span, pad_val, out, C, T, (hipStream_t)stream, nullptr,
-                                        nullptr, 0, ovf, false, grid);
-  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("dec_bank_h3: ") + hipGetErrorString(e));
-  return ND_OK;
-}
-
 int nd_op_bank_pack_d8(const float* x, const float* ln_g, const float* ln_b, void* bank, float* kscale,
                        int32_t* kemax, const int32_t* span, int32_t B, int32_t T, int32_t* ovf, void* stream) {
   if (!x || !bank || !kscale || !kemax || (ln_g == nullptr) != (ln_b == nullptr))
@@ -2090,17 +2000,6 @@ int nd_op_dec_bank_d8(const float* qp, const void* bank, const float* kscale, co
   hipError_t e = nd::launch_dec_bank_d8(qp, bank, kscale, kemax, signal, span, pad_val, out, C, T,
                                         (hipStream_t)stream, nullptr, nullptr, 0, ovf, false, grid);
   if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("dec_bank_d8: ") + hipGetErrorString(e));
-  return ND_OK;
-}
-
-int nd_op_dec_bank_d8_beam(const float* qp, const void* bank, const float* kscale, const int32_t* kemax,
-                           const float* signal, const int32_t* span, float pad_val, float* out, int32_t C,
-                           int32_t rpc, int32_t T, const int32_t* done, int32_t* ovf, void* stream) {
-  if (!qp || !bank || !kscale || !kemax || !signal || !span || !out)
-    return fail(ND_ERR_ARG, "dec_bank_d8_beam: bad arguments");
-  hipError_t e = nd::launch_dec_bank_d8_beam(qp, bank, kscale, kemax, signal, span, pad_val, out, C, rpc, T, done,
-                                             (hipStream_t)stream, nullptr, ovf);
-  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("dec_bank_d8_beam: ") + hipGetErrorString(e));
   return ND_OK;
 }
 

@@ -872,12 +872,8 @@ template <int BM, int BN, int WM, int WN, int BK = 32>
 static hipError_t launch_cfg(GemmArgs& g, hipStream_t s) {
   if (g.K % BK != 0) return hipErrorInvalidValue;
   count_route(BM == 256 ? ND_ROUTE_TILE256 : BM == 128 ? ND_ROUTE_TILE128 : ND_ROUTE_TILE64);  // (32 counts as 64)
-  static const int xcd = [] {
-    const char* e = getenv("ND_GEMM_XCD");  // 0: column tile fastest (A/B timing)
-    return e ? atoi(e) : 1;
-  }();
   const int nmb = (g.M + BM - 1) / BM;
-  g.xcd_map = xcd && nmb % 8 == 0;
+  g.xcd_map = nmb % 8 == 0;
   dim3 grid((g.N / BN) * nmb), block(WM * WN * 64);
   g.part_n_out = g.N / BN;
   if (g.Wh)
@@ -891,13 +887,9 @@ static hipError_t launch_cfg(GemmArgs& g, hipStream_t s) {
 // each XCD's L2 fetches: GY / a row blocks of A plus GX / (8 / a) column
 // groups of W (NT column blocks each); 0 when no split divides the grid.
 static int p16_xcd_rows(int GX, int GY, int NT) {
-  static const bool on = [] {
-    const char* e = getenv("ND_P16_XCD");  // 0: grid order (A/B timing)
-    return !(e && atoi(e) == 0);
-  }();
   int best = 0;
   long cost = 0;
-  for (int a = 1; a <= 8 && on; a *= 2) {
+  for (int a = 1; a <= 8; a *= 2) {
     const int b = 8 / a;
     if (GY % a || GX % b) continue;
     const long c = (long)GY / a + (long)NT * GX / b;
@@ -1005,36 +997,20 @@ hipError_t launch_gemm(GemmArgs& g, hipStream_t s) {
       return hipErrorInvalidValue;
     return launch_cfg<256, 256, 2, 4>(g, s);
   }
-  static const int big = [] {
-    const char* e = getenv("ND_GEMM_TILE");  // 128: force the 128x128 tiles (A/B timing)
-    return !(e && atoi(e) == 128);
-  }();
   // 256x256 tiles, 8 waves of 128x64: half the global->LDS bytes per flop and
   // half the per-tile prologue/epilogue share of the 128x128 tile
   const long t256 = (long)((g.M + 255) / 256) * (g.N / 256);
-  if (big && g.N % 256 == 0 && t256 >= 256) return launch_cfg<256, 256, 2, 4>(g, s);
+  if (g.N % 256 == 0 && t256 >= 256) return launch_cfg<256, 256, 2, 4>(g, s);
   const long t128 = (long)((g.M + 127) / 128) * (g.N / 128);
   if (g.N % 128 == 0 && t128 >= 512) return launch_cfg<128, 128, 2, 2>(g, s);
   if (g.N % 64 != 0) return hipErrorInvalidValue;
-  static const int bkl = [] {
-    const char* e = getenv("ND_GEMM_BKL");  // k step of the 64x64 tiles at K >= 1024 (32, 64, 128)
-    const int v = e ? atoi(e) : 64;
-    return v == 32 || v == 128 ? v : 64;
-  }();
   // long K on few small tiles (the beam decoder's K = 2048 products at M = 5120):
   // deeper k steps keep more of the next step's operands in flight.  Measured
   // at M = 5120, N = 256, K = 2048: BK 32 / 64 / 128 = 49.1 / 45.8 / 71.7 us
-  // (128: 135 KB of LDS, one workgroup per CU); beam B = 1024 168.9 -> 164.7 ms
-  static const int t32 = [] {
-    const char* e = getenv("ND_GEMM_T32");  // 1: 32 x 64 tiles for the long-K products (A/B timing)
-    return e ? atoi(e) : 0;
-  }();
-  if (g.K >= 1024 && g.K % 128 == 0) {
-    // fewer 64 x 64 tiles than two per CU: 32 x 64 tiles (two waves) double them
-    if (t32 && (long)((g.M + 63) / 64) * (g.N / 64) < 512) return launch_cfg<32, 64, 1, 2, 64>(g, s);
-    if (bkl == 128) return launch_cfg<64, 64, 2, 2, 128>(g, s);
-    if (bkl == 64) return launch_cfg<64, 64, 2, 2, 64>(g, s);
-  }
+  // (128: 135 KB of LDS, one workgroup per CU); beam B = 1024 168.9 -> 164.7 ms.
+  // 32 x 64 tiles there (two waves, twice the workgroups): 76.2 -> 78.2 ms per
+  // pooled configs[3] call (round 4), dropped.
+  if (g.K >= 1024 && g.K % 64 == 0) return launch_cfg<64, 64, 2, 2, 64>(g, s);
   return launch_cfg<64, 64, 2, 2>(g, s);
 }
 
@@ -1044,10 +1020,7 @@ hipError_t launch_gemm_p16(GemmArgs& g, hipStream_t s) {
   if (!g.W && !g.Wh) return hipErrorInvalidValue;
   hipError_t e = check_args(g);
   if (e != hipSuccess) return e;
-  static const int big_min = [] {
-    const char* e = getenv("ND_P16_BIG_MIN");  // rows from which the LDS-tiled kernel takes P16 GEMMs
-    return e ? atoi(e) : 2048;
-  }();
+  constexpr int big_min = 2048;  // rows from which the LDS-tiled kernel takes P16 GEMMs
   if (g.M >= big_min && !g.prefer_p16 && !g.c_rm && g.Wh_rm && !gemm_f32_only() && g.N % 64 == 0 &&
       (g.N >= 512 || g.K >= 1024)) {
     // many rows (beam search over large batches): the encoder's LDS-tiled
@@ -1077,14 +1050,8 @@ hipError_t launch_gemm_p16(GemmArgs& g, hipStream_t s) {
     if (g.N % 64 == 0 && (long)(g.N / 64) * ((g.M + 15) / 16) >= 128) return launch_p16<4, 2, 128>(g, s);
     return launch_p16<1, 4, 64>(g, s);
   }
-  if (g.K == 2048) {
-    static const int k16 = [] {
-      const char* e = getenv("ND_P16_K2048");  // 1: 16 K-slice waves of 128 (A/B timing); 0: 8 of 256
-      return e ? atoi(e) : 0;
-    }();
-    if (k16 == 1) return launch_p16<1, 16, 128>(g, s);
-    return launch_p16<1, 8, 256>(g, s);
-  }
+  // K = 2048 on 8 K-slice waves of 256 (16 waves of 128: pooled greedy 16.30 -> 16.63 ms, round 4, dropped)
+  if (g.K == 2048) return launch_p16<1, 8, 256>(g, s);
   if (g.K == 1024) return launch_p16<1, 8, 128>(g, s);
   if (g.K == 512) return launch_p16<1, 8, 64>(g, s);
   return hipErrorInvalidValue;

@@ -248,14 +248,8 @@ hipError_t launch_attn_rows_softmax(float* a, const int* span, int B, int S, int
 hipError_t launch_stamp_reset(unsigned long long* stamps, int pairs, hipStream_t s);
 // encoder output rows x[b*T+t] -> memory bank rows b*ldT+t, row-major (LN when
 // ln_g; rows t >= T of each chunk zero)
-// split-fp16 memory bank (mem_attention.hip): the fragment bank of
-// dec_bank_h3_kernel (T in (448, 512], bank buffers of >= 512 rows per chunk)
-bool bank_h3_eligible(int T, int ldT);
-hipError_t launch_bank_pack_h3(const float* x, const float* ln_g, const float* ln_b, uint16_t* out, int B, int T,
-                               int* ovf, hipStream_t s);
-hipError_t launch_dec_bank_h3(const float* qp, const uint16_t* bank, const float* signal, const int* span,
-                              float pad_val, float* out, int C, int T, hipStream_t s, unsigned long long* stamp,
-                              float* attn_dbg, size_t dbg_stride, int* ovf, bool nt = false, int grid = 0);
+// the 24-bit digit bank serves T in (448, 512] with bank buffers of >= 512 rows per chunk
+bool bank_eligible(int T, int ldT);
 hipError_t launch_memory_pack(const float* x, const float* ln_g, const float* ln_b, float* out, int B, int T, int ldT,
                               hipStream_t s);
 hipError_t init_mem_attributes();
@@ -267,11 +261,6 @@ hipError_t launch_dec_bank_d8(const float* qp, const void* bank, const float* ks
                               const float* signal, const int* span, float pad_val, float* out, int C, int T,
                               hipStream_t s, unsigned long long* stamp, float* attn_dbg, size_t dbg_stride, int* ovf,
                               bool nt = false, int grid = 0);
-// --fast beam rows on the same bank: rows c * rpc + j (rpc 2..6) of q' [C * rpc, 2048] P16 -> U P16;
-// chunks with done[c] != 0 skipped (done nullable)
-hipError_t launch_dec_bank_d8_beam(const float* qp, const void* bank, const float* kscale, const int* kemax,
-                                   const float* signal, const int* span, float pad_val, float* out, int C, int rpc,
-                                   int T, const int* done, hipStream_t s, unsigned long long* stamp, int* ovf);
 hipError_t init_bank8_attributes();
 // signal front end (frontend.hip): per-read normalisation (method 0 none, 1
 // median/MAD, 2 median/std; fp64 math, float32 out) of reads concatenated at

@@ -414,48 +414,23 @@ hipError_t launch_lstm_layer(const float* xp, const float* signal, const float* 
     return (e && atoi(e) != 0) || (g && atoi(g) != 0);
   }();
   const bool f32 = f32_env || exact;
-  static const bool fast = [] {
-    const char* e = getenv("ND_LSTM_LIBM");  // 1: libm expf / tanhf in the cell
-    return !(e && atoi(e) != 0);
-  }();
-  static const int ns_env = [] {
-    const char* e = getenv("ND_LSTM_SEQ");  // sequences per workgroup on the split-fp16 path: 16, 8 or 4
-    const int v = e ? atoi(e) : 4;  // measured: 0.95 ms per layer at 4, 1.04 at 8, 1.52 at 16
-    return v == 16 || v == 8 ? v : 4;
-  }();
-  const int ns = f32 ? 16 : ns_env;
+  // split-fp16: 4 sequences per workgroup (measured: 0.95 ms per layer at 4, 1.04 at 8, 1.52 at 16), the
+  // cell's sigmoid / tanh on the hardware exp and reciprocal; fp32 MFMAs: 16 sequences per workgroup
+  const int ns = f32 ? 16 : 4;
   dim3 grid((B + ns - 1) / ns, 2), block(ns == 4 ? 512 : 1024);
 #define ND_LSTM_GO(L0, H, F, S)                                                                                       \
   hipLaunchKernelGGL((lstm_dir_kernel<L0, H, F, S>), grid, block, 0, s, xp, signal, wih0, bsum, whh, len, B, T, out, \
                      bn_scale, bn_shift)
-#define ND_LSTM_NS(F, S)                \
-  do {                                  \
-    if (layer0)                         \
-      ND_LSTM_GO(true, true, F, S);     \
-    else                                \
-      ND_LSTM_GO(false, true, F, S);    \
-  } while (0)
-#define ND_LSTM_H3(F)                   \
-  do {                                  \
-    if (ns == 4)                        \
-      ND_LSTM_NS(F, 4);                 \
-    else if (ns == 8)                   \
-      ND_LSTM_NS(F, 8);                 \
-    else                                \
-      ND_LSTM_NS(F, 16);                \
-  } while (0)
   if (f32) {
     if (layer0)
       ND_LSTM_GO(true, false, false, 16);
     else
       ND_LSTM_GO(false, false, false, 16);
-  } else if (fast) {
-    ND_LSTM_H3(true);
+  } else if (layer0) {
+    ND_LSTM_GO(true, true, true, 4);
   } else {
-    ND_LSTM_H3(false);
+    ND_LSTM_GO(false, true, true, 4);
   }
-#undef ND_LSTM_NS
-#undef ND_LSTM_H3
 #undef ND_LSTM_GO
   return hipGetLastError();
 }

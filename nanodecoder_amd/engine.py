@@ -102,8 +102,8 @@ class Engine:
         self.bank_grid = int(workgroups)
 
     def bank_form(self) -> int:
-        """The memory bank the last call streamed (nd_bank_form): 0 fp32 (or none: a beam call on the
-        K/V form), 1 split-fp16, 2 24-bit digits (greedy, or beam rows with ND_BEAM_BANK=1)."""
+        """The memory bank the last call streamed (nd_bank_form): 0 fp32 (greedy in exact fp32, or a
+        beam call on fp32 K/V), 2 24-bit digits (greedy), 3 the 24-bit context K/V (beam)."""
         return int(self._L.nd_bank_form(self._h))
 
     def set_timing(self, on: bool):
@@ -674,28 +674,6 @@ def op_dec_mem_attention(qp, mem_p, signal, span, pad_val, rpc, out=None):
     return out
 
 
-def op_bank_pack_h3(x, B, T, ln_g=None, ln_b=None, ovf=None):
-    """Split-fp16 fragment bank (nd_op_bank_pack_h3): x [B*T, 256] -> uint16
-    [B * 512 * 512] (hi / lo planes of 512 rows per chunk)."""
-    out = torch.empty(B * 512 * 512, dtype=torch.int16, device=x.device)
-    s = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
-    _lib.check(_lib.lib().nd_op_bank_pack_h3(_ptr(x), _ptr(ln_g), _ptr(ln_b), _ptr(out), B, T, _ptr(ovf), s),
-               "nd_op_bank_pack_h3")
-    return out
-
-
-def op_dec_bank_h3(qp, bank, signal, span, pad_val, out=None, ovf=None, grid=0):
-    """Memory-bank context attention on the split-fp16 bank (nd_op_dec_bank_h3):
-    qp [C, 2048] row-major, T in (448, 512]; returns U [C16, 2048] packed."""
-    C, T = signal.shape
-    if out is None:
-        out = torch.empty((C + 15) // 16 * 16, qp.shape[1], dtype=torch.float32, device=qp.device)
-    s = ctypes.c_void_p(torch.cuda.current_stream(qp.device).cuda_stream)
-    _lib.check(_lib.lib().nd_op_dec_bank_h3(_ptr(qp), _ptr(bank), _ptr(signal), _ptr(span), float(pad_val),
-                                            _ptr(out), C, T, _ptr(ovf), int(grid), s), "nd_op_dec_bank_h3")
-    return out
-
-
 def op_bank_pack_d8(x, B, T, ln_g=None, ln_b=None, ovf=None, span=None):
     """24-bit digit bank (nd_op_bank_pack_d8): x [B*T, 256] -> (digits uint8
     [B * 512 * 256 * 3], row scales [B * 512], each chunk's largest row scale
@@ -723,22 +701,6 @@ def op_dec_bank_d8(qp, bank, signal, span, pad_val, out=None, ovf=None, grid=0):
     _lib.check(_lib.lib().nd_op_dec_bank_d8(_ptr(qp), _ptr(digits), _ptr(ks), _ptr(em), _ptr(signal), _ptr(span),
                                             float(pad_val), _ptr(out), C, T, _ptr(ovf), int(grid), s),
                "nd_op_dec_bank_d8")
-    return out
-
-
-def op_dec_bank_d8_beam(qp, bank, signal, span, pad_val, rpc, out=None, done=None, ovf=None):
-    """Beam rows on the 24-bit digit bank (nd_op_dec_bank_d8_beam): qp [C*rpc, 2048]
-    in the P16 layout (pack_p16), rows c*rpc + j of chunk c; returns U [R16, 2048] packed."""
-    C, T = signal.shape
-    digits, ks, em = bank
-    R = C * rpc
-    if out is None:
-        out = torch.zeros((R + 15) // 16 * 16, qp.shape[1], dtype=torch.float32, device=qp.device)
-    s = ctypes.c_void_p(torch.cuda.current_stream(qp.device).cuda_stream)
-    _lib.check(_lib.lib().nd_op_dec_bank_d8_beam(_ptr(qp), _ptr(digits), _ptr(ks), _ptr(em), _ptr(signal),
-                                                 _ptr(span), float(pad_val), _ptr(out), C, int(rpc), T, _ptr(done),
-                                                 _ptr(ovf), s),
-               "nd_op_dec_bank_d8_beam")
     return out
 
 

@@ -96,16 +96,17 @@ def test_hot_path_kernels_do_not_drain_loads(tmp_path):
         return out.read_text()
 
     with cf.ThreadPoolExecutor(4) as ex:
-        src = dict(zip(["attention", "mem_attention", "search", "gemm"],
-                       ex.map(asm, ["attention", "mem_attention", "search", "gemm"])))
+        src = dict(zip(["attention", "bank8", "search", "gemm"],
+                       ex.map(asm, ["attention", "bank8", "search", "gemm"])))
     want = [("attention", r"dec_self_attention_kernelILi\d+ELi\d+ELb0ELb0E", 0),  # no beam ancestry
             # the form that runs the previous step's head: wave 0 waits for the
             # head's own loads, then issues its cache loads (the one allowed)
             ("attention", r"dec_self_attention_kernelILi\d+ELi\d+ELb0ELb1E", 1),
-            ("mem_attention", r"dec_bank_h3_kernelILb\dELb0E", 0),  # one chunk per workgroup
-            # the walking form (pool lanes): the loop's load schedule drains the
-            # first half blocks once per chunk
-            ("mem_attention", r"dec_bank_h3_kernelILb\dELb1E", 2),
+            # the 24-bit digit bank: the walking form (pool lanes) issues straight-line;
+            # the one-chunk form's two sit in the unrolled key loop: the wait for the last fragment of the
+            # half block being multiplied, right before the next half block's loads (reviewed, round 5)
+            ("bank8", r"dec_bank_d8_kernelILb\dELb1E", 0),
+            ("bank8", r"dec_bank_d8_kernelILb\dELb0E", 2),
             # the standalone head (the last step only when the head is fused):
             # the V > 8 generator loop's loads follow the first 8 rows' wait
             ("search", r"greedy_head_kernel", 1),
@@ -131,7 +132,6 @@ def test_hot_path_kernels_do_not_drain_loads(tmp_path):
 # paired accesses in a listed one, fails until it is reviewed again.
 DYNAMIC_LDS = {  # kernels launched with dynamic LDS (metadata says 0): bytes at the launch site
     "dec_bank_d8_kernel": 138064,        # bank8.hip B8_LDS
-    "dec_bank_h3_kernel": 139904,        # mem_attention.hip BH_LDS
     "dec_mem_attention_kernel": 158208,  # mem_lds_bytes()
     "dec_ctx_attention_kernel": 52224,   # ctx_lds_bytes(6) (the attribute allows 160 KB; launches take this)
     "gemm_p16s_kernel": 98304,           # 2x4 tiles
@@ -148,7 +148,6 @@ REVIEWED_PAIRED = {
                                      "form); launched with at most 52 KB, listed in case that grows"),
     "dec_bank_d8_kernel": (3, "the (m, l) merge and the q' digit rows (cross-wave, after a barrier); "
                               "pool-tested at the bench's configuration"),
-    "dec_bank_h3_kernel": (2, "the (m, l) merge, as dec_bank_d8_kernel"),
     "dec_mem_attention_kernel": (25, "the fp32 bank kernel (exact fp32 / short chunks): slab reads after "
                                      "barriers"),
 }

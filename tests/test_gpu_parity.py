@@ -302,65 +302,18 @@ def test_mem_attention_vs_fp64(T):
 
 @pytest.mark.parametrize("T,ln,grid", [(512, True, 0), (480, False, 0), (449, True, 0), (512, True, 5),
                                        (512, False, 1)])
-def test_bank_h3_vs_fp64(T, ln, grid):
-    """Split-fp16 memory-bank attention (bank_pack_h3 + dec_bank_h3_kernel, the
-    greedy path at 512-sample chunks) against an fp64 softmax(q' M^T) M per
-    head: ragged spans (key-block / wave boundaries, single key, waves owning
-    no key), pad-masked keys, an all-masked chunk, a peaked chunk whose scores
-    climb past the lazy-rescale threshold, with and without the LayerNorm.
-    grid > 0: that many workgroups walk the 12 chunks (nd_set_bank_grid's
-    form; 5 leaves a ragged last round)."""
-    from nanodecoder_amd.engine import op_bank_pack_h3, op_dec_bank_h3, pack_p16, unpack_p16
-    rng = np.random.default_rng(7)
-    C, PAD = 12, 1.0
-    spans = np.array([T, 1, 64, 65, 16, 17, 8, T, T - 3, 130, 300, T], np.int32)
-    sig = rng.standard_normal((C, T)).astype(np.float32)
-    sig[2, ::5] = PAD                      # pad-masked keys
-    sig[7, :] = PAD                        # every key masked -> uniform over the span
-    x = rng.standard_normal((C * T, 256)).astype(np.float32)
-    q = (rng.standard_normal((C, 2048)) * 0.3).astype(np.float32)
-    q[11] *= 8.0                           # scores spread ~+-50: running-maximum rescales
-    x[11 * T + 400] *= 4.0                 # a late key far above the first blocks' maximum
-    g = (rng.random(256) + 0.5).astype(np.float32)
-    b = (rng.standard_normal(256) * 0.1).astype(np.float32)
-    dev = torch.device("cuda", 0)
-    xt = torch.from_numpy(x).to(dev)
-    ovf = torch.zeros(1, dtype=torch.int32, device=dev)
-    if ln:
-        bank = op_bank_pack_h3(xt, C, T, torch.from_numpy(g).to(dev), torch.from_numpy(b).to(dev), ovf=ovf)
-        mu = x.mean(1, keepdims=True)
-        var = ((x - mu) ** 2).mean(1, keepdims=True)
-        xm = ((x - mu) / np.sqrt(var + 1e-6) * g + b).astype(np.float64)
-    else:
-        bank = op_bank_pack_h3(xt, C, T, ovf=ovf)
-        xm = x.astype(np.float64)
-    out = op_dec_bank_h3(torch.from_numpy(q).to(dev), bank, torch.from_numpy(sig).to(dev),  # q' row-major
-                         torch.from_numpy(spans).to(dev), PAD, ovf=ovf, grid=grid)
-    got = unpack_p16(out, C).cpu().numpy()
-    assert int(ovf.item()) == 0
-    for c in range(C):
-        L = int(spans[c])
-        M = xm[c * T: c * T + L]
-        for h in range(8):
-            s = M @ q[c, h * 256:(h + 1) * 256].astype(np.float64)
-            s[sig[c, :L] == PAD] = -1e18
-            p = np.exp(s - s.max())
-            want = (p / p.sum()) @ M
-            err = np.abs(got[c, h * 256:(h + 1) * 256] - want).max()
-            assert err < 2e-5 * max(1.0, np.abs(want).max()), (c, h, L, err)
-
-
-@pytest.mark.parametrize("T,ln,grid", [(512, True, 0), (480, False, 0), (449, True, 0), (512, True, 5),
-                                       (512, False, 1)])
 def test_bank_d8_vs_fp64(T, ln, grid):
     """24-bit digit-bank attention (bank_pack_d8 + dec_bank_d8_kernel, the
     greedy path at 512-sample chunks) against an fp64 softmax(q' M^T) M per
-    head, on the cases of test_bank_h3_vs_fp64 (ragged spans, pad-masked keys,
-    an all-masked chunk, running-maximum rescales) plus rows of very
+    head: ragged spans (key-block / wave boundaries, single key, waves owning
+    no key), pad-masked keys, an all-masked chunk, a peaked chunk whose scores
+    climb past the lazy-rescale threshold, with and without the LayerNorm
+    (grid > 0: that many workgroups walk the 12 chunks, nd_set_bank_grid's
+    form; 5 leaves a ragged last round), plus rows of very
     different magnitude (per-row exponents 2^e_t far below the chunk's
     largest) and a head of q' a thousand times the others (per-head digit
-    scales).  Tolerance: 2e-5 relative to the output's magnitude, as the
-    split-fp16 bank (digits carry 22-23 bits per row)."""
+    scales).  Tolerance: 2e-5 relative to the output's magnitude (digits
+    carry 22-23 bits per row)."""
     from nanodecoder_amd.engine import op_bank_pack_d8, op_dec_bank_d8, unpack_p16
     rng = np.random.default_rng(7)
     C, PAD = 12, 1.0
@@ -405,66 +358,6 @@ def test_bank_d8_vs_fp64(T, ln, grid):
             want = (p / p.sum()) @ M
             err = np.abs(got[c, h * 256:(h + 1) * 256] - want).max()
             assert err < 2e-5 * max(1.0, np.abs(want).max()), (c, h, L, err)
-
-
-@pytest.mark.parametrize("rpc", [2, 5, 6])
-def test_bank_d8_beam_vs_fp64(rpc):
-    """Beam rows on the digit bank (dec_bank_d8_beam_kernel: the rpc rows of a
-    chunk share one pass over its bank) against fp64 softmax(q' M^T) M per row
-    and head: ragged spans (1, 15, 16, 17, a partial last key block), pad-masked
-    keys, an all-masked chunk, running-maximum rescales in some rows only, a
-    head a thousand times the others, a zero row of q', and finished chunks
-    (done != 0: their rows untouched).  Tolerance as the greedy digit bank."""
-    from nanodecoder_amd.engine import op_bank_pack_d8, op_dec_bank_d8_beam, pack_p16, unpack_p16
-    rng = np.random.default_rng(17 + rpc)
-    C, T, PAD = 10, 512, 1.0
-    spans = np.array([T, 1, 15, 16, 17, 300, T, T - 3, 200, T], np.int32)
-    sig = rng.standard_normal((C, T)).astype(np.float32)
-    sig[3, ::4] = PAD
-    sig[6, :] = PAD
-    x = rng.standard_normal((C * T, 256)).astype(np.float32)
-    x[9 * T + 450] *= 5.0                      # a late key far above the first blocks' maximum
-    x[5 * T: 6 * T: 2] *= 1e-3
-    x[4 * T + 17:5 * T] = 1e30                 # rows past a span (never attended; the encoder leaves them
-    x[8 * T + 200:9 * T] = np.nan              # unspecified) must not set the chunk's scale or trip ovf
-    R = C * rpc
-    q = (rng.standard_normal((R, 2048)) * 0.3).astype(np.float32)
-    q[9 * rpc] *= 8.0                          # this row rescales; its chunk's other rows less so
-    q[2 * rpc + 1, 2 * 256:3 * 256] *= 1e3
-    q[7 * rpc + rpc - 1] = 0.0                 # a zero row: uniform weights
-    done = np.zeros(C, np.int32)
-    done[8] = 1
-    g = (rng.random(256) + 0.5).astype(np.float32)
-    b = (rng.standard_normal(256) * 0.1).astype(np.float32)
-    dev = torch.device("cuda", 0)
-    ovf = torch.zeros(1, dtype=torch.int32, device=dev)
-    bank = op_bank_pack_d8(torch.from_numpy(x).to(dev), C, T, torch.from_numpy(g).to(dev),
-                           torch.from_numpy(b).to(dev), ovf=ovf, span=torch.from_numpy(spans).to(dev))
-    qp = pack_p16(torch.from_numpy(q).to(dev))
-    out = op_dec_bank_d8_beam(qp, bank, torch.from_numpy(sig).to(dev), torch.from_numpy(spans).to(dev), PAD, rpc,
-                              done=torch.from_numpy(done).to(dev), ovf=ovf)
-    torch.cuda.synchronize()
-    got = unpack_p16(out, R).cpu().numpy()
-    assert int(ovf.item()) == 0
-    with np.errstate(invalid="ignore", over="ignore"):
-        mu = x.mean(1, keepdims=True)
-        var = ((x - mu) ** 2).mean(1, keepdims=True)
-        xm = ((x - mu) / np.sqrt(var + 1e-6) * g + b).astype(np.float64)
-    for c in range(C):
-        L = int(spans[c])
-        M = xm[c * T: c * T + L]
-        for j in range(rpc):
-            r = c * rpc + j
-            if done[c]:
-                assert not got[r].any(), (c, j)
-                continue
-            for h in range(8):
-                s = M @ q[r, h * 256:(h + 1) * 256].astype(np.float64)
-                s[sig[c, :L] == PAD] = -1e18
-                p = np.exp(s - s.max())
-                want = (p / p.sum()) @ M
-                err = np.abs(got[r, h * 256:(h + 1) * 256] - want).max()
-                assert err < 2e-5 * max(1.0, np.abs(want).max()), (c, j, h, L, err)
 
 
 def test_ctx_pack_q24_bitexact():
@@ -654,8 +547,7 @@ def test_ctx_attention_tail_list_split(rpc, nsplit, q24):
 
 def test_engine_reports_bank_form():
     """A greedy call at 512-sample chunks streams the 24-bit digit bank by
-    default (nd_bank_form 2; ND_BANK_D8=0: the split-fp16 bank, 1), exact
-    fp32 the fp32 bank (0).  The digit bank's end-to-end parity is the golden
+    default (nd_bank_form 2), exact fp32 the fp32 bank (0).  The digit bank's end-to-end parity is the golden
     and config tests, which run on it."""
     cfg = synth.ModelConfig()
     W = synth.make_weights(cfg, seed=11, eos_bias=-3.0)
@@ -663,7 +555,7 @@ def test_engine_reports_bank_form():
     lens = np.full(8, 512, np.int32)
     eng = _engine(cfg, W, max_batch=8, max_steps=20, max_beam=3)
     eng.translate_greedy(sig, lens, lens, max_len=20)
-    assert eng.bank_form() == (1 if os.environ.get("ND_BANK_D8") == "0" else 2)
+    assert eng.bank_form() == 2
     eng.set_exact_fp32(True)
     eng.translate_greedy(sig, lens, lens, max_len=20)
     assert eng.bank_form() == 0
@@ -672,8 +564,7 @@ def test_engine_reports_bank_form():
     assert eng.bank_form() == 0
     eng.set_exact_fp32(False)
     eng.translate_beam(sig, lens, lens, beam=3, max_len=20)
-    want = 2 if os.environ.get("ND_BEAM_BANK") == "1" else 0 if os.environ.get("ND_CTX_Q24") == "0" else 3
-    assert eng.bank_form() == want
+    assert eng.bank_form() == 3
     eng.close()
 
 
@@ -1077,7 +968,7 @@ def test_split_fp16_range_guard(where):
 
 def test_beam_large_batch_vs_oracle():
     """--fast beam 5 on 416 chunks (2080 decoder rows: the LDS-tiled
-    split-fp16 GEMMs of ND_P16_BIG_MIN's large-M path, as configs[3]'s
+    split-fp16 GEMMs of the large-M path (from 2048 rows), as configs[3]'s
     B = 1024 runs) against the oracle on a sample of the chunks.  Every
     chunk is a full 512-sample window, so its padded length (and result) does
     not depend on the rest of its batch: the sample runs as its own batch."""
@@ -1296,8 +1187,8 @@ def test_nano_lstm_layer_vs_torch_lstm(layer0, bn):
     """One BiLSTM layer through nd_op_lstm_layer against torch.nn.LSTM (CPU,
     fp32) over packed ragged sequences (encoder/nano_encoder.py:92-111: pack,
     bidirectional LSTM, unpack with zeros past each length, eval BatchNorm).
-    B = 6 leaves a partly filled last workgroup at every sequences-per-
-    workgroup setting (ND_LSTM_SEQ 16 / 8 / 4).  Tolerance 1e-4 absolute:
+    B = 6 leaves a partly filled last workgroup (4 sequences per workgroup
+    on the split-fp16 path, 16 on the fp32 one).  Tolerance 1e-4 absolute:
     split-fp16 recurrent products (22-bit operands) and the hardware exp /
     reciprocal in the cell, over 48 steps."""
     from torch.nn.utils.rnn import pack_padded_sequence, pad_packed_sequence
