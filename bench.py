@@ -250,6 +250,16 @@ def _mfma_counters(which):
             "top_kernels": {n: {x: v[x] for x in ("avg_us", "f16_tflops", "f32_tflops", "mfma_util")} for n, v in top}}
 
 
+def dtype_of(form: int) -> str:
+    """The arithmetic a call ran in, from the engine's nd_bank_form (each leg states its own)."""
+    base = "f32 (fp32 values; products as split-fp16 x3 on fp16 MFMA: 22-bit operands, fp32 accumulate"
+    if form == 2:
+        return base + "; the greedy memory bank as 24-bit fixed point per key row: int8 digit MFMAs summed exactly in int32)"
+    if form == 3:
+        return base + "; the beam's context K/V as 24-bit integers with a power-of-two scale per (key, head))"
+    return base + ")"
+
+
 def count_bases(tok: np.ndarray, eos: int) -> int:
     """Base tokens (ids >= 4: not <unk>/<blank>/<s>/</s>) before the first EOS."""
     is_eos = tok == eos
@@ -303,10 +313,22 @@ def kernel_roofline(eng, B, mode, beam, encoder="transformer", alive=None, secon
         nbytes = B * per_chunk
         extra = {}
         if alive is not None and n > 0:
-            # mean bytes of a stamped launch (3 layers per step with >= 1 alive chunk)
-            nbytes = int(3 * sum(alive) * per_chunk / n)
+            # mean bytes of a stamped launch (3 layers per step with >= 1 alive chunk); a pool's stamps are
+            # every lane's last call, each the same workload
+            lanes = len(eng.engines) if hasattr(eng, "engines") else 1
+            nbytes = int(3 * sum(alive) * per_chunk * lanes / n)
             extra = {"alive_chunks_per_launch": round(3 * sum(alive) / n, 1)}
     ach = nbytes / (ms * 1e-3) / 1e9
+    if mode == "greedy" and form == 2:
+        # SURVEY.md §8(d) prices the context attention as fp32 K and V per layer (1,048,576 B per chunk per
+        # layer-step); this kernel moves neither: the K / V projections are folded into the query and output
+        # sides (all three layers read the one LN'd encoder output: x 0.5) and that bank is 24-bit (x 0.75)
+        s8d = B * 2 * T * D * 4
+        extra["survey_8d_byte_model"] = {
+            "bytes_per_launch": s8d, "equivalent_rate_gbs": round(s8d / (ms * 1e-3) / 1e9, 1),
+            "note": ("fp32 K+V per chunk per layer-step (SURVEY §8d); the kernel streams a folded bank (x 0.5: "
+                     "W_k folded into q', W_v into the output projection) in 24 bits (x 0.75) = 0.375 of these "
+                     "bytes, so this equivalent rate is not a fraction of the HBM peak")}
     out = {"bound": "hbm", "kernel": name, "achieved": round(ach, 1), "peak": HBM_PEAK, "unit": "GB/s",
            "frac": round(ach / HBM_PEAK, 4), "traffic": _pmc(name, "kernels" if mode == "greedy" else "kernels_beam"),
            "algorithmic_bytes_per_launch": nbytes,
@@ -397,7 +419,9 @@ def lstm_view(dev, B, T):
 def mfma_view(args, eng, sig, lens, ms_per_step):
     """Algorithmic MFMA utilisation (SURVEY §8d FLOP counts) of the whole
     path and of the encoder alone (nd_encode timed by itself), against the
-    fp32 MFMA peak and the split-fp16 fp32-equivalent peak."""
+    peak of the pipe the products run on: the fp16 matrix pipe, three fp16
+    products per fp32 multiply-add (split-fp16), i.e. dense fp16 peak / 3.
+    The exact-fp32 leg carries its own roofline against the fp32 MFMA peak."""
     B = args.batch
     enc_flop = ENC_FLOP_PER_CHUNK if args.encoder == "transformer" else NANO_ENC_FLOP_PER_CHUNK
     path_flop = (enc_flop + DEC_FLOP_PER_CHUNK) * B
@@ -410,13 +434,12 @@ def mfma_view(args, eng, sig, lens, ms_per_step):
     path_tf = path_flop / (ms_per_step * 1e-3) / 1e12
     enc_tf = enc_flop * B / (enc_ms * 1e-3) / 1e12
     out = {"algorithmic_flop_per_chunk": enc_flop + DEC_FLOP_PER_CHUNK,
-           "path": {"tflops": round(path_tf, 2), "frac_fp32_peak": round(path_tf / FP32_PEAK, 4),
-                    "frac_split_peak": round(path_tf / SPLIT_PEAK, 4)},
+           "path": {"tflops": round(path_tf, 2), "frac_split_peak": round(path_tf / SPLIT_PEAK, 4)},
            "encoder_only": {"ms": round(enc_ms, 4), "tflops": round(enc_tf, 2),
-                            "frac_fp32_peak": round(enc_tf / FP32_PEAK, 4),
                             "frac_split_peak": round(enc_tf / SPLIT_PEAK, 4),
-                            "note": "nd_encode incl. its memory-bank LayerNorm copy"},
-           "peaks": {"fp32": FP32_PEAK, "split_fp16_fp32_equiv": round(SPLIT_PEAK, 1), "unit": "TFLOP/s"}}
+                            "note": "nd_encode incl. its memory-bank pack"},
+           "peak": {"split_fp16_fp32_equiv": round(SPLIT_PEAK, 1), "unit": "TFLOP/s",
+                    "note": "fp32-equivalent work on the fp16 matrix pipe: dense fp16 peak 2516.6 / 3 products"}}
     cnt = _mfma_counters("nano" if args.encoder == "nano" else "greedy")
     if cnt is not None:
         out["rocprof_counters"] = cnt
@@ -533,6 +556,39 @@ def timed(pool, n, call, world, every_lane=False):
     return dt, out
 
 
+def beam_steps_and_worst_case(args, pool, sig, lens, call, out, world, res):
+    """--fast beam legs: the decoder steps executed, the steps each chunk ran
+    (the reference drops a finished chunk's batch at that step,
+    translate/translator.py:793-823), and the forced-100-step worst case (EOS
+    masked at every step: -min_length = max_length), into ``res``; returns
+    the alive-chunk count per step for the roofline's byte count.  Leaves the
+    timed workload's graphs replayed last (the kernel stamps read after come
+    from those)."""
+    e0 = pool.engines[0]
+    res["decoder_steps_executed"] = int(out["steps"].cpu().item())
+    rr = e0.translate_beam(sig, lens, lens, beam=args.beam, max_len=args.max_length, min_len=args.min_length,
+                           return_attn=True)
+    done = rr["done_step"].cpu().numpy()
+    alive = [int((done > s_).sum()) for s_ in range(res["decoder_steps_executed"])]
+    B = int(sig.shape[0])
+    res["chunk_steps"] = {"executed_share": round(sum(alive) / (B * len(alive)), 4),
+                          "done_step_percentiles_0_50_99_100": np.percentile(done, [0, 50, 99, 100]).tolist(),
+                          "note": "finished chunks' attention workgroups and GEMM row tiles exit at once"}
+    del rr
+    n_wc = max(3, min(10, args.steps // 10))
+    wcall = make_call(args, "beam", sig, lens, min_len=args.max_length)
+    run_calls(pool, pool.lanes, wcall)
+    wc, _ = timed(pool, n_wc, wcall, world)
+    wc /= n_wc
+    res["worst_case_all_steps"] = {"ms_per_step": round(wc * 1e3, 3),
+                                   "samples_per_sec_per_gpu": round(float(B * 512) / wc, 1),
+                                   "note": f"min_length {args.max_length}: no chunk finishes before step "
+                                           f"{args.max_length}, {n_wc} calls, {pool.lanes} in flight"}
+    run_calls(pool, pool.lanes, call)
+    torch.cuda.synchronize()
+    return alive
+
+
 def run_batch(args, world, rank, dev, cfg, W):
     from nanodecoder_amd import synth
     from nanodecoder_amd.engine import EnginePool
@@ -563,9 +619,7 @@ def run_batch(args, world, rank, dev, cfg, W):
         "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None,
-        "dtype": ("f32 (fp32 values; products as split-fp16 x3 on fp16 MFMA: 22-bit operands, fp32 accumulate; "
-                  "the greedy memory bank as 24-bit fixed point per key row: int8 digit MFMAs summed exactly in "
-                  "int32)"),
+        "dtype": dtype_of(eng.engines[0].bank_form()),
         "data": "synthetic reads, random-init weights",
         "config": {"workload": workload(args), "chunks_per_gpu_per_step": args.batch,
                    "global_batch": args.batch * world, "seq_len": 512, "parallelism": f"read-shard x{world}",
@@ -604,30 +658,7 @@ def run_batch(args, world, rank, dev, cfg, W):
         eng.engines[0].set_bank_grid(eng.bank_grid)
     alive = None
     if args.mode == "beam":
-        e0 = eng.engines[0]
-        res["decoder_steps_executed"] = int(out["steps"].cpu().item())
-        # the steps each chunk ran (the reference drops a finished chunk's batch
-        # at that step, translate/translator.py:793-823); same inputs, same search
-        rr = e0.translate_beam(sig, lens, lens, beam=args.beam, max_len=args.max_length, min_len=args.min_length,
-                               return_attn=True)
-        done = rr["done_step"].cpu().numpy()
-        alive = [int((done > s_).sum()) for s_ in range(res["decoder_steps_executed"])]
-        res["chunk_steps"] = {"executed_share": round(sum(alive) / (args.batch * len(alive)), 4),
-                              "done_step_percentiles_0_50_99_100": np.percentile(done, [0, 50, 99, 100]).tolist(),
-                              "note": "finished chunks' attention workgroups and GEMM row tiles exit at once"}
-        del rr
-        # the forced-100-step worst case: EOS masked at every step (-min_length = max_length)
-        n_wc = max(2, min(10, args.steps // 10))
-        wcall = make_call(args, "beam", sig, lens, min_len=args.max_length)
-        run_calls(eng, eng.lanes, wcall)
-        wc, _ = timed(eng, n_wc, wcall, world)
-        wc /= n_wc
-        res["worst_case_all_steps"] = {"ms_per_step": round(wc * 1e3, 3),
-                                       "samples_per_sec_per_gpu": round(float(lens_np.sum()) / wc, 1),
-                                       "note": f"min_length {args.max_length}: no chunk finishes before step "
-                                               f"{args.max_length}, {n_wc} calls"}
-        run_calls(eng, eng.lanes, call)  # the timed workload's graphs again (kernel stamps below come from these)
-        torch.cuda.synchronize()
+        alive = beam_steps_and_worst_case(args, eng, sig, lens, call, out, world, res)
     extras = {}
     if rank == 0:
         if roof_iso is not None:
@@ -648,8 +679,18 @@ def run_batch(args, world, rank, dev, cfg, W):
         extras["exact_fp32"] = {"value_per_gpu": round(float(lens_np.sum()) * n_ex / dte, 1), "unit": "samples/s",
                                 "ms_per_step": round(dte / n_ex * 1e3, 3), "steps": n_ex,
                                 "note": "every GEMM, the encoder attention and the BiLSTM on fp32 MFMAs"}
+        if args.mode == "greedy":
+            enc_flop = ENC_FLOP_PER_CHUNK if args.encoder == "transformer" else NANO_ENC_FLOP_PER_CHUNK
+            etf = (enc_flop + DEC_FLOP_PER_CHUNK) * args.batch / (dte / n_ex) / 1e12
+            extras["exact_fp32"]["roofline"] = {
+                "bound": "mfma", "achieved": round(etf, 2), "peak": FP32_PEAK, "unit": "TFLOP/s",
+                "frac": round(etf / FP32_PEAK, 4),
+                "note": "path-level algorithmic FLOPs (SURVEY §8d) per call over the call time, against the dense "
+                        "fp32 MFMA peak (the pipe this leg runs on)"}
     if args.host_inclusive and args.mode == "greedy":
         extras["host_inclusive"] = host_inclusive(args, cfg, eng, sig_np, lens_np)
+        extras["host_inclusive"]["ratio_to_value"] = round(extras["host_inclusive"]["value_per_gpu"] /
+                                                           (value / world), 4)
     res.update(extras)
     return res, eng, sig_np, lens_np
 
@@ -671,6 +712,7 @@ def config_legs(args, world, rank, dev):
         sig = torch.from_numpy(synth.synth_chunk_batch(B, 512, seed=2000 + rank, inject_masks=False)).to(dev)
         lens = torch.full((B,), 512, dtype=torch.int32, device=dev)
         call = make_call(args, mode, sig, lens)
+        pool.set_kernel_stamps(mode == "beam" and not args.no_roofline)
         run_calls(pool, max(2, pool.lanes), call)
         dt, outs = timed(pool, n, call, world, every_lane=True)
         out = outs[(n - 1) % pool.lanes]
@@ -683,10 +725,18 @@ def config_legs(args, world, rank, dev):
                      "value": round(B * 512 * n * world / dt, 1), "unit": "samples/s", "n_gpus": world,
                      "samples_per_sec_per_gpu": round(B * 512 * n / dt, 1),
                      "bases_per_sec": round(count_bases(tok, cfg.eos_idx) * n * world / dt, 1),
-                     "ms_per_step": round(dt / n * 1e3, 3), "steps": n, "calls_in_flight_per_gpu": pool.lanes}
-        if mode == "beam":
-            legs[key]["decoder_steps_executed"] = int(out["steps"].cpu().item())
+                     "ms_per_step": round(dt / n * 1e3, 3), "steps": n, "calls_in_flight_per_gpu": pool.lanes,
+                     "dtype": dtype_of(pool.engines[0].bank_form())}
         legs[key]["pool_check"] = pool_check(cfg, W, args, mode, B, beam, call, outs)
+        if mode == "beam":
+            bargs = argparse.Namespace(**vars(args))
+            bargs.steps = n
+            alive = beam_steps_and_worst_case(bargs, pool, sig, lens, call, out, world, legs[key])
+            if rank == 0 and not args.no_roofline:
+                legs[key]["roofline"] = kernel_roofline(pool, B, "beam", beam, "transformer", alive)
+                legs[key]["roofline"]["timing"] = ("in-kernel wall-clock stamps, launches of the last call of "
+                                                   "the leg's workload (other lanes' calls beside it)")
+            pool.set_kernel_stamps(False)
         pool.close()
         del pool, sig, lens
         torch.cuda.empty_cache()
@@ -703,7 +753,9 @@ def host_inclusive(args, cfg, eng, sig_np, lens_np):
                                 min_length=args.min_length, beam_size=1, batch_size=args.batch,
                                 engine_max_batch=args.batch)
     tr = Translator(cfg, None, opt, engine=eng)
-    n = max(4, min(40, args.steps // 4))
+    # 40 batches whatever --steps is: with 3 calls in flight the first call's latency is paid once, and
+    # at 5 batches (the driver's --steps 20 / 4) that fill alone is ~7 % of the leg
+    n = 40
     # each "read" is one chunk here: batches are exactly the timed batch
     reads = [[sig_np[i % args.batch]] for i in range(args.batch * n)]
     list(tr.stream_reads(reads[: 2 * args.batch], batch_size=1))
@@ -805,7 +857,7 @@ def main():
         res = {"metric": METRIC, "value": rs["value"], "unit": "samples/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup,
                "ms_per_step": None, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-               "dtype": "f32 (fp32 values; products as split-fp16 x3 on fp16 MFMA)",
+               "dtype": dtype_of(2),
                "data": "synthetic reads, random-init weights",
                "config": {"workload": workload(args), "seq_len": 512, "parallelism": f"read-shard x{world}"},
                "read_shard": rs}
