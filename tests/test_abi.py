@@ -57,47 +57,49 @@ def test_code_object_targets_gfx950(lib):
     assert b"amdgcn-amd-amdhsa--gfx950" in blob
 
 
-def test_inline_asm_lds_ring_has_no_hazard(tmp_path):
+@pytest.fixture(scope="module")
+def listings(tmp_path_factory):
+    """hipcc -S (gfx950, the library's flags) of every csrc/*.hip, compiled once for this module."""
+    import concurrent.futures as cf
+    import glob
+    import subprocess
+    from nanodecoder_amd import build
+    if not os.path.exists(build.HIPCC):
+        pytest.skip("no hipcc")
+    tmp = tmp_path_factory.mktemp("asm")
+    names = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(build.CSRC, "*.hip")))
+
+    def asm(name):
+        out = tmp / (name + ".s")
+        subprocess.run([build.HIPCC] + build.CFLAGS + ["--cuda-device-only", "-S", os.path.join(build.CSRC, name + ".hip"),
+                        "-o", str(out)], check=True, capture_output=True)
+        return str(out)
+
+    with cf.ThreadPoolExecutor(8) as ex:
+        return dict(zip(names, ex.map(asm, names)))
+
+
+def test_inline_asm_lds_ring_has_no_hazard(listings):
     """ffn.hip's inline-asm LDS read ring: in the compiled gfx950 code no
     instruction touches a ring destination register between its ds_read and
     the s_waitcnt that retires it (tools/lds_ring_check.py)."""
     import subprocess
     import sys
-    from nanodecoder_amd import build
-    if not os.path.exists(build.HIPCC):
-        pytest.skip("no hipcc")
-    out = tmp_path / "ffn.s"
-    subprocess.run([build.HIPCC] + build.CFLAGS + ["--cuda-device-only", "-S", os.path.join(build.CSRC, "ffn.hip"),
-                    "-o", str(out)], check=True, capture_output=True)
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "lds_ring_check.py"), str(out), "enc_ffn"],
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "lds_ring_check.py"), listings["ffn"], "enc_ffn"],
                        capture_output=True, text=True)
     assert r.returncode == 0 and "0 hazards" in r.stdout, r.stdout + r.stderr
 
 
-def test_hot_path_kernels_do_not_drain_loads(tmp_path):
+def test_hot_path_kernels_do_not_drain_loads(listings):
     """The greedy decoder's kernels issue their loads straight-line: no
     `s_waitcnt vmcnt(0)` followed by more loads (hipcc's lowering of a load
     under a runtime condition drains every load in flight; DESIGN.md §3,
     "Straight-line loads").  The P16 GEMMs keep one: the `--fast` beam's
     finished-chunk probe (rows_dead), which runs only with a skip list."""
-    import concurrent.futures as cf
-    import subprocess
     import sys
-    from nanodecoder_amd import build
-    if not os.path.exists(build.HIPCC):
-        pytest.skip("no hipcc")
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     from isa_loops import drains
-
-    def asm(name):
-        out = tmp_path / (name + ".s")
-        subprocess.run([build.HIPCC] + build.CFLAGS + ["--cuda-device-only", "-S", os.path.join(build.CSRC, name + ".hip"),
-                        "-o", str(out)], check=True, capture_output=True)
-        return out.read_text()
-
-    with cf.ThreadPoolExecutor(4) as ex:
-        src = dict(zip(["attention", "bank8", "search", "gemm"],
-                       ex.map(asm, ["attention", "bank8", "search", "gemm"])))
+    src = {k: open(v).read() for k, v in listings.items() if k in ("attention", "bank8", "search", "gemm")}
     want = [("attention", r"dec_self_attention_kernelILi\d+ELi\d+ELb0ELb0E", 0),  # no beam ancestry
             # the form that runs the previous step's head: wave 0 waits for the
             # head's own loads, then issues its cache loads (the one allowed)
@@ -119,6 +121,62 @@ def test_hot_path_kernels_do_not_drain_loads(tmp_path):
         assert found, rx
         bad = {k: v for k, v in found.items() if v > most}
         assert not bad, bad
+
+
+# ----------------------------------------------------------------- MFMA wait states
+# DESIGN.md section 3 "MFMA results and wait states" (round 5): round 4's beam
+# digit-bank kernel returned wrong components 0-1 of an accumulator when a
+# branch around its rescale made hipcc copy the accumulators 11-14 wait
+# states after a v_mfma_f32_16x16x16_f16 (tools/hazard_branchy_beam.py).
+# tools/isa_hazard.py walks every path (branches, loop back-edges) after every
+# MFMA of every shipped kernel and fails on any instruction that touches the
+# MFMA's destination before the form's required wait states (the larger of
+# hipcc's own pad and the hardware probe's, tools/probe_mfma_hazard.py).
+def _isa_hazard():
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import isa_hazard
+    return isa_hazard
+
+
+def test_mfma_hazard_scanner_finds_known_violations():
+    """The scanner itself: a VALU read 5 states after a 16x16x32 MFMA is
+    flagged; 8 states (the pad) is not; a read reached only through a taken
+    branch is flagged; an accumulate chain (srcC only) is not."""
+    H = _isa_hazard()
+    mf = "\tv_mfma_f32_16x16x32_f16 v[0:3], v[4:7], v[8:11], v[0:3]\n"
+
+    def fn(body):
+        return "_Zfoo:\n" + body + "\ts_endpgm\n.Lfunc_end0:\n"
+    near = fn(mf + "\ts_nop 3\n\tv_mov_b32_e32 v20, v1\n")
+    far = fn(mf + "\ts_nop 7\n\tv_mov_b32_e32 v20, v1\n")
+    branch = fn(mf + "\ts_cbranch_scc1 .LBB0_2\n\ts_nop 15\n\ts_nop 15\n.LBB0_2:\n\tv_mov_b32_e32 v20, v3\n")
+    chain = fn(mf + "\tv_mfma_f32_16x16x32_f16 v[12:15], v[4:7], v[8:11], v[0:3]\n\ts_nop 15\n")
+    assert len(H.scan(near)["_Zfoo"]) == 1
+    assert H.scan(far)["_Zfoo"] == []
+    assert len(H.scan(branch)["_Zfoo"]) == 1
+    assert H.scan(chain)["_Zfoo"] == []
+
+
+def test_mfma_results_respect_wait_states(listings):
+    """Every MFMA of every shipped kernel, on every path: no instruction
+    reads or writes its destination registers inside the required wait
+    states.  Covers dec_bank_d8_kernel's lazy-rescale branch (bank8.hip,
+    `if (__any(gm > m + B8_THR))` over the U accumulators) and every other
+    MFMA consumer; the context attention's online_update_lazy runs on VALU
+    accumulators (no MFMA there)."""
+    H = _isa_hazard()
+    total, bad = 0, {}
+    for name, path in listings.items():
+        asm = open(path).read()
+        total += sum(H.count_mfma(asm).values())
+        for k, hz in H.scan(asm).items():
+            if hz:
+                bad[k] = hz[:3]
+    assert total > 1000, total  # the scan saw the kernels' MFMAs
+    assert not bad, bad
+    d8 = H.count_mfma(open(listings["bank8"]).read(), r"dec_bank_d8_kernel")
+    assert d8 and all(n > 0 for n in d8.values())
 
 
 # ----------------------------------------------------------------- LDS rule

@@ -107,8 +107,9 @@ def split_mfma(ops):
     return parts[0], parts[1], parts[2], parts[3] if len(parts) > 3 else ""
 
 
-def scan_function(ins, labels):
-    """[(mfma line, hazard line, states elapsed, required)]"""
+def scan_function(ins, labels, every=False):
+    """[(mfma line, hazard line, states elapsed, required)]; every: report
+    every toucher on a path, not only the first"""
     found = []
     for i, (mn, ops, raw) in enumerate(ins):
         if not mn.startswith("v_mfma_"):
@@ -133,20 +134,21 @@ def scan_function(ins, labels):
                     if not (regs(a2) | regs(b2)) & dst:
                         continue  # srcC only: the matrix pipe's accumulator forwarding (the compiler pads it)
                 found.append((raw, raw2, st, need))
-                continue
+                if not every:
+                    continue
             st2 = st + states(mn2, ops2)
             for k in succ(ins, labels, j):
                 stack.append((k, st2))
     return found
 
 
-def scan(asm, regex=None):
+def scan(asm, regex=None, every=False):
     """{kernel symbol: [hazards]} for every kernel (matching regex) in a listing"""
     out = {}
     for name, (ins, labels) in parse(asm).items():
         if regex and not re.search(regex, name):
             continue
-        out[name] = scan_function(ins, labels)
+        out[name] = scan_function(ins, labels, every)
     return out
 
 
