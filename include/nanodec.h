@@ -293,7 +293,8 @@ const char* nd_version(void);
 #define ND_ROUTE_TILE256 7     /* gemm_f32_kernel 256x256 tiles */
 #define ND_ROUTE_TILE128 8     /* gemm_f32_kernel 128x128 tiles */
 #define ND_ROUTE_TILE64 9      /* gemm_f32_kernel 64x64 tiles */
-#define ND_ROUTE_N 10
+#define ND_ROUTE_P16_SPLITK 10 /* gemm_p16k_kernel (K = 1024 / 2048, 32 x 32 tiles split over K, 128 < M) */
+#define ND_ROUTE_N 11
 /* counts[0 .. min(n, ND_ROUTE_N) - 1] <- launches per route since the last
  * reset; reset != 0 zeroes the counters afterwards. */
 int nd_gemm_routes(int64_t* counts, int32_t n, int32_t reset);
@@ -373,6 +374,18 @@ int nd_op_enc_ffn_wo(const float* att, const float* x_in, const uint16_t* woh, f
 int nd_op_gemm_p16_split(const float* A, const uint16_t* Wh, float wscale, const float* bias, const float* R, float* C,
                          int32_t M, int32_t N, int32_t K, const float* part_in, int32_t part_n_in, float* part_out,
                          int32_t relu, int32_t* part_n_out, void* stream);
+/* The split-K form of the long-K decoder products (gemm_p16k_kernel: 32 x 32
+ * tiles, K / 512 slices over workgroups, the slices summed in slice order by
+ * the last arriving workgroup; the engine's route for W_vo and FFN2 at
+ * 128 < rows <= 1024; decoder/transformer.py:88-93, position_ffn.py:38-40):
+ * operands as nd_op_gemm_p16_split (no LN, no relu).  slab: >= tiles * 4096
+ * floats; tickets: >= tiles int32, zero before the first call (each tile's
+ * last arriver resets its own); tiles >= ceil(M / 32) * N / 32.  Fails if the
+ * route is not taken. */
+int nd_op_gemm_p16_splitk(const float* A, const uint16_t* Wh, float wscale, const float* bias, const float* R,
+                          float* C, int32_t M, int32_t N, int32_t K, float* part_out, float* slab, int32_t* tickets,
+                          int32_t tiles, int32_t* part_n_out, void* stream);
+
 /* The same GEMM with the weight's row-major split image too (nd_op_split_weight
  * of the row-major W): from M >= 2048 rows (beam search over large batches)
  * the engine runs it on the LDS-tiled kernel with P16 operands. */

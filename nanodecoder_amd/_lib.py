@@ -81,6 +81,7 @@ SIGNATURES = {
     "nd_op_gemm_p16_split": (_I, [_P, _P, _F, _P, _P, _P, _I, _I, _I, _P, _I, _P, _I, _P, _P]),
     "nd_op_enc_ffn": (_I, [_P, _P, _F, _P, _P, _F, _P, _P, _P, _I, _I, _P, _P]),
     "nd_op_enc_ffn_wo": (_I, [_P, _P, _P, _F, _P, _P, _F, _P, _P, _F, _P, _P, _P, _P, _F, _P, _P, _I, _I, _P, _P]),
+    "nd_op_gemm_p16_splitk": (_I, [_P, _P, ctypes.c_float, _P, _P, _P, _I, _I, _I, _P, _P, _P, _I, _P, _P]),
     "nd_op_gemm_p16_split_rm": (_I, [_P, _P, _F, _P, _F, _P, _P, _P, _I, _I, _I, _P, _I, _P, _I, _P, _P]),
     "nd_op_dec_mem_attention": (_I, [_P, _P, _P, _P, ctypes.c_float, _P, _I, _I, _I, _I, _P]),
     "nd_op_memory_pack": (_I, [_P, _P, _P, _P, _I, _I, _I, _P]),
@@ -124,7 +125,7 @@ def lib():
 
 
 ROUTES = ["p16_small", "p16_n64", "p16_ln128", "p16s_2x4", "p16s_2x2", "p16_longk", "p16_big", "tile256",
-          "tile128", "tile64"]  # include/nanodec.h ND_ROUTE_*
+          "tile128", "tile64", "p16_splitk"]  # include/nanodec.h ND_ROUTE_*
 
 
 def gemm_routes(reset: bool = False):

@@ -23,12 +23,13 @@
 // with their power-of-two weights.  Score error on LN-like rows: below a
 // plain fp32 dot product's rounding (tests/test_bank_d8_scheme.py).
 //
-// U = P^T M on f16 MFMAs as in the h3 form, the digits turned into exact f16
-// integers (magic-number conversion) from a per-wave transposed LDS image
-// read by ds_read_b64_tr_b8: one 16x16x32 product per dim block takes
-// [P, P] against [a2 * 2^8 (4 keys), a1 (4 keys)], one 16x16x16 product P
-// against a0 * 2^-8.  P is p s_t 2^7 / s_max (s_max: the chunk's largest s_t,
-// so <= 2^7 e^6 < 65504) split hi | lo as in the h3 form.
+// U = P^T M on f16 MFMAs, the digits turned into exact f16 integers
+// (magic-number conversion) from a per-wave transposed LDS image read by
+// ds_read_b64_tr_b8: one 16x16x32 product per dim block takes [P, P] against
+// [a2 * 2^8 (4 keys), a1 (4 keys)], a second [P, 0] against a0 * 2^-8 (one
+// MFMA shape per accumulator: mfma_d8h16as32).  P is p s_t 2^7 / s_max
+// (s_max: the chunk's largest s_t, so <= 2^7 e^6 < 65504) split hi | lo (the
+// rows of head h carry hi, the rows of h + 8 lo).
 //
 // 3 bytes per element: 103.9 MB per launch at 256 chunks against 138.9 MB.
 #include "common.hpp"
@@ -79,8 +80,15 @@ __device__ __forceinline__ i32x4 mfma_i8(i32x4 a, i32x4 b, i32x4 c) {
 __device__ __forceinline__ f32x4 mfma_d8h32(d8h8 a, d8h8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
-__device__ __forceinline__ f32x4 mfma_d8h16(d8h4 a, d8h4 b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c, 0, 0, 0);
+// The a0 plane's product on the same 16x16x32 form as the a2 / a1 products ([P | 0] against [a0 | a0]: the
+// same lane pairs, zeros in the second k half): every MFMA of an accumulator then has ONE shape.  A
+// 16x16x16_f16 that accumulates onto a 16x16x32_f16's destination reads components 0-1 of srcC stale
+// unless >= 4 VALU / 5 other instructions separate them (tools/probe_mfma_hazard.py, profiles/
+// r05_mfma_hazard_probe.json); hipcc 7.2 pads such a pair with nothing.
+__device__ __forceinline__ f32x4 mfma_d8h16as32(d8h4 a, d8h4 b, f32x4 c) {
+  const d8h8 a8 = {a[0], a[1], a[2], a[3], (_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f};
+  const d8h8 b8 = {b[0], b[1], b[2], b[3], b[0], b[1], b[2], b[3]};
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a8, b8, c, 0, 0, 0);
 }
 
 // 4 signed bytes -> 4 exact f16: f16 bits 0x64uu = 1024 + u with u = b + 128
@@ -290,9 +298,9 @@ __device__ __forceinline__ void bank_d8_chunk(int c, const float* __restrict__ q
       const d8h8 b1 = {b1a[0], b1a[1], b1a[2], b1a[3], b1b[0], b1b[1], b1b[2], b1b[3]};
       const d8h8 b2 = {b2a[0], b2a[1], b2a[2], b2a[3], b2b[0], b2b[1], b2b[2], b2b[3]};
       ua[2 * kp2] = mfma_d8h32(pa8, b1, ua[2 * kp2]);
-      ua[2 * kp2] = mfma_d8h16(pa, d8_cvt(r3.x, 0), ua[2 * kp2]);
+      ua[2 * kp2] = mfma_d8h16as32(pa, d8_cvt(r3.x, 0), ua[2 * kp2]);
       ua[2 * kp2 + 1] = mfma_d8h32(pa8, b2, ua[2 * kp2 + 1]);
-      ua[2 * kp2 + 1] = mfma_d8h16(pa, d8_cvt(r3.y, 0), ua[2 * kp2 + 1]);
+      ua[2 * kp2 + 1] = mfma_d8h16as32(pa, d8_cvt(r3.y, 0), ua[2 * kp2 + 1]);
     }
   }
 

@@ -180,6 +180,9 @@ struct nd_ctx {
   int* bank_em = nullptr;                 // digit bank: per-chunk max e_t (biased) [B]
   int last_bank_form = 0;                 // nd_bank_form
   float *dqk = nullptr, *dU = nullptr;    // [R, 8*256] P16 (memory-bank path)
+  float* sk_slab = nullptr;               // split-K P16 GEMMs: fp32 partial slabs (gemm_p16k_kernel)
+  int* sk_cnt = nullptr;                  // ... and their per-tile tickets (zeroed per call)
+  int sk_tiles = 0;                       // 32 x 32 tiles the slab serves
   // average self-attention step buffers (P16): xn, avg (+ its row stats), the
   // average_layer hidden, a = FFN(avg), the gate pre-activations [R, 512]
   float *axn = nullptr, *aavg = nullptr, *aavg_part = nullptr, *ah = nullptr, *aa = nullptr, *ag = nullptr;
@@ -376,6 +379,27 @@ static int build_registry(nd_ctx* c) {
   return ND_OK;
 }
 
+static int alloc_ctx_kv(nd_ctx* c) {
+  if (c->ctxkv) return ND_OK;
+  const auto& cfg = c->cfg;
+  const size_t B = cfg.max_batch, T = cfg.max_src_len, D = c->D, Ld = cfg.dec_layers;
+  hipError_t e;
+#define WSK(ptr, n)                                         \
+  if ((e = dalloc(c, &(ptr), (size_t)(n))) != hipSuccess) \
+    return fail(ND_ERR_HIP, std::string("hipMalloc workspace " #ptr ": ") + hipGetErrorString(e));
+  WSK(c->ctxkv, B * T * Ld * 2 * D);
+  float* q = nullptr;
+  WSK(q, B * T * Ld * (CTXQ_ROW / 4));
+  c->ctxq = reinterpret_cast<uint8_t*>(q);
+  float* l = nullptr;
+  WSK(l, B);
+  c->clist = reinterpret_cast<int*>(l);
+  // ceil(B/16) listed chunks x up to 32 splits x rows x {num[256], max[8], den[8]}
+  WSK(c->ctx_part, (B + 15) / 16 * 32 * std::max(1, cfg.max_beam) * (D + 16));
+#undef WSK
+  return ND_OK;
+}
+
 static int alloc_workspaces(nd_ctx* c) {
   const auto& cfg = c->cfg;
   const size_t B = cfg.max_batch, T = cfg.max_src_len, S = cfg.max_steps;
@@ -393,16 +417,23 @@ static int alloc_workspaces(nd_ctx* c) {
   WS(c->y, B * T * D);
   WS(c->att, B * T * D);
   WS(c->big, B * T * std::max(F, 3 * D));
-  WS(c->ctxkv, B * T * Ld * 2 * D);
+  // the per-layer context K/V (fp32 and the 24-bit image) and the beam tail's buffers: beam-capable
+  // contexts only (a greedy context allocates them on nd_set_ctx_path(1)); ADVICE r04: 1.4 GB per
+  // greedy lane at B = 256
+  if (cfg.max_beam > 1) {
+    const int rc = alloc_ctx_kv(c);
+    if (rc != ND_OK) return rc;
+  }
   {
-    float* q = nullptr;
-    WS(q, B * T * Ld * (CTXQ_ROW / 4));
-    c->ctxq = reinterpret_cast<uint8_t*>(q);
-    float* l = nullptr;
-    WS(l, B);
-    c->clist = reinterpret_cast<int*>(l);
-    // ceil(B/16) listed chunks x up to 32 splits x rows x {num[256], max[8], den[8]}
-    WS(c->ctx_part, (B + 15) / 16 * 32 * std::max(1, cfg.max_beam) * (D + 16));
+    // split-K P16 GEMMs (K = 2048 / 1024 at 128 < R <= 1024): 32 x 32 tiles x 4 slices x 4 KB
+    const int tiles = (int)std::min<size_t>((R + 31) / 32, 32) * (int)(D / 32);
+    WS(c->sk_slab, (size_t)tiles * 4 * 1024);
+    float* t = nullptr;
+    WS(t, (size_t)(tiles + 3) / 4 * 4);
+    c->sk_cnt = reinterpret_cast<int*>(t);
+    c->sk_tiles = tiles;
+    if ((e = hipMemset(c->sk_cnt, 0, (size_t)(tiles + 3) / 4 * 16)) != hipSuccess)
+      return fail(ND_ERR_HIP, std::string("hipMemset split-K tickets: ") + hipGetErrorString(e));
   }
   WS(c->mem_p, B * T * D);
   WS(c->bank_ks, B * 512);
@@ -541,6 +572,13 @@ struct G {
   G& small_m(bool on) { a.prefer_p16 = on ? 1 : 0; return *this; }
   G& c_rowmajor(bool on) { a.c_rm = on ? 1 : 0; return *this; }  // P16 GEMMs: C row-major
   G& q24(uint8_t* img, int ld) { a.q24 = img; a.q24_ld = ld; return *this; }  // the 24-bit K/V image, not C
+  // long-K P16 products may split over workgroups (gemm_p16k_kernel) into the context's slab
+  G& splitk(const nd_ctx* c) {
+    a.sk_slab = c->sk_slab;
+    a.sk_cnt = c->sk_cnt;
+    a.sk_tiles = c->sk_tiles;
+    return *this;
+  }
   bool packed = false;
   G& p16() { packed = true; return *this; }  // decoder-step operands in the P16 layout
   hipError_t run(hipStream_t s, int* pn_out = nullptr) {
@@ -784,7 +822,7 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
   int pnx = 1, pnq = 0, pnm = 0;
   // a decoder-step GEMM over the R rows: P16 operands, split-fp16 weights, dead chunks skipped
   auto dg = [&](const float* A, int lda, const float* W, int N, int K, const float* bias, float* out, int ldc) {
-    return G(A, lda, W, N, K, bias, out, ldc, R).p16().h3(c).skip(done, rpc).small_m(c->beam_tail);
+    return G(A, lda, W, N, K, bias, out, ldc, R).p16().h3(c).skip(done, rpc).small_m(c->beam_tail).splitk(c);
   };
   for (int i = 0; i < Ld; ++i) {
     DecLayer& L = c->dec[i];
@@ -859,6 +897,7 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
 static hipError_t enqueue_memory(nd_ctx* c, int B, int T, int rpc, hipStream_t s) {
   set_memory_view(c, T, rpc);
   if (!use_memory_bank(c, rpc)) {
+    if (!c->ctxkv) return hipErrorInvalidValue;  // a beam call on a context created with max_beam 1
     // the fused form needs the split-fp16 weights (h3): exact fp32 never takes the image
     const bool fuse = c->ctx_q24 && use_ctx_q24_fuse() && !nd::gemm_f32_forced();
     LCHK(enqueue_ctxkv(c, B, T, s, fuse));
@@ -1699,6 +1738,11 @@ int nd_set_graphs(nd_ctx* c, int enable) {
 int nd_set_ctx_path(nd_ctx* c, int path) {
   if (!c) return fail(ND_ERR_ARG, "null ctx");
   if (path < 0 || path > 1) return fail(ND_ERR_ARG, "path must be 0 (auto) or 1 (K/V form)");
+  if (path == 1) {  // a greedy-only context allocates the context K/V now (beam contexts have it)
+    HIPCHK(hipSetDevice(c->cfg.device));
+    const int rc = alloc_ctx_kv(c);
+    if (rc != ND_OK) return rc;
+  }
   if (c->ctx_path != path) {
     for (auto& kv : c->graphs) (void)hipGraphExecDestroy(kv.second);
     c->graphs.clear();
@@ -1896,6 +1940,25 @@ int nd_op_gemm_p16_split(const float* A, const uint16_t* Wh, float wscale, const
   return ND_OK;
 }
 
+int nd_op_gemm_p16_splitk(const float* A, const uint16_t* Wh, float wscale, const float* bias, const float* R,
+                          float* C, int32_t M, int32_t N, int32_t K, float* part_out, float* slab, int32_t* tickets,
+                          int32_t tiles, int32_t* part_n_out, void* stream) {
+  if (int rc = ensure_attributes()) return rc;
+  if (!A || !Wh || !C || !slab || !tickets || tiles < 1) return fail(ND_ERR_ARG, "gemm_p16_splitk: bad arguments");
+  if ((K != 1024 && K != 2048) || N % 32 || M <= 128 || ((M + 31) / 32) * (N / 32) > tiles)
+    return fail(ND_ERR_ARG, "gemm_p16_splitk: needs K 1024 / 2048, N % 32 == 0, M > 128 and enough tiles");
+  nd::GemmArgs g;
+  g.A = A; g.Wh = Wh; g.wscale = wscale; g.bias = bias; g.R = R; g.C = C; g.M = M; g.N = N; g.K = K;
+  g.part_out = part_out;
+  g.sk_slab = slab; g.sk_cnt = tickets; g.sk_tiles = tiles;
+  const long long before = nd::gemm_route_count(ND_ROUTE_P16_SPLITK, false);
+  hipError_t e = nd::launch_gemm_p16(g, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("gemm_p16_splitk: ") + hipGetErrorString(e));
+  if (nd::gemm_route_count(ND_ROUTE_P16_SPLITK, false) == before) return fail(ND_ERR_ARG, "gemm_p16_splitk: not taken");
+  if (part_n_out) *part_n_out = g.part_n_out;
+  return ND_OK;
+}
+
 int nd_op_gemm_p16_split_rm(const float* A, const uint16_t* Wh, float wscale, const uint16_t* Wh_rm, float wscale_rm,
                             const float* bias, const float* R, float* C, int32_t M, int32_t N, int32_t K,
                             const float* part_in, int32_t part_n_in, float* part_out, int32_t relu,
@@ -2078,6 +2141,10 @@ static hipError_t enqueue_encode_nano(nd_ctx* c, int B, int T, hipStream_t s) {
 }
 
 static hipError_t enqueue_encode(nd_ctx* c, int B, int T, hipStream_t s) {
+  // every call starts with the split-K tickets at zero (a memset node in the call's graph): each tile's last
+  // arriver resets its own, this repairs a ticket left by an aborted call (cdna_hip_programming.md §6,
+  // Guideline 16 "Re-initialise every call")
+  if (c->sk_cnt) LCHK(hipMemsetAsync(c->sk_cnt, 0, (size_t)(c->sk_tiles + 3) / 4 * 16, s));
   if (c->cfg.encoder_type == ND_ENC_TRANSFORMER) return enqueue_encode_transformer(c, B, T, s);
   return enqueue_encode_nano(c, B, T, s);
 }

@@ -134,6 +134,7 @@ __device__ __forceinline__ float group_sum(float v) {
 // single ds_read_b128 per plane.
 typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ f32x16 mfma32h(h8 a, h8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
@@ -700,6 +701,131 @@ __global__ void __launch_bounds__(BMB* BNB * 64) gemm_p16s_kernel(const GemmArgs
   }
 }
 
+// Long-K decoder products (the memory bank's output projection W_vo and
+// FFN2, K = 2048, at 128 < M <= 1024 rows) split over workgroups.  The
+// one-block-per-workgroup kernel above (16 x 16 outputs, the whole K on 8
+// waves) pulls 256 KB of A and W into every CU for 16 x 16 outputs; here a
+// workgroup owns a 32 x 32 tile (2 x 2 blocks) over one K-slice of 512 (4
+// waves of 128 k), so a CU takes in 128 KB for 4 blocks and the launch moves
+// half the L2 -> CU bytes (MI355X_MICROARCH.md: per-CU ingest bounds these
+// latency-bound shapes).  The 4 waves' partials are summed through LDS in wave
+// order; the K / 512 slices of a tile meet in an fp32 slab: write-through
+// (sc1) stores, every wave's vmcnt(0), one agent-scope ticket per workgroup;
+// the workgroup that draws the last ticket reads the slabs back with sc1 loads
+// and sums them in slice order (deterministic: the result does not depend on
+// which slice arrives last), adds bias / residual, writes C and the row
+// statistics, and resets the tile's ticket for the next launch
+// (cdna_hip_programming.md §5 "Projection GEMM at M = 256", §6 Guideline 16).
+#define PK_NW 4    // waves per workgroup (k sub-slices)
+#define PK_KPW 4   // 32-k pairs per wave
+#define PK_SLICE (PK_NW * PK_KPW * 32)  // k per workgroup (512)
+
+__device__ __forceinline__ void pk_store_sc1(__amdgpu_buffer_rsrc_t r, int off, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, v), r, off, 0, 16);  // aux 16 = sc1
+}
+__device__ __forceinline__ f32x4 pk_load_sc1(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16));
+}
+
+template <bool RESID>
+__global__ void __launch_bounds__(PK_NW * 64) gemm_p16k_kernel(const GemmArgs g) {
+  // ONE shared array: the waves' partial blocks, then the last-arriver word
+  __shared__ __attribute__((aligned(16))) f32x4 red[PK_NW * 4 * 64 + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int S = g.K / PK_SLICE, NBT = g.N >> 5;  // slices; 32-column tiles across N
+  const int tile = blockIdx.x / S, sl = blockIdx.x % S;
+  const int mb0 = 2 * (tile / NBT), nb0 = 2 * (tile % NBT);
+  const int MB = (g.M + 15) >> 4, KB = g.K >> 4, KP = g.K >> 5, NB = g.N >> 4;
+  const f32x4* __restrict__ A4 = reinterpret_cast<const f32x4*>(g.A);
+  const f32x4* __restrict__ W4 = reinterpret_cast<const f32x4*>(g.Wh);
+  // this wave's k pairs: sl * 16 + wave * 4 .. + 3; loads in order of use, straight-line
+  const int kp0 = sl * (PK_NW * PK_KPW) + wave * PK_KPW;
+  f32x4 a[2][2 * PK_KPW], w[2][2 * PK_KPW];
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int f = 0; f < 2 * PK_KPW; ++f) a[r][f] = A4[((size_t)min(mb0 + r, MB - 1) * KB + 2 * kp0 + f) * 64 + lane];
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int f = 0; f < 2 * PK_KPW; ++f) w[c][f] = W4[(((size_t)(nb0 + c) * KP + kp0) * 2 + f) * 64 + lane];
+  // the epilogue operands of the block this wave finishes (rb, cb) = (wave >> 1, wave & 1)
+  const int rb = wave >> 1, cb = wave & 1, mb = mb0 + rb, nb = nb0 + cb;
+  const size_t ct = ((size_t)min(mb, MB - 1) * NB + nb) * 64 + lane;
+  const f32x4 bv = ld4((g.bias ? g.bias + nb * 16 : nd_zero16) + 4 * (lane >> 4));
+  f32x4 rv = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (RESID) rv = reinterpret_cast<const f32x4*>(g.R)[ct];
+  __builtin_amdgcn_sched_barrier(0);
+  float amax = 0.f;
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int f = 0; f < 2 * PK_KPW; ++f) amax = fmaxf(amax, absmax4(a[r][f]));
+  flag_overflow(g.ovf, amax);
+  f32x4 acc0[4], acc1[4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) acc0[b] = acc1[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int p = 0; p < PK_KPW; ++p) {
+    h8 ah[2], al[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) split8(a[r][2 * p], a[r][2 * p + 1], ah[r], al[r]);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const h8 wh = __builtin_bit_cast(h8, w[b & 1][2 * p]), wl = __builtin_bit_cast(h8, w[b & 1][2 * p + 1]);
+      acc0[b] = mfma16h(wh, ah[b >> 1], acc0[b]);
+      acc1[b] = mfma16h(wh, al[b >> 1], acc1[b]);
+      acc1[b] = mfma16h(wl, ah[b >> 1], acc1[b]);
+    }
+  }
+  // the workgroup's slice: block b summed over the 4 waves in wave order, by wave b
+#pragma unroll
+  for (int b = 0; b < 4; ++b) red[(wave * 4 + b) * 64 + lane] = acc0[b] + acc1[b];
+  lds_barrier();
+  f32x4 v = red[(0 * 4 + wave) * 64 + lane];
+#pragma unroll
+  for (int w2 = 1; w2 < PK_NW; ++w2) v += red[(w2 * 4 + wave) * 64 + lane];
+  if (S > 1) {
+    // slab [tile][slice][block][64 lanes] f32x4, write-through
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        g.sk_slab + (size_t)tile * S * 4 * 256, 0, S * 4 * 1024, 0x00020000);
+    pk_store_sc1(rs, ((sl * 4 + wave) * 64 + lane) * 16, v);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave, before the ticket
+    __syncthreads();
+    if (tid == 0) {
+      const int t = __hip_atomic_fetch_add(g.sk_cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      reinterpret_cast<int*>(&red[PK_NW * 4 * 64])[0] = t;
+    }
+    __syncthreads();
+    if (reinterpret_cast<const int*>(&red[PK_NW * 4 * 64])[0] != S - 1) return;  // not the last slice
+    // the last arriver: every slice of block `wave` (S <= 4), all loads in flight at once (sc1; its own
+    // from registers), summed in slice order
+    f32x4 pp[4];
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) pp[s2] = pk_load_sc1(rs, ((min(s2, S - 1) * 4 + wave) * 64 + lane) * 16);
+    f32x4 sum = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2)
+      if (s2 < S) sum += s2 == sl ? v : pp[s2];
+    v = sum;
+    if (tid == 0) __hip_atomic_store(g.sk_cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  v = v * g.wscale + bv;
+  if constexpr (RESID) v += rv;
+  if (mb >= MB) return;
+  reinterpret_cast<f32x4*>(g.C)[ct] = v;
+  if (g.part_out) {
+    const float m_ = xor32_sum(xor16_sum(v.x + v.y + v.z + v.w)) * (1.0f / 16.0f);
+    const f32x4 d = v - m_;
+    const float q = xor32_sum(xor16_sum(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w));
+    if (lane < 16) {
+      float* pp = g.part_out + ((size_t)(mb * 16 + lane) * ND_PART_LD + nb) * 2;
+      pp[0] = m_;
+      pp[1] = q;
+    }
+  }
+}
+
 // row-major [M, N] (leading dim ld) -> P16 packed, one thread per float4
 __global__ void __launch_bounds__(256)
 pack_p16_kernel(const float* __restrict__ src, int ld, float* __restrict__ dst, int M, int N) {
@@ -1049,6 +1175,21 @@ hipError_t launch_gemm_p16(GemmArgs& g, hipStream_t s) {
     if (g.norm && g.N % 128 == 0 && (long)(g.N / 128) * ((g.M + 15) / 16) >= 128) return launch_p16<8, 1, 256>(g, s);
     if (g.N % 64 == 0 && (long)(g.N / 64) * ((g.M + 15) / 16) >= 128) return launch_p16<4, 2, 128>(g, s);
     return launch_p16<1, 4, 64>(g, s);
+  }
+  // split over workgroups (gemm_p16k_kernel): 32 x 32 tiles x K / 512 slices, when the tiles x slices fill
+  // the chip at least half (M from 128 rows) and the context gave the slab / tickets for that many tiles
+  if (g.Wh && !g.skip && !g.c_rm && !g.relu && (g.K == 2048 || g.K == 1024) && g.N % 32 == 0 && g.sk_slab &&
+      g.sk_cnt) {
+    const int tiles = ((g.M + 31) / 32) * (g.N / 32), S = g.K / PK_SLICE;
+    if (g.M > 128 && tiles <= g.sk_tiles) {
+      count_route(ND_ROUTE_P16_SPLITK);
+      g.part_n_out = g.N / 16;
+      if (g.R)
+        hipLaunchKernelGGL((gemm_p16k_kernel<true>), dim3(tiles * S), dim3(PK_NW * 64), 0, s, g);
+      else
+        hipLaunchKernelGGL((gemm_p16k_kernel<false>), dim3(tiles * S), dim3(PK_NW * 64), 0, s, g);
+      return hipGetLastError();
+    }
   }
   // K = 2048 on 8 K-slice waves of 256 (16 waves of 128: pooled greedy 16.30 -> 16.63 ms, round 4, dropped)
   if (g.K == 2048) return launch_p16<1, 8, 256>(g, s);

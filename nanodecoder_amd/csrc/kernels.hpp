@@ -64,6 +64,12 @@ struct GemmArgs {
   // instead of C; nullable
   uint8_t* q24 = nullptr;
   int q24_ld = 0;
+  // P16 GEMMs at K >= 1024: the split-K form's fp32 slab and per-tile tickets
+  // (zero before the first launch; the last arriver of a tile resets its
+  // ticket), sized for sk_tiles 32 x 32 tiles; null: the one-workgroup form
+  float* sk_slab = nullptr;
+  int* sk_cnt = nullptr;
+  int sk_tiles = 0;
 };
 #define ND_PART_LD 16  // partial-stat slots per row (max column tiles of a 256-wide row)
 // row-major operands (encoder, large M): LDS-tiled MFMA kernel

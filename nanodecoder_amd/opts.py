@@ -66,9 +66,10 @@ def translate_parser() -> argparse.ArgumentParser:
               "0 = as many reads as fill the engine batch")
     _add(g, "engine_max_batch", type=int, default=0,
          help="engine batch capacity in chunks (0 = max(batch_size, 256): a full MI355X batch)")
-    _add(g, "engine_lanes", type=int, default=3,
+    _add(g, "engine_lanes", type=int, default=0,
          help="translate calls kept on the GPU at once (EnginePool lanes: one engine context and hardware queue "
-              "each; the calls' kernels share the CUs); 1 = one call at a time")
+              "each, each holding its own workspaces; the calls' kernels share the CUs); 1 = one call at a time; "
+              "0 = 3 for greedy / sampling, 1 for beam search")
     _add(g, "seed", type=int, default=-1, help="random sampling seed (-1: fresh entropy per run)")
     _add(g, "frontend", default="cpu", choices=["cpu", "gpu"],
          help="gpu: normalise and window the reads on the GPU (frontend.hip) instead of in the worker pool")

@@ -125,9 +125,13 @@ class Translator(object):
             kw = dict(device=dev, max_batch=self.max_batch, max_steps=self.max_length,
                       max_src_len=min(512, int(getattr(opt, "src_seq_length", 512))),
                       max_beam=max(1, self.beam_size))
-            # -engine_lanes (default 3): that many calls in flight on the GPU
-            # (EnginePool), stream_reads keeping every lane busy
-            lanes = int(getattr(opt, "engine_lanes", 3) or 1)
+            # -engine_lanes: that many calls in flight on the GPU (EnginePool),
+            # stream_reads keeping every lane busy.  Default 3 for greedy /
+            # sampling; 1 for beam search, whose calls poll the host between
+            # graph segments (stream_reads' one host thread would serialise
+            # them) and whose lanes each hold the context K/V (~2.4 GB at
+            # B = 1024, beam 5)
+            lanes = int(getattr(opt, "engine_lanes", 0) or 0) or (3 if self.beam_size == 1 else 1)
             if lanes > 1 and Engine is _HipEngine:
                 engine = EnginePool(cfg, weights, lanes=lanes, **kw)
             else:

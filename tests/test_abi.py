@@ -124,10 +124,12 @@ def test_hot_path_kernels_do_not_drain_loads(listings):
 
 
 # ----------------------------------------------------------------- MFMA wait states
-# DESIGN.md section 3 "MFMA results and wait states" (round 5): round 4's beam
-# digit-bank kernel returned wrong components 0-1 of an accumulator when a
-# branch around its rescale made hipcc copy the accumulators 11-14 wait
-# states after a v_mfma_f32_16x16x16_f16 (tools/hazard_branchy_beam.py).
+# DESIGN.md section 3 "MFMA results and wait states" (round 5).  The hardware
+# probe (tools/probe_mfma_hazard.py) found one hazard class hipcc 7.2 does not
+# pad: an MFMA of another shape accumulating onto an MFMA's destination
+# (16x16x32_f16 then 16x16x16_f16, or the reverse) reads half of srcC stale
+# unless >= 4 VALU / 5 SALU instructions separate them; the greedy digit-bank
+# kernel had such a pair 4 instructions apart (now one shape per accumulator).
 # tools/isa_hazard.py walks every path (branches, loop back-edges) after every
 # MFMA of every shipped kernel and fails on any instruction that touches the
 # MFMA's destination before the form's required wait states (the larger of
@@ -142,7 +144,8 @@ def _isa_hazard():
 def test_mfma_hazard_scanner_finds_known_violations():
     """The scanner itself: a VALU read 5 states after a 16x16x32 MFMA is
     flagged; 8 states (the pad) is not; a read reached only through a taken
-    branch is flagged; an accumulate chain (srcC only) is not."""
+    branch is flagged; a same-form accumulate chain (srcC only) is not; a
+    16x16x16 accumulating onto it is, unless 5 states apart."""
     H = _isa_hazard()
     mf = "\tv_mfma_f32_16x16x32_f16 v[0:3], v[4:7], v[8:11], v[0:3]\n"
 
@@ -152,10 +155,15 @@ def test_mfma_hazard_scanner_finds_known_violations():
     far = fn(mf + "\ts_nop 7\n\tv_mov_b32_e32 v20, v1\n")
     branch = fn(mf + "\ts_cbranch_scc1 .LBB0_2\n\ts_nop 15\n\ts_nop 15\n.LBB0_2:\n\tv_mov_b32_e32 v20, v3\n")
     chain = fn(mf + "\tv_mfma_f32_16x16x32_f16 v[12:15], v[4:7], v[8:11], v[0:3]\n\ts_nop 15\n")
+    # a 16x16x16 accumulating onto the 16x16x32's destination: stale srcC half unless 5 states apart
+    mixed = fn(mf + "\tv_mfma_f32_16x16x16_f16 v[0:3], v[4:5], v[8:9], v[0:3]\n\ts_nop 15\n")
+    mixed_far = fn(mf + "\ts_nop 4\n\tv_mfma_f32_16x16x16_f16 v[0:3], v[4:5], v[8:9], v[0:3]\n\ts_nop 15\n")
     assert len(H.scan(near)["_Zfoo"]) == 1
     assert H.scan(far)["_Zfoo"] == []
     assert len(H.scan(branch)["_Zfoo"]) == 1
     assert H.scan(chain)["_Zfoo"] == []
+    assert len(H.scan(mixed)["_Zfoo"]) == 1
+    assert H.scan(mixed_far)["_Zfoo"] == []
 
 
 def test_mfma_results_respect_wait_states(listings):

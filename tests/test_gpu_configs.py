@@ -76,8 +76,10 @@ def test_greedy_config_batch256_vs_oracle(encoder):
     r = eng.translate_greedy(sig, lens, lens, max_len=S, min_len=MINL)  # the bench's graph (no log-prob dump)
     routes = _routes()
     # 256 rows: the N = 2048 products (query projection, FFN1) on gemm_p16s<2,4>, the QKV products on
-    # gemm_p16s<2,2>, the K = 2048 products on the long-K kernel (Wo, N = K = 256, stays on gemm_p16<1,4,64>)
-    assert routes["p16s_2x4"] > 0 and routes["p16s_2x2"] > 0 and routes["p16_longk"] > 0, routes
+    # gemm_p16s<2,2>, the K = 2048 products (W_vo, FFN2) split over K (gemm_p16k_kernel; Wo, N = K = 256,
+    # stays on gemm_p16<1,4,64>)
+    assert routes["p16s_2x4"] > 0 and routes["p16s_2x2"] > 0 and routes["p16_splitk"] > 0, routes
+    assert routes["p16_longk"] == 0, routes
     rl = eng.translate_greedy(sig, lens, lens, max_len=S, min_len=MINL, return_logp=True)
     tok = r["tokens"].cpu().numpy()
     assert (tok == rl["tokens"].cpu().numpy()).all()

@@ -141,6 +141,42 @@ def test_split_weight_image(N, K, mag):
     assert (err <= W.double().abs() * 2.0 ** -21 + 2.0 ** -25 / s).all(), err.max().item()
 
 
+@pytest.mark.parametrize("M,N,K,res", [(256, 256, 2048, True), (256, 256, 1024, False), (1024, 256, 2048, True),
+                                         (144, 256, 2048, True), (400, 512, 2048, False)])
+def test_gemm_p16_splitk_vs_fp64(M, N, K, res):
+    """The split-K long-K P16 GEMM (W_vo / FFN2 route at 128 < rows <= 1024):
+    against fp64 within the split-fp16 bound, row partials for the next
+    LayerNorm, rows past M (M not a multiple of 32) left to the padding, the
+    tickets back at zero after every launch, and three launches on the same
+    tickets bitwise equal (the slices are summed in slice order whichever
+    workgroup arrives last)."""
+    from nanodecoder_amd.engine import op_gemm_p16_splitk, op_pack_p16h, pack_p16, row_partials, unpack_p16
+    g = torch.Generator().manual_seed(3 * M + K)
+    A = torch.randn(M, K, generator=g)
+    W = torch.randn(N, K, generator=g) / K ** 0.5
+    b = torch.randn(N, generator=g)
+    R = torch.randn(M, N, generator=g)
+    dev = torch.device("cuda", 0)
+    Wh, sc = op_pack_p16h(W.to(dev))
+    Ap = pack_p16(torch.cat([A, A.new_zeros((-M) % 16, K)]).to(dev))
+    Rp = pack_p16(torch.cat([R, R.new_zeros((-M) % 16, N)]).to(dev)) if res else None
+    part_out = torch.full(((M + 15) // 16 * 16, 16, 2), float("nan"), device=dev)
+    outs, tk = [], None
+    for _ in range(3):
+        Cp, pn, tk = op_gemm_p16_splitk(Ap, Wh, sc, b.to(dev), M, N, K, Rp, part_out, tickets=tk)
+        torch.cuda.synchronize()
+        assert int(tk.abs().sum().item()) == 0  # every tile's last arriver reset its ticket
+        outs.append(unpack_p16(Cp, M).cpu())
+    assert all(torch.equal(outs[0], o) for o in outs[1:])
+    ref = A.double() @ W.double().t() + b.double() + (R.double() if res else 0)
+    assert (outs[0].double() - ref).abs().max().item() < 2e-4
+    assert pn == N // 16
+    want = row_partials(outs[0], pn)[:, :pn]
+    got = part_out[:M, :pn].cpu()
+    assert torch.allclose(got[:, :, 0], want[:, :, 0], atol=1e-5)
+    assert torch.allclose(got[:, :, 1], want[:, :, 1], rtol=1e-4, atol=1e-4)
+
+
 @pytest.mark.parametrize("M,N,K,ln,relu,res,stats", [(256, 768, 256, True, False, False, False),
                                                       (256, 256, 256, False, False, True, True),
                                                       (256, 256, 256, True, False, False, False),

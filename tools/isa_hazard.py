@@ -11,9 +11,13 @@ back-edges, not only straight-line code.
 For each MFMA in each kernel it walks the control-flow graph forward,
 counting wait states (one per instruction, k + 1 for `s_nop k`), until the
 form's requirement is met.  Any instruction on the way that names one of the
-destination registers is a hazard, except an MFMA that reads them as its
-srcC only: accumulator chains are the matrix pipe's own forwarding, which
-hipcc pads by its rules (the probe's chained form checks one such pair).
+destination registers is a hazard, except an MFMA of the SAME form that reads
+them as its srcC only (an accumulator chain: the matrix pipe forwards it at
+no wait state).  An MFMA of another form reading them as srcC is a hazard
+inside MIXED_SRCC states: a 16x16x16_f16 accumulating onto a 16x16x32_f16's
+destination (or the reverse) reads half of srcC stale with fewer than 4 VALU
+/ 5 SALU or s_nop states between them, and hipcc 7.2 emits such pairs back
+to back (tools/probe_mfma_hazard.py, profiles/r05_mfma_hazard_probe.json).
 
 Required states per form: the larger of the compiler's own pad (hipcc 7.2,
 measured on a VALU read right after the MFMA) and the hardware probe's
@@ -42,6 +46,7 @@ REQUIRED = {
     "f32_4x4x4_16b_f16": 4,
 }
 DEFAULT_REQUIRED = 19  # an unlisted form: the longest (16-pass) requirement
+MIXED_SRCC = 5  # states between an MFMA and another form's MFMA taking its destination as srcC
 
 REG = re.compile(r"\b([va])(?:(\d+)|\[(\d+):(\d+)\])")
 
@@ -132,7 +137,12 @@ def scan_function(ins, labels, every=False):
                 if mn2.startswith("v_mfma_"):
                     d2, a2, b2, c2 = split_mfma(ops2)
                     if not (regs(a2) | regs(b2)) & dst:
-                        continue  # srcC only: the matrix pipe's accumulator forwarding (the compiler pads it)
+                        if mn2 == mn or st >= MIXED_SRCC:
+                            continue  # srcC only, same form (forwarded) or far enough: the chain takes over
+                        found.append((raw, raw2, st, MIXED_SRCC))
+                        if not every:
+                            continue
+                        continue
                 found.append((raw, raw2, st, need))
                 if not every:
                     continue

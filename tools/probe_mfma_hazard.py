@@ -45,6 +45,9 @@ FORMS = {
     "32x32x2_f32": ("v_mfma_f32_32x32x2_f32", 16, 1, 1, ONE, 0x40000000, None),     # 2.0
     # the bank kernels' chain: a 16x16x32 then a 16x16x16 on the same accumulator (32 + 16 = 48.0)
     "chain_32_then_16": ("v_mfma_f32_16x16x16_f16", 4, 2, 2, F16, 0x42400000, "v_mfma_f32_16x16x32_f16"),
+    "chain_16_then_32": ("v_mfma_f32_16x16x32_f16", 4, 4, 4, F16, 0x42400000, "v_mfma_f32_16x16x16_f16_first"),
+    "chain_32_then_32": ("v_mfma_f32_16x16x32_f16", 4, 4, 4, F16, 0x42800000, "v_mfma_f32_16x16x32_f16"),
+    "chain_16_then_16": ("v_mfma_f32_16x16x16_f16", 4, 2, 2, F16, 0x42000000, "v_mfma_f32_16x16x16_f16_first"),
 }
 SENT = "0x7FC0DEAD"
 D0, A0, B0, C0 = 100, 116, 120, 124  # register bases (D up to 16, A/B up to 4, C up to 16)
@@ -63,7 +66,16 @@ def nops(n):
     return s
 
 
-def kernel(name, form, n, mode):
+def filler(kind, g):
+    """g wait states of one kind: s_nop states, VALU moves (unrelated registers) or SALU adds"""
+    if kind == "nop":
+        return nops(g)
+    if kind == "valu":
+        return "".join("v_mov_b32 v115, v114\\n" for _ in range(g))
+    return "".join("s_add_u32 s90, s90, 1\\n" for _ in range(g))
+
+
+def kernel(name, form, n, mode, gap=0, fill="nop"):
     mn, nd, na, nb, abits, _, first = FORMS[form]
     body = ""
     for i in range(nd):
@@ -74,7 +86,9 @@ def kernel(name, form, n, mode):
         body += f"v_mov_b32 v{A0 + i}, {abits}\\nv_mov_b32 v{B0 + i}, {abits}\\n"
     body += "s_nop 7\\n"
     if first:  # chain: the 16x16x32 writes D from zero C, the probed MFMA accumulates onto D
-        body += f"{first} {rng(D0, nd)}, {rng(A0, 4)}, {rng(B0, 4)}, {rng(C0, nd)}\\n"
+        fm = first.replace("_first", "")
+        fw = 2 if "16x16x16" in fm else 4
+        body += f"{fm} {rng(D0, nd)}, {rng(A0, fw)}, {rng(B0, fw)}, {rng(C0, nd)}\\n" + filler(fill, gap)
         body += f"{mn} {rng(D0, nd)}, {rng(A0, na)}, {rng(B0, nb)}, {rng(D0, nd)}\\n"
     else:
         body += f"{mn} {rng(D0, nd)}, {rng(A0, na)}, {rng(B0, nb)}, {rng(C0, nd)}\\n"
@@ -82,8 +96,8 @@ def kernel(name, form, n, mode):
     if mode == "waw":
         body += f"v_mov_b32 v{D0}, 0x40E00000\\n" + nops(32)
     body += "".join(f"v_mov_b32 %{i}, v{D0 + i}\\n" for i in range(4)) + nops(32)
-    clob = ", ".join(f'"v{r}"' for r in list(range(D0, D0 + nd)) + list(range(A0, A0 + 4)) + list(range(B0, B0 + 4))
-                     + list(range(C0, C0 + nd)))
+    regs_ = list(range(D0, D0 + nd)) + list(range(A0, A0 + 4)) + list(range(B0, B0 + 4)) + list(range(C0, C0 + nd))
+    clob = ", ".join([f'"v{r}"' for r in regs_ + [114, 115]] + ['"s90"'])
     return f"""
 extern "C" __global__ void {name}(unsigned* out) {{
   unsigned r0, r1, r2, r3;
@@ -95,28 +109,92 @@ extern "C" __global__ void {name}(unsigned* out) {{
 """
 
 
+GAPS = (0, 1, 2, 3, 4, 5, 6, 8, 10, 12, 16)
+
+
+# VALU write -> MFMA operand read: srcC (or srcA) written by v_mov_b32 in the order
+# component 3, 2, 1, 0 (component c written c + 1 states before the gap's end), g wait states, then
+# the MFMA; its result read 32 states later.  A component read before its write landed keeps the
+# sentinel (srcC) or the stale operand value.
+VALU_FORMS = {
+    "valu_srcC_16x16x16": ("v_mfma_f32_16x16x16_f16", 2, "C"),
+    "valu_srcC_16x16x32": ("v_mfma_f32_16x16x32_f16", 4, "C"),
+    "valu_srcA_16x16x32": ("v_mfma_f32_16x16x32_f16", 4, "A"),
+}
+VGAPS = tuple(range(0, 13))
+
+
+def valu_kernel(name, form, g):
+    mn, w, which = VALU_FORMS[form]
+    body = ""
+    for i in range(4):
+        body += f"v_mov_b32 v{D0 + i}, {SENT}\\nv_mov_b32 v{C0 + i}, {SENT}\\n"
+    for i in range(4):
+        body += f"v_mov_b32 v{A0 + i}, {F16 if which == 'C' else '0x7C007C00'}\\nv_mov_b32 v{B0 + i}, {F16}\\n"
+    body += "s_nop 15\\ns_nop 15\\n"
+    if which == "C":  # the real srcC (zeros), component 3 first .. component 0 last
+        for i in (3, 2, 1, 0):
+            body += f"v_mov_b32 v{C0 + i}, 0\\n"
+    else:  # srcA: the real operand (ones) over an inf-filled A, register 3 first .. 0 last
+        for i in (3, 2, 1, 0):
+            body += f"v_mov_b32 v{A0 + i}, {F16}\\n"
+        for i in range(4):
+            body += ""
+    body += nops(g)
+    cop = rng(C0, 4) if which == "C" else "0"
+    body += f"{mn} {rng(D0, 4)}, {rng(A0, w)}, {rng(B0, w)}, {cop}\\n" + nops(32)
+    body += "".join(f"v_mov_b32 %{i}, v{D0 + i}\\n" for i in range(4)) + nops(32)
+    clob = ", ".join(f'"v{r}"' for r in list(range(D0, D0 + 4)) + list(range(A0, A0 + 4)) + list(range(B0, B0 + 4))
+                     + list(range(C0, C0 + 4)))
+    return f"""
+extern "C" __global__ void {name}(unsigned* out) {{
+  unsigned r0, r1, r2, r3;
+  asm volatile("{body}" : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3) : : {clob});
+  unsigned* o = out + (size_t)(blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  o[0] = r0; o[1] = r1; o[2] = r2; o[3] = r3;
+}}
+"""
+
+
 def names():
     for form in FORMS:
         for mode in ("raw", "waw"):
             for n in range(NMAX + 1):
-                yield form, mode, n, f"hz_{form}_{mode}_{n}".replace("x", "X")
+                yield form, mode, n, 0, f"hz_{form}_{mode}_{n}".replace("x", "X")
+    # chained forms: g wait states between the two MFMAs, the read n states after the second
+    for form in [f for f in FORMS if FORMS[f][6]]:
+        for g in GAPS:
+            for n in range(0, NMAX + 1, 2):
+                yield form, f"gap{g}", n, g, f"hz_{form}_gap{g}_{n}".replace("x", "X")
+    # mixed-shape chains with VALU / SALU fillers in the gap (the read 20 states after)
+    for form in ("chain_32_then_16", "chain_16_then_32"):
+        for kind in ("valu", "salu"):
+            for g in range(0, 9):
+                yield form, f"{kind}{g}", 20, g, f"hz_{form}_{kind}{g}".replace("x", "X")
 
 
 def build():
     os.makedirs(OUT, exist_ok=True)
     src = ['#include <hip/hip_runtime.h>\n#include <cstdio>\n#include <cstring>\n#include <vector>\n']
     table = []
-    for form, mode, n, nm in names():
-        src.append(kernel(nm, form, n, mode))
+    for form, mode, n, g, nm in names():
+        kind = "valu" if mode.startswith("valu") else "salu" if mode.startswith("salu") else "nop"
+        src.append(kernel(nm, form, n, mode if mode in ("raw", "waw") else "raw", g, kind))
         exp = FORMS[form][5]
         table.append(f'  {{"{form}", "{mode}", {n}, {nm}, {exp}u}},')
+    for form, (mn, w, which) in VALU_FORMS.items():
+        exp = 0x41800000 if "16x16x16" in mn else 0x42000000  # K ones: 16.0 / 32.0
+        for g in VGAPS:
+            nm = f"hz_{form}_g{g}".replace("x", "X")
+            src.append(valu_kernel(nm, form, g))
+            table.append(f'  {{"{form}", "vgap", {g}, {nm}, {exp}u}},')
     src.append("""
 struct Case { const char* form; const char* mode; int n; void (*k)(unsigned*); unsigned exp; };
 static const Case cases[] = {
 """ + "\n".join(table) + """
 };
 int main(int argc, char** argv) {
-  const int blocks = 2048, reps = 8;
+  const int blocks = 512, reps = 4;
   unsigned* d;
   if (hipMalloc(&d, (size_t)blocks * 256 * 4 * 4) != hipSuccess) return 1;
   std::vector<unsigned> h((size_t)blocks * 256 * 4);
@@ -156,6 +234,26 @@ def run():
         sys.exit(r.returncode)
     rows = json.loads(r.stdout)
     summary = {}
+    for form in ("chain_32_then_16", "chain_16_then_32"):
+        for kind in ("valu", "salu"):
+            sel = [x for x in rows if x["form"] == form and x["mode"].startswith(kind) and x["threads"] == 64]
+            need = min([int(x["mode"][len(kind):]) for x in sel
+                        if all(sum(y["bad"]) == 0 for y in sel if int(y["mode"][len(kind):]) >= int(x["mode"][len(kind):]))]
+                       or [None])
+            summary[f"{form}/{kind}_fill"] = {x["mode"]: x["bad"] for x in sel}
+            print(f"{form:18s} {kind} fillers: clean from {need} ({[(x['mode'], x['bad']) for x in sel]})")
+    for form in VALU_FORMS:
+        sel = [x for x in rows if x["form"] == form and x["threads"] == 64]
+        for x in sel:
+            print(f"{form:20s} gap {x['n']:2d}: bad per component {x['bad']}")
+        summary[form] = {x["n"]: x["bad"] for x in sel}
+    for form in [f for f in FORMS if FORMS[f][6]]:
+        for g in GAPS:
+            sel = [x for x in rows if x["form"] == form and x["mode"] == f"gap{g}"]
+            clean = [x["n"] for x in sel if sum(x["bad"]) == 0]
+            bad01 = [x["n"] for x in sel if x["bad"][0] or x["bad"][1]]
+            summary[f"{form}/gap{g}"] = {"clean_reads_at_n": clean, "slots01_bad_at_n": bad01}
+            print(f"{form:18s} gap {g:2d}: reads clean at n = {clean}")
     for form in FORMS:
         for mode in ("raw", "waw"):
             sel = [x for x in rows if x["form"] == form and x["mode"] == mode]
