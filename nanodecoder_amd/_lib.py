@@ -116,8 +116,13 @@ def lib():
         raise NanodecError(f"{LIB_PATH} not found: build it with `python -m nanodecoder_amd.build` "
                            "(there is no CPU fallback)")
     L = ctypes.CDLL(LIB_PATH)
+    intree = os.path.realpath(LIB_PATH) == os.path.realpath(os.path.join(HERE, "libnanodec_hip.so"))
     for name, (res, args) in SIGNATURES.items():
-        fn = getattr(L, name)
+        fn = getattr(L, name, None)
+        if fn is None:
+            if intree:
+                raise NanodecError(f"{LIB_PATH} does not export {name}: rebuild it")
+            continue  # an older timing-variant library (NANODEC_LIB, A/B runs): entry points it lacks stay unbound
         fn.restype = res
         fn.argtypes = args
     _lib = L

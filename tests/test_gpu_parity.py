@@ -160,7 +160,8 @@ def test_gemm_p16_splitk_vs_fp64(M, N, K, res):
     Wh, sc = op_pack_p16h(W.to(dev))
     Ap = pack_p16(torch.cat([A, A.new_zeros((-M) % 16, K)]).to(dev))
     Rp = pack_p16(torch.cat([R, R.new_zeros((-M) % 16, N)]).to(dev)) if res else None
-    part_out = torch.full(((M + 15) // 16 * 16, 16, 2), float("nan"), device=dev)
+    # row partials are statistics of whole 256-wide rows (the next LayerNorm's); wider outputs have none
+    part_out = torch.full(((M + 15) // 16 * 16, 16, 2), float("nan"), device=dev) if N == 256 else None
     outs, tk = [], None
     for _ in range(3):
         Cp, pn, tk = op_gemm_p16_splitk(Ap, Wh, sc, b.to(dev), M, N, K, Rp, part_out, tickets=tk)
@@ -170,6 +171,8 @@ def test_gemm_p16_splitk_vs_fp64(M, N, K, res):
     assert all(torch.equal(outs[0], o) for o in outs[1:])
     ref = A.double() @ W.double().t() + b.double() + (R.double() if res else 0)
     assert (outs[0].double() - ref).abs().max().item() < 2e-4
+    if part_out is None:
+        return
     assert pn == N // 16
     want = row_partials(outs[0], pn)[:, :pn]
     got = part_out[:M, :pn].cpu()
