@@ -317,7 +317,7 @@ def kernel_roofline(eng, B, mode, beam, encoder="transformer", alive=None, secon
             # every lane's last call, each the same workload
             lanes = len(eng.engines) if hasattr(eng, "engines") else 1
             nbytes = int(3 * sum(alive) * per_chunk * lanes / n)
-            extra = {"alive_chunks_per_launch": round(3 * sum(alive) / n, 1)}
+            extra = {"alive_chunks_per_launch": round(3 * sum(alive) * lanes / n, 1)}
     ach = nbytes / (ms * 1e-3) / 1e9
     if mode == "greedy" and form == 2:
         # SURVEY.md §8(d) prices the context attention as fp32 K and V per layer (1,048,576 B per chunk per

@@ -121,6 +121,65 @@ def test_enc_ffn_fused_vs_fp64(M, F, wo):
         assert (qkv.cpu().double() - qref).abs().max().item() < 2e-4
 
 
+@pytest.mark.parametrize("M,F,ns", [(5120, 2048, 6), (1024, 2048, 8), (1040, 2048, 8), (1280, 512, 3),
+                                     (256, 2048, 1)])
+def test_dec_ffn_split_vs_fp64(M, F, ns):
+    """The beam decoder's fused FFN block (nd_op_dec_ffn: P16 rows, d_ff split
+    over ns workgroups per 128-row block, partials summed in split order by the
+    block's last arriver) against fp64 within the split GEMMs' 2e-4; the exact
+    row statistics; three launches on the same tickets bitwise equal and the
+    tickets back at zero; a ragged last row block (M = 1040); and with a skip
+    vector the row blocks whose chunks are all done left untouched (rows of a
+    live block computed whole)."""
+    from nanodecoder_amd.engine import op_dec_ffn, pack_p16, unpack_p16
+    g = torch.Generator().manual_seed(M + F + ns)
+    y = torch.randn(M, 256, generator=g) * 2 + 0.5
+    W1 = torch.randn(F, 256, generator=g) / 16
+    b1 = torch.randn(F, generator=g) * 0.1
+    W2 = torch.randn(256, F, generator=g) / F ** 0.5
+    b2 = torch.randn(256, generator=g) * 0.1
+    lg = 1 + 0.1 * torch.randn(256, generator=g)
+    lb = 0.1 * torch.randn(256, generator=g)
+    dev = torch.device("cuda", 0)
+    yp = pack_p16(y.to(dev))
+    args = [t.to(dev) for t in (W1, b1, W2, b2, lg, lb)]
+    outs, tk = [], None
+    for _ in range(3):
+        x, st, ov, tk = op_dec_ffn(yp, *args, ns, tickets=tk)
+        torch.cuda.synchronize()
+        assert int(tk.abs().sum().item()) == 0
+        outs.append(unpack_p16(x, M).cpu())
+    assert all(torch.equal(outs[0], o) for o in outs[1:])
+    yd = y.double()
+    h = torch.relu(torch.nn.functional.layer_norm(yd, (256,), lg.double(), lb.double(), 1e-6) @ W1.double().t()
+                   + b1.double())
+    ref = yd + h @ W2.double().t() + b2.double()
+    got = outs[0].double()
+    assert (got - ref).abs().max().item() < 2e-4
+    st = st[:M].cpu().double()
+    assert torch.allclose(st[:, 0], got.mean(1), atol=1e-5)
+    assert torch.allclose(st[:, 1], ((got - got.mean(1, keepdim=True)) ** 2).sum(1), rtol=1e-4, atol=1e-3)
+    assert int(ov.cpu()[0]) == 0
+    if M >= 1024:
+        # beam rows: 5 per chunk; every chunk of row block 1 done, one chunk of row block 2 alive
+        rpc = 5
+        done = torch.ones((M + rpc - 1) // rpc, dtype=torch.int32)
+        done[: 128 // rpc] = 0
+        done[(2 * 128 + 40) // rpc] = 0
+        done[(3 * 128) // rpc:] = 0
+        x2, _, _, tk = op_dec_ffn(yp, *args, ns, skip=done.to(dev), skip_rpc=rpc, tickets=tk)
+        torch.cuda.synchronize()
+        assert int(tk.abs().sum().item()) == 0
+        got2 = unpack_p16(x2, M).cpu()
+        dead = torch.zeros(M, dtype=torch.bool)
+        for rb in range((M + 127) // 128):
+            r0, r1 = rb * 128, min(M, rb * 128 + 128)
+            dead[r0:r1] = bool(done[r0 // rpc:(r1 - 1) // rpc + 1].all())
+        assert dead[128:256].all() and not dead[256:384].any()
+        assert torch.isnan(got2[dead]).all()  # untouched (op_dec_ffn fills x with NaN)
+        assert torch.equal(got2[~dead], outs[0][~dead])
+
+
 @pytest.mark.parametrize("N,K,mag", [(256, 256, 1.0), (768, 256, 3e-4), (256, 2048, 40.0)])
 def test_split_weight_image(N, K, mag):
     """nd_op_split_weight: hi + lo reproduces W * 2^s to 2^-21 relative (half
@@ -1204,7 +1263,7 @@ def test_cli_gpu_frontend_matches_host(tmp_path):
                                            "0", "-beam_size", "1", "-batch_size", str(bs), "-thread", "2",
                                            "-max_length", str(S), "-min_length", "4", "-engine_max_batch", "8",
                                            "-frontend", m])
-            assert o.engine_lanes == 3
+            assert o.engine_lanes == 0  # auto: 3 lanes for a greedy translator (the spy below checks)
             assert cli.main(o) == len(raws)
             outs[m] = {name: ((out / "segment" / f"{name}.txt").read_text(),
                               (out / "result" / f"{name}.fasta").read_text()) for name in raws}
