@@ -358,6 +358,19 @@ int nd_op_pack_p16h(const float* W, int32_t N, int32_t K, uint16_t* out, float* 
  * hidden value leaves the fp16 range. */
 int nd_op_enc_ffn(const float* y, const uint16_t* w1h, float w1s, const float* b1, const uint16_t* w2h, float w2s,
                   const float* b2, float* x, float* xpart, int32_t M, int32_t F, int32_t* overflow, void* stream);
+/* The same block over the beam's decoder rows (decoder/transformer.py:92,
+ * position_ffn.py:27-40): y and x P16-packed [M, 256] (M % 16 == 0, x != y),
+ * the d_ff walk split over nsplit workgroups per 128-row block whose partial
+ * sums meet in slab (nd_op_dec_ffn_slab_floats(M, nsplit) floats) and are
+ * added in split order by the block's last workgroup (tickets: one int per
+ * row block, zero before the launch and zero again after it).  skip
+ * (nullable): per chunk of skip_rpc rows, nonzero = finished; a row block of
+ * finished chunks is left as it was.  xpart: each row's {mean, M2} in one
+ * partial.  Replaces the FFN1 + FFN2 GEMM pair of nd_translate_beam*'s step. */
+int nd_op_dec_ffn(const float* y, const uint16_t* w1h, float w1s, const float* b1, const uint16_t* w2h, float w2s,
+                  const float* b2, float* x, float* xpart, int32_t M, int32_t F, int32_t nsplit, float* slab,
+                  int32_t* tickets, const int32_t* skip, int32_t skip_rpc, int32_t* overflow, void* stream);
+int64_t nd_op_dec_ffn_slab_floats(int32_t M, int32_t nsplit);
 /* The same block with the attention's output projection folded in front
  * (encoder/transformer.py:45-54, one launch for the rest of the layer):
  * y = x_in + att Wo^T + bo, then x = y + W2 relu(W1' LN(y) + b1') + b2.

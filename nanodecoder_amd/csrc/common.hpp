@@ -165,6 +165,17 @@ __device__ __forceinline__ float ln_rsqrt(float x) { return __builtin_amdgcn_rsq
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
 
+// --fast beam: every row of [r0, r0 + n) (rows < M) belongs to a finished
+// chunk (skip[row / rpc] != 0).  Wave-uniform; each wave of a workgroup
+// computes the same answer, so a dead tile returns before any barrier.
+__device__ __forceinline__ bool rows_dead(const int* __restrict__ skip, int rpc, int r0, int n, int M) {
+  if (skip == nullptr) return false;
+  const int c0 = r0 / rpc, c1 = (min(r0 + n, M) - 1) / rpc;
+  bool alive = false;
+  for (int c = c0 + (int)(threadIdx.x & 63); c <= c1; c += 64) alive |= skip[c] == 0;
+  return __ballot(alive) == 0;
+}
+
 // Split-fp16 range guard.  An activation split as hi = fp16(x), lo =
 // fp16(x - hi) leaves the fp16 range from |x| = 65504 on (hi becomes inf
 // where the fp32 reference is finite).  Every kernel that splits an

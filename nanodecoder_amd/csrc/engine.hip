@@ -183,6 +183,9 @@ struct nd_ctx {
   float* sk_slab = nullptr;               // split-K P16 GEMMs: fp32 partial slabs (gemm_p16k_kernel)
   int* sk_cnt = nullptr;                  // ... and their per-tile tickets (zeroed per call)
   int sk_tiles = 0;                       // 32 x 32 tiles the slab serves
+  float* dffn_slab = nullptr;             // beam rows' split fused FFN (ffn.hip DecFfn): partial slabs
+  int* dffn_cnt = nullptr;                // ... and per-row-block tickets (zeroed per call)
+  int dffn_rb = 0;                        // 128-row blocks they serve
   // average self-attention step buffers (P16): xn, avg (+ its row stats), the
   // average_layer hidden, a = FFN(avg), the gate pre-activations [R, 512]
   float *axn = nullptr, *aavg = nullptr, *aavg_part = nullptr, *ah = nullptr, *aa = nullptr, *ag = nullptr;
@@ -396,6 +399,17 @@ static int alloc_ctx_kv(nd_ctx* c) {
   c->clist = reinterpret_cast<int*>(l);
   // ceil(B/16) listed chunks x up to 32 splits x rows x {num[256], max[8], den[8]}
   WSK(c->ctx_part, (B + 15) / 16 * 32 * std::max(1, cfg.max_beam) * (D + 16));
+  {
+    // the beam's split fused FFN: up to 8 splits per 128-row block
+    const int R = (int)((B * (size_t)std::max(1, cfg.max_beam) + 15) / 16 * 16);
+    c->dffn_rb = (R + 127) / 128;
+    WSK(c->dffn_slab, nd::dec_ffn_slab_floats(R, 8));
+    float* t = nullptr;
+    WSK(t, (size_t)(c->dffn_rb + 3) / 4 * 4);
+    c->dffn_cnt = reinterpret_cast<int*>(t);
+    if ((e = hipMemset(c->dffn_cnt, 0, (size_t)(c->dffn_rb + 3) / 4 * 16)) != hipSuccess)
+      return fail(ND_ERR_HIP, std::string("hipMemset FFN tickets: ") + hipGetErrorString(e));
+  }
 #undef WSK
   return ND_OK;
 }
@@ -811,6 +825,27 @@ static void set_memory_view(nd_ctx* c, int T, int rpc) {
   c->last_bank_form = c->bank_d8 ? 2 : 0;
 }
 
+// The beam's decoder FFN as one fused launch (ffn.hip launch_dec_ffn) at
+// R >= 1024 rows outside the tail: d_ff split so that about 256 workgroups
+// (one per CU, 128 KB of LDS each) run at once, at most 8 splits per row
+// block (the last arriver reads the others' 128 KB partials).  0: the two
+// GEMMs (greedy rows, the tail, exact fp32, no split images).
+// ND_DEC_FFN=0 keeps the GEMMs, ND_DEC_FFN=n > 1 forces n splits (A/B).
+static int dec_ffn_splits(const nd_ctx* c, int R) {
+  static const int knob = [] {
+    const char* e = getenv("ND_DEC_FFN");
+    return e ? atoi(e) : 1;
+  }();
+  if (knob == 0 || c->exact || c->beam_tail || !c->dffn_slab || R < 1024 || R % 16 || nd::gemm_f32_forced()) return 0;
+  const int F = c->F;
+  const DecLayer& L = c->dec[0];
+  if (F % 32 || F > 2048 || !c->split.count(L.pw1) || !c->split.count(L.pw2)) return 0;
+  const int rb = (R + 127) / 128;
+  if (rb > c->dffn_rb) return 0;
+  if (knob > 1) return std::min({knob, 8, F / 32});
+  return std::max(1, std::min({8, 256 / rb, F / 32}));
+}
+
 // done: per chunk, nonzero = finished (--fast beam; null otherwise): its rows'
 // tiles and attention workgroups exit without work
 static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, const int* anc, int anc_ld,
@@ -886,8 +921,22 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
                                           false, clist, ccap, ctx_split(), c->ctx_part));
       LCHK(dg(c->datt, D, L.pcwo, D, D, L.cbo, c->dmid, D).res(c->dq1, D).stats(c->dmid_part).run(s, &pnm));
     }
-    LCHK(dg(c->dmid, D, L.pw1, F, D, L.nb1, c->dhid, F).ln(c->dmid_part, pnm).relu().run(s));
-    LCHK(dg(c->dhid, F, L.pw2, D, F, L.b2, c->dx, D).res(c->dmid, D).stats(c->dx_part).run(s, &pnx));
+    if (const int ns = dec_ffn_splits(c, R)) {  // beam rows: the fused block, hidden on chip (ffn.hip)
+      const auto& i1 = c->split.at(L.pw1);
+      const auto& i2 = c->split.at(L.pw2);
+      nd::DecFfn df;
+      df.nsplit = ns;
+      df.slab = c->dffn_slab;
+      df.tickets = c->dffn_cnt;
+      df.skip = done;
+      df.skip_rpc = rpc;
+      LCHK(nd::launch_dec_ffn(c->dmid, i1.first, i1.second, L.nb1, i2.first, i2.second, L.b2, c->dx, c->dx_part, R, F,
+                              c->ovf, df, s));
+      pnx = 1;  // each row's exact statistics in one partial
+    } else {
+      LCHK(dg(c->dmid, D, L.pw1, F, D, L.nb1, c->dhid, F).ln(c->dmid_part, pnm).relu().run(s));
+      LCHK(dg(c->dhid, F, L.pw2, D, F, L.b2, c->dx, D).res(c->dmid, D).stats(c->dx_part).run(s, &pnx));
+    }
   }
   return hipSuccess;
 }
@@ -1710,7 +1759,8 @@ static const struct {
   const char* name;
   int def;
 } kSwitches[] = {{"ND_GEMM_F32", 0},  {"ND_ENC_ATTN_F32", 0}, {"ND_LSTM_F32", 0},
-                 {"ND_ENC_ATTN0", 1}, {"ND_BEAM_COMPACT", 1}, {"ND_CTX_SPLIT", 16}};
+                 {"ND_ENC_ATTN0", 1}, {"ND_BEAM_COMPACT", 1}, {"ND_CTX_SPLIT", 16},
+                 {"ND_DEC_FFN", 1}};
 
 int nd_switches(char* buf, int32_t len) {
   std::string out;
@@ -1875,6 +1925,25 @@ int nd_op_gemm_split_q24(const float* A, const uint16_t* Wh, float wscale, const
 static int ensure_attributes() {
   static hipError_t e = nd::init_kernel_attributes();
   return e == hipSuccess ? ND_OK : fail(ND_ERR_HIP, "hipFuncSetAttribute failed");
+}
+
+int nd_op_dec_ffn(const float* y, const uint16_t* w1h, float w1s, const float* b1, const uint16_t* w2h, float w2s,
+                  const float* b2, float* x, float* xpart, int32_t M, int32_t F, int32_t nsplit, float* slab,
+                  int32_t* tickets, const int32_t* skip, int32_t skip_rpc, int32_t* overflow, void* stream) {
+  if (int rc = ensure_attributes()) return rc;
+  nd::DecFfn df;
+  df.nsplit = nsplit;
+  df.slab = slab;
+  df.tickets = tickets;
+  df.skip = skip;
+  df.skip_rpc = skip_rpc;
+  hipError_t e = nd::launch_dec_ffn(y, w1h, w1s, b1, w2h, w2s, b2, x, xpart, M, F, overflow, df, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("dec_ffn: ") + hipGetErrorString(e));
+  return ND_OK;
+}
+
+int64_t nd_op_dec_ffn_slab_floats(int32_t M, int32_t nsplit) {
+  return M > 0 && nsplit > 0 ? (int64_t)nd::dec_ffn_slab_floats(M, nsplit) : 0;
 }
 
 int nd_op_gemm_p16(const float* A, const float* W, const float* bias, const float* R, float* C, int32_t M,
@@ -2145,6 +2214,7 @@ static hipError_t enqueue_encode(nd_ctx* c, int B, int T, hipStream_t s) {
   // arriver resets its own, this repairs a ticket left by an aborted call (cdna_hip_programming.md §6,
   // Guideline 16 "Re-initialise every call")
   if (c->sk_cnt) LCHK(hipMemsetAsync(c->sk_cnt, 0, (size_t)(c->sk_tiles + 3) / 4 * 16, s));
+  if (c->dffn_cnt) LCHK(hipMemsetAsync(c->dffn_cnt, 0, (size_t)(c->dffn_rb + 3) / 4 * 16, s));
   if (c->cfg.encoder_type == ND_ENC_TRANSFORMER) return enqueue_encode_transformer(c, B, T, s);
   return enqueue_encode_nano(c, B, T, s);
 }

@@ -104,6 +104,15 @@ __device__ __forceinline__ void ff_wait(f32x4 (&rh)[RING], f32x4 (&rl)[RING]) {
   asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(rh[U % RING]), "+v"(rl[U % RING]) : "n"(2 * left));
 }
 
+// write-through (sc1) slab store / load of the split form (as gemm.hip's split-K)
+typedef unsigned ffu4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void ff_store_sc1(__amdgpu_buffer_rsrc_t r, int off, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ffu4, v), r, off, 0, 16);  // aux 16 = sc1
+}
+__device__ __forceinline__ f32x4 ff_load_sc1(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16));
+}
+
 __device__ __forceinline__ void ff_split(f32x4 x0, f32x4 x1, fh8& hi, fh8& lo) {
   hi = {(_Float16)x0.x, (_Float16)x0.y, (_Float16)x0.z, (_Float16)x0.w,
         (_Float16)x1.x, (_Float16)x1.y, (_Float16)x1.z, (_Float16)x1.w};
@@ -164,15 +173,22 @@ __device__ __forceinline__ void ff_copy_w2(ff_src w2h, int kp, int j, char* dst,
 // WO: y is the block's residual input (the layer input x; x may alias it:
 // a workgroup reads its rows before it writes them), att the attention
 // output.  !WO: y is the FFN's input.
-template <int RG, bool WO, bool QK>
+// DEC (launch_dec_ffn, kernels.hpp DecFfn): y and x P16-packed, the d_ff
+// chunks of split blockIdx.y only, the splits' partial accumulators summed by
+// the row block's last workgroup (no WO / QK fold).
+template <int RG, bool WO, bool QK, bool DEC>
 __global__ void __launch_bounds__(FF_BM / (16 * RG) * 64)
 enc_ffn_kernel(const float* y, const uint16_t* __restrict__ w1h, float w1s, const float* __restrict__ b1,
                const uint16_t* __restrict__ w2h, float w2s, const float* __restrict__ b2, float* x,
-               float* __restrict__ xpart, int M, int F, int* ovf, EncWo wo, EncQkv qk) {
+               float* __restrict__ xpart, int M, int F, int* ovf, EncWo wo, EncQkv qk, DecFfn df) {
 #ifdef ND_SKIP_FFN  // timing probe only (tools/build_variant.sh): the kernel's marginal cost
   if (threadIdx.x < 100000) return;
 #endif
+  static_assert(!DEC || (!WO && !QK && RG == 1), "the decoder form folds nothing");
   constexpr int NW = FF_BM / (16 * RG), NT = NW * 64;
+  // every split of a dead row block exits alike (its ticket stays 0)
+  if constexpr (DEC)
+    if (rows_dead(df.skip, df.skip_rpc, blockIdx.x * FF_BM, FF_BM, M)) return;
   // ONE shared array (a second __shared__ object beside LDS-DMA staging can
   // make hipcc drain vmcnt before every ds_read)
   __shared__ __attribute__((aligned(16))) char smem[4 * FF_SLICE + (FF_MAXF + ND_D + (QK ? 3 * ND_D : 0)) * 4];
@@ -184,12 +200,18 @@ enc_ffn_kernel(const float* y, const uint16_t* __restrict__ w1h, float w1s, cons
   float* sqb = sb2 + ND_D;  // (QK) the next layer's q | k | v bias
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, q = lane >> 4;
-  const int nch = F / FF_HC, kp = F / 32;
-  const ff_src W1 = ff_source(w1h), W2 = ff_source(w2h);
+  // this workgroup's d_ff chunks c0 .. c0 + nch - 1 (DEC: split sp of nsplit;
+  // a chunk's W1 slice and W2 k-block sit at fixed strides in the images, so
+  // the split offsets the bases; kp stays the whole W2 image's k-pair count)
+  const int nall = F / FF_HC, kp = F / 32;
+  const int sp = DEC ? (int)blockIdx.y : 0;
+  const int c0 = DEC ? sp * nall / df.nsplit : 0;
+  const int nch = DEC ? (sp + 1) * nall / df.nsplit - c0 : nall;
+  const ff_src W1 = ff_source(w1h + (size_t)c0 * (FF_SLICE / 2)), W2 = ff_source(w2h + (size_t)c0 * 1024);
 
   // biases (ordinary loads: done before the first copy is issued, so no wait
   // on them later drains an in-flight copy)
-  for (int i = tid; i < F; i += NT) sb1[i] = b1[i];
+  for (int i = tid; i < nch * FF_HC; i += NT) sb1[i] = b1[c0 * FF_HC + i];
   for (int i = tid; i < ND_D; i += NT) sb2[i] = b2[i];
   if constexpr (QK)
     for (int i = tid; i < 3 * ND_D; i += NT) sqb[i] = qk.bias[i];
@@ -310,14 +332,24 @@ enc_ffn_kernel(const float* y, const uint16_t* __restrict__ w1h, float w1s, cons
   } else {
 #pragma unroll
     for (int g = 0; g < RG; ++g) {
-      const float* yr = y + (size_t)min(row[g], M - 1) * ND_D + 4 * q;
+      const int rc = min(row[g], M - 1);
+      const float* yr = y + (size_t)rc * ND_D + 4 * q;
       f32x4 ya[8], yb[8];
 #pragma unroll
       for (int kb = 0; kb < 8; ++kb) {
-        ya[kb] = ld4(yr + 32 * kb);
-        yb[kb] = ld4(yr + 32 * kb + 16);
+        if constexpr (DEC) {
+          ya[kb] = ld4(y + pk(rc, 32 * kb + 4 * q, ND_D));
+          yb[kb] = ld4(y + pk(rc, 32 * kb + 16 + 4 * q, ND_D));
+        } else {
+          ya[kb] = ld4(yr + 32 * kb);
+          yb[kb] = ld4(yr + 32 * kb + 16);
+        }
       }
       ln_split(g, ya, yb, b2);
+      if constexpr (DEC)
+        if (sp > 0)  // b2 and the residual enter once, through split 0
+#pragma unroll
+          for (int nt = 0; nt < 16; ++nt) acc[g][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
     __syncthreads();  // the biases in LDS (and every ordinary load retired)
     ff_copy_w1<NW>(W1, 0, w1slot(0), wave, lane);
@@ -425,6 +457,44 @@ enc_ffn_kernel(const float* y, const uint16_t* __restrict__ w1h, float w1s, cons
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   flag_overflow(ovf, hmax);
+  if constexpr (DEC) {
+    if (df.nsplit > 1) {
+      // the row block's slab [split][16 tiles][NT threads] f32x4: write-through
+      // (sc1) stores, every wave's vmcnt(0), one agent-scope ticket; the last
+      // arriver reads the other splits back with sc1 loads and sums all of
+      // them in split order (its own from registers: the same bits it stored)
+      const int S = df.nsplit;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          df.slab + (size_t)blockIdx.x * S * 16 * NT * 4, 0, S * 16 * NT * 16, 0x00020000);
+#pragma unroll
+      for (int nt = 0; nt < 16; ++nt) ff_store_sc1(rs, ((sp * 16 + nt) * NT + tid) * 16, acc[0][nt]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      int* tword = reinterpret_cast<int*>(sb2);  // (b2 came from global memory: the slot is free)
+      if (tid == 0) tword[0] = __hip_atomic_fetch_add(df.tickets + blockIdx.x, 1, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      if (tword[0] != S - 1) return;  // not the row block's last split
+      f32x4 sum[16];
+#pragma unroll
+      for (int nt = 0; nt < 16; ++nt) sum[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int s2 = 0; s2 < S; ++s2) {
+        if (s2 == sp) {
+#pragma unroll
+          for (int nt = 0; nt < 16; ++nt) sum[nt] += acc[0][nt];
+        } else {
+          f32x4 pp[16];
+#pragma unroll
+          for (int nt = 0; nt < 16; ++nt) pp[nt] = ff_load_sc1(rs, ((s2 * 16 + nt) * NT + tid) * 16);
+#pragma unroll
+          for (int nt = 0; nt < 16; ++nt) sum[nt] += pp[nt];
+        }
+      }
+#pragma unroll
+      for (int nt = 0; nt < 16; ++nt) acc[0][nt] = sum[nt];
+      if (tid == 0) __hip_atomic_store(df.tickets + blockIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 
   // ---- epilogue: x = out * w2s (b2 and the residual were the accumulators'
   //      initial value), and the row's exact statistics
@@ -451,7 +521,12 @@ enc_ffn_kernel(const float* y, const uint16_t* __restrict__ w1h, float w1s, cons
     if (row[g] < M) {
       float* xr = x + (size_t)row[g] * ND_D + 4 * q;
 #pragma unroll
-      for (int nt = 0; nt < 16; ++nt) st4(xr + 16 * nt, o[nt]);
+      for (int nt = 0; nt < 16; ++nt) {
+        if constexpr (DEC)
+          st4(x + pk(row[g], 16 * nt + 4 * q, ND_D), o[nt]);
+        else
+          st4(xr + 16 * nt, o[nt]);
+      }
       if (q == 0 && xpart) {
         float* p = xpart + (size_t)row[g] * ND_PART_LD * 2;
         p[0] = m2;
@@ -514,8 +589,8 @@ hipError_t launch_enc_ffn(const float* y, const uint16_t* w1h, float w1s, const 
   const EncWo w = wo ? *wo : EncWo();
   const EncQkv k = qk ? *qk : EncQkv();
 #define ND_FFN_GO(WO, QK)                                                                                          \
-  hipLaunchKernelGGL((enc_ffn_kernel<1, WO, QK>), grid, block, 0, s, y, w1h, w1s, b1, w2h, w2s, b2, x, xpart, M, F, \
-                     ovf, w, k)
+  hipLaunchKernelGGL((enc_ffn_kernel<1, WO, QK, false>), grid, block, 0, s, y, w1h, w1s, b1, w2h, w2s, b2, x, xpart, \
+                     M, F, ovf, w, k, DecFfn())
   if (wo && qk)
     ND_FFN_GO(true, true);
   else if (wo)
@@ -525,6 +600,25 @@ hipError_t launch_enc_ffn(const float* y, const uint16_t* w1h, float w1s, const 
   else
     ND_FFN_GO(false, false);
 #undef ND_FFN_GO
+  return hipGetLastError();
+}
+
+size_t dec_ffn_slab_floats(int M, int nsplit) {
+  return (size_t)((M + FF_BM - 1) / FF_BM) * nsplit * 16 * (FF_BM / 16 * 64) * 4;
+}
+
+hipError_t launch_dec_ffn(const float* y, const uint16_t* w1h, float w1s, const float* b1, const uint16_t* w2h,
+                          float w2s, const float* b2, float* x, float* xpart, int M, int F, int* ovf,
+                          const DecFfn& df, hipStream_t s) {
+  if (M <= 0) return hipSuccess;
+  if (F % FF_HC != 0 || F > FF_MAXF || F < FF_HC || M % 16 || !y || !w1h || !b1 || !w2h || !b2 || !x || x == y)
+    return hipErrorInvalidValue;
+  if (df.nsplit < 1 || df.nsplit > F / FF_HC || (df.nsplit > 1 && (!df.slab || !df.tickets)) ||
+      (df.skip && df.skip_rpc < 1))
+    return hipErrorInvalidValue;
+  const dim3 grid((M + FF_BM - 1) / FF_BM, df.nsplit), block(FF_BM / 16 * 64);
+  hipLaunchKernelGGL((enc_ffn_kernel<1, false, false, true>), grid, block, 0, s, y, w1h, w1s, b1, w2h, w2s, b2, x,
+                     xpart, M, F, ovf, EncWo(), EncQkv(), df);
   return hipGetLastError();
 }
 

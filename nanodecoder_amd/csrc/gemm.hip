@@ -90,16 +90,6 @@ __device__ __forceinline__ void merge_stats(const float* __restrict__ p, int P, 
   merge_loaded(v, P, mu, rs);
 }
 
-// --fast beam: every row of [r0, r0 + n) (rows < M) belongs to a finished
-// chunk (skip[row / rpc] != 0).  Wave-uniform; each wave of a workgroup
-// computes the same answer, so a dead tile returns before any barrier.
-__device__ __forceinline__ bool rows_dead(const int* __restrict__ skip, int rpc, int r0, int n, int M) {
-  if (skip == nullptr) return false;
-  const int c0 = r0 / rpc, c1 = (min(r0 + n, M) - 1) / rpc;
-  bool alive = false;
-  for (int c = c0 + (int)(threadIdx.x & 63); c <= c1; c += 64) alive |= skip[c] == 0;
-  return __ballot(alive) == 0;
-}
 
 // Sum over aligned groups of TPR lanes (16, 32 or the whole wave).
 template <int TPR>

@@ -171,6 +171,24 @@ struct EncQkv {
 hipError_t launch_enc_ffn(const float* y, const uint16_t* w1h, float w1s, const float* b1, const uint16_t* w2h,
                           float w2s, const float* b2, float* x, float* xpart, int M, int F, int* ovf, hipStream_t s,
                           const EncWo* wo = nullptr, const EncQkv* qk = nullptr);
+// The same block for the beam's decoder rows (P16-packed y and x, the layer's
+// position_ffn.py:27-40 at decoder/transformer.py:92): the d_ff walk split
+// over nsplit workgroups per 128-row block (blockIdx.y), whose partial
+// accumulators meet in an fp32 slab; the workgroup that draws a row block's
+// last ticket sums them in split order (deterministic), adds nothing else
+// (b2 and the residual are split 0's initial value) and writes x and the
+// rows' exact statistics.  Row blocks whose chunks are all done (skip) exit.
+struct DecFfn {
+  int nsplit = 1;
+  float* slab = nullptr;    // [row block][split][16 tiles][512 threads] f32x4
+  int* tickets = nullptr;   // [row block], zero between launches
+  const int* skip = nullptr;
+  int skip_rpc = 1;
+};
+size_t dec_ffn_slab_floats(int M, int nsplit);
+hipError_t launch_dec_ffn(const float* y, const uint16_t* w1h, float w1s, const float* b1, const uint16_t* w2h,
+                          float w2s, const float* b2, float* x, float* xpart, int M, int F, int* ovf,
+                          const DecFfn& df, hipStream_t s);
 // out[r] = LN(x[r]) (rows of 256)
 hipError_t launch_layernorm(const float* x, const float* g, const float* b, float* out, int rows, hipStream_t s);
 

@@ -545,6 +545,32 @@ def op_enc_ffn(y, W1, b1, W2, b2, ln_g, ln_b, att=None, Wo=None, bo=None, inplac
     return x, part[:, 0, :], ov
 
 
+def op_dec_ffn(yp, W1, b1, W2, b2, ln_g, ln_b, nsplit, skip=None, skip_rpc=1, tickets=None, slab=None):
+    """The beam decoder's fused FFN block (nd_op_dec_ffn) on P16-packed rows
+    yp [M16, 256] (M16 % 16 == 0): x = y + W2 relu(W1 LN(y) + b1) + b2 with d_ff
+    split over nsplit workgroups per 128-row block.  Weights folded / packed
+    here as the engine does at load time.  Returns (x packed, row stats
+    [M16, 2] = {mean, M2}, overflow flag, tickets) -- pass the tickets back
+    to reuse them (zero between launches)."""
+    M, F = yp.shape[0], W1.shape[0]
+    W1f, b1f = op_fold_layernorm(W1, b1, ln_g, ln_b)
+    w1h, w1s = op_pack_p16h(W1f)
+    w2h, w2s = op_pack_p16h(W2)
+    x = torch.full_like(yp, float("nan"))
+    part = torch.zeros(M, 16, 2, dtype=torch.float32, device=yp.device)
+    ov = torch.zeros(1, dtype=torch.int32, device=yp.device)
+    if tickets is None:
+        tickets = torch.zeros((M + 127) // 128, dtype=torch.int32, device=yp.device)
+    if slab is None:
+        n = int(_lib.lib().nd_op_dec_ffn_slab_floats(M, nsplit))
+        slab = torch.empty(max(n, 1), dtype=torch.float32, device=yp.device)
+    s = ctypes.c_void_p(torch.cuda.current_stream(yp.device).cuda_stream)
+    _lib.check(_lib.lib().nd_op_dec_ffn(_ptr(yp), _ptr(w1h), w1s, _ptr(b1f), _ptr(w2h), w2s, _ptr(b2), _ptr(x),
+                                        _ptr(part), M, F, nsplit, _ptr(slab), _ptr(tickets), _ptr(skip), skip_rpc,
+                                        _ptr(ov), s), "nd_op_dec_ffn")
+    return x, part[:, 0, :], ov, tickets
+
+
 def op_gemm_p16(Ap, Wp, bias, M, N, K, Rp=None, part_in=None, relu=False, part_out=None, Wh=None, wscale=1.0,
                 Wh_rm=None, wscale_rm=1.0):
     """The decoder-step GEMM on packed operands (see pack_p16).  Returns the
