@@ -826,10 +826,14 @@ static void set_memory_view(nd_ctx* c, int T, int rpc) {
 }
 
 // The beam's decoder FFN as one fused launch (ffn.hip launch_dec_ffn) at
-// R >= 1024 rows outside the tail: d_ff split so that about 256 workgroups
+// R >= 1024 rows outside the tail: d_ff split so that about 160 workgroups
 // (one per CU, 128 KB of LDS each) run at once, at most 8 splits per row
-// block (the last arriver reads the others' 128 KB partials).  0: the two
-// GEMMs (greedy rows, the tail, exact fp32, no split images).
+// block (the last arriver reads the others' 128 KB partials).  Measured at
+// R = 5120 (40 row blocks, configs[3], same box, two reps each): 3 / 4 / 5 /
+// 6 / 8 splits = 70.3-71.0 / 70.1-70.6 / 71.8-72.0 / 71.0-71.2 / 71.4-72.0 ms
+// per pooled call (one call: 89.5 / 88.2 / 87.2 / 87.0 / 91.1 ms); the two
+// GEMMs 74.0 / 92.6.  0: the two GEMMs (greedy rows, the tail, exact fp32,
+// no split images).
 // ND_DEC_FFN=0 keeps the GEMMs, ND_DEC_FFN=n > 1 forces n splits (A/B).
 static int dec_ffn_splits(const nd_ctx* c, int R) {
   static const int knob = [] {
@@ -843,7 +847,7 @@ static int dec_ffn_splits(const nd_ctx* c, int R) {
   const int rb = (R + 127) / 128;
   if (rb > c->dffn_rb) return 0;
   if (knob > 1) return std::min({knob, 8, F / 32});
-  return std::max(1, std::min({8, 256 / rb, F / 32}));
+  return std::max(1, std::min({8, 160 / rb, F / 32}));
 }
 
 // done: per chunk, nonzero = finished (--fast beam; null otherwise): its rows'
