@@ -164,15 +164,24 @@ def test_mfma_hazard_scanner_finds_known_violations():
     assert H.scan(chain)["_Zfoo"] == []
     assert len(H.scan(mixed)["_Zfoo"]) == 1
     assert H.scan(mixed_far)["_Zfoo"] == []
+    # a VALU result read by the next MFMA: as srcC 0 states apart (needs 1), as srcA 1 apart (needs 2)
+    valu_c = fn("\tv_mul_f32_e32 v1, 2.0, v1\n" + mf)
+    valu_c_ok = fn("\tv_mul_f32_e32 v1, 2.0, v1\n\ts_nop 0\n" + mf)
+    valu_a = fn("\tv_mov_b32_e32 v5, v40\n\ts_nop 0\n" + mf)
+    valu_a_ok = fn("\tv_mov_b32_e32 v5, v40\n\ts_nop 1\n" + mf)
+    one = lambda a: H.scan_valu_to_mfma(*H.parse(a)["_Zfoo"])
+    assert len(one(valu_c)) == 1 and one(valu_c_ok) == []
+    assert len(one(valu_a)) == 1 and one(valu_a_ok) == []
 
 
 def test_mfma_results_respect_wait_states(listings):
     """Every MFMA of every shipped kernel, on every path: no instruction
     reads or writes its destination registers inside the required wait
-    states.  Covers dec_bank_d8_kernel's lazy-rescale branch (bank8.hip,
-    `if (__any(gm > m + B8_THR))` over the U accumulators) and every other
-    MFMA consumer; the context attention's online_update_lazy runs on VALU
-    accumulators (no MFMA there)."""
+    states, and no MFMA reads a VALU result as an operand inside the probed
+    window (srcC 1 state, srcA / srcB 2).  Covers dec_bank_d8_kernel's
+    lazy-rescale branch (bank8.hip, `if (__any(gm > m + B8_THR))` over the U
+    accumulators) and every other MFMA consumer; the context attention's
+    online_update_lazy runs on VALU accumulators (no MFMA there)."""
     H = _isa_hazard()
     total, bad = 0, {}
     for name, path in listings.items():
@@ -181,6 +190,10 @@ def test_mfma_results_respect_wait_states(listings):
         for k, hz in H.scan(asm).items():
             if hz:
                 bad[k] = hz[:3]
+        for k, (ins, labels) in H.parse(asm).items():
+            vm = H.scan_valu_to_mfma(ins, labels)
+            if vm:
+                bad[k + " (VALU->MFMA)"] = vm[:3]
     assert total > 1000, total  # the scan saw the kernels' MFMAs
     assert not bad, bad
     d8 = H.count_mfma(open(listings["bank8"]).read(), r"dec_bank_d8_kernel")

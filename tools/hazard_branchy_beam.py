@@ -5,8 +5,9 @@ Rebuilds the two-phase dec_bank_d8_beam_kernel from git history (the last
 commit that shipped it), puts back the branch around its accumulator rescale
 that round 4 saw return wrong components 0-1 of the second dim block, compiles
 both forms for gfx950 and reports, per form, every instruction that reads or
-writes a 16x16x16_f16 MFMA's destination within 24 wait states of it
-(tools/isa_hazard.py's walk over all paths).  CPU only; no GPU run.
+writes a 16x16x16_f16 MFMA's destination within 24 wait states of it, and
+every MFMA of another form that accumulates onto an MFMA's destination within
+isa_hazard.MIXED_SRCC states (tools/isa_hazard.py's walk over all paths).  CPU only; no GPU run.
 
     python tools/hazard_branchy_beam.py [COMMIT] > profiles/r05_hazard_branchy_beam.txt
 """
@@ -19,6 +20,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 sys.path.insert(0, HERE)
 import isa_hazard as H  # noqa: E402
+import re  # noqa: E402
 
 COMMIT = sys.argv[1] if len(sys.argv) > 1 else "e81496e"  # round 5, before the kernel's deletion
 HIPCC = "/opt/rocm/bin/hipcc"
@@ -62,6 +64,21 @@ def main():
                     print("   no instruction touches a 16x16x16_f16 destination within 24 states")
                 for mf, h, st, _ in rows[:12]:
                     print(f"   {st:2d} states after {mf}\n      -> {h}")
+                # the mixed-form srcC chain (hardware-probed, tools/probe_mfma_hazard.py): an MFMA of
+                # another form accumulating onto the destination within MIXED_SRCC states
+                mixed = sorted({(mf, h, st) for mf, h, st, need in hz
+                                if need == H.MIXED_SRCC and h.startswith("v_mfma")}, key=lambda x: x[2])
+                print(f"   mixed-form srcC chains within {H.MIXED_SRCC} states: {len(mixed)}")
+                for mf, h, st in mixed[:8]:
+                    print(f"   {st:2d} states after {mf}\n      -> {h}")
+            # a VALU result read by an MFMA operand too soon (srcC within 1 state, srcA / srcB within 2)
+            for name, (ins, labels) in H.parse(asm).items():
+                if not re.search(r"dec_bank_d8_beam_kernelILi2E", name):
+                    continue
+                vm = H.scan_valu_to_mfma(ins, labels)
+                print(f"   VALU results read by an MFMA inside the probed window: {len(vm)}")
+                for v, mf, st, need in vm[:8]:
+                    print(f"   {st} states (needs {need}) from {v}\n      -> {mf}")
 
 
 if __name__ == "__main__":

@@ -152,6 +152,48 @@ def scan_function(ins, labels, every=False):
     return found
 
 
+# VALU -> MFMA operand (hardware-probed, tools/probe_mfma_hazard.py valu_srcC /
+# valu_srcA rows): a VALU result read by an MFMA as srcC needs 1 intervening
+# state, as srcA / srcB 2; gap 0 returned the stale value
+VALU_SRCC = 1
+VALU_SRCAB = 2
+
+
+def scan_valu_to_mfma(ins, labels):
+    """[(VALU line, MFMA line, states elapsed, required)]: an MFMA reading a
+    VALU-written VGPR (as srcC within VALU_SRCC states, as srcA / srcB within
+    VALU_SRCAB) on some path"""
+    found = []
+    horizon = max(VALU_SRCC, VALU_SRCAB)
+    for i, (mn, ops, raw) in enumerate(ins):
+        if not mn.startswith("v_") or mn.startswith(("v_mfma_", "v_cmp", "v_readlane", "v_readfirstlane")):
+            continue
+        parts = [p.strip() for p in re.split(r",(?![^\[]*\])", ops)]
+        if not parts:
+            continue
+        dst = regs(parts[0])
+        if not dst:
+            continue
+        best = {}
+        stack = [(j, 0) for j in succ(ins, labels, i)]
+        while stack:
+            j, st = stack.pop()
+            if st >= horizon or best.get(j, horizon) <= st:
+                continue
+            best[j] = st
+            mn2, ops2, raw2 = ins[j]
+            if mn2.startswith("v_mfma_"):
+                d2, a2, b2, c2 = split_mfma(ops2)
+                if st < VALU_SRCC and regs(c2) & dst:
+                    found.append((raw, raw2, st, VALU_SRCC))
+                if st < VALU_SRCAB and (regs(a2) | regs(b2)) & dst:
+                    found.append((raw, raw2, st, VALU_SRCAB))
+            st2 = st + states(mn2, ops2)
+            for k in succ(ins, labels, j):
+                stack.append((k, st2))
+    return found
+
+
 def scan(asm, regex=None, every=False):
     """{kernel symbol: [hazards]} for every kernel (matching regex) in a listing"""
     out = {}
