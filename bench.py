@@ -305,10 +305,10 @@ def kernel_roofline(eng, B, mode, beam, encoder="transformer", alive=None, secon
     else:
         form = eng.engines[0].bank_form() if hasattr(eng, "engines") else eng.bank_form()
         if form == 3:  # the 24-bit context K/V image (1600 B per key: 3-byte k, v + 8 head scales each)
-            name = f"dec_ctx_attention_kernel<{beam}, true>"
+            name = f"dec_ctx_q24_kernel<{beam}>"
             per_chunk = T * 1600 + T * 4 + 2 * beam * D * 4
         else:
-            name = f"dec_ctx_attention_kernel<{beam}, false>"
+            name = f"dec_ctx_attention_kernel<{beam}>"
             per_chunk = T * 2 * D * 4 + T * 4 + 2 * beam * D * 4
         nbytes = B * per_chunk
         extra = {}

@@ -498,21 +498,23 @@ int nd_op_dec_ctx_attention(const float* q, const float* kv, int32_t ld, int32_t
  * multi_headed_attn.py:142-177, on 0.78x the bytes).  nd_op_ctx_pack_q24:
  * fp32 K/V kv [B*T, ld] (layer l's k at column l*512, v at l*512+256; the
  * reference's linear_keys / linear_values outputs, multi_headed_attn.py:
- * 142-150) -> image out [B*T][layers][1600 B]: per (key, layer) k's 256
+ * 142-150) -> image out [layers][B*T][1600 B] (layer-major: one layer's
+ * keys of a chunk are contiguous): per (layer, key) k's 256
  * values as 24-bit integers (3 bytes each; the 12 bytes at 12*i hold dims
  * 4i..4i+3), v's at byte 768, then per head h {2^(e_k - 23), 2^(e_v - 23)}
  * as floats at byte 1536 + 8h, with e the head's exponent (max|x| < 2^e); an
  * element's error is at most 2^-23 of its head's largest |x|.  Rows t >=
  * span[c] are not written.  nd_op_dec_ctx_attention_q24: as
- * nd_op_dec_ctx_attention with K/V of layer `layer` from that image. */
+ * nd_op_dec_ctx_attention with K/V of layer `layer` from that image (C*T
+ * rows per layer plane). */
 int nd_op_ctx_pack_q24(const float* kv, int32_t ld, int32_t layers, void* out, const int32_t* span, int32_t B,
                        int32_t T, void* stream);
 /* The engine's form: the memory's K / V projection (split-fp16, as
  * nd_op_gemm_split, N = layers * 512) whose epilogue writes that image
- * (ld bytes per row >= layers * 1600) instead of fp32 K / V; every row is
- * written. */
-int nd_op_gemm_split_q24(const float* A, const uint16_t* Wh, float wscale, const float* bias, void* img, int32_t ld,
-                         int32_t M, int32_t N, int32_t K, int32_t norm, void* stream);
+ * (layer planes of plane_rows >= M rows) instead of fp32 K / V; every row
+ * is written. */
+int nd_op_gemm_split_q24(const float* A, const uint16_t* Wh, float wscale, const float* bias, void* img,
+                         int32_t plane_rows, int32_t M, int32_t N, int32_t K, int32_t norm, void* stream);
 int nd_op_dec_ctx_attention_q24(const float* q, const void* kvq, int32_t layers, int32_t layer, const float* signal,
                                 const int32_t* span, float pad_val, float* out, int32_t C, int32_t rpc, int32_t T,
                                 void* stream);
@@ -522,8 +524,8 @@ int nd_op_dec_ctx_attention_q24(const float* q, const void* kvq, int32_t layers,
  * most a sixteenth of them remain).  nd_op_alive_list: chunks c < C with
  * done[c] == 0, ascending, into list[0 .. cap), the rest -1; more than cap
  * alive sets *ovf (nullable) to 1.  nd_op_dec_ctx_attention_list: the context
- * attention (fp32 K/V, or the 24-bit image when q24 != 0 with ld / koff in
- * bytes) for the listed chunks only (list entries -1 and chunks with done[c]
+ * attention (fp32 K/V, or one layer plane of the 24-bit image when q24 != 0,
+ * ld = 1600 and koff = 0 bytes) for the listed chunks only (list entries -1 and chunks with done[c]
  * != 0 untouched), each chunk's keys in nsplit workgroups (1..64) whose
  * partial softmax states go to part (ccap * nsplit * rpc * 272 floats) and
  * are combined by a second launch. */

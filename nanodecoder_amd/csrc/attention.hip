@@ -1072,14 +1072,11 @@ struct CtxTile {
   static constexpr int U = RPC <= CTX_URPC ? 4 : CTX_UHI;  // keys per block (register budget)
 };
 
-// Q24 (round 4): the chunk's K/V in 24-bit fixed point (ctx_pack_q24_kernel
-// below): per key row 1600 B instead of 2 KB, so the HBM-bound kernel streams
-// 0.78x the bytes; the integers convert exactly to fp32 and the per-(key,
-// head) power-of-two scales fold into the score (after the head's 8-lane
-// sum) and into v.  kv, ld and koff are then bytes.
-template <int RPC, bool Q24>
+// fp32 K/V (exact fp32 calls): K at kv[(c*T + t)*ld + koff], V at + 256.
+// The 24-bit image (every other beam call) runs dec_ctx_q24_kernel below.
+template <int RPC>
 __global__ void __launch_bounds__(CTX_NW * 64)
-dec_ctx_attention_kernel(const float* __restrict__ q, const void* __restrict__ kv_, int ld, int koff,
+dec_ctx_attention_kernel(const float* __restrict__ q, const float* __restrict__ kv, int ld, int koff,
                          const float* __restrict__ signal, const int* __restrict__ span, float pad_val,
                          float* __restrict__ out, int T, unsigned long long* stamp, float* __restrict__ dbg,
                          size_t dbg_stride, const int* __restrict__ skip, const int* __restrict__ clist, int nsplit,
@@ -1110,26 +1107,15 @@ dec_ctx_attention_kernel(const float* __restrict__ q, const void* __restrict__ k
     m[j] = -INFINITY;
     l[j] = 0.f;
   }
-  // a key's registers: fp32 k, v (Q24: the 12 bytes of k's and of v's four
-  // integers in .xyz, the head's k and v scales in k.w, v.w)
   f32x4 kc[U], vc[U];
   float sg[U];
   auto load = [&](int blk, f32x4* kk, f32x4* vv, float* ss) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int t = min(blk * U + u, L - 1);
-      if constexpr (Q24) {
-        const uint8_t* row = static_cast<const uint8_t*>(kv_) + (base + t) * ld + koff;
-        const u32x3 kb = *reinterpret_cast<const u32x3*>(row + 12 * lane);
-        const u32x3 vb = *reinterpret_cast<const u32x3*>(row + CTXQ_V + 12 * lane);
-        const f32x2 sc = *reinterpret_cast<const f32x2*>(row + CTXQ_S + 8 * (lane >> 3));
-        kk[u] = f32x4{__uint_as_float(kb.x), __uint_as_float(kb.y), __uint_as_float(kb.z), sc.x};
-        vv[u] = f32x4{__uint_as_float(vb.x), __uint_as_float(vb.y), __uint_as_float(vb.z), sc.y};
-      } else {
-        const float* kvc = static_cast<const float*>(kv_) + (base + t) * ld + koff + lane * 4;
-        kk[u] = ld4(kvc);
-        vv[u] = ld4(kvc + ND_D);
-      }
+      const float* kvc = kv + (base + t) * ld + koff + lane * 4;
+      kk[u] = ld4(kvc);
+      vv[u] = ld4(kvc + ND_D);
       ss[u] = sgc[t];
     }
   };
@@ -1144,35 +1130,22 @@ dec_ctx_attention_kernel(const float* __restrict__ q, const void* __restrict__ k
     const bool more = blk + CTX_NW < b1;
     if (more) load(blk + CTX_NW, kn, vn, sn);
     float sc[RPC][U];
-    f32x4 vf[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const bool valid = blk * U + u < L;
       const bool masked = sg[u] == pad_val;
-      f32x4 kf = kc[u];
-      float ks = 1.f;
-      if constexpr (Q24) {
-        kf = q24_unpack(kc[u]);
-        ks = kc[u].w;
-        vf[u] = q24_unpack(vc[u]) * vc[u].w;
-      } else {
-        vf[u] = vc[u];
-      }
 #pragma unroll
       for (int j = 0; j < RPC; ++j) {
-        float d = sum8(qv[j].x * kf.x + qv[j].y * kf.y + qv[j].z * kf.z + qv[j].w * kf.w);
-        if constexpr (Q24) d *= ks;
-        sc[j][u] = d;
+        const float d = sum8(qv[j].x * kc[u].x + qv[j].y * kc[u].y + qv[j].z * kc[u].z + qv[j].w * kc[u].w);
+        sc[j][u] = valid ? (masked ? ND_MASK_FILL : d) : -INFINITY;
       }
-#pragma unroll
-      for (int j = 0; j < RPC; ++j) sc[j][u] = valid ? (masked ? ND_MASK_FILL : sc[j][u]) : -INFINITY;
       // -attn_debug / coverage: head 0 (lanes 0..7 after sum8) of every row of the chunk
       if (dbg && lane == 0 && valid)
 #pragma unroll
         for (int j = 0; j < RPC; ++j)  // natural units (the -1e18 fill as it stands)
           dbg[((size_t)c * RPC + j) * dbg_stride + blk * U + u] = sc[j][u];
     }
-    online_update_lazy<RPC, U>(sc, vf, m, l, acc);
+    online_update_lazy<RPC, U>(sc, vc, m, l, acc);
     if (more) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -1188,6 +1161,208 @@ dec_ctx_attention_kernel(const float* __restrict__ q, const void* __restrict__ k
   else
     merge_waves<RPC, CTX_NW>(accs, ms, ls, m, l, acc, wave, lane, tid, out, c * RPC);
   stamp_end(stamp);
+}
+
+// The 24-bit image (round 4, ctx_pack_q24_kernel below / the K/V GEMM's
+// epilogue): per key 1600 B instead of 2 KB; the integers convert exactly to
+// fp32 and the per-(key, head) power-of-two scales fold into the score (after
+// the head's 8-lane sum) and into v.
+//
+// Its key rows reach LDS by DMA (round 5).  The round-4 form (the fp32
+// kernel above on the image) kept one block of U keys in flight per wave in
+// registers (2 x 1600 B at 5 rows: every more key costs 9 VGPRs and the 4th
+// wave per SIMD); timed alone at B = 1024 x 5 rows (tools/ctx_time.py) its
+// loads by themselves took 158 us (5.3 TB/s), its arithmetic by itself 89
+// us, and the kernel 204-211 us: the two barely overlapped.  Here every wave streams its
+// blocks through a private ring of CQ_D LDS slots by global_load_lds (no VGPR
+// holds a block in flight, no barrier: the wave that copies a block is the
+// one that reads it), CQ_P blocks ahead of the one it computes, and waits for
+// a block with a counted vmcnt.  The block's rows land in LDS byte for byte
+// as in HBM (16-B pieces: row u's bytes at u * 1600), followed by its keys'
+// signal samples; the lane reads its 12 bytes of k and of v as three dwords
+// each (12-B lane stride: a ds_read_b96 off its 16-B alignment replays) and
+// its head's two scales as one b64.  The LDS reads are inline asm: an
+// ordinary LDS read after an LDS-DMA makes hipcc wait for every DMA in
+// flight (vmcnt(0)), which is the prefetch this kernel exists for.  Same
+// arithmetic as the register form, key for key (bitwise equal outputs,
+// checked on the GPU before that form was deleted: 493,824 outputs, rpc 1, 2,
+// 5, 6, ragged spans).  Alone: 205 -> 195 us; with the layer-major image
+// (every chunk's keys of a layer one contiguous run) 172 us (its copies
+// alone 150 us); configs[3] pooled 70.0 -> 69.0 ms (profiles/r05_ctx_ab.txt).
+#ifndef CQ_P
+#define CQ_P 2  // blocks in flight beyond the one computed
+#endif
+#define CQ_D (CQ_P + 1)  // ring slots per wave
+static_assert(CTXQ_ROW % 16 == 0, "16-B pieces");
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(3))) char lds_char_t;
+// a block of U keys (the register form's blocking, CtxTile): U rows + their U
+// signal samples (16-B aligned); DMA instructions per block
+template <int U>
+struct CqBlock {
+  static constexpr int PIECES = U * CTXQ_ROW / 16;
+  static constexpr int SLOT = U * CTXQ_ROW + 16;
+  static constexpr int NI = (PIECES + 63) / 64 + 1;
+};
+
+template <int OFF>
+__device__ __forceinline__ float cq_ld32(uint32_t a) {
+  float r;
+  asm volatile("ds_read_b32 %0, %1 offset:%2" : "=&v"(r) : "v"(a), "n"(OFF) : "memory");
+  return r;
+}
+template <int OFF>
+__device__ __forceinline__ f32x2 cq_ld64(uint32_t a) {
+  f32x2 r;
+  asm volatile("ds_read_b64 %0, %1 offset:%2" : "=&v"(r) : "v"(a), "n"(OFF) : "memory");
+  return r;
+}
+// key u of the slot at sb: the lane's 12 bytes of k and of v (three dwords
+// each), its head's two scales, the key's signal sample; every value passes
+// through the lgkmcnt wait (the reads land there, not at the asm statements).
+// Each call waits for everything the wave has in flight on LDS, so the keys'
+// reads go out together only when the caller issues them all first: it
+// calls cq_key_issue for every key, then cq_key_land for every key.
+struct CqKey {
+  float k0, k1, k2, v0, v1, v2, sg;
+  f32x2 s;
+};
+template <int U, int u>
+__device__ __forceinline__ void cq_key_issue(CqKey& o, uint32_t a12, uint32_t a8, uint32_t sb) {
+  o.k0 = cq_ld32<u * CTXQ_ROW>(a12);
+  o.k1 = cq_ld32<u * CTXQ_ROW + 4>(a12);
+  o.k2 = cq_ld32<u * CTXQ_ROW + 8>(a12);
+  o.v0 = cq_ld32<u * CTXQ_ROW + CTXQ_V>(a12);
+  o.v1 = cq_ld32<u * CTXQ_ROW + CTXQ_V + 4>(a12);
+  o.v2 = cq_ld32<u * CTXQ_ROW + CTXQ_V + 8>(a12);
+  o.s = cq_ld64<u * CTXQ_ROW>(a8);
+  o.sg = cq_ld32<U * CTXQ_ROW + 4 * u>(sb);
+}
+__device__ __forceinline__ void cq_key_land(CqKey& o) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(o.k0), "+v"(o.k1), "+v"(o.k2), "+v"(o.v0), "+v"(o.v1), "+v"(o.v2), "+v"(o.s), "+v"(o.sg)
+               :
+               : "memory");
+}
+
+template <int RPC>
+__global__ void __launch_bounds__(CTX_NW * 64)
+dec_ctx_q24_kernel(const float* __restrict__ q, const uint8_t* __restrict__ kv, int ld, int koff,
+                   const float* __restrict__ signal, const int* __restrict__ span, float pad_val,
+                   float* __restrict__ out, int T, unsigned long long* stamp, float* __restrict__ dbg,
+                   size_t dbg_stride, const int* __restrict__ skip, const int* __restrict__ clist, int nsplit,
+                   float* __restrict__ part) {
+  constexpr int U = CtxTile<RPC>::U;
+  using BK = CqBlock<U>;
+  const int c = clist ? clist[blockIdx.x / nsplit] : (int)blockIdx.x;
+  if (c < 0 || (skip && skip[c])) return;  // finished chunk (--fast beam, translator.py:793-823)
+  stamp_begin(stamp);
+  extern __shared__ __attribute__((aligned(16))) char cq_sm[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wu = __builtin_amdgcn_readfirstlane(wave);
+  char* ring = cq_sm + wu * (CQ_D * BK::SLOT);  // this wave's slots
+  const int L = min(span[c], T);
+  const size_t base = (size_t)c * T;
+  const float* sgc = signal + base;
+  f32x4 qv[RPC], acc[RPC];
+  float m[RPC], l[RPC];
+#pragma unroll
+  for (int j = 0; j < RPC; ++j) {
+    qv[j] = ld4(q + pk(c * RPC + j, lane * 4, ND_D)) / ND_SQRT_DH;
+    acc[j] = {0.f, 0.f, 0.f, 0.f};
+    m[j] = -INFINITY;
+    l[j] = 0.f;
+  }
+  // q is in registers before the first DMA goes out (its wait stays out of the loop): the values
+  // feed an empty statement that no memory operation may cross
+#pragma unroll
+  for (int j = 0; j < RPC; ++j) asm volatile("" ::"v"(qv[j].x), "v"(qv[j].y), "v"(qv[j].z), "v"(qv[j].w) : "memory");
+  // this lane's 16-B piece of each DMA instruction: key pu of the block, byte po of its row
+  int pu[BK::NI - 1], po[BK::NI - 1];
+#pragma unroll
+  for (int j = 0; j < BK::NI - 1; ++j) {
+    const int p = min(j * 64 + lane, BK::PIECES - 1);
+    pu[j] = p / (CTXQ_ROW / 16);
+    po[j] = (p % (CTXQ_ROW / 16)) * 16;
+  }
+  const uint8_t* kvc = kv + base * ld + koff;
+  // block b (keys clamped into the span: the copies stay straight-line) into slot s
+  auto issue = [&](int b, int s) {
+    char* dst = ring + s * BK::SLOT;
+#pragma unroll
+    for (int j = 0; j < BK::NI - 1; ++j) {
+      const int t = min(b * U + pu[j], L - 1);
+      const uint8_t* src = kvc + (size_t)t * ld + po[j];
+      if (j < BK::PIECES / 64 || lane < BK::PIECES % 64)
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)(dst + j * 1024), 16, 0, 0);
+    }
+    if (lane < U)
+      __builtin_amdgcn_global_load_lds((const void*)(sgc + min(b * U + lane, L - 1)),
+                                       (lds_void_t*)(dst + U * CTXQ_ROW), 4, 0, 0);
+  };
+  const int nblk = (L + U - 1) / U, bps = (nblk + nsplit - 1) / nsplit;
+  const int b0 = (blockIdx.x % nsplit) * bps, b1 = min(nblk, b0 + bps);
+  int blk = b0 + wu;
+  if (blk < b1) {
+#pragma unroll
+    for (int p = 0; p < CQ_P; ++p) issue(min(blk + p * CTX_NW, b1 - 1), p);
+    int slot = 0;
+    const uint32_t lbase = (uint32_t)reinterpret_cast<uintptr_t>((lds_char_t*)ring);  // LDS byte address
+    for (; blk < b1; blk += CTX_NW) {
+      {
+        const int s2 = slot + CQ_P;
+        issue(min(blk + CQ_P * CTX_NW, b1 - 1), s2 >= CQ_D ? s2 - CQ_D : s2);
+      }
+      // block blk's copies are the oldest NI of the (CQ_P + 1) NI in flight
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(BK::NI * CQ_P) : "memory");
+      const uint32_t sb = lbase + (uint32_t)(slot * BK::SLOT);
+      const uint32_t a12 = sb + 12 * lane, a8 = sb + CTXQ_S + 8 * (lane >> 3);
+      CqKey key[U];
+      cq_key_issue<U, 0>(key[0], a12, a8, sb);
+      cq_key_issue<U, 1>(key[1], a12, a8, sb);
+      if constexpr (U > 2) {
+        cq_key_issue<U, 2>(key[2], a12, a8, sb);
+        cq_key_issue<U, 3>(key[3], a12, a8, sb);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) cq_key_land(key[u]);
+      float sc[RPC][U];
+      f32x4 vf[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool valid = blk * U + u < L;
+        const bool masked = key[u].sg == pad_val;
+        const f32x4 kf = q24_unpack(f32x4{key[u].k0, key[u].k1, key[u].k2, 0.f});
+        const float ks = key[u].s.x;
+        vf[u] = q24_unpack(f32x4{key[u].v0, key[u].v1, key[u].v2, 0.f}) * key[u].s.y;
+#pragma unroll
+        for (int j = 0; j < RPC; ++j) {
+          const float d = sum8(qv[j].x * kf.x + qv[j].y * kf.y + qv[j].z * kf.z + qv[j].w * kf.w) * ks;
+          sc[j][u] = valid ? (masked ? ND_MASK_FILL : d) : -INFINITY;
+        }
+        if (dbg && lane == 0 && valid)
+#pragma unroll
+          for (int j = 0; j < RPC; ++j) dbg[((size_t)c * RPC + j) * dbg_stride + blk * U + u] = sc[j][u];
+      }
+      online_update_lazy<RPC, U>(sc, vf, m, l, acc);
+      slot = slot + 1 == CQ_D ? 0 : slot + 1;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped copies past b1 land before the rings are reused
+  }
+  __syncthreads();  // every wave is out of its ring: the rings become the merge image
+  float* accs = reinterpret_cast<float*>(cq_sm);  // [NW][RPC][256]
+  float* ms = accs + CTX_NW * RPC * ND_D;         // [NW][RPC][8]
+  float* ls = ms + CTX_NW * RPC * ND_H;           // [NW][RPC][8]
+  if (part)
+    merge_waves_part<RPC, CTX_NW>(accs, ms, ls, m, l, acc, wave, lane, tid, part + (size_t)blockIdx.x * RPC * CTX_PART);
+  else
+    merge_waves<RPC, CTX_NW>(accs, ms, ls, m, l, acc, wave, lane, tid, out, c * RPC);
+  stamp_end(stamp);
+}
+
+static size_t cq_lds_bytes(int rpc) {
+  const size_t slot = rpc <= CTX_URPC ? CqBlock<4>::SLOT : CqBlock<CTX_UHI>::SLOT;
+  return std::max((size_t)CTX_NW * CQ_D * slot, (size_t)CTX_NW * rpc * (ND_D + 2 * ND_H) * sizeof(float));
 }
 
 // The split form's combine: row j of listed chunk b from its nsplit partial
@@ -1212,8 +1387,8 @@ ctx_split_merge_kernel(const float* __restrict__ part, const int* __restrict__ c
   out[pk(c * rpc + j, d & ~3, ND_D) + (d & 3)] = den > 0.f ? num * __builtin_amdgcn_rcpf(den) : 0.f;
 }
 
-// fp32 K/V [M][ld] (layer l's k | v at column koff + l * 512) -> the 24-bit
-// image [M][Ld][CTXQ_ROW] bytes: per (key, layer) k's and v's 256 integers
+// fp32 K/V [M][ld] (layer l's k | v at column l * 512) -> the 24-bit image
+// [Ld][M][CTXQ_ROW] bytes: per (layer, key) k's and v's 256 integers
 // (3 bytes each, little-endian two's complement, lane-major: lane i's 12
 // bytes hold dims 4i..4i+3), then per head {2^(e_k - 23), 2^(e_v - 23)} as
 // floats.  e = the head's exponent: max|x| < 2^e, so |x| 2^(23-e) < 2^23 and
@@ -1230,7 +1405,7 @@ ctx_pack_q24_kernel(const float* __restrict__ kv, int ld, int Ld, uint8_t* __res
   const int row = w / Ld, layer = w % Ld;
   if (row % T >= min(span[row / T], T)) return;
   const float* src = kv + (size_t)row * ld + (size_t)layer * 2 * ND_D + lane * 4;
-  uint8_t* dst = out + ((size_t)row * Ld + layer) * CTXQ_ROW;
+  uint8_t* dst = out + ((size_t)layer * (n / Ld) + row) * CTXQ_ROW;  // layer-major planes of n / Ld rows
   float scl[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) scl[h] = q24_quant_store(ld4(src + h * ND_D), dst + h * CTXQ_V + 12 * lane);
@@ -1257,18 +1432,18 @@ hipError_t launch_dec_ctx_attention(const float* q, const void* kv, int ld, int 
   if (nsplit < 1 || nsplit > 64) return hipErrorInvalidValue;
   float* const pout = nsplit > 1 ? part : nullptr;
   const int grid = clist ? ccap * nsplit : C;
-  const size_t lds = ctx_lds_bytes(rpc);
+  const size_t lds = q24 ? cq_lds_bytes(rpc) : ctx_lds_bytes(rpc);
   switch (rpc) {
 #define ND_CTX_CASE(R)                                                                                            \
   case R:                                                                                                         \
     if (q24)                                                                                                      \
-      hipLaunchKernelGGL((dec_ctx_attention_kernel<R, true>), dim3(grid), dim3(CTX_NW * 64), lds, s, q, kv, ld,   \
-                         koff, signal, span, pad_val, out, T, stamp, attn_dbg, dbg_stride, skip, clist, nsplit,   \
-                         pout);                                                                                   \
+      hipLaunchKernelGGL((dec_ctx_q24_kernel<R>), dim3(grid), dim3(CTX_NW * 64), lds, s, q,                       \
+                         static_cast<const uint8_t*>(kv), ld, koff, signal, span, pad_val, out, T, stamp,         \
+                         attn_dbg, dbg_stride, skip, clist, nsplit, pout);                                        \
     else                                                                                                          \
-      hipLaunchKernelGGL((dec_ctx_attention_kernel<R, false>), dim3(grid), dim3(CTX_NW * 64), lds, s, q, kv, ld,  \
-                         koff, signal, span, pad_val, out, T, stamp, attn_dbg, dbg_stride, skip, clist, nsplit,   \
-                         pout);                                                                                   \
+      hipLaunchKernelGGL((dec_ctx_attention_kernel<R>), dim3(grid), dim3(CTX_NW * 64), lds, s, q,                 \
+                         static_cast<const float*>(kv), ld, koff, signal, span, pad_val, out, T, stamp, attn_dbg, \
+                         dbg_stride, skip, clist, nsplit, pout);                                                  \
     break;
     ND_CTX_CASE(1)
     ND_CTX_CASE(2)
@@ -1329,12 +1504,12 @@ hipError_t launch_alive_list(const int* done, int C, int* list, int cap, int* ov
 
 hipError_t init_kernel_attributes() {
   const void* fns[] = {
-      (const void*)dec_ctx_attention_kernel<1, false>, (const void*)dec_ctx_attention_kernel<2, false>,
-      (const void*)dec_ctx_attention_kernel<3, false>, (const void*)dec_ctx_attention_kernel<4, false>,
-      (const void*)dec_ctx_attention_kernel<5, false>, (const void*)dec_ctx_attention_kernel<6, false>,
-      (const void*)dec_ctx_attention_kernel<1, true>,  (const void*)dec_ctx_attention_kernel<2, true>,
-      (const void*)dec_ctx_attention_kernel<3, true>,  (const void*)dec_ctx_attention_kernel<4, true>,
-      (const void*)dec_ctx_attention_kernel<5, true>,  (const void*)dec_ctx_attention_kernel<6, true>};
+      (const void*)dec_ctx_attention_kernel<1>, (const void*)dec_ctx_attention_kernel<2>,
+      (const void*)dec_ctx_attention_kernel<3>, (const void*)dec_ctx_attention_kernel<4>,
+      (const void*)dec_ctx_attention_kernel<5>, (const void*)dec_ctx_attention_kernel<6>,
+      (const void*)dec_ctx_q24_kernel<1>,              (const void*)dec_ctx_q24_kernel<2>,
+      (const void*)dec_ctx_q24_kernel<3>,              (const void*)dec_ctx_q24_kernel<4>,
+      (const void*)dec_ctx_q24_kernel<5>,              (const void*)dec_ctx_q24_kernel<6>};
   for (const void* f : fns) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;

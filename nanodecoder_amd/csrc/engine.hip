@@ -175,7 +175,7 @@ struct nd_ctx {
   bool ctx_q24 = false;                   // beam rows read the 24-bit context K/V image (ctxq), not fp32 ctxkv
   int* clist = nullptr;                   // --fast beam tail: the alive chunks (launch_alive_list), ceil(B/16)
   float* ctx_part = nullptr;              // ... and the split context attention's partial states
-  uint8_t* ctxq = nullptr;                // [B * T][layers][CTXQ_ROW] (attention.hip ctx_pack_q24_kernel)
+  uint8_t* ctxq = nullptr;                // [layers][B * T][CTXQ_ROW] (attention.hip ctx_pack_q24_kernel)
   float* bank_ks = nullptr;               // digit bank: per-row scales 2^e_t [B * 512]
   int* bank_em = nullptr;                 // digit bank: per-chunk max e_t (biased) [B]
   int last_bank_form = 0;                 // nd_bank_form
@@ -585,7 +585,7 @@ struct G {
   G& skip(const int* done, int rpc) { a.skip = done; a.skip_rpc = rpc; return *this; }
   G& small_m(bool on) { a.prefer_p16 = on ? 1 : 0; return *this; }
   G& c_rowmajor(bool on) { a.c_rm = on ? 1 : 0; return *this; }  // P16 GEMMs: C row-major
-  G& q24(uint8_t* img, int ld) { a.q24 = img; a.q24_ld = ld; return *this; }  // the 24-bit K/V image, not C
+  G& q24(uint8_t* img, size_t plane) { a.q24 = img; a.q24_plane = plane; return *this; }  // the 24-bit image, not C
   // long-K P16 products may split over workgroups (gemm_p16k_kernel) into the context's slab
   G& splitk(const nd_ctx* c) {
     a.sk_slab = c->sk_slab;
@@ -708,10 +708,10 @@ static hipError_t enqueue_encode_transformer(nd_ctx* c, int B, int T, hipStream_
 static hipError_t enqueue_ctxkv(nd_ctx* c, int B, int T, hipStream_t s, bool q24 = false) {
   const int M = B * T, D = c->D, N = (int)c->dec.size() * 2 * D;
   uint8_t* img = q24 ? c->ctxq : nullptr;
-  const int ld = (int)c->dec.size() * CTXQ_ROW;
+  const size_t plane = (size_t)M * CTXQ_ROW;  // one layer's keys of the call (enqueue_dec_step reads the same)
   if (c->cfg.encoder_type == ND_ENC_TRANSFORMER)
-    return G(c->x, D, c->nctxkv_w, N, D, c->nctxkv_b, c->ctxkv, N, M).h3(c).ln(c->x_part, c->x_pn).q24(img, ld).run(s);
-  return G(c->x, D, c->ctxkv_w, N, D, c->ctxkv_b, c->ctxkv, N, M).h3(c).q24(img, ld).run(s);
+    return G(c->x, D, c->nctxkv_w, N, D, c->nctxkv_b, c->ctxkv, N, M).h3(c).ln(c->x_part, c->x_pn).q24(img, plane).run(s);
+  return G(c->x, D, c->ctxkv_w, N, D, c->ctxkv_b, c->ctxkv, N, M).h3(c).q24(img, plane).run(s);
 }
 
 // the 24-bit image straight from the K/V GEMM's epilogue (fp32-forced GEMMs: fp32 K/V, then the pack kernel)
@@ -916,7 +916,7 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
     } else {
       LCHK(dg(c->dq1, D, L.pcwq, D, D, L.ncbq, c->dcq, D).ln(c->dq1_part, pnq).run(s));
       if (c->ctx_q24)
-        LCHK(nd::launch_dec_ctx_attention(c->dcq, c->ctxq, Ld * CTXQ_ROW, i * CTXQ_ROW, c->sig, c->span,
+        LCHK(nd::launch_dec_ctx_attention(c->dcq, c->ctxq + (size_t)i * C * T * CTXQ_ROW, CTXQ_ROW, 0, c->sig, c->span,
                                           (float)c->cfg.pad_idx, c->datt, C, rpc, T, s, stamp, dbg, dbg_stride, done,
                                           true, clist, ccap, ctx_split(), c->ctx_part));
       else
@@ -1913,14 +1913,14 @@ int nd_op_gemm_split(const float* A, const uint16_t* Wh, float wscale, const flo
   return ND_OK;
 }
 
-int nd_op_gemm_split_q24(const float* A, const uint16_t* Wh, float wscale, const float* bias, void* img, int32_t ld,
-                         int32_t M, int32_t N, int32_t K, int32_t norm, void* stream) {
-  if (!Wh || !img) return fail(ND_ERR_ARG, "gemm_split_q24: null Wh / image");
+int nd_op_gemm_split_q24(const float* A, const uint16_t* Wh, float wscale, const float* bias, void* img,
+                         int32_t plane_rows, int32_t M, int32_t N, int32_t K, int32_t norm, void* stream) {
+  if (!Wh || !img || plane_rows < M) return fail(ND_ERR_ARG, "gemm_split_q24: null Wh / image, or plane_rows < M");
   G g(A, K, nullptr, N, K, bias, nullptr, N, M);
   g.a.Wh = Wh;
   g.a.wscale = wscale;
   g.a.norm = norm != 0;
-  g.q24(static_cast<uint8_t*>(img), ld);
+  g.q24(static_cast<uint8_t*>(img), (size_t)plane_rows * CTXQ_ROW);
   hipError_t e = g.run((hipStream_t)stream);
   if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("gemm_split_q24: ") + hipGetErrorString(e));
   return ND_OK;
@@ -2186,8 +2186,9 @@ int nd_op_dec_ctx_attention_q24(const float* q, const void* kvq, int32_t layers,
   if (int rc = ensure_attributes()) return rc;
   if (!q || !kvq || !signal || !span || !out || layer < 0 || layer >= layers)
     return fail(ND_ERR_ARG, "dec_ctx_attention_q24: bad arguments");
-  hipError_t e = nd::launch_dec_ctx_attention(q, kvq, layers * CTXQ_ROW, layer * CTXQ_ROW, signal, span, pad_val, out,
-                                              C, rpc, T, (hipStream_t)stream, nullptr, nullptr, 0, nullptr, true);
+  const uint8_t* plane = static_cast<const uint8_t*>(kvq) + (size_t)layer * C * T * CTXQ_ROW;
+  hipError_t e = nd::launch_dec_ctx_attention(q, plane, CTXQ_ROW, 0, signal, span, pad_val, out, C, rpc, T,
+                                              (hipStream_t)stream, nullptr, nullptr, 0, nullptr, true);
   if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("dec_ctx_attention_q24: ") + hipGetErrorString(e));
   return ND_OK;
 }

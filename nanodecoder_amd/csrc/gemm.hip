@@ -377,7 +377,7 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
         // (BN >= 256: one wave = 64 threads of one row, so `row < M` is wave-uniform)
         if (g.q24 && row < M) {
           const int col = n0 + c4, layer = col / (2 * ND_D), half = (col / ND_D) & 1, d = col % ND_D;
-          uint8_t* dst = g.q24 + (size_t)row * g.q24_ld + (size_t)layer * CTXQ_ROW;
+          uint8_t* dst = g.q24 + (size_t)layer * g.q24_plane + (size_t)row * CTXQ_ROW;
           const float sc = q24_quant_store(v, dst + half * CTXQ_V + 3 * d);
           if ((d & (ND_DH - 1)) == 0) reinterpret_cast<float*>(dst + CTXQ_S)[2 * (d / ND_DH) + half] = sc;
         }
@@ -1109,7 +1109,7 @@ hipError_t launch_gemm(GemmArgs& g, hipStream_t s) {
   if (e != hipSuccess) return e;
   // the 24-bit context K/V image: the 256 x 256 tiles (a wave holds one row's 256 columns = k or v of a layer)
   if (g.q24) {
-    if (g.N % (2 * ND_D) || g.p16io || g.R || g.relu || g.q24_ld < (g.N / (2 * ND_D)) * CTXQ_ROW)
+    if (g.N % (2 * ND_D) || g.p16io || g.R || g.relu || g.q24_plane < (size_t)g.M * CTXQ_ROW)
       return hipErrorInvalidValue;
     return launch_cfg<256, 256, 2, 4>(g, s);
   }

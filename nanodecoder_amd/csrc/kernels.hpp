@@ -60,10 +60,10 @@ struct GemmArgs {
   // 16 B of every 64 B line; PMC: 4x over-fetch of q' in the P16 layout)
   int c_rm = 0;
   // row-major LDS-tiled kernel, N = layers * 512 (the beam's context K / V):
-  // write the 24-bit image (CTXQ_ROW bytes per layer, q24_ld bytes per row)
-  // instead of C; nullable
+  // write the 24-bit image instead of C: layer l's row r at q24 + l *
+  // q24_plane + r * CTXQ_ROW (layer-major planes, launch_ctx_pack_q24); nullable
   uint8_t* q24 = nullptr;
-  int q24_ld = 0;
+  size_t q24_plane = 0;
   // P16 GEMMs at K >= 1024: the split-K form's fp32 slab and per-tile tickets
   // (zero before the first launch; the last arriver of a tile resets its
   // ticket), sized for sk_tiles 32 x 32 tiles; null: the one-workgroup form
@@ -239,8 +239,10 @@ hipError_t launch_dec_ctx_attention(const float* q, const void* kv, int ld, int 
 hipError_t launch_alive_list(const int* done, int C, int* list, int cap, int* ovf, hipStream_t s);
 // 24-bit context K/V (beam rows): per (key row, layer) CTXQ_ROW bytes = k's 256
 // integers (3 bytes each, lane i's 12 bytes = dims 4i..4i+3) | v's | per head
-// {k scale, v scale} (powers of two, f32).  Image [B*T][Ld][CTXQ_ROW] from the
-// fp32 [B*T][ld] K/V (layer l at column l*512); rows t >= span not written.
+// {k scale, v scale} (powers of two, f32).  Image [Ld][B*T][CTXQ_ROW] (layer-
+// major: one layer's keys of a chunk are one contiguous 819 KB run, round 5)
+// from the fp32 [B*T][ld] K/V (layer l at column l*512); rows t >= span not
+// written.
 #define CTXQ_V 768
 #define CTXQ_S 1536
 #define CTXQ_ROW 1600

@@ -444,14 +444,14 @@ def op_gemm(A: torch.Tensor, W: torch.Tensor, bias=None, R=None, ln_g=None, ln_b
 
 def op_gemm_split_q24(A: torch.Tensor, W: torch.Tensor, bias=None, norm=False):
     """The beam's K / V projection writing the 24-bit image (nd_op_gemm_split_q24): A [M, K], W [layers*512, K]
-    (split-fp16 as op_gemm(split=True)) -> uint8 [M, layers, 1600]."""
+    (split-fp16 as op_gemm(split=True)) -> uint8 [layers, M, 1600] (layer-major)."""
     M, K = A.shape
     N = W.shape[0]
     layers = N // 512
-    img = torch.zeros(M, layers, 1600, dtype=torch.uint8, device=A.device)
+    img = torch.zeros(layers, M, 1600, dtype=torch.uint8, device=A.device)
     Wh, sc = op_split_weight(W)
     s = ctypes.c_void_p(torch.cuda.current_stream(A.device).cuda_stream)
-    _lib.check(_lib.lib().nd_op_gemm_split_q24(_ptr(A), _ptr(Wh), sc, _ptr(bias), _ptr(img), layers * 1600, M, N, K,
+    _lib.check(_lib.lib().nd_op_gemm_split_q24(_ptr(A), _ptr(Wh), sc, _ptr(bias), _ptr(img), M, M, N, K,
                                                int(norm), s), "nd_op_gemm_split_q24")
     return img
 
@@ -646,9 +646,9 @@ CTXQ_ROW = 1600  # bytes per (key row, layer) of the 24-bit context K/V image (k
 
 def op_ctx_pack_q24(kv, ld, layers, span, B, T):
     """24-bit context K/V image (nd_op_ctx_pack_q24): kv [B*T, ld] f32 (layer l's
-    k | v at columns l*512 .. l*512+511) -> uint8 [B*T, layers, 1600]; rows t >=
-    span[c] of chunk c are not written (left zero here)."""
-    out = torch.zeros(B * T, layers, CTXQ_ROW, dtype=torch.uint8, device=kv.device)
+    k | v at columns l*512 .. l*512+511) -> uint8 [layers, B*T, 1600] (layer-major);
+    rows t >= span[c] of chunk c are not written (left zero here)."""
+    out = torch.zeros(layers, B * T, CTXQ_ROW, dtype=torch.uint8, device=kv.device)
     s = ctypes.c_void_p(torch.cuda.current_stream(kv.device).cuda_stream)
     _lib.check(_lib.lib().nd_op_ctx_pack_q24(_ptr(kv), ld, layers, _ptr(out), _ptr(span), B, T, s),
                "nd_op_ctx_pack_q24")
@@ -661,7 +661,7 @@ def op_dec_ctx_attention_q24(qp, kvq, layer, signal, span, pad_val, rpc):
     C, T = signal.shape
     out = torch.empty(qp.shape[0], qp.shape[1], dtype=torch.float32, device=qp.device)
     s = ctypes.c_void_p(torch.cuda.current_stream(qp.device).cuda_stream)
-    _lib.check(_lib.lib().nd_op_dec_ctx_attention_q24(_ptr(qp), _ptr(kvq), kvq.shape[1], layer, _ptr(signal),
+    _lib.check(_lib.lib().nd_op_dec_ctx_attention_q24(_ptr(qp), _ptr(kvq), kvq.shape[0], layer, _ptr(signal),
                                                       _ptr(span), float(pad_val), _ptr(out), C, rpc, T, s),
                "nd_op_dec_ctx_attention_q24")
     return out

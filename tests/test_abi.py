@@ -79,15 +79,18 @@ def listings(tmp_path_factory):
         return dict(zip(names, ex.map(asm, names)))
 
 
-def test_inline_asm_lds_ring_has_no_hazard(listings):
-    """ffn.hip's inline-asm LDS read ring: in the compiled gfx950 code no
-    instruction touches a ring destination register between its ds_read and
-    the s_waitcnt that retires it (tools/lds_ring_check.py)."""
+@pytest.mark.parametrize("src,kernel", [("ffn", "enc_ffn"), ("attention", "dec_ctx_q24_kernel")])
+def test_inline_asm_lds_ring_has_no_hazard(listings, src, kernel):
+    """The inline-asm LDS reads (ffn.hip's read ring; the beam context
+    attention's reads of its DMA ring, attention.hip): in the compiled gfx950
+    code no instruction touches a destination register between its ds_read
+    and the s_waitcnt that retires it (tools/lds_ring_check.py)."""
     import subprocess
     import sys
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "lds_ring_check.py"), listings["ffn"], "enc_ffn"],
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "lds_ring_check.py"), listings[src], kernel],
                        capture_output=True, text=True)
-    assert r.returncode == 0 and "0 hazards" in r.stdout, r.stdout + r.stderr
+    assert r.returncode == 0 and " 0 hazards" in r.stdout and "hazards" in r.stdout, r.stdout + r.stderr
+    assert all(" 0 hazards" in ln for ln in r.stdout.splitlines() if "hazards" in ln), r.stdout
 
 
 def test_hot_path_kernels_do_not_drain_loads(listings):
@@ -213,6 +216,7 @@ DYNAMIC_LDS = {  # kernels launched with dynamic LDS (metadata says 0): bytes at
     "dec_bank_d8_kernel": 138064,        # bank8.hip B8_LDS
     "dec_mem_attention_kernel": 158208,  # mem_lds_bytes()
     "dec_ctx_attention_kernel": 52224,   # ctx_lds_bytes(6) (the attribute allows 160 KB; launches take this)
+    "dec_ctx_q24_kernel": 76992,         # cq_lds_bytes(<= 2 rows): 4 waves x 3 slots x 6416 B
     "gemm_p16s_kernel": 98304,           # 2x4 tiles
 }
 REVIEWED_PAIRED = {
@@ -225,6 +229,9 @@ REVIEWED_PAIRED = {
                             "barrier; encoder-side GEMMs of the beam / exact / NanoEncoder paths, pool-tested"),
     "dec_ctx_attention_kernel": (36, "the (m, l, acc) merge of the beam context attention (and of its split "
                                      "form); launched with at most 52 KB, listed in case that grows"),
+    "dec_ctx_q24_kernel": (24, "the (m, l, acc) merge after a barrier behind the DMA rings' last use; the merge "
+                               "image sits at LDS byte 0 (< 22 KB), far below 64 KB (the rings above it take no "
+                               "paired form)"),
     "dec_bank_d8_kernel": (3, "the (m, l) merge and the q' digit rows (cross-wave, after a barrier); "
                               "pool-tested at the bench's configuration"),
     "dec_mem_attention_kernel": (25, "the fp32 bank kernel (exact fp32 / short chunks): slab reads after "

@@ -32,27 +32,27 @@ def _quant(x):
 
 
 def pack_q24(kv, ld, layers, span, B, T):
-    """numpy image of nd_op_ctx_pack_q24: kv [B*T, ld] f32 -> uint8 [B*T, layers,
-    1600]; rows t >= span[c] stay zero (the kernel does not write them)."""
-    out = np.zeros((B * T, layers, ROW), np.uint8)
+    """numpy image of nd_op_ctx_pack_q24: kv [B*T, ld] f32 -> uint8 [layers, B*T,
+    1600] (layer-major); rows t >= span[c] stay zero (the kernel does not write them)."""
+    out = np.zeros((layers, B * T, ROW), np.uint8)
     for layer in range(layers):
         k = kv[:, layer * 2 * D: layer * 2 * D + D].reshape(-1, H, DH)
         v = kv[:, layer * 2 * D + D: (layer + 1) * 2 * D].reshape(-1, H, DH)
         for off, x in ((0, k), (768, v)):
             q, _ = _quant(x)
             b = q.reshape(-1, D).astype("<i4").view(np.uint8).reshape(-1, D, 4)[:, :, :3]
-            out[:, layer, off:off + 768] = b.reshape(-1, 768)
+            out[layer, :, off:off + 768] = b.reshape(-1, 768)
         sk, sv = _quant(k)[1], _quant(v)[1]
-        out[:, layer, 1536:1600] = np.stack([sk, sv], -1).astype("<f4").view(np.uint8).reshape(-1, 64)
+        out[layer, :, 1536:1600] = np.stack([sk, sv], -1).astype("<f4").view(np.uint8).reshape(-1, 64)
     t = np.arange(B * T) % T
     live = t < np.minimum(np.repeat(np.asarray(span), T), T)
-    out[~live] = 0
+    out[:, ~live] = 0
     return out
 
 
 def unpack_q24(img, layer):
     """image -> (k, v) f32 [rows, 256], decoded as the kernel does (q24_unpack)."""
-    r = img[:, layer]
+    r = img[layer]
 
     def ints(b):
         b = b.reshape(-1, D, 3).astype(np.int32)
@@ -124,7 +124,7 @@ def test_rows_past_span_untouched_and_nonfinite_heads_stay_nonfinite():
     kv[3, 5] = np.nan
     kv[4, 300] = np.inf
     img = pack_q24(kv, 512, layers, np.array([6, 2], np.int32), B, T)
-    assert not img[6:8].any() and not img[T + 2:].any() and img[:6].any()
+    assert not img[:, 6:8].any() and not img[:, T + 2:].any() and img[:, :6].any()
     k, v = unpack_q24(img, 0)
     assert np.isnan(k[3, :DH]).all() and np.isfinite(k[3, DH:]).all()
     assert np.isnan(v[4, DH:2 * DH]).all() and np.isfinite(v[4, :DH]).all()

@@ -276,6 +276,55 @@ def test_pool_at_bench_config_matches_single_engine(key):
     pool.close()
 
 
+def test_pooled_encoder_memory_matches_serial():
+    """The encoder's output (the memory bank, before its pack) when another
+    lane's decoders share the CUs equals the serial encoder's bitwise (ADVICE
+    r04: the layer-0 closed-form attention, whose round-3 layout returned
+    wrong chunks only beside another engine's kernels, DESIGN.md section 5, is
+    guarded here on its own output, not only through the tokens it changes).
+    Three lanes at the bench's sizes: lanes 0 and 1 run greedy calls
+    (max_length 100) while lane 2 encodes on its own stream, three rounds."""
+    import torch
+    from nanodecoder_amd.engine import EnginePool
+    cfg = synth.ModelConfig()
+    W = synth.make_weights(cfg, seed=11, eos_bias=-3.0)
+    B, S = 256, 100
+    inputs = []
+    for k in range(3):
+        sig = synth.synth_chunk_batch(B, 512, seed=700 + k, inject_masks=True)
+        inputs.append(_ragged(sig, 950 + k) if k % 2 else (sig, np.full(B, 512, np.int32),
+                                                            np.full(B, 512, np.int32)))
+    one = _engine(cfg, W, max_batch=B, max_steps=S)
+    exp = []
+    for sig, ln, sp in inputs:
+        m = one.encode(sig, ln, sp).cpu().numpy()
+        exp.append([m[b, : sp[b]] for b in range(B)])  # rows >= span are unspecified
+    one.close()
+    pool = EnginePool(cfg, W, device=0, lanes=3, max_batch=B, max_steps=S)
+    dev_in = [tuple(torch.from_numpy(a).cuda() for a in i) for i in inputs]
+    enc = pool.engines[2]
+    for rnd in range(3):
+        got = []
+        for k, inp in enumerate(dev_in):
+            pool._next = 0  # lanes 0 and 1 decode
+            r0 = pool.translate_greedy(*inp, max_len=S, min_len=57)
+            r1 = pool.translate_greedy(*dev_in[(k + 1) % len(dev_in)], max_len=S, min_len=57)
+            enc.stream.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(enc.stream):
+                mem = enc.encode(*inp)
+            torch.cuda.current_stream().wait_stream(enc.stream)
+            got.append(mem)
+            del r0, r1
+        pool.synchronize()
+        torch.cuda.synchronize()
+        for k, mem in enumerate(got):
+            m = mem.cpu().numpy()
+            sp = inputs[k][2]
+            bad = [b for b in range(B) if not np.array_equal(m[b, : sp[b]], exp[k][b])]
+            assert not bad, (rnd, k, bad[:8])
+    pool.close()
+
+
 def test_translator_reads_with_pool_vs_oracle():
     """Translator.translate_reads on an EnginePool (two engine batches in
     flight while the next is packed): identical strings and scores to the

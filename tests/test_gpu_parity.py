@@ -484,7 +484,7 @@ def test_ctx_pack_q24_bitexact():
     assert bad.size == 0, bad[:8]
     kv[3 * T + 2, 256 + 40] = np.nan  # v of head 1, layer 0
     got = op_ctx_pack_q24(torch.from_numpy(kv).to(dev), Ld * 512, Ld, torch.from_numpy(spans).to(dev), B, T)
-    sc = got[3 * T + 2, 0, 1536:1600].cpu().numpy().view(np.float32).reshape(8, 2)
+    sc = got[0, 3 * T + 2, 1536:1600].cpu().numpy().view(np.float32).reshape(8, 2)
     assert np.isnan(sc[1, 1]) and np.isfinite(np.delete(sc.reshape(-1), 3)).all()
 
 
@@ -613,7 +613,7 @@ def test_ctx_attention_tail_list_split(rpc, nsplit, q24):
     if q24:
         img = op_ctx_pack_q24(kvd, Ld * 512, Ld, sp, C, T)
         whole = op_dec_ctx_attention_q24(qp, img, 0, sg, sp, PAD, rpc)
-        got = op_dec_ctx_attention_list(qp, img, Ld * 1600, 0, sg, sp, PAD, rpc, torch.from_numpy(clist).to(dev),
+        got = op_dec_ctx_attention_list(qp, img, 1600, 0, sg, sp, PAD, rpc, torch.from_numpy(clist).to(dev),
                                         nsplit, q24=True, done=dn)
     else:
         whole = op_dec_ctx_attention(qp, kvd, Ld * 512, 0, sg, sp, PAD, rpc, packed=True)

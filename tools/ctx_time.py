@@ -31,8 +31,12 @@ def main():
     img = E.op_ctx_pack_q24(kv, Ld * 512, Ld, span, C, T)
     t32 = timeit(lambda: E.op_dec_ctx_attention(q, kv, Ld * 512, 512, sig, span, 1.0, rpc, packed=True))
     t24 = timeit(lambda: E.op_dec_ctx_attention_q24(q, img, 1, sig, span, 1.0, rpc))
+    # one layer's image alone ([C*T][1600]: every chunk's keys contiguous, the layer-major layout's stream)
+    img1 = E.op_ctx_pack_q24(kv[:, 512:1024].contiguous(), 512, 1, span, C, T)
+    t1 = timeit(lambda: E.op_dec_ctx_attention_q24(q, img1, 0, sig, span, 1.0, rpc))
     print(f"{tag:10s} ctx C={C} rpc={rpc}: fp32 K/V {t32:7.1f} us ({C * T * 2048 / t32 / 1e6:.2f} TB/s), "
-          f"24-bit {t24:7.1f} us ({C * T * 1600 / t24 / 1e6:.2f} TB/s)", flush=True)
+          f"24-bit {t24:7.1f} us ({C * T * 1600 / t24 / 1e6:.2f} TB/s), "
+          f"24-bit contiguous {t1:7.1f} us ({C * T * 1600 / t1 / 1e6:.2f} TB/s)", flush=True)
 
 
 if __name__ == "__main__":
