@@ -380,7 +380,7 @@ def kernel_roofline(eng, B, mode, beam, encoder="transformer", alive=None, secon
     gms = _StreamTimer(dev).time(ffn, 10)
     flops = 2 * M * D * D + 4 * M * F * D + 6 * M * D * D
     tf = flops / (gms * 1e-3) / 1e12
-    out["mfma_kernel"] = {"kernel": "enc_ffn_kernel<1, true, true> (the engine's form for encoder layers 0-1: "
+    out["mfma_kernel"] = {"kernel": "enc_ffn_kernel<1, true, true, false> (the engine's form for encoder layers 0-1: "
                                     "Wo + residual, LN + W1 + ReLU + W2 + residual, next layer's LN + QKV; split-fp16)",
                           "achieved": round(tf, 2), "peak": round(SPLIT_PEAK, 1),
                           "unit": "TFLOP/s fp32-equivalent (fp16 MFMA peak / 3 products)",
