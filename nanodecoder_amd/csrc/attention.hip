@@ -917,8 +917,17 @@ dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cac
       const int t = min(t0 + u, tmax);  // wave-uniform
       const int slot = ANC ? __builtin_amdgcn_readlane(sv, u) : r;
       const float* row = cache + ((size_t)slot * S + t) * 2 * ND_D + lane * 4;
-      k[u] = ld4(row);
-      v[u] = ld4(row + ND_D);
+      if constexpr (!ANC) {
+        // a greedy row's history is read by that row alone: non-temporal, which leaves the Infinity Cache to
+        // the memory bank that every layer re-reads (pooled configs[1] 16.05 / 16.00 -> 15.88 / 15.77 ms per
+        // call, same box; beam rows share their ancestors' slots and keep the default policy: non-temporal
+        // there cost configs[3] 69.8 -> 71.7 ms)
+        k[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(row));
+        v[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(row + ND_D));
+      } else {
+        k[u] = ld4(row);
+        v[u] = ld4(row + ND_D);
+      }
     }
   };
   // the first pass's cache loads go out before the row's q | k | v, whose

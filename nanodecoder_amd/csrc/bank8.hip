@@ -358,20 +358,28 @@ __global__ void __launch_bounds__(B8_NW * 64)
 dec_bank_d8_kernel(const float* __restrict__ qp, const i32x4* __restrict__ bank, const float* __restrict__ kscale,
                    const int* __restrict__ kemax, const float* __restrict__ signal, const int* __restrict__ span,
                    float pad_val, float* __restrict__ out, int T, int C, unsigned long long* stamp,
-                   float* __restrict__ dbg, size_t dbg_stride, int* ovf) {
+                   float* __restrict__ dbg, size_t dbg_stride, int* ovf, int cached) {
 #ifdef ND_SKIP_BANK  // timing probe only (tools/build_variant.sh, tools/marginal.sh): the kernel's marginal cost
   if (threadIdx.x < 100000) return;
 #endif
   const unsigned long long t_entry = wall_clock64();
+  // NT: chunks c >= cached stream non-temporally; the first `cached` chunks' banks keep the default policy
+  // (they stay in the Infinity Cache between the call's 300 launches, bank_cached below)
+  auto one = [&](int c) {
+    if (NT && c >= cached)
+      bank_d8_chunk<true>(c, qp, bank, kscale, kemax, signal, span, pad_val, out, T, stamp, dbg, dbg_stride, ovf,
+                          t_entry);
+    else
+      bank_d8_chunk<false>(c, qp, bank, kscale, kemax, signal, span, pad_val, out, T, stamp, dbg, dbg_stride, ovf,
+                           t_entry);
+  };
   if constexpr (WALK) {
     for (int c = blockIdx.x; c < C; c += gridDim.x) {
       if (c != (int)blockIdx.x) lds_barrier();  // the previous chunk's merge reads of LDS are done
-      bank_d8_chunk<NT>(c, qp, bank, kscale, kemax, signal, span, pad_val, out, T, stamp, dbg, dbg_stride, ovf,
-                        t_entry);
+      one(c);
     }
   } else {
-    bank_d8_chunk<NT>(blockIdx.x, qp, bank, kscale, kemax, signal, span, pad_val, out, T, stamp, dbg, dbg_stride, ovf,
-                      t_entry);
+    one(blockIdx.x);
   }
   stamp_end(stamp);
 }
@@ -443,6 +451,13 @@ hipError_t launch_bank_pack_d8(const float* x, const float* ln_g, const float* l
   return hipGetLastError();
 }
 
+// When the bank streams non-temporally (the pool's lanes, EnginePool.bank_nt_lanes), the first quarter of
+// a call's chunks keep the default policy: with three lanes that is 75 MB of bank held in the 256 MB
+// Infinity Cache across the call's 300 launches.  Pooled configs[1], same box, two reps each (ND_BANK_CACHED
+// A/B, round 5): none 16.10 / 16.07 ms per call; 32 of 256 chunks 15.92 / 15.91; 64: 15.91 / 15.90; 96: 15.98
+// / 15.95; 128: 15.87 / 15.89; 192: 16.09 / 16.03; all 256: 16.38 / 16.39 (the banks then evict the rest)
+static int bank_cached(int C) { return C / 4; }
+
 hipError_t launch_dec_bank_d8(const float* qp, const void* bank, const float* kscale, const int* kemax,
                               const float* signal, const int* span, float pad_val, float* out, int C, int T,
                               hipStream_t s, unsigned long long* stamp, float* attn_dbg, size_t dbg_stride, int* ovf,
@@ -452,7 +467,7 @@ hipError_t launch_dec_bank_d8(const float* qp, const void* bank, const float* ks
 #define ND_BANK8_GO(N, W)                                                                                         \
   hipLaunchKernelGGL((dec_bank_d8_kernel<N, W>), dim3(G), dim3(B8_NW * 64), B8_LDS, s, qp,                       \
                      reinterpret_cast<const i32x4*>(bank), kscale, kemax, signal, span, pad_val, out, T, C, stamp,  \
-                     attn_dbg, dbg_stride, ovf)
+                     attn_dbg, dbg_stride, ovf, bank_cached(C))
   if (G < C) {
     if (nt)
       ND_BANK8_GO(true, true);

@@ -406,9 +406,15 @@ enc_ffn_kernel(const float* y, const uint16_t* __restrict__ w1h, float w1s, cons
   for (int k = 0; k < nch; ++k) {
     // W2_k, W1_{k+1} landed (issued a step ago, the only copies in flight),
     // every wave's too; every wave is done with step k - 1's slots
+#ifdef FF_PROBE_NOBAR  // timing probe only: no step barrier (wrong results)
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#else
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#endif
+#ifndef FF_PROBE_NOCOPY  // timing probe only: no weight copies in the main loop (wrong results)
     if (k + 1 < nch) ff_copy_w2<NW>(W2, kp, k + 1, w2slot(k + 1), wave, lane);
     if (k + 2 < nch) ff_copy_w1<NW>(W1, k + 2, w1slot(k), wave, lane);
+#endif
     const f32x4* A2 = reinterpret_cast<const f32x4*>(w2slot(k)) + lane;
     const f32x4* A1 = reinterpret_cast<const f32x4*>(w1slot(k + 1)) + lane;
     if (k + 1 == nch) {  // the last step: phase 2 alone (QK: the W1 slots take W'_qkv's first slices)

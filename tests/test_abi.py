@@ -111,7 +111,10 @@ def test_hot_path_kernels_do_not_drain_loads(listings):
             # the one-chunk form's two sit in the unrolled key loop: the wait for the last fragment of the
             # half block being multiplied, right before the next half block's loads (reviewed, round 5)
             ("bank8", r"dec_bank_d8_kernelILb\dELb1E", 0),
-            ("bank8", r"dec_bank_d8_kernelILb\dELb0E", 2),
+            # (the non-temporal forms hold the chunk body twice: the call's first quarter of chunks keeps the
+            # default cache policy, bank_cached in bank8.hip)
+            ("bank8", r"dec_bank_d8_kernelILb0ELb0E", 2),
+            ("bank8", r"dec_bank_d8_kernelILb1ELb0E", 4),
             # the standalone head (the last step only when the head is fused):
             # the V > 8 generator loop's loads follow the first 8 rows' wait
             ("search", r"greedy_head_kernel", 1),
@@ -232,8 +235,9 @@ REVIEWED_PAIRED = {
     "dec_ctx_q24_kernel": (24, "the (m, l, acc) merge after a barrier behind the DMA rings' last use; the merge "
                                "image sits at LDS byte 0 (< 22 KB), far below 64 KB (the rings above it take no "
                                "paired form)"),
-    "dec_bank_d8_kernel": (3, "the (m, l) merge and the q' digit rows (cross-wave, after a barrier); "
-                              "pool-tested at the bench's configuration"),
+    "dec_bank_d8_kernel": (6, "the (m, l) merge and the q' digit rows (cross-wave, after a barrier), twice in "
+                              "the non-temporal forms (two chunk bodies, bank8.hip bank_cached); pool-tested at the "
+                              "bench's configuration"),
     "dec_mem_attention_kernel": (25, "the fp32 bank kernel (exact fp32 / short chunks): slab reads after "
                                      "barriers"),
 }
