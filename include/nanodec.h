@@ -75,6 +75,15 @@ int nd_load_weight(nd_ctx* ctx, const char* name, const float* host, const int64
  * weights.  Must be called once before any translate call. */
 int nd_finalize(nd_ctx* ctx);
 
+/* ctx (just created, no weight loaded, the same model configuration as src)
+ * reads src's weights and every image nd_finalize derived from them instead
+ * of holding its own; ctx is finalized by this call.  src must be finalized,
+ * on the same device, and outlive ctx.  For several contexts of one model on
+ * one GPU (EnginePool lanes): one copy of the weights in the caches they
+ * share (L2 per XCD, the Infinity Cache).  No reference counterpart (the
+ * reference holds one model per process). */
+int nd_share_weights(nd_ctx* ctx, const nd_ctx* src);
+
 /* Greedy translate of a batch of chunks: encoder forward + max_len decoder
  * steps with argmax selection.  Replaces Translator.translate_batch ->
  * _translate_random_sampling (translate/translator.py:396-540) for

@@ -44,6 +44,7 @@ SIGNATURES = {
     "nd_create": (_I, [ctypes.POINTER(NdConfig), ctypes.POINTER(_P)]),
     "nd_load_weight": (_I, [_P, ctypes.c_char_p, _P, ctypes.POINTER(ctypes.c_int64), _I]),
     "nd_finalize": (_I, [_P]),
+    "nd_share_weights": (_I, [_P, _P]),
     "nd_translate_greedy": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P]),
     "nd_translate_greedy_attn": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
     "nd_translate_sample": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _F, _I, ctypes.c_uint64, _P, _P, _P, _P, _P]),

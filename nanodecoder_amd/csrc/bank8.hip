@@ -456,6 +456,8 @@ hipError_t launch_bank_pack_d8(const float* x, const float* ln_g, const float* l
 // Infinity Cache across the call's 300 launches.  Pooled configs[1], same box, two reps each (ND_BANK_CACHED
 // A/B, round 5): none 16.10 / 16.07 ms per call; 32 of 256 chunks 15.92 / 15.91; 64: 15.91 / 15.90; 96: 15.98
 // / 15.95; 128: 15.87 / 15.89; 192: 16.09 / 16.03; all 256: 16.38 / 16.39 (the banks then evict the rest)
+// (with the lanes' weights shared, nd_share_weights: a third or half of the chunks 15.50 / 15.58 and 15.54 /
+// 15.55 ms against a quarter's 15.48 / 15.53, same box)
 static int bank_cached(int C) { return C / 4; }
 
 hipError_t launch_dec_bank_d8(const float* qp, const void* bank, const float* kscale, const int* kemax,

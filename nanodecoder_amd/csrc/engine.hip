@@ -1434,6 +1434,49 @@ int nd_finalize(nd_ctx* c) {
   return ND_OK;
 }
 
+int nd_share_weights(nd_ctx* c, const nd_ctx* src) {
+  if (!c || !src) return fail(ND_ERR_ARG, "null ctx");
+  if (!src->finalized) return fail(ND_ERR_STATE, "nd_share_weights: the source context is not finalized");
+  if (c == src || c->finalized) return fail(ND_ERR_STATE, "nd_share_weights: the context already holds weights");
+  const nd_config &a = c->cfg, &b = src->cfg;
+  if (a.encoder_type != b.encoder_type || a.self_attn_type != b.self_attn_type || a.enc_layers != b.enc_layers ||
+      a.dec_layers != b.dec_layers || a.d_model != b.d_model || a.heads != b.heads || a.d_ff != b.d_ff ||
+      a.vocab != b.vocab || a.rnn_hidden != b.rnn_hidden || a.position_encoding != b.position_encoding ||
+      a.pad_idx != b.pad_idx || a.bos_idx != b.bos_idx || a.eos_idx != b.eos_idx || a.device != b.device)
+    return fail(ND_ERR_ARG, "nd_share_weights: the model configurations differ");
+  // every weight pointer and every image nd_finalize derived (the layer structs hold both; nothing in them is
+  // a workspace); the context's own weight buffers from nd_create stay allocated and unread
+  c->enc = src->enc;
+  c->nano = src->nano;
+  c->nano_W = src->nano_W;
+  c->dec = src->dec;
+  c->enc_lin_w = src->enc_lin_w;
+  c->enc_lin_b = src->enc_lin_b;
+  c->enc_ln_g = src->enc_ln_g;
+  c->enc_ln_b = src->enc_ln_b;
+  c->eq_ac = src->eq_ac;
+  c->eq_scal = src->eq_scal;
+  for (int i = 0; i < 3; ++i) c->eq_m[i] = src->eq_m[i];
+  c->eq_ready = src->eq_ready;
+  c->eq_coef = src->eq_coef;
+  c->ctxkv_w = src->ctxkv_w;
+  c->ctxkv_b = src->ctxkv_b;
+  c->nctxkv_w = src->nctxkv_w;
+  c->nctxkv_b = src->nctxkv_b;
+  c->emb = src->emb;
+  c->pe = src->pe;
+  c->dec_ln_g = src->dec_ln_g;
+  c->dec_ln_b = src->dec_ln_b;
+  c->gen_w = src->gen_w;
+  c->gen_b = src->gen_b;
+  c->split = src->split;
+  c->split_rm = src->split_rm;
+  for (auto& kv : c->graphs) (void)hipGraphExecDestroy(kv.second);
+  c->graphs.clear();
+  c->finalized = true;
+  return ND_OK;
+}
+
 static int check_call(nd_ctx* c, int B, int T, int S) {
   if (!c) return fail(ND_ERR_ARG, "null ctx");
   if (!c->finalized) return fail(ND_ERR_STATE, "nd_finalize has not been called");
