@@ -436,6 +436,13 @@ int nd_op_enc_attention(const float* qkv, const float* signal, const int32_t* sp
  * [r][step]); anc nullable [R, anc_ld] slot ancestry (NULL = identity). */
 int nd_op_dec_self_attention(const float* qkv, float* cache, const int32_t* anc, int32_t anc_ld, int32_t step,
                              int32_t max_steps, float* out, int32_t R, void* stream);
+/* The same for beam rows, rpc (2..6) consecutive rows per chunk (R a
+ * multiple of rpc) on the chunk-per-workgroup kernel the engine runs for
+ * them: anc [R, anc_ld] required (each row's slots), done nullable [R / rpc]
+ * (rows of chunks with done != 0 untouched, translate/translator.py:793-823). */
+int nd_op_dec_self_attention_beam(const float* qkv, float* cache, const int32_t* anc, int32_t anc_ld, int32_t step,
+                                  int32_t max_steps, float* out, int32_t R, int32_t rpc, const int32_t* done,
+                                  void* stream);
 
 /* Memory-bank context attention (greedy form, engine.hip
  * derive_memory_bank_weights; replaces the context MultiHeadedAttention of

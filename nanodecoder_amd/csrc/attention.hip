@@ -1011,9 +1011,131 @@ dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cac
   merge_waves<1, NW>(accs, ms, ls, m, l, acc, wave, lane, tid, out, r);
 }
 
+// Beam rows (round 5): one workgroup per chunk for its RPC rows.  The rows of
+// a chunk are hypotheses that share most of their history (anc[r][t] is the
+// same slot for every row until they diverge), so the per-row kernel above
+// pulled the same cache lines into up to RPC CUs, once per row, and at
+// 5120 rows it was bound by that L2 -> CU traffic (step 48: 70 us for 503 MB
+// of logical reads).  Here a wave walks its keys for all RPC rows at once:
+// the RPC loads of a key that name one slot are consecutive instructions of
+// one wave, so the repeats are served by the CU's L1 (hit on the line just
+// requested).  Per key and row the same arithmetic as the per-row kernel (its
+// scores, its online softmax), keys taken one at a time with the next key's
+// loads in flight.  Each row's own key (t == step) is read from this step's
+// q | k | v, not from the cache that this launch appends it to.
+template <int RPC, int NW>
+__global__ void __launch_bounds__(NW * 64)
+dec_self_attention_beam_kernel(const float* __restrict__ qkv, float* __restrict__ cache, const int* __restrict__ anc,
+                               int anc_ld, int step, int S, float* __restrict__ out, const int* __restrict__ skip,
+                               QkvRows qr, const int* __restrict__ clist) {
+  __shared__ float accs[NW * RPC * ND_D];
+  __shared__ float ms[NW * RPC * ND_H], ls[NW * RPC * ND_H];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c = clist ? clist[blockIdx.x] : (int)blockIdx.x;
+  if (c < 0 || (skip && skip[c])) return;  // finished chunk (translate/translator.py:793-823)
+  const int wu = __builtin_amdgcn_readfirstlane(wave);
+  const int n = step + 1;
+  // this step's q | k | v of row j: P16 [R, 768] or the layer-0 table (row-major, by the row's token)
+  auto qkv_at = [&](int j, int part) -> const float* {
+    const int r = c * RPC + j;
+    const int qrow = qr.tok ? step * qr.V + (step == 0 ? qr.tok0 : qr.tok[r]) : r;
+    return qkv + (qr.rm ? (size_t)qrow * 3 * ND_D + part * ND_D + lane * 4 : pk(qrow, part * ND_D + lane * 4, 3 * ND_D));
+  };
+  f32x4 qv[RPC], acc[RPC];
+  float m[RPC], l[RPC];
+#pragma unroll
+  for (int j = 0; j < RPC; ++j) {
+    qv[j] = ld4(qkv_at(j, 0)) / ND_SQRT_DH;
+    acc[j] = {0.f, 0.f, 0.f, 0.f};
+    m[j] = -INFINITY;
+    l[j] = 0.f;
+  }
+  // this wave's keys t = wu + NW i (i = lane): every row's slot for them, one load per row
+  int sl[RPC];
+  {
+    const int t = min(wu + NW * lane, max(step - 1, 0));
+#pragma unroll
+    for (int j = 0; j < RPC; ++j) sl[j] = anc[(size_t)(c * RPC + j) * anc_ld + t];
+  }
+  // key t of row j: the cache row of its slot, or (t == step) this step's k | v
+  auto src = [&](int j, int t, int slot) -> const float* {
+    return t < step ? cache + ((size_t)slot * S + t) * 2 * ND_D + lane * 4 : qkv_at(j, 1);
+  };
+  auto vstep = [&](int t) -> size_t { return t < step ? (size_t)ND_D : (size_t)(qr.rm ? ND_D : pk(0, ND_D, 3 * ND_D)); };
+  auto load = [&](int i, f32x4 (&kk)[RPC], f32x4 (&vv)[RPC]) {
+    const int t = min(wu + NW * i, n - 1);  // wave-uniform; clamped (straight-line loads)
+#pragma unroll
+    for (int j = 0; j < RPC; ++j) {
+      const float* p = src(j, t, __builtin_amdgcn_readlane(sl[j], min(i, 63)));
+      kk[j] = ld4(p);
+      vv[j] = ld4(p + vstep(t));
+    }
+  };
+  const int nk = wu < n ? (n - 1 - wu) / NW + 1 : 0;  // this wave's keys
+  auto update = [&](const f32x4 (&kk)[RPC], const f32x4 (&vv)[RPC]) {
+#pragma unroll
+    for (int j = 0; j < RPC; ++j) {
+      const float d = sum8(qv[j].x * kk[j].x + qv[j].y * kk[j].y + qv[j].z * kk[j].z + qv[j].w * kk[j].w);
+      const float mx = fmaxf(m[j], d);
+      const float sc = __expf(m[j] - mx);  // m = -inf: 0 (acc, l are 0)
+      const float p = __expf(d - mx);
+      acc[j] = acc[j] * sc + p * vv[j];
+      l[j] = l[j] * sc + p;
+      m[j] = mx;
+    }
+  };
+  // two register sets in turn (a copy from one to the other would make hipcc wait for the loads it
+  // just issued); the loads past the last key are clamped to it (straight-line) and never used
+  f32x4 ka[RPC], va[RPC], kb[RPC], vb[RPC];
+  if (nk > 0) {
+    load(0, ka, va);
+    for (int i = 0; i < nk; i += 2) {
+      load(min(i + 1, nk - 1), kb, vb);
+      update(ka, va);
+      if (i + 1 >= nk) break;
+      load(min(i + 2, nk - 1), ka, va);
+      update(kb, vb);
+    }
+  }
+  // append every row's k | v at t = step to its own slot (read above from q | k | v, not from here)
+  for (int j = wu; j < RPC; j += NW) {
+    const float* kp = qkv_at(j, 1);
+    const f32x4 kme = ld4(kp), vme = ld4(kp + vstep(step));
+    float* mine = cache + ((size_t)(c * RPC + j) * S + step) * 2 * ND_D;
+    st4(mine + lane * 4, kme);
+    st4(mine + ND_D + lane * 4, vme);
+  }
+  merge_waves<RPC, NW>(accs, ms, ls, m, l, acc, wave, lane, tid, out, c * RPC);
+}
+
+// the chunk-per-workgroup form for rpc beam rows (ancestry, no fused head)
+static bool use_self_beam(const int* anc, int rpc, const GreedyHead* head) { return anc && rpc >= 2 && !head; }
+
 hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* anc, int anc_ld, int step,
                                      int max_steps, float* out, int R, hipStream_t s, int rpc, const int* skip,
                                      const QkvRows& qr, const GreedyHead* head, const int* clist, int ccap) {
+  if (use_self_beam(anc, rpc, head) && R % rpc == 0) {
+    if (qr.tok && (qr.V < 1 || qr.tok0 < 0 || qr.tok0 >= qr.V)) return hipErrorInvalidValue;
+    if (clist && (ccap < 1 || (long)ccap * rpc > R)) return hipErrorInvalidValue;
+    if (step >= max_steps || step >= SELF_MAXS) return hipErrorInvalidValue;
+    const int grid = clist ? ccap : R / rpc;
+    switch (rpc) {
+#define ND_SELFB(RP)                                                                                               \
+  case RP:                                                                                                         \
+    hipLaunchKernelGGL((dec_self_attention_beam_kernel<RP, 4>), dim3(grid), dim3(4 * 64), 0, s, qkv, cache, anc,  \
+                       anc_ld, step, max_steps, out, skip, qr, clist);                                             \
+    break;
+      ND_SELFB(2)
+      ND_SELFB(3)
+      ND_SELFB(4)
+      ND_SELFB(5)
+      ND_SELFB(6)
+#undef ND_SELFB
+      default:
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   if (qr.tok && (qr.V < 1 || qr.tok0 < 0 || qr.tok0 >= qr.V)) return hipErrorInvalidValue;
   if (head) {
     if (!qr.tok || anc || skip || rpc != 1 || step < 1 || head->V != qr.V || head->V > SELF_TABV ||

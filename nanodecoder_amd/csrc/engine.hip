@@ -2118,6 +2118,17 @@ int nd_op_dec_self_attention(const float* qkv, float* cache, const int32_t* anc,
   return ND_OK;
 }
 
+int nd_op_dec_self_attention_beam(const float* qkv, float* cache, const int32_t* anc, int32_t anc_ld, int32_t step,
+                                  int32_t max_steps, float* out, int32_t R, int32_t rpc, const int32_t* done,
+                                  void* stream) {
+  if (!qkv || !cache || !anc || !out || rpc < 2 || rpc > 6 || R % rpc)
+    return fail(ND_ERR_ARG, "dec_self_attention_beam: bad arguments");
+  hipError_t e = nd::launch_dec_self_attention(qkv, cache, anc, anc_ld, step, max_steps, out, R, (hipStream_t)stream,
+                                               rpc, done);
+  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("dec_self_attention_beam: ") + hipGetErrorString(e));
+  return ND_OK;
+}
+
 int nd_op_dec_mem_attention(const float* qp, const float* mem, const float* signal, const int32_t* span, float pad_val,
                             float* out, int32_t C, int32_t rpc, int32_t T, int32_t ldT, void* stream) {
   if (int rc = ensure_attributes()) return rc;

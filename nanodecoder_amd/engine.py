@@ -643,6 +643,20 @@ def op_dec_self_attention(qkv, cache, step, anc=None, anc_ld=0, packed=False):
     return out if packed else unpack_p16(out, R)
 
 
+def op_dec_self_attention_beam(qkv, cache, step, anc, rpc, done=None):
+    """Beam rows' self-attention (nd_op_dec_self_attention_beam): qkv [R, 768] row-major, R = chunks * rpc,
+    anc [R, S] each row's slots; returns out [R, 256] row-major."""
+    R = qkv.shape[0]
+    S = cache.shape[1]
+    qp = pack_p16(qkv)
+    out = torch.empty(qp.shape[0], 256, dtype=torch.float32, device=qkv.device)
+    s = ctypes.c_void_p(torch.cuda.current_stream(qkv.device).cuda_stream)
+    _lib.check(_lib.lib().nd_op_dec_self_attention_beam(_ptr(qp), _ptr(cache), _ptr(anc), anc.shape[1], step, S,
+                                                        _ptr(out), R, rpc, _ptr(done), s),
+               "nd_op_dec_self_attention_beam")
+    return unpack_p16(out, R)
+
+
 def op_dec_ctx_attention(q, kv, ld, koff, signal, span, pad_val, rpc, packed=False):
     """q [C*rpc, 256] row-major (or P16-packed with packed=True); returns out
     in the same convention."""

@@ -330,6 +330,49 @@ def test_dec_self_attention_vs_fp64(step, beam):
     assert torch.equal(appended, qkv[:, 256:])
 
 
+@pytest.mark.parametrize("rpc,step", [(5, 0), (5, 1), (5, 47), (2, 130), (6, 63), (3, 255)])
+def test_dec_self_attention_beam_vs_fp64(rpc, step):
+    """Beam rows' self-attention on the chunk-per-workgroup kernel: the rows of
+    a chunk share most of their history (slots from the chunk's rows, with
+    divergent tails), keys 0..step-1 through each row's ancestry, key `step`
+    from this step's k/v, appended to the row's own slot; rows of a finished
+    chunk untouched (multi_headed_attn.py:124-141, translate/translator.py:
+    793-823).  Tolerance as the per-row form's test (1e-5)."""
+    from nanodecoder_amd.engine import op_dec_self_attention_beam
+    C, S = 7, 256
+    R = C * rpc
+    g = torch.Generator().manual_seed(step + 100 * rpc)
+    qkv = torch.randn(R, 768, generator=g)
+    cache = torch.randn(R, S, 512, generator=g)
+    anc = torch.empty(R, S, dtype=torch.int32)
+    for c in range(C):
+        split = int(torch.randint(0, max(step, 1), (1,), generator=g))  # shared prefix, then per-row slots
+        for j in range(rpc):
+            r = c * rpc + j
+            anc[r, :split] = c * rpc
+            anc[r, split:] = torch.randint(0, rpc, (S - split,), generator=g, dtype=torch.int32) + c * rpc
+    done = torch.zeros(C, dtype=torch.int32)
+    done[3] = 1
+    dev = torch.device("cuda", 0)
+    cd = cache.to(dev)
+    out = op_dec_self_attention_beam(qkv.to(dev), cd, step, anc.to(dev), rpc, done.to(dev)).cpu().double()
+    q = qkv[:, :256].double().view(R, 8, 32) / np.float32(np.sqrt(32.0))
+    for r in range(R):
+        if done[r // rpc]:
+            continue
+        slots = anc[r, :step].long()
+        kv = cache[slots, torch.arange(step)].double()
+        k = torch.cat([kv[:, :256], qkv[r:r + 1, 256:512].double()]).view(-1, 8, 32)
+        v = torch.cat([kv[:, 256:], qkv[r:r + 1, 512:].double()]).view(-1, 8, 32)
+        p = torch.softmax(torch.einsum("hd,thd->ht", q[r], k), dim=-1)
+        ref = torch.einsum("ht,thd->hd", p, v).reshape(256)
+        assert (out[r] - ref).abs().max().item() < 1e-5, (r, step)
+    live = torch.tensor([not done[r // rpc] for r in range(R)])
+    appended = cd[torch.arange(R), step].cpu()
+    assert torch.equal(appended[live], qkv[live, 256:])
+    assert torch.equal(appended[~live], cache[~live, step])  # a finished chunk's rows are not written
+
+
 @pytest.mark.parametrize("scale", [1.0, 4.0, "rising"])
 def test_enc_attention_vs_oracle(scale):
     """Split-fp16 encoder attention against the oracle's attend: masked keys,
