@@ -443,6 +443,15 @@ int nd_op_dec_self_attention(const float* qkv, float* cache, const int32_t* anc,
 int nd_op_dec_self_attention_beam(const float* qkv, float* cache, const int32_t* anc, int32_t anc_ld, int32_t step,
                                   int32_t max_steps, float* out, int32_t R, int32_t rpc, const int32_t* done,
                                   void* stream);
+/* The engine's form for beam rows outside exact fp32 (greedy rows keep the fp32 history above): the
+ * cache holds each (slot, t) as 1600 bytes, k's 256 values as 24-bit
+ * integers | v's | per head {k scale, v scale} (the layout of
+ * nd_op_ctx_pack_q24's rows), [R, max_steps, 1600] bytes; this step's k|v
+ * is quantised and appended.  rpc 1: the per-row kernel (anc nullable), 2..6:
+ * the chunk kernel (anc required). */
+int nd_op_dec_self_attention_q24(const float* qkv, void* cache, const int32_t* anc, int32_t anc_ld, int32_t step,
+                                 int32_t max_steps, float* out, int32_t R, int32_t rpc, const int32_t* done,
+                                 void* stream);
 
 /* Memory-bank context attention (greedy form, engine.hip
  * derive_memory_bank_weights; replaces the context MultiHeadedAttention of

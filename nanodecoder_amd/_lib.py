@@ -95,6 +95,7 @@ SIGNATURES = {
     "nd_op_enc_attention": (_I, [_P, _P, _P, _P, _I, _I, _P]),
     "nd_op_dec_self_attention": (_I, [_P, _P, _P, _I, _I, _I, _P, _I, _P]),
     "nd_op_dec_self_attention_beam": (_I, [_P, _P, _P, _I, _I, _I, _P, _I, _I, _P, _P]),
+    "nd_op_dec_self_attention_q24": (_I, [_P, _P, _P, _I, _I, _I, _P, _I, _I, _P, _P]),
     "nd_op_dec_ctx_attention": (_I, [_P, _P, _I, _I, _P, _P, _F, _P, _I, _I, _I, _P]),
     "nd_op_ctx_pack_q24": (_I, [_P, _I, _I, _P, _P, _I, _I, _P]),
     "nd_op_gemm_split_q24": (_I, [_P, _P, _F, _P, _P, _I, _I, _I, _I, _I, _P]),

@@ -874,7 +874,15 @@ __device__ __forceinline__ void merge_waves_part(float* accs, float* ms, float* 
 // previous step's greedy head for the row (head.hpp), whose token picks the
 // row's q | k | v in the table; the other waves' cache loads are in flight
 // meanwhile.  One launch per step fewer than a standalone head kernel.
-template <int NW, int KW, bool ANC, bool HEAD>
+// Q24 (round 5, every call outside exact fp32): the cache holds each (slot,
+// t) as the 24-bit image of the beam's context K/V (k's 256 integers | v's |
+// per head {k scale, v scale}: SELF_Q24_ROW = 1600 B instead of 2 KB,
+// common.hpp q24_quant); a lane's key is its 12 bytes of k and of v and its
+// head's scales, the step's own key is quantised the same way in registers
+// (the one value every later step reads back), and the scores and v are
+// dequantised exactly as the context attention does.
+#define SELF_Q24_ROW CTXQ_ROW
+template <int NW, int KW, bool ANC, bool HEAD, bool Q24>
 __global__ void __launch_bounds__(NW * 64)
 dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cache, const int* __restrict__ anc,
                           int anc_ld, int step, int S, float* __restrict__ out, int rpc, const int* __restrict__ skip,
@@ -907,8 +915,14 @@ dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cac
   // loads are straight-line (t clamped into the history; a branch around
   // each made hipcc wait vmcnt(0) before the next, one round trip per key)
   f32x4 k[KW], v[KW];
+  u32v3 kr[KW], vr[KW];  // Q24: the lane's 12 bytes of k and of v
+  f32x2 sr[KW];          // Q24: its head's {k scale, v scale}
+  const int wu = __builtin_amdgcn_readfirstlane(wave);
   auto load_pass = [&](int base) {
-    const int t0 = base + wave * KW, tmax = max(step - 1, 0);
+    // Q24: the wave index from an SGPR, so each key's row address is a scalar base plus the lane's constant
+    // offsets (its three loads per key otherwise held two 64-bit vector addresses per key in flight and
+    // spilled at KW = 16); the fp32 forms keep the vector form, whose schedule has no drain
+    const int t0 = base + (Q24 ? wu : wave) * KW, tmax = max(step - 1, 0);
     // slots of this wave's keys (lane u < KW: key t0 + u; beam ancestry)
     int sv = r;
     if constexpr (ANC) sv = anc[(size_t)r * anc_ld + min(t0 + (lane % KW), tmax)];
@@ -916,6 +930,23 @@ dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cac
     for (int u = 0; u < KW; ++u) {
       const int t = min(t0 + u, tmax);  // wave-uniform
       const int slot = ANC ? __builtin_amdgcn_readlane(sv, u) : r;
+      if constexpr (Q24) {
+        // straight into the registers the arithmetic reads (a composed f32x4 made hipcc stage and wait)
+        const uint8_t* rb = reinterpret_cast<const uint8_t*>(cache) + ((size_t)slot * S + t) * SELF_Q24_ROW;
+        const u32v3* kp = reinterpret_cast<const u32v3*>(rb + 12 * lane);
+        const u32v3* vp = reinterpret_cast<const u32v3*>(rb + CTXQ_V + 12 * lane);
+        const f32x2* sp = reinterpret_cast<const f32x2*>(rb + CTXQ_S + 8 * (lane >> 3));
+        if constexpr (!ANC) {  // non-temporal, as the fp32 form below
+          kr[u] = __builtin_nontemporal_load(kp);
+          vr[u] = __builtin_nontemporal_load(vp);
+          sr[u] = __builtin_nontemporal_load(sp);
+        } else {
+          kr[u] = *kp;
+          vr[u] = *vp;
+          sr[u] = *sp;
+        }
+        continue;
+      }
       const float* row = cache + ((size_t)slot * S + t) * 2 * ND_D + lane * 4;
       if constexpr (!ANC) {
         // a greedy row's history is read by that row alone: non-temporal, which leaves the Infinity Cache to
@@ -937,7 +968,6 @@ dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cac
   // V candidate table rows (every token the head can pick) for LDS, then
   // their cache loads, so the row's q | k | v is an LDS read once the token
   // is known (not a global round trip after the barrier)
-  const int wu = __builtin_amdgcn_readfirstlane(wave);
   f32x4 qv, kme, vme;
   if constexpr (HEAD) {
     __shared__ float hlp[ND_MAXV];
@@ -981,6 +1011,10 @@ dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cac
     kme = ld4(qr0 + qstep);
     vme = ld4(qr0 + 2 * qstep);
   }
+  if constexpr (Q24) {  // the step's own key as every later step will read it back
+    kme = q24_raw(kme);
+    vme = q24_raw(vme);
+  }
   float m[1] = {-INFINITY}, l[1] = {0.f};
   f32x4 acc[1] = {{0.f, 0.f, 0.f, 0.f}};
   // one pass covers NW * KW keys (every step of max_length <= 128 in one)
@@ -990,23 +1024,49 @@ dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cac
 #pragma unroll
     for (int u = 0; u < KW; ++u)
       if (t0 + u >= step) {  // this step's own key (and masked keys past it)
-        k[u] = kme;
-        v[u] = vme;
+        if constexpr (Q24) {
+          kr[u] = u32v3{__float_as_uint(kme.x), __float_as_uint(kme.y), __float_as_uint(kme.z)};
+          vr[u] = u32v3{__float_as_uint(vme.x), __float_as_uint(vme.y), __float_as_uint(vme.z)};
+          sr[u] = f32x2{kme.w, vme.w};
+        } else {
+          k[u] = kme;
+          v[u] = vme;
+        }
       }
     if (t0 < n) {
       float sc[1][KW];
+      f32x4 vf[KW];
 #pragma unroll
       for (int u = 0; u < KW; ++u) {
-        const float d = sum8(qv.x * k[u].x + qv.y * k[u].y + qv.z * k[u].z + qv.w * k[u].w);
+        f32x4 kf = k[u];
+        float ks = 1.f;
+        vf[u] = v[u];
+        if constexpr (Q24) {
+          kf = q24_unpack(f32x4{__uint_as_float(kr[u].x), __uint_as_float(kr[u].y), __uint_as_float(kr[u].z), 0.f});
+          ks = sr[u].x;
+          vf[u] = q24_unpack(f32x4{__uint_as_float(vr[u].x), __uint_as_float(vr[u].y), __uint_as_float(vr[u].z), 0.f}) *
+                  sr[u].y;
+        }
+        float d = sum8(qv.x * kf.x + qv.y * kf.y + qv.z * kf.z + qv.w * kf.w);
+        if constexpr (Q24) d *= ks;
         sc[0][u] = t0 + u < n ? d : -INFINITY;
       }
-      online_update<1, KW>(sc, v, m, l, acc);
+      online_update<1, KW>(sc, vf, m, l, acc);
     }
   }
   if (wave == 0) {
-    float* mine = cache + ((size_t)r * S + step) * 2 * ND_D;
-    st4(mine + lane * 4, kme);
-    st4(mine + ND_D + lane * 4, vme);
+    if constexpr (Q24) {
+      uint8_t* mine = reinterpret_cast<uint8_t*>(cache) + ((size_t)r * S + step) * SELF_Q24_ROW;
+      *reinterpret_cast<u32x3*>(mine + 12 * lane) = u32x3{__float_as_uint(kme.x), __float_as_uint(kme.y),
+                                                          __float_as_uint(kme.z)};
+      *reinterpret_cast<u32x3*>(mine + CTXQ_V + 12 * lane) = u32x3{__float_as_uint(vme.x), __float_as_uint(vme.y),
+                                                                   __float_as_uint(vme.z)};
+      if ((lane & 7) == 0) *reinterpret_cast<f32x2*>(mine + CTXQ_S + 8 * (lane >> 3)) = f32x2{kme.w, vme.w};
+    } else {
+      float* mine = cache + ((size_t)r * S + step) * 2 * ND_D;
+      st4(mine + lane * 4, kme);
+      st4(mine + ND_D + lane * 4, vme);
+    }
   }
   merge_waves<1, NW>(accs, ms, ls, m, l, acc, wave, lane, tid, out, r);
 }
@@ -1014,16 +1074,15 @@ dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cac
 // Beam rows (round 5): one workgroup per chunk for its RPC rows.  The rows of
 // a chunk are hypotheses that share most of their history (anc[r][t] is the
 // same slot for every row until they diverge), so the per-row kernel above
-// pulled the same cache lines into up to RPC CUs, once per row, and at
-// 5120 rows it was bound by that L2 -> CU traffic (step 48: 70 us for 503 MB
-// of logical reads).  Here a wave walks its keys for all RPC rows at once:
-// the RPC loads of a key that name one slot are consecutive instructions of
-// one wave, so the repeats are served by the CU's L1 (hit on the line just
-// requested).  Per key and row the same arithmetic as the per-row kernel (its
-// scores, its online softmax), keys taken one at a time with the next key's
-// loads in flight.  Each row's own key (t == step) is read from this step's
-// q | k | v, not from the cache that this launch appends it to.
-template <int RPC, int NW>
+// pulled the same cache lines into up to RPC CUs, once per row.  Here a wave
+// walks its keys for all RPC rows at once: the RPC loads of a key that name
+// one slot are consecutive instructions of one wave, so the repeats are
+// served by the CU's L1.  Per key and row the per-row kernel's scores and
+// online softmax, keys one at a time with the next key's loads in flight.
+// The rows' own keys (t == step) are appended first (Q24: quantised as the
+// per-row kernel does), and after a workgroup barrier every key, the own one
+// included, is read from the cache.
+template <int RPC, int NW, bool Q24>
 __global__ void __launch_bounds__(NW * 64)
 dec_self_attention_beam_kernel(const float* __restrict__ qkv, float* __restrict__ cache, const int* __restrict__ anc,
                                int anc_ld, int step, int S, float* __restrict__ out, const int* __restrict__ skip,
@@ -1041,6 +1100,24 @@ dec_self_attention_beam_kernel(const float* __restrict__ qkv, float* __restrict_
     const int qrow = qr.tok ? step * qr.V + (step == 0 ? qr.tok0 : qr.tok[r]) : r;
     return qkv + (qr.rm ? (size_t)qrow * 3 * ND_D + part * ND_D + lane * 4 : pk(qrow, part * ND_D + lane * 4, 3 * ND_D));
   };
+  // append every row's k | v at t = step to its own slot
+  for (int j = wu; j < RPC; j += NW) {
+    const f32x4 kme = ld4(qkv_at(j, 1)), vme = ld4(qkv_at(j, 2));
+    const size_t at = (size_t)(c * RPC + j) * S + step;
+    if constexpr (Q24) {
+      const f32x4 kr = q24_raw(kme), vr = q24_raw(vme);
+      uint8_t* mine = reinterpret_cast<uint8_t*>(cache) + at * SELF_Q24_ROW;
+      *reinterpret_cast<u32x3*>(mine + 12 * lane) = u32x3{__float_as_uint(kr.x), __float_as_uint(kr.y),
+                                                          __float_as_uint(kr.z)};
+      *reinterpret_cast<u32x3*>(mine + CTXQ_V + 12 * lane) = u32x3{__float_as_uint(vr.x), __float_as_uint(vr.y),
+                                                                   __float_as_uint(vr.z)};
+      if ((lane & 7) == 0) *reinterpret_cast<f32x2*>(mine + CTXQ_S + 8 * (lane >> 3)) = f32x2{kr.w, vr.w};
+    } else {
+      float* mine = cache + at * 2 * ND_D;
+      st4(mine + lane * 4, kme);
+      st4(mine + ND_D + lane * 4, vme);
+    }
+  }
   f32x4 qv[RPC], acc[RPC];
   float m[RPC], l[RPC];
 #pragma unroll
@@ -1050,36 +1127,54 @@ dec_self_attention_beam_kernel(const float* __restrict__ qkv, float* __restrict_
     m[j] = -INFINITY;
     l[j] = 0.f;
   }
-  // this wave's keys t = wu + NW i (i = lane): every row's slot for them, one load per row
+  // this wave's keys t = wu + NW i (i = lane): every row's slot for them (t == step: its own slot)
   int sl[RPC];
   {
-    const int t = min(wu + NW * lane, max(step - 1, 0));
+    const int t = wu + NW * lane;
 #pragma unroll
-    for (int j = 0; j < RPC; ++j) sl[j] = anc[(size_t)(c * RPC + j) * anc_ld + t];
+    for (int j = 0; j < RPC; ++j) {
+      const int r = c * RPC + j;
+      sl[j] = t < step ? anc[(size_t)r * anc_ld + t] : r;
+    }
   }
-  // key t of row j: the cache row of its slot, or (t == step) this step's k | v
-  auto src = [&](int j, int t, int slot) -> const float* {
-    return t < step ? cache + ((size_t)slot * S + t) * 2 * ND_D + lane * 4 : qkv_at(j, 1);
-  };
-  auto vstep = [&](int t) -> size_t { return t < step ? (size_t)ND_D : (size_t)(qr.rm ? ND_D : pk(0, ND_D, 3 * ND_D)); };
+  // the appends are visible to every wave of the workgroup: each storing wave's stores retired, then a barrier
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // key i of this wave for every row: fp32 k | v, or (Q24) the raw image, scales in .w
   auto load = [&](int i, f32x4 (&kk)[RPC], f32x4 (&vv)[RPC]) {
     const int t = min(wu + NW * i, n - 1);  // wave-uniform; clamped (straight-line loads)
 #pragma unroll
     for (int j = 0; j < RPC; ++j) {
-      const float* p = src(j, t, __builtin_amdgcn_readlane(sl[j], min(i, 63)));
-      kk[j] = ld4(p);
-      vv[j] = ld4(p + vstep(t));
+      const size_t at = (size_t)__builtin_amdgcn_readlane(sl[j], min(i, 63)) * S + t;
+      if constexpr (Q24) {
+        const uint8_t* rb = reinterpret_cast<const uint8_t*>(cache) + at * SELF_Q24_ROW;
+        const u32x3 kb = *reinterpret_cast<const u32x3*>(rb + 12 * lane);
+        const u32x3 vb = *reinterpret_cast<const u32x3*>(rb + CTXQ_V + 12 * lane);
+        const f32x2 sc = *reinterpret_cast<const f32x2*>(rb + CTXQ_S + 8 * (lane >> 3));
+        kk[j] = f32x4{__uint_as_float(kb.x), __uint_as_float(kb.y), __uint_as_float(kb.z), sc.x};
+        vv[j] = f32x4{__uint_as_float(vb.x), __uint_as_float(vb.y), __uint_as_float(vb.z), sc.y};
+      } else {
+        const float* p = cache + at * 2 * ND_D + lane * 4;
+        kk[j] = ld4(p);
+        vv[j] = ld4(p + ND_D);
+      }
     }
   };
   const int nk = wu < n ? (n - 1 - wu) / NW + 1 : 0;  // this wave's keys
   auto update = [&](const f32x4 (&kk)[RPC], const f32x4 (&vv)[RPC]) {
 #pragma unroll
     for (int j = 0; j < RPC; ++j) {
-      const float d = sum8(qv[j].x * kk[j].x + qv[j].y * kk[j].y + qv[j].z * kk[j].z + qv[j].w * kk[j].w);
+      f32x4 kf = kk[j], vf = vv[j];
+      if constexpr (Q24) {
+        kf = q24_unpack(kk[j]);
+        vf = q24_unpack(vv[j]) * vv[j].w;
+      }
+      float d = sum8(qv[j].x * kf.x + qv[j].y * kf.y + qv[j].z * kf.z + qv[j].w * kf.w);
+      if constexpr (Q24) d *= kk[j].w;
       const float mx = fmaxf(m[j], d);
       const float sc = __expf(m[j] - mx);  // m = -inf: 0 (acc, l are 0)
       const float p = __expf(d - mx);
-      acc[j] = acc[j] * sc + p * vv[j];
+      acc[j] = acc[j] * sc + p * vf;
       l[j] = l[j] * sc + p;
       m[j] = mx;
     }
@@ -1097,14 +1192,6 @@ dec_self_attention_beam_kernel(const float* __restrict__ qkv, float* __restrict_
       update(kb, vb);
     }
   }
-  // append every row's k | v at t = step to its own slot (read above from q | k | v, not from here)
-  for (int j = wu; j < RPC; j += NW) {
-    const float* kp = qkv_at(j, 1);
-    const f32x4 kme = ld4(kp), vme = ld4(kp + vstep(step));
-    float* mine = cache + ((size_t)(c * RPC + j) * S + step) * 2 * ND_D;
-    st4(mine + lane * 4, kme);
-    st4(mine + ND_D + lane * 4, vme);
-  }
   merge_waves<RPC, NW>(accs, ms, ls, m, l, acc, wave, lane, tid, out, c * RPC);
 }
 
@@ -1113,7 +1200,8 @@ static bool use_self_beam(const int* anc, int rpc, const GreedyHead* head) { ret
 
 hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* anc, int anc_ld, int step,
                                      int max_steps, float* out, int R, hipStream_t s, int rpc, const int* skip,
-                                     const QkvRows& qr, const GreedyHead* head, const int* clist, int ccap) {
+                                     const QkvRows& qr, const GreedyHead* head, const int* clist, int ccap,
+                                     bool q24) {
   if (use_self_beam(anc, rpc, head) && R % rpc == 0) {
     if (qr.tok && (qr.V < 1 || qr.tok0 < 0 || qr.tok0 >= qr.V)) return hipErrorInvalidValue;
     if (clist && (ccap < 1 || (long)ccap * rpc > R)) return hipErrorInvalidValue;
@@ -1122,8 +1210,12 @@ hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* 
     switch (rpc) {
 #define ND_SELFB(RP)                                                                                               \
   case RP:                                                                                                         \
-    hipLaunchKernelGGL((dec_self_attention_beam_kernel<RP, 4>), dim3(grid), dim3(4 * 64), 0, s, qkv, cache, anc,  \
-                       anc_ld, step, max_steps, out, skip, qr, clist);                                             \
+    if (q24)                                                                                                       \
+      hipLaunchKernelGGL((dec_self_attention_beam_kernel<RP, 4, true>), dim3(grid), dim3(4 * 64), 0, s, qkv,      \
+                         cache, anc, anc_ld, step, max_steps, out, skip, qr, clist);                              \
+    else                                                                                                           \
+      hipLaunchKernelGGL((dec_self_attention_beam_kernel<RP, 4, false>), dim3(grid), dim3(4 * 64), 0, s, qkv,     \
+                         cache, anc, anc_ld, step, max_steps, out, skip, qr, clist);                              \
     break;
       ND_SELFB(2)
       ND_SELFB(3)
@@ -1151,9 +1243,16 @@ hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* 
   const int grid = clist ? ccap * skip_rpc : R;
   if (step >= max_steps || step >= SELF_MAXS) return hipErrorInvalidValue;
   const int n = step + 1;
-#define ND_SELF2(NW, KW, A, HD)                                                                                  \
-  hipLaunchKernelGGL((dec_self_attention_kernel<NW, KW, A, HD>), dim3(grid), dim3(NW * 64), 0, s, qkv, cache, anc,  \
-                     anc_ld, step, max_steps, out, rpc, skip, skip_rpc, qr, hd, clist)
+#define ND_SELF3(NW, KW, A, HD, Q)                                                                                \
+  hipLaunchKernelGGL((dec_self_attention_kernel<NW, KW, A, HD, Q>), dim3(grid), dim3(NW * 64), 0, s, qkv, cache,   \
+                     anc, anc_ld, step, max_steps, out, rpc, skip, skip_rpc, qr, hd, clist)
+#define ND_SELF2(NW, KW, A, HD)       \
+  do {                                \
+    if (q24)                          \
+      ND_SELF3(NW, KW, A, HD, true);  \
+    else                              \
+      ND_SELF3(NW, KW, A, HD, false); \
+  } while (0)
 #define ND_SELF(NW, KW)                \
   if (anc)                             \
     ND_SELF2(NW, KW, true, false);     \
@@ -1172,6 +1271,7 @@ hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* 
   else ND_SELF(8, 16);  // two passes beyond 128 keys
 #undef ND_SELF
 #undef ND_SELF2
+#undef ND_SELF3
   return hipGetLastError();
 }
 

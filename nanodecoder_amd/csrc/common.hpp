@@ -14,6 +14,8 @@
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+// 12 bytes as one dwordx3 access where only 4-byte alignment holds (a lane's 3 words of the 24-bit images)
+typedef unsigned u32v3 __attribute__((ext_vector_type(3), aligned(4)));
 struct u32x3 {  // 12 bytes, 4-byte aligned (one dwordx3 access)
   uint32_t x, y, z;
 };
@@ -23,7 +25,7 @@ struct u32x3 {  // 12 bytes, 4-byte aligned (one dwordx3 access)
 // a 32-wide head held by 8 consecutive lanes (lane & 7 = the dims' quad).
 // Stores the lane's 12 bytes at dst (little-endian 3-byte integers) and
 // returns the head's scale 2^(e-23) (NaN for a head holding a NaN / inf).
-__device__ __forceinline__ float q24_quant_store(f32x4 x, uint8_t* dst) {
+__device__ __forceinline__ float q24_quant(f32x4 x, u32x3& b) {
   float mx = fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w)));
   if (!(fabsf(x.x) <= 3.4028235e38f && fabsf(x.y) <= 3.4028235e38f && fabsf(x.z) <= 3.4028235e38f &&
         fabsf(x.w) <= 3.4028235e38f))
@@ -39,13 +41,23 @@ __device__ __forceinline__ float q24_quant_store(f32x4 x, uint8_t* dst) {
   const float xs[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
   for (int i = 0; i < 4; ++i) v[i] = (int)fminf(fmaxf(rintf(xs[i] * up), -8388607.f), 8388607.f);
-  u32x3 b;
   b.x = (uint32_t)(v[0] & 0xffffff) | ((uint32_t)v[1] << 24);
   b.y = (((uint32_t)v[1] >> 8) & 0xffff) | ((uint32_t)v[2] << 16);
   b.z = (((uint32_t)v[2] >> 16) & 0xff) | ((uint32_t)v[3] << 8);
-  *reinterpret_cast<u32x3*>(dst) = b;
   // a non-finite head keeps a NaN scale, so its scores / values stay non-finite as in fp32
   return mx <= 3.4028235e38f ? ldexpf(1.f, e - 23) : __builtin_nanf("");
+}
+__device__ __forceinline__ float q24_quant_store(f32x4 x, uint8_t* dst) {
+  u32x3 b;
+  const float sc = q24_quant(x, b);
+  *reinterpret_cast<u32x3*>(dst) = b;
+  return sc;
+}
+// the same 12 bytes in a register image: .xyz the three words, .w the head's scale (q24_unpack(r) * r.w = x)
+__device__ __forceinline__ f32x4 q24_raw(f32x4 x) {
+  u32x3 b;
+  const float sc = q24_quant(x, b);
+  return f32x4{__uint_as_float(b.x), __uint_as_float(b.y), __uint_as_float(b.z), sc};
 }
 
 // Four 24-bit two's-complement integers packed little-endian in the bits of

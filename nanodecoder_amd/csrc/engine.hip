@@ -865,7 +865,14 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
   };
   for (int i = 0; i < Ld; ++i) {
     DecLayer& L = c->dec[i];
-    float* cache = c->cache + (size_t)i * R * S * 2 * D;
+    // the self-attention history: beam rows keep 24-bit rows (1600 B per key, attention.hip
+    // SELF_Q24_ROW) outside exact fp32; greedy rows, exact fp32 and the average-attention layers keep
+    // fp32 k | v (2 KB).  Same box, two reps (profiles/r05_self_q24_ab.txt): configs[3] pooled
+    // 67.71 / 67.78 -> 67.28 / 67.17 ms; greedy configs[1] pooled 15.55 / 15.53 -> 15.70 / 15.74 (the
+    // row's own history is 100 keys at most: the dequantise costs more than the bytes it saves)
+    const bool sq24 = anc && !c->exact && c->cfg.self_attn_type != ND_SELF_AVERAGE;
+    float* cache = sq24 ? reinterpret_cast<float*>(reinterpret_cast<uint8_t*>(c->cache) + (size_t)i * R * S * CTXQ_ROW)
+                        : c->cache + (size_t)i * R * S * 2 * D;
     unsigned long long* stamp = c->kstamp_on ? c->kstamp + 2 * ((size_t)step * Ld + i) : nullptr;
     // -attn_debug (greedy): the last layer's head-0 context scores, [B][S][T]
     float* dbg = (c->attn_on && i == Ld - 1) ? c->attn_raw + (size_t)step * T : nullptr;
@@ -890,7 +897,7 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
         qr.tok0 = c->cfg.bos_idx;
         qr.rm = 1;  // the table is row-major (enqueue_qkv_table)
         LCHK(nd::launch_dec_self_attention(c->qtab, cache, anc, anc_ld, step, S, c->datt, R, s, rpc, done, qr, head,
-                                           clist, ccap));
+                                           clist, ccap, sq24));
       } else {
         // greedy rows (one workgroup each): q | k | v row-major; beam keeps P16 (its M = 5120 GEMMs
         // take the LDS-tiled route, which writes P16)
@@ -898,7 +905,7 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
         q12.rm = (rpc == 1 && !anc && !done) ? 1 : 0;
         LCHK(dg(c->dx, D, L.pwqkv, 3 * D, D, L.nbqkv, c->dqkv, 3 * D).ln(c->dx_part, pnx).c_rowmajor(q12.rm).run(s));
         LCHK(nd::launch_dec_self_attention(c->dqkv, cache, anc, anc_ld, step, S, c->datt, R, s, rpc, done, q12, nullptr,
-                                           clist, ccap));
+                                           clist, ccap, sq24));
       }
       LCHK(dg(c->datt, D, L.pwo, D, D, L.bo, c->dq1, D).res(c->dx, D).stats(c->dq1_part).run(s, &pnq));
     }
@@ -2126,6 +2133,18 @@ int nd_op_dec_self_attention_beam(const float* qkv, float* cache, const int32_t*
   hipError_t e = nd::launch_dec_self_attention(qkv, cache, anc, anc_ld, step, max_steps, out, R, (hipStream_t)stream,
                                                rpc, done);
   if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("dec_self_attention_beam: ") + hipGetErrorString(e));
+  return ND_OK;
+}
+
+int nd_op_dec_self_attention_q24(const float* qkv, void* cache, const int32_t* anc, int32_t anc_ld, int32_t step,
+                                 int32_t max_steps, float* out, int32_t R, int32_t rpc, const int32_t* done,
+                                 void* stream) {
+  if (!qkv || !cache || !out || rpc < 1 || rpc > 6 || R % rpc || (rpc > 1 && !anc))
+    return fail(ND_ERR_ARG, "dec_self_attention_q24: bad arguments");
+  hipError_t e = nd::launch_dec_self_attention(qkv, static_cast<float*>(cache), anc, anc_ld, step, max_steps, out, R,
+                                               (hipStream_t)stream, rpc, done, nd::QkvRows(), nullptr, nullptr, 0,
+                                               true);
+  if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("dec_self_attention_q24: ") + hipGetErrorString(e));
   return ND_OK;
 }
 

@@ -223,7 +223,9 @@ struct GreedyHead;
 hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* anc, int anc_ld, int step,
                                      int max_steps, float* out, int R, hipStream_t s, int rpc = 1,
                                      const int* skip = nullptr, const QkvRows& qr = QkvRows(),
-                                     const GreedyHead* head = nullptr, const int* clist = nullptr, int ccap = 0);
+                                     const GreedyHead* head = nullptr, const int* clist = nullptr, int ccap = 0,
+                                     bool q24 = false);
+// q24: the cache holds 1600-B 24-bit rows (attention.hip SELF_Q24_ROW) instead of [512] floats
 // context attention: rows r = c*rpc + j attend over ctxkv rows of chunk c
 // (K at kv[(c*T+t)*ld + koff], V at +256), mask signal == pad_val, keys < span.
 // q24: kv is the 24-bit image of launch_ctx_pack_q24 (ld, koff in bytes).

@@ -657,6 +657,20 @@ def op_dec_self_attention_beam(qkv, cache, step, anc, rpc, done=None):
     return unpack_p16(out, R)
 
 
+def op_dec_self_attention_q24(qkv, cache, step, anc=None, rpc=1, done=None):
+    """The 24-bit-history self-attention (nd_op_dec_self_attention_q24): qkv [R, 768] row-major, cache uint8
+    [R, S, 1600] (appended in place), anc [R, S] or None (rpc 1); returns out [R, 256] row-major."""
+    R = qkv.shape[0]
+    S = cache.shape[1]
+    qp = pack_p16(qkv)
+    out = torch.empty(qp.shape[0], 256, dtype=torch.float32, device=qkv.device)
+    s = ctypes.c_void_p(torch.cuda.current_stream(qkv.device).cuda_stream)
+    _lib.check(_lib.lib().nd_op_dec_self_attention_q24(_ptr(qp), _ptr(cache), _ptr(anc), S if anc is not None else 0,
+                                                       step, S, _ptr(out), R, rpc, _ptr(done), s),
+               "nd_op_dec_self_attention_q24")
+    return unpack_p16(out, R)
+
+
 def op_dec_ctx_attention(q, kv, ld, koff, signal, span, pad_val, rpc, packed=False):
     """q [C*rpc, 256] row-major (or P16-packed with packed=True); returns out
     in the same convention."""

@@ -373,6 +373,48 @@ def test_dec_self_attention_beam_vs_fp64(rpc, step):
     assert torch.equal(appended[~live], cache[~live, step])  # a finished chunk's rows are not written
 
 
+@pytest.mark.parametrize("rpc,beam", [(1, False), (1, True), (5, True), (2, True)])
+def test_dec_self_attention_q24_history_vs_fp64(rpc, beam):
+    """The engine's default self-attention history: every step quantises its
+    k|v to the 24-bit rows and appends them; 70 steps run in order (the
+    per-row kernel's 4- and 8-wave forms, one and two key passes are crossed
+    at 16 / 32 / 64 keys) and each step's output is held against fp64 over
+    the fp32 k|v every earlier step appended (beam: through a fixed ancestry,
+    a shared prefix then per-row slots of the chunk).  Tolerance 2e-5 of the
+    values' magnitude (a 24-bit element carries 2^-23 of its head's largest
+    value, as the context image)."""
+    from nanodecoder_amd.engine import op_dec_self_attention_q24
+    C, S, steps = 9, 128, 70
+    R = C * rpc
+    g = torch.Generator().manual_seed(17 + rpc + 10 * beam)
+    qkv = [torch.randn(R, 768, generator=g) for _ in range(steps)]
+    qkv[40][:, 256 + 32: 256 + 64] *= 1e3   # one head of one step's keys 1000x the rest
+    anc = None
+    if beam:
+        anc = torch.empty(R, S, dtype=torch.int32)
+        for c in range(C):
+            for j in range(rpc):
+                r = c * rpc + j
+                anc[r, :20] = c * rpc
+                anc[r, 20:] = torch.randint(0, rpc, (S - 20,), generator=g, dtype=torch.int32) + c * rpc
+    dev = torch.device("cuda", 0)
+    cache = torch.zeros(R, S, 1600, dtype=torch.uint8, device=dev)
+    ad = anc.to(dev) if beam else None
+    for step in range(steps):
+        out = op_dec_self_attention_q24(qkv[step].to(dev), cache, step, anc=ad, rpc=rpc).cpu().double()
+        if step not in (0, 1, 15, 16, 17, 33, 40, 41, 64, 65, 69):
+            continue
+        q = qkv[step][:, :256].double().view(R, 8, 32) / np.float32(np.sqrt(32.0))
+        for r in range(R):
+            src = [(int(anc[r, t]) if beam else r) for t in range(step)] + [r]
+            kv = torch.stack([qkv[t][src[t], 256:].double() for t in range(step + 1)])   # [step + 1, 512]
+            k, v = kv[:, :256].view(-1, 8, 32), kv[:, 256:].view(-1, 8, 32)
+            p = torch.softmax(torch.einsum("hd,thd->ht", q[r], k), dim=-1)
+            ref = torch.einsum("ht,thd->hd", p, v).reshape(256)
+            err = (out[r] - ref).abs().max().item()
+            assert err < 2e-5 * max(1.0, v.abs().max().item()), (r, step, err)
+
+
 @pytest.mark.parametrize("scale", [1.0, 4.0, "rising"])
 def test_enc_attention_vs_oracle(scale):
     """Split-fp16 encoder attention against the oracle's attend: masked keys,
