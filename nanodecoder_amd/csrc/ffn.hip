@@ -71,6 +71,12 @@ typedef __attribute__((address_space(3))) void lds_void;
 #define FF_HC 32                    // hidden columns per chunk (one k-block of phase 2)
 #define FF_SLICE 32768              // bytes of one weight slice in LDS
 #define FF_MAXF 2048                // d_ff bound (b1 staged whole in LDS)
+#ifndef FF_SPREAD
+#define FF_SPREAD 1  // the main loop's copies issued between its MFMA units (0: all at the step's start)
+#endif
+#ifndef FF_SPREAD_STRIDE
+#define FF_SPREAD_STRIDE 2  // one piece every this many units, from unit 1
+#endif
 #ifndef FF_AHEAD
 #define FF_AHEAD 2                  // units whose LDS reads are in flight beyond the one computed
 #endif
@@ -155,6 +161,18 @@ __device__ __forceinline__ void ff_copy_w1(ff_src w1h, int j, char* dst, int wav
     ff_piece(w1h, j * FF_SLICE + blk * 1024, dst + blk * 1024, lane);
   }
 }
+// piece i of this wave's share of the W1 / W2 slice copies (the main loop
+// issues them one at a time between its MFMA units)
+template <int NW>
+__device__ __forceinline__ void ff_piece_w1(ff_src w1h, int j, char* dst, int wave, int lane, int i) {
+  const int blk = __builtin_amdgcn_readfirstlane(wave) * (32 / NW) + i;
+  ff_piece(w1h, j * FF_SLICE + blk * 1024, dst + blk * 1024, lane);
+}
+template <int NW>
+__device__ __forceinline__ void ff_piece_w2(ff_src w2h, int kp, int j, char* dst, int wave, int lane, int i) {
+  const int blk = __builtin_amdgcn_readfirstlane(wave) * (32 / NW) + i, nt = blk >> 1, pl = blk & 1;
+  ff_piece(w2h, ((nt * kp + j) * 2 + pl) * 1024, dst + blk * 1024, lane);
+}
 // W2 slice j: output tile nt, k-block j, plane -> LDS block nt * 2 + plane
 template <int NW>
 __device__ __forceinline__ void ff_copy_w2(ff_src w2h, int kp, int j, char* dst, int wave, int lane) {
@@ -186,6 +204,9 @@ enc_ffn_kernel(const float* y, const uint16_t* __restrict__ w1h, float w1s, cons
 #endif
   static_assert(!DEC || (!WO && !QK && RG == 1), "the decoder form folds nothing");
   constexpr int NW = FF_BM / (16 * RG), NT = NW * 64;
+  // the main loop's copies between its MFMA units (not in the decoder form: 6 VGPRs spilled there)
+  constexpr bool SPREAD = FF_SPREAD && !DEC;
+  static_assert(!SPREAD || 2 * (32 / NW) == 8, "the spread copies are 8 pieces per wave");
   // every split of a dead row block exits alike (its ticket stays 0)
   if constexpr (DEC)
     if (rows_dead(df.skip, df.skip_rpc, blockIdx.x * FF_BM, FF_BM, M)) return;
@@ -412,8 +433,10 @@ enc_ffn_kernel(const float* y, const uint16_t* __restrict__ w1h, float w1s, cons
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #endif
 #ifndef FF_PROBE_NOCOPY  // timing probe only: no weight copies in the main loop (wrong results)
-    if (k + 1 < nch) ff_copy_w2<NW>(W2, kp, k + 1, w2slot(k + 1), wave, lane);
-    if (k + 2 < nch) ff_copy_w1<NW>(W1, k + 2, w1slot(k), wave, lane);
+    if constexpr (!SPREAD) {
+      if (k + 1 < nch) ff_copy_w2<NW>(W2, kp, k + 1, w2slot(k + 1), wave, lane);
+      if (k + 2 < nch) ff_copy_w1<NW>(W1, k + 2, w1slot(k), wave, lane);
+    }
 #endif
     const f32x4* A2 = reinterpret_cast<const f32x4*>(w2slot(k)) + lane;
     const f32x4* A1 = reinterpret_cast<const f32x4*>(w1slot(k + 1)) + lane;
@@ -447,9 +470,22 @@ enc_ffn_kernel(const float* y, const uint16_t* __restrict__ w1h, float w1s, cons
     for (int g = 0; g < RG; ++g) h[g][0] = h[g][1] = f32x4{0.f, 0.f, 0.f, 0.f};
     ff_static_for([&](auto uc) { ff_fetch<decltype(uc)::value, RING>(rh, rl, a1, a2); },
                   std::make_integer_sequence<int, FF_AHEAD>{});
+    // SPREAD: this step's copies (W2_{k+1}, then W1_{k+2}: its chunk index clamped, so the
+    // step before the last re-copies a slice into the free slot instead of branching
+    // inside the read ring), one piece every second unit of the first half: each
+    // piece's issue sits between MFMAs the SIMD's other wave keeps running, and
+    // 16 units remain for the last to land before the next step's vmcnt(0)
+    const int j1 = min(k + 2, nch - 1);
     ff_static_for(
         [&](auto uc) {
           constexpr int u = decltype(uc)::value;
+          if constexpr (SPREAD && u % FF_SPREAD_STRIDE == 1 && u < 1 + 8 * FF_SPREAD_STRIDE) {
+            constexpr int p = u / FF_SPREAD_STRIDE;
+            if constexpr (p < 32 / NW)
+              ff_piece_w2<NW>(W2, kp, k + 1, w2slot(k + 1), wave, lane, p);
+            else
+              ff_piece_w1<NW>(W1, j1, w1slot(k), wave, lane, p - 32 / NW);
+          }
           if constexpr (u + FF_AHEAD < 32) ff_fetch<u + FF_AHEAD, RING>(rh, rl, a1, a2);
           ff_wait<u, RING, 32>(rh, rl);
           const fh8 wh = __builtin_bit_cast(fh8, rh[u % RING]), wl = __builtin_bit_cast(fh8, rl[u % RING]);
