@@ -299,6 +299,44 @@ def test_gemm_p16_vs_fp64(M, N, K, ln, relu, res, stats, split):
         assert torch.allclose(got[:, :, 1], want[:, :, 1], rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("lg", [0, -7, -14, -20])
+@pytest.mark.parametrize("M,K", [(256, 256), (256, 2048), (1280, 256)])
+def test_gemm_split_small_rows_follow_the_scheme(lg, M, K):
+    """Activation rows of scale 2^lg through the split-fp16 P16 GEMM (no
+    LayerNorm in front: W_o / W_2 / W_vo's operands): the kernel follows the
+    numpy restatement of the split (tests/test_split_fp16_scheme.py) to fp32
+    accumulation -- fp16 subnormal lo parts are kept, not flushed -- so its
+    error relative to the row's own output is ~2^-24 / sigma below sigma ~
+    2^-3 and, added to an O(1) residual, within twice that residual's fp32
+    rounding at every scale."""
+    from nanodecoder_amd.engine import op_gemm_p16, op_pack_p16h, pack_p16, unpack_p16
+    from tests.test_split_fp16_scheme import split_product
+    N = 256
+    g = torch.Generator().manual_seed(11 * M + K - lg)
+    A = torch.randn(M, K, generator=g) * 2.0 ** lg
+    W = torch.randn(N, K, generator=g) / 16
+    R = torch.rand(M, N, generator=g) + 1.0  # a residual in [1, 2): its fp32 rounding is 2^-24 .. 2^-23
+    dev = torch.device("cuda", 0)
+    zero = torch.zeros(N, device=dev)
+    Wh, sc = op_pack_p16h(W.to(dev))
+    Ap = pack_p16(A.to(dev))
+    C0 = unpack_p16(op_gemm_p16(Ap, None, zero, M, N, K, Wh=Wh, wscale=sc)[0], M).cpu().double()
+    C1 = unpack_p16(op_gemm_p16(Ap, None, zero, M, N, K, pack_p16(R.to(dev)), Wh=Wh, wscale=sc)[0], M).cpu().double()
+    emu = torch.from_numpy(split_product(A.numpy(), W.numpy()))
+    ref = A.double() @ W.double().t()
+    rms = ref.pow(2).mean(1, keepdim=True).sqrt()
+    l1 = W.abs().sum(1).max().item()
+    # the kernel is the scheme, to fp32 accumulation (plus 2^-30 / sigma: at sigma 2^-20, M = 1280 differs from
+    # the restatement by 3.9e-6 of the row, against the scheme's own 8e-2; a flushed lo would differ by ~1e-1)
+    assert ((C0 - emu).abs() / rms).max().item() < 2.0 ** -18 * (K / 256) ** 0.5 + 2.0 ** -30 / 2.0 ** lg
+    # the scheme's error: relative to the row below 4e-6 + 2^-23 / sigma ...
+    assert ((C0 - ref).abs() / rms).max().item() < 4e-6 + 2.0 ** -23 / 2.0 ** lg
+    # ... and scale-free in absolute terms: rows of scale <= 2^-7 added to a residual in [1, 2) stay within
+    # the residual sum's own rounding (at scale 1 the output's own fp32 rounding dominates: the line above)
+    if lg <= -7:
+        assert (C1 - (ref + R.double())).abs().max().item() < 2.0 ** -23 + 2.0 ** -24 * l1 * (K / 256) ** 0.5
+
+
 @pytest.mark.parametrize("step", [0, 1, 31, 32, 63, 64, 99, 127, 128, 200])
 @pytest.mark.parametrize("beam", [False, True])
 def test_dec_self_attention_vs_fp64(step, beam):
