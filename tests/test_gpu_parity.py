@@ -254,7 +254,11 @@ def test_gemm_p16_splitk_vs_fp64(M, N, K, res):
                                                       (5120, 2048, 256, True, True, False, False),   # beam 5 x 1024
                                                       (5120, 256, 2048, False, False, True, True),
                                                       (5120, 768, 256, True, False, False, False),
-                                                      (2560, 256, 256, True, False, True, True)])
+                                                      (2560, 256, 256, True, False, True, True),
+                                                      (5120, 256, 256, False, False, True, True),    # beam Wo (64 x 64 tiles)
+                                                      (5120, 256, 256, True, False, False, False),   # beam context query
+                                                      (2048, 128, 256, True, True, False, False),
+                                                      (4100, 256, 256, False, False, True, True)])   # ragged last tile
 @pytest.mark.parametrize("split", [False, True, "rm"])
 def test_gemm_p16_vs_fp64(M, N, K, ln, relu, res, stats, split):
     """The decoder-step GEMM on the P16 layout: LN from handed-over row
