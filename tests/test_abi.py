@@ -263,3 +263,25 @@ def test_lds_paired_forms_above_64k_are_reviewed():
     # the closed-form layer-0 attention keeps its whole allocation at 64 KB
     r2 = [r for r in kernel_meta.collect() if "enc_attention_rank2_kernel" in r["name"]]
     assert r2 and all(r["lds"] <= 65536 for r in r2)
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    """No HIP library, no engine: with the library path pointing at nothing, the
+    product path (an Engine, a Translator's first call) raises NanodecError
+    naming the build step; there is no CPU fallback to run instead."""
+    import subprocess
+    import sys
+    code = ("import sys\n"
+            "from nanodecoder_amd import _lib, synth\n"
+            "from nanodecoder_amd.engine import Engine\n"
+            "cfg = synth.ModelConfig()\n"
+            "try:\n"
+            "    Engine(cfg, synth.make_weights(cfg, seed=1), device=0)\n"
+            "except _lib.NanodecError as e:\n"
+            "    print('raised:', e)\n"
+            "    sys.exit(0)\n"
+            "sys.exit(3)\n")
+    env = dict(os.environ, NANODEC_LIB=str(tmp_path / "absent.so"))
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "not found" in r.stdout and "no CPU fallback" in r.stdout, r.stdout
