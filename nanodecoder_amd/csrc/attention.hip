@@ -1140,37 +1140,46 @@ dec_self_attention_beam_kernel(const float* __restrict__ qkv, float* __restrict_
   // the appends are visible to every wave of the workgroup: each storing wave's stores retired, then a barrier
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  // key i of this wave for every row: fp32 k | v, or (Q24) the raw image, scales in .w
-  auto load = [&](int i, f32x4 (&kk)[RPC], f32x4 (&vv)[RPC]) {
+  // key i of this wave for every row: fp32 k | v, or (Q24) the raw image loaded into the registers the
+  // arithmetic reads (12 + 12 bytes and the head's two scales: composing them into one f32x4 per row made
+  // hipcc wait for each key's loads right after issuing them)
+  struct Key {
+    f32x4 k, v;   // fp32 form
+    u32v3 kq, vq;  // Q24 form
+    f32x2 sq;
+  };
+  auto load = [&](int i, Key (&kk)[RPC]) {
     const int t = min(wu + NW * i, n - 1);  // wave-uniform; clamped (straight-line loads)
 #pragma unroll
     for (int j = 0; j < RPC; ++j) {
       const size_t at = (size_t)__builtin_amdgcn_readlane(sl[j], min(i, 63)) * S + t;
       if constexpr (Q24) {
         const uint8_t* rb = reinterpret_cast<const uint8_t*>(cache) + at * SELF_Q24_ROW;
-        const u32x3 kb = *reinterpret_cast<const u32x3*>(rb + 12 * lane);
-        const u32x3 vb = *reinterpret_cast<const u32x3*>(rb + CTXQ_V + 12 * lane);
-        const f32x2 sc = *reinterpret_cast<const f32x2*>(rb + CTXQ_S + 8 * (lane >> 3));
-        kk[j] = f32x4{__uint_as_float(kb.x), __uint_as_float(kb.y), __uint_as_float(kb.z), sc.x};
-        vv[j] = f32x4{__uint_as_float(vb.x), __uint_as_float(vb.y), __uint_as_float(vb.z), sc.y};
+        kk[j].kq = *reinterpret_cast<const u32v3*>(rb + 12 * lane);
+        kk[j].vq = *reinterpret_cast<const u32v3*>(rb + CTXQ_V + 12 * lane);
+        kk[j].sq = *reinterpret_cast<const f32x2*>(rb + CTXQ_S + 8 * (lane >> 3));
       } else {
         const float* p = cache + at * 2 * ND_D + lane * 4;
-        kk[j] = ld4(p);
-        vv[j] = ld4(p + ND_D);
+        kk[j].k = ld4(p);
+        kk[j].v = ld4(p + ND_D);
       }
     }
   };
   const int nk = wu < n ? (n - 1 - wu) / NW + 1 : 0;  // this wave's keys
-  auto update = [&](const f32x4 (&kk)[RPC], const f32x4 (&vv)[RPC]) {
+  auto update = [&](const Key (&kk)[RPC]) {
 #pragma unroll
     for (int j = 0; j < RPC; ++j) {
-      f32x4 kf = kk[j], vf = vv[j];
+      f32x4 kf, vf;
       if constexpr (Q24) {
-        kf = q24_unpack(kk[j]);
-        vf = q24_unpack(vv[j]) * vv[j].w;
+        kf = q24_unpack(f32x4{__uint_as_float(kk[j].kq.x), __uint_as_float(kk[j].kq.y), __uint_as_float(kk[j].kq.z), 0.f});
+        vf = q24_unpack(f32x4{__uint_as_float(kk[j].vq.x), __uint_as_float(kk[j].vq.y), __uint_as_float(kk[j].vq.z), 0.f}) *
+             kk[j].sq.y;
+      } else {
+        kf = kk[j].k;
+        vf = kk[j].v;
       }
       float d = sum8(qv[j].x * kf.x + qv[j].y * kf.y + qv[j].z * kf.z + qv[j].w * kf.w);
-      if constexpr (Q24) d *= kk[j].w;
+      if constexpr (Q24) d *= kk[j].sq.x;
       const float mx = fmaxf(m[j], d);
       const float sc = __expf(m[j] - mx);  // m = -inf: 0 (acc, l are 0)
       const float p = __expf(d - mx);
@@ -1181,15 +1190,15 @@ dec_self_attention_beam_kernel(const float* __restrict__ qkv, float* __restrict_
   };
   // two register sets in turn (a copy from one to the other would make hipcc wait for the loads it
   // just issued); the loads past the last key are clamped to it (straight-line) and never used
-  f32x4 ka[RPC], va[RPC], kb[RPC], vb[RPC];
+  Key ka[RPC], kb[RPC];
   if (nk > 0) {
-    load(0, ka, va);
+    load(0, ka);
     for (int i = 0; i < nk; i += 2) {
-      load(min(i + 1, nk - 1), kb, vb);
-      update(ka, va);
+      load(min(i + 1, nk - 1), kb);
+      update(ka);
       if (i + 1 >= nk) break;
-      load(min(i + 2, nk - 1), ka, va);
-      update(kb, vb);
+      load(min(i + 2, nk - 1), ka);
+      update(kb);
     }
   }
   merge_waves<RPC, NW>(accs, ms, ls, m, l, acc, wave, lane, tid, out, c * RPC);

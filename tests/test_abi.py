@@ -107,6 +107,10 @@ def test_hot_path_kernels_do_not_drain_loads(listings):
             # the form that runs the previous step's head: wave 0 waits for the
             # head's own loads, then issues its cache loads (the one allowed)
             ("attention", r"dec_self_attention_kernelILi\d+ELi\d+ELb0ELb1E", 1),
+            # beam rows, the bench's beam 5 on the 24-bit history: the one wait is the appends' (vmcnt(0) and a
+            # barrier before any wave reads the cache); the keys' loads go straight into the registers the
+            # arithmetic reads (composing them made hipcc wait per key: 7 drains before)
+            ("attention", r"dec_self_attention_beam_kernelILi5ELi4ELb1E", 1),
             # the 24-bit digit bank: the walking form (pool lanes) issues straight-line;
             # the one-chunk form's two sit in the unrolled key loop: the wait for the last fragment of the
             # half block being multiplied, right before the next half block's loads (reviewed, round 5)
