@@ -874,7 +874,8 @@ __device__ __forceinline__ void merge_waves_part(float* accs, float* ms, float* 
 // previous step's greedy head for the row (head.hpp), whose token picks the
 // row's q | k | v in the table; the other waves' cache loads are in flight
 // meanwhile.  One launch per step fewer than a standalone head kernel.
-// Q24 (round 5, every call outside exact fp32): the cache holds each (slot,
+// Q24 (round 5; beam rows outside exact fp32, engine.hip enqueue_dec_step; greedy rows keep fp32, which
+// measured faster for them; the greedy Q24 form is the op entry's): the cache holds each (slot,
 // t) as the 24-bit image of the beam's context K/V (k's 256 integers | v's |
 // per head {k scale, v scale}: SELF_Q24_ROW = 1600 B instead of 2 KB,
 // common.hpp q24_quant); a lane's key is its 12 bytes of k and of v and its
