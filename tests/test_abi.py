@@ -289,3 +289,14 @@ def test_missing_library_fails_loudly(tmp_path):
     r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "not found" in r.stdout and "no CPU fallback" in r.stdout, r.stdout
+
+
+def test_integration_names_every_entry_point():
+    """INTEGRATION.md, the maintainer's binding guide, names every entry point
+    include/nanodec.h declares (with the reference interface it replaces, or
+    'no reference equivalent')."""
+    import re
+    with open(os.path.join(ROOT, "INTEGRATION.md")) as f:
+        doc = f.read()
+    missing = [s for s in sorted(declared_symbols()) if s not in doc]
+    assert not missing, missing
