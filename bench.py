@@ -329,6 +329,13 @@ def kernel_roofline(eng, B, mode, beam, encoder="transformer", alive=None, secon
             "note": ("fp32 K+V per chunk per layer-step (SURVEY §8d); the kernel streams a folded bank (x 0.5: "
                      "W_k folded into q', W_v into the output projection) in 24 bits (x 0.75) = 0.375 of these "
                      "bytes, so this equivalent rate is not a fraction of the HBM peak")}
+        # the bound the probe found: a lone call's 104 MB bank stays in the 256 MB Infinity Cache across the
+        # step's launches; resident vs evicted measured 22.5 vs 25.8 us (tools/bank_mall.py)
+        extra["residency"] = {"infinity_cache_resident_us": 22.54, "evicted_us": 25.79,
+                              "source": "profiles/r05_bank_mall.txt",
+                              "note": ("HBM bytes set ~13% of this kernel's time; the rest is its per-key-block "
+                                       "issue work (LDS image writes and transposed reads, digit -> f16 "
+                                       "conversions, MFMAs at two waves per SIMD), DESIGN.md §8")}
     out = {"bound": "hbm", "kernel": name, "achieved": round(ach, 1), "peak": HBM_PEAK, "unit": "GB/s",
            "frac": round(ach / HBM_PEAK, 4), "traffic": _pmc(name, "kernels" if mode == "greedy" else "kernels_beam"),
            "algorithmic_bytes_per_launch": nbytes,
