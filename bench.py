@@ -220,13 +220,43 @@ class _StreamTimer:
 
 
 def _pmc(name, key="kernels"):
-    """HBM bytes per launch for kernel `name` from the committed PMC summary
-    (profiles/pmc_summary.json, tools/pmc_summary.py: rocprofv3 --pmc
-    FETCH_SIZE / WRITE_SIZE passes with the gfx950 x2 FETCH_SIZE correction)."""
+    """(HBM bytes per launch, the table entry used) for kernel `name` from the
+    committed PMC summary (profiles/pmc_summary.json, tools/pmc_summary.py:
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes with the gfx950 x2
+    FETCH_SIZE correction), or (None, None).  The table keys kernels by their
+    full template name ('dec_bank_d8_kernel<false, false>'): an exact name is
+    looked up as given; a bare name takes its only instantiation in the table,
+    or the plain '<false, false>' one among several."""
     p = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(p) as f:
-            return json.load(f)[key][name]["hbm_bytes_per_launch"]
+            table = json.load(f)[key]
+    except Exception:
+        return None, None
+    if name in table:
+        return table[name]["hbm_bytes_per_launch"], name
+    forms = sorted(k for k in table if k.split("<")[0] == name.split("<")[0])
+    if len(forms) > 1:
+        forms = [k for k in forms if k.endswith("<false, false>")] or forms
+    if len(forms) == 1:
+        return table[forms[0]]["hbm_bytes_per_launch"], forms[0]
+    return None, None
+
+
+def _pmc_beam():
+    """configs[3]'s context-attention counter traffic per alive chunk-launch
+    from the newest committed profiles/rNN_pmc_beam.json (tools/pmc_beam.py:
+    FETCH_SIZE / WRITE_SIZE passes over exactly the config_legs workload), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc_beam.json")))
+    if not files:
+        return None
+    try:
+        with open(files[-1]) as f:
+            d = json.load(f)
+        c = d["ctx_attention"]
+        return {"per_alive_chunk": c["traffic_per_alive_chunk_launch"], "ratio": c["ratio"],
+                "source": "profiles/" + os.path.basename(files[-1]), "workload": d["workload"]}
     except Exception:
         return None
 
@@ -293,7 +323,9 @@ def kernel_roofline(eng, B, mode, beam, encoder="transformer", alive=None, secon
         # float scale per key row); exact fp32 runs the fp32 bank kernel
         form = eng.engines[0].bank_form() if hasattr(eng, "engines") else eng.bank_form()
         if form == 2:
-            name = "dec_bank_d8_kernel"
+            e0 = eng.engines[0] if hasattr(eng, "engines") else eng
+            # the instantiation this call launched (bank8.hip: <non-temporal, grid walk>), as the PMC table keys it
+            name = f"dec_bank_d8_kernel<{'true' if e0.bank_nt else 'false'}, {'true' if e0.bank_grid else 'false'}>"
             nbytes = B * T * D * 3 + B * T * 4 + B * 4 + B * T * 4 + 2 * B * 8 * D * 4
         else:
             name = "dec_mem_attention_kernel<8>"
@@ -336,8 +368,21 @@ def kernel_roofline(eng, B, mode, beam, encoder="transformer", alive=None, secon
                               "note": ("HBM bytes set ~13% of this kernel's time; the rest is its per-key-block "
                                        "issue work (LDS image writes and transposed reads, digit -> f16 "
                                        "conversions, MFMAs at two waves per SIMD), DESIGN.md §8")}
+    traffic, tsrc = _pmc(name, "kernels" if mode == "greedy" else "kernels_beam")
+    if mode == "greedy":
+        tnote = (f"profiles/pmc_summary.json kernels['{tsrc}'] (one configs[1] call, rocprofv3 FETCH_SIZE / "
+                 f"WRITE_SIZE passes: L2 <-> fabric bytes, HBM or Infinity Cache; the non-temporal form moves "
+                 f"the same lines)" if tsrc else None)
+    else:
+        pb = _pmc_beam() if "alive_chunks_per_launch" in extra else None
+        traffic, tnote = None, None
+        if pb is not None:
+            # the counter pass's bytes per alive chunk-launch x this leg's alive chunks per launch (same workload)
+            traffic = int(pb["per_alive_chunk"] * extra["alive_chunks_per_launch"])
+            tnote = (f"{pb['source']}: {pb['per_alive_chunk']:.0f} B per alive chunk-launch, {pb['ratio']}x the "
+                     f"algorithmic {nbytes / max(extra['alive_chunks_per_launch'], 1e-9):.0f}; {pb['workload']}")
     out = {"bound": "hbm", "kernel": name, "achieved": round(ach, 1), "peak": HBM_PEAK, "unit": "GB/s",
-           "frac": round(ach / HBM_PEAK, 4), "traffic": _pmc(name, "kernels" if mode == "greedy" else "kernels_beam"),
+           "frac": round(ach / HBM_PEAK, 4), "traffic": traffic, "traffic_source": tnote,
            "algorithmic_bytes_per_launch": nbytes,
            "avg_launch_ms": round(ms, 5), "timed_launches": n,
            "timing": "in-kernel wall-clock stamps, launches of the last timed call",
@@ -501,6 +546,7 @@ def pool_check(cfg, W, args, mode, B, beam, call, outs):
     from nanodecoder_amd.engine import Engine
     one = Engine(cfg, W, device=torch.cuda.current_device(), max_batch=B, max_src_len=512,
                  max_steps=args.max_length, max_beam=beam)
+    one.set_gemm_splitk(args.inflight > 1)  # the lanes' K = 2048 product form (nd_set_gemm_splitk)
     try:
         ref = call(one)
         keys = ("tokens", "scores") + (("lens",) if mode == "beam" else ())
@@ -513,7 +559,8 @@ def pool_check(cfg, W, args, mode, B, beam, call, outs):
                     bad.append(f"lane {lane} {k}")
         return {"result": "identical" if not bad else "DIFFERENT: " + ", ".join(bad),
                 "lanes_compared": sum(o is not None for o in outs),
-                "against": "a fresh single Engine (one call in flight, bank kernel one workgroup per chunk)"}
+                "against": "a fresh single Engine (one call in flight, bank kernel one workgroup per chunk, the "
+                           "lanes' split-K form)"}
     finally:
         one.close()
 
@@ -650,6 +697,7 @@ def run_batch(args, world, rank, dev, cfg, W):
         one = eng.subset(1)
         # a lone call has every CU: the bank kernel at one workgroup per chunk (nd_set_bank_grid)
         eng.engines[0].set_bank_grid(0)
+        eng.engines[0].set_gemm_splitk(False)  # and the long-K products one workgroup per tile
         n1 = max(3, min(40, args.steps // 4))
         run_calls(one, 2, call)
         dt1, _ = timed(one, n1, call, world)
@@ -663,6 +711,7 @@ def run_batch(args, world, rank, dev, cfg, W):
             roof_iso["timing"] = ("in-kernel wall-clock stamps, launches of the last call of the timed "
                                   "one-call-in-flight leg (the kernel alone on the GPU, one workgroup per chunk)")
         eng.engines[0].set_bank_grid(eng.bank_grid)
+        eng.engines[0].set_gemm_splitk(eng.splitk)
     alive = None
     if args.mode == "beam":
         alive = beam_steps_and_worst_case(args, eng, sig, lens, call, out, world, res)

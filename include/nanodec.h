@@ -78,7 +78,9 @@ int nd_finalize(nd_ctx* ctx);
 /* ctx (just created, no weight loaded, the same model configuration as src)
  * reads src's weights and every image nd_finalize derived from them instead
  * of holding its own; ctx is finalized by this call.  src must be finalized,
- * on the same device, and outlive ctx.  For several contexts of one model on
+ * on the same device, and outlive ctx.  ND_ERR_STATE if a weight was loaded
+ * into ctx; nd_load_weight on ctx afterwards returns ND_ERR_STATE.  ctx's own
+ * raw weight buffers from nd_create stay allocated and unread.  For several contexts of one model on
  * one GPU (EnginePool lanes): one copy of the weights in the caches they
  * share (L2 per XCD, the Infinity Cache).  No reference counterpart (the
  * reference holds one model per process). */
@@ -253,6 +255,14 @@ int nd_set_bank_policy(nd_ctx* ctx, int nontemporal);
  * Same results (each chunk is one workgroup's work either way).  No reference
  * counterpart. */
 int nd_set_bank_grid(nd_ctx* ctx, int32_t workgroups);
+
+/* The decoder step's K = 2048 products (W_vo, FFN2 at 256 rows) split over
+ * workgroups (gemm_p16k_kernel, partial slabs + arrival tickets) instead of
+ * one workgroup per output tile.  Default 0 (off): a lone call is faster
+ * without; several calls in flight (EnginePool lanes) gain from it (DESIGN.md
+ * section 3).  Results differ from the unsplit kernel's in fp32 rounding of
+ * the K sum only.  No reference counterpart. */
+int nd_set_gemm_splitk(nd_ctx* ctx, int32_t on);
 
 /* Split-fp16 range guard.  An activation operand the split form carries as
  * fp16 hi/lo leaves the fp16 range from |x| = 65504 on, where the

@@ -18,6 +18,7 @@ ND_ENC_TRANSFORMER = 0
 ND_ENC_NANO = 1
 ND_SELF_SCALED_DOT = 0
 ND_SELF_AVERAGE = 1
+ND_ERR_ARG, ND_ERR_WEIGHT, ND_ERR_HIP, ND_ERR_STATE = 1, 2, 3, 4  # include/nanodec.h status codes
 
 _CFG_FIELDS = ["encoder_type", "enc_layers", "dec_layers", "d_model", "heads", "d_ff", "vocab", "rnn_hidden",
                "position_encoding", "pad_idx", "bos_idx", "eos_idx", "max_batch", "max_src_len", "max_steps",
@@ -61,6 +62,7 @@ SIGNATURES = {
     "nd_set_exact_fp32": (_I, [_P, _I]),
     "nd_set_bank_policy": (_I, [_P, _I]),
     "nd_set_bank_grid": (_I, [_P, _I]),
+    "nd_set_gemm_splitk": (_I, [_P, _I]),
     "nd_take_overflow": (_I, [_P, _P, _P]),
     "nd_set_ctx_path": (_I, [_P, _I]),
     "nd_last_timing": (_I, [_P, ctypes.POINTER(_F), ctypes.POINTER(_F)]),
@@ -121,15 +123,21 @@ def lib():
         raise NanodecError(f"{LIB_PATH} not found: build it with `python -m nanodecoder_amd.build` "
                            "(there is no CPU fallback)")
     L = ctypes.CDLL(LIB_PATH)
-    intree = os.path.realpath(LIB_PATH) == os.path.realpath(os.path.join(HERE, "libnanodec_hip.so"))
+    # an older timing-variant library (NANODEC_LIB) in an A/B run (tools/ab_lib*.sh set NANODEC_AB=1) may lack
+    # entry points added since: they stay unbound there.  Anywhere else a missing entry point is a stale or
+    # mismatched library, refused at load time
+    ab = os.environ.get("NANODEC_AB") == "1"
+    missing = []
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(L, name, None)
         if fn is None:
-            if intree:
-                raise NanodecError(f"{LIB_PATH} does not export {name}: rebuild it")
-            continue  # an older timing-variant library (NANODEC_LIB, A/B runs): entry points it lacks stay unbound
+            missing.append(name)
+            continue
         fn.restype = res
         fn.argtypes = args
+    if missing and not ab:
+        raise NanodecError(f"{LIB_PATH} does not export {', '.join(missing)}: rebuild it (or set NANODEC_AB=1 "
+                           "for an A/B timing run on an older library)")
     _lib = L
     return L
 

@@ -104,13 +104,14 @@ struct GraphKey {
   int exact = 0;  // exact fp32 products (set by run_graph from the ctx)
   int bank_nt = 0;  // memory bank streamed non-temporally (set by run_graph from the ctx)
   int bank_grid = 0;  // the bank kernel's workgroup cap (set by run_graph from the ctx)
+  int splitk = 0;     // long-K step GEMMs split over workgroups (set by run_graph from the ctx)
   int tail = 0;   // --fast beam tail segments (nd_ctx.beam_tail)
   bool operator<(const GraphKey& o) const {
     return std::tie(mode, B, T, S, min_len, beam, n_best, seg, logp, alpha, stamp, attn, cov, stepwise, ngram, excl,
-                    beta, topk, temp, exact, tail, bank_nt, bank_grid) <
+                    beta, topk, temp, exact, tail, bank_nt, bank_grid, splitk) <
            std::tie(o.mode, o.B, o.T, o.S, o.min_len, o.beam, o.n_best, o.seg, o.logp, o.alpha, o.stamp, o.attn,
                     o.cov, o.stepwise, o.ngram, o.excl, o.beta, o.topk, o.temp, o.exact, o.tail, o.bank_nt,
-                    o.bank_grid);
+                    o.bank_grid, o.splitk);
   }
 };
 
@@ -120,6 +121,7 @@ struct nd_ctx {
   std::map<std::string, Slot> slots;
   std::vector<void*> allocs;
   bool finalized = false;
+  bool shares = false;  // reads another context's weights (nd_share_weights)
   bool use_graphs = true;
   int ctx_path = 0;  // 0: memory-bank form for greedy, K/V form for beam; 1: always K/V
   bool kstamp_on = false;                 // stamp every context-attention launch (bench roofline)
@@ -141,9 +143,17 @@ struct nd_ctx {
   bool bank_nt = false;
   // workgroups of the bank kernel at most (nd_set_bank_grid; 0 = one per chunk)
   int bank_grid = 0;
+  // the K = 2048 step GEMMs split over workgroups (gemm_p16k_kernel, nd_set_gemm_splitk).  Off by default:
+  // a lone call is faster on the one-workgroup-per-tile long-K kernel; EnginePool lanes (several calls in
+  // flight) turn it on ("Decoder GEMMs at 256 rows")
+  bool splitk = false;
 
   // weights
   float *enc_lin_w = nullptr, *enc_lin_b = nullptr, *enc_ln_g = nullptr, *enc_ln_b = nullptr;
+  // the memory bank's LayerNorm affine divided by its per-dimension power-of-two
+  // scales (derive_bank_dim_scales; transformer encoder), and the scales
+  float *bank_ln_g = nullptr, *bank_ln_b = nullptr;
+  std::vector<float> bank_dim_scale;
   // encoder layer 0's QKV in the rank-2 form (kernels.hpp EmbedQkv): a | c on
   // the device, the three means on the host (kernel arguments); set at finalize
   float* eq_ac = nullptr;
@@ -588,6 +598,7 @@ struct G {
   G& q24(uint8_t* img, size_t plane) { a.q24 = img; a.q24_plane = plane; return *this; }  // the 24-bit image, not C
   // long-K P16 products may split over workgroups (gemm_p16k_kernel) into the context's slab
   G& splitk(const nd_ctx* c) {
+    if (!c->splitk) return *this;
     a.sk_slab = c->sk_slab;
     a.sk_cnt = c->sk_cnt;
     a.sk_tiles = c->sk_tiles;
@@ -967,10 +978,10 @@ static hipError_t enqueue_memory(nd_ctx* c, int B, int T, int rpc, hipStream_t s
   }
   const bool tf = c->cfg.encoder_type == ND_ENC_TRANSFORMER;
   if (c->bank_d8)
-    return nd::launch_bank_pack_d8(c->x, tf ? c->enc_ln_g : nullptr, tf ? c->enc_ln_b : nullptr, c->mem_p, c->bank_ks,
+    return nd::launch_bank_pack_d8(c->x, tf ? c->bank_ln_g : nullptr, tf ? c->bank_ln_b : nullptr, c->mem_p, c->bank_ks,
                                    c->bank_em, c->span, B, T, c->ovf, s);
   if (!tf) return hipSuccess;  // the NanoEncoder's output is the bank as it stands
-  return nd::launch_memory_pack(c->x, c->enc_ln_g, c->enc_ln_b, c->mem_p, B, T, T, s);
+  return nd::launch_memory_pack(c->x, c->bank_ln_g, c->bank_ln_b, c->mem_p, B, T, T, s);
 }
 
 static hipError_t enqueue_greedy(nd_ctx* c, int B, int T, int S, int min_len, bool logp, hipStream_t s,
@@ -1062,6 +1073,7 @@ static int run_graph(nd_ctx* c, const GraphKey& key, F&& enqueue) {
   k.tail = c->beam_tail ? 1 : 0;
   k.bank_nt = c->bank_nt ? 1 : 0;
   k.bank_grid = c->bank_grid;
+  k.splitk = c->splitk ? 1 : 0;
   auto it = c->graphs.find(k);
   if (it == c->graphs.end()) {
     hipGraph_t g = nullptr;
@@ -1164,6 +1176,7 @@ int nd_create(const nd_config* cfg, nd_ctx** out) {
 
 int nd_load_weight(nd_ctx* c, const char* name, const float* host, const int64_t* shape, int ndim) {
   if (!c || !name || !host || (!shape && ndim > 0)) return fail(ND_ERR_ARG, "null argument");
+  if (c->shares) return fail(ND_ERR_STATE, "nd_load_weight: the context reads another context's weights");
   const std::string n(name);
   auto it = c->slots.find(n);
   if (it == c->slots.end()) {
@@ -1217,6 +1230,43 @@ static hipError_t pack_step_weight(nd_ctx* c, const float* src, int ld, float* d
   return hipSuccess;
 }
 
+// Per-dimension power-of-two scales of the memory bank (transformer encoder).
+// The bank holds m_i / c_i with m = LN(x) g + b (encoder/transformer.py:127):
+// a dimension whose LN affine makes it far larger than the rest (an "outlier
+// dimension", common in trained transformers) would otherwise set every row's
+// 24-bit scale (bank8.hip: one scale per key row) and cost the other
+// dimensions that many bits.  c_i = 2^k_i, k_i = clamp(floor(log2(a_i /
+// median a)), 0, 12), a_i = 3 |g_i| + |b_i| (a LayerNorm'd value lies mostly
+// within +-3); c_i is folded back exactly into W_qk's rows and W_vo's
+// columns (derive_memory_bank_weights), so scores and context vectors are
+// unchanged in exact arithmetic.  The NanoEncoder's bank keeps c = 1.
+static int derive_bank_dim_scales(nd_ctx* c) {
+  const int D = c->D;
+  c->bank_dim_scale.assign(D, 1.f);
+  if (c->cfg.encoder_type != ND_ENC_TRANSFORMER) return ND_OK;
+  std::vector<float> g(D), b(D);
+  HIPCHK(hipMemcpy(g.data(), c->enc_ln_g, D * 4, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(b.data(), c->enc_ln_b, D * 4, hipMemcpyDeviceToHost));
+  std::vector<double> a(D);
+  for (int i = 0; i < D; ++i) a[i] = 3.0 * std::fabs((double)g[i]) + std::fabs((double)b[i]);
+  std::vector<double> srt(a);
+  std::nth_element(srt.begin(), srt.begin() + D / 2, srt.end());
+  const double med = srt[D / 2];
+  for (int i = 0; i < D; ++i) {
+    int k = 0;
+    if (med > 0 && a[i] > 0 && std::isfinite(a[i])) k = (int)std::floor(std::log2(a[i] / med));
+    k = std::min(std::max(k, 0), 12);
+    c->bank_dim_scale[i] = std::ldexp(1.f, k);
+    g[i] = std::ldexp(g[i], -k);
+    b[i] = std::ldexp(b[i], -k);
+  }
+  if (!c->bank_ln_g && dalloc(c, &c->bank_ln_g, D) != hipSuccess) return fail(ND_ERR_HIP, "alloc");
+  if (!c->bank_ln_b && dalloc(c, &c->bank_ln_b, D) != hipSuccess) return fail(ND_ERR_HIP, "alloc");
+  HIPCHK(hipMemcpy(c->bank_ln_g, g.data(), D * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(c->bank_ln_b, b.data(), D * 4, hipMemcpyHostToDevice));
+  return ND_OK;
+}
+
 // Memory-bank form of the context attention (attention.hip): per decoder
 // layer, in f64 on the host from the reference weights,
 //   W_qk[h*256+i][k] = sum_a W_k[32h+a][i] W_q'[32h+a][k] / sqrt(32)
@@ -1225,6 +1275,8 @@ static hipError_t pack_step_weight(nd_ctx* c, const float* src, int ld, float* d
 //   b_vo[n]          = W_o[n] . b_v + b_o[n]
 // with W_q' = W_q diag(ln2_g), b_q' = W_q ln2_b + b_q (layer_norm_2 folded).
 // q_h . b_k,h is constant over keys and drops out of the softmax exactly.
+// Row h*256+i of W_qk / b_qk and column h*256+i of W_vo carry the bank's
+// per-dimension scale c_i (derive_bank_dim_scales; powers of two: exact).
 static int derive_memory_bank_weights(nd_ctx* c) {
   const int D = c->D, H = ND_H, DH = ND_DH, Ld = (int)c->dec.size();
   auto down = [&](const float* d, size_t n, std::vector<float>& h) {
@@ -1269,8 +1321,9 @@ static int derive_memory_bank_weights(nd_ctx* c) {
           for (int k = 0; k < D; ++k) row[k] += wk * wr[k];
           sb += wk * bq2[h * DH + a];
         }
-        for (int k = 0; k < D; ++k) wqk[((size_t)h * D + ii) * D + k] = (float)(row[k] * inv);
-        bqk[(size_t)h * D + ii] = (float)(sb * inv);
+        const double ci = c->bank_dim_scale[ii];
+        for (int k = 0; k < D; ++k) wqk[((size_t)h * D + ii) * D + k] = (float)(row[k] * inv * ci);
+        bqk[(size_t)h * D + ii] = (float)(sb * inv * ci);
       }
     for (int n = 0; n < D; ++n) {
       double sb = bo[n];
@@ -1283,7 +1336,7 @@ static int derive_memory_bank_weights(nd_ctx* c) {
           const float* vr = &Wv[(size_t)(h * DH + a) * D];
           for (int ii = 0; ii < D; ++ii) row[ii] += wo * vr[ii];
         }
-        for (int ii = 0; ii < D; ++ii) wvo[(size_t)n * H * D + h * D + ii] = (float)row[ii];
+        for (int ii = 0; ii < D; ++ii) wvo[(size_t)n * H * D + h * D + ii] = (float)(row[ii] * c->bank_dim_scale[ii]);
       }
     }
     if ((e = hipMemcpy(scratch, wqk.data(), wqk.size() * 4, hipMemcpyHostToDevice)) != hipSuccess ||
@@ -1432,7 +1485,8 @@ int nd_finalize(nd_ctx* c) {
     HIPCHK(hipStreamSynchronize(c->es));
   }
   {
-    int rc = derive_memory_bank_weights(c);
+    int rc = derive_bank_dim_scales(c);
+    if (!rc) rc = derive_memory_bank_weights(c);
     if (rc) return rc;
   }
   for (auto& kv : c->graphs) (void)hipGraphExecDestroy(kv.second);
@@ -1445,6 +1499,8 @@ int nd_share_weights(nd_ctx* c, const nd_ctx* src) {
   if (!c || !src) return fail(ND_ERR_ARG, "null ctx");
   if (!src->finalized) return fail(ND_ERR_STATE, "nd_share_weights: the source context is not finalized");
   if (c == src || c->finalized) return fail(ND_ERR_STATE, "nd_share_weights: the context already holds weights");
+  for (const auto& kv : c->slots)
+    if (kv.second.loaded) return fail(ND_ERR_STATE, "nd_share_weights: weights were loaded into the context");
   const nd_config &a = c->cfg, &b = src->cfg;
   if (a.encoder_type != b.encoder_type || a.self_attn_type != b.self_attn_type || a.enc_layers != b.enc_layers ||
       a.dec_layers != b.dec_layers || a.d_model != b.d_model || a.heads != b.heads || a.d_ff != b.d_ff ||
@@ -1452,7 +1508,9 @@ int nd_share_weights(nd_ctx* c, const nd_ctx* src) {
       a.pad_idx != b.pad_idx || a.bos_idx != b.bos_idx || a.eos_idx != b.eos_idx || a.device != b.device)
     return fail(ND_ERR_ARG, "nd_share_weights: the model configurations differ");
   // every weight pointer and every image nd_finalize derived (the layer structs hold both; nothing in them is
-  // a workspace); the context's own weight buffers from nd_create stay allocated and unread
+  // a workspace).  The context's own raw weight buffers from nd_create stay allocated and are never read (a
+  // few tens of MB at d_model 256): the derived images -- the split-fp16 and P16 forms, the memory-bank
+  // products -- are what sharing saves, and every lane reads one copy.
   c->enc = src->enc;
   c->nano = src->nano;
   c->nano_W = src->nano_W;
@@ -1461,6 +1519,9 @@ int nd_share_weights(nd_ctx* c, const nd_ctx* src) {
   c->enc_lin_b = src->enc_lin_b;
   c->enc_ln_g = src->enc_ln_g;
   c->enc_ln_b = src->enc_ln_b;
+  c->bank_ln_g = src->bank_ln_g;
+  c->bank_ln_b = src->bank_ln_b;
+  c->bank_dim_scale = src->bank_dim_scale;
   c->eq_ac = src->eq_ac;
   c->eq_scal = src->eq_scal;
   for (int i = 0; i < 3; ++i) c->eq_m[i] = src->eq_m[i];
@@ -1480,6 +1541,7 @@ int nd_share_weights(nd_ctx* c, const nd_ctx* src) {
   c->split_rm = src->split_rm;
   for (auto& kv : c->graphs) (void)hipGraphExecDestroy(kv.second);
   c->graphs.clear();
+  c->shares = true;
   c->finalized = true;
   return ND_OK;
 }
@@ -1865,6 +1927,12 @@ int nd_set_bank_grid(nd_ctx* c, int32_t workgroups) {
   if (!c) return fail(ND_ERR_ARG, "null ctx");
   if (workgroups < 0) return fail(ND_ERR_ARG, "bank grid: workgroups must be >= 0");
   c->bank_grid = workgroups;  // graphs are keyed by it
+  return ND_OK;
+}
+
+int nd_set_gemm_splitk(nd_ctx* c, int32_t on) {
+  if (!c) return fail(ND_ERR_ARG, "null ctx");
+  c->splitk = on != 0;  // graphs are keyed by it
   return ND_OK;
 }
 

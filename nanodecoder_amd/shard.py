@@ -4,8 +4,8 @@ Reads are independent, so the path shards with NO collective in the hot
 loop: one process per GPU (torch.distributed.run), reads assigned to ranks by
 a longest-processing-time balance on sample count, rank 0's weights sent once
 as one packed fp32 blob (``broadcast`` — RCCL over xGMI with backend "nccl"),
-and one final ``all_reduce`` of [samples, bases, chunks] (+ MAX of seconds)
-for reporting.  Each rank packs chunks of many reads into full engine
+and after the loop the failure flags and one ``all_reduce`` of [samples,
+bases, chunks] (+ MAX of seconds) for reporting, on a CPU gloo group.  Each rank packs chunks of many reads into full engine
 batches; every chunk keeps the span of its reference batch (consecutive
 ``batch_size`` chunks of its own read), so outputs equal the reference's
 per-read translate.
@@ -235,6 +235,13 @@ def _merge(a, b):
     return a
 
 
+def _device_sync(device):
+    """Wait for the rank's device work (a HIP call: never made on a rank whose
+    engine has failed, whose device error may be sticky)."""
+    if device.type == "cuda" and torch.cuda.is_available():
+        torch.cuda.synchronize(device)
+
+
 def run_distributed(n_reads: int, translator_factory: Callable, weights_factory: Callable, device,
                     batch_size: int = 100, seed: int = 0, keep_predictions: bool = False, pregenerate: bool = False,
                     warmup_reads: int = 0, frontend: str = "auto", retry: bool = True):
@@ -242,19 +249,31 @@ def run_distributed(n_reads: int, translator_factory: Callable, weights_factory:
     The timed region (max over ranks) covers the front end, packing, the
     engine and the token copies of the rank's reads.
 
+    Collectives: the weight blob goes out in ONE broadcast on the default
+    group (RCCL over xGMI with backend "nccl", from HIP memory), before the
+    timed region; the translate loop runs none.  Everything after the loop
+    -- the failure flags, the counters, the MAX of the seconds and the closing
+    barrier -- runs on a CPU gloo group (``ctl``) with host tensors: a few
+    numbers, and a rank whose device has faulted can still take part.  With
+    an initialised process group the collectives run at every world size,
+    one included (the RCCL path is exercised by a one-GPU run).
+
     Rank failure (reads are independent, so a failed shard is
     rerun): a rank whose translator raises keeps its process and its place in
-    the collectives.  After the first pass one all_reduce of per-rank failure
-    flags tells every rank which shards failed; their reads are re-assigned
-    by LPT to the ranks that did not fail and translated there (``retried``
-    in the stats).  Reads that still fail, or a job where every rank failed,
-    raise ``ShardFailure`` naming them on every rank (the launcher exits
-    non-zero).  A rank PROCESS that dies is the launcher's to report:
-    torch.distributed.run stops the other workers and exits non-zero; a
-    rerun of the CLI skips the reads already written (translate.py's
+    the (gloo) collectives and makes NO further device call -- an engine fault
+    is usually a sticky HIP error, after which any HIP call, an RCCL
+    collective included, raises or hangs.  One all_reduce of per-rank failure
+    flags tells every rank which shards failed; their reads are re-assigned by
+    LPT to the ranks that did not fail and translated there (``retried`` and
+    ``failed_ranks`` in the stats).  Reads that still fail, or a job where
+    every rank failed, raise ``ShardFailure`` naming them on every rank (the
+    launcher exits non-zero).  A rank PROCESS that dies is the launcher's to
+    report: torch.distributed.run stops the other workers and exits non-zero;
+    a rerun of the CLI skips the reads already written (translate.py's
     resume)."""
-    multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    multi = dist.is_available() and dist.is_initialized()
     rank, world = (dist.get_rank(), dist.get_world_size()) if multi else (0, 1)
+    ctl = dist.new_group(backend="gloo") if multi else None
     lengths = read_lengths(n_reads, seed)
     parts = lpt_assign(lengths.tolist(), world)
     mine = parts[rank]
@@ -267,38 +286,39 @@ def run_distributed(n_reads: int, translator_factory: Callable, weights_factory:
         raws = [synth_raw(int(i), int(lengths[i])) for i in mine]
     if warmup_reads:  # graphs captured and pinned buffers made outside the timed region
         ReadShard(tr, batch_size=batch_size, frontend=frontend).run(mine[:warmup_reads], lengths)
-    on_gpu = device.type == "cuda" and torch.cuda.is_available()
     if multi:
         dist.barrier()
-    if on_gpu:
-        torch.cuda.synchronize(device)
+    _device_sync(device)
     shard = ReadShard(tr, batch_size=batch_size, frontend=frontend)
     t0 = time.perf_counter()
-    failures = {}
+    device_ok = True
 
     def attempt(ids, raw_list):
+        nonlocal device_ok
         try:
             st, pr = shard.run(ids, lengths, keep_predictions, raws=raw_list)
-            if on_gpu:
-                torch.cuda.synchronize(device)
+            _device_sync(device)
             return st, pr, None
         except Exception as e:  # this rank's shard failed; the others take its reads
+            device_ok = False
             return _empty_stats(shard.frontend), {}, f"rank {rank}: {type(e).__name__}: {e}"
+
+    def exchange(flag):
+        flags = torch.zeros(world, dtype=torch.float64)
+        flags[rank] = flag
+        dist.all_reduce(flags, group=ctl)
+        return [r for r in range(world) if flags[r] > 0]
 
     stats, preds, err = attempt(mine, raws)
     retried = 0
-    if err is not None:
-        failures[rank] = err
+    failed = []
     if multi:
-        flags = torch.zeros(world, dtype=torch.float64, device=device)
-        flags[rank] = 1.0 if err is not None else 0.0
-        dist.all_reduce(flags)
-        failed = [r for r in range(world) if flags[r] > 0]
+        failed = exchange(1.0 if err is not None else 0.0)
         if failed:
             ok = [r for r in range(world) if r not in failed]
             todo = sorted(i for r in failed for i in parts[r])
             if not ok or not retry:
-                raise ShardFailure(todo, f"failed ranks {failed}")
+                raise ShardFailure(todo, f"failed ranks {failed}" + (f": {err}" if err else ""))
             share = lpt_assign([int(lengths[i]) for i in todo], len(ok))
             extra = [todo[j] for j in share[ok.index(rank)]] if rank in ok else []
             retried = len(todo)
@@ -308,10 +328,7 @@ def run_distributed(n_reads: int, translator_factory: Callable, weights_factory:
                 st2, pr2, err2 = attempt(extra, xraws)
                 stats = _merge(stats, st2)
                 preds.update(pr2)
-            flags.zero_()
-            flags[rank] = 1.0 if err2 is not None else 0.0
-            dist.all_reduce(flags)
-            failed2 = [r for r in range(world) if flags[r] > 0]
+            failed2 = exchange(1.0 if err2 is not None else 0.0)
             if failed2:
                 lost = sorted(i for r in failed2 for i in
                               ([todo[j] for j in share[ok.index(r)]] if r in ok else []))
@@ -319,20 +336,20 @@ def run_distributed(n_reads: int, translator_factory: Callable, weights_factory:
     elif err is not None:
         raise ShardFailure(mine, err)
     stats["seconds"] = time.perf_counter() - t0
-    if multi:
-        dist.barrier()
-    red = torch.tensor([stats["samples"], stats["bases"], stats["chunks"]], dtype=torch.float64, device=device)
-    secs = torch.tensor([stats["seconds"]], dtype=torch.float64, device=device)
-    per_rank = torch.zeros(world, dtype=torch.float64, device=device)
+    red = torch.tensor([stats["samples"], stats["bases"], stats["chunks"]], dtype=torch.float64)
+    secs = torch.tensor([stats["seconds"]], dtype=torch.float64)
+    per_rank = torch.zeros(world, dtype=torch.float64)
     per_rank[rank] = stats["samples"]
     if multi:
-        dist.all_reduce(red)
-        dist.all_reduce(per_rank)
-        dist.all_reduce(secs, op=dist.ReduceOp.MAX)
-    loads = per_rank.cpu().numpy()
+        dist.barrier(group=ctl)
+        dist.all_reduce(red, group=ctl)
+        dist.all_reduce(per_rank, group=ctl)
+        dist.all_reduce(secs, op=dist.ReduceOp.MAX, group=ctl)
+    loads = per_rank.numpy()
     g = dict(samples=int(red[0]), bases=int(red[1]), chunks=int(red[2]), seconds=float(secs[0]), world=world,
              reads=int(n_reads), samples_per_rank=[int(x) for x in loads], frontend=shard.frontend,
-             load_imbalance=float(loads.max() / max(loads.mean(), 1.0)), retried=retried)
+             load_imbalance=float(loads.max() / max(loads.mean(), 1.0)), retried=retried, failed_ranks=failed,
+             device_ok=device_ok)
     return g, preds
 
 

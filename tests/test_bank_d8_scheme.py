@@ -120,3 +120,32 @@ def test_context_product_scale():
     U = (hi.astype(np.float64) + lo.astype(np.float64)) @ Mp * (2.0 * smax)
     exact = p @ m.astype(np.float64)
     assert np.abs(U - exact).max() <= 2.0 ** -21 * np.abs(m).max() * p.sum()
+
+
+def bank_dim_scales(g, b):
+    """engine.hip derive_bank_dim_scales: per-dimension powers of two c_i =
+    2^clamp(floor(log2(a_i / median a)), 0, 12), a_i = 3 |g_i| + |b_i|, of the
+    encoder's final LayerNorm affine; the bank holds m_i / c_i."""
+    a = 3.0 * np.abs(np.asarray(g, np.float64)) + np.abs(np.asarray(b, np.float64))
+    med = np.partition(a, a.size // 2)[a.size // 2]
+    with np.errstate(divide="ignore"):
+        k = np.where((a > 0) & (med > 0), np.floor(np.log2(np.where(a > 0, a, 1.0) / med)), 0.0)
+    return np.ldexp(np.float32(1), np.clip(k, 0, 12).astype(np.int32)).astype(np.float32)
+
+
+def test_bank_dim_scales_remove_an_outlier_dimension():
+    """An LN gain 10^3 x the rest: its dimension is divided by 2^9 (2^10 > the
+    ratio of 10^3 x 1.5 / median), every other stays 1; the rows of m / c then
+    lose at most ~2 bits to it instead of ~10 (the 24-bit per-row scale, above)."""
+    rng = np.random.default_rng(4)
+    g = (rng.random(256) + 0.5).astype(np.float32)
+    b = (rng.standard_normal(256) * 0.1).astype(np.float32)
+    assert (bank_dim_scales(g, b) == 1).all()
+    g[77] *= 1e3
+    b[77] *= 1e3
+    c = bank_dim_scales(g, b)
+    assert c[77] in (512.0, 1024.0) and (np.delete(c, 77) == 1).all()
+    n = rng.standard_normal((512, 256))
+    m = (n * g + b) / c
+    ratio = np.abs(m).max(1) / np.abs(np.delete(m, 77, axis=1)).max(1)
+    assert ratio.max() < 4.0

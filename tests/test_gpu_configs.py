@@ -59,12 +59,14 @@ def _tie_rows(got, exp_tokens, exp_logp):
     return rows
 
 
-@pytest.mark.parametrize("encoder", ["transformer", "nano"])
-def test_greedy_config_batch256_vs_oracle(encoder):
+@pytest.mark.parametrize("encoder,splitk", [("transformer", True), ("transformer", False), ("nano", True)])
+def test_greedy_config_batch256_vs_oracle(encoder, splitk):
     """configs[1] (3+3 transformer) and configs[2] (NanoEncoder + transformer
     decoder): 256 chunks x 512 samples, greedy, max_length 100, -min_length 57
     (the bench's workload, mask samples injected), every chunk against the
-    oracle.  Asserts the M = 256 GEMM kernels ran (gemm_p16s, long-K P16)."""
+    oracle.  Asserts the M = 256 GEMM kernels ran (gemm_p16s, and the K = 2048
+    products split over workgroups as EnginePool lanes run them, or on the
+    long-K P16 kernel as a lone engine does: nd_set_gemm_splitk)."""
     ref = _oracle()
     cfg = synth.ModelConfig(encoder_type=encoder)
     W = synth.make_weights(cfg, seed=11, eos_bias=-3.0)
@@ -72,14 +74,18 @@ def test_greedy_config_batch256_vs_oracle(encoder):
     sig = synth.synth_chunk_batch(B, 512, seed=1000)
     lens = np.full(B, 512, np.int32)
     eng = _engine(cfg, W, max_batch=B, max_steps=S)
+    eng.set_gemm_splitk(splitk)
     _routes()
     r = eng.translate_greedy(sig, lens, lens, max_len=S, min_len=MINL)  # the bench's graph (no log-prob dump)
     routes = _routes()
     # 256 rows: the N = 2048 products (query projection, FFN1) on gemm_p16s<2,4>, the QKV products on
-    # gemm_p16s<2,2>, the K = 2048 products (W_vo, FFN2) split over K (gemm_p16k_kernel; Wo, N = K = 256,
-    # stays on gemm_p16<1,4,64>)
-    assert routes["p16s_2x4"] > 0 and routes["p16s_2x2"] > 0 and routes["p16_splitk"] > 0, routes
-    assert routes["p16_longk"] == 0, routes
+    # gemm_p16s<2,2>, the K = 2048 products (W_vo, FFN2) split over K (gemm_p16k_kernel) or on the long-K P16
+    # kernel (Wo, N = K = 256, stays on gemm_p16<1,4,64>)
+    assert routes["p16s_2x4"] > 0 and routes["p16s_2x2"] > 0, routes
+    if splitk:
+        assert routes["p16_splitk"] > 0 and routes["p16_longk"] == 0, routes
+    else:
+        assert routes["p16_splitk"] == 0 and routes["p16_longk"] > 0, routes
     rl = eng.translate_greedy(sig, lens, lens, max_len=S, min_len=MINL, return_logp=True)
     tok = r["tokens"].cpu().numpy()
     assert (tok == rl["tokens"].cpu().numpy()).all()
@@ -96,32 +102,37 @@ def test_greedy_config_batch256_vs_oracle(encoder):
 
 def test_beam_config3_batch1024_sampled_vs_oracle():
     """configs[3]: --fast beam 5 on 1024 chunks, max_length 100, -min_length
-    57 (the bench's workload).  Most chunks finish at step ~58; the few that
-    run on are decoded by the tail segments (GraphKey.tail: <= 1/16 of the
-    chunks alive, small-M GEMM kernels).  16 chunks are compared with the
-    oracle: every chunk that ran into the tail plus random others."""
+    57, mask samples injected (src==0 encoder keys, src==1 context keys: the
+    24-bit context K/V image and the tail's list-split kernels meet masked
+    keys at size).  Most chunks finish at step ~58; the few that run on are
+    decoded by the tail segments (GraphKey.tail: <= 1/16 of the chunks alive,
+    small-M GEMM kernels).  64 chunks are compared with the oracle: every
+    chunk that ran into the tail (up to 32) plus random others."""
     ref = _oracle()
     cfg = synth.ModelConfig()
     W = synth.make_weights(cfg, seed=11, eos_bias=-3.0)
-    B, S, MINL = 1024, 100, 57
-    sig = synth.synth_chunk_batch(B, 512, seed=2000, inject_masks=False)
+    B, S, MINL, NPICK = 1024, 100, 57, 64
+    sig = synth.synth_chunk_batch(B, 512, seed=2000, inject_masks=True)
     lens = np.full(B, 512, np.int32)
     eng = _engine(cfg, W, max_batch=B, max_steps=S, max_beam=5)
     _routes()
     r = eng.translate_beam(sig, lens, lens, beam=5, n_best=1, max_len=S, min_len=MINL)  # the bench's graphs
     routes = _routes()
+    assert eng.bank_form() == 3
     ra = eng.translate_beam(sig, lens, lens, beam=5, n_best=1, max_len=S, min_len=MINL, return_attn=True)
     tok, sc, ln = (r[k].cpu().numpy() for k in ("tokens", "scores", "lens"))
     assert (tok == ra["tokens"].cpu().numpy()).all() and (ln == ra["lens"].cpu().numpy()).all()
+    assert int(r["overflow"].cpu()[0]) == 0
     done = ra["done_step"].cpu().numpy()
     steps = int(r["steps"].cpu()[0])
     # the segment polls see at most B / 16 chunks alive from some step on: the tail ran
     alive_at = [int((done > s0).sum()) for s0 in range(10, steps, 10)]
     assert any(16 * a <= B for a in alive_at), alive_at
     assert routes["p16_big"] > 0 and routes["p16_longk"] > 0, routes  # large-M route and the tail's small-M kernels
-    tail = [int(i) for i in np.nonzero(done > 60)[0]][:8]
+    tail = [int(i) for i in np.nonzero(done > 60)[0]][: NPICK // 2]
+    assert tail, "no chunk ran into the tail"
     rng = np.random.default_rng(5)
-    rest = [int(i) for i in rng.choice(np.setdiff1d(np.arange(B), tail), 16 - len(tail), replace=False)]
+    rest = [int(i) for i in rng.choice(np.setdiff1d(np.arange(B), tail), NPICK - len(tail), replace=False)]
     pick = sorted(tail + rest)
     exp = ref.fast_beam(ref.RefModel(cfg, W), sig[pick], lens[pick], beam_size=5, n_best=1, max_length=S,
                         min_length=MINL)
@@ -155,6 +166,7 @@ def test_pool_matches_single_engine(encoder, mode):
             return e.translate_greedy(b, lens, lens, max_len=S, min_len=5, return_logp=True)
         return e.translate_beam(b, lens, lens, beam=beam, n_best=2, max_len=S, min_len=3)
     one = _engine(cfg, W, max_batch=B, max_steps=S, max_beam=beam)
+    one.set_gemm_splitk(True)  # the pool lanes' form
     exp = [{k: v.cpu() for k, v in call(one, b).items() if k in keys} for b in batches]
     one.close()
     # bank_grid 16: each lane's memory-bank workgroups walk 4 of the 64 chunks (nd_set_bank_grid)
@@ -240,9 +252,11 @@ def test_pool_at_bench_config_matches_single_engine(key):
             return e.translate_greedy(sig, ln, sp, max_len=S, min_len=MINL)
         return e.translate_beam(sig, ln, sp, beam=beam, n_best=1, max_len=S, min_len=MINL)
     one = _engine(cfg, W, max_batch=B, max_steps=S, max_beam=beam)
+    one.set_gemm_splitk(True)  # the pool lanes' K = 2048 product form (its own test: the config tests above)
     exp = [{k: v.cpu() for k, v in call(one, i).items() if k in keys} for i in inputs]
     one.close()
     pool = EnginePool(cfg, W, device=0, lanes=lanes, max_batch=B, max_steps=S, max_beam=beam)
+    assert pool.splitk
     assert pool.bank_nt_lanes == (0, 1, 2)
     assert pool.bank_grid == torch.cuda.get_device_properties(0).multi_processor_count // 2
     dev_in = [tuple(torch.from_numpy(a).cuda() for a in i) for i in inputs]
@@ -430,3 +444,33 @@ def test_beam1_segments_captured_after_exact_call():
     assert int(f["steps"].cpu()[0]) > 10
     for k in ("tokens", "scores", "lens"):
         assert (c[k].cpu().numpy() == f[k].cpu().numpy()).all(), k
+
+
+def test_shared_weights_outlive_an_early_close():
+    """closing the engine whose weights other lanes read (lane 0,
+    or a pool made by subset) must not free them under the readers: the
+    source refuses calls from then on and is freed with its last reader;
+    the reader's results are unchanged.  A weight load into a sharing context
+    is refused (nd_share_weights' contract)."""
+    import ctypes
+    from nanodecoder_amd import _lib
+    from nanodecoder_amd.engine import Engine
+    cfg = synth.ModelConfig()
+    W = synth.make_weights(cfg, seed=11, eos_bias=-3.0)
+    sig = synth.synth_chunk_batch(8, 512, seed=3)
+    lens = np.full(8, 512, np.int32)
+    src = Engine(cfg, W, device=0, max_batch=8, max_steps=30)
+    want = src.translate_greedy(sig, lens, lens, max_len=30)["tokens"].cpu()
+    lane = Engine(cfg, W, device=0, max_batch=8, max_steps=30, share_from=src)
+    a = np.zeros(4, np.float32)
+    shape = (ctypes.c_int64 * 1)(4)
+    rc = lane._L.nd_load_weight(lane._h, b"encoder.layer_norm.bias", a.ctypes.data_as(ctypes.c_void_p), shape, 1)
+    assert rc == _lib.ND_ERR_STATE
+    src.close()
+    assert src._h is not None and src._close_pending          # still alive: lane reads its weights
+    with pytest.raises(_lib.NanodecError):
+        src.translate_greedy(sig, lens, lens, max_len=30)
+    got = lane.translate_greedy(sig, lens, lens, max_len=30)["tokens"].cpu()
+    assert (got == want).all()
+    lane.close()
+    assert lane._h is None and src._h is None                  # the source went with its last reader

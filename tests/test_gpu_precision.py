@@ -1,0 +1,339 @@
+"""Precision modes and storage forms against the oracle at the sizes the bench
+reports (needs an MI355X).
+
+1. Exact fp32 (``set_exact_fp32``: every product on fp32 MFMAs, fp32 K/V and
+   memory bank; the reference's precision, the bench line's ``exact_fp32``
+   leg) at configs[1] (B = 256) and configs[3] (B = 1024, --fast beam 5),
+   against oracle/ref_cpu.py (the reference's algorithm in torch fp32, pinned
+   to its own outputs by tests/golden).  The product also takes this mode for
+   every call that trips the split-fp16 range guard.
+2. The three 24-bit storage forms on rows with one outlier
+   dimension 10^3 x the rest, op by op against fp64, and end to end on a
+   function-preserving transform of the weights (tests/outlier_util.py)
+   against the oracle.
+
+Bars: log-probs within 1e-3 (fp32 outputs, BASELINE.json north_star),
+identical tokens except after a genuine oracle near-tie (top-2 margin < 1e-4),
+as tests/test_gpu_configs.py.  Reference: translate/translator.py:396-503
+(greedy), :619-825 (--fast beam); decoder/transformer.py:220-221 (the src==1
+context mask the injected samples exercise).
+"""
+import numpy as np
+import pytest
+import torch
+
+from nanodecoder_amd import synth
+from tests import golden_util as gu
+from tests.outlier_util import outlier_weights
+from tests.test_gpu_configs import LOGP_ATOL, _engine, _oracle, _routes, _tie_rows
+
+pytestmark = pytest.mark.gpu
+
+OUTLIER = 1e3
+
+
+def _greedy_vs_oracle(cfg, W, sig, lens, S, MINL, exact, max_ties=3):
+    ref = _oracle()
+    B = sig.shape[0]
+    eng = _engine(cfg, W, max_batch=B, max_steps=S)
+    eng.set_exact_fp32(exact)
+    _routes()
+    r = eng.translate_greedy(sig, lens, lens, max_len=S, min_len=MINL, return_logp=True)
+    routes = _routes()
+    form = eng.bank_form()
+    tok = r["tokens"].cpu().numpy()
+    lp = r["logp"].cpu().numpy()
+    sc = r["scores"].cpu().numpy()
+    assert int(r["overflow"].cpu()[0]) == 0  # the path under test ran (no range-guard rerun)
+    eng.close()
+    o = ref.greedy(ref.RefModel(cfg, W), sig, lens, max_length=S, min_length=MINL)
+    ties = _tie_rows(tok, o["tokens"], o["logp"])
+    assert len(ties) <= max_ties, ties
+    keep = np.array([b not in ties for b in range(B)])
+    normal = np.abs(o["logp"][keep]) < 1e3  # the -1e4-biased specials: their fp32 ulp is ~1e-3 (logp_close's rtol)
+    err = float(np.abs(lp[keep] - o["logp"][keep])[normal].max())
+    print(f"\n[precision] greedy B={B} exact={exact}: logp max|diff| {err:.3e}, tie rows {len(ties)}")
+    assert gu.logp_close(lp[keep], o["logp"][keep], atol=LOGP_ATOL).all(), err
+    assert np.abs(sc[keep] - o["scores"][keep]).max() < LOGP_ATOL
+    return routes, form
+
+
+def _beam_sampled_vs_oracle(cfg, W, sig, lens, S, MINL, exact, pick_n, beam=5):
+    """--fast beam on all chunks; pick_n of them against the oracle: every chunk that ran past step 60 (the
+    tail segments, <= B / 16 alive), the rest at random."""
+    ref = _oracle()
+    B = sig.shape[0]
+    eng = _engine(cfg, W, max_batch=B, max_steps=S, max_beam=beam)
+    eng.set_exact_fp32(exact)
+    r = eng.translate_beam(sig, lens, lens, beam=beam, n_best=1, max_len=S, min_len=MINL, return_attn=True)
+    form = eng.bank_form()
+    tok, sc, ln = (r[k].cpu().numpy() for k in ("tokens", "scores", "lens"))
+    done = r["done_step"].cpu().numpy()
+    assert int(r["overflow"].cpu()[0]) == 0
+    eng.close()
+    tail = [int(i) for i in np.nonzero(done > 60)[0]]
+    rng = np.random.default_rng(5)
+    tail = tail[: pick_n // 2]
+    rest = [int(i) for i in rng.choice(np.setdiff1d(np.arange(B), tail), pick_n - len(tail), replace=False)]
+    pick = sorted(tail + rest)
+    exp = ref.fast_beam(ref.RefModel(cfg, W), sig[pick], lens[pick], beam_size=beam, n_best=1, max_length=S,
+                        min_length=MINL)
+    worst = 0.0
+    for j, i in enumerate(pick):
+        s, p = exp[j][0]
+        assert ln[i, 0] == len(p), (i, ln[i, 0], len(p))
+        assert (tok[i, 0, : len(p)] == p).all(), i
+        worst = max(worst, abs(sc[i, 0] - s))
+        assert abs(sc[i, 0] - s) < LOGP_ATOL, (i, sc[i, 0], s)
+    print(f"\n[precision] beam B={B} exact={exact}: {len(pick)} chunks ({len(tail)} from the tail), "
+          f"score max|diff| {worst:.3e}")
+    return form, len(tail)
+
+
+# ------------------------------------------------------------ 1. exact fp32
+@pytest.mark.parametrize("encoder", ["transformer", "nano"])
+def test_exact_fp32_config1_batch256_vs_oracle(encoder):
+    """configs[1] / configs[2] in exact fp32: 256 chunks x 512 samples, greedy,
+    max_length 100, -min_length 57, mask samples injected (src==0 keys,
+    src==1 context keys), every chunk against the oracle.  The fp32-MFMA
+    tile kernels ran and no split-fp16 product; the fp32 memory bank."""
+    cfg = synth.ModelConfig(encoder_type=encoder)
+    W = synth.make_weights(cfg, seed=11, eos_bias=-3.0)
+    B = 256
+    sig = synth.synth_chunk_batch(B, 512, seed=1000, inject_masks=True)
+    routes, form = _greedy_vs_oracle(cfg, W, sig, np.full(B, 512, np.int32), 100, 57, exact=True)
+    assert form == 0
+    assert routes["tile256"] + routes["tile128"] + routes["tile64"] > 0, routes
+    assert sum(v for k, v in routes.items() if k.startswith("p16")) == 0, routes
+
+
+def test_exact_fp32_config3_batch1024_sampled_vs_oracle():
+    """configs[3] in exact fp32: --fast beam 5 on 1024 chunks (fp32 context
+    K/V, fp32 self history), max_length 100, -min_length 57, masks injected;
+    32 chunks against the oracle (the tail's chunks among them)."""
+    cfg = synth.ModelConfig()
+    W = synth.make_weights(cfg, seed=11, eos_bias=-3.0)
+    B = 1024
+    sig = synth.synth_chunk_batch(B, 512, seed=2000, inject_masks=True)
+    form, _ = _beam_sampled_vs_oracle(cfg, W, sig, np.full(B, 512, np.int32), 100, 57, exact=True, pick_n=32)
+    assert form == 0
+
+
+# ------------------------------------------- 2. 24-bit forms on outlier rows
+def _attend64(q, K, V, mask=None):
+    s = K @ q
+    if mask is not None:
+        s[mask] = -1e18
+    p = np.exp(s - s.max())
+    return (p / p.sum()) @ V
+
+
+def _attend32(q, K, V, mask=None):
+    """The reference's fp32 arithmetic (torch CPU fp32 in the oracle) on the same inputs."""
+    q, K, V = (np.asarray(a, np.float32) for a in (q, K, V))
+    s = K @ q
+    if mask is not None:
+        s[mask] = np.float32(-1e18)
+    p = np.exp(s - s.max())
+    return (p / p.sum()).astype(np.float32) @ V
+
+
+def test_bank_d8_outlier_dimension_vs_fp64():
+    """The greedy 24-bit digit bank (one scale per key row) on chunks whose
+    rows carry one dimension 10^3 x the rest, as an encoder LayerNorm with one
+    large gain produces, q' reading that dimension 10^-3 as strongly (the
+    function-preserving case, tests/outlier_util.py).
+
+    (a) The engine's form: the bank holds each dimension divided by a power
+    of two taken from the LN affine (engine.hip derive_bank_dim_scales,
+    restated in tests/test_bank_d8_scheme.py::bank_dim_scales), folded back
+    into q' and the output: the outlier costs no bits, so every dimension
+    meets the plain rows' bar, 2e-5 of its magnitude.
+    (b) Rows whose outlier no per-dimension scale removes (the pack without
+    the LN, half of chunk 2's rows without it): the scheme's own bound,
+    2^-23.4 max|row| per element (test_bank_d8_scheme.py), so the small
+    dimensions' values carry 2^-23.4 x 10^3 x 3 ~ 3e-4 and the scores of
+    their products with q' ~ sqrt(256) x 0.3 x that: held within 2^-10 of
+    their magnitude (~1), the outlier dimension within 2e-5 of its own."""
+    from nanodecoder_amd.engine import op_bank_pack_d8, op_dec_bank_d8, unpack_p16
+    from tests.test_bank_d8_scheme import bank_dim_scales
+    rng = np.random.default_rng(71)
+    C, T, PAD, d0 = 6, 512, 1.0, 77
+    spans = np.array([T, 300, T, 65, T, T], np.int32)
+    sig = rng.standard_normal((C, T)).astype(np.float32)
+    sig[1, ::5] = PAD
+    x = (rng.standard_normal((C * T, 256)) * 3.0 + 0.5).astype(np.float32)   # pre-LN rows
+    mu = x.mean(1, keepdims=True, dtype=np.float64)
+    n = (x - mu) / np.sqrt(((x - mu) ** 2).mean(1, keepdims=True) + 1e-6)  # LayerNorm'd (fp64)
+    g = (rng.random(256) + 0.5).astype(np.float32)
+    b = (rng.standard_normal(256) * 0.1).astype(np.float32)
+    g[d0] *= np.float32(OUTLIER)
+    b[d0] *= np.float32(OUTLIER)
+    q = (rng.standard_normal((C, 2048)) * 0.3).astype(np.float32)
+    q[:, d0::256] /= np.float32(OUTLIER)
+    dev = torch.device("cuda", 0)
+    ovf = torch.zeros(1, dtype=torch.int32, device=dev)
+    span_d = torch.from_numpy(spans).to(dev)
+    sig_d = torch.from_numpy(sig).to(dev)
+    xm = n * g + b                                                        # the memory bank, fp64
+    # (a) the engine's per-dimension scales
+    cs = bank_dim_scales(g, b)
+    assert cs[d0] >= 256 and (np.delete(cs, d0) == 1).all(), cs[d0]
+    bank = op_bank_pack_d8(torch.from_numpy(x).to(dev), C, T, torch.from_numpy(g / cs).to(dev),
+                           torch.from_numpy(b / cs).to(dev), ovf=ovf, span=span_d)
+    qs = (q.reshape(C, 8, 256) * cs).reshape(C, 2048).astype(np.float32)
+    out = op_dec_bank_d8(torch.from_numpy(qs).to(dev), bank, sig_d, span_d, PAD, ovf=ovf)
+    got_eq = (unpack_p16(out, C).cpu().numpy().reshape(C, 8, 256) * cs).reshape(C, 2048)
+    # (b) raw rows, the outlier in the data (no LN in the pack)
+    xr = xm.astype(np.float32)
+    xr[2 * T: 3 * T: 2, d0] /= np.float32(OUTLIER)
+    bank2 = op_bank_pack_d8(torch.from_numpy(xr).to(dev), C, T, ovf=ovf, span=span_d)
+    out2 = op_dec_bank_d8(torch.from_numpy(q).to(dev), bank2, sig_d, span_d, PAD, ovf=ovf)
+    got_raw = unpack_p16(out2, C).cpu().numpy()
+    assert int(ovf.item()) == 0
+    small = np.arange(256) != d0
+    rep = []
+    for got, M64 in ((got_eq, xm), (got_raw, xr.astype(np.float64))):
+        w_small, w_out, w32 = 0.0, 0.0, 0.0
+        for c in range(C):
+            L = int(spans[c])
+            M = M64[c * T: c * T + L]
+            mask = sig[c, :L] == PAD
+            for h in range(8):
+                qh = q[c, h * 256:(h + 1) * 256].astype(np.float64)
+                want = _attend64(qh, M, M, mask)
+                e = np.abs(got[c, h * 256:(h + 1) * 256] - want)
+                w_small = max(w_small, e[small].max())
+                w_out = max(w_out, e[d0] / np.abs(M[:, d0]).max())
+                w32 = max(w32, np.abs(_attend32(qh, M, M, mask) - want)[small].max())
+        rep.append((w_small, w_out, w32))
+    print(f"\n[precision] bank outlier: per-dimension scales: small-dim err {rep[0][0]:.2e} (fp32 {rep[0][2]:.2e}), "
+          f"outlier rel {rep[0][1]:.2e}; raw rows: small-dim err {rep[1][0]:.2e} (fp32 {rep[1][2]:.2e}), "
+          f"outlier rel {rep[1][1]:.2e}")
+    assert rep[0][0] < 2e-5 and rep[0][1] < 2e-5, rep[0]
+    assert rep[1][0] < 2.0 ** -10 and rep[1][1] < 2e-5, rep[1]
+
+
+@pytest.mark.parametrize("layer", [0, 2])
+def test_ctx_q24_outlier_dimension_vs_fp64(layer):
+    """The beam's 24-bit context K/V (one power-of-two scale per (key, head))
+    with key dimension 45 and value dimension 45 (head 1) 10^3 x the rest, q
+    reading the key dimension 10^-3 as strongly.  Bound: an element carries
+    2^-24 of a power of two above its head's largest value, so head 1's other
+    dimensions keep 2^-24 x 2^11 of the outlier's 10^3 / their ~1: within
+    2^-12 absolute; the outlier dimension within 2e-5 of its magnitude; every
+    other head at the plain 2e-5 bar."""
+    from nanodecoder_amd.engine import op_ctx_pack_q24, op_dec_ctx_attention_q24, pack_p16, unpack_p16
+    rng = np.random.default_rng(83 + layer)
+    C, T, Ld, PAD, rpc, j = 5, 512, 3, 1.0, 5, 45
+    spans = np.array([T, 300, 17, T, T], np.int32)
+    sig = rng.standard_normal((C, T)).astype(np.float32)
+    sig[3, ::4] = PAD
+    kv = rng.standard_normal((C * T, Ld * 512)).astype(np.float32)
+    kv[:, layer * 512 + j] *= np.float32(OUTLIER)
+    kv[:, layer * 512 + 256 + j] *= np.float32(OUTLIER)
+    q = rng.standard_normal((C * rpc, 256)).astype(np.float32)
+    q[:, j] /= np.float32(OUTLIER)
+    dev = torch.device("cuda", 0)
+    sp = torch.from_numpy(spans).to(dev)
+    img = op_ctx_pack_q24(torch.from_numpy(kv).to(dev), Ld * 512, Ld, sp, C, T)
+    out = op_dec_ctx_attention_q24(pack_p16(torch.from_numpy(q).to(dev)), img, layer,
+                                   torch.from_numpy(sig).to(dev), sp, PAD, rpc)
+    torch.cuda.synchronize()
+    got = unpack_p16(out, C * rpc).cpu().numpy()
+    K = kv[:, layer * 512: layer * 512 + 256].astype(np.float64)
+    V = kv[:, layer * 512 + 256: (layer + 1) * 512].astype(np.float64)
+    w = {"head1_small": 0.0, "outlier_rel": 0.0, "other": 0.0, "fp32_head1_small": 0.0}
+    for c in range(C):
+        L = int(spans[c])
+        mask = sig[c, :L] == PAD
+        for r in range(c * rpc, (c + 1) * rpc):
+            for h in range(8):
+                hs = slice(h * 32, (h + 1) * 32)
+                Kh, Vh = K[c * T: c * T + L, hs], V[c * T: c * T + L, hs]
+                qh = q[r, hs].astype(np.float64) / np.sqrt(32)
+                want = _attend64(qh, Kh, Vh, mask)
+                e = np.abs(got[r, hs] - want)
+                if h == 1:
+                    sm = np.arange(32) != j - 32
+                    w["head1_small"] = max(w["head1_small"], e[sm].max())
+                    w["outlier_rel"] = max(w["outlier_rel"], e[j - 32] / np.abs(Vh[:, j - 32]).max())
+                    w["fp32_head1_small"] = max(w["fp32_head1_small"],
+                                                np.abs(_attend32(qh, Kh, Vh, mask) - want)[sm].max())
+                else:
+                    w["other"] = max(w["other"], e.max() / max(1.0, np.abs(Vh).max()))
+    print(f"\n[precision] ctx q24 outlier layer {layer}: " + ", ".join(f"{k} {v:.2e}" for k, v in w.items()))
+    assert w["head1_small"] < 2.0 ** -12, w
+    assert w["outlier_rel"] < 2e-5 and w["other"] < 2e-5, w
+
+
+def test_self_q24_history_outlier_dimension_vs_fp64():
+    """The beam rows' 24-bit self-attention history (one power-of-two scale
+    per (key, head), appended every step) with key and value dimension 45
+    10^3 x the rest on every step, q reading the key dimension 10^-3 as
+    strongly; 40 steps through a fixed ancestry.  Same bound as the context
+    image: head 1's other dimensions within 2^-12, the outlier dimension 2e-5
+    of its magnitude, the other heads 2e-5."""
+    from nanodecoder_amd.engine import op_dec_self_attention_q24
+    C, S, steps, rpc, j = 7, 64, 40, 5, 45
+    R = C * rpc
+    g = torch.Generator().manual_seed(91)
+    qkv = [torch.randn(R, 768, generator=g) for _ in range(steps)]
+    for x in qkv:
+        x[:, 256 + j] *= OUTLIER
+        x[:, 512 + j] *= OUTLIER
+        x[:, j] /= OUTLIER
+    anc = torch.empty(R, S, dtype=torch.int32)
+    for c in range(C):
+        for k in range(rpc):
+            r = c * rpc + k
+            anc[r, :10] = c * rpc
+            anc[r, 10:] = torch.randint(0, rpc, (S - 10,), generator=g, dtype=torch.int32) + c * rpc
+    dev = torch.device("cuda", 0)
+    cache = torch.zeros(R, S, 1600, dtype=torch.uint8, device=dev)
+    ad = anc.to(dev)
+    w = {"head1_small": 0.0, "outlier_rel": 0.0, "other": 0.0}
+    for step in range(steps):
+        out = op_dec_self_attention_q24(qkv[step].to(dev), cache, step, anc=ad, rpc=rpc).cpu().double()
+        if step not in (0, 1, 9, 10, 17, 33, 39):
+            continue
+        q = qkv[step][:, :256].double().view(R, 8, 32) / np.float32(np.sqrt(32.0))
+        for r in range(R):
+            src = [int(anc[r, t]) for t in range(step)] + [r]
+            kv = torch.stack([qkv[t][src[t], 256:].double() for t in range(step + 1)])
+            k, v = kv[:, :256].view(-1, 8, 32), kv[:, 256:].view(-1, 8, 32)
+            p = torch.softmax(torch.einsum("hd,thd->ht", q[r], k), dim=-1)
+            ref = torch.einsum("ht,thd->hd", p, v)
+            e = (out[r].view(8, 32) - ref).abs()
+            sm = torch.arange(32) != j - 32
+            w["head1_small"] = max(w["head1_small"], e[1, sm].max().item())
+            w["outlier_rel"] = max(w["outlier_rel"], e[1, j - 32].item() / v[:, 1, j - 32].abs().max().item())
+            w["other"] = max(w["other"], e[torch.arange(8) != 1].max().item() / max(1.0, v.abs().max().item()))
+    print("\n[precision] self q24 outlier: " + ", ".join(f"{k} {v:.2e}" for k, v in w.items()))
+    assert w["head1_small"] < 2.0 ** -12, w
+    assert w["outlier_rel"] < 2e-5 and w["other"] < 2e-5, w
+
+
+def test_greedy_outlier_model_vs_oracle():
+    """End to end, greedy (the 24-bit digit bank): the model with one memory
+    dimension 10^3 x the rest and 10^3-times key / value dimensions in every
+    decoder attention (tests/outlier_util.py; the oracle's outputs are those
+    of the untouched model, test_oracle.py), 64 chunks, max_length 100,
+    -min_length 57, masks injected: the 1e-3 / identical-token bar."""
+    cfg = synth.ModelConfig()
+    W = outlier_weights(cfg, synth.make_weights(cfg, seed=11, eos_bias=-3.0), OUTLIER)
+    B = 64
+    sig = synth.synth_chunk_batch(B, 512, seed=1500, inject_masks=True)
+    _, form = _greedy_vs_oracle(cfg, W, sig, np.full(B, 512, np.int32), 100, 57, exact=False, max_ties=1)
+    assert form == 2
+
+
+def test_beam_outlier_model_vs_oracle():
+    """End to end, --fast beam 5 (the 24-bit context K/V and self history) on
+    the outlier model, 48 chunks, masks injected, all 48 against the oracle."""
+    cfg = synth.ModelConfig()
+    W = outlier_weights(cfg, synth.make_weights(cfg, seed=11, eos_bias=-3.0), OUTLIER)
+    B = 48
+    sig = synth.synth_chunk_batch(B, 512, seed=1600, inject_masks=True)
+    form, _ = _beam_sampled_vs_oracle(cfg, W, sig, np.full(B, 512, np.int32), 100, 57, exact=False, pick_n=B)
+    assert form == 3

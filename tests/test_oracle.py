@@ -162,3 +162,26 @@ def test_sampling_matches_reference_draws():
         sc = lg.gather(dim=1, index=ids)
         assert (ids[:, 0].numpy() == z["ids"][k]).all()
         np.testing.assert_array_equal(sc[:, 0].numpy(), z["scores"][k])
+
+
+def test_outlier_transform_preserves_function():
+    """tests/outlier_util.py's outlier-dimension transform (the GPU tests'
+    worst case for the 24-bit storage forms) leaves the oracle's outputs
+    unchanged: identical greedy tokens and --fast beam hypotheses, log-probs
+    within fp32 reassociation of the untouched model's."""
+    from tests.outlier_util import outlier_weights
+    cfg = synth.ModelConfig()
+    W = synth.make_weights(cfg, seed=11, eos_bias=-3.0)
+    Wo = outlier_weights(cfg, W, 1e3)
+    assert np.abs(Wo["encoder.layer_norm.weight"]).max() > 100 * np.abs(W["encoder.layer_norm.weight"]).max()
+    sig = synth.synth_chunk_batch(6, 512, seed=77)
+    lens = np.full(6, 512, np.int32)
+    a = ref_cpu.greedy(ref_cpu.RefModel(cfg, W), sig, lens, max_length=30, min_length=10)
+    b = ref_cpu.greedy(ref_cpu.RefModel(cfg, Wo), sig, lens, max_length=30, min_length=10)
+    assert (a["tokens"] == b["tokens"]).all()
+    assert gu.logp_close(b["logp"], a["logp"], atol=1e-4).all()
+    assert np.abs(b["memory"][..., 77]).max() > 100 * np.abs(np.delete(b["memory"], 77, axis=-1)).max()
+    ba = ref_cpu.fast_beam(ref_cpu.RefModel(cfg, W), sig[:3], lens[:3], beam_size=3, max_length=20, min_length=5)
+    bb = ref_cpu.fast_beam(ref_cpu.RefModel(cfg, Wo), sig[:3], lens[:3], beam_size=3, max_length=20, min_length=5)
+    for x, y in zip(ba, bb):
+        assert (np.asarray(x[0][1]) == np.asarray(y[0][1])).all() and abs(x[0][0] - y[0][0]) < 1e-4

@@ -135,6 +135,34 @@ def _worker(rank, world, port, n_reads, q, fail):
             return FakeTranslator(W, fail_sizes={int(x) for x in lengths})
         return FakeTranslator(W, fail_sizes=fail.get("sizes", ()))
 
+    if fail.get("sticky") and fail.get("rank") == rank:
+        # a sticky device fault: once the engine has raised, every later device call on this rank raises too --
+        # the rank's syncs and any collective on the default (device, RCCL in production) group
+        state = {"broken": False}
+        orig_run = shard.ReadShard.run
+
+        def run(self, *a, **k):
+            try:
+                return orig_run(self, *a, **k)
+            except Exception:
+                state["broken"] = True
+                raise
+
+        def guard(fn):
+            def wrapped(*a, **k):
+                if state["broken"] and k.get("group") is None:
+                    raise RuntimeError(f"{fn.__name__} on the device group after a sticky fault")
+                return fn(*a, **k)
+            return wrapped
+
+        def sync(_dev):
+            if state["broken"]:
+                raise RuntimeError("device call after a sticky fault")
+        shard.ReadShard.run = run
+        shard._device_sync = sync
+        for name in ("all_reduce", "barrier", "broadcast", "all_gather"):
+            setattr(dist, name, guard(getattr(dist, name)))
+
     try:
         g, preds = shard.run_distributed(n_reads, tf, lambda: W0, dev, batch_size=100, keep_predictions=True)
         q.put((rank, g, preds, seen["W"]["w"].tolist(), None))
@@ -207,3 +235,18 @@ def test_reads_failing_everywhere_are_named():
     named = [r[4] for r in res]
     assert all(x is not None for x in named) and named[0] == named[1]
     assert 7 in named[0]
+
+
+def test_sticky_device_fault_keeps_rank_in_the_job():
+    """world 3, rank 1's engine raises and from then on every
+    device call on that rank raises too (a sticky HIP error: syncs and
+    collectives on the device group).  The flag exchanges, the counters and
+    the closing barrier run on the CPU gloo group, so the faulted rank still
+    takes part: its reads are re-assigned, nobody blocks, every rank returns
+    the job's stats (failed_ranks [1]) and the output equals a failure-free
+    run."""
+    n, world = 90, 3
+    res = _run_world(world, n, {"rank": 1, "sticky": True})
+    g = _check_complete(res, n)
+    assert g["failed_ranks"] == [1]
+    assert res[1][1]["device_ok"] is False and res[0][1]["device_ok"] is True

@@ -4,7 +4,7 @@ a=$1; b=$2; shift 2
 R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out; mkdir -p $O; cd $R
 for rep in 1 2; do
   for v in $a $b; do
-    NANODEC_LIB=$R/tools/_ab/$v.so timeout -k 10 300 python -u bench.py --allow-switches --steps 60 --warmup 3 \
+    NANODEC_AB=1 NANODEC_LIB=$R/tools/_ab/$v.so timeout -k 10 300 python -u bench.py --allow-switches --steps 60 --warmup 3 \
       --cpu-baseline 0 --exact 0 --host-inclusive 0 --read-shard 0 --config-legs 0 "$@" \
       > $O/ab_lib_${v}_$rep.json 2> $O/ab_lib_${v}_$rep.err || exit $?
     python3 -c "

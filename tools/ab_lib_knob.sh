@@ -5,7 +5,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out; mkdir -p $O; cd $R
 for rep in 1 2; do
   for p in $pairs; do
     lib=${p%%:*}; val=${p#*:}
-    env $var=$val NANODEC_LIB=$R/tools/_ab/$lib.so timeout -k 10 300 python -u bench.py --allow-switches --steps 40 --warmup 3 \
+    env $var=$val NANODEC_AB=1 NANODEC_LIB=$R/tools/_ab/$lib.so timeout -k 10 300 python -u bench.py --allow-switches --steps 40 --warmup 3 \
       --cpu-baseline 0 --exact 0 --host-inclusive 0 --read-shard 0 --config-legs 0 "$@" > $O/abk_${lib}_${val}_$rep.json \
       2> $O/abk_${lib}_${val}_$rep.err || exit $?
     python3 -c "

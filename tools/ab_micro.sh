@@ -5,6 +5,6 @@ case_=$1; shift
 for rep in 1 2; do
   for v in "$@"; do
     echo "== $v rep $rep"
-    NANODEC_LIB=$R/tools/_ab/$v.so timeout -k 10 120 python -u tools/microbench.py $case_ 2>&1 | grep -v amdgpu.ids || exit 1
+    NANODEC_AB=1 NANODEC_LIB=$R/tools/_ab/$v.so timeout -k 10 120 python -u tools/microbench.py $case_ 2>&1 | grep -v amdgpu.ids || exit 1
   done
 done

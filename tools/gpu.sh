@@ -9,6 +9,7 @@
 #   bash tools/gpu.sh pmc TAG "CTRS" [args]     one rocprofv3 --pmc pass (one counter group)
 #   bash tools/gpu.sh mfma TAG [args]          rocprofv3 MFMA counter pass -> gpurun_out/TAG_mfma.json
 #   bash tools/gpu.sh pmcmb TAG "CTRS" CASE   one --pmc pass over a microbench case
+#   bash tools/gpu.sh pmcpy TAG "CTRS" tool.py [args]   one --pmc pass over a python tool
 #   bash tools/gpu.sh list                      rocprofv3 -L (available counters)
 #   bash tools/gpu.sh py TAG script.py [args]   any python tool (probes, microbenches)
 # Steps chain with &&:  bash tools/gpu.sh test && bash tools/gpu.sh bench r02_greedy
@@ -76,6 +77,13 @@ case $step in
     MB_EAGER=1 timeout -s KILL 180 rocprofv3 --pmc $ctrs --kernel-trace -d $O/$tag -o run --output-format csv -- \
       python3 $R/tools/microbench.py "$@" > $O/$tag.log 2>&1
     rc=$?; echo "pmcmb $tag rc=$rc"; exit $rc ;;
+  pmcpy)
+    # one --pmc pass over any python tool (e.g. tools/pmc_beam.py run K)
+    tag=$1; ctrs=$2; shift 2
+    cd /tmp && export TMPDIR=/tmp
+    timeout -s KILL 240 rocprofv3 --pmc $ctrs --kernel-trace -d $O/$tag -o run --output-format csv -- \
+      python3 "$@" > $O/$tag.log 2>&1
+    rc=$?; echo "pmcpy $tag rc=$rc"; exit $rc ;;
   list)
     cd /tmp && export TMPDIR=/tmp
     timeout -s KILL 60 rocprofv3 -L > $O/counters.txt 2>&1

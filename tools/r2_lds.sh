@@ -20,7 +20,7 @@ rc=$?; echo "parity rc=$rc"; tail -2 $O/r2lds_parity.log; [ $rc -ne 0 ] && exit 
 for v in $VARIANTS; do
   lib=$R/nanodecoder_amd/libnanodec_hip.so
   [ $v != default ] && lib=$R/tools/_ab/$v.so
-  NANODEC_LIB=$lib ND_ENC_ATTN0=1 PROBE_ROUNDS=4 PROBE_SHORT=1 PROBE_WHERE=1 timeout -k 10 200 \
+  NANODEC_AB=1 NANODEC_LIB=$lib ND_ENC_ATTN0=1 PROBE_ROUNDS=4 PROBE_SHORT=1 PROBE_WHERE=1 timeout -k 10 200 \
     python -u tools/rank2_probe.py > $O/r2lds_$v.log 2>&1 || exit $?
   echo "== $v"; grep -v amdgpu.ids $O/r2lds_$v.log | grep -E "round|bad chunks" | tail -6
 done
