@@ -94,6 +94,9 @@ __device__ __forceinline__ f32x4 mfma_d8h16as32(d8h4 a, d8h4 b, f32x4 c) {
 // 4 signed bytes -> 4 exact f16: f16 bits 0x64uu = 1024 + u with u = b + 128
 // (b ^ 0x80), minus 1152 (exact); then the plane weight (exact power of two)
 __device__ __forceinline__ d8h4 d8_cvt(unsigned x, int plane) {
+#ifdef B8_PROBE_NOCVT  // timing probe only: the bytes reinterpreted, no conversion
+  return __builtin_bit_cast(d8h4, d8u2{x, x ^ (unsigned)plane});
+#endif
   const unsigned t = x ^ 0x80808080u;
   const d8h2 lo = __builtin_bit_cast(d8h2, __builtin_amdgcn_perm(0x64646464u, t, 0x04010400u));
   const d8h2 hi = __builtin_bit_cast(d8h2, __builtin_amdgcn_perm(0x64646464u, t, 0x04030402u));
@@ -141,7 +144,11 @@ __device__ __forceinline__ void bank_d8_chunk(int c, const float* __restrict__ q
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
       const int db = 2 * (h & 1) + i / 3, pl = 2 - i % 3;
+#ifdef B8_PROBE_NOLOAD  // timing probe only (tools/bank_probe.sh): every chunk reads chunk 0's bank (L2-resident)
+      const i32x4* p = bank + (((((size_t)0) * B8_KB + w + B8_NW * (h >> 1)) * 4 + db) * 3 + pl) * 64 + lane;
+#else
       const i32x4* p = bank + ((((size_t)c * B8_KB + w + B8_NW * (h >> 1)) * 4 + db) * 3 + pl) * 64 + lane;
+#endif
       if constexpr (NT)
         f[i] = __builtin_nontemporal_load(p);
       else
@@ -231,6 +238,10 @@ __device__ __forceinline__ void bank_d8_chunk(int c, const float* __restrict__ q
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int db = 2 * part + j;
+#ifdef B8_PROBE_NOSCORE  // timing probe only: no score products (X stays 0 + the fragments' first word)
+        X1[0] += f[3 * j][0] ^ f[3 * j + 1][1] ^ f[3 * j + 2][2];
+        continue;
+#endif
         X1 = mfma_i8(f[3 * j], qb1[db], X1);
         X2 = mfma_i8(f[3 * j], qb2[db], X2);
         X3 = mfma_i8(f[3 * j + 1], qb1[db], X3);
@@ -291,6 +302,10 @@ __device__ __forceinline__ void bank_d8_chunk(int c, const float* __restrict__ q
     }
     const d8h8 pa8 = {pa[0], pa[1], pa[2], pa[3], pa[0], pa[1], pa[2], pa[3]};
     // ---- U += P^T M': dim blocks (2 kp, 2 kp + 1) of 16 dims, dims 16 k + col
+#ifdef B8_PROBE_NOU  // timing probe only: no context product (U stays the P sums)
+    ua[kb][0] += pa[0] + pa[1];
+    continue;
+#endif
 #pragma unroll
     for (int kp2 = 0; kp2 < 8; ++kp2) {
       const d8u2 r1 = tr_b8(rb1 + 32 * kp2), r2 = tr_b8(rb1 + 32 * kp2 + 16), r3 = tr_b8(rb3 + 32 * kp2);

@@ -154,6 +154,15 @@ struct nd_ctx {
   // scales (derive_bank_dim_scales; transformer encoder), and the scales
   float *bank_ln_g = nullptr, *bank_ln_b = nullptr;
   std::vector<float> bank_dim_scale;
+  // per-dimension power-of-two rebalancing of the decoder attentions' key / query and value / output
+  // projections (rebalance_attention): for a weight buffer, the scale of each of its rows (or columns), which
+  // nd_load_weight applies to a tensor loaded into it later so the set stays consistent
+  struct Rescale {
+    std::vector<float> s;
+    bool cols = false;
+  };
+  std::map<const float*, Rescale> rescale;
+  bool rebalanced = false;
   // encoder layer 0's QKV in the rank-2 form (kernels.hpp EmbedQkv): a | c on
   // the device, the three means on the host (kernel arguments); set at finalize
   float* eq_ac = nullptr;
@@ -1201,7 +1210,16 @@ int nd_load_weight(nd_ctx* c, const char* name, const float* host, const int64_t
     copy = (size_t)s.copy_rows * (numel / (size_t)shape[0]);
   }
   HIPCHK(hipSetDevice(c->cfg.device));
-  HIPCHK(hipMemcpy(s.dst, host, copy * sizeof(float), hipMemcpyHostToDevice));
+  auto rs = c->rescale.find(s.dst);
+  if (rs != c->rescale.end()) {  // a weight the context already rebalanced: the same exact scales
+    const auto& R = rs->second;
+    const size_t cols = ndim >= 2 ? (size_t)shape[ndim - 1] : 1;
+    std::vector<float> tmp(host, host + copy);
+    for (size_t e = 0; e < copy; ++e) tmp[e] *= R.s[R.cols ? e % cols : e / cols];
+    HIPCHK(hipMemcpy(s.dst, tmp.data(), copy * sizeof(float), hipMemcpyHostToDevice));
+  } else {
+    HIPCHK(hipMemcpy(s.dst, host, copy * sizeof(float), hipMemcpyHostToDevice));
+  }
   s.loaded = true;
   c->finalized = false;
   return ND_OK;
@@ -1228,6 +1246,122 @@ static hipError_t pack_step_weight(nd_ctx* c, const float* src, int ld, float* d
   if ((e = nd::launch_split_weight(src, rows, cols, hr, &sc, c->es, ld)) != hipSuccess) return e;
   c->split_rm[dst] = {hr, sc};
   return hipSuccess;
+}
+
+// Per-dimension power-of-two rebalancing of the decoder's attentions (self
+// and context, onmt/modules/multi_headed_attn.py:124-177).  The beam path
+// stores keys and values as 24-bit integers with one scale per (key, head)
+// (the context K/V image, the self-attention history), so a dimension far
+// larger than the rest of its head -- an "outlier dimension", common in
+// trained transformers -- would cost the head's other dimensions that many
+// bits.  Scores q.k and the context W_o v are unchanged when key dimension j
+// is divided by c_j and query dimension j multiplied by it (value dimension
+// j divided, output column j multiplied), so with c_j a power of two the
+// model's function is unchanged in exact arithmetic and in fp32 alike.  c_j =
+// 2^clamp(floor(log2(a_j / median of a over j's head)), 0, 12), a_j the
+// predicted magnitude of projection row j over its input (a LayerNorm output
+// y = n g + b: mean b, variance g^2; the NanoEncoder's memory: 0, 1):
+// sqrt(sum_i W_ji^2 g_i^2) + |bias_j + sum_i W_ji b_i|.  Applied in place to
+// the loaded weights once (nd_finalize); a weight loaded into the context
+// afterwards gets the same scales (nd_load_weight).
+static void rebalance_scales(const std::vector<float>& W, const std::vector<float>& b, const float* mu,
+                             const float* var, int D, std::vector<float>& c) {
+  std::vector<double> a(D);
+  for (int j = 0; j < D; ++j) {
+    double v = 0.0, m = b[j];
+    for (int i = 0; i < D; ++i) {
+      const double w = W[(size_t)j * D + i];
+      v += w * w * (var ? (double)var[i] : 1.0);
+      m += mu ? w * mu[i] : 0.0;
+    }
+    a[j] = std::sqrt(v) + std::fabs(m);
+  }
+  c.assign(D, 1.f);
+  for (int h = 0; h < ND_H; ++h) {
+    std::vector<double> hd(a.begin() + h * ND_DH, a.begin() + (h + 1) * ND_DH);
+    std::nth_element(hd.begin(), hd.begin() + ND_DH / 2, hd.end());
+    const double med = hd[ND_DH / 2];
+    for (int j = h * ND_DH; j < (h + 1) * ND_DH; ++j) {
+      int k = 0;
+      if (med > 0 && a[j] > 0 && std::isfinite(a[j])) k = (int)std::floor(std::log2(a[j] / med));
+      c[j] = std::ldexp(1.f, std::min(std::max(k, 0), 12));
+    }
+  }
+}
+
+static int rebalance_attention(nd_ctx* c) {
+  if (c->rebalanced) return ND_OK;
+  const int D = c->D;
+  auto down = [&](const float* d, size_t n, std::vector<float>& h) {
+    h.resize(n);
+    return hipMemcpy(h.data(), d, n * 4, hipMemcpyDeviceToHost);
+  };
+  // scale rows (or columns) of a D x D buffer / a D vector by f(c_j), upload, record the scales
+  auto apply = [&](float* dst, std::vector<float>& h, const std::vector<float>& cs, bool inv, bool cols,
+                   size_t rows) -> hipError_t {
+    nd_ctx::Rescale R;
+    R.cols = cols;
+    R.s.resize(cs.size());
+    for (size_t j = 0; j < cs.size(); ++j) R.s[j] = inv ? 1.f / cs[j] : cs[j];
+    const size_t ncol = h.size() / rows;
+    for (size_t e = 0; e < h.size(); ++e) h[e] *= R.s[cols ? e % ncol : e / ncol];
+    c->rescale[dst] = R;
+    return hipMemcpy(dst, h.data(), h.size() * 4, hipMemcpyHostToDevice);
+  };
+  std::vector<float> g, bb, Wq, bq, Wk, bk, Wv, bv, Wo, ck, cv;
+  std::vector<float> mg, mb;  // the memory's LN affine (transformer encoder)
+  const bool tf = c->cfg.encoder_type == ND_ENC_TRANSFORMER;
+  if (tf) {
+    HIPCHK(down(c->enc_ln_g, D, mg));
+    HIPCHK(down(c->enc_ln_b, D, mb));
+    for (auto& x : mg) x *= x;  // variance g^2
+  }
+  for (size_t i = 0; i < c->dec.size(); ++i) {
+    DecLayer& L = c->dec[i];
+    if (c->cfg.self_attn_type != ND_SELF_AVERAGE) {
+      HIPCHK(down(L.ln1_g, D, g));
+      HIPCHK(down(L.ln1_b, D, bb));
+      for (auto& x : g) x *= x;
+      HIPCHK(down(L.wqkv, (size_t)D * D, Wq));
+      HIPCHK(down(L.bqkv, D, bq));
+      HIPCHK(down(L.wqkv + (size_t)D * D, (size_t)D * D, Wk));
+      HIPCHK(down(L.bqkv + D, D, bk));
+      HIPCHK(down(L.wqkv + (size_t)2 * D * D, (size_t)D * D, Wv));
+      HIPCHK(down(L.bqkv + 2 * D, D, bv));
+      HIPCHK(down(L.wo, (size_t)D * D, Wo));
+      rebalance_scales(Wk, bk, bb.data(), g.data(), D, ck);
+      rebalance_scales(Wv, bv, bb.data(), g.data(), D, cv);
+      HIPCHK(apply(L.wqkv, Wq, ck, false, false, D));
+      HIPCHK(apply(L.bqkv, bq, ck, false, false, D));
+      HIPCHK(apply(L.wqkv + (size_t)D * D, Wk, ck, true, false, D));
+      HIPCHK(apply(L.bqkv + D, bk, ck, true, false, D));
+      HIPCHK(apply(L.wqkv + (size_t)2 * D * D, Wv, cv, true, false, D));
+      HIPCHK(apply(L.bqkv + 2 * D, bv, cv, true, false, D));
+      HIPCHK(apply(L.wo, Wo, cv, false, true, D));
+    }
+    float* wk = c->ctxkv_w + (size_t)(2 * i) * D * D;
+    float* wv = c->ctxkv_w + (size_t)(2 * i + 1) * D * D;
+    float* bk_ = c->ctxkv_b + (size_t)(2 * i) * D;
+    float* bv_ = c->ctxkv_b + (size_t)(2 * i + 1) * D;
+    HIPCHK(down(L.cwq, (size_t)D * D, Wq));
+    HIPCHK(down(L.cbq, D, bq));
+    HIPCHK(down(wk, (size_t)D * D, Wk));
+    HIPCHK(down(bk_, D, bk));
+    HIPCHK(down(wv, (size_t)D * D, Wv));
+    HIPCHK(down(bv_, D, bv));
+    HIPCHK(down(L.cwo, (size_t)D * D, Wo));
+    rebalance_scales(Wk, bk, tf ? mb.data() : nullptr, tf ? mg.data() : nullptr, D, ck);
+    rebalance_scales(Wv, bv, tf ? mb.data() : nullptr, tf ? mg.data() : nullptr, D, cv);
+    HIPCHK(apply(L.cwq, Wq, ck, false, false, D));
+    HIPCHK(apply(L.cbq, bq, ck, false, false, D));
+    HIPCHK(apply(wk, Wk, ck, true, false, D));
+    HIPCHK(apply(bk_, bk, ck, true, false, D));
+    HIPCHK(apply(wv, Wv, cv, true, false, D));
+    HIPCHK(apply(bv_, bv, cv, true, false, D));
+    HIPCHK(apply(L.cwo, Wo, cv, false, true, D));
+  }
+  c->rebalanced = true;
+  return ND_OK;
 }
 
 // Per-dimension power-of-two scales of the memory bank (transformer encoder).
@@ -1360,6 +1494,7 @@ int nd_finalize(nd_ctx* c) {
     if (kv.second.required && !kv.second.loaded) missing += (missing.empty() ? "" : ", ") + kv.first;
   if (!missing.empty()) return fail(ND_ERR_WEIGHT, "missing weights: " + missing);
   HIPCHK(hipSetDevice(c->cfg.device));
+  if (int rc = rebalance_attention(c)) return rc;
   if (c->cfg.encoder_type == ND_ENC_NANO) {
     // derived: b_ih + b_hh per gate; eval BatchNorm as scale/shift
     const int Hh = c->H;
