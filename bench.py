@@ -133,6 +133,13 @@ def dist_setup(args):
             torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             torch.distributed.init_process_group("gloo")
+    elif args.backend == "nccl" and args.read_shard and not args.selftest_cpu and torch.cuda.is_available():
+        # N = 1 without a launcher: a one-rank RCCL group, so the read-shard leg's weight broadcast (from HIP
+        # memory) and its gloo control exchanges run as at N > 1 (shard.run_distributed)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", local))
     return world, rank, local
 
 
@@ -858,6 +865,9 @@ def run_reads(args, world, rank, dev, cfg, W, n_reads_per_gpu):
             "load_imbalance_max_over_mean": round(g["load_imbalance"], 4),
             "scaling": "weak" if args.workload == "batch" else "weak (reads per GPU fixed)",
             "frontend": g.get("frontend"),
+            "process_group": (f"{torch.distributed.get_backend()} x{torch.distributed.get_world_size()}: weights "
+                              f"broadcast from HIP memory, flags / counters on a gloo group"
+                              if torch.distributed.is_initialized() else None),
             "workload": (f"configs[4]: {n_reads_per_gpu} synthetic reads per GPU, lengths U[256,1024], LPT shard, "
                          f"engine batch {args.batch}, reference batch_size 100, greedy, max_length "
                          f"{args.max_length}; raw reads handed to the translator, median/MAD + windowing on the "

@@ -126,55 +126,98 @@ __device__ __forceinline__ d8u2 tr_b8(const char* p) {
   return __builtin_bit_cast(d8u2, __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)p));
 }
 
-template <bool NT>
-__device__ __forceinline__ void bank_d8_chunk(int c, const float* __restrict__ qp, const i32x4* __restrict__ bank,
+// timing probe only (tools/bank_phases.py, B8_PROBE_PHASES): wave w of chunk c writes the wall clock at
+// phase i to the u64 slot [c][w][i] past the C16 x 2048 output (the probe allocates it)
+#ifdef B8_PROBE_PHASES
+#define B8_PHASE(i)                                                                                                  \
+  if (lane == 0)                                                                                                     \
+    reinterpret_cast<unsigned long long*>(out + (size_t)((C_ + 15) / 16 * 16) * (ND_H * ND_D))[(c * B8_NW + w) * 8 + \
+                                                                                          (i)] = wall_clock64()
+#else
+#define B8_PHASE(i)
+#endif
+
+// What a chunk's prologue loads: q' of the wave's head (4 dims per lane), this lane's key scales (keys
+// 16 (w + 8 kb) + 4 g + i), the signal, the chunk's largest row scale, then the first two half blocks.
+// WALK: the next chunk's head is loaded before this chunk's merge (its latency hides behind the merge).
+struct B8Head {
+  f32x4 qv;
+  f32x4 ksc[B8_KPW];
+  float sg, smax;
+  i32x4 F[3][6];
+};
+
+// half block h of chunk c: key block w + 8 (h >> 1), dim blocks 2 (h & 1) + j (j = 0, 1), planes 2, 1, 0:
+// f[3 j + 2 - pl]
+template <bool NT>  // non-temporal loads (a runtime condition around loads makes hipcc drain every load in flight)
+__device__ __forceinline__ void b8_hload(const i32x4* __restrict__ bank, int c, int h, int w, int lane,
+                                         i32x4 (&f)[6]) {
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int db = 2 * (h & 1) + i / 3, pl = 2 - i % 3;
+#ifdef B8_PROBE_NOLOAD  // timing probe only (tools/bank_probe.sh): every chunk reads chunk 0's bank (L2-resident)
+    const i32x4* p = bank + (((((size_t)0) * B8_KB + w + B8_NW * (h >> 1)) * 4 + db) * 3 + pl) * 64 + lane;
+#else
+    const i32x4* p = bank + ((((size_t)c * B8_KB + w + B8_NW * (h >> 1)) * 4 + db) * 3 + pl) * 64 + lane;
+#endif
+    if constexpr (NT)
+      f[i] = __builtin_nontemporal_load(p);
+    else
+      f[i] = *p;
+  }
+}
+
+template <bool NT, bool BOTH>  // BOTH: the first two half blocks (else the first only: the WALK prefetch)
+__device__ __forceinline__ void b8_head(int c, const float* __restrict__ qp, const i32x4* __restrict__ bank,
+                                        const float* __restrict__ kscale, const int* __restrict__ kemax,
+                                        const float* __restrict__ signal, int T, B8Head& hd) {
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4;
+  hd.qv = ld4(qp + (size_t)c * (ND_H * ND_D) + w * ND_D + 4 * lane);
+#pragma unroll
+  for (int kb = 0; kb < B8_KPW; ++kb) hd.ksc[kb] = ld4(kscale + (size_t)c * 512 + 16 * (w + B8_NW * kb) + 4 * g);
+  {
+    const int bkey = 16 * (w + B8_NW * (lane >> 4)) + (lane & 15);  // lane l: row l & 15 of key block w + 8 (l >> 4)
+    hd.sg = signal[(size_t)c * T + min(bkey, T - 1)];
+  }
+  hd.smax = __builtin_bit_cast(float, kemax[c]);  // the chunk's largest row scale
+  // issue order = retire order: q' and the scales first, then half block 0, then 1 (a wait for an
+  // earlier load leaves the later ones in flight)
+  __builtin_amdgcn_sched_barrier(0);
+  b8_hload<NT>(bank, c, 0, w, lane, hd.F[0]);
+  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (BOTH) {
+    b8_hload<NT>(bank, c, 1, w, lane, hd.F[1]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// chunk c from its loaded head (need1: its second half block still to load); nx >= 0: the next chunk this
+// workgroup walks to, whose head (first half block) goes into hd before the merge
+template <bool NT, bool NXNT>  // this chunk's and the next chunk's load policy
+__device__ __forceinline__ void bank_d8_chunk(int c, B8Head& hd, bool need1, int nx,
+                                              const float* __restrict__ qp, const i32x4* __restrict__ bank,
                                               const float* __restrict__ kscale, const int* __restrict__ kemax,
                                               const float* __restrict__ signal, const int* __restrict__ span,
                                               float pad_val, float* __restrict__ out, int T,
                                               unsigned long long* stamp, float* __restrict__ dbg, size_t dbg_stride,
-                                              int* ovf, unsigned long long t_entry) {
+                                              int* ovf, unsigned long long t_entry, int C_) {
   extern __shared__ float lds[];
   char* lb = reinterpret_cast<char*>(lds);
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int col = lane & 15, g = lane >> 4;
   char* img = lb + w * B8_IMG;
-  // half block h: key block w + 8 (h >> 1), dim blocks 2 (h & 1) + j (j = 0, 1), planes 2, 1, 0: f[3 j + 2 - pl]
-  auto hload = [&](int h, i32x4(&f)[6]) {
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      const int db = 2 * (h & 1) + i / 3, pl = 2 - i % 3;
-#ifdef B8_PROBE_NOLOAD  // timing probe only (tools/bank_probe.sh): every chunk reads chunk 0's bank (L2-resident)
-      const i32x4* p = bank + (((((size_t)0) * B8_KB + w + B8_NW * (h >> 1)) * 4 + db) * 3 + pl) * 64 + lane;
-#else
-      const i32x4* p = bank + ((((size_t)c * B8_KB + w + B8_NW * (h >> 1)) * 4 + db) * 3 + pl) * 64 + lane;
-#endif
-      if constexpr (NT)
-        f[i] = __builtin_nontemporal_load(p);
-      else
-        f[i] = *p;
-    }
-  };
-  // q' of head w (4 dims per lane), this lane's key scales (keys 16 (w + 8 kb) + 4 g + i), the signal,
-  // e_max: then the first half blocks
-  const f32x4 qv = ld4(qp + (size_t)c * (ND_H * ND_D) + w * ND_D + 4 * lane);
-  f32x4 ksc[B8_KPW];
-#pragma unroll
-  for (int kb = 0; kb < B8_KPW; ++kb) ksc[kb] = ld4(kscale + (size_t)c * 512 + 16 * (w + B8_NW * kb) + 4 * g);
-  float sg;
-  {
-    const int bkey = 16 * (w + B8_NW * (lane >> 4)) + (lane & 15);  // lane l: row l & 15 of key block w + 8 (l >> 4)
-    sg = signal[(size_t)c * T + min(bkey, T - 1)];
+  (void)C_;
+  B8_PHASE(0);
+  i32x4(&F)[3][6] = hd.F;
+  if (need1) {
+    b8_hload<NT>(bank, c, 1, w, lane, F[1]);
+    __builtin_amdgcn_sched_barrier(0);
   }
-  const float smax = __builtin_bit_cast(float, kemax[c]);  // the chunk's largest row scale
-  i32x4 F[3][6];
-  // issue order = retire order: q' and the scales first, then half block 0, then 1 (a wait for an
-  // earlier load leaves the later ones in flight)
-  __builtin_amdgcn_sched_barrier(0);
-  hload(0, F[0]);
-  __builtin_amdgcn_sched_barrier(0);
-  hload(1, F[1]);
-  __builtin_amdgcn_sched_barrier(0);
+  const f32x4 qv = hd.qv;
+  const float sg = hd.sg, smax = hd.smax;
   stamp_begin_at(stamp, t_entry);
   const int L = min(span[c], T);
   // q' of head w in digits (every wave one head)
@@ -197,6 +240,7 @@ __device__ __forceinline__ void bank_d8_chunk(int c, const float* __restrict__ q
     if (w == 0 && lane < 4) reinterpret_cast<unsigned*>(lb + B8_ZERO)[lane] = 0u;
   }
   lds_barrier();  // LDS only: the bank loads stay in flight
+  B8_PHASE(1);
   // B operands: column col = head col & 7; B1 = q2 (col < 8) | q1, B2 = 0 (col < 8) | q0; dims 64 db + 16 g ..
   i32x4 qb1[4], qb2[4];
   {
@@ -254,14 +298,14 @@ __device__ __forceinline__ void bank_d8_chunk(int c, const float* __restrict__ q
         *reinterpret_cast<i32x4*>(wimg + pl * B8_PLANE + 64 * db) = f[i];
       }
       __builtin_amdgcn_sched_barrier(0);  // the next loads reuse f's registers
-      if (h + 2 < 2 * B8_KPW) hload(h + 2, F[(h + 2) % 3]);
+      if (h + 2 < 2 * B8_KPW) b8_hload<NT>(bank, c, h + 2, w, lane, F[(h + 2) % 3]);
     }
     // ---- scores: columns h and h + 8 hold the high and low digit products of head h
     f32x4 s;
 #pragma unroll
     for (int i = 0; i < 4; ++i) s[i] = (float)X1[i] * w1 + (float)X2[i] * w2 + (float)X3[i] * w3 + (float)X4[i] * w4;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) s[i] = (s[i] + dpp_mov<0x128>(s[i])) * (ksc[kb][i] * sgm);
+    for (int i = 0; i < 4; ++i) s[i] = (s[i] + dpp_mov<0x128>(s[i])) * (hd.ksc[kb][i] * sgm);
     const int kbase = 16 * (w + B8_NW * kb) + 4 * g;  // key of row i
     const unsigned pb = (unsigned)(padm >> (16 * kb + 4 * g)) & 0xFu;
     float gm = -INFINITY;
@@ -296,7 +340,7 @@ __device__ __forceinline__ void bank_d8_chunk(int c, const float* __restrict__ q
     d8h4 pa;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const float x = p[i] * (ksc[kb][i] * kp);
+      const float x = p[i] * (hd.ksc[kb][i] * kp);
       const _Float16 hi = (_Float16)x;
       pa[i] = col < 8 ? hi : (_Float16)(x - (float)hi);
     }
@@ -317,7 +361,13 @@ __device__ __forceinline__ void bank_d8_chunk(int c, const float* __restrict__ q
       ua[2 * kp2 + 1] = mfma_d8h32(pa8, b2, ua[2 * kp2 + 1]);
       ua[2 * kp2 + 1] = mfma_d8h16as32(pa, d8_cvt(r3.y, 0), ua[2 * kp2 + 1]);
     }
+#ifdef B8_PROBE_PHASES
+    if (kb == 0) { B8_PHASE(2); }
+    if (kb == 1) { B8_PHASE(3); }
+    if (kb == 2) { B8_PHASE(4); }
+#endif
   }
+  B8_PHASE(5);
 
   // ---- merge the 8 waves (as dec_bank_h3_kernel): unmerged U^T fragments to the wave's own image, (m, l)
   //      beside, wave 0 turns them into merge weights and the output scale 2 s_max / den
@@ -328,6 +378,9 @@ __device__ __forceinline__ void bank_d8_chunk(int c, const float* __restrict__ q
 #pragma unroll
     for (int k = 0; k < 16; ++k) red[k * 64 + lane] = ua[k];
   }
+  // WALK: the next chunk's head (q', scales, its first half blocks) goes out now, into registers that are
+  // all dead here (U sits in LDS); its latency hides behind the rest of this chunk's merge
+  if (nx >= 0) b8_head<NXNT, false>(nx, qp, bank, kscale, kemax, signal, T, hd);
   if (lane < 8) {
     ml[(w * ND_H + lane) * 2] = m;
     ml[(w * ND_H + lane) * 2 + 1] = l;
@@ -349,6 +402,7 @@ __device__ __forceinline__ void bank_d8_chunk(int c, const float* __restrict__ q
     if (v == 0) fw[B8_NW * ND_H + hh] = den > 0.f ? __builtin_amdgcn_rcpf(den) * (2.0f * smax) : 0.f;
   }
   lds_barrier();
+  B8_PHASE(6);
 #pragma unroll
   for (int e = threadIdx.x; e < 512; e += B8_NW * 64) {
     const int hs = e >> 8, d = e & 255, k = d >> 4, cl = d & 15;
@@ -366,6 +420,7 @@ __device__ __forceinline__ void bank_d8_chunk(int c, const float* __restrict__ q
       out[pk(c, n & ~3, ND_H * ND_D) + (n & 3)] = num[i];
     }
   }
+  B8_PHASE(7);
 }
 
 template <bool NT, bool WALK>
@@ -380,22 +435,57 @@ dec_bank_d8_kernel(const float* __restrict__ qp, const i32x4* __restrict__ bank,
   const unsigned long long t_entry = wall_clock64();
   // NT: chunks c >= cached stream non-temporally; the first `cached` chunks' banks keep the default policy
   // (they stay in the Infinity Cache between the call's 300 launches, bank_cached below)
-  auto one = [&](int c) {
-    if (NT && c >= cached)
-      bank_d8_chunk<true>(c, qp, bank, kscale, kemax, signal, span, pad_val, out, T, stamp, dbg, dbg_stride, ovf,
-                          t_entry);
-    else
-      bank_d8_chunk<false>(c, qp, bank, kscale, kemax, signal, span, pad_val, out, T, stamp, dbg, dbg_stride, ovf,
-                           t_entry);
-  };
+  auto ntc = [&](int c) { return NT && c >= cached; };
+  // every load policy is a template argument (a branch around loads drains them), so each policy pair is its
+  // own copy of the chunk body
+#define B8_CHUNK(A, B, c_, need1_, nx_)                                                                            \
+  bank_d8_chunk<A, B>(c_, hd, need1_, nx_, qp, bank, kscale, kemax, signal, span, pad_val, out, T, stamp, dbg,      \
+                      dbg_stride, ovf, t_entry, C)
+  B8Head hd;
   if constexpr (WALK) {
-    for (int c = blockIdx.x; c < C; c += gridDim.x) {
-      if (c != (int)blockIdx.x) lds_barrier();  // the previous chunk's merge reads of LDS are done
-      one(c);
+    int c = blockIdx.x;
+    const int G = gridDim.x;
+    if (C <= 2 * G) {
+      // at most two chunks per workgroup (the pool's grid: half the CUs): straight-line, the second chunk's head
+      // loaded during the first one's merge (a runtime loop would carry the head's registers across its
+      // back-edge and spill)
+      // (each policy case one straight-line path: the head's registers never meet at a join).  The second
+      // chunk c + G >= G > C / 4 = cached is always past the cached quarter: non-temporal when NT is
+      const int nx = c + G < C ? c + G : -1;
+      if (!NT || !ntc(c)) {
+        b8_head<false, true>(c, qp, bank, kscale, kemax, signal, T, hd);
+        B8_CHUNK(false, NT, c, false, nx);
+      } else {
+        b8_head<NT, true>(c, qp, bank, kscale, kemax, signal, T, hd);
+        B8_CHUNK(NT, NT, c, false, nx);
+      }
+      if (nx >= 0) {
+        lds_barrier();  // the first chunk's merge reads of LDS are done
+        B8_CHUNK(NT, false, nx, true, -1);
+      }
+    } else {
+      for (; c < C; c += G) {
+        if (c != (int)blockIdx.x) lds_barrier();  // the previous chunk's merge reads of LDS are done
+        if (ntc(c)) {
+          b8_head<NT, true>(c, qp, bank, kscale, kemax, signal, T, hd);
+          B8_CHUNK(NT, false, c, false, -1);
+        } else {
+          b8_head<false, true>(c, qp, bank, kscale, kemax, signal, T, hd);
+          B8_CHUNK(false, false, c, false, -1);
+        }
+      }
     }
   } else {
-    one(blockIdx.x);
+    const int c = blockIdx.x;
+    if (ntc(c)) {
+      b8_head<NT, true>(c, qp, bank, kscale, kemax, signal, T, hd);
+      B8_CHUNK(NT, false, c, false, -1);
+    } else {
+      b8_head<false, true>(c, qp, bank, kscale, kemax, signal, T, hd);
+      B8_CHUNK(false, false, c, false, -1);
+    }
   }
+#undef B8_CHUNK
   stamp_end(stamp);
 }
 

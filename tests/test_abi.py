@@ -111,10 +111,14 @@ def test_hot_path_kernels_do_not_drain_loads(listings):
             # barrier before any wave reads the cache); the keys' loads go straight into the registers the
             # arithmetic reads (composing them made hipcc wait per key: 7 drains before)
             ("attention", r"dec_self_attention_beam_kernelILi5ELi4ELb1E", 1),
-            # the 24-bit digit bank: the walking form (pool lanes) issues straight-line;
-            # the one-chunk form's two sit in the unrolled key loop: the wait for the last fragment of the
-            # half block being multiplied, right before the next half block's loads (reviewed, round 5)
-            ("bank8", r"dec_bank_d8_kernelILb\dELb1E", 0),
+            # the 24-bit digit bank: the one-chunk form's two sit in the unrolled key loop: the wait for the
+            # last fragment of the half block being multiplied, right before the next half block's loads
+            # (reviewed, round 5).  The walking form (pool lanes) holds that body once per chunk and load
+            # policy: two chunks straight-line (the second's head loaded during the first's merge, round 6:
+            # pooled configs[1] 15.34 -> 15.20 ms, profiles/r06_ab_walk.txt) plus the general loop, each
+            # body with the same waits
+            ("bank8", r"dec_bank_d8_kernelILb0ELb1E", 3),
+            ("bank8", r"dec_bank_d8_kernelILb1ELb1E", 8),
             # (the non-temporal forms hold the chunk body twice: the call's first quarter of chunks keeps the
             # default cache policy, bank_cached in bank8.hip)
             ("bank8", r"dec_bank_d8_kernelILb0ELb0E", 2),
@@ -239,9 +243,11 @@ REVIEWED_PAIRED = {
     "dec_ctx_q24_kernel": (24, "the (m, l, acc) merge after a barrier behind the DMA rings' last use; the merge "
                                "image sits at LDS byte 0 (< 22 KB), far below 64 KB (the rings above it take no "
                                "paired form)"),
-    "dec_bank_d8_kernel": (6, "the (m, l) merge and the q' digit rows (cross-wave, after a barrier), twice in "
-                              "the non-temporal forms (two chunk bodies, bank8.hip bank_cached); pool-tested at the "
-                              "bench's configuration"),
+    "dec_bank_d8_kernel": (15, "the (m, l) merge and the q' digit rows (cross-wave, after a barrier), once per "
+                               "chunk body: twice in the non-temporal one-chunk form (bank8.hip bank_cached), up to "
+                               "five in the walking non-temporal form (round 6: the two-chunk straight-line path "
+                               "per load policy plus the general loop); pool-tested at the bench's configuration "
+                               "(profiles/r06_gpu4.log)"),
     "dec_mem_attention_kernel": (25, "the fp32 bank kernel (exact fp32 / short chunks): slab reads after "
                                      "barriers"),
 }

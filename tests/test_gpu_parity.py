@@ -526,7 +526,7 @@ def test_mem_attention_vs_fp64(T):
 
 
 @pytest.mark.parametrize("T,ln,grid", [(512, True, 0), (480, False, 0), (449, True, 0), (512, True, 5),
-                                       (512, False, 1)])
+                                       (512, False, 1), (512, True, 8), (480, False, 6)])
 def test_bank_d8_vs_fp64(T, ln, grid):
     """24-bit digit-bank attention (bank_pack_d8 + dec_bank_d8_kernel, the
     greedy path at 512-sample chunks) against an fp64 softmax(q' M^T) M per
@@ -534,7 +534,9 @@ def test_bank_d8_vs_fp64(T, ln, grid):
     no key), pad-masked keys, an all-masked chunk, a peaked chunk whose scores
     climb past the lazy-rescale threshold, with and without the LayerNorm
     (grid > 0: that many workgroups walk the 12 chunks, nd_set_bank_grid's
-    form; 5 leaves a ragged last round), plus rows of very
+    form; 5 leaves a ragged last round; 8 and 6 take the two-chunk
+    straight-line form, the second chunk's head loaded during the first
+    one's merge), plus rows of very
     different magnitude (per-row exponents 2^e_t far below the chunk's
     largest) and a head of q' a thousand times the others (per-head digit
     scales).  Tolerance: 2e-5 relative to the output's magnitude (digits

@@ -9,6 +9,7 @@ for rep in 1 2; do
       > $O/ab_lib_${v}_$rep.json 2> $O/ab_lib_${v}_$rep.err || exit $?
     python3 -c "
 import json; d=json.loads(open('$O/ab_lib_${v}_$rep.json').read().strip().splitlines()[-1]); r=d.get('roofline') or {}
-print('$v rep $rep: %.3f ms/step  one call %s  %s %.2f us' % (d['ms_per_step'], (d.get('one_call_in_flight') or {}).get('ms_per_step'), r.get('kernel'), 1e3*r.get('avg_launch_ms', 0)))"
+rp = d.get('roofline_pooled') or {}
+print('$v rep $rep: %.3f ms/step  one call %s  %s %.2f us  pooled %.2f us' % (d['ms_per_step'], (d.get('one_call_in_flight') or {}).get('ms_per_step'), r.get('kernel'), 1e3*r.get('avg_launch_ms', 0), 1e3*rp.get('avg_launch_ms', 0)))"
   done
 done
