@@ -470,9 +470,10 @@ int nd_op_dec_self_attention_q24(const float* qkv, void* cache, const int32_t* a
  * memory space) attends over the row-major memory bank mem (chunk c's
  * position t at row c*ldT + t, T <= ldT) with keys t < span[c] and key mask
  * signal[c*T+t] == pad_val; out = U [C, 8*256] P16 (head h: the
- * softmax-weighted sum of memory rows). */
+ * softmax-weighted sum of memory rows).  grid > 0: that many workgroups walk
+ * the chunks (the form nd_set_bank_grid selects for pool lanes). */
 int nd_op_dec_mem_attention(const float* qp, const float* mem, const float* signal, const int32_t* span, float pad_val,
-                            float* out, int32_t C, int32_t rpc, int32_t T, int32_t ldT, void* stream);
+                            float* out, int32_t C, int32_t rpc, int32_t T, int32_t ldT, int32_t grid, void* stream);
 
 /* One NanoEncoder BiLSTM layer, both directions (encoder/nano_encoder.py:92-111,
  * nn.LSTM(in, 128, bidirectional) over packed sequences): out [B*T, 256]

@@ -1072,12 +1072,6 @@ dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cac
   merge_waves<1, NW>(accs, ms, ls, m, l, acc, wave, lane, tid, out, r);
 }
 
-#ifndef SB_DEDUP
-#define SB_DEDUP 0  // beam self-attention: rows sharing a key's slot unpack it once
-#endif
-#ifndef SB_LAZY
-#define SB_LAZY 0   // beam self-attention: lazy running maximum
-#endif
 // Beam rows (round 5): one workgroup per chunk for its RPC rows.  The rows of
 // a chunk are hypotheses that share most of their history (anc[r][t] is the
 // same slot for every row until they diverge), so the per-row kernel above
@@ -1173,65 +1167,6 @@ dec_self_attention_beam_kernel(const float* __restrict__ qkv, float* __restrict_
     }
   };
   const int nk = wu < n ? (n - 1 - wu) / NW + 1 : 0;  // this wave's keys
-#if SB_DEDUP || SB_LAZY
-  // one row's score and online-softmax step on key (kf, vf, ks); lazy maximum (SB_LAZY): a row's running max
-  // moves only when a score passes it by more than 8 (its weights stay <= e^8, (m, l, acc) consistent)
-  auto row_step = [&](int j, const f32x4& kf, const f32x4& vf, float ks) {
-    float d = sum8(qv[j].x * kf.x + qv[j].y * kf.y + qv[j].z * kf.z + qv[j].w * kf.w);
-    if constexpr (Q24) d *= ks;
-#if SB_LAZY
-    if (d > m[j] + 8.0f) {  // divergent, rare after a chunk's first keys
-      const float sc = __expf(m[j] - d);  // m = -inf: 0 (acc, l are 0)
-      acc[j] *= sc;
-      l[j] *= sc;
-      m[j] = d;
-    }
-    const float p = __expf(d - m[j]);
-    acc[j] += p * vf;
-    l[j] += p;
-#else
-    const float mx = fmaxf(m[j], d);
-    const float sc = __expf(m[j] - mx);
-    const float p = __expf(d - mx);
-    acc[j] = acc[j] * sc + p * vf;
-    l[j] = l[j] * sc + p;
-    m[j] = mx;
-#endif
-  };
-#endif
-#if SB_DEDUP
-  // rows whose key i lives in one slot (the beam's shared history: anc[r][t] is one slot for most rows of a
-  // chunk) unpack it once: slot ids are wave-uniform, so the sharing test is scalar and every register index
-  // static (the loads stay unconditional: a load under a branch drains the ones in flight)
-  int slt_a[RPC], slt_b[RPC];
-  auto slots_of = [&](int i, int (&st)[RPC]) {
-#pragma unroll
-    for (int j = 0; j < RPC; ++j) st[j] = __builtin_amdgcn_readlane(sl[j], min(i, 63));
-  };
-  auto update_dd = [&](const Key (&kk)[RPC], const int (&st)[RPC]) {
-#pragma unroll
-    for (int d0 = 0; d0 < RPC; ++d0) {
-      bool first = true;
-#pragma unroll
-      for (int e = 0; e < d0; ++e) first = first && st[e] != st[d0];
-      if (!first) continue;
-      f32x4 kf, vf;
-      float ks = 1.f;
-      if constexpr (Q24) {
-        kf = q24_unpack(f32x4{__uint_as_float(kk[d0].kq.x), __uint_as_float(kk[d0].kq.y), __uint_as_float(kk[d0].kq.z), 0.f});
-        vf = q24_unpack(f32x4{__uint_as_float(kk[d0].vq.x), __uint_as_float(kk[d0].vq.y), __uint_as_float(kk[d0].vq.z), 0.f}) *
-             kk[d0].sq.y;
-        ks = kk[d0].sq.x;
-      } else {
-        kf = kk[d0].k;
-        vf = kk[d0].v;
-      }
-#pragma unroll
-      for (int j = d0; j < RPC; ++j)
-        if (j == d0 || st[j] == st[d0]) row_step(j, kf, vf, ks);
-    }
-  };
-#endif
   auto update = [&](const Key (&kk)[RPC]) {
 #pragma unroll
     for (int j = 0; j < RPC; ++j) {
@@ -1257,21 +1192,6 @@ dec_self_attention_beam_kernel(const float* __restrict__ qkv, float* __restrict_
   // two register sets in turn (a copy from one to the other would make hipcc wait for the loads it
   // just issued); the loads past the last key are clamped to it (straight-line) and never used
   Key ka[RPC], kb[RPC];
-#if SB_DEDUP
-  if (nk > 0) {
-    load(0, ka);
-    slots_of(0, slt_a);
-    for (int i = 0; i < nk; i += 2) {
-      load(min(i + 1, nk - 1), kb);
-      slots_of(min(i + 1, nk - 1), slt_b);
-      update_dd(ka, slt_a);
-      if (i + 1 >= nk) break;
-      load(min(i + 2, nk - 1), ka);
-      slots_of(min(i + 2, nk - 1), slt_a);
-      update_dd(kb, slt_b);
-    }
-  }
-#else
   if (nk > 0) {
     load(0, ka);
     for (int i = 0; i < nk; i += 2) {
@@ -1282,7 +1202,6 @@ dec_self_attention_beam_kernel(const float* __restrict__ qkv, float* __restrict_
       update(kb);
     }
   }
-#endif
   merge_waves<RPC, NW>(accs, ms, ls, m, l, acc, wave, lane, tid, out, c * RPC);
 }
 

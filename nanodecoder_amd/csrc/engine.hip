@@ -938,7 +938,7 @@ static hipError_t enqueue_dec_step(nd_ctx* c, int C, int rpc, int T, int step, c
                                     c->dU, C, T, s, stamp, dbg, dbg_stride, c->ovf, c->bank_nt, c->bank_grid));
       else
         LCHK(nd::launch_dec_mem_attention(c->dqk, c->mem, c->sig, c->span, (float)c->cfg.pad_idx, c->dU, C, rpc, T,
-                                          T, s, stamp, dbg, dbg_stride));
+                                          T, s, stamp, dbg, dbg_stride, c->bank_grid));
       LCHK(dg(c->dU, HD, L.pwvo, D, HD, L.bvo, c->dmid, D).res(c->dq1, D).stats(c->dmid_part).run(s, &pnm));
     } else {
       LCHK(dg(c->dq1, D, L.pcwq, D, D, L.ncbq, c->dcq, D).ln(c->dq1_part, pnq).run(s));
@@ -2352,9 +2352,10 @@ int nd_op_dec_self_attention_q24(const float* qkv, void* cache, const int32_t* a
 }
 
 int nd_op_dec_mem_attention(const float* qp, const float* mem, const float* signal, const int32_t* span, float pad_val,
-                            float* out, int32_t C, int32_t rpc, int32_t T, int32_t ldT, void* stream) {
+                            float* out, int32_t C, int32_t rpc, int32_t T, int32_t ldT, int32_t grid, void* stream) {
   if (int rc = ensure_attributes()) return rc;
-  hipError_t e = nd::launch_dec_mem_attention(qp, mem, signal, span, pad_val, out, C, rpc, T, ldT, (hipStream_t)stream);
+  hipError_t e = nd::launch_dec_mem_attention(qp, mem, signal, span, pad_val, out, C, rpc, T, ldT, (hipStream_t)stream,
+                                              nullptr, nullptr, 0, grid);
   if (e != hipSuccess) return fail(ND_ERR_ARG, std::string("dec_mem_attention: ") + hipGetErrorString(e));
   return ND_OK;
 }

@@ -269,7 +269,7 @@ struct NextEmbed {
 hipError_t launch_dec_mem_attention(const float* qp, const float* mem, const float* signal, const int* span,
                                     float pad_val, float* out, int C, int rpc, int T, int ldT, hipStream_t s,
                                     unsigned long long* stamp = nullptr, float* attn_dbg = nullptr,
-                                    size_t dbg_stride = 0);
+                                    size_t dbg_stride = 0, int grid = 0);
 // -attn_debug: raw head-0 score rows [B*S][T] (keys < span[c]) -> probabilities
 hipError_t launch_attn_rows_softmax(float* a, const int* span, int B, int S, int T, hipStream_t s);
 // stamp pairs (earliest start, latest end) <- (UINT64_MAX, 0)

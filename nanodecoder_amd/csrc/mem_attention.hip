@@ -75,14 +75,12 @@ __device__ __forceinline__ float sum_by8(float v) {
 // straight-line code and the compiler's wait counts on the in-flight tile
 // loads stay exact (a runtime loop makes it drain them every iteration).
 template <int NT>
-__global__ void __launch_bounds__(MB_NW * 64)
-dec_mem_attention_kernel(const float* __restrict__ qp, const float* __restrict__ mem,
-                         const float* __restrict__ signal, const int* __restrict__ span, float pad_val,
-                         float* __restrict__ out, int T, int ldT, unsigned long long* stamp,
-                         float* __restrict__ dbg, size_t dbg_stride) {
-  stamp_begin(stamp);
+__device__ __forceinline__ void mem_chunk(int c, const float* __restrict__ qp, const float* __restrict__ mem,
+                                          const float* __restrict__ signal, const int* __restrict__ span,
+                                          float pad_val, float* __restrict__ out, int T, int ldT,
+                                          float* __restrict__ dbg, size_t dbg_stride) {
   extern __shared__ float lds[];
-  const int c = blockIdx.x, lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (scalar addressing)
   float* slab = lds + w * MB_WAVE;            // [2][8 keys][256], row k rotated by 4k floats
   float* spart = slab + 2 * MB_KW * ND_D;     // [2][4 dp][8 heads][8 keys]
@@ -260,6 +258,22 @@ dec_mem_attention_kernel(const float* __restrict__ qp, const float* __restrict__
     num += f * ld4(red + ((size_t)v * 512 + h * 64 + lane) * 4);
   }
   st4(out + pk(c, h * ND_D + 4 * lane, ND_H * ND_D), num * (den > 0.f ? __builtin_amdgcn_rcpf(den) : 0.f));
+}
+
+// one workgroup per chunk, or (gridDim.x < C: EnginePool lanes, nd_set_bank_grid) fewer workgroups walking
+// the chunks, so the other lanes' kernels fit beside this one's 150 KB of LDS (the digit bank's walking form,
+// bank8.hip)
+template <int NT>
+__global__ void __launch_bounds__(MB_NW * 64)
+dec_mem_attention_kernel(const float* __restrict__ qp, const float* __restrict__ mem,
+                         const float* __restrict__ signal, const int* __restrict__ span, float pad_val,
+                         float* __restrict__ out, int T, int ldT, unsigned long long* stamp,
+                         float* __restrict__ dbg, size_t dbg_stride, int C) {
+  stamp_begin(stamp);
+  for (int c = blockIdx.x; c < C; c += gridDim.x) {
+    if (c != (int)blockIdx.x) __syncthreads();  // the previous chunk's merge reads of LDS are done
+    mem_chunk<NT>(c, qp, mem, signal, span, pad_val, out, T, ldT, dbg, dbg_stride);
+  }
   stamp_end(stamp);
 }
 
@@ -274,15 +288,19 @@ static_assert(MB_NW * 512 * 4 <= MB_U, "merge slots overlap the q' image");
 
 hipError_t launch_dec_mem_attention(const float* qp, const float* mem, const float* signal, const int* span,
                                     float pad_val, float* out, int C, int rpc, int T, int ldT, hipStream_t s,
-                                    unsigned long long* stamp, float* attn_dbg, size_t dbg_stride) {
-  if (rpc != 1 || T < 1 || T > 512 || ldT < T || C < 1) return hipErrorInvalidValue;
+                                    unsigned long long* stamp, float* attn_dbg, size_t dbg_stride, int grid) {
+  if (rpc != 1 || T < 1 || T > 512 || ldT < T || C < 1 || grid < 0) return hipErrorInvalidValue;
+#ifdef MB_NO_WALK  // timing variant only (tools/build_variant.sh): one workgroup per chunk always
+  grid = 0;
+#endif
+  const int G = grid > 0 ? std::min(C, grid) : C;
   const bool full = (T + MB_TILE - 1) / MB_TILE == 8;  // the 512-sample chunks of every bench / translate batch
   if (full)
-    hipLaunchKernelGGL((dec_mem_attention_kernel<8>), dim3(C), dim3(MB_NW * 64), mem_lds_bytes(), s, qp, mem, signal,
-                       span, pad_val, out, T, ldT, stamp, attn_dbg, dbg_stride);
+    hipLaunchKernelGGL((dec_mem_attention_kernel<8>), dim3(G), dim3(MB_NW * 64), mem_lds_bytes(), s, qp, mem, signal,
+                       span, pad_val, out, T, ldT, stamp, attn_dbg, dbg_stride, C);
   else
-    hipLaunchKernelGGL((dec_mem_attention_kernel<0>), dim3(C), dim3(MB_NW * 64), mem_lds_bytes(), s, qp, mem, signal,
-                       span, pad_val, out, T, ldT, stamp, attn_dbg, dbg_stride);
+    hipLaunchKernelGGL((dec_mem_attention_kernel<0>), dim3(G), dim3(MB_NW * 64), mem_lds_bytes(), s, qp, mem, signal,
+                       span, pad_val, out, T, ldT, stamp, attn_dbg, dbg_stride, C);
   return hipGetLastError();
 }
 

@@ -779,17 +779,18 @@ def op_memory_pack(x, B, T, ln_g=None, ln_b=None, ldT=None):
     return out
 
 
-def op_dec_mem_attention(qp, mem_p, signal, span, pad_val, rpc, out=None):
+def op_dec_mem_attention(qp, mem_p, signal, span, pad_val, rpc, out=None, grid=0):
     """Memory-bank context attention: qp [R16, 2048] packed, mem_p the
     row-major bank [C*ldT, 256] (op_memory_pack); returns U [R16, 2048] packed
-    (rows of chunks c < C written).  rpc must be 1."""
+    (rows of chunks c < C written).  rpc must be 1; grid > 0: that many
+    workgroups walk the chunks (nd_set_bank_grid's form)."""
     C, T = signal.shape
     ldT = mem_p.shape[0] // C
     if out is None:
         out = torch.empty(qp.shape[0], qp.shape[1], dtype=torch.float32, device=qp.device)
     s = ctypes.c_void_p(torch.cuda.current_stream(qp.device).cuda_stream)
     _lib.check(_lib.lib().nd_op_dec_mem_attention(_ptr(qp), _ptr(mem_p), _ptr(signal), _ptr(span), float(pad_val),
-                                                  _ptr(out), C, rpc, T, ldT, s), "nd_op_dec_mem_attention")
+                                                  _ptr(out), C, rpc, T, ldT, int(grid), s), "nd_op_dec_mem_attention")
     return out
 
 

@@ -493,11 +493,12 @@ def test_enc_attention_vs_oracle(scale):
         assert (out[b * T: b * T + L] - exp).abs().max().item() < tol, b
 
 
-@pytest.mark.parametrize("T", [512, 200, 37])
-def test_mem_attention_vs_fp64(T):
+@pytest.mark.parametrize("T,grid", [(512, 0), (200, 0), (37, 0), (512, 5), (512, 7), (200, 1)])
+def test_mem_attention_vs_fp64(T, grid):
     """Memory-bank context attention (dec_mem_attention_kernel) against an
     fp64 softmax(q' M^T) M per head, with ragged spans (tile/wave boundaries,
-    single key, waves owning no key), pad-masked keys and an all-masked chunk."""
+    single key, waves owning no key), pad-masked keys and an all-masked chunk;
+    grid > 0: that many workgroups walk the 12 chunks (the pool lanes' form)."""
     from nanodecoder_amd.engine import op_dec_mem_attention, op_memory_pack, pack_p16, unpack_p16
     rng = np.random.default_rng(3)
     C, PAD = 12, 1.0
@@ -511,7 +512,7 @@ def test_mem_attention_vs_fp64(T):
     dev = torch.device("cuda", 0)
     mem = op_memory_pack(torch.from_numpy(x).to(dev), C, T)
     out = op_dec_mem_attention(pack_p16(torch.from_numpy(q).to(dev)), mem, torch.from_numpy(sig).to(dev),
-                               torch.from_numpy(spans).to(dev), PAD, 1)
+                               torch.from_numpy(spans).to(dev), PAD, 1, grid=grid)
     got = unpack_p16(out, C).cpu().numpy()
     for c in range(C):
         L = int(spans[c])
