@@ -9,6 +9,6 @@ for rep in 1 2; do
     python3 -c "
 import json,sys; d=json.loads(open('$O/ab_${var}_${v}_$rep.json').read().strip().splitlines()[-1])
 r=d.get('roofline') or {}
-print('$var=$v rep $rep: %.3f ms/step  value %.0f  dominant %s %.2f us' % (d['ms_per_step'], d['value'], r.get('kernel'), 1e3*r.get('avg_launch_ms', 0)))"
+print('$var=$v rep $rep: %.3f ms/step  one call %s  value %.0f  dominant %s %.2f us' % (d['ms_per_step'], (d.get('one_call_in_flight') or {}).get('ms_per_step'), d['value'], r.get('kernel'), 1e3*r.get('avg_launch_ms', 0)))"
   done
 done
