@@ -72,7 +72,12 @@ int nd_create(const nd_config* cfg, nd_ctx** out);
 int nd_load_weight(nd_ctx* ctx, const char* name, const float* host, const int64_t* shape, int ndim);
 
 /* Checks that every required weight was loaded and builds derived packed
- * weights.  Must be called once before any translate call. */
+ * weights.  Must be called once before any translate call.  The first call
+ * also rebalances the decoder attentions' key / query and value / output
+ * projections by exact powers of two per dimension (the model's function is
+ * unchanged; a dimension far larger than the rest of its head would otherwise
+ * cost the 24-bit K/V forms their bits); a weight loaded afterwards gets the
+ * same scales. */
 int nd_finalize(nd_ctx* ctx);
 
 /* ctx (just created, no weight loaded, the same model configuration as src)
