@@ -444,7 +444,12 @@ def kernel_roofline(eng, B, mode, beam, encoder="transformer", alive=None, secon
                           "achieved": round(tf, 2), "peak": round(SPLIT_PEAK, 1),
                           "unit": "TFLOP/s fp32-equivalent (fp16 MFMA peak / 3 products)",
                           "frac": round(tf / SPLIT_PEAK, 4), "avg_launch_ms": round(gms, 4),
-                          "algorithmic_flops_per_launch": int(flops), "rows": M}
+                          "algorithmic_flops_per_launch": int(flops), "rows": M,
+                          "timing": ("10 back-to-back launches on random operands (HIP events): the sustained "
+                                     "rate, at the lower clock the chip holds under this kernel alone; inside "
+                                     "a translate call it runs between the decoder's short kernels and the "
+                                     "kernel trace times it ~10-15% faster (profiles/r06f_one_call_kernel_"
+                                     "stats.txt, DESIGN.md section 5)")}
     del Y, X, W1, w1h, w2h
     return out
 
