@@ -423,6 +423,13 @@ int nd_op_gemm_p16_splitk(const float* A, const uint16_t* Wh, float wscale, cons
                           float* C, int32_t M, int32_t N, int32_t K, float* part_out, float* slab, int32_t* tickets,
                           int32_t tiles, int32_t* part_n_out, void* stream);
 
+/* The same split-K route in exact fp32 (nd_set_exact_fp32: the pool lanes'
+ * form of W_vo / FFN2 there): W is the fp32 weight [N, K] in the P16 layout
+ * (as A), products on v_mfma_f32_16x16x4f32, no weight scale. */
+int nd_op_gemm_p16_splitk_f32(const float* A, const float* W, const float* bias, const float* R, float* C,
+                              int32_t M, int32_t N, int32_t K, float* part_out, float* slab, int32_t* tickets,
+                              int32_t tiles, int32_t* part_n_out, void* stream);
+
 /* The same GEMM with the weight's row-major split image too (nd_op_split_weight
  * of the row-major W): from M >= 2048 rows (beam search over large batches)
  * the engine runs it on the LDS-tiled kernel with P16 operands. */

@@ -87,6 +87,7 @@ SIGNATURES = {
     "nd_op_dec_ffn": (_I, [_P, _P, _F, _P, _P, _F, _P, _P, _P, _I, _I, _I, _P, _P, _P, _I, _P, _P]),
     "nd_op_dec_ffn_slab_floats": (ctypes.c_int64, [_I, _I]),
     "nd_op_gemm_p16_splitk": (_I, [_P, _P, ctypes.c_float, _P, _P, _P, _I, _I, _I, _P, _P, _P, _I, _P, _P]),
+    "nd_op_gemm_p16_splitk_f32": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _I, _P, _P]),
     "nd_op_gemm_p16_split_rm": (_I, [_P, _P, _F, _P, _F, _P, _P, _P, _I, _I, _I, _P, _I, _P, _I, _P, _P]),
     "nd_op_dec_mem_attention": (_I, [_P, _P, _P, _P, ctypes.c_float, _P, _I, _I, _I, _I, _I, _P]),
     "nd_op_memory_pack": (_I, [_P, _P, _P, _P, _I, _I, _I, _P]),

@@ -2266,15 +2266,16 @@ int nd_op_gemm_p16_split(const float* A, const uint16_t* Wh, float wscale, const
   return ND_OK;
 }
 
-int nd_op_gemm_p16_splitk(const float* A, const uint16_t* Wh, float wscale, const float* bias, const float* R,
-                          float* C, int32_t M, int32_t N, int32_t K, float* part_out, float* slab, int32_t* tickets,
-                          int32_t tiles, int32_t* part_n_out, void* stream) {
+static int gemm_p16_splitk(const float* A, const uint16_t* Wh, const float* W, float wscale, const float* bias,
+                           const float* R, float* C, int32_t M, int32_t N, int32_t K, float* part_out, float* slab,
+                           int32_t* tickets, int32_t tiles, int32_t* part_n_out, void* stream) {
   if (int rc = ensure_attributes()) return rc;
-  if (!A || !Wh || !C || !slab || !tickets || tiles < 1) return fail(ND_ERR_ARG, "gemm_p16_splitk: bad arguments");
+  if (!A || (!Wh && !W) || !C || !slab || !tickets || tiles < 1)
+    return fail(ND_ERR_ARG, "gemm_p16_splitk: bad arguments");
   if ((K != 1024 && K != 2048) || N % 32 || M <= 128 || ((M + 31) / 32) * (N / 32) > tiles)
     return fail(ND_ERR_ARG, "gemm_p16_splitk: needs K 1024 / 2048, N % 32 == 0, M > 128 and enough tiles");
   nd::GemmArgs g;
-  g.A = A; g.Wh = Wh; g.wscale = wscale; g.bias = bias; g.R = R; g.C = C; g.M = M; g.N = N; g.K = K;
+  g.A = A; g.Wh = Wh; g.W = W; g.wscale = wscale; g.bias = bias; g.R = R; g.C = C; g.M = M; g.N = N; g.K = K;
   g.part_out = part_out;
   g.sk_slab = slab; g.sk_cnt = tickets; g.sk_tiles = tiles;
   const long long before = nd::gemm_route_count(ND_ROUTE_P16_SPLITK, false);
@@ -2283,6 +2284,22 @@ int nd_op_gemm_p16_splitk(const float* A, const uint16_t* Wh, float wscale, cons
   if (nd::gemm_route_count(ND_ROUTE_P16_SPLITK, false) == before) return fail(ND_ERR_ARG, "gemm_p16_splitk: not taken");
   if (part_n_out) *part_n_out = g.part_n_out;
   return ND_OK;
+}
+
+int nd_op_gemm_p16_splitk(const float* A, const uint16_t* Wh, float wscale, const float* bias, const float* R,
+                          float* C, int32_t M, int32_t N, int32_t K, float* part_out, float* slab, int32_t* tickets,
+                          int32_t tiles, int32_t* part_n_out, void* stream) {
+  if (!Wh) return fail(ND_ERR_ARG, "gemm_p16_splitk: null Wh");
+  return gemm_p16_splitk(A, Wh, nullptr, wscale, bias, R, C, M, N, K, part_out, slab, tickets, tiles, part_n_out,
+                         stream);
+}
+
+int nd_op_gemm_p16_splitk_f32(const float* A, const float* W, const float* bias, const float* R, float* C,
+                              int32_t M, int32_t N, int32_t K, float* part_out, float* slab, int32_t* tickets,
+                              int32_t tiles, int32_t* part_n_out, void* stream) {
+  if (!W) return fail(ND_ERR_ARG, "gemm_p16_splitk_f32: null W");
+  return gemm_p16_splitk(A, nullptr, W, 1.0f, bias, R, C, M, N, K, part_out, slab, tickets, tiles, part_n_out,
+                         stream);
 }
 
 int nd_op_gemm_p16_split_rm(const float* A, const uint16_t* Wh, float wscale, const uint16_t* Wh_rm, float wscale_rm,

@@ -717,7 +717,9 @@ __device__ __forceinline__ f32x4 pk_load_sc1(__amdgpu_buffer_rsrc_t r, int off) 
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16));
 }
 
-template <bool RESID>
+// !H3 (exact fp32, nd_set_exact_fp32): the same tiles and slices on the fp32 P16 weight (16-k blocks, 4
+// v_mfma_f32_16x16x4f32 per block and output block), no range guard, no weight scale
+template <bool H3, bool RESID>
 __global__ void __launch_bounds__(PK_NW * 64) gemm_p16k_kernel(const GemmArgs g) {
   // ONE shared array: the waves' partial blocks, then the last-arriver word
   __shared__ __attribute__((aligned(16))) f32x4 red[PK_NW * 4 * 64 + 1];
@@ -727,7 +729,7 @@ __global__ void __launch_bounds__(PK_NW * 64) gemm_p16k_kernel(const GemmArgs g)
   const int mb0 = 2 * (tile / NBT), nb0 = 2 * (tile % NBT);
   const int MB = (g.M + 15) >> 4, KB = g.K >> 4, KP = g.K >> 5, NB = g.N >> 4;
   const f32x4* __restrict__ A4 = reinterpret_cast<const f32x4*>(g.A);
-  const f32x4* __restrict__ W4 = reinterpret_cast<const f32x4*>(g.Wh);
+  const f32x4* __restrict__ W4 = reinterpret_cast<const f32x4*>(H3 ? (const void*)g.Wh : (const void*)g.W);
   // this wave's k pairs: sl * 16 + wave * 4 .. + 3; loads in order of use, straight-line
   const int kp0 = sl * (PK_NW * PK_KPW) + wave * PK_KPW;
   f32x4 a[2][2 * PK_KPW], w[2][2 * PK_KPW];
@@ -735,10 +737,13 @@ __global__ void __launch_bounds__(PK_NW * 64) gemm_p16k_kernel(const GemmArgs g)
   for (int r = 0; r < 2; ++r)
 #pragma unroll
     for (int f = 0; f < 2 * PK_KPW; ++f) a[r][f] = A4[((size_t)min(mb0 + r, MB - 1) * KB + 2 * kp0 + f) * 64 + lane];
+  // H3: the P16H image's hi / lo planes of each k pair; fp32: the P16 blocks 2 kp0 .. + 7, as A
 #pragma unroll
   for (int c = 0; c < 2; ++c)
 #pragma unroll
-    for (int f = 0; f < 2 * PK_KPW; ++f) w[c][f] = W4[(((size_t)(nb0 + c) * KP + kp0) * 2 + f) * 64 + lane];
+    for (int f = 0; f < 2 * PK_KPW; ++f)
+      w[c][f] = H3 ? W4[(((size_t)(nb0 + c) * KP + kp0) * 2 + f) * 64 + lane]
+                   : W4[((size_t)(nb0 + c) * KB + 2 * kp0 + f) * 64 + lane];
   // the epilogue operands of the block this wave finishes (rb, cb) = (wave >> 1, wave & 1)
   const int rb = wave >> 1, cb = wave & 1, mb = mb0 + rb, nb = nb0 + cb;
   const size_t ct = ((size_t)min(mb, MB - 1) * NB + nb) * 64 + lane;
@@ -746,27 +751,40 @@ __global__ void __launch_bounds__(PK_NW * 64) gemm_p16k_kernel(const GemmArgs g)
   f32x4 rv = {0.f, 0.f, 0.f, 0.f};
   if constexpr (RESID) rv = reinterpret_cast<const f32x4*>(g.R)[ct];
   __builtin_amdgcn_sched_barrier(0);
-  float amax = 0.f;
-#pragma unroll
-  for (int r = 0; r < 2; ++r)
-#pragma unroll
-    for (int f = 0; f < 2 * PK_KPW; ++f) amax = fmaxf(amax, absmax4(a[r][f]));
-  flag_overflow(g.ovf, amax);
   f32x4 acc0[4], acc1[4];
 #pragma unroll
   for (int b = 0; b < 4; ++b) acc0[b] = acc1[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if constexpr (H3) {
+    float amax = 0.f;
 #pragma unroll
-  for (int p = 0; p < PK_KPW; ++p) {
-    h8 ah[2], al[2];
+    for (int r = 0; r < 2; ++r)
 #pragma unroll
-    for (int r = 0; r < 2; ++r) split8(a[r][2 * p], a[r][2 * p + 1], ah[r], al[r]);
+      for (int f = 0; f < 2 * PK_KPW; ++f) amax = fmaxf(amax, absmax4(a[r][f]));
+    flag_overflow(g.ovf, amax);
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const h8 wh = __builtin_bit_cast(h8, w[b & 1][2 * p]), wl = __builtin_bit_cast(h8, w[b & 1][2 * p + 1]);
-      acc0[b] = mfma16h(wh, ah[b >> 1], acc0[b]);
-      acc1[b] = mfma16h(wh, al[b >> 1], acc1[b]);
-      acc1[b] = mfma16h(wl, ah[b >> 1], acc1[b]);
+    for (int p = 0; p < PK_KPW; ++p) {
+      h8 ah[2], al[2];
+#pragma unroll
+      for (int r = 0; r < 2; ++r) split8(a[r][2 * p], a[r][2 * p + 1], ah[r], al[r]);
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const h8 wh = __builtin_bit_cast(h8, w[b & 1][2 * p]), wl = __builtin_bit_cast(h8, w[b & 1][2 * p + 1]);
+        acc0[b] = mfma16h(wh, ah[b >> 1], acc0[b]);
+        acc1[b] = mfma16h(wh, al[b >> 1], acc1[b]);
+        acc1[b] = mfma16h(wl, ah[b >> 1], acc1[b]);
+      }
     }
+  } else {
+#pragma unroll
+    for (int f = 0; f < 2 * PK_KPW; ++f)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const f32x4 wv = w[b & 1][f], av = a[b >> 1][f];
+        acc0[b] = mfma16(wv[0], av[0], acc0[b]);
+        acc1[b] = mfma16(wv[1], av[1], acc1[b]);
+        acc0[b] = mfma16(wv[2], av[2], acc0[b]);
+        acc1[b] = mfma16(wv[3], av[3], acc1[b]);
+      }
   }
   // the workgroup's slice: block b summed over the 4 waves in wave order, by wave b
 #pragma unroll
@@ -800,7 +818,8 @@ __global__ void __launch_bounds__(PK_NW * 64) gemm_p16k_kernel(const GemmArgs g)
     v = sum;
     if (tid == 0) __hip_atomic_store(g.sk_cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  v = v * g.wscale + bv;
+  if constexpr (H3) v *= g.wscale;
+  v += bv;
   if constexpr (RESID) v += rv;
   if (mb >= MB) return;
   reinterpret_cast<f32x4*>(g.C)[ct] = v;
@@ -1168,16 +1187,23 @@ hipError_t launch_gemm_p16(GemmArgs& g, hipStream_t s) {
   }
   // split over workgroups (gemm_p16k_kernel): 32 x 32 tiles x K / 512 slices, when the tiles x slices fill
   // the chip at least half (M from 128 rows) and the context gave the slab / tickets for that many tiles
-  if (g.Wh && !g.skip && !g.c_rm && !g.relu && (g.K == 2048 || g.K == 1024) && g.N % 32 == 0 && g.sk_slab &&
-      g.sk_cnt) {
+  // (exact fp32: the fp32 P16 weight, same tiles and slices)
+  if (!g.skip && !g.c_rm && !g.relu && (g.K == 2048 || g.K == 1024) && g.N % 32 == 0 && g.sk_slab && g.sk_cnt) {
     const int tiles = ((g.M + 31) / 32) * (g.N / 32), S = g.K / PK_SLICE;
     if (g.M > 128 && tiles <= g.sk_tiles) {
       count_route(ND_ROUTE_P16_SPLITK);
       g.part_n_out = g.N / 16;
-      if (g.R)
-        hipLaunchKernelGGL((gemm_p16k_kernel<true>), dim3(tiles * S), dim3(PK_NW * 64), 0, s, g);
-      else
-        hipLaunchKernelGGL((gemm_p16k_kernel<false>), dim3(tiles * S), dim3(PK_NW * 64), 0, s, g);
+      const dim3 grid(tiles * S), block(PK_NW * 64);
+      if (g.Wh) {
+        if (g.R)
+          hipLaunchKernelGGL((gemm_p16k_kernel<true, true>), grid, block, 0, s, g);
+        else
+          hipLaunchKernelGGL((gemm_p16k_kernel<true, false>), grid, block, 0, s, g);
+      } else if (g.R) {
+        hipLaunchKernelGGL((gemm_p16k_kernel<false, true>), grid, block, 0, s, g);
+      } else {
+        hipLaunchKernelGGL((gemm_p16k_kernel<false, false>), grid, block, 0, s, g);
+      }
       return hipGetLastError();
     }
   }

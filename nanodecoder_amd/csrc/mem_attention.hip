@@ -70,15 +70,60 @@ __device__ __forceinline__ float sum_by8(float v) {
   return xor32_sum(xor16_sum(v));
 }
 
+// What a chunk's prologue loads before its first LDS store: the source samples of the wave's keys, its
+// first two tiles, this thread's 16 B of q'.  The walking form (two chunks per workgroup) loads the second
+// chunk's head before the first chunk's merge, so its latency hides behind the merge (as bank8.hip's).
+struct MbHead {
+  float sgv;
+  f32x4 qv;
+  f32x4 R0[MB_KW], R1[MB_KW];
+};
+
+// rows r * 64 + w * 8 + k (k < 8) of a chunk's bank (clamped to T - 1): lane l's 16 B of each
+__device__ __forceinline__ void mb_fetch(const float* __restrict__ mc, int r, int w, int lane, int T,
+                                         f32x4 (&dst)[MB_KW]) {
+#pragma unroll
+  for (int k = 0; k < MB_KW; ++k) {
+    const int t = min(r * MB_TILE + w * MB_KW + k, T - 1);
+    dst[k] = ld4(mc + (size_t)t * ND_D + 4 * lane);
+  }
+}
+
+__device__ __forceinline__ const float* mb_chunk_base(const float* mem, int c, int ldT) {
+#ifdef MB_PROBE_NOLOAD  // timing probe only (tools/mem_probe.sh): every chunk reads chunk 0's bank (L2-resident)
+  (void)c;
+  (void)ldT;
+  return mem;
+#else
+  return mem + (size_t)c * ldT * ND_D;
+#endif
+}
+
+// the head of chunk c: the source samples first (the waits that retire the tile loads then retire them
+// too, so no wait for them is left inside the loop, where it would drain the prefetched tiles), then the
+// first two tiles, then q'
+__device__ __forceinline__ void mb_head(int c, const float* __restrict__ qp, const float* __restrict__ mem,
+                                        const float* __restrict__ signal, int T, int ldT, int ntile, MbHead& hd) {
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const float* mc = mb_chunk_base(mem, c, ldT);
+  hd.sgv = signal[(size_t)c * T + min((lane >> 3) * MB_TILE + w * MB_KW + (lane & 7), T - 1)];
+  if (ntile > 0) mb_fetch(mc, 0, w, lane, T, hd.R0);
+  if (ntile > 1) mb_fetch(mc, 1, w, lane, T, hd.R1);
+  hd.qv = ld4(qp + pk(c, (threadIdx.x >> 6) * ND_D + 4 * (threadIdx.x & 63), ND_H * ND_D));
+}
+
 // NT > 0: the tile count is the compile-time NT (T in (64 (NT-1), 64 NT]);
 // every tile is processed (keys >= span masked), so the tile loop unrolls to
 // straight-line code and the compiler's wait counts on the in-flight tile
 // loads stay exact (a runtime loop makes it drain them every iteration).
-template <int NT>
-__device__ __forceinline__ void mem_chunk(int c, const float* __restrict__ qp, const float* __restrict__ mem,
-                                          const float* __restrict__ signal, const int* __restrict__ span,
-                                          float pad_val, float* __restrict__ out, int T, int ldT,
-                                          float* __restrict__ dbg, size_t dbg_stride) {
+// hd: chunk c's head (mb_head, loaded by the caller); nx >= 0 (NEXT): the next chunk this workgroup walks to,
+// whose head goes into hd before this chunk's merge.
+template <int NT, bool NEXT>
+__device__ __forceinline__ void mem_chunk(int c, MbHead& hd, int nx, const float* __restrict__ qp,
+                                          const float* __restrict__ mem, const float* __restrict__ signal,
+                                          const int* __restrict__ span, float pad_val, float* __restrict__ out,
+                                          int T, int ldT, float* __restrict__ dbg, size_t dbg_stride) {
   extern __shared__ float lds[];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (scalar addressing)
@@ -88,7 +133,7 @@ __device__ __forceinline__ void mem_chunk(int c, const float* __restrict__ qp, c
   const float* ub = lds + MB_U;
   const int L = min(span[c], T);
   const int ntile = NT > 0 ? NT : (L + MB_TILE - 1) / MB_TILE;
-  const float* mc = mem + (size_t)c * ldT * ND_D;
+  const float* mc = mb_chunk_base(mem, c, ldT);
 
   // ---- lane roles
   // S: block b = lane >> 2, x = lane & 3
@@ -104,13 +149,7 @@ __device__ __forceinline__ void mem_chunk(int c, const float* __restrict__ qp, c
   // Staging through registers, four tiles in flight (two in registers, two
   // in LDS): lane l loads 16 B of each of the wave's 8 rows (one coalesced
   // 1 KB row per instruction) and writes them to a slab at the row's rotation.
-  auto fetch = [&](int r, f32x4(&dst)[MB_KW]) {
-#pragma unroll
-    for (int k = 0; k < MB_KW; ++k) {
-      const int t = min(r * MB_TILE + w * MB_KW + k, T - 1);
-      dst[k] = ld4(mc + (size_t)t * ND_D + 4 * lane);
-    }
-  };
+  auto fetch = [&](int r, f32x4(&dst)[MB_KW]) { mb_fetch(mc, r, w, lane, T, dst); };
   auto put = [&](int r, const f32x4(&src)[MB_KW]) {
     float* dst = slab + (r & 1) * (MB_KW * ND_D);
 #pragma unroll
@@ -123,6 +162,11 @@ __device__ __forceinline__ void mem_chunk(int c, const float* __restrict__ qp, c
     f32x4 s4[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) s4[e] = {0.f, 0.f, 0.f, 0.f};
+#ifdef MB_PROBE_NOSCORE  // timing probe only: no score reads / MFMAs (scores 0)
+    (void)arow;
+    (void)urow;
+    return s4[0];
+#endif
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk) {
       const f32x4 a = ld4(arow + ((64 * dp + 4 * kk + 4 * skey) & (ND_D - 1)));
@@ -134,18 +178,14 @@ __device__ __forceinline__ void mem_chunk(int c, const float* __restrict__ qp, c
   };
   auto put_scores = [&](int r, f32x4 v) { st4(spart + (r & 1) * 256 + (dp * 8 + shead) * 8 + 4 * kg, v); };
 
-  // The source samples of this wave's keys (lane l -> tile l >> 3, key l & 7)
-  // load FIRST: the waits that retire the tile loads below then retire it
-  // too, so no wait for it is left inside the loop (where it would drain
-  // the prefetched tiles every iteration).
-  const float sgv = signal[(size_t)c * T + min((lane >> 3) * MB_TILE + w * MB_KW + (lane & 7), T - 1)];
-  f32x4 R0[MB_KW], R1[MB_KW];
-  if (ntile > 0) fetch(0, R0);
-  if (ntile > 1) fetch(1, R1);
+  // the source samples of this wave's keys (lane l -> tile l >> 3, key l & 7), tiles 0 and 1, q': hd
+  const float sgv = hd.sgv;
+  f32x4(&R0)[MB_KW] = hd.R0;
+  f32x4(&R1)[MB_KW] = hd.R1;
   // q' image (all heads; 512 threads x 16 B)
   {
     const int h = threadIdx.x >> 6, q = threadIdx.x & 63;
-    st4(lds + MB_U + h * ND_D + ((4 * q + 4 * h) & (ND_D - 1)), ld4(qp + pk(c, h * ND_D + 4 * q, ND_H * ND_D)));
+    st4(lds + MB_U + h * ND_D + ((4 * q + 4 * h) & (ND_D - 1)), hd.qv);
   }
   if (ntile > 0) put(0, R0);
   if (ntile > 1) put(1, R1);
@@ -195,6 +235,10 @@ __device__ __forceinline__ void mem_chunk(int c, const float* __restrict__ qp, c
     // ---- U += P^T M over the tile's 8 keys of this wave
     const f32x4 p0 = ld4(pbuf + sh * 8), p1 = ld4(pbuf + sh * 8 + 4);
     const float* tile = slab + (r & 1) * (MB_KW * ND_D);
+#ifdef MB_PROBE_NOU  // timing probe only: no context product (U stays the P sums)
+    acc[0] += p0 + p1;
+    (void)tile;
+#else
 #pragma unroll
     for (int k = 0; k < MB_KW; ++k) {
       const float* row = tile + k * ND_D;
@@ -207,6 +251,7 @@ __device__ __forceinline__ void mem_chunk(int c, const float* __restrict__ qp, c
         acc[4 + e] = mfma4x4(pk_, b1[e], acc[4 + e]);
       }
     }
+#endif
     put_scores(r + 1, snext);
     // the wave's LDS accesses retire in order: tile r + 2 lands after tile r's reads
     if (r + 2 < ntile) put(r + 2, R);
@@ -225,6 +270,13 @@ __device__ __forceinline__ void mem_chunk(int c, const float* __restrict__ qp, c
     }
   }
 
+  // NEXT: the next chunk's head goes out now, into registers dead here (R0 / R1's last tiles are in LDS)
+  // (fenced: hoisted into the tile loop they would raise its register peak past 256 and spill)
+  if constexpr (NEXT) {
+    __builtin_amdgcn_sched_barrier(0);
+    mb_head(nx, qp, mem, signal, T, ldT, NT, hd);
+    __builtin_amdgcn_sched_barrier(0);
+  }
   // ---- merge the waves: head h's slots are combined by wave h
   __syncthreads();  // every wave is done with its slabs
   float* red = lds;               // [NW][512 slots][4]; slot = head * 64 + dim quad
@@ -270,9 +322,31 @@ dec_mem_attention_kernel(const float* __restrict__ qp, const float* __restrict__
                          float* __restrict__ out, int T, int ldT, unsigned long long* stamp,
                          float* __restrict__ dbg, size_t dbg_stride, int C) {
   stamp_begin(stamp);
+  MbHead hd;
+  auto ntile = [&](int c) { return NT > 0 ? NT : (min(span[c], T) + MB_TILE - 1) / MB_TILE; };
+#ifndef MB_NO_PREFETCH  // timing variant only (tools/build_variant.sh): the walking form without the prefetch
+  if (NT > 0 && C <= 2 * (int)gridDim.x) {
+    // at most two chunks per workgroup (the pool's grid): straight-line, the second chunk's head loaded
+    // during the first one's merge (a runtime loop would carry it across the back-edge)
+    // (each case loads its own head: a head loaded before the branch is live into both and spills)
+    const int c = blockIdx.x, nx = c + (int)gridDim.x;
+    if (nx < C) {
+      mb_head(c, qp, mem, signal, T, ldT, ntile(c), hd);
+      mem_chunk<NT, true>(c, hd, nx, qp, mem, signal, span, pad_val, out, T, ldT, dbg, dbg_stride);
+      __syncthreads();  // the first chunk's merge reads of LDS are done
+      mem_chunk<NT, false>(nx, hd, -1, qp, mem, signal, span, pad_val, out, T, ldT, dbg, dbg_stride);
+    } else {
+      mb_head(c, qp, mem, signal, T, ldT, ntile(c), hd);
+      mem_chunk<NT, false>(c, hd, -1, qp, mem, signal, span, pad_val, out, T, ldT, dbg, dbg_stride);
+    }
+    stamp_end(stamp);
+    return;
+  }
+#endif
   for (int c = blockIdx.x; c < C; c += gridDim.x) {
     if (c != (int)blockIdx.x) __syncthreads();  // the previous chunk's merge reads of LDS are done
-    mem_chunk<NT>(c, qp, mem, signal, span, pad_val, out, T, ldT, dbg, dbg_stride);
+    mb_head(c, qp, mem, signal, T, ldT, ntile(c), hd);
+    mem_chunk<NT, false>(c, hd, -1, qp, mem, signal, span, pad_val, out, T, ldT, dbg, dbg_stride);
   }
   stamp_end(stamp);
 }

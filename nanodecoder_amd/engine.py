@@ -663,6 +663,23 @@ def op_gemm_p16_splitk(Ap, Wh, wscale, bias, M, N, K, Rp=None, part_out=None, ti
     return Cp, pn.value, tickets
 
 
+def op_gemm_p16_splitk_f32(Ap, Wp, bias, M, N, K, Rp=None, part_out=None, tickets=None, slab=None):
+    """The same split-K route in exact fp32 (nd_op_gemm_p16_splitk_f32): Wp the fp32 weight [N, K] P16-packed
+    (pack_p16); returns (C packed [M16, N], output row partials per row, tickets)."""
+    tiles = ((M + 31) // 32) * (N // 32)
+    Cp = torch.empty((M + 15) // 16 * 16, N, dtype=torch.float32, device=Ap.device)
+    if tickets is None:
+        tickets = torch.zeros(tiles, dtype=torch.int32, device=Ap.device)
+    if slab is None:
+        slab = torch.empty(tiles * 4096, dtype=torch.float32, device=Ap.device)
+    pn = ctypes.c_int32(0)
+    s = ctypes.c_void_p(torch.cuda.current_stream(Ap.device).cuda_stream)
+    _lib.check(_lib.lib().nd_op_gemm_p16_splitk_f32(_ptr(Ap), _ptr(Wp), _ptr(bias), _ptr(Rp), _ptr(Cp), M, N, K,
+                                                    _ptr(part_out), _ptr(slab), _ptr(tickets), tiles,
+                                                    ctypes.byref(pn), s), "nd_op_gemm_p16_splitk_f32")
+    return Cp, pn.value, tickets
+
+
 def op_dec_self_attention(qkv, cache, step, anc=None, anc_ld=0, packed=False):
     """qkv [R, 768] row-major (or P16-packed with packed=True); returns out
     [R, 256] in the same convention."""

@@ -248,8 +248,11 @@ REVIEWED_PAIRED = {
                                "five in the walking non-temporal form (round 6: the two-chunk straight-line path "
                                "per load policy plus the general loop); pool-tested at the bench's configuration "
                                "(profiles/r06_gpu4.log)"),
-    "dec_mem_attention_kernel": (25, "the fp32 bank kernel (exact fp32 / short chunks): slab reads after "
-                                     "barriers"),
+    "dec_mem_attention_kernel": (92, "the fp32 bank kernel (exact fp32 / short chunks): slab reads after "
+                                     "barriers, 23-25 per chunk body; the 512-key form holds four bodies (round 6: "
+                                     "the walking form's two-chunk straight-line path, its one-chunk case, the "
+                                     "general loop); pool-tested bitwise in exact fp32 at the bench's "
+                                     "configuration (test_pool_at_bench_config_matches_single_engine)"),
 }
 
 

@@ -217,7 +217,7 @@ def _ragged(sig, seed):
     return sig, lens, spans
 
 
-@pytest.mark.parametrize("key", ["configs[1]", "configs[2]", "configs[3]"])
+@pytest.mark.parametrize("key", ["configs[1]", "configs[2]", "configs[3]", "configs[1] exact"])
 def test_pool_at_bench_config_matches_single_engine(key):
     """The bench's headline mode exactly (bench.py run_batch / config_legs):
     EnginePool with 3 lanes, the memory-bank kernel on half the CUs (the
@@ -228,12 +228,18 @@ def test_pool_at_bench_config_matches_single_engine(key):
     spans < T) go through the pool twice, three calls in flight (greedy:
     one host thread; beam: one thread per lane, as the bench); every pooled
     call equals a single engine's bitwise.  The single engine is pinned to
-    the oracle at these sizes by the two tests above."""
+    the oracle at these sizes by the two tests above.  "configs[1] exact":
+    the bench's exact_fp32 leg (nd_set_exact_fp32 on every lane: the fp32
+    bank kernel walking two chunks per workgroup with the second chunk's
+    head prefetched, the fp32 split-K products), against a single exact
+    engine (tests/test_gpu_precision.py pins that one to the oracle)."""
     import threading
     import torch
     from nanodecoder_amd.engine import EnginePool
     enc, mode, B = {"configs[1]": ("transformer", "greedy", 256), "configs[2]": ("nano", "greedy", 256),
-                    "configs[3]": ("transformer", "beam", 1024)}[key]
+                    "configs[3]": ("transformer", "beam", 1024),
+                    "configs[1] exact": ("transformer", "greedy", 256)}[key]
+    exact = key.endswith("exact")
     cfg = synth.ModelConfig(encoder_type=enc)
     W = synth.make_weights(cfg, seed=11, eos_bias=-3.0)
     S, MINL, beam, lanes = 100, 57, (5 if mode == "beam" else 1), 3
@@ -253,9 +259,11 @@ def test_pool_at_bench_config_matches_single_engine(key):
         return e.translate_beam(sig, ln, sp, beam=beam, n_best=1, max_len=S, min_len=MINL)
     one = _engine(cfg, W, max_batch=B, max_steps=S, max_beam=beam)
     one.set_gemm_splitk(True)  # the pool lanes' K = 2048 product form (its own test: the config tests above)
+    one.set_exact_fp32(exact)
     exp = [{k: v.cpu() for k, v in call(one, i).items() if k in keys} for i in inputs]
     one.close()
     pool = EnginePool(cfg, W, device=0, lanes=lanes, max_batch=B, max_steps=S, max_beam=beam)
+    pool.set_exact_fp32(exact)
     assert pool.splitk
     assert pool.bank_nt_lanes == (0, 1, 2)
     assert pool.bank_grid == torch.cuda.get_device_properties(0).multi_processor_count // 2

@@ -239,6 +239,38 @@ def test_gemm_p16_splitk_vs_fp64(M, N, K, res):
     assert torch.allclose(got[:, :, 1], want[:, :, 1], rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("M,N,K,res", [(256, 256, 2048, True), (400, 256, 1024, False)])
+def test_gemm_p16_splitk_f32_vs_fp64(M, N, K, res):
+    """The split-K route in exact fp32 (the pool lanes' W_vo / FFN2 under
+    nd_set_exact_fp32): fp32 products against fp64 within fp32 rounding of a
+    K-term sum, row partials, tickets reset, repeat launches bitwise equal."""
+    from nanodecoder_amd.engine import op_gemm_p16_splitk_f32, pack_p16, row_partials, unpack_p16
+    g = torch.Generator().manual_seed(5 * M + K)
+    A = torch.randn(M, K, generator=g)
+    W = torch.randn(N, K, generator=g) / K ** 0.5
+    b = torch.randn(N, generator=g)
+    R = torch.randn(M, N, generator=g)
+    dev = torch.device("cuda", 0)
+    Wp = pack_p16(W.to(dev))
+    Ap = pack_p16(torch.cat([A, A.new_zeros((-M) % 16, K)]).to(dev))
+    Rp = pack_p16(torch.cat([R, R.new_zeros((-M) % 16, N)]).to(dev)) if res else None
+    part_out = torch.full(((M + 15) // 16 * 16, 16, 2), float("nan"), device=dev)
+    outs, tk = [], None
+    for _ in range(3):
+        Cp, pn, tk = op_gemm_p16_splitk_f32(Ap, Wp, b.to(dev), M, N, K, Rp, part_out, tickets=tk)
+        torch.cuda.synchronize()
+        assert int(tk.abs().sum().item()) == 0
+        outs.append(unpack_p16(Cp, M).cpu())
+    assert all(torch.equal(outs[0], o) for o in outs[1:])
+    ref = A.double() @ W.double().t() + b.double() + (R.double() if res else 0)
+    assert (outs[0].double() - ref).abs().max().item() < 2e-5
+    assert pn == N // 16
+    want = row_partials(outs[0], pn)[:, :pn]
+    got = part_out[:M, :pn].cpu()
+    assert torch.allclose(got[:, :, 0], want[:, :, 0], atol=1e-5)
+    assert torch.allclose(got[:, :, 1], want[:, :, 1], rtol=1e-4, atol=1e-4)
+
+
 @pytest.mark.parametrize("M,N,K,ln,relu,res,stats", [(256, 768, 256, True, False, False, False),
                                                       (256, 256, 256, False, False, True, True),
                                                       (256, 256, 256, True, False, False, False),

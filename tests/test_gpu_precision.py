@@ -32,11 +32,12 @@ pytestmark = pytest.mark.gpu
 OUTLIER = 1e3
 
 
-def _greedy_vs_oracle(cfg, W, sig, lens, S, MINL, exact, max_ties=3):
+def _greedy_vs_oracle(cfg, W, sig, lens, S, MINL, exact, max_ties=3, splitk=False):
     ref = _oracle()
     B = sig.shape[0]
     eng = _engine(cfg, W, max_batch=B, max_steps=S)
     eng.set_exact_fp32(exact)
+    eng.set_gemm_splitk(splitk)
     _routes()
     r = eng.translate_greedy(sig, lens, lens, max_len=S, min_len=MINL, return_logp=True)
     routes = _routes()
@@ -91,18 +92,21 @@ def _beam_sampled_vs_oracle(cfg, W, sig, lens, S, MINL, exact, pick_n, beam=5):
 
 
 # ------------------------------------------------------------ 1. exact fp32
-@pytest.mark.parametrize("encoder", ["transformer", "nano"])
-def test_exact_fp32_config1_batch256_vs_oracle(encoder):
+@pytest.mark.parametrize("encoder,splitk", [("transformer", False), ("transformer", True), ("nano", False)])
+def test_exact_fp32_config1_batch256_vs_oracle(encoder, splitk):
     """configs[1] / configs[2] in exact fp32: 256 chunks x 512 samples, greedy,
     max_length 100, -min_length 57, mask samples injected (src==0 keys,
     src==1 context keys), every chunk against the oracle.  The fp32-MFMA
-    tile kernels ran and no split-fp16 product; the fp32 memory bank."""
+    tile kernels ran and no split-fp16 product; the fp32 memory bank.
+    splitk: the pool lanes' form (the K = 2048 products split over
+    workgroups, in fp32: nd_op_gemm_p16_splitk_f32)."""
     cfg = synth.ModelConfig(encoder_type=encoder)
     W = synth.make_weights(cfg, seed=11, eos_bias=-3.0)
     B = 256
     sig = synth.synth_chunk_batch(B, 512, seed=1000, inject_masks=True)
-    routes, form = _greedy_vs_oracle(cfg, W, sig, np.full(B, 512, np.int32), 100, 57, exact=True)
+    routes, form = _greedy_vs_oracle(cfg, W, sig, np.full(B, 512, np.int32), 100, 57, exact=True, splitk=splitk)
     assert form == 0
+    assert (routes["p16_splitk"] > 0) == splitk, routes
     # the encoder's products on the fp32-MFMA tile kernels (the decoder step's P16-layout kernels take the
     # fp32 weights in this mode: no split image is attached, gemm.hip)
     assert routes["tile256"] + routes["tile128"] + routes["tile64"] > 0, routes
