@@ -52,7 +52,7 @@ typedef struct nd_config {
   int32_t pad_idx, bos_idx, eos_idx;
   int32_t max_batch;          /* chunks per call */
   int32_t max_src_len;        /* 512 (src_seq_length) */
-  int32_t max_steps;          /* max_length (100) */
+  int32_t max_steps;          /* max_length (100), at most 512 */
   int32_t max_beam;           /* beam_size upper bound (1 = greedy only) */
   int32_t device;             /* HIP device ordinal */
   int32_t self_attn_type;     /* decoder self-attention: ND_SELF_SCALED_DOT | ND_SELF_AVERAGE

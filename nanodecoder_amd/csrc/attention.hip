@@ -868,7 +868,7 @@ __device__ __forceinline__ void merge_waves_part(float* accs, float* ms, float* 
 // w*KW .. w*KW+KW-1 and issues every one of their loads before the first
 // score (one memory round trip per step; a loop over key blocks would pay
 // one per block), then the NW partial states merge through LDS.
-#define SELF_MAXS 256
+#define SELF_MAXS 512  // max_steps bound (nd_create); the beam rows' kernel holds two lane-indexed slot tables
 #define SELF_TABV 8  // vocabulary bound of the head-fused form (its candidate table rows sit in LDS)
 // HEAD (greedy, layer 0 in table mode, step > 0): wave 0 first runs the
 // previous step's greedy head for the row (head.hpp), whose token picks the
@@ -1128,16 +1128,19 @@ dec_self_attention_beam_kernel(const float* __restrict__ qkv, float* __restrict_
     m[j] = -INFINITY;
     l[j] = 0.f;
   }
-  // this wave's keys t = wu + NW i (i = lane): every row's slot for them (t == step: its own slot)
-  int sl[RPC];
+  // this wave's keys t = wu + NW i: every row's slot for them (t == step: its own slot), key i in lane i & 63
+  // of sl (i < 64) or sl2 (64 <= i < 128: steps past NW * 64, SELF_MAXS)
+  int sl[RPC], sl2[RPC];
   {
-    const int t = wu + NW * lane;
+    const int t = wu + NW * lane, t2 = t + NW * 64;
 #pragma unroll
     for (int j = 0; j < RPC; ++j) {
       const int r = c * RPC + j;
       sl[j] = t < step ? anc[(size_t)r * anc_ld + t] : r;
+      sl2[j] = t2 < step ? anc[(size_t)r * anc_ld + t2] : r;
     }
   }
+  static_assert(SELF_MAXS <= NW * 128, "two slot tables of 64 keys per wave");
   // the appends are visible to every wave of the workgroup: each storing wave's stores retired, then a barrier
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -1153,7 +1156,7 @@ dec_self_attention_beam_kernel(const float* __restrict__ qkv, float* __restrict_
     const int t = min(wu + NW * i, n - 1);  // wave-uniform; clamped (straight-line loads)
 #pragma unroll
     for (int j = 0; j < RPC; ++j) {
-      const size_t at = (size_t)__builtin_amdgcn_readlane(sl[j], min(i, 63)) * S + t;
+      const size_t at = (size_t)__builtin_amdgcn_readlane(i < 64 ? sl[j] : sl2[j], i & 63) * S + t;
       if constexpr (Q24) {
         const uint8_t* rb = reinterpret_cast<const uint8_t*>(cache) + at * SELF_Q24_ROW;
         kk[j].kq = *reinterpret_cast<const u32v3*>(rb + 12 * lane);

@@ -1143,7 +1143,7 @@ int nd_create(const nd_config* cfg, nd_ctx** out) {
   if (cfg->d_ff <= 0 || cfg->d_ff % 128) return fail(ND_ERR_ARG, "d_ff must be a positive multiple of 128");
   if (cfg->vocab < 4 || cfg->vocab > ND_MAXV) return fail(ND_ERR_ARG, "vocab must be in [4, 32]");
   if (cfg->max_src_len < 1 || cfg->max_src_len > 512) return fail(ND_ERR_ARG, "max_src_len must be in [1, 512]");
-  if (cfg->max_steps < 1 || cfg->max_steps > 256) return fail(ND_ERR_ARG, "max_steps must be in [1, 256]");
+  if (cfg->max_steps < 1 || cfg->max_steps > 512) return fail(ND_ERR_ARG, "max_steps must be in [1, 512]");
   if (cfg->max_beam < 1 || cfg->max_beam > 6) return fail(ND_ERR_ARG, "max_beam must be in [1, 6]");
   if (cfg->max_batch < 1) return fail(ND_ERR_ARG, "max_batch must be >= 1");
   if (cfg->enc_layers < 1 || cfg->dec_layers < 1) return fail(ND_ERR_ARG, "layers must be >= 1");

@@ -143,6 +143,47 @@ def test_beam_config3_batch1024_sampled_vs_oracle():
         assert abs(sc[i, 0] - s) < LOGP_ATOL, (i, sc[i, 0], s)
 
 
+@pytest.mark.parametrize("mode", ["greedy", "beam"])
+def test_long_max_length_vs_oracle(mode):
+    """max_length 400 (up to 512 supported; the reference takes any,
+    models/opts.py:577): -min_length 380 keeps every hypothesis decoding past
+    step 256, so the self-attention histories run three and four key passes
+    and the beam rows' chunk kernel its second slot table.  Greedy: 16 chunks,
+    every one against the oracle; --fast beam 5: 4 chunks (20 rows, the
+    chunk-per-workgroup self-attention over the 24-bit history)."""
+    ref = _oracle()
+    cfg = synth.ModelConfig()
+    W = synth.make_weights(cfg, seed=11, eos_bias=-3.0)
+    S, MINL = 400, 380
+    B = 16 if mode == "greedy" else 4
+    sig = synth.synth_chunk_batch(B, 512, seed=3000, inject_masks=True)
+    lens = np.full(B, 512, np.int32)
+    if mode == "greedy":
+        eng = _engine(cfg, W, max_batch=B, max_steps=S)
+        r = eng.translate_greedy(sig, lens, lens, max_len=S, min_len=MINL, return_logp=True)
+        assert int(r["overflow"].cpu()[0]) == 0
+        tok, lp = r["tokens"].cpu().numpy(), r["logp"].cpu().numpy()
+        o = ref.greedy(ref.RefModel(cfg, W), sig, lens, max_length=S, min_length=MINL)
+        ties = _tie_rows(tok, o["tokens"], o["logp"])
+        assert len(ties) <= 1, ties
+        keep = np.array([b not in ties for b in range(B)])
+        assert gu.logp_close(lp[keep], o["logp"][keep], atol=LOGP_ATOL).all()
+        assert np.abs(r["scores"].cpu().numpy()[keep] - o["scores"][keep]).max() < LOGP_ATOL
+    else:
+        eng = _engine(cfg, W, max_batch=B, max_steps=S, max_beam=5)
+        r = eng.translate_beam(sig, lens, lens, beam=5, n_best=1, max_len=S, min_len=MINL)
+        assert int(r["overflow"].cpu()[0]) == 0
+        assert int(r["steps"].cpu()[0]) > 300
+        tok, sc, ln = (r[k].cpu().numpy() for k in ("tokens", "scores", "lens"))
+        exp = ref.fast_beam(ref.RefModel(cfg, W), sig, lens, beam_size=5, n_best=1, max_length=S, min_length=MINL)
+        for i in range(B):
+            s, p = exp[i][0]
+            assert ln[i, 0] == len(p), (i, ln[i, 0], len(p))
+            assert (tok[i, 0, : len(p)] == p).all(), i
+            assert abs(sc[i, 0] - s) < LOGP_ATOL, (i, sc[i, 0], s)
+    eng.close()
+
+
 @pytest.mark.parametrize("encoder,mode", [("transformer", "greedy"), ("nano", "greedy"), ("transformer", "beam")])
 def test_pool_matches_single_engine(encoder, mode):
     """EnginePool (two calls in flight, one engine context and hardware

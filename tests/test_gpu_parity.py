@@ -373,15 +373,16 @@ def test_gemm_split_small_rows_follow_the_scheme(lg, M, K):
         assert (C1 - (ref + R.double())).abs().max().item() < 2.0 ** -23 + 2.0 ** -24 * l1 * (K / 256) ** 0.5
 
 
-@pytest.mark.parametrize("step", [0, 1, 31, 32, 63, 64, 99, 127, 128, 200])
+@pytest.mark.parametrize("step", [0, 1, 31, 32, 63, 64, 99, 127, 128, 200, 300, 511])
 @pytest.mark.parametrize("beam", [False, True])
 def test_dec_self_attention_vs_fp64(step, beam):
     """Decoder self-attention step (multi_headed_attn.py:124-141 + :167-179):
     keys 0..step-1 from the cache through the ancestry table (beam) or the
     row's own slot, key `step` from this step's k/v, which is also appended
-    to the row's slot."""
+    to the row's slot.  Steps past 256 on a 512-step cache (max_length up to
+    512: three and four key passes)."""
     from nanodecoder_amd.engine import op_dec_self_attention
-    R, S = 37, 256
+    R, S = 37, (256 if step < 256 else 512)
     g = torch.Generator().manual_seed(step + 1000 * beam)
     qkv = torch.randn(R, 768, generator=g)
     cache = torch.randn(R, S, 512, generator=g)
@@ -404,16 +405,18 @@ def test_dec_self_attention_vs_fp64(step, beam):
     assert torch.equal(appended, qkv[:, 256:])
 
 
-@pytest.mark.parametrize("rpc,step", [(5, 0), (5, 1), (5, 47), (2, 130), (6, 63), (3, 255)])
+@pytest.mark.parametrize("rpc,step", [(5, 0), (5, 1), (5, 47), (2, 130), (6, 63), (3, 255), (5, 256), (5, 300),
+                                      (6, 511)])
 def test_dec_self_attention_beam_vs_fp64(rpc, step):
     """Beam rows' self-attention on the chunk-per-workgroup kernel: the rows of
     a chunk share most of their history (slots from the chunk's rows, with
     divergent tails), keys 0..step-1 through each row's ancestry, key `step`
     from this step's k/v, appended to the row's own slot; rows of a finished
     chunk untouched (multi_headed_attn.py:124-141, translate/translator.py:
-    793-823).  Tolerance as the per-row form's test (1e-5)."""
+    793-823).  Tolerance as the per-row form's test (1e-5).  Steps from 256
+    on a 512-step cache: the keys past 64 per wave take the second slot table."""
     from nanodecoder_amd.engine import op_dec_self_attention_beam
-    C, S = 7, 256
+    C, S = 7, (256 if step < 256 else 512)
     R = C * rpc
     g = torch.Generator().manual_seed(step + 100 * rpc)
     qkv = torch.randn(R, 768, generator=g)

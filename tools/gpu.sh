@@ -52,6 +52,16 @@ case $step in
     python3 $R/tools/trace_steps.py $O/$tag/run_kernel_trace.csv > $O/${tag}_steps.txt
     find $O/$tag -name '*.csv' ! -name '*kernel_stats.csv' -delete
     head -20 $O/${tag}_steps.txt; exit 0 ;;
+  busy)
+    # kernel trace of a bench run: how busy the GPU is, window by window (tools/trace_busy.py)
+    tag=$1; shift
+    cd /tmp && export TMPDIR=/tmp
+    timeout -k 10 600 rocprofv3 --kernel-trace -d $O/$tag -o run --output-format csv -- \
+      python3 $R/bench.py $SHORT "$@" > $O/$tag.log 2>&1
+    rc=$?; echo "busy $tag rc=$rc"; [ $rc -ne 0 ] && exit $rc
+    python3 $R/tools/trace_busy.py $(find $O/$tag -name '*kernel_trace.csv' | head -1) 5 > $O/${tag}_busy.txt
+    find $O/$tag -name '*.csv' -delete
+    tail -20 $O/${tag}_busy.txt; exit 0 ;;
   pmc)
     tag=$1; ctrs=$2; shift 2
     cd /tmp && export TMPDIR=/tmp
