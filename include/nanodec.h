@@ -507,7 +507,7 @@ int nd_op_memory_pack(const float* x, const float* ln_g, const float* ln_b, floa
                       int32_t ldT, void* stream);
 
 /* 24-bit fixed-point memory bank (the greedy decoder's context attention at
- * T in (448, 512]; multi_headed_attn.py:142-177 in the memory-bank form of
+ * every chunk length T <= 512; multi_headed_attn.py:142-177 in the memory-bank form of
  * nd_op_dec_mem_attention).  nd_op_bank_pack_d8: x [B*T, 256] row-major -> the
  * digit bank (B x 512 rows; every row t as s_t times an integer of at most
  * 126 * 2^16 in magnitude in three signed 8-bit digit planes, B * 512 * 256 *
@@ -517,7 +517,8 @@ int nd_op_memory_pack(const float* x, const float* ln_g, const float* ln_b, floa
  * span (nullable, [B]) is given, zero with scale 0 (the engine passes the
  * call's spans: rows past a chunk's span are never attended and must not set
  * its largest scale).  nd_op_dec_bank_d8: qp [C, 2048] ROW-MAJOR (one row
- * per chunk), T in (448, 512]; out U [C16, 2048] P16.  grid: workgroups at
+ * per chunk), T in [1, 512] (the first ceil(T / 128) key blocks of each wave
+ * streamed); out U [C16, 2048] P16.  grid: workgroups at
  * most (0 = one per chunk; fewer walk the chunks, as nd_set_bank_grid).  ovf
  * (nullable): set to 1 on a non-finite operand. */
 int nd_op_bank_pack_d8(const float* x, const float* ln_g, const float* ln_b, void* bank, float* kscale,

@@ -142,7 +142,7 @@ __device__ __forceinline__ d8u2 tr_b8(const char* p) {
 // WALK: the next chunk's head is loaded before this chunk's merge (its latency hides behind the merge).
 struct B8Head {
   f32x4 qv;
-  f32x4 ksc[B8_KPW];
+  f32x4 ksc[B8_KPW];  // the first KPW used
   float sg, smax;
   i32x4 F[3][6];
 };
@@ -167,7 +167,8 @@ __device__ __forceinline__ void b8_hload(const i32x4* __restrict__ bank, int c, 
   }
 }
 
-template <bool NT, bool BOTH>  // BOTH: the first two half blocks (else the first only: the WALK prefetch)
+// KPW: the key blocks per wave this launch processes (T <= 128 KPW; bank8_kpw)
+template <bool NT, bool BOTH, int KPW>  // BOTH: the first two half blocks (else the first only: the WALK prefetch)
 __device__ __forceinline__ void b8_head(int c, const float* __restrict__ qp, const i32x4* __restrict__ bank,
                                         const float* __restrict__ kscale, const int* __restrict__ kemax,
                                         const float* __restrict__ signal, int T, B8Head& hd) {
@@ -176,7 +177,7 @@ __device__ __forceinline__ void b8_head(int c, const float* __restrict__ qp, con
   const int g = lane >> 4;
   hd.qv = ld4(qp + (size_t)c * (ND_H * ND_D) + w * ND_D + 4 * lane);
 #pragma unroll
-  for (int kb = 0; kb < B8_KPW; ++kb) hd.ksc[kb] = ld4(kscale + (size_t)c * 512 + 16 * (w + B8_NW * kb) + 4 * g);
+  for (int kb = 0; kb < KPW; ++kb) hd.ksc[kb] = ld4(kscale + (size_t)c * 512 + 16 * (w + B8_NW * kb) + 4 * g);
   {
     const int bkey = 16 * (w + B8_NW * (lane >> 4)) + (lane & 15);  // lane l: row l & 15 of key block w + 8 (l >> 4)
     hd.sg = signal[(size_t)c * T + min(bkey, T - 1)];
@@ -195,7 +196,7 @@ __device__ __forceinline__ void b8_head(int c, const float* __restrict__ qp, con
 
 // chunk c from its loaded head (need1: its second half block still to load); nx >= 0: the next chunk this
 // workgroup walks to, whose head (first half block) goes into hd before the merge
-template <bool NT, bool NXNT>  // this chunk's and the next chunk's load policy
+template <bool NT, bool NXNT, int KPW>  // this chunk's and the next chunk's load policy; key blocks per wave
 __device__ __forceinline__ void bank_d8_chunk(int c, B8Head& hd, bool need1, int nx,
                                               const float* __restrict__ qp, const i32x4* __restrict__ bank,
                                               const float* __restrict__ kscale, const int* __restrict__ kemax,
@@ -273,7 +274,7 @@ __device__ __forceinline__ void bank_d8_chunk(int c, B8Head& hd, bool need1, int
   float m = -INFINITY, l = 0.f;
 
 #pragma unroll
-  for (int kb = 0; kb < B8_KPW; ++kb) {
+  for (int kb = 0; kb < KPW; ++kb) {
     i32x4 X1 = {0, 0, 0, 0}, X2 = X1, X3 = X1, X4 = X1;
 #pragma unroll
     for (int part = 0; part < 2; ++part) {
@@ -298,7 +299,7 @@ __device__ __forceinline__ void bank_d8_chunk(int c, B8Head& hd, bool need1, int
         *reinterpret_cast<i32x4*>(wimg + pl * B8_PLANE + 64 * db) = f[i];
       }
       __builtin_amdgcn_sched_barrier(0);  // the next loads reuse f's registers
-      if (h + 2 < 2 * B8_KPW) b8_hload<NT>(bank, c, h + 2, w, lane, F[(h + 2) % 3]);
+      if (h + 2 < 2 * KPW) b8_hload<NT>(bank, c, h + 2, w, lane, F[(h + 2) % 3]);
     }
     // ---- scores: columns h and h + 8 hold the high and low digit products of head h
     f32x4 s;
@@ -380,7 +381,7 @@ __device__ __forceinline__ void bank_d8_chunk(int c, B8Head& hd, bool need1, int
   }
   // WALK: the next chunk's head (q', scales, its first half blocks) goes out now, into registers that are
   // all dead here (U sits in LDS); its latency hides behind the rest of this chunk's merge
-  if (nx >= 0) b8_head<NXNT, false>(nx, qp, bank, kscale, kemax, signal, T, hd);
+  if (nx >= 0) b8_head<NXNT, false, KPW>(nx, qp, bank, kscale, kemax, signal, T, hd);
   if (lane < 8) {
     ml[(w * ND_H + lane) * 2] = m;
     ml[(w * ND_H + lane) * 2 + 1] = l;
@@ -423,7 +424,8 @@ __device__ __forceinline__ void bank_d8_chunk(int c, B8Head& hd, bool need1, int
   B8_PHASE(7);
 }
 
-template <bool NT, bool WALK>
+// KPW < 4 (T <= 384): the key blocks past 128 KPW keys (zero rows of the pack, keys >= T) are not streamed
+template <bool NT, bool WALK, int KPW>
 __global__ void __launch_bounds__(B8_NW * 64)
 dec_bank_d8_kernel(const float* __restrict__ qp, const i32x4* __restrict__ bank, const float* __restrict__ kscale,
                    const int* __restrict__ kemax, const float* __restrict__ signal, const int* __restrict__ span,
@@ -439,7 +441,7 @@ dec_bank_d8_kernel(const float* __restrict__ qp, const i32x4* __restrict__ bank,
   // every load policy is a template argument (a branch around loads drains them), so each policy pair is its
   // own copy of the chunk body
 #define B8_CHUNK(A, B, c_, need1_, nx_)                                                                            \
-  bank_d8_chunk<A, B>(c_, hd, need1_, nx_, qp, bank, kscale, kemax, signal, span, pad_val, out, T, stamp, dbg,      \
+  bank_d8_chunk<A, B, KPW>(c_, hd, need1_, nx_, qp, bank, kscale, kemax, signal, span, pad_val, out, T, stamp, dbg,      \
                       dbg_stride, ovf, t_entry, C)
   B8Head hd;
   if constexpr (WALK) {
@@ -453,10 +455,10 @@ dec_bank_d8_kernel(const float* __restrict__ qp, const i32x4* __restrict__ bank,
       // chunk c + G >= G > C / 4 = cached is always past the cached quarter: non-temporal when NT is
       const int nx = c + G < C ? c + G : -1;
       if (!NT || !ntc(c)) {
-        b8_head<false, true>(c, qp, bank, kscale, kemax, signal, T, hd);
+        b8_head<false, true, KPW>(c, qp, bank, kscale, kemax, signal, T, hd);
         B8_CHUNK(false, NT, c, false, nx);
       } else {
-        b8_head<NT, true>(c, qp, bank, kscale, kemax, signal, T, hd);
+        b8_head<NT, true, KPW>(c, qp, bank, kscale, kemax, signal, T, hd);
         B8_CHUNK(NT, NT, c, false, nx);
       }
       if (nx >= 0) {
@@ -467,10 +469,10 @@ dec_bank_d8_kernel(const float* __restrict__ qp, const i32x4* __restrict__ bank,
       for (; c < C; c += G) {
         if (c != (int)blockIdx.x) lds_barrier();  // the previous chunk's merge reads of LDS are done
         if (ntc(c)) {
-          b8_head<NT, true>(c, qp, bank, kscale, kemax, signal, T, hd);
+          b8_head<NT, true, KPW>(c, qp, bank, kscale, kemax, signal, T, hd);
           B8_CHUNK(NT, false, c, false, -1);
         } else {
-          b8_head<false, true>(c, qp, bank, kscale, kemax, signal, T, hd);
+          b8_head<false, true, KPW>(c, qp, bank, kscale, kemax, signal, T, hd);
           B8_CHUNK(false, false, c, false, -1);
         }
       }
@@ -478,10 +480,10 @@ dec_bank_d8_kernel(const float* __restrict__ qp, const i32x4* __restrict__ bank,
   } else {
     const int c = blockIdx.x;
     if (ntc(c)) {
-      b8_head<NT, true>(c, qp, bank, kscale, kemax, signal, T, hd);
+      b8_head<NT, true, KPW>(c, qp, bank, kscale, kemax, signal, T, hd);
       B8_CHUNK(NT, false, c, false, -1);
     } else {
-      b8_head<false, true>(c, qp, bank, kscale, kemax, signal, T, hd);
+      b8_head<false, true, KPW>(c, qp, bank, kscale, kemax, signal, T, hd);
       B8_CHUNK(false, false, c, false, -1);
     }
   }
@@ -565,33 +567,53 @@ hipError_t launch_bank_pack_d8(const float* x, const float* ln_g, const float* l
 // 15.55 ms against a quarter's 15.48 / 15.53, same box)
 static int bank_cached(int C) { return C / 4; }
 
+// key blocks per wave a launch processes: 8 waves x 16 keys per block, so T <= 128 KPW (the pack leaves the
+// rows past T zero with scale 0, and they are masked: the blocks past them need not be streamed)
+static int bank8_kpw(int T) { return std::min(B8_KPW, (T + 127) / 128); }
+
 hipError_t launch_dec_bank_d8(const float* qp, const void* bank, const float* kscale, const int* kemax,
                               const float* signal, const int* span, float pad_val, float* out, int C, int T,
                               hipStream_t s, unsigned long long* stamp, float* attn_dbg, size_t dbg_stride, int* ovf,
                               bool nt, int grid) {
   if (T < 1 || T > 512 || C < 1 || grid < 0 || !bank || !kscale || !kemax) return hipErrorInvalidValue;
   const int G = grid > 0 ? std::min(C, grid) : C;
-#define ND_BANK8_GO(N, W)                                                                                         \
-  hipLaunchKernelGGL((dec_bank_d8_kernel<N, W>), dim3(G), dim3(B8_NW * 64), B8_LDS, s, qp,                       \
+  const int kpw = bank8_kpw(T);
+#define ND_BANK8_GO(N, W, K)                                                                                      \
+  hipLaunchKernelGGL((dec_bank_d8_kernel<N, W, K>), dim3(G), dim3(B8_NW * 64), B8_LDS, s, qp,                    \
                      reinterpret_cast<const i32x4*>(bank), kscale, kemax, signal, span, pad_val, out, T, C, stamp,  \
                      attn_dbg, dbg_stride, ovf, bank_cached(C))
+#define ND_BANK8_K(N, W)         \
+  do {                           \
+    if (kpw == 4)                \
+      ND_BANK8_GO(N, W, 4);      \
+    else if (kpw == 3)           \
+      ND_BANK8_GO(N, W, 3);      \
+    else if (kpw == 2)           \
+      ND_BANK8_GO(N, W, 2);      \
+    else                         \
+      ND_BANK8_GO(N, W, 1);      \
+  } while (0)
   if (G < C) {
     if (nt)
-      ND_BANK8_GO(true, true);
+      ND_BANK8_K(true, true);
     else
-      ND_BANK8_GO(false, true);
+      ND_BANK8_K(false, true);
   } else if (nt) {
-    ND_BANK8_GO(true, false);
+    ND_BANK8_K(true, false);
   } else {
-    ND_BANK8_GO(false, false);
+    ND_BANK8_K(false, false);
   }
+#undef ND_BANK8_K
 #undef ND_BANK8_GO
   return hipGetLastError();
 }
 
 hipError_t init_bank8_attributes() {
-  const void* fns[] = {(const void*)dec_bank_d8_kernel<false, false>, (const void*)dec_bank_d8_kernel<true, false>,
-                       (const void*)dec_bank_d8_kernel<false, true>, (const void*)dec_bank_d8_kernel<true, true>};
+#define ND_BANK8_FNS(K)                                                                                           \
+  (const void*)dec_bank_d8_kernel<false, false, K>, (const void*)dec_bank_d8_kernel<true, false, K>,              \
+      (const void*)dec_bank_d8_kernel<false, true, K>, (const void*)dec_bank_d8_kernel<true, true, K>
+  const void* fns[] = {ND_BANK8_FNS(4), ND_BANK8_FNS(3), ND_BANK8_FNS(2), ND_BANK8_FNS(1)};
+#undef ND_BANK8_FNS
   for (const void* f : fns) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, B8_LDS);
     if (e != hipSuccess) return e;

@@ -468,7 +468,8 @@ static int alloc_workspaces(nd_ctx* c) {
     if ((e = hipMemset(c->sk_cnt, 0, (size_t)(tiles + 3) / 4 * 16)) != hipSuccess)
       return fail(ND_ERR_HIP, std::string("hipMemset split-K tickets: ") + hipGetErrorString(e));
   }
-  WS(c->mem_p, B * T * D);
+  // the fp32 bank [B * T, 256], or the digit bank: 512 rows per chunk whatever T is (B * 512 * 256 * 3 bytes)
+  WS(c->mem_p, std::max(B * T * D, B * 512 * ND_D * 3 / 4));
   WS(c->bank_ks, B * 512);
   {
     float* em = nullptr;

@@ -276,7 +276,7 @@ hipError_t launch_attn_rows_softmax(float* a, const int* span, int B, int S, int
 hipError_t launch_stamp_reset(unsigned long long* stamps, int pairs, hipStream_t s);
 // encoder output rows x[b*T+t] -> memory bank rows b*ldT+t, row-major (LN when
 // ln_g; rows t >= T of each chunk zero)
-// the 24-bit digit bank serves T in (448, 512] with bank buffers of >= 512 rows per chunk
+// the 24-bit digit bank serves T in [1, 512] (the context's bank buffer holds 512 rows per chunk)
 bool bank_eligible(int T, int ldT);
 hipError_t launch_memory_pack(const float* x, const float* ln_g, const float* ln_b, float* out, int B, int T, int ldT,
                               hipStream_t s);

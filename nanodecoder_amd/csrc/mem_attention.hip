@@ -351,10 +351,16 @@ dec_mem_attention_kernel(const float* __restrict__ qp, const float* __restrict__
   stamp_end(stamp);
 }
 
-// The 24-bit digit bank (bank8.hip) serves 512-sample chunks (T in (448, 512]
-// with 512-row bank buffers: every bench and translate batch); the fp32 kernel
-// above serves exact fp32 and shorter chunks.
-bool bank_eligible(int T, int ldT) { return T > 448 && T <= 512 && ldT >= 512; }
+// The 24-bit digit bank (bank8.hip) serves every chunk length up to 512 (its
+// buffer holds 512 rows per chunk whatever max_src_len is, alloc_workspaces;
+// below 385 samples it streams ceil(T / 128) key blocks per wave): faster than
+// this fp32 kernel at every T (profiles/r06_bank_T_probe.txt: 19.1 vs 26.5 us
+// at T = 300, the reference authors' production chunks).  The fp32 kernel
+// above serves exact fp32.
+bool bank_eligible(int T, int ldT) {
+  (void)ldT;
+  return T >= 1 && T <= 512;
+}
 
 static constexpr size_t mem_lds_bytes() { return (size_t)MB_LDS_FLOATS * sizeof(float); }
 static_assert(MB_LDS_FLOATS * 4 <= 160 * 1024, "LDS");
@@ -368,13 +374,19 @@ hipError_t launch_dec_mem_attention(const float* qp, const float* mem, const flo
   grid = 0;
 #endif
   const int G = grid > 0 ? std::min(C, grid) : C;
-  const bool full = (T + MB_TILE - 1) / MB_TILE == 8;  // the 512-sample chunks of every bench / translate batch
-  if (full)
-    hipLaunchKernelGGL((dec_mem_attention_kernel<8>), dim3(G), dim3(MB_NW * 64), mem_lds_bytes(), s, qp, mem, signal,
-                       span, pad_val, out, T, ldT, stamp, attn_dbg, dbg_stride, C);
-  else
-    hipLaunchKernelGGL((dec_mem_attention_kernel<0>), dim3(G), dim3(MB_NW * 64), mem_lds_bytes(), s, qp, mem, signal,
-                       span, pad_val, out, T, ldT, stamp, attn_dbg, dbg_stride, C);
+  // the tile count as a compile-time constant for chunks of 257..512 samples (the 512-sample chunks of every bench
+  // batch; the reference authors' production runs use 300); shorter ones take the runtime count
+#define ND_MEM_GO(N)                                                                                              \
+  hipLaunchKernelGGL((dec_mem_attention_kernel<N>), dim3(G), dim3(MB_NW * 64), mem_lds_bytes(), s, qp, mem, signal, \
+                     span, pad_val, out, T, ldT, stamp, attn_dbg, dbg_stride, C)
+  switch ((T + MB_TILE - 1) / MB_TILE) {
+    case 8: ND_MEM_GO(8); break;
+    case 7: ND_MEM_GO(7); break;
+    case 6: ND_MEM_GO(6); break;
+    case 5: ND_MEM_GO(5); break;
+    default: ND_MEM_GO(0); break;
+  }
+#undef ND_MEM_GO
   return hipGetLastError();
 }
 
@@ -445,7 +457,9 @@ hipError_t launch_stamp_reset(unsigned long long* stamps, int pairs, hipStream_t
 }
 
 hipError_t init_mem_attributes() {
-  const void* fns[] = {(const void*)dec_mem_attention_kernel<0>, (const void*)dec_mem_attention_kernel<8>};
+  const void* fns[] = {(const void*)dec_mem_attention_kernel<0>, (const void*)dec_mem_attention_kernel<5>,
+                       (const void*)dec_mem_attention_kernel<6>, (const void*)dec_mem_attention_kernel<7>,
+                       (const void*)dec_mem_attention_kernel<8>};
   for (const void* f : fns) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mem_lds_bytes());
     if (e != hipSuccess) return e;

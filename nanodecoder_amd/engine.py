@@ -828,7 +828,8 @@ def op_bank_pack_d8(x, B, T, ln_g=None, ln_b=None, ovf=None, span=None):
 
 def op_dec_bank_d8(qp, bank, signal, span, pad_val, out=None, ovf=None, grid=0):
     """Memory-bank context attention on the 24-bit digit bank (nd_op_dec_bank_d8):
-    qp [C, 2048] row-major, bank = op_bank_pack_d8's triple, T in (448, 512];
+    qp [C, 2048] row-major, bank = op_bank_pack_d8's triple, T in [1, 512] (ceil(T / 128) key blocks per
+    wave streamed);
     returns U [C16, 2048] packed."""
     C, T = signal.shape
     digits, ks, em = bank

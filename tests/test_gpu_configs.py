@@ -143,6 +143,33 @@ def test_beam_config3_batch1024_sampled_vs_oracle():
         assert abs(sc[i, 0] - s) < LOGP_ATOL, (i, sc[i, 0], s)
 
 
+@pytest.mark.parametrize("B,T", [(256, 300), (64, 200)])
+def test_greedy_short_chunks_vs_oracle(B, T):
+    """Chunks shorter than 512 samples: the reference authors' production
+    runs use -src_seq_length 300 (pipeline.evaluate.sh:83-89),
+    the 24-bit digit bank streams ceil(T / 128) key blocks per wave there
+    (bank8.hip bank8_kpw).  Greedy, max_length 100, -min_length 57, mask
+    samples injected, every chunk against the oracle."""
+    ref = _oracle()
+    cfg = synth.ModelConfig()
+    W = synth.make_weights(cfg, seed=11, eos_bias=-3.0)
+    S, MINL = 100, 57
+    sig = synth.synth_chunk_batch(B, T, seed=4000 + T, inject_masks=True)
+    lens = np.full(B, T, np.int32)
+    eng = _engine(cfg, W, max_batch=B, max_steps=S)
+    r = eng.translate_greedy(sig, lens, lens, max_len=S, min_len=MINL, return_logp=True)
+    assert eng.bank_form() == 2
+    assert int(r["overflow"].cpu()[0]) == 0
+    eng.close()
+    tok, lp = r["tokens"].cpu().numpy(), r["logp"].cpu().numpy()
+    o = ref.greedy(ref.RefModel(cfg, W), sig, lens, max_length=S, min_length=MINL)
+    ties = _tie_rows(tok, o["tokens"], o["logp"])
+    assert len(ties) <= 3, ties
+    keep = np.array([b not in ties for b in range(B)])
+    assert gu.logp_close(lp[keep], o["logp"][keep], atol=LOGP_ATOL).all()
+    assert np.abs(r["scores"].cpu().numpy()[keep] - o["scores"][keep]).max() < LOGP_ATOL
+
+
 @pytest.mark.parametrize("mode", ["greedy", "beam"])
 def test_long_max_length_vs_oracle(mode):
     """max_length 400 (up to 512 supported; the reference takes any,
