@@ -231,9 +231,9 @@ def _pmc(name, key="kernels"):
     committed PMC summary (profiles/pmc_summary.json, tools/pmc_summary.py:
     rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes with the gfx950 x2
     FETCH_SIZE correction), or (None, None).  The table keys kernels by their
-    full template name ('dec_bank_d8_kernel<false, false>'): an exact name is
+    full template name ('dec_bank_d8_kernel<false, false, 4>'): an exact name is
     looked up as given; a bare name takes its only instantiation in the table,
-    or the plain '<false, false>' one among several."""
+    or the plain '<false, false, ...>' one among several."""
     p = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(p) as f:
@@ -244,7 +244,7 @@ def _pmc(name, key="kernels"):
         return table[name]["hbm_bytes_per_launch"], name
     forms = sorted(k for k in table if k.split("<")[0] == name.split("<")[0])
     if len(forms) > 1:
-        forms = [k for k in forms if k.endswith("<false, false>")] or forms
+        forms = [k for k in forms if k.split("<", 1)[-1].startswith("false, false")] or forms
     if len(forms) == 1:
         return table[forms[0]]["hbm_bytes_per_launch"], forms[0]
     return None, None
@@ -332,7 +332,9 @@ def kernel_roofline(eng, B, mode, beam, encoder="transformer", alive=None, secon
         if form == 2:
             e0 = eng.engines[0] if hasattr(eng, "engines") else eng
             # the instantiation this call launched (bank8.hip: <non-temporal, grid walk>), as the PMC table keys it
-            name = f"dec_bank_d8_kernel<{'true' if e0.bank_nt else 'false'}, {'true' if e0.bank_grid else 'false'}>"
+            # <non-temporal, walking, key blocks per wave> (4 at T = 512: bank8.hip bank8_kpw)
+            name = (f"dec_bank_d8_kernel<{'true' if e0.bank_nt else 'false'}, {'true' if e0.bank_grid else 'false'}, "
+                    f"{min(4, (512 + 127) // 128)}>")
             nbytes = B * T * D * 3 + B * T * 4 + B * 4 + B * T * 4 + 2 * B * 8 * D * 4
         else:
             name = "dec_mem_attention_kernel<8>"
