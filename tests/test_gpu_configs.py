@@ -143,15 +143,15 @@ def test_beam_config3_batch1024_sampled_vs_oracle():
         assert abs(sc[i, 0] - s) < LOGP_ATOL, (i, sc[i, 0], s)
 
 
-@pytest.mark.parametrize("B,T", [(256, 300), (64, 200)])
-def test_greedy_short_chunks_vs_oracle(B, T):
+@pytest.mark.parametrize("B,T,encoder", [(256, 300, "transformer"), (64, 200, "transformer"), (64, 300, "nano")])
+def test_greedy_short_chunks_vs_oracle(B, T, encoder):
     """Chunks shorter than 512 samples: the reference authors' production
     runs use -src_seq_length 300 (pipeline.evaluate.sh:83-89),
     the 24-bit digit bank streams ceil(T / 128) key blocks per wave there
     (bank8.hip bank8_kpw).  Greedy, max_length 100, -min_length 57, mask
     samples injected, every chunk against the oracle."""
     ref = _oracle()
-    cfg = synth.ModelConfig()
+    cfg = synth.ModelConfig(encoder_type=encoder)
     W = synth.make_weights(cfg, seed=11, eos_bias=-3.0)
     S, MINL = 100, 57
     sig = synth.synth_chunk_batch(B, T, seed=4000 + T, inject_masks=True)
@@ -168,6 +168,32 @@ def test_greedy_short_chunks_vs_oracle(B, T):
     keep = np.array([b not in ties for b in range(B)])
     assert gu.logp_close(lp[keep], o["logp"][keep], atol=LOGP_ATOL).all()
     assert np.abs(r["scores"].cpu().numpy()[keep] - o["scores"][keep]).max() < LOGP_ATOL
+
+
+def test_beam_short_chunks_vs_oracle():
+    """The production beam flags' chunk length (-src_seq_length 300, beam 5,
+    pipeline.evaluate.sh:100-106): --fast beam 5 on 64 chunks of 300 samples
+    (the 24-bit context K/V image and the tail's list kernels at T = 300),
+    max_length 100, -min_length 57, masks injected, every chunk against the
+    oracle."""
+    ref = _oracle()
+    cfg = synth.ModelConfig()
+    W = synth.make_weights(cfg, seed=11, eos_bias=-3.0)
+    B, T, S, MINL = 64, 300, 100, 57
+    sig = synth.synth_chunk_batch(B, T, seed=4100, inject_masks=True)
+    lens = np.full(B, T, np.int32)
+    eng = _engine(cfg, W, max_batch=B, max_steps=S, max_beam=5)
+    r = eng.translate_beam(sig, lens, lens, beam=5, n_best=1, max_len=S, min_len=MINL)
+    assert eng.bank_form() == 3
+    assert int(r["overflow"].cpu()[0]) == 0
+    eng.close()
+    tok, sc, ln = (r[k].cpu().numpy() for k in ("tokens", "scores", "lens"))
+    exp = ref.fast_beam(ref.RefModel(cfg, W), sig, lens, beam_size=5, n_best=1, max_length=S, min_length=MINL)
+    for i in range(B):
+        s, p = exp[i][0]
+        assert ln[i, 0] == len(p), (i, ln[i, 0], len(p))
+        assert (tok[i, 0, : len(p)] == p).all(), i
+        assert abs(sc[i, 0] - s) < LOGP_ATOL, (i, sc[i, 0], s)
 
 
 @pytest.mark.parametrize("mode", ["greedy", "beam"])

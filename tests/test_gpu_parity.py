@@ -528,7 +528,8 @@ def test_enc_attention_vs_oracle(scale):
         assert (out[b * T: b * T + L] - exp).abs().max().item() < tol, b
 
 
-@pytest.mark.parametrize("T,grid", [(512, 0), (200, 0), (37, 0), (512, 5), (512, 7), (200, 1)])
+@pytest.mark.parametrize("T,grid", [(512, 0), (200, 0), (37, 0), (512, 5), (512, 7), (200, 1), (300, 0), (384, 6),
+                                    (448, 0), (300, 4)])
 def test_mem_attention_vs_fp64(T, grid):
     """Memory-bank context attention (dec_mem_attention_kernel) against an
     fp64 softmax(q' M^T) M per head, with ragged spans (tile/wave boundaries,
