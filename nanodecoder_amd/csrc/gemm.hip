@@ -1174,20 +1174,6 @@ hipError_t launch_gemm_p16(GemmArgs& g, hipStream_t s) {
     return e;
   }
   if (g.N % 16 != 0 || (g.norm && !g.part_in)) return hipErrorInvalidValue;
-#ifndef ND_F32_SHORTCHAIN
-#define ND_F32_SHORTCHAIN 0
-#endif
-#if ND_F32_SHORTCHAIN
-  // exact fp32 (no split image) at greedy row counts: an fp32 16x16x4 MFMA covers 4 k in 32 cycles where the
-  // split form's three 16x16x32 cover 32 k in 48, so the one-wave-per-block chains run 5x longer; split K over
-  // more waves instead (the LDS-staged kernel's waves each walk the whole K = 256)
-  if (!g.Wh && g.M <= 1024) {
-    if (g.K == 256 && g.N % 64 == 0) return launch_p16<4, 2, 128>(g, s);
-#if ND_F32_SHORTCHAIN > 1
-    if (g.K == 2048) return launch_p16<1, 16, 128>(g, s);
-#endif
-  }
-#endif
   if (g.K == 256) {
     // LN consumers share the row statistics across many column blocks
     // LDS-staged tiles when they still give >= 128 workgroups (measured on
