@@ -2,7 +2,7 @@
 # round 6's record on the final tree, one GPU call: smoke, every GPU test, the bench line, the kernel traces
 # (one call, three in flight, exact fp32 one call), the PMC byte passes (greedy; configs[3]'s beam pass on the
 # bench workload), the MFMA counter passes.  Each step time-limited; stops at the first failure.
-t=${1:-r06f}
+t=${1:-r06g}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
 export PYTHONUNBUFFERED=1
