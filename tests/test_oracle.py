@@ -185,3 +185,63 @@ def test_outlier_transform_preserves_function():
     bb = ref_cpu.fast_beam(ref_cpu.RefModel(cfg, Wo), sig[:3], lens[:3], beam_size=3, max_length=20, min_length=5)
     for x, y in zip(ba, bb):
         assert (np.asarray(x[0][1]) == np.asarray(y[0][1])).all() and abs(x[0][0] - y[0][0]) < 1e-4
+
+
+def test_beam_ancestry_table_and_distinct_history():
+    """The engine keeps one self-attention history slot per beam row and
+    an ancestry table (key t of row r lives in slot anc[r][t]: the row that
+    wrote it at step t) instead of reordering the cache as the reference does
+    (map_state / index_select, translate/translator.py:791-792).  Following
+    the oracle's --fast beam selections, the table reconstructs every live
+    hypothesis' input tokens exactly.  It also measures what a beam
+    self-attention launch must read at least: the distinct slots per key
+    among a chunk's 5 rows, on the bench's configs[3] workload (16 of its
+    chunks; DESIGN.md section 3 "Round 6" sets the engine's counter traffic
+    beside it)."""
+    import torch
+    cfg = synth.ModelConfig()
+    W = synth.make_weights(cfg, seed=11, eos_bias=-3.0)
+    B, K, S, MINL = 16, 5, 100, 57
+    sig = synth.synth_chunk_batch(1024, 512, seed=2000, inject_masks=False)[:B]
+    lens = np.full(B, 512, np.int32)
+    model = ref_cpu.RefModel(cfg, W)
+    V = cfg.vocab
+    R = B * K
+    with torch.no_grad():
+        memory = model.encode(torch.as_tensor(sig), lens)
+        st = model.decoder_state(ref_cpu.tile(memory, K), ref_cpu.tile(torch.as_tensor(sig), K))
+        alive = torch.full((R, 1), cfg.bos_idx, dtype=torch.long)
+        tlp = torch.tensor([0.0] + [float("-inf")] * (K - 1)).repeat(B)
+        anc = np.zeros((R, S), np.int64)
+        written = np.zeros((R, S), np.int64)  # the input token each slot wrote at step t
+        done = np.zeros(B, bool)
+        reads = keys = launches = 0
+        for step in range(S):
+            cur = anc.copy()
+            cur[:, step] = np.arange(R)           # this step's own key: the row's slot
+            written[:, step] = alive[:, -1].numpy()
+            # the table gives every row its exact input history
+            hist = written[cur[:, : step + 1], np.arange(step + 1)[None, :]]
+            assert (hist == alive.numpy()).all(), step
+            for c in np.nonzero(~done)[0]:
+                rows = cur[c * K:(c + 1) * K, : step + 1]
+                reads += sum(len(set(rows[:, t])) for t in range(step + 1))
+                keys += step + 1
+                launches += 1
+            lp = model.decode_step(st, alive[:, -1], step)
+            if step < MINL:
+                lp[:, cfg.eos_idx] = -1e20
+            sc, ids = (lp + tlp.view(-1, 1)).reshape(-1, K * V).topk(K, dim=-1)
+            sel = (torch.div(ids, V, rounding_mode="floor") + torch.arange(0, R, K).unsqueeze(1)).view(-1)
+            alive = torch.cat([alive.index_select(0, sel), (ids % V).view(-1, 1)], -1)
+            anc = cur[sel.numpy()]                # a child inherits its parent's table row
+            fin = (ids % V).eq(cfg.eos_idx)
+            done |= fin[:, 0].numpy() & (step >= MINL)
+            tlp = sc.reshape(-1).masked_fill(fin.view(-1), -1e10)
+            model.reorder(st, sel)
+            if done.all():
+                break
+    per_key = reads / keys
+    print(f"\n[beam history] {step + 1} steps: {per_key:.2f} distinct slots per key of {K} rows, "
+          f"{reads * 1600 / launches / 1e3:.1f} KB of 24-bit history rows per alive chunk-launch")
+    assert 1.0 < per_key < K
