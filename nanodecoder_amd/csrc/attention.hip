@@ -1083,7 +1083,8 @@ dec_self_attention_kernel(const float* __restrict__ qkv, float* __restrict__ cac
 // The rows' own keys (t == step) are appended first (Q24: quantised as the
 // per-row kernel does), and after a workgroup barrier every key, the own one
 // included, is read from the cache.
-template <int RPC, int NW, bool Q24>
+// LONG: steps from NW * 64 on (max_length > 256): a second lane-indexed slot table
+template <int RPC, int NW, bool Q24, bool LONG>
 __global__ void __launch_bounds__(NW * 64)
 dec_self_attention_beam_kernel(const float* __restrict__ qkv, float* __restrict__ cache, const int* __restrict__ anc,
                                int anc_ld, int step, int S, float* __restrict__ out, const int* __restrict__ skip,
@@ -1129,7 +1130,7 @@ dec_self_attention_beam_kernel(const float* __restrict__ qkv, float* __restrict_
     l[j] = 0.f;
   }
   // this wave's keys t = wu + NW i: every row's slot for them (t == step: its own slot), key i in lane i & 63
-  // of sl (i < 64) or sl2 (64 <= i < 128: steps past NW * 64, SELF_MAXS)
+  // of sl (i < 64) or (LONG) sl2 (64 <= i < 128: steps past NW * 64, SELF_MAXS)
   int sl[RPC], sl2[RPC];
   {
     const int t = wu + NW * lane, t2 = t + NW * 64;
@@ -1137,7 +1138,7 @@ dec_self_attention_beam_kernel(const float* __restrict__ qkv, float* __restrict_
     for (int j = 0; j < RPC; ++j) {
       const int r = c * RPC + j;
       sl[j] = t < step ? anc[(size_t)r * anc_ld + t] : r;
-      sl2[j] = t2 < step ? anc[(size_t)r * anc_ld + t2] : r;
+      if constexpr (LONG) sl2[j] = t2 < step ? anc[(size_t)r * anc_ld + t2] : r;
     }
   }
   static_assert(SELF_MAXS <= NW * 128, "two slot tables of 64 keys per wave");
@@ -1156,7 +1157,8 @@ dec_self_attention_beam_kernel(const float* __restrict__ qkv, float* __restrict_
     const int t = min(wu + NW * i, n - 1);  // wave-uniform; clamped (straight-line loads)
 #pragma unroll
     for (int j = 0; j < RPC; ++j) {
-      const size_t at = (size_t)__builtin_amdgcn_readlane(i < 64 ? sl[j] : sl2[j], i & 63) * S + t;
+      const size_t at = LONG ? (size_t)__builtin_amdgcn_readlane(i < 64 ? sl[j] : sl2[j], i & 63) * S + t
+                             : (size_t)__builtin_amdgcn_readlane(sl[j], min(i, 63)) * S + t;
       if constexpr (Q24) {
         const uint8_t* rb = reinterpret_cast<const uint8_t*>(cache) + at * SELF_Q24_ROW;
         kk[j].kq = *reinterpret_cast<const u32v3*>(rb + 12 * lane);
@@ -1220,22 +1222,31 @@ hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* 
     if (clist && (ccap < 1 || (long)ccap * rpc > R)) return hipErrorInvalidValue;
     if (step >= max_steps || step >= SELF_MAXS) return hipErrorInvalidValue;
     const int grid = clist ? ccap : R / rpc;
+    const bool lng = step >= 4 * 64;  // keys past the first slot table (4 waves x 64 lanes)
     switch (rpc) {
-#define ND_SELFB(RP)                                                                                               \
-  case RP:                                                                                                         \
-    if (q24)                                                                                                       \
-      hipLaunchKernelGGL((dec_self_attention_beam_kernel<RP, 4, true>), dim3(grid), dim3(4 * 64), 0, s, qkv,      \
-                         cache, anc, anc_ld, step, max_steps, out, skip, qr, clist);                              \
-    else                                                                                                           \
-      hipLaunchKernelGGL((dec_self_attention_beam_kernel<RP, 4, false>), dim3(grid), dim3(4 * 64), 0, s, qkv,     \
-                         cache, anc, anc_ld, step, max_steps, out, skip, qr, clist);                              \
+#define ND_SELFB2(RP, Q, L)                                                                                       \
+  hipLaunchKernelGGL((dec_self_attention_beam_kernel<RP, 4, Q, L>), dim3(grid), dim3(4 * 64), 0, s, qkv, cache,    \
+                     anc, anc_ld, step, max_steps, out, skip, qr, clist)
+#define ND_SELFB(RP)                    \
+  case RP:                              \
+    if (q24 && !lng)                    \
+      ND_SELFB2(RP, true, false);       \
+    else if (q24)                       \
+      ND_SELFB2(RP, true, true);        \
+    else if (!lng)                      \
+      ND_SELFB2(RP, false, false);      \
+    else                                \
+      ND_SELFB2(RP, false, true);       \
     break;
       ND_SELFB(2)
       ND_SELFB(3)
       ND_SELFB(4)
       ND_SELFB(5)
       ND_SELFB(6)
+      ND_SELFB(7)
+      ND_SELFB(8)
 #undef ND_SELFB
+#undef ND_SELFB2
       default:
         return hipErrorInvalidValue;
     }
@@ -1310,7 +1321,7 @@ hipError_t launch_dec_self_attention(const float* qkv, float* cache, const int* 
 #define CTX_NW 4
 #define CTX_URPC 2  // rows per chunk up to which a block holds 4 keys (else 2)
 #define CTX_UHI 2   // keys per block above CTX_URPC rows
-#define CTX_MAXR 6
+#define CTX_MAXR 8  // beam_size bound (nd_create max_beam; search.hip BEAM_MAX)
 template <int RPC>
 struct CtxTile {
   static constexpr int U = RPC <= CTX_URPC ? 4 : CTX_UHI;  // keys per block (register budget)
@@ -1695,6 +1706,8 @@ hipError_t launch_dec_ctx_attention(const float* q, const void* kv, int ld, int 
     ND_CTX_CASE(4)
     ND_CTX_CASE(5)
     ND_CTX_CASE(6)
+    ND_CTX_CASE(7)
+    ND_CTX_CASE(8)
 #undef ND_CTX_CASE
   }
   if (nsplit > 1) {
@@ -1751,9 +1764,11 @@ hipError_t init_kernel_attributes() {
       (const void*)dec_ctx_attention_kernel<1>, (const void*)dec_ctx_attention_kernel<2>,
       (const void*)dec_ctx_attention_kernel<3>, (const void*)dec_ctx_attention_kernel<4>,
       (const void*)dec_ctx_attention_kernel<5>, (const void*)dec_ctx_attention_kernel<6>,
+      (const void*)dec_ctx_attention_kernel<7>, (const void*)dec_ctx_attention_kernel<8>,
       (const void*)dec_ctx_q24_kernel<1>,              (const void*)dec_ctx_q24_kernel<2>,
       (const void*)dec_ctx_q24_kernel<3>,              (const void*)dec_ctx_q24_kernel<4>,
-      (const void*)dec_ctx_q24_kernel<5>,              (const void*)dec_ctx_q24_kernel<6>};
+      (const void*)dec_ctx_q24_kernel<5>,              (const void*)dec_ctx_q24_kernel<6>,
+      (const void*)dec_ctx_q24_kernel<7>,              (const void*)dec_ctx_q24_kernel<8>};
   for (const void* f : fns) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;

@@ -1145,7 +1145,7 @@ int nd_create(const nd_config* cfg, nd_ctx** out) {
   if (cfg->vocab < 4 || cfg->vocab > ND_MAXV) return fail(ND_ERR_ARG, "vocab must be in [4, 32]");
   if (cfg->max_src_len < 1 || cfg->max_src_len > 512) return fail(ND_ERR_ARG, "max_src_len must be in [1, 512]");
   if (cfg->max_steps < 1 || cfg->max_steps > 512) return fail(ND_ERR_ARG, "max_steps must be in [1, 512]");
-  if (cfg->max_beam < 1 || cfg->max_beam > 6) return fail(ND_ERR_ARG, "max_beam must be in [1, 6]");
+  if (cfg->max_beam < 1 || cfg->max_beam > 8) return fail(ND_ERR_ARG, "max_beam must be in [1, 8]");
   if (cfg->max_batch < 1) return fail(ND_ERR_ARG, "max_batch must be >= 1");
   if (cfg->enc_layers < 1 || cfg->dec_layers < 1) return fail(ND_ERR_ARG, "layers must be >= 1");
   if (cfg->encoder_type != ND_ENC_TRANSFORMER && cfg->encoder_type != ND_ENC_NANO)
@@ -2349,7 +2349,7 @@ int nd_op_dec_self_attention(const float* qkv, float* cache, const int32_t* anc,
 int nd_op_dec_self_attention_beam(const float* qkv, float* cache, const int32_t* anc, int32_t anc_ld, int32_t step,
                                   int32_t max_steps, float* out, int32_t R, int32_t rpc, const int32_t* done,
                                   void* stream) {
-  if (!qkv || !cache || !anc || !out || rpc < 2 || rpc > 6 || R % rpc)
+  if (!qkv || !cache || !anc || !out || rpc < 2 || rpc > 8 || R % rpc)
     return fail(ND_ERR_ARG, "dec_self_attention_beam: bad arguments");
   hipError_t e = nd::launch_dec_self_attention(qkv, cache, anc, anc_ld, step, max_steps, out, R, (hipStream_t)stream,
                                                rpc, done);
@@ -2360,7 +2360,7 @@ int nd_op_dec_self_attention_beam(const float* qkv, float* cache, const int32_t*
 int nd_op_dec_self_attention_q24(const float* qkv, void* cache, const int32_t* anc, int32_t anc_ld, int32_t step,
                                  int32_t max_steps, float* out, int32_t R, int32_t rpc, const int32_t* done,
                                  void* stream) {
-  if (!qkv || !cache || !out || rpc < 1 || rpc > 6 || R % rpc || (rpc > 1 && !anc))
+  if (!qkv || !cache || !out || rpc < 1 || rpc > 8 || R % rpc || (rpc > 1 && !anc))
     return fail(ND_ERR_ARG, "dec_self_attention_q24: bad arguments");
   hipError_t e = nd::launch_dec_self_attention(qkv, static_cast<float*>(cache), anc, anc_ld, step, max_steps, out, R,
                                                (hipStream_t)stream, rpc, done, nd::QkvRows(), nullptr, nullptr, 0,

@@ -240,7 +240,7 @@ REVIEWED_PAIRED = {
                             "barrier; encoder-side GEMMs of the beam / exact / NanoEncoder paths, pool-tested"),
     "dec_ctx_attention_kernel": (36, "the (m, l, acc) merge of the beam context attention (and of its split "
                                      "form); launched with at most 52 KB, listed in case that grows"),
-    "dec_ctx_q24_kernel": (24, "the (m, l, acc) merge after a barrier behind the DMA rings' last use; the merge "
+    "dec_ctx_q24_kernel": (26, "the (m, l, acc) merge after a barrier behind the DMA rings' last use; the merge "
                                "image sits at LDS byte 0 (< 22 KB), far below 64 KB (the rings above it take no "
                                "paired form)"),
     "dec_bank_d8_kernel": (15, "the (m, l) merge and the q' digit rows (cross-wave, after a barrier), once per "

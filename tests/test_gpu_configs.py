@@ -170,6 +170,36 @@ def test_greedy_short_chunks_vs_oracle(B, T, encoder):
     assert np.abs(r["scores"].cpu().numpy()[keep] - o["scores"][keep]).max() < LOGP_ATOL
 
 
+@pytest.mark.parametrize("beam,fast", [(7, True), (8, True), (8, False)])
+def test_beam_up_to_8_vs_oracle(beam, fast):
+    """beam_size 7 and 8 (the reference takes any, models/opts.py:581; the
+    engine's bound is 8): --fast beam (and the classic Beam at 8) on 16
+    chunks, n_best 2, max_length 100, -min_length 57, masks injected, every
+    chunk's two best hypotheses against the oracle."""
+    ref = _oracle()
+    cfg = synth.ModelConfig()
+    W = synth.make_weights(cfg, seed=11, eos_bias=-3.0)
+    B, S, MINL, NB = 16, 100, 57, 2
+    sig = synth.synth_chunk_batch(B, 512, seed=4200 + beam, inject_masks=True)
+    lens = np.full(B, 512, np.int32)
+    eng = _engine(cfg, W, max_batch=B, max_steps=S, max_beam=beam)
+    if fast:
+        r = eng.translate_beam(sig, lens, lens, beam=beam, n_best=NB, max_len=S, min_len=MINL)
+    else:
+        r = eng.translate_beam_classic(sig, lens, lens, beam=beam, n_best=NB, max_len=S, min_len=MINL)
+    assert int(r["overflow"].cpu()[0]) == 0
+    eng.close()
+    tok, sc, ln = (r[k].cpu().numpy() for k in ("tokens", "scores", "lens"))
+    run = ref.fast_beam if fast else ref.classic_beam
+    exp = run(ref.RefModel(cfg, W), sig, lens, beam_size=beam, n_best=NB, max_length=S, min_length=MINL)
+    for i in range(B):
+        for n in range(NB):
+            s, p = exp[i][n]
+            assert ln[i, n] == len(p), (i, n, ln[i, n], len(p))
+            assert (tok[i, n, : len(p)] == p).all(), (i, n)
+            assert abs(sc[i, n] - s) < LOGP_ATOL, (i, n, sc[i, n], s)
+
+
 def test_beam_short_chunks_vs_oracle():
     """The production beam flags' chunk length (-src_seq_length 300, beam 5,
     pipeline.evaluate.sh:100-106): --fast beam 5 on 64 chunks of 300 samples

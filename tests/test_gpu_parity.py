@@ -406,7 +406,7 @@ def test_dec_self_attention_vs_fp64(step, beam):
 
 
 @pytest.mark.parametrize("rpc,step", [(5, 0), (5, 1), (5, 47), (2, 130), (6, 63), (3, 255), (5, 256), (5, 300),
-                                      (6, 511)])
+                                      (6, 511), (8, 100), (7, 300)])
 def test_dec_self_attention_beam_vs_fp64(rpc, step):
     """Beam rows' self-attention on the chunk-per-workgroup kernel: the rows of
     a chunk share most of their history (slots from the chunk's rows, with
@@ -678,7 +678,7 @@ def test_gemm_q24_epilogue_equals_pack(norm):
     assert bad.numel() == 0, bad[:8].tolist()
 
 
-@pytest.mark.parametrize("rpc", [1, 2, 5, 6])
+@pytest.mark.parametrize("rpc", [1, 2, 5, 6, 7, 8])
 @pytest.mark.parametrize("q24", [False, True])
 def test_ctx_attention_vs_fp64(rpc, q24):
     """The beam's context attention (dec_ctx_attention_kernel, fp32 K/V or the
@@ -747,7 +747,8 @@ def test_alive_list():
     assert got.tolist() == alive[:5] and int(ovf.item()) == 1
 
 
-@pytest.mark.parametrize("rpc,nsplit,q24", [(5, 16, True), (5, 16, False), (2, 7, True), (6, 32, True), (5, 1, True)])
+@pytest.mark.parametrize("rpc,nsplit,q24", [(5, 16, True), (5, 16, False), (2, 7, True), (6, 32, True), (5, 1, True),
+                                           (8, 16, True), (7, 8, False)])
 def test_ctx_attention_tail_list_split(rpc, nsplit, q24):
     """The --fast beam tail's context attention: workgroups over a chunk list
     only, each chunk's keys in nsplit workgroups combined by a second launch,
