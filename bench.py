@@ -128,7 +128,7 @@ def dist_setup(args):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        if args.backend == "nccl":
+        if args.backend == "nccl" and not args.selftest_cpu:  # the CPU self-test is gloo whatever --backend says
             torch.cuda.set_device(local)
             torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
