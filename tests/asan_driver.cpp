@@ -138,8 +138,8 @@ static void config_paths() {
       {"vocab large", [](nd_config& c) { c.vocab = 33; }},
       {"src len", [](nd_config& c) { c.max_src_len = 513; }},
       {"src len 0", [](nd_config& c) { c.max_src_len = 0; }},
-      {"steps", [](nd_config& c) { c.max_steps = 257; }},
-      {"beam", [](nd_config& c) { c.max_beam = 7; }},
+      {"steps", [](nd_config& c) { c.max_steps = 513; }},
+      {"beam", [](nd_config& c) { c.max_beam = 9; }},
       {"batch", [](nd_config& c) { c.max_batch = 0; }},
       {"layers", [](nd_config& c) { c.dec_layers = 0; }},
       {"encoder", [](nd_config& c) { c.encoder_type = 5; }},
