@@ -72,6 +72,8 @@ def main():
             "f16_frac_peak": round(f16 / s / 1e12 / F16_PEAK, 4), "f32_frac_peak": round(f32 / s / 1e12 / F32_PEAK, 4),
             "mfma_util": round(k["SQ_VALU_MFMA_BUSY_CYCLES"] / max(1.0, k["GRBM_GUI_ACTIVE"] / XCDS * SIMDS), 4),
             "cu_busy": round(k["SQ_BUSY_CU_CYCLES"] / max(1.0, k["GRBM_GUI_ACTIVE"] / XCDS * CUS), 4),
+            # the clock the dispatches ran at: GUI-active cycles per XCD over their span
+            "clock_ghz": round(k["GRBM_GUI_ACTIVE"] / XCDS / max(1.0, k["ns"]), 3),
         }
     s = tot["ns"] * 1e-9
     out["path"] = {
