@@ -136,10 +136,6 @@ __device__ __forceinline__ void split4(f32x4 v, h4& hi, h4& lo) {
         (_Float16)(v.w - (float)hi.w)};
 }
 
-template <int BM, int BN, int WM, int WN, int EP, bool H3, bool RELU, bool RESID>
-__device__ __forceinline__ void f32_tile_epilogue(const GemmArgs& g, f32x16 (&acc)[BM / WM / 32][BN / WN / 32],
-                                                  float* Cs, int m0, int n0, int nbt);
-
 // BK: k depth of a main-loop step (32; 64 for the small-tile, long-K shapes,
 // whose steps are otherwise too short to cover the next step's load latency)
 template <int BM, int BN, int WM, int WN, int BK, bool H3, bool LN, bool RELU, bool RESID>
@@ -343,21 +339,7 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
     __syncthreads();
   }
   if constexpr (H3 && !LN) flag_overflow(g.ovf, amax);
-  f32_tile_epilogue<BM, BN, WM, WN, EP, H3, RELU, RESID>(g, acc, Cs, m0, n0, nbt);
-}
 
-// The row-major LDS-tiled kernels' epilogue: the C tile staged through LDS (Cs, EP passes of BM / EP rows) so
-// output / residual traffic is coalesced float4 rows; bias (+ relu), residual, the 24-bit context image, row
-// statistics
-template <int BM, int BN, int WM, int WN, int EP, bool H3, bool RELU, bool RESID>
-__device__ __forceinline__ void f32_tile_epilogue(const GemmArgs& g, f32x16 (&acc)[BM / WM / 32][BN / WN / 32],
-                                                  float* Cs, int m0, int n0, int nbt) {
-  constexpr int NT = WM * WN * 64, LDC = BN + 4, RP = BM / EP;
-  constexpr int FM = BM / WM / 32, FN = BN / WN / 32;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / WN, wn = wave % WN;
-  const int lr = lane & 31;
-  const int M = g.M;
   constexpr int TPR = BN / 4, RPP = NT / TPR;
   const int c4 = (tid % TPR) * 4;
 #pragma unroll
@@ -413,215 +395,6 @@ __device__ __forceinline__ void f32_tile_epilogue(const GemmArgs& g, f32x16 (&ac
     }
     if (EP > 1) __syncthreads();
   }
-}
-
-// ---------------------------------------------------------------------------
-// Exact fp32 at large M (the encoder's GEMMs under exact fp32): the same
-// 256x256 tile, 8 waves of 128x64 and v_mfma_f32_32x32x2_f32 products as
-// gemm_f32_kernel (the same k order per output, so bitwise the same C), with
-// the operands brought to LDS by DMA instead of through registers.
-// Measured on the register-staged kernel (profiles/r06h_mfma_exact_mfma.json,
-// tools/microbench.py enc): the matrix cores busy 0.70-0.74 of the cycles,
-// FFN2 (K = 2048) 1100 us against 922 us for the library's fp32 GEMM at the
-// same shape: a step's register staging, LDS stores and barrier all sit
-// between one k step's products and the next.  Here:
-//  - k steps of 16 (32 KB: A 16 KB + W 16 KB) in a ring of 4 LDS slots, every
-//    wave copying 4 KB of each by buffer_load ... lds (lane-linear 1 KB per
-//    instruction, the lane's row offset its only vector operand, the k step
-//    in the scalar offset); three steps in flight beyond the one computed;
-//  - a row's four 16-B k chunks are stored XOR-swizzled by (row >> 2) & 3, so
-//    the MFMA operand reads (lane = row, 16 B of k) are conflict-free
-//    ds_read_b128 and the DMA's destination stays lane-linear;
-//  - the LDS reads are inline asm with counted lgkmcnt waits (an ordinary LDS
-//    read after an LDS-DMA makes hipcc wait for every copy in flight), raw
-//    s_barrier with a counted vmcnt (a __syncthreads drains the ring);
-//  - one barrier per k step, between its two 8-k halves: it publishes the next
-//    step's copies and frees the slot just read, so the next step's first
-//    operand reads and the next copy go out while this step's second half of
-//    products runs;
-//  - the LayerNorm is applied to the operand registers ((a - mean) * rstd per
-//    row, as the register-staged kernel applies it at its LDS store).
-#define FD_BK 16                       // k per step
-#define FD_SLOTS 4                     // ring slots (steps in flight + the one computed)
-#define FD_SLOT (2 * 256 * FD_BK * 4)  // bytes per slot: A tile, then W tile
-typedef __attribute__((address_space(3))) void fd_lds_void;
-
-template <int OFF>
-__device__ __forceinline__ f32x4 fd_ld(uint32_t a) {
-  f32x4 r;
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=&v"(r) : "v"(a), "n"(OFF) : "memory");
-  return r;
-}
-// one 8-k half of a step: the lane's A rows (4 blocks 2048 B apart) and W rows (2 blocks)
-struct FdOps {
-  f32x4 a[4], b[2];
-};
-__device__ __forceinline__ void fd_issue_reads(FdOps& o, uint32_t aa, uint32_t ab) {
-  o.a[0] = fd_ld<0>(aa);
-  o.a[1] = fd_ld<2048>(aa);
-  o.a[2] = fd_ld<4096>(aa);
-  o.a[3] = fd_ld<6144>(aa);
-  o.b[0] = fd_ld<0>(ab);
-  o.b[1] = fd_ld<2048>(ab);
-}
-template <int N>
-__device__ __forceinline__ void fd_land(FdOps& o) {
-  asm volatile("s_waitcnt lgkmcnt(%6)"
-               : "+v"(o.a[0]), "+v"(o.a[1]), "+v"(o.a[2]), "+v"(o.a[3]), "+v"(o.b[0]), "+v"(o.b[1])
-               : "n"(N)
-               : "memory");
-}
-
-template <bool LN, bool RELU, bool RESID>
-__global__ void __launch_bounds__(512) gemm_f32d_kernel(const GemmArgs g) {
-  constexpr int BM = 256, BN = 256, WM = 2, WN = 4, NT = 512, EP = WM;
-  constexpr int RING = FD_SLOTS * FD_SLOT, CBYTES = (BM / EP) * (BN + 4) * 4;
-  __shared__ __attribute__((aligned(16))) char fd_sm[RING > CBYTES ? RING : CBYTES];
-  __shared__ float s_mu[LN ? BM : 1], s_rs[LN ? BM : 1];
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wu = __builtin_amdgcn_readfirstlane(wave);
-  const int ntn = g.N / BN;
-  int nbt, mbk;
-  if (g.xcd_map) {  // as gemm_f32_kernel: XCD x keeps the row blocks x, x + 8, ... with all their column tiles
-    const int b = blockIdx.x, j = b >> 3;
-    nbt = j % ntn;
-    mbk = (j / ntn) * 8 + (b & 7);
-  } else {
-    nbt = blockIdx.x % ntn;
-    mbk = blockIdx.x / ntn;
-  }
-  const int n0 = nbt * BN, m0 = mbk * BM;
-  const int M = g.M, K = g.K, KT = K / FD_BK;
-
-  // copies: wave w moves pieces j = 2w, 2w + 1 of each tile (1 KB each: 16 rows x 4 chunks of 16 B); the
-  // lane's piece is row 16 j + lane / 4, k chunk (lane & 3) ^ ((lane >> 4) & 3) (rows past M clamped: their C
-  // rows are never stored)
-  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.A + (size_t)m0 * g.lda), 0,
-                                                                      0x7fffffff, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.W + (size_t)n0 * g.ldw), 0,
-                                                                      0x7fffffff, 0x00020000);
-  const int kc = (lane & 3) ^ ((lane >> 4) & 3);
-  int voa[2], vow[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = (2 * wu + i) * 16 + (lane >> 2);
-    voa[i] = min(row, M - 1 - m0) * g.lda * 4 + kc * 16;
-    vow[i] = row * g.ldw * 4 + kc * 16;
-  }
-  auto issue = [&](int st) {  // k step st into slot st % FD_SLOTS
-    char* sl = fd_sm + (st % FD_SLOTS) * FD_SLOT;
-    const int so = st * FD_BK * 4;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (fd_lds_void*)(sl + (2 * wu + i) * 1024), 16, voa[i], so, 0, 0);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (fd_lds_void*)(sl + FD_SLOT / 2 + (2 * wu + i) * 1024), 16,
-                                               vow[i], so, 0, 0);
-  };
-
-  if (rows_dead(g.skip, g.skip_rpc, m0, BM, M)) return;
-#pragma unroll
-  for (int p = 0; p < FD_SLOTS; ++p)
-    if (p < KT) issue(p);
-
-  const int wm = wave / WN, wn = wave % WN;
-  const int lr = lane & 31, lh = lane >> 5;
-  float mu[4], rs[4];
-  if constexpr (LN) {
-    // the row statistics' loads go out beside the first copies (the LDS stores below wait for both)
-    if (g.part_in) {
-      for (int r = tid; r < BM; r += NT) {
-        float m_, r_;
-        merge_stats(g.part_in + (size_t)min(m0 + r, M - 1) * ND_PART_LD * 2, g.part_n_in, m_, r_);
-        s_mu[r] = m_;
-        s_rs[r] = r_;
-      }
-    } else {
-      // two-pass row statistics, one wave per row (K == 256, host-checked)
-      constexpr int NW = NT / 64, RPW = BM / NW, G = 8;
-      for (int r0 = 0; r0 < RPW; r0 += G) {
-        f32x4 v[G];
-#pragma unroll
-        for (int i = 0; i < G; ++i) v[i] = ld4(g.A + (size_t)min(m0 + wave + (r0 + i) * NW, M - 1) * g.lda + lane * 4);
-#pragma unroll
-        for (int i = 0; i < G; ++i) {
-          const int r = wave + (r0 + i) * NW;
-          const float m_ = wave_sum(v[i].x + v[i].y + v[i].z + v[i].w) * (1.0f / 256.0f);
-          const f32x4 d = v[i] - m_;
-          const float var = wave_sum(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w) * (1.0f / 256.0f);
-          if (lane == 0) {
-            s_mu[r] = m_;
-            s_rs[r] = ln_rsqrt(var + ND_LN_EPS);
-          }
-        }
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      mu[a] = s_mu[wm * 128 + a * 32 + lr];
-      rs[a] = s_rs[wm * 128 + a * 32 + lr];
-    }
-  }
-
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-
-  // the lane's operand addresses: row block base (a, b = 0) + swizzled chunk of 8-k half h
-  const uint32_t lbase = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)fd_sm);
-  const int sw = (lr >> 2) & 3;
-  const uint32_t oa = (uint32_t)((wm * 128 + lr) * 64), ob = (uint32_t)(FD_SLOT / 2 + (wn * 64 + lr) * 64);
-  const uint32_t x0 = (uint32_t)((lh ^ sw) * 16), x1 = (uint32_t)(((2 + lh) ^ sw) * 16);
-  auto products = [&](FdOps& o) {
-    if constexpr (LN) {
-#pragma unroll
-      for (int a = 0; a < 4; ++a) o.a[a] = (o.a[a] - mu[a]) * rs[a];
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 2; ++b) acc[a][b] = mfma32(o.a[a][i], o.b[b][i], acc[a][b]);
-  };
-
-  // step 0 published (its copies and every wave's LDS statistics)
-  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(4 * (FD_SLOTS - 1)) : "memory");
-  FdOps h0, h1;
-  fd_issue_reads(h0, lbase + oa + x0, lbase + ob + x0);
-  for (int kt = 0; kt < KT; ++kt) {
-    const uint32_t sb = lbase + (uint32_t)((kt % FD_SLOTS) * FD_SLOT);
-    fd_issue_reads(h1, sb + oa + x1, sb + ob + x1);
-    fd_land<6>(h0);
-    products(h0);
-    __builtin_amdgcn_sched_barrier(0);  // the wait for h1 stays behind h0's products (hipcc hoists it otherwise)
-    fd_land<0>(h1);
-    if (kt + 1 < KT) {
-      // step kt + 1 landed for every wave (younger steps in flight: kt + 2, kt + 3 when they exist), and every
-      // wave is done reading slot kt: it takes step kt + 4
-      const int younger = KT - 2 - kt;
-      if (younger >= 2)
-        asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
-      else if (younger == 1)
-        asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-      if (kt + FD_SLOTS < KT) issue(kt + FD_SLOTS);
-      const uint32_t nb = lbase + (uint32_t)(((kt + 1) % FD_SLOTS) * FD_SLOT);
-      fd_issue_reads(h0, nb + oa + x0, nb + ob + x0);
-    }
-    products(h1);
-  }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __syncthreads();  // every wave is done with the ring: it becomes the C tile
-  f32_tile_epilogue<BM, BN, WM, WN, EP, false, RELU, RESID>(g, acc, reinterpret_cast<float*>(fd_sm), m0, n0, nbt);
 }
 
 // ---------------------------------------------------------------------------
@@ -1245,32 +1018,6 @@ static hipError_t launch_cfg(GemmArgs& g, hipStream_t s) {
   return hipGetLastError();
 }
 
-#ifndef ND_F32D
-#define ND_F32D 1  // exact fp32 at large M on the DMA-ring kernel (0: the register-staged one, for A/B)
-#endif
-// gemm_f32d_kernel: fp32 weights, row-major A / C, 256 x 256 tiles, at least 4 k steps
-static bool f32d_eligible(const GemmArgs& g, long t256) {
-  return ND_F32D && !g.Wh && !g.p16io && !g.q24 && g.N % 256 == 0 && t256 >= 256 && g.K % FD_BK == 0 &&
-         g.K >= FD_SLOTS * FD_BK;
-}
-static hipError_t launch_f32d(GemmArgs& g, hipStream_t s) {
-  count_route(ND_ROUTE_TILE256);
-  const int nmb = (g.M + 255) / 256;
-  g.xcd_map = nmb % 8 == 0;
-  dim3 grid((g.N / 256) * nmb), block(512);
-  g.part_n_out = g.N / 256;
-  const bool ln = g.norm, re = g.relu, rs = g.R != nullptr;
-  if (!ln && !re && !rs) hipLaunchKernelGGL((gemm_f32d_kernel<false, false, false>), grid, block, 0, s, g);
-  if (!ln && !re && rs) hipLaunchKernelGGL((gemm_f32d_kernel<false, false, true>), grid, block, 0, s, g);
-  if (!ln && re && !rs) hipLaunchKernelGGL((gemm_f32d_kernel<false, true, false>), grid, block, 0, s, g);
-  if (!ln && re && rs) hipLaunchKernelGGL((gemm_f32d_kernel<false, true, true>), grid, block, 0, s, g);
-  if (ln && !re && !rs) hipLaunchKernelGGL((gemm_f32d_kernel<true, false, false>), grid, block, 0, s, g);
-  if (ln && !re && rs) hipLaunchKernelGGL((gemm_f32d_kernel<true, false, true>), grid, block, 0, s, g);
-  if (ln && re && !rs) hipLaunchKernelGGL((gemm_f32d_kernel<true, true, false>), grid, block, 0, s, g);
-  if (ln && re && rs) hipLaunchKernelGGL((gemm_f32d_kernel<true, true, true>), grid, block, 0, s, g);
-  return hipGetLastError();
-}
-
 // Row split a (a x 8/a rectangle of XCDs) that minimises the operand blocks
 // each XCD's L2 fetches: GY / a row blocks of A plus GX / (8 / a) column
 // groups of W (NT column blocks each); 0 when no split divides the grid.
@@ -1388,12 +1135,6 @@ hipError_t launch_gemm(GemmArgs& g, hipStream_t s) {
   // 256x256 tiles, 8 waves of 128x64: half the global->LDS bytes per flop and
   // half the per-tile prologue/epilogue share of the 128x128 tile
   const long t256 = (long)((g.M + 255) / 256) * (g.N / 256);
-#ifdef ND_F32_TILE  // timing variants only (tools/build_variant.sh): the fp32 products' tile
-  if (!g.Wh && ND_F32_TILE == 128 && g.N % 128 == 0) return launch_cfg<128, 128, 2, 2>(g, s);
-  if (!g.Wh && ND_F32_TILE == 129 && g.N % 256 == 0) return launch_cfg<128, 256, 2, 4>(g, s);
-  if (!g.Wh && ND_F32_TILE == 130 && g.N % 128 == 0) return launch_cfg<128, 128, 2, 4>(g, s);
-#endif
-  if (f32d_eligible(g, t256)) return launch_f32d(g, s);
   if (g.N % 256 == 0 && t256 >= 256) return launch_cfg<256, 256, 2, 4>(g, s);
   const long t128 = (long)((g.M + 127) / 128) * (g.N / 128);
   if (g.N % 128 == 0 && t128 >= 512) return launch_cfg<128, 128, 2, 2>(g, s);
