@@ -130,6 +130,10 @@ __device__ __forceinline__ f32x16 mfma32h(h8 a, h8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
+__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
 __device__ __forceinline__ void split4(f32x4 v, h4& hi, h4& lo) {
   hi = {(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
   lo = {(_Float16)(v.x - (float)hi.x), (_Float16)(v.y - (float)hi.y), (_Float16)(v.z - (float)hi.z),
@@ -138,10 +142,26 @@ __device__ __forceinline__ void split4(f32x4 v, h4& hi, h4& lo) {
 
 // BK: k depth of a main-loop step (32; 64 for the small-tile, long-K shapes,
 // whose steps are otherwise too short to cover the next step's load latency)
+//
+// Exact fp32 products (!H3) at BK = 32 run on v_mfma_f32_16x16x4_f32 (M16)
+// rather than 32x32x2: the same cycles per FLOP, but the chip holds a higher
+// clock on the 16x16 shape under this load (MI355X_MICROARCH.md 'DVFS
+// give-back' item 7; the library's fp32 GEMM at these shapes is a 16x16 one,
+// profiles/r06h_mfma_sgemm.json).  Lane (row r = l & 15, k quad q = l >> 4)
+// reads 16 B (4 consecutive k) of its row per 16-k block and feeds 4 MFMAs
+// (MFMA e sums k = {e, 4 + e, 8 + e, 12 + e}: a permutation of K that A and W
+// share).  The LDS rows are unpadded (32 floats) with their 16-B chunks
+// XOR-swizzled by (row >> 1) & 7, which makes those reads conflict-free and
+// keeps a staging row's 8 chunks one contiguous 128-B store.
+#ifndef ND_F32_M16
+#define ND_F32_M16 1
+#endif
 template <int BM, int BN, int WM, int WN, int BK, bool H3, bool LN, bool RELU, bool RESID>
 __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g) {
   constexpr int NT = WM * WN * 64;
-  constexpr int LDK = BK + 4, LDC = BN + 4;
+  constexpr bool M16 = ND_F32_M16 && !H3 && BK == 32;
+  constexpr int LDK = M16 ? BK : BK + 4, LDC = BN + 4;
+  constexpr int FM16 = BM / WM / 16, FN16 = BN / WN / 16;  // M16: 16x16 blocks per wave
   constexpr int TPK = BK / 4;  // threads per row of a row-major BK-wide slice
   constexpr int FM = BM / WM / 32, FN = BN / WN / 32;
   constexpr int A4 = BM * BK / 4 / NT;
@@ -229,6 +249,8 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
         float* p = &As[buf * BM * LDK + row * LDK + (c >> 3) * 8 + ((c >> 2) & 1) * 2];
         *reinterpret_cast<h4*>(p) = hi;
         *reinterpret_cast<h4*>(p + 4) = lo;
+      } else if constexpr (M16) {
+        st4(&As[buf * BM * LDK + row * LDK + (((c >> 2) ^ ((row >> 1) & 7)) << 2)], ra[i]);
       } else {
         st4(&As[buf * BM * LDK + row * LDK + c], ra[i]);
       }
@@ -236,17 +258,28 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
 #pragma unroll
     for (int i = 0; i < W4; ++i) {
       const int f = tid + i * NT, row = f / TPK, c = (f % TPK) * 4;
-      st4(&Ws[buf * BN * LDK + row * LDK + c], rw[i]);
+      if constexpr (M16)
+        st4(&Ws[buf * BN * LDK + row * LDK + (((c >> 2) ^ ((row >> 1) & 7)) << 2)], rw[i]);
+      else
+        st4(&Ws[buf * BN * LDK + row * LDK + c], rw[i]);
     }
   };
 
-  f32x16 acc[FM][FN];
+  f32x16 acc[M16 ? 1 : FM][M16 ? 1 : FN];
+  f32x4 acc16[M16 ? FM16 : 1][M16 ? FN16 : 1];
+  if constexpr (M16) {
 #pragma unroll
-  for (int a = 0; a < FM; ++a)
+    for (int a = 0; a < FM16; ++a)
 #pragma unroll
-    for (int b = 0; b < FN; ++b)
+      for (int b = 0; b < FN16; ++b) acc16[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  } else {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+    for (int a = 0; a < FM; ++a)
+#pragma unroll
+      for (int b = 0; b < FN; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  }
 
   const int wm = wave / WN, wn = wave % WN;
   const int lr = lane & 31, lh = lane >> 5;
@@ -318,6 +351,28 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
             acc[a][b] = mfma32h(ah[a], bh[b], acc[a][b]);
           }
       }
+    } else if constexpr (M16) {
+      const int r16 = lane & 15, kq = lane >> 4;
+#pragma unroll
+      for (int kb = 0; kb < BK / 16; ++kb) {
+        // a row block at a time: the W operands of the 16-k block stay, one A operand is live (the register
+        // peak of holding all eight spilled)
+        f32x4 bf[FN16];
+#pragma unroll
+        for (int b = 0; b < FN16; ++b) {
+          const int row = wn * FN16 * 16 + b * 16 + r16;
+          bf[b] = ld4(&Ws[buf * BN * LDK + row * LDK + (((kb * 4 + kq) ^ ((row >> 1) & 7)) << 2)]);
+        }
+#pragma unroll
+        for (int a = 0; a < FM16; ++a) {
+          const int row = wm * FM16 * 16 + a * 16 + r16;
+          const f32x4 af = ld4(&As[buf * BM * LDK + row * LDK + (((kb * 4 + kq) ^ ((row >> 1) & 7)) << 2)]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int b = 0; b < FN16; ++b) acc16[a][b] = mfma16(af[e], bf[b][e], acc16[a][b]);
+        }
+      }
     } else
 #pragma unroll
     for (int kb = 0; kb < BK / 8; ++kb) {
@@ -345,7 +400,24 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
 #pragma unroll
   for (int ep = 0; ep < EP; ++ep) {
     // epilogue 1: bias (+relu) into the LDS C tile (rows ep*RP .. +RP)
-    if (EP == 1 || wm == ep) {
+    if constexpr (M16) {
+      // lane l, reg r of block (a, b): row 16 a + 4 (l >> 4) + r, column 16 b + (l & 15)
+      if (EP == 1 || wm == ep) {
+#pragma unroll
+        for (int b = 0; b < FN16; ++b) {
+          const int cl = wn * FN16 * 16 + b * 16 + (lane & 15);
+          const float bv = g.bias ? g.bias[n0 + cl] : 0.f;
+#pragma unroll
+          for (int a = 0; a < FM16; ++a)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float v = acc16[a][b][r] + bv;
+              if constexpr (RELU) v = fmaxf(v, 0.f);
+              Cs[(wm * FM16 * 16 + a * 16 + 4 * (lane >> 4) + r - ep * RP) * LDC + cl] = v;
+            }
+        }
+      }
+    } else if (EP == 1 || wm == ep) {
 #pragma unroll
       for (int a = 0; a < FM; ++a)
 #pragma unroll
@@ -417,9 +489,6 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
 // load in flight before the epilogue operands were even requested)
 __device__ __attribute__((aligned(16))) float nd_zero16[16];
 
-__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
 
 // Split-fp16 form on the P16 layout (H3, see the row-major kernel): the
 // 16x16x32 f16 MFMA takes 8 k per lane; lane l supplies the 4 k of its P16
