@@ -141,6 +141,9 @@ hipError_t launch_layernorm(const float* x, const float* g, const float* b, floa
 __global__ void __launch_bounds__(1024)
 enc_attention_kernel(const float* __restrict__ qkv, const float* __restrict__ signal, const int* __restrict__ span,
                      float* __restrict__ out, int T) {
+#ifdef ND_SKIP_EATTN32  // timing probe only (tools/marginal_exact.sh): the kernel's marginal cost
+  if (threadIdx.x < 100000) return;
+#endif
   __shared__ __attribute__((aligned(16))) float Ks[ENC_MAXT * ENC_KLD];
   __shared__ __attribute__((aligned(16))) float Vt[ND_DH * ENC_VLD];
   __shared__ int kflag[ENC_MAXT];  // 0 = key, 1 = masked (signal == 0), 2 = absent (t >= span)

@@ -156,8 +156,50 @@ __device__ __forceinline__ void split4(f32x4 v, h4& hi, h4& lo) {
 #ifndef ND_F32_M16
 #define ND_F32_M16 1
 #endif
+// Epilogue of the row-major LDS-tiled kernels, second half: RP rows of the C tile staged in LDS (Cs, stride
+// BN + 4) leave as coalesced float4 rows (+ residual), or as the 24-bit context image; row statistics
+template <int BN, int NT, int RP, bool RELU, bool RESID>
+__device__ __forceinline__ void f32_tile_rows(const GemmArgs& g, const float* Cs, int row0, int n0, int nbt) {
+  constexpr int LDC = BN + 4, TPR = BN / 4, RPP = NT / TPR;
+  const int tid = threadIdx.x, c4 = (tid % TPR) * 4, M = g.M;
+  for (int r0 = 0; r0 < RP; r0 += RPP) {
+    const int rl = r0 + tid / TPR, row = row0 + rl;
+    f32x4 v = ld4(&Cs[rl * LDC + c4]);
+    if (row < M) {
+      const size_t ro = g.p16io ? pk(row, n0 + c4, g.N) : (size_t)row * g.ldr + n0 + c4;
+      const size_t co = g.p16io ? pk(row, n0 + c4, g.N) : (size_t)row * g.ldc + n0 + c4;
+      if constexpr (RESID) v += ld4(g.R + ro);
+      if (!g.q24) st4(g.C + co, v);
+    }
+    if constexpr (BN % ND_D == 0 && !RESID && !RELU) {
+      // the 24-bit context K/V image (q24_quant_store: the head's 8 lanes are
+      // this row's threads c4 / 4 .. + 7, every lane of them active here)
+      // (BN >= 256: one wave = 64 threads of one row, so `row < M` is wave-uniform)
+      if (g.q24 && row < M) {
+        const int col = n0 + c4, layer = col / (2 * ND_D), half = (col / ND_D) & 1, d = col % ND_D;
+        uint8_t* dst = g.q24 + (size_t)layer * g.q24_plane + (size_t)row * CTXQ_ROW;
+        const float sc = q24_quant_store(v, dst + half * CTXQ_V + 3 * d);
+        if ((d & (ND_DH - 1)) == 0) reinterpret_cast<float*>(dst + CTXQ_S)[2 * (d / ND_DH) + half] = sc;
+      }
+    }
+    if (g.part_out) {
+      const float mu = group_sum<TPR>(v.x + v.y + v.z + v.w) * (1.0f / BN);
+      const f32x4 d = v - mu;
+      const float q = group_sum<TPR>(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w);
+      if ((tid % TPR) == 0 && row < M) {
+        float* p = g.part_out + ((size_t)row * ND_PART_LD + nbt) * 2;
+        p[0] = mu;
+        p[1] = q;
+      }
+    }
+  }
+}
+
 template <int BM, int BN, int WM, int WN, int BK, bool H3, bool LN, bool RELU, bool RESID>
 __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g) {
+#ifdef ND_SKIP_F32GEMM  // timing probe only (tools/marginal_exact.sh): the fp32 products' marginal cost
+  if (!H3 && threadIdx.x < 100000) return;
+#endif
   constexpr int NT = WM * WN * 64;
   constexpr bool M16 = ND_F32_M16 && !H3 && BK == 32;
   constexpr int LDK = M16 ? BK : BK + 4, LDC = BN + 4;
@@ -395,8 +437,6 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
   }
   if constexpr (H3 && !LN) flag_overflow(g.ovf, amax);
 
-  constexpr int TPR = BN / 4, RPP = NT / TPR;
-  const int c4 = (tid % TPR) * 4;
 #pragma unroll
   for (int ep = 0; ep < EP; ++ep) {
     // epilogue 1: bias (+relu) into the LDS C tile (rows ep*RP .. +RP)
@@ -433,38 +473,237 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_f32_kernel(const GemmArgs g)
         }
     }
     __syncthreads();
-    // epilogue 2: coalesced float4 rows (+ residual), row statistics
-    for (int r0 = 0; r0 < RP; r0 += RPP) {
-      const int rl = r0 + tid / TPR, row = m0 + ep * RP + rl;
-      f32x4 v = ld4(&Cs[rl * LDC + c4]);
-      if (row < M) {
-        const size_t ro = g.p16io ? pk(row, n0 + c4, g.N) : (size_t)row * g.ldr + n0 + c4;
-        const size_t co = g.p16io ? pk(row, n0 + c4, g.N) : (size_t)row * g.ldc + n0 + c4;
-        if constexpr (RESID) v += ld4(g.R + ro);
-        if (!g.q24) st4(g.C + co, v);
+    f32_tile_rows<BN, NT, RP, RELU, RESID>(g, Cs, m0 + ep * RP, n0, nbt);
+    if (EP > 1) __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Exact fp32 at large M (the encoder's GEMMs under exact fp32) with the
+// operands brought to LDS by DMA (ND_F32D): the 256x256 tile, 8 waves of
+// 128x64 and 16x16x4 MFMAs of gemm_f32_kernel's M16 form, in its k order (so
+// bitwise its C), on a ring instead of register staging.
+//  - k steps of 16 (A 16 KB + W 16 KB) in a ring of 4 LDS slots, every wave
+//    copying 4 KB of each by buffer_load ... lds (lane-linear 1 KB per
+//    instruction; the lane's row offset its only vector operand, the k step
+//    in the scalar offset); FD_SLOTS - 1 steps in flight beyond the one
+//    computed, one barrier per step;
+//  - a row's four 16-B k chunks stored XOR-swizzled by (row >> 1) & 3, so a
+//    lane's (row, 4-k) operand read is a conflict-free ds_read_b128;
+//  - the LDS reads are inline asm with a counted lgkmcnt wait (an ordinary
+//    LDS read after an LDS-DMA makes hipcc wait for every copy in flight),
+//    the barrier a raw s_barrier behind a counted vmcnt;
+//  - the LayerNorm applied to the operand registers, (a - mean) * rstd, as
+//    the register-staged kernel applies it at its LDS store.
+// (The 32x32x2 form of this ring, ca5ef35, was busier but held a 9% lower
+// clock: DESIGN.md §3 "Exact fp32 encoder GEMMs".)
+#ifndef ND_F32D
+#define ND_F32D 1
+#endif
+#define FD_BK 16                       // k per step
+// Ring slots and epilogue passes: the smaller LDS footprint wins under the pool's three calls in flight
+// (exact leg, same box: register-staged 27.21 ms per call, 4 slots / 2 passes (135 KB) 27.10, 4 / 4 (133 KB)
+// 27.06, 3 / 4 (100 KB) 27.00; profiles/r06_ab_f32d_ring.txt), although alone the ring kernel runs FFN1 and FFN2
+// 5-8% slower than the register-staged one (lower clock, profiles/r06_f32d_s3e4_check.txt)
+#ifndef FD_SLOTS
+#define FD_SLOTS 3                     // ring slots (two steps in flight beyond the one computed)
+#endif
+#ifndef FD_EP
+#define FD_EP 4                        // epilogue passes (row groups of 256 / FD_EP rows staged in LDS)
+#endif
+#define FD_SLOT (2 * 256 * FD_BK * 4)  // bytes per slot: A tile, then W tile
+typedef __attribute__((address_space(3))) void fd_lds_void;
+
+template <int OFF>
+__device__ __forceinline__ f32x4 fd_ld(uint32_t a) {
+  f32x4 r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=&v"(r) : "v"(a), "n"(OFF) : "memory");
+  return r;
+}
+// a step's operands of one lane: its 8 A row blocks and 4 W row blocks (16 rows = 1 KB apart)
+struct FdOps {
+  f32x4 a[8], b[4];
+};
+__device__ __forceinline__ void fd_issue(FdOps& o, uint32_t aa, uint32_t ab) {
+  o.a[0] = fd_ld<0>(aa);
+  o.a[1] = fd_ld<1024>(aa);
+  o.a[2] = fd_ld<2048>(aa);
+  o.a[3] = fd_ld<3072>(aa);
+  o.a[4] = fd_ld<4096>(aa);
+  o.a[5] = fd_ld<5120>(aa);
+  o.a[6] = fd_ld<6144>(aa);
+  o.a[7] = fd_ld<7168>(aa);
+  o.b[0] = fd_ld<0>(ab);
+  o.b[1] = fd_ld<1024>(ab);
+  o.b[2] = fd_ld<2048>(ab);
+  o.b[3] = fd_ld<3072>(ab);
+}
+__device__ __forceinline__ void fd_land(FdOps& o) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(o.a[0]), "+v"(o.a[1]), "+v"(o.a[2]), "+v"(o.a[3]), "+v"(o.a[4]), "+v"(o.a[5]), "+v"(o.a[6]),
+                 "+v"(o.a[7]), "+v"(o.b[0]), "+v"(o.b[1]), "+v"(o.b[2]), "+v"(o.b[3])
+               :
+               : "memory");
+}
+
+template <bool LN, bool RELU, bool RESID>
+__global__ void __launch_bounds__(512) gemm_f32d_kernel(const GemmArgs g) {
+  constexpr int BM = 256, BN = 256, WM = 2, WN = 4, NT = 512, EP = FD_EP, RP = BM / EP, LDC = BN + 4;
+  static_assert(EP == 2 || EP == 4, "a pass is one wave row group or half of one");
+  constexpr int FM16 = 8, FN16 = 4;
+  constexpr int RING = FD_SLOTS * FD_SLOT, CBYTES = RP * LDC * 4;
+  __shared__ __attribute__((aligned(16))) char fd_sm[RING > CBYTES ? RING : CBYTES];
+  __shared__ float s_mu[LN ? BM : 1], s_rs[LN ? BM : 1];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wu = __builtin_amdgcn_readfirstlane(wave);
+  const int ntn = g.N / BN;
+  int nbt, mbk;
+  if (g.xcd_map) {  // as gemm_f32_kernel
+    const int b = blockIdx.x, j = b >> 3;
+    nbt = j % ntn;
+    mbk = (j / ntn) * 8 + (b & 7);
+  } else {
+    nbt = blockIdx.x % ntn;
+    mbk = blockIdx.x / ntn;
+  }
+  const int n0 = nbt * BN, m0 = mbk * BM;
+  const int M = g.M, KT = g.K / FD_BK;
+
+  // copies: wave w moves pieces 2w, 2w + 1 of each tile (1 KB each: 16 rows x 4 chunks); the lane's piece is
+  // row 16 j + lane / 4, k chunk (lane & 3) ^ ((lane >> 3) & 3) (rows past M clamped: never stored)
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.A + (size_t)m0 * g.lda), 0,
+                                                                      0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.W + (size_t)n0 * g.ldw), 0,
+                                                                      0x7fffffff, 0x00020000);
+  const int kc = (lane & 3) ^ ((lane >> 3) & 3);
+  int voa[2], vow[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (2 * wu + i) * 16 + (lane >> 2);
+    voa[i] = min(row, M - 1 - m0) * g.lda * 4 + kc * 16;
+    vow[i] = row * g.ldw * 4 + kc * 16;
+  }
+  auto issue = [&](int st) {  // k step st into slot st % FD_SLOTS
+    char* sl = fd_sm + (st % FD_SLOTS) * FD_SLOT;
+    const int so = st * FD_BK * 4;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (fd_lds_void*)(sl + (2 * wu + i) * 1024), 16, voa[i], so, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (fd_lds_void*)(sl + FD_SLOT / 2 + (2 * wu + i) * 1024), 16,
+                                               vow[i], so, 0, 0);
+  };
+
+  if (rows_dead(g.skip, g.skip_rpc, m0, BM, M)) return;
+#pragma unroll
+  for (int p = 0; p < FD_SLOTS - 1; ++p) issue(p);  // KT >= FD_SLOTS (host-checked)
+
+  const int wm = wave / WN, wn = wave % WN;
+  const int r16 = lane & 15, kq = lane >> 4;
+  float mu[FM16], rs[FM16];
+  if constexpr (LN) {
+    // the row statistics' loads go out beside the first copies (the LDS stores below wait for both)
+    if (g.part_in) {
+      for (int r = tid; r < BM; r += NT) {
+        float m_, r_;
+        merge_stats(g.part_in + (size_t)min(m0 + r, M - 1) * ND_PART_LD * 2, g.part_n_in, m_, r_);
+        s_mu[r] = m_;
+        s_rs[r] = r_;
       }
-      if constexpr (BN % ND_D == 0 && !RESID && !RELU) {
-        // the 24-bit context K/V image (q24_quant_store: the head's 8 lanes are
-        // this row's threads c4 / 4 .. + 7, every lane of them active here)
-        // (BN >= 256: one wave = 64 threads of one row, so `row < M` is wave-uniform)
-        if (g.q24 && row < M) {
-          const int col = n0 + c4, layer = col / (2 * ND_D), half = (col / ND_D) & 1, d = col % ND_D;
-          uint8_t* dst = g.q24 + (size_t)layer * g.q24_plane + (size_t)row * CTXQ_ROW;
-          const float sc = q24_quant_store(v, dst + half * CTXQ_V + 3 * d);
-          if ((d & (ND_DH - 1)) == 0) reinterpret_cast<float*>(dst + CTXQ_S)[2 * (d / ND_DH) + half] = sc;
-        }
-      }
-      if (g.part_out) {
-        const float mu = group_sum<TPR>(v.x + v.y + v.z + v.w) * (1.0f / BN);
-        const f32x4 d = v - mu;
-        const float q = group_sum<TPR>(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w);
-        if ((tid % TPR) == 0 && row < M) {
-          float* p = g.part_out + ((size_t)row * ND_PART_LD + nbt) * 2;
-          p[0] = mu;
-          p[1] = q;
+    } else {
+      // two-pass row statistics, one wave per row (K == 256, host-checked)
+      constexpr int NW = NT / 64, RPW = BM / NW, G = 8;
+      for (int r0 = 0; r0 < RPW; r0 += G) {
+        f32x4 v[G];
+#pragma unroll
+        for (int i = 0; i < G; ++i) v[i] = ld4(g.A + (size_t)min(m0 + wave + (r0 + i) * NW, M - 1) * g.lda + lane * 4);
+#pragma unroll
+        for (int i = 0; i < G; ++i) {
+          const int r = wave + (r0 + i) * NW;
+          const float m_ = wave_sum(v[i].x + v[i].y + v[i].z + v[i].w) * (1.0f / 256.0f);
+          const f32x4 d = v[i] - m_;
+          const float var = wave_sum(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w) * (1.0f / 256.0f);
+          if (lane == 0) {
+            s_mu[r] = m_;
+            s_rs[r] = ln_rsqrt(var + ND_LN_EPS);
+          }
         }
       }
     }
+    __syncthreads();
+#pragma unroll
+    for (int a = 0; a < FM16; ++a) {
+      mu[a] = s_mu[wm * FM16 * 16 + a * 16 + r16];
+      rs[a] = s_rs[wm * FM16 * 16 + a * 16 + r16];
+    }
+  }
+
+  f32x4 acc16[FM16][FN16];
+#pragma unroll
+  for (int a = 0; a < FM16; ++a)
+#pragma unroll
+    for (int b = 0; b < FN16; ++b) acc16[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // the lane's operand addresses in a slot: its A / W row in block 0 and its swizzled 16-B chunk
+  const uint32_t lbase = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)fd_sm);
+  const uint32_t x = (uint32_t)((kq ^ ((r16 >> 1) & 3)) * 16);
+  const uint32_t oa = (uint32_t)((wm * FM16 * 16 + r16) * 64) + x;
+  const uint32_t ob = (uint32_t)(FD_SLOT / 2 + (wn * FN16 * 16 + r16) * 64) + x;
+  FdOps o;
+  for (int kt = 0; kt < KT; ++kt) {
+    // step kt landed for every wave (younger steps in flight: kt + 1, kt + 2 when they exist), and every wave is
+    // done reading slot kt - 1: it takes step kt + 3
+    const int younger = KT - 1 - kt;
+    if (FD_SLOTS >= 4 && younger >= 2)
+      asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+    else if (younger >= 1)
+      asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    if (kt + FD_SLOTS - 1 < KT) issue(kt + FD_SLOTS - 1);
+    const uint32_t sb = lbase + (uint32_t)((kt % FD_SLOTS) * FD_SLOT);
+    fd_issue(o, sb + oa, sb + ob);
+    fd_land(o);
+    if constexpr (LN) {
+#pragma unroll
+      for (int a = 0; a < FM16; ++a) o.a[a] = (o.a[a] - mu[a]) * rs[a];
+    }
+#pragma unroll
+    for (int a = 0; a < FM16; ++a)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int b = 0; b < FN16; ++b) acc16[a][b] = mfma16(o.a[a][e], o.b[b][e], acc16[a][b]);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();  // every wave is done with the ring: it becomes the C tile
+  float* Cs = reinterpret_cast<float*>(fd_sm);
+#pragma unroll
+  for (int ep = 0; ep < EP; ++ep) {
+    constexpr int AP = FM16 * WM / EP;  // row blocks of a wave per pass
+    if (wm == ep * WM / EP) {
+      // lane l, reg r of block (a, b): row 16 a + 4 (l >> 4) + r, column 16 b + (l & 15)
+      const int a0 = (ep % (EP / WM)) * AP;
+#pragma unroll
+      for (int b = 0; b < FN16; ++b) {
+        const int cl = wn * FN16 * 16 + b * 16 + r16;
+        const float bv = g.bias ? g.bias[n0 + cl] : 0.f;
+#pragma unroll
+        for (int a = 0; a < FM16; ++a) {
+          if (a < a0 || a >= a0 + AP) continue;  // compile-time per pass after unrolling
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = acc16[a][b][r] + bv;
+            if constexpr (RELU) v = fmaxf(v, 0.f);
+            Cs[((a - a0) * 16 + 4 * kq + r) * LDC + cl] = v;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    f32_tile_rows<BN, NT, RP, RELU, RESID>(g, Cs, m0 + ep * RP, n0, nbt);
     if (EP > 1) __syncthreads();
   }
 }
@@ -1087,6 +1326,29 @@ static hipError_t launch_cfg(GemmArgs& g, hipStream_t s) {
   return hipGetLastError();
 }
 
+// gemm_f32d_kernel: fp32 weights, row-major A / C, 256 x 256 tiles, at least FD_SLOTS k steps
+static bool f32d_eligible(const GemmArgs& g, long t256) {
+  return ND_F32D && !g.Wh && !g.p16io && !g.q24 && g.N % 256 == 0 && t256 >= 256 && g.K % FD_BK == 0 &&
+         g.K >= FD_SLOTS * FD_BK;
+}
+static hipError_t launch_f32d(GemmArgs& g, hipStream_t s) {
+  count_route(ND_ROUTE_TILE256);
+  const int nmb = (g.M + 255) / 256;
+  g.xcd_map = nmb % 8 == 0;
+  dim3 grid((g.N / 256) * nmb), block(512);
+  g.part_n_out = g.N / 256;
+  const bool ln = g.norm, re = g.relu, rs = g.R != nullptr;
+  if (!ln && !re && !rs) hipLaunchKernelGGL((gemm_f32d_kernel<false, false, false>), grid, block, 0, s, g);
+  if (!ln && !re && rs) hipLaunchKernelGGL((gemm_f32d_kernel<false, false, true>), grid, block, 0, s, g);
+  if (!ln && re && !rs) hipLaunchKernelGGL((gemm_f32d_kernel<false, true, false>), grid, block, 0, s, g);
+  if (!ln && re && rs) hipLaunchKernelGGL((gemm_f32d_kernel<false, true, true>), grid, block, 0, s, g);
+  if (ln && !re && !rs) hipLaunchKernelGGL((gemm_f32d_kernel<true, false, false>), grid, block, 0, s, g);
+  if (ln && !re && rs) hipLaunchKernelGGL((gemm_f32d_kernel<true, false, true>), grid, block, 0, s, g);
+  if (ln && re && !rs) hipLaunchKernelGGL((gemm_f32d_kernel<true, true, false>), grid, block, 0, s, g);
+  if (ln && re && rs) hipLaunchKernelGGL((gemm_f32d_kernel<true, true, true>), grid, block, 0, s, g);
+  return hipGetLastError();
+}
+
 // Row split a (a x 8/a rectangle of XCDs) that minimises the operand blocks
 // each XCD's L2 fetches: GY / a row blocks of A plus GX / (8 / a) column
 // groups of W (NT column blocks each); 0 when no split divides the grid.
@@ -1204,6 +1466,7 @@ hipError_t launch_gemm(GemmArgs& g, hipStream_t s) {
   // 256x256 tiles, 8 waves of 128x64: half the global->LDS bytes per flop and
   // half the per-tile prologue/epilogue share of the 128x128 tile
   const long t256 = (long)((g.M + 255) / 256) * (g.N / 256);
+  if (f32d_eligible(g, t256)) return launch_f32d(g, s);
   if (g.N % 256 == 0 && t256 >= 256) return launch_cfg<256, 256, 2, 4>(g, s);
   const long t128 = (long)((g.M + 127) / 128) * (g.N / 128);
   if (g.N % 128 == 0 && t128 >= 512) return launch_cfg<128, 128, 2, 2>(g, s);
