@@ -238,6 +238,10 @@ REVIEWED_PAIRED = {
                           "barrier; pool-tested"),
     "gemm_f32_kernel": (48, "A / W tile staging (ds_write2_b32 / _b64 / 2st64) read by other waves after a "
                             "barrier; encoder-side GEMMs of the beam / exact / NanoEncoder paths, pool-tested"),
+    "gemm_f32d_kernel": (8, "the LayerNorm row statistics (ds_write2st64_b32, one lane per row, mean and rstd) "
+                            "read by every wave after a barrier, as gemm_f32_kernel's; the operand ring takes no "
+                            "paired form (DMA writes, inline-asm ds_read_b128); exact fp32 pool-tested bitwise at "
+                            "the bench's configuration (test_pool_at_bench_config_matches_single_engine)"),
     "dec_ctx_attention_kernel": (36, "the (m, l, acc) merge of the beam context attention (and of its split "
                                      "form); launched with at most 52 KB, listed in case that grows"),
     "dec_ctx_q24_kernel": (26, "the (m, l, acc) merge after a barrier behind the DMA rings' last use; the merge "
